@@ -1,0 +1,219 @@
+#!/usr/bin/env python3
+"""Headline benchmark (BASELINE.json metric): rows/s of filter + project + GROUP BY over
+device-resident synthetic RecordBatches, config 4:
+
+    SELECT k, SUM(a + b), COUNT(*), MIN(a), MAX(b) FROM t WHERE a > 2^19 GROUP BY k
+    k = u0 mod 1024, a = u1 mod 2^20, b = u2 mod 2^20 (int64; splitmix64 counter generator)
+
+One step = one full query over this rank's 1B-row batch (inputs resident in HBM before the
+timed region): fused filter -> project -> partial hash-aggregate kernel, then (N > 1) the
+hash-sharded all-to-all of partial aggregates over RCCL and the owner-side merge, then the
+final one-batch materialisation. Weak scaling: every rank owns 1B rows.
+
+    python bench.py [--gpus N --steps K --warmup W]      (N > 1: launched by torch.distributed.run)
+"""
+from __future__ import annotations
+
+import argparse
+import ctypes as C
+import json
+import os
+import pathlib
+import sys
+import time
+
+ROOT = pathlib.Path(__file__).resolve().parent
+sys.path.insert(0, str(ROOT / "query-engines_amd"))
+
+METRIC = "rows/sec filter+project+group-by over 1B-row Arrow batch; % HBM roofline"
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md chip table)
+BYTES_PER_ROW = 24     # k, a, b int64: algorithmic bytes read per row
+
+
+def c4_spec(N, threshold=1 << 19):
+    spec = N.QeFusedSpec()
+    spec.mask_col = -1
+    spec.nterms = 1
+    spec.terms[0].col = 1
+    spec.terms[0].op = N.OP_GT
+    spec.terms[0].rhs_col = -1
+    spec.terms[0].lit = N.scalar(threshold)
+    spec.key_cols[0] = 0
+    p = spec.inputs[0]  # SUM(a + b)
+    p.ntokens = 3
+    p.tokens[0] = N.QeToken(N.TOK_COL, 1, N.QeScalar())
+    p.tokens[1] = N.QeToken(N.TOK_COL, 2, N.QeScalar())
+    p.tokens[2] = N.QeToken(N.TOK_ADD, 0, N.QeScalar())
+    spec.inputs[2].ntokens = 1  # MIN(a)
+    spec.inputs[2].tokens[0] = N.QeToken(N.TOK_COL, 1, N.QeScalar())
+    spec.inputs[3].ntokens = 1  # MAX(b)
+    spec.inputs[3].tokens[0] = N.QeToken(N.TOK_COL, 2, N.QeScalar())
+    return spec
+
+
+def cpu_baseline(sample_rows: int, threads: int) -> dict:
+    """Timed CPU leg (rank 0, N = 1): the oracle's reference-faithful C restatement of the same
+    query (oracle/cpu_baseline.c: row-at-a-time Selection -> Projection -> HashMap aggregate,
+    partition-parallel like Main.kt:1309-1325) on a bounded sample of the same rows."""
+    lib_path = ROOT / "oracle" / "build" / "libqe_oracle.so"
+    if not lib_path.exists():
+        import subprocess
+
+        subprocess.run(["make", "-C", str(ROOT / "oracle")], check=True, capture_output=True)
+
+    class G(C.Structure):
+        _fields_ = [(n, C.c_int64) for n in ("key", "sum", "count", "min", "max")]
+
+    lib = C.CDLL(str(lib_path))
+    lib.qe_cpu_c4.restype = C.c_double
+    lib.qe_cpu_c4.argtypes = [C.c_int64, C.c_int64, C.c_uint64, C.c_int, C.c_int64, C.c_int64,
+                              C.POINTER(G), C.c_int64, C.POINTER(C.c_int64)]
+    out = (G * 2048)()
+    ng = C.c_int64()
+    secs = lib.qe_cpu_c4(0, sample_rows, 42, threads, 1 << 19, 1024, out, 2048, C.byref(ng))
+    return {"value": sample_rows / secs, "unit": "rows/s", "cores": threads, "kind": "port",
+            "sample": f"first {sample_rows} rows of the same C4 table (seed 42), {threads} threads, "
+                      f"{secs:.3f} s; C restatement of the reference operator chain (oracle/cpu_baseline.c)"}
+
+
+def load_traffic(rows: int):
+    """HBM bytes per fused-kernel launch from the committed rocprofv3 PMC summary (profiles/),
+    FETCH_SIZE doubled per MI355X_MICROARCH.md §HBM (gfx950 counts half of wide streaming reads)."""
+    p = ROOT / "profiles" / "traffic.json"
+    if not p.exists():
+        return None
+    try:
+        t = json.loads(p.read_text())
+        if int(t.get("rows", -1)) == rows:
+            return float(t["hbm_bytes_per_launch"])
+    except Exception:
+        return None
+    return None
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--rows", type=int, default=1_000_000_000, help="rows per GPU")
+    ap.add_argument("--cpu-sample-rows", type=int, default=200_000_000)
+    ap.add_argument("--cpu-threads", type=int, default=0)
+    ap.add_argument("--no-cpu", action="store_true")
+    args = ap.parse_args()
+
+    import torch
+    import torch.distributed as dist
+
+    from kquery import native as N
+    from kquery.aggregate import HashAggregateState
+    from kquery.columnar import Context
+    from kquery.datasource import C4_COLUMNS, generate_column
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        print(f"warning: --gpus {args.gpus} but WORLD_SIZE {world}; using WORLD_SIZE", file=sys.stderr)
+    torch.cuda.set_device(local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    from kquery.exchange import exchange_partials
+
+    ctx = Context.get(local)
+    rows = args.rows
+    row0 = rank * rows
+    cols = [generate_column(s, rows, row0, 42, ctx) for s in C4_COLUMNS]
+    ctx.synchronize()
+    aggs = [(N.AGG_SUM, N.TYPE_INT64), (N.AGG_COUNT_STAR, N.TYPE_INT64), (N.AGG_MIN, N.TYPE_INT64),
+            (N.AGG_MAX, N.TYPE_INT64)]
+    partial = HashAggregateState(ctx, [N.TYPE_INT64], aggs, 1024)
+    owner = HashAggregateState(ctx, [N.TYPE_INT64], aggs, 1024) if world > 1 else None
+    spec = c4_spec(N)
+    kernel_ms = []
+
+    def step():
+        partial.reset()
+        partial.set_row_base(row0)
+        partial.update_fused(cols, spec)
+        kernel_ms.append(partial.last_kernel_time())
+        final = partial
+        if world > 1:
+            owner.reset()
+            exchange_partials(partial, owner)
+            final = owner
+        return final.finalize()
+
+    def barrier():
+        if world > 1:
+            dist.barrier()
+
+    for _ in range(args.warmup):
+        step()
+    kernel_ms.clear()
+    barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        keys, res = step()
+    torch.cuda.synchronize()
+    barrier()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+
+    # sanity: every group present once across owners, COUNT(*) adds up to the filtered rows
+    groups = torch.tensor([keys[0].length, int(res[1].to_numpy().sum())], dtype=torch.int64, device="cuda")
+    if world > 1:
+        dist.all_reduce(groups)
+    ms_step = elapsed / args.steps * 1e3
+    launches = sum(k for _, k in kernel_ms)
+    avg_kernel_ms = sum(m for m, _ in kernel_ms) / max(1, launches)
+    achieved = rows * BYTES_PER_ROW / (avg_kernel_ms * 1e-3) / 1e9
+    traffic = load_traffic(rows)
+    line = {
+        "metric": METRIC,
+        "value": world * rows / (ms_step * 1e-3),
+        "unit": "rows/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": ms_step,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "int64",
+        "data": "synthetic (counter-based splitmix64 generator, seed 42), device-resident before timing",
+        "config": {
+            "workload": "C4: SELECT k, SUM(a+b), COUNT(*), MIN(a), MAX(b) WHERE a > 2^19 GROUP BY k",
+            "rows_per_gpu": rows,
+            "groups": 1024,
+            "columns": "k, a, b int64 (Arrow, no nulls)",
+            "parallelism": f"hash-sharded partial aggregate x{world}" + (" + RCCL all-to-all" if world > 1 else ""),
+        },
+        "roofline": {
+            "bound": "hbm",
+            "achieved": achieved,
+            "peak": HBM_PEAK_GBS,
+            "unit": "GB/s",
+            "frac": achieved / HBM_PEAK_GBS,
+            "traffic": traffic,
+            "kernel": "k_hashagg<3,true> (fused filter+project+LDS hash aggregate)",
+            "avg_kernel_ms": avg_kernel_ms,
+            "bytes_per_launch": rows * BYTES_PER_ROW,
+        },
+        "check": {"groups": int(groups[0].item()), "count_star_total": int(groups[1].item())},
+    }
+    if rank == 0 and world == 1 and not args.no_cpu:
+        threads = args.cpu_threads or min(16, os.cpu_count() or 1)
+        line["cpu_baseline"] = cpu_baseline(args.cpu_sample_rows, threads)
+    if rank == 0:
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

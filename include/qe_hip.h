@@ -1,0 +1,304 @@
+/*
+ * qe_hip.h — C ABI of the MI355X (gfx950) columnar execution kernel for kquerydiy.
+ *
+ * This is the drop-in boundary for the reference's hot path: the evaluation inside the
+ * physical operators of folkol/query-engines `kquerydiy/src/Main.kt` ("K:" below).
+ * The Kotlin DataFrame / LogicalPlan / PhysicalPlan layers stay as they are; a JNI shim
+ *  or Python ctypes (kquery/native.py) calls these entry points with plain
+ * device pointers and sizes. No torch, no C++ types cross this boundary.
+ *
+ * Reference interfaces each entry point replaces:
+ *   Expression.evaluate(RecordBatch): ColumnVector ............ K:448-450
+ *     ColumnExpression (zero-copy column reference) ........... K:452-455  -> no call needed
+ *     binary arithmetic / comparison / boolean / literal ...... absent in reference,
+ *                                                                build-defined: qe_eval_*
+ *   SelectionExec (filter) .................................... absent in reference, build-defined:
+ *                                                                qe_filter_count / qe_filter_apply
+ *   AggregateExpression/Accumulator, MaxAccumulator ........... K:514-562  -> qe_agg_global,
+ *                                                                qe_hashagg_*
+ *   HashAggregateExec.execute ................................. K:615-651  -> qe_hashagg_*
+ *   main() partial -> final merge (two-phase aggregate) ....... K:1309-1325 -> qe_hashagg_export /
+ *                                                                qe_hashagg_import
+ *
+ * Error behaviour: every entry point returns an int status (QE_OK = 0, negative = error
+ * class) and sets a thread-local message readable with qe_last_error(). A JNI shim maps
+ * QE_ERR_UNSUPPORTED -> IllegalStateException (K:195, K:469, K:677, K:792, K:799),
+ * QE_ERR_INVALID_ARG -> IllegalArgumentException (K:49), the rest -> RuntimeException.
+ *
+ * Threading: re-entrant. No global mutable state besides the thread-local error string;
+ * each qe_ctx owns one HIP stream and its scratch memory (the reference calls the engine
+ * concurrently from coroutine workers, one ExecutionContext each, K:1309-1313, K:1333).
+ *
+ * Memory: all column buffers are DEVICE pointers on the ctx's device (hipMalloc'ed or
+ * torch-allocated). Layout is the Arrow columnar format: fixed-width values buffer,
+ * optional LSB-first validity bitmap (NULL = no nulls), bit-packed booleans, offset 0.
+ * Results are written into caller-provided device buffers; sizes are queried first.
+ */
+#ifndef QE_HIP_H
+#define QE_HIP_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define QE_ABI_VERSION 1
+
+/* ---- status codes ---------------------------------------------------------------------- */
+#define QE_OK 0
+#define QE_ERR_INVALID_ARG (-1)  /* IllegalArgumentException (K:49) */
+#define QE_ERR_UNSUPPORTED (-2)  /* IllegalStateException / UnsupportedOperationException */
+#define QE_ERR_OOM (-3)
+#define QE_ERR_DEVICE (-4)       /* HIP runtime error */
+#define QE_ERR_CAPACITY (-5)     /* output buffer too small */
+
+/* ---- types ------------------------------------------------------------------------------ */
+/* Arrow type ids used by this kernel. The reference knows only Float8 (fp64) and Utf8
+ * (K:19-22, K:184-196); int64/int32/uint8/date32/bool are build-added. */
+#define QE_TYPE_INT64 1
+#define QE_TYPE_FLOAT64 2
+#define QE_TYPE_BOOL 3   /* bit-packed values, LSB first */
+#define QE_TYPE_UTF8 4   /* int32 offsets (length+1) + bytes */
+#define QE_TYPE_INT32 5
+#define QE_TYPE_UINT8 6
+#define QE_TYPE_DATE32 7 /* int32 days since epoch */
+
+/* One Arrow array (offset 0). Used for inputs and outputs. */
+typedef struct qe_column {
+  int32_t type;
+  int32_t reserved;
+  int64_t length;
+  uint8_t* validity; /* device; NULL = all valid (inputs) / do not write (outputs) */
+  void* values;      /* device; fixed-width values, bit-packed bools, or UTF-8 bytes */
+  int32_t* offsets;  /* device; UTF-8 offsets (length+1), NULL otherwise */
+} qe_column;
+
+/* A literal (build-defined; the reference SQL has no literals).
+ * `bits` holds an int64 value or the IEEE-754 bits of a double. */
+typedef struct qe_scalar {
+  int32_t type; /* QE_TYPE_INT64 or QE_TYPE_FLOAT64 */
+  int32_t is_null;
+  int64_t bits;
+} qe_scalar;
+
+/* Operand of a binary expression: a column, or a literal when `col` is NULL. */
+typedef struct qe_operand {
+  const qe_column* col;
+  qe_scalar lit;
+} qe_operand;
+
+/* ---- context ---------------------------------------------------------------------------- */
+typedef struct qe_ctx qe_ctx;
+
+/* Create a context on HIP device `device`. `stream` is a hipStream_t to launch on
+ * (NULL = the ctx creates and owns one). */
+int qe_ctx_create(int device, void* stream, qe_ctx** out);
+int qe_ctx_destroy(qe_ctx* ctx);
+/* The hipStream_t every kernel of this ctx is launched on. */
+void* qe_ctx_stream(qe_ctx* ctx);
+/* Wait for all work queued on the ctx's stream. */
+int qe_ctx_synchronize(qe_ctx* ctx);
+/* Thread-local message of the last failing call on this thread ("" if none). */
+const char* qe_last_error(void);
+int qe_abi_version(void);
+
+/* Device memory helpers for hosts without their own allocator (JNI). */
+int qe_device_alloc(qe_ctx* ctx, size_t bytes, void** out);
+int qe_device_free(qe_ctx* ctx, void* ptr);
+int qe_copy_to_device(qe_ctx* ctx, void* dst, const void* src, size_t bytes);   /* sync */
+int qe_copy_to_host(qe_ctx* ctx, void* dst, const void* src, size_t bytes);     /* sync */
+
+/* ---- synthetic RecordBatch generator (measurement harness) ------------------------------ */
+/* Counter-based: u = splitmix64(seed ^ col*0x9E3779B97F4A7C15 ^ row), row = row0 + i.
+ * Distributions (oracle/gen.py restates them bit-for-bit):
+ *   QE_GEN_MOD     int64: u mod param              (param > 0)
+ *   QE_GEN_RAW     int64: (int64)u                 (full range, exercises wrap)
+ *   QE_GEN_UNIT53  fp64 : (u >> 11) * 2^-42 - 1024 (exact in fp64)
+ *   QE_GEN_MOD_F64 fp64 : (double)(u mod param) * 0.01
+ * If `null_permille` > 0 the validity bitmap is filled: row valid unless
+ * splitmix64(seed ^ (col+0x1000)*phi ^ row) mod 1000 < null_permille. */
+#define QE_GEN_MOD 1
+#define QE_GEN_RAW 2
+#define QE_GEN_UNIT53 3
+#define QE_GEN_MOD_F64 4
+int qe_generate(qe_ctx* ctx, qe_column* out, int32_t dist, int64_t param, uint64_t seed,
+                uint64_t col, int64_t row0, int32_t null_permille);
+
+/* ---- vectorised expressions: Expression.evaluate (K:448-450) ---------------------------- */
+#define QE_OP_ADD 1
+#define QE_OP_SUB 2
+#define QE_OP_MUL 3
+#define QE_OP_DIV 4
+#define QE_OP_EQ 10
+#define QE_OP_NE 11
+#define QE_OP_LT 12
+#define QE_OP_LE 13
+#define QE_OP_GT 14
+#define QE_OP_GE 15
+#define QE_OP_AND 20
+#define QE_OP_OR 21
+#define QE_OP_NOT 22
+#define QE_OP_IS_NULL 23
+#define QE_OP_IS_NOT_NULL 24
+
+/* Arithmetic (K1). int64 +,-,* wrap (two's complement, JVM Long); int64 / truncates,
+ * x/0 -> null; any fp64 operand promotes to fp64 (IEEE). Null in -> null out.
+ * out->values: length*8 bytes; out->validity required iff an operand can be null. */
+int qe_eval_arith(qe_ctx* ctx, int32_t op, const qe_operand* lhs, const qe_operand* rhs,
+                  qe_column* out);
+
+/* Comparison (K2) -> QE_TYPE_BOOL bitmap. Signed int64 / IEEE fp64 (NaN: only NE true),
+ * mixed int64/fp64 compares as fp64; UTF8 supports EQ/NE against a UTF8 literal column of
+ * length 1 (byte equality). out->values: ceil(length/8) bytes. */
+int qe_eval_cmp(qe_ctx* ctx, int32_t op, const qe_operand* lhs, const qe_operand* rhs,
+                qe_column* out);
+
+/* Boolean (K3a): AND / OR (SQL three-valued), NOT, IS_NULL, IS_NOT_NULL.
+ * `rhs` is ignored (may be NULL) for the unary ops. */
+int qe_eval_bool(qe_ctx* ctx, int32_t op, const qe_column* lhs, const qe_column* rhs,
+                 qe_column* out);
+
+/* ---- SelectionExec (K3b): order-preserving compaction ----------------------------------- */
+/* Rows whose mask is true (null -> dropped) are kept, in input order. */
+int qe_filter_count(qe_ctx* ctx, const qe_column* mask, int64_t* out_count);
+/* Gathers the selected rows of every input column into outs[i] (capacity >= count;
+ * fixed-width types only). outs[i].validity is written when inputs[i] has one.
+ * *out_count receives the number of rows written (also set as outs[i].length). */
+int qe_filter_apply(qe_ctx* ctx, const qe_column* mask, const qe_column* inputs,
+                    int32_t ncols, qe_column* outs, int64_t* out_count);
+
+/* ---- aggregates ------------------------------------------------------------------------- */
+#define QE_AGG_SUM 1
+#define QE_AGG_MIN 2
+#define QE_AGG_MAX 3        /* MaxAccumulator semantics, K:538-561 */
+#define QE_AGG_COUNT 4      /* COUNT(x): non-null rows */
+#define QE_AGG_COUNT_STAR 5 /* COUNT(*): rows */
+#define QE_AGG_AVG 6        /* fp64 SUM / COUNT */
+
+/* Global (no GROUP BY) aggregate of one column (K4a), all functions in one pass.
+ * min/max follow MaxAccumulator (K:538-561): nulls skipped; the first non-null value
+ * seeds; replaced only on strictly greater (less) => a NaN seed is sticky, a later NaN
+ * never wins, +0.0/-0.0 ties keep the earliest. `valid` = 1 iff count > 0. */
+typedef struct qe_global_agg {
+  int64_t rows;   /* COUNT(*) over rows passing the mask */
+  int64_t count;  /* COUNT(x) */
+  int32_t type;   /* input type: INT64 or FLOAT64 */
+  int32_t valid;  /* SUM/MIN/MAX/AVG non-null */
+  int64_t sum;    /* int64 value, or fp64 bits */
+  int64_t min;    /* int64 value, or fp64 bits */
+  int64_t max;    /* int64 value, or fp64 bits */
+  double avg;
+} qe_global_agg;
+int qe_agg_global(qe_ctx* ctx, const qe_column* col, const qe_column* mask /*nullable*/,
+                  qe_global_agg* out);
+
+/* ---- HashAggregateExec (K4b) ------------------------------------------------------------ */
+/* Group keys: 0..4 columns. One key of any fixed-width type, or several narrow keys
+ * (uint8/int32/date32/bool) whose widths + one null bit each fit in 63 bits. A null key
+ * is a group of its own (List.equals semantics, K:621-627). Group order is unspecified
+ * (HashMap iteration, K:639). */
+#define QE_MAX_KEYS 4
+#define QE_MAX_AGGS 8
+#define QE_MAX_COLS 8
+#define QE_MAX_TERMS 8
+#define QE_MAX_TOKENS 8
+
+typedef struct qe_agg_desc {
+  int32_t fn;         /* QE_AGG_* */
+  int32_t input_type; /* INT64 or FLOAT64 (ignored for COUNT_STAR; AVG accumulates fp64) */
+} qe_agg_desc;
+
+typedef struct qe_hashagg qe_hashagg;
+
+int qe_hashagg_create(qe_ctx* ctx, int32_t nkeys, const int32_t* key_types, int32_t naggs,
+                      const qe_agg_desc* aggs, int64_t expected_groups, qe_hashagg** out);
+int qe_hashagg_destroy(qe_hashagg* agg);
+/* Forget all groups (keeps allocations). */
+int qe_hashagg_reset(qe_hashagg* agg);
+
+/* One input batch: per-row keys and pre-evaluated aggregate inputs (agg_inputs[j] is the
+ * column of aggregate j; ignored for COUNT_STAR, may be a zeroed struct). `mask` (BOOL,
+ * nullable pointer) selects rows. Row indices continue across calls in call order: they
+ * define "first"/"earliest" for MIN/MAX ties exactly like the reference's batch loop. */
+int qe_hashagg_update(qe_hashagg* agg, const qe_column* keys, const qe_column* agg_inputs,
+                      const qe_column* mask);
+
+/* Fused filter -> project -> partial aggregate over the columns of one batch, one pass
+ * over HBM. Predicate = AND of terms (col CMP literal | col CMP col) and optional BOOL mask
+ * column; keys are column slots; each aggregate input is a postfix program over column
+ * slots and literals (tokens below). Semantics are those of composing
+ * SelectionExec -> ProjectionExec -> HashAggregateExec with the per-family functions. */
+#define QE_TOK_COL 1 /* push column slot `arg` */
+#define QE_TOK_LIT 2 /* push literal */
+#define QE_TOK_ADD 3
+#define QE_TOK_SUB 4
+#define QE_TOK_MUL 5
+#define QE_TOK_DIV 6
+
+typedef struct qe_pred_term {
+  int32_t col;     /* column slot (lhs) */
+  int32_t op;      /* QE_OP_EQ..QE_OP_GE */
+  int32_t rhs_col; /* column slot, or -1 => compare against `lit` */
+  int32_t reserved;
+  qe_scalar lit;
+} qe_pred_term;
+
+typedef struct qe_token {
+  int32_t op;  /* QE_TOK_* */
+  int32_t arg; /* column slot for QE_TOK_COL */
+  qe_scalar lit;
+} qe_token;
+
+typedef struct qe_agg_program {
+  int32_t ntokens; /* 0 for COUNT_STAR */
+  int32_t reserved;
+  qe_token tokens[QE_MAX_TOKENS];
+} qe_agg_program;
+
+typedef struct qe_fused_spec {
+  int32_t mask_col; /* BOOL column slot used as selection (null -> dropped), or -1 */
+  int32_t nterms;
+  qe_pred_term terms[QE_MAX_TERMS];
+  int32_t key_cols[QE_MAX_KEYS];
+  qe_agg_program inputs[QE_MAX_AGGS];
+} qe_fused_spec;
+
+int qe_hashagg_update_fused(qe_hashagg* agg, const qe_column* cols, int32_t ncols,
+                            const qe_fused_spec* spec);
+
+/* Number of groups so far (synchronises). */
+int qe_hashagg_num_groups(qe_hashagg* agg, int64_t* out);
+/* Materialise the single output batch (K:635-650): key columns then one column per
+ * aggregate. out_keys[i]/out_aggs[j] must hold num_groups rows; validity buffers are
+ * written when non-NULL (required for nullable results: any key, SUM/MIN/MAX/AVG).
+ * Output types: keys as declared; SUM/MIN/MAX as input type; COUNT/COUNT_STAR int64;
+ * AVG fp64. */
+int qe_hashagg_finalize(qe_hashagg* agg, qe_column* out_keys, qe_column* out_aggs,
+                        int64_t* out_groups);
+
+/* Two-phase / multi-GPU aggregate (K:1309-1325 pattern):
+ * export the partial groups bucketed by destination partition = hash(key) mod nparts
+ * as fixed-size records, then import records (from any rank) into another state. */
+int qe_hashagg_record_bytes(qe_hashagg* agg, int64_t* out);
+/* counts[p] = records for partition p (host array of nparts, synchronises). */
+int qe_hashagg_export_counts(qe_hashagg* agg, int32_t nparts, int64_t* counts);
+/* Writes all records into `dst` (device, sum(counts)*record_bytes), partition-major in
+ * partition order, matching the counts of the preceding export_counts call. */
+int qe_hashagg_export(qe_hashagg* agg, int32_t nparts, void* dst);
+/* Merge `nrecords` records (device) into this state (combine semantics per aggregate). */
+int qe_hashagg_import(qe_hashagg* agg, const void* records, int64_t nrecords);
+
+/* Offset added to row indices of the next update (for shards of one logical stream). */
+int qe_hashagg_set_row_base(qe_hashagg* agg, int64_t row_base);
+
+/* Measurement hook: device time (HIP events on the ctx stream) of the aggregation kernel
+ * launches made by the last update call, and how many launches it took (1 unless the table
+ * had to grow and deferred rows were re-applied). */
+int qe_hashagg_last_kernel_time(qe_hashagg* agg, double* ms, int32_t* launches);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* QE_HIP_H */

@@ -1,0 +1,293 @@
+/*
+ * ORACLE (test infrastructure + timed CPU baseline only — never linked into the product).
+ *
+ * Reference-faithful C restatement of the kquerydiy CPU path for the headline query
+ *   SELECT k, SUM(a+b), COUNT(*), MIN(a), MAX(b) FROM t WHERE a > K GROUP BY k
+ * as the reference's operator chain would execute it (folkol/query-engines kquerydiy/src/Main.kt):
+ *   - per input batch, SelectionExec materialises the selected rows (build-defined operator),
+ *   - ProjectionExec evaluates a+b into a new column (K:589-594),
+ *   - HashAggregateExec.execute loops row at a time (K:620), looks the key tuple up in a chained
+ *     hash map (java.util.HashMap, K:616/K:627: boxed key, bucket array, node per group) and calls
+ *     each Accumulator through a virtual interface (K:519-522, K:628-631) with boxed values.
+ *   - partition parallelism mirrors main() (K:1309-1325): T partitions aggregated concurrently,
+ *     then a final merge of the partial maps.
+ * The synthetic columns are regenerated here bit-for-bit (splitmix64, oracle/gen.py) before the
+ * timed region starts.
+ */
+#include <pthread.h>
+#include <stdint.h>
+#include <stdlib.h>
+#include <string.h>
+#include <time.h>
+
+static uint64_t splitmix64(uint64_t x) {
+  uint64_t z = x + 0x9E3779B97F4A7C15ull;
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  return z ^ (z >> 31);
+}
+static uint64_t gen_u64(uint64_t seed, uint64_t col, uint64_t row) {
+  return splitmix64(seed ^ (col * 0x9E3779B97F4A7C15ull) ^ row);
+}
+
+/* ---- boxed values and the Accumulator interface (K:519-522) ------------------------------ */
+typedef struct {
+  int is_null;
+  int64_t v;
+} boxed;
+
+typedef struct accumulator accumulator;
+struct accumulator {
+  void (*accumulate)(accumulator*, const boxed*);
+  int has;
+  int64_t value;
+};
+
+static void sum_acc(accumulator* a, const boxed* x) {
+  if (x->is_null) return;
+  a->value = (int64_t)((uint64_t)a->value + (uint64_t)x->v);
+  a->has = 1;
+}
+static void count_acc(accumulator* a, const boxed* x) {
+  (void)x;
+  a->value += 1;
+  a->has = 1;
+}
+static void min_acc(accumulator* a, const boxed* x) {
+  if (x->is_null) return;
+  if (!a->has || x->v < a->value) a->value = x->v;
+  a->has = 1;
+}
+static void max_acc(accumulator* a, const boxed* x) { /* MaxAccumulator K:540-557 */
+  if (x->is_null) return;
+  if (!a->has) {
+    a->value = x->v;
+    a->has = 1;
+  } else if (x->v > a->value) {
+    a->value = x->v;
+  }
+}
+
+/* ---- java.util.HashMap-like chained map keyed by the boxed key tuple (K:616, K:627) --------- */
+typedef struct node {
+  boxed key;
+  uint32_t hash;
+  struct node* next;
+  accumulator acc[4];
+} node;
+
+typedef struct {
+  node** buckets;
+  size_t nbuckets;
+  size_t size;
+} hashmap;
+
+static uint32_t box_hash(const boxed* k) { /* Long.hashCode + HashMap.hash spreading */
+  uint32_t h = k->is_null ? 0u : (uint32_t)(k->v ^ ((uint64_t)k->v >> 32));
+  return h ^ (h >> 16);
+}
+
+static void map_init(hashmap* m) {
+  m->nbuckets = 16;
+  m->buckets = (node**)calloc(m->nbuckets, sizeof(node*));
+  m->size = 0;
+}
+
+static void map_grow(hashmap* m) {
+  size_t nb = m->nbuckets * 2;
+  node** b = (node**)calloc(nb, sizeof(node*));
+  for (size_t i = 0; i < m->nbuckets; ++i) {
+    node* n = m->buckets[i];
+    while (n) {
+      node* nx = n->next;
+      size_t j = n->hash & (nb - 1);
+      n->next = b[j];
+      b[j] = n;
+      n = nx;
+    }
+  }
+  free(m->buckets);
+  m->buckets = b;
+  m->nbuckets = nb;
+}
+
+static node* map_get_or_put(hashmap* m, const boxed* key) {
+  uint32_t h = box_hash(key);
+  node* n = m->buckets[h & (m->nbuckets - 1)];
+  for (; n; n = n->next)
+    if (n->hash == h && n->key.is_null == key->is_null && (key->is_null || n->key.v == key->v)) return n;
+  n = (node*)calloc(1, sizeof(node));
+  n->key = *key;
+  n->hash = h;
+  n->acc[0].accumulate = sum_acc;
+  n->acc[1].accumulate = count_acc;
+  n->acc[2].accumulate = min_acc;
+  n->acc[3].accumulate = max_acc;
+  size_t b = h & (m->nbuckets - 1);
+  n->next = m->buckets[b];
+  m->buckets[b] = n;
+  if (++m->size > m->nbuckets * 3 / 4) map_grow(m);
+  return n;
+}
+
+static void map_free(hashmap* m) {
+  for (size_t i = 0; i < m->nbuckets; ++i) {
+    node* n = m->buckets[i];
+    while (n) {
+      node* nx = n->next;
+      free(n);
+      n = nx;
+    }
+  }
+  free(m->buckets);
+}
+
+/* ---- one partition: batches of BATCH rows through Selection -> Projection -> HashAggregate ---- */
+#define BATCH 65536
+
+typedef struct {
+  const int64_t *k, *a, *b;
+  int64_t n, threshold;
+  hashmap map;
+} part;
+
+static void run_partition(part* p) {
+  int64_t* sk = (int64_t*)malloc(BATCH * sizeof(int64_t));
+  int64_t* sa = (int64_t*)malloc(BATCH * sizeof(int64_t));
+  int64_t* sb = (int64_t*)malloc(BATCH * sizeof(int64_t));
+  int64_t* proj = (int64_t*)malloc(BATCH * sizeof(int64_t));
+  map_init(&p->map);
+  for (int64_t s = 0; s < p->n; s += BATCH) {
+    const int64_t m = p->n - s < BATCH ? p->n - s : BATCH;
+    /* SelectionExec: evaluate predicate, materialise selected rows */
+    int64_t c = 0;
+    for (int64_t i = 0; i < m; ++i) {
+      if (p->a[s + i] > p->threshold) {
+        sk[c] = p->k[s + i];
+        sa[c] = p->a[s + i];
+        sb[c] = p->b[s + i];
+        ++c;
+      }
+    }
+    /* ProjectionExec: a + b (JVM Long wrap) */
+    for (int64_t i = 0; i < c; ++i) proj[i] = (int64_t)((uint64_t)sa[i] + (uint64_t)sb[i]);
+    /* HashAggregateExec row loop (K:620-631) */
+    for (int64_t i = 0; i < c; ++i) {
+      boxed key = {0, sk[i]};
+      node* n = map_get_or_put(&p->map, &key);
+      boxed in0 = {0, proj[i]}, in1 = {0, 1}, in2 = {0, sa[i]}, in3 = {0, sb[i]};
+      n->acc[0].accumulate(&n->acc[0], &in0);
+      n->acc[1].accumulate(&n->acc[1], &in1);
+      n->acc[2].accumulate(&n->acc[2], &in2);
+      n->acc[3].accumulate(&n->acc[3], &in3);
+    }
+  }
+  free(sk);
+  free(sa);
+  free(sb);
+  free(proj);
+}
+
+static void* part_main(void* arg) {
+  run_partition((part*)arg);
+  return NULL;
+}
+
+typedef struct {
+  int64_t *k, *a, *b;
+  int64_t row0, n, nkeys;
+  uint64_t seed;
+} gen_job;
+
+static void* gen_main(void* arg) { /* untimed: regenerate the synthetic rows (oracle/gen.py) */
+  gen_job* g = (gen_job*)arg;
+  for (int64_t i = 0; i < g->n; ++i) {
+    const uint64_t r = (uint64_t)(g->row0 + i);
+    g->k[i] = (int64_t)(gen_u64(g->seed, 0, r) % (uint64_t)g->nkeys);
+    g->a[i] = (int64_t)(gen_u64(g->seed, 1, r) % (1ull << 20));
+    g->b[i] = (int64_t)(gen_u64(g->seed, 2, r) % (1ull << 20));
+  }
+  return NULL;
+}
+
+typedef struct {
+  int64_t key;
+  int64_t sum, count, min, max;
+} qe_group_out;
+
+static double now_s(void) {
+  struct timespec ts;
+  clock_gettime(CLOCK_MONOTONIC, &ts);
+  return ts.tv_sec + ts.tv_nsec * 1e-9;
+}
+
+/* Returns seconds spent in the (timed) query; fills out[] (cap entries) and *ngroups.
+ * Data: k = u0 % 1024, a = u1 % 2^20, b = u2 % 2^20 for rows row0..row0+rows-1. */
+double qe_cpu_c4(int64_t row0, int64_t rows, uint64_t seed, int threads, int64_t threshold, int64_t nkeys,
+                 qe_group_out* out, int64_t cap, int64_t* ngroups) {
+  if (threads < 1) threads = 1;
+  int64_t* k = (int64_t*)malloc(rows * sizeof(int64_t));
+  int64_t* a = (int64_t*)malloc(rows * sizeof(int64_t));
+  int64_t* b = (int64_t*)malloc(rows * sizeof(int64_t));
+  part* parts = (part*)calloc(threads, sizeof(part));
+  pthread_t* tid = (pthread_t*)calloc(threads, sizeof(pthread_t));
+  const int64_t per = (rows + threads - 1) / threads;
+  gen_job* jobs = (gen_job*)calloc(threads, sizeof(gen_job));
+  for (int t = 0; t < threads; ++t) {
+    const int64_t s = t * per, e = (s + per < rows) ? s + per : rows;
+    jobs[t] = (gen_job){k + s, a + s, b + s, row0 + s, e > s ? e - s : 0, nkeys, seed};
+    pthread_create(&tid[t], NULL, gen_main, &jobs[t]);
+  }
+  for (int t = 0; t < threads; ++t) pthread_join(tid[t], NULL);
+  free(jobs);
+  const double t0 = now_s();
+  for (int t = 0; t < threads; ++t) {
+    const int64_t s = t * per, e = (s + per < rows) ? s + per : rows;
+    parts[t].k = k + s;
+    parts[t].a = a + s;
+    parts[t].b = b + s;
+    parts[t].n = e > s ? e - s : 0;
+    parts[t].threshold = threshold;
+    pthread_create(&tid[t], NULL, part_main, &parts[t]);
+  }
+  for (int t = 0; t < threads; ++t) pthread_join(tid[t], NULL);
+  /* final merge of the partial maps, in partition order (K:1314-1325) */
+  hashmap fin;
+  map_init(&fin);
+  for (int t = 0; t < threads; ++t) {
+    for (size_t i = 0; i < parts[t].map.nbuckets; ++i) {
+      for (node* n = parts[t].map.buckets[i]; n; n = n->next) {
+        node* f = map_get_or_put(&fin, &n->key);
+        boxed s0 = {0, n->acc[0].value}, s2 = {!n->acc[2].has, n->acc[2].value}, s3 = {!n->acc[3].has, n->acc[3].value};
+        f->acc[0].accumulate(&f->acc[0], &s0);
+        f->acc[1].value += n->acc[1].value;
+        f->acc[1].has = 1;
+        f->acc[2].accumulate(&f->acc[2], &s2);
+        f->acc[3].accumulate(&f->acc[3], &s3);
+      }
+    }
+  }
+  const double t1 = now_s();
+  int64_t g = 0;
+  for (size_t i = 0; i < fin.nbuckets; ++i) {
+    for (node* n = fin.buckets[i]; n; n = n->next) {
+      if (g < cap && out) {
+        out[g].key = n->key.v;
+        out[g].sum = n->acc[0].value;
+        out[g].count = n->acc[1].value;
+        out[g].min = n->acc[2].value;
+        out[g].max = n->acc[3].value;
+      }
+      ++g;
+    }
+  }
+  *ngroups = g;
+  map_free(&fin);
+  for (int t = 0; t < threads; ++t) map_free(&parts[t].map);
+  free(parts);
+  free(tid);
+  free(k);
+  free(a);
+  free(b);
+  return t1 - t0;
+}

@@ -1,0 +1,277 @@
+// SelectionExec (K3b): order-preserving compaction of the rows whose predicate is true.
+// Build-defined operator (absent in the reference; interface PhysicalPlan K:442-446):
+// a null predicate drops the row; the output keeps input row order (bit-exact parity).
+//
+// Algorithm (no atomics on the data path, deterministic):
+//   1. k_tile_count : per 8192-row tile, popcount(mask & validity)      -> tile_counts
+//   2. k_scan       : exclusive scan of tile counts (one block)          -> tile_offsets, total
+//   3. k_compact    : per tile, 4 rows per lane; the lane's rank inside the wave comes from
+//                     the 3 bit-planes of its per-lane count via ballot + mbcnt; wave totals are
+//                     scanned through LDS; selected values are written at their final position.
+// Traffic per input row: mask 1/8 B twice + every gathered column once + selected rows written.
+#include "qe_internal.hpp"
+
+namespace qe {
+
+constexpr int FT_THREADS = 256;
+constexpr int FT_ROWS_PER_LANE = 4;
+constexpr int FT_ITERS = 8;
+constexpr int64_t FT_TILE = (int64_t)FT_THREADS * FT_ROWS_PER_LANE * FT_ITERS;  // 8192 rows
+
+__device__ __forceinline__ uint8_t sel_byte(const uint8_t* __restrict__ mv, const uint8_t* __restrict__ ml,
+                                            int64_t byte, int64_t n) {
+  uint8_t s = mv[byte];
+  if (ml) s &= ml[byte];
+  const int64_t r0 = byte << 3;
+  if (r0 + 8 > n) s &= (uint8_t)((1u << (n - r0)) - 1);
+  return s;
+}
+
+__global__ void __launch_bounds__(FT_THREADS) k_tile_count(const uint8_t* __restrict__ mv,
+                                                           const uint8_t* __restrict__ ml, int64_t n,
+                                                           int64_t* __restrict__ tile_counts) {
+  __shared__ int64_t part[FT_THREADS / 64];
+  const int64_t tile = blockIdx.x;
+  const int64_t nbytes = (n + 7) >> 3;
+  const int64_t b0 = tile * (FT_TILE / 8);  // 1024 bytes per tile, 4 per thread
+  int c = 0;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const int64_t b = b0 + k * FT_THREADS + threadIdx.x;
+    if (b < nbytes) c += __popc(sel_byte(mv, ml, b, n));
+  }
+  for (int off = 32; off > 0; off >>= 1) c += __shfl_xor(c, off);
+  if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = c;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    int64_t t = 0;
+    for (int w = 0; w < FT_THREADS / 64; ++w) t += part[w];
+    tile_counts[tile] = t;
+  }
+}
+
+// Exclusive scan of `n` int64 counts with one 1024-thread block; writes total to out[n].
+__global__ void __launch_bounds__(1024) k_scan(const int64_t* __restrict__ in, int64_t* __restrict__ out,
+                                               int64_t n) {
+  __shared__ int64_t wsum[16];
+  __shared__ int64_t carry;
+  if (threadIdx.x == 0) carry = 0;
+  __syncthreads();
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  for (int64_t base = 0; base < n; base += 1024) {
+    const int64_t i = base + threadIdx.x;
+    const int64_t v = i < n ? in[i] : 0;
+    int64_t x = v;  // inclusive wave scan
+    for (int off = 1; off < 64; off <<= 1) {
+      const int64_t y = __shfl_up(x, off);
+      if (lane >= off) x += y;
+    }
+    if (lane == 63) wsum[wid] = x;
+    __syncthreads();
+    int64_t wprefix = 0;
+    for (int w = 0; w < wid; ++w) wprefix += wsum[w];
+    const int64_t c = carry;
+    if (i < n) out[i] = c + wprefix + x - v;
+    __syncthreads();
+    if (threadIdx.x == 1023) carry = c + wprefix + x;
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) out[n] = carry;
+}
+
+int exclusive_scan_i64(qe_ctx* ctx, const int64_t* in, int64_t* out, int64_t n) {
+  hipLaunchKernelGGL(k_scan, dim3(1), dim3(1024), 0, ctx->stream, in, out, n);
+  return launch_check("k_scan");
+}
+
+struct GatherCol {
+  const void* in;
+  const uint8_t* in_valid;
+  void* out;
+  uint32_t* out_valid;  // zeroed by the host; bits set with atomicOr
+  int32_t width;        // 8, 4 or 1
+  int32_t pad;
+};
+
+constexpr int FT_MAX_COLS = 8;
+struct GatherArgs {
+  GatherCol cols[FT_MAX_COLS];
+  int32_t ncols;
+};
+
+__device__ __forceinline__ void gather_store(const GatherCol& c, int64_t row0, int nsel_mask, int64_t pos0,
+                                             const int (&rank)[4], bool full) {
+  // Loads the lane's 4 rows (vectorised when the tile is full) and stores the selected ones.
+  if (c.width == 8) {
+    int64_t v[4];
+    if (full) {
+      typedef long long i64x2 __attribute__((ext_vector_type(2)));
+      const i64x2* p = (const i64x2*)((const int64_t*)c.in + row0);
+      const i64x2 a = p[0], b = p[1];
+      v[0] = a.x; v[1] = a.y; v[2] = b.x; v[3] = b.y;
+    } else {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) v[j] = (nsel_mask >> j) & 1 ? ((const int64_t*)c.in)[row0 + j] : 0;
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+      if ((nsel_mask >> j) & 1) ((int64_t*)c.out)[pos0 + rank[j]] = v[j];
+  } else if (c.width == 4) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+      if ((nsel_mask >> j) & 1) ((int32_t*)c.out)[pos0 + rank[j]] = ((const int32_t*)c.in)[row0 + j];
+  } else {
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+      if ((nsel_mask >> j) & 1) ((uint8_t*)c.out)[pos0 + rank[j]] = ((const uint8_t*)c.in)[row0 + j];
+  }
+  if (c.out_valid) {
+    const uint8_t vb = c.in_valid ? (uint8_t)(c.in_valid[row0 >> 3] >> (row0 & 7)) : (uint8_t)0xF;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      if (((nsel_mask >> j) & 1) && ((vb >> j) & 1)) {
+        const int64_t p = pos0 + rank[j];
+        atomicOr(&c.out_valid[p >> 5], 1u << (p & 31));
+      }
+    }
+  }
+}
+
+__global__ void __launch_bounds__(FT_THREADS) k_compact(const uint8_t* __restrict__ mv, const uint8_t* __restrict__ ml,
+                                                        int64_t n, const int64_t* __restrict__ tile_offsets,
+                                                        GatherArgs args) {
+  __shared__ int wtot[FT_THREADS / 64];
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int64_t tile = blockIdx.x;
+  int64_t base = tile_offsets[tile];
+  const uint64_t lt = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
+  for (int it = 0; it < FT_ITERS; ++it) {
+    const int64_t row0 = tile * FT_TILE + (int64_t)it * (FT_THREADS * FT_ROWS_PER_LANE) +
+                         (int64_t)threadIdx.x * FT_ROWS_PER_LANE;
+    int sel = 0;
+    if (row0 < n) sel = (sel_byte(mv, ml, row0 >> 3, n) >> (row0 & 7)) & 0xF;
+    const int c = __popc(sel);
+    // exclusive prefix of c over lanes, from its bit planes
+    const uint64_t b0 = __ballot(c & 1), b1 = __ballot(c & 2), b2 = __ballot(c & 4);
+    const int prefix = __popcll(b0 & lt) + 2 * __popcll(b1 & lt) + 4 * __popcll(b2 & lt);
+    const int total = __popcll(b0) + 2 * __popcll(b1) + 4 * __popcll(b2);
+    if (lane == 0) wtot[wid] = total;
+    __syncthreads();
+    int woff = 0, btot = 0;
+#pragma unroll
+    for (int w = 0; w < FT_THREADS / 64; ++w) {
+      woff += w < wid ? wtot[w] : 0;
+      btot += wtot[w];
+    }
+    if (sel) {
+      int rank[4];
+      int r = 0;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        rank[j] = r;
+        r += (sel >> j) & 1;
+      }
+      const int64_t pos0 = base + woff + prefix;
+      const bool full = row0 + 4 <= n;
+      for (int k = 0; k < args.ncols; ++k) gather_store(args.cols[k], row0, sel, pos0, rank, full);
+    }
+    base += btot;
+    __syncthreads();
+  }
+}
+
+struct FilterPlan {
+  int64_t ntiles;
+  int64_t* counts;   // ntiles
+  int64_t* offsets;  // ntiles + 1
+};
+
+static int filter_prepare(qe_ctx* ctx, const qe_column* mask, FilterPlan* fp) {
+  QE_CHECK(mask && mask->type == QE_TYPE_BOOL, QE_ERR_INVALID_ARG, "mask must be a BOOL column");
+  QE_CHECK(mask->values || mask->length == 0, QE_ERR_INVALID_ARG, "null mask values");
+  const int64_t n = mask->length;
+  fp->ntiles = (int64_t)div_up((uint64_t)n, FT_TILE);
+  void* s;
+  QE_TRY(ctx_scratch(ctx, (size_t)(2 * fp->ntiles + 1) * 8, &s));
+  fp->counts = (int64_t*)s;
+  fp->offsets = fp->counts + fp->ntiles;
+  if (n == 0) {
+    QE_HIP(hipMemsetAsync(fp->offsets, 0, 8, ctx->stream));
+    return QE_OK;
+  }
+  hipLaunchKernelGGL(k_tile_count, dim3((unsigned)fp->ntiles), dim3(FT_THREADS), 0, ctx->stream,
+                     (const uint8_t*)mask->values, mask->validity, n, fp->counts);
+  QE_TRY(launch_check("k_tile_count"));
+  hipLaunchKernelGGL(k_scan, dim3(1), dim3(1024), 0, ctx->stream, fp->counts, fp->offsets, fp->ntiles);
+  return launch_check("k_scan");
+}
+
+static int read_total(qe_ctx* ctx, const FilterPlan& fp, int64_t* total) {
+  void* h;
+  QE_TRY(ctx_pinned(ctx, 8, &h));
+  QE_HIP(hipMemcpyAsync(h, fp.offsets + fp.ntiles, 8, hipMemcpyDeviceToHost, ctx->stream));
+  QE_HIP(hipStreamSynchronize(ctx->stream));
+  *total = *(int64_t*)h;
+  return QE_OK;
+}
+
+}  // namespace qe
+
+using namespace qe;
+
+extern "C" {
+
+int qe_filter_count(qe_ctx* ctx, const qe_column* mask, int64_t* out_count) {
+  QE_TRY(ctx_enter(ctx));
+  QE_CHECK(out_count, QE_ERR_INVALID_ARG, "null out_count");
+  FilterPlan fp;
+  QE_TRY(filter_prepare(ctx, mask, &fp));
+  return read_total(ctx, fp, out_count);
+}
+
+int qe_filter_apply(qe_ctx* ctx, const qe_column* mask, const qe_column* inputs, int32_t ncols, qe_column* outs,
+                    int64_t* out_count) {
+  QE_TRY(ctx_enter(ctx));
+  QE_CHECK(ncols >= 0 && ncols <= FT_MAX_COLS, QE_ERR_UNSUPPORTED, "at most %d columns per call", FT_MAX_COLS);
+  QE_CHECK(ncols == 0 || (inputs && outs), QE_ERR_INVALID_ARG, "null column arrays");
+  QE_CHECK(mask != nullptr, QE_ERR_INVALID_ARG, "null mask");
+  const int64_t n = mask->length;
+  GatherArgs args{};
+  args.ncols = ncols;
+  for (int i = 0; i < ncols; ++i) {
+    const qe_column& in = inputs[i];
+    qe_column& out = outs[i];
+    QE_CHECK(in.length == n, QE_ERR_INVALID_ARG, "column %d has %lld rows, mask %lld", i, (long long)in.length,
+             (long long)n);
+    QE_CHECK(is_fixed(in.type), QE_ERR_UNSUPPORTED, "filter: column %d type %d not supported (fixed-width only)", i,
+             in.type);
+    QE_CHECK(out.type == in.type && (out.values || out.length == 0), QE_ERR_INVALID_ARG,
+             "output %d must have the input's type", i);
+    QE_CHECK(!in.validity || out.validity, QE_ERR_INVALID_ARG, "output %d needs a validity buffer", i);
+    args.cols[i] = GatherCol{in.values, in.validity, out.values, in.validity ? (uint32_t*)out.validity : nullptr,
+                             type_width(in.type), 0};
+  }
+  FilterPlan fp;
+  QE_TRY(filter_prepare(ctx, mask, &fp));
+  int64_t total;
+  QE_TRY(read_total(ctx, fp, &total));
+  for (int i = 0; i < ncols; ++i) {
+    QE_CHECK(outs[i].length >= total, QE_ERR_CAPACITY, "output %d holds %lld rows, need %lld", i,
+             (long long)outs[i].length, (long long)total);
+    if (args.cols[i].out_valid) {
+      // atomicOr works on 32-bit words: the buffer must be 4-byte aligned and padded.
+      QE_CHECK(((uintptr_t)outs[i].validity & 3) == 0, QE_ERR_INVALID_ARG, "validity buffer must be 4-byte aligned");
+      QE_HIP(hipMemsetAsync(outs[i].validity, 0, (size_t)div_up((uint64_t)total, 32) * 4, ctx->stream));
+    }
+  }
+  if (total > 0 && ncols > 0) {
+    hipLaunchKernelGGL(k_compact, dim3((unsigned)fp.ntiles), dim3(FT_THREADS), 0, ctx->stream,
+                       (const uint8_t*)mask->values, mask->validity, n, fp.offsets, args);
+    QE_TRY(launch_check("k_compact"));
+  }
+  for (int i = 0; i < ncols; ++i) outs[i].length = total;
+  if (out_count) *out_count = total;
+  return QE_OK;
+}
+
+}  // extern "C"

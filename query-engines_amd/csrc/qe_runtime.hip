@@ -1,0 +1,222 @@
+// Context, errors, device memory and the synthetic RecordBatch generator.
+#include <stdarg.h>
+#include <stdio.h>
+
+#include "qe_internal.hpp"
+
+namespace qe {
+
+static thread_local std::string g_last_error;
+
+int fail(int code, const char* fmt, ...) {
+  char buf[1024];
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(buf, sizeof(buf), fmt, ap);
+  va_end(ap);
+  g_last_error = buf;
+  return code;
+}
+
+void clear_error() { g_last_error.clear(); }
+
+int ctx_enter(qe_ctx* ctx) {
+  QE_CHECK(ctx != nullptr, QE_ERR_INVALID_ARG, "null qe_ctx");
+  QE_HIP(hipSetDevice(ctx->device));
+  return QE_OK;
+}
+
+int ctx_scratch(qe_ctx* ctx, size_t bytes, void** out) {
+  if (bytes == 0) bytes = 256;
+  if (bytes > ctx->scratch_bytes) {
+    if (ctx->scratch) {
+      QE_HIP(hipStreamSynchronize(ctx->stream));
+      QE_HIP(hipFree(ctx->scratch));
+      ctx->scratch = nullptr;
+      ctx->scratch_bytes = 0;
+    }
+    size_t want = bytes < 2 * ctx->scratch_bytes ? 2 * ctx->scratch_bytes : bytes;
+    want = (want + 4095) & ~size_t(4095);
+    if (hipMalloc(&ctx->scratch, want) != hipSuccess) {
+      (void)hipGetLastError();
+      return fail(QE_ERR_OOM, "scratch allocation of %zu bytes failed", want);
+    }
+    ctx->scratch_bytes = want;
+  }
+  *out = ctx->scratch;
+  return QE_OK;
+}
+
+int ctx_pinned(qe_ctx* ctx, size_t bytes, void** out) {
+  if (bytes > ctx->pinned_bytes) {
+    if (ctx->pinned) QE_HIP(hipHostFree(ctx->pinned));
+    ctx->pinned = nullptr;
+    size_t want = bytes < 4096 ? 4096 : bytes;
+    QE_HIP(hipHostMalloc(&ctx->pinned, want, hipHostMallocDefault));
+    ctx->pinned_bytes = want;
+  }
+  *out = ctx->pinned;
+  return QE_OK;
+}
+
+int launch_check(const char* what) {
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return fail(QE_ERR_DEVICE, "launch of %s failed: %s", what, hipGetErrorString(e));
+  return QE_OK;
+}
+
+// ---- generator ------------------------------------------------------------------------------
+// One thread = 8 consecutive rows = one validity byte (restated in oracle/gen.py).
+__device__ __forceinline__ int64_t gen_value(int32_t dist, int64_t param, uint64_t u) {
+  switch (dist) {
+    case QE_GEN_MOD: return (int64_t)(u % (uint64_t)param);
+    case QE_GEN_RAW: return (int64_t)u;
+    case QE_GEN_UNIT53: return f64_bits((double)(u >> 11) * 0x1p-42 - 1024.0);
+    default: return f64_bits((double)(u % (uint64_t)param) * 0.01);  // QE_GEN_MOD_F64
+  }
+}
+
+__global__ void __launch_bounds__(256) k_generate(void* __restrict__ values, uint8_t* __restrict__ validity,
+                                                  int32_t type, int32_t dist, int64_t param, uint64_t seed,
+                                                  uint64_t col, int64_t row0, int64_t n, int32_t null_permille) {
+  const int64_t nbytes = (n + 7) >> 3;
+  for (int64_t b = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; b < nbytes;
+       b += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t i0 = b << 3;
+    uint8_t vbits = 0, bbits = 0;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int64_t i = i0 + j;
+      if (i < n) {
+        const uint64_t row = (uint64_t)(row0 + i);
+        const uint64_t u = gen_u64(seed, col, row);
+        const int64_t v = gen_value(dist, param, u);
+        switch (type) {
+          case QE_TYPE_INT64:
+          case QE_TYPE_FLOAT64: ((int64_t*)values)[i] = v; break;
+          case QE_TYPE_INT32:
+          case QE_TYPE_DATE32: ((int32_t*)values)[i] = (int32_t)v; break;
+          case QE_TYPE_UINT8: ((uint8_t*)values)[i] = (uint8_t)v; break;
+          case QE_TYPE_BOOL: bbits |= (uint8_t)((v & 1) << j); break;
+        }
+        bool valid = true;
+        if (null_permille > 0) valid = (gen_u64(seed, col + 0x1000, row) % 1000) >= (uint64_t)null_permille;
+        vbits |= (uint8_t)(valid << j);
+      }
+    }
+    if (type == QE_TYPE_BOOL) ((uint8_t*)values)[b] = bbits;
+    if (validity) validity[b] = vbits;
+  }
+}
+
+}  // namespace qe
+
+using namespace qe;
+
+extern "C" {
+
+const char* qe_last_error(void) { return g_last_error.c_str(); }
+int qe_abi_version(void) { return QE_ABI_VERSION; }
+
+int qe_ctx_create(int device, void* stream, qe_ctx** out) {
+  clear_error();
+  QE_CHECK(out != nullptr, QE_ERR_INVALID_ARG, "null out");
+  int ndev = 0;
+  QE_HIP(hipGetDeviceCount(&ndev));
+  QE_CHECK(device >= 0 && device < ndev, QE_ERR_INVALID_ARG, "device %d out of range (%d devices)", device, ndev);
+  QE_HIP(hipSetDevice(device));
+  qe_ctx* c = new qe_ctx();
+  c->device = device;
+  if (stream) {
+    c->stream = (hipStream_t)stream;
+  } else {
+    hipError_t e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
+    if (e != hipSuccess) {
+      delete c;
+      return fail(QE_ERR_DEVICE, "hipStreamCreate: %s", hipGetErrorString(e));
+    }
+    c->own_stream = true;
+  }
+  hipDeviceProp_t prop;
+  if (hipGetDeviceProperties(&prop, device) == hipSuccess) c->num_cus = prop.multiProcessorCount;
+  *out = c;
+  return QE_OK;
+}
+
+int qe_ctx_destroy(qe_ctx* ctx) {
+  if (!ctx) return QE_OK;
+  (void)hipSetDevice(ctx->device);
+  (void)hipStreamSynchronize(ctx->stream);
+  if (ctx->scratch) (void)hipFree(ctx->scratch);
+  if (ctx->pinned) (void)hipHostFree(ctx->pinned);
+  if (ctx->own_stream) (void)hipStreamDestroy(ctx->stream);
+  delete ctx;
+  return QE_OK;
+}
+
+void* qe_ctx_stream(qe_ctx* ctx) { return ctx ? (void*)ctx->stream : nullptr; }
+
+int qe_ctx_synchronize(qe_ctx* ctx) {
+  QE_TRY(ctx_enter(ctx));
+  QE_HIP(hipStreamSynchronize(ctx->stream));
+  return QE_OK;
+}
+
+int qe_device_alloc(qe_ctx* ctx, size_t bytes, void** out) {
+  QE_TRY(ctx_enter(ctx));
+  QE_CHECK(out != nullptr, QE_ERR_INVALID_ARG, "null out");
+  if (hipMalloc(out, bytes ? bytes : 1) != hipSuccess) {
+    (void)hipGetLastError();
+    return fail(QE_ERR_OOM, "hipMalloc(%zu) failed", bytes);
+  }
+  return QE_OK;
+}
+
+int qe_device_free(qe_ctx* ctx, void* ptr) {
+  QE_TRY(ctx_enter(ctx));
+  if (ptr) QE_HIP(hipFree(ptr));
+  return QE_OK;
+}
+
+int qe_copy_to_device(qe_ctx* ctx, void* dst, const void* src, size_t bytes) {
+  QE_TRY(ctx_enter(ctx));
+  QE_HIP(hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, ctx->stream));
+  QE_HIP(hipStreamSynchronize(ctx->stream));
+  return QE_OK;
+}
+
+int qe_copy_to_host(qe_ctx* ctx, void* dst, const void* src, size_t bytes) {
+  QE_TRY(ctx_enter(ctx));
+  QE_HIP(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, ctx->stream));
+  QE_HIP(hipStreamSynchronize(ctx->stream));
+  return QE_OK;
+}
+
+int qe_generate(qe_ctx* ctx, qe_column* out, int32_t dist, int64_t param, uint64_t seed, uint64_t col,
+                int64_t row0, int32_t null_permille) {
+  QE_TRY(ctx_enter(ctx));
+  QE_CHECK(out && out->values, QE_ERR_INVALID_ARG, "null output column");
+  QE_CHECK(out->length >= 0, QE_ERR_INVALID_ARG, "negative length");
+  QE_CHECK(is_fixed(out->type) || out->type == QE_TYPE_BOOL, QE_ERR_UNSUPPORTED,
+           "generator: unsupported type %d", out->type);
+  QE_CHECK(dist >= QE_GEN_MOD && dist <= QE_GEN_MOD_F64, QE_ERR_INVALID_ARG, "bad distribution %d", dist);
+  QE_CHECK((dist != QE_GEN_MOD && dist != QE_GEN_MOD_F64) || param > 0, QE_ERR_INVALID_ARG,
+           "QE_GEN_MOD needs param > 0");
+  const bool is_f = dist == QE_GEN_UNIT53 || dist == QE_GEN_MOD_F64;
+  QE_CHECK(is_f == (out->type == QE_TYPE_FLOAT64), QE_ERR_INVALID_ARG,
+           "distribution %d does not match column type %d", dist, out->type);
+  QE_CHECK(null_permille == 0 || out->validity, QE_ERR_INVALID_ARG, "nulls requested without validity buffer");
+  if (out->length == 0) return QE_OK;
+  const int64_t nbytes = (out->length + 7) >> 3;
+  const int64_t blocks = (int64_t)div_up(nbytes, 256);
+  const int grid = (int)(blocks < 16384 ? blocks : 16384);
+  hipLaunchKernelGGL(k_generate, dim3(grid), dim3(256), 0, ctx->stream, out->values,
+                     null_permille > 0 ? out->validity : nullptr, out->type, dist, param, seed, col, row0,
+                     out->length, null_permille);
+  QE_TRY(launch_check("k_generate"));
+  if (out->validity && null_permille == 0)
+    QE_HIP(hipMemsetAsync(out->validity, 0xFF, (size_t)nbytes, ctx->stream));
+  return QE_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,383 @@
+"""Physical operators (Main.kt:442-446, :564-660) over device-resident RecordBatches.
+
+``ScanExec`` / ``ProjectionExec`` / ``HashAggregateExec`` keep the reference's names, arguments
+and pull-based ``execute()`` sequence; ``SelectionExec`` is the north star's filter operator
+(absent from the reference). ``fuse`` is the planner hook (the reference's selection
+point is createPhysicalPlan, Main.kt:680-706): it rewrites HashAggregateExec over a
+Selection/Projection/Scan chain into ``FusedHashAggregateExec`` — one HIP kernel pass over HBM.
+"""
+from __future__ import annotations
+
+from typing import Iterator, List, Optional, Sequence
+
+from . import native as N
+from .aggregate import HashAggregateState, output_type
+from .columnar import DeviceColumn, Field, RecordBatch, Schema
+from .expressions import (
+    AggregateExpression,
+    AndExpression,
+    ArithmeticExpression,
+    ColumnExpression,
+    ComparisonExpression,
+    Expression,
+    LiteralDoubleExpression,
+    LiteralLongExpression,
+    ScalarColumn,
+)
+
+
+class PhysicalPlan:
+    def schema(self) -> Schema:
+        raise NotImplementedError
+
+    def execute(self) -> Iterator[RecordBatch]:
+        raise NotImplementedError
+
+    def children(self) -> List["PhysicalPlan"]:
+        raise NotImplementedError
+
+
+class ScanExec(PhysicalPlan):
+    """Main.kt:564-580."""
+
+    def __init__(self, ds, projection: Sequence[str]):
+        self.ds = ds
+        self.projection = list(projection)
+
+    def schema(self) -> Schema:
+        return self.ds.schema().select(self.projection)
+
+    def execute(self) -> Iterator[RecordBatch]:
+        return self.ds.scan(self.projection)
+
+    def children(self) -> List[PhysicalPlan]:
+        return []
+
+    def __repr__(self) -> str:
+        return f"ScanExec: schema={self.schema()}, projection={self.projection}"
+
+
+class ProjectionExec(PhysicalPlan):
+    """Main.kt:582-603: per batch, evaluate every expression; row count and order unchanged."""
+
+    def __init__(self, input: PhysicalPlan, schema: Schema, expr: Sequence[Expression]):  # noqa: A002
+        self.input = input
+        self._schema = schema
+        self.expr = list(expr)
+
+    def schema(self) -> Schema:
+        return self._schema
+
+    def execute(self) -> Iterator[RecordBatch]:
+        for batch in self.input.execute():
+            yield RecordBatch(self._schema, [e.evaluate(batch) for e in self.expr])
+
+    def children(self) -> List[PhysicalPlan]:
+        return [self.input]
+
+    def __repr__(self) -> str:
+        return f"ProjectionExec: {self.expr}"
+
+
+class SelectionExec(PhysicalPlan):
+    """Filter (build-defined): keeps rows whose predicate is true (null -> dropped), in order.
+    K3b order-preserving compaction (qe_filter_apply)."""
+
+    def __init__(self, input: PhysicalPlan, expr: Expression):  # noqa: A002
+        self.input = input
+        self.expr = expr
+
+    def schema(self) -> Schema:
+        return self.input.schema()
+
+    def execute(self) -> Iterator[RecordBatch]:
+        for batch in self.input.execute():
+            mask = self.expr.evaluate(batch)
+            if not isinstance(mask, DeviceColumn) or mask.type != N.TYPE_BOOL:
+                raise N.IllegalStateException(N.QE_ERR_UNSUPPORTED, "selection predicate must be BOOLEAN")
+            yield filter_batch(batch, mask)
+
+    def children(self) -> List[PhysicalPlan]:
+        return [self.input]
+
+    def __repr__(self) -> str:
+        return f"SelectionExec: {self.expr}"
+
+
+def filter_batch(batch: RecordBatch, mask: DeviceColumn) -> RecordBatch:
+    ctx = mask.ctx
+    cnt = N.C.c_int64()
+    mc = mask.as_c()
+    N.check(N.lib().qe_filter_count(ctx.handle, N.C.byref(mc), N.C.byref(cnt)))
+    n = cnt.value
+    cols = batch.fields
+    for c in cols:
+        if not isinstance(c, DeviceColumn):
+            raise N.IllegalStateException(N.QE_ERR_UNSUPPORTED, "selection input must be device columns")
+    outs = [DeviceColumn.empty(c.type, n, c.nullable, ctx=ctx) for c in cols]
+    done: list = [None] * len(cols)
+    # qe_filter_apply gathers up to 8 columns per launch
+    for s in range(0, len(cols), N.MAX_COLS):
+        part = cols[s:s + N.MAX_COLS]
+        ins = (N.QeColumn * len(part))(*[c.as_c() for c in part])
+        os_ = (N.QeColumn * len(part))(*[o.as_c() for o in outs[s:s + N.MAX_COLS]])
+        got = N.C.c_int64()
+        N.check(N.lib().qe_filter_apply(ctx.handle, N.C.byref(mc), ins, len(part), os_, N.C.byref(got)))
+        for k, o in enumerate(outs[s:s + N.MAX_COLS]):
+            o.length = got.value
+            done[s + k] = o
+    return RecordBatch(batch.schema, done)
+
+
+class HashAggregateExec(PhysicalPlan):
+    """Main.kt:605-660: consumes every input batch, emits ONE batch of group columns then
+    aggregate columns. Row-at-a-time HashMap + Accumulator objects are replaced by the device
+    hash-aggregate (K4b). A global aggregate over empty input yields 0 rows (Main.kt:637)."""
+
+    def __init__(self, input: PhysicalPlan, groupExpr: Sequence[Expression],  # noqa: A002,N803
+                 aggregateExpr: Sequence[AggregateExpression], schema: Schema,  # noqa: N803
+                 expected_groups: int = 1024):
+        self.input = input
+        self.groupExpr = list(groupExpr)
+        self.aggregateExpr = list(aggregateExpr)
+        self._schema = schema
+        self.expected_groups = expected_groups
+        self.state: Optional[HashAggregateState] = None
+
+    def schema(self) -> Schema:
+        return self._schema
+
+    def children(self) -> List[PhysicalPlan]:
+        return [self.input]
+
+    def partial_state(self) -> Optional[HashAggregateState]:
+        """Runs the aggregation and returns the device state (for the two-phase exchange)."""
+        state = None
+        for batch in self.input.execute():
+            keys = [e.evaluate(batch) for e in self.groupExpr]
+            inputs = [a.inputExpression().evaluate(batch) if a.inputExpression() is not None else None
+                      for a in self.aggregateExpr]
+            for c in keys + [i for i in inputs if i is not None]:
+                if not isinstance(c, DeviceColumn):
+                    raise N.IllegalStateException(N.QE_ERR_UNSUPPORTED, "aggregate inputs must be device columns")
+            if state is None:
+                ctx = (keys + [i for i in inputs if i is not None])[0].ctx if (keys or any(inputs)) else None
+                if ctx is None:
+                    raise N.IllegalStateException(N.QE_ERR_UNSUPPORTED, "COUNT(*) needs an input column")
+                state = HashAggregateState(
+                    ctx, [k.type for k in keys],
+                    [(a.fn, (i.type if i is not None else N.TYPE_INT64)) for a, i in zip(self.aggregateExpr, inputs)],
+                    self.expected_groups)
+            state.update(keys, [i if a.fn != N.AGG_COUNT_STAR else None for a, i in zip(self.aggregateExpr, inputs)])
+        self.state = state
+        return state
+
+    def execute(self) -> Iterator[RecordBatch]:
+        state = self.partial_state()
+        yield finalize_batch(state, self._schema, self.groupExpr, self.aggregateExpr)
+
+    def __repr__(self) -> str:
+        return f"HashAggregateExec: groupExpr={self.groupExpr}, aggrExpr={self.aggregateExpr}"
+
+
+def finalize_batch(state: Optional[HashAggregateState], schema: Schema, groupExpr, aggregateExpr) -> RecordBatch:  # noqa: N803
+    if state is None:  # no input batch at all: empty output
+        from .columnar import Context
+
+        ctx = Context.get(0)
+        cols = [DeviceColumn.empty(f.dataType if f.dataType in N.FIXED_WIDTH else N.TYPE_INT64, 0, True, ctx=ctx)
+                for f in schema.fields]
+        return RecordBatch(schema, cols)
+    keys, aggs = state.finalize()
+    return RecordBatch(schema, keys + aggs)
+
+
+# ---------------------------------------------------------------------------------------------------
+# Fusion: HashAggregateExec(Projection?(Selection?(Scan))) -> one kernel
+# ---------------------------------------------------------------------------------------------------
+class FusedHashAggregateExec(PhysicalPlan):
+    """SelectionExec -> ProjectionExec -> HashAggregateExec in ONE pass over the scanned columns
+    (qe_hashagg_update_fused). Same results as the unfused chain."""
+
+    def __init__(self, scan: PhysicalPlan, slots: Sequence[int], spec: N.QeFusedSpec, key_types, aggs,
+                 schema: Schema, groupExpr, aggregateExpr, expected_groups: int = 1024):  # noqa: N803
+        self.scan = scan
+        self.slots = list(slots)  # scan column index per slot
+        self.spec = spec
+        self.key_types = list(key_types)
+        self.aggs = list(aggs)
+        self._schema = schema
+        self.groupExpr = groupExpr
+        self.aggregateExpr = aggregateExpr
+        self.expected_groups = expected_groups
+        self.state: Optional[HashAggregateState] = None
+
+    def schema(self) -> Schema:
+        return self._schema
+
+    def children(self) -> List[PhysicalPlan]:
+        return [self.scan]
+
+    def partial_state(self, state: Optional[HashAggregateState] = None) -> Optional[HashAggregateState]:
+        for batch in self.scan.execute():
+            cols = [batch.field(i) for i in self.slots]
+            if state is None:
+                state = HashAggregateState(cols[0].ctx, self.key_types, self.aggs, self.expected_groups)
+            state.update_fused(cols, self.spec)
+        self.state = state
+        return state
+
+    def execute(self) -> Iterator[RecordBatch]:
+        yield finalize_batch(self.partial_state(), self._schema, self.groupExpr, self.aggregateExpr)
+
+    def __repr__(self) -> str:
+        return f"FusedHashAggregateExec: slots={self.slots}, aggrExpr={self.aggregateExpr}"
+
+
+class _NotFusable(Exception):
+    pass
+
+
+def _conjuncts(e: Expression) -> List[Expression]:
+    if isinstance(e, AndExpression):
+        return _conjuncts(e.l) + _conjuncts(e.r)
+    return [e]
+
+
+class _SlotMap:
+    def __init__(self, scan_schema: Schema):
+        self.schema = scan_schema
+        self.slots: List[int] = []
+
+    def slot(self, col_index: int) -> int:
+        if col_index not in self.slots:
+            if len(self.slots) >= N.MAX_COLS:
+                raise _NotFusable("too many columns")
+            self.slots.append(col_index)
+        return self.slots.index(col_index)
+
+    def type_of(self, col_index: int) -> int:
+        return self.schema.fields[col_index].dataType
+
+
+def _resolve(e: Expression, proj: Optional[List[Expression]]) -> Expression:
+    """Substitute projection outputs (ColumnExpression over a ProjectionExec) by their definitions."""
+    if proj is None:
+        return e
+    if isinstance(e, ColumnExpression):
+        return proj[e.i]
+    if isinstance(e, ArithmeticExpression):
+        return type(e)(_resolve(e.l, proj), _resolve(e.r, proj))
+    if isinstance(e, ComparisonExpression):
+        return type(e)(_resolve(e.l, proj), _resolve(e.r, proj))
+    return e
+
+
+def _literal(e: Expression):
+    if isinstance(e, LiteralLongExpression):
+        return N.scalar(e.value, N.TYPE_INT64)
+    if isinstance(e, LiteralDoubleExpression):
+        return N.scalar(e.value, N.TYPE_FLOAT64)
+    return None
+
+
+def _program(e: Expression, sm: _SlotMap, out: list) -> bool:
+    """Postfix tokens for an arithmetic tree; returns whether the result is fp64."""
+    if isinstance(e, ColumnExpression):
+        t = sm.type_of(e.i)
+        if t not in N.FIXED_WIDTH:
+            raise _NotFusable("non fixed-width input")
+        out.append(N.QeToken(N.TOK_COL, sm.slot(e.i), N.QeScalar()))
+        return t == N.TYPE_FLOAT64
+    lit = _literal(e)
+    if lit is not None:
+        out.append(N.QeToken(N.TOK_LIT, 0, lit))
+        return lit.type == N.TYPE_FLOAT64
+    if isinstance(e, ArithmeticExpression):
+        fl = _program(e.l, sm, out)
+        fr = _program(e.r, sm, out)
+        out.append(N.QeToken({N.OP_ADD: N.TOK_ADD, N.OP_SUB: N.TOK_SUB, N.OP_MUL: N.TOK_MUL,
+                               N.OP_DIV: N.TOK_DIV}[e.op], 0, N.QeScalar()))
+        return fl or fr
+    raise _NotFusable(f"expression {e!r}")
+
+
+def fuse(plan: PhysicalPlan) -> PhysicalPlan:
+    """Rewrite HashAggregateExec over [ProjectionExec] over [SelectionExec] over ScanExec into a
+    FusedHashAggregateExec when every expression is expressible in the fused kernel; otherwise
+    return ``plan`` unchanged (the per-family operators then run)."""
+    if not isinstance(plan, HashAggregateExec):
+        return plan
+    try:
+        node = plan.input
+        proj = None
+        if isinstance(node, ProjectionExec):
+            proj = node.expr
+            node = node.input
+        pred = None
+        if isinstance(node, SelectionExec):
+            pred = node.expr
+            node = node.input
+        if not isinstance(node, ScanExec):
+            raise _NotFusable("input is not a scan")
+        sm = _SlotMap(node.schema())
+        spec = N.QeFusedSpec()
+        spec.mask_col = -1
+        terms = _conjuncts(pred) if pred is not None else []
+        if len(terms) > N.MAX_TERMS:
+            raise _NotFusable("too many predicate terms")
+        for i, t in enumerate(terms):
+            if not isinstance(t, ComparisonExpression) or not isinstance(t.l, ColumnExpression):
+                raise _NotFusable("predicate term")
+            if sm.type_of(t.l.i) not in N.FIXED_WIDTH:
+                raise _NotFusable("predicate on non fixed-width column")
+            pt = spec.terms[i]
+            pt.col = sm.slot(t.l.i)
+            pt.op = t.op
+            if isinstance(t.r, ColumnExpression):
+                if sm.type_of(t.r.i) not in N.FIXED_WIDTH:
+                    raise _NotFusable("predicate on non fixed-width column")
+                pt.rhs_col = sm.slot(t.r.i)
+            else:
+                lit = _literal(t.r)
+                if lit is None:
+                    raise _NotFusable("predicate rhs")
+                pt.rhs_col = -1
+                pt.lit = lit
+        spec.nterms = len(terms)
+        key_types = []
+        for k, g in enumerate(plan.groupExpr):
+            g = _resolve(g, proj)
+            if not isinstance(g, ColumnExpression):
+                raise _NotFusable("group key must be a column")
+            spec.key_cols[k] = sm.slot(g.i)
+            key_types.append(sm.type_of(g.i))
+        aggs = []
+        for j, a in enumerate(plan.aggregateExpr):
+            if a.fn == N.AGG_COUNT_STAR:
+                aggs.append((a.fn, N.TYPE_INT64))
+                continue
+            toks: list = []
+            is_f = _program(_resolve(a.inputExpression(), proj), sm, toks)
+            if len(toks) > N.MAX_TOKENS:
+                raise _NotFusable("expression too long")
+            spec.inputs[j].ntokens = len(toks)
+            for t, tok in enumerate(toks):
+                spec.inputs[j].tokens[t] = tok
+            aggs.append((a.fn, N.TYPE_FLOAT64 if is_f else N.TYPE_INT64))
+        if not sm.slots:
+            raise _NotFusable("no input columns")
+        return FusedHashAggregateExec(node, sm.slots, spec, key_types, aggs, plan.schema(), plan.groupExpr,
+                                      plan.aggregateExpr, plan.expected_groups)
+    except _NotFusable:
+        return plan
+
+
+def aggregate_schema(input_schema: Schema, group_cols: Sequence[int], aggs: Sequence[AggregateExpression],
+                     agg_input_types: Sequence[int]) -> Schema:
+    """Output schema helper: group fields then one field per aggregate named by the function
+    (the reference names every aggregate field after its function, Main.kt:91/:99)."""
+    fields = [input_schema.fields[i] for i in group_cols]
+    for a, t in zip(aggs, agg_input_types):
+        fields.append(Field(a.name, output_type(a.fn, t)))
+    return Schema(fields)

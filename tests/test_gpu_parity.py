@@ -1,0 +1,582 @@
+"""GPU parity tests: every HIP kernel family, through the C ABI (libqe_hip.so via kquery), against
+the CPU oracle on the same seeded inputs. Bit-exact for integer/byte/index work; fp64 SUM/AVG
+within 1e-9 relative of the exact (fsum / long double) sum."""
+import math
+
+import numpy as np
+import pytest
+
+from oracle import gen
+from oracle import semantics as S
+
+pytestmark = pytest.mark.gpu
+
+from kquery import native as N  # noqa: E402
+from kquery.aggregate import HashAggregateState  # noqa: E402
+from kquery.columnar import DeviceColumn  # noqa: E402
+
+REL = 1e-9  # fp64 SUM / AVG tolerance (north_star)
+
+
+def dcol(ctx, t, values, valid=None):
+    return DeviceColumn.from_numpy(t, values, valid, ctx=ctx)
+
+
+def col_values(c: DeviceColumn):
+    return c.to_numpy(), c.valid_mask()
+
+
+def _rand(rng, n, kind, null_rate=0.0):
+    if kind == "i64":
+        v = rng.integers(-2**63, 2**63 - 1, n, dtype=np.int64, endpoint=True)
+    elif kind == "small":
+        v = rng.integers(-4, 5, n).astype(np.int64)
+    else:
+        v = rng.normal(size=n) * 100
+        v[rng.random(n) < 0.05] = np.nan
+        v[rng.random(n) < 0.05] = 0.0
+        v[rng.random(n) < 0.05] = -0.0
+        v[rng.random(n) < 0.01] = np.inf
+    valid = (rng.random(n) >= null_rate) if null_rate > 0 else None
+    return v, valid
+
+
+SIZES = [0, 1, 7, 8, 9, 1000, 8191, 8193, 100_003]
+
+
+# ---- generator ------------------------------------------------------------------------------------
+@pytest.mark.parametrize("dist,param,t", [
+    (N.GEN_MOD, 1024, N.TYPE_INT64), (N.GEN_RAW, 0, N.TYPE_INT64), (N.GEN_UNIT53, 0, N.TYPE_FLOAT64),
+    (N.GEN_MOD_F64, 10000, N.TYPE_FLOAT64), (N.GEN_MOD, 1000, N.TYPE_INT32), (N.GEN_MOD, 3, N.TYPE_UINT8),
+    (N.GEN_MOD, 2, N.TYPE_BOOL)])
+def test_generator_bit_exact(gpu_ctx, dist, param, t):
+    from kquery.datasource import ColumnSpec, generate_column
+
+    n, row0 = 100_005, 777
+    c = generate_column(ColumnSpec("x", t, dist, param, 5, null_permille=100), n, row0, 42, gpu_ctx)
+    ref, valid = gen.generate(dist, param, 42, 5, row0, n, 100)
+    got, gv = col_values(c)
+    if t == N.TYPE_INT32:
+        ref = ref.astype(np.int32)
+    elif t == N.TYPE_UINT8:
+        ref = ref.astype(np.uint8)
+    elif t == N.TYPE_BOOL:
+        ref = (ref & 1).astype(bool)
+    assert np.array_equal(gv, valid)
+    if t == N.TYPE_FLOAT64:
+        assert np.array_equal(got.view(np.int64), ref.view(np.int64))
+    else:
+        assert np.array_equal(got, ref)
+
+
+# ---- K1 arithmetic ---------------------------------------------------------------------------------
+def _eval(ctx, fn_name, op, lhs, rhs, out):
+    keep = []
+
+    def operand(x):
+        if isinstance(x, DeviceColumn):
+            c = x.as_c()
+            keep.append(c)
+            return N.QeOperand(N.C.pointer(c), N.QeScalar())
+        return N.QeOperand(None, N.scalar(x))
+
+    a, b = operand(lhs), operand(rhs)
+    oc = out.as_c()
+    N.check(getattr(N.lib(), fn_name)(ctx.handle, op, N.C.byref(a), N.C.byref(b), N.C.byref(oc)))
+    return out
+
+
+@pytest.mark.parametrize("n", SIZES)
+@pytest.mark.parametrize("op", [N.OP_ADD, N.OP_SUB, N.OP_MUL, N.OP_DIV])
+def test_arith_int64(gpu_ctx, n, op):
+    rng = np.random.default_rng(n * 10 + op)
+    a = rng.integers(-2**63, 2**63 - 1, n, dtype=np.int64, endpoint=True)
+    b = rng.integers(-2**63, 2**63 - 1, n, dtype=np.int64, endpoint=True)
+    if n:
+        b[rng.random(n) < 0.2] = rng.integers(-3, 4, 1)[0]
+        b[: min(n, 3)] = [0, -1, 1][: min(n, 3)]
+        a[0] = -2**63
+    av = rng.random(n) > 0.1
+    out = DeviceColumn.empty(N.TYPE_INT64, n, True, ctx=gpu_ctx)
+    _eval(gpu_ctx, "qe_eval_arith", op, dcol(gpu_ctx, N.TYPE_INT64, a, av), dcol(gpu_ctx, N.TYPE_INT64, b), out)
+    r, v = S.arith(op, a, av, b, None)
+    got, gv = col_values(out)
+    assert np.array_equal(gv, v)
+    assert np.array_equal(got[v], r[v])
+
+
+@pytest.mark.parametrize("op", [N.OP_ADD, N.OP_SUB, N.OP_MUL, N.OP_DIV])
+def test_arith_f64_mixed_and_literals(gpu_ctx, op):
+    rng = np.random.default_rng(op)
+    n = 10_007
+    x, xv = _rand(rng, n, "f64", 0.1)
+    i = rng.integers(-1000, 1000, n).astype(np.int64)
+    out = DeviceColumn.empty(N.TYPE_FLOAT64, n, True, ctx=gpu_ctx)
+    _eval(gpu_ctx, "qe_eval_arith", op, dcol(gpu_ctx, N.TYPE_FLOAT64, x, xv), dcol(gpu_ctx, N.TYPE_INT64, i), out)
+    r, v = S.arith(op, x, xv, i.astype(np.float64), None)
+    got, gv = col_values(out)
+    assert np.array_equal(gv, v)
+    assert np.array_equal(got[v].view(np.int64), r[v].view(np.int64))
+    # column op literal, literal op column
+    out2 = DeviceColumn.empty(N.TYPE_INT64, n, True, ctx=gpu_ctx)
+    _eval(gpu_ctx, "qe_eval_arith", op, dcol(gpu_ctx, N.TYPE_INT64, i), 7, out2)
+    r2, v2 = S.arith(op, i, None, np.int64(7), None)
+    g2, gv2 = col_values(out2)
+    assert np.array_equal(g2[v2], r2[v2]) and np.array_equal(gv2, v2)
+    out3 = DeviceColumn.empty(N.TYPE_FLOAT64, n, False, ctx=gpu_ctx)
+    _eval(gpu_ctx, "qe_eval_arith", op, 1.5, dcol(gpu_ctx, N.TYPE_INT64, i + 2000), out3)
+    r3, _ = S.arith(op, 1.5, None, (i + 2000).astype(np.float64), None)
+    assert np.array_equal(out3.to_numpy().view(np.int64), r3.view(np.int64))
+
+
+def test_arith_null_literal_and_errors(gpu_ctx):
+    n = 100
+    a = np.arange(n, dtype=np.int64)
+    out = DeviceColumn.empty(N.TYPE_INT64, n, True, ctx=gpu_ctx)
+    _eval(gpu_ctx, "qe_eval_arith", N.OP_ADD, dcol(gpu_ctx, N.TYPE_INT64, a), None, out)
+    assert not out.valid_mask().any()
+    with pytest.raises(N.IllegalArgumentException):  # int DIV can produce nulls: validity required
+        _eval(gpu_ctx, "qe_eval_arith", N.OP_DIV, dcol(gpu_ctx, N.TYPE_INT64, a), 3,
+              DeviceColumn.empty(N.TYPE_INT64, n, False, ctx=gpu_ctx))
+    with pytest.raises(N.CapacityError):
+        _eval(gpu_ctx, "qe_eval_arith", N.OP_ADD, dcol(gpu_ctx, N.TYPE_INT64, a), 3,
+              DeviceColumn.empty(N.TYPE_INT64, n - 1, False, ctx=gpu_ctx))
+
+
+# ---- K2 comparison ---------------------------------------------------------------------------------
+@pytest.mark.parametrize("op", [N.OP_EQ, N.OP_NE, N.OP_LT, N.OP_LE, N.OP_GT, N.OP_GE])
+@pytest.mark.parametrize("kind", ["small", "f64", "mixed", "lit"])
+def test_cmp(gpu_ctx, op, kind):
+    rng = np.random.default_rng(op * 7 + len(kind))
+    n = 20_011
+    if kind == "small":
+        a, av = _rand(rng, n, "small", 0.1)
+        b, bv = _rand(rng, n, "small", 0.1)
+        ta = tb = N.TYPE_INT64
+    elif kind == "f64":
+        a, av = _rand(rng, n, "f64", 0.1)
+        b, bv = _rand(rng, n, "f64", 0.1)
+        b[::3] = a[::3]
+        ta = tb = N.TYPE_FLOAT64
+    elif kind == "mixed":
+        a, av = _rand(rng, n, "small", 0.1)
+        b, bv = _rand(rng, n, "f64", 0.0)
+        b[::2] = np.round(b[::2]) % 5
+        ta, tb = N.TYPE_INT64, N.TYPE_FLOAT64
+    else:
+        a, av = _rand(rng, n, "small", 0.1)
+        ta = N.TYPE_INT64
+    out = DeviceColumn.empty(N.TYPE_BOOL, n, True, ctx=gpu_ctx)
+    if kind == "lit":
+        _eval(gpu_ctx, "qe_eval_cmp", op, dcol(gpu_ctx, ta, a, av), 1, out)
+        r, v = S.cmp(op, a, av, np.int64(1), None)
+    else:
+        _eval(gpu_ctx, "qe_eval_cmp", op, dcol(gpu_ctx, ta, a, av), dcol(gpu_ctx, tb, b, bv), out)
+        r, v = S.cmp(op, a, av, b, bv)
+    got, gv = col_values(out)
+    assert np.array_equal(gv, v)
+    assert np.array_equal(got & gv, r)
+
+
+def test_cmp_utf8_employee(gpu_ctx):
+    """Config 1's predicate state = 'CA' on the reference fixture's column, on device."""
+    import pathlib
+
+    from oracle import csv_ref
+
+    rows = csv_ref.read_csv(str(pathlib.Path(__file__).parent / "golden" / "employee.csv"))[0]
+    states = rows["state"] + ["CA", None, "C", "CAX"]
+    col = DeviceColumn.from_strings(states, ctx=gpu_ctx)
+    for lit, op in (("CA", N.OP_EQ), ("Uppsala", N.OP_EQ), ("CA", N.OP_NE)):
+        out = DeviceColumn.empty(N.TYPE_BOOL, len(states), True, ctx=gpu_ctx)
+        litc = DeviceColumn.from_strings([lit], ctx=gpu_ctx)
+        _eval(gpu_ctx, "qe_eval_cmp", op, col, litc, out)
+        r, v = S.cmp_utf8(op, states, lit)
+        got, gv = col_values(out)
+        assert np.array_equal(gv, v) and np.array_equal(got & gv, r)
+    # the reference fixture itself: state='CA' selects nothing (known answer)
+    out = DeviceColumn.empty(N.TYPE_BOOL, 3, False, ctx=gpu_ctx)
+    _eval(gpu_ctx, "qe_eval_cmp", N.OP_EQ, DeviceColumn.from_strings(rows["state"], ctx=gpu_ctx),
+          DeviceColumn.from_strings(["CA"], ctx=gpu_ctx), out)
+    assert not out.to_numpy().any()
+
+
+# ---- K3a boolean -------------------------------------------------------------------------------------
+@pytest.mark.parametrize("op", [N.OP_AND, N.OP_OR, N.OP_NOT, N.OP_IS_NULL, N.OP_IS_NOT_NULL])
+@pytest.mark.parametrize("n", [1, 9, 64, 1000, 100_001])
+def test_bool3(gpu_ctx, op, n):
+    rng = np.random.default_rng(op + n)
+    a = rng.random(n) < 0.5
+    av = rng.random(n) < 0.8
+    b = rng.random(n) < 0.5
+    bv = rng.random(n) < 0.8
+    A, B = dcol(gpu_ctx, N.TYPE_BOOL, a, av), dcol(gpu_ctx, N.TYPE_BOOL, b, bv)
+    out = DeviceColumn.empty(N.TYPE_BOOL, n, True, ctx=gpu_ctx)
+    ac, bc, oc = A.as_c(), B.as_c(), out.as_c()
+    N.check(N.lib().qe_eval_bool(gpu_ctx.handle, op, N.C.byref(ac), N.C.byref(bc), N.C.byref(oc)))
+    r, v = S.bool3(op, a, av, b, bv)
+    got, gv = col_values(out)
+    assert np.array_equal(gv, v)
+    assert np.array_equal(got & gv, r & v)
+
+
+# ---- K3b selection ----------------------------------------------------------------------------------
+@pytest.mark.parametrize("n", SIZES + [3_000_017])
+@pytest.mark.parametrize("sel_rate", [0.0, 0.01, 0.5, 1.0])
+def test_filter_order_preserving(gpu_ctx, n, sel_rate):
+    from kquery.columnar import RecordBatch, Schema
+    from kquery.operators import filter_batch
+
+    rng = np.random.default_rng(n + int(sel_rate * 100))
+    m = rng.random(n) < sel_rate
+    mv = rng.random(n) > 0.05
+    a = rng.integers(-2**63, 2**63 - 1, n, dtype=np.int64, endpoint=True)
+    av = rng.random(n) > 0.3
+    f = rng.normal(size=n)
+    i32 = rng.integers(-2**31, 2**31, n).astype(np.int32)
+    u8 = rng.integers(0, 256, n).astype(np.uint8)
+    cols = [dcol(gpu_ctx, N.TYPE_INT64, a, av), dcol(gpu_ctx, N.TYPE_FLOAT64, f),
+            dcol(gpu_ctx, N.TYPE_INT32, i32), dcol(gpu_ctx, N.TYPE_UINT8, u8)]
+    out = filter_batch(RecordBatch(Schema([]), cols), dcol(gpu_ctx, N.TYPE_BOOL, m, mv))
+    sel = S.select_mask(m, mv)
+    assert out.rowCount() == int(sel.sum())
+    ga, gav = col_values(out.field(0))
+    assert np.array_equal(gav, av[sel]) and np.array_equal(ga[gav], a[sel][av[sel]])
+    assert np.array_equal(out.field(1).to_numpy().view(np.int64), f[sel].view(np.int64))
+    assert np.array_equal(out.field(2).to_numpy(), i32[sel])
+    assert np.array_equal(out.field(3).to_numpy(), u8[sel])
+
+
+# ---- K4a global aggregate ----------------------------------------------------------------------------
+def _global(ctx, col, mask=None):
+    r = N.QeGlobalAgg()
+    c = col.as_c()
+    mc = mask.as_c() if mask is not None else None
+    N.check(N.lib().qe_agg_global(ctx.handle, N.C.byref(c), N.C.byref(mc) if mc is not None else None,
+                                  N.C.byref(r)))
+    return r
+
+
+def _check_global(r, ref, is_f):
+    from kquery.columnar import f64_from_bits
+
+    assert r.rows == ref["rows"] and r.count == ref["count"]
+    if ref["count"] == 0:
+        assert r.valid == 0
+        return
+    assert r.valid == 1
+    if is_f:
+        assert S.rows_equal(f64_from_bits(r.sum), ref["sum"], REL), (f64_from_bits(r.sum), ref["sum"])
+        assert S.rows_equal(f64_from_bits(r.min), ref["min"]), (f64_from_bits(r.min), ref["min"])
+        assert S.rows_equal(f64_from_bits(r.max), ref["max"]), (f64_from_bits(r.max), ref["max"])
+    else:
+        assert (r.sum, r.min, r.max) == (ref["sum"], ref["min"], ref["max"])
+    assert S.rows_equal(r.avg, ref["avg"], REL)
+
+
+@pytest.mark.parametrize("n", SIZES)
+@pytest.mark.parametrize("kind", ["i64", "f64", "f64_nulls_mask"])
+def test_global_aggregate(gpu_ctx, n, kind):
+    rng = np.random.default_rng(n + len(kind))
+    if kind == "i64":
+        x = rng.integers(-2**63, 2**63 - 1, n, dtype=np.int64, endpoint=True)
+        xv, m, mv = None, None, None
+        t = N.TYPE_INT64
+    else:
+        x, xv = _rand(rng, n, "f64", 0.0 if kind == "f64" else 0.2)
+        x[np.isinf(x)] = 3.0
+        m = rng.random(n) < 0.7 if kind.endswith("mask") else None
+        mv = rng.random(n) < 0.9 if m is not None else None
+        t = N.TYPE_FLOAT64
+    r = _global(gpu_ctx, dcol(gpu_ctx, t, x, xv), dcol(gpu_ctx, N.TYPE_BOOL, m, mv) if m is not None else None)
+    _check_global(r, S.global_aggregate(x, xv, m, mv), t == N.TYPE_FLOAT64)
+
+
+@pytest.mark.parametrize("case", [[np.nan, 1.0, 2.0], [1.0, np.nan, 2.0], [-1.0, -0.0, 0.0], [0.0, -0.0],
+                                  [-0.0, 0.0, 1.0], [np.nan, np.nan], [5.0]])
+def test_global_max_order_semantics(gpu_ctx, case):
+    """MaxAccumulator K:538-561 order rules, with the cases spread across lanes / blocks."""
+    base = np.array(case, dtype=np.float64)
+    for pad in (0, 1000, 70_000):
+        x = np.concatenate([np.full(pad, np.nan), base, np.full(pad, -5.0)])
+        xv = np.concatenate([np.zeros(pad, bool), np.ones(len(base), bool), np.ones(pad, bool)])
+        r = _global(gpu_ctx, dcol(gpu_ctx, N.TYPE_FLOAT64, x, xv))
+        _check_global(r, S.global_aggregate(x, xv), True)
+
+
+# ---- K4b hash aggregate --------------------------------------------------------------------------------
+def result_dict(keys, aggs):
+    kv = [k.to_pylist() for k in keys]
+    av = [a.to_pylist() for a in aggs]
+    n = aggs[0].length if aggs else keys[0].length
+    return {tuple(k[i] for k in kv): [a[i] for a in av] for i in range(n)}
+
+
+def assert_groups_equal(got, ref, fns):
+    assert len(got) == len(ref), (len(got), len(ref))
+    gk = {tuple(S.canon(x) for x in k): v for k, v in got.items()}
+    for k, want in ref.items():
+        ck = tuple(S.canon(x) for x in k)
+        assert ck in gk, k
+        for j, (a, b) in enumerate(zip(gk[ck], want)):
+            rel = REL if fns[j] in (N.AGG_SUM, N.AGG_AVG) and isinstance(b, float) else 0.0
+            assert S.rows_equal(a, b, rel), (k, j, a, b)
+
+
+ALL_FNS = [N.AGG_SUM, N.AGG_MIN, N.AGG_MAX, N.AGG_COUNT, N.AGG_COUNT_STAR, N.AGG_AVG]
+
+
+@pytest.mark.parametrize("ngroups,expected", [(1, 16), (10, 1024), (1000, 1024), (5000, 100), (200_000, 1024)])
+@pytest.mark.parametrize("vtype", ["i64", "f64"])
+def test_hashagg_int64_key(gpu_ctx, ngroups, expected, vtype):
+    rng = np.random.default_rng(ngroups)
+    n = 400_000
+    k = rng.integers(0, ngroups, n).astype(np.int64) * 7919 - 3
+    kv = rng.random(n) > 0.01
+    k[rng.random(n) < 0.001] = -2**63  # the EMPTY sentinel value is a legal key
+    if vtype == "i64":
+        x = rng.integers(-2**62, 2**62, n).astype(np.int64)
+        xv = rng.random(n) > 0.1
+        t = N.TYPE_INT64
+    else:
+        x, xv = _rand(rng, n, "f64", 0.1)
+        t = N.TYPE_FLOAT64
+    st = HashAggregateState(gpu_ctx, [N.TYPE_INT64], [(f, t) for f in ALL_FNS], expected)
+    K, X = dcol(gpu_ctx, N.TYPE_INT64, k, kv), dcol(gpu_ctx, t, x, xv)
+    st.update([K], [X] * len(ALL_FNS))
+    keys, aggs = st.finalize()
+    ref = S.group_aggregate([k], [kv], [x] * 6, [xv] * 6, ALL_FNS)
+    assert_groups_equal(result_dict(keys, aggs), ref, ALL_FNS)
+
+
+def test_hashagg_f64_key_and_multibatch_order(gpu_ctx):
+    """fp64 keys (Double.equals: NaN one group, +0/-0 distinct) and MIN/MAX ties across batches:
+    row order continues across update calls, like the reference's batch loop (K:617-620)."""
+    rng = np.random.default_rng(5)
+    n = 50_000
+    k = rng.choice(np.array([np.nan, 0.0, -0.0, 1.5, -2.25, np.inf]), n)
+    x = rng.choice(np.array([0.0, -0.0, -1.0, np.nan, -3.0]), n)
+    xv = rng.random(n) > 0.2
+    fns = [N.AGG_MAX, N.AGG_MIN, N.AGG_COUNT, N.AGG_SUM]
+    st = HashAggregateState(gpu_ctx, [N.TYPE_FLOAT64], [(f, N.TYPE_FLOAT64) for f in fns], 16)
+    for s in range(0, n, 12_345):
+        e = min(n, s + 12_345)
+        st.update([dcol(gpu_ctx, N.TYPE_FLOAT64, k[s:e])], [dcol(gpu_ctx, N.TYPE_FLOAT64, x[s:e], xv[s:e])] * 4)
+    keys, aggs = st.finalize()
+    ref = S.group_aggregate([k], [None], [x] * 4, [xv] * 4, fns)
+    assert_groups_equal(result_dict(keys, aggs), ref, fns)
+
+
+@pytest.mark.parametrize("types", [(N.TYPE_UINT8, N.TYPE_UINT8), (N.TYPE_INT32, N.TYPE_DATE32),
+                                   (N.TYPE_UINT8, N.TYPE_INT32, N.TYPE_UINT8)])
+def test_hashagg_multi_key(gpu_ctx, types):
+    rng = np.random.default_rng(len(types))
+    n = 200_000
+    keys, kvs, dcols = [], [], []
+    for t in types:
+        if t == N.TYPE_UINT8:
+            v = rng.integers(0, 3, n).astype(np.uint8)
+        else:
+            v = rng.integers(-5, 5, n).astype(np.int32)
+        kv = rng.random(n) > 0.05
+        keys.append(v.astype(np.int64))
+        kvs.append(kv)
+        dcols.append(dcol(gpu_ctx, t, v, kv))
+    x = rng.integers(-1000, 1000, n).astype(np.int64)
+    st = HashAggregateState(gpu_ctx, list(types), [(f, N.TYPE_INT64) for f in ALL_FNS], 256)
+    st.update(dcols, [dcol(gpu_ctx, N.TYPE_INT64, x)] * 6)
+    kk, aa = st.finalize()
+    ref = S.group_aggregate(keys, kvs, [x] * 6, [None] * 6, ALL_FNS)
+    assert_groups_equal(result_dict(kk, aa), ref, ALL_FNS)
+
+
+def test_hashagg_mask_and_no_keys(gpu_ctx):
+    rng = np.random.default_rng(11)
+    n = 300_000
+    x = rng.integers(-100, 100, n).astype(np.int64)
+    m = rng.random(n) < 0.3
+    mv = rng.random(n) > 0.1
+    st = HashAggregateState(gpu_ctx, [], [(f, N.TYPE_INT64) for f in ALL_FNS], 1)
+    st.update([], [dcol(gpu_ctx, N.TYPE_INT64, x)] * 6, dcol(gpu_ctx, N.TYPE_BOOL, m, mv))
+    kk, aa = st.finalize()
+    ref = S.group_aggregate([], [], [x] * 6, [None] * 6, ALL_FNS, S.select_mask(m, mv))
+    assert_groups_equal(result_dict(kk, aa), ref, ALL_FNS)
+    # empty input: zero groups (Main.kt:637: the map stays empty)
+    st2 = HashAggregateState(gpu_ctx, [], [(N.AGG_MAX, N.TYPE_INT64)], 1)
+    st2.update([], [dcol(gpu_ctx, N.TYPE_INT64, x)], dcol(gpu_ctx, N.TYPE_BOOL, np.zeros(n, bool)))
+    assert st2.num_groups() == 0
+
+
+def _c4_spec(threshold=1 << 19):
+    """Slots: 0 k, 1 a, 2 b. WHERE a > threshold GROUP BY k: SUM(a+b), COUNT(*), MIN(a), MAX(b)."""
+    spec = N.QeFusedSpec()
+    spec.mask_col = -1
+    spec.nterms = 1
+    spec.terms[0].col = 1
+    spec.terms[0].op = N.OP_GT
+    spec.terms[0].rhs_col = -1
+    spec.terms[0].lit = N.scalar(threshold)
+    spec.key_cols[0] = 0
+    p = spec.inputs[0]
+    p.ntokens = 3
+    p.tokens[0] = N.QeToken(N.TOK_COL, 1, N.QeScalar())
+    p.tokens[1] = N.QeToken(N.TOK_COL, 2, N.QeScalar())
+    p.tokens[2] = N.QeToken(N.TOK_ADD, 0, N.QeScalar())
+    spec.inputs[2].ntokens = 1
+    spec.inputs[2].tokens[0] = N.QeToken(N.TOK_COL, 1, N.QeScalar())
+    spec.inputs[3].ntokens = 1
+    spec.inputs[3].tokens[0] = N.QeToken(N.TOK_COL, 2, N.QeScalar())
+    return spec
+
+
+C4_AGGS = [(N.AGG_SUM, N.TYPE_INT64), (N.AGG_COUNT_STAR, N.TYPE_INT64), (N.AGG_MIN, N.TYPE_INT64),
+           (N.AGG_MAX, N.TYPE_INT64)]
+C4_FNS = [f for f, _ in C4_AGGS]
+
+
+@pytest.mark.parametrize("n,row0", [(1, 0), (1000, 5), (10_000_000, 0)])
+def test_fused_c4_vs_oracle(gpu_ctx, n, row0):
+    from kquery.datasource import C4_COLUMNS, generate_column
+
+    cols = [generate_column(s, n, row0, 42, gpu_ctx) for s in C4_COLUMNS]
+    st = HashAggregateState(gpu_ctx, [N.TYPE_INT64], C4_AGGS, 1024)
+    st.update_fused(cols, _c4_spec())
+    kk, aa = st.finalize()
+    k, _ = gen.generate(gen.GEN_MOD, 1024, 42, 0, row0, n)
+    a, _ = gen.generate(gen.GEN_MOD, 1 << 20, 42, 1, row0, n)
+    b, _ = gen.generate(gen.GEN_MOD, 1 << 20, 42, 2, row0, n)
+    ref = S.group_aggregate([k], [None], [S.arith(S.OP_ADD, a, None, b, None)[0], None, a, b], [None] * 4, C4_FNS,
+                            a > (1 << 19))
+    assert_groups_equal(result_dict(kk, aa), ref, C4_FNS)
+
+
+def test_fused_equals_unfused_operators(gpu_ctx):
+    """Scan -> Selection -> Projection -> HashAggregate: per-family operators and the fused kernel
+    give identical batches; both match the oracle (C2-shaped predicate, nullable inputs)."""
+    from kquery.columnar import Field, Schema
+    from kquery.datasource import InMemoryDataSource
+    from kquery.expressions import (AddExpression, AndExpression, ColumnExpression, CountStarExpression,
+                                    GtExpression, LiteralLongExpression, LtExpression, MaxExpression,
+                                    MinExpression, MultiplyExpression, SumExpression, AvgExpression)
+    from kquery.operators import (FusedHashAggregateExec, HashAggregateExec, ProjectionExec, ScanExec,
+                                  SelectionExec, fuse)
+    from kquery.columnar import RecordBatch
+
+    rng = np.random.default_rng(3)
+    n = 1_000_003
+    k = rng.integers(0, 300, n).astype(np.int64)
+    a = rng.integers(0, 1 << 20, n).astype(np.int64)
+    av = rng.random(n) > 0.1
+    b = rng.integers(-2**40, 2**40, n).astype(np.int64)
+    schema = Schema([Field("k", N.TYPE_INT64), Field("a", N.TYPE_INT64), Field("b", N.TYPE_INT64)])
+    batches = []
+    for s in range(0, n, 300_000):
+        e = min(n, s + 300_000)
+        batches.append(RecordBatch(schema, [dcol(gpu_ctx, N.TYPE_INT64, k[s:e]),
+                                            dcol(gpu_ctx, N.TYPE_INT64, a[s:e], av[s:e]),
+                                            dcol(gpu_ctx, N.TYPE_INT64, b[s:e])]))
+    scan = ScanExec(InMemoryDataSource(schema, batches), ["k", "a", "b"])
+    pred = AndExpression(GtExpression(ColumnExpression(1), LiteralLongExpression(1 << 18)),
+                         LtExpression(ColumnExpression(2), LiteralLongExpression(2**39)))
+    sel = SelectionExec(scan, pred)
+    proj = ProjectionExec(sel, Schema([Field("k", N.TYPE_INT64), Field("ab", N.TYPE_INT64), Field("a", N.TYPE_INT64),
+                                       Field("b3", N.TYPE_INT64)]),
+                          [ColumnExpression(0), AddExpression(ColumnExpression(1), ColumnExpression(2)),
+                           ColumnExpression(1), MultiplyExpression(ColumnExpression(2), LiteralLongExpression(3))])
+    aggs = [SumExpression(ColumnExpression(1)), CountStarExpression(), MinExpression(ColumnExpression(2)),
+            MaxExpression(ColumnExpression(3)), AvgExpression(ColumnExpression(1))]
+    out_schema = Schema([Field("k", N.TYPE_INT64)] + [Field(x.name, N.TYPE_INT64) for x in aggs])
+    plan = HashAggregateExec(proj, [ColumnExpression(0)], aggs, out_schema)
+    fused = fuse(plan)
+    assert isinstance(fused, FusedHashAggregateExec)
+    r1 = next(plan.execute())
+    r2 = next(fused.execute())
+    d1 = result_dict(r1.fields[:1], r1.fields[1:])
+    d2 = result_dict(r2.fields[:1], r2.fields[1:])
+    fns = [x.fn for x in aggs]
+    sel_m = (a > (1 << 18)) & av & (b < 2**39)
+    ab, abv = S.arith(S.OP_ADD, a, av, b, None)
+    b3, _ = S.arith(S.OP_MUL, b, None, np.int64(3), None)
+    ref = S.group_aggregate([k], [None], [ab, None, a, b3, ab], [abv, None, av, None, abv], fns, sel_m)
+    assert_groups_equal(d1, ref, fns)
+    assert_groups_equal(d2, ref, fns)
+
+
+def test_export_import_two_phase(gpu_ctx):
+    """main()'s two-phase aggregate (K:1309-1325): shard rows into partitions, partial-aggregate
+    each, export records bucketed by hash(key) mod P, import every bucket into its owner, and the
+    union of the owners' groups equals the single-pass result."""
+    rng = np.random.default_rng(9)
+    n = 600_000
+    P = 3
+    k = rng.integers(0, 5000, n).astype(np.int64)
+    kv = rng.random(n) > 0.01
+    x, xv = _rand(rng, n, "f64", 0.1)
+    fns = [N.AGG_MAX, N.AGG_MIN, N.AGG_SUM, N.AGG_COUNT, N.AGG_COUNT_STAR]
+    aggs = [(f, N.TYPE_FLOAT64) for f in fns]
+    owners = [HashAggregateState(gpu_ctx, [N.TYPE_INT64], aggs, 4096) for _ in range(P)]
+    bounds = np.linspace(0, n, P + 1).astype(int)
+    for p in range(P):
+        s, e = bounds[p], bounds[p + 1]
+        st = HashAggregateState(gpu_ctx, [N.TYPE_INT64], aggs, 4096)
+        st.set_row_base(int(s))
+        st.update([dcol(gpu_ctx, N.TYPE_INT64, k[s:e], kv[s:e])], [dcol(gpu_ctx, N.TYPE_FLOAT64, x[s:e], xv[s:e])] * 5)
+        recs, counts = st.export(P)
+        rb = st.record_bytes()
+        off = 0
+        for q in range(P):
+            owners[q].import_records(recs[off * rb:(off + counts[q]) * rb], counts[q])
+            off += counts[q]
+    got = {}
+    for o in owners:
+        kk, aa = o.finalize()
+        d = result_dict(kk, aa)
+        assert not (set(d) & set(got))  # each group has exactly one owner
+        got.update(d)
+    ref = S.group_aggregate([k], [kv], [x] * 5, [xv] * 5, fns)
+    assert_groups_equal(got, ref, fns)
+
+
+def test_hashagg_growth_from_tiny_table(gpu_ctx):
+    """expected_groups far too small: the global table grows and deferred rows / overflow records
+    are re-applied exactly once."""
+    rng = np.random.default_rng(17)
+    n = 2_000_000
+    k = rng.integers(0, 300_000, n).astype(np.int64)
+    x = rng.integers(0, 10, n).astype(np.int64)
+    st = HashAggregateState(gpu_ctx, [N.TYPE_INT64], [(N.AGG_SUM, N.TYPE_INT64), (N.AGG_COUNT_STAR, N.TYPE_INT64)], 8)
+    st.update([dcol(gpu_ctx, N.TYPE_INT64, k)], [dcol(gpu_ctx, N.TYPE_INT64, x), None])
+    kk, aa = st.finalize()
+    ref = S.group_aggregate([k], [None], [x, None], [None, None], [N.AGG_SUM, N.AGG_COUNT_STAR])
+    assert_groups_equal(result_dict(kk, aa), ref, [N.AGG_SUM, N.AGG_COUNT_STAR])
+
+
+@pytest.mark.slow
+def test_c4_full_size_properties(gpu_ctx):
+    """BASELINE config 4 at full size (1B rows, one GPU): size-independent properties.
+    Sum over groups of COUNT(*) == rows passing the filter (qe_filter_count on the predicate);
+    sum over groups of SUM(a+b) == global SUM of a+b over the selected rows (qe_agg_global);
+    global MIN(a) / MAX(b) == min / max over the groups; exactly 1024 groups."""
+    from kquery.datasource import C4_COLUMNS, generate_column
+
+    n = 1_000_000_000
+    cols = [generate_column(s, n, 0, 42, gpu_ctx) for s in C4_COLUMNS]
+    st = HashAggregateState(gpu_ctx, [N.TYPE_INT64], C4_AGGS, 1024)
+    st.update_fused(cols, _c4_spec())
+    kk, aa = st.finalize()
+    assert kk[0].length == 1024
+    sums, counts, mins, maxs = (x.to_numpy() for x in aa)
+    mask = DeviceColumn.empty(N.TYPE_BOOL, n, False, ctx=gpu_ctx)
+    _eval(gpu_ctx, "qe_eval_cmp", N.OP_GT, cols[1], 1 << 19, mask)
+    cnt = N.C.c_int64()
+    mc = mask.as_c()
+    N.check(N.lib().qe_filter_count(gpu_ctx.handle, N.C.byref(mc), N.C.byref(cnt)))
+    assert int(counts.sum()) == cnt.value
+    ab = DeviceColumn.empty(N.TYPE_INT64, n, False, ctx=gpu_ctx)
+    _eval(gpu_ctx, "qe_eval_arith", N.OP_ADD, cols[1], cols[2], ab)
+    g = _global(gpu_ctx, ab, mask)
+    assert g.count == cnt.value
+    assert int(sums.astype(np.uint64).sum(dtype=np.uint64).view(np.int64)) == g.sum
+    ga = _global(gpu_ctx, cols[1], mask)
+    gb = _global(gpu_ctx, cols[2], mask)
+    assert int(mins.min()) == ga.min and int(maxs.max()) == gb.max
