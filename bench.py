@@ -164,6 +164,15 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
 
+    # stream-read ceiling over the same 24 B/row (k, a, b), median of 5
+    cc = (N.QeColumn * 3)(*[c.as_c() for c in cols])
+    sr = []
+    for _ in range(5):
+        ms = C.c_double()
+        N.check(N.lib().qe_stream_read(ctx.handle, cc, 3, C.byref(ms)))
+        sr.append(ms.value)
+    stream_gbs = rows * BYTES_PER_ROW / (sorted(sr)[2] * 1e-3) / 1e9
+
     # sanity: every group present once across owners, COUNT(*) adds up to the filtered rows
     groups = torch.tensor([keys[0].length, int(res[1].to_numpy().sum())], dtype=torch.int64, device="cuda")
     if world > 1:
@@ -203,6 +212,7 @@ def main():
             "kernel": "k_hashagg<3,true> (fused filter+project+LDS hash aggregate)",
             "avg_kernel_ms": avg_kernel_ms,
             "bytes_per_launch": rows * BYTES_PER_ROW,
+            "stream_read_ceiling_gbs": stream_gbs,
         },
         "check": {"groups": int(groups[0].item()), "count_star_total": int(groups[1].item())},
     }

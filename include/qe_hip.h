@@ -92,9 +92,14 @@ typedef struct qe_operand {
 /* ---- context ---------------------------------------------------------------------------- */
 typedef struct qe_ctx qe_ctx;
 
-/* Create a context on HIP device `device`. `stream` is a hipStream_t to launch on
- * (NULL = the ctx creates and owns one). */
+/* Create a context on HIP device `device` that launches on hipStream_t `stream`
+ * (NULL = the legacy default stream, e.g. torch's default stream). */
 int qe_ctx_create(int device, void* stream, qe_ctx** out);
+/* Same, with a non-blocking stream the ctx creates and owns (hosts without streams: JNI). */
+int qe_ctx_create_owned(int device, qe_ctx** out);
+/* Per-plan kernel specialisation of the fused aggregate (hipRTC, default on; env QE_JIT=0
+ * turns it off at ctx creation). 0 = always run the generic (interpreting) kernel. */
+int qe_ctx_set_jit(qe_ctx* ctx, int32_t enable);
 int qe_ctx_destroy(qe_ctx* ctx);
 /* The hipStream_t every kernel of this ctx is launched on. */
 void* qe_ctx_stream(qe_ctx* ctx);
@@ -125,6 +130,11 @@ int qe_copy_to_host(qe_ctx* ctx, void* dst, const void* src, size_t bytes);     
 #define QE_GEN_MOD_F64 4
 int qe_generate(qe_ctx* ctx, qe_column* out, int32_t dist, int64_t param, uint64_t seed,
                 uint64_t col, int64_t row0, int32_t null_permille);
+
+/* Measurement harness: device time (ms) of one pass that reads every byte of `ncols`
+ * fixed-width columns with 16-B loads — the achievable stream-read ceiling for the bytes a
+ * query scans (reported next to the roofline). */
+int qe_stream_read(qe_ctx* ctx, const qe_column* cols, int32_t ncols, double* ms);
 
 /* ---- vectorised expressions: Expression.evaluate (K:448-450) ---------------------------- */
 #define QE_OP_ADD 1
@@ -297,6 +307,9 @@ int qe_hashagg_set_row_base(qe_hashagg* agg, int64_t row_base);
  * launches made by the last update call, and how many launches it took (1 unless the table
  * had to grow and deferred rows were re-applied). */
 int qe_hashagg_last_kernel_time(qe_hashagg* agg, double* ms, int32_t* launches);
+/* Whether the last update ran a plan-specialised kernel (1) or the generic one (0), and why
+ * not (NUL-terminated note, may be NULL). */
+int qe_hashagg_last_kernel_kind(qe_hashagg* agg, int32_t* specialized, char* note, int32_t note_len);
 
 #ifdef __cplusplus
 }

@@ -389,7 +389,7 @@ def rows_equal(a: Any, b: Any, rel: float = 0.0) -> bool:
         a, b = float(a), float(b)
         if math.isnan(a) or math.isnan(b):
             return math.isnan(a) and math.isnan(b)
-        if rel == 0.0:
+        if rel == 0.0 or math.isinf(a) or math.isinf(b):
             return a == b and math.copysign(1, a) == math.copysign(1, b)
         return abs(a - b) <= rel * max(abs(a), abs(b), 1e-300)
     return a == b

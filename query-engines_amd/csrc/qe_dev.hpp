@@ -1,0 +1,313 @@
+// qe_dev.hpp — device-side definitions of the hash-aggregate engine, shared by
+//   * the ahead-of-time kernels of libqe_hip.so (hipcc, gfx950), and
+//   * the per-plan kernels generated at run time (qe_jit.hip -> hipRTC -> gfx950 code object),
+// so both compile exactly the same table layout, probing and combine code.
+// Self-contained on purpose: no standard headers (hipRTC compiles it on its own).
+#ifndef QE_DEV_HPP
+#define QE_DEV_HPP
+
+#ifndef QE_OP_EQ  // comparison op codes (include/qe_hip.h)
+#define QE_OP_EQ 10
+#define QE_OP_NE 11
+#define QE_OP_LT 12
+#define QE_OP_LE 13
+#define QE_OP_GT 14
+#define QE_OP_GE 15
+#endif
+#ifndef QE_MAX_KEYS
+#define QE_MAX_KEYS 4
+#define QE_MAX_AGGS 8
+#define QE_MAX_COLS 8
+#define QE_MAX_TERMS 8
+#define QE_MAX_TOKENS 8
+#endif
+#ifndef QE_AGG_SUM
+#define QE_AGG_SUM 1
+#define QE_AGG_MIN 2
+#define QE_AGG_MAX 3
+#define QE_AGG_COUNT 4
+#define QE_AGG_COUNT_STAR 5
+#define QE_AGG_AVG 6
+#endif
+
+namespace qe {
+
+typedef long long qi64;
+typedef unsigned long long qu64;
+typedef int qi32;
+typedef unsigned int qu32;
+typedef unsigned short qu16;
+typedef unsigned char qu8;
+typedef long long qi64x2 __attribute__((ext_vector_type(2)));
+
+constexpr qi64 EMPTY_KEY = (qi64)0x8000000000000000ull;  // LDS/global slot sentinel (INT64_MIN)
+constexpr qu64 NULL_SALT = 0x6A09E667F3BCC909ull;
+constexpr int HA_LDS_MAXP = 32;      // probe limit in the LDS table
+constexpr int HA_GLOBAL_MAXP = 256;  // probe limit in the global table
+
+// Operand kinds understood by the device loaders (uniform per launch).
+enum SrcKind : int { K_LIT = 0, K_I64 = 1, K_F64 = 2, K_I32 = 3, K_U8 = 4, K_BOOL = 5 };
+enum AccKind : int { ACC_NONE = 0, ACC_SUM_I = 1, ACC_SUM_F = 2, ACC_MIN_I = 3, ACC_MAX_I = 4, ACC_MIN_F = 5, ACC_MAX_F = 6 };
+enum TokOp : int {
+  T_COL = 1, T_LIT, T_I2F0, T_I2F1,
+  T_ADD_I, T_SUB_I, T_MUL_I, T_DIV_I,
+  T_ADD_F, T_SUB_F, T_MUL_F, T_DIV_F
+};
+
+// ---- launch description (host fills it; kernels read it as their only argument) ---------------
+struct DTok {
+  qi32 op, arg;
+  qi64 lit;
+  qi32 lit_null, lit_f64;
+};
+
+struct DAgg {
+  qi32 fn, acc;
+  qi32 pkind;     // 0: no input (COUNT_STAR), 1: column slot, 2: token program, 3: slot OP slot|literal
+  qi32 col;       // slot for pkind 1, lhs slot for pkind 3
+  qi32 cvt_i2f;   // pkind 1: convert integral slot to fp64
+  qi32 ntok;
+  qi32 track_nn;  // the input can be null in this launch (else nn == cstar)
+  qi32 bop;       // pkind 3: typed binary op (T_ADD_I ... T_DIV_F)
+  qi32 rhs;       // pkind 3: rhs slot, or -1 => literal
+  qi32 rhs_null;  // pkind 3: literal is null
+  qi64 rhs_lit;   // pkind 3: literal bits
+  DTok tok[QE_MAX_TOKENS];
+};
+
+struct DCol {
+  const void* p;
+  const qu8* valid;
+  qi32 kind;  // SrcKind
+  qi32 pad;
+};
+
+struct DTerm {
+  qi32 lhs, op, rhs, f64;  // rhs < 0: literal; f64: compare as fp64
+  qi32 lhs_f, rhs_f, lit_null, pad;
+  qi64 lit;  // in the compare domain
+};
+
+struct DTable {
+  qi64* keys;
+  qu64* cstar;
+  qi64* acc[QE_MAX_AGGS];
+  qu64* nn[QE_MAX_AGGS];
+  qu64* idx[QE_MAX_AGGS];  // 4 arrays of cap+2 each (fp64 MIN/MAX only)
+  qu64 cap;                // power of two; slots cap, cap+1 special
+  qu64* ctl;               // [0] groups, [1] deferred rows, [2] overflow records, [3] lost
+};
+
+struct Plan {
+  DCol cols[QE_MAX_COLS];
+  DTerm terms[QE_MAX_TERMS];
+  DAgg aggs[QE_MAX_AGGS];
+  DTable t;
+  qi64 n, row_base;
+  const qu32* defer_in;  // retry pass: only these rows
+  qu32* defer_out;       // rows the global table could not take
+  qu8* ovf;              // overflow records (LDS flush)
+  qu64 ovf_cap;
+  qi32 ncols, nterms, mask_col, naggs;
+  qi32 key_mode, nkeys, key_f64, rec_bytes;
+  qi32 key_col[QE_MAX_KEYS], key_shift[QE_MAX_KEYS], key_nullbit[QE_MAX_KEYS], pad0;
+  qi64 key_fmask[QE_MAX_KEYS];
+  qi32 lds_log2, off_cstar;
+  qi32 all8, pad1;  // every column slot is 8 bytes wide (straight-line loads)
+  qi32 off_acc[QE_MAX_AGGS], off_nn[QE_MAX_AGGS], off_idx[QE_MAX_AGGS];
+};
+
+// ---- scalar helpers ---------------------------------------------------------------------------------
+__host__ __device__ inline qi64 f64_bits(double d) { return __builtin_bit_cast(qi64, d); }
+__host__ __device__ inline double bits_f64(qi64 b) { return __builtin_bit_cast(double, b); }
+
+// Order-preserving int64 key of a non-NaN double with +0.0 and -0.0 mapped to the same key
+// (they compare equal under IEEE `>`, Main.kt:547; the earliest one is tracked separately).
+__host__ __device__ inline qi64 f64_okey(double d) {
+  const qi64 b = f64_bits(d == 0.0 ? 0.0 : d);
+  return b >= 0 ? b : (b ^ 0x7FFFFFFFFFFFFFFFll);
+}
+__host__ __device__ inline double okey_f64(qi64 k) { return bits_f64(k >= 0 ? k : (k ^ 0x7FFFFFFFFFFFFFFFll)); }
+
+// murmur3 finaliser: global-table slot and exchange partition hash.
+__host__ __device__ inline qu64 fmix64(qu64 k) {
+  k ^= k >> 33;
+  k *= 0xFF51AFD7ED558CCDull;
+  k ^= k >> 33;
+  k *= 0xC4CEB9FE1A85EC53ull;
+  k ^= k >> 33;
+  return k;
+}
+
+// Cheap slot hash for the per-workgroup LDS table: one 32-bit multiply (Fibonacci hashing).
+__device__ inline qu32 lds_hash(qu64 key) {
+  const qu32 x = (qu32)key ^ (qu32)(key >> 32) * 0x85EBCA6Bu;
+  return x * 0x9E3779B1u;
+}
+
+// JVM Long division: truncating; MIN / -1 wraps to MIN; callers null out b == 0.
+__device__ inline qi64 idiv(qi64 a, qi64 b) {
+  if (b == 0) return 0;
+  if (b == -1) return (qi64)(0ull - (qu64)a);
+  return a / b;
+}
+
+__host__ __device__ inline bool acc_is_f64mm(int acc) { return acc == ACC_MIN_F || acc == ACC_MAX_F; }
+__host__ __device__ inline qi64 acc_identity(int acc) {
+  switch (acc) {
+    case ACC_MIN_I:
+    case ACC_MIN_F: return 0x7FFFFFFFFFFFFFFFll;
+    case ACC_MAX_I:
+    case ACC_MAX_F: return EMPTY_KEY;
+    default: return 0;
+  }
+}
+
+// Record layout (export/import/overflow):
+// [0] key  [8] flags (bit0 null key)  [16] cstar  then per aggregate: acc, nn, (4 x idx if fp64 MIN/MAX)
+__host__ __device__ inline int agg_rec_bytes(int acc) { return 16 + (acc_is_f64mm(acc) ? 32 : 0); }
+
+// ---- global table -------------------------------------------------------------------------------------
+__device__ inline bool gtable_find(const DTable& t, qi64 key, bool knull, qu64& slot) {
+  if (knull) {
+    slot = t.cap;
+    return true;
+  }
+  if (key == EMPTY_KEY) {
+    slot = t.cap + 1;
+    return true;
+  }
+  qu64 h = fmix64((qu64)key) & (t.cap - 1);
+#pragma unroll 1
+  for (int p = 0; p < HA_GLOBAL_MAXP; ++p) {
+    const qi64 k = __hip_atomic_load(&t.keys[h], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (k == key) {
+      slot = h;
+      return true;
+    }
+    if (k == EMPTY_KEY) {
+      const qi64 old = (qi64)atomicCAS((qu64*)&t.keys[h], (qu64)EMPTY_KEY, (qu64)key);
+      if (old == EMPTY_KEY) {
+        atomicAdd(&t.ctl[0], 1ull);
+        slot = h;
+        return true;
+      }
+      if (old == key) {
+        slot = h;
+        return true;
+      }
+    }
+    h = (h + 1) & (t.cap - 1);
+  }
+  return false;
+}
+
+__device__ inline void gadd_cstar(const DTable& t, qu64 slot, qu64 c) {
+  const qu64 old = atomicAdd(&t.cstar[slot], c);
+  if (slot >= t.cap && old == 0) atomicAdd(&t.ctl[0], 1ull);  // a special group appears
+}
+
+// Combine one aggregate's partial state into global slot `s` (device-scope atomics).
+__device__ inline void gcombine(const DTable& t, int acck, int j, qu64 s, qi64 acc, qu64 nn, qu64 i0, qu64 i1,
+                                qu64 i2, qu64 i3) {
+  if (nn == 0) return;
+  atomicAdd(&t.nn[j][s], nn);
+  switch (acck) {
+    case ACC_SUM_I:
+      if (acc) atomicAdd((qu64*)&t.acc[j][s], (qu64)acc);
+      break;
+    case ACC_SUM_F: atomicAdd((double*)&t.acc[j][s], bits_f64(acc)); break;
+    case ACC_MIN_I:
+    case ACC_MIN_F:
+      if (acc != 0x7FFFFFFFFFFFFFFFll) atomicMin(&t.acc[j][s], acc);
+      break;
+    case ACC_MAX_I:
+    case ACC_MAX_F:
+      if (acc != EMPTY_KEY) atomicMax(&t.acc[j][s], acc);
+      break;
+    default: break;
+  }
+  if (acc_is_f64mm(acck)) {
+    const qu64 stride = t.cap + 2;
+    qu64* ix = t.idx[j];
+    if (i0 != ~0ull) atomicMin(&ix[s], i0);
+    if (i1 != ~0ull) atomicMin(&ix[stride + s], i1);
+    if (i2 != ~0ull) atomicMin(&ix[2 * stride + s], i2);
+    if (i3 != ~0ull) atomicMin(&ix[3 * stride + s], i3);
+  }
+}
+
+// Per-row contribution of one aggregate in partial form.
+struct RowVal {
+  qi64 acc;
+  qu64 i0, i1, i2, i3;
+};
+
+__device__ inline RowVal row_partial(int acck, qi64 x, qu64 row) {
+  RowVal r{acc_identity(acck), ~0ull, ~0ull, ~0ull, ~0ull};
+  switch (acck) {
+    case ACC_SUM_I:
+    case ACC_SUM_F:
+    case ACC_MIN_I:
+    case ACC_MAX_I: r.acc = x; break;
+    case ACC_MIN_F:
+    case ACC_MAX_F: {
+      const double d = bits_f64(x);
+      r.i0 = row;
+      if (d != d) {
+        r.i1 = row;
+      } else {
+        r.acc = f64_okey(d);
+        if (d == 0.0) {
+          if (x < 0) r.i2 = row;
+          else r.i3 = row;
+        }
+      }
+      break;
+    }
+    default: break;
+  }
+  return r;
+}
+
+__device__ inline void write_record_head(qu8* rec, qi64 key, bool knull, qu64 cstar) {
+  ((qi64*)rec)[0] = key;
+  ((qu64*)rec)[1] = knull ? 1ull : 0ull;
+  ((qu64*)rec)[2] = cstar;
+}
+
+// ---- LDS table helpers ----------------------------------------------------------------------------------
+// Continue probing the LDS table from slot h (already found to hold another key); inserts the
+// key into the first empty slot. Returns the slot, or -1 when the probe limit is hit.
+__device__ inline int lds_probe(qi64* keys, int log2, qi64 key, qu32 h) {
+  const qu32 mask = (1u << log2) - 1;
+#pragma unroll 1
+  for (int p = 0; p < HA_LDS_MAXP; ++p) {
+    const qi64 k = keys[h];
+    if (k == key) return (int)h;
+    if (k == EMPTY_KEY) {
+      const qi64 old = (qi64)atomicCAS((qu64*)&keys[h], (qu64)EMPTY_KEY, (qu64)key);
+      if (old == EMPTY_KEY || old == key) return (int)h;
+    }
+    h = (h + 1) & mask;
+  }
+  return -1;
+}
+
+// fp64 MIN/MAX row into LDS accumulators (MaxAccumulator order semantics, Main.kt:538-561).
+template <bool IS_MAX>
+__device__ inline void lds_f64mm(qi64* acc, qu64* idx, int SS, int s, qi64 x, qu64 row) {
+  const double d = bits_f64(x);
+  atomicMin(&idx[s], row);
+  if (d != d) {
+    atomicMin(&idx[SS + s], row);
+  } else {
+    if (IS_MAX) atomicMax(&acc[s], f64_okey(d));
+    else atomicMin(&acc[s], f64_okey(d));
+    if (d == 0.0) atomicMin(&idx[(x < 0 ? 2 : 3) * SS + s], row);
+  }
+}
+
+}  // namespace qe
+
+#endif  // QE_DEV_HPP

@@ -11,7 +11,7 @@
 //  * output is one batch: key columns then aggregate columns; group order unspecified (K:639).
 //
 // Data layout in HBM (per state): a global open-addressing table, SoA, capacity G (power of two)
-// plus two special slots (G: null key, G+1: key == INT64_MIN, the EMPTY sentinel):
+// plus two special slots (G: null key, G+1: key == EMPTY_KEY, the EMPTY sentinel):
 //   keys int64[G+2] | cstar u64[G+2] | per aggregate: acc 64-bit[G+2], nn u64[G+2],
 //   and for fp64 MIN/MAX four u64[G+2] first-row indices.
 // Kernel: each workgroup owns a private LDS hash table (2^k slots, keys + per-aggregate
@@ -29,204 +29,16 @@
 
 namespace qe {
 
-constexpr int HA_THREADS = 256;
-constexpr int HA_LDS_MAXP = 32;      // probe limit in the LDS table
-constexpr int HA_GLOBAL_MAXP = 256;  // probe limit in the global table
-constexpr int64_t EMPTY_KEY = INT64_MIN;
-constexpr uint64_t NULL_SALT = 0x6A09E667F3BCC909ull;
+constexpr int HA_THREADS = 512;
 constexpr size_t HA_LDS_BUDGET = 80 * 1024;  // bytes of LDS per workgroup (2 workgroups / CU)
 
-enum AccKind : int32_t { ACC_NONE = 0, ACC_SUM_I = 1, ACC_SUM_F = 2, ACC_MIN_I = 3, ACC_MAX_I = 4, ACC_MIN_F = 5, ACC_MAX_F = 6 };
-enum TokOp : int32_t {
-  T_COL = 1, T_LIT, T_I2F0, T_I2F1,
-  T_ADD_I, T_SUB_I, T_MUL_I, T_DIV_I,
-  T_ADD_F, T_SUB_F, T_MUL_F, T_DIV_F
-};
-
-__host__ __device__ inline bool acc_is_f64mm(int32_t acc) { return acc == ACC_MIN_F || acc == ACC_MAX_F; }
-__host__ __device__ inline int64_t acc_identity(int32_t acc) {
-  switch (acc) {
-    case ACC_MIN_I:
-    case ACC_MIN_F: return INT64_MAX;
-    case ACC_MAX_I:
-    case ACC_MAX_F: return INT64_MIN;
-    default: return 0;
-  }
-}
-
-struct DTok {
-  int32_t op, arg;
-  int64_t lit;
-  int32_t lit_null, pad;
-};
-
-struct DAgg {
-  int32_t fn, acc;
-  int32_t pkind;     // 0: no input (COUNT_STAR), 1: column slot, 2: token program
-  int32_t col;       // slot for pkind 1
-  int32_t cvt_i2f;   // pkind 1: convert integral slot to fp64
-  int32_t ntok;
-  int32_t track_nn;  // the input can be null in this launch (else nn == cstar)
-  int32_t pad;
-  DTok tok[QE_MAX_TOKENS];
-};
-
-struct DCol {
-  const void* p;
-  const uint8_t* valid;
-  int32_t kind;  // SrcKind
-  int32_t pad;
-};
-
-struct DTerm {
-  int32_t lhs, op, rhs, f64;  // rhs < 0: literal; f64: compare as fp64
-  int32_t lhs_f, rhs_f, lit_null, pad;
-  int64_t lit;  // in the compare domain
-};
-
-struct DTable {
-  int64_t* keys;
-  uint64_t* cstar;
-  int64_t* acc[QE_MAX_AGGS];
-  uint64_t* nn[QE_MAX_AGGS];
-  uint64_t* idx[QE_MAX_AGGS];  // 4 arrays of cap+2 each (fp64 MIN/MAX only)
-  uint64_t cap;                // power of two; slots cap, cap+1 special
-  uint64_t* ctl;               // [0] groups, [1] deferred rows, [2] overflow records, [3] lost
-};
-
-struct Plan {
-  DCol cols[QE_MAX_COLS];
-  DTerm terms[QE_MAX_TERMS];
-  DAgg aggs[QE_MAX_AGGS];
-  DTable t;
-  int64_t n, row_base;
-  const uint32_t* defer_in;  // retry pass: only these rows
-  uint32_t* defer_out;       // rows the global table could not take
-  uint8_t* ovf;              // overflow records (LDS flush)
-  uint64_t ovf_cap;
-  int32_t ncols, nterms, mask_col, naggs;
-  int32_t key_mode, nkeys, key_f64, rec_bytes;
-  int32_t key_col[QE_MAX_KEYS], key_shift[QE_MAX_KEYS], key_nullbit[QE_MAX_KEYS], pad0;
-  int64_t key_fmask[QE_MAX_KEYS];
-  int32_t lds_log2, off_cstar;
-  int32_t off_acc[QE_MAX_AGGS], off_nn[QE_MAX_AGGS], off_idx[QE_MAX_AGGS];
-};
-
-// ---- record layout (export/import/overflow) --------------------------------------------------
-// [0] key  [8] flags (bit0 null key)  [16] cstar  then per aggregate: acc, nn, (4 x idx if fp64 MIN/MAX)
-__host__ __device__ inline int agg_rec_bytes(int32_t acc) { return 16 + (acc_is_f64mm(acc) ? 32 : 0); }
-
-// ---- global table ------------------------------------------------------------------------------
-__device__ __forceinline__ bool gtable_find(const DTable& t, int64_t key, bool knull, uint64_t& slot) {
-  if (knull) {
-    slot = t.cap;
-    return true;
-  }
-  if (key == EMPTY_KEY) {
-    slot = t.cap + 1;
-    return true;
-  }
-  uint64_t h = fmix64((uint64_t)key) & (t.cap - 1);
-#pragma unroll 1
-  for (int p = 0; p < HA_GLOBAL_MAXP; ++p) {
-    int64_t k = __hip_atomic_load(&t.keys[h], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (k == key) {
-      slot = h;
-      return true;
-    }
-    if (k == EMPTY_KEY) {
-      const int64_t old = (int64_t)atomicCAS((unsigned long long*)&t.keys[h], (unsigned long long)EMPTY_KEY,
-                                             (unsigned long long)key);
-      if (old == EMPTY_KEY) {
-        atomicAdd((unsigned long long*)&t.ctl[0], 1ull);
-        slot = h;
-        return true;
-      }
-      if (old == key) {
-        slot = h;
-        return true;
-      }
-    }
-    h = (h + 1) & (t.cap - 1);
-  }
-  return false;
-}
-
-__device__ __forceinline__ void gadd_cstar(const DTable& t, uint64_t slot, uint64_t c) {
-  const uint64_t old = atomicAdd((unsigned long long*)&t.cstar[slot], (unsigned long long)c);
-  if (slot >= t.cap && old == 0) atomicAdd((unsigned long long*)&t.ctl[0], 1ull);  // special group appears
-}
-
-// Combine one aggregate's partial state into global slot `s`.
-__device__ __forceinline__ void gcombine(const DTable& t, const DAgg& a, int j, uint64_t s, int64_t acc, uint64_t nn,
-                                         uint64_t i0, uint64_t i1, uint64_t i2, uint64_t i3) {
-  if (nn == 0) return;
-  atomicAdd((unsigned long long*)&t.nn[j][s], (unsigned long long)nn);
-  switch (a.acc) {
-    case ACC_SUM_I:
-      if (acc) atomicAdd((unsigned long long*)&t.acc[j][s], (unsigned long long)acc);
-      break;
-    case ACC_SUM_F: atomicAdd((double*)&t.acc[j][s], bits_f64(acc)); break;
-    case ACC_MIN_I:
-    case ACC_MIN_F:
-      if (acc != INT64_MAX) atomicMin((long long*)&t.acc[j][s], (long long)acc);
-      break;
-    case ACC_MAX_I:
-    case ACC_MAX_F:
-      if (acc != INT64_MIN) atomicMax((long long*)&t.acc[j][s], (long long)acc);
-      break;
-    default: break;
-  }
-  if (acc_is_f64mm(a.acc)) {
-    const uint64_t stride = t.cap + 2;
-    unsigned long long* ix = (unsigned long long*)t.idx[j];
-    if (i0 != UINT64_MAX) atomicMin(&ix[s], (unsigned long long)i0);
-    if (i1 != UINT64_MAX) atomicMin(&ix[stride + s], (unsigned long long)i1);
-    if (i2 != UINT64_MAX) atomicMin(&ix[2 * stride + s], (unsigned long long)i2);
-    if (i3 != UINT64_MAX) atomicMin(&ix[3 * stride + s], (unsigned long long)i3);
-  }
-}
-
-// Per-row contribution of one aggregate in partial form.
-struct RowVal {
-  int64_t acc;
-  uint64_t i0, i1, i2, i3;
-};
-
-__device__ __forceinline__ RowVal row_partial(int32_t acck, int64_t x, uint64_t row) {
-  RowVal r{acc_identity(acck), UINT64_MAX, UINT64_MAX, UINT64_MAX, UINT64_MAX};
-  switch (acck) {
-    case ACC_SUM_I:
-    case ACC_SUM_F:
-    case ACC_MIN_I:
-    case ACC_MAX_I: r.acc = x; break;
-    case ACC_MIN_F:
-    case ACC_MAX_F: {
-      const double d = bits_f64(x);
-      r.i0 = row;
-      if (d != d) {
-        r.i1 = row;
-      } else {
-        r.acc = f64_okey(d);
-        if (d == 0.0) {
-          if (x < 0) r.i2 = row;
-          else r.i3 = row;
-        }
-      }
-      break;
-    }
-    default: break;
-  }
-  return r;
-}
-
 // ---- LDS table -----------------------------------------------------------------------------------
-__device__ __forceinline__ int64_t* lds_keys(char* smem) { return (int64_t*)smem; }
+__device__ __forceinline__ qi64* lds_keys(char* smem) { return (qi64*)smem; }
 
-__device__ void lds_init(const Plan& P, char* smem) {
+__device__ __forceinline__ void lds_init(const Plan& P, char* smem) {
   const int SS = (1 << P.lds_log2) + 2;
-  int64_t* keys = lds_keys(smem);
-  uint32_t* cst = (uint32_t*)(smem + P.off_cstar);
+  qi64* keys = lds_keys(smem);
+  qu32* cst = (qu32*)(smem + P.off_cstar);
   for (int s = threadIdx.x; s < SS; s += blockDim.x) {
     keys[s] = EMPTY_KEY;
     cst[s] = 0;
@@ -236,48 +48,35 @@ __device__ void lds_init(const Plan& P, char* smem) {
     if (j >= P.naggs) break;
     const DAgg& a = P.aggs[j];
     if (a.acc != ACC_NONE) {
-      int64_t* acc = (int64_t*)(smem + P.off_acc[j]);
-      const int64_t id = acc_identity(a.acc);
+      qi64* acc = (qi64*)(smem + P.off_acc[j]);
+      const qi64 id = acc_identity(a.acc);
       for (int s = threadIdx.x; s < SS; s += blockDim.x) acc[s] = id;
     }
     if (a.track_nn) {
-      uint32_t* nn = (uint32_t*)(smem + P.off_nn[j]);
+      qu32* nn = (qu32*)(smem + P.off_nn[j]);
       for (int s = threadIdx.x; s < SS; s += blockDim.x) nn[s] = 0;
     }
     if (acc_is_f64mm(a.acc)) {
-      uint64_t* ix = (uint64_t*)(smem + P.off_idx[j]);
-      for (int s = threadIdx.x; s < 4 * SS; s += blockDim.x) ix[s] = UINT64_MAX;
+      qu64* ix = (qu64*)(smem + P.off_idx[j]);
+      for (int s = threadIdx.x; s < 4 * SS; s += blockDim.x) ix[s] = ~0ull;
     }
   }
 }
 
 // Slot of `key` in the LDS table, inserting it if absent; -1 when the probe limit is hit.
-__device__ __forceinline__ int lds_find(const Plan& P, char* smem, int64_t key, bool knull) {
+__device__ __forceinline__ int lds_find(const Plan& P, char* smem, qi64 key, bool knull) {
   const int S = 1 << P.lds_log2;
   if (knull) return S;
   if (key == EMPTY_KEY) return S + 1;
-  int64_t* keys = lds_keys(smem);
-  uint32_t h = lds_hash((uint64_t)key) >> (32 - P.lds_log2);
-#pragma unroll 1
-  for (int p = 0; p < HA_LDS_MAXP; ++p) {
-    const int64_t k = keys[h];
-    if (k == key) return (int)h;
-    if (k == EMPTY_KEY) {
-      const int64_t old = (int64_t)atomicCAS((unsigned long long*)&keys[h], (unsigned long long)EMPTY_KEY,
-                                             (unsigned long long)key);
-      if (old == EMPTY_KEY || old == key) return (int)h;
-    }
-    h = (h + 1) & (uint32_t)(S - 1);
-  }
-  return -1;
+  return lds_probe(lds_keys(smem), P.lds_log2, key, lds_hash((qu64)key) >> (32 - P.lds_log2));
 }
 
-__device__ __forceinline__ void lds_accum(const Plan& P, char* smem, int j, int s, int64_t x, bool valid,
-                                          uint64_t row) {
+__device__ __forceinline__ void lds_accum(const Plan& P, char* smem, int j, int s, qi64 x, bool valid,
+                                          qu64 row) {
   const DAgg& a = P.aggs[j];
   if (!valid) return;
-  if (a.track_nn) atomicAdd((uint32_t*)(smem + P.off_nn[j]) + s, 1u);
-  int64_t* acc = (int64_t*)(smem + P.off_acc[j]);
+  if (a.track_nn) atomicAdd((qu32*)(smem + P.off_nn[j]) + s, 1u);
+  qi64* acc = (qi64*)(smem + P.off_acc[j]);
   switch (a.acc) {
     case ACC_SUM_I: atomicAdd((unsigned long long*)&acc[s], (unsigned long long)x); break;
     case ACC_SUM_F: atomicAdd((double*)&acc[s], bits_f64(x)); break;
@@ -289,13 +88,13 @@ __device__ __forceinline__ void lds_accum(const Plan& P, char* smem, int j, int 
       const int SS = (1 << P.lds_log2) + 2;
       unsigned long long* ix = (unsigned long long*)(smem + P.off_idx[j]);
       atomicMin(&ix[s], (unsigned long long)r.i0);
-      if (r.i1 != UINT64_MAX) {
+      if (r.i1 != ~0ull) {
         atomicMin(&ix[SS + s], (unsigned long long)r.i1);
       } else {
         if (a.acc == ACC_MIN_F) atomicMin((long long*)&acc[s], (long long)r.acc);
         else atomicMax((long long*)&acc[s], (long long)r.acc);
-        if (r.i2 != UINT64_MAX) atomicMin(&ix[2 * SS + s], (unsigned long long)r.i2);
-        if (r.i3 != UINT64_MAX) atomicMin(&ix[3 * SS + s], (unsigned long long)r.i3);
+        if (r.i2 != ~0ull) atomicMin(&ix[2 * SS + s], (unsigned long long)r.i2);
+        if (r.i3 != ~0ull) atomicMin(&ix[3 * SS + s], (unsigned long long)r.i3);
       }
       break;
     }
@@ -303,35 +102,29 @@ __device__ __forceinline__ void lds_accum(const Plan& P, char* smem, int j, int 
   }
 }
 
-__device__ __forceinline__ void write_record_head(uint8_t* rec, int64_t key, bool knull, uint64_t cstar) {
-  ((int64_t*)rec)[0] = key;
-  ((uint64_t*)rec)[1] = knull ? 1ull : 0ull;
-  ((uint64_t*)rec)[2] = cstar;
-}
-
 // Merge the workgroup's LDS table into the global table (or the overflow records).
-__device__ void lds_flush(const Plan& P, char* smem) {
+__device__ __forceinline__ void lds_flush(const Plan& P, char* smem) {
   const int S = 1 << P.lds_log2;
   const int SS = S + 2;
-  const int64_t* keys = lds_keys(smem);
-  const uint32_t* cst = (const uint32_t*)(smem + P.off_cstar);
+  const qi64* keys = lds_keys(smem);
+  const qu32* cst = (const qu32*)(smem + P.off_cstar);
   for (int s = threadIdx.x; s < SS; s += blockDim.x) {
-    const uint32_t c = cst[s];
+    const qu32 c = cst[s];
     if (c == 0) continue;  // an occupied slot always has at least one row
     const bool knull = s == S;
-    const int64_t key = s == S ? 0 : (s == S + 1 ? EMPTY_KEY : keys[s]);
-    uint64_t gs;
+    const qi64 key = s == S ? 0 : (s == S + 1 ? EMPTY_KEY : keys[s]);
+    qu64 gs;
     const bool ok = gtable_find(P.t, key, knull, gs);
-    uint8_t* rec = nullptr;
+    qu8* rec = nullptr;
     if (ok) {
       gadd_cstar(P.t, gs, c);
     } else {
-      const uint64_t r = atomicAdd((unsigned long long*)&P.t.ctl[2], 1ull);
+      const qu64 r = atomicAdd((unsigned long long*)&P.t.ctl[2], 1ull);
       if (r >= P.ovf_cap) {
         atomicAdd((unsigned long long*)&P.t.ctl[3], 1ull);
         continue;
       }
-      rec = P.ovf + r * (uint64_t)P.rec_bytes;
+      rec = P.ovf + r * (qu64)P.rec_bytes;
       write_record_head(rec, key, knull, c);
     }
     int off = 24;
@@ -339,21 +132,21 @@ __device__ void lds_flush(const Plan& P, char* smem) {
     for (int j = 0; j < QE_MAX_AGGS; ++j) {
       if (j >= P.naggs) break;
       const DAgg& a = P.aggs[j];
-      const int64_t acc = a.acc != ACC_NONE ? ((const int64_t*)(smem + P.off_acc[j]))[s] : 0;
-      const uint64_t nn = a.track_nn ? ((const uint32_t*)(smem + P.off_nn[j]))[s] : c;
-      uint64_t i0 = UINT64_MAX, i1 = UINT64_MAX, i2 = UINT64_MAX, i3 = UINT64_MAX;
+      const qi64 acc = a.acc != ACC_NONE ? ((const qi64*)(smem + P.off_acc[j]))[s] : 0;
+      const qu64 nn = a.track_nn ? ((const qu32*)(smem + P.off_nn[j]))[s] : c;
+      qu64 i0 = ~0ull, i1 = ~0ull, i2 = ~0ull, i3 = ~0ull;
       if (acc_is_f64mm(a.acc)) {
-        const uint64_t* ix = (const uint64_t*)(smem + P.off_idx[j]);
+        const qu64* ix = (const qu64*)(smem + P.off_idx[j]);
         i0 = ix[s];
         i1 = ix[SS + s];
         i2 = ix[2 * SS + s];
         i3 = ix[3 * SS + s];
       }
       if (ok) {
-        if (a.fn != QE_AGG_COUNT_STAR) gcombine(P.t, a, j, gs, acc, nn, i0, i1, i2, i3);
+        if (a.fn != QE_AGG_COUNT_STAR) gcombine(P.t, a.acc, j, gs, acc, nn, i0, i1, i2, i3);
       } else {
-        uint64_t* f = (uint64_t*)(rec + off);
-        f[0] = (uint64_t)acc;
+        qu64* f = (qu64*)(rec + off);
+        f[0] = (qu64)acc;
         f[1] = nn;
         if (acc_is_f64mm(a.acc)) {
           f[2] = i0;
@@ -380,19 +173,52 @@ template <int NC>
 struct ColRegs {
   static constexpr int W = NC <= 1 ? 4 : NC <= 2 ? 8 : NC <= 4 ? 16 : 32;
   typename VecT<W>::type v;
-  uint32_t valid;  // nibble per slot
-  __device__ __forceinline__ int64_t get(int slot, int r) const { return v[4 * slot + r]; }
+  qu32 valid;  // nibble per slot
+  __device__ __forceinline__ qi64 get(int slot, int r) const { return v[4 * slot + r]; }
   __device__ __forceinline__ bool ok(int slot, int r) const { return (valid >> (4 * slot + r)) & 1u; }
 };
 
 typedef long long i64x2 __attribute__((ext_vector_type(2)));
 
-__device__ __forceinline__ int64_t row_of(int64_t base, int lane, int r) {
+__device__ __forceinline__ qi64 row_of(qi64 base, int lane, int r) {
   return base + 128 * (r >> 1) + 2 * lane + (r & 1);
 }
 
 template <int NC>
-__device__ __forceinline__ void load_cols(const Plan& P, int64_t base, int lane, bool full, ColRegs<NC>& R) {
+__device__ __forceinline__ void load_cols(const Plan& P, qi64 base, int lane, bool full, ColRegs<NC>& R) {
+  if (full && P.all8) {
+    // common case: every slot an 8-byte column, whole step in range -> 2*NC straight-line
+    // 16-B loads (each wave instruction = one contiguous KiB), validity nibbles after
+#pragma unroll
+    for (int c = 0; c < NC; ++c) {
+      if (c < P.ncols) {
+        const qi64* p = (const qi64*)P.cols[c].p + base + 2 * lane;
+        const i64x2 t0 = *(const i64x2*)p;
+        const i64x2 t1 = *(const i64x2*)(p + 128);
+        R.v[4 * c + 0] = t0.x;
+        R.v[4 * c + 1] = t0.y;
+        R.v[4 * c + 2] = t1.x;
+        R.v[4 * c + 3] = t1.y;
+      } else {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) R.v[4 * c + r] = 0;
+      }
+    }
+    qu32 valid = 0;
+#pragma unroll
+    for (int c = 0; c < NC; ++c) {
+      qu32 vv = 15u;
+      if (c < P.ncols && P.cols[c].valid) {
+        const qi64 r0 = base + 2 * lane;
+        const qu32 lo = (qu32)(P.cols[c].valid[r0 >> 3] >> (r0 & 7)) & 3u;
+        const qu32 hi = (qu32)(P.cols[c].valid[(r0 + 128) >> 3] >> (r0 & 7)) & 3u;
+        vv = lo | (hi << 2);
+      }
+      valid |= vv << (4 * c);
+    }
+    R.valid = valid;
+    return;
+  }
   R.valid = 0;
 #pragma unroll
   for (int c = 0; c < NC; ++c) {
@@ -404,31 +230,31 @@ __device__ __forceinline__ void load_cols(const Plan& P, int64_t base, int lane,
     const DCol& col = P.cols[c];
 #pragma unroll
     for (int q = 0; q < 2; ++q) {
-      const int64_t r0 = base + 128 * q + 2 * lane;
-      int64_t a = 0, b = 0;
+      const qi64 r0 = base + 128 * q + 2 * lane;
+      qi64 a = 0, b = 0;
       if (full) {
         switch (col.kind) {
           case K_I64:
           case K_F64: {
-            const i64x2 t = *(const i64x2*)((const int64_t*)col.p + r0);
+            const i64x2 t = *(const i64x2*)((const qi64*)col.p + r0);
             a = t.x;
             b = t.y;
             break;
           }
           case K_I32: {
-            const int2 t = *(const int2*)((const int32_t*)col.p + r0);
+            const int2 t = *(const int2*)((const qi32*)col.p + r0);
             a = t.x;
             b = t.y;
             break;
           }
           case K_U8: {
-            const uint16_t t = *(const uint16_t*)((const uint8_t*)col.p + r0);
+            const uint16_t t = *(const uint16_t*)((const qu8*)col.p + r0);
             a = t & 0xFF;
             b = t >> 8;
             break;
           }
           default: {  // K_BOOL
-            const uint32_t t = ((const uint8_t*)col.p)[r0 >> 3] >> (r0 & 7);
+            const qu32 t = ((const qu8*)col.p)[r0 >> 3] >> (r0 & 7);
             a = t & 1;
             b = (t >> 1) & 1;
           }
@@ -436,15 +262,15 @@ __device__ __forceinline__ void load_cols(const Plan& P, int64_t base, int lane,
       } else {
 #pragma unroll
         for (int e = 0; e < 2; ++e) {
-          const int64_t r = r0 + e;
-          int64_t x = 0;
+          const qi64 r = r0 + e;
+          qi64 x = 0;
           if (r < P.n) {
             switch (col.kind) {
               case K_I64:
-              case K_F64: x = ((const int64_t*)col.p)[r]; break;
-              case K_I32: x = ((const int32_t*)col.p)[r]; break;
-              case K_U8: x = ((const uint8_t*)col.p)[r]; break;
-              default: x = (((const uint8_t*)col.p)[r >> 3] >> (r & 7)) & 1;
+              case K_F64: x = ((const qi64*)col.p)[r]; break;
+              case K_I32: x = ((const qi32*)col.p)[r]; break;
+              case K_U8: x = ((const qu8*)col.p)[r]; break;
+              default: x = (((const qu8*)col.p)[r >> 3] >> (r & 7)) & 1;
             }
           }
           if (e) b = x;
@@ -453,13 +279,13 @@ __device__ __forceinline__ void load_cols(const Plan& P, int64_t base, int lane,
       }
       R.v[4 * c + 2 * q] = a;
       R.v[4 * c + 2 * q + 1] = b;
-      const uint32_t vv = col.valid ? ((uint32_t)(col.valid[r0 >> 3] >> (r0 & 7)) & 3u) : 3u;
+      const qu32 vv = col.valid ? ((qu32)(col.valid[r0 >> 3] >> (r0 & 7)) & 3u) : 3u;
       R.valid |= vv << (4 * c + 2 * q);
     }
   }
 }
 
-__device__ __forceinline__ bool cmp_i(int32_t op, int64_t a, int64_t b) {
+__device__ __forceinline__ bool cmp_i(qi32 op, qi64 a, qi64 b) {
   switch (op) {
     case QE_OP_EQ: return a == b;
     case QE_OP_NE: return a != b;
@@ -469,7 +295,7 @@ __device__ __forceinline__ bool cmp_i(int32_t op, int64_t a, int64_t b) {
     default: return a >= b;
   }
 }
-__device__ __forceinline__ bool cmp_f(int32_t op, double a, double b) {
+__device__ __forceinline__ bool cmp_f(qi32 op, double a, double b) {
   switch (op) {
     case QE_OP_EQ: return a == b;
     case QE_OP_NE: return a != b;
@@ -482,8 +308,8 @@ __device__ __forceinline__ bool cmp_f(int32_t op, double a, double b) {
 
 // Postfix program with a 4-deep register stack (constant-index rotations only).
 template <int NC>
-__device__ __forceinline__ int64_t eval_program(const DAgg& a, const ColRegs<NC>& R, int r, bool& valid) {
-  int64_t s0 = 0, s1 = 0, s2 = 0, s3 = 0;
+__device__ __forceinline__ qi64 eval_program(const DAgg& a, const ColRegs<NC>& R, int r, bool& valid) {
+  qi64 s0 = 0, s1 = 0, s2 = 0, s3 = 0;
   bool n0 = true, n1 = true, n2 = true, n3 = true;  // validity
   for (int t = 0; t < a.ntok; ++t) {
     const DTok& k = a.tok[t];
@@ -504,16 +330,16 @@ __device__ __forceinline__ int64_t eval_program(const DAgg& a, const ColRegs<NC>
     } else if (op == T_I2F1) {
       s1 = f64_bits((double)s1);
     } else {
-      int64_t res;
+      qi64 res;
       bool ok = n0 && n1;
-      const uint64_t ua = (uint64_t)s1, ub = (uint64_t)s0;
+      const qu64 ua = (qu64)s1, ub = (qu64)s0;
       switch (op) {
-        case T_ADD_I: res = (int64_t)(ua + ub); break;
-        case T_SUB_I: res = (int64_t)(ua - ub); break;
-        case T_MUL_I: res = (int64_t)(ua * ub); break;
+        case T_ADD_I: res = (qi64)(ua + ub); break;
+        case T_SUB_I: res = (qi64)(ua - ub); break;
+        case T_MUL_I: res = (qi64)(ua * ub); break;
         case T_DIV_I:
           if (s0 == 0) { res = 0; ok = false; }
-          else if (s0 == -1) res = (int64_t)(0ull - ua);
+          else if (s0 == -1) res = (qi64)(0ull - ua);
           else res = s1 / s0;
           break;
         case T_ADD_F: res = f64_bits(bits_f64(s1) + bits_f64(s0)); break;
@@ -530,114 +356,358 @@ __device__ __forceinline__ int64_t eval_program(const DAgg& a, const ColRegs<NC>
   return s0;
 }
 
-// Aggregate j's input for row r: value bits, validity in `valid`.
-template <int NC>
-__device__ __forceinline__ int64_t eval_input(const DAgg& a, const ColRegs<NC>& R, int r, bool& valid) {
-  if (a.pkind == 1) {
-    valid = R.ok(a.col, r);
-    const int64_t x = R.get(a.col, r);
-    return a.cvt_i2f ? f64_bits((double)x) : x;
+__device__ __forceinline__ qi64 binop(qi32 op, qi64 l, qi64 r, bool& ok) {
+  const qu64 ua = (qu64)l, ub = (qu64)r;
+  switch (op) {
+    case T_ADD_I: return (qi64)(ua + ub);
+    case T_SUB_I: return (qi64)(ua - ub);
+    case T_MUL_I: return (qi64)(ua * ub);
+    case T_DIV_I:
+      if (r == 0) {
+        ok = false;
+        return 0;
+      }
+      return r == -1 ? (qi64)(0ull - ua) : l / r;
+    case T_ADD_F: return f64_bits(bits_f64(l) + bits_f64(r));
+    case T_SUB_F: return f64_bits(bits_f64(l) - bits_f64(r));
+    case T_MUL_F: return f64_bits(bits_f64(l) * bits_f64(r));
+    default: return f64_bits(bits_f64(l) / bits_f64(r));
   }
-  return eval_program<NC>(a, R, r, valid);
+}
+
+// Aggregate input for row r without the interpreter (pkind 1 and 3).
+template <int NC>
+__device__ __forceinline__ qi64 eval_fast(const DAgg& a, const ColRegs<NC>& R, int r, bool& valid) {
+  const qi64 x = R.get(a.col, r);
+  valid = R.ok(a.col, r);
+  if (a.pkind == 1) return a.cvt_i2f ? f64_bits((double)x) : x;
+  const qi64 y = a.rhs >= 0 ? R.get(a.rhs, r) : a.rhs_lit;
+  valid = valid && (a.rhs >= 0 ? R.ok(a.rhs, r) : !a.rhs_null);
+  return binop(a.bop, x, y, valid);
+}
+
+typedef long long i64x4 __attribute__((ext_vector_type(4)));
+
+// Row-parallel accumulate of one aggregate input into its group slot (LDS or global).
+__device__ __forceinline__ void accum_row(const Plan& P, char* smem, int j, const DAgg& a, int s, qu64 gs,
+                                          qi64 x, bool valid, qu64 row) {
+  if (s >= 0) {
+    lds_accum(P, smem, j, s, x, valid, row);
+  } else if (valid) {
+    const RowVal rv = row_partial(a.acc, x, row);
+    gcombine(P.t, a.acc, j, gs, rv.acc, 1, rv.i0, rv.i1, rv.i2, rv.i3);
+  }
+}
+
+// ---- unswitched helpers: every uniform decision is taken once per step, rows loop inside ----
+// The 4 rows of slot `c` (compile-time register indices inside each case).
+template <int NC>
+__device__ __forceinline__ void get4(const ColRegs<NC>& R, int c, qi64 (&x)[4], qu32& ok) {
+#pragma unroll
+  for (int k = 0; k < NC; ++k) {
+    if (c == k) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) x[r] = R.v[4 * k + r];
+      ok = (R.valid >> (4 * k)) & 15u;
+    }
+  }
+}
+
+template <typename F>
+__device__ __forceinline__ qu32 cmp4(const qi64 (&a)[4], const qi64 (&b)[4], F f) {
+  qu32 m = 0;
+#pragma unroll
+  for (int r = 0; r < 4; ++r) m |= (qu32)f(a[r], b[r]) << r;
+  return m;
+}
+
+// Rows of `a` (op) `b` that are true, as a 4-bit mask (op and domain are wave-uniform).
+__device__ __forceinline__ qu32 compare4(qi32 op, bool f64, const qi64 (&a)[4], const qi64 (&b)[4]) {
+  if (!f64) {
+    switch (op) {
+      case QE_OP_EQ: return cmp4(a, b, [](qi64 x, qi64 y) { return x == y; });
+      case QE_OP_NE: return cmp4(a, b, [](qi64 x, qi64 y) { return x != y; });
+      case QE_OP_LT: return cmp4(a, b, [](qi64 x, qi64 y) { return x < y; });
+      case QE_OP_LE: return cmp4(a, b, [](qi64 x, qi64 y) { return x <= y; });
+      case QE_OP_GT: return cmp4(a, b, [](qi64 x, qi64 y) { return x > y; });
+      default: return cmp4(a, b, [](qi64 x, qi64 y) { return x >= y; });
+    }
+  }
+  switch (op) {
+    case QE_OP_EQ: return cmp4(a, b, [](qi64 x, qi64 y) { return bits_f64(x) == bits_f64(y); });
+    case QE_OP_NE: return cmp4(a, b, [](qi64 x, qi64 y) { return bits_f64(x) != bits_f64(y); });
+    case QE_OP_LT: return cmp4(a, b, [](qi64 x, qi64 y) { return bits_f64(x) < bits_f64(y); });
+    case QE_OP_LE: return cmp4(a, b, [](qi64 x, qi64 y) { return bits_f64(x) <= bits_f64(y); });
+    case QE_OP_GT: return cmp4(a, b, [](qi64 x, qi64 y) { return bits_f64(x) > bits_f64(y); });
+    default: return cmp4(a, b, [](qi64 x, qi64 y) { return bits_f64(x) >= bits_f64(y); });
+  }
+}
+
+template <typename F>
+__device__ __forceinline__ void map4(qi64 (&x)[4], const qi64 (&y)[4], F f) {
+#pragma unroll
+  for (int r = 0; r < 4; ++r) x[r] = f(x[r], y[r]);
+}
+
+// x = x (op) y for the 4 rows; int64 division by zero clears the row's bit in `ok`.
+__device__ __forceinline__ void binop4(qi32 op, qi64 (&x)[4], const qi64 (&y)[4], qu32& ok) {
+  switch (op) {
+    case T_ADD_I: map4(x, y, [](qi64 a, qi64 b) { return (qi64)((qu64)a + (qu64)b); }); break;
+    case T_SUB_I: map4(x, y, [](qi64 a, qi64 b) { return (qi64)((qu64)a - (qu64)b); }); break;
+    case T_MUL_I: map4(x, y, [](qi64 a, qi64 b) { return (qi64)((qu64)a * (qu64)b); }); break;
+    case T_ADD_F: map4(x, y, [](qi64 a, qi64 b) { return f64_bits(bits_f64(a) + bits_f64(b)); }); break;
+    case T_SUB_F: map4(x, y, [](qi64 a, qi64 b) { return f64_bits(bits_f64(a) - bits_f64(b)); }); break;
+    case T_MUL_F: map4(x, y, [](qi64 a, qi64 b) { return f64_bits(bits_f64(a) * bits_f64(b)); }); break;
+    case T_DIV_F: map4(x, y, [](qi64 a, qi64 b) { return f64_bits(bits_f64(a) / bits_f64(b)); }); break;
+    default:  // T_DIV_I
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        bool v = true;
+        x[r] = binop(T_DIV_I, x[r], y[r], v);
+        if (!v) ok &= ~(1u << r);
+      }
+  }
+}
+
+// LDS accumulate of one aggregate for the active rows (acc kind switched once).
+__device__ __forceinline__ void lds_accum4(const Plan& P, char* smem, int j, const DAgg& a, const int (&slot)[4],
+                                           const qi64 (&x)[4], qu32 m, qi64 row0, int lane) {
+  if (a.track_nn) {
+    qu32* nn = (qu32*)(smem + P.off_nn[j]);
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+      if ((m >> r) & 1) atomicAdd(nn + slot[r], 1u);
+  }
+  qi64* acc = (qi64*)(smem + P.off_acc[j]);
+  switch (a.acc) {
+    case ACC_SUM_I:
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+        if ((m >> r) & 1) atomicAdd((unsigned long long*)&acc[slot[r]], (unsigned long long)x[r]);
+      break;
+    case ACC_SUM_F:
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+        if ((m >> r) & 1) atomicAdd((double*)&acc[slot[r]], bits_f64(x[r]));
+      break;
+    case ACC_MIN_I:
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+        if ((m >> r) & 1) atomicMin((long long*)&acc[slot[r]], (long long)x[r]);
+      break;
+    case ACC_MAX_I:
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+        if ((m >> r) & 1) atomicMax((long long*)&acc[slot[r]], (long long)x[r]);
+      break;
+    case ACC_MIN_F:
+    case ACC_MAX_F:
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+        if ((m >> r) & 1) lds_accum(P, smem, j, slot[r], x[r], true, (qu64)(row0 + row_of(0, lane, r)));
+      break;
+    default: break;
+  }
 }
 
 template <int NC, bool USE_LDS>
-__global__ void __launch_bounds__(HA_THREADS) k_hashagg(const Plan P) {
+__device__ __forceinline__ void process_step(const Plan& P, char* smem, const ColRegs<NC>& R, qi64 base,
+                                             int lane) {
+  qu32 act = 0;
+#pragma unroll
+  for (int r = 0; r < 4; ++r) act |= (qu32)(row_of(base, lane, r) < P.n) << r;
+  if (P.defer_in) {
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const qi64 row = row_of(base, lane, r);
+      if (row < P.n && !((P.defer_in[row >> 5] >> (row & 31)) & 1)) act &= ~(1u << r);
+    }
+  }
+  if (P.mask_col >= 0) {
+    qi64 mv[4];
+    qu32 ok = 0;
+    get4(R, P.mask_col, mv, ok);
+    qu32 bits = 0;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) bits |= (qu32)(mv[r] & 1) << r;
+    act &= bits & ok;
+  }
+  for (int t = 0; t < P.nterms; ++t) {
+    const DTerm& T = P.terms[t];
+    qi64 a[4], b[4];
+    qu32 aok = 0, bok = 15u;
+    get4(R, T.lhs, a, aok);
+    if (T.rhs >= 0) {
+      get4(R, T.rhs, b, bok);
+    } else {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) b[r] = T.lit;
+      bok = T.lit_null ? 0u : 15u;
+    }
+    if (T.f64) {  // integral sides promote to fp64
+      if (!T.lhs_f) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) a[r] = f64_bits((double)a[r]);
+      }
+      if (!T.rhs_f) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) b[r] = f64_bits((double)b[r]);
+      }
+    }
+    act &= compare4(T.op, T.f64, a, b) & aok & bok;
+  }
+  if (act == 0) return;
+  // ---- group keys of the lane's 4 rows
+  qi64 key[4] = {0, 0, 0, 0};
+  qu32 knull = 0;
+  if (P.key_mode == 1) {
+    qu32 ok = 0;
+    get4(R, P.key_col[0], key, ok);
+    knull = ~ok & 15u;
+    if (P.key_f64) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+        if (bits_f64(key[r]) != bits_f64(key[r])) key[r] = 0x7FF8000000000000ll;  // Double.equals: one NaN
+    }
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+      if ((knull >> r) & 1) key[r] = 0;
+  } else if (P.key_mode == 2) {
+    for (int q = 0; q < P.nkeys; ++q) {
+      qi64 x[4];
+      qu32 ok = 0;
+      get4(R, P.key_col[q], x, ok);
+      const qi64 fm = P.key_fmask[q];
+      const int sh = P.key_shift[q], nb = P.key_nullbit[q];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const bool isn = !((ok >> r) & 1);
+        key[r] |= ((isn ? 0 : (x[r] & fm)) << sh) | ((qi64)isn << nb);
+      }
+    }
+  }
+  // ---- slots: first LDS probe of all 4 rows issued together; collisions (rare) probe on
+  int slot[4] = {-1, -1, -1, -1};
+  if (USE_LDS) {
+    const int S = 1 << P.lds_log2;
+    const qi64* keys = lds_keys(smem);
+    qu32 h[4];
+    qi64 k0[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      h[r] = lds_hash((qu64)key[r]) >> (32 - P.lds_log2);
+      k0[r] = ((act >> r) & 1) ? keys[h[r]] : 0;
+    }
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      if ((knull >> r) & 1) slot[r] = S;
+      else if (key[r] == EMPTY_KEY) slot[r] = S + 1;
+      else if (k0[r] == key[r]) slot[r] = (int)h[r];
+    }
+    qu32 miss = 0;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) miss |= (qu32)(slot[r] < 0) << r;
+    miss &= act;
+    if (__any(miss != 0)) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+        if ((miss >> r) & 1) slot[r] = lds_find(P, smem, key[r], false);
+    }
+  }
+  qu32 glob = 0;  // rows whose group lives only in the global table (rare slow path)
+#pragma unroll
+  for (int r = 0; r < 4; ++r) glob |= (qu32)(slot[r] < 0) << r;
+  glob &= act;
+  const qu32 loc = act & ~glob;
+  qu32* cst = (qu32*)(smem + P.off_cstar);
+#pragma unroll
+  for (int r = 0; r < 4; ++r)
+    if ((loc >> r) & 1) atomicAdd(cst + slot[r], 1u);
+  // ---- aggregate inputs, LDS rows
+  if (__any(loc != 0)) {
+    for (int j = 0; j < P.naggs; ++j) {
+      const DAgg& a = P.aggs[j];
+      if (a.pkind == 0) continue;
+      qi64 x[4];
+      qu32 xok = 0;
+      if (a.pkind == 2) {
+        i64x4 xv;
+        for (int r = 0; r < 4; ++r) {
+          bool ok = false;
+          xv[r] = ((loc >> r) & 1) ? eval_program<NC>(a, R, r, ok) : 0;
+          xok |= (qu32)ok << r;
+        }
+#pragma unroll
+        for (int r = 0; r < 4; ++r) x[r] = xv[r];
+      } else {
+        get4(R, a.col, x, xok);
+        if (a.pkind == 1) {
+          if (a.cvt_i2f) {
+#pragma unroll
+            for (int r = 0; r < 4; ++r) x[r] = f64_bits((double)x[r]);
+          }
+        } else {
+          qi64 y[4];
+          qu32 yok = 15u;
+          if (a.rhs >= 0) {
+            get4(R, a.rhs, y, yok);
+          } else {
+#pragma unroll
+            for (int r = 0; r < 4; ++r) y[r] = a.rhs_lit;
+            yok = a.rhs_null ? 0u : 15u;
+          }
+          xok &= yok;
+          binop4(a.bop, x, y, xok);
+        }
+      }
+      lds_accum4(P, smem, j, a, slot, x, loc & xok, P.row_base + base, lane);
+    }
+  }
+  // ---- rows whose group is only in the global table (LDS table full / global-only mode)
+  if (__any(glob != 0)) {
+    for (int r = 0; r < 4; ++r) {
+      if (!((glob >> r) & 1)) continue;
+      qu64 gs;
+      const qi64 lr = row_of(base, lane, r);
+      if (!gtable_find(P.t, key[r], (knull >> r) & 1, gs)) {  // global table full: defer the row
+        atomicOr(&P.defer_out[lr >> 5], 1u << (lr & 31));
+        atomicAdd((unsigned long long*)&P.t.ctl[1], 1ull);
+        continue;
+      }
+      gadd_cstar(P.t, gs, 1);
+      const qu64 row = (qu64)(P.row_base + lr);
+      for (int j = 0; j < P.naggs; ++j) {
+        const DAgg& a = P.aggs[j];
+        if (a.pkind == 0) continue;
+        bool valid;
+        const qi64 x = a.pkind == 2 ? eval_program<NC>(a, R, r, valid) : eval_fast<NC>(a, R, r, valid);
+        if (!valid) continue;
+        const RowVal rv = row_partial(a.acc, x, row);
+        gcombine(P.t, a.acc, j, gs, rv.acc, 1, rv.i0, rv.i1, rv.i2, rv.i3);
+      }
+    }
+  }
+}
+
+template <int NC, bool USE_LDS>
+__global__ void __launch_bounds__(HA_THREADS, 4) k_hashagg(const Plan P) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   if (USE_LDS) {
     lds_init(P, smem);
     __syncthreads();
   }
   const int lane = threadIdx.x & 63;
-  const int64_t wave = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 6;
-  const int64_t nwaves = ((int64_t)gridDim.x * blockDim.x) >> 6;
-  for (int64_t base = wave * 256; base < P.n; base += nwaves * 256) {
-    const bool full = base + 256 <= P.n;
-    ColRegs<NC> R;
-    load_cols<NC>(P, base, lane, full, R);
-    uint32_t act = 0;
-#pragma unroll
-    for (int r = 0; r < 4; ++r) act |= (uint32_t)(row_of(base, lane, r) < P.n) << r;
-    if (P.defer_in) {
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int64_t row = row_of(base, lane, r);
-        if (row < P.n && !((P.defer_in[row >> 5] >> (row & 31)) & 1)) act &= ~(1u << r);
-      }
-    }
-    if (P.mask_col >= 0) {
-#pragma unroll
-      for (int r = 0; r < 4; ++r)
-        if (!(R.get(P.mask_col, r) & 1) || !R.ok(P.mask_col, r)) act &= ~(1u << r);
-    }
-    for (int t = 0; t < P.nterms; ++t) {
-      const DTerm& T = P.terms[t];
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int64_t a = R.get(T.lhs, r);
-        const int64_t b = T.rhs >= 0 ? R.get(T.rhs, r) : T.lit;
-        const bool bv = T.rhs >= 0 ? R.ok(T.rhs, r) : !T.lit_null;
-        bool ok;
-        if (T.f64) {
-          const double da = T.lhs_f ? bits_f64(a) : (double)a;
-          const double db = T.rhs_f ? bits_f64(b) : (double)b;
-          ok = cmp_f(T.op, da, db);
-        } else {
-          ok = cmp_i(T.op, a, b);
-        }
-        if (!(ok && R.ok(T.lhs, r) && bv)) act &= ~(1u << r);
-      }
-    }
-    if (act == 0) continue;
-#pragma unroll 1
-    for (int r = 0; r < 4; ++r) {
-      if (!((act >> r) & 1)) continue;
-      const uint64_t row = (uint64_t)(P.row_base + row_of(base, lane, r));
-      // ---- group key
-      int64_t key = 0;
-      bool knull = false;
-      if (P.key_mode == 1) {
-        key = R.get(P.key_col[0], r);
-        knull = !R.ok(P.key_col[0], r);
-        if (P.key_f64 && bits_f64(key) != bits_f64(key)) key = 0x7FF8000000000000ll;  // Double.equals: one NaN
-        if (knull) key = 0;
-      } else if (P.key_mode == 2) {
-        for (int k = 0; k < P.nkeys; ++k) {
-          const int c = P.key_col[k];
-          const bool isn = !R.ok(c, r);
-          const int64_t x = isn ? 0 : (R.get(c, r) & P.key_fmask[k]);
-          key |= (x << P.key_shift[k]) | ((int64_t)isn << P.key_nullbit[k]);
-        }
-      }
-      // ---- slot: LDS table first, the global table when the LDS probe fails
-      int s = -1;
-      uint64_t gs = 0;
-      if (USE_LDS) s = lds_find(P, smem, key, knull);
-      if (s >= 0) {
-        atomicAdd((uint32_t*)(smem + P.off_cstar) + s, 1u);
-      } else {
-        if (!gtable_find(P.t, key, knull, gs)) {
-          const int64_t lr = row_of(base, lane, r);
-          atomicOr(&P.defer_out[lr >> 5], 1u << (lr & 31));
-          atomicAdd((unsigned long long*)&P.t.ctl[1], 1ull);
-          continue;
-        }
-        gadd_cstar(P.t, gs, 1);
-      }
-      // ---- aggregate inputs (one inlined evaluator per kernel)
-      for (int j = 0; j < P.naggs; ++j) {
-        const DAgg& a = P.aggs[j];
-        if (a.pkind == 0) continue;
-        bool valid;
-        const int64_t x = eval_input<NC>(a, R, r, valid);
-        if (s >= 0) {
-          lds_accum(P, smem, j, s, x, valid, row);
-        } else if (valid) {
-          const RowVal rv = row_partial(a.acc, x, row);
-          gcombine(P.t, a, j, gs, rv.acc, 1, rv.i0, rv.i1, rv.i2, rv.i3);
-        }
-      }
-    }
+  const qi64 wave = (blockIdx.x * (qi64)blockDim.x + threadIdx.x) >> 6;
+  const qi64 stride = (((qi64)gridDim.x * blockDim.x) >> 6) * 256;
+  // Register double buffer: the next step's columns are in flight while this step is processed.
+  ColRegs<NC> cur, nxt;
+  qi64 base = wave * 256;
+  if (base < P.n) load_cols<NC>(P, base, lane, base + 256 <= P.n, cur);
+  for (; base < P.n; base += stride) {
+    const qi64 nb = base + stride;
+    if (nb < P.n) load_cols<NC>(P, nb, lane, nb + 256 <= P.n, nxt);
+    process_step<NC, USE_LDS>(P, smem, cur, base, lane);
+    cur = nxt;
   }
   if (USE_LDS) {
     __syncthreads();
@@ -647,37 +717,37 @@ __global__ void __launch_bounds__(HA_THREADS) k_hashagg(const Plan P) {
 
 // ---- table maintenance kernels -------------------------------------------------------------------
 struct AggMeta {
-  int32_t naggs;
-  int32_t fn[QE_MAX_AGGS];
-  int32_t acc[QE_MAX_AGGS];
+  qi32 naggs;
+  qi32 fn[QE_MAX_AGGS];
+  qi32 acc[QE_MAX_AGGS];
 };
 
 __global__ void k_table_init(DTable t, AggMeta m) {
-  const uint64_t SS = t.cap + 2;
-  for (uint64_t s = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; s < SS; s += (uint64_t)gridDim.x * blockDim.x) {
+  const qu64 SS = t.cap + 2;
+  for (qu64 s = blockIdx.x * (qu64)blockDim.x + threadIdx.x; s < SS; s += (qu64)gridDim.x * blockDim.x) {
     t.keys[s] = EMPTY_KEY;
     t.cstar[s] = 0;
     for (int j = 0; j < m.naggs; ++j) {
       t.acc[j][s] = acc_identity(m.acc[j]);
       t.nn[j][s] = 0;
       if (acc_is_f64mm(m.acc[j]))
-        for (int k = 0; k < 4; ++k) t.idx[j][k * SS + s] = UINT64_MAX;
+        for (int k = 0; k < 4; ++k) t.idx[j][k * SS + s] = ~0ull;
     }
   }
 }
 
-__device__ __forceinline__ bool gslot_occupied(const DTable& t, uint64_t s) {
+__device__ __forceinline__ bool gslot_occupied(const DTable& t, qu64 s) {
   return s < t.cap ? t.keys[s] != EMPTY_KEY : t.cstar[s] > 0;
 }
 
 // Merge every occupied slot of `src` into `dst` (table growth).
 __global__ void k_rehash(DTable src, DTable dst, AggMeta m) {
-  const uint64_t SS = src.cap + 2;
-  for (uint64_t s = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; s < SS; s += (uint64_t)gridDim.x * blockDim.x) {
+  const qu64 SS = src.cap + 2;
+  for (qu64 s = blockIdx.x * (qu64)blockDim.x + threadIdx.x; s < SS; s += (qu64)gridDim.x * blockDim.x) {
     if (!gslot_occupied(src, s)) continue;
     const bool knull = s == src.cap;
-    const int64_t key = knull ? 0 : (s == src.cap + 1 ? EMPTY_KEY : src.keys[s]);
-    uint64_t d;
+    const qi64 key = knull ? 0 : (s == src.cap + 1 ? EMPTY_KEY : src.keys[s]);
+    qu64 d;
     if (!gtable_find(dst, key, knull, d)) {
       atomicAdd((unsigned long long*)&dst.ctl[3], 1ull);
       continue;
@@ -687,22 +757,22 @@ __global__ void k_rehash(DTable src, DTable dst, AggMeta m) {
       DAgg a{};
       a.fn = m.fn[j];
       a.acc = m.acc[j];
-      uint64_t i[4] = {UINT64_MAX, UINT64_MAX, UINT64_MAX, UINT64_MAX};
+      qu64 i[4] = {~0ull, ~0ull, ~0ull, ~0ull};
       if (acc_is_f64mm(a.acc))
         for (int k = 0; k < 4; ++k) i[k] = src.idx[j][k * SS + s];
-      gcombine(dst, a, j, d, src.acc[j][s], src.nn[j][s], i[0], i[1], i[2], i[3]);
+      gcombine(dst, a.acc, j, d, src.acc[j][s], src.nn[j][s], i[0], i[1], i[2], i[3]);
     }
   }
 }
 
 // Merge fixed-size records (export format) into `dst`.
-__global__ void k_import(const uint8_t* __restrict__ recs, int64_t nrec, int32_t rec_bytes, DTable dst, AggMeta m) {
-  for (int64_t r = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; r < nrec; r += (int64_t)gridDim.x * blockDim.x) {
-    const uint8_t* rec = recs + r * rec_bytes;
-    const int64_t key = ((const int64_t*)rec)[0];
-    const bool knull = ((const uint64_t*)rec)[1] & 1;
-    const uint64_t c = ((const uint64_t*)rec)[2];
-    uint64_t d;
+__global__ void k_import(const qu8* __restrict__ recs, qi64 nrec, qi32 rec_bytes, DTable dst, AggMeta m) {
+  for (qi64 r = blockIdx.x * (qi64)blockDim.x + threadIdx.x; r < nrec; r += (qi64)gridDim.x * blockDim.x) {
+    const qu8* rec = recs + r * rec_bytes;
+    const qi64 key = ((const qi64*)rec)[0];
+    const bool knull = ((const qu64*)rec)[1] & 1;
+    const qu64 c = ((const qu64*)rec)[2];
+    qu64 d;
     if (!gtable_find(dst, key, knull, d)) {
       atomicAdd((unsigned long long*)&dst.ctl[3], 1ull);
       continue;
@@ -713,46 +783,46 @@ __global__ void k_import(const uint8_t* __restrict__ recs, int64_t nrec, int32_t
       DAgg a{};
       a.fn = m.fn[j];
       a.acc = m.acc[j];
-      const uint64_t* f = (const uint64_t*)(rec + off);
+      const qu64* f = (const qu64*)(rec + off);
       if (a.fn != QE_AGG_COUNT_STAR) {
-        if (acc_is_f64mm(a.acc)) gcombine(dst, a, j, d, (int64_t)f[0], f[1], f[2], f[3], f[4], f[5]);
-        else gcombine(dst, a, j, d, (int64_t)f[0], f[1], UINT64_MAX, UINT64_MAX, UINT64_MAX, UINT64_MAX);
+        if (acc_is_f64mm(a.acc)) gcombine(dst, a.acc, j, d, (qi64)f[0], f[1], f[2], f[3], f[4], f[5]);
+        else gcombine(dst, a.acc, j, d, (qi64)f[0], f[1], ~0ull, ~0ull, ~0ull, ~0ull);
       }
       off += agg_rec_bytes(a.acc);
     }
   }
 }
 
-__device__ __forceinline__ uint32_t partition_of(int64_t key, bool knull, int32_t nparts) {
-  const uint64_t h = fmix64((uint64_t)key ^ (knull ? NULL_SALT : 0ull));
-  return (uint32_t)(((h >> 32) * (uint64_t)nparts) >> 32);
+__device__ __forceinline__ qu32 partition_of(qi64 key, bool knull, qi32 nparts) {
+  const qu64 h = fmix64((qu64)key ^ (knull ? NULL_SALT : 0ull));
+  return (qu32)(((h >> 32) * (qu64)nparts) >> 32);
 }
 
-__global__ void k_export_count(DTable t, int32_t nparts, unsigned long long* counts) {
-  const uint64_t SS = t.cap + 2;
-  for (uint64_t s = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; s < SS; s += (uint64_t)gridDim.x * blockDim.x) {
+__global__ void k_export_count(DTable t, qi32 nparts, unsigned long long* counts) {
+  const qu64 SS = t.cap + 2;
+  for (qu64 s = blockIdx.x * (qu64)blockDim.x + threadIdx.x; s < SS; s += (qu64)gridDim.x * blockDim.x) {
     if (!gslot_occupied(t, s)) continue;
     const bool knull = s == t.cap;
-    const int64_t key = knull ? 0 : (s == t.cap + 1 ? EMPTY_KEY : t.keys[s]);
+    const qi64 key = knull ? 0 : (s == t.cap + 1 ? EMPTY_KEY : t.keys[s]);
     atomicAdd(&counts[partition_of(key, knull, nparts)], 1ull);
   }
 }
 
-__global__ void k_export(DTable t, AggMeta m, int32_t nparts, int32_t rec_bytes, unsigned long long* cursor,
-                         uint8_t* __restrict__ dst) {
-  const uint64_t SS = t.cap + 2;
-  for (uint64_t s = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; s < SS; s += (uint64_t)gridDim.x * blockDim.x) {
+__global__ void k_export(DTable t, AggMeta m, qi32 nparts, qi32 rec_bytes, unsigned long long* cursor,
+                         qu8* __restrict__ dst) {
+  const qu64 SS = t.cap + 2;
+  for (qu64 s = blockIdx.x * (qu64)blockDim.x + threadIdx.x; s < SS; s += (qu64)gridDim.x * blockDim.x) {
     if (!gslot_occupied(t, s)) continue;
     const bool knull = s == t.cap;
-    const int64_t key = knull ? 0 : (s == t.cap + 1 ? EMPTY_KEY : t.keys[s]);
-    const uint32_t p = partition_of(key, knull, nparts);
-    const uint64_t pos = atomicAdd(&cursor[p], 1ull);
-    uint8_t* rec = dst + pos * (uint64_t)rec_bytes;
+    const qi64 key = knull ? 0 : (s == t.cap + 1 ? EMPTY_KEY : t.keys[s]);
+    const qu32 p = partition_of(key, knull, nparts);
+    const qu64 pos = atomicAdd(&cursor[p], 1ull);
+    qu8* rec = dst + pos * (qu64)rec_bytes;
     write_record_head(rec, key, knull, t.cstar[s]);
     int off = 24;
     for (int j = 0; j < m.naggs; ++j) {
-      uint64_t* f = (uint64_t*)(rec + off);
-      f[0] = (uint64_t)t.acc[j][s];
+      qu64* f = (qu64*)(rec + off);
+      f[0] = (qu64)t.acc[j][s];
       f[1] = t.nn[j][s];
       if (acc_is_f64mm(m.acc[j]))
         for (int k = 0; k < 4; ++k) f[2 + k] = t.idx[j][k * SS + s];
@@ -762,14 +832,14 @@ __global__ void k_export(DTable t, AggMeta m, int32_t nparts, int32_t rec_bytes,
 }
 
 // ---- finalize: occupied slots -> one output batch --------------------------------------------------
-__global__ void k_occ_count(DTable t, int64_t* __restrict__ tile_counts, int32_t tile_slots) {
+__global__ void k_occ_count(DTable t, qi64* __restrict__ tile_counts, qi32 tile_slots) {
   // one block per tile of `tile_slots` slots
-  __shared__ int64_t part[4];
-  const uint64_t SS = t.cap + 2;
-  const uint64_t s0 = (uint64_t)blockIdx.x * tile_slots;
-  int64_t c = 0;
+  __shared__ qi64 part[4];
+  const qu64 SS = t.cap + 2;
+  const qu64 s0 = (qu64)blockIdx.x * tile_slots;
+  qi64 c = 0;
   for (int i = threadIdx.x; i < tile_slots; i += blockDim.x) {
-    const uint64_t s = s0 + i;
+    const qu64 s = s0 + i;
     if (s < SS && gslot_occupied(t, s)) ++c;
   }
   for (int off = 32; off > 0; off >>= 1) c += __shfl_xor(c, off);
@@ -784,38 +854,38 @@ struct OutCols {
 };
 
 struct KeyMeta {
-  int32_t mode, nkeys;
-  int32_t type[QE_MAX_KEYS], shift[QE_MAX_KEYS], nullbit[QE_MAX_KEYS];
-  int64_t fmask[QE_MAX_KEYS];
+  qi32 mode, nkeys;
+  qi32 type[QE_MAX_KEYS], shift[QE_MAX_KEYS], nullbit[QE_MAX_KEYS];
+  qi64 fmask[QE_MAX_KEYS];
 };
 
-__device__ __forceinline__ void set_bit(uint8_t* bm, int64_t i, bool v) {
+__device__ __forceinline__ void set_bit(qu8* bm, qi64 i, bool v) {
   // bytes are written by whole 32-bit atomics: the host zeroes validity buffers first
-  if (v) atomicOr((uint32_t*)bm + (i >> 5), 1u << (i & 31));
+  if (v) atomicOr((qu32*)bm + (i >> 5), 1u << (i & 31));
 }
 
-__device__ __forceinline__ void store_typed(void* p, int32_t type, int64_t i, int64_t x) {
+__device__ __forceinline__ void store_typed(void* p, qi32 type, qi64 i, qi64 x) {
   switch (type) {
     case QE_TYPE_INT64:
-    case QE_TYPE_FLOAT64: ((int64_t*)p)[i] = x; break;
+    case QE_TYPE_FLOAT64: ((qi64*)p)[i] = x; break;
     case QE_TYPE_INT32:
-    case QE_TYPE_DATE32: ((int32_t*)p)[i] = (int32_t)x; break;
-    default: ((uint8_t*)p)[i] = (uint8_t)x;
+    case QE_TYPE_DATE32: ((qi32*)p)[i] = (qi32)x; break;
+    default: ((qu8*)p)[i] = (qu8)x;
   }
 }
 
-__global__ void k_finalize(DTable t, AggMeta m, KeyMeta km, const int64_t* __restrict__ tile_offsets,
-                           int32_t tile_slots, OutCols out) {
+__global__ void k_finalize(DTable t, AggMeta m, KeyMeta km, const qi64* __restrict__ tile_offsets,
+                           qi32 tile_slots, OutCols out) {
   // one block per tile; each wave scans its slots in order (ballot + popc keeps slot order)
   __shared__ int wtot[4];
-  const uint64_t SS = t.cap + 2;
+  const qu64 SS = t.cap + 2;
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-  const uint64_t lt = lane ? (~0ull >> (64 - lane)) : 0ull;
-  int64_t base = tile_offsets[blockIdx.x];
+  const qu64 lt = lane ? (~0ull >> (64 - lane)) : 0ull;
+  qi64 base = tile_offsets[blockIdx.x];
   for (int it = 0; it < tile_slots; it += blockDim.x) {
-    const uint64_t s = (uint64_t)blockIdx.x * tile_slots + it + threadIdx.x;
+    const qu64 s = (qu64)blockIdx.x * tile_slots + it + threadIdx.x;
     const bool occ = (it + (int)threadIdx.x) < tile_slots && s < SS && gslot_occupied(t, s);
-    const uint64_t b = __ballot(occ);
+    const qu64 b = __ballot(occ);
     if (lane == 0) wtot[wid] = __popcll(b);
     __syncthreads();
     int woff = 0, btot = 0;
@@ -824,9 +894,9 @@ __global__ void k_finalize(DTable t, AggMeta m, KeyMeta km, const int64_t* __res
       btot += wtot[w];
     }
     if (occ) {
-      const int64_t o = base + woff + __popcll(b & lt);
+      const qi64 o = base + woff + __popcll(b & lt);
       const bool knull = s == t.cap;
-      const int64_t key = knull ? 0 : (s == t.cap + 1 ? EMPTY_KEY : t.keys[s]);
+      const qi64 key = knull ? 0 : (s == t.cap + 1 ? EMPTY_KEY : t.keys[s]);
       // keys
       if (km.mode == 1) {
         store_typed(out.keys[0].values, km.type[0], o, key);
@@ -834,27 +904,27 @@ __global__ void k_finalize(DTable t, AggMeta m, KeyMeta km, const int64_t* __res
       } else if (km.mode == 2) {
         for (int k = 0; k < km.nkeys; ++k) {
           const bool isn = (key >> km.nullbit[k]) & 1;
-          int64_t x = (key >> km.shift[k]) & km.fmask[k];
-          if (km.type[k] == QE_TYPE_INT32 || km.type[k] == QE_TYPE_DATE32) x = (int64_t)(int32_t)x;  // sign
+          qi64 x = (key >> km.shift[k]) & km.fmask[k];
+          if (km.type[k] == QE_TYPE_INT32 || km.type[k] == QE_TYPE_DATE32) x = (qi64)(qi32)x;  // sign
           store_typed(out.keys[k].values, km.type[k], o, x);
           if (out.keys[k].validity) set_bit(out.keys[k].validity, o, !isn);
         }
       }
       // aggregates
       for (int j = 0; j < m.naggs; ++j) {
-        const uint64_t nn = t.nn[j][s];
-        const int64_t acc = t.acc[j][s];
-        int64_t val = 0;
+        const qu64 nn = t.nn[j][s];
+        const qi64 acc = t.acc[j][s];
+        qi64 val = 0;
         bool valid = nn > 0;
         switch (m.fn[j]) {
-          case QE_AGG_COUNT: val = (int64_t)nn; valid = true; break;
-          case QE_AGG_COUNT_STAR: val = (int64_t)t.cstar[s]; valid = true; break;
+          case QE_AGG_COUNT: val = (qi64)nn; valid = true; break;
+          case QE_AGG_COUNT_STAR: val = (qi64)t.cstar[s]; valid = true; break;
           case QE_AGG_AVG: val = f64_bits(bits_f64(acc) / (double)nn); break;
           default:
             if (acc_is_f64mm(m.acc[j])) {
-              const uint64_t i0 = t.idx[j][s], i1 = t.idx[j][SS + s];
-              const uint64_t i2 = t.idx[j][2 * SS + s], i3 = t.idx[j][3 * SS + s];
-              if (i1 != UINT64_MAX && i1 == i0) {
+              const qu64 i0 = t.idx[j][s], i1 = t.idx[j][SS + s];
+              const qu64 i2 = t.idx[j][2 * SS + s], i3 = t.idx[j][3 * SS + s];
+              if (i1 != ~0ull && i1 == i0) {
                 val = 0x7FF8000000000000ll;  // first non-null value was NaN: sticky seed
               } else {
                 const double d = okey_f64(acc);
@@ -864,7 +934,7 @@ __global__ void k_finalize(DTable t, AggMeta m, KeyMeta km, const int64_t* __res
               val = acc;
             }
         }
-        ((int64_t*)out.aggs[j].values)[o] = valid ? val : 0;
+        ((qi64*)out.aggs[j].values)[o] = valid ? val : 0;
         if (out.aggs[j].validity) set_bit(out.aggs[j].validity, o, valid);
       }
     }
@@ -893,7 +963,7 @@ struct qe_hashagg {
   // global table
   void* table_mem = nullptr;
   DTable t{};
-  uint64_t* ctl = nullptr;  // device, 8 words
+  qu64* ctl = nullptr;  // device, 8 words
   // LDS sizing
   int32_t lds_log2 = 0;  // largest LDS table (log2 slots); 0 => global-only mode
   int32_t lds_log2_min = 0;
@@ -909,6 +979,8 @@ struct qe_hashagg {
   hipEvent_t ev[2] = {nullptr, nullptr};
   double last_kernel_ms = 0.0;
   int last_launches = 0;
+  int last_specialized = 0;  // 1: the last update ran a hipRTC-specialised kernel
+  std::string jit_note;      // why the last update could not specialise (empty if it did)
 };
 
 namespace qe {
@@ -939,17 +1011,17 @@ static int table_alloc(qe_hashagg* h, uint64_t cap, void** mem, DTable* t) {
   const uint64_t SS = cap + 2;
   char* p = (char*)*mem;
   *t = DTable{};
-  t->keys = (int64_t*)p;
+  t->keys = (qi64*)p;
   p += 8 * SS;
-  t->cstar = (uint64_t*)p;
+  t->cstar = (qu64*)p;
   p += 8 * SS;
   for (int j = 0; j < h->naggs; ++j) {
-    t->acc[j] = (int64_t*)p;
+    t->acc[j] = (qi64*)p;
     p += 8 * SS;
-    t->nn[j] = (uint64_t*)p;
+    t->nn[j] = (qu64*)p;
     p += 8 * SS;
     if (acc_is_f64mm(h->acc[j])) {
-      t->idx[j] = (uint64_t*)p;
+      t->idx[j] = (qu64*)p;
       p += 32 * SS;
     }
   }
@@ -1046,6 +1118,8 @@ static int compile_plan(qe_hashagg* h, const qe_column* cols, int32_t ncols, con
     col_f64[c] = k.type == QE_TYPE_FLOAT64;
   }
   P->ncols = ncols;
+  P->all8 = 1;
+  for (int c = 0; c < ncols; ++c) P->all8 &= (cols[c].type == QE_TYPE_INT64 || cols[c].type == QE_TYPE_FLOAT64) ? 1 : 0;
   P->n = n;
   P->row_base = h->row_base;
   // mask
@@ -1110,9 +1184,9 @@ static int compile_plan(qe_hashagg* h, const qe_column* cols, int32_t ncols, con
     bool st_f[QE_MAX_TOKENS + 4];
     int depth = 0, nt = 0;
     bool nullable = false;
-    auto emit = [&](int32_t op, int32_t arg, int64_t lit, int32_t lit_null) -> int {
+    auto emit = [&](int32_t op, int32_t arg, int64_t lit, int32_t lit_null, int32_t lit_f64 = 0) -> int {
       QE_CHECK(nt < QE_MAX_TOKENS, QE_ERR_UNSUPPORTED, "aggregate %d: program too long after type promotion", j);
-      a.tok[nt++] = DTok{op, arg, lit, lit_null, 0};
+      a.tok[nt++] = DTok{op, arg, lit, lit_null, lit_f64};
       return QE_OK;
     };
     for (int t = 0; t < pg.ntokens; ++t) {
@@ -1128,7 +1202,7 @@ static int compile_plan(qe_hashagg* h, const qe_column* cols, int32_t ncols, con
         QE_CHECK(tk.lit.type == QE_TYPE_INT64 || tk.lit.type == QE_TYPE_FLOAT64, QE_ERR_UNSUPPORTED,
                  "aggregate %d: literal type", j);
         QE_CHECK(depth < 4, QE_ERR_UNSUPPORTED, "aggregate %d: expression deeper than 4", j);
-        QE_TRY(emit(T_LIT, 0, tk.lit.bits, tk.lit.is_null));
+        QE_TRY(emit(T_LIT, 0, tk.lit.bits, tk.lit.is_null, tk.lit.type == QE_TYPE_FLOAT64 ? 1 : 0));
         st_f[depth++] = tk.lit.type == QE_TYPE_FLOAT64;
         nullable = nullable || tk.lit.is_null;
       } else if (tk.op >= QE_TOK_ADD && tk.op <= QE_TOK_DIV) {
@@ -1162,6 +1236,14 @@ static int compile_plan(qe_hashagg* h, const qe_column* cols, int32_t ncols, con
       a.pkind = 1;
       a.col = a.tok[0].arg;
       a.cvt_i2f = 1;
+    } else if (nt == 3 && a.tok[0].op == T_COL && (a.tok[1].op == T_COL || a.tok[1].op == T_LIT) &&
+               a.tok[2].op >= T_ADD_I) {
+      a.pkind = 3;
+      a.col = a.tok[0].arg;
+      a.bop = a.tok[2].op;
+      a.rhs = a.tok[1].op == T_COL ? a.tok[1].arg : -1;
+      a.rhs_lit = a.tok[1].lit;
+      a.rhs_null = a.tok[1].lit_null;
     } else {
       a.pkind = 2;
     }
@@ -1272,8 +1354,36 @@ static int run_update(qe_hashagg* h, Plan& P) {
     const int64_t gcap = std::min<int64_t>((int64_t)ctx->num_cus * per_cu, h->grid);
     int grid = (int)std::min<int64_t>((int64_t)div_up((uint64_t)waves, HA_THREADS / 64), gcap);
     if (grid < 1) grid = 1;
+    // specialised kernel for this plan shape when possible, else the generic interpreter
+    hipFunction_t jfn = nullptr;
+    int jgrid = 0;
+    if (lds && ctx->jit) {
+      std::string src;
+      size_t jl = 0;
+      if (gen_fused_source(P, P.lds_log2, &src, &jl)) {
+        int bpc = 0;
+        if (jit_kernel(ctx, src, &jfn, &bpc) == QE_OK) {
+          jgrid = (int)std::min<int64_t>(std::min<int64_t>((int64_t)ctx->num_cus * bpc, h->grid),
+                                         (int64_t)div_up((uint64_t)waves, HA_THREADS / 64));
+          if (jgrid < 1) jgrid = 1;
+          h->jit_note.clear();
+        } else {
+          h->jit_note = qe_last_error();
+          jfn = nullptr;
+        }
+      } else {
+        h->jit_note = "plan shape not specialisable";
+      }
+    } else {
+      h->jit_note = lds ? "jit disabled" : "global-only launch";
+    }
     QE_HIP(hipEventRecord(h->ev[0], ctx->stream));
-    QE_TRY(launch_hashagg(P, grid, lds, ctx->stream));
+    if (jfn) {
+      QE_TRY(jit_launch(ctx, jfn, jgrid, P));
+    } else {
+      QE_TRY(launch_hashagg(P, grid, lds, ctx->stream));
+    }
+    h->last_specialized = jfn ? 1 : 0;
     QE_TRY(launch_check("k_hashagg"));
     QE_HIP(hipEventRecord(h->ev[1], ctx->stream));
     uint64_t c[4];
@@ -1427,6 +1537,16 @@ int qe_hashagg_destroy(qe_hashagg* h) {
   return QE_OK;
 }
 
+int qe_hashagg_last_kernel_kind(qe_hashagg* h, int32_t* specialized, char* note, int32_t note_len) {
+  QE_CHECK(h && specialized, QE_ERR_INVALID_ARG, "null argument");
+  *specialized = h->last_specialized;
+  if (note && note_len > 0) {
+    strncpy(note, h->jit_note.c_str(), (size_t)note_len - 1);
+    note[note_len - 1] = 0;
+  }
+  return QE_OK;
+}
+
 int qe_hashagg_last_kernel_time(qe_hashagg* h, double* ms, int32_t* launches) {
   QE_CHECK(h && ms, QE_ERR_INVALID_ARG, "null argument");
   *ms = h->last_kernel_ms;
@@ -1556,10 +1676,10 @@ int qe_hashagg_finalize(qe_hashagg* h, qe_column* out_keys, qe_column* out_aggs,
   QE_TRY(ctx_scratch(ctx, (size_t)(2 * ntiles + 1) * 8, &s));
   int64_t* counts = (int64_t*)s;
   int64_t* offs = counts + ntiles;
-  hipLaunchKernelGGL(k_occ_count, dim3((unsigned)ntiles), dim3(256), 0, ctx->stream, h->t, counts, tile_slots);
+  hipLaunchKernelGGL(k_occ_count, dim3((unsigned)ntiles), dim3(256), 0, ctx->stream, h->t, (qi64*)counts, tile_slots);
   QE_TRY(launch_check("k_occ_count"));
   QE_TRY(exclusive_scan_i64(ctx, counts, offs, ntiles));
-  hipLaunchKernelGGL(k_finalize, dim3((unsigned)ntiles), dim3(256), 0, ctx->stream, h->t, agg_meta(h), h->km, offs,
+  hipLaunchKernelGGL(k_finalize, dim3((unsigned)ntiles), dim3(256), 0, ctx->stream, h->t, agg_meta(h), h->km, (const qi64*)offs,
                      tile_slots, oc);
   QE_TRY(launch_check("k_finalize"));
   QE_HIP(hipStreamSynchronize(ctx->stream));

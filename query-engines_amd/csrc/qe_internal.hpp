@@ -10,6 +10,7 @@
 #include <string>
 
 #include "qe_hip.h"
+#include "qe_dev.hpp"
 
 struct qe_ctx {
   int device = 0;
@@ -20,6 +21,7 @@ struct qe_ctx {
   size_t scratch_bytes = 0;
   void* pinned = nullptr;        // small pinned host buffer for read-backs
   size_t pinned_bytes = 0;
+  int jit = 1;                   // specialise fused plans with hipRTC (qe_jit.hip)
 };
 
 namespace qe {
@@ -50,6 +52,10 @@ int ctx_enter(qe_ctx* ctx);                                   // validates + hip
 int ctx_scratch(qe_ctx* ctx, size_t bytes, void** out);       // grow-only scratch
 int ctx_pinned(qe_ctx* ctx, size_t bytes, void** out);        // grow-only pinned host
 int launch_check(const char* what);                           // hipGetLastError wrapper
+// Per-plan kernel specialisation (qe_jit.hip).
+bool gen_fused_source(const qe::Plan& P, int log2, std::string* src, size_t* lds_bytes);
+int jit_kernel(qe_ctx* ctx, const std::string& src, hipFunction_t* fn, int* blocks_per_cu);
+int jit_launch(qe_ctx* ctx, hipFunction_t fn, int grid, const qe::Plan& P);
 // Exclusive scan of n int64 on the ctx stream (one block); out[n] = total. (qe_filter.hip)
 int exclusive_scan_i64(qe_ctx* ctx, const int64_t* in, int64_t* out, int64_t n);
 
@@ -68,9 +74,6 @@ inline bool is_fixed(int32_t t) { return type_width(t) > 0; }
 inline bool is_integral(int32_t t) {
   return t == QE_TYPE_INT64 || t == QE_TYPE_INT32 || t == QE_TYPE_DATE32 || t == QE_TYPE_UINT8;
 }
-
-// Operand kinds understood by the device loaders (uniform per launch).
-enum SrcKind : int32_t { K_LIT = 0, K_I64 = 1, K_F64 = 2, K_I32 = 3, K_U8 = 4, K_BOOL = 5 };
 
 inline int32_t kind_of(int32_t type) {
   switch (type) {
@@ -98,44 +101,6 @@ __host__ __device__ __forceinline__ uint64_t splitmix64(uint64_t x) {
 
 __host__ __device__ __forceinline__ uint64_t gen_u64(uint64_t seed, uint64_t col, uint64_t row) {
   return splitmix64(seed ^ (col * PHI64) ^ row);
-}
-
-// murmur3 finaliser: partition hash for the multi-GPU exchange and the global table.
-__host__ __device__ __forceinline__ uint64_t fmix64(uint64_t k) {
-  k ^= k >> 33;
-  k *= 0xFF51AFD7ED558CCDull;
-  k ^= k >> 33;
-  k *= 0xC4CEB9FE1A85EC53ull;
-  k ^= k >> 33;
-  return k;
-}
-
-// Cheap slot hash for the per-workgroup LDS table: one 32-bit multiply (Fibonacci hashing).
-__device__ __forceinline__ uint32_t lds_hash(uint64_t key) {
-  uint32_t x = (uint32_t)key ^ (uint32_t)(key >> 32) * 0x85EBCA6Bu;
-  return x * 0x9E3779B1u;
-}
-
-__host__ __device__ __forceinline__ int64_t f64_bits(double d) {
-  int64_t b;
-  memcpy(&b, &d, 8);
-  return b;
-}
-__host__ __device__ __forceinline__ double bits_f64(int64_t b) {
-  double d;
-  memcpy(&d, &b, 8);
-  return d;
-}
-
-// Order-preserving int64 key of a non-NaN double with +0.0 and -0.0 mapped to the same key
-// (they compare equal under IEEE `>`, K:547; the earliest one is tracked separately).
-__host__ __device__ __forceinline__ int64_t f64_okey(double d) {
-  int64_t b = f64_bits(d == 0.0 ? 0.0 : d);
-  return b >= 0 ? b : (b ^ 0x7FFFFFFFFFFFFFFFll);
-}
-__host__ __device__ __forceinline__ double okey_f64(int64_t k) {
-  int64_t b = k >= 0 ? k : (k ^ 0x7FFFFFFFFFFFFFFFll);
-  return bits_f64(b);
 }
 
 }  // namespace qe

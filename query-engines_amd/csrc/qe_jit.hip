@@ -1,0 +1,447 @@
+// Per-plan kernel specialisation for the fused SelectionExec -> ProjectionExec ->
+// HashAggregateExec pipeline (the north star's one-pass hot path).
+//
+// A query engine's expression interpreter costs instructions on every row; on MI355X the fused
+// aggregate is otherwise HBM-bound, so the interpreter is what separates the generic kernel
+// (k_hashagg, qe_hashagg.hip) from the HBM roofline. For each distinct plan SHAPE (column types
+// and nullability, predicate structure, key packing, aggregate functions and expression trees,
+// LDS table size) this file emits a straight-line HIP kernel in which every slot, operator and
+// accumulator is a compile-time constant, compiles it once with hipRTC for the device's gfx950
+// target, and caches the code object (in memory per device, and on disk by source hash). Literal
+// VALUES stay runtime kernel arguments (Plan), so `a > 1` and `a > 2` share one kernel.
+//
+// The emitted code uses exactly the same table layout / probing / combine helpers as the
+// ahead-of-time kernels (qe_dev.hpp is compiled into both), so results are identical; the AOT
+// generic kernel remains the fallback when a plan cannot be specialised or hipRTC fails.
+#include <hip/hiprtc.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <sys/stat.h>
+#include <unistd.h>
+
+#include <map>
+#include <mutex>
+#include <sstream>
+#include <vector>
+
+#include "qe_internal.hpp"
+
+namespace qe {
+
+static const char* kDevHeader =
+#include "qe_dev.inc"
+    ;
+
+// ---- source generation -------------------------------------------------------------------------------
+namespace {
+
+struct Expr {
+  std::string v;   // C expression (qi64 for integral, double for fp64)
+  std::string ok;  // C expression of its validity (0/1)
+  bool f;          // fp64
+};
+
+std::string col_raw(int c) { return "c" + std::to_string(c) + "[r]"; }
+std::string col_ok(const Plan& P, int c) {
+  return P.cols[c].valid ? "((v" + std::to_string(c) + " >> r) & 1u)" : std::string("1u");
+}
+bool col_is_f(const Plan& P, int c) { return P.cols[c].kind == K_F64; }
+std::string col_val(const Plan& P, int c) {
+  return col_is_f(P, c) ? "bits_f64(" + col_raw(c) + ")" : col_raw(c);
+}
+
+// Expression of aggregate j's typed token program (qe_hashagg.hip compile_plan) for row r.
+bool agg_expr(const Plan& P, int j, Expr* out) {
+  const DAgg& a = P.aggs[j];
+  std::vector<Expr> st;
+  for (int t = 0; t < a.ntok; ++t) {
+    const DTok& k = a.tok[t];
+    const std::string litref = "P.aggs[" + std::to_string(j) + "].tok[" + std::to_string(t) + "].lit";
+    switch (k.op) {
+      case T_COL: st.push_back({col_val(P, k.arg), col_ok(P, k.arg), col_is_f(P, k.arg)}); break;
+      case T_LIT:
+        st.push_back({k.lit_f64 ? "bits_f64(" + litref + ")" : litref, k.lit_null ? "0u" : "1u", k.lit_f64 != 0});
+        break;
+      case T_I2F0:
+        if (st.empty()) return false;
+        st.back() = {"((double)(" + st.back().v + "))", st.back().ok, true};
+        break;
+      case T_I2F1:
+        if (st.size() < 2) return false;
+        st[st.size() - 2] = {"((double)(" + st[st.size() - 2].v + "))", st[st.size() - 2].ok, true};
+        break;
+      default: {
+        if (st.size() < 2) return false;
+        const Expr b = st.back();
+        st.pop_back();
+        const Expr l = st.back();
+        st.pop_back();
+        Expr e;
+        e.ok = "(" + l.ok + " & " + b.ok + ")";
+        switch (k.op) {
+          case T_ADD_I: e = {"((qi64)((qu64)(" + l.v + ") + (qu64)(" + b.v + ")))", e.ok, false}; break;
+          case T_SUB_I: e = {"((qi64)((qu64)(" + l.v + ") - (qu64)(" + b.v + ")))", e.ok, false}; break;
+          case T_MUL_I: e = {"((qi64)((qu64)(" + l.v + ") * (qu64)(" + b.v + ")))", e.ok, false}; break;
+          case T_DIV_I:
+            e = {"idiv((" + l.v + "), (" + b.v + "))", "(" + e.ok + " & (qu32)((" + b.v + ") != 0))", false};
+            break;
+          case T_ADD_F: e = {"((" + l.v + ") + (" + b.v + "))", e.ok, true}; break;
+          case T_SUB_F: e = {"((" + l.v + ") - (" + b.v + "))", e.ok, true}; break;
+          case T_MUL_F: e = {"((" + l.v + ") * (" + b.v + "))", e.ok, true}; break;
+          case T_DIV_F: e = {"((" + l.v + ") / (" + b.v + "))", e.ok, true}; break;
+          default: return false;
+        }
+        st.push_back(e);
+      }
+    }
+  }
+  if (st.size() != 1) return false;
+  *out = st[0];
+  if (out->f) out->v = "f64_bits(" + out->v + ")";
+  return true;
+}
+
+const char* cmp_sym(int op) {
+  switch (op) {
+    case QE_OP_EQ: return "==";
+    case QE_OP_NE: return "!=";
+    case QE_OP_LT: return "<";
+    case QE_OP_LE: return "<=";
+    case QE_OP_GT: return ">";
+    default: return ">=";
+  }
+}
+
+std::string acc_init(int acc) {
+  switch (acc) {
+    case ACC_MIN_I:
+    case ACC_MIN_F: return "0x7FFFFFFFFFFFFFFFll";
+    case ACC_MAX_I:
+    case ACC_MAX_F: return "EMPTY_KEY";
+    default: return "0";
+  }
+}
+
+}  // namespace
+
+// Returns false when the plan shape is outside what the generator emits (caller uses the
+// generic kernel). `log2` is the LDS table size chosen for this launch.
+bool gen_fused_source(const Plan& P, int log2, std::string* src, size_t* lds_bytes) {
+  if (log2 < 4 || log2 > 16 || P.ncols < 1 || P.ncols > QE_MAX_COLS) return false;
+  std::ostringstream o;
+  const int S = 1 << log2, SS = S + 2;
+  o << "\nusing namespace qe;\n"
+    << "extern \"C\" __global__ void __launch_bounds__(512) qe_fused(const Plan P) {\n"
+    << "  constexpr int LOG2 = " << log2 << ", S = " << S << ", SS = " << SS << ";\n"
+    << "  __shared__ qi64 s_keys[SS];\n  __shared__ qu32 s_cst[SS];\n";
+  size_t lds = (size_t)SS * 12;
+  for (int j = 0; j < P.naggs; ++j) {
+    const DAgg& a = P.aggs[j];
+    if (a.acc != ACC_NONE) {
+      o << "  __shared__ qi64 s_acc" << j << "[SS];\n";
+      lds += 8 * SS;
+    }
+    if (a.track_nn) {
+      o << "  __shared__ qu32 s_nn" << j << "[SS];\n";
+      lds += 4 * SS;
+    }
+    if (acc_is_f64mm(a.acc)) {
+      o << "  __shared__ qu64 s_idx" << j << "[4 * SS];\n";
+      lds += 32 * SS;
+    }
+  }
+  *lds_bytes = lds;
+  // ---- init
+  o << "  for (int s = threadIdx.x; s < SS; s += blockDim.x) {\n    s_keys[s] = EMPTY_KEY;\n    s_cst[s] = 0;\n";
+  for (int j = 0; j < P.naggs; ++j) {
+    const DAgg& a = P.aggs[j];
+    if (a.acc != ACC_NONE) o << "    s_acc" << j << "[s] = " << acc_init(a.acc) << ";\n";
+    if (a.track_nn) o << "    s_nn" << j << "[s] = 0;\n";
+    if (acc_is_f64mm(a.acc))
+      o << "    for (int k = 0; k < 4; ++k) s_idx" << j << "[k * SS + s] = ~0ull;\n";
+  }
+  o << "  }\n  __syncthreads();\n"
+    << "  const int lane = threadIdx.x & 63;\n"
+    << "  const qi64 wave = (blockIdx.x * (qi64)blockDim.x + threadIdx.x) >> 6;\n"
+    << "  const qi64 stride = (((qi64)gridDim.x * blockDim.x) >> 6) * 256;\n"
+    << "  for (qi64 base = wave * 256; base < P.n; base += stride) {\n"
+    << "    const bool full = base + 256 <= P.n;\n"
+    << "    const qi64 r0 = base + 2 * lane;\n";
+  // ---- column loads: lane rows r0 + {0,1} and r0 + 128 + {0,1}
+  for (int c = 0; c < P.ncols; ++c) {
+    const std::string cs = std::to_string(c);
+    o << "    qi64 c" << cs << "[4];\n";
+    const int kind = P.cols[c].kind;
+    const char* ty = kind == K_I32 ? "qi32" : kind == K_U8 ? "qu8" : kind == K_BOOL ? "qu8" : "qi64";
+    o << "    {\n      const " << ty << "* p = (const " << ty << "*)P.cols[" << cs << "].p;\n";
+    if (kind == K_BOOL) {
+      o << "      for (int r = 0; r < 4; ++r) { const qi64 row = r0 + 128 * (r >> 1) + (r & 1);\n"
+        << "        c" << cs << "[r] = (full || row < P.n) ? ((p[row >> 3] >> (row & 7)) & 1) : 0; }\n";
+    } else {
+      o << "      if (full) {\n";
+      if (kind == K_I64 || kind == K_F64) {
+        o << "        const qi64x2 a = *(const qi64x2*)(p + r0), b = *(const qi64x2*)(p + r0 + 128);\n"
+          << "        c" << cs << "[0] = a.x; c" << cs << "[1] = a.y; c" << cs << "[2] = b.x; c" << cs << "[3] = b.y;\n";
+      } else if (kind == K_I32) {
+        o << "        const int2 a = *(const int2*)(p + r0), b = *(const int2*)(p + r0 + 128);\n"
+          << "        c" << cs << "[0] = a.x; c" << cs << "[1] = a.y; c" << cs << "[2] = b.x; c" << cs << "[3] = b.y;\n";
+      } else {  // K_U8
+        o << "        const qu16 a = *(const qu16*)(p + r0), b = *(const qu16*)(p + r0 + 128);\n"
+          << "        c" << cs << "[0] = a & 0xFF; c" << cs << "[1] = a >> 8; c" << cs << "[2] = b & 0xFF; c" << cs
+          << "[3] = b >> 8;\n";
+      }
+      o << "      } else {\n"
+        << "        for (int r = 0; r < 4; ++r) { const qi64 row = r0 + 128 * (r >> 1) + (r & 1);\n"
+        << "          c" << cs << "[r] = row < P.n ? (qi64)p[row] : 0; }\n      }\n";
+    }
+    o << "    }\n";
+    if (P.cols[c].valid) {
+      o << "    qu32 v" << cs << ";\n    {\n      const qu8* vb = P.cols[" << cs << "].valid;\n"
+        << "      const qu32 lo = (qu32)(vb[r0 >> 3] >> (r0 & 7)) & 3u;\n"
+        << "      const qu32 hi = (full || r0 + 128 < P.n) ? ((qu32)(vb[(r0 + 128) >> 3] >> (r0 & 7)) & 3u) : 0u;\n"
+        << "      v" << cs << " = lo | (hi << 2);\n    }\n";
+    }
+  }
+  // ---- active rows: range, retry set, mask, predicate terms
+  o << "    qu32 act = 15u;\n"
+    << "    if (!full) { act = 0; for (int r = 0; r < 4; ++r) act |= (qu32)(r0 + 128 * (r >> 1) + (r & 1) < P.n) << r; }\n"
+    << "    if (P.defer_in) {\n      for (int r = 0; r < 4; ++r) { const qi64 row = r0 + 128 * (r >> 1) + (r & 1);\n"
+    << "        if (row < P.n && !((P.defer_in[row >> 5] >> (row & 31)) & 1)) act &= ~(1u << r); }\n    }\n";
+  if (P.mask_col >= 0) {
+    o << "#pragma unroll\n    for (int r = 0; r < 4; ++r) if (!((qu32)(" << col_raw(P.mask_col) << " & 1) & "
+      << col_ok(P, P.mask_col) << ")) act &= ~(1u << r);\n";
+  }
+  for (int t = 0; t < P.nterms; ++t) {
+    const DTerm& T = P.terms[t];
+    const std::string lit = "P.terms[" + std::to_string(t) + "].lit";
+    std::string lhs, rhs, ok = col_ok(P, T.lhs);
+    if (T.f64) {
+      lhs = col_is_f(P, T.lhs) ? col_val(P, T.lhs) : "((double)" + col_raw(T.lhs) + ")";
+      if (T.rhs >= 0) rhs = col_is_f(P, T.rhs) ? col_val(P, T.rhs) : "((double)" + col_raw(T.rhs) + ")";
+      else rhs = "bits_f64(" + lit + ")";
+    } else {
+      lhs = col_raw(T.lhs);
+      rhs = T.rhs >= 0 ? col_raw(T.rhs) : lit;
+    }
+    if (T.rhs >= 0) ok += " & " + col_ok(P, T.rhs);
+    else if (T.lit_null) ok = "0u";
+    o << "#pragma unroll\n    for (int r = 0; r < 4; ++r) if (!((" << lhs << ") " << cmp_sym(T.op) << " (" << rhs
+      << ")) || !(" << ok << ")) act &= ~(1u << r);\n";
+  }
+  o << "    if (act == 0) continue;\n";
+  // ---- keys
+  o << "    qi64 key[4] = {0, 0, 0, 0};\n    qu32 knull = 0;\n";
+  if (P.key_mode == 1) {
+    const int c = P.key_col[0];
+    o << "#pragma unroll\n    for (int r = 0; r < 4; ++r) {\n      qi64 k = " << col_raw(c) << ";\n";
+    if (P.key_f64) o << "      if (bits_f64(k) != bits_f64(k)) k = 0x7FF8000000000000ll;\n";
+    if (P.cols[c].valid)
+      o << "      if (!" << col_ok(P, c) << ") { k = 0; knull |= 1u << r; }\n";
+    o << "      key[r] = k;\n    }\n";
+  } else if (P.key_mode == 2) {
+    o << "#pragma unroll\n    for (int r = 0; r < 4; ++r) {\n      qi64 k = 0;\n";
+    for (int q = 0; q < P.nkeys; ++q) {
+      const int c = P.key_col[q];
+      o << "      { const bool isn = !" << col_ok(P, c) << "; k |= ((isn ? 0ll : (" << col_raw(c) << " & "
+        << P.key_fmask[q] << "ll)) << " << P.key_shift[q] << ") | ((qi64)isn << " << P.key_nullbit[q] << "); }\n";
+    }
+    o << "      key[r] = k;\n    }\n";
+  }
+  // ---- LDS slots: first probe of the 4 rows together, collisions probe on
+  o << "    int slot[4];\n    qu32 h[4];\n    qi64 k0[4];\n"
+    << "#pragma unroll\n    for (int r = 0; r < 4; ++r) { h[r] = lds_hash((qu64)key[r]) >> (32 - LOG2); k0[r] = ((act >> r) & 1) ? s_keys[h[r]] : 0; }\n"
+    << "#pragma unroll\n    for (int r = 0; r < 4; ++r) slot[r] = ((knull >> r) & 1) ? S : (key[r] == EMPTY_KEY ? S + 1 : (k0[r] == key[r] ? (int)h[r] : -1));\n"
+    << "    qu32 miss = 0;\n"
+    << "#pragma unroll\n    for (int r = 0; r < 4; ++r) miss |= (qu32)(slot[r] < 0) << r;\n"
+    << "    miss &= act;\n"
+    << "    if (miss) {\n      for (int r = 0; r < 4; ++r) if ((miss >> r) & 1) slot[r] = lds_probe(s_keys, LOG2, key[r], h[r]);\n    }\n"
+    << "    qu32 glob = 0;\n"
+    << "#pragma unroll\n    for (int r = 0; r < 4; ++r) glob |= (qu32)(slot[r] < 0) << r;\n"
+    << "    glob &= act;\n    const qu32 loc = act & ~glob;\n"
+    << "#pragma unroll\n    for (int r = 0; r < 4; ++r) if ((loc >> r) & 1) atomicAdd(&s_cst[slot[r]], 1u);\n";
+  // ---- aggregate inputs into LDS
+  std::vector<Expr> ex(P.naggs);
+  for (int j = 0; j < P.naggs; ++j) {
+    const DAgg& a = P.aggs[j];
+    if (a.pkind == 0) continue;
+    if (!agg_expr(P, j, &ex[j])) return false;
+    const std::string js = std::to_string(j);
+    o << "    {\n#pragma unroll\n      for (int r = 0; r < 4; ++r) {\n"
+      << "        if (!((loc >> r) & 1)) continue;\n"
+      << "        if (!(" << ex[j].ok << ")) continue;\n"
+      << "        const qi64 x = " << ex[j].v << ";\n"
+      << "        const int s = slot[r];\n";
+    if (a.track_nn) o << "        atomicAdd(&s_nn" << js << "[s], 1u);\n";
+    switch (a.acc) {
+      case ACC_SUM_I: o << "        atomicAdd((qu64*)&s_acc" << js << "[s], (qu64)x);\n"; break;
+      case ACC_SUM_F: o << "        atomicAdd((double*)&s_acc" << js << "[s], bits_f64(x));\n"; break;
+      case ACC_MIN_I: o << "        atomicMin(&s_acc" << js << "[s], x);\n"; break;
+      case ACC_MAX_I: o << "        atomicMax(&s_acc" << js << "[s], x);\n"; break;
+      case ACC_MIN_F:
+      case ACC_MAX_F:
+        o << "        lds_f64mm<" << (a.acc == ACC_MAX_F ? "true" : "false") << ">(s_acc" << js << ", s_idx" << js
+          << ", SS, s, x, (qu64)(P.row_base + r0 + 128 * (r >> 1) + (r & 1)));\n";
+        break;
+      default: break;
+    }
+    o << "      }\n    }\n";
+  }
+  // ---- rows whose group only fits the global table (rare)
+  o << "    if (glob) {\n      for (int r = 0; r < 4; ++r) {\n        if (!((glob >> r) & 1)) continue;\n"
+    << "        const qi64 lr = r0 + 128 * (r >> 1) + (r & 1);\n        qu64 gs;\n"
+    << "        if (!gtable_find(P.t, key[r], (knull >> r) & 1, gs)) {\n"
+    << "          atomicOr((qu32*)&P.defer_out[lr >> 5], 1u << (lr & 31));\n"
+    << "          atomicAdd(&P.t.ctl[1], 1ull);\n          continue;\n        }\n"
+    << "        gadd_cstar(P.t, gs, 1);\n        const qu64 row = (qu64)(P.row_base + lr);\n";
+  for (int j = 0; j < P.naggs; ++j) {
+    const DAgg& a = P.aggs[j];
+    if (a.pkind == 0) continue;
+    o << "        if (" << ex[j].ok << ") { const RowVal rv = row_partial(" << a.acc << ", " << ex[j].v
+      << ", row); gcombine(P.t, " << a.acc << ", " << j << ", gs, rv.acc, 1, rv.i0, rv.i1, rv.i2, rv.i3); }\n";
+  }
+  o << "      }\n    }\n  }\n";
+  // ---- flush the workgroup table into the global table (or overflow records)
+  o << "  __syncthreads();\n"
+    << "  for (int s = threadIdx.x; s < SS; s += blockDim.x) {\n"
+    << "    const qu32 c = s_cst[s];\n    if (c == 0) continue;\n"
+    << "    const bool knl = s == S;\n    const qi64 key = knl ? 0 : (s == S + 1 ? EMPTY_KEY : s_keys[s]);\n"
+    << "    qu64 gs;\n    const bool ok = gtable_find(P.t, key, knl, gs);\n    qu8* rec = nullptr;\n"
+    << "    if (ok) {\n      gadd_cstar(P.t, gs, c);\n    } else {\n"
+    << "      const qu64 ri = atomicAdd(&P.t.ctl[2], 1ull);\n"
+    << "      if (ri >= P.ovf_cap) { atomicAdd(&P.t.ctl[3], 1ull); continue; }\n"
+    << "      rec = P.ovf + ri * (qu64)P.rec_bytes;\n      write_record_head(rec, key, knl, c);\n    }\n";
+  int off = 24;
+  for (int j = 0; j < P.naggs; ++j) {
+    const DAgg& a = P.aggs[j];
+    const std::string js = std::to_string(j);
+    o << "    {\n      const qi64 acc = " << (a.acc != ACC_NONE ? "s_acc" + js + "[s]" : std::string("0")) << ";\n"
+      << "      const qu64 nn = " << (a.track_nn ? "s_nn" + js + "[s]" : std::string("c")) << ";\n";
+    if (acc_is_f64mm(a.acc))
+      o << "      const qu64 i0 = s_idx" << js << "[s], i1 = s_idx" << js << "[SS + s], i2 = s_idx" << js
+        << "[2 * SS + s], i3 = s_idx" << js << "[3 * SS + s];\n";
+    else
+      o << "      const qu64 i0 = ~0ull, i1 = ~0ull, i2 = ~0ull, i3 = ~0ull;\n";
+    if (a.fn != QE_AGG_COUNT_STAR)
+      o << "      if (ok) gcombine(P.t, " << a.acc << ", " << j << ", gs, acc, nn, i0, i1, i2, i3);\n";
+    o << "      if (!ok) { qu64* f = (qu64*)(rec + " << off << "); f[0] = (qu64)acc; f[1] = nn;";
+    if (acc_is_f64mm(a.acc)) o << " f[2] = i0; f[3] = i1; f[4] = i2; f[5] = i3;";
+    o << " }\n    }\n";
+    off += agg_rec_bytes(a.acc);
+  }
+  o << "  }\n}\n";
+  *src = std::string(kDevHeader) + o.str();
+  return true;
+}
+
+// ---- hipRTC compile + cache ------------------------------------------------------------------------------
+namespace {
+
+struct Entry {
+  hipModule_t mod = nullptr;
+  hipFunction_t fn = nullptr;
+  int blocks_per_cu = 0;
+};
+
+std::mutex g_mu;
+std::map<std::pair<int, std::string>, Entry> g_cache;
+
+uint64_t fnv1a(const std::string& s) {
+  uint64_t h = 1469598103934665603ull;
+  for (unsigned char c : s) {
+    h ^= c;
+    h *= 1099511628211ull;
+  }
+  return h;
+}
+
+std::string cache_dir() {
+  const char* d = getenv("QE_JIT_CACHE");
+  return d && *d ? std::string(d) : std::string("/tmp/qe_jit_cache");
+}
+
+bool read_file(const std::string& path, std::vector<char>* out) {
+  FILE* f = fopen(path.c_str(), "rb");
+  if (!f) return false;
+  fseek(f, 0, SEEK_END);
+  const long n = ftell(f);
+  fseek(f, 0, SEEK_SET);
+  out->resize(n > 0 ? (size_t)n : 0);
+  const bool ok = n > 0 && fread(out->data(), 1, (size_t)n, f) == (size_t)n;
+  fclose(f);
+  return ok;
+}
+
+void write_file(const std::string& path, const std::vector<char>& data) {
+  const std::string tmp = path + ".tmp" + std::to_string((long)getpid());
+  FILE* f = fopen(tmp.c_str(), "wb");
+  if (!f) return;
+  const bool ok = fwrite(data.data(), 1, data.size(), f) == data.size();
+  fclose(f);
+  if (ok) rename(tmp.c_str(), path.c_str());
+  else remove(tmp.c_str());
+}
+
+}  // namespace
+
+// Compiled kernel for `src` on the ctx's device (compiling / loading it on first use).
+int jit_kernel(qe_ctx* ctx, const std::string& src, hipFunction_t* fn, int* blocks_per_cu) {
+  std::lock_guard<std::mutex> lk(g_mu);
+  const auto key = std::make_pair(ctx->device, src);
+  auto it = g_cache.find(key);
+  if (it != g_cache.end()) {
+    *fn = it->second.fn;
+    *blocks_per_cu = it->second.blocks_per_cu;
+    return QE_OK;
+  }
+  hipDeviceProp_t prop;
+  QE_HIP(hipGetDeviceProperties(&prop, ctx->device));
+  std::string arch = prop.gcnArchName;
+  const std::string opt_arch = "--offload-arch=" + arch;
+  const char* opts[] = {opt_arch.c_str(), "-O3", "-munsafe-fp-atomics", "-std=c++17"};
+  char name[64];
+  snprintf(name, sizeof(name), "%016llx", (unsigned long long)fnv1a(src + arch));
+  const std::string dir = cache_dir();
+  const std::string path = dir + "/" + name + ".co";
+  std::vector<char> code;
+  if (!read_file(path, &code)) {
+    hiprtcProgram prog;
+    if (hiprtcCreateProgram(&prog, src.c_str(), "qe_fused.hip", 0, nullptr, nullptr) != HIPRTC_SUCCESS)
+      return fail(QE_ERR_DEVICE, "hiprtcCreateProgram failed");
+    const hiprtcResult r = hiprtcCompileProgram(prog, 4, opts);
+    if (r != HIPRTC_SUCCESS) {
+      size_t ls = 0;
+      hiprtcGetProgramLogSize(prog, &ls);
+      std::string log(ls, '\0');
+      if (ls) hiprtcGetProgramLog(prog, &log[0]);
+      hiprtcDestroyProgram(&prog);
+      return fail(QE_ERR_DEVICE, "hipRTC compile of the fused kernel failed: %s", log.substr(0, 900).c_str());
+    }
+    size_t cs = 0;
+    hiprtcGetCodeSize(prog, &cs);
+    code.resize(cs);
+    hiprtcGetCode(prog, code.data());
+    hiprtcDestroyProgram(&prog);
+    mkdir(dir.c_str(), 0777);
+    write_file(path, code);
+  }
+  Entry e;
+  QE_HIP(hipModuleLoadData(&e.mod, code.data()));
+  QE_HIP(hipModuleGetFunction(&e.fn, e.mod, "qe_fused"));
+  int nb = 0;
+  QE_HIP(hipModuleOccupancyMaxActiveBlocksPerMultiprocessor(&nb, e.fn, 512, 0));
+  e.blocks_per_cu = nb > 0 ? nb : 1;
+  g_cache[key] = e;
+  *fn = e.fn;
+  *blocks_per_cu = e.blocks_per_cu;
+  return QE_OK;
+}
+
+int jit_launch(qe_ctx* ctx, hipFunction_t fn, int grid, const Plan& P) {
+  Plan arg = P;
+  size_t sz = sizeof(Plan);
+  void* cfg[] = {HIP_LAUNCH_PARAM_BUFFER_POINTER, &arg, HIP_LAUNCH_PARAM_BUFFER_SIZE, &sz, HIP_LAUNCH_PARAM_END};
+  QE_HIP(hipModuleLaunchKernel(fn, grid, 1, 1, 512, 1, 1, 0, ctx->stream, nullptr, cfg));
+  return QE_OK;
+}
+
+}  // namespace qe

@@ -1,6 +1,7 @@
 // Context, errors, device memory and the synthetic RecordBatch generator.
 #include <stdarg.h>
 #include <stdio.h>
+#include <stdlib.h>
 
 #include "qe_internal.hpp"
 
@@ -109,6 +110,34 @@ __global__ void __launch_bounds__(256) k_generate(void* __restrict__ values, uin
   }
 }
 
+// ---- stream-read ceiling (measurement harness) ----------------------------------
+// Reads every byte of up to 8 fixed-width columns with 16-B loads (one contiguous KiB per wave
+// instruction, 4 in flight per lane) and XOR-folds them into one word so nothing is dead code.
+typedef long long i64x2_rt __attribute__((ext_vector_type(2)));
+struct StreamCols {
+  const i64x2_rt* p[8];
+  int64_t n16[8];  // 16-byte chunks per column
+  int32_t ncols;
+};
+
+__global__ void __launch_bounds__(512) k_stream_read(StreamCols c, unsigned long long* out) {
+  unsigned long long acc = 0;
+  const int64_t tid = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  const int64_t nthr = (int64_t)gridDim.x * blockDim.x;
+  for (int k = 0; k < c.ncols; ++k) {
+    const i64x2_rt* p = c.p[k];
+    const int64_t n = c.n16[k];
+    int64_t i = tid;
+    for (; i + 3 * nthr < n; i += 4 * nthr) {
+      const i64x2_rt a = p[i], b = p[i + nthr], d = p[i + 2 * nthr], e = p[i + 3 * nthr];
+      acc ^= (unsigned long long)(a.x ^ a.y ^ b.x ^ b.y ^ d.x ^ d.y ^ e.x ^ e.y);
+    }
+    for (; i < n; i += nthr) acc ^= (unsigned long long)(p[i].x ^ p[i].y);
+  }
+  for (int m = 32; m > 0; m >>= 1) acc ^= __shfl_xor(acc, m);
+  if ((threadIdx.x & 63) == 0 && acc == 0x5A5A5A5A5A5A5A5Aull) atomicXor(out, acc);  // practically never
+}
+
 }  // namespace qe
 
 using namespace qe;
@@ -118,7 +147,7 @@ extern "C" {
 const char* qe_last_error(void) { return g_last_error.c_str(); }
 int qe_abi_version(void) { return QE_ABI_VERSION; }
 
-int qe_ctx_create(int device, void* stream, qe_ctx** out) {
+static int ctx_create(int device, void* stream, bool owned, qe_ctx** out) {
   clear_error();
   QE_CHECK(out != nullptr, QE_ERR_INVALID_ARG, "null out");
   int ndev = 0;
@@ -127,9 +156,8 @@ int qe_ctx_create(int device, void* stream, qe_ctx** out) {
   QE_HIP(hipSetDevice(device));
   qe_ctx* c = new qe_ctx();
   c->device = device;
-  if (stream) {
-    c->stream = (hipStream_t)stream;
-  } else {
+  c->stream = (hipStream_t)stream;
+  if (owned) {
     hipError_t e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
     if (e != hipSuccess) {
       delete c;
@@ -139,9 +167,15 @@ int qe_ctx_create(int device, void* stream, qe_ctx** out) {
   }
   hipDeviceProp_t prop;
   if (hipGetDeviceProperties(&prop, device) == hipSuccess) c->num_cus = prop.multiProcessorCount;
+  const char* jit = getenv("QE_JIT");
+  if (jit && jit[0] == '0') c->jit = 0;
   *out = c;
   return QE_OK;
 }
+
+int qe_ctx_create(int device, void* stream, qe_ctx** out) { return ctx_create(device, stream, false, out); }
+
+int qe_ctx_create_owned(int device, qe_ctx** out) { return ctx_create(device, nullptr, true, out); }
 
 int qe_ctx_destroy(qe_ctx* ctx) {
   if (!ctx) return QE_OK;
@@ -151,6 +185,12 @@ int qe_ctx_destroy(qe_ctx* ctx) {
   if (ctx->pinned) (void)hipHostFree(ctx->pinned);
   if (ctx->own_stream) (void)hipStreamDestroy(ctx->stream);
   delete ctx;
+  return QE_OK;
+}
+
+int qe_ctx_set_jit(qe_ctx* ctx, int32_t enable) {
+  QE_CHECK(ctx, QE_ERR_INVALID_ARG, "null qe_ctx");
+  ctx->jit = enable ? 1 : 0;
   return QE_OK;
 }
 
@@ -190,6 +230,34 @@ int qe_copy_to_host(qe_ctx* ctx, void* dst, const void* src, size_t bytes) {
   QE_HIP(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, ctx->stream));
   QE_HIP(hipStreamSynchronize(ctx->stream));
   return QE_OK;
+}
+
+int qe_stream_read(qe_ctx* ctx, const qe_column* cols, int32_t ncols, double* ms) {
+  QE_TRY(ctx_enter(ctx));
+  QE_CHECK(cols && ncols >= 1 && ncols <= 8 && ms, QE_ERR_INVALID_ARG, "1..8 columns");
+  StreamCols c{};
+  c.ncols = ncols;
+  for (int k = 0; k < ncols; ++k) {
+    QE_CHECK(is_fixed(cols[k].type), QE_ERR_UNSUPPORTED, "fixed-width columns only");
+    QE_CHECK(((uintptr_t)cols[k].values & 15) == 0, QE_ERR_INVALID_ARG, "16-byte aligned columns only");
+    c.p[k] = (const i64x2_rt*)cols[k].values;
+    c.n16[k] = cols[k].length * type_width(cols[k].type) / 16;
+  }
+  void* s;
+  QE_TRY(ctx_scratch(ctx, 64, &s));
+  hipEvent_t e0, e1;
+  QE_HIP(hipEventCreate(&e0));
+  QE_HIP(hipEventCreate(&e1));
+  QE_HIP(hipEventRecord(e0, ctx->stream));
+  hipLaunchKernelGGL(k_stream_read, dim3(ctx->num_cus * 4), dim3(512), 0, ctx->stream, c, (unsigned long long*)s);
+  QE_HIP(hipEventRecord(e1, ctx->stream));
+  QE_HIP(hipEventSynchronize(e1));
+  float f = 0.f;
+  QE_HIP(hipEventElapsedTime(&f, e0, e1));
+  *ms = f;
+  (void)hipEventDestroy(e0);
+  (void)hipEventDestroy(e1);
+  return launch_check("k_stream_read");
 }
 
 int qe_generate(qe_ctx* ctx, qe_column* out, int32_t dist, int64_t param, uint64_t seed, uint64_t col,

@@ -66,6 +66,13 @@ class HashAggregateState:
         N.check(N.lib().qe_hashagg_last_kernel_time(self.handle, N.C.byref(ms), N.C.byref(k)))
         return ms.value, k.value
 
+    def last_kernel_kind(self):
+        """(specialized: bool, note) for the last update's aggregation kernel."""
+        k = N.C.c_int32()
+        buf = N.C.create_string_buffer(512)
+        N.check(N.lib().qe_hashagg_last_kernel_kind(self.handle, N.C.byref(k), buf, 512))
+        return bool(k.value), buf.value.decode(errors="replace")
+
     def reset(self) -> None:
         N.check(N.lib().qe_hashagg_reset(self.handle))
 

@@ -158,6 +158,8 @@ _COLP = C.POINTER(QeColumn)
 _OPP = C.POINTER(QeOperand)
 SIGNATURES = [
     ("qe_ctx_create", C.c_int, [C.c_int, _P, _PP]),
+    ("qe_ctx_create_owned", C.c_int, [C.c_int, _PP]),
+    ("qe_ctx_set_jit", C.c_int, [_P, C.c_int32]),
     ("qe_ctx_destroy", C.c_int, [_P]),
     ("qe_ctx_stream", _P, [_P]),
     ("qe_ctx_synchronize", C.c_int, [_P]),
@@ -168,6 +170,7 @@ SIGNATURES = [
     ("qe_copy_to_device", C.c_int, [_P, _P, _P, C.c_size_t]),
     ("qe_copy_to_host", C.c_int, [_P, _P, _P, C.c_size_t]),
     ("qe_generate", C.c_int, [_P, _COLP, C.c_int32, C.c_int64, C.c_uint64, C.c_uint64, C.c_int64, C.c_int32]),
+    ("qe_stream_read", C.c_int, [_P, _COLP, C.c_int32, C.POINTER(C.c_double)]),
     ("qe_eval_arith", C.c_int, [_P, C.c_int32, _OPP, _OPP, _COLP]),
     ("qe_eval_cmp", C.c_int, [_P, C.c_int32, _OPP, _OPP, _COLP]),
     ("qe_eval_bool", C.c_int, [_P, C.c_int32, _COLP, _COLP, _COLP]),
@@ -188,6 +191,7 @@ SIGNATURES = [
     ("qe_hashagg_import", C.c_int, [_P, _P, C.c_int64]),
     ("qe_hashagg_set_row_base", C.c_int, [_P, C.c_int64]),
     ("qe_hashagg_last_kernel_time", C.c_int, [_P, C.POINTER(C.c_double), C.POINTER(C.c_int32)]),
+    ("qe_hashagg_last_kernel_kind", C.c_int, [_P, C.POINTER(C.c_int32), C.c_char_p, C.c_int32]),
 ]
 
 

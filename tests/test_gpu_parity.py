@@ -44,6 +44,25 @@ def _rand(rng, n, kind, null_rate=0.0):
 SIZES = [0, 1, 7, 8, 9, 1000, 8191, 8193, 100_003]
 
 
+@pytest.fixture(params=["jit", "generic"])
+def agg_ctx(request, gpu_ctx):
+    """Hash-aggregate tests run through both kernels: the hipRTC plan-specialised one and the
+    generic interpreting one; both must match the oracle exactly."""
+    N.check(N.lib().qe_ctx_set_jit(gpu_ctx.handle, 1 if request.param == "jit" else 0))
+    gpu_ctx.kernel_mode = request.param
+    yield gpu_ctx
+    N.check(N.lib().qe_ctx_set_jit(gpu_ctx.handle, 1))
+
+
+def check_kernel_kind(ctx, st, lds_mode=True):
+    spec, note = st.last_kernel_kind()
+    if getattr(ctx, "kernel_mode", "jit") == "jit" and lds_mode:
+        # plans whose on-chip table does not fit the LDS budget run global-only (generic kernel)
+        assert spec or note == "global-only launch", f"expected the specialised kernel: {note}"
+    elif getattr(ctx, "kernel_mode", "jit") == "generic":
+        assert not spec
+
+
 # ---- generator ------------------------------------------------------------------------------------
 @pytest.mark.parametrize("dist,param,t", [
     (N.GEN_MOD, 1024, N.TYPE_INT64), (N.GEN_RAW, 0, N.TYPE_INT64), (N.GEN_UNIT53, 0, N.TYPE_FLOAT64),
@@ -328,7 +347,7 @@ ALL_FNS = [N.AGG_SUM, N.AGG_MIN, N.AGG_MAX, N.AGG_COUNT, N.AGG_COUNT_STAR, N.AGG
 
 @pytest.mark.parametrize("ngroups,expected", [(1, 16), (10, 1024), (1000, 1024), (5000, 100), (200_000, 1024)])
 @pytest.mark.parametrize("vtype", ["i64", "f64"])
-def test_hashagg_int64_key(gpu_ctx, ngroups, expected, vtype):
+def test_hashagg_int64_key(agg_ctx, ngroups, expected, vtype):
     rng = np.random.default_rng(ngroups)
     n = 400_000
     k = rng.integers(0, ngroups, n).astype(np.int64) * 7919 - 3
@@ -341,15 +360,16 @@ def test_hashagg_int64_key(gpu_ctx, ngroups, expected, vtype):
     else:
         x, xv = _rand(rng, n, "f64", 0.1)
         t = N.TYPE_FLOAT64
-    st = HashAggregateState(gpu_ctx, [N.TYPE_INT64], [(f, t) for f in ALL_FNS], expected)
-    K, X = dcol(gpu_ctx, N.TYPE_INT64, k, kv), dcol(gpu_ctx, t, x, xv)
+    st = HashAggregateState(agg_ctx, [N.TYPE_INT64], [(f, t) for f in ALL_FNS], expected)
+    K, X = dcol(agg_ctx, N.TYPE_INT64, k, kv), dcol(agg_ctx, t, x, xv)
     st.update([K], [X] * len(ALL_FNS))
+    check_kernel_kind(agg_ctx, st, ngroups <= expected * 4)
     keys, aggs = st.finalize()
     ref = S.group_aggregate([k], [kv], [x] * 6, [xv] * 6, ALL_FNS)
     assert_groups_equal(result_dict(keys, aggs), ref, ALL_FNS)
 
 
-def test_hashagg_f64_key_and_multibatch_order(gpu_ctx):
+def test_hashagg_f64_key_and_multibatch_order(agg_ctx):
     """fp64 keys (Double.equals: NaN one group, +0/-0 distinct) and MIN/MAX ties across batches:
     row order continues across update calls, like the reference's batch loop (K:617-620)."""
     rng = np.random.default_rng(5)
@@ -358,18 +378,24 @@ def test_hashagg_f64_key_and_multibatch_order(gpu_ctx):
     x = rng.choice(np.array([0.0, -0.0, -1.0, np.nan, -3.0]), n)
     xv = rng.random(n) > 0.2
     fns = [N.AGG_MAX, N.AGG_MIN, N.AGG_COUNT, N.AGG_SUM]
-    st = HashAggregateState(gpu_ctx, [N.TYPE_FLOAT64], [(f, N.TYPE_FLOAT64) for f in fns], 16)
+    st = HashAggregateState(agg_ctx, [N.TYPE_FLOAT64], [(f, N.TYPE_FLOAT64) for f in fns], 16)
     for s in range(0, n, 12_345):
         e = min(n, s + 12_345)
-        st.update([dcol(gpu_ctx, N.TYPE_FLOAT64, k[s:e])], [dcol(gpu_ctx, N.TYPE_FLOAT64, x[s:e], xv[s:e])] * 4)
+        st.update([dcol(agg_ctx, N.TYPE_FLOAT64, k[s:e])], [dcol(agg_ctx, N.TYPE_FLOAT64, x[s:e], xv[s:e])] * 4)
     keys, aggs = st.finalize()
     ref = S.group_aggregate([k], [None], [x] * 4, [xv] * 4, fns)
     assert_groups_equal(result_dict(keys, aggs), ref, fns)
 
 
-@pytest.mark.parametrize("types", [(N.TYPE_UINT8, N.TYPE_UINT8), (N.TYPE_INT32, N.TYPE_DATE32),
-                                   (N.TYPE_UINT8, N.TYPE_INT32, N.TYPE_UINT8)])
-def test_hashagg_multi_key(gpu_ctx, types):
+def test_hashagg_multi_key_too_wide(gpu_ctx):
+    """Two 32-bit keys + null bits exceed the packed 63-bit key: rejected loudly."""
+    with pytest.raises(N.IllegalStateException):
+        HashAggregateState(gpu_ctx, [N.TYPE_INT32, N.TYPE_DATE32], [(N.AGG_COUNT_STAR, N.TYPE_INT64)], 16)
+
+
+@pytest.mark.parametrize("types", [(N.TYPE_UINT8, N.TYPE_UINT8), (N.TYPE_INT32, N.TYPE_UINT8),
+                                   (N.TYPE_UINT8, N.TYPE_DATE32, N.TYPE_UINT8)])
+def test_hashagg_multi_key(agg_ctx, types):
     rng = np.random.default_rng(len(types))
     n = 200_000
     keys, kvs, dcols = [], [], []
@@ -381,29 +407,29 @@ def test_hashagg_multi_key(gpu_ctx, types):
         kv = rng.random(n) > 0.05
         keys.append(v.astype(np.int64))
         kvs.append(kv)
-        dcols.append(dcol(gpu_ctx, t, v, kv))
+        dcols.append(dcol(agg_ctx, t, v, kv))
     x = rng.integers(-1000, 1000, n).astype(np.int64)
-    st = HashAggregateState(gpu_ctx, list(types), [(f, N.TYPE_INT64) for f in ALL_FNS], 256)
-    st.update(dcols, [dcol(gpu_ctx, N.TYPE_INT64, x)] * 6)
+    st = HashAggregateState(agg_ctx, list(types), [(f, N.TYPE_INT64) for f in ALL_FNS], 256)
+    st.update(dcols, [dcol(agg_ctx, N.TYPE_INT64, x)] * 6)
     kk, aa = st.finalize()
     ref = S.group_aggregate(keys, kvs, [x] * 6, [None] * 6, ALL_FNS)
     assert_groups_equal(result_dict(kk, aa), ref, ALL_FNS)
 
 
-def test_hashagg_mask_and_no_keys(gpu_ctx):
+def test_hashagg_mask_and_no_keys(agg_ctx):
     rng = np.random.default_rng(11)
     n = 300_000
     x = rng.integers(-100, 100, n).astype(np.int64)
     m = rng.random(n) < 0.3
     mv = rng.random(n) > 0.1
-    st = HashAggregateState(gpu_ctx, [], [(f, N.TYPE_INT64) for f in ALL_FNS], 1)
-    st.update([], [dcol(gpu_ctx, N.TYPE_INT64, x)] * 6, dcol(gpu_ctx, N.TYPE_BOOL, m, mv))
+    st = HashAggregateState(agg_ctx, [], [(f, N.TYPE_INT64) for f in ALL_FNS], 1)
+    st.update([], [dcol(agg_ctx, N.TYPE_INT64, x)] * 6, dcol(agg_ctx, N.TYPE_BOOL, m, mv))
     kk, aa = st.finalize()
     ref = S.group_aggregate([], [], [x] * 6, [None] * 6, ALL_FNS, S.select_mask(m, mv))
     assert_groups_equal(result_dict(kk, aa), ref, ALL_FNS)
     # empty input: zero groups (Main.kt:637: the map stays empty)
-    st2 = HashAggregateState(gpu_ctx, [], [(N.AGG_MAX, N.TYPE_INT64)], 1)
-    st2.update([], [dcol(gpu_ctx, N.TYPE_INT64, x)], dcol(gpu_ctx, N.TYPE_BOOL, np.zeros(n, bool)))
+    st2 = HashAggregateState(agg_ctx, [], [(N.AGG_MAX, N.TYPE_INT64)], 1)
+    st2.update([], [dcol(agg_ctx, N.TYPE_INT64, x)], dcol(agg_ctx, N.TYPE_BOOL, np.zeros(n, bool)))
     assert st2.num_groups() == 0
 
 
@@ -435,12 +461,13 @@ C4_FNS = [f for f, _ in C4_AGGS]
 
 
 @pytest.mark.parametrize("n,row0", [(1, 0), (1000, 5), (10_000_000, 0)])
-def test_fused_c4_vs_oracle(gpu_ctx, n, row0):
+def test_fused_c4_vs_oracle(agg_ctx, n, row0):
     from kquery.datasource import C4_COLUMNS, generate_column
 
-    cols = [generate_column(s, n, row0, 42, gpu_ctx) for s in C4_COLUMNS]
-    st = HashAggregateState(gpu_ctx, [N.TYPE_INT64], C4_AGGS, 1024)
+    cols = [generate_column(s, n, row0, 42, agg_ctx) for s in C4_COLUMNS]
+    st = HashAggregateState(agg_ctx, [N.TYPE_INT64], C4_AGGS, 1024)
     st.update_fused(cols, _c4_spec())
+    check_kernel_kind(agg_ctx, st)
     kk, aa = st.finalize()
     k, _ = gen.generate(gen.GEN_MOD, 1024, 42, 0, row0, n)
     a, _ = gen.generate(gen.GEN_MOD, 1 << 20, 42, 1, row0, n)
@@ -450,7 +477,7 @@ def test_fused_c4_vs_oracle(gpu_ctx, n, row0):
     assert_groups_equal(result_dict(kk, aa), ref, C4_FNS)
 
 
-def test_fused_equals_unfused_operators(gpu_ctx):
+def test_fused_equals_unfused_operators(agg_ctx):
     """Scan -> Selection -> Projection -> HashAggregate: per-family operators and the fused kernel
     give identical batches; both match the oracle (C2-shaped predicate, nullable inputs)."""
     from kquery.columnar import Field, Schema
@@ -472,9 +499,9 @@ def test_fused_equals_unfused_operators(gpu_ctx):
     batches = []
     for s in range(0, n, 300_000):
         e = min(n, s + 300_000)
-        batches.append(RecordBatch(schema, [dcol(gpu_ctx, N.TYPE_INT64, k[s:e]),
-                                            dcol(gpu_ctx, N.TYPE_INT64, a[s:e], av[s:e]),
-                                            dcol(gpu_ctx, N.TYPE_INT64, b[s:e])]))
+        batches.append(RecordBatch(schema, [dcol(agg_ctx, N.TYPE_INT64, k[s:e]),
+                                            dcol(agg_ctx, N.TYPE_INT64, a[s:e], av[s:e]),
+                                            dcol(agg_ctx, N.TYPE_INT64, b[s:e])]))
     scan = ScanExec(InMemoryDataSource(schema, batches), ["k", "a", "b"])
     pred = AndExpression(GtExpression(ColumnExpression(1), LiteralLongExpression(1 << 18)),
                          LtExpression(ColumnExpression(2), LiteralLongExpression(2**39)))
@@ -502,7 +529,7 @@ def test_fused_equals_unfused_operators(gpu_ctx):
     assert_groups_equal(d2, ref, fns)
 
 
-def test_export_import_two_phase(gpu_ctx):
+def test_export_import_two_phase(agg_ctx):
     """main()'s two-phase aggregate (K:1309-1325): shard rows into partitions, partial-aggregate
     each, export records bucketed by hash(key) mod P, import every bucket into its owner, and the
     union of the owners' groups equals the single-pass result."""
@@ -514,13 +541,13 @@ def test_export_import_two_phase(gpu_ctx):
     x, xv = _rand(rng, n, "f64", 0.1)
     fns = [N.AGG_MAX, N.AGG_MIN, N.AGG_SUM, N.AGG_COUNT, N.AGG_COUNT_STAR]
     aggs = [(f, N.TYPE_FLOAT64) for f in fns]
-    owners = [HashAggregateState(gpu_ctx, [N.TYPE_INT64], aggs, 4096) for _ in range(P)]
+    owners = [HashAggregateState(agg_ctx, [N.TYPE_INT64], aggs, 4096) for _ in range(P)]
     bounds = np.linspace(0, n, P + 1).astype(int)
     for p in range(P):
         s, e = bounds[p], bounds[p + 1]
-        st = HashAggregateState(gpu_ctx, [N.TYPE_INT64], aggs, 4096)
+        st = HashAggregateState(agg_ctx, [N.TYPE_INT64], aggs, 4096)
         st.set_row_base(int(s))
-        st.update([dcol(gpu_ctx, N.TYPE_INT64, k[s:e], kv[s:e])], [dcol(gpu_ctx, N.TYPE_FLOAT64, x[s:e], xv[s:e])] * 5)
+        st.update([dcol(agg_ctx, N.TYPE_INT64, k[s:e], kv[s:e])], [dcol(agg_ctx, N.TYPE_FLOAT64, x[s:e], xv[s:e])] * 5)
         recs, counts = st.export(P)
         rb = st.record_bytes()
         off = 0
@@ -537,15 +564,15 @@ def test_export_import_two_phase(gpu_ctx):
     assert_groups_equal(got, ref, fns)
 
 
-def test_hashagg_growth_from_tiny_table(gpu_ctx):
+def test_hashagg_growth_from_tiny_table(agg_ctx):
     """expected_groups far too small: the global table grows and deferred rows / overflow records
     are re-applied exactly once."""
     rng = np.random.default_rng(17)
     n = 2_000_000
     k = rng.integers(0, 300_000, n).astype(np.int64)
     x = rng.integers(0, 10, n).astype(np.int64)
-    st = HashAggregateState(gpu_ctx, [N.TYPE_INT64], [(N.AGG_SUM, N.TYPE_INT64), (N.AGG_COUNT_STAR, N.TYPE_INT64)], 8)
-    st.update([dcol(gpu_ctx, N.TYPE_INT64, k)], [dcol(gpu_ctx, N.TYPE_INT64, x), None])
+    st = HashAggregateState(agg_ctx, [N.TYPE_INT64], [(N.AGG_SUM, N.TYPE_INT64), (N.AGG_COUNT_STAR, N.TYPE_INT64)], 8)
+    st.update([dcol(agg_ctx, N.TYPE_INT64, k)], [dcol(agg_ctx, N.TYPE_INT64, x), None])
     kk, aa = st.finalize()
     ref = S.group_aggregate([k], [None], [x, None], [None, None], [N.AGG_SUM, N.AGG_COUNT_STAR])
     assert_groups_equal(result_dict(kk, aa), ref, [N.AGG_SUM, N.AGG_COUNT_STAR])
