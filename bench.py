@@ -72,7 +72,7 @@ def cpu_baseline(sample_rows: int, threads: int) -> dict:
     ng = C.c_int64()
     secs = lib.qe_cpu_c4(0, sample_rows, 42, threads, 1 << 19, 1024, out, 2048, C.byref(ng))
     return {"value": sample_rows / secs, "unit": "rows/s", "cores": threads, "kind": "port",
-            "sample": f"first {sample_rows} rows of the same C4 table (seed 42), {threads} threads, "
+            "sample": f"rows 0..{sample_rows - 1} of the same C4 table (seed 42), {threads} threads, "
                       f"{secs:.3f} s; C restatement of the reference operator chain (oracle/cpu_baseline.c)"}
 
 
@@ -97,7 +97,7 @@ def main():
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--rows", type=int, default=1_000_000_000, help="rows per GPU")
-    ap.add_argument("--cpu-sample-rows", type=int, default=200_000_000)
+    ap.add_argument("--cpu-sample-rows", type=int, default=0, help="default: the same rows as one GPU")
     ap.add_argument("--cpu-threads", type=int, default=0)
     ap.add_argument("--no-cpu", action="store_true")
     args = ap.parse_args()
@@ -131,12 +131,14 @@ def main():
     owner = HashAggregateState(ctx, [N.TYPE_INT64], aggs, 1024) if world > 1 else None
     spec = c4_spec(N)
     kernel_ms = []
+    kinds = []
 
     def step():
         partial.reset()
         partial.set_row_base(row0)
         partial.update_fused(cols, spec)
         kernel_ms.append(partial.last_kernel_time())
+        kinds.append(partial.last_kernel_kind())
         final = partial
         if world > 1:
             owner.reset()
@@ -209,7 +211,8 @@ def main():
             "unit": "GB/s",
             "frac": achieved / HBM_PEAK_GBS,
             "traffic": traffic,
-            "kernel": "k_hashagg<3,true> (fused filter+project+LDS hash aggregate)",
+            "kernel": ("qe_fused (hipRTC plan-specialised filter+project+LDS hash aggregate)" if kinds[-1][0]
+                       else f"k_hashagg generic interpreter ({kinds[-1][1]})"),
             "avg_kernel_ms": avg_kernel_ms,
             "bytes_per_launch": rows * BYTES_PER_ROW,
             "stream_read_ceiling_gbs": stream_gbs,
@@ -218,7 +221,7 @@ def main():
     }
     if rank == 0 and world == 1 and not args.no_cpu:
         threads = args.cpu_threads or min(16, os.cpu_count() or 1)
-        line["cpu_baseline"] = cpu_baseline(args.cpu_sample_rows, threads)
+        line["cpu_baseline"] = cpu_baseline(args.cpu_sample_rows or rows, threads)
     if rank == 0:
         print(json.dumps(line), flush=True)
     if world > 1:

@@ -259,7 +259,7 @@ def hash_aggregate_rows(keys: Sequence[Sequence[Any]], inputs: Sequence[Sequence
             groups[hk] = (raw, [make_accumulator(f, isf) for f, isf in zip(fns, input_is_f64)])
         for j, acc in enumerate(groups[hk][1]):  # K:628-631
             acc.accumulate(inputs[j][row] if fns[j] != AGG_COUNT_STAR else 1)
-    return {raw: [a.finalValue() for a in accs] for raw, accs in groups.values()}
+    return {tuple(canon(v) for v in raw): [a.finalValue() for a in accs] for raw, accs in groups.values()}
 
 
 # ---- vectorised aggregates ---------------------------------------------------------------------------
@@ -299,7 +299,8 @@ def group_aggregate(keys: Sequence[np.ndarray], key_valid: Sequence[Optional[np.
                     inputs: Sequence[Optional[np.ndarray]], input_valid: Sequence[Optional[np.ndarray]],
                     fns: Sequence[int], sel: Optional[np.ndarray] = None) -> Dict[tuple, list]:
     """Vectorised HashAggregateExec: {key tuple -> [final values]}; null key -> None in the tuple.
-    fp64 keys follow Double.equals (one NaN group; +0.0 and -0.0 distinct)."""
+    fp64 keys follow Double.equals (one NaN group; +0.0 and -0.0 distinct). Key tuples hold
+    canon() forms, because Python dicts would merge 0.0 and -0.0."""
     n = len(keys[0]) if keys else len(next(i for i in inputs if i is not None))
     if sel is None:
         sel = np.ones(n, dtype=bool)
@@ -369,7 +370,7 @@ def group_aggregate(keys: Sequence[np.ndarray], key_valid: Sequence[Optional[np.
                 kt.append(float(np.int64(uniq[code]).view(np.float64)))
             else:
                 kt.append(int(uniq[code]))
-        result[tuple(kt)] = [col[g] for col in cols]
+        result[tuple(canon(x) for x in kt)] = [col[g] for col in cols]
     return result
 
 

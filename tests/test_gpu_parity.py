@@ -328,7 +328,7 @@ def result_dict(keys, aggs):
     kv = [k.to_pylist() for k in keys]
     av = [a.to_pylist() for a in aggs]
     n = aggs[0].length if aggs else keys[0].length
-    return {tuple(k[i] for k in kv): [a[i] for a in av] for i in range(n)}
+    return {tuple(S.canon(k[i]) for k in kv): [a[i] for a in av] for i in range(n)}
 
 
 def assert_groups_equal(got, ref, fns):

@@ -204,3 +204,15 @@ def test_cpu_baseline_matches_oracle(threads, row0):
                             [S.AGG_SUM, S.AGG_COUNT_STAR, S.AGG_MIN, S.AGG_MAX], a > (1 << 19))
     got = {(o.key,): [o.sum, o.count, o.min, o.max] for o in out[: ng.value]}
     assert got == ref
+
+
+def test_double_key_equality_semantics():
+    """Double.equals (K:621-627 keys are boxed Doubles): +0.0 and -0.0 are different groups,
+    every NaN is one group — hand-derived expectation."""
+    k = np.array([0.0, -0.0, 0.0, np.nan, float("nan"), -0.0, 1.0])
+    x = np.arange(7, dtype=np.int64)
+    got = S.group_aggregate([k], [None], [x], [None], [S.AGG_COUNT_STAR])
+    want = {(S.canon(0.0),): [2], (S.canon(-0.0),): [2], (S.canon(math.nan),): [2], (S.canon(1.0),): [1]}
+    assert got == want
+    lit = S.hash_aggregate_rows([[float(v) for v in k]], [[1] * 7], [S.AGG_COUNT_STAR], [False])
+    assert lit == want
