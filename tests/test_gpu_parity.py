@@ -607,3 +607,59 @@ def test_c4_full_size_properties(gpu_ctx):
     ga = _global(gpu_ctx, cols[1], mask)
     gb = _global(gpu_ctx, cols[2], mask)
     assert int(mins.min()) == ga.min and int(maxs.max()) == gb.max
+
+
+def test_export_partition_matches_oracle(gpu_ctx):
+    """qe_hashagg_export buckets groups by the same hash(key) mod P as oracle/records.py."""
+    import struct
+
+    from oracle import records as R
+
+    rng = np.random.default_rng(21)
+    k = rng.integers(-10**12, 10**12, 100_000).astype(np.int64)
+    st = HashAggregateState(gpu_ctx, [N.TYPE_INT64], [(N.AGG_COUNT_STAR, N.TYPE_INT64)], 1 << 17)
+    st.update([dcol(gpu_ctx, N.TYPE_INT64, k)], [None])
+    for P in (1, 3, 8):
+        recs, counts = st.export(P)
+        raw = recs.cpu().numpy().tobytes()
+        rb = st.record_bytes()
+        off = 0
+        for p in range(P):
+            for i in range(counts[p]):
+                key = struct.unpack_from("<q", raw, (off + i) * rb)[0]
+                assert R.partition_of(key, False, P) == p
+            off += counts[p]
+        assert off == len(np.unique(k))
+
+
+def test_exchange_rccl_single_rank(gpu_ctx):
+    """The RCCL path of kquery.exchange (backend nccl = RCCL) end to end on one rank."""
+    import os
+    import socket
+
+    import torch
+    import torch.distributed as dist
+
+    from kquery.exchange import exchange_partials
+
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda", 0))
+    try:
+        rng = np.random.default_rng(4)
+        k = rng.integers(0, 5000, 200_000).astype(np.int64)
+        x = rng.integers(-100, 100, 200_000).astype(np.int64)
+        aggs = [(N.AGG_SUM, N.TYPE_INT64), (N.AGG_COUNT_STAR, N.TYPE_INT64)]
+        part = HashAggregateState(gpu_ctx, [N.TYPE_INT64], aggs, 8192)
+        owner = HashAggregateState(gpu_ctx, [N.TYPE_INT64], aggs, 8192)
+        part.update([dcol(gpu_ctx, N.TYPE_INT64, k)], [dcol(gpu_ctx, N.TYPE_INT64, x), None])
+        n = exchange_partials(part, owner)
+        assert n == len(np.unique(k))
+        kk, aa = owner.finalize()
+        ref = S.group_aggregate([k], [None], [x, None], [None, None], [N.AGG_SUM, N.AGG_COUNT_STAR])
+        assert_groups_equal(result_dict(kk, aa), ref, [N.AGG_SUM, N.AGG_COUNT_STAR])
+    finally:
+        dist.destroy_process_group()
