@@ -31,24 +31,9 @@ BYTES_PER_ROW = 24     # k, a, b int64: algorithmic bytes read per row (SURVEY Â
 
 
 def c4_spec(N, threshold=1 << 19):
-    spec = N.QeFusedSpec()
-    spec.mask_col = -1
-    spec.nterms = 1
-    spec.terms[0].col = 1
-    spec.terms[0].op = N.OP_GT
-    spec.terms[0].rhs_col = -1
-    spec.terms[0].lit = N.scalar(threshold)
-    spec.key_cols[0] = 0
-    p = spec.inputs[0]  # SUM(a + b)
-    p.ntokens = 3
-    p.tokens[0] = N.QeToken(N.TOK_COL, 1, N.QeScalar())
-    p.tokens[1] = N.QeToken(N.TOK_COL, 2, N.QeScalar())
-    p.tokens[2] = N.QeToken(N.TOK_ADD, 0, N.QeScalar())
-    spec.inputs[2].ntokens = 1  # MIN(a)
-    spec.inputs[2].tokens[0] = N.QeToken(N.TOK_COL, 1, N.QeScalar())
-    spec.inputs[3].ntokens = 1  # MAX(b)
-    spec.inputs[3].tokens[0] = N.QeToken(N.TOK_COL, 2, N.QeScalar())
-    return spec
+    from kquery.workloads import c4_spec as spec
+
+    return spec(threshold)
 
 
 def cpu_baseline(sample_rows: int, threads: int) -> dict:

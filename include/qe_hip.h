@@ -213,7 +213,7 @@ int qe_agg_global(qe_ctx* ctx, const qe_column* col, const qe_column* mask /*nul
 #define QE_MAX_AGGS 8
 #define QE_MAX_COLS 8
 #define QE_MAX_TERMS 8
-#define QE_MAX_TOKENS 8
+#define QE_MAX_TOKENS 16
 
 typedef struct qe_agg_desc {
   int32_t fn;         /* QE_AGG_* */

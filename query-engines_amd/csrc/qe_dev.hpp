@@ -19,7 +19,7 @@
 #define QE_MAX_AGGS 8
 #define QE_MAX_COLS 8
 #define QE_MAX_TERMS 8
-#define QE_MAX_TOKENS 8
+#define QE_MAX_TOKENS 16
 #endif
 #ifndef QE_AGG_SUM
 #define QE_AGG_SUM 1
@@ -55,10 +55,11 @@ enum TokOp : int {
 };
 
 // ---- launch description (host fills it; kernels read it as their only argument) ---------------
-struct DTok {
-  qi32 op, arg;
+struct DTok {  // 16 bytes: the Plan (kernel argument) stays under 4 KiB
+  short op;
+  char lit_null, lit_f64;
+  qi32 arg;
   qi64 lit;
-  qi32 lit_null, lit_f64;
 };
 
 struct DAgg {

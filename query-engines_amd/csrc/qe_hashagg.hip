@@ -1186,7 +1186,7 @@ static int compile_plan(qe_hashagg* h, const qe_column* cols, int32_t ncols, con
     bool nullable = false;
     auto emit = [&](int32_t op, int32_t arg, int64_t lit, int32_t lit_null, int32_t lit_f64 = 0) -> int {
       QE_CHECK(nt < QE_MAX_TOKENS, QE_ERR_UNSUPPORTED, "aggregate %d: program too long after type promotion", j);
-      a.tok[nt++] = DTok{op, arg, lit, lit_null, lit_f64};
+      a.tok[nt++] = DTok{(short)op, (char)lit_null, (char)lit_f64, arg, lit};
       return QE_OK;
     };
     for (int t = 0; t < pg.ntokens; ++t) {
@@ -1570,6 +1570,8 @@ int qe_hashagg_set_row_base(qe_hashagg* h, int64_t row_base) {
   h->row_base = row_base;
   return QE_OK;
 }
+
+static_assert(sizeof(Plan) <= 4096, "kernel argument must stay under 4 KiB");
 
 int qe_hashagg_update_fused(qe_hashagg* h, const qe_column* cols, int32_t ncols, const qe_fused_spec* spec) {
   QE_CHECK(h && cols && spec, QE_ERR_INVALID_ARG, "null argument");

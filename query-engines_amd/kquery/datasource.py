@@ -73,6 +73,18 @@ C4_COLUMNS = [  # 1B rows: SELECT k, SUM(a+b), COUNT(*), MIN(a), MAX(b) WHERE a 
 ]
 C4_THRESHOLD = 1 << 19
 
+# 10B rows over 8 GPUs (1.25B per GPU), TPC-H-lineitem-shaped, 38 B/row
+C5_COLUMNS = [
+    ColumnSpec("l_quantity", N.TYPE_INT64, N.GEN_MOD, 50, 10),             # [0, 50)
+    ColumnSpec("l_extendedprice", N.TYPE_FLOAT64, N.GEN_MOD_F64, 10_000_000, 11),  # [0, 100000) step 0.01
+    ColumnSpec("l_discount", N.TYPE_FLOAT64, N.GEN_MOD_F64, 11, 12),        # 0.00 .. 0.10
+    ColumnSpec("l_tax", N.TYPE_FLOAT64, N.GEN_MOD_F64, 9, 13),              # 0.00 .. 0.08
+    ColumnSpec("l_returnflag", N.TYPE_UINT8, N.GEN_MOD, 3, 14),             # dictionary code of A/N/R
+    ColumnSpec("l_linestatus", N.TYPE_UINT8, N.GEN_MOD, 2, 15),             # dictionary code of F/O
+    ColumnSpec("l_shipdate", N.TYPE_DATE32, N.GEN_MOD, 2557, 16),           # days in a 7-year window
+]
+C5_SHIPDATE_MAX = 2400
+
 
 def generate_column(spec: ColumnSpec, n: int, row0: int = 0, seed: int = SEED, ctx: Context = None) -> DeviceColumn:
     ctx = ctx or Context.get(0)

@@ -44,7 +44,7 @@ OP_AND, OP_OR, OP_NOT, OP_IS_NULL, OP_IS_NOT_NULL = 20, 21, 22, 23, 24
 
 AGG_SUM, AGG_MIN, AGG_MAX, AGG_COUNT, AGG_COUNT_STAR, AGG_AVG = 1, 2, 3, 4, 5, 6
 
-MAX_KEYS, MAX_AGGS, MAX_COLS, MAX_TERMS, MAX_TOKENS = 4, 8, 8, 8, 8
+MAX_KEYS, MAX_AGGS, MAX_COLS, MAX_TERMS, MAX_TOKENS = 4, 8, 8, 8, 16
 TOK_COL, TOK_LIT, TOK_ADD, TOK_SUB, TOK_MUL, TOK_DIV = 1, 2, 3, 4, 5, 6
 
 FIXED_WIDTH = {TYPE_INT64: 8, TYPE_FLOAT64: 8, TYPE_INT32: 4, TYPE_DATE32: 4, TYPE_UINT8: 1}

@@ -663,3 +663,31 @@ def test_exchange_rccl_single_rank(gpu_ctx):
         assert_groups_equal(result_dict(kk, aa), ref, [N.AGG_SUM, N.AGG_COUNT_STAR])
     finally:
         dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("n", [1_000_003, 4_000_000])
+def test_fused_c5_lineitem_vs_oracle(agg_ctx, n):
+    """BASELINE config 5 shape (Q1-like): date32 / fp64 / int64 predicates (one a range), two
+    uint8 keys packed, nested fp64 expressions, AVG and COUNT(*)."""
+    from kquery.datasource import C5_COLUMNS, generate_column
+    from kquery.workloads import C5_AGGS, C5_KEY_TYPES, c5_spec
+
+    row0 = 1234567
+    cols = [generate_column(s, n, row0, 42, agg_ctx) for s in C5_COLUMNS]
+    st = HashAggregateState(agg_ctx, C5_KEY_TYPES, C5_AGGS, 16)
+    st.update_fused(cols, c5_spec())
+    check_kernel_kind(agg_ctx, st)
+    kk, aa = st.finalize()
+    v = {s.name: gen.generate(s.dist, s.param, 42, s.col_id, row0, n)[0] for s in C5_COLUMNS}
+    qty, price, disc, tax = v["l_quantity"], v["l_extendedprice"], v["l_discount"], v["l_tax"]
+    flag, status = v["l_returnflag"].astype(np.uint8), v["l_linestatus"].astype(np.uint8)
+    ship = v["l_shipdate"].astype(np.int32)
+    sel = (ship <= 2400) & (disc >= 0.05) & (disc <= 0.07) & (qty < 24)
+    dp = price * (1.0 - disc)
+    dpt = dp * (1.0 + tax)
+    fns = [f for f, _ in C5_AGGS]
+    ref = S.group_aggregate([flag.astype(np.int64), status.astype(np.int64)], [None, None],
+                            [qty, price, dp, dpt, price, None], [None] * 6, fns, sel)
+    got = result_dict(kk, aa)
+    assert_groups_equal(got, ref, fns)
+    assert len(got) == 6

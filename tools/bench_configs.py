@@ -1,0 +1,117 @@
+#!/usr/bin/env python3
+"""Per-configuration measurements (BASELINE.json configs[1..4] on one MI355X), next to the headline
+bench.py line. Each config: device-resident synthetic input, warmup, then the median of N timed
+runs (HIP events on the stream the kernels run on), reported as rows/s and as algorithmic
+HBM bytes / time against the 8 TB/s peak. Writes one JSON object per config to stdout.
+
+  C2  10M int64:  SelectionExec(a > 2^19) -> ProjectionExec(a + b)        per-family operators
+  C3  100M fp64:  SUM/MIN/MAX/COUNT/AVG global aggregate                   qe_agg_global
+  C4  1B int64:   fused filter+project+GROUP BY (the headline)              qe_hashagg_update_fused
+  C5  1.25B rows (10B / 8 GPUs) lineitem-shaped Q1-like, 2 keys, 3 predicates  fused
+"""
+import json
+import pathlib
+import statistics
+import sys
+
+ROOT = pathlib.Path(__file__).resolve().parents[1]
+sys.path[:0] = [str(ROOT), str(ROOT / "query-engines_amd")]
+
+import torch  # noqa: E402
+
+from kquery import native as N  # noqa: E402
+from kquery.aggregate import HashAggregateState  # noqa: E402
+from kquery.columnar import Context, DeviceColumn, Field, RecordBatch, Schema  # noqa: E402
+from kquery.datasource import (C2_COLUMNS, C3_COLUMNS, C4_COLUMNS, C5_COLUMNS, InMemoryDataSource,  # noqa: E402
+                               generate_column)
+from kquery.expressions import (AddExpression, ColumnExpression, GtExpression,  # noqa: E402
+                                LiteralLongExpression)
+from kquery.operators import ProjectionExec, ScanExec, SelectionExec  # noqa: E402
+from kquery.workloads import C4_AGGS, C5_AGGS, C5_KEY_TYPES, c4_spec, c5_spec  # noqa: E402
+
+PEAK = 8000.0
+
+
+def timed(fn, reps=10, warmup=3):
+    for _ in range(warmup):
+        fn()
+    ts = []
+    for _ in range(reps):
+        s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        s.record()
+        fn()
+        e.record()
+        e.synchronize()
+        ts.append(s.elapsed_time(e))
+    return statistics.median(ts)
+
+
+def report(cfg, rows, bytes_per_row, ms, **extra):
+    gbs = rows * bytes_per_row / (ms * 1e-3) / 1e9
+    d = {"config": cfg, "rows": rows, "ms": ms, "rows_per_s": rows / (ms * 1e-3), "alg_bytes_per_row": bytes_per_row,
+         "achieved_gbs": gbs, "peak_gbs": PEAK, "frac": gbs / PEAK}
+    d.update(extra)
+    print(json.dumps(d), flush=True)
+
+
+def main():
+    ctx = Context.get(0)
+    which = sys.argv[1:] or ["C2", "C3", "C4", "C5"]
+    if "C2" in which:
+        n = 10_000_000
+        cols = [generate_column(s, n, 0, 42, ctx) for s in C2_COLUMNS]
+        schema = Schema([s.field() for s in C2_COLUMNS])
+        scan = ScanExec(InMemoryDataSource(schema, [RecordBatch(schema, cols)]), ["a", "b"])
+        sel = SelectionExec(scan, GtExpression(ColumnExpression(0), LiteralLongExpression(1 << 19)))
+        proj = ProjectionExec(sel, Schema([Field("ab", N.TYPE_INT64)]),
+                              [AddExpression(ColumnExpression(0), ColumnExpression(1))])
+        out = {}
+
+        def run():
+            out["b"] = next(proj.execute())
+
+        ms = timed(run)
+        sel_rows = out["b"].rowCount()
+        # algorithmic: read a, b (16 B) + write a+b for the selected rows
+        report("C2 filter(a>2^19)+project(a+b), 10M int64 (160 MB: fits the 256 MB MALL)", n,
+               16 + 8 * sel_rows / n, ms, selected=sel_rows, path="per-family operators (cmp, count, compact, arith)")
+        del cols, out
+    if "C3" in which:
+        n = 100_000_000
+        col = generate_column(C3_COLUMNS[0], n, 0, 42, ctx)
+        c = col.as_c()
+        r = N.QeGlobalAgg()
+
+        def run():
+            N.check(N.lib().qe_agg_global(ctx.handle, N.C.byref(c), None, N.C.byref(r)))
+
+        ms = timed(run)
+        report("C3 SUM/MIN/MAX/COUNT/AVG global aggregate, 100M fp64", n, 8, ms, path="k_agg_global + final")
+        del col
+    for cfg, specs, rows, aggs, keys, spec, bpr, ng in (
+            ("C4", C4_COLUMNS, 1_000_000_000, C4_AGGS, [N.TYPE_INT64], c4_spec(), 24, 1024),
+            ("C5", C5_COLUMNS, 1_250_000_000, C5_AGGS, C5_KEY_TYPES, c5_spec(), 38, 16)):
+        if cfg not in which:
+            continue
+        cols = [generate_column(s, rows, 0, 42, ctx) for s in specs]
+        st = HashAggregateState(ctx, keys, aggs, ng)
+        kms = []
+
+        def run():
+            st.reset()
+            st.update_fused(cols, spec)
+            kms.append(st.last_kernel_time()[0])
+            st.finalize()
+
+        ms = timed(run)
+        kind = st.last_kernel_kind()
+        kmed = statistics.median(kms[-10:])
+        name = ("C4 SELECT k,SUM(a+b),COUNT(*),MIN(a),MAX(b) WHERE a>2^19 GROUP BY k, 1B int64" if cfg == "C4" else
+                "C5 lineitem Q1-like (3 predicates, GROUP BY returnflag,linestatus, 4 SUM+AVG+COUNT), 1.25B rows/GPU")
+        report(name, rows, bpr, ms, kernel_ms=kmed, kernel_gbs=rows * bpr / (kmed * 1e-3) / 1e9,
+               specialised=kind[0], note=kind[1], groups=st.num_groups())
+        del cols, st
+
+
+if __name__ == "__main__":
+    main()
