@@ -170,11 +170,22 @@ int qe_eval_cmp(qe_ctx* ctx, int32_t op, const qe_operand* lhs, const qe_operand
 int qe_eval_bool(qe_ctx* ctx, int32_t op, const qe_column* lhs, const qe_column* rhs,
                  qe_column* out);
 
+/* CastExpression (K6, K:772-805): UTF8 -> FLOAT64 with java.lang.Double.parseDouble semantics
+ * (the reference's `vv.toDouble()`, K:791): trimmed, signed, NaN/Infinity, decimal with optional
+ * exponent, hex with binary exponent, optional [fFdD] suffix; correctly rounded (half-even).
+ * Null rows stay null (K:787-788). A string outside the grammar fails the whole call with
+ * QE_ERR_INVALID_ARG (NumberFormatException, a subclass of IllegalArgumentException) and, if
+ * `error_row` is non-NULL, stores the first offending row there (-1 when none).
+ * `out` is FLOAT64 with capacity >= in->length rows and a validity buffer when `in` has one. */
+int qe_cast_utf8_to_f64(qe_ctx* ctx, const qe_column* in, qe_column* out, int64_t* error_row);
+
 /* ---- SelectionExec (K3b): order-preserving compaction ----------------------------------- */
 /* Rows whose mask is true (null -> dropped) are kept, in input order. */
 int qe_filter_count(qe_ctx* ctx, const qe_column* mask, int64_t* out_count);
-/* Gathers the selected rows of every input column into outs[i] (capacity >= count;
- * fixed-width types only). outs[i].validity is written when inputs[i] has one.
+/* Gathers the selected rows of every input column into outs[i] (capacity >= count rows).
+ * Fixed-width and UTF8 columns; a UTF8 output needs offsets for count+1 entries and a values
+ * buffer as large as the input's (offsets[n] - offsets[0]) bytes. outs[i].validity is written
+ * when inputs[i] has one (buffer padded to whole 32-bit words).
  * *out_count receives the number of rows written (also set as outs[i].length). */
 int qe_filter_apply(qe_ctx* ctx, const qe_column* mask, const qe_column* inputs,
                     int32_t ncols, qe_column* outs, int64_t* out_count);

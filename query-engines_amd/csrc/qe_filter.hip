@@ -89,8 +89,9 @@ struct GatherCol {
   const uint8_t* in_valid;
   void* out;
   uint32_t* out_valid;  // zeroed by the host; bits set with atomicOr
-  int32_t width;        // 8, 4 or 1
+  int32_t width;        // 8, 4 or 1; 0 = UTF-8 (out = int64 {src offset, length} per selected row)
   int32_t pad;
+  const int32_t* in_offs;  // UTF-8 input offsets
 };
 
 constexpr int FT_MAX_COLS = 8;
@@ -102,7 +103,15 @@ struct GatherArgs {
 __device__ __forceinline__ void gather_store(const GatherCol& c, int64_t row0, int nsel_mask, int64_t pos0,
                                              const int (&rank)[4], bool full) {
   // Loads the lane's 4 rows (vectorised when the tile is full) and stores the selected ones.
-  if (c.width == 8) {
+  if (c.width == 0) {  // UTF-8: record (source byte offset, length); bytes are copied after the scan
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      if ((nsel_mask >> j) & 1) {
+        const int32_t s0 = c.in_offs[row0 + j], s1 = c.in_offs[row0 + j + 1];
+        ((int2*)c.out)[pos0 + rank[j]] = make_int2(s0, s1 - s0);
+      }
+    }
+  } else if (c.width == 8) {
     int64_t v[4];
     if (full) {
       typedef long long i64x2 __attribute__((ext_vector_type(2)));
@@ -180,6 +189,66 @@ __global__ void __launch_bounds__(FT_THREADS) k_compact(const uint8_t* __restric
   }
 }
 
+// ---- UTF-8 gather: (src, len) pairs -> offsets (device-wide exclusive scan) -> bytes ------------
+constexpr int SC_TILE = 2048;  // elements per tile, 8 per thread
+
+__global__ void __launch_bounds__(256) k_len_tile_sum(const int2* __restrict__ sl, int64_t n, int64_t* __restrict__ sums) {
+  __shared__ int64_t part[4];
+  int64_t c = 0;
+  const int64_t b0 = (int64_t)blockIdx.x * SC_TILE;
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    const int64_t i = b0 + k * 256 + threadIdx.x;
+    if (i < n) c += sl[i].y;
+  }
+  for (int off = 32; off > 0; off >>= 1) c += __shfl_xor(c, off);
+  if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = c;
+  __syncthreads();
+  if (threadIdx.x == 0) sums[blockIdx.x] = part[0] + part[1] + part[2] + part[3];
+}
+
+// offsets[i] = tile_offset + exclusive prefix of lengths inside the tile; offsets[n] = total.
+__global__ void __launch_bounds__(256) k_len_tile_scan(const int2* __restrict__ sl, int64_t n,
+                                                       const int64_t* __restrict__ tile_off, int32_t* __restrict__ offs) {
+  __shared__ int64_t wsum[4];
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int64_t base = (int64_t)blockIdx.x * SC_TILE + (int64_t)threadIdx.x * 8;  // 8 consecutive per thread
+  int64_t v[8], t = 0;
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    v[k] = base + k < n ? sl[base + k].y : 0;
+    t += v[k];
+  }
+  int64_t x = t;  // inclusive scan of thread totals within the wave
+  for (int off = 1; off < 64; off <<= 1) {
+    const int64_t y = __shfl_up(x, off);
+    if (lane >= off) x += y;
+  }
+  if (lane == 63) wsum[wid] = x;
+  __syncthreads();
+  int64_t run = tile_off[blockIdx.x] + x - t;
+  for (int w = 0; w < wid; ++w) run += wsum[w];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    if (base + k < n) offs[base + k] = (int32_t)run;
+    run += v[k];
+  }
+}
+
+__global__ void k_write_total(const int64_t* __restrict__ total, int32_t* __restrict__ offs, int64_t n) {
+  offs[n] = (int32_t)*total;
+}
+
+__global__ void __launch_bounds__(256) k_copy_bytes(const int2* __restrict__ sl, const int32_t* __restrict__ offs,
+                                                    const uint8_t* __restrict__ src, uint8_t* __restrict__ dst, int64_t n) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    const int2 e = sl[i];
+    const uint8_t* s = src + e.x;
+    uint8_t* d = dst + offs[i];
+    for (int k = 0; k < e.y; ++k) d[k] = s[k];
+  }
+}
+
 struct FilterPlan {
   int64_t ntiles;
   int64_t* counts;   // ntiles
@@ -243,13 +312,14 @@ int qe_filter_apply(qe_ctx* ctx, const qe_column* mask, const qe_column* inputs,
     qe_column& out = outs[i];
     QE_CHECK(in.length == n, QE_ERR_INVALID_ARG, "column %d has %lld rows, mask %lld", i, (long long)in.length,
              (long long)n);
-    QE_CHECK(is_fixed(in.type), QE_ERR_UNSUPPORTED, "filter: column %d type %d not supported (fixed-width only)", i,
-             in.type);
+    const bool utf8 = in.type == QE_TYPE_UTF8;
+    QE_CHECK(is_fixed(in.type) || utf8, QE_ERR_UNSUPPORTED, "filter: column %d type %d not supported", i, in.type);
     QE_CHECK(out.type == in.type && (out.values || out.length == 0), QE_ERR_INVALID_ARG,
              "output %d must have the input's type", i);
     QE_CHECK(!in.validity || out.validity, QE_ERR_INVALID_ARG, "output %d needs a validity buffer", i);
+    QE_CHECK(!utf8 || (in.offsets && out.offsets), QE_ERR_INVALID_ARG, "UTF8 column %d needs offsets", i);
     args.cols[i] = GatherCol{in.values, in.validity, out.values, in.validity ? (uint32_t*)out.validity : nullptr,
-                             type_width(in.type), 0};
+                             utf8 ? 0 : type_width(in.type), 0, utf8 ? in.offsets : nullptr};
   }
   FilterPlan fp;
   QE_TRY(filter_prepare(ctx, mask, &fp));
@@ -264,11 +334,53 @@ int qe_filter_apply(qe_ctx* ctx, const qe_column* mask, const qe_column* inputs,
       QE_HIP(hipMemsetAsync(outs[i].validity, 0, (size_t)div_up((uint64_t)total, 32) * 4, ctx->stream));
     }
   }
+  // UTF-8 columns: k_compact writes (src offset, length) pairs into scratch, then a scan + copy
+  int nutf8 = 0;
+  for (int i = 0; i < ncols; ++i) nutf8 += args.cols[i].width == 0;
+  int2* pairs = nullptr;
+  int64_t* tsum = nullptr;
+  const int64_t stiles = (int64_t)div_up((uint64_t)(total > 0 ? total : 1), SC_TILE);
+  if (nutf8 && total > 0) {
+    // after the filter plan's tile arrays (2*ntiles+1 int64), keep them alive
+    const size_t base = (size_t)(2 * fp.ntiles + 1) * 8;
+    const size_t need = base + (size_t)nutf8 * total * sizeof(int2) + (size_t)(2 * stiles + 1) * 8 + 256;
+    void* sb;
+    QE_TRY(ctx_scratch(ctx, need, &sb));
+    // the scratch may have moved: the tile offsets must be recomputed
+    QE_TRY(filter_prepare(ctx, mask, &fp));
+    pairs = (int2*)((char*)sb + ((base + 15) & ~size_t(15)));
+    tsum = (int64_t*)(pairs + (size_t)nutf8 * total);
+    int u = 0;
+    for (int i = 0; i < ncols; ++i) {
+      if (args.cols[i].width != 0) continue;
+      args.cols[i].pad = u;
+      args.cols[i].out = pairs + (size_t)u * total;
+      ++u;
+    }
+  }
   if (total > 0 && ncols > 0) {
     hipLaunchKernelGGL(k_compact, dim3((unsigned)fp.ntiles), dim3(FT_THREADS), 0, ctx->stream,
                        (const uint8_t*)mask->values, mask->validity, n, fp.offsets, args);
     QE_TRY(launch_check("k_compact"));
   }
+  for (int i = 0; i < ncols && total > 0; ++i) {
+    if (args.cols[i].width != 0) continue;
+    const int2* sl = (const int2*)args.cols[i].out;
+    hipLaunchKernelGGL(k_len_tile_sum, dim3((unsigned)stiles), dim3(256), 0, ctx->stream, sl, total, tsum);
+    QE_TRY(launch_check("k_len_tile_sum"));
+    QE_TRY(exclusive_scan_i64(ctx, tsum, tsum + stiles, stiles));
+    hipLaunchKernelGGL(k_len_tile_scan, dim3((unsigned)stiles), dim3(256), 0, ctx->stream, sl, total,
+                       tsum + stiles, outs[i].offsets);
+    QE_TRY(launch_check("k_len_tile_scan"));
+    hipLaunchKernelGGL(k_write_total, dim3(1), dim3(1), 0, ctx->stream, tsum + 2 * stiles, outs[i].offsets, total);
+    QE_TRY(launch_check("k_write_total"));
+    const int64_t grid = std::min<int64_t>((int64_t)div_up((uint64_t)total, 256), (int64_t)ctx->num_cus * 8);
+    hipLaunchKernelGGL(k_copy_bytes, dim3((unsigned)grid), dim3(256), 0, ctx->stream, sl, outs[i].offsets,
+                       (const uint8_t*)inputs[i].values, (uint8_t*)outs[i].values, total);
+    QE_TRY(launch_check("k_copy_bytes"));
+  }
+  for (int i = 0; i < ncols; ++i)
+    if (args.cols[i].width == 0 && total == 0) QE_HIP(hipMemsetAsync(outs[i].offsets, 0, 4, ctx->stream));
   for (int i = 0; i < ncols; ++i) outs[i].length = total;
   if (out_count) *out_count = total;
   return QE_OK;

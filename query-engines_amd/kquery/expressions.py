@@ -13,6 +13,8 @@ from __future__ import annotations
 
 from typing import Optional, Union
 
+import numpy as np
+
 from . import native as N
 from .columnar import ColumnVector, DeviceColumn, RecordBatch
 
@@ -261,9 +263,10 @@ class IsNotNullExpression(UnaryBooleanExpression):
 
 
 class CastExpression(Expression):
-    """Main.kt:772-805. int64 -> fp64 is supported on device; the reference's Utf8 -> fp64
-    (Java Double.parseDouble grammar) is SURVEY §8f 'next' and raises IllegalStateException
-    here, like the reference does for casts it does not support (Main.kt:792, :799)."""
+    """Main.kt:772-805. Only String values cast (K:791 ``vv.toDouble()``, i.e.
+    java.lang.Double.parseDouble): a UTF8 column runs qe_cast_utf8_to_f64 on the device. Any other
+    input type throws on its first non-null value, as the reference does (K:792); an all-null
+    column casts to all-null. Targets other than double throw (K:799)."""
 
     def __init__(self, expr: Expression, dataType: int):  # noqa: N803
         self.expr = expr
@@ -273,12 +276,23 @@ class CastExpression(Expression):
         v = self.expr.evaluate(input)
         if self.dataType != N.TYPE_FLOAT64:
             raise N.IllegalStateException(N.QE_ERR_UNSUPPORTED, f"Cast to {self.dataType} is not supported")
-        if isinstance(v, DeviceColumn) and v.type == N.TYPE_FLOAT64:
-            raise N.IllegalStateException(N.QE_ERR_UNSUPPORTED, "Cannot cast value to Double: Double")
-        if isinstance(v, DeviceColumn) and v.type in (N.TYPE_INT64, N.TYPE_INT32, N.TYPE_UINT8):
-            # (double)x == x + 0.0 exactly for integers (no -0.0 can arise)
-            return AddExpression(_Given(v), LiteralDoubleExpression(0.0)).evaluate(input)
-        raise N.IllegalStateException(N.QE_ERR_UNSUPPORTED, "Utf8 -> Double cast kernel is not built yet (SURVEY §8f)")
+        n = v.size()
+        if isinstance(v, DeviceColumn) and v.type == N.TYPE_UTF8:
+            out = DeviceColumn.empty(N.TYPE_FLOAT64, n, v.nullable, ctx=v.ctx)
+            oc, ic = out.as_c(), v.as_c()
+            row = N.C.c_int64(-1)
+            st = N.lib().qe_cast_utf8_to_f64(v.ctx.handle, N.C.byref(ic), N.C.byref(oc), N.C.byref(row))
+            if st == N.QE_ERR_INVALID_ARG and row.value >= 0:
+                raise N.NumberFormatException(st, N.lib().qe_last_error().decode(errors="replace"))
+            N.check(st)
+            return out
+        # K:790-792: the first non-null non-String value throws; nulls stay null
+        first = (int(np.argmax(v.valid_mask())) if v.valid_mask().any() else -1) if isinstance(v, DeviceColumn) \
+            else next((i for i in range(n) if v.getValue(i) is not None), -1)
+        if first >= 0:
+            raise N.IllegalStateException(N.QE_ERR_UNSUPPORTED, f"Cannot cast value to Double: {v.getValue(first)}")
+        ctx = v.ctx if isinstance(v, DeviceColumn) else None
+        return DeviceColumn.empty(N.TYPE_FLOAT64, n, True, ctx=ctx)
 
     def __repr__(self) -> str:
         return f"CAST({self.expr} AS {self.dataType})"

@@ -67,6 +67,10 @@ class IllegalArgumentException(QueryEngineError):
     """QE_ERR_INVALID_ARG (Main.kt:49)."""
 
 
+class NumberFormatException(IllegalArgumentException):
+    """CAST(utf8 AS double) of a string outside java.lang.Double.parseDouble's grammar (K:791)."""
+
+
 class CapacityError(QueryEngineError):
     """QE_ERR_CAPACITY: an output buffer is too small."""
 
@@ -174,6 +178,7 @@ SIGNATURES = [
     ("qe_eval_arith", C.c_int, [_P, C.c_int32, _OPP, _OPP, _COLP]),
     ("qe_eval_cmp", C.c_int, [_P, C.c_int32, _OPP, _OPP, _COLP]),
     ("qe_eval_bool", C.c_int, [_P, C.c_int32, _COLP, _COLP, _COLP]),
+    ("qe_cast_utf8_to_f64", C.c_int, [_P, _COLP, _COLP, _I64P]),
     ("qe_filter_count", C.c_int, [_P, _COLP, _I64P]),
     ("qe_filter_apply", C.c_int, [_P, _COLP, _COLP, C.c_int32, _COLP, _I64P]),
     ("qe_agg_global", C.c_int, [_P, _COLP, _COLP, C.POINTER(QeGlobalAgg)]),

@@ -104,6 +104,20 @@ class SelectionExec(PhysicalPlan):
         return f"SelectionExec: {self.expr}"
 
 
+def _alloc_like(c: DeviceColumn, n: int, ctx) -> DeviceColumn:
+    if c.type != N.TYPE_UTF8:
+        return DeviceColumn.empty(c.type, n, c.nullable, ctx=ctx)
+    import torch
+
+    from .columnar import bitmap_bytes
+
+    nbytes = int(c.offsets[c.length].item() - c.offsets[0].item()) if c.length else 0
+    dev = ctx.torch_device
+    return DeviceColumn(N.TYPE_UTF8, n, torch.empty(max(nbytes, 1), dtype=torch.uint8, device=dev),
+                        torch.zeros(max(bitmap_bytes(n), 4), dtype=torch.uint8, device=dev) if c.nullable else None,
+                        torch.empty(n + 1, dtype=torch.int32, device=dev), ctx)
+
+
 def filter_batch(batch: RecordBatch, mask: DeviceColumn) -> RecordBatch:
     ctx = mask.ctx
     cnt = N.C.c_int64()
@@ -114,7 +128,7 @@ def filter_batch(batch: RecordBatch, mask: DeviceColumn) -> RecordBatch:
     for c in cols:
         if not isinstance(c, DeviceColumn):
             raise N.IllegalStateException(N.QE_ERR_UNSUPPORTED, "selection input must be device columns")
-    outs = [DeviceColumn.empty(c.type, n, c.nullable, ctx=ctx) for c in cols]
+    outs = [_alloc_like(c, n, ctx) for c in cols]
     done: list = [None] * len(cols)
     # qe_filter_apply gathers up to 8 columns per launch
     for s in range(0, len(cols), N.MAX_COLS):

@@ -691,3 +691,50 @@ def test_fused_c5_lineitem_vs_oracle(agg_ctx, n):
     got = result_dict(kk, aa)
     assert_groups_equal(got, ref, fns)
     assert len(got) == 6
+
+
+@pytest.mark.parametrize("state,field", [("CA", "filter_state_CA_project_id_first_name"),
+                                         ("Uppsala", "filter_state_Uppsala_ids")])
+def test_config1_employee_csv_on_device(gpu_ctx, state, field):
+    """BASELINE config 1: employee.csv scan -> filter(state = lit) -> project(id, first_name),
+    through the device operators (UTF-8 predicate + UTF-8 compaction), against the reference
+    fixture's known answers."""
+    import json
+    import pathlib
+
+    from kquery.csv_source import CsvDataSource
+    from kquery.columnar import Field, Schema
+    from kquery.expressions import ColumnExpression, EqExpression, LiteralStringExpression
+    from kquery.operators import ProjectionExec, ScanExec, SelectionExec
+
+    gold = pathlib.Path(__file__).parent / "golden"
+    kat = json.loads((gold / "employee_kat.json").read_text())
+    ds = CsvDataSource(str(gold / "employee.csv"), True, 1000, ctx=gpu_ctx)
+    scan = ScanExec(ds, ["first_name", "id", "state"])
+    sel = SelectionExec(scan, EqExpression(ColumnExpression(2), LiteralStringExpression(state)))
+    proj = ProjectionExec(sel, Schema([Field("id", N.TYPE_UTF8), Field("first_name", N.TYPE_UTF8)]),
+                          [ColumnExpression(1), ColumnExpression(0)])
+    out = list(proj.execute())
+    ids = [v for b in out for v in b.field(0).to_pylist()]
+    names = [v for b in out for v in b.field(1).to_pylist()]
+    if state == "CA":
+        assert [[i, nm] for i, nm in zip(ids, names)] == kat[field]
+    else:
+        assert ids == kat[field] and names == ["Matte", "Other"]
+
+
+@pytest.mark.parametrize("n", [1, 100, 8193, 200_001])
+def test_filter_utf8_columns(gpu_ctx, n):
+    from kquery.columnar import RecordBatch, Schema
+    from kquery.operators import filter_batch
+
+    rng = np.random.default_rng(n)
+    words = ["", "a", "Pärsson", "Uppsala", "x" * 40, "tripdata", "VendorID"]
+    strs = [None if rng.random() < 0.1 else words[rng.integers(len(words))] + str(rng.integers(1000)) for _ in range(n)]
+    m = rng.random(n) < 0.4
+    col = DeviceColumn.from_strings(strs, ctx=gpu_ctx)
+    out = filter_batch(RecordBatch(Schema([]), [col, dcol(gpu_ctx, N.TYPE_INT64, np.arange(n, dtype=np.int64))]),
+                       dcol(gpu_ctx, N.TYPE_BOOL, m))
+    want = [s for s, keep in zip(strs, m) if keep]
+    assert out.field(0).to_pylist() == want
+    assert out.field(1).to_numpy().tolist() == np.nonzero(m)[0].tolist()
