@@ -322,6 +322,25 @@ int qe_hashagg_last_kernel_time(qe_hashagg* agg, double* ms, int32_t* launches);
  * not (NUL-terminated note, may be NULL). */
 int qe_hashagg_last_kernel_kind(qe_hashagg* agg, int32_t* specialized, char* note, int32_t note_len);
 
+/* ---- UTF-8 group keys (K:620-627: row key = String(bytes), HashMap content equality) ------
+ * A device string dictionary maps each distinct byte string to a dense int32 code, stable for
+ * the dictionary's lifetime (codes are assigned in first-insertion order within a call, which
+ * is unordered across rows). A hash aggregate groups by the codes (key type INT32); finalize
+ * decodes them back to strings. Equality is byte equality of the whole string. */
+typedef struct qe_strdict qe_strdict;
+int qe_strdict_create(qe_ctx* ctx, int64_t expected_distinct, qe_strdict** out);
+int qe_strdict_destroy(qe_strdict* dict);
+/* Number of distinct strings inserted so far. */
+int qe_strdict_size(qe_strdict* dict, int64_t* out);
+/* codes (INT32, capacity >= in->length; validity required iff `in` has one, copied from it):
+ * the code of every non-null row of the UTF8 column `in`, inserting new strings. */
+int qe_strdict_encode(qe_strdict* dict, const qe_column* in, qe_column* codes);
+/* Total bytes of the strings the non-null rows of `codes` (INT32) decode to. */
+int qe_strdict_decode_bytes(qe_strdict* dict, const qe_column* codes, int64_t* out_bytes);
+/* out (UTF8): offsets for codes->length+1 entries, values >= decode_bytes bytes, validity
+ * iff codes has one. QE_ERR_INVALID_ARG if a code was not issued by this dictionary. */
+int qe_strdict_decode(qe_strdict* dict, const qe_column* codes, qe_column* out);
+
 #ifdef __cplusplus
 }
 #endif

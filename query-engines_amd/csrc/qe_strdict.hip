@@ -1,0 +1,457 @@
+// UTF-8 group keys for HashAggregateExec (Main.kt:620-627: the row key is String(bytes), looked up
+// in a HashMap<List<Any?>, ...> by content equality). The device replaces that HashMap's string
+// hashing/equality with a string dictionary that gives every distinct byte string a dense, stable
+// int32 code; the hash aggregate then groups by codes (bit-exact integer work) and finalize
+// decodes the codes back to strings.
+//
+// Layout in HBM (all owned by the dictionary, sized for growth):
+//   slots    s_hash[cap] (u64, 0 = empty; hashes are forced nonzero), s_code[cap] (i32, -1 = not
+//            yet published, -2 = insertion failed for capacity) — open addressing, linear probing,
+//            cap = 2 * ccap so the load factor stays <= 1/2;
+//   codes    code_off[ccap] (i64 arena offset), code_len[ccap] (i32), code_hash[ccap] (u64);
+//   arena    the distinct strings' bytes, bump-allocated.
+// Equality is byte equality of the full string (the 64-bit hash only filters). Insertion: CAS the
+// hash into an empty slot; the winner copies its bytes to the arena, takes the next code and
+// publishes it. A row that meets a matching hash whose code is not yet published does not wait:
+// it is marked in a retry bitmap and resolved by a second pass after the kernel boundary.
+// Capacity overflow (codes, arena or probe limit) flags the batch; the host grows the arrays,
+// rebuilds the slots from the code arrays (codes keep their numbers) and re-runs the batch.
+#include "qe_internal.hpp"
+
+struct qe_strdict;
+
+namespace qe {
+
+namespace {
+
+struct DictDev {
+  uint64_t* s_hash;
+  int32_t* s_code;
+  uint64_t mask;  // cap - 1
+  int64_t* code_off;
+  int32_t* code_len;
+  uint64_t* code_hash;
+  int64_t ccap;
+  uint8_t* arena;
+  int64_t acap;
+  unsigned int* ncodes;
+  unsigned long long* arena_used;
+  unsigned int* flags;  // [0] overflow, [1] unresolved rows
+};
+
+constexpr int R_RETRY = -1, R_OVERFLOW = -2;
+
+__device__ __forceinline__ uint64_t load_u64_unaligned(const uint8_t* p, int n) {
+  uint64_t w = 0;
+  if (n >= 8) {
+    __builtin_memcpy(&w, p, 8);
+  } else {
+    for (int k = 0; k < n; ++k) w |= (uint64_t)p[k] << (8 * k);
+  }
+  return w;
+}
+
+__device__ __forceinline__ uint64_t str_hash(const uint8_t* p, int len) {
+  uint64_t h = 0x9E3779B97F4A7C15ull ^ ((uint64_t)len * 0xC2B2AE3D27D4EB4Full);
+  int i = 0;
+  for (; i + 8 <= len; i += 8) h = fmix64(h ^ load_u64_unaligned(p + i, 8)) + 0x165667B19E3779F9ull;
+  if (i < len) h = fmix64(h ^ load_u64_unaligned(p + i, len - i) ^ ((uint64_t)(len - i) << 59));
+  h = fmix64(h);
+  return h ? h : 1;
+}
+
+__device__ __forceinline__ bool bytes_equal(const uint8_t* a, const uint8_t* b, int len) {
+  int i = 0;
+  for (; i + 8 <= len; i += 8)
+    if (load_u64_unaligned(a + i, 8) != load_u64_unaligned(b + i, 8)) return false;
+  for (; i < len; ++i)
+    if (a[i] != b[i]) return false;
+  return true;
+}
+
+// code >= 0, R_RETRY (matching hash not yet published) or R_OVERFLOW.
+__device__ int dict_find_or_insert(const DictDev& D, const uint8_t* p, int len, uint64_t h) {
+  uint64_t slot = h & D.mask;
+  for (uint64_t probe = 0; probe <= D.mask; ++probe, slot = (slot + 1) & D.mask) {
+    uint64_t sh = __hip_atomic_load(&D.s_hash[slot], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (sh == 0) {
+      const uint64_t prev = atomicCAS((unsigned long long*)&D.s_hash[slot], 0ull, (unsigned long long)h);
+      if (prev == 0) {  // this lane owns the slot: allocate arena bytes + a code, then publish
+        int c = R_OVERFLOW;
+        const unsigned long long a = atomicAdd(D.arena_used, (unsigned long long)len);
+        if ((int64_t)(a + len) <= D.acap) {
+          const unsigned int cc = atomicAdd(D.ncodes, 1u);
+          if ((int64_t)cc < D.ccap) {
+            for (int k = 0; k < len; ++k) D.arena[a + k] = p[k];
+            D.code_off[cc] = (int64_t)a;
+            D.code_len[cc] = len;
+            D.code_hash[cc] = h;
+            c = (int)cc;
+          }
+        }
+        __threadfence();
+        __hip_atomic_store(&D.s_code[slot], c, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+        if (c < 0) atomicOr(&D.flags[0], 1u);
+        return c;
+      }
+      sh = prev;
+    }
+    if (sh == h) {
+      const int c = __hip_atomic_load(&D.s_code[slot], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
+      if (c == -1) return R_RETRY;
+      if (c == R_OVERFLOW) return R_OVERFLOW;
+      if (D.code_len[c] == len && bytes_equal(D.arena + D.code_off[c], p, len)) return c;
+    }
+  }
+  atomicOr(&D.flags[0], 1u);
+  return R_OVERFLOW;
+}
+
+constexpr int ENC_THREADS = 256;
+
+__device__ __forceinline__ void encode_row(const DictDev& D, const int32_t* offs, const uint8_t* bytes, int64_t i,
+                                           int32_t* codes, uint32_t* retry) {
+  const int32_t s0 = offs[i], len = offs[i + 1] - s0;
+  const uint8_t* p = bytes + s0;
+  const int c = dict_find_or_insert(D, p, len, str_hash(p, len));
+  codes[i] = c >= 0 ? c : 0;
+  if (c == R_RETRY) {
+    atomicOr(&retry[i >> 5], 1u << (i & 31));
+    atomicAdd(&D.flags[1], 1u);
+  }
+}
+
+__global__ void __launch_bounds__(ENC_THREADS) k_dict_encode(DictDev D, const int32_t* __restrict__ offs,
+                                                             const uint8_t* __restrict__ bytes,
+                                                             const uint8_t* __restrict__ valid, int64_t n,
+                                                             int32_t* __restrict__ codes, uint32_t* __restrict__ retry) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    if (valid && !((valid[i >> 3] >> (i & 7)) & 1)) {
+      codes[i] = 0;
+      continue;
+    }
+    encode_row(D, offs, bytes, i, codes, retry);
+  }
+}
+
+// Second pass over the rows of `retry_in` (all codes seen by pass 1 are published by now).
+__global__ void __launch_bounds__(ENC_THREADS) k_dict_encode_retry(DictDev D, const int32_t* __restrict__ offs,
+                                                                   const uint8_t* __restrict__ bytes, int64_t n,
+                                                                   int32_t* __restrict__ codes,
+                                                                   const uint32_t* __restrict__ retry_in,
+                                                                   uint32_t* __restrict__ retry_out) {
+  const int64_t words = (n + 31) >> 5;
+  for (int64_t w = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; w < words; w += (int64_t)gridDim.x * blockDim.x) {
+    uint32_t bits = retry_in[w];
+    while (bits) {
+      const int j = __builtin_ctz(bits);
+      bits &= bits - 1;
+      encode_row(D, offs, bytes, (w << 5) + j, codes, retry_out);
+    }
+  }
+}
+
+__global__ void k_dict_rebuild(DictDev D, int64_t ncodes) {
+  for (int64_t c = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; c < ncodes; c += (int64_t)gridDim.x * blockDim.x) {
+    const uint64_t h = D.code_hash[c];
+    uint64_t slot = h & D.mask;
+    for (;;) {
+      if (atomicCAS((unsigned long long*)&D.s_hash[slot], 0ull, (unsigned long long)h) == 0) {
+        D.s_code[slot] = (int32_t)c;
+        break;
+      }
+      slot = (slot + 1) & D.mask;
+    }
+  }
+}
+
+__global__ void k_dict_decode_len(const int32_t* __restrict__ codes, const uint8_t* __restrict__ valid, int64_t n,
+                                  const int32_t* __restrict__ code_len, int64_t ncodes, int64_t* __restrict__ lens,
+                                  unsigned int* __restrict__ bad) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    int64_t l = 0;
+    if (!valid || ((valid[i >> 3] >> (i & 7)) & 1)) {
+      const int32_t c = codes[i];
+      if (c < 0 || c >= ncodes) atomicOr(bad, 1u);
+      else l = code_len[c];
+    }
+    lens[i] = l;
+  }
+}
+
+__global__ void k_dict_decode_copy(const int32_t* __restrict__ codes, const uint8_t* __restrict__ valid, int64_t n,
+                                   const int64_t* __restrict__ code_off, const int32_t* __restrict__ code_len,
+                                   const uint8_t* __restrict__ arena, const int64_t* __restrict__ starts,
+                                   int32_t* __restrict__ out_offs, uint8_t* __restrict__ out_bytes) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i <= n; i += (int64_t)gridDim.x * blockDim.x) {
+    out_offs[i] = (int32_t)starts[i];
+    if (i == n) continue;
+    if (valid && !((valid[i >> 3] >> (i & 7)) & 1)) continue;
+    const int32_t c = codes[i];
+    const uint8_t* src = arena + code_off[c];
+    uint8_t* dst = out_bytes + starts[i];
+    for (int k = 0; k < code_len[c]; ++k) dst[k] = src[k];
+  }
+}
+
+}  // namespace
+
+}  // namespace qe
+
+using namespace qe;
+
+struct qe_strdict {
+  qe_ctx* ctx = nullptr;
+  uint64_t cap = 0;  // slots (power of two)
+  int64_t ccap = 0, acap = 0;
+  uint64_t* s_hash = nullptr;
+  int32_t* s_code = nullptr;
+  int64_t* code_off = nullptr;
+  int32_t* code_len = nullptr;
+  uint64_t* code_hash = nullptr;
+  uint8_t* arena = nullptr;
+  // ctl: ncodes (u32) | pad | arena_used (u64) | flags[2] (u32)
+  uint8_t* ctl = nullptr;
+  int64_t ncodes = 0;
+  int64_t arena_used = 0;
+
+  unsigned int* d_ncodes() { return (unsigned int*)ctl; }
+  unsigned long long* d_arena_used() { return (unsigned long long*)(ctl + 8); }
+  unsigned int* d_flags() { return (unsigned int*)(ctl + 16); }
+  DictDev dev() {
+    return DictDev{s_hash, s_code, cap - 1, code_off, code_len, code_hash, ccap, arena, acap,
+                   d_ncodes(), d_arena_used(), d_flags()};
+  }
+};
+
+namespace {
+
+int dict_free(qe_strdict* d) {
+  void* ptrs[] = {d->s_hash, d->s_code, d->code_off, d->code_len, d->code_hash, d->arena, d->ctl};
+  for (void* p : ptrs)
+    if (p) (void)hipFree(p);
+  return QE_OK;
+}
+
+int grow_slots(qe_strdict* d, uint64_t cap) {
+  qe_ctx* ctx = d->ctx;
+  if (d->s_hash) QE_HIP(hipFree(d->s_hash));
+  if (d->s_code) QE_HIP(hipFree(d->s_code));
+  d->s_hash = nullptr;
+  d->s_code = nullptr;
+  QE_HIP(hipMalloc(&d->s_hash, cap * 8));
+  QE_HIP(hipMalloc(&d->s_code, cap * 4));
+  d->cap = cap;
+  QE_HIP(hipMemsetAsync(d->s_hash, 0, cap * 8, ctx->stream));
+  QE_HIP(hipMemsetAsync(d->s_code, 0xFF, cap * 4, ctx->stream));
+  if (d->ncodes > 0) {
+    const int grid = (int)std::min<int64_t>((int64_t)div_up((uint64_t)d->ncodes, 256), (int64_t)ctx->num_cus * 8);
+    hipLaunchKernelGGL(k_dict_rebuild, dim3(grid), dim3(256), 0, ctx->stream, d->dev(), d->ncodes);
+    QE_TRY(launch_check("k_dict_rebuild"));
+  }
+  return QE_OK;
+}
+
+template <typename T>
+int grow_array(qe_ctx* ctx, T** p, int64_t old_n, int64_t new_n) {
+  T* q = nullptr;
+  QE_HIP(hipMalloc(&q, (size_t)new_n * sizeof(T)));
+  if (*p) {
+    if (old_n > 0) QE_HIP(hipMemcpyAsync(q, *p, (size_t)old_n * sizeof(T), hipMemcpyDeviceToDevice, ctx->stream));
+    QE_HIP(hipStreamSynchronize(ctx->stream));
+    QE_HIP(hipFree(*p));
+  }
+  *p = q;
+  return QE_OK;
+}
+
+// Reads the control block back; returns the flags.
+int read_ctl(qe_strdict* d, uint32_t* overflow, uint32_t* unresolved) {
+  uint8_t h[24];
+  QE_HIP(hipMemcpyAsync(h, d->ctl, 24, hipMemcpyDeviceToHost, d->ctx->stream));
+  QE_HIP(hipStreamSynchronize(d->ctx->stream));
+  uint32_t nc;
+  uint64_t au;
+  memcpy(&nc, h, 4);
+  memcpy(&au, h + 8, 8);
+  memcpy(overflow, h + 16, 4);
+  memcpy(unresolved, h + 20, 4);
+  d->ncodes = std::min<int64_t>((int64_t)nc, d->ccap);  // codes >= ccap were never published
+  d->arena_used = (int64_t)au;
+  return QE_OK;
+}
+
+int write_ctl(qe_strdict* d) {
+  uint8_t h[24] = {0};
+  const uint32_t nc = (uint32_t)d->ncodes;
+  const uint64_t au = (uint64_t)d->arena_used;
+  memcpy(h, &nc, 4);
+  memcpy(h + 8, &au, 8);
+  QE_HIP(hipMemcpyAsync(d->ctl, h, 24, hipMemcpyHostToDevice, d->ctx->stream));
+  QE_HIP(hipStreamSynchronize(d->ctx->stream));
+  return QE_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int qe_strdict_create(qe_ctx* ctx, int64_t expected_distinct, qe_strdict** out) {
+  QE_TRY(ctx_enter(ctx));
+  QE_CHECK(out, QE_ERR_INVALID_ARG, "null argument");
+  *out = nullptr;
+  qe_strdict* d = new qe_strdict();
+  d->ctx = ctx;
+  int64_t cc = 1024;
+  while (cc < expected_distinct && cc < (1ll << 30)) cc <<= 1;
+  d->ccap = cc;
+  d->acap = std::max<int64_t>(1 << 16, cc * 16);
+  int st = QE_OK;
+  if ((st = grow_array(ctx, &d->code_off, 0, d->ccap)) != QE_OK || (st = grow_array(ctx, &d->code_len, 0, d->ccap)) ||
+      (st = grow_array(ctx, &d->code_hash, 0, d->ccap)) || (st = grow_array(ctx, &d->arena, 0, d->acap)) ||
+      (st = grow_array(ctx, &d->ctl, 0, 24)) || (st = grow_slots(d, (uint64_t)d->ccap * 2)) || (st = write_ctl(d))) {
+    dict_free(d);
+    delete d;
+    return st;
+  }
+  *out = d;
+  return QE_OK;
+}
+
+int qe_strdict_destroy(qe_strdict* d) {
+  if (!d) return QE_OK;
+  (void)hipSetDevice(d->ctx->device);
+  (void)hipStreamSynchronize(d->ctx->stream);
+  dict_free(d);
+  delete d;
+  return QE_OK;
+}
+
+int qe_strdict_size(qe_strdict* d, int64_t* n) {
+  QE_CHECK(d && n, QE_ERR_INVALID_ARG, "null argument");
+  *n = d->ncodes;
+  return QE_OK;
+}
+
+int qe_strdict_encode(qe_strdict* d, const qe_column* in, qe_column* codes) {
+  QE_CHECK(d && in && codes, QE_ERR_INVALID_ARG, "null argument");
+  qe_ctx* ctx = d->ctx;
+  QE_TRY(ctx_enter(ctx));
+  QE_CHECK(in->type == QE_TYPE_UTF8 && in->offsets, QE_ERR_UNSUPPORTED, "string dictionary input must be UTF8");
+  QE_CHECK(codes->type == QE_TYPE_INT32, QE_ERR_INVALID_ARG, "codes column must be INT32");
+  const int64_t n = in->length;
+  QE_CHECK(codes->length >= n && (codes->values || n == 0), QE_ERR_CAPACITY, "codes column too small");
+  QE_CHECK(!in->validity || codes->validity, QE_ERR_INVALID_ARG, "codes validity buffer required");
+  codes->length = n;
+  if (n == 0) return QE_OK;
+  if (in->validity)
+    QE_HIP(hipMemcpyAsync(codes->validity, in->validity, (size_t)div_up((uint64_t)n, 32) * 4, hipMemcpyDeviceToDevice,
+                          ctx->stream));
+  const int64_t words = (int64_t)div_up((uint64_t)n, 32);
+  void* s;
+  QE_TRY(ctx_scratch(ctx, (size_t)words * 8, &s));
+  uint32_t* retry[2] = {(uint32_t*)s, (uint32_t*)s + words};
+  const int grid = (int)std::min<int64_t>((int64_t)div_up((uint64_t)n, ENC_THREADS), (int64_t)ctx->num_cus * 16);
+  for (int attempt = 0; attempt < 64; ++attempt) {
+    QE_HIP(hipMemsetAsync(retry[0], 0, (size_t)words * 4, ctx->stream));
+    QE_HIP(hipMemsetAsync(d->d_flags(), 0, 8, ctx->stream));
+    hipLaunchKernelGGL(k_dict_encode, dim3(grid), dim3(ENC_THREADS), 0, ctx->stream, d->dev(), in->offsets,
+                       (const uint8_t*)in->values, in->validity, n, (int32_t*)codes->values, retry[0]);
+    QE_TRY(launch_check("k_dict_encode"));
+    uint32_t ovf = 0, unres = 0;
+    QE_TRY(read_ctl(d, &ovf, &unres));
+    int cur = 0;
+    for (int pass = 0; pass < 64 && unres && !ovf; ++pass) {
+      QE_HIP(hipMemsetAsync(retry[1 - cur], 0, (size_t)words * 4, ctx->stream));
+      QE_HIP(hipMemsetAsync(d->d_flags() + 1, 0, 4, ctx->stream));
+      const int g2 = (int)std::min<int64_t>((int64_t)div_up((uint64_t)words, 256), (int64_t)ctx->num_cus * 4);
+      hipLaunchKernelGGL(k_dict_encode_retry, dim3(g2), dim3(256), 0, ctx->stream, d->dev(), in->offsets,
+                         (const uint8_t*)in->values, n, (int32_t*)codes->values, retry[cur], retry[1 - cur]);
+      QE_TRY(launch_check("k_dict_encode_retry"));
+      QE_TRY(read_ctl(d, &ovf, &unres));
+      cur = 1 - cur;
+    }
+    if (!ovf && !unres) return QE_OK;
+    // grow: codes x4 (slots follow), arena to twice what is in use plus this batch's bytes
+    int32_t o[2] = {0, 0};
+    QE_HIP(hipMemcpy(o, in->offsets + n, 4, hipMemcpyDeviceToHost));
+    QE_HIP(hipMemcpy(o + 1, in->offsets, 4, hipMemcpyDeviceToHost));
+    const int64_t batch_bytes = (int64_t)o[0] - o[1];
+    const int64_t new_ccap = d->ncodes * 2 >= d->ccap ? d->ccap * 4 : d->ccap;
+    const int64_t used = std::min<int64_t>(d->arena_used, d->acap);
+    const int64_t new_acap = d->arena_used + 64 > d->acap ? std::max<int64_t>(d->acap * 2, used * 2 + batch_bytes)
+                                                           : d->acap;
+    QE_CHECK(new_ccap <= (1ll << 31), QE_ERR_CAPACITY, "more than 2^31 distinct strings");
+    if (new_ccap != d->ccap) {
+      QE_TRY(grow_array(ctx, &d->code_off, d->ncodes, new_ccap));
+      QE_TRY(grow_array(ctx, &d->code_len, d->ncodes, new_ccap));
+      QE_TRY(grow_array(ctx, &d->code_hash, d->ncodes, new_ccap));
+      d->ccap = new_ccap;
+    }
+    if (new_acap != d->acap) {
+      QE_TRY(grow_array(ctx, &d->arena, used, new_acap));
+      d->acap = new_acap;
+    }
+    if (d->arena_used > d->acap) d->arena_used = used;  // drop reservations past the old end
+    QE_TRY(write_ctl(d));
+    QE_TRY(grow_slots(d, (uint64_t)d->ccap * 2));  // also clears failed (-2) slots
+  }
+  return fail(QE_ERR_DEVICE, "string dictionary did not converge");
+}
+
+int qe_strdict_decode_bytes(qe_strdict* d, const qe_column* codes, int64_t* out_bytes) {
+  QE_CHECK(d && codes && out_bytes, QE_ERR_INVALID_ARG, "null argument");
+  qe_ctx* ctx = d->ctx;
+  QE_TRY(ctx_enter(ctx));
+  QE_CHECK(codes->type == QE_TYPE_INT32, QE_ERR_INVALID_ARG, "codes column must be INT32");
+  const int64_t n = codes->length;
+  *out_bytes = 0;
+  if (n == 0) return QE_OK;
+  void* s;
+  QE_TRY(ctx_scratch(ctx, (size_t)(2 * n + 2) * 8, &s));
+  int64_t* lens = (int64_t*)s;
+  int64_t* starts = lens + n;
+  unsigned int* bad = (unsigned int*)(starts + n + 1);
+  QE_HIP(hipMemsetAsync(bad, 0, 4, ctx->stream));
+  const int grid = (int)std::min<int64_t>((int64_t)div_up((uint64_t)n, 256), (int64_t)ctx->num_cus * 8);
+  hipLaunchKernelGGL(k_dict_decode_len, dim3(grid), dim3(256), 0, ctx->stream, (const int32_t*)codes->values,
+                     codes->validity, n, d->code_len, d->ncodes, lens, bad);
+  QE_TRY(launch_check("k_dict_decode_len"));
+  QE_TRY(exclusive_scan_i64(ctx, lens, starts, n));
+  int64_t h[2] = {0, 0};
+  QE_HIP(hipMemcpyAsync(h, starts + n, 8, hipMemcpyDeviceToHost, ctx->stream));
+  QE_HIP(hipMemcpyAsync(h + 1, bad, 4, hipMemcpyDeviceToHost, ctx->stream));
+  QE_HIP(hipStreamSynchronize(ctx->stream));
+  QE_CHECK((uint32_t)h[1] == 0, QE_ERR_INVALID_ARG, "code out of range for this dictionary");
+  *out_bytes = h[0];
+  return QE_OK;
+}
+
+int qe_strdict_decode(qe_strdict* d, const qe_column* codes, qe_column* out) {
+  QE_CHECK(d && codes && out, QE_ERR_INVALID_ARG, "null argument");
+  qe_ctx* ctx = d->ctx;
+  QE_CHECK(out->type == QE_TYPE_UTF8 && out->offsets, QE_ERR_INVALID_ARG, "output must be UTF8 with offsets");
+  const int64_t n = codes->length;
+  QE_CHECK(!codes->validity || out->validity, QE_ERR_INVALID_ARG, "output validity buffer required");
+  int64_t total = 0;
+  QE_TRY(qe_strdict_decode_bytes(d, codes, &total));  // leaves starts in scratch
+  QE_CHECK(total < (1ll << 31), QE_ERR_CAPACITY, "decoded strings exceed 2^31 bytes");
+  out->length = n;
+  if (n == 0) {
+    QE_HIP(hipMemsetAsync(out->offsets, 0, 4, ctx->stream));
+    return QE_OK;
+  }
+  QE_CHECK(out->values || total == 0, QE_ERR_CAPACITY, "output values buffer required");
+  const int64_t* starts = (const int64_t*)ctx->scratch + n;
+  const int grid = (int)std::min<int64_t>((int64_t)div_up((uint64_t)n + 1, 256), (int64_t)ctx->num_cus * 8);
+  hipLaunchKernelGGL(k_dict_decode_copy, dim3(grid), dim3(256), 0, ctx->stream, (const int32_t*)codes->values,
+                     codes->validity, n, d->code_off, d->code_len, d->arena, starts, out->offsets,
+                     (uint8_t*)out->values);
+  QE_TRY(launch_check("k_dict_decode_copy"));
+  if (codes->validity)
+    QE_HIP(hipMemcpyAsync(out->validity, codes->validity, (size_t)div_up((uint64_t)n, 32) * 4,
+                          hipMemcpyDeviceToDevice, ctx->stream));
+  return QE_OK;
+}
+
+}  // extern "C"

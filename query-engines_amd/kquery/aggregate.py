@@ -22,10 +22,16 @@ class HashAggregateState:
 
     def __init__(self, ctx: Context, key_types: Sequence[int], aggs: Sequence[Tuple[int, int]],
                  expected_groups: int = 1024):
+        from .strdict import StringDictionary
+
         self.ctx = ctx
         self.key_types = list(key_types)
         self.aggs = [(int(f), int(t)) for f, t in aggs]
-        kt = (N.C.c_int32 * max(1, len(self.key_types)))(*self.key_types)
+        # UTF-8 keys: grouped by their dictionary code (INT32), decoded in finalize
+        self.dicts = {i: StringDictionary(ctx, expected_groups) for i, t in enumerate(self.key_types)
+                      if t == N.TYPE_UTF8}
+        self.device_key_types = [N.TYPE_INT32 if t == N.TYPE_UTF8 else t for t in self.key_types]
+        kt = (N.C.c_int32 * max(1, len(self.key_types)))(*self.device_key_types)
         ad = (N.QeAggDesc * max(1, len(self.aggs)))(*[N.QeAggDesc(f, t) for f, t in self.aggs])
         h = N.C.c_void_p()
         N.check(N.lib().qe_hashagg_create(ctx.handle, len(self.key_types), kt, len(self.aggs), ad,
@@ -33,6 +39,8 @@ class HashAggregateState:
         self.handle = h
 
     def close(self) -> None:
+        for d in getattr(self, "dicts", {}).values():
+            d.close()
         if getattr(self, "handle", None) is not None:
             N.lib().qe_hashagg_destroy(self.handle)
             self.handle = None
@@ -46,6 +54,7 @@ class HashAggregateState:
     # ---- updates --------------------------------------------------------------------------------
     def update(self, keys: Sequence[DeviceColumn], inputs: Sequence[Optional[DeviceColumn]],
                mask: Optional[DeviceColumn] = None) -> None:
+        keys = [self.dicts[i].encode(k) if i in self.dicts else k for i, k in enumerate(keys)]
         kc = (N.QeColumn * max(1, len(keys)))(*[k.as_c() for k in keys])
         ic = (N.QeColumn * max(1, len(self.aggs)))(
             *[(x.as_c() if x is not None else N.QeColumn()) for x in inputs])
@@ -53,6 +62,8 @@ class HashAggregateState:
         N.check(N.lib().qe_hashagg_update(self.handle, kc, ic, N.C.byref(mc) if mc is not None else None))
 
     def update_fused(self, cols: Sequence[DeviceColumn], spec: N.QeFusedSpec) -> None:
+        if self.dicts:
+            raise N.IllegalStateException(N.QE_ERR_UNSUPPORTED, "fused update with UTF-8 keys")
         cc = (N.QeColumn * len(cols))(*[c.as_c() for c in cols])
         N.check(N.lib().qe_hashagg_update_fused(self.handle, cc, len(cols), N.C.byref(spec)))
 
@@ -85,7 +96,7 @@ class HashAggregateState:
     def finalize(self) -> Tuple[List[DeviceColumn], List[DeviceColumn]]:
         """One output batch (Main.kt:635-650): key columns, aggregate columns."""
         g = self.num_groups()
-        keys = [DeviceColumn.empty(t, g, True, ctx=self.ctx) for t in self.key_types]
+        keys = [DeviceColumn.empty(t, g, True, ctx=self.ctx) for t in self.device_key_types]
         aggs = [DeviceColumn.empty(output_type(f, t), g, f not in (N.AGG_COUNT, N.AGG_COUNT_STAR), ctx=self.ctx)
                 for f, t in self.aggs]
         kc = (N.QeColumn * max(1, len(keys)))(*[k.as_c() for k in keys])
@@ -94,6 +105,7 @@ class HashAggregateState:
         N.check(N.lib().qe_hashagg_finalize(self.handle, kc, ac, N.C.byref(out)))
         for c in keys + aggs:
             c.length = out.value
+        keys = [self.dicts[i].decode(k) if i in self.dicts else k for i, k in enumerate(keys)]
         return keys, aggs
 
     # ---- partial records (exchange) -----------------------------------------------------------------
@@ -102,7 +114,13 @@ class HashAggregateState:
         N.check(N.lib().qe_hashagg_record_bytes(self.handle, N.C.byref(n)))
         return n.value
 
+    def _check_exportable(self) -> None:
+        if self.dicts:  # codes are local to this state's dictionary
+            raise N.IllegalStateException(N.QE_ERR_UNSUPPORTED,
+                                          "partial records with UTF-8 keys are not exchangeable yet")
+
     def export_counts(self, nparts: int) -> List[int]:
+        self._check_exportable()
         arr = (N.C.c_int64 * nparts)()
         N.check(N.lib().qe_hashagg_export_counts(self.handle, nparts, arr))
         return list(arr)
@@ -118,6 +136,7 @@ class HashAggregateState:
         return buf[: sum(counts) * rb], counts
 
     def import_records(self, records, nrecords: int) -> None:
+        self._check_exportable()
         if nrecords == 0:
             return
         N.check(N.lib().qe_hashagg_import(self.handle, N.C.c_void_p(records.data_ptr()), int(nrecords)))

@@ -364,6 +364,8 @@ def fuse(plan: PhysicalPlan) -> PhysicalPlan:
             g = _resolve(g, proj)
             if not isinstance(g, ColumnExpression):
                 raise _NotFusable("group key must be a column")
+            if sm.type_of(g.i) not in N.FIXED_WIDTH:
+                raise _NotFusable("UTF-8 group keys go through the string dictionary (unfused)")
             spec.key_cols[k] = sm.slot(g.i)
             key_types.append(sm.type_of(g.i))
         aggs = []

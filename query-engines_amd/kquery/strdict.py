@@ -1,0 +1,59 @@
+"""Device string dictionary (qe_strdict_*): UTF-8 group keys for HashAggregateExec.
+
+The reference keys its HashMap by ``String(bytes)`` (Main.kt:620-627) and compares keys by
+content. Here every distinct byte string gets a dense int32 code on the device; the hash
+aggregate groups by codes and finalize decodes them back to strings.
+"""
+from __future__ import annotations
+
+from . import native as N
+from .columnar import Context, DeviceColumn
+
+
+class StringDictionary:
+    def __init__(self, ctx: Context, expected_distinct: int = 1024):
+        self.ctx = ctx
+        h = N.C.c_void_p()
+        N.check(N.lib().qe_strdict_create(ctx.handle, int(expected_distinct), N.C.byref(h)))
+        self.handle = h
+
+    def close(self) -> None:
+        if getattr(self, "handle", None) is not None:
+            N.lib().qe_strdict_destroy(self.handle)
+            self.handle = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def size(self) -> int:
+        n = N.C.c_int64()
+        N.check(N.lib().qe_strdict_size(self.handle, N.C.byref(n)))
+        return n.value
+
+    def encode(self, col: DeviceColumn) -> DeviceColumn:
+        """UTF8 column -> INT32 codes (nulls stay null)."""
+        if col.type != N.TYPE_UTF8:
+            raise N.IllegalStateException(N.QE_ERR_UNSUPPORTED, f"string dictionary input type {col.type}")
+        out = DeviceColumn.empty(N.TYPE_INT32, col.length, col.nullable, ctx=self.ctx)
+        ic, oc = col.as_c(), out.as_c()
+        N.check(N.lib().qe_strdict_encode(self.handle, N.C.byref(ic), N.C.byref(oc)))
+        return out
+
+    def decode(self, codes: DeviceColumn) -> DeviceColumn:
+        """INT32 codes -> UTF8 column."""
+        import torch
+
+        cc = codes.as_c()
+        nbytes = N.C.c_int64()
+        N.check(N.lib().qe_strdict_decode_bytes(self.handle, N.C.byref(cc), N.C.byref(nbytes)))
+        dev = self.ctx.torch_device
+        n = codes.length
+        out = DeviceColumn(N.TYPE_UTF8, n, torch.empty(max(1, nbytes.value), dtype=torch.uint8, device=dev),
+                           codes.validity.clone() if codes.validity is not None else None,
+                           torch.empty(n + 1, dtype=torch.int32, device=dev), self.ctx)
+        oc = out.as_c()
+        N.check(N.lib().qe_strdict_decode(self.handle, N.C.byref(cc), N.C.byref(oc)))
+        return out
