@@ -341,6 +341,77 @@ int qe_strdict_decode_bytes(qe_strdict* dict, const qe_column* codes, int64_t* o
  * iff codes has one. QE_ERR_INVALID_ARG if a code was not issued by this dictionary. */
 int qe_strdict_decode(qe_strdict* dict, const qe_column* codes, qe_column* out);
 
+/* ---- Arrow C Data Interface boundary -----------------------------------------
+ * Arrow Java exports a VectorSchemaRoot (the reference's batches, K:635-650) as a struct
+ * ArrowArray + ArrowSchema (org.apache.arrow.c.Data.exportVectorSchemaRoot); these entry points
+ * take and return exactly that, so the JNI shim passes two struct addresses per batch.
+ * Standard ABI structs (Arrow C data / C device data interface specification). */
+#ifndef ARROW_C_DATA_INTERFACE
+#define ARROW_C_DATA_INTERFACE
+#define ARROW_FLAG_DICTIONARY_ORDERED 1
+#define ARROW_FLAG_NULLABLE 2
+#define ARROW_FLAG_MAP_KEYS_SORTED 4
+struct ArrowSchema {
+  const char* format;
+  const char* name;
+  const char* metadata;
+  int64_t flags;
+  int64_t n_children;
+  struct ArrowSchema** children;
+  struct ArrowSchema* dictionary;
+  void (*release)(struct ArrowSchema*);
+  void* private_data;
+};
+struct ArrowArray {
+  int64_t length;
+  int64_t null_count;
+  int64_t offset;
+  int64_t n_buffers;
+  int64_t n_children;
+  const void** buffers;
+  struct ArrowArray** children;
+  struct ArrowArray* dictionary;
+  void (*release)(struct ArrowArray*);
+  void* private_data;
+};
+#endif
+#ifndef ARROW_C_DEVICE_DATA_INTERFACE
+#define ARROW_C_DEVICE_DATA_INTERFACE
+typedef int32_t ArrowDeviceType;
+struct ArrowDeviceArray {
+  struct ArrowArray array;
+  int64_t device_id;
+  ArrowDeviceType device_type;
+  void* sync_event;
+  int64_t reserved[3];
+};
+#endif
+#define QE_ARROW_DEVICE_CPU 1
+#define QE_ARROW_DEVICE_ROCM 10
+typedef struct ArrowSchema ArrowSchema;
+typedef struct ArrowArray ArrowArray;
+typedef struct ArrowDeviceArray ArrowDeviceArray;
+
+/* A device-resident batch: the columns of one RecordBatch (K:56-61) in HBM. */
+typedef struct qe_batch qe_batch;
+/* Host record batch (struct array "+s"; children l/g/u/U/i/C/tdD/b, any offset, nullable) ->
+ * device copy owned by the batch. H2D goes through double-buffered pinned staging. The caller
+ * keeps ownership of (and later releases) `array`/`schema`. Unsupported formats ->
+ * QE_ERR_UNSUPPORTED (cf. K:195). */
+int qe_batch_import(qe_ctx* ctx, const ArrowSchema* schema, const ArrowArray* array, qe_batch** out);
+/* Zero-copy view of a record batch already in HBM (device_type QE_ARROW_DEVICE_ROCM on the ctx
+ * device); waits on `sync_event` (a hipEvent_t*) when given. The buffers must outlive the view. */
+int qe_batch_import_device(qe_ctx* ctx, const ArrowSchema* schema, const ArrowDeviceArray* array,
+                           qe_batch** out);
+int qe_batch_destroy(qe_batch* batch);
+int qe_batch_num_columns(const qe_batch* batch, int32_t* ncols, int64_t* length);
+/* View of column i (valid while the batch lives); *name (may be NULL) is the field name. */
+int qe_batch_column(const qe_batch* batch, int32_t i, qe_column* out, const char** name);
+/* Device columns (equal lengths) -> host struct array + schema (all fields nullable, K:31).
+ * The consumer owns both and calls their release callbacks (Arrow C data interface rules). */
+int qe_batch_export(qe_ctx* ctx, const qe_column* cols, int32_t ncols, const char* const* names,
+                    ArrowSchema* out_schema, ArrowArray* out_array);
+
 #ifdef __cplusplus
 }
 #endif

@@ -203,6 +203,12 @@ SIGNATURES = [
     ("qe_strdict_encode", C.c_int, [_P, _COLP, _COLP]),
     ("qe_strdict_decode_bytes", C.c_int, [_P, _COLP, _I64P]),
     ("qe_strdict_decode", C.c_int, [_P, _COLP, _COLP]),
+    ("qe_batch_import", C.c_int, [_P, _P, _P, _PP]),
+    ("qe_batch_import_device", C.c_int, [_P, _P, _P, _PP]),
+    ("qe_batch_destroy", C.c_int, [_P]),
+    ("qe_batch_num_columns", C.c_int, [_P, C.POINTER(C.c_int32), _I64P]),
+    ("qe_batch_column", C.c_int, [_P, C.c_int32, _COLP, C.POINTER(C.c_char_p)]),
+    ("qe_batch_export", C.c_int, [_P, _COLP, C.c_int32, C.POINTER(C.c_char_p), _P, _P]),
 ]
 
 

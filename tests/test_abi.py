@@ -54,6 +54,9 @@ int main(void){
    sizeof(qe_fused_spec));
  printf("%zu %zu %zu %zu\n", offsetof(qe_fused_spec, terms), offsetof(qe_fused_spec, key_cols),
    offsetof(qe_fused_spec, inputs), offsetof(qe_global_agg, avg));
+ printf("%zu %zu %zu %zu %zu\n", sizeof(struct ArrowSchema), sizeof(struct ArrowArray),
+   sizeof(struct ArrowDeviceArray), offsetof(struct ArrowDeviceArray, device_type),
+   offsetof(struct ArrowDeviceArray, sync_event));
  return 0; }
 """
     with tempfile.TemporaryDirectory() as d:
@@ -68,6 +71,12 @@ int main(void){
                                            N.QePredTerm, N.QeToken, N.QeAggProgram, N.QeFusedSpec)]
     assert offs == [N.QeFusedSpec.terms.offset, N.QeFusedSpec.key_cols.offset, N.QeFusedSpec.inputs.offset,
                     N.QeGlobalAgg.avg.offset]
+    from kquery import arrow_io as A
+
+    arrow = [int(x) for x in out[2].split()]
+    assert arrow == [C.sizeof(A.ArrowSchemaC), C.sizeof(A.ArrowArrayC), C.sizeof(A.ArrowDeviceArrayC),
+                     A.ArrowDeviceArrayC.device_type.offset, A.ArrowDeviceArrayC.sync_event.offset]
+    assert arrow[:3] == [72, 80, 128]  # the Arrow C (device) data interface ABI
 
 
 def test_missing_library_fails_loudly(tmp_path):
