@@ -289,6 +289,25 @@ typedef struct qe_fused_spec {
 int qe_hashagg_update_fused(qe_hashagg* agg, const qe_column* cols, int32_t ncols,
                             const qe_fused_spec* spec);
 
+/* ---- fused SelectionExec -> ProjectionExec (ProjectionExec.execute K:589-594 over A5) ------
+ * One pass over `cols`: rows passing the mask/terms (null -> dropped) are written, in input
+ * order, as the value of each output program (same token language and null rules as the
+ * aggregate inputs; a lone column reference keeps its type, other programs give INT64 or
+ * FLOAT64). outs[k]: capacity >= cols[0].length rows, type = the program's type; validity
+ * written when non-NULL. *out_count = rows written (also each outs[k].length).
+ * Needs per-plan kernel specialisation: QE_ERR_UNSUPPORTED when it is off or the shape is
+ * outside the generator (callers then run qe_eval_cmp + qe_filter_apply + qe_eval_arith). */
+typedef struct qe_select_spec {
+  int32_t mask_col; /* BOOL column slot used as selection, or -1 */
+  int32_t nterms;
+  qe_pred_term terms[QE_MAX_TERMS];
+  int32_t nout;
+  int32_t reserved;
+  qe_agg_program outputs[QE_MAX_AGGS];
+} qe_select_spec;
+int qe_select_project(qe_ctx* ctx, const qe_column* cols, int32_t ncols, const qe_select_spec* spec,
+                      qe_column* outs, int64_t* out_count);
+
 /* Number of groups so far (synchronises). */
 int qe_hashagg_num_groups(qe_hashagg* agg, int64_t* out);
 /* Materialise the single output batch (K:635-650): key columns then one column per

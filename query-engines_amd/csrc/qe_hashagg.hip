@@ -1101,12 +1101,13 @@ static int ensure_defer(qe_hashagg* h, int64_t n) {
 }
 
 // Compiled launch description (host side mirror of qe_fused_spec after type checking).
-static int compile_plan(qe_hashagg* h, const qe_column* cols, int32_t ncols, const qe_fused_spec* spec, Plan* P) {
+// Columns, mask and predicate terms of a fused plan (shared with qe_selproj.hip).
+int compile_inputs(const qe_column* cols, int32_t ncols, int32_t mask_col, int32_t nterms, const qe_pred_term* terms,
+                   Plan* P, bool* col_f64) {
   *P = Plan{};
-  QE_CHECK(ncols >= 1 && ncols <= QE_MAX_COLS, QE_ERR_UNSUPPORTED, "fused aggregate takes 1..%d columns (got %d)",
+  QE_CHECK(ncols >= 1 && ncols <= QE_MAX_COLS, QE_ERR_UNSUPPORTED, "fused plan takes 1..%d columns (got %d)",
            QE_MAX_COLS, ncols);
   const int64_t n = cols[0].length;
-  bool col_f64[QE_MAX_COLS];
   for (int c = 0; c < ncols; ++c) {
     const qe_column& k = cols[c];
     QE_CHECK(k.length == n, QE_ERR_INVALID_ARG, "column %d has %lld rows, column 0 %lld", c, (long long)k.length,
@@ -1121,18 +1122,17 @@ static int compile_plan(qe_hashagg* h, const qe_column* cols, int32_t ncols, con
   P->all8 = 1;
   for (int c = 0; c < ncols; ++c) P->all8 &= (cols[c].type == QE_TYPE_INT64 || cols[c].type == QE_TYPE_FLOAT64) ? 1 : 0;
   P->n = n;
-  P->row_base = h->row_base;
   // mask
-  P->mask_col = spec->mask_col;
-  if (spec->mask_col >= 0) {
-    QE_CHECK(spec->mask_col < ncols && cols[spec->mask_col].type == QE_TYPE_BOOL, QE_ERR_INVALID_ARG,
+  P->mask_col = mask_col;
+  if (mask_col >= 0) {
+    QE_CHECK(mask_col < ncols && cols[mask_col].type == QE_TYPE_BOOL, QE_ERR_INVALID_ARG,
              "mask_col must name a BOOL column");
   }
   // predicate terms
-  QE_CHECK(spec->nterms >= 0 && spec->nterms <= QE_MAX_TERMS, QE_ERR_UNSUPPORTED, "too many predicate terms");
-  P->nterms = spec->nterms;
-  for (int i = 0; i < spec->nterms; ++i) {
-    const qe_pred_term& s = spec->terms[i];
+  QE_CHECK(nterms >= 0 && nterms <= QE_MAX_TERMS, QE_ERR_UNSUPPORTED, "too many predicate terms");
+  P->nterms = nterms;
+  for (int i = 0; i < nterms; ++i) {
+    const qe_pred_term& s = terms[i];
     DTerm& d = P->terms[i];
     QE_CHECK(s.col >= 0 && s.col < ncols && is_fixed(cols[s.col].type), QE_ERR_INVALID_ARG, "term %d: bad lhs column", i);
     QE_CHECK(s.op >= QE_OP_EQ && s.op <= QE_OP_GE, QE_ERR_INVALID_ARG, "term %d: bad comparison op", i);
@@ -1154,6 +1154,63 @@ static int compile_plan(qe_hashagg* h, const qe_column* cols, int32_t ncols, con
       d.lit = (d.f64 && !lf) ? f64_bits((double)s.lit.bits) : s.lit.bits;
     }
   }
+  return QE_OK;
+}
+
+// Type-checks postfix program `pg` and emits its typed tokens into a->tok / a->ntok.
+// *is_f: the result is fp64; *nullable: the result can be null (nullable column, null literal,
+// or int64 division, whose x / 0 is null).
+int compile_program(const qe_column* cols, int32_t ncols, const bool* col_f64, const qe_agg_program& pg, int j,
+                    DAgg* a, bool* is_f, bool* nullable) {
+  QE_CHECK(pg.ntokens >= 1 && pg.ntokens <= QE_MAX_TOKENS, QE_ERR_INVALID_ARG, "expression %d: empty program", j);
+  bool st_f[QE_MAX_TOKENS + 4];
+  int depth = 0, nt = 0;
+  *nullable = false;
+  auto emit = [&](int32_t op, int32_t arg, int64_t lit, int32_t lit_null, int32_t lit_f64 = 0) -> int {
+    QE_CHECK(nt < QE_MAX_TOKENS, QE_ERR_UNSUPPORTED, "expression %d: program too long after type promotion", j);
+    a->tok[nt++] = DTok{(short)op, (char)lit_null, (char)lit_f64, arg, lit};
+    return QE_OK;
+  };
+  for (int t = 0; t < pg.ntokens; ++t) {
+    const qe_token& tk = pg.tokens[t];
+    if (tk.op == QE_TOK_COL) {
+      QE_CHECK(tk.arg >= 0 && tk.arg < ncols && is_fixed(cols[tk.arg].type), QE_ERR_INVALID_ARG,
+               "expression %d: bad column slot %d", j, tk.arg);
+      QE_CHECK(depth < 4, QE_ERR_UNSUPPORTED, "expression %d: deeper than 4", j);
+      QE_TRY(emit(T_COL, tk.arg, 0, 0));
+      st_f[depth++] = col_f64[tk.arg];
+      *nullable = *nullable || cols[tk.arg].validity != nullptr;
+    } else if (tk.op == QE_TOK_LIT) {
+      QE_CHECK(tk.lit.type == QE_TYPE_INT64 || tk.lit.type == QE_TYPE_FLOAT64, QE_ERR_UNSUPPORTED,
+               "expression %d: literal type", j);
+      QE_CHECK(depth < 4, QE_ERR_UNSUPPORTED, "expression %d: deeper than 4", j);
+      QE_TRY(emit(T_LIT, 0, tk.lit.bits, tk.lit.is_null, tk.lit.type == QE_TYPE_FLOAT64 ? 1 : 0));
+      st_f[depth++] = tk.lit.type == QE_TYPE_FLOAT64;
+      *nullable = *nullable || tk.lit.is_null;
+    } else if (tk.op >= QE_TOK_ADD && tk.op <= QE_TOK_DIV) {
+      QE_CHECK(depth >= 2, QE_ERR_INVALID_ARG, "expression %d: stack underflow", j);
+      const bool f = st_f[depth - 1] || st_f[depth - 2];
+      if (f && !st_f[depth - 1]) QE_TRY(emit(T_I2F0, 0, 0, 0));
+      if (f && !st_f[depth - 2]) QE_TRY(emit(T_I2F1, 0, 0, 0));
+      const int32_t base_op = f ? T_ADD_F : T_ADD_I;
+      QE_TRY(emit(base_op + (tk.op - QE_TOK_ADD), 0, 0, 0));
+      if (!f && tk.op == QE_TOK_DIV) *nullable = true;  // x / 0 -> null
+      --depth;
+      st_f[depth - 1] = f;
+    } else {
+      return fail(QE_ERR_INVALID_ARG, "expression %d: bad token op %d", j, tk.op);
+    }
+  }
+  QE_CHECK(depth == 1, QE_ERR_INVALID_ARG, "expression %d: program leaves %d values", j, depth);
+  a->ntok = nt;
+  *is_f = st_f[0];
+  return QE_OK;
+}
+
+static int compile_plan(qe_hashagg* h, const qe_column* cols, int32_t ncols, const qe_fused_spec* spec, Plan* P) {
+  bool col_f64[QE_MAX_COLS];
+  QE_TRY(compile_inputs(cols, ncols, spec->mask_col, spec->nterms, spec->terms, P, col_f64));
+  P->row_base = h->row_base;
   // keys
   P->key_mode = h->km.mode;
   P->nkeys = h->nkeys;
@@ -1178,54 +1235,17 @@ static int compile_plan(qe_hashagg* h, const qe_column* cols, int32_t ncols, con
       a.pkind = 0;
       continue;
     }
-    const qe_agg_program& pg = spec->inputs[j];
-    QE_CHECK(pg.ntokens >= 1 && pg.ntokens <= QE_MAX_TOKENS, QE_ERR_INVALID_ARG, "aggregate %d: empty program", j);
-    // type-check the postfix program; emit typed tokens
-    bool st_f[QE_MAX_TOKENS + 4];
-    int depth = 0, nt = 0;
-    bool nullable = false;
-    auto emit = [&](int32_t op, int32_t arg, int64_t lit, int32_t lit_null, int32_t lit_f64 = 0) -> int {
-      QE_CHECK(nt < QE_MAX_TOKENS, QE_ERR_UNSUPPORTED, "aggregate %d: program too long after type promotion", j);
-      a.tok[nt++] = DTok{(short)op, (char)lit_null, (char)lit_f64, arg, lit};
-      return QE_OK;
-    };
-    for (int t = 0; t < pg.ntokens; ++t) {
-      const qe_token& tk = pg.tokens[t];
-      if (tk.op == QE_TOK_COL) {
-        QE_CHECK(tk.arg >= 0 && tk.arg < ncols && is_fixed(cols[tk.arg].type), QE_ERR_INVALID_ARG,
-                 "aggregate %d: bad column slot %d", j, tk.arg);
-        QE_CHECK(depth < 4, QE_ERR_UNSUPPORTED, "aggregate %d: expression deeper than 4", j);
-        QE_TRY(emit(T_COL, tk.arg, 0, 0));
-        st_f[depth++] = col_f64[tk.arg];
-        nullable = nullable || cols[tk.arg].validity != nullptr;
-      } else if (tk.op == QE_TOK_LIT) {
-        QE_CHECK(tk.lit.type == QE_TYPE_INT64 || tk.lit.type == QE_TYPE_FLOAT64, QE_ERR_UNSUPPORTED,
-                 "aggregate %d: literal type", j);
-        QE_CHECK(depth < 4, QE_ERR_UNSUPPORTED, "aggregate %d: expression deeper than 4", j);
-        QE_TRY(emit(T_LIT, 0, tk.lit.bits, tk.lit.is_null, tk.lit.type == QE_TYPE_FLOAT64 ? 1 : 0));
-        st_f[depth++] = tk.lit.type == QE_TYPE_FLOAT64;
-        nullable = nullable || tk.lit.is_null;
-      } else if (tk.op >= QE_TOK_ADD && tk.op <= QE_TOK_DIV) {
-        QE_CHECK(depth >= 2, QE_ERR_INVALID_ARG, "aggregate %d: stack underflow", j);
-        const bool f = st_f[depth - 1] || st_f[depth - 2];
-        if (f && !st_f[depth - 1]) QE_TRY(emit(T_I2F0, 0, 0, 0));
-        if (f && !st_f[depth - 2]) QE_TRY(emit(T_I2F1, 0, 0, 0));
-        const int32_t base_op = f ? T_ADD_F : T_ADD_I;
-        QE_TRY(emit(base_op + (tk.op - QE_TOK_ADD), 0, 0, 0));
-        if (!f && tk.op == QE_TOK_DIV) nullable = true;  // x / 0 -> null
-        --depth;
-        st_f[depth - 1] = f;
-      } else {
-        return fail(QE_ERR_INVALID_ARG, "aggregate %d: bad token op %d", j, tk.op);
-      }
-    }
-    QE_CHECK(depth == 1, QE_ERR_INVALID_ARG, "aggregate %d: program leaves %d values", j, depth);
+    bool is_f = false, nullable = false;
+    QE_TRY(compile_program(cols, ncols, col_f64, spec->inputs[j], j, &a, &is_f, &nullable));
+    int nt = a.ntok;
     const bool want_f = h->aggs[j].fn == QE_AGG_AVG || h->aggs[j].input_type == QE_TYPE_FLOAT64;
-    const bool is_f = st_f[0];
     if (a.fn != QE_AGG_COUNT) {
       QE_CHECK(!(is_f && !want_f), QE_ERR_INVALID_ARG,
                "aggregate %d: fp64 input for an int64 aggregate (declare input_type FLOAT64)", j);
-      if (want_f && !is_f) QE_TRY(emit(T_I2F0, 0, 0, 0));
+      if (want_f && !is_f) {
+        QE_CHECK(nt < QE_MAX_TOKENS, QE_ERR_UNSUPPORTED, "aggregate %d: program too long after type promotion", j);
+        a.tok[nt++] = DTok{(short)T_I2F0, 0, 0, 0, 0};
+      }
     }
     a.ntok = nt;
     a.track_nn = nullable ? 1 : 0;

@@ -54,8 +54,16 @@ int ctx_pinned(qe_ctx* ctx, size_t bytes, void** out);        // grow-only pinne
 int launch_check(const char* what);                           // hipGetLastError wrapper
 // Per-plan kernel specialisation (qe_jit.hip).
 bool gen_fused_source(const qe::Plan& P, int log2, std::string* src, size_t* lds_bytes);
-int jit_kernel(qe_ctx* ctx, const std::string& src, hipFunction_t* fn, int* blocks_per_cu);
-int jit_launch(qe_ctx* ctx, hipFunction_t fn, int grid, const qe::Plan& P);
+int jit_kernel(qe_ctx* ctx, const std::string& src, hipFunction_t* fn, int* blocks_per_cu,
+               const char* name = "qe_fused", int block = 512);
+int jit_launch(qe_ctx* ctx, hipFunction_t fn, int grid, const qe::Plan& P, int block = 512);
+// Fused-plan compilation shared by the aggregate and select-project paths (qe_hashagg.hip).
+int compile_inputs(const qe_column* cols, int32_t ncols, int32_t mask_col, int32_t nterms, const qe_pred_term* terms,
+                   qe::Plan* P, bool* col_f64);
+int compile_program(const qe_column* cols, int32_t ncols, const bool* col_f64, const qe_agg_program& pg, int j,
+                    qe::DAgg* a, bool* is_f, bool* nullable);
+// Select-project kernel source (qe_jit.hip): R rows per thread, 256 threads.
+bool gen_selproj_source(const qe::Plan& P, const int32_t* out_kind, int nout, std::string* src);
 // Exclusive scan of n int64 on the ctx stream (one block); out[n] = total. (qe_filter.hip)
 int exclusive_scan_i64(qe_ctx* ctx, const int64_t* in, int64_t* out, int64_t n);
 

@@ -122,6 +122,32 @@ std::string acc_init(int acc) {
   }
 }
 
+// Mask column and predicate terms: clears bit r of `act` for rows r in [0, rows) that fail.
+void emit_predicate(const Plan& P, std::ostringstream& o, int rows) {
+  const std::string loop = "#pragma unroll\n    for (int r = 0; r < " + std::to_string(rows) + "; ++r) ";
+  if (P.mask_col >= 0) {
+    o << loop << "if (!((qu32)(" << col_raw(P.mask_col) << " & 1) & " << col_ok(P, P.mask_col)
+      << ")) act &= ~(1u << r);\n";
+  }
+  for (int t = 0; t < P.nterms; ++t) {
+    const DTerm& T = P.terms[t];
+    const std::string lit = "P.terms[" + std::to_string(t) + "].lit";
+    std::string lhs, rhs, ok = col_ok(P, T.lhs);
+    if (T.f64) {
+      lhs = col_is_f(P, T.lhs) ? col_val(P, T.lhs) : "((double)" + col_raw(T.lhs) + ")";
+      if (T.rhs >= 0) rhs = col_is_f(P, T.rhs) ? col_val(P, T.rhs) : "((double)" + col_raw(T.rhs) + ")";
+      else rhs = "bits_f64(" + lit + ")";
+    } else {
+      lhs = col_raw(T.lhs);
+      rhs = T.rhs >= 0 ? col_raw(T.rhs) : lit;
+    }
+    if (T.rhs >= 0) ok += " & " + col_ok(P, T.rhs);
+    else if (T.lit_null) ok = "0u";
+    o << loop << "if (!((" << lhs << ") " << cmp_sym(T.op) << " (" << rhs << ")) || !(" << ok
+      << ")) act &= ~(1u << r);\n";
+  }
+}
+
 }  // namespace
 
 // Returns false when the plan shape is outside what the generator emits (caller uses the
@@ -207,27 +233,7 @@ bool gen_fused_source(const Plan& P, int log2, std::string* src, size_t* lds_byt
     << "    if (!full) { act = 0; for (int r = 0; r < 4; ++r) act |= (qu32)(r0 + 128 * (r >> 1) + (r & 1) < P.n) << r; }\n"
     << "    if (P.defer_in) {\n      for (int r = 0; r < 4; ++r) { const qi64 row = r0 + 128 * (r >> 1) + (r & 1);\n"
     << "        if (row < P.n && !((P.defer_in[row >> 5] >> (row & 31)) & 1)) act &= ~(1u << r); }\n    }\n";
-  if (P.mask_col >= 0) {
-    o << "#pragma unroll\n    for (int r = 0; r < 4; ++r) if (!((qu32)(" << col_raw(P.mask_col) << " & 1) & "
-      << col_ok(P, P.mask_col) << ")) act &= ~(1u << r);\n";
-  }
-  for (int t = 0; t < P.nterms; ++t) {
-    const DTerm& T = P.terms[t];
-    const std::string lit = "P.terms[" + std::to_string(t) + "].lit";
-    std::string lhs, rhs, ok = col_ok(P, T.lhs);
-    if (T.f64) {
-      lhs = col_is_f(P, T.lhs) ? col_val(P, T.lhs) : "((double)" + col_raw(T.lhs) + ")";
-      if (T.rhs >= 0) rhs = col_is_f(P, T.rhs) ? col_val(P, T.rhs) : "((double)" + col_raw(T.rhs) + ")";
-      else rhs = "bits_f64(" + lit + ")";
-    } else {
-      lhs = col_raw(T.lhs);
-      rhs = T.rhs >= 0 ? col_raw(T.rhs) : lit;
-    }
-    if (T.rhs >= 0) ok += " & " + col_ok(P, T.rhs);
-    else if (T.lit_null) ok = "0u";
-    o << "#pragma unroll\n    for (int r = 0; r < 4; ++r) if (!((" << lhs << ") " << cmp_sym(T.op) << " (" << rhs
-      << ")) || !(" << ok << ")) act &= ~(1u << r);\n";
-  }
+  emit_predicate(P, o, 4);
   o << "    if (act == 0) continue;\n";
   // ---- keys
   o << "    qi64 key[4] = {0, 0, 0, 0};\n    qu32 knull = 0;\n";
@@ -333,6 +339,116 @@ bool gen_fused_source(const Plan& P, int log2, std::string* src, size_t* lds_byt
   return true;
 }
 
+// Fused SelectionExec -> ProjectionExec (qe_selproj.hip): one pass, order-preserving.
+// Tile = 256 threads x R stripes of 256 consecutive rows (row = base + r*256 + thread, so loads
+// are coalesced and (stripe, wave) chunks are in row order). Per tile: predicate -> ballots ->
+// per-(stripe, wave) counts -> wave-0 exclusive scan -> decoupled look-back over the previous
+// tiles' status words (flag in bits 62-63: 1 aggregate, 2 inclusive prefix) -> each selected row
+// evaluates the projection programs and stores at its global position. Tile ids come from an
+// atomic counter, so every predecessor of a waiting tile is already running.
+// Pointers ride in the Plan's table fields: t.acc[k] output k values, t.nn[k] output k validity
+// words (nullable outputs only), t.keys tile status, t.ctl[0] tile counter, t.ctl[1] total,
+// t.cap number of tiles. out_kind[k] = byte width (8, 4, 1) | 0x100 if the output is nullable.
+bool gen_selproj_source(const Plan& P, const int32_t* out_kind, int nout, std::string* src) {
+  if (P.ncols < 1 || P.ncols > QE_MAX_COLS || nout < 1 || nout > QE_MAX_AGGS) return false;
+  const int R = P.ncols <= 3 ? 16 : (P.ncols <= 6 ? 8 : 4);
+  std::ostringstream o;
+  o << "\nusing namespace qe;\n"
+    << "extern \"C\" __global__ void __launch_bounds__(256) qe_selproj(const Plan P) {\n"
+    << "  constexpr int R = " << R << ";\n"
+    << "  constexpr qu64 F_AGG = 1ull << 62, F_INC = 2ull << 62, VMASK = (1ull << 62) - 1;\n"
+    << "  __shared__ qu32 s_cnt[R * 4];\n  __shared__ qu64 s_base;\n  __shared__ qu32 s_tile;\n"
+    << "  const int t = threadIdx.x, lane = t & 63, w = t >> 6;\n"
+    << "  if (t == 0) s_tile = (qu32)atomicAdd((unsigned long long*)&P.t.ctl[0], 1ull);\n"
+    << "  __syncthreads();\n"
+    << "  const qu32 tile = s_tile;\n"
+    << "  const qi64 base = (qi64)tile * (R * 256);\n"
+    << "  const bool full = base + R * 256 <= P.n;\n";
+  for (int c = 0; c < P.ncols; ++c) {
+    const std::string cs = std::to_string(c);
+    const int kind = P.cols[c].kind;
+    const char* ty = kind == K_I32 ? "qi32" : (kind == K_U8 || kind == K_BOOL) ? "qu8" : "qi64";
+    o << "  qi64 c" << cs << "[R];\n  {\n    const " << ty << "* p = (const " << ty << "*)P.cols[" << cs << "].p;\n"
+      << "#pragma unroll\n    for (int r = 0; r < R; ++r) {\n      const qi64 row = base + r * 256 + t;\n";
+    if (kind == K_BOOL)
+      o << "      c" << cs << "[r] = (full || row < P.n) ? ((p[row >> 3] >> (row & 7)) & 1) : 0;\n";
+    else
+      o << "      c" << cs << "[r] = (full || row < P.n) ? (qi64)p[row] : 0;\n";
+    o << "    }\n  }\n";
+    if (P.cols[c].valid) {
+      o << "  qu32 v" << cs << " = 0;\n  {\n    const qu8* vb = P.cols[" << cs << "].valid;\n"
+        << "#pragma unroll\n    for (int r = 0; r < R; ++r) {\n      const qi64 row = base + r * 256 + t;\n"
+        << "      if (full || row < P.n) v" << cs << " |= (qu32)((vb[row >> 3] >> (row & 7)) & 1) << r;\n    }\n  }\n";
+    }
+  }
+  o << "  qu32 act = 0;\n"
+    << "#pragma unroll\n  for (int r = 0; r < R; ++r) act |= (qu32)(full || base + r * 256 + t < P.n) << r;\n";
+  {
+    std::ostringstream q;
+    emit_predicate(P, q, 16);  // emits with a fixed trip count; R <= 16 and bits >= R are clear
+    std::string body = q.str();
+    const std::string from = "r < 16;", to = "r < R;";
+    for (size_t k = body.find(from); k != std::string::npos; k = body.find(from, k)) body.replace(k, from.size(), to);
+    o << body;
+  }
+  o << "  qu64 bal[R];\n"
+    << "#pragma unroll\n  for (int r = 0; r < R; ++r) bal[r] = __ballot((act >> r) & 1u);\n"
+    << "  if (lane == 0) {\n#pragma unroll\n    for (int r = 0; r < R; ++r) s_cnt[r * 4 + w] = (qu32)__popcll(bal[r]);\n  }\n"
+    << "  __syncthreads();\n"
+    << "  if (w == 0) {\n"
+    << "    const qu32 x = lane < R * 4 ? s_cnt[lane] : 0u;\n"
+    << "    qu32 inc = x;\n"
+    << "#pragma unroll\n    for (int d = 1; d < 64; d <<= 1) { const qu32 y = __shfl_up(inc, d); if (lane >= d) inc += y; }\n"
+    << "    const qu64 total = (qu64)__shfl(inc, 63);\n"
+    << "    if (lane < R * 4) s_cnt[lane] = inc - x;\n"
+    << "    qu64* st = (qu64*)P.t.keys;\n"
+    << "    if (lane == 0) __hip_atomic_store(&st[tile], (tile == 0 ? F_INC : F_AGG) | total, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);\n"
+    << "    qu64 excl = 0;\n"
+    << "    if (tile > 0) {\n"
+    << "      qi64 pos = (qi64)tile - 1;\n"
+    << "      for (;;) {\n"
+    << "        const qi64 idx = pos - lane;\n"
+    << "        qu64 v;\n"
+    << "        do { v = idx >= 0 ? __hip_atomic_load(&st[idx], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : F_INC; }\n"
+    << "        while (__any((v >> 62) == 0));\n"
+    << "        const qu64 incm = __ballot((v >> 62) == 2);\n"
+    << "        qu64 c = v & VMASK;\n"
+    << "        if (incm) { const int first = __ffsll((long long)incm) - 1; if (lane > first) c = 0; }\n"
+    << "#pragma unroll\n        for (int d = 32; d >= 1; d >>= 1) c += __shfl_xor(c, d);\n"
+    << "        excl += c;\n"
+    << "        if (incm) break;\n"
+    << "        pos -= 64;\n"
+    << "      }\n"
+    << "      if (lane == 0) __hip_atomic_store(&st[tile], F_INC | (excl + total), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);\n"
+    << "    }\n"
+    << "    if (lane == 0) {\n      s_base = excl;\n"
+    << "      if ((qu64)tile == P.t.cap - 1) __hip_atomic_store(&P.t.ctl[1], excl + total, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);\n    }\n"
+    << "  }\n  __syncthreads();\n"
+    << "  const qu64 tb = s_base;\n"
+    << "  const qu64 below = (1ull << lane) - 1;\n"
+    << "#pragma unroll\n  for (int r = 0; r < R; ++r) {\n"
+    << "    if (!((act >> r) & 1u)) continue;\n"
+    << "    const qu64 pos = tb + s_cnt[r * 4 + w] + (qu64)__popcll(bal[r] & below);\n";
+  for (int k = 0; k < nout; ++k) {
+    Expr e;
+    if (!agg_expr(P, k, &e)) return false;
+    const std::string ks = std::to_string(k);
+    const int width = out_kind[k] & 0xFF;
+    const bool nullable = (out_kind[k] & 0x100) != 0;
+    o << "    {\n      const qi64 x = " << e.v << ";\n";
+    if (width == 8) o << "      ((qi64*)P.t.acc[" << ks << "])[pos] = x;\n";
+    else if (width == 4) o << "      ((qi32*)P.t.acc[" << ks << "])[pos] = (qi32)x;\n";
+    else if (width == 1) o << "      ((qu8*)P.t.acc[" << ks << "])[pos] = (qu8)x;\n";
+    else return false;
+    if (nullable)
+      o << "      if (" << e.ok << ") atomicOr(&((qu32*)P.t.nn[" << ks << "])[pos >> 5], 1u << (pos & 31));\n";
+    o << "    }\n";
+  }
+  o << "  }\n}\n";
+  *src = std::string(kDevHeader) + o.str();
+  return true;
+}
+
 // ---- hipRTC compile + cache ------------------------------------------------------------------------------
 namespace {
 
@@ -384,7 +500,7 @@ void write_file(const std::string& path, const std::vector<char>& data) {
 }  // namespace
 
 // Compiled kernel for `src` on the ctx's device (compiling / loading it on first use).
-int jit_kernel(qe_ctx* ctx, const std::string& src, hipFunction_t* fn, int* blocks_per_cu) {
+int jit_kernel(qe_ctx* ctx, const std::string& src, hipFunction_t* fn, int* blocks_per_cu, const char* kname, int block) {
   std::lock_guard<std::mutex> lk(g_mu);
   const auto key = std::make_pair(ctx->device, src);
   auto it = g_cache.find(key);
@@ -397,9 +513,10 @@ int jit_kernel(qe_ctx* ctx, const std::string& src, hipFunction_t* fn, int* bloc
   QE_HIP(hipGetDeviceProperties(&prop, ctx->device));
   std::string arch = prop.gcnArchName;
   const std::string opt_arch = "--offload-arch=" + arch;
-  const char* opts[] = {opt_arch.c_str(), "-O3", "-munsafe-fp-atomics", "-std=c++17"};
+  // no FMA contraction: a*b+c rounds twice, as the reference (JVM) arithmetic does
+  const char* opts[] = {opt_arch.c_str(), "-O3", "-ffp-contract=off", "-munsafe-fp-atomics", "-std=c++17"};
   char name[64];
-  snprintf(name, sizeof(name), "%016llx", (unsigned long long)fnv1a(src + arch));
+  snprintf(name, sizeof(name), "%016llx", (unsigned long long)fnv1a(src + arch + " -O3 -ffp-contract=off -munsafe-fp-atomics"));
   const std::string dir = cache_dir();
   const std::string path = dir + "/" + name + ".co";
   std::vector<char> code;
@@ -407,7 +524,7 @@ int jit_kernel(qe_ctx* ctx, const std::string& src, hipFunction_t* fn, int* bloc
     hiprtcProgram prog;
     if (hiprtcCreateProgram(&prog, src.c_str(), "qe_fused.hip", 0, nullptr, nullptr) != HIPRTC_SUCCESS)
       return fail(QE_ERR_DEVICE, "hiprtcCreateProgram failed");
-    const hiprtcResult r = hiprtcCompileProgram(prog, 4, opts);
+    const hiprtcResult r = hiprtcCompileProgram(prog, (int)(sizeof(opts) / sizeof(opts[0])), opts);
     if (r != HIPRTC_SUCCESS) {
       size_t ls = 0;
       hiprtcGetProgramLogSize(prog, &ls);
@@ -426,9 +543,9 @@ int jit_kernel(qe_ctx* ctx, const std::string& src, hipFunction_t* fn, int* bloc
   }
   Entry e;
   QE_HIP(hipModuleLoadData(&e.mod, code.data()));
-  QE_HIP(hipModuleGetFunction(&e.fn, e.mod, "qe_fused"));
+  QE_HIP(hipModuleGetFunction(&e.fn, e.mod, kname));
   int nb = 0;
-  QE_HIP(hipModuleOccupancyMaxActiveBlocksPerMultiprocessor(&nb, e.fn, 512, 0));
+  QE_HIP(hipModuleOccupancyMaxActiveBlocksPerMultiprocessor(&nb, e.fn, block, 0));
   e.blocks_per_cu = nb > 0 ? nb : 1;
   g_cache[key] = e;
   *fn = e.fn;
@@ -436,11 +553,11 @@ int jit_kernel(qe_ctx* ctx, const std::string& src, hipFunction_t* fn, int* bloc
   return QE_OK;
 }
 
-int jit_launch(qe_ctx* ctx, hipFunction_t fn, int grid, const Plan& P) {
+int jit_launch(qe_ctx* ctx, hipFunction_t fn, int grid, const Plan& P, int block) {
   Plan arg = P;
   size_t sz = sizeof(Plan);
   void* cfg[] = {HIP_LAUNCH_PARAM_BUFFER_POINTER, &arg, HIP_LAUNCH_PARAM_BUFFER_SIZE, &sz, HIP_LAUNCH_PARAM_END};
-  QE_HIP(hipModuleLaunchKernel(fn, grid, 1, 1, 512, 1, 1, 0, ctx->stream, nullptr, cfg));
+  QE_HIP(hipModuleLaunchKernel(fn, grid, 1, 1, block, 1, 1, 0, ctx->stream, nullptr, cfg));
   return QE_OK;
 }
 

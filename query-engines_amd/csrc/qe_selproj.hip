@@ -1,0 +1,87 @@
+// Fused SelectionExec -> ProjectionExec: ProjectionExec.execute (Main.kt:589-594) over the
+// build-defined SelectionExec, in ONE pass over the scanned columns. The
+// per-family chain (qe_eval_cmp -> qe_filter_count -> qe_filter_apply -> qe_eval_arith) writes
+// and re-reads a mask, the compacted inputs and synchronises the host between kernels; this
+// kernel reads each input once and writes only the projected rows (HBM roofline: read
+// ncols*width + write selected*out_width bytes per row).
+//
+// The kernel is generated per plan shape and compiled with hipRTC (qe_jit.hip gen_selproj_source);
+// without hipRTC the call returns QE_ERR_UNSUPPORTED and callers run the per-family operators.
+#include "qe_internal.hpp"
+
+using namespace qe;
+
+namespace {
+
+// Output column type a program produces: a lone column reference keeps the column's type;
+// anything else is INT64 or FLOAT64 by promotion.
+int32_t program_type(const qe_column* cols, const DAgg& a, bool is_f) {
+  if (a.ntok == 1 && a.tok[0].op == T_COL) return cols[a.tok[0].arg].type;
+  return is_f ? QE_TYPE_FLOAT64 : QE_TYPE_INT64;
+}
+
+}  // namespace
+
+extern "C" int qe_select_project(qe_ctx* ctx, const qe_column* cols, int32_t ncols, const qe_select_spec* spec,
+                                 qe_column* outs, int64_t* out_count) {
+  QE_TRY(ctx_enter(ctx));
+  QE_CHECK(cols && spec && outs && out_count, QE_ERR_INVALID_ARG, "null argument");
+  QE_CHECK(spec->nout >= 1 && spec->nout <= QE_MAX_AGGS, QE_ERR_UNSUPPORTED, "select-project takes 1..%d outputs",
+           QE_MAX_AGGS);
+  Plan P;
+  bool col_f64[QE_MAX_COLS];
+  QE_TRY(compile_inputs(cols, ncols, spec->mask_col, spec->nterms, spec->terms, &P, col_f64));
+  const int64_t n = P.n;
+  int32_t out_kind[QE_MAX_AGGS];
+  bool nullable[QE_MAX_AGGS];
+  P.naggs = spec->nout;
+  for (int k = 0; k < spec->nout; ++k) {
+    bool is_f = false;
+    DAgg& a = P.aggs[k];
+    QE_TRY(compile_program(cols, ncols, col_f64, spec->outputs[k], k, &a, &is_f, &nullable[k]));
+    const int32_t t = program_type(cols, a, is_f);
+    QE_CHECK(t != QE_TYPE_BOOL, QE_ERR_UNSUPPORTED, "output %d: BOOL pass-through is not fused", k);
+    QE_CHECK(outs[k].type == t, QE_ERR_INVALID_ARG, "output %d: column type %d, expression yields %d", k, outs[k].type,
+             t);
+    QE_CHECK(outs[k].length >= n && (outs[k].values || n == 0), QE_ERR_CAPACITY,
+             "output %d: capacity %lld rows, input has %lld", k, (long long)outs[k].length, (long long)n);
+    out_kind[k] = type_width(t) | ((nullable[k] && outs[k].validity) ? 0x100 : 0);
+    P.t.acc[k] = (qi64*)outs[k].values;
+    P.t.nn[k] = (qu64*)outs[k].validity;
+  }
+  if (!ctx->jit) return fail(QE_ERR_UNSUPPORTED, "fused select-project needs kernel specialisation (jit is off)");
+  std::string src;
+  if (!gen_selproj_source(P, out_kind, spec->nout, &src))
+    return fail(QE_ERR_UNSUPPORTED, "plan shape is outside the select-project generator");
+  hipFunction_t fn;
+  int bpc = 0;
+  QE_TRY(jit_kernel(ctx, src, &fn, &bpc, "qe_selproj", 256));
+  // validity: nullable outputs start all-null (the kernel sets bits); others all-valid
+  for (int k = 0; k < spec->nout; ++k) {
+    if (!outs[k].validity) continue;
+    const size_t vb = (size_t)div_up((uint64_t)(n > 0 ? n : 1), 32) * 4;
+    QE_HIP(hipMemsetAsync(outs[k].validity, (out_kind[k] & 0x100) ? 0 : 0xFF, vb, ctx->stream));
+  }
+  *out_count = 0;
+  if (n > 0) {
+    const int R = P.ncols <= 3 ? 16 : (P.ncols <= 6 ? 8 : 4);  // gen_selproj_source's stripes per thread
+    const int64_t tiles = (int64_t)div_up((uint64_t)n, (uint64_t)R * 256);
+    QE_CHECK(tiles < (1ll << 31), QE_ERR_CAPACITY, "too many rows for one select-project call");
+    void* s;
+    QE_TRY(ctx_scratch(ctx, (size_t)(tiles + 2) * 8, &s));
+    qu64* ctl = (qu64*)s;
+    QE_HIP(hipMemsetAsync(s, 0, (size_t)(tiles + 2) * 8, ctx->stream));
+    P.t.ctl = ctl;
+    P.t.keys = (qi64*)(ctl + 2);
+    P.t.cap = (qu64)tiles;
+    QE_TRY(jit_launch(ctx, fn, (int)tiles, P, 256));
+    QE_TRY(launch_check("qe_selproj"));
+    void* pin;
+    QE_TRY(ctx_pinned(ctx, 8, &pin));
+    QE_HIP(hipMemcpyAsync(pin, ctl + 1, 8, hipMemcpyDeviceToHost, ctx->stream));
+    QE_HIP(hipStreamSynchronize(ctx->stream));
+    *out_count = *(int64_t*)pin;
+  }
+  for (int k = 0; k < spec->nout; ++k) outs[k].length = *out_count;
+  return QE_OK;
+}

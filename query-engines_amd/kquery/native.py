@@ -151,6 +151,17 @@ class QeFusedSpec(C.Structure):
     ]
 
 
+class QeSelectSpec(C.Structure):
+    _fields_ = [
+        ("mask_col", C.c_int32),
+        ("nterms", C.c_int32),
+        ("terms", QePredTerm * MAX_TERMS),
+        ("nout", C.c_int32),
+        ("reserved", C.c_int32),
+        ("outputs", QeAggProgram * MAX_AGGS),
+    ]
+
+
 # ---- library ------------------------------------------------------------------------------------
 _lib = None
 
@@ -203,6 +214,7 @@ SIGNATURES = [
     ("qe_strdict_encode", C.c_int, [_P, _COLP, _COLP]),
     ("qe_strdict_decode_bytes", C.c_int, [_P, _COLP, _I64P]),
     ("qe_strdict_decode", C.c_int, [_P, _COLP, _COLP]),
+    ("qe_select_project", C.c_int, [_P, _COLP, C.c_int32, C.POINTER(QeSelectSpec), _COLP, _I64P]),
     ("qe_batch_import", C.c_int, [_P, _P, _P, _PP]),
     ("qe_batch_import_device", C.c_int, [_P, _P, _P, _PP]),
     ("qe_batch_destroy", C.c_int, [_P]),

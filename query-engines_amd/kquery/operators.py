@@ -248,6 +248,84 @@ class FusedHashAggregateExec(PhysicalPlan):
         return f"FusedHashAggregateExec: slots={self.slots}, aggrExpr={self.aggregateExpr}"
 
 
+class FusedSelectProjectExec(PhysicalPlan):
+    """SelectionExec -> ProjectionExec (or a bare SelectionExec) in ONE pass over the scanned
+    columns (qe_select_project): order-preserving, same rows and values as the unfused chain.
+    Falls back to the unfused operators when the kernel cannot take the plan."""
+
+    def __init__(self, scan: PhysicalPlan, slots: Sequence[int], spec: N.QeSelectSpec, out_types: Sequence[int],
+                 schema: Schema, unfused: PhysicalPlan):
+        self.scan = scan
+        self.slots = list(slots)
+        self.spec = spec
+        self.out_types = list(out_types)
+        self._schema = schema
+        self.unfused = unfused
+        self.last_kernel_rows = 0
+
+    def schema(self) -> Schema:
+        return self._schema
+
+    def children(self) -> List[PhysicalPlan]:
+        return [self.scan]
+
+    def run_batch(self, batch: RecordBatch) -> Optional[RecordBatch]:
+        cols = [batch.field(i) for i in self.slots]
+        ctx = cols[0].ctx
+        n = cols[0].length
+        outs = [DeviceColumn.empty(t, n, True, ctx=ctx) for t in self.out_types]
+        cc = (N.QeColumn * len(cols))(*[c.as_c() for c in cols])
+        oc = (N.QeColumn * len(outs))(*[o.as_c() for o in outs])
+        cnt = N.C.c_int64()
+        st = N.lib().qe_select_project(ctx.handle, cc, len(cols), N.C.byref(self.spec), oc, N.C.byref(cnt))
+        if st == N.QE_ERR_UNSUPPORTED:
+            return None
+        N.check(st)
+        for o in outs:
+            o.length = cnt.value
+        return RecordBatch(self._schema, outs)
+
+    def execute(self) -> Iterator[RecordBatch]:
+        for batch in self.scan.execute():
+            out = self.run_batch(batch)
+            if out is None:  # kernel specialisation unavailable: per-family operators
+                yield from _replay(self.unfused, batch)
+            else:
+                yield out
+
+    def __repr__(self) -> str:
+        return f"FusedSelectProjectExec: slots={self.slots}, outputs={self.out_types}"
+
+
+class _OneBatch(PhysicalPlan):
+    def __init__(self, batch: RecordBatch):
+        self.batch = batch
+
+    def execute(self) -> Iterator[RecordBatch]:
+        yield self.batch
+
+
+def _replay(plan: PhysicalPlan, batch: RecordBatch) -> Iterator[RecordBatch]:
+    """Runs the unfused Projection/Selection chain of ``plan`` over one scanned batch."""
+    if isinstance(plan, ProjectionExec):
+        return ProjectionExec(_ReplayInput(plan.input, batch), plan.schema(), plan.expr).execute()
+    if isinstance(plan, SelectionExec):
+        return SelectionExec(_ReplayInput(plan.input, batch), plan.expr).execute()
+    return iter([batch])
+
+
+class _ReplayInput(PhysicalPlan):
+    def __init__(self, plan: PhysicalPlan, batch: RecordBatch):
+        self.plan = plan
+        self.batch = batch
+
+    def schema(self) -> Schema:
+        return self.plan.schema()
+
+    def execute(self) -> Iterator[RecordBatch]:
+        return _replay(self.plan, self.batch)
+
+
 class _NotFusable(Exception):
     pass
 
@@ -320,6 +398,8 @@ def fuse(plan: PhysicalPlan) -> PhysicalPlan:
     """Rewrite HashAggregateExec over [ProjectionExec] over [SelectionExec] over ScanExec into a
     FusedHashAggregateExec when every expression is expressible in the fused kernel; otherwise
     return ``plan`` unchanged (the per-family operators then run)."""
+    if isinstance(plan, (ProjectionExec, SelectionExec)):
+        return _fuse_select_project(plan)
     if not isinstance(plan, HashAggregateExec):
         return plan
     try:
@@ -385,6 +465,76 @@ def fuse(plan: PhysicalPlan) -> PhysicalPlan:
             raise _NotFusable("no input columns")
         return FusedHashAggregateExec(node, sm.slots, spec, key_types, aggs, plan.schema(), plan.groupExpr,
                                       plan.aggregateExpr, plan.expected_groups)
+    except _NotFusable:
+        return plan
+
+
+def _terms_into(pred: Optional[Expression], sm: "_SlotMap", terms, max_terms: int) -> int:
+    conj = _conjuncts(pred) if pred is not None else []
+    if len(conj) > max_terms:
+        raise _NotFusable("too many predicate terms")
+    for i, t in enumerate(conj):
+        if not isinstance(t, ComparisonExpression) or not isinstance(t.l, ColumnExpression):
+            raise _NotFusable("predicate term")
+        if sm.type_of(t.l.i) not in N.FIXED_WIDTH:
+            raise _NotFusable("predicate on non fixed-width column")
+        pt = terms[i]
+        pt.col = sm.slot(t.l.i)
+        pt.op = t.op
+        if isinstance(t.r, ColumnExpression):
+            if sm.type_of(t.r.i) not in N.FIXED_WIDTH:
+                raise _NotFusable("predicate on non fixed-width column")
+            pt.rhs_col = sm.slot(t.r.i)
+        else:
+            lit = _literal(t.r)
+            if lit is None:
+                raise _NotFusable("predicate rhs")
+            pt.rhs_col = -1
+            pt.lit = lit
+    return len(conj)
+
+
+def _fuse_select_project(plan: PhysicalPlan) -> PhysicalPlan:
+    """ProjectionExec(SelectionExec(ScanExec)), SelectionExec(ScanExec) or
+    ProjectionExec(ScanExec) -> FusedSelectProjectExec; anything else unchanged."""
+    try:
+        node = plan
+        proj = None
+        if isinstance(node, ProjectionExec):
+            proj = node.expr
+            node = node.input
+        pred = None
+        if isinstance(node, SelectionExec):
+            pred = node.expr
+            node = node.input
+        if not isinstance(node, ScanExec) or (proj is None and pred is None):
+            raise _NotFusable("not a selection/projection over a scan")
+        sm = _SlotMap(node.schema())
+        spec = N.QeSelectSpec()
+        spec.mask_col = -1
+        spec.nterms = _terms_into(pred, sm, spec.terms, N.MAX_TERMS)
+        exprs = proj if proj is not None else [ColumnExpression(i) for i in range(len(node.schema().fields))]
+        if len(exprs) > N.MAX_AGGS:
+            raise _NotFusable("too many outputs")
+        out_types = []
+        for k, e in enumerate(exprs):
+            toks: list = []
+            is_f = _program(e, sm, toks)
+            if len(toks) > N.MAX_TOKENS:
+                raise _NotFusable("expression too long")
+            spec.outputs[k].ntokens = len(toks)
+            for t, tok in enumerate(toks):
+                spec.outputs[k].tokens[t] = tok
+            if isinstance(e, ColumnExpression):
+                if sm.type_of(e.i) == N.TYPE_BOOL:
+                    raise _NotFusable("BOOL pass-through")
+                out_types.append(sm.type_of(e.i))
+            else:
+                out_types.append(N.TYPE_FLOAT64 if is_f else N.TYPE_INT64)
+        spec.nout = len(exprs)
+        if not sm.slots:
+            raise _NotFusable("no input columns")
+        return FusedSelectProjectExec(node, sm.slots, spec, out_types, plan.schema(), plan)
     except _NotFusable:
         return plan
 

@@ -54,6 +54,7 @@ int main(void){
    sizeof(qe_fused_spec));
  printf("%zu %zu %zu %zu\n", offsetof(qe_fused_spec, terms), offsetof(qe_fused_spec, key_cols),
    offsetof(qe_fused_spec, inputs), offsetof(qe_global_agg, avg));
+ printf("%zu %zu\n", sizeof(qe_select_spec), offsetof(qe_select_spec, outputs));
  printf("%zu %zu %zu %zu %zu\n", sizeof(struct ArrowSchema), sizeof(struct ArrowArray),
    sizeof(struct ArrowDeviceArray), offsetof(struct ArrowDeviceArray, device_type),
    offsetof(struct ArrowDeviceArray, sync_event));
@@ -73,7 +74,9 @@ int main(void){
                     N.QeGlobalAgg.avg.offset]
     from kquery import arrow_io as A
 
-    arrow = [int(x) for x in out[2].split()]
+    sel = [int(x) for x in out[2].split()]
+    assert sel == [C.sizeof(N.QeSelectSpec), N.QeSelectSpec.outputs.offset]
+    arrow = [int(x) for x in out[3].split()]
     assert arrow == [C.sizeof(A.ArrowSchemaC), C.sizeof(A.ArrowArrayC), C.sizeof(A.ArrowDeviceArrayC),
                      A.ArrowDeviceArrayC.device_type.offset, A.ArrowDeviceArrayC.sync_event.offset]
     assert arrow[:3] == [72, 80, 128]  # the Arrow C (device) data interface ABI

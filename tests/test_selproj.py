@@ -1,0 +1,160 @@
+"""Fused SelectionExec -> ProjectionExec (qe_select_project): one pass, order-preserving, bit-exact
+against the oracle's select_mask / filter_columns / arith restatements and against the unfused
+per-family operator chain. Covers tile boundaries (4096-row tiles), selectivity 0..100 %,
+nullable inputs, int64 x/0 -> null, fp64 outputs, narrow-type pass-through and the planner rule."""
+import numpy as np
+import pytest
+
+from oracle import gen
+from oracle import semantics as S
+
+pytestmark = pytest.mark.gpu
+
+
+def _spec(N, terms, outputs):
+    spec = N.QeSelectSpec()
+    spec.mask_col = -1
+    spec.nterms = len(terms)
+    for i, (col, op, rhs_col, lit) in enumerate(terms):
+        t = spec.terms[i]
+        t.col, t.op, t.rhs_col = col, op, rhs_col
+        if lit is not None:
+            t.lit = N.scalar(lit)
+    spec.nout = len(outputs)
+    for k, toks in enumerate(outputs):
+        spec.outputs[k].ntokens = len(toks)
+        for j, (op, arg, lit) in enumerate(toks):
+            spec.outputs[k].tokens[j] = N.QeToken(op, arg, N.scalar(lit) if lit is not None else N.QeScalar())
+    return spec
+
+
+def _run(ctx, cols, spec, out_types):
+    from kquery import native as N
+    from kquery.columnar import DeviceColumn
+
+    n = cols[0].length
+    outs = [DeviceColumn.empty(t, n, True, ctx=ctx) for t in out_types]
+    cc = (N.QeColumn * len(cols))(*[c.as_c() for c in cols])
+    oc = (N.QeColumn * len(outs))(*[o.as_c() for o in outs])
+    cnt = N.C.c_int64()
+    N.check(N.lib().qe_select_project(ctx.handle, cc, len(cols), N.C.byref(spec), oc, N.C.byref(cnt)))
+    for o in outs:
+        o.length = cnt.value
+    return cnt.value, outs
+
+
+@pytest.mark.parametrize("n", [0, 1, 255, 4095, 4096, 4097, 100_003, 3_000_000])
+@pytest.mark.parametrize("k", [0, 1 << 10, 1 << 19, (1 << 20) - 1, 1 << 20])
+def test_c2_shape(gpu_ctx, n, k):
+    """C2: SELECT a + b WHERE a > k (a uniform in [0, 2^20), b full-range int64: wrap)."""
+    from kquery import native as N
+    from kquery.datasource import C2_COLUMNS, generate_column
+
+    cols = [generate_column(s, n, 0, 42, gpu_ctx) for s in C2_COLUMNS]
+    spec = _spec(N, [(0, N.OP_GT, -1, k)], [[(N.TOK_COL, 0, None), (N.TOK_COL, 1, None), (N.TOK_ADD, 0, None)],
+                                           [(N.TOK_COL, 1, None)]])
+    cnt, (ab, b) = _run(gpu_ctx, cols, spec, [N.TYPE_INT64, N.TYPE_INT64])
+    a_h, _ = gen.generate(C2_COLUMNS[0].dist, C2_COLUMNS[0].param, 42, C2_COLUMNS[0].col_id, 0, n)
+    b_h, _ = gen.generate(C2_COLUMNS[1].dist, C2_COLUMNS[1].param, 42, C2_COLUMNS[1].col_id, 0, n)
+    m, mv = S.cmp(S.OP_GT, a_h, None, k, None)
+    fa, fb = S.filter_columns(m, mv, [a_h, b_h])
+    want, _ = S.arith(S.OP_ADD, fa, None, fb, None)
+    assert cnt == len(fa)
+    assert (ab.to_numpy() == want).all()
+    assert (b.to_numpy() == fb).all()
+    assert ab.valid_mask().all()
+
+
+@pytest.mark.parametrize("n", [1000, 70_001])
+def test_nulls_division_f64_and_narrow_types(gpu_ctx, n):
+    from kquery import native as N
+    from kquery.columnar import DeviceColumn
+
+    rng = np.random.default_rng(n)
+    x = rng.integers(-5, 6, n).astype(np.int64)
+    xv = rng.random(n) > 0.1
+    y = rng.integers(-3, 4, n).astype(np.int64)  # zeros: x / y -> null
+    f = rng.normal(size=n)
+    fv = rng.random(n) > 0.2
+    i32 = rng.integers(-2**31, 2**31 - 1, n).astype(np.int32)
+    u8 = rng.integers(0, 256, n).astype(np.uint8)
+    cols = [DeviceColumn.from_numpy(N.TYPE_INT64, x, xv, ctx=gpu_ctx), DeviceColumn.from_numpy(N.TYPE_INT64, y, ctx=gpu_ctx),
+            DeviceColumn.from_numpy(N.TYPE_FLOAT64, f, fv, ctx=gpu_ctx), DeviceColumn.from_numpy(N.TYPE_INT32, i32, ctx=gpu_ctx),
+            DeviceColumn.from_numpy(N.TYPE_UINT8, u8, ctx=gpu_ctx)]
+    # WHERE f > -0.5 AND y <= 2 ; SELECT x / y, f * x + 1.5, i32, u8
+    spec = _spec(N, [(2, N.OP_GT, -1, -0.5), (1, N.OP_LE, -1, 2)],
+                 [[(N.TOK_COL, 0, None), (N.TOK_COL, 1, None), (N.TOK_DIV, 0, None)],
+                  [(N.TOK_COL, 2, None), (N.TOK_COL, 0, None), (N.TOK_MUL, 0, None), (N.TOK_LIT, 0, 1.5),
+                   (N.TOK_ADD, 0, None)],
+                  [(N.TOK_COL, 3, None)], [(N.TOK_COL, 4, None)]])
+    cnt, outs = _run(gpu_ctx, cols, spec, [N.TYPE_INT64, N.TYPE_FLOAT64, N.TYPE_INT32, N.TYPE_UINT8])
+    m1, v1 = S.cmp(S.OP_GT, f, fv, -0.5, None)
+    m2, v2 = S.cmp(S.OP_LE, y, None, 2, None)
+    sel = S.select_mask(m1 & m2, v1 & v2)
+    assert cnt == int(sel.sum())
+    q, qv = S.arith(S.OP_DIV, x, xv, y, None)
+    fx, fxv = S.arith(S.OP_MUL, f, fv, x.astype(np.float64), xv)
+    r, rv = S.arith(S.OP_ADD, fx, fxv, 1.5, None)
+    for out, (val, valid) in zip(outs[:2], [(q, qv), (r, rv)]):
+        got_v = out.valid_mask()
+        assert (got_v == valid[sel]).all()
+        g = out.to_numpy()[got_v]
+        w = val[sel][valid[sel]]
+        assert (g.view(np.int64) == w.view(np.int64)).all()
+    assert (outs[2].to_numpy() == i32[sel]).all() and (outs[3].to_numpy() == u8[sel]).all()
+    assert outs[2].valid_mask().all()
+
+
+def test_projection_only_and_bare_selection_planner(gpu_ctx):
+    """fuse() turns ProjectionExec/SelectionExec over a scan into FusedSelectProjectExec; results
+    equal the unfused operators batch for batch."""
+    from kquery import native as N
+    from kquery.columnar import Field, RecordBatch, Schema
+    from kquery.datasource import C2_COLUMNS, InMemoryDataSource, generate_column
+    from kquery.expressions import (AddExpression, ColumnExpression, GtExpression, LiteralLongExpression,
+                                    MultiplyExpression)
+    from kquery.operators import FusedSelectProjectExec, ProjectionExec, ScanExec, SelectionExec, fuse
+
+    schema = Schema([s.field() for s in C2_COLUMNS])
+    batches = [RecordBatch(schema, [generate_column(s, n, r0, 42, gpu_ctx) for s in C2_COLUMNS])
+               for n, r0 in ((50_000, 0), (7, 50_000), (123_457, 50_007))]
+    ds = InMemoryDataSource(schema, batches)
+    plans = [
+        ProjectionExec(SelectionExec(ScanExec(ds, ["a", "b"]), GtExpression(ColumnExpression(0), LiteralLongExpression(1 << 19))),
+                       Schema([Field("ab", N.TYPE_INT64)]), [AddExpression(ColumnExpression(0), ColumnExpression(1))]),
+        SelectionExec(ScanExec(ds, ["a", "b"]), GtExpression(ColumnExpression(1), LiteralLongExpression(0))),
+        ProjectionExec(ScanExec(ds, ["a", "b"]), Schema([Field("x", N.TYPE_INT64), Field("b", N.TYPE_INT64)]),
+                       [MultiplyExpression(ColumnExpression(0), LiteralLongExpression(3)), ColumnExpression(1)]),
+    ]
+    for plan in plans:
+        fused = fuse(plan)
+        assert isinstance(fused, FusedSelectProjectExec), plan
+        got = list(fused.execute())
+        want = list(plan.execute())
+        assert len(got) == len(want)
+        for g, w in zip(got, want):
+            assert g.rowCount() == w.rowCount()
+            for i in range(len(w.fields)):
+                assert (g.field(i).to_numpy() == w.field(i).to_numpy()).all()
+
+
+def test_jit_off_falls_back_to_unfused(gpu_ctx):
+    from kquery import native as N
+    from kquery.columnar import Field, RecordBatch, Schema
+    from kquery.datasource import C2_COLUMNS, InMemoryDataSource, generate_column
+    from kquery.expressions import AddExpression, ColumnExpression, GtExpression, LiteralLongExpression
+    from kquery.operators import ProjectionExec, ScanExec, SelectionExec, fuse
+
+    schema = Schema([s.field() for s in C2_COLUMNS])
+    ds = InMemoryDataSource(schema, [RecordBatch(schema, [generate_column(s, 10_000, 0, 42, gpu_ctx)
+                                                          for s in C2_COLUMNS])])
+    plan = ProjectionExec(SelectionExec(ScanExec(ds, ["a", "b"]), GtExpression(ColumnExpression(0),
+                                                                                LiteralLongExpression(1 << 19))),
+                          Schema([Field("ab", N.TYPE_INT64)]), [AddExpression(ColumnExpression(0), ColumnExpression(1))])
+    want = next(plan.execute()).field(0).to_numpy()
+    N.check(N.lib().qe_ctx_set_jit(gpu_ctx.handle, 0))
+    try:
+        got = next(fuse(plan).execute()).field(0).to_numpy()
+    finally:
+        N.check(N.lib().qe_ctx_set_jit(gpu_ctx.handle, 1))
+    assert (got == want).all()
