@@ -64,6 +64,7 @@ int compile_program(const qe_column* cols, int32_t ncols, const bool* col_f64, c
                     qe::DAgg* a, bool* is_f, bool* nullable);
 // Select-project kernel source (qe_jit.hip): R rows per thread, 256 threads.
 bool gen_selproj_source(const qe::Plan& P, const int32_t* out_kind, int nout, std::string* src);
+int selproj_rows_per_thread(const qe::Plan& P);
 // Exclusive scan of n int64 on the ctx stream (one block); out[n] = total. (qe_filter.hip)
 int exclusive_scan_i64(qe_ctx* ctx, const int64_t* in, int64_t* out, int64_t n);
 

@@ -64,7 +64,7 @@ extern "C" int qe_select_project(qe_ctx* ctx, const qe_column* cols, int32_t nco
   }
   *out_count = 0;
   if (n > 0) {
-    const int R = P.ncols <= 3 ? 16 : (P.ncols <= 6 ? 8 : 4);  // gen_selproj_source's stripes per thread
+    const int R = selproj_rows_per_thread(P);
     const int64_t tiles = (int64_t)div_up((uint64_t)n, (uint64_t)R * 256);
     QE_CHECK(tiles < (1ll << 31), QE_ERR_CAPACITY, "too many rows for one select-project call");
     void* s;
@@ -74,7 +74,7 @@ extern "C" int qe_select_project(qe_ctx* ctx, const qe_column* cols, int32_t nco
     P.t.ctl = ctl;
     P.t.keys = (qi64*)(ctl + 2);
     P.t.cap = (qu64)tiles;
-    QE_TRY(jit_launch(ctx, fn, (int)tiles, P, 256));
+    QE_TRY(jit_launch(ctx, fn, (int)tiles, P, 256));  // one tile per workgroup, ids in start order
     QE_TRY(launch_check("qe_selproj"));
     void* pin;
     QE_TRY(ctx_pinned(ctx, 8, &pin));

@@ -26,7 +26,7 @@ from kquery.datasource import (C2_COLUMNS, C3_COLUMNS, C4_COLUMNS, C5_COLUMNS, I
                                generate_column)
 from kquery.expressions import (AddExpression, ColumnExpression, GtExpression,  # noqa: E402
                                 LiteralLongExpression)
-from kquery.operators import ProjectionExec, ScanExec, SelectionExec  # noqa: E402
+from kquery.operators import ProjectionExec, ScanExec, SelectionExec, fuse  # noqa: E402
 from kquery.workloads import C4_AGGS, C5_AGGS, C5_KEY_TYPES, c4_spec, c5_spec  # noqa: E402
 
 PEAK = 8000.0
@@ -75,6 +75,39 @@ def main():
         # algorithmic: read a, b (16 B) + write a+b for the selected rows
         report("C2 filter(a>2^19)+project(a+b), 10M int64 (160 MB: fits the 256 MB MALL)", n,
                16 + 8 * sel_rows / n, ms, selected=sel_rows, path="per-family operators (cmp, count, compact, arith)")
+        fused = fuse(proj)
+        assert type(fused).__name__ == "FusedSelectProjectExec"
+
+        def run_fused():
+            out["f"] = next(fused.execute())
+
+        ms_f = timed(run_fused)
+        assert out["f"].rowCount() == sel_rows
+        # kernel-only time (HIP events on the ctx stream around the one launch)
+        c = [x.as_c() for x in cols]
+        cc = (N.QeColumn * 2)(*c)
+        o = DeviceColumn.empty(N.TYPE_INT64, n, False, ctx=ctx)
+        oc = (N.QeColumn * 1)(o.as_c())
+        cnt = N.C.c_int64()
+
+        def run_kernel():
+            oc[0].length = n  # the call sets it to the selected count
+            N.check(N.lib().qe_select_project(ctx.handle, cc, 2, N.C.byref(fused.spec), oc, N.C.byref(cnt)))
+
+        ms_k = timed(run_kernel)
+        report("C2 fused select+project (qe_select_project), 10M int64", n, 16 + 8 * sel_rows / n, ms_f,
+               selected=sel_rows, call_ms=ms_k, call_gbs=n * (16 + 8 * sel_rows / n) / (ms_k * 1e-3) / 1e9,
+               path="one hipRTC-specialised kernel: predicate, look-back compaction, projection")
+        for sel_k in (1 << 13, (1 << 20) - (1 << 13)):  # ~1 % / ~99 % selectivity sweep
+            spec2 = N.QeSelectSpec.from_buffer_copy(fused.spec)
+            spec2.terms[0].lit = N.scalar(sel_k, N.TYPE_INT64)
+
+            def run_sweep():
+                oc[0].length = n
+                N.check(N.lib().qe_select_project(ctx.handle, cc, 2, N.C.byref(spec2), oc, N.C.byref(cnt)))
+
+            ms_s = timed(run_sweep)
+            report(f"C2 fused, a > {sel_k}", n, 16 + 8 * cnt.value / n, ms_s, selected=cnt.value)
         del cols, out
     if "C3" in which:
         n = 100_000_000
