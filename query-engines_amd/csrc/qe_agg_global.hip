@@ -163,6 +163,97 @@ __global__ void __launch_bounds__(256) k_agg_global(const int64_t* __restrict__ 
   }
 }
 
+// Dense fp64 column (no validity, no mask): the C3 shape. Eight independent compensated sums per
+// thread (one per row slot) break the fp64 add dependency chain that otherwise bounds the
+// kernel; min/max run on the doubles with fmin/fmax (which ignore NaN: NaN rows are recorded in a
+// rare branch), first-row indices are set on first sight (each thread visits rows in order).
+__global__ void __launch_bounds__(256) k_agg_global_f64_dense(const int64_t* __restrict__ vals, int64_t n,
+                                                              GPart* __restrict__ partials) {
+  const int lane = threadIdx.x & 63;
+  const int64_t wave = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 6;
+  const int64_t nwaves = ((int64_t)gridDim.x * blockDim.x) >> 6;
+  double s[8], c[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) s[k] = c[k] = 0.0;
+  double mn = __builtin_inf(), mx = -__builtin_inf();
+  int64_t count = 0;
+  uint64_t first_nn = UINT64_MAX, first_nan = UINT64_MAX, first_negz = UINT64_MAX, first_posz = UINT64_MAX;
+  for (int64_t base = wave * 512; base < n; base += nwaves * 512) {
+    const bool full = base + 512 <= n;
+    double d[8];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int64_t r0 = base + 128 * q + 2 * lane;
+      if (full) {
+        const i64x2 t = *(const i64x2*)(vals + r0);
+        d[2 * q] = bits_f64(t.x);
+        d[2 * q + 1] = bits_f64(t.y);
+      } else {
+        d[2 * q] = r0 < n ? bits_f64(vals[r0]) : 0.0;
+        d[2 * q + 1] = r0 + 1 < n ? bits_f64(vals[r0 + 1]) : 0.0;
+      }
+    }
+    if (first_nn == UINT64_MAX) first_nn = (uint64_t)(base + 2 * lane);  // rows base+2*lane.. exist
+    if (full) {
+      count += 8;
+    } else {
+#pragma unroll
+      for (int k = 0; k < 8; ++k) count += (base + 128 * (k >> 1) + 2 * lane + (k & 1) < n) ? 1 : 0;
+    }
+    bool special = false;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      neumaier_add(s[k], c[k], d[k]);  // out-of-range rows read as 0.0: no effect on the sum
+      const bool in = full || base + 128 * (k >> 1) + 2 * lane + (k & 1) < n;
+      const double dm = in ? d[k] : __builtin_nan("");  // fmin/fmax ignore NaN
+      mn = fmin(mn, dm);
+      mx = fmax(mx, dm);
+      special |= (d[k] != d[k]) | (d[k] == 0.0);
+    }
+    if (special) {  // NaN or a zero among these 8 rows (rare): exact first-occurrence bookkeeping
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        const int64_t row = base + 128 * (k >> 1) + 2 * lane + (k & 1);
+        if (row >= n) continue;
+        if (d[k] != d[k]) first_nan = min(first_nan, (uint64_t)row);
+        else if (d[k] == 0.0) {
+          if (f64_bits(d[k]) < 0) first_negz = min(first_negz, (uint64_t)row);
+          else first_posz = min(first_posz, (uint64_t)row);
+        }
+      }
+    }
+  }
+  GPart p;
+  gpart_init(p);
+  p.rows = p.count = count;
+  p.first_nn = count ? first_nn : UINT64_MAX;
+  p.first_nan = first_nan;
+  p.first_negz = first_negz;
+  p.first_posz = first_posz;
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {  // fixed fold order
+    p.c += c[k];
+    neumaier_add(p.s, p.c, s[k]);
+  }
+  if (mn == mn && count) {  // fmin/fmax skipped NaN; all-NaN leaves the identities (+-inf)
+    p.kmin = f64_okey(mn);
+    p.kmax = f64_okey(mx);
+  }
+  if (first_nan != UINT64_MAX && mn == __builtin_inf() && mx == -__builtin_inf()) {
+    p.kmin = INT64_MAX;  // only NaNs seen by this thread
+    p.kmax = INT64_MIN;
+  }
+  gpart_wave_reduce(p);
+  __shared__ GPart wp[4];
+  if (lane == 0) wp[threadIdx.x >> 6] = p;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    GPart b = wp[0];
+    for (int w = 1; w < 4; ++w) gpart_merge(b, wp[w]);
+    partials[blockIdx.x] = b;
+  }
+}
+
 __global__ void __launch_bounds__(256) k_agg_global_final(GPart* __restrict__ partials, int nparts) {
   // Fixed-order reduction: thread t folds partials t, t+256, ...; then a fixed wave/block tree.
   GPart p;
@@ -212,7 +303,10 @@ extern "C" int qe_agg_global(qe_ctx* ctx, const qe_column* col, const qe_column*
   GPart* parts = (GPart*)s;
   const uint8_t* mv = mask ? (const uint8_t*)mask->values : nullptr;
   const uint8_t* ml = mask ? mask->validity : nullptr;
-  if (f64)
+  if (f64 && !col->validity && !mv)
+    hipLaunchKernelGGL(k_agg_global_f64_dense, dim3((unsigned)blocks), dim3(256), 0, ctx->stream,
+                       (const int64_t*)col->values, n, parts);
+  else if (f64)
     hipLaunchKernelGGL(k_agg_global<true>, dim3((unsigned)blocks), dim3(256), 0, ctx->stream,
                        (const int64_t*)col->values, col->validity, mv, ml, n, parts);
   else
