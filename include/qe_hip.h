@@ -431,6 +431,30 @@ int qe_batch_column(const qe_batch* batch, int32_t i, qe_column* out, const char
 int qe_batch_export(qe_ctx* ctx, const qe_column* cols, int32_t ncols, const char* const* names,
                     ArrowSchema* out_schema, ArrowArray* out_array);
 
+/* ---- GPU CSV scan (CsvDataSource / ReaderIterator, K:204-357) ------------------
+ * Tokenises a CSV file that is already in HBM into Utf8 columns (grammar in qe_csv.hip and
+ * oracle/csv_ref.py: quotes with "" escapes, \n / \r\n / \r records, blank and '#' lines
+ * skipped, values trimmed as K:263 does, missing trailing fields read as ""). The host resolves
+ * the header (first kept record) and the projection to field positions. */
+typedef struct qe_csv_options {
+  int32_t delimiter;          /* field delimiter byte (the reference detects it; the host passes it) */
+  int32_t has_header;         /* 1: the first kept record is the header and yields no row */
+  int32_t nfields;            /* number of projected fields (1..32) */
+  int32_t reserved;
+  const int32_t* field_index; /* host array of nfields 0-based field positions (< 1024) */
+} qe_csv_options;
+typedef struct qe_csv_table qe_csv_table;
+int qe_csv_parse(qe_ctx* ctx, const uint8_t* data, int64_t nbytes, const qe_csv_options* opt,
+                 qe_csv_table** out);
+int qe_csv_rows(const qe_csv_table* table, int64_t* rows);
+/* View of projected column i (UTF8, no validity), valid while the table lives. */
+int qe_csv_column(const qe_csv_table* table, int32_t i, qe_column* out);
+/* Bytes of projected column i, and a device-to-device copy into caller buffers (offsets for
+ * rows+1 entries, values >= qe_csv_column_bytes). */
+int qe_csv_column_bytes(const qe_csv_table* table, int32_t i, int64_t* nbytes);
+int qe_csv_column_copy(const qe_csv_table* table, int32_t i, qe_column* dst);
+int qe_csv_destroy(qe_csv_table* table);
+
 #ifdef __cplusplus
 }
 #endif

@@ -1,0 +1,510 @@
+// GPU CSV scan: CsvDataSource / ReaderIterator (Main.kt:204-357) turn a CSV file
+// into Utf8 RecordBatches; this file does the tokenising on the device, from the file's bytes in
+// HBM to device Utf8 columns.
+//
+// Grammar (restated identically in oracle/csv_ref.py; the reference delegates to univocity
+// CsvParser with delimiter / line-separator detection and skipEmptyLines, K:290-297, whose version
+// is unpinned):
+//   * '"' toggles the quoted state wherever it occurs; outside quotes, '\n', "\r\n" and a lone '\r'
+//     end a record and the delimiter byte ends a field;
+//   * records whose bytes are all <= 0x20 (empty / blank lines) or whose first byte is '#'
+//     (univocity's default comment character) are skipped; the first kept record is the header
+//     when the file has one;
+//   * a field value is its bytes with chars <= 0x20 trimmed from both ends; if that starts and ends
+//     with '"' (length >= 2) the quotes are removed, "" becomes ", and the result is trimmed again
+//     (K:263 calls String.trim() on every value); a missing trailing field reads as "" (K:263).
+// Pipeline (all HBM-streaming, one wave per 64 KiB segment for the byte passes):
+//   k_csv_quotes   quotes per segment                -> scan -> quote state at segment start
+//   k_csv_terms    record terminators per segment    -> scan -> terminator positions (k_csv_emit)
+//   k_csv_keep     per line: kept?                   -> scan -> kept-line list
+//   k_csv_fields   per kept row: projected field ranges, unescaped lengths
+//   k_csv_copy     per projected column: offsets (scan of lengths) + bytes
+#include <vector>
+
+#include "qe_internal.hpp"
+
+struct qe_csv_table {
+  qe_ctx* ctx = nullptr;
+  int64_t rows = 0;
+  std::vector<qe_column> cols;
+  std::vector<void*> owned;
+};
+
+namespace qe {
+namespace {
+
+constexpr int SEG = 64 * 1024;  // bytes per wave-task: 64 steps x 64 lanes x 16 B
+constexpr int CSV_MAX_FIELDS = 32;
+constexpr int CSV_MAX_FIELD_INDEX = 1024;
+
+struct Lane16 {
+  uint32_t w[4];
+  __device__ __forceinline__ uint32_t byte(int k) const { return (w[k >> 2] >> (8 * (k & 3))) & 0xFFu; }
+};
+
+__device__ __forceinline__ Lane16 load16(const uint8_t* data, int64_t nbytes, int64_t pos) {
+  Lane16 v;
+  if (pos + 16 <= nbytes) {
+    const uint4 t = *(const uint4*)(data + pos);
+    v.w[0] = t.x;
+    v.w[1] = t.y;
+    v.w[2] = t.z;
+    v.w[3] = t.w;
+  } else {
+    v.w[0] = v.w[1] = v.w[2] = v.w[3] = 0;
+    for (int k = 0; k < 16 && pos + k < nbytes; ++k) v.w[k >> 2] |= (uint32_t)data[pos + k] << (8 * (k & 3));
+  }
+  return v;
+}
+
+// Number of '"' bytes in the 16 bytes (bytes past the end read as 0).
+__device__ __forceinline__ int quotes16(const Lane16& v) {
+  int q = 0;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const uint32_t x = v.w[i] ^ 0x22222222u;  // zero byte where the byte is '"'
+    // exact per-byte zero test (the (x - 0x01..) & ~x form has borrow false positives)
+    q += __popc(~(((x & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | x | 0x7F7F7F7Fu));
+  }
+  return q;
+}
+
+__global__ void __launch_bounds__(256) k_csv_quotes(const uint8_t* __restrict__ data, int64_t nbytes, int64_t nseg,
+                                                    int64_t* __restrict__ seg_q) {
+  const int lane = threadIdx.x & 63;
+  const int64_t seg = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  if (seg >= nseg) return;
+  const int64_t base = seg * SEG;
+  int q = 0;
+  for (int step = 0; step < SEG / 1024; ++step) {
+    const int64_t pos = base + step * 1024 + lane * 16;
+    if (pos >= nbytes) break;
+    q += quotes16(load16(data, nbytes, pos));
+  }
+  for (int d = 32; d >= 1; d >>= 1) q += __shfl_xor(q, d);
+  if (lane == 0) seg_q[seg] = q;
+}
+
+// Terminator mask (bit k = byte k ends a record) of a lane's 16 bytes, given the quote state at
+// its first byte; returns the state after the 16 bytes.
+__device__ __forceinline__ uint32_t terms16(const Lane16& v, const uint8_t* data, int64_t nbytes, int64_t pos,
+                                            uint32_t inq, uint32_t* inq_out) {
+  uint32_t m = 0;
+#pragma unroll
+  for (int k = 0; k < 16; ++k) {
+    const uint32_t c = v.byte(k);
+    if (pos + k >= nbytes) break;
+    if (c == '"') {
+      inq ^= 1u;
+    } else if (!inq) {
+      if (c == '\n') {
+        m |= 1u << k;
+      } else if (c == '\r') {
+        const uint32_t nx = k < 15 ? v.byte(k + 1) : (pos + 16 < nbytes ? data[pos + 16] : 0u);
+        const bool last = pos + k + 1 >= nbytes;
+        if (last || nx != '\n') m |= 1u << k;
+      }
+    }
+  }
+  *inq_out = inq;
+  return m;
+}
+
+// EMIT = false: count terminators per segment; true: write their positions.
+template <bool EMIT>
+__global__ void __launch_bounds__(256) k_csv_terms(const uint8_t* __restrict__ data, int64_t nbytes, int64_t nseg,
+                                                   const int64_t* __restrict__ seg_qstart, int64_t* __restrict__ seg_t,
+                                                   const int64_t* __restrict__ seg_tstart, int64_t* __restrict__ ends) {
+  const int lane = threadIdx.x & 63;
+  const int64_t seg = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  if (seg >= nseg) return;
+  const int64_t base = seg * SEG;
+  const uint64_t below = (1ull << lane) - 1;
+  uint32_t carry = (uint32_t)(seg_qstart[seg] & 1);
+  int64_t out = EMIT ? seg_tstart[seg] : 0;
+  int64_t count = 0;
+  for (int step = 0; step < SEG / 1024; ++step) {
+    const int64_t row0 = base + step * 1024;
+    if (row0 >= nbytes) break;
+    const int64_t pos = row0 + lane * 16;
+    const Lane16 v = load16(data, nbytes, pos);
+    const uint32_t qodd = (uint32_t)(quotes16(v) & 1);
+    const uint64_t par = __ballot(qodd);
+    const uint32_t inq0 = carry ^ ((uint32_t)__popcll(par & below) & 1u);
+    uint32_t inq1;
+    const uint32_t m = terms16(v, data, nbytes, pos, inq0, &inq1);
+    carry ^= (uint32_t)__popcll(par) & 1u;
+    const int c = __popc(m);
+    // wave exclusive prefix of c
+    int incl = c;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+      const int y = __shfl_up(incl, d);
+      if (lane >= d) incl += y;
+    }
+    const int total = __shfl(incl, 63);
+    if (EMIT) {
+      int64_t o = out + (incl - c);
+      uint32_t mm = m;
+      while (mm) {
+        const int k = __builtin_ctz(mm);
+        mm &= mm - 1;
+        ends[o++] = pos + k;
+      }
+      out += total;
+    }
+    count += total;
+  }
+  if (!EMIT && lane == 0) seg_t[seg] = count;
+}
+
+// Line i is [start(i), ends[i]) with start(0) = 0, start(i) = ends[i-1] + 1.
+__device__ __forceinline__ int64_t line_start(const int64_t* ends, int64_t i) { return i == 0 ? 0 : ends[i - 1] + 1; }
+
+__global__ void k_csv_keep(const uint8_t* __restrict__ data, const int64_t* __restrict__ ends, int64_t nlines,
+                           int64_t* __restrict__ keep) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < nlines; i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t s = line_start(ends, i), e = ends[i];
+    int64_t k = 0;
+    if (s < e && data[s] != '#') {
+      for (int64_t p = s; p < e; ++p)
+        if (data[p] > 0x20) {
+          k = 1;
+          break;
+        }
+    }
+    keep[i] = k;
+  }
+}
+
+__global__ void k_csv_compact_lines(const int64_t* __restrict__ keep, const int64_t* __restrict__ kstart,
+                                    int64_t nlines, int64_t* __restrict__ kept) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < nlines; i += (int64_t)gridDim.x * blockDim.x)
+    if (keep[i]) kept[kstart[i]] = i;
+}
+
+struct FieldArgs {
+  int16_t slot[CSV_MAX_FIELD_INDEX];  // field index -> projected column slot, -1 = not projected
+  int64_t* start[CSV_MAX_FIELDS];     // per column: byte position of the (trimmed, unquoted) value
+  int64_t* len[CSV_MAX_FIELDS];       // per column: output length (after unescaping)
+  uint8_t* quoted[CSV_MAX_FIELDS];    // per column: 1 if "" sequences must be unescaped
+  int32_t max_field;                  // largest projected field index
+  int32_t delim;
+};
+
+__device__ __forceinline__ void trim(const uint8_t* d, int64_t& s, int64_t& e) {
+  while (s < e && d[s] <= 0x20) ++s;
+  while (e > s && d[e - 1] <= 0x20) --e;
+}
+
+__device__ void record_field(const uint8_t* d, const FieldArgs& A, int f, int64_t s, int64_t e, int64_t row) {
+  if (f > A.max_field) return;
+  const int sl = A.slot[f];
+  if (sl < 0) return;
+  trim(d, s, e);
+  uint8_t q = 0;
+  int64_t len = e - s;
+  if (len >= 2 && d[s] == '"' && d[e - 1] == '"') {
+    ++s;
+    --e;
+    // unescaped length: every "" pair counts once; then trim again (String.trim on the value)
+    int64_t a = s, b = e;
+    // trimming after unescaping: leading/trailing bytes <= 0x20 are never quotes, so trimming the
+    // escaped span first gives the same bytes
+    trim(d, a, b);
+    int64_t n = 0;
+    for (int64_t p = a; p < b; ++p) {
+      if (d[p] == '"' && p + 1 < b && d[p + 1] == '"') ++p;
+      ++n;
+    }
+    s = a;
+    len = n;
+    q = 1;
+  }
+  A.start[sl][row] = s;
+  A.len[sl][row] = len;
+  A.quoted[sl][row] = q;
+}
+
+__global__ void k_csv_fields(const uint8_t* __restrict__ data, const int64_t* __restrict__ ends,
+                             const int64_t* __restrict__ kept, int64_t first_row_line, int64_t nrows, FieldArgs A,
+                             int32_t nproj) {
+  for (int64_t r = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; r < nrows; r += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t li = kept[first_row_line + r];
+    const int64_t s = line_start(ends, li), e = ends[li];
+    for (int c = 0; c < nproj; ++c) {  // missing fields read as ""
+      A.start[c][r] = s;
+      A.len[c][r] = 0;
+      A.quoted[c][r] = 0;
+    }
+    int f = 0;
+    int64_t fs = s;
+    uint32_t inq = 0;
+    for (int64_t p = s; p < e && f <= A.max_field; ++p) {
+      const uint32_t c = data[p];
+      if (c == '"') {
+        inq ^= 1u;
+      } else if (!inq && c == (uint32_t)A.delim) {
+        record_field(data, A, f, fs, p, r);
+        ++f;
+        fs = p + 1;
+      }
+    }
+    if (f <= A.max_field) record_field(data, A, f, fs, e, r);
+  }
+}
+
+__global__ void k_csv_offsets(const int64_t* __restrict__ starts64, int64_t n, int32_t* __restrict__ offs) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i <= n; i += (int64_t)gridDim.x * blockDim.x)
+    offs[i] = (int32_t)starts64[i];
+}
+
+__global__ void k_csv_copy(const uint8_t* __restrict__ data, const int64_t* __restrict__ start,
+                           const int64_t* __restrict__ len, const uint8_t* __restrict__ quoted,
+                           const int32_t* __restrict__ offs, int64_t n, uint8_t* __restrict__ out) {
+  for (int64_t r = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; r < n; r += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t s = start[r], l = len[r];
+    uint8_t* dst = out + offs[r];
+    if (!quoted[r]) {
+      for (int64_t k = 0; k < l; ++k) dst[k] = data[s + k];
+    } else {
+      int64_t p = s;
+      for (int64_t k = 0; k < l; ++k) {
+        const uint8_t c = data[p];
+        dst[k] = c;
+        p += (c == '"' && data[p + 1] == '"') ? 2 : 1;
+      }
+    }
+  }
+}
+
+int dmalloc(qe_csv_table* t, size_t bytes, void** p) {
+  if (hipMalloc(p, bytes ? bytes : 1) != hipSuccess) {
+    (void)hipGetLastError();
+    return fail(QE_ERR_OOM, "hipMalloc(%zu) failed in CSV scan", bytes);
+  }
+  t->owned.push_back(*p);
+  return QE_OK;
+}
+
+int grid_for(qe_ctx* ctx, int64_t n, int threads = 256) {
+  return (int)std::max<int64_t>(1, std::min<int64_t>((int64_t)div_up((uint64_t)(n > 0 ? n : 1), threads),
+                                                      (int64_t)ctx->num_cus * 8));
+}
+
+int read_i64(qe_ctx* ctx, const int64_t* p, int64_t* out) {
+  QE_HIP(hipMemcpyAsync(out, p, 8, hipMemcpyDeviceToHost, ctx->stream));
+  QE_HIP(hipStreamSynchronize(ctx->stream));
+  return QE_OK;
+}
+
+int csv_parse(qe_ctx* ctx, const uint8_t* data, int64_t nbytes, const qe_csv_options* opt, qe_csv_table* t) {
+  const int32_t nproj = opt->nfields;
+  QE_CHECK(nproj >= 1 && nproj <= CSV_MAX_FIELDS, QE_ERR_UNSUPPORTED, "CSV scan projects 1..%d fields (got %d)",
+           CSV_MAX_FIELDS, nproj);
+  QE_CHECK(opt->delimiter > 0 && opt->delimiter < 256 && opt->delimiter != '"' && opt->delimiter != '\n' &&
+               opt->delimiter != '\r',
+           QE_ERR_INVALID_ARG, "bad CSV delimiter %d", opt->delimiter);
+  FieldArgs A;
+  for (int i = 0; i < CSV_MAX_FIELD_INDEX; ++i) A.slot[i] = -1;
+  A.max_field = -1;
+  A.delim = opt->delimiter;
+  for (int c = 0; c < nproj; ++c) {
+    const int f = opt->field_index ? opt->field_index[c] : c;
+    QE_CHECK(f >= 0 && f < CSV_MAX_FIELD_INDEX, QE_ERR_UNSUPPORTED, "CSV field index %d out of range", f);
+    QE_CHECK(A.slot[f] < 0, QE_ERR_INVALID_ARG, "CSV field %d projected twice", f);
+    A.slot[f] = (int16_t)c;
+    A.max_field = std::max(A.max_field, f);
+  }
+  // ---- record terminators
+  const int64_t nseg = (int64_t)div_up((uint64_t)(nbytes > 0 ? nbytes : 1), SEG);
+  void* p;
+  QE_TRY(dmalloc(t, (size_t)(4 * nseg + 4) * 8, &p));
+  int64_t* seg_q = (int64_t*)p;
+  int64_t* seg_qs = seg_q + nseg;
+  int64_t* seg_t = seg_qs + nseg + 1;
+  int64_t* seg_ts = seg_t + nseg;
+  const int wgrid = (int)div_up((uint64_t)nseg, 4);  // 4 waves per 256-thread block
+  if (nbytes > 0) {
+    hipLaunchKernelGGL(k_csv_quotes, dim3(wgrid), dim3(256), 0, ctx->stream, data, nbytes, nseg, seg_q);
+    QE_TRY(launch_check("k_csv_quotes"));
+  } else {
+    QE_HIP(hipMemsetAsync(seg_q, 0, 8, ctx->stream));
+  }
+  QE_TRY(exclusive_scan_i64(ctx, seg_q, seg_qs, nseg));
+  hipLaunchKernelGGL(k_csv_terms<false>, dim3(wgrid), dim3(256), 0, ctx->stream, data, nbytes, nseg, seg_qs, seg_t,
+                     nullptr, nullptr);
+  QE_TRY(launch_check("k_csv_terms"));
+  QE_TRY(exclusive_scan_i64(ctx, seg_t, seg_ts, nseg));
+  int64_t nterm = 0;
+  QE_TRY(read_i64(ctx, seg_ts + nseg, &nterm));
+  QE_TRY(dmalloc(t, (size_t)(3 * nterm + 7) * 8, &p));
+  int64_t* ends = (int64_t*)p;
+  int64_t* keep = ends + nterm + 2;
+  int64_t* kstart = keep + nterm + 2;
+  int64_t last_end = -1;
+  if (nterm > 0) {
+    hipLaunchKernelGGL(k_csv_terms<true>, dim3(wgrid), dim3(256), 0, ctx->stream, data, nbytes, nseg, seg_qs, nullptr,
+                       seg_ts, ends);
+    QE_TRY(launch_check("k_csv_terms<emit>"));
+    QE_TRY(read_i64(ctx, ends + nterm - 1, &last_end));
+  }
+  // bytes after the last terminator form a final record (also an unterminated quote at EOF)
+  const int64_t nlines = nterm + (last_end + 1 < nbytes ? 1 : 0);
+  if (nlines > nterm) {
+    QE_HIP(hipMemcpyAsync(ends + nterm, &nbytes, 8, hipMemcpyHostToDevice, ctx->stream));
+    QE_HIP(hipStreamSynchronize(ctx->stream));  // &nbytes is a host stack address
+  }
+  // ---- kept records
+  int64_t nkept = 0;
+  if (nlines > 0) {
+    hipLaunchKernelGGL(k_csv_keep, dim3(grid_for(ctx, nlines)), dim3(256), 0, ctx->stream, data, ends, nlines, keep);
+    QE_TRY(launch_check("k_csv_keep"));
+    QE_TRY(exclusive_scan_i64(ctx, keep, kstart, nlines));
+    QE_TRY(read_i64(ctx, kstart + nlines, &nkept));
+  }
+  int64_t* kept = nullptr;
+  QE_TRY(dmalloc(t, (size_t)(nkept + 1) * 8, &p));
+  kept = (int64_t*)p;
+  if (nkept > 0) {
+    hipLaunchKernelGGL(k_csv_compact_lines, dim3(grid_for(ctx, nlines)), dim3(256), 0, ctx->stream, keep, kstart,
+                       nlines, kept);
+    QE_TRY(launch_check("k_csv_compact_lines"));
+  }
+  const int64_t first = opt->has_header ? 1 : 0;
+  const int64_t rows = std::max<int64_t>(0, nkept - first);
+  t->rows = rows;
+  // ---- fields
+  QE_TRY(dmalloc(t, (size_t)nproj * (size_t)(rows + 1) * 17 + 64, &p));
+  uint8_t* fb = (uint8_t*)p;
+  for (int c = 0; c < nproj; ++c) {
+    A.start[c] = (int64_t*)(fb + (size_t)c * (rows + 1) * 8);
+    A.len[c] = (int64_t*)(fb + (size_t)(nproj + c) * (rows + 1) * 8);
+    A.quoted[c] = fb + (size_t)nproj * (rows + 1) * 16 + (size_t)c * (rows + 1);
+  }
+  if (rows > 0) {
+    hipLaunchKernelGGL(k_csv_fields, dim3(grid_for(ctx, rows)), dim3(256), 0, ctx->stream, data, ends, kept, first,
+                       rows, A, nproj);
+    QE_TRY(launch_check("k_csv_fields"));
+  }
+  // ---- columns
+  int64_t* starts64;
+  QE_TRY(dmalloc(t, (size_t)(rows + 1) * 8, &p));
+  starts64 = (int64_t*)p;
+  for (int c = 0; c < nproj; ++c) {
+    qe_column col{};
+    col.type = QE_TYPE_UTF8;
+    col.length = rows;
+    QE_TRY(dmalloc(t, (size_t)(rows + 1) * 4, &p));
+    col.offsets = (int32_t*)p;
+    int64_t total = 0;
+    if (rows > 0) {
+      QE_TRY(exclusive_scan_i64(ctx, A.len[c], starts64, rows));
+      QE_TRY(read_i64(ctx, starts64 + rows, &total));
+    }
+    QE_CHECK(total < (1ll << 31), QE_ERR_CAPACITY, "CSV column %d holds more than 2^31 bytes", c);
+    if (rows > 0) {
+      hipLaunchKernelGGL(k_csv_offsets, dim3(grid_for(ctx, rows + 1)), dim3(256), 0, ctx->stream, starts64, rows,
+                         col.offsets);
+      QE_TRY(launch_check("k_csv_offsets"));
+    } else {
+      QE_HIP(hipMemsetAsync(col.offsets, 0, 4, ctx->stream));
+    }
+    QE_TRY(dmalloc(t, (size_t)total, &p));
+    col.values = p;
+    if (rows > 0 && total > 0) {
+      hipLaunchKernelGGL(k_csv_copy, dim3(grid_for(ctx, rows)), dim3(256), 0, ctx->stream, data, A.start[c], A.len[c],
+                         A.quoted[c], col.offsets, rows, (uint8_t*)col.values);
+      QE_TRY(launch_check("k_csv_copy"));
+    }
+    t->cols.push_back(col);
+  }
+  QE_HIP(hipStreamSynchronize(ctx->stream));
+  // scratch arrays are freed now; the columns stay
+  std::vector<void*> keep_bufs;
+  for (const qe_column& c : t->cols) {
+    keep_bufs.push_back(c.offsets);
+    keep_bufs.push_back(c.values);
+  }
+  for (void* q : t->owned) {
+    bool kept_buf = false;
+    for (void* k : keep_bufs) kept_buf |= (k == q);
+    if (!kept_buf) (void)hipFree(q);
+  }
+  t->owned = keep_bufs;
+  return QE_OK;
+}
+
+}  // namespace
+}  // namespace qe
+
+using namespace qe;
+
+extern "C" {
+
+int qe_csv_parse(qe_ctx* ctx, const uint8_t* data, int64_t nbytes, const qe_csv_options* opt, qe_csv_table** out) {
+  QE_TRY(ctx_enter(ctx));
+  QE_CHECK(opt && out && (data || nbytes == 0) && nbytes >= 0, QE_ERR_INVALID_ARG, "null argument");
+  *out = nullptr;
+  qe_csv_table* t = new qe_csv_table();
+  t->ctx = ctx;
+  const int rc = csv_parse(ctx, data, nbytes, opt, t);
+  if (rc != QE_OK) {
+    (void)hipStreamSynchronize(ctx->stream);
+    for (void* q : t->owned) (void)hipFree(q);
+    delete t;
+    return rc;
+  }
+  *out = t;
+  return QE_OK;
+}
+
+int qe_csv_rows(const qe_csv_table* t, int64_t* rows) {
+  QE_CHECK(t && rows, QE_ERR_INVALID_ARG, "null argument");
+  *rows = t->rows;
+  return QE_OK;
+}
+
+int qe_csv_column(const qe_csv_table* t, int32_t i, qe_column* out) {
+  QE_CHECK(t && out, QE_ERR_INVALID_ARG, "null argument");
+  QE_CHECK(i >= 0 && (size_t)i < t->cols.size(), QE_ERR_INVALID_ARG, "CSV column %d out of range", i);
+  *out = t->cols[(size_t)i];
+  return QE_OK;
+}
+
+int qe_csv_column_bytes(const qe_csv_table* t, int32_t i, int64_t* nbytes) {
+  QE_CHECK(t && nbytes, QE_ERR_INVALID_ARG, "null argument");
+  QE_CHECK(i >= 0 && (size_t)i < t->cols.size(), QE_ERR_INVALID_ARG, "CSV column %d out of range", i);
+  const qe_column& c = t->cols[(size_t)i];
+  int32_t last = 0;
+  if (c.length > 0) QE_HIP(hipMemcpy(&last, c.offsets + c.length, 4, hipMemcpyDeviceToHost));
+  *nbytes = last;
+  return QE_OK;
+}
+
+int qe_csv_column_copy(const qe_csv_table* t, int32_t i, qe_column* dst) {
+  QE_CHECK(t && dst, QE_ERR_INVALID_ARG, "null argument");
+  QE_CHECK(i >= 0 && (size_t)i < t->cols.size(), QE_ERR_INVALID_ARG, "CSV column %d out of range", i);
+  QE_CHECK(dst->type == QE_TYPE_UTF8 && dst->offsets && dst->length >= t->rows, QE_ERR_INVALID_ARG,
+           "destination must be UTF8 with room for %lld rows", (long long)t->rows);
+  const qe_column& c = t->cols[(size_t)i];
+  qe_ctx* ctx = t->ctx;
+  QE_TRY(ctx_enter(ctx));
+  int64_t nb = 0;
+  QE_TRY(qe_csv_column_bytes(t, i, &nb));
+  QE_HIP(hipMemcpyAsync(dst->offsets, c.offsets, (size_t)(c.length + 1) * 4, hipMemcpyDeviceToDevice, ctx->stream));
+  if (nb > 0) QE_HIP(hipMemcpyAsync(dst->values, c.values, (size_t)nb, hipMemcpyDeviceToDevice, ctx->stream));
+  dst->length = c.length;
+  return QE_OK;
+}
+
+int qe_csv_destroy(qe_csv_table* t) {
+  if (!t) return QE_OK;
+  (void)hipSetDevice(t->ctx->device);
+  (void)hipStreamSynchronize(t->ctx->stream);
+  for (void* q : t->owned) (void)hipFree(q);
+  delete t;
+  return QE_OK;
+}
+
+}  // extern "C"

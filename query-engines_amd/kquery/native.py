@@ -151,6 +151,11 @@ class QeFusedSpec(C.Structure):
     ]
 
 
+class QeCsvOptions(C.Structure):
+    _fields_ = [("delimiter", C.c_int32), ("has_header", C.c_int32), ("nfields", C.c_int32),
+                ("reserved", C.c_int32), ("field_index", C.POINTER(C.c_int32))]
+
+
 class QeSelectSpec(C.Structure):
     _fields_ = [
         ("mask_col", C.c_int32),
@@ -215,6 +220,12 @@ SIGNATURES = [
     ("qe_strdict_decode_bytes", C.c_int, [_P, _COLP, _I64P]),
     ("qe_strdict_decode", C.c_int, [_P, _COLP, _COLP]),
     ("qe_select_project", C.c_int, [_P, _COLP, C.c_int32, C.POINTER(QeSelectSpec), _COLP, _I64P]),
+    ("qe_csv_parse", C.c_int, [_P, _P, C.c_int64, C.POINTER(QeCsvOptions), _PP]),
+    ("qe_csv_rows", C.c_int, [_P, _I64P]),
+    ("qe_csv_column", C.c_int, [_P, C.c_int32, _COLP]),
+    ("qe_csv_column_bytes", C.c_int, [_P, C.c_int32, _I64P]),
+    ("qe_csv_column_copy", C.c_int, [_P, C.c_int32, _COLP]),
+    ("qe_csv_destroy", C.c_int, [_P]),
     ("qe_batch_import", C.c_int, [_P, _P, _P, _PP]),
     ("qe_batch_import_device", C.c_int, [_P, _P, _P, _PP]),
     ("qe_batch_destroy", C.c_int, [_P]),
