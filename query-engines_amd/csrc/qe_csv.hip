@@ -87,8 +87,29 @@ __global__ void __launch_bounds__(256) k_csv_quotes(const uint8_t* __restrict__ 
 
 // Terminator mask (bit k = byte k ends a record) of a lane's 16 bytes, given the quote state at
 // its first byte; returns the state after the 16 bytes.
+// 16-bit mask of the bytes equal to `b` (exact SWAR byte compare, 4 bytes per word).
+__device__ __forceinline__ uint32_t eq16(const Lane16& v, uint32_t b) {
+  const uint32_t rep = b * 0x01010101u;
+  uint32_t m = 0;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const uint32_t x = v.w[i] ^ rep;
+    const uint32_t hb = ~(((x & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | x | 0x7F7F7F7Fu);  // bit 7 of each matching byte
+    m |= (((hb >> 7) & 1u) | ((hb >> 14) & 2u) | ((hb >> 21) & 4u) | ((hb >> 28) & 8u)) << (4 * i);
+  }
+  return m;
+}
+
 __device__ __forceinline__ uint32_t terms16(const Lane16& v, const uint8_t* data, int64_t nbytes, int64_t pos,
                                             uint32_t inq, uint32_t* inq_out) {
+  if (eq16(v, '"') == 0) {  // no quote in these 16 bytes: the state is constant (common case)
+    *inq_out = inq;
+    if (inq) return 0;
+    const uint32_t valid = pos + 16 <= nbytes ? 0xFFFFu : ((1u << (nbytes - pos)) - 1u);
+    const uint32_t nl = eq16(v, '\n') & valid, cr = eq16(v, '\r') & valid;
+    const uint32_t next_nl = (nl >> 1) | ((pos + 16 < nbytes && data[pos + 16] == '\n') ? 0x8000u : 0u);
+    return nl | (cr & ~next_nl);
+  }
   uint32_t m = 0;
 #pragma unroll
   for (int k = 0; k < 16; ++k) {
@@ -226,7 +247,7 @@ __device__ void record_field(const uint8_t* d, const FieldArgs& A, int f, int64_
   A.quoted[sl][row] = q;
 }
 
-__global__ void k_csv_fields(const uint8_t* __restrict__ data, const int64_t* __restrict__ ends,
+__global__ void k_csv_fields(const uint8_t* __restrict__ data, int64_t nbytes, const int64_t* __restrict__ ends,
                              const int64_t* __restrict__ kept, int64_t first_row_line, int64_t nrows, FieldArgs A,
                              int32_t nproj) {
   for (int64_t r = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; r < nrows; r += (int64_t)gridDim.x * blockDim.x) {
@@ -240,15 +261,28 @@ __global__ void k_csv_fields(const uint8_t* __restrict__ data, const int64_t* __
     int f = 0;
     int64_t fs = s;
     uint32_t inq = 0;
-    for (int64_t p = s; p < e && f <= A.max_field; ++p) {
-      const uint32_t c = data[p];
-      if (c == '"') {
-        inq ^= 1u;
-      } else if (!inq && c == (uint32_t)A.delim) {
-        record_field(data, A, f, fs, p, r);
-        ++f;
-        fs = p + 1;
+    // 16-byte aligned loads; bytes outside [s, e) are skipped
+    for (int64_t a = s & ~(int64_t)15; a < e && f <= A.max_field; a += 16) {
+      const Lane16 v = load16(data, nbytes, a);
+      const uint32_t lo = (uint32_t)(s > a ? s - a : 0);
+      const uint32_t hi = (uint32_t)(e - a < 16 ? e - a : 16);
+      const uint32_t in = (hi >= 32 ? 0xFFFFu : ((1u << hi) - 1u)) & ~((1u << lo) - 1u);
+      uint32_t q = eq16(v, '"') & in, d = eq16(v, (uint32_t)A.delim) & in;
+      if (q == 0 && inq) continue;
+      while (d && f <= A.max_field) {
+        const int k = __builtin_ctz(d);
+        // quote toggles before this delimiter
+        const uint32_t before = q & ((1u << k) - 1u);
+        inq ^= (uint32_t)__popc(before) & 1u;
+        q &= ~((1u << k) - 1u);
+        d &= d - 1;
+        if (!inq) {
+          record_field(data, A, f, fs, a + k, r);
+          ++f;
+          fs = a + k + 1;
+        }
       }
+      inq ^= (uint32_t)__popc(q) & 1u;
     }
     if (f <= A.max_field) record_field(data, A, f, fs, e, r);
   }
@@ -383,8 +417,8 @@ int csv_parse(qe_ctx* ctx, const uint8_t* data, int64_t nbytes, const qe_csv_opt
     A.quoted[c] = fb + (size_t)nproj * (rows + 1) * 16 + (size_t)c * (rows + 1);
   }
   if (rows > 0) {
-    hipLaunchKernelGGL(k_csv_fields, dim3(grid_for(ctx, rows)), dim3(256), 0, ctx->stream, data, ends, kept, first,
-                       rows, A, nproj);
+    hipLaunchKernelGGL(k_csv_fields, dim3(grid_for(ctx, rows)), dim3(256), 0, ctx->stream, data, nbytes, ends, kept,
+                       first, rows, A, nproj);
     QE_TRY(launch_check("k_csv_fields"));
   }
   // ---- columns

@@ -79,9 +79,86 @@ __global__ void __launch_bounds__(1024) k_scan(const int64_t* __restrict__ in, i
   if (threadIdx.x == 0) out[n] = carry;
 }
 
+// Device-wide scan for large inputs: per-8192-element block sums -> one-block scan of the sums
+// -> per-block scan with the block's offset (3 launches, 2 passes over the input).
+constexpr int GS_THREADS = 1024, GS_PER = 8;
+constexpr int64_t GS_TILE = (int64_t)GS_THREADS * GS_PER;
+
+__device__ __forceinline__ int64_t block_excl_scan(int64_t v, int64_t* wsum, int64_t* total) {
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  int64_t x = v;
+  for (int off = 1; off < 64; off <<= 1) {
+    const int64_t y = __shfl_up(x, off);
+    if (lane >= off) x += y;
+  }
+  if (lane == 63) wsum[wid] = x;
+  __syncthreads();
+  int64_t wprefix = 0, all = 0;
+  for (int w = 0; w < GS_THREADS / 64; ++w) {
+    if (w < wid) wprefix += wsum[w];
+    all += wsum[w];
+  }
+  *total = all;
+  return wprefix + x - v;
+}
+
+__global__ void __launch_bounds__(GS_THREADS) k_scan_reduce(const int64_t* __restrict__ in, int64_t n,
+                                                             int64_t* __restrict__ sums) {
+  __shared__ int64_t wsum[GS_THREADS / 64];
+  const int64_t i0 = blockIdx.x * GS_TILE + (int64_t)threadIdx.x * GS_PER;
+  int64_t t = 0;
+#pragma unroll
+  for (int k = 0; k < GS_PER; ++k) t += (i0 + k < n) ? in[i0 + k] : 0;
+  int64_t total;
+  (void)block_excl_scan(t, wsum, &total);
+  if (threadIdx.x == 0) sums[blockIdx.x] = total;
+}
+
+__global__ void __launch_bounds__(GS_THREADS) k_scan_apply(const int64_t* __restrict__ in, int64_t* __restrict__ out,
+                                                            int64_t n, const int64_t* __restrict__ offs, int64_t nb) {
+  __shared__ int64_t wsum[GS_THREADS / 64];
+  const int64_t i0 = blockIdx.x * GS_TILE + (int64_t)threadIdx.x * GS_PER;
+  int64_t v[GS_PER], t = 0;
+#pragma unroll
+  for (int k = 0; k < GS_PER; ++k) {
+    v[k] = (i0 + k < n) ? in[i0 + k] : 0;
+    t += v[k];
+  }
+  int64_t total;
+  int64_t run = offs[blockIdx.x] + block_excl_scan(t, wsum, &total);
+#pragma unroll
+  for (int k = 0; k < GS_PER; ++k) {
+    if (i0 + k < n) out[i0 + k] = run;
+    run += v[k];
+  }
+  if (blockIdx.x == nb - 1 && threadIdx.x == 0) out[n] = offs[nb];
+}
+
 int exclusive_scan_i64(qe_ctx* ctx, const int64_t* in, int64_t* out, int64_t n) {
-  hipLaunchKernelGGL(k_scan, dim3(1), dim3(1024), 0, ctx->stream, in, out, n);
-  return launch_check("k_scan");
+  if (n <= 4 * GS_TILE) {
+    hipLaunchKernelGGL(k_scan, dim3(1), dim3(1024), 0, ctx->stream, in, out, n);
+    return launch_check("k_scan");
+  }
+  const int64_t nb = (n + GS_TILE - 1) / GS_TILE;
+  const size_t need = (size_t)(2 * nb + 2) * 8;
+  if (need > ctx->scan_tmp_bytes) {
+    if (ctx->scan_tmp) {
+      QE_HIP(hipStreamSynchronize(ctx->stream));
+      QE_HIP(hipFree(ctx->scan_tmp));
+    }
+    ctx->scan_tmp = nullptr;
+    ctx->scan_tmp_bytes = 0;
+    QE_HIP(hipMalloc(&ctx->scan_tmp, need));
+    ctx->scan_tmp_bytes = need;
+  }
+  int64_t* sums = (int64_t*)ctx->scan_tmp;
+  int64_t* offs = sums + nb + 1;
+  hipLaunchKernelGGL(k_scan_reduce, dim3((unsigned)nb), dim3(GS_THREADS), 0, ctx->stream, in, n, sums);
+  QE_TRY(launch_check("k_scan_reduce"));
+  hipLaunchKernelGGL(k_scan, dim3(1), dim3(1024), 0, ctx->stream, sums, offs, nb);
+  QE_TRY(launch_check("k_scan"));
+  hipLaunchKernelGGL(k_scan_apply, dim3((unsigned)nb), dim3(GS_THREADS), 0, ctx->stream, in, out, n, offs, nb);
+  return launch_check("k_scan_apply");
 }
 
 struct GatherCol {

@@ -22,6 +22,8 @@ struct qe_ctx {
   void* pinned = nullptr;        // small pinned host buffer for read-backs
   size_t pinned_bytes = 0;
   int jit = 1;                   // specialise fused plans with hipRTC (qe_jit.hip)
+  void* scan_tmp = nullptr;      // block sums of exclusive_scan_i64 (never aliases `scratch`)
+  size_t scan_tmp_bytes = 0;
 };
 
 namespace qe {

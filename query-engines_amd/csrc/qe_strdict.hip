@@ -121,16 +121,97 @@ __device__ __forceinline__ void encode_row(const DictDev& D, const int32_t* offs
   }
 }
 
+// Per-workgroup LDS cache of resolved strings: low-cardinality keys (the reference's VendorID)
+// resolve without touching the global table, whose slots all rows would otherwise hit. An entry
+// is published with state 2 after its fields are written. Only keys of up to 32 bytes are cached
+// (they compare entirely in LDS); longer keys always take the global path.
+constexpr int LC_SLOTS = 512, LC_BYTES = 32;
+struct LdsCache {
+  uint32_t state[LC_SLOTS];  // 0 empty, 1 being written, 2 ready
+  uint64_t hash[LC_SLOTS];
+  int32_t len[LC_SLOTS];
+  int32_t code[LC_SLOTS];
+  uint64_t head[LC_SLOTS][LC_BYTES / 8];
+};
+
+__device__ __forceinline__ void head32(const uint8_t* p, int len, uint64_t (&h)[LC_BYTES / 8]) {
+#pragma unroll
+  for (int k = 0; k < LC_BYTES / 8; ++k) {
+    const int o = 8 * k;
+    h[k] = o < len ? load_u64_unaligned(p + o, len - o >= 8 ? 8 : len - o) : 0;
+  }
+}
+
 __global__ void __launch_bounds__(ENC_THREADS) k_dict_encode(DictDev D, const int32_t* __restrict__ offs,
                                                              const uint8_t* __restrict__ bytes,
                                                              const uint8_t* __restrict__ valid, int64_t n,
                                                              int32_t* __restrict__ codes, uint32_t* __restrict__ retry) {
-  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
-    if (valid && !((valid[i >> 3] >> (i & 7)) & 1)) {
-      codes[i] = 0;
-      continue;
+  __shared__ LdsCache C;
+  for (int k = threadIdx.x; k < LC_SLOTS; k += blockDim.x) C.state[k] = 0;
+  __syncthreads();
+  const int lane = threadIdx.x & 63;
+  // every lane runs the same trip count so the wave-level dedup below sees whole waves
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  const int64_t start = blockIdx.x * (int64_t)blockDim.x + threadIdx.x - lane;  // wave's first row
+  for (int64_t i0 = start; i0 < n; i0 += stride) {
+    const int64_t i = i0 + lane;
+    const bool live = i < n && (!valid || ((valid[i >> 3] >> (i & 7)) & 1));
+    int32_t len = 0;
+    const uint8_t* p = bytes;
+    uint64_t h = 0;
+    uint64_t hd[LC_BYTES / 8] = {0, 0, 0, 0};
+    int c = -1;
+    if (live) {
+      const int32_t s0 = offs[i];
+      len = offs[i + 1] - s0;
+      p = bytes + s0;
+      h = str_hash(p, len);
+      head32(p, len, hd);
+      const int slot = (int)(h & (LC_SLOTS - 1));
+      if (len <= LC_BYTES &&
+          __hip_atomic_load(&C.state[slot], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) == 2 &&
+          C.hash[slot] == h && C.len[slot] == len) {
+        bool eq = true;
+#pragma unroll
+        for (int k = 0; k < LC_BYTES / 8; ++k) eq &= C.head[slot][k] == hd[k];
+        if (eq) c = C.code[slot];
+      }
     }
-    encode_row(D, offs, bytes, i, codes, retry);
+    // misses: one global lookup per distinct key in the wave (leader election on the key)
+    uint64_t todo = __ballot(live && c < 0);
+    while (todo) {
+      const int leader = __ffsll((long long)todo) - 1;
+      const uint64_t hl = __shfl(h, leader);
+      const int32_t ll = __shfl(len, leader);
+      bool same = (todo >> lane) & 1;
+      same = same && h == hl && len == ll && (ll <= LC_BYTES || lane == leader);
+#pragma unroll
+      for (int k = 0; k < LC_BYTES / 8; ++k) same = same && hd[k] == __shfl(hd[k], leader);
+      const uint64_t grp = __ballot(same);
+      int code = 0;
+      if (lane == leader) {
+        code = dict_find_or_insert(D, p, len, h);
+        const int slot = (int)(h & (LC_SLOTS - 1));
+        if (code >= 0 && len <= LC_BYTES && atomicCAS(&C.state[slot], 0u, 1u) == 0u) {
+          C.hash[slot] = h;
+          C.len[slot] = len;
+          C.code[slot] = code;
+#pragma unroll
+          for (int k = 0; k < LC_BYTES / 8; ++k) C.head[slot][k] = hd[k];
+          __hip_atomic_store(&C.state[slot], 2u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+        }
+      }
+      code = __shfl(code, leader);
+      if (same) c = code;
+      todo &= ~grp;
+    }
+    if (i < n) {
+      codes[i] = (live && c >= 0) ? c : 0;
+      if (live && c == R_RETRY) {
+        atomicOr(&retry[i >> 5], 1u << (i & 31));
+        atomicAdd(&D.flags[1], 1u);
+      }
+    }
   }
 }
 

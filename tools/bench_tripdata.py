@@ -1,0 +1,131 @@
+#!/usr/bin/env python3
+"""The reference's own workload (Main.kt:1330-1337), on the device end to end:
+
+    SELECT VendorID, MAX(CAST(fare_amount AS double)) AS max_amount FROM tripdata GROUP BY VendorID
+
+over a synthetic yellow-taxi-shaped CSV (18 columns, 2019 TLC layout, ~110 B/row). Stages, each
+timed with HIP events on the context stream after a warm-up:
+  upload   file bytes -> HBM (PCIe, reported separately; not part of the device rate)
+  scan     qe_csv_parse of VendorID + fare_amount (GPU CSV scan)
+  cast     qe_cast_utf8_to_f64 (Double.parseDouble semantics)
+  agg      string-dictionary encode of VendorID + hash aggregate MAX, finalize
+Checked against pandas (float_precision='round_trip', i.e. correctly rounded parsing).
+"""
+import json
+import pathlib
+import statistics
+import sys
+import time
+
+import numpy as np
+
+ROOT = pathlib.Path(__file__).resolve().parents[1]
+sys.path[:0] = [str(ROOT), str(ROOT / "query-engines_amd")]
+
+import torch  # noqa: E402
+
+from kquery import native as N  # noqa: E402
+from kquery.aggregate import HashAggregateState  # noqa: E402
+from kquery.columnar import Context, DeviceColumn  # noqa: E402
+from kquery.csv_source import CsvDataSource  # noqa: E402
+
+HEADER = ("VendorID,tpep_pickup_datetime,tpep_dropoff_datetime,passenger_count,trip_distance,RatecodeID,"
+          "store_and_fwd_flag,PULocationID,DOLocationID,payment_type,fare_amount,extra,mta_tax,tip_amount,"
+          "tolls_amount,improvement_surcharge,total_amount,congestion_surcharge")
+
+
+def make_csv(path: pathlib.Path, rows: int, seed: int = 7) -> None:
+    rng = np.random.default_rng(seed)
+    distinct = 200_000
+    vend = rng.choice(["1", "2", "4"], distinct, p=[0.35, 0.6, 0.05])
+    fare = rng.gamma(2.0, 7.0, distinct)
+    lines = []
+    for i in range(distinct):
+        d = int(rng.integers(1, 29))
+        h = int(rng.integers(0, 24))
+        m = int(rng.integers(0, 60))
+        dist = rng.gamma(1.5, 2.0)
+        f = fare[i]
+        tip = round(f * rng.choice([0, 0.1, 0.2]), 2)
+        lines.append(f"{vend[i]},2019-01-{d:02d} {h:02d}:{m:02d}:00,2019-01-{d:02d} {h:02d}:{(m + 9) % 60:02d}:00,"
+                     f"{int(rng.integers(1, 7))},{dist:.2f},1,N,{int(rng.integers(1, 266))},{int(rng.integers(1, 266))},"
+                     f"{int(rng.integers(1, 5))},{f:.2f},0.5,0.5,{tip:.2f},0,0.3,{f + tip + 1.3:.2f},2.5")
+    enc = np.array([ln.encode() + b"\n" for ln in lines], dtype=object)
+    pick = rng.integers(0, distinct, rows)
+    with open(path, "wb") as fh:
+        fh.write(HEADER.encode() + b"\n")
+        for s in range(0, rows, 1_000_000):
+            fh.write(b"".join(enc[pick[s:s + 1_000_000]]))
+
+
+def timed(ctx, fn, reps=5):
+    fn()
+    ts = []
+    for _ in range(reps):
+        s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        s.record()
+        out = fn()
+        e.record()
+        e.synchronize()
+        ts.append(s.elapsed_time(e))
+    return statistics.median(ts), out
+
+
+def main():
+    rows = int(sys.argv[1]) if len(sys.argv) > 1 else 4_000_000
+    path = pathlib.Path("/tmp") / f"yc-synthetic-{rows}.csv"
+    if not path.exists():
+        t0 = time.time()
+        make_csv(path, rows)
+        print(f"generated {path} in {time.time() - t0:.1f}s", file=sys.stderr)
+    nbytes = path.stat().st_size
+    ctx = Context.get(0)
+    ds = CsvDataSource(str(path), True, 0, ctx=ctx)
+    names = [f.name for f in ds.schema().fields]
+    idx = [names.index("VendorID"), names.index("fare_amount")]
+    raw = np.fromfile(path, dtype=np.uint8)
+    host = torch.from_numpy(raw).pin_memory()
+    dev = torch.empty(nbytes, dtype=torch.uint8, device=ctx.torch_device)
+
+    ms_up, _ = timed(ctx, lambda: dev.copy_(host, non_blocking=True))
+    ms_scan, cols = timed(ctx, lambda: ds._parse(ctx, dev, nbytes, idx))
+    vendor, fare_s = cols
+
+    def cast():
+        out = DeviceColumn.empty(N.TYPE_FLOAT64, fare_s.length, False, ctx=ctx)
+        ic, oc = fare_s.as_c(), out.as_c()
+        N.check(N.lib().qe_cast_utf8_to_f64(ctx.handle, N.C.byref(ic), N.C.byref(oc), None))
+        return out
+
+    ms_cast, fare = timed(ctx, cast)
+
+    def agg():
+        st = HashAggregateState(ctx, [N.TYPE_UTF8], [(N.AGG_MAX, N.TYPE_FLOAT64)], 16)
+        st.update([vendor], [fare])
+        return st.finalize()
+
+    ms_agg, (keys, vals) = timed(ctx, agg)
+    got = dict(zip(keys[0].to_pylist(), vals[0].to_pylist()))
+    n = vendor.length
+    check = None
+    try:
+        import pandas as pd
+
+        df = pd.read_csv(path, usecols=["VendorID", "fare_amount"], dtype={"VendorID": str},
+                         float_precision="round_trip")
+        want = df.groupby("VendorID")["fare_amount"].max().to_dict()
+        check = all(got.get(k) == v for k, v in want.items()) and len(want) == len(got)
+    except Exception as e:  # pandas missing or different parsing: report, do not fail the bench
+        print("pandas check skipped:", e, file=sys.stderr)
+    device_ms = ms_scan + ms_cast + ms_agg
+    print(json.dumps({
+        "workload": "SELECT VendorID, MAX(CAST(fare_amount AS double)) FROM tripdata GROUP BY VendorID (K:1336)",
+        "rows": n, "csv_bytes": nbytes, "groups": got, "check_vs_pandas": check,
+        "ms": {"upload_pcie": ms_up, "scan": ms_scan, "cast": ms_cast, "agg": ms_agg, "device_total": device_ms},
+        "rows_per_s_device": n / (device_ms * 1e-3), "csv_GBps_device": nbytes / (device_ms * 1e-3) / 1e9,
+        "csv_GBps_scan": nbytes / (ms_scan * 1e-3) / 1e9, "pcie_GBps": nbytes / (ms_up * 1e-3) / 1e9,
+    }))
+
+
+if __name__ == "__main__":
+    main()
