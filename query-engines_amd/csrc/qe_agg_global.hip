@@ -185,7 +185,7 @@ __global__ void __launch_bounds__(256) k_agg_global_f64_dense(const int64_t* __r
     for (int q = 0; q < 4; ++q) {
       const int64_t r0 = base + 128 * q + 2 * lane;
       if (full) {
-        const i64x2 t = *(const i64x2*)(vals + r0);
+        const i64x2 t = __builtin_nontemporal_load((const i64x2*)(vals + r0));  // once-read stream
         d[2 * q] = bits_f64(t.x);
         d[2 * q + 1] = bits_f64(t.y);
       } else {

@@ -39,6 +39,7 @@ typedef unsigned int qu32;
 typedef unsigned short qu16;
 typedef unsigned char qu8;
 typedef long long qi64x2 __attribute__((ext_vector_type(2)));
+typedef int qi32x2 __attribute__((ext_vector_type(2)));
 
 constexpr qi64 EMPTY_KEY = (qi64)0x8000000000000000ull;  // LDS/global slot sentinel (INT64_MIN)
 constexpr qu64 NULL_SALT = 0x6A09E667F3BCC909ull;

@@ -120,6 +120,13 @@ struct StreamCols {
   int32_t ncols;
 };
 
+template <bool NT>
+__device__ __forceinline__ i64x2_rt ld16(const i64x2_rt* p) {
+  if (NT) return __builtin_nontemporal_load(p);
+  return *p;
+}
+
+template <bool NT>
 __global__ void __launch_bounds__(512) k_stream_read(StreamCols c, unsigned long long* out) {
   unsigned long long acc = 0;
   const int64_t tid = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
@@ -129,7 +136,8 @@ __global__ void __launch_bounds__(512) k_stream_read(StreamCols c, unsigned long
     const int64_t n = c.n16[k];
     int64_t i = tid;
     for (; i + 3 * nthr < n; i += 4 * nthr) {
-      const i64x2_rt a = p[i], b = p[i + nthr], d = p[i + 2 * nthr], e = p[i + 3 * nthr];
+      const i64x2_rt a = ld16<NT>(p + i), b = ld16<NT>(p + i + nthr), d = ld16<NT>(p + i + 2 * nthr),
+                     e = ld16<NT>(p + i + 3 * nthr);
       acc ^= (unsigned long long)(a.x ^ a.y ^ b.x ^ b.y ^ d.x ^ d.y ^ e.x ^ e.y);
     }
     for (; i < n; i += nthr) acc ^= (unsigned long long)(p[i].x ^ p[i].y);
@@ -250,7 +258,12 @@ int qe_stream_read(qe_ctx* ctx, const qe_column* cols, int32_t ncols, double* ms
   QE_HIP(hipEventCreate(&e0));
   QE_HIP(hipEventCreate(&e1));
   QE_HIP(hipEventRecord(e0, ctx->stream));
-  hipLaunchKernelGGL(k_stream_read, dim3(ctx->num_cus * 4), dim3(512), 0, ctx->stream, c, (unsigned long long*)s);
+  if (!(getenv("QE_NT") && getenv("QE_NT")[0] == '0'))  // non-temporal (default), as the fused kernels
+    hipLaunchKernelGGL(k_stream_read<true>, dim3(ctx->num_cus * 4), dim3(512), 0, ctx->stream, c,
+                       (unsigned long long*)s);
+  else
+    hipLaunchKernelGGL(k_stream_read<false>, dim3(ctx->num_cus * 4), dim3(512), 0, ctx->stream, c,
+                       (unsigned long long*)s);
   QE_HIP(hipEventRecord(e1, ctx->stream));
   QE_HIP(hipEventSynchronize(e1));
   float f = 0.f;
