@@ -359,6 +359,13 @@ int qe_strdict_decode_bytes(qe_strdict* dict, const qe_column* codes, int64_t* o
 /* out (UTF8): offsets for codes->length+1 entries, values >= decode_bytes bytes, validity
  * iff codes has one. QE_ERR_INVALID_ARG if a code was not issued by this dictionary. */
 int qe_strdict_decode(qe_strdict* dict, const qe_column* codes, qe_column* out);
+/* Composite group keys (K:621-626 `List` of key values) whose packing exceeds 63 bits: each row's
+ * tuple of up to QE_MAX_KEYS fixed-width / BOOL key columns (nulls and fp64 NaNs as
+ * List/Double.equals see them) gets a dense int32 code; codes->validity (optional) is set all-valid.
+ * A dictionary holds either strings or tuples of one layout. decode_tuple writes the key columns
+ * (types as encoded; validity where outs[k].validity is non-NULL) for `codes`. */
+int qe_strdict_encode_tuple(qe_strdict* dict, const qe_column* keys, int32_t nkeys, qe_column* codes);
+int qe_strdict_decode_tuple(qe_strdict* dict, const qe_column* codes, int32_t nkeys, qe_column* outs);
 
 /* ---- Arrow C Data Interface boundary -----------------------------------------
  * Arrow Java exports a VectorSchemaRoot (the reference's batches, K:635-650) as a struct

@@ -123,9 +123,9 @@ __device__ __forceinline__ void encode_row(const DictDev& D, const int32_t* offs
 
 // Per-workgroup LDS cache of resolved strings: low-cardinality keys (the reference's VendorID)
 // resolve without touching the global table, whose slots all rows would otherwise hit. An entry
-// is published with state 2 after its fields are written. Only keys of up to 32 bytes are cached
+// is published with state 2 after its fields are written. Only keys of up to 40 bytes are cached
 // (they compare entirely in LDS); longer keys always take the global path.
-constexpr int LC_SLOTS = 512, LC_BYTES = 32;
+constexpr int LC_SLOTS = 512, LC_BYTES = 40;
 struct LdsCache {
   uint32_t state[LC_SLOTS];  // 0 empty, 1 being written, 2 ready
   uint64_t hash[LC_SLOTS];
@@ -159,7 +159,7 @@ __global__ void __launch_bounds__(ENC_THREADS) k_dict_encode(DictDev D, const in
     int32_t len = 0;
     const uint8_t* p = bytes;
     uint64_t h = 0;
-    uint64_t hd[LC_BYTES / 8] = {0, 0, 0, 0};
+    uint64_t hd[LC_BYTES / 8] = {0, 0, 0, 0, 0};
     int c = -1;
     if (live) {
       const int32_t s0 = offs[i];
@@ -232,6 +232,228 @@ __global__ void __launch_bounds__(ENC_THREADS) k_dict_encode_retry(DictDev D, co
   }
 }
 
+// ---- composite keys: a row's key tuple as 5 words (up to 4 keys + a null-flag word) -------------
+// Key k occupies word k (fp64 NaN canonicalised: Double.equals puts every NaN in one group, and
+// +0.0 / -0.0 stay apart); word 4 holds the null flags. Every tuple is 40 bytes, so tuple arenas
+// stay 8-byte aligned and compare word by word.
+constexpr int TW = 5;
+enum : int32_t { TK_I64 = 0, TK_F64 = 1, TK_I32 = 2, TK_U8 = 3, TK_BOOL = 4 };
+struct TupleCols {
+  const void* v[QE_MAX_KEYS];
+  const uint8_t* valid[QE_MAX_KEYS];
+  int32_t kind[QE_MAX_KEYS];
+  int32_t nkeys;
+};
+
+__device__ __forceinline__ void tuple_words(const TupleCols& T, int64_t i, uint64_t (&w)[TW]) {
+  uint64_t flags = 0;
+#pragma unroll
+  for (int k = 0; k < QE_MAX_KEYS; ++k) {
+    uint64_t x = 0;
+    if (k < T.nkeys) {
+      const bool ok = !T.valid[k] || ((T.valid[k][i >> 3] >> (i & 7)) & 1);
+      if (ok) {
+        switch (T.kind[k]) {
+          case TK_I64: x = ((const uint64_t*)T.v[k])[i]; break;
+          case TK_F64: {
+            x = ((const uint64_t*)T.v[k])[i];
+            const double d = bits_f64((int64_t)x);
+            if (d != d) x = 0x7FF8000000000000ull;
+            break;
+          }
+          case TK_I32: x = (uint32_t)((const int32_t*)T.v[k])[i]; break;
+          case TK_U8: x = ((const uint8_t*)T.v[k])[i]; break;
+          default: x = (((const uint8_t*)T.v[k])[i >> 3] >> (i & 7)) & 1u; break;
+        }
+      } else {
+        flags |= 1ull << k;
+      }
+    }
+    w[k] = x;
+  }
+  w[TW - 1] = flags;
+}
+
+__device__ __forceinline__ uint64_t tuple_hash(const uint64_t (&w)[TW]) {
+  uint64_t h = 0x9E3779B97F4A7C15ull;
+#pragma unroll
+  for (int k = 0; k < TW; ++k) h = fmix64(h ^ w[k]) + 0x165667B19E3779F9ull;
+  h = fmix64(h);
+  return h ? h : 1;
+}
+
+__device__ int tuple_find_or_insert(const DictDev& D, const uint64_t (&w)[TW], uint64_t h) {
+  const int len = 8 * TW;
+  uint64_t slot = h & D.mask;
+  for (uint64_t probe = 0; probe <= D.mask; ++probe, slot = (slot + 1) & D.mask) {
+    uint64_t sh = __hip_atomic_load(&D.s_hash[slot], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (sh == 0) {
+      const uint64_t prev = atomicCAS((unsigned long long*)&D.s_hash[slot], 0ull, (unsigned long long)h);
+      if (prev == 0) {
+        int c = R_OVERFLOW;
+        const unsigned long long a = atomicAdd(D.arena_used, (unsigned long long)len);
+        if ((int64_t)(a + len) <= D.acap) {
+          const unsigned int cc = atomicAdd(D.ncodes, 1u);
+          if ((int64_t)cc < D.ccap) {
+            uint64_t* dst = (uint64_t*)(D.arena + a);
+#pragma unroll
+            for (int k = 0; k < TW; ++k) dst[k] = w[k];
+            D.code_off[cc] = (int64_t)a;
+            D.code_len[cc] = len;
+            D.code_hash[cc] = h;
+            c = (int)cc;
+          }
+        }
+        __threadfence();
+        __hip_atomic_store(&D.s_code[slot], c, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+        if (c < 0) atomicOr(&D.flags[0], 1u);
+        return c;
+      }
+      sh = prev;
+    }
+    if (sh == h) {
+      const int c = __hip_atomic_load(&D.s_code[slot], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
+      if (c == -1) return R_RETRY;
+      if (c == R_OVERFLOW) return R_OVERFLOW;
+      const uint64_t* t = (const uint64_t*)(D.arena + D.code_off[c]);
+      bool eq = true;
+#pragma unroll
+      for (int k = 0; k < TW; ++k) eq &= t[k] == w[k];
+      if (eq) return c;
+    }
+  }
+  atomicOr(&D.flags[0], 1u);
+  return R_OVERFLOW;
+}
+
+__global__ void __launch_bounds__(ENC_THREADS) k_tuple_encode(DictDev D, TupleCols T, int64_t n,
+                                                              int32_t* __restrict__ codes,
+                                                              uint32_t* __restrict__ retry) {
+  __shared__ LdsCache C;
+  for (int k = threadIdx.x; k < LC_SLOTS; k += blockDim.x) C.state[k] = 0;
+  __syncthreads();
+  const int lane = threadIdx.x & 63;
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  const int64_t start = blockIdx.x * (int64_t)blockDim.x + threadIdx.x - lane;
+  for (int64_t i0 = start; i0 < n; i0 += stride) {
+    const int64_t i = i0 + lane;
+    const bool live = i < n;
+    uint64_t w[TW] = {0, 0, 0, 0, 0};
+    uint64_t h = 0;
+    int c = -1;
+    if (live) {
+      tuple_words(T, i, w);
+      h = tuple_hash(w);
+      const int slot = (int)(h & (LC_SLOTS - 1));
+      if (__hip_atomic_load(&C.state[slot], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) == 2 && C.hash[slot] == h) {
+        bool eq = true;
+#pragma unroll
+        for (int k = 0; k < TW; ++k) eq &= C.head[slot][k] == w[k];
+        if (eq) c = C.code[slot];
+      }
+    }
+    uint64_t todo = __ballot(live && c < 0);
+    while (todo) {
+      const int leader = __ffsll((long long)todo) - 1;
+      bool same = (todo >> lane) & 1;
+#pragma unroll
+      for (int k = 0; k < TW; ++k) same = same && w[k] == __shfl(w[k], leader);
+      const uint64_t grp = __ballot(same);
+      int code = 0;
+      if (lane == leader) {
+        code = tuple_find_or_insert(D, w, h);
+        const int slot = (int)(h & (LC_SLOTS - 1));
+        if (code >= 0 && atomicCAS(&C.state[slot], 0u, 1u) == 0u) {
+          C.hash[slot] = h;
+          C.len[slot] = 8 * TW;
+          C.code[slot] = code;
+#pragma unroll
+          for (int k = 0; k < TW; ++k) C.head[slot][k] = w[k];
+          __hip_atomic_store(&C.state[slot], 2u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+        }
+      }
+      code = __shfl(code, leader);
+      if (same) c = code;
+      todo &= ~grp;
+    }
+    if (live) {
+      codes[i] = c >= 0 ? c : 0;
+      if (c == R_RETRY) {
+        atomicOr(&retry[i >> 5], 1u << (i & 31));
+        atomicAdd(&D.flags[1], 1u);
+      }
+    }
+  }
+}
+
+__global__ void __launch_bounds__(ENC_THREADS) k_tuple_encode_retry(DictDev D, TupleCols T, int64_t n,
+                                                                    int32_t* __restrict__ codes,
+                                                                    const uint32_t* __restrict__ retry_in,
+                                                                    uint32_t* __restrict__ retry_out) {
+  const int64_t words = (n + 31) >> 5;
+  for (int64_t wd = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; wd < words; wd += (int64_t)gridDim.x * blockDim.x) {
+    uint32_t bits = retry_in[wd];
+    while (bits) {
+      const int j = __builtin_ctz(bits);
+      bits &= bits - 1;
+      const int64_t i = (wd << 5) + j;
+      uint64_t w[TW];
+      tuple_words(T, i, w);
+      const int c = tuple_find_or_insert(D, w, tuple_hash(w));
+      codes[i] = c >= 0 ? c : 0;
+      if (c == R_RETRY) {
+        atomicOr(&retry_out[i >> 5], 1u << (i & 31));
+        atomicAdd(&D.flags[1], 1u);
+      }
+    }
+  }
+}
+
+struct TupleOut {
+  void* v[QE_MAX_KEYS];
+  uint8_t* valid[QE_MAX_KEYS];  // byte-addressed; 8 rows per thread own one byte each
+  int32_t kind[QE_MAX_KEYS];
+  int32_t nkeys;
+};
+
+__global__ void k_tuple_decode(const int32_t* __restrict__ codes, int64_t n, int64_t ncodes,
+                               const int64_t* __restrict__ code_off, const uint8_t* __restrict__ arena, TupleOut O,
+                               unsigned int* __restrict__ bad) {
+  const int64_t groups = (n + 7) >> 3;
+  for (int64_t g = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; g < groups; g += (int64_t)gridDim.x * blockDim.x) {
+    uint8_t vb[QE_MAX_KEYS] = {0, 0, 0, 0};
+    uint8_t bb[QE_MAX_KEYS] = {0, 0, 0, 0};
+    for (int j = 0; j < 8; ++j) {
+      const int64_t i = (g << 3) + j;
+      if (i >= n) break;
+      const int32_t c = codes[i];
+      if (c < 0 || c >= ncodes) {
+        atomicOr(bad, 1u);
+        continue;
+      }
+      const uint64_t* t = (const uint64_t*)(arena + code_off[c]);
+      const uint64_t flags = t[TW - 1];
+#pragma unroll
+      for (int k = 0; k < QE_MAX_KEYS; ++k) {
+        if (k >= O.nkeys) break;
+        const uint64_t x = t[k];
+        if (!((flags >> k) & 1)) vb[k] |= (uint8_t)(1u << j);
+        switch (O.kind[k]) {
+          case TK_I64:
+          case TK_F64: ((uint64_t*)O.v[k])[i] = x; break;
+          case TK_I32: ((uint32_t*)O.v[k])[i] = (uint32_t)x; break;
+          case TK_U8: ((uint8_t*)O.v[k])[i] = (uint8_t)x; break;
+          default: bb[k] |= (uint8_t)((x & 1u) << j); break;
+        }
+      }
+    }
+    for (int k = 0; k < O.nkeys; ++k) {
+      if (O.valid[k]) O.valid[k][g] = vb[k];
+      if (O.kind[k] == TK_BOOL) ((uint8_t*)O.v[k])[g] = bb[k];
+    }
+  }
+}
+
 __global__ void k_dict_rebuild(DictDev D, int64_t ncodes) {
   for (int64_t c = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; c < ncodes; c += (int64_t)gridDim.x * blockDim.x) {
     const uint64_t h = D.code_hash[c];
@@ -295,6 +517,9 @@ struct qe_strdict {
   uint8_t* ctl = nullptr;
   int64_t ncodes = 0;
   int64_t arena_used = 0;
+  int32_t mode = 0;  // 0 unused, 1 strings, 2 key tuples (kinds below)
+  int32_t tuple_nkeys = 0;
+  int32_t tuple_type[QE_MAX_KEYS] = {0, 0, 0, 0};
 
   unsigned int* d_ncodes() { return (unsigned int*)ctl; }
   unsigned long long* d_arena_used() { return (unsigned long long*)(ctl + 8); }
@@ -414,55 +639,40 @@ int qe_strdict_size(qe_strdict* d, int64_t* n) {
   return QE_OK;
 }
 
-int qe_strdict_encode(qe_strdict* d, const qe_column* in, qe_column* codes) {
-  QE_CHECK(d && in && codes, QE_ERR_INVALID_ARG, "null argument");
+}  // extern "C"
+
+namespace {
+
+// Pass 1 over all rows, retry passes until every row resolved; on overflow grow the code arrays /
+// arena, rebuild the slots and run the batch again (re-encoding is idempotent).
+template <typename Pass1, typename Retry>
+int encode_loop(qe_strdict* d, int64_t n, int64_t batch_bytes, Pass1 pass1, Retry retry_pass) {
   qe_ctx* ctx = d->ctx;
-  QE_TRY(ctx_enter(ctx));
-  QE_CHECK(in->type == QE_TYPE_UTF8 && in->offsets, QE_ERR_UNSUPPORTED, "string dictionary input must be UTF8");
-  QE_CHECK(codes->type == QE_TYPE_INT32, QE_ERR_INVALID_ARG, "codes column must be INT32");
-  const int64_t n = in->length;
-  QE_CHECK(codes->length >= n && (codes->values || n == 0), QE_ERR_CAPACITY, "codes column too small");
-  QE_CHECK(!in->validity || codes->validity, QE_ERR_INVALID_ARG, "codes validity buffer required");
-  codes->length = n;
-  if (n == 0) return QE_OK;
-  if (in->validity)
-    QE_HIP(hipMemcpyAsync(codes->validity, in->validity, (size_t)div_up((uint64_t)n, 32) * 4, hipMemcpyDeviceToDevice,
-                          ctx->stream));
   const int64_t words = (int64_t)div_up((uint64_t)n, 32);
   void* s;
   QE_TRY(ctx_scratch(ctx, (size_t)words * 8, &s));
   uint32_t* retry[2] = {(uint32_t*)s, (uint32_t*)s + words};
-  const int grid = (int)std::min<int64_t>((int64_t)div_up((uint64_t)n, ENC_THREADS), (int64_t)ctx->num_cus * 16);
   for (int attempt = 0; attempt < 64; ++attempt) {
     QE_HIP(hipMemsetAsync(retry[0], 0, (size_t)words * 4, ctx->stream));
     QE_HIP(hipMemsetAsync(d->d_flags(), 0, 8, ctx->stream));
-    hipLaunchKernelGGL(k_dict_encode, dim3(grid), dim3(ENC_THREADS), 0, ctx->stream, d->dev(), in->offsets,
-                       (const uint8_t*)in->values, in->validity, n, (int32_t*)codes->values, retry[0]);
-    QE_TRY(launch_check("k_dict_encode"));
+    QE_TRY(pass1(retry[0]));
     uint32_t ovf = 0, unres = 0;
     QE_TRY(read_ctl(d, &ovf, &unres));
     int cur = 0;
     for (int pass = 0; pass < 64 && unres && !ovf; ++pass) {
       QE_HIP(hipMemsetAsync(retry[1 - cur], 0, (size_t)words * 4, ctx->stream));
       QE_HIP(hipMemsetAsync(d->d_flags() + 1, 0, 4, ctx->stream));
-      const int g2 = (int)std::min<int64_t>((int64_t)div_up((uint64_t)words, 256), (int64_t)ctx->num_cus * 4);
-      hipLaunchKernelGGL(k_dict_encode_retry, dim3(g2), dim3(256), 0, ctx->stream, d->dev(), in->offsets,
-                         (const uint8_t*)in->values, n, (int32_t*)codes->values, retry[cur], retry[1 - cur]);
-      QE_TRY(launch_check("k_dict_encode_retry"));
+      QE_TRY(retry_pass(retry[cur], retry[1 - cur], words));
       QE_TRY(read_ctl(d, &ovf, &unres));
       cur = 1 - cur;
     }
     if (!ovf && !unres) return QE_OK;
     // grow: codes x4 (slots follow), arena to twice what is in use plus this batch's bytes
-    int32_t o[2] = {0, 0};
-    QE_HIP(hipMemcpy(o, in->offsets + n, 4, hipMemcpyDeviceToHost));
-    QE_HIP(hipMemcpy(o + 1, in->offsets, 4, hipMemcpyDeviceToHost));
-    const int64_t batch_bytes = (int64_t)o[0] - o[1];
     const int64_t new_ccap = d->ncodes * 2 >= d->ccap ? d->ccap * 4 : d->ccap;
     const int64_t used = std::min<int64_t>(d->arena_used, d->acap);
     const int64_t new_acap = d->arena_used + 64 > d->acap ? std::max<int64_t>(d->acap * 2, used * 2 + batch_bytes)
                                                            : d->acap;
-    QE_CHECK(new_ccap <= (1ll << 31), QE_ERR_CAPACITY, "more than 2^31 distinct strings");
+    QE_CHECK(new_ccap <= (1ll << 31), QE_ERR_CAPACITY, "more than 2^31 distinct keys");
     if (new_ccap != d->ccap) {
       QE_TRY(grow_array(ctx, &d->code_off, d->ncodes, new_ccap));
       QE_TRY(grow_array(ctx, &d->code_len, d->ncodes, new_ccap));
@@ -474,10 +684,146 @@ int qe_strdict_encode(qe_strdict* d, const qe_column* in, qe_column* codes) {
       d->acap = new_acap;
     }
     if (d->arena_used > d->acap) d->arena_used = used;  // drop reservations past the old end
+    if (d->mode == 2) d->arena_used = (d->arena_used + 7) & ~7ll;  // tuples stay 8-byte aligned
     QE_TRY(write_ctl(d));
     QE_TRY(grow_slots(d, (uint64_t)d->ccap * 2));  // also clears failed (-2) slots
   }
-  return fail(QE_ERR_DEVICE, "string dictionary did not converge");
+  return fail(QE_ERR_DEVICE, "key dictionary did not converge");
+}
+
+int32_t tuple_kind(int32_t type) {
+  switch (type) {
+    case QE_TYPE_INT64: return TK_I64;
+    case QE_TYPE_FLOAT64: return TK_F64;
+    case QE_TYPE_INT32:
+    case QE_TYPE_DATE32: return TK_I32;
+    case QE_TYPE_UINT8: return TK_U8;
+    case QE_TYPE_BOOL: return TK_BOOL;
+    default: return -1;
+  }
+}
+
+}  // namespace
+
+extern "C" {
+
+int qe_strdict_encode(qe_strdict* d, const qe_column* in, qe_column* codes) {
+  QE_CHECK(d && in && codes, QE_ERR_INVALID_ARG, "null argument");
+  qe_ctx* ctx = d->ctx;
+  QE_TRY(ctx_enter(ctx));
+  QE_CHECK(in->type == QE_TYPE_UTF8 && in->offsets, QE_ERR_UNSUPPORTED, "string dictionary input must be UTF8");
+  QE_CHECK(d->mode != 2, QE_ERR_INVALID_ARG, "dictionary holds key tuples, not strings");
+  QE_CHECK(codes->type == QE_TYPE_INT32, QE_ERR_INVALID_ARG, "codes column must be INT32");
+  const int64_t n = in->length;
+  QE_CHECK(codes->length >= n && (codes->values || n == 0), QE_ERR_CAPACITY, "codes column too small");
+  QE_CHECK(!in->validity || codes->validity, QE_ERR_INVALID_ARG, "codes validity buffer required");
+  d->mode = 1;
+  codes->length = n;
+  if (n == 0) return QE_OK;
+  if (in->validity)
+    QE_HIP(hipMemcpyAsync(codes->validity, in->validity, (size_t)div_up((uint64_t)n, 32) * 4, hipMemcpyDeviceToDevice,
+                          ctx->stream));
+  int32_t o[2] = {0, 0};
+  QE_HIP(hipMemcpy(o, in->offsets + n, 4, hipMemcpyDeviceToHost));
+  QE_HIP(hipMemcpy(o + 1, in->offsets, 4, hipMemcpyDeviceToHost));
+  const int grid = (int)std::min<int64_t>((int64_t)div_up((uint64_t)n, ENC_THREADS), (int64_t)ctx->num_cus * 16);
+  return encode_loop(
+      d, n, (int64_t)o[0] - o[1],
+      [&](uint32_t* retry) {
+        hipLaunchKernelGGL(k_dict_encode, dim3(grid), dim3(ENC_THREADS), 0, ctx->stream, d->dev(), in->offsets,
+                           (const uint8_t*)in->values, in->validity, n, (int32_t*)codes->values, retry);
+        return launch_check("k_dict_encode");
+      },
+      [&](const uint32_t* rin, uint32_t* rout, int64_t words) {
+        const int g2 = (int)std::min<int64_t>((int64_t)div_up((uint64_t)words, 256), (int64_t)ctx->num_cus * 4);
+        hipLaunchKernelGGL(k_dict_encode_retry, dim3(g2), dim3(256), 0, ctx->stream, d->dev(), in->offsets,
+                           (const uint8_t*)in->values, n, (int32_t*)codes->values, rin, rout);
+        return launch_check("k_dict_encode_retry");
+      });
+}
+
+int qe_strdict_encode_tuple(qe_strdict* d, const qe_column* keys, int32_t nkeys, qe_column* codes) {
+  QE_CHECK(d && keys && codes, QE_ERR_INVALID_ARG, "null argument");
+  qe_ctx* ctx = d->ctx;
+  QE_TRY(ctx_enter(ctx));
+  QE_CHECK(nkeys >= 1 && nkeys <= QE_MAX_KEYS, QE_ERR_UNSUPPORTED, "key tuples take 1..%d columns", QE_MAX_KEYS);
+  QE_CHECK(d->mode != 1, QE_ERR_INVALID_ARG, "dictionary holds strings, not key tuples");
+  QE_CHECK(codes->type == QE_TYPE_INT32, QE_ERR_INVALID_ARG, "codes column must be INT32");
+  const int64_t n = keys[0].length;
+  TupleCols T{};
+  T.nkeys = nkeys;
+  for (int k = 0; k < nkeys; ++k) {
+    QE_CHECK(keys[k].length == n, QE_ERR_INVALID_ARG, "key %d has %lld rows, key 0 %lld", k,
+             (long long)keys[k].length, (long long)n);
+    const int32_t kind = tuple_kind(keys[k].type);
+    QE_CHECK(kind >= 0, QE_ERR_UNSUPPORTED, "key %d: type %d cannot be part of a key tuple (encode UTF8 first)", k,
+             keys[k].type);
+    QE_CHECK(keys[k].values || n == 0, QE_ERR_INVALID_ARG, "key %d: null values", k);
+    if (d->mode == 2)
+      QE_CHECK(d->tuple_nkeys == nkeys && d->tuple_type[k] == keys[k].type, QE_ERR_INVALID_ARG,
+               "key %d: type %d differs from the dictionary's tuple layout", k, keys[k].type);
+    T.v[k] = keys[k].values;
+    T.valid[k] = keys[k].validity;
+    T.kind[k] = kind;
+  }
+  QE_CHECK(codes->length >= n && (codes->values || n == 0), QE_ERR_CAPACITY, "codes column too small");
+  if (d->mode == 0) {
+    d->mode = 2;
+    d->tuple_nkeys = nkeys;
+    for (int k = 0; k < nkeys; ++k) d->tuple_type[k] = keys[k].type;
+  }
+  codes->length = n;
+  if (n == 0) return QE_OK;
+  if (codes->validity)  // a tuple with null members is still a (non-null) group key
+    QE_HIP(hipMemsetAsync(codes->validity, 0xFF, (size_t)div_up((uint64_t)n, 32) * 4, ctx->stream));
+  const int grid = (int)std::min<int64_t>((int64_t)div_up((uint64_t)n, ENC_THREADS), (int64_t)ctx->num_cus * 16);
+  return encode_loop(
+      d, n, 8 * TW * std::min<int64_t>(n, 1 << 20),
+      [&](uint32_t* retry) {
+        hipLaunchKernelGGL(k_tuple_encode, dim3(grid), dim3(ENC_THREADS), 0, ctx->stream, d->dev(), T, n,
+                           (int32_t*)codes->values, retry);
+        return launch_check("k_tuple_encode");
+      },
+      [&](const uint32_t* rin, uint32_t* rout, int64_t words) {
+        const int g2 = (int)std::min<int64_t>((int64_t)div_up((uint64_t)words, 256), (int64_t)ctx->num_cus * 4);
+        hipLaunchKernelGGL(k_tuple_encode_retry, dim3(g2), dim3(256), 0, ctx->stream, d->dev(), T, n,
+                           (int32_t*)codes->values, rin, rout);
+        return launch_check("k_tuple_encode_retry");
+      });
+}
+
+int qe_strdict_decode_tuple(qe_strdict* d, const qe_column* codes, int32_t nkeys, qe_column* outs) {
+  QE_CHECK(d && codes && outs, QE_ERR_INVALID_ARG, "null argument");
+  qe_ctx* ctx = d->ctx;
+  QE_TRY(ctx_enter(ctx));
+  QE_CHECK(d->mode == 2 && d->tuple_nkeys == nkeys, QE_ERR_INVALID_ARG, "dictionary does not hold %d-key tuples",
+           nkeys);
+  QE_CHECK(codes->type == QE_TYPE_INT32, QE_ERR_INVALID_ARG, "codes column must be INT32");
+  const int64_t n = codes->length;
+  TupleOut O{};
+  O.nkeys = nkeys;
+  for (int k = 0; k < nkeys; ++k) {
+    QE_CHECK(outs[k].type == d->tuple_type[k], QE_ERR_INVALID_ARG, "output %d: type %d, tuple holds %d", k,
+             outs[k].type, d->tuple_type[k]);
+    QE_CHECK(outs[k].length >= n && (outs[k].values || n == 0), QE_ERR_CAPACITY, "output %d too small", k);
+    O.v[k] = outs[k].values;
+    O.valid[k] = outs[k].validity;
+    O.kind[k] = tuple_kind(outs[k].type);
+    outs[k].length = n;
+  }
+  if (n == 0) return QE_OK;
+  void* s;
+  QE_TRY(ctx_scratch(ctx, 8, &s));
+  QE_HIP(hipMemsetAsync(s, 0, 4, ctx->stream));
+  const int grid = (int)std::min<int64_t>((int64_t)div_up(div_up((uint64_t)n, 8), 256), (int64_t)ctx->num_cus * 8);
+  hipLaunchKernelGGL(k_tuple_decode, dim3(grid), dim3(256), 0, ctx->stream, (const int32_t*)codes->values, n,
+                     d->ncodes, d->code_off, d->arena, O, (unsigned int*)s);
+  QE_TRY(launch_check("k_tuple_decode"));
+  uint32_t bad = 0;
+  QE_HIP(hipMemcpyAsync(&bad, s, 4, hipMemcpyDeviceToHost, ctx->stream));
+  QE_HIP(hipStreamSynchronize(ctx->stream));
+  QE_CHECK(bad == 0, QE_ERR_INVALID_ARG, "code out of range for this dictionary");
+  return QE_OK;
 }
 
 int qe_strdict_decode_bytes(qe_strdict* d, const qe_column* codes, int64_t* out_bytes) {

@@ -17,6 +17,21 @@ def output_type(fn: int, input_type: int) -> int:
     return input_type
 
 
+_KEY_BITS = {N.TYPE_INT32: 32, N.TYPE_DATE32: 32, N.TYPE_UINT8: 8}
+
+
+def packable(key_types) -> bool:
+    """Whether qe_hashagg packs these keys itself (one int64/fp64 key, or narrow keys whose values
+    plus null bits fit 63 bits — qe_hashagg_create's rule)."""
+    if len(key_types) == 0:
+        return True
+    if len(key_types) == 1 and key_types[0] in (N.TYPE_INT64, N.TYPE_FLOAT64):
+        return True
+    if any(t not in _KEY_BITS for t in key_types) or len(key_types) > N.MAX_KEYS:
+        return False
+    return sum(_KEY_BITS[t] + 1 for t in key_types) <= 63
+
+
 class HashAggregateState:
     """Owns one qe_hashagg. Keys: ``key_types``; aggregates: (fn, input_type) pairs."""
 
@@ -30,17 +45,26 @@ class HashAggregateState:
         # UTF-8 keys: grouped by their dictionary code (INT32), decoded in finalize
         self.dicts = {i: StringDictionary(ctx, expected_groups) for i, t in enumerate(self.key_types)
                       if t == N.TYPE_UTF8}
-        self.device_key_types = [N.TYPE_INT32 if t == N.TYPE_UTF8 else t for t in self.key_types]
-        kt = (N.C.c_int32 * max(1, len(self.key_types)))(*self.device_key_types)
+        self.member_types = [N.TYPE_INT32 if t == N.TYPE_UTF8 else t for t in self.key_types]
+        # key sets that do not pack into 63 bits group by one code per distinct key tuple
+        self.tuple_dict = None
+        if not packable(self.member_types):
+            if len(self.member_types) > N.MAX_KEYS:
+                raise N.IllegalStateException(N.QE_ERR_UNSUPPORTED, f"at most {N.MAX_KEYS} group keys")
+            self.tuple_dict = StringDictionary(ctx, expected_groups)
+        self.device_key_types = [N.TYPE_INT32] if self.tuple_dict is not None else list(self.member_types)
+        kt = (N.C.c_int32 * max(1, len(self.device_key_types)))(*self.device_key_types)
         ad = (N.QeAggDesc * max(1, len(self.aggs)))(*[N.QeAggDesc(f, t) for f, t in self.aggs])
         h = N.C.c_void_p()
-        N.check(N.lib().qe_hashagg_create(ctx.handle, len(self.key_types), kt, len(self.aggs), ad,
+        N.check(N.lib().qe_hashagg_create(ctx.handle, len(self.device_key_types), kt, len(self.aggs), ad,
                                           int(expected_groups), N.C.byref(h)))
         self.handle = h
 
     def close(self) -> None:
         for d in getattr(self, "dicts", {}).values():
             d.close()
+        if getattr(self, "tuple_dict", None) is not None:
+            self.tuple_dict.close()
         if getattr(self, "handle", None) is not None:
             N.lib().qe_hashagg_destroy(self.handle)
             self.handle = None
@@ -55,6 +79,8 @@ class HashAggregateState:
     def update(self, keys: Sequence[DeviceColumn], inputs: Sequence[Optional[DeviceColumn]],
                mask: Optional[DeviceColumn] = None) -> None:
         keys = [self.dicts[i].encode(k) if i in self.dicts else k for i, k in enumerate(keys)]
+        if self.tuple_dict is not None:
+            keys = [self.tuple_dict.encode_tuple(keys)]
         kc = (N.QeColumn * max(1, len(keys)))(*[k.as_c() for k in keys])
         ic = (N.QeColumn * max(1, len(self.aggs)))(
             *[(x.as_c() if x is not None else N.QeColumn()) for x in inputs])
@@ -62,8 +88,8 @@ class HashAggregateState:
         N.check(N.lib().qe_hashagg_update(self.handle, kc, ic, N.C.byref(mc) if mc is not None else None))
 
     def update_fused(self, cols: Sequence[DeviceColumn], spec: N.QeFusedSpec) -> None:
-        if self.dicts:
-            raise N.IllegalStateException(N.QE_ERR_UNSUPPORTED, "fused update with UTF-8 keys")
+        if self.dicts or self.tuple_dict is not None:
+            raise N.IllegalStateException(N.QE_ERR_UNSUPPORTED, "fused update with dictionary-encoded keys")
         cc = (N.QeColumn * len(cols))(*[c.as_c() for c in cols])
         N.check(N.lib().qe_hashagg_update_fused(self.handle, cc, len(cols), N.C.byref(spec)))
 
@@ -105,6 +131,8 @@ class HashAggregateState:
         N.check(N.lib().qe_hashagg_finalize(self.handle, kc, ac, N.C.byref(out)))
         for c in keys + aggs:
             c.length = out.value
+        if self.tuple_dict is not None:
+            keys = self.tuple_dict.decode_tuple(keys[0], self.member_types)
         keys = [self.dicts[i].decode(k) if i in self.dicts else k for i, k in enumerate(keys)]
         return keys, aggs
 
@@ -115,7 +143,7 @@ class HashAggregateState:
         return n.value
 
     def _check_exportable(self) -> None:
-        if self.dicts:  # codes are local to this state's dictionary
+        if self.dicts or self.tuple_dict is not None:  # codes are local to this state's dictionary
             raise N.IllegalStateException(N.QE_ERR_UNSUPPORTED,
                                           "partial records with UTF-8 keys are not exchangeable yet")
 

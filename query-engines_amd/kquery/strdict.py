@@ -57,3 +57,19 @@ class StringDictionary:
         oc = out.as_c()
         N.check(N.lib().qe_strdict_decode(self.handle, N.C.byref(cc), N.C.byref(oc)))
         return out
+
+    def encode_tuple(self, cols) -> DeviceColumn:
+        """Composite key columns (fixed-width / BOOL, nullable) -> INT32 tuple codes (non-null)."""
+        n = cols[0].length
+        out = DeviceColumn.empty(N.TYPE_INT32, n, False, ctx=self.ctx)
+        kc = (N.QeColumn * len(cols))(*[c.as_c() for c in cols])
+        oc = out.as_c()
+        N.check(N.lib().qe_strdict_encode_tuple(self.handle, kc, len(cols), N.C.byref(oc)))
+        return out
+
+    def decode_tuple(self, codes: DeviceColumn, types) -> list:
+        outs = [DeviceColumn.empty(t, codes.length, True, ctx=self.ctx) for t in types]
+        cc = codes.as_c()
+        oc = (N.QeColumn * len(outs))(*[o.as_c() for o in outs])
+        N.check(N.lib().qe_strdict_decode_tuple(self.handle, N.C.byref(cc), len(outs), oc))
+        return outs

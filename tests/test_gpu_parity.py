@@ -388,9 +388,15 @@ def test_hashagg_f64_key_and_multibatch_order(agg_ctx):
 
 
 def test_hashagg_multi_key_too_wide(gpu_ctx):
-    """Two 32-bit keys + null bits exceed the packed 63-bit key: rejected loudly."""
-    with pytest.raises(N.IllegalStateException):
-        HashAggregateState(gpu_ctx, [N.TYPE_INT32, N.TYPE_DATE32], [(N.AGG_COUNT_STAR, N.TYPE_INT64)], 16)
+    """Two 32-bit keys + null bits exceed the packed 63-bit key: the C ABI rejects the packing
+    loudly; HashAggregateState then groups by key-tuple codes (tests/test_tuplekeys.py)."""
+    kt = (N.C.c_int32 * 2)(N.TYPE_INT32, N.TYPE_DATE32)
+    ad = (N.QeAggDesc * 1)(N.QeAggDesc(N.AGG_COUNT_STAR, N.TYPE_INT64))
+    h = N.C.c_void_p()
+    st = N.lib().qe_hashagg_create(gpu_ctx.handle, 2, kt, 1, ad, 16, N.C.byref(h))
+    assert st == N.QE_ERR_UNSUPPORTED and "66 bits" in N.lib().qe_last_error().decode()
+    state = HashAggregateState(gpu_ctx, [N.TYPE_INT32, N.TYPE_DATE32], [(N.AGG_COUNT_STAR, N.TYPE_INT64)], 16)
+    assert state.tuple_dict is not None and state.device_key_types == [N.TYPE_INT32]
 
 
 @pytest.mark.parametrize("types", [(N.TYPE_UINT8, N.TYPE_UINT8), (N.TYPE_INT32, N.TYPE_UINT8),
