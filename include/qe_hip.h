@@ -454,10 +454,12 @@ typedef struct qe_csv_table qe_csv_table;
 int qe_csv_parse(qe_ctx* ctx, const uint8_t* data, int64_t nbytes, const qe_csv_options* opt,
                  qe_csv_table** out);
 int qe_csv_rows(const qe_csv_table* table, int64_t* rows);
-/* View of projected column i (UTF8, no validity), valid while the table lives. */
+/* `data` must stay valid until every wanted column has been built (column_copy / column).
+ * View of projected column i (UTF8, no validity), built into table-owned memory on first request
+ * and valid while the table lives. */
 int qe_csv_column(const qe_csv_table* table, int32_t i, qe_column* out);
-/* Bytes of projected column i, and a device-to-device copy into caller buffers (offsets for
- * rows+1 entries, values >= qe_csv_column_bytes). */
+/* Bytes of projected column i, and building it straight into caller buffers (offsets for
+ * rows+1 entries, values >= qe_csv_column_bytes; stream-ordered, no synchronisation). */
 int qe_csv_column_bytes(const qe_csv_table* table, int32_t i, int64_t* nbytes);
 int qe_csv_column_copy(const qe_csv_table* table, int32_t i, qe_column* dst);
 int qe_csv_destroy(qe_csv_table* table);

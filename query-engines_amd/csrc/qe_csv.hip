@@ -25,9 +25,17 @@
 
 struct qe_csv_table {
   qe_ctx* ctx = nullptr;
+  const uint8_t* data = nullptr;  // the file bytes (the caller keeps them until the columns are built)
   int64_t rows = 0;
-  std::vector<qe_column> cols;
+  int32_t nproj = 0;
+  void* block = nullptr;          // per projected column: start i64, len i64, byte start i64 [rows+1], quoted u8
+  std::vector<int64_t> total;     // per projected column: bytes
+  std::vector<qe_column> cols;    // materialised views (qe_csv_column), built on first request
   std::vector<void*> owned;
+  int64_t* start(int c) { return (int64_t*)block + (size_t)c * (rows + 1); }
+  int64_t* len(int c) { return (int64_t*)block + (size_t)(nproj + c) * (rows + 1); }
+  int64_t* bstart(int c) { return (int64_t*)block + (size_t)(2 * nproj + c) * (rows + 1); }
+  uint8_t* quoted(int c) { return (uint8_t*)((int64_t*)block + (size_t)3 * nproj * (rows + 1)) + (size_t)c * (rows + 1); }
 };
 
 namespace qe {
@@ -69,6 +77,19 @@ __device__ __forceinline__ int quotes16(const Lane16& v) {
   return q;
 }
 
+// Whether any of the 16 bytes may equal `b`: the classic has-zero-byte test (no false negatives;
+// a false positive only sends the lane down the exact path). ~5 VALU ops per word.
+__device__ __forceinline__ bool has_byte(const Lane16& v, uint32_t b) {
+  const uint32_t rep = b * 0x01010101u;
+  uint32_t any = 0;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const uint32_t x = v.w[i] ^ rep;
+    any |= (x - 0x01010101u) & ~x & 0x80808080u;
+  }
+  return any != 0;
+}
+
 __global__ void __launch_bounds__(256) k_csv_quotes(const uint8_t* __restrict__ data, int64_t nbytes, int64_t nseg,
                                                     int64_t* __restrict__ seg_q) {
   const int lane = threadIdx.x & 63;
@@ -76,10 +97,15 @@ __global__ void __launch_bounds__(256) k_csv_quotes(const uint8_t* __restrict__ 
   if (seg >= nseg) return;
   const int64_t base = seg * SEG;
   int q = 0;
-  for (int step = 0; step < SEG / 1024; ++step) {
-    const int64_t pos = base + step * 1024 + lane * 16;
-    if (pos >= nbytes) break;
-    q += quotes16(load16(data, nbytes, pos));
+  for (int step = 0; step < SEG / 1024; step += 4) {  // 4 loads in flight per lane
+    Lane16 v[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int64_t pos = base + (step + u) * 1024 + lane * 16;
+      v[u] = pos < nbytes ? load16(data, nbytes, pos) : Lane16{{0, 0, 0, 0}};
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) q += has_byte(v[u], '"') ? quotes16(v[u]) : 0;
   }
   for (int d = 32; d >= 1; d >>= 1) q += __shfl_xor(q, d);
   if (lane == 0) seg_q[seg] = q;
@@ -100,14 +126,15 @@ __device__ __forceinline__ uint32_t eq16(const Lane16& v, uint32_t b) {
   return m;
 }
 
-__device__ __forceinline__ uint32_t terms16(const Lane16& v, const uint8_t* data, int64_t nbytes, int64_t pos,
+// `next` = the byte after these 16 (the next lane's first byte, passed by shuffle; 0 past the end).
+__device__ __forceinline__ uint32_t terms16(const Lane16& v, uint32_t next, int64_t nbytes, int64_t pos,
                                             uint32_t inq, uint32_t* inq_out) {
-  if (eq16(v, '"') == 0) {  // no quote in these 16 bytes: the state is constant (common case)
+  if (!has_byte(v, '"') || eq16(v, '"') == 0) {  // no quote: the state is constant (common case)
     *inq_out = inq;
-    if (inq) return 0;
+    if (inq || (!has_byte(v, '\n') && !has_byte(v, '\r'))) return 0;
     const uint32_t valid = pos + 16 <= nbytes ? 0xFFFFu : ((1u << (nbytes - pos)) - 1u);
     const uint32_t nl = eq16(v, '\n') & valid, cr = eq16(v, '\r') & valid;
-    const uint32_t next_nl = (nl >> 1) | ((pos + 16 < nbytes && data[pos + 16] == '\n') ? 0x8000u : 0u);
+    const uint32_t next_nl = (nl >> 1) | ((pos + 16 < nbytes && next == '\n') ? 0x8000u : 0u);
     return nl | (cr & ~next_nl);
   }
   uint32_t m = 0;
@@ -121,7 +148,7 @@ __device__ __forceinline__ uint32_t terms16(const Lane16& v, const uint8_t* data
       if (c == '\n') {
         m |= 1u << k;
       } else if (c == '\r') {
-        const uint32_t nx = k < 15 ? v.byte(k + 1) : (pos + 16 < nbytes ? data[pos + 16] : 0u);
+        const uint32_t nx = k < 15 ? v.byte(k + 1) : (pos + 16 < nbytes ? next : 0u);
         const bool last = pos + k + 1 >= nbytes;
         if (last || nx != '\n') m |= 1u << k;
       }
@@ -144,28 +171,41 @@ __global__ void __launch_bounds__(256) k_csv_terms(const uint8_t* __restrict__ d
   uint32_t carry = (uint32_t)(seg_qstart[seg] & 1);
   int64_t out = EMIT ? seg_tstart[seg] : 0;
   int64_t count = 0;
+  Lane16 vq[4];
   for (int step = 0; step < SEG / 1024; ++step) {
     const int64_t row0 = base + step * 1024;
     if (row0 >= nbytes) break;
     const int64_t pos = row0 + lane * 16;
-    const Lane16 v = load16(data, nbytes, pos);
-    const uint32_t qodd = (uint32_t)(quotes16(v) & 1);
+    if ((step & 3) == 0) {  // 4 loads in flight per lane: this step and the next three
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int64_t pu = pos + u * 1024;
+        vq[u] = pu < nbytes ? load16(data, nbytes, pu) : Lane16{{0, 0, 0, 0}};
+      }
+    }
+    const Lane16 v = vq[step & 3];
+    const uint32_t qodd = has_byte(v, '"') ? (uint32_t)(quotes16(v) & 1) : 0u;
     const uint64_t par = __ballot(qodd);
     const uint32_t inq0 = carry ^ ((uint32_t)__popcll(par & below) & 1u);
     uint32_t inq1;
-    const uint32_t m = terms16(v, data, nbytes, pos, inq0, &inq1);
+    // byte after this lane's 16: the next lane's first byte; lane 63 reads it (rare)
+    uint32_t next = (uint32_t)__shfl_down((int)(v.w[0] & 0xFFu), 1);
+    // lane 63: only a trailing '\r' needs the next byte (a load here on every step would put a
+    // full memory round trip on every step's critical path)
+    if (lane == 63) next = (v.byte(15) == '\r' && pos + 16 < nbytes) ? data[pos + 16] : 0u;
+    const uint32_t m = terms16(v, next, nbytes, pos, inq0, &inq1);
     carry ^= (uint32_t)__popcll(par) & 1u;
-    const int c = __popc(m);
-    // wave exclusive prefix of c
-    int incl = c;
+    const int c = __popc(m);  // 0..16
+    // wave exclusive prefix and total of c from its 5 bit-planes (ballot + popcount, no LDS)
+    int excl = 0, total = 0;
 #pragma unroll
-    for (int d = 1; d < 64; d <<= 1) {
-      const int y = __shfl_up(incl, d);
-      if (lane >= d) incl += y;
+    for (int b = 0; b < 5; ++b) {
+      const uint64_t plane = __ballot((c >> b) & 1);
+      excl += __popcll(plane & below) << b;
+      total += __popcll(plane) << b;
     }
-    const int total = __shfl(incl, 63);
     if (EMIT) {
-      int64_t o = out + (incl - c);
+      int64_t o = out + excl;
       uint32_t mm = m;
       while (mm) {
         const int k = __builtin_ctz(mm);
@@ -353,7 +393,7 @@ int csv_parse(qe_ctx* ctx, const uint8_t* data, int64_t nbytes, const qe_csv_opt
   // ---- record terminators
   const int64_t nseg = (int64_t)div_up((uint64_t)(nbytes > 0 ? nbytes : 1), SEG);
   void* p;
-  QE_TRY(dmalloc(t, (size_t)(4 * nseg + 4) * 8, &p));
+  QE_TRY(ctx_workspace(ctx, 0, (size_t)(4 * nseg + 4) * 8, &p));
   int64_t* seg_q = (int64_t*)p;
   int64_t* seg_qs = seg_q + nseg;
   int64_t* seg_t = seg_qs + nseg + 1;
@@ -372,7 +412,7 @@ int csv_parse(qe_ctx* ctx, const uint8_t* data, int64_t nbytes, const qe_csv_opt
   QE_TRY(exclusive_scan_i64(ctx, seg_t, seg_ts, nseg));
   int64_t nterm = 0;
   QE_TRY(read_i64(ctx, seg_ts + nseg, &nterm));
-  QE_TRY(dmalloc(t, (size_t)(3 * nterm + 7) * 8, &p));
+  QE_TRY(ctx_workspace(ctx, 1, (size_t)(3 * nterm + 7) * 8, &p));
   int64_t* ends = (int64_t*)p;
   int64_t* keep = ends + nterm + 2;
   int64_t* kstart = keep + nterm + 2;
@@ -398,7 +438,7 @@ int csv_parse(qe_ctx* ctx, const uint8_t* data, int64_t nbytes, const qe_csv_opt
     QE_TRY(read_i64(ctx, kstart + nlines, &nkept));
   }
   int64_t* kept = nullptr;
-  QE_TRY(dmalloc(t, (size_t)(nkept + 1) * 8, &p));
+  QE_TRY(ctx_workspace(ctx, 2, (size_t)(nkept + 1) * 8, &p));
   kept = (int64_t*)p;
   if (nkept > 0) {
     hipLaunchKernelGGL(k_csv_compact_lines, dim3(grid_for(ctx, nlines)), dim3(256), 0, ctx->stream, keep, kstart,
@@ -408,64 +448,54 @@ int csv_parse(qe_ctx* ctx, const uint8_t* data, int64_t nbytes, const qe_csv_opt
   const int64_t first = opt->has_header ? 1 : 0;
   const int64_t rows = std::max<int64_t>(0, nkept - first);
   t->rows = rows;
-  // ---- fields
-  QE_TRY(dmalloc(t, (size_t)nproj * (size_t)(rows + 1) * 17 + 64, &p));
-  uint8_t* fb = (uint8_t*)p;
+  // ---- fields (kept in the table until the columns are built)
+  t->nproj = nproj;
+  t->data = data;
+  QE_TRY(dmalloc(t, (size_t)nproj * (size_t)(rows + 1) * 25 + 64, &p));
+  t->block = p;
   for (int c = 0; c < nproj; ++c) {
-    A.start[c] = (int64_t*)(fb + (size_t)c * (rows + 1) * 8);
-    A.len[c] = (int64_t*)(fb + (size_t)(nproj + c) * (rows + 1) * 8);
-    A.quoted[c] = fb + (size_t)nproj * (rows + 1) * 16 + (size_t)c * (rows + 1);
+    A.start[c] = t->start(c);
+    A.len[c] = t->len(c);
+    A.quoted[c] = t->quoted(c);
   }
   if (rows > 0) {
     hipLaunchKernelGGL(k_csv_fields, dim3(grid_for(ctx, rows)), dim3(256), 0, ctx->stream, data, nbytes, ends, kept,
                        first, rows, A, nproj);
     QE_TRY(launch_check("k_csv_fields"));
   }
-  // ---- columns
-  int64_t* starts64;
-  QE_TRY(dmalloc(t, (size_t)(rows + 1) * 8, &p));
-  starts64 = (int64_t*)p;
-  for (int c = 0; c < nproj; ++c) {
-    qe_column col{};
-    col.type = QE_TYPE_UTF8;
-    col.length = rows;
-    QE_TRY(dmalloc(t, (size_t)(rows + 1) * 4, &p));
-    col.offsets = (int32_t*)p;
-    int64_t total = 0;
-    if (rows > 0) {
-      QE_TRY(exclusive_scan_i64(ctx, A.len[c], starts64, rows));
-      QE_TRY(read_i64(ctx, starts64 + rows, &total));
+  // ---- per column: byte positions of the values (scan of lengths) and the column's size
+  t->total.assign((size_t)nproj, 0);
+  for (int c = 0; c < nproj && rows > 0; ++c) QE_TRY(exclusive_scan_i64(ctx, A.len[c], t->bstart(c), rows));
+  if (rows > 0) {
+    void* pin;
+    QE_TRY(ctx_pinned(ctx, (size_t)nproj * 8, &pin));
+    for (int c = 0; c < nproj; ++c)
+      QE_HIP(hipMemcpyAsync((int64_t*)pin + c, t->bstart(c) + rows, 8, hipMemcpyDeviceToHost, ctx->stream));
+    QE_HIP(hipStreamSynchronize(ctx->stream));
+    for (int c = 0; c < nproj; ++c) {
+      t->total[(size_t)c] = ((int64_t*)pin)[c];
+      QE_CHECK(t->total[(size_t)c] < (1ll << 31), QE_ERR_CAPACITY, "CSV column %d holds more than 2^31 bytes", c);
     }
-    QE_CHECK(total < (1ll << 31), QE_ERR_CAPACITY, "CSV column %d holds more than 2^31 bytes", c);
-    if (rows > 0) {
-      hipLaunchKernelGGL(k_csv_offsets, dim3(grid_for(ctx, rows + 1)), dim3(256), 0, ctx->stream, starts64, rows,
-                         col.offsets);
-      QE_TRY(launch_check("k_csv_offsets"));
-    } else {
-      QE_HIP(hipMemsetAsync(col.offsets, 0, 4, ctx->stream));
-    }
-    QE_TRY(dmalloc(t, (size_t)total, &p));
-    col.values = p;
-    if (rows > 0 && total > 0) {
-      hipLaunchKernelGGL(k_csv_copy, dim3(grid_for(ctx, rows)), dim3(256), 0, ctx->stream, data, A.start[c], A.len[c],
-                         A.quoted[c], col.offsets, rows, (uint8_t*)col.values);
-      QE_TRY(launch_check("k_csv_copy"));
-    }
-    t->cols.push_back(col);
   }
-  QE_HIP(hipStreamSynchronize(ctx->stream));
-  // scratch arrays are freed now; the columns stay
-  std::vector<void*> keep_bufs;
-  for (const qe_column& c : t->cols) {
-    keep_bufs.push_back(c.offsets);
-    keep_bufs.push_back(c.values);
+  return QE_OK;
+}
+
+// Offsets + bytes of projected column c into dst (offsets for rows+1 entries, values >= total).
+int build_column(qe_csv_table* t, int c, int32_t* offsets, uint8_t* values) {
+  qe_ctx* ctx = t->ctx;
+  const int64_t rows = t->rows;
+  if (rows == 0) {
+    QE_HIP(hipMemsetAsync(offsets, 0, 4, ctx->stream));
+    return QE_OK;
   }
-  for (void* q : t->owned) {
-    bool kept_buf = false;
-    for (void* k : keep_bufs) kept_buf |= (k == q);
-    if (!kept_buf) (void)hipFree(q);
+  hipLaunchKernelGGL(k_csv_offsets, dim3(grid_for(ctx, rows + 1)), dim3(256), 0, ctx->stream, t->bstart(c), rows,
+                     offsets);
+  QE_TRY(launch_check("k_csv_offsets"));
+  if (t->total[(size_t)c] > 0) {
+    hipLaunchKernelGGL(k_csv_copy, dim3(grid_for(ctx, rows)), dim3(256), 0, ctx->stream, t->data, t->start(c),
+                       t->len(c), t->quoted(c), offsets, rows, values);
+    QE_TRY(launch_check("k_csv_copy"));
   }
-  t->owned = keep_bufs;
   return QE_OK;
 }
 
@@ -499,36 +529,45 @@ int qe_csv_rows(const qe_csv_table* t, int64_t* rows) {
   return QE_OK;
 }
 
-int qe_csv_column(const qe_csv_table* t, int32_t i, qe_column* out) {
-  QE_CHECK(t && out, QE_ERR_INVALID_ARG, "null argument");
-  QE_CHECK(i >= 0 && (size_t)i < t->cols.size(), QE_ERR_INVALID_ARG, "CSV column %d out of range", i);
-  *out = t->cols[(size_t)i];
+int qe_csv_column(const qe_csv_table* tc, int32_t i, qe_column* out) {
+  QE_CHECK(tc && out, QE_ERR_INVALID_ARG, "null argument");
+  qe_csv_table* t = const_cast<qe_csv_table*>(tc);
+  QE_CHECK(i >= 0 && i < t->nproj, QE_ERR_INVALID_ARG, "CSV column %d out of range", i);
+  QE_TRY(ctx_enter(t->ctx));
+  if (t->cols.empty()) t->cols.assign((size_t)t->nproj, qe_column{});
+  qe_column& c = t->cols[(size_t)i];
+  if (!c.offsets) {  // first request: build the column into table-owned buffers
+    void* o;
+    void* v;
+    QE_TRY(dmalloc(t, (size_t)(t->rows + 1) * 4, &o));
+    QE_TRY(dmalloc(t, (size_t)t->total[(size_t)i], &v));
+    QE_TRY(build_column(t, i, (int32_t*)o, (uint8_t*)v));
+    c.type = QE_TYPE_UTF8;
+    c.length = t->rows;
+    c.offsets = (int32_t*)o;
+    c.values = v;
+  }
+  *out = c;
   return QE_OK;
 }
 
 int qe_csv_column_bytes(const qe_csv_table* t, int32_t i, int64_t* nbytes) {
   QE_CHECK(t && nbytes, QE_ERR_INVALID_ARG, "null argument");
-  QE_CHECK(i >= 0 && (size_t)i < t->cols.size(), QE_ERR_INVALID_ARG, "CSV column %d out of range", i);
-  const qe_column& c = t->cols[(size_t)i];
-  int32_t last = 0;
-  if (c.length > 0) QE_HIP(hipMemcpy(&last, c.offsets + c.length, 4, hipMemcpyDeviceToHost));
-  *nbytes = last;
+  QE_CHECK(i >= 0 && i < t->nproj, QE_ERR_INVALID_ARG, "CSV column %d out of range", i);
+  *nbytes = t->total[(size_t)i];
   return QE_OK;
 }
 
-int qe_csv_column_copy(const qe_csv_table* t, int32_t i, qe_column* dst) {
-  QE_CHECK(t && dst, QE_ERR_INVALID_ARG, "null argument");
-  QE_CHECK(i >= 0 && (size_t)i < t->cols.size(), QE_ERR_INVALID_ARG, "CSV column %d out of range", i);
+int qe_csv_column_copy(const qe_csv_table* tc, int32_t i, qe_column* dst) {
+  QE_CHECK(tc && dst, QE_ERR_INVALID_ARG, "null argument");
+  qe_csv_table* t = const_cast<qe_csv_table*>(tc);
+  QE_CHECK(i >= 0 && i < t->nproj, QE_ERR_INVALID_ARG, "CSV column %d out of range", i);
   QE_CHECK(dst->type == QE_TYPE_UTF8 && dst->offsets && dst->length >= t->rows, QE_ERR_INVALID_ARG,
            "destination must be UTF8 with room for %lld rows", (long long)t->rows);
-  const qe_column& c = t->cols[(size_t)i];
-  qe_ctx* ctx = t->ctx;
-  QE_TRY(ctx_enter(ctx));
-  int64_t nb = 0;
-  QE_TRY(qe_csv_column_bytes(t, i, &nb));
-  QE_HIP(hipMemcpyAsync(dst->offsets, c.offsets, (size_t)(c.length + 1) * 4, hipMemcpyDeviceToDevice, ctx->stream));
-  if (nb > 0) QE_HIP(hipMemcpyAsync(dst->values, c.values, (size_t)nb, hipMemcpyDeviceToDevice, ctx->stream));
-  dst->length = c.length;
+  QE_CHECK(dst->values || t->total[(size_t)i] == 0, QE_ERR_CAPACITY, "destination values buffer required");
+  QE_TRY(ctx_enter(t->ctx));
+  QE_TRY(build_column(t, i, dst->offsets, (uint8_t*)dst->values));
+  dst->length = t->rows;
   return QE_OK;
 }
 

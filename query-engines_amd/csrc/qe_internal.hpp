@@ -24,6 +24,8 @@ struct qe_ctx {
   int jit = 1;                   // specialise fused plans with hipRTC (qe_jit.hip)
   void* scan_tmp = nullptr;      // block sums of exclusive_scan_i64 (never aliases `scratch`)
   size_t scan_tmp_bytes = 0;
+  void* ws[8] = {};              // grow-only workspace slots (CSV scan intermediates)
+  size_t ws_bytes[8] = {};
 };
 
 namespace qe {
@@ -54,6 +56,7 @@ int ctx_enter(qe_ctx* ctx);                                   // validates + hip
 int ctx_scratch(qe_ctx* ctx, size_t bytes, void** out);       // grow-only scratch
 int ctx_pinned(qe_ctx* ctx, size_t bytes, void** out);        // grow-only pinned host
 int launch_check(const char* what);                           // hipGetLastError wrapper
+int ctx_workspace(qe_ctx* ctx, int slot, size_t bytes, void** out);  // grow-only, contents not kept
 // Per-plan kernel specialisation (qe_jit.hip).
 bool gen_fused_source(const qe::Plan& P, int log2, std::string* src, size_t* lds_bytes);
 int jit_kernel(qe_ctx* ctx, const std::string& src, hipFunction_t* fn, int* blocks_per_cu,

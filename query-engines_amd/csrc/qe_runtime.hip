@@ -60,6 +60,25 @@ int ctx_pinned(qe_ctx* ctx, size_t bytes, void** out) {
   return QE_OK;
 }
 
+int ctx_workspace(qe_ctx* ctx, int slot, size_t bytes, void** out) {
+  if (bytes > ctx->ws_bytes[slot]) {
+    if (ctx->ws[slot]) {
+      QE_HIP(hipStreamSynchronize(ctx->stream));
+      QE_HIP(hipFree(ctx->ws[slot]));
+    }
+    ctx->ws[slot] = nullptr;
+    ctx->ws_bytes[slot] = 0;
+    const size_t want = bytes + bytes / 4 + 4096;  // headroom: a slightly larger next input reuses it
+    if (hipMalloc(&ctx->ws[slot], want) != hipSuccess) {
+      (void)hipGetLastError();
+      return fail(QE_ERR_OOM, "hipMalloc(%zu) for workspace failed", want);
+    }
+    ctx->ws_bytes[slot] = want;
+  }
+  *out = ctx->ws[slot];
+  return QE_OK;
+}
+
 int launch_check(const char* what) {
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return fail(QE_ERR_DEVICE, "launch of %s failed: %s", what, hipGetErrorString(e));
@@ -191,6 +210,8 @@ int qe_ctx_destroy(qe_ctx* ctx) {
   (void)hipStreamSynchronize(ctx->stream);
   if (ctx->scratch) (void)hipFree(ctx->scratch);
   if (ctx->scan_tmp) (void)hipFree(ctx->scan_tmp);
+  for (void* w : ctx->ws)
+    if (w) (void)hipFree(w);
   if (ctx->pinned) (void)hipHostFree(ctx->pinned);
   if (ctx->own_stream) (void)hipStreamDestroy(ctx->stream);
   delete ctx;
