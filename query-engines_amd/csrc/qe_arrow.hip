@@ -214,6 +214,11 @@ void schema_release(ArrowSchema* s) {
 }
 
 }  // namespace
+
+int parallel_h2d_copy(qe_ctx* ctx, void* dst, const void* src, size_t n) {
+  return parallel_h2d(ctx, std::vector<H2DJob>{{(uint8_t*)dst, (const uint8_t*)src, n}});
+}
+
 }  // namespace qe
 
 using namespace qe;

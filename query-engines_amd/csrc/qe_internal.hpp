@@ -57,6 +57,8 @@ int ctx_scratch(qe_ctx* ctx, size_t bytes, void** out);       // grow-only scrat
 int ctx_pinned(qe_ctx* ctx, size_t bytes, void** out);        // grow-only pinned host
 int launch_check(const char* what);                           // hipGetLastError wrapper
 int ctx_workspace(qe_ctx* ctx, int slot, size_t bytes, void** out);  // grow-only, contents not kept
+// Host (pageable) -> device through pinned staging with 8 host threads; synchronous (qe_arrow.hip).
+int parallel_h2d_copy(qe_ctx* ctx, void* dst, const void* src, size_t n);
 // Per-plan kernel specialisation (qe_jit.hip).
 bool gen_fused_source(const qe::Plan& P, int log2, std::string* src, size_t* lds_bytes);
 int jit_kernel(qe_ctx* ctx, const std::string& src, hipFunction_t* fn, int* blocks_per_cu,

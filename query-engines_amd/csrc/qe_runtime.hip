@@ -250,6 +250,7 @@ int qe_device_free(qe_ctx* ctx, void* ptr) {
 
 int qe_copy_to_device(qe_ctx* ctx, void* dst, const void* src, size_t bytes) {
   QE_TRY(ctx_enter(ctx));
+  if (bytes >= ((size_t)32 << 20)) return parallel_h2d_copy(ctx, dst, src, bytes);  // large: staged, 8 threads
   QE_HIP(hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, ctx->stream));
   QE_HIP(hipStreamSynchronize(ctx->stream));
   return QE_OK;

@@ -109,10 +109,14 @@ class CsvDataSource(DataSource):
         names = [f.name for f in schema.fields]
         idx = [names.index(f.name) for f in read_schema.fields]
         ctx = self.ctx or Context.get(0)
-        raw = np.fromfile(self.filename, dtype=np.uint8)
-        dev = torch.from_numpy(raw).to(ctx.torch_device) if raw.size else torch.zeros(1, dtype=torch.uint8,
-                                                                                        device=ctx.torch_device)
-        cols = self._parse(ctx, dev, raw.size, idx)
+        size = os.path.getsize(self.filename)
+        dev = torch.empty(max(1, size), dtype=torch.uint8, device=ctx.torch_device)
+        if size:  # file -> HBM: mapped pages go through the library's pinned multi-threaded staging,
+            raw = np.memmap(self.filename, dtype=np.uint8, mode="r")  # so the page reads run in parallel
+            N.check(N.lib().qe_copy_to_device(ctx.handle, N.C.c_void_p(dev.data_ptr()),
+                                              N.C.c_void_p(raw.ctypes.data), size))
+            del raw
+        cols = self._parse(ctx, dev, size, idx)
         n = cols[0].length if cols else 0
         step = self.batchSize if self.batchSize and self.batchSize > 0 else max(n, 1)
         for s in range(0, n, step):
