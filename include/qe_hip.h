@@ -366,6 +366,10 @@ int qe_strdict_decode(qe_strdict* dict, const qe_column* codes, qe_column* out);
  * (types as encoded; validity where outs[k].validity is non-NULL) for `codes`. */
 int qe_strdict_encode_tuple(qe_strdict* dict, const qe_column* keys, int32_t nkeys, qe_column* codes);
 int qe_strdict_decode_tuple(qe_strdict* dict, const qe_column* codes, int32_t nkeys, qe_column* outs);
+/* Destination partition of every row by the CONTENT of its key columns (UTF8 bytes, fixed-width
+ * values with fp64 NaNs as one key, nulls): part[i] in [0, nparts), identical on every rank for
+ * equal keys. Used to route dictionary-keyed partials, whose codes are local to one state. */
+int qe_hash_partition(qe_ctx* ctx, const qe_column* cols, int32_t ncols, int32_t nparts, int32_t* part);
 
 /* ---- Arrow C Data Interface boundary -----------------------------------------
  * Arrow Java exports a VectorSchemaRoot (the reference's batches, K:635-650) as a struct

@@ -454,6 +454,50 @@ __global__ void k_tuple_decode(const int32_t* __restrict__ codes, int64_t n, int
   }
 }
 
+// ---- content-hash partitioning of rows (exchange of dictionary-keyed partials) -------------------
+struct HashCols {
+  const void* v[QE_MAX_KEYS];
+  const uint8_t* valid[QE_MAX_KEYS];
+  const int32_t* offs[QE_MAX_KEYS];  // UTF8
+  int32_t kind[QE_MAX_KEYS];         // TK_* or 5 = UTF8
+  int32_t ncols;
+};
+constexpr int32_t TK_UTF8 = 5;
+
+__global__ void k_hash_partition(HashCols H, int64_t n, int32_t nparts, int32_t* __restrict__ part) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    uint64_t h = 0x2545F4914F6CDD1Dull;
+    for (int k = 0; k < H.ncols; ++k) {
+      uint64_t x;
+      const bool ok = !H.valid[k] || ((H.valid[k][i >> 3] >> (i & 7)) & 1);
+      if (!ok) {
+        x = 0x6A09E667F3BCC909ull;  // null member
+      } else {
+        switch (H.kind[k]) {
+          case TK_UTF8: {
+            const int32_t s0 = H.offs[k][i];
+            x = str_hash((const uint8_t*)H.v[k] + s0, H.offs[k][i + 1] - s0);
+            break;
+          }
+          case TK_F64: {
+            x = ((const uint64_t*)H.v[k])[i];
+            const double d = bits_f64((int64_t)x);
+            if (d != d) x = 0x7FF8000000000000ull;  // Double.equals: every NaN is one key
+            break;
+          }
+          case TK_I64: x = ((const uint64_t*)H.v[k])[i]; break;
+          case TK_I32: x = (uint32_t)((const int32_t*)H.v[k])[i]; break;
+          case TK_U8: x = ((const uint8_t*)H.v[k])[i]; break;
+          default: x = (((const uint8_t*)H.v[k])[i >> 3] >> (i & 7)) & 1u; break;
+        }
+      }
+      h = fmix64(h ^ x) + 0x165667B19E3779F9ull * (uint64_t)(k + 1);
+    }
+    h = fmix64(h);
+    part[i] = (int32_t)(((h >> 32) * (uint64_t)nparts) >> 32);
+  }
+}
+
 __global__ void k_dict_rebuild(DictDev D, int64_t ncodes) {
   for (int64_t c = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; c < ncodes; c += (int64_t)gridDim.x * blockDim.x) {
     const uint64_t h = D.code_hash[c];
@@ -790,6 +834,29 @@ int qe_strdict_encode_tuple(qe_strdict* d, const qe_column* keys, int32_t nkeys,
                            (int32_t*)codes->values, rin, rout);
         return launch_check("k_tuple_encode_retry");
       });
+}
+
+int qe_hash_partition(qe_ctx* ctx, const qe_column* cols, int32_t ncols, int32_t nparts, int32_t* part) {
+  QE_TRY(ctx_enter(ctx));
+  QE_CHECK(cols && part && ncols >= 1 && ncols <= QE_MAX_KEYS, QE_ERR_INVALID_ARG, "1..%d key columns", QE_MAX_KEYS);
+  QE_CHECK(nparts >= 1, QE_ERR_INVALID_ARG, "nparts must be >= 1");
+  const int64_t n = cols[0].length;
+  HashCols H{};
+  H.ncols = ncols;
+  for (int k = 0; k < ncols; ++k) {
+    QE_CHECK(cols[k].length == n, QE_ERR_INVALID_ARG, "column %d length differs", k);
+    const int32_t kind = cols[k].type == QE_TYPE_UTF8 ? TK_UTF8 : tuple_kind(cols[k].type);
+    QE_CHECK(kind >= 0, QE_ERR_UNSUPPORTED, "column %d: type %d cannot be hashed", k, cols[k].type);
+    QE_CHECK(kind != TK_UTF8 || cols[k].offsets, QE_ERR_INVALID_ARG, "UTF8 column %d without offsets", k);
+    H.v[k] = cols[k].values;
+    H.valid[k] = cols[k].validity;
+    H.offs[k] = cols[k].offsets;
+    H.kind[k] = kind;
+  }
+  if (n == 0) return QE_OK;
+  const int grid = (int)std::min<int64_t>((int64_t)div_up((uint64_t)n, 256), (int64_t)ctx->num_cus * 8);
+  hipLaunchKernelGGL(k_hash_partition, dim3(grid), dim3(256), 0, ctx->stream, H, n, nparts, part);
+  return launch_check("k_hash_partition");
 }
 
 int qe_strdict_decode_tuple(qe_strdict* d, const qe_column* codes, int32_t nkeys, qe_column* outs) {

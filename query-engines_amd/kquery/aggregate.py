@@ -20,6 +20,22 @@ def output_type(fn: int, input_type: int) -> int:
 _KEY_BITS = {N.TYPE_INT32: 32, N.TYPE_DATE32: 32, N.TYPE_UINT8: 8}
 
 
+def _device_column(ctx, type_id: int, vals, valid) -> DeviceColumn:
+    """DeviceColumn from int64 device values (narrowed to `type_id`) and a bool validity tensor."""
+    import torch
+
+    from .columnar import bitmap_bytes
+
+    n = vals.numel()
+    dt = {N.TYPE_INT32: torch.int32, N.TYPE_DATE32: torch.int32, N.TYPE_UINT8: torch.uint8}[type_id]
+    v = vals.to(dt).contiguous() if n else torch.zeros(1, dtype=dt, device=vals.device)
+    bits = torch.zeros(max(bitmap_bytes(n), 4) * 8, dtype=torch.uint8, device=vals.device)
+    bits[:n] = valid.to(torch.uint8)
+    w = torch.tensor([1, 2, 4, 8, 16, 32, 64, 128], dtype=torch.uint8, device=vals.device)
+    vb = (bits.view(-1, 8) * w).sum(dim=1).to(torch.uint8)
+    return DeviceColumn(type_id, n, v, vb, None, ctx)
+
+
 def packable(key_types) -> bool:
     """Whether qe_hashagg packs these keys itself (one int64/fp64 key, or narrow keys whose values
     plus null bits fit 63 bits — qe_hashagg_create's rule)."""
@@ -145,7 +161,94 @@ class HashAggregateState:
     def _check_exportable(self) -> None:
         if self.dicts or self.tuple_dict is not None:  # codes are local to this state's dictionary
             raise N.IllegalStateException(N.QE_ERR_UNSUPPORTED,
-                                          "partial records with UTF-8 keys are not exchangeable yet")
+                                          "dictionary-keyed partials move by key content: use "
+                                          "kquery.exchange.exchange_partials (export_all / import_keyed)")
+
+    # ---- dictionary-keyed states: keys travel as their content (kquery/exchange.py) -----------------
+    @property
+    def keyed_by_dictionary(self) -> bool:
+        return bool(self.dicts) or self.tuple_dict is not None
+
+    def _packing(self):
+        """(shift, nullbit, width) per device key, as qe_hashagg_create packs narrow keys."""
+        out, bit = [], 0
+        for t in self.device_key_types:
+            w = _KEY_BITS[t]
+            out.append((bit, bit + w, w))
+            bit += w + 1
+        return out
+
+    def record_key_columns(self, records, n: int) -> List[DeviceColumn]:
+        """The original key columns (UTF8 included) of `n` exported records of this state."""
+        import torch
+
+        if n == 0:
+            return self._empty_keys()
+        rec = records[: n * self.record_bytes()].view(torch.int64).view(n, -1)
+        packed = rec[:, 0]
+        members = []
+        for (shift, nullbit, w), t in zip(self._packing(), self.device_key_types):
+            vals = (packed >> shift) & ((1 << w) - 1)
+            valid = ((packed >> nullbit) & 1) == 0
+            members.append(_device_column(self.ctx, t, vals, valid))
+        if self.tuple_dict is not None:
+            members = self.tuple_dict.decode_tuple(members[0], self.member_types)
+        return [self.dicts[i].decode(k) if i in self.dicts else k for i, k in enumerate(members)]
+
+    def _empty_keys(self) -> List[DeviceColumn]:
+        import torch
+
+        out = []
+        for t in self.key_types:
+            if t == N.TYPE_UTF8:
+                out.append(DeviceColumn(N.TYPE_UTF8, 0, torch.zeros(1, dtype=torch.uint8, device=self.ctx.torch_device),
+                                        None, torch.zeros(1, dtype=torch.int32, device=self.ctx.torch_device), self.ctx))
+            else:
+                out.append(DeviceColumn.empty(t, 0, True, ctx=self.ctx))
+        return out
+
+    def packed_keys(self, key_cols: Sequence[DeviceColumn]):
+        """int64 packed device keys of rows given as original key columns (encodes new strings /
+        tuples into this state's dictionaries)."""
+        import torch
+
+        members = [self.dicts[i].encode(k) if i in self.dicts else k for i, k in enumerate(key_cols)]
+        if self.tuple_dict is not None:
+            members = [self.tuple_dict.encode_tuple(members)]
+        n = members[0].length
+        packed = torch.zeros(n, dtype=torch.int64, device=self.ctx.torch_device)
+        for (shift, nullbit, w), m in zip(self._packing(), members):
+            vals = m.values[:n].to(torch.int64) & ((1 << w) - 1)
+            valid = torch.from_numpy(m.valid_mask()).to(self.ctx.torch_device)
+            packed |= torch.where(valid, vals << shift, torch.zeros_like(vals)) | ((~valid).to(torch.int64) << nullbit)
+        return packed
+
+    def import_keyed(self, records, n: int, key_cols: Sequence[DeviceColumn]) -> None:
+        """Import records whose keys come from another state: rewrite their key field from the
+        key columns' content, then merge (qe_hashagg_import)."""
+        import torch
+
+        if n == 0:
+            return
+        rec = records[: n * self.record_bytes()].view(torch.int64).view(n, -1)
+        rec[:, 0] = self.packed_keys(key_cols)
+        rec[:, 1] = 0  # narrow packed keys never use the null-key slot
+        N.check(N.lib().qe_hashagg_import(self.handle, N.C.c_void_p(records.data_ptr()), int(n)))
+
+    def export_all(self):
+        """All partial records, unbucketed: (uint8 device tensor, count)."""
+        import torch
+
+        counts = self._export_counts_raw(1)
+        rb = self.record_bytes()
+        buf = torch.empty(max(1, counts[0] * rb), dtype=torch.uint8, device=self.ctx.torch_device)
+        N.check(N.lib().qe_hashagg_export(self.handle, 1, N.C.c_void_p(buf.data_ptr())))
+        return buf, counts[0]
+
+    def _export_counts_raw(self, nparts: int) -> List[int]:
+        arr = (N.C.c_int64 * nparts)()
+        N.check(N.lib().qe_hashagg_export_counts(self.handle, nparts, arr))
+        return list(arr)
 
     def export_counts(self, nparts: int) -> List[int]:
         self._check_exportable()

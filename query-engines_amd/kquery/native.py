@@ -221,6 +221,7 @@ SIGNATURES = [
     ("qe_strdict_decode", C.c_int, [_P, _COLP, _COLP]),
     ("qe_strdict_encode_tuple", C.c_int, [_P, _COLP, C.c_int32, _COLP]),
     ("qe_strdict_decode_tuple", C.c_int, [_P, _COLP, C.c_int32, _COLP]),
+    ("qe_hash_partition", C.c_int, [_P, _COLP, C.c_int32, C.c_int32, _P]),
     ("qe_select_project", C.c_int, [_P, _COLP, C.c_int32, C.POINTER(QeSelectSpec), _COLP, _I64P]),
     ("qe_csv_parse", C.c_int, [_P, _P, C.c_int64, C.POINTER(QeCsvOptions), _PP]),
     ("qe_csv_rows", C.c_int, [_P, _I64P]),

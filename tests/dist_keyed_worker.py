@@ -1,0 +1,82 @@
+"""Worker for tests/test_dist_keyed.py (launched by torch.distributed.run, 2 ranks sharing cuda:0,
+gloo backend): each rank partial-aggregates its own rows of a string- and tuple-keyed table,
+exchange_partials moves every group to its owner by key content, and rank 0 checks the union of
+the owners' groups against the oracle over all rows."""
+import json
+import os
+import pathlib
+import sys
+
+ROOT = pathlib.Path(__file__).resolve().parents[1]
+sys.path[:0] = [str(ROOT), str(ROOT / "query-engines_amd")]
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+from oracle import semantics as S  # noqa: E402
+
+
+def table(seed, n):
+    rng = np.random.default_rng(seed)
+    words = ["1", "2", "VTS", "", "Pärsson", "x" * 45]
+    s = [None if rng.random() < 0.03 else words[i] for i in rng.integers(0, len(words), n)]
+    k = rng.integers(-3, 4, n).astype(np.int64) * (2 ** 40)
+    kv = rng.random(n) > 0.05
+    v = rng.integers(-1000, 1000, n).astype(np.int64)
+    return s, k, kv, v
+
+
+def main():
+    dist.init_process_group("gloo")
+    rank, world = dist.get_rank(), dist.get_world_size()
+    from kquery import native as N
+    from kquery.aggregate import HashAggregateState
+    from kquery.columnar import Context, DeviceColumn
+    from kquery.exchange import exchange_partials
+
+    ctx = Context.get(0)
+    results = {}
+    for mode in ("utf8", "tuple"):
+        s, k, kv, v = table(100 + rank, 30_000 + 7000 * rank)
+        types = [N.TYPE_UTF8] if mode == "utf8" else [N.TYPE_UTF8, N.TYPE_INT64]
+        aggs = [(N.AGG_SUM, N.TYPE_INT64), (N.AGG_COUNT_STAR, N.TYPE_INT64), (N.AGG_MIN, N.TYPE_INT64)]
+        partial = HashAggregateState(ctx, types, aggs, 64)
+        owner = HashAggregateState(ctx, types, aggs, 64)
+        keys = [DeviceColumn.from_strings(s, ctx=ctx)]
+        if mode == "tuple":
+            keys.append(DeviceColumn.from_numpy(N.TYPE_INT64, k, kv, ctx=ctx))
+        vc = DeviceColumn.from_numpy(N.TYPE_INT64, v, ctx=ctx)
+        partial.update(keys, [vc, None, vc])
+        exchange_partials(partial, owner)
+        ko, ao = owner.finalize()
+        cols = [c.to_pylist() for c in ko] + [c.to_pylist() for c in ao]
+        mine = [list(r) for r in zip(*cols)]
+        allrows = [None] * world
+        dist.all_gather_object(allrows, mine)
+        if rank == 0:
+            got = {}
+            for rows in allrows:
+                for r in rows:
+                    key = tuple(r[: len(types)])
+                    assert key not in got, f"group {key} owned by two ranks"
+                    got[key] = r[len(types):]
+            ks, kk, kvs, vs = [], [], [], []
+            for r in range(world):
+                s2, k2, kv2, v2 = table(100 + r, 30_000 + 7000 * r)
+                ks += s2
+                kk += [int(x) if ok else None for x, ok in zip(k2, kv2)]
+                vs += v2.tolist()
+            kcols = [ks] if mode == "utf8" else [ks, kk]
+            want = S.hash_aggregate_rows(kcols, [vs, [1] * len(vs), vs], [S.AGG_SUM, S.AGG_COUNT_STAR, S.AGG_MIN],
+                                         [False] * 3)
+            ok = len(got) == len(want) and all(got[key] == w for key, w in want.items())
+            results[mode] = {"ok": ok, "groups": len(got)}
+    if rank == 0:
+        print("RESULT " + json.dumps(results), flush=True)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()
