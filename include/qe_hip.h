@@ -228,7 +228,9 @@ int qe_agg_global(qe_ctx* ctx, const qe_column* col, const qe_column* mask /*nul
 
 typedef struct qe_agg_desc {
   int32_t fn;         /* QE_AGG_* */
-  int32_t input_type; /* INT64 or FLOAT64 (ignored for COUNT_STAR; AVG accumulates fp64) */
+  int32_t input_type; /* FLOAT64, or INT64 / INT32 / DATE32 / UINT8 (accumulated as int64, so
+                         integer SUM/MIN/MAX outputs are INT64); ignored for COUNT_STAR; AVG
+                         accumulates fp64 */
 } qe_agg_desc;
 
 typedef struct qe_hashagg qe_hashagg;
@@ -240,7 +242,9 @@ int qe_hashagg_destroy(qe_hashagg* agg);
 int qe_hashagg_reset(qe_hashagg* agg);
 
 /* One input batch: per-row keys and pre-evaluated aggregate inputs (agg_inputs[j] is the
- * column of aggregate j; ignored for COUNT_STAR, may be a zeroed struct). `mask` (BOOL,
+ * column of aggregate j; its values are never read for COUNT_STAR, which may pass a zeroed
+ * struct — or, when the state has no keys and no other inputs, any column of the batch, whose
+ * length is then the row count). `mask` (BOOL,
  * nullable pointer) selects rows. Row indices continue across calls in call order: they
  * define "first"/"earliest" for MIN/MAX ties exactly like the reference's batch loop. */
 int qe_hashagg_update(qe_hashagg* agg, const qe_column* keys, const qe_column* agg_inputs,

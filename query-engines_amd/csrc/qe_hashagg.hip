@@ -1493,8 +1493,12 @@ int qe_hashagg_create(qe_ctx* ctx, int32_t nkeys, const int32_t* key_types, int3
     const qe_agg_desc& d = aggs[j];
     h->aggs[j] = d;
     const bool f = d.input_type == QE_TYPE_FLOAT64;
-    if (d.fn != QE_AGG_COUNT_STAR && d.fn != QE_AGG_COUNT && d.input_type != QE_TYPE_INT64 && !f)
-      return bail(fail(QE_ERR_UNSUPPORTED, "aggregate %d: input type %d (int64/fp64 only)", j, d.input_type));
+    // integer inputs of any width accumulate as int64 (the column load sign-/zero-extends)
+    const bool i = d.input_type == QE_TYPE_INT64 || d.input_type == QE_TYPE_INT32 ||
+                   d.input_type == QE_TYPE_DATE32 || d.input_type == QE_TYPE_UINT8;
+    if (d.fn != QE_AGG_COUNT_STAR && d.fn != QE_AGG_COUNT && !i && !f)
+      return bail(fail(QE_ERR_UNSUPPORTED, "aggregate %d: input type %d (int64/int32/date32/uint8/fp64 only)", j,
+                       d.input_type));
     switch (d.fn) {
       case QE_AGG_SUM: h->acc[j] = f ? ACC_SUM_F : ACC_SUM_I; break;
       case QE_AGG_MIN: h->acc[j] = f ? ACC_MIN_F : ACC_MIN_I; break;
@@ -1638,8 +1642,22 @@ int qe_hashagg_update(qe_hashagg* h, const qe_column* keys, const qe_column* agg
   }
   if (mask) QE_TRY(slot_of(*mask, &spec.mask_col));
   if (ncols == 0) {
-    // COUNT(*) only, no keys: still need a row count; use the mask or fail.
-    return fail(QE_ERR_INVALID_ARG, "update needs at least one input column");
+    // COUNT(*) only, no keys: the row count comes from a column passed as a COUNT(*) input
+    // (its values are never read; a UTF-8 column is described by its int32 offsets).
+    for (int j = 0; j < h->naggs && ncols == 0; ++j) {
+      const qe_column& c = agg_inputs[j];
+      if (h->aggs[j].fn != QE_AGG_COUNT_STAR || c.type == 0) continue;
+      qe_column r = c;
+      if (c.type == QE_TYPE_UTF8) {
+        QE_CHECK(c.offsets || c.length == 0, QE_ERR_INVALID_ARG, "COUNT(*) row source: null offsets");
+        r.type = QE_TYPE_INT32;
+        r.values = c.offsets;
+        r.offsets = nullptr;
+      }
+      int s;
+      QE_TRY(slot_of(r, &s));
+    }
+    if (ncols == 0) return fail(QE_ERR_INVALID_ARG, "update needs at least one input column");
   }
   Plan P;
   QE_TRY(compile_plan(h, cols, ncols, &spec, &P));

@@ -12,9 +12,9 @@ from .columnar import Context, DeviceColumn
 def output_type(fn: int, input_type: int) -> int:
     if fn in (N.AGG_COUNT, N.AGG_COUNT_STAR):
         return N.TYPE_INT64
-    if fn == N.AGG_AVG:
+    if fn == N.AGG_AVG or input_type == N.TYPE_FLOAT64:
         return N.TYPE_FLOAT64
-    return input_type
+    return N.TYPE_INT64  # integer inputs of every width accumulate (and come out) as int64
 
 
 _KEY_BITS = {N.TYPE_INT32: 32, N.TYPE_DATE32: 32, N.TYPE_UINT8: 8}
@@ -46,6 +46,16 @@ def packable(key_types) -> bool:
     if any(t not in _KEY_BITS for t in key_types) or len(key_types) > N.MAX_KEYS:
         return False
     return sum(_KEY_BITS[t] + 1 for t in key_types) <= 63
+
+
+def dictionary_keys(key_types) -> Optional[int]:
+    """None when qe_hashagg groups by these keys directly; otherwise the number of device key
+    columns the dictionaries turn them into (UTF-8 keys -> one int32 code each; a key set that
+    does not pack -> one tuple code)."""
+    member = [N.TYPE_INT32 if t == N.TYPE_UTF8 else t for t in key_types]
+    if not packable(member):
+        return 1
+    return len(member) if N.TYPE_UTF8 in key_types else None
 
 
 class HashAggregateState:
@@ -92,20 +102,41 @@ class HashAggregateState:
             pass
 
     # ---- updates --------------------------------------------------------------------------------
-    def update(self, keys: Sequence[DeviceColumn], inputs: Sequence[Optional[DeviceColumn]],
-               mask: Optional[DeviceColumn] = None) -> None:
+    def device_keys(self, keys: Sequence[DeviceColumn]) -> List[DeviceColumn]:
+        """The key columns qe_hashagg groups by: dictionary codes for UTF-8 keys / key tuples."""
         keys = [self.dicts[i].encode(k) if i in self.dicts else k for i, k in enumerate(keys)]
         if self.tuple_dict is not None:
             keys = [self.tuple_dict.encode_tuple(keys)]
+        return keys
+
+    def update(self, keys: Sequence[DeviceColumn], inputs: Sequence[Optional[DeviceColumn]],
+               mask: Optional[DeviceColumn] = None) -> None:
+        """A COUNT(*) input may be any column of the batch: with no keys and no other inputs its
+        length is the row count (qe_hashagg_update)."""
+        keys = self.device_keys(keys)
         kc = (N.QeColumn * max(1, len(keys)))(*[k.as_c() for k in keys])
         ic = (N.QeColumn * max(1, len(self.aggs)))(
             *[(x.as_c() if x is not None else N.QeColumn()) for x in inputs])
         mc = mask.as_c() if mask is not None else None
         N.check(N.lib().qe_hashagg_update(self.handle, kc, ic, N.C.byref(mc) if mc is not None else None))
 
-    def update_fused(self, cols: Sequence[DeviceColumn], spec: N.QeFusedSpec) -> None:
-        if self.dicts or self.tuple_dict is not None:
-            raise N.IllegalStateException(N.QE_ERR_UNSUPPORTED, "fused update with dictionary-encoded keys")
+    def update_fused(self, cols: Sequence[DeviceColumn], spec: N.QeFusedSpec,
+                     key_cols: Optional[Sequence[DeviceColumn]] = None) -> None:
+        """Dictionary-keyed states take the original key columns in `key_cols`: they are encoded
+        (over every row; codes of rows the predicate drops never form a group) and their codes
+        join the fused launch as extra column slots after `cols`."""
+        cols = list(cols)
+        if self.keyed_by_dictionary:
+            if key_cols is None:
+                raise N.IllegalStateException(N.QE_ERR_UNSUPPORTED,
+                                              "fused update with dictionary-encoded keys needs the key columns")
+            codes = self.device_keys(key_cols)
+            if len(cols) + len(codes) > N.MAX_COLS:
+                raise N.IllegalStateException(N.QE_ERR_UNSUPPORTED, f"fused plan takes at most {N.MAX_COLS} columns")
+            spec = N.QeFusedSpec.from_buffer_copy(spec)
+            for k in range(len(codes)):
+                spec.key_cols[k] = len(cols) + k
+            cols += codes
         cc = (N.QeColumn * len(cols))(*[c.as_c() for c in cols])
         N.check(N.lib().qe_hashagg_update_fused(self.handle, cc, len(cols), N.C.byref(spec)))
 

@@ -11,7 +11,7 @@ from __future__ import annotations
 from typing import Iterator, List, Optional, Sequence
 
 from . import native as N
-from .aggregate import HashAggregateState, output_type
+from .aggregate import HashAggregateState, dictionary_keys, output_type
 from .columnar import DeviceColumn, Field, RecordBatch, Schema
 from .expressions import (
     AggregateExpression,
@@ -174,15 +174,19 @@ class HashAggregateExec(PhysicalPlan):
             for c in keys + [i for i in inputs if i is not None]:
                 if not isinstance(c, DeviceColumn):
                     raise N.IllegalStateException(N.QE_ERR_UNSUPPORTED, "aggregate inputs must be device columns")
+            present = keys + [i for i in inputs if i is not None]
+            if not present and batch.fields:  # COUNT(*) alone: any column gives the row count
+                present = [batch.field(0)]
+                inputs = [present[0] if a.fn == N.AGG_COUNT_STAR else i for a, i in zip(self.aggregateExpr, inputs)]
+            if not present:
+                raise N.IllegalStateException(N.QE_ERR_UNSUPPORTED, "COUNT(*) over a batch without columns")
             if state is None:
-                ctx = (keys + [i for i in inputs if i is not None])[0].ctx if (keys or any(inputs)) else None
-                if ctx is None:
-                    raise N.IllegalStateException(N.QE_ERR_UNSUPPORTED, "COUNT(*) needs an input column")
                 state = HashAggregateState(
-                    ctx, [k.type for k in keys],
-                    [(a.fn, (i.type if i is not None else N.TYPE_INT64)) for a, i in zip(self.aggregateExpr, inputs)],
+                    present[0].ctx, [k.type for k in keys],
+                    [(a.fn, (i.type if i is not None and a.fn != N.AGG_COUNT_STAR else N.TYPE_INT64))
+                     for a, i in zip(self.aggregateExpr, inputs)],
                     self.expected_groups)
-            state.update(keys, [i if a.fn != N.AGG_COUNT_STAR else None for a, i in zip(self.aggregateExpr, inputs)])
+            state.update(keys, inputs)
         self.state = state
         return state
 
@@ -214,8 +218,10 @@ class FusedHashAggregateExec(PhysicalPlan):
     (qe_hashagg_update_fused). Same results as the unfused chain."""
 
     def __init__(self, scan: PhysicalPlan, slots: Sequence[int], spec: N.QeFusedSpec, key_types, aggs,
-                 schema: Schema, groupExpr, aggregateExpr, expected_groups: int = 1024):  # noqa: N803
+                 schema: Schema, groupExpr, aggregateExpr, expected_groups: int = 1024,  # noqa: N803
+                 key_scan: Optional[Sequence[int]] = None):
         self.scan = scan
+        self.key_scan = list(key_scan) if key_scan is not None else None  # dictionary keys: scan columns
         self.slots = list(slots)  # scan column index per slot
         self.spec = spec
         self.key_types = list(key_types)
@@ -235,9 +241,10 @@ class FusedHashAggregateExec(PhysicalPlan):
     def partial_state(self, state: Optional[HashAggregateState] = None) -> Optional[HashAggregateState]:
         for batch in self.scan.execute():
             cols = [batch.field(i) for i in self.slots]
+            key_cols = [batch.field(i) for i in self.key_scan] if self.key_scan is not None else None
             if state is None:
-                state = HashAggregateState(cols[0].ctx, self.key_types, self.aggs, self.expected_groups)
-            state.update_fused(cols, self.spec)
+                state = HashAggregateState((cols or key_cols)[0].ctx, self.key_types, self.aggs, self.expected_groups)
+            state.update_fused(cols, self.spec, key_cols)
         self.state = state
         return state
 
@@ -439,15 +446,21 @@ def fuse(plan: PhysicalPlan) -> PhysicalPlan:
                 pt.rhs_col = -1
                 pt.lit = lit
         spec.nterms = len(terms)
-        key_types = []
-        for k, g in enumerate(plan.groupExpr):
+        key_types, key_scan = [], []
+        for g in plan.groupExpr:
             g = _resolve(g, proj)
             if not isinstance(g, ColumnExpression):
                 raise _NotFusable("group key must be a column")
-            if sm.type_of(g.i) not in N.FIXED_WIDTH:
-                raise _NotFusable("UTF-8 group keys go through the string dictionary (unfused)")
-            spec.key_cols[k] = sm.slot(g.i)
+            if sm.type_of(g.i) not in N.FIXED_WIDTH and sm.type_of(g.i) != N.TYPE_UTF8:
+                raise _NotFusable("group key type")
+            key_scan.append(g.i)
             key_types.append(sm.type_of(g.i))
+        # UTF-8 keys / key sets wider than 63 bits: encoded to dictionary codes per batch, which
+        # join the launch as extra slots (HashAggregateState.update_fused)
+        ndict = dictionary_keys(key_types)
+        if ndict is None:
+            for k, i in enumerate(key_scan):
+                spec.key_cols[k] = sm.slot(i)
         aggs = []
         for j, a in enumerate(plan.aggregateExpr):
             if a.fn == N.AGG_COUNT_STAR:
@@ -461,10 +474,13 @@ def fuse(plan: PhysicalPlan) -> PhysicalPlan:
             for t, tok in enumerate(toks):
                 spec.inputs[j].tokens[t] = tok
             aggs.append((a.fn, N.TYPE_FLOAT64 if is_f else N.TYPE_INT64))
-        if not sm.slots:
+        if ndict is not None and len(sm.slots) + ndict > N.MAX_COLS:
+            raise _NotFusable("too many columns with the key codes")
+        if not sm.slots and ndict is None:
             raise _NotFusable("no input columns")
         return FusedHashAggregateExec(node, sm.slots, spec, key_types, aggs, plan.schema(), plan.groupExpr,
-                                      plan.aggregateExpr, plan.expected_groups)
+                                      plan.aggregateExpr, plan.expected_groups,
+                                      key_scan if ndict is not None else None)
     except _NotFusable:
         return plan
 
