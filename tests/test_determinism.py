@@ -1,0 +1,147 @@
+"""Run-to-run determinism on the GPU (SURVEY §5 "Race detection / sanitizers": the device side's
+race check). Every device path runs several times over the same inputs, on the default stream and
+on a second context (own HIP stream); results must be identical bit for bit, except where the
+design documents otherwise:
+
+* compaction (filter, select-project), CAST, CSV scan, global aggregate (per-block partials and a
+  fixed-order final pass), and every integer / MIN / MAX / COUNT group result: bit-identical;
+* hash-aggregate fp64 SUM / AVG: the per-group sums combine workgroup partials with fp64 atomics,
+  so their rounding depends on arrival order. Run to run they must agree within 1e-13 × Σ|x| of
+  the group (a condition-aware bound: cancelling sums amplify the relative spread; the parity
+  contract of 1e-9 against the oracle holds either way) — DESIGN.md "Determinism".
+Group ORDER is unspecified (HashMap iteration order, K:639), so groups are compared as maps."""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+RUNS = 4
+
+
+def _runs(gpu_ctx):
+    """Yields the context of each run: the default context three times, then a second context on
+    its own HIP stream; each run allocates and launches under that context's stream."""
+    import torch
+
+    from kquery.columnar import Context
+
+    s = torch.cuda.Stream()
+    with torch.cuda.stream(s):
+        other = Context.get(0)
+    for ctx, stream in [(gpu_ctx, torch.cuda.current_stream())] * (RUNS - 1) + [(other, s)]:
+        with torch.cuda.stream(stream):
+            yield ctx
+            ctx.synchronize()
+
+
+def _bits(c):
+    from kquery import native as N
+
+    if c.type == N.TYPE_UTF8:
+        return c.offsets[: c.length + 1].cpu().numpy().tobytes(), c.to_numpy().tolist(), c.valid_mask().tobytes()
+    return c.to_numpy().view(np.uint8).tobytes(), c.valid_mask().tobytes()
+
+
+def test_filter_and_select_project(gpu_ctx):
+    from kquery import native as N
+    from kquery.columnar import DeviceColumn, RecordBatch, Schema
+    from kquery.operators import filter_batch
+    from test_selproj import _run, _spec
+
+    rng = np.random.default_rng(3)
+    n = 6_000_001
+    a = rng.integers(-2**63, 2**63 - 1, n, dtype=np.int64, endpoint=True)
+    f = rng.normal(size=n)
+    m = rng.random(n) < 0.5
+    av = rng.random(n) > 0.1
+    outs = []
+    for ctx in _runs(gpu_ctx):
+        cols = [DeviceColumn.from_numpy(N.TYPE_INT64, a, av, ctx=ctx),
+                DeviceColumn.from_numpy(N.TYPE_FLOAT64, f, None, ctx=ctx)]
+        fb = filter_batch(RecordBatch(Schema([]), cols), DeviceColumn.from_numpy(N.TYPE_BOOL, m, None, ctx=ctx))
+        spec = _spec(N, [(1, N.OP_GT, -1, 0.25)], [[(N.TOK_COL, 0, None), (N.TOK_COL, 1, None), (N.TOK_MUL, 0, None)],
+                                                  [(N.TOK_COL, 0, None)]])
+        cnt, sp = _run(ctx, cols, spec, [N.TYPE_FLOAT64, N.TYPE_INT64])
+        ctx.synchronize()
+        outs.append([_bits(c) for c in fb.fields] + [cnt] + [_bits(c) for c in sp])
+    assert all(o == outs[0] for o in outs[1:])
+
+
+def test_global_aggregate_f64(gpu_ctx):
+    from kquery import native as N
+    from kquery.columnar import DeviceColumn
+    from test_gpu_parity import _global
+
+    rng = np.random.default_rng(5)
+    n = 40_000_003
+    x = rng.normal(size=n) * np.exp(rng.normal(size=n) * 8)  # wide dynamic range: order-sensitive
+    res = []
+    for ctx in _runs(gpu_ctx):
+        r = _global(ctx, DeviceColumn.from_numpy(N.TYPE_FLOAT64, x, None, ctx=ctx))
+        res.append((r.sum, r.min, r.max, r.count, r.avg))
+    assert all(r == res[0] for r in res[1:]), res
+
+
+def test_hash_aggregate(gpu_ctx):
+    from kquery import native as N
+    from kquery.aggregate import HashAggregateState
+    from kquery.columnar import DeviceColumn
+
+    rng = np.random.default_rng(9)
+    n = 8_000_000
+    k = rng.integers(0, 5000, n).astype(np.int64)  # beyond one LDS table: global merge path too
+    x = rng.normal(size=n) * 1e3
+    y = rng.integers(-2**40, 2**40, n).astype(np.int64)
+    aggs = [(N.AGG_SUM, N.TYPE_FLOAT64), (N.AGG_AVG, N.TYPE_FLOAT64), (N.AGG_MIN, N.TYPE_FLOAT64),
+            (N.AGG_MAX, N.TYPE_FLOAT64), (N.AGG_SUM, N.TYPE_INT64), (N.AGG_COUNT, N.TYPE_INT64),
+            (N.AGG_MIN, N.TYPE_INT64)]
+    yv = rng.random(n) > 0.2
+    runs = []
+    for ctx in _runs(gpu_ctx):
+        kc = DeviceColumn.from_numpy(N.TYPE_INT64, k, None, ctx=ctx)
+        xc = DeviceColumn.from_numpy(N.TYPE_FLOAT64, x, None, ctx=ctx)
+        yc = DeviceColumn.from_numpy(N.TYPE_INT64, y, yv, ctx=ctx)
+        st = HashAggregateState(ctx, [N.TYPE_INT64], aggs, 1024)
+        st.update([kc], [xc, xc, xc, xc, yc, yc, yc])
+        keys, vals = st.finalize()
+        ctx.synchronize()
+        cols = [v.to_pylist() for v in vals]
+        runs.append({kk: [c[i] for c in cols] for i, kk in enumerate(keys[0].to_pylist())})
+    absum = np.bincount(k, weights=np.abs(x))
+    cnt = np.bincount(k)
+    base = runs[0]
+    for r in runs[1:]:
+        assert r.keys() == base.keys()
+        for kk, v in r.items():
+            b = base[kk]
+            assert v[2:] == b[2:], kk  # MIN/MAX fp64 and every integer result: bit-identical
+            bound = 1e-13 * absum[kk]  # fp64 SUM / AVG: atomic arrival order
+            assert abs(v[0] - b[0]) <= bound, (kk, v[0], b[0])
+            assert abs(v[1] - b[1]) <= bound / cnt[kk], (kk, v[1], b[1])
+
+
+def test_csv_cast_string_keys(gpu_ctx, tmp_path):
+    from kquery import native as N
+    from kquery.aggregate import HashAggregateState
+    from kquery.columnar import DeviceColumn
+    from kquery.csv_source import CsvDataSource
+
+    rng = np.random.default_rng(1)
+    rows = 300_000
+    vend = rng.choice(["1", "2", "VTS", "CMT", '"q,x"'], rows)
+    fare = rng.uniform(-5, 500, rows)
+    p = tmp_path / "t.csv"
+    p.write_text("VendorID,fare_amount\n" + "".join(f"{v},{x:.3f}\n" for v, x in zip(vend, fare)))
+    outs = []
+    for ctx in _runs(gpu_ctx):
+        b = next(CsvDataSource(str(p), True, 0, ctx=ctx).scan(["VendorID", "fare_amount"]))
+        fs = b.field(1)
+        out = DeviceColumn.empty(N.TYPE_FLOAT64, fs.length, False, ctx=ctx)
+        ic, oc = fs.as_c(), out.as_c()
+        N.check(N.lib().qe_cast_utf8_to_f64(ctx.handle, N.C.byref(ic), N.C.byref(oc), None))
+        st = HashAggregateState(ctx, [N.TYPE_UTF8], [(N.AGG_MAX, N.TYPE_FLOAT64), (N.AGG_COUNT, N.TYPE_FLOAT64)], 16)
+        st.update([b.field(0)], [out, out])
+        keys, vals = st.finalize()
+        ctx.synchronize()
+        groups = dict(zip(keys[0].to_pylist(), zip(*[v.to_pylist() for v in vals])))
+        outs.append((_bits(b.field(0)), _bits(fs), _bits(out), groups))
+    assert all(o == outs[0] for o in outs[1:])
