@@ -329,10 +329,26 @@ int qe_hashagg_record_bytes(qe_hashagg* agg, int64_t* out);
 /* counts[p] = records for partition p (host array of nparts, synchronises). */
 int qe_hashagg_export_counts(qe_hashagg* agg, int32_t nparts, int64_t* counts);
 /* Writes all records into `dst` (device, sum(counts)*record_bytes), partition-major in
- * partition order, matching the counts of the preceding export_counts call. */
+ * partition order (counts as qe_hashagg_export_counts reports them). Stream-ordered, no host
+ * synchronisation. */
 int qe_hashagg_export(qe_hashagg* agg, int32_t nparts, void* dst);
 /* Merge `nrecords` records (device) into this state (combine semantics per aggregate). */
 int qe_hashagg_import(qe_hashagg* agg, const void* records, int64_t nrecords);
+
+/* Fixed-capacity exchange: ONE equal-split all-to-all and no host synchronisation before it.
+ * export_slots writes `nparts` slots of QE_SLOT_HEADER + slot_records * record_bytes bytes into
+ * `dst` (device): slot p holds the first `slot_records` groups of partition p (same partition
+ * function as qe_hashagg_export); its header's int64 word 0 is the partition's full count, word 1
+ * the largest count over all of this state's partitions. import_slots merges `nslots` received
+ * slots (one per sender); *max_count = the largest count any sender reported (every receiver sees
+ * every sender's word 1, so all ranks get the same value). If *max_count > slot_records some
+ * sender's groups did not fit: NOTHING is imported, and every rank should exchange again with
+ * qe_hashagg_export / qe_hashagg_import. *nrecords (optional) = records the slots hold.
+ * import_slots synchronises once (to read the headers); export_slots does not. */
+#define QE_SLOT_HEADER 64
+int qe_hashagg_export_slots(qe_hashagg* agg, int32_t nparts, int64_t slot_records, void* dst);
+int qe_hashagg_import_slots(qe_hashagg* agg, const void* slots, int32_t nslots, int64_t slot_records,
+                            int64_t* max_count, int64_t* nrecords);
 
 /* Offset added to row indices of the next update (for shards of one logical stream). */
 int qe_hashagg_set_row_base(qe_hashagg* agg, int64_t row_base);

@@ -52,6 +52,38 @@ def encode(groups: Dict[int, Tuple[int, List[Tuple[int, int]]]], fns: Sequence[i
     return b"".join(b"".join(b) for b in buckets), [len(b) for b in buckets]
 
 
+SLOT_HEADER = 64
+
+
+def encode_slots(groups: Dict[int, Tuple[int, List[Tuple[int, int]]]], fns: Sequence[int], nparts: int,
+                 slot_records: int) -> bytes:
+    """qe_hashagg_export_slots' layout: per partition a 64-byte header (word 0 = the partition's
+    full count, word 1 = the largest count over all partitions) then `slot_records` record
+    places, the first min(count, slot_records) filled."""
+    payload, counts = encode(groups, fns, nparts)
+    rb = record_bytes(len(fns))
+    out, off = b"", 0
+    for c in counts:
+        recs = payload[off: off + min(c, slot_records) * rb]
+        off += c * rb
+        hdr = struct.pack("<QQ", c, max(counts)) + bytes(SLOT_HEADER - 16)
+        out += hdr + recs + bytes(slot_records * rb - len(recs))
+    return out
+
+
+def decode_slots(buf: bytes, nslots: int, slot_records: int, naggs: int):
+    """Received slots -> (records, largest count any sender reported) — qe_hashagg_import_slots'
+    reading; when the largest count exceeds slot_records the records are incomplete."""
+    rb = record_bytes(naggs)
+    sb = SLOT_HEADER + slot_records * rb
+    recs, mx = [], 0
+    for i in range(nslots):
+        c, m = struct.unpack_from("<QQ", buf, i * sb)
+        mx = max(mx, m)
+        recs += decode(buf[i * sb + SLOT_HEADER: i * sb + SLOT_HEADER + min(c, slot_records) * rb], naggs)
+    return recs, mx
+
+
 def decode(payload: bytes, naggs: int) -> List[Tuple[int, int, List[Tuple[int, int]]]]:
     rb = record_bytes(naggs)
     out = []

@@ -766,30 +766,65 @@ __global__ void k_rehash(DTable src, DTable dst, AggMeta m) {
 }
 
 // Merge fixed-size records (export format) into `dst`.
+__device__ void import_record(const qu8* __restrict__ rec, DTable& dst, const AggMeta& m) {
+  const qi64 key = ((const qi64*)rec)[0];
+  const bool knull = ((const qu64*)rec)[1] & 1;
+  const qu64 c = ((const qu64*)rec)[2];
+  qu64 d;
+  if (!gtable_find(dst, key, knull, d)) {
+    atomicAdd((unsigned long long*)&dst.ctl[3], 1ull);
+    return;
+  }
+  gadd_cstar(dst, d, c);
+  int off = 24;
+  for (int j = 0; j < m.naggs; ++j) {
+    DAgg a{};
+    a.fn = m.fn[j];
+    a.acc = m.acc[j];
+    const qu64* f = (const qu64*)(rec + off);
+    if (a.fn != QE_AGG_COUNT_STAR) {
+      if (acc_is_f64mm(a.acc)) gcombine(dst, a.acc, j, d, (qi64)f[0], f[1], f[2], f[3], f[4], f[5]);
+      else gcombine(dst, a.acc, j, d, (qi64)f[0], f[1], ~0ull, ~0ull, ~0ull, ~0ull);
+    }
+    off += agg_rec_bytes(a.acc);
+  }
+}
+
 __global__ void k_import(const qu8* __restrict__ recs, qi64 nrec, qi32 rec_bytes, DTable dst, AggMeta m) {
-  for (qi64 r = blockIdx.x * (qi64)blockDim.x + threadIdx.x; r < nrec; r += (qi64)gridDim.x * blockDim.x) {
-    const qu8* rec = recs + r * rec_bytes;
-    const qi64 key = ((const qi64*)rec)[0];
-    const bool knull = ((const qu64*)rec)[1] & 1;
-    const qu64 c = ((const qu64*)rec)[2];
-    qu64 d;
-    if (!gtable_find(dst, key, knull, d)) {
-      atomicAdd((unsigned long long*)&dst.ctl[3], 1ull);
-      continue;
-    }
-    gadd_cstar(dst, d, c);
-    int off = 24;
-    for (int j = 0; j < m.naggs; ++j) {
-      DAgg a{};
-      a.fn = m.fn[j];
-      a.acc = m.acc[j];
-      const qu64* f = (const qu64*)(rec + off);
-      if (a.fn != QE_AGG_COUNT_STAR) {
-        if (acc_is_f64mm(a.acc)) gcombine(dst, a.acc, j, d, (qi64)f[0], f[1], f[2], f[3], f[4], f[5]);
-        else gcombine(dst, a.acc, j, d, (qi64)f[0], f[1], ~0ull, ~0ull, ~0ull, ~0ull);
-      }
-      off += agg_rec_bytes(a.acc);
-    }
+  for (qi64 r = blockIdx.x * (qi64)blockDim.x + threadIdx.x; r < nrec; r += (qi64)gridDim.x * blockDim.x)
+    import_record(recs + r * rec_bytes, dst, m);
+}
+
+// Received slots (qe_hashagg_import_slots): header word 0 = records in the slot (the sender's
+// count; may exceed the capacity), word 1 = the sender's largest count over all its slots.
+__global__ void k_slots_scan(const qu8* __restrict__ slots, qi32 nslots, qu64 slot_bytes, qu64* ctl) {
+  // one wave: ctl[4] = max over senders of their largest count, ctl[5] = records held in total
+  qu64 mx = 0, tot = 0;
+  for (int i = threadIdx.x; i < nslots; i += blockDim.x) {
+    const qu64* hd = (const qu64*)(slots + (qu64)i * slot_bytes);
+    mx = hd[1] > mx ? hd[1] : mx;
+    tot += hd[0];
+  }
+  for (int off = 32; off > 0; off >>= 1) {
+    const qu64 o = __shfl_xor(mx, off);
+    mx = o > mx ? o : mx;
+    tot += __shfl_xor(tot, off);
+  }
+  if (threadIdx.x == 0) {
+    ctl[4] = mx;
+    ctl[5] = tot;
+  }
+}
+
+__global__ void k_import_slots(const qu8* __restrict__ slots, qi32 nslots, qi64 slot_records, qi32 rec_bytes,
+                               DTable dst, AggMeta m) {
+  const qu64 slot_bytes = QE_SLOT_HEADER + (qu64)slot_records * rec_bytes;
+  const qi64 total = (qi64)nslots * slot_records;
+  for (qi64 r = blockIdx.x * (qi64)blockDim.x + threadIdx.x; r < total; r += (qi64)gridDim.x * blockDim.x) {
+    const qi64 sl = r / slot_records, i = r - sl * slot_records;
+    const qu8* base = slots + (qu64)sl * slot_bytes;
+    if ((qu64)i >= ((const qu64*)base)[0]) continue;
+    import_record(base + QE_SLOT_HEADER + (qu64)i * rec_bytes, dst, m);
   }
 }
 
@@ -808,6 +843,32 @@ __global__ void k_export_count(DTable t, qi32 nparts, unsigned long long* counts
   }
 }
 
+__device__ void write_record(qu8* rec, const DTable& t, const AggMeta& m, qu64 s, qi64 key, bool knull) {
+  const qu64 SS = t.cap + 2;
+  write_record_head(rec, key, knull, t.cstar[s]);
+  int off = 24;
+  for (int j = 0; j < m.naggs; ++j) {
+    qu64* f = (qu64*)(rec + off);
+    f[0] = (qu64)t.acc[j][s];
+    f[1] = t.nn[j][s];
+    if (acc_is_f64mm(m.acc[j]))
+      for (int k = 0; k < 4; ++k) f[2 + k] = t.idx[j][k * SS + s];
+    off += agg_rec_bytes(m.acc[j]);
+  }
+}
+
+// counts (nparts) -> exclusive offsets in place; one wave, nparts is a rank count
+__global__ void k_counts_to_cursors(unsigned long long* c, qi32 nparts) {
+  if (threadIdx.x == 0) {
+    unsigned long long run = 0;
+    for (int p = 0; p < nparts; ++p) {
+      const unsigned long long x = c[p];
+      c[p] = run;
+      run += x;
+    }
+  }
+}
+
 __global__ void k_export(DTable t, AggMeta m, qi32 nparts, qi32 rec_bytes, unsigned long long* cursor,
                          qu8* __restrict__ dst) {
   const qu64 SS = t.cap + 2;
@@ -817,17 +878,41 @@ __global__ void k_export(DTable t, AggMeta m, qi32 nparts, qi32 rec_bytes, unsig
     const qi64 key = knull ? 0 : (s == t.cap + 1 ? EMPTY_KEY : t.keys[s]);
     const qu32 p = partition_of(key, knull, nparts);
     const qu64 pos = atomicAdd(&cursor[p], 1ull);
-    qu8* rec = dst + pos * (qu64)rec_bytes;
-    write_record_head(rec, key, knull, t.cstar[s]);
-    int off = 24;
-    for (int j = 0; j < m.naggs; ++j) {
-      qu64* f = (qu64*)(rec + off);
-      f[0] = (qu64)t.acc[j][s];
-      f[1] = t.nn[j][s];
-      if (acc_is_f64mm(m.acc[j]))
-        for (int k = 0; k < 4; ++k) f[2 + k] = t.idx[j][k * SS + s];
-      off += agg_rec_bytes(m.acc[j]);
-    }
+    write_record(dst + pos * (qu64)rec_bytes, t, m, s, key, knull);
+  }
+}
+
+// Fixed-capacity slots (qe_hashagg_export_slots): the first `slot_records` groups of partition p
+// go to slot p; cursor[p] ends as the partition's full count
+__global__ void k_export_slots(DTable t, AggMeta m, qi32 nparts, qi32 rec_bytes, qi64 slot_records,
+                               unsigned long long* cursor, qu8* __restrict__ dst) {
+  const qu64 SS = t.cap + 2;
+  const qu64 slot_bytes = QE_SLOT_HEADER + (qu64)slot_records * rec_bytes;
+  for (qu64 s = blockIdx.x * (qu64)blockDim.x + threadIdx.x; s < SS; s += (qu64)gridDim.x * blockDim.x) {
+    if (!gslot_occupied(t, s)) continue;
+    const bool knull = s == t.cap;
+    const qi64 key = knull ? 0 : (s == t.cap + 1 ? EMPTY_KEY : t.keys[s]);
+    const qu32 p = partition_of(key, knull, nparts);
+    const qu64 pos = atomicAdd(&cursor[p], 1ull);
+    if (pos < (qu64)slot_records)
+      write_record(dst + p * slot_bytes + QE_SLOT_HEADER + pos * (qu64)rec_bytes, t, m, s, key, knull);
+  }
+}
+
+__global__ void k_slot_headers(const unsigned long long* __restrict__ cursor, qi32 nparts, qu64 slot_bytes,
+                               qu8* __restrict__ dst) {
+  // one wave: word 0 = this slot's count, word 1 = the largest count over all slots
+  qu64 mx = 0;
+  for (int p = threadIdx.x; p < nparts; p += blockDim.x) mx = cursor[p] > mx ? cursor[p] : mx;
+  for (int off = 32; off > 0; off >>= 1) {
+    const qu64 o = __shfl_xor(mx, off);
+    mx = o > mx ? o : mx;
+  }
+  for (int p = threadIdx.x; p < nparts; p += blockDim.x) {
+    qu64* hd = (qu64*)(dst + (qu64)p * slot_bytes);
+    hd[0] = cursor[p];
+    hd[1] = mx;
+    for (int w = 2; w < QE_SLOT_HEADER / 8; ++w) hd[w] = 0;
   }
 }
 
@@ -874,6 +959,62 @@ __device__ __forceinline__ void store_typed(void* p, qi32 type, qi64 i, qi64 x) 
   }
 }
 
+// one occupied slot -> output row o of the batch. Validity bits go to the output bitmaps with
+// global atomics, or (lbits != nullptr) to per-column LDS bitmaps of FS_WORDS words each.
+constexpr int FS_WORDS = 512;
+__device__ __forceinline__ void put_bit(qu8* gbm, qu32* lbits, int col, qi64 o, bool v) {
+  if (!v) return;
+  if (lbits) atomicOr(lbits + col * FS_WORDS + (o >> 5), 1u << (o & 31));
+  else set_bit(gbm, o, true);
+}
+
+__device__ __forceinline__ void finalize_slot(const DTable& t, const AggMeta& m, const KeyMeta& km,
+                                              const OutCols& out, qu64 s, qi64 o, qu32* lbits = nullptr) {
+  const qu64 SS = t.cap + 2;
+  const bool knull = s == t.cap;
+  const qi64 key = knull ? 0 : (s == t.cap + 1 ? EMPTY_KEY : t.keys[s]);
+  // keys
+  if (km.mode == 1) {
+    store_typed(out.keys[0].values, km.type[0], o, key);
+    if (out.keys[0].validity) put_bit(out.keys[0].validity, lbits, 0, o, !knull);
+  } else if (km.mode == 2) {
+    for (int k = 0; k < km.nkeys; ++k) {
+      const bool isn = (key >> km.nullbit[k]) & 1;
+      qi64 x = (key >> km.shift[k]) & km.fmask[k];
+      if (km.type[k] == QE_TYPE_INT32 || km.type[k] == QE_TYPE_DATE32) x = (qi64)(qi32)x;  // sign
+      store_typed(out.keys[k].values, km.type[k], o, x);
+      if (out.keys[k].validity) put_bit(out.keys[k].validity, lbits, k, o, !isn);
+    }
+  }
+  // aggregates
+  for (int j = 0; j < m.naggs; ++j) {
+    const qu64 nn = t.nn[j][s];
+    const qi64 acc = t.acc[j][s];
+    qi64 val = 0;
+    bool valid = nn > 0;
+    switch (m.fn[j]) {
+      case QE_AGG_COUNT: val = (qi64)nn; valid = true; break;
+      case QE_AGG_COUNT_STAR: val = (qi64)t.cstar[s]; valid = true; break;
+      case QE_AGG_AVG: val = f64_bits(bits_f64(acc) / (double)nn); break;
+      default:
+        if (acc_is_f64mm(m.acc[j])) {
+          const qu64 i0 = t.idx[j][s], i1 = t.idx[j][SS + s];
+          const qu64 i2 = t.idx[j][2 * SS + s], i3 = t.idx[j][3 * SS + s];
+          if (i1 != ~0ull && i1 == i0) {
+            val = 0x7FF8000000000000ll;  // first non-null value was NaN: sticky seed
+          } else {
+            const double d = okey_f64(acc);
+            val = d == 0.0 ? f64_bits(i2 < i3 ? -0.0 : 0.0) : f64_bits(d);
+          }
+        } else {
+          val = acc;
+        }
+    }
+    ((qi64*)out.aggs[j].values)[o] = valid ? val : 0;
+    if (out.aggs[j].validity) put_bit(out.aggs[j].validity, lbits, QE_MAX_KEYS + j, o, valid);
+  }
+}
+
 __global__ void k_finalize(DTable t, AggMeta m, KeyMeta km, const qi64* __restrict__ tile_offsets,
                            qi32 tile_slots, OutCols out) {
   // one block per tile; each wave scans its slots in order (ballot + popc keeps slot order)
@@ -893,53 +1034,66 @@ __global__ void k_finalize(DTable t, AggMeta m, KeyMeta km, const qi64* __restri
       woff += w < wid ? wtot[w] : 0;
       btot += wtot[w];
     }
-    if (occ) {
-      const qi64 o = base + woff + __popcll(b & lt);
-      const bool knull = s == t.cap;
-      const qi64 key = knull ? 0 : (s == t.cap + 1 ? EMPTY_KEY : t.keys[s]);
-      // keys
-      if (km.mode == 1) {
-        store_typed(out.keys[0].values, km.type[0], o, key);
-        if (out.keys[0].validity) set_bit(out.keys[0].validity, o, !knull);
-      } else if (km.mode == 2) {
-        for (int k = 0; k < km.nkeys; ++k) {
-          const bool isn = (key >> km.nullbit[k]) & 1;
-          qi64 x = (key >> km.shift[k]) & km.fmask[k];
-          if (km.type[k] == QE_TYPE_INT32 || km.type[k] == QE_TYPE_DATE32) x = (qi64)(qi32)x;  // sign
-          store_typed(out.keys[k].values, km.type[k], o, x);
-          if (out.keys[k].validity) set_bit(out.keys[k].validity, o, !isn);
-        }
-      }
-      // aggregates
-      for (int j = 0; j < m.naggs; ++j) {
-        const qu64 nn = t.nn[j][s];
-        const qi64 acc = t.acc[j][s];
-        qi64 val = 0;
-        bool valid = nn > 0;
-        switch (m.fn[j]) {
-          case QE_AGG_COUNT: val = (qi64)nn; valid = true; break;
-          case QE_AGG_COUNT_STAR: val = (qi64)t.cstar[s]; valid = true; break;
-          case QE_AGG_AVG: val = f64_bits(bits_f64(acc) / (double)nn); break;
-          default:
-            if (acc_is_f64mm(m.acc[j])) {
-              const qu64 i0 = t.idx[j][s], i1 = t.idx[j][SS + s];
-              const qu64 i2 = t.idx[j][2 * SS + s], i3 = t.idx[j][3 * SS + s];
-              if (i1 != ~0ull && i1 == i0) {
-                val = 0x7FF8000000000000ll;  // first non-null value was NaN: sticky seed
-              } else {
-                const double d = okey_f64(acc);
-                val = d == 0.0 ? f64_bits(i2 < i3 ? -0.0 : 0.0) : f64_bits(d);
-              }
-            } else {
-              val = acc;
-            }
-        }
-        ((qi64*)out.aggs[j].values)[o] = valid ? val : 0;
-        if (out.aggs[j].validity) set_bit(out.aggs[j].validity, o, valid);
-      }
-    }
+    if (occ) finalize_slot(t, m, km, out, s, base + woff + __popcll(b & lt));
     base += btot;
     __syncthreads();
+  }
+}
+
+// Small tables (<= FS_THREADS * FS_PER slots): the whole finalize in ONE workgroup — validity
+// zeroing, occupancy, slot-order prefix and the writes — instead of memsets + count + scan +
+// write launches. Slot s = FS_THREADS * i + tid (chunk i): every occupancy load is coalesced and
+// independent of the others; the prefix is ballots + one LDS exchange.
+constexpr int FS_THREADS = 1024, FS_PER = 16, FS_WAVES = FS_THREADS / 64;
+static_assert(FS_THREADS * FS_PER / 2 / 32 <= FS_WORDS, "LDS bitmaps hold every group of a small table");
+__global__ void __launch_bounds__(FS_THREADS) k_finalize_small(DTable t, AggMeta m, KeyMeta km, OutCols out,
+                                                               qi64 groups) {
+  __shared__ qi32 wcnt[FS_PER][FS_WAVES];  // set slots per (chunk, wave)
+  __shared__ qu64 wbal[FS_PER][FS_WAVES];  // their ballots
+  __shared__ qu32 lbits[(QE_MAX_KEYS + QE_MAX_AGGS) * FS_WORDS];  // validity, copied out at the end
+  __shared__ qi32 cbase[FS_PER + 1];       // rows before each chunk
+  const qu64 SS = t.cap + 2;
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const qu64 lt = lane ? (~0ull >> (64 - lane)) : 0ull;
+  const int words = (int)((groups + 31) >> 5);  // <= FS_WORDS: groups <= half the slots
+  for (int w = tid; w < (QE_MAX_KEYS + QE_MAX_AGGS) * FS_WORDS; w += FS_THREADS) lbits[w] = 0;
+  qu32 occ = 0;
+#pragma unroll
+  for (int i = 0; i < FS_PER; ++i) {
+    const qu64 s = (qu64)i * FS_THREADS + tid;
+    if (s < SS && gslot_occupied(t, s)) occ |= 1u << i;
+  }
+#pragma unroll
+  for (int i = 0; i < FS_PER; ++i) {
+    const qu64 b = __ballot((occ >> i) & 1);
+    if (lane == 0) {
+      wbal[i][wid] = b;
+      wcnt[i][wid] = __popcll(b);
+    }
+  }
+  __syncthreads();  // also orders the LDS zeroing before any bit is set
+  if (tid == 0) {
+    qi32 run = 0;
+    for (int i = 0; i < FS_PER; ++i) {
+      cbase[i] = run;
+      for (int w = 0; w < FS_WAVES; ++w) run += wcnt[i][w];
+    }
+    cbase[FS_PER] = run;
+  }
+  __syncthreads();
+  while (occ) {
+    const int i = __ffs(occ) - 1;
+    occ &= occ - 1;
+    qi64 o = cbase[i] + __popcll(wbal[i][wid] & lt);
+    for (int w = 0; w < wid; ++w) o += wcnt[i][w];
+    finalize_slot(t, m, km, out, (qu64)i * FS_THREADS + tid, o, lbits);
+  }
+  __syncthreads();
+  for (int w = tid; w < words; w += FS_THREADS) {
+    for (int k = 0; k < QE_MAX_KEYS; ++k)
+      if (k < km.nkeys && out.keys[k].validity) ((qu32*)out.keys[k].validity)[w] = lbits[k * FS_WORDS + w];
+    for (int j = 0; j < m.naggs; ++j)
+      if (out.aggs[j].validity) ((qu32*)out.aggs[j].validity)[w] = lbits[(QE_MAX_KEYS + j) * FS_WORDS + w];
   }
 }
 
@@ -960,6 +1114,7 @@ struct qe_hashagg {
   KeyMeta km{};
   int32_t rec_bytes = 0;
   int64_t row_base = 0;
+  int64_t known_groups = 0;  // group count as of the last update/reset; -1 = read the device counter
   // global table
   void* table_mem = nullptr;
   DTable t{};
@@ -1032,12 +1187,14 @@ static int table_alloc(qe_hashagg* h, uint64_t cap, void** mem, DTable* t) {
   return launch_check("k_table_init");
 }
 
-static int read_ctl(qe_hashagg* h, uint64_t out[4]) {
+// ctl words: [0] groups, [1] deferred rows, [2] overflow records, [3] lost groups,
+// [4] largest slot count reported by the senders of an import_slots, [5] their records in total
+static int read_ctl(qe_hashagg* h, uint64_t out[8]) {
   void* p;
-  QE_TRY(ctx_pinned(h->ctx, 32, &p));
-  QE_HIP(hipMemcpyAsync(p, h->ctl, 32, hipMemcpyDeviceToHost, h->ctx->stream));
+  QE_TRY(ctx_pinned(h->ctx, 64, &p));
+  QE_HIP(hipMemcpyAsync(p, h->ctl, 64, hipMemcpyDeviceToHost, h->ctx->stream));
   QE_HIP(hipStreamSynchronize(h->ctx->stream));
-  memcpy(out, p, 32);
+  memcpy(out, p, 64);
   return QE_OK;
 }
 
@@ -1060,7 +1217,7 @@ static int table_grow(qe_hashagg* h, uint64_t want_cap) {
   const int grid = (int)std::min<uint64_t>(div_up(h->t.cap + 2, 256), 8192);
   hipLaunchKernelGGL(k_rehash, dim3(grid), dim3(256), 0, h->ctx->stream, h->t, nt, agg_meta(h));
   QE_TRY(launch_check("k_rehash"));
-  uint64_t c[4];
+  uint64_t c[8];
   QE_TRY(read_ctl(h, c));  // synchronises: the old table can go
   QE_CHECK(c[3] == 0, QE_ERR_CAPACITY, "hash table rehash lost %llu groups", (unsigned long long)c[3]);
   QE_HIP(hipFree(h->table_mem));
@@ -1075,7 +1232,7 @@ static int import_records(qe_hashagg* h, const void* recs, int64_t nrec) {
   hipLaunchKernelGGL(k_import, dim3(grid), dim3(256), 0, h->ctx->stream, (const uint8_t*)recs, nrec, h->rec_bytes,
                      h->t, agg_meta(h));
   QE_TRY(launch_check("k_import"));
-  uint64_t c[4];
+  uint64_t c[8];
   QE_TRY(read_ctl(h, c));
   QE_CHECK(c[3] == 0, QE_ERR_CAPACITY, "hash table import lost %llu groups", (unsigned long long)c[3]);
   return QE_OK;
@@ -1355,6 +1512,7 @@ static int run_update(qe_hashagg* h, Plan& P) {
   P.ovf = h->ovf;
   P.ovf_cap = h->ovf_cap;
   QE_TRY(ensure_defer(h, n));
+  h->known_groups = -1;
   h->last_kernel_ms = 0.0;
   h->last_launches = 0;
   int out_i = 0;
@@ -1406,7 +1564,7 @@ static int run_update(qe_hashagg* h, Plan& P) {
     h->last_specialized = jfn ? 1 : 0;
     QE_TRY(launch_check("k_hashagg"));
     QE_HIP(hipEventRecord(h->ev[1], ctx->stream));
-    uint64_t c[4];
+    uint64_t c[8];
     QE_TRY(read_ctl(h, c));
     {
       float ms = 0.f;
@@ -1418,6 +1576,7 @@ static int run_update(qe_hashagg* h, Plan& P) {
     const uint64_t groups = c[0], deferred = c[1], ovf_recs = c[2];
     if (deferred == 0 && ovf_recs == 0) {
       if (groups * 2 > h->t.cap) QE_TRY(table_grow(h, 4 * h->t.cap));
+      h->known_groups = (int64_t)groups;  // saves finalize a device round trip
       break;
     }
     // grow, then re-apply what could not be inserted
@@ -1586,6 +1745,7 @@ int qe_hashagg_reset(qe_hashagg* h) {
   hipLaunchKernelGGL(k_table_init, dim3(grid), dim3(256), 0, h->ctx->stream, h->t, agg_meta(h));
   QE_TRY(launch_check("k_table_init"));
   h->row_base = 0;
+  h->known_groups = 0;
   return QE_OK;
 }
 
@@ -1667,9 +1827,14 @@ int qe_hashagg_update(qe_hashagg* h, const qe_column* keys, const qe_column* agg
 int qe_hashagg_num_groups(qe_hashagg* h, int64_t* out) {
   QE_CHECK(h && out, QE_ERR_INVALID_ARG, "null argument");
   QE_TRY(ctx_enter(h->ctx));
-  uint64_t c[4];
+  if (h->known_groups >= 0) {
+    *out = h->known_groups;
+    return QE_OK;
+  }
+  uint64_t c[8];
   QE_TRY(read_ctl(h, c));
-  *out = (int64_t)c[0];
+  QE_CHECK(c[3] == 0, QE_ERR_CAPACITY, "hash table lost %llu groups", (unsigned long long)c[3]);
+  *out = h->known_groups = (int64_t)c[0];
   return QE_OK;
 }
 
@@ -1679,6 +1844,8 @@ int qe_hashagg_finalize(qe_hashagg* h, qe_column* out_keys, qe_column* out_aggs,
   qe_ctx* ctx = h->ctx;
   int64_t groups;
   QE_TRY(qe_hashagg_num_groups(h, &groups));
+  // small tables finalise in one workgroup that also zeroes the validity bitmaps
+  const bool small = h->t.cap + 2 <= (uint64_t)FS_THREADS * FS_PER && groups <= (int64_t)FS_WORDS * 32;
   OutCols oc{};
   for (int k = 0; k < h->nkeys; ++k) {
     QE_CHECK(out_keys, QE_ERR_INVALID_ARG, "null out_keys");
@@ -1689,7 +1856,7 @@ int qe_hashagg_finalize(qe_hashagg* h, qe_column* out_keys, qe_column* out_aggs,
              k, (long long)c.length, (long long)groups);
     QE_CHECK(!c.validity || ((uintptr_t)c.validity & 3) == 0, QE_ERR_INVALID_ARG, "validity must be 4-byte aligned");
     oc.keys[k] = c;
-    if (c.validity) QE_HIP(hipMemsetAsync(c.validity, 0, div_up((uint64_t)groups, 32) * 4, ctx->stream));
+    if (c.validity && !small) QE_HIP(hipMemsetAsync(c.validity, 0, div_up((uint64_t)groups, 32) * 4, ctx->stream));
   }
   for (int j = 0; j < h->naggs; ++j) {
     QE_CHECK(out_aggs, QE_ERR_INVALID_ARG, "null out_aggs");
@@ -1703,13 +1870,22 @@ int qe_hashagg_finalize(qe_hashagg* h, qe_column* out_keys, qe_column* out_aggs,
              "aggregate output %d holds %lld rows, need %lld", j, (long long)c.length, (long long)groups);
     QE_CHECK(!c.validity || ((uintptr_t)c.validity & 3) == 0, QE_ERR_INVALID_ARG, "validity must be 4-byte aligned");
     oc.aggs[j] = c;
-    if (c.validity) QE_HIP(hipMemsetAsync(c.validity, 0, div_up((uint64_t)groups, 32) * 4, ctx->stream));
+    if (c.validity && !small) QE_HIP(hipMemsetAsync(c.validity, 0, div_up((uint64_t)groups, 32) * 4, ctx->stream));
   }
   if (out_groups) *out_groups = groups;
   for (int k = 0; k < h->nkeys; ++k) out_keys[k].length = groups;
   for (int j = 0; j < h->naggs; ++j) out_aggs[j].length = groups;
   if (groups == 0) return QE_OK;
-  const int32_t tile_slots = 4096;
+  if (small) {
+    hipLaunchKernelGGL(k_finalize_small, dim3(1), dim3(FS_THREADS), 0, ctx->stream, h->t, agg_meta(h), h->km, oc,
+                       (qi64)groups);
+    QE_TRY(launch_check("k_finalize_small"));
+    QE_HIP(hipStreamSynchronize(ctx->stream));
+    return QE_OK;
+  }
+  // one 256-slot tile per workgroup: a single pass each, so the chip finalises in one wave of
+  // workgroups instead of a serial walk of long tiles
+  const int32_t tile_slots = 256;
   const uint64_t SS = h->t.cap + 2;
   const int64_t ntiles = (int64_t)div_up(SS, tile_slots);
   void* s;
@@ -1751,41 +1927,66 @@ int qe_hashagg_export(qe_hashagg* h, int32_t nparts, void* dst) {
   QE_CHECK(h && nparts >= 1, QE_ERR_INVALID_ARG, "bad arguments");
   QE_TRY(ctx_enter(h->ctx));
   qe_ctx* ctx = h->ctx;
-  // counts -> exclusive offsets used as cursors
-  int64_t* hc = new int64_t[nparts];
-  int st = qe_hashagg_export_counts(h, nparts, hc);
-  if (st != QE_OK) {
-    delete[] hc;
-    return st;
-  }
-  int64_t total = 0;
-  for (int p = 0; p < nparts; ++p) {
-    const int64_t c = hc[p];
-    hc[p] = total;
-    total += c;
-  }
-  if (total == 0) {
-    delete[] hc;
-    return QE_OK;
-  }
-  if (!dst) {
-    delete[] hc;
-    return fail(QE_ERR_INVALID_ARG, "null destination");
-  }
+  int64_t groups;
+  QE_TRY(qe_hashagg_num_groups(h, &groups));
+  if (groups == 0) return QE_OK;
+  QE_CHECK(dst, QE_ERR_INVALID_ARG, "null destination");
+  // counts -> exclusive offsets (cursors) on the device: no host round trip
   void* s;
-  st = ctx_scratch(ctx, (size_t)nparts * 8, &s);
-  if (st == QE_OK) {
-    hipError_t e = hipMemcpyAsync(s, hc, (size_t)nparts * 8, hipMemcpyHostToDevice, ctx->stream);
-    if (e == hipSuccess) e = hipStreamSynchronize(ctx->stream);
-    if (e != hipSuccess) st = fail(QE_ERR_DEVICE, "cursor upload: %s", hipGetErrorString(e));
-  }
-  delete[] hc;
-  if (st != QE_OK) return st;
+  QE_TRY(ctx_scratch(ctx, (size_t)nparts * 8, &s));
+  QE_HIP(hipMemsetAsync(s, 0, (size_t)nparts * 8, ctx->stream));
   const int grid = (int)std::min<uint64_t>(div_up(h->t.cap + 2, 256), 8192);
+  hipLaunchKernelGGL(k_export_count, dim3(grid), dim3(256), 0, ctx->stream, h->t, nparts, (unsigned long long*)s);
+  QE_TRY(launch_check("k_export_count"));
+  hipLaunchKernelGGL(k_counts_to_cursors, dim3(1), dim3(64), 0, ctx->stream, (unsigned long long*)s, nparts);
+  QE_TRY(launch_check("k_counts_to_cursors"));
   hipLaunchKernelGGL(k_export, dim3(grid), dim3(256), 0, ctx->stream, h->t, agg_meta(h), nparts, h->rec_bytes,
                      (unsigned long long*)s, (uint8_t*)dst);
   QE_TRY(launch_check("k_export"));
-  QE_HIP(hipStreamSynchronize(ctx->stream));
+  return QE_OK;
+}
+
+int qe_hashagg_export_slots(qe_hashagg* h, int32_t nparts, int64_t slot_records, void* dst) {
+  QE_CHECK(h && nparts >= 1 && slot_records >= 1 && dst, QE_ERR_INVALID_ARG, "bad arguments");
+  QE_TRY(ctx_enter(h->ctx));
+  qe_ctx* ctx = h->ctx;
+  void* s;
+  QE_TRY(ctx_scratch(ctx, (size_t)nparts * 8, &s));
+  QE_HIP(hipMemsetAsync(s, 0, (size_t)nparts * 8, ctx->stream));
+  const int grid = (int)std::min<uint64_t>(div_up(h->t.cap + 2, 256), 8192);
+  hipLaunchKernelGGL(k_export_slots, dim3(grid), dim3(256), 0, ctx->stream, h->t, agg_meta(h), nparts, h->rec_bytes,
+                     (qi64)slot_records, (unsigned long long*)s, (uint8_t*)dst);
+  QE_TRY(launch_check("k_export_slots"));
+  const uint64_t slot_bytes = QE_SLOT_HEADER + (uint64_t)slot_records * h->rec_bytes;
+  hipLaunchKernelGGL(k_slot_headers, dim3(1), dim3(64), 0, ctx->stream, (const unsigned long long*)s, nparts,
+                     (qu64)slot_bytes, (uint8_t*)dst);
+  QE_TRY(launch_check("k_slot_headers"));
+  return QE_OK;
+}
+
+int qe_hashagg_import_slots(qe_hashagg* h, const void* slots, int32_t nslots, int64_t slot_records,
+                            int64_t* max_count, int64_t* nrecords) {
+  QE_CHECK(h && slots && nslots >= 1 && slot_records >= 1 && max_count, QE_ERR_INVALID_ARG, "bad arguments");
+  QE_TRY(ctx_enter(h->ctx));
+  qe_ctx* ctx = h->ctx;
+  const uint64_t slot_bytes = QE_SLOT_HEADER + (uint64_t)slot_records * h->rec_bytes;
+  // the senders' counts decide, identically on every rank, whether the slots held everything
+  hipLaunchKernelGGL(k_slots_scan, dim3(1), dim3(64), 0, ctx->stream, (const uint8_t*)slots, nslots,
+                     (qu64)slot_bytes, h->ctl);
+  QE_TRY(launch_check("k_slots_scan"));
+  uint64_t c[8];
+  QE_TRY(read_ctl(h, c));
+  *max_count = (int64_t)c[4];
+  if (nrecords) *nrecords = (int64_t)c[5];
+  if (c[4] > (uint64_t)slot_records) return QE_OK;  // some sender overflowed a slot: nothing imported
+  if (c[5] == 0) return QE_OK;
+  if (2 * (c[0] + c[5]) > h->t.cap) QE_TRY(table_grow(h, 2 * (c[0] + c[5])));
+  h->known_groups = -1;
+  QE_HIP(hipMemsetAsync(h->ctl + 3, 0, 8, ctx->stream));
+  const int grid = (int)std::min<uint64_t>(div_up((uint64_t)nslots * slot_records, 256), 8192);
+  hipLaunchKernelGGL(k_import_slots, dim3(grid), dim3(256), 0, ctx->stream, (const uint8_t*)slots, nslots,
+                     (qi64)slot_records, h->rec_bytes, h->t, agg_meta(h));
+  QE_TRY(launch_check("k_import_slots"));
   return QE_OK;
 }
 
@@ -1793,7 +1994,8 @@ int qe_hashagg_import(qe_hashagg* h, const void* records, int64_t nrecords) {
   QE_CHECK(h && nrecords >= 0 && (records || nrecords == 0), QE_ERR_INVALID_ARG, "bad arguments");
   QE_TRY(ctx_enter(h->ctx));
   if (nrecords == 0) return QE_OK;
-  uint64_t c[4];
+  h->known_groups = -1;
+  uint64_t c[8];
   QE_TRY(read_ctl(h, c));
   if (2 * (c[0] + (uint64_t)nrecords) > h->t.cap) QE_TRY(table_grow(h, 2 * (c[0] + (uint64_t)nrecords)));
   QE_HIP(hipMemsetAsync(h->ctl + 3, 0, 8, h->ctx->stream));

@@ -48,6 +48,29 @@ def packable(key_types) -> bool:
     return sum(_KEY_BITS[t] + 1 for t in key_types) <= 63
 
 
+def _carve(ctx: Context, n: int, specs) -> List[DeviceColumn]:
+    """Fixed-width output columns of `n` rows from two device allocations (values; validity
+    bitmaps), split with one unbind each — per-column slicing costs more host time than the
+    finalize kernel. Validity is left uninitialised: qe_hashagg_finalize writes whole bitmaps."""
+    import torch
+
+    from .columnar import _torch_dtype, bitmap_bytes
+
+    dev = ctx.torch_device
+    vals = torch.empty((len(specs), max(n, 1)), dtype=torch.int64, device=dev).unbind(0)
+    nv = sum(1 for _, nullable in specs if nullable)
+    bits = torch.empty((max(nv, 1), max(bitmap_bytes(n), 4)), dtype=torch.uint8, device=dev).unbind(0) if nv else []
+    out, b = [], 0
+    for (t, nullable), v in zip(specs, vals):
+        if t not in (N.TYPE_INT64, N.TYPE_FLOAT64):
+            v = v.view(_torch_dtype(t))  # narrow key types: a prefix of the int64 row
+        elif t == N.TYPE_FLOAT64:
+            v = v.view(torch.float64)
+        out.append(DeviceColumn(t, n, v, bits[b] if nullable else None, None, ctx))
+        b += 1 if nullable else 0
+    return out
+
+
 def dictionary_keys(key_types) -> Optional[int]:
     """None when qe_hashagg groups by these keys directly; otherwise the number of device key
     columns the dictionaries turn them into (UTF-8 keys -> one int32 code each; a key set that
@@ -66,6 +89,7 @@ class HashAggregateState:
         from .strdict import StringDictionary
 
         self.ctx = ctx
+        self.expected_groups = int(expected_groups)
         self.key_types = list(key_types)
         self.aggs = [(int(f), int(t)) for f, t in aggs]
         # UTF-8 keys: grouped by their dictionary code (INT32), decoded in finalize
@@ -169,9 +193,9 @@ class HashAggregateState:
     def finalize(self) -> Tuple[List[DeviceColumn], List[DeviceColumn]]:
         """One output batch (Main.kt:635-650): key columns, aggregate columns."""
         g = self.num_groups()
-        keys = [DeviceColumn.empty(t, g, True, ctx=self.ctx) for t in self.device_key_types]
-        aggs = [DeviceColumn.empty(output_type(f, t), g, f not in (N.AGG_COUNT, N.AGG_COUNT_STAR), ctx=self.ctx)
-                for f, t in self.aggs]
+        cols = _carve(self.ctx, g, [(t, True) for t in self.device_key_types] +
+                      [(output_type(f, t), f not in (N.AGG_COUNT, N.AGG_COUNT_STAR)) for f, t in self.aggs])
+        keys, aggs = cols[:len(self.device_key_types)], cols[len(self.device_key_types):]
         kc = (N.QeColumn * max(1, len(keys)))(*[k.as_c() for k in keys])
         ac = (N.QeColumn * max(1, len(aggs)))(*[a.as_c() for a in aggs])
         out = N.C.c_int64()
@@ -296,6 +320,29 @@ class HashAggregateState:
         buf = torch.empty(max(1, sum(counts) * rb), dtype=torch.uint8, device=self.ctx.torch_device)
         N.check(N.lib().qe_hashagg_export(self.handle, nparts, N.C.c_void_p(buf.data_ptr())))
         return buf[: sum(counts) * rb], counts
+
+    def slot_bytes(self, slot_records: int) -> int:
+        return N.SLOT_HEADER + int(slot_records) * self.record_bytes()
+
+    def export_slots(self, nparts: int, slot_records: int):
+        """-> uint8 device tensor of `nparts` fixed-capacity slots (qe_hashagg_export_slots):
+        no host synchronisation, so the all-to-all can follow the aggregation kernel directly."""
+        import torch
+
+        self._check_exportable()
+        buf = torch.empty(nparts * self.slot_bytes(slot_records), dtype=torch.uint8, device=self.ctx.torch_device)
+        N.check(N.lib().qe_hashagg_export_slots(self.handle, int(nparts), int(slot_records),
+                                                N.C.c_void_p(buf.data_ptr())))
+        return buf
+
+    def import_slots(self, slots, nslots: int, slot_records: int) -> Optional[int]:
+        """Merges received slots; returns the records merged, or None when some sender's
+        partition exceeded the slot capacity (nothing merged; the same on every rank)."""
+        self._check_exportable()
+        mx, n = N.C.c_int64(), N.C.c_int64()
+        N.check(N.lib().qe_hashagg_import_slots(self.handle, N.C.c_void_p(slots.data_ptr()), int(nslots),
+                                                int(slot_records), N.C.byref(mx), N.C.byref(n)))
+        return None if mx.value > slot_records else n.value
 
     def import_records(self, records, nrecords: int) -> None:
         self._check_exportable()

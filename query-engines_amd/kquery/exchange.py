@@ -150,12 +150,35 @@ def exchange_keyed_partials(partial, owner, group: Optional[dist.ProcessGroup] =
     return nrecv
 
 
-def exchange_partials(partial, owner, group: Optional[dist.ProcessGroup] = None) -> int:
+def all_to_all_slots(send: torch.Tensor, group: Optional[dist.ProcessGroup] = None) -> torch.Tensor:
+    """Equal-split all-to-all of `world` fixed-size slots (slot p goes to rank p). No sizes are
+    exchanged first and nothing waits on the host: with RCCL it queues behind the export kernel
+    on the device. gloo (CPU tests) stages device tensors through host memory."""
+    stage = dist.get_backend(group) == "gloo" and send.device.type != "cpu"
+    src = send.cpu() if stage else send
+    out = torch.empty_like(src)
+    dist.all_to_all_single(out, src, group=group)
+    return out.to(send.device) if stage else out
+
+
+def exchange_partials(partial, owner, group: Optional[dist.ProcessGroup] = None,
+                      slot_records: Optional[int] = None) -> int:
     """Moves every group of `partial` (this rank's HashAggregateState) to the rank that owns its
-    key and merges what this rank receives into `owner`. Returns the records received."""
+    key and merges what this rank receives into `owner`. Returns the records received.
+
+    Fast path: fixed-capacity slots of `slot_records` groups per destination (default: the
+    state's expected_groups, the same on every rank), ONE all-to-all, no host round trip before
+    it. If any rank had more groups for one owner than a slot holds, every rank sees it in the
+    slot headers and all of them fall back to the variable-size exchange (counts all-to-all,
+    then records)."""
     if getattr(partial, "keyed_by_dictionary", False):
         return exchange_keyed_partials(partial, owner, group)
     world = dist.get_world_size(group)
+    cap = int(slot_records or partial.expected_groups)
+    recv = all_to_all_slots(partial.export_slots(world, cap), group)
+    n = owner.import_slots(recv, world, cap)
+    if n is not None:
+        return n
     recs, counts = partial.export(world)
     recv, n = all_to_all_records(recs, counts, partial.record_bytes(), group)
     owner.import_records(recv, n)

@@ -176,6 +176,8 @@ _PP = C.POINTER(C.c_void_p)
 _I64P = C.POINTER(C.c_int64)
 _COLP = C.POINTER(QeColumn)
 _OPP = C.POINTER(QeOperand)
+SLOT_HEADER = 64  # QE_SLOT_HEADER: bytes before a slot's records
+
 SIGNATURES = [
     ("qe_ctx_create", C.c_int, [C.c_int, _P, _PP]),
     ("qe_ctx_create_owned", C.c_int, [C.c_int, _PP]),
@@ -210,6 +212,8 @@ SIGNATURES = [
     ("qe_hashagg_export_counts", C.c_int, [_P, C.c_int32, _I64P]),
     ("qe_hashagg_export", C.c_int, [_P, C.c_int32, _P]),
     ("qe_hashagg_import", C.c_int, [_P, _P, C.c_int64]),
+    ("qe_hashagg_export_slots", C.c_int, [_P, C.c_int32, C.c_int64, _P]),
+    ("qe_hashagg_import_slots", C.c_int, [_P, _P, C.c_int32, C.c_int64, _I64P, _I64P]),
     ("qe_hashagg_set_row_base", C.c_int, [_P, C.c_int64]),
     ("qe_hashagg_last_kernel_time", C.c_int, [_P, C.POINTER(C.c_double), C.POINTER(C.c_int32)]),
     ("qe_hashagg_last_kernel_kind", C.c_int, [_P, C.POINTER(C.c_int32), C.c_char_p, C.c_int32]),

@@ -72,6 +72,42 @@ def main():
                                          [False] * 3)
             ok = len(got) == len(want) and all(got[key] == w for key, w in want.items())
             results[mode] = {"ok": ok, "groups": len(got)}
+    # numeric keys: fixed-capacity slot exchange, and its fallback when a slot overflows
+    for mode, cap in (("slots", None), ("slots_overflow", 50)):
+        rng = np.random.default_rng(300 + rank)
+        n = 50_000 + 1000 * rank
+        k = rng.integers(0, 3000, n).astype(np.int64)
+        kv = rng.random(n) > 0.01
+        x = rng.normal(size=n)
+        aggs = [(N.AGG_SUM, N.TYPE_INT64), (N.AGG_MAX, N.TYPE_FLOAT64), (N.AGG_COUNT_STAR, N.TYPE_INT64)]
+        partial = HashAggregateState(ctx, [N.TYPE_INT64], aggs, 4096)
+        owner = HashAggregateState(ctx, [N.TYPE_INT64], aggs, 4096)
+        partial.set_row_base(rank * 10_000_000)
+        kc = DeviceColumn.from_numpy(N.TYPE_INT64, k, kv, ctx=ctx)
+        partial.update([kc], [kc, DeviceColumn.from_numpy(N.TYPE_FLOAT64, x, ctx=ctx), None])
+        exchange_partials(partial, owner, slot_records=cap)
+        ko, ao = owner.finalize()
+        mine = [list(r) for r in zip(*([c.to_pylist() for c in ko] + [c.to_pylist() for c in ao]))]
+        allrows = [None] * world
+        dist.all_gather_object(allrows, mine)
+        if rank == 0:
+            got = {}
+            for rows in allrows:
+                for r in rows:
+                    assert r[0] not in got, f"group {r[0]} owned by two ranks"
+                    got[r[0]] = r[1:]
+            kk, xs = [], []
+            for r in range(world):
+                g = np.random.default_rng(300 + r)
+                n2 = 50_000 + 1000 * r
+                k2 = g.integers(0, 3000, n2).astype(np.int64)
+                kv2 = g.random(n2) > 0.01
+                kk += [int(a) if ok else None for a, ok in zip(k2, kv2)]
+                xs += g.normal(size=n2).tolist()
+            want = S.hash_aggregate_rows([kk], [kk, xs, [1] * len(kk)], [S.AGG_SUM, S.AGG_MAX, S.AGG_COUNT_STAR],
+                                         [False, True, False])
+            ok = len(got) == len(want) and all(got[key[0]] == w for key, w in want.items())
+            results[mode] = {"ok": ok, "groups": len(got)}
     if rank == 0:
         print("RESULT " + json.dumps(results), flush=True)
     dist.barrier()

@@ -25,7 +25,7 @@ def _data(row0, n):
     return k, a, b
 
 
-def _worker(rank, world, port, q):
+def _worker(rank, world, port, q, slot_records=None):
     import sys
     import pathlib
 
@@ -33,15 +33,25 @@ def _worker(rank, world, port, q):
     sys.path[:0] = [str(root), str(root / "query-engines_amd")]
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
-    from kquery.exchange import all_to_all_records
+    from kquery.exchange import all_to_all_records, all_to_all_slots
 
     k, a, b = _data(rank * ROWS, ROWS)
     parts = R.partials_c4(k, a, b, THR)
-    payload, counts = R.encode(parts, FNS, world)
-    t = torch.frombuffer(bytearray(payload), dtype=torch.uint8) if payload else torch.empty(0, dtype=torch.uint8)
-    recv, n = all_to_all_records(t, counts, R.record_bytes(len(FNS)))
+    recs = None
+    if slot_records is not None:  # the fast path: fixed slots, one all-to-all (exchange_partials)
+        send = torch.frombuffer(bytearray(R.encode_slots(parts, FNS, world, slot_records)), dtype=torch.uint8)
+        got, mx = R.decode_slots(bytes(all_to_all_slots(send).numpy().tobytes()), world, slot_records, len(FNS))
+        seen = [None] * world
+        dist.all_gather_object(seen, mx > slot_records)
+        assert len(set(seen)) == 1  # every rank takes the same path
+        recs = None if mx > slot_records else got
+    if recs is None:
+        payload, counts = R.encode(parts, FNS, world)
+        t = torch.frombuffer(bytearray(payload), dtype=torch.uint8) if payload else torch.empty(0, dtype=torch.uint8)
+        recv, n = all_to_all_records(t, counts, R.record_bytes(len(FNS)))
+        recs = R.decode(bytes(recv.numpy().tobytes()), len(FNS))
     owned = {}
-    for key, cstar, aggs in R.decode(bytes(recv.numpy().tobytes()), len(FNS)):
+    for key, cstar, aggs in recs:
         assert R.partition_of(key, False, world) == rank
         R.combine(FNS, owned, key, cstar, aggs)
     gathered = [None] * world
@@ -59,12 +69,14 @@ def _free_port():
     return p
 
 
-@pytest.mark.parametrize("world", [2])
-def test_exchange_gloo_matches_single_process(world):
+@pytest.mark.parametrize("world,slot_records", [(2, None), (2, 1024), (2, 100), (3, 400)])
+def test_exchange_gloo_matches_single_process(world, slot_records):
+    """slot_records None: variable-size exchange; 1024 / 400: fixed slots hold every partition;
+    100: slots overflow (≈512 groups per owner), every rank falls back together."""
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q, slot_records)) for r in range(world)]
     for p in procs:
         p.start()
     gathered = q.get(timeout=240)

@@ -638,8 +638,10 @@ def test_export_partition_matches_oracle(gpu_ctx):
         assert off == len(np.unique(k))
 
 
-def test_exchange_rccl_single_rank(gpu_ctx):
-    """The RCCL path of kquery.exchange (backend nccl = RCCL) end to end on one rank."""
+@pytest.mark.parametrize("slot_records", [None, 10])
+def test_exchange_rccl_single_rank(gpu_ctx, slot_records):
+    """The RCCL path of kquery.exchange (backend nccl = RCCL) end to end on one rank: fixed slots
+    (None: capacity = expected groups), and slots too small for the ~4990 groups (fallback)."""
     import os
     import socket
 
@@ -662,7 +664,7 @@ def test_exchange_rccl_single_rank(gpu_ctx):
         part = HashAggregateState(gpu_ctx, [N.TYPE_INT64], aggs, 8192)
         owner = HashAggregateState(gpu_ctx, [N.TYPE_INT64], aggs, 8192)
         part.update([dcol(gpu_ctx, N.TYPE_INT64, k)], [dcol(gpu_ctx, N.TYPE_INT64, x), None])
-        n = exchange_partials(part, owner)
+        n = exchange_partials(part, owner, slot_records=slot_records)
         assert n == len(np.unique(k))
         kk, aa = owner.finalize()
         ref = S.group_aggregate([k], [None], [x, None], [None, None], [N.AGG_SUM, N.AGG_COUNT_STAR])
