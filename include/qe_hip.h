@@ -214,6 +214,17 @@ typedef struct qe_global_agg {
 } qe_global_agg;
 int qe_agg_global(qe_ctx* ctx, const qe_column* col, const qe_column* mask /*nullable*/,
                   qe_global_agg* out);
+/* The same aggregate over a column split across batches or GPUs (one exchange of a
+ * fixed-size partial). qe_agg_global_partial writes this column's mergeable partial (sums, min /
+ * max keys and first-row indices, QE_GLOBAL_PARTIAL_BYTES of device memory); `row_base` is the
+ * global index of the column's first row, so MIN/MAX keep MaxAccumulator's row-order rules
+ * (NaN seed, earliest of +0.0 / -0.0) across the pieces. qe_agg_global_merge folds n partials
+ * (device, packed QE_GLOBAL_PARTIAL_BYTES apart, any order) in a fixed order into the final
+ * result: every rank merging the same all-gathered partials gets the same bits. */
+#define QE_GLOBAL_PARTIAL_BYTES 128
+int qe_agg_global_partial(qe_ctx* ctx, const qe_column* col, const qe_column* mask /*nullable*/,
+                          int64_t row_base, void* partial);
+int qe_agg_global_merge(qe_ctx* ctx, int32_t type, const void* partials, int32_t n, qe_global_agg* out);
 
 /* ---- HashAggregateExec (K4b) ------------------------------------------------------------ */
 /* Group keys: 0..4 columns. One key of any fixed-width type, or several narrow keys

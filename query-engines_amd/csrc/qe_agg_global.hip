@@ -254,6 +254,23 @@ __global__ void __launch_bounds__(256) k_agg_global_f64_dense(const int64_t* __r
   }
 }
 
+static_assert(sizeof(GPart) <= QE_GLOBAL_PARTIAL_BYTES, "partial record size");
+
+// Row indices of a partial -> global rows (multi-batch / multi-GPU merges keep row order).
+__global__ void k_agg_global_rebase(GPart* __restrict__ p, int64_t row_base) {
+  if (threadIdx.x == 0) {
+    if (p->first_nn != UINT64_MAX) p->first_nn += (uint64_t)row_base;
+    if (p->first_nan != UINT64_MAX) p->first_nan += (uint64_t)row_base;
+    if (p->first_negz != UINT64_MAX) p->first_negz += (uint64_t)row_base;
+    if (p->first_posz != UINT64_MAX) p->first_posz += (uint64_t)row_base;
+  }
+}
+
+// Packed partial records (QE_GLOBAL_PARTIAL_BYTES apart) -> a GPart array.
+__global__ void k_agg_global_unpack(const uint8_t* __restrict__ recs, int n, GPart* __restrict__ out) {
+  for (int i = threadIdx.x; i < n; i += blockDim.x) out[i] = *(const GPart*)(recs + (size_t)i * QE_GLOBAL_PARTIAL_BYTES);
+}
+
 __global__ void __launch_bounds__(256) k_agg_global_final(GPart* __restrict__ partials, int nparts) {
   // Fixed-order reduction: thread t folds partials t, t+256, ...; then a fixed wave/block tree.
   GPart p;
@@ -282,9 +299,11 @@ static int64_t finalize_f64_minmax(const GPart& p, bool is_max) {
 
 using namespace qe;
 
-extern "C" int qe_agg_global(qe_ctx* ctx, const qe_column* col, const qe_column* mask, qe_global_agg* out) {
-  QE_TRY(ctx_enter(ctx));
-  QE_CHECK(col && out, QE_ERR_INVALID_ARG, "null argument");
+namespace qe {
+
+// The column's partial, reduced on the device into *result (a GPart in scratch).
+static int agg_global_partial(qe_ctx* ctx, const qe_column* col, const qe_column* mask, GPart** result) {
+  QE_CHECK(col, QE_ERR_INVALID_ARG, "null argument");
   QE_CHECK(col->type == QE_TYPE_INT64 || col->type == QE_TYPE_FLOAT64, QE_ERR_UNSUPPORTED,
            "global aggregate over type %d not supported (int64/fp64)", col->type);
   const int64_t n = col->length;
@@ -315,15 +334,22 @@ extern "C" int qe_agg_global(qe_ctx* ctx, const qe_column* col, const qe_column*
   QE_TRY(launch_check("k_agg_global"));
   hipLaunchKernelGGL(k_agg_global_final, dim3(1), dim3(256), 0, ctx->stream, parts, (int)blocks);
   QE_TRY(launch_check("k_agg_global_final"));
+  *result = parts + blocks;
+  return QE_OK;
+}
+
+// Device GPart -> qe_global_agg (synchronises).
+static int agg_global_finish(qe_ctx* ctx, const GPart* dp, int32_t type, qe_global_agg* out) {
   void* h;
   QE_TRY(ctx_pinned(ctx, sizeof(GPart), &h));
-  QE_HIP(hipMemcpyAsync(h, parts + blocks, sizeof(GPart), hipMemcpyDeviceToHost, ctx->stream));
+  QE_HIP(hipMemcpyAsync(h, dp, sizeof(GPart), hipMemcpyDeviceToHost, ctx->stream));
   QE_HIP(hipStreamSynchronize(ctx->stream));
   const GPart p = *(const GPart*)h;
+  const bool f64 = type == QE_TYPE_FLOAT64;
   memset(out, 0, sizeof(*out));
   out->rows = p.rows;
   out->count = p.count;
-  out->type = col->type;
+  out->type = type;
   out->valid = p.count > 0 ? 1 : 0;
   const double fsum = std::isfinite(p.s) ? p.s + p.c : p.s;
   if (p.count > 0) {
@@ -339,4 +365,42 @@ extern "C" int qe_agg_global(qe_ctx* ctx, const qe_column* col, const qe_column*
     out->avg = fsum / (double)p.count;
   }
   return QE_OK;
+}
+
+}  // namespace qe
+
+extern "C" int qe_agg_global(qe_ctx* ctx, const qe_column* col, const qe_column* mask, qe_global_agg* out) {
+  QE_TRY(ctx_enter(ctx));
+  QE_CHECK(out, QE_ERR_INVALID_ARG, "null argument");
+  GPart* p;
+  QE_TRY(agg_global_partial(ctx, col, mask, &p));
+  return agg_global_finish(ctx, p, col->type, out);
+}
+
+extern "C" int qe_agg_global_partial(qe_ctx* ctx, const qe_column* col, const qe_column* mask, int64_t row_base,
+                                     void* partial) {
+  QE_TRY(ctx_enter(ctx));
+  QE_CHECK(partial && row_base >= 0, QE_ERR_INVALID_ARG, "bad arguments");
+  GPart* p;
+  QE_TRY(agg_global_partial(ctx, col, mask, &p));
+  hipLaunchKernelGGL(k_agg_global_rebase, dim3(1), dim3(64), 0, ctx->stream, p, row_base);
+  QE_TRY(launch_check("k_agg_global_rebase"));
+  QE_HIP(hipMemsetAsync(partial, 0, QE_GLOBAL_PARTIAL_BYTES, ctx->stream));
+  QE_HIP(hipMemcpyAsync(partial, p, sizeof(GPart), hipMemcpyDeviceToDevice, ctx->stream));
+  return QE_OK;
+}
+
+extern "C" int qe_agg_global_merge(qe_ctx* ctx, int32_t type, const void* partials, int32_t n, qe_global_agg* out) {
+  QE_TRY(ctx_enter(ctx));
+  QE_CHECK(out && partials && n >= 1 && (type == QE_TYPE_INT64 || type == QE_TYPE_FLOAT64), QE_ERR_INVALID_ARG,
+           "bad arguments");
+  void* s;
+  QE_TRY(ctx_scratch(ctx, (size_t)(n + 1) * sizeof(GPart), &s));
+  GPart* parts = (GPart*)s;
+  hipLaunchKernelGGL(k_agg_global_unpack, dim3(1), dim3(256), 0, ctx->stream, (const uint8_t*)partials, n, parts);
+  QE_TRY(launch_check("k_agg_global_unpack"));
+  // fixed-order fold: the same partials give the same bits on every rank
+  hipLaunchKernelGGL(k_agg_global_final, dim3(1), dim3(256), 0, ctx->stream, parts, (int)n);
+  QE_TRY(launch_check("k_agg_global_final"));
+  return agg_global_finish(ctx, parts + n, type, out);
 }

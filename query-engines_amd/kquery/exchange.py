@@ -183,3 +183,32 @@ def exchange_partials(partial, owner, group: Optional[dist.ProcessGroup] = None,
     recv, n = all_to_all_records(recs, counts, partial.record_bytes(), group)
     owner.import_records(recv, n)
     return n
+
+
+def global_aggregate(col, mask=None, row_base: int = 0, group: Optional[dist.ProcessGroup] = None):
+    """SUM/MIN/MAX/COUNT/AVG without GROUP BY over a column whose rows are split across ranks
+    (SURVEY §8e "global aggregate: one exchange"): this rank's 128-byte partial
+    (qe_agg_global_partial, row indices offset by `row_base` — this rank's first global row),
+    ONE all-gather, and the same fixed-order merge on every rank (qe_agg_global_merge), so every
+    rank returns identical bits. Without an initialised process group: this column alone."""
+    from . import native as N
+
+    ctx = col.ctx
+    world = dist.get_world_size(group) if dist.is_initialized() else 1
+    part = torch.empty(N.GLOBAL_PARTIAL_BYTES, dtype=torch.uint8, device=ctx.torch_device)
+    cc = col.as_c()
+    mc = mask.as_c() if mask is not None else None
+    N.check(N.lib().qe_agg_global_partial(ctx.handle, N.C.byref(cc), N.C.byref(mc) if mc is not None else None,
+                                          int(row_base), N.C.c_void_p(part.data_ptr())))
+    parts = part
+    if world > 1:
+        if dist.get_backend(group) == "gloo":  # CPU collectives: stage through host memory
+            got = [torch.empty_like(part, device="cpu") for _ in range(world)]
+            dist.all_gather(got, part.cpu(), group=group)
+            parts = torch.cat(got).to(part.device)
+        else:
+            parts = torch.empty(world * N.GLOBAL_PARTIAL_BYTES, dtype=torch.uint8, device=part.device)
+            dist.all_gather_into_tensor(parts, part, group=group)
+    out = N.QeGlobalAgg()
+    N.check(N.lib().qe_agg_global_merge(ctx.handle, col.type, N.C.c_void_p(parts.data_ptr()), world, N.C.byref(out)))
+    return out

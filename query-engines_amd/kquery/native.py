@@ -177,6 +177,7 @@ _I64P = C.POINTER(C.c_int64)
 _COLP = C.POINTER(QeColumn)
 _OPP = C.POINTER(QeOperand)
 SLOT_HEADER = 64  # QE_SLOT_HEADER: bytes before a slot's records
+GLOBAL_PARTIAL_BYTES = 128  # QE_GLOBAL_PARTIAL_BYTES
 
 SIGNATURES = [
     ("qe_ctx_create", C.c_int, [C.c_int, _P, _PP]),
@@ -200,6 +201,8 @@ SIGNATURES = [
     ("qe_filter_count", C.c_int, [_P, _COLP, _I64P]),
     ("qe_filter_apply", C.c_int, [_P, _COLP, _COLP, C.c_int32, _COLP, _I64P]),
     ("qe_agg_global", C.c_int, [_P, _COLP, _COLP, C.POINTER(QeGlobalAgg)]),
+    ("qe_agg_global_partial", C.c_int, [_P, _COLP, _COLP, C.c_int64, _P]),
+    ("qe_agg_global_merge", C.c_int, [_P, C.c_int32, _P, C.c_int32, C.POINTER(QeGlobalAgg)]),
     ("qe_hashagg_create", C.c_int,
      [_P, C.c_int32, C.POINTER(C.c_int32), C.c_int32, C.POINTER(QeAggDesc), C.c_int64, _PP]),
     ("qe_hashagg_destroy", C.c_int, [_P]),

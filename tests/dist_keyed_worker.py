@@ -108,6 +108,38 @@ def main():
                                          [False, True, False])
             ok = len(got) == len(want) and all(got[key[0]] == w for key, w in want.items())
             results[mode] = {"ok": ok, "groups": len(got)}
+    # global aggregate over rank shards: one all-gather of partials, identical merge on every rank
+    from kquery.exchange import global_aggregate
+
+    g = np.random.default_rng(500 + rank)
+    n = 40_000 + 333 * rank
+    x = g.normal(size=n)
+    xv = g.random(n) > 0.05
+    if rank == 1:
+        x[:3] = [np.nan, -0.0, 5.0]  # NaN first in rank 1: rank 0's rows come first, so no seed
+    r = global_aggregate(DeviceColumn.from_numpy(N.TYPE_FLOAT64, x, xv, ctx=ctx), row_base=rank * 10_000_000)
+    mine = [r.rows, r.count, r.sum, r.min, r.max]
+    everyone = [None] * world
+    dist.all_gather_object(everyone, mine)
+    if rank == 0:
+        xs, vs = [], []
+        for q in range(world):
+            g2 = np.random.default_rng(500 + q)
+            n2 = 40_000 + 333 * q
+            x2 = g2.normal(size=n2)
+            v2 = g2.random(n2) > 0.05
+            if q == 1:
+                x2[:3] = [np.nan, -0.0, 5.0]
+            xs.append(x2)
+            vs.append(v2)
+        want = S.global_aggregate(np.concatenate(xs), np.concatenate(vs))
+        from kquery.columnar import f64_from_bits
+
+        same = all(e == everyone[0] for e in everyone)  # every rank merged to the same bits
+        ok = (same and r.rows == want["rows"] and r.count == want["count"]
+              and S.rows_equal(f64_from_bits(r.sum), want["sum"], 1e-9)
+              and S.rows_equal(f64_from_bits(r.min), want["min"]) and S.rows_equal(f64_from_bits(r.max), want["max"]))
+        results["global"] = {"ok": bool(ok)}
     if rank == 0:
         print("RESULT " + json.dumps(results), flush=True)
     dist.barrier()

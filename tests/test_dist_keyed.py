@@ -29,4 +29,4 @@ def test_keyed_exchange_two_ranks():
     line = [ln for ln in r.stdout.splitlines() if ln.startswith("RESULT ")]
     assert line, r.stdout[-2000:] + r.stderr[-2000:]
     res = json.loads(line[0][len("RESULT "):])
-    assert all(res[m]["ok"] for m in ("utf8", "tuple", "slots", "slots_overflow")), res
+    assert all(res[m]["ok"] for m in ("utf8", "tuple", "slots", "slots_overflow", "global")), res
