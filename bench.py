@@ -36,10 +36,7 @@ def c4_spec(N, threshold=1 << 19):
     return spec(threshold)
 
 
-def cpu_baseline(sample_rows: int, threads: int) -> dict:
-    """Timed CPU leg (rank 0, N = 1): the oracle's reference-faithful C restatement of the same
-    query (oracle/cpu_baseline.c: row-at-a-time Selection -> Projection -> HashMap aggregate,
-    partition-parallel like Main.kt:1309-1325) on a bounded sample of the same rows."""
+def _cpu_lib():
     lib_path = ROOT / "oracle" / "build" / "libqe_oracle.so"
     if not lib_path.exists():
         import subprocess
@@ -50,15 +47,36 @@ def cpu_baseline(sample_rows: int, threads: int) -> dict:
         _fields_ = [(n, C.c_int64) for n in ("key", "sum", "count", "min", "max")]
 
     lib = C.CDLL(str(lib_path))
-    lib.qe_cpu_c4.restype = C.c_double
-    lib.qe_cpu_c4.argtypes = [C.c_int64, C.c_int64, C.c_uint64, C.c_int, C.c_int64, C.c_int64,
-                              C.POINTER(G), C.c_int64, C.POINTER(C.c_int64)]
+    for fn in (lib.qe_cpu_c4, lib.qe_cpu_c4_fast):
+        fn.restype = C.c_double
+        fn.argtypes = [C.c_int64, C.c_int64, C.c_uint64, C.c_int, C.c_int64, C.c_int64,
+                       C.POINTER(G), C.c_int64, C.POINTER(C.c_int64)]
+    return lib, G
+
+
+def cpu_baseline(sample_rows: int, threads: int) -> dict:
+    """Timed CPU legs (rank 0, N = 1) on bounded samples of the same rows:
+    * `value`: the oracle's reference-faithful C restatement of the query (oracle/cpu_baseline.c:
+      row-at-a-time Selection -> Projection -> HashMap aggregate with boxed keys and virtual
+      accumulators, partition-parallel like Main.kt:1309-1325) on `threads` threads;
+    * `single_thread`: the same port on one thread (SURVEY §8d: 1 thread and all threads);
+    * `tuned`: a tuned C implementation (no boxing or materialisation, per-thread open-addressing
+      tables), so the GPU is also compared with a fast CPU engine."""
+    lib, G = _cpu_lib()
     out = (G * 2048)()
     ng = C.c_int64()
     secs = lib.qe_cpu_c4(0, sample_rows, 42, threads, 1 << 19, 1024, out, 2048, C.byref(ng))
+    one_rows = min(sample_rows, 100_000_000)
+    secs1 = lib.qe_cpu_c4(0, one_rows, 42, 1, 1 << 19, 1024, out, 2048, C.byref(ng))
+    secs_t = lib.qe_cpu_c4_fast(0, sample_rows, 42, threads, 1 << 19, 1024, out, 2048, C.byref(ng))
     return {"value": sample_rows / secs, "unit": "rows/s", "cores": threads, "kind": "port",
             "sample": f"rows 0..{sample_rows - 1} of the same C4 table (seed 42), {threads} threads, "
-                      f"{secs:.3f} s; C restatement of the reference operator chain (oracle/cpu_baseline.c)"}
+                      f"{secs:.3f} s; C restatement of the reference operator chain (oracle/cpu_baseline.c)",
+            "single_thread": {"value": one_rows / secs1, "cores": 1,
+                              "sample": f"rows 0..{one_rows - 1}, 1 thread, {secs1:.3f} s"},
+            "tuned": ({"value": sample_rows / secs_t, "cores": threads,
+                       "sample": f"rows 0..{sample_rows - 1}, {threads} threads, {secs_t:.3f} s; "
+                                 "per-thread open-addressing tables (qe_cpu_c4_fast)"} if secs_t > 0 else None)}
 
 
 def load_traffic(rows: int):

@@ -187,16 +187,22 @@ def _oracle_lib():
     lib.qe_cpu_c4.restype = C.c_double
     lib.qe_cpu_c4.argtypes = [C.c_int64, C.c_int64, C.c_uint64, C.c_int, C.c_int64, C.c_int64,
                               C.POINTER(_G), C.c_int64, C.POINTER(C.c_int64)]
+    lib.qe_cpu_c4_fast.restype = C.c_double
+    lib.qe_cpu_c4_fast.argtypes = lib.qe_cpu_c4.argtypes
     return lib
 
 
+@pytest.mark.parametrize("fast", [False, True])
 @pytest.mark.parametrize("threads,row0", [(1, 0), (3, 12345)])
-def test_cpu_baseline_matches_oracle(threads, row0):
+def test_cpu_baseline_matches_oracle(threads, row0, fast):
+    """Both CPU legs of bench.py: the reference-faithful port and the tuned implementation."""
     lib = _oracle_lib()
     n = 100_000
     out = (_G * 2048)()
     ng = C.c_int64()
-    lib.qe_cpu_c4(row0, n, 42, threads, 1 << 19, 1024, out, 2048, C.byref(ng))
+    secs = (lib.qe_cpu_c4_fast if fast else lib.qe_cpu_c4)(row0, n, 42, threads, 1 << 19, 1024, out, 2048,
+                                                           C.byref(ng))
+    assert secs >= 0
     k, _ = gen.generate(gen.GEN_MOD, 1024, 42, 0, row0, n)
     a, _ = gen.generate(gen.GEN_MOD, 1 << 20, 42, 1, row0, n)
     b, _ = gen.generate(gen.GEN_MOD, 1 << 20, 42, 2, row0, n)
