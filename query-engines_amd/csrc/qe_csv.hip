@@ -27,15 +27,16 @@ struct qe_csv_table {
   qe_ctx* ctx = nullptr;
   const uint8_t* data = nullptr;  // the file bytes (the caller keeps them until the columns are built)
   int64_t rows = 0;
+  int64_t stride = 0;             // entries per array of the block (>= rows + 1)
   int32_t nproj = 0;
-  void* block = nullptr;          // per projected column: start i64, len i64, byte start i64 [rows+1], quoted u8
+  void* block = nullptr;          // per projected column: start i64, len i64, byte start i64 [stride], quoted u8
   std::vector<int64_t> total;     // per projected column: bytes
   std::vector<qe_column> cols;    // materialised views (qe_csv_column), built on first request
   std::vector<void*> owned;
-  int64_t* start(int c) { return (int64_t*)block + (size_t)c * (rows + 1); }
-  int64_t* len(int c) { return (int64_t*)block + (size_t)(nproj + c) * (rows + 1); }
-  int64_t* bstart(int c) { return (int64_t*)block + (size_t)(2 * nproj + c) * (rows + 1); }
-  uint8_t* quoted(int c) { return (uint8_t*)((int64_t*)block + (size_t)3 * nproj * (rows + 1)) + (size_t)c * (rows + 1); }
+  int64_t* start(int c) { return (int64_t*)block + (size_t)c * stride; }
+  int64_t* len(int c) { return (int64_t*)block + (size_t)(nproj + c) * stride; }
+  int64_t* bstart(int c) { return (int64_t*)block + (size_t)(2 * nproj + c) * stride; }
+  uint8_t* quoted(int c) { return (uint8_t*)((int64_t*)block + (size_t)3 * nproj * stride) + (size_t)c * stride; }
 };
 
 namespace qe {
@@ -183,7 +184,13 @@ __global__ void __launch_bounds__(256) k_csv_terms(const uint8_t* __restrict__ d
         vq[u] = pu < nbytes ? load16(data, nbytes, pu) : Lane16{{0, 0, 0, 0}};
       }
     }
-    const Lane16 v = vq[step & 3];
+    Lane16 v;
+    switch (step & 3) {  // constant indices keep vq in registers
+      case 0: v = vq[0]; break;
+      case 1: v = vq[1]; break;
+      case 2: v = vq[2]; break;
+      default: v = vq[3]; break;
+    }
     const uint32_t qodd = has_byte(v, '"') ? (uint32_t)(quotes16(v) & 1) : 0u;
     const uint64_t par = __ballot(qodd);
     const uint32_t inq0 = carry ^ ((uint32_t)__popcll(par & below) & 1u);
@@ -251,15 +258,41 @@ struct FieldArgs {
   uint8_t* quoted[CSV_MAX_FIELDS];    // per column: 1 if "" sequences must be unescaped
   int32_t max_field;                  // largest projected field index
   int32_t delim;
+  uint64_t low_mask;                  // bit f: field f < 64 is projected (skips the table lookup)
 };
 
-__device__ __forceinline__ void trim(const uint8_t* d, int64_t& s, int64_t& e) {
+// Bytes of the file by global position: straight from HBM, or from a wave's LDS copy of a block.
+struct GBytes {
+  const uint8_t* d;
+  int64_t nbytes;
+  __device__ __forceinline__ uint32_t operator[](int64_t i) const { return d[i]; }
+  __device__ __forceinline__ Lane16 load16(int64_t a) const { return qe::load16(d, nbytes, a); }
+};
+struct LBytes {
+  const uint8_t* L;  // LDS copy of [base, base + span), base 16-byte aligned
+  int64_t base;
+  __device__ __forceinline__ uint32_t operator[](int64_t i) const { return L[i - base]; }
+  __device__ __forceinline__ Lane16 load16(int64_t a) const {  // a: 16-byte aligned, inside the copy
+    const uint4 t = *(const uint4*)(L + (a - base));
+    Lane16 v;
+    v.w[0] = t.x;
+    v.w[1] = t.y;
+    v.w[2] = t.z;
+    v.w[3] = t.w;
+    return v;
+  }
+};
+
+template <typename D>
+__device__ __forceinline__ void trim(const D& d, int64_t& s, int64_t& e) {
   while (s < e && d[s] <= 0x20) ++s;
   while (e > s && d[e - 1] <= 0x20) --e;
 }
 
-__device__ void record_field(const uint8_t* d, const FieldArgs& A, int f, int64_t s, int64_t e, int64_t row) {
+template <typename D>
+__device__ void record_field(const D& d, const FieldArgs& A, int f, int64_t s, int64_t e, int64_t row) {
   if (f > A.max_field) return;
+  if (f < 64 && !((A.low_mask >> f) & 1)) return;
   const int sl = A.slot[f];
   if (sl < 0) return;
   trim(d, s, e);
@@ -287,44 +320,130 @@ __device__ void record_field(const uint8_t* d, const FieldArgs& A, int f, int64_
   A.quoted[sl][row] = q;
 }
 
+// One record [s, e): the projected fields' ranges into row `r` (missing fields read as "").
+template <typename D>
+__device__ void walk_record(const D& data, int64_t s, int64_t e, const FieldArgs& A, int32_t nproj, int64_t r) {
+  for (int c = 0; c < nproj; ++c) {
+    A.start[c][r] = s;
+    A.len[c][r] = 0;
+    A.quoted[c][r] = 0;
+  }
+  int f = 0;
+  int64_t fs = s;
+  uint32_t inq = 0;
+  // 16-byte aligned loads; bytes outside [s, e) are skipped
+  for (int64_t a = s & ~(int64_t)15; a < e && f <= A.max_field; a += 16) {
+    const Lane16 v = data.load16(a);
+    const uint32_t lo = (uint32_t)(s > a ? s - a : 0);
+    const uint32_t hi = (uint32_t)(e - a < 16 ? e - a : 16);
+    const uint32_t in = (hi >= 32 ? 0xFFFFu : ((1u << hi) - 1u)) & ~((1u << lo) - 1u);
+    uint32_t q = eq16(v, '"') & in, d = eq16(v, (uint32_t)A.delim) & in;
+    if (q == 0 && inq) continue;
+    while (d && f <= A.max_field) {
+      const int k = __builtin_ctz(d);
+      // quote toggles before this delimiter
+      const uint32_t before = q & ((1u << k) - 1u);
+      inq ^= (uint32_t)__popc(before) & 1u;
+      q &= ~((1u << k) - 1u);
+      d &= d - 1;
+      if (!inq) {
+        record_field(data, A, f, fs, a + k, r);
+        ++f;
+        fs = a + k + 1;
+      }
+    }
+    inq ^= (uint32_t)__popc(q) & 1u;
+  }
+  if (f <= A.max_field) record_field(data, A, f, fs, e, r);
+}
+
+// The field table in LDS: indexing kernel arguments by a per-lane field number would turn every
+// field into a memory round trip.
+__device__ __forceinline__ void stage_args(FieldArgs& S, const FieldArgs& A) {
+  const int16_t* src = A.slot;
+  for (int i = threadIdx.x; i <= A.max_field; i += blockDim.x) S.slot[i] = src[i];
+  if (threadIdx.x < CSV_MAX_FIELDS) {
+    S.start[threadIdx.x] = A.start[threadIdx.x];
+    S.len[threadIdx.x] = A.len[threadIdx.x];
+    S.quoted[threadIdx.x] = A.quoted[threadIdx.x];
+  }
+  if (threadIdx.x == 0) {
+    S.max_field = A.max_field;
+    S.delim = A.delim;
+    S.low_mask = A.low_mask;
+  }
+  __syncthreads();
+}
+
 __global__ void k_csv_fields(const uint8_t* __restrict__ data, int64_t nbytes, const int64_t* __restrict__ ends,
-                             const int64_t* __restrict__ kept, int64_t first_row_line, int64_t nrows, FieldArgs A,
+                             const int64_t* __restrict__ kept, int64_t first_row_line, int64_t nrows, FieldArgs Ag,
                              int32_t nproj) {
+  __shared__ FieldArgs A;
+  stage_args(A, Ag);
   for (int64_t r = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; r < nrows; r += (int64_t)gridDim.x * blockDim.x) {
     const int64_t li = kept[first_row_line + r];
-    const int64_t s = line_start(ends, li), e = ends[li];
-    for (int c = 0; c < nproj; ++c) {  // missing fields read as ""
-      A.start[c][r] = s;
-      A.len[c][r] = 0;
-      A.quoted[c][r] = 0;
-    }
-    int f = 0;
-    int64_t fs = s;
-    uint32_t inq = 0;
-    // 16-byte aligned loads; bytes outside [s, e) are skipped
-    for (int64_t a = s & ~(int64_t)15; a < e && f <= A.max_field; a += 16) {
-      const Lane16 v = load16(data, nbytes, a);
-      const uint32_t lo = (uint32_t)(s > a ? s - a : 0);
-      const uint32_t hi = (uint32_t)(e - a < 16 ? e - a : 16);
-      const uint32_t in = (hi >= 32 ? 0xFFFFu : ((1u << hi) - 1u)) & ~((1u << lo) - 1u);
-      uint32_t q = eq16(v, '"') & in, d = eq16(v, (uint32_t)A.delim) & in;
-      if (q == 0 && inq) continue;
-      while (d && f <= A.max_field) {
-        const int k = __builtin_ctz(d);
-        // quote toggles before this delimiter
-        const uint32_t before = q & ((1u << k) - 1u);
-        inq ^= (uint32_t)__popc(before) & 1u;
-        q &= ~((1u << k) - 1u);
-        d &= d - 1;
-        if (!inq) {
-          record_field(data, A, f, fs, a + k, r);
-          ++f;
-          fs = a + k + 1;
-        }
+    walk_record(GBytes{data, nbytes}, line_start(ends, li), ends[li], A, nproj, r);
+  }
+}
+
+// All lines at once, for files whose every line is a record (the common case; otherwise the
+// host reruns the kept-line path above): one wave per 64 consecutive lines copies their bytes
+// into LDS with coalesced 16-byte loads and each lane walks its line there (a lane per line
+// reading HBM directly touches 64 different rows per load instruction). Lines whose block does
+// not fit LB_BYTES walk HBM. Row r = line r + first (the header is line 0). `nskip` counts the
+// lines that are not records (blank, or '#' first).
+constexpr int LB_BYTES = 8192;
+__global__ void __launch_bounds__(256) k_csv_lines(const uint8_t* __restrict__ data, int64_t nbytes,
+                                                   const int64_t* __restrict__ ends, int64_t nlines, int64_t first,
+                                                   FieldArgs Ag, int32_t nproj,
+                                                   unsigned long long* __restrict__ nskip) {
+  __shared__ __attribute__((aligned(16))) uint8_t lds[4][LB_BYTES];
+  __shared__ FieldArgs A;
+  stage_args(A, Ag);
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  uint8_t* L = lds[wid];
+  const int64_t wstride = (int64_t)gridDim.x * 4 * 64;
+  for (int64_t l0 = ((int64_t)blockIdx.x * 4 + wid) * 64; l0 < nlines; l0 += wstride) {
+    const int64_t li = l0 + lane;
+    const bool live = li < nlines;
+    const int64_t s = live ? line_start(ends, li) : 0, e = live ? ends[li] : 0;
+    const int last = (int)(min(l0 + 63, nlines - 1) - l0);
+    const int64_t base = __shfl(s, 0) & ~(int64_t)15;
+    const int64_t span = __shfl(e, last) - base;
+    const bool staged = span <= LB_BYTES;
+    if (staged) {  // all of the block's loads in flight at once, then into LDS
+      Lane16 v[LB_BYTES / 1024];
+#pragma unroll
+      for (int k = 0; k < LB_BYTES / 1024; ++k) {
+        const int64_t off = (int64_t)k * 1024 + lane * 16;
+        if (off < span) v[k] = load16(data, nbytes, base + off);
       }
-      inq ^= (uint32_t)__popc(q) & 1u;
+#pragma unroll
+      for (int k = 0; k < LB_BYTES / 1024; ++k) {
+        const int64_t off = (int64_t)k * 1024 + lane * 16;
+        if (off < span) *(uint4*)(L + off) = make_uint4(v[k].w[0], v[k].w[1], v[k].w[2], v[k].w[3]);
+      }
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     }
-    if (f <= A.max_field) record_field(data, A, f, fs, e, r);
+    if (live) {
+      bool keep = false;
+      if (staged) {
+        const LBytes d{L, base};
+        if (s < e && d[s] != '#')
+          for (int64_t p = s; p < e && !keep; ++p) keep = d[p] > 0x20;
+        if (keep && li >= first) walk_record(d, s, e, A, nproj, li - first);
+      } else {
+        const GBytes d{data, nbytes};
+        if (s < e && d[s] != '#')
+          for (int64_t p = s; p < e && !keep; ++p) keep = d[p] > 0x20;
+        if (keep && li >= first) walk_record(d, s, e, A, nproj, li - first);
+      }
+      if (!keep) atomicAdd(nskip, 1ull);
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");  // the block's LDS is rewritten next
+    __builtin_amdgcn_wave_barrier();
   }
 }
 
@@ -383,12 +502,14 @@ int csv_parse(qe_ctx* ctx, const uint8_t* data, int64_t nbytes, const qe_csv_opt
   for (int i = 0; i < CSV_MAX_FIELD_INDEX; ++i) A.slot[i] = -1;
   A.max_field = -1;
   A.delim = opt->delimiter;
+  A.low_mask = 0;
   for (int c = 0; c < nproj; ++c) {
     const int f = opt->field_index ? opt->field_index[c] : c;
     QE_CHECK(f >= 0 && f < CSV_MAX_FIELD_INDEX, QE_ERR_UNSUPPORTED, "CSV field index %d out of range", f);
     QE_CHECK(A.slot[f] < 0, QE_ERR_INVALID_ARG, "CSV field %d projected twice", f);
     A.slot[f] = (int16_t)c;
     A.max_field = std::max(A.max_field, f);
+    if (f < 64) A.low_mask |= 1ull << f;
   }
   // ---- record terminators
   const int64_t nseg = (int64_t)div_up((uint64_t)(nbytes > 0 ? nbytes : 1), SEG);
@@ -429,40 +550,53 @@ int csv_parse(qe_ctx* ctx, const uint8_t* data, int64_t nbytes, const qe_csv_opt
     QE_HIP(hipMemcpyAsync(ends + nterm, &nbytes, 8, hipMemcpyHostToDevice, ctx->stream));
     QE_HIP(hipStreamSynchronize(ctx->stream));  // &nbytes is a host stack address
   }
-  // ---- kept records
-  int64_t nkept = 0;
-  if (nlines > 0) {
-    hipLaunchKernelGGL(k_csv_keep, dim3(grid_for(ctx, nlines)), dim3(256), 0, ctx->stream, data, ends, nlines, keep);
-    QE_TRY(launch_check("k_csv_keep"));
-    QE_TRY(exclusive_scan_i64(ctx, keep, kstart, nlines));
-    QE_TRY(read_i64(ctx, kstart + nlines, &nkept));
-  }
-  int64_t* kept = nullptr;
-  QE_TRY(ctx_workspace(ctx, 2, (size_t)(nkept + 1) * 8, &p));
-  kept = (int64_t*)p;
-  if (nkept > 0) {
-    hipLaunchKernelGGL(k_csv_compact_lines, dim3(grid_for(ctx, nlines)), dim3(256), 0, ctx->stream, keep, kstart,
-                       nlines, kept);
-    QE_TRY(launch_check("k_csv_compact_lines"));
-  }
+  // ---- records and their projected fields
   const int64_t first = opt->has_header ? 1 : 0;
-  const int64_t rows = std::max<int64_t>(0, nkept - first);
-  t->rows = rows;
-  // ---- fields (kept in the table until the columns are built)
   t->nproj = nproj;
   t->data = data;
-  QE_TRY(dmalloc(t, (size_t)nproj * (size_t)(rows + 1) * 25 + 64, &p));
+  t->stride = nlines + 1;
+  QE_TRY(dmalloc(t, (size_t)nproj * (size_t)t->stride * 25 + 64, &p));
   t->block = p;
   for (int c = 0; c < nproj; ++c) {
     A.start[c] = t->start(c);
     A.len[c] = t->len(c);
     A.quoted[c] = t->quoted(c);
   }
-  if (rows > 0) {
-    hipLaunchKernelGGL(k_csv_fields, dim3(grid_for(ctx, rows)), dim3(256), 0, ctx->stream, data, nbytes, ends, kept,
-                       first, rows, A, nproj);
-    QE_TRY(launch_check("k_csv_fields"));
+  int64_t rows = 0;
+  if (nlines > 0) {
+    // every line a record (the common case): one pass over the lines, no kept-line list
+    unsigned long long* nskip = (unsigned long long*)keep;
+    QE_HIP(hipMemsetAsync(nskip, 0, 8, ctx->stream));
+    const int64_t blocks = std::min<int64_t>((int64_t)div_up(div_up((uint64_t)nlines, 64), 4), (int64_t)ctx->num_cus * 8);
+    hipLaunchKernelGGL(k_csv_lines, dim3((unsigned)blocks), dim3(256), 0, ctx->stream, data, nbytes, ends, nlines, first,
+                       A, nproj, nskip);
+    QE_TRY(launch_check("k_csv_lines"));
+    int64_t skipped = 0;
+    QE_TRY(read_i64(ctx, (const int64_t*)nskip, &skipped));
+    if (skipped == 0) {
+      rows = std::max<int64_t>(0, nlines - first);
+    } else {  // blank or comment lines: kept-line list, then the fields of the kept rows
+      hipLaunchKernelGGL(k_csv_keep, dim3(grid_for(ctx, nlines)), dim3(256), 0, ctx->stream, data, ends, nlines, keep);
+      QE_TRY(launch_check("k_csv_keep"));
+      QE_TRY(exclusive_scan_i64(ctx, keep, kstart, nlines));
+      int64_t nkept = 0;
+      QE_TRY(read_i64(ctx, kstart + nlines, &nkept));
+      QE_TRY(ctx_workspace(ctx, 2, (size_t)(nkept + 1) * 8, &p));
+      int64_t* kept = (int64_t*)p;
+      if (nkept > 0) {
+        hipLaunchKernelGGL(k_csv_compact_lines, dim3(grid_for(ctx, nlines)), dim3(256), 0, ctx->stream, keep, kstart,
+                           nlines, kept);
+        QE_TRY(launch_check("k_csv_compact_lines"));
+      }
+      rows = std::max<int64_t>(0, nkept - first);
+      if (rows > 0) {
+        hipLaunchKernelGGL(k_csv_fields, dim3(grid_for(ctx, rows)), dim3(256), 0, ctx->stream, data, nbytes, ends, kept,
+                           first, rows, A, nproj);
+        QE_TRY(launch_check("k_csv_fields"));
+      }
+    }
   }
+  t->rows = rows;
   // ---- per column: byte positions of the values (scan of lengths) and the column's size
   t->total.assign((size_t)nproj, 0);
   for (int c = 0; c < nproj && rows > 0; ++c) QE_TRY(exclusive_scan_i64(ctx, A.len[c], t->bstart(c), rows));

@@ -176,3 +176,23 @@ def test_missing_file_raises(tmp_path):
 
     with pytest.raises(FileNotFoundError):
         CsvDataSource(str(tmp_path / "nope.csv")).schema()
+
+
+@pytest.mark.gpu
+def test_gpu_csv_long_lines_and_blank_lines(gpu_ctx, tmp_path):
+    """Line blocks too long for a wave's LDS copy (k_csv_lines walks HBM for those), and large
+    files with blank / comment lines in the middle (the kept-line path)."""
+    rng = random.Random(9)
+    body = []
+    for i in range(40_000):
+        w = rng.choice([1, 5, 300, 2000]) if (i // 500) % 3 == 1 else rng.choice([1, 3, 8])
+        body.append(f"{i},{'y' * w},\"q\"\"{i % 13}\"")
+    long_data = ("a,b,c\n" + "\n".join(body) + "\n").encode()
+    mixed = body[:]
+    for at in (5, 20_000, 39_990):
+        mixed.insert(at, rng.choice(["", "   ", "#comment,x", "\t"]))
+    for data in (long_data, ("a,b,c\n" + "\n".join(mixed) + "\n").encode()):
+        names, proj, cols, _ = _gpu_scan(gpu_ctx, tmp_path, data)
+        onames, _, rows = R.parse(data)
+        assert names == onames
+        assert cols == R.project(rows, range(len(onames)))

@@ -1,0 +1,9 @@
+#!/bin/bash
+# PMC passes over tools/bench_tripdata.py (CSV scan kernels), on the GPU box.
+set -o pipefail
+export TMPDIR=/tmp
+OUT=${GRAFT_REPO_ROOT:-$PWD}/gpurun_out/csvpmc
+mkdir -p $OUT
+B="python3 tools/bench_tripdata.py ${ROWS:-1000000}"
+timeout -k 10 300 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_SALU SQ_WAIT_INST_LDS --output-format csv -d $OUT/sq -o run -- $B > $OUT/sq.log 2>&1 || exit 1
+timeout -k 10 300 rocprofv3 --pmc SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_INSTS_VMEM GRBM_GUI_ACTIVE --output-format csv -d $OUT/lds -o run -- $B > $OUT/lds.log 2>&1 || exit 1
