@@ -103,6 +103,8 @@ def main():
     ap.add_argument("--cpu-sample-rows", type=int, default=0, help="default: the same rows as one GPU")
     ap.add_argument("--cpu-threads", type=int, default=0)
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--exchange", action="store_true",
+                    help="run the multi-GPU exchange leg even with one rank (tests the N > 1 step on one GPU)")
     args = ap.parse_args()
 
     import torch
@@ -119,7 +121,9 @@ def main():
     if world != args.gpus:
         print(f"warning: --gpus {args.gpus} but WORLD_SIZE {world}; using WORLD_SIZE", file=sys.stderr)
     torch.cuda.set_device(local)
-    if world > 1:
+    if world > 1 or args.exchange:
+        for k, v in (("MASTER_ADDR", "127.0.0.1"), ("MASTER_PORT", "29511"), ("RANK", "0"), ("WORLD_SIZE", "1")):
+            os.environ.setdefault(k, v)
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     from kquery.exchange import exchange_partials
 
@@ -131,7 +135,8 @@ def main():
     aggs = [(N.AGG_SUM, N.TYPE_INT64), (N.AGG_COUNT_STAR, N.TYPE_INT64), (N.AGG_MIN, N.TYPE_INT64),
             (N.AGG_MAX, N.TYPE_INT64)]
     partial = HashAggregateState(ctx, [N.TYPE_INT64], aggs, 1024)
-    owner = HashAggregateState(ctx, [N.TYPE_INT64], aggs, 1024) if world > 1 else None
+    exchange = world > 1 or args.exchange
+    owner = HashAggregateState(ctx, [N.TYPE_INT64], aggs, 1024) if exchange else None
     spec = c4_spec(N)
     kernel_ms = []
     kinds = []
@@ -143,7 +148,7 @@ def main():
         kernel_ms.append(partial.last_kernel_time())
         kinds.append(partial.last_kernel_kind())
         final = partial
-        if world > 1:
+        if exchange:
             owner.reset()
             exchange_partials(partial, owner)
             final = owner
@@ -205,7 +210,7 @@ def main():
             "rows_per_gpu": rows,
             "groups": 1024,
             "columns": "k, a, b int64 (Arrow, no nulls)",
-            "parallelism": f"hash-sharded partial aggregate x{world}" + (" + RCCL all-to-all" if world > 1 else ""),
+            "parallelism": f"hash-sharded partial aggregate x{world}" + (" + RCCL all-to-all" if exchange else ""),
         },
         "roofline": {
             "bound": "hbm",
@@ -227,7 +232,7 @@ def main():
         line["cpu_baseline"] = cpu_baseline(args.cpu_sample_rows or rows, threads)
     if rank == 0:
         print(json.dumps(line), flush=True)
-    if world > 1:
+    if dist.is_initialized():
         dist.destroy_process_group()
 
 
