@@ -117,6 +117,10 @@ struct Plan {
   qi32 lds_log2, off_cstar;
   qi32 all8, pad1;  // every column slot is 8 bytes wide (straight-line loads)
   qi32 off_acc[QE_MAX_AGGS], off_nn[QE_MAX_AGGS], off_idx[QE_MAX_AGGS];
+  // radix-partitioned aggregation (high group counts, qe_jit.hip gen_part_source / gen_pagg_source)
+  qu8* part_rec;   // records grouped by key-hash bucket (scatter output, partition-aggregate input)
+  qi64* part_off;  // count: per (bucket, workgroup) record counts; scatter: their exclusive scan
+  qi64 part_tw;    // rows (count / scatter) or records (partition aggregate) per workgroup
 };
 
 // ---- scalar helpers ---------------------------------------------------------------------------------

@@ -1122,7 +1122,13 @@ struct qe_hashagg {
   // LDS sizing
   int32_t lds_log2 = 0;  // largest LDS table (log2 slots); 0 => global-only mode
   int32_t lds_log2_min = 0;
+  int64_t expected_groups = 0;
   int grid = 0;          // workgroups per launch (cap)
+  // radix-partitioned updates (expected groups beyond the LDS table): counts / offsets, records
+  int64_t* part_cnt = nullptr;
+  size_t part_cnt_bytes = 0;
+  uint8_t* part_rec = nullptr;
+  size_t part_rec_bytes = 0;
   // overflow records
   uint8_t* ovf = nullptr;
   uint64_t ovf_cap = 0;
@@ -1504,17 +1510,131 @@ static int launch_hashagg(const Plan& P, int grid, size_t lds, hipStream_t st) {
   }
 }
 
+template <typename T>
+static int grow_buffer(T** p, size_t* have, size_t need, hipStream_t st, const char* what) {
+  if (need <= *have) return QE_OK;
+  if (*p) {
+    QE_HIP(hipStreamSynchronize(st));
+    QE_HIP(hipFree(*p));
+  }
+  *p = nullptr;
+  *have = 0;
+  if (hipMalloc((void**)p, need) != hipSuccess) {
+    (void)hipGetLastError();
+    return fail(QE_ERR_OOM, "%s: allocation of %zu bytes failed", what, need);
+  }
+  *have = need;
+  return QE_OK;
+}
+
+// Radix-partitioned update, steps 1-3 (qe_jit.hip, "radix-partitioned aggregation"): count the
+// selected rows per (key-hash bucket, workgroup), scan, scatter one record per selected row into
+// its bucket. On return P describes the aggregation pass over the records (P.n = records,
+// P.part_tw = records per workgroup) and *fn / *grid its kernel.
+static int partition_rows(qe_hashagg* h, Plan& P, hipFunction_t* fn, int* grid) {
+  qe_ctx* ctx = h->ctx;
+  // aggregation-pass LDS table: the largest that fits the per-workgroup budget
+  int tlog2 = 16;
+  while (tlog2 >= 8 && lds_layout_at(h, &P, tlog2) > HA_LDS_BUDGET) --tlog2;
+  QE_CHECK(tlog2 >= 8, QE_ERR_UNSUPPORTED, "aggregate state too wide for a partitioned LDS table");
+  // buckets: about a quarter of the table's slots in groups per bucket (a slice spans <= 2 buckets)
+  int log2p = 1;
+  while (log2p < 13 && (((int64_t)1 << tlog2) >> 2) * ((int64_t)1 << log2p) < h->expected_groups) ++log2p;
+  std::string sc, ss, sa;
+  size_t jl = 0;
+  QE_CHECK(gen_part_source(P, log2p, false, &sc) && gen_part_source(P, log2p, true, &ss) &&
+               gen_pagg_source(P, tlog2, &sa, &jl),
+           QE_ERR_UNSUPPORTED, "plan shape not specialisable");
+  hipFunction_t fc, fs;
+  int bpc = 0;
+  QE_TRY(jit_kernel(ctx, sc, &fc, &bpc, "qe_pcount"));
+  QE_TRY(jit_kernel(ctx, ss, &fs, &bpc, "qe_pscatter"));
+  QE_TRY(jit_kernel(ctx, sa, fn, &bpc, "qe_pagg"));
+  const int64_t n = P.n;
+  int64_t g = std::min<int64_t>((int64_t)ctx->num_cus * 2, (int64_t)div_up((uint64_t)n, 256));
+  const int64_t tw = (int64_t)div_up(div_up((uint64_t)n, (uint64_t)g), 256) * 256;
+  g = (int64_t)div_up((uint64_t)n, (uint64_t)tw);
+  const size_t cells = ((size_t)1 << log2p) * (size_t)g;
+  QE_TRY(grow_buffer(&h->part_cnt, &h->part_cnt_bytes, (2 * cells + 1) * 8, ctx->stream, "partition counts"));
+  int64_t* cnt = h->part_cnt;
+  int64_t* off = cnt + cells;
+  P.part_tw = tw;
+  P.part_off = (qi64*)cnt;
+  QE_TRY(jit_launch(ctx, fc, (int)g, P));
+  QE_TRY(launch_check("qe_pcount"));
+  QE_TRY(exclusive_scan_i64(ctx, cnt, off, (int64_t)cells));
+  void* pin;
+  QE_TRY(ctx_pinned(ctx, 8, &pin));
+  QE_HIP(hipMemcpyAsync(pin, off + cells, 8, hipMemcpyDeviceToHost, ctx->stream));
+  QE_HIP(hipStreamSynchronize(ctx->stream));
+  const int64_t R = *(int64_t*)pin;
+  // overflow records of the aggregation pass (bounded; groups beyond it retry their records)
+  if (!h->ovf || h->ovf_cap < (1ull << 20)) {
+    uint8_t* ovf = nullptr;
+    size_t have = 0;
+    QE_TRY(grow_buffer(&ovf, &have, (size_t)(1ull << 20) * h->rec_bytes, ctx->stream, "overflow area"));
+    if (h->ovf) (void)hipFree(h->ovf);
+    h->ovf = ovf;
+    h->ovf_cap = 1ull << 20;
+  }
+  P.ovf = h->ovf;
+  P.ovf_cap = h->ovf_cap;
+  const PartLayout L = part_layout(P);
+  const size_t rb = 8 * (size_t)L.words;
+  if (R > 0) {
+    QE_TRY(grow_buffer(&h->part_rec, &h->part_rec_bytes, (size_t)R * rb, ctx->stream, "partition records"));
+    P.part_off = (qi64*)off;
+    P.part_rec = h->part_rec;
+    QE_TRY(jit_launch(ctx, fs, (int)g, P));
+    QE_TRY(launch_check("qe_pscatter"));
+  }
+  // aggregation slices of about one bucket's records each
+  const int64_t cw = std::max<int64_t>(256, (int64_t)div_up(div_up((uint64_t)std::max<int64_t>(R, 1), (uint64_t)1 << log2p), 256) * 256);
+  P.n = R;
+  P.part_tw = cw;
+  P.part_rec = h->part_rec;
+  *grid = (int)div_up((uint64_t)std::max<int64_t>(R, 1), (uint64_t)cw);
+  h->jit_note = "radix-partitioned: " + std::to_string(1 << log2p) + " buckets, " + std::to_string(R) + " records";
+  return QE_OK;
+}
+
 static int run_update(qe_hashagg* h, Plan& P) {
   qe_ctx* ctx = h->ctx;
-  const int64_t n = P.n;
-  if (n == 0) return QE_OK;
+  const int64_t rows = P.n;
+  if (rows == 0) return QE_OK;
   const size_t lds = lds_layout(h, &P);
   P.ovf = h->ovf;
   P.ovf_cap = h->ovf_cap;
-  QE_TRY(ensure_defer(h, n));
+  QE_TRY(ensure_defer(h, rows));
   h->known_groups = -1;
   h->last_kernel_ms = 0.0;
   h->last_launches = 0;
+  // groups beyond the LDS table: radix-partition the selected rows by key hash first, then
+  // aggregate record slices in LDS (events bracket the whole sequence)
+  hipFunction_t pfn = nullptr;
+  int pgrid = 0;
+  QE_HIP(hipEventRecord(h->ev[0], ctx->stream));
+  if (!lds && ctx->jit && h->expected_groups > 0) {
+    Plan Q = P;
+    if (partition_rows(h, Q, &pfn, &pgrid) == QE_OK) {
+      P = Q;
+      if (P.n == 0) {
+        QE_HIP(hipEventRecord(h->ev[1], ctx->stream));
+        QE_HIP(hipEventSynchronize(h->ev[1]));
+        float ms = 0.f;
+        QE_HIP(hipEventElapsedTime(&ms, h->ev[0], h->ev[1]));
+        h->last_kernel_ms = ms;
+        h->last_launches = 1;
+        h->last_specialized = 1;
+        h->row_base += rows;
+        return QE_OK;
+      }
+    } else {
+      h->jit_note = std::string("partitioning unavailable: ") + qe_last_error();
+      pfn = nullptr;
+    }
+  }
+  const int64_t n = P.n;
   int out_i = 0;
   const uint32_t* defer_in = nullptr;
   for (int pass = 0;; ++pass) {
@@ -1533,9 +1653,11 @@ static int run_update(qe_hashagg* h, Plan& P) {
     int grid = (int)std::min<int64_t>((int64_t)div_up((uint64_t)waves, HA_THREADS / 64), gcap);
     if (grid < 1) grid = 1;
     // specialised kernel for this plan shape when possible, else the generic interpreter
-    hipFunction_t jfn = nullptr;
-    int jgrid = 0;
-    if (lds && ctx->jit) {
+    hipFunction_t jfn = pfn;
+    int jgrid = pgrid;
+    if (pfn) {
+      // records of the partitioned update
+    } else if (lds && ctx->jit) {
       std::string src;
       size_t jl = 0;
       if (gen_fused_source(P, P.lds_log2, &src, &jl)) {
@@ -1552,10 +1674,10 @@ static int run_update(qe_hashagg* h, Plan& P) {
       } else {
         h->jit_note = "plan shape not specialisable";
       }
-    } else {
+    } else if (h->jit_note.rfind("partitioning unavailable", 0) != 0) {
       h->jit_note = lds ? "jit disabled" : "global-only launch";
     }
-    QE_HIP(hipEventRecord(h->ev[0], ctx->stream));
+    if (pass > 0) QE_HIP(hipEventRecord(h->ev[0], ctx->stream));
     if (jfn) {
       QE_TRY(jit_launch(ctx, jfn, jgrid, P));
     } else {
@@ -1573,7 +1695,7 @@ static int run_update(qe_hashagg* h, Plan& P) {
       h->last_launches += 1;
     }
     QE_CHECK(c[3] == 0, QE_ERR_CAPACITY, "hash aggregate lost %llu groups (overflow area)", (unsigned long long)c[3]);
-    const uint64_t groups = c[0], deferred = c[1], ovf_recs = c[2];
+    const uint64_t groups = c[0], deferred = c[1], ovf_recs = std::min<uint64_t>(c[2], P.ovf_cap);
     if (deferred == 0 && ovf_recs == 0) {
       if (groups * 2 > h->t.cap) QE_TRY(table_grow(h, 4 * h->t.cap));
       h->known_groups = (int64_t)groups;  // saves finalize a device round trip
@@ -1590,7 +1712,7 @@ static int run_update(qe_hashagg* h, Plan& P) {
     defer_in = h->defer[out_i];
     out_i ^= 1;
   }
-  h->row_base += n;
+  h->row_base += rows;
   return QE_OK;
 }
 
@@ -1677,6 +1799,7 @@ int qe_hashagg_create(qe_ctx* ctx, int32_t nkeys, const int32_t* key_types, int3
   // LDS table: 2x the expected groups (load factor <= 0.5); a launch may shrink it down to
   // 1.25x (lds_log2_min) to fit the per-workgroup budget, else the launch is global-only.
   const int64_t eg = expected_groups > 0 ? expected_groups : 1024;
+  h->expected_groups = eg;
   int log2 = 8, log2_min = 8;
   while (log2 < 16 && ((int64_t)1 << log2) < 2 * eg) ++log2;
   while (log2_min < 16 && ((int64_t)1 << log2_min) < (5 * eg + 3) / 4) ++log2_min;
@@ -1712,6 +1835,8 @@ int qe_hashagg_destroy(qe_hashagg* h) {
   if (h->table_mem) (void)hipFree(h->table_mem);
   if (h->ctl) (void)hipFree(h->ctl);
   if (h->ovf) (void)hipFree(h->ovf);
+  if (h->part_cnt) (void)hipFree(h->part_cnt);
+  if (h->part_rec) (void)hipFree(h->part_rec);
   for (int i = 0; i < 2; ++i) {
     if (h->defer[i]) (void)hipFree(h->defer[i]);
     if (h->ev[i]) (void)hipEventDestroy(h->ev[i]);

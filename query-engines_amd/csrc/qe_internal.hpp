@@ -61,6 +61,18 @@ int ctx_workspace(qe_ctx* ctx, int slot, size_t bytes, void** out);  // grow-onl
 int parallel_h2d_copy(qe_ctx* ctx, void* dst, const void* src, size_t n);
 // Per-plan kernel specialisation (qe_jit.hip).
 bool gen_fused_source(const qe::Plan& P, int log2, std::string* src, size_t* lds_bytes);
+// Radix-partitioned aggregation for group counts beyond the LDS table (qe_jit.hip).
+struct PartLayout {
+  int words = 0;  // record width in 8-byte words (even)
+  int used = 0;   // words holding fields (the rest is padding)
+  int val_word[QE_MAX_AGGS] = {};  // word of aggregate j's input value, -1 if it has none
+  int flags_word = -1;             // bit 0 null key, bit 1 + j input j valid; -1 if nothing is nullable
+  int row_word = -1;               // global row index (fp64 MIN/MAX); -1 if not needed
+  bool row = false;
+};
+PartLayout part_layout(const qe::Plan& P);
+bool gen_part_source(const qe::Plan& P, int log2p, bool scatter, std::string* src);
+bool gen_pagg_source(const qe::Plan& P, int log2, std::string* src, size_t* lds_bytes);
 int jit_kernel(qe_ctx* ctx, const std::string& src, hipFunction_t* fn, int* blocks_per_cu,
                const char* name = "qe_fused", int block = 512);
 int jit_launch(qe_ctx* ctx, hipFunction_t fn, int grid, const qe::Plan& P, int block = 512);

@@ -160,53 +160,24 @@ void emit_predicate(const Plan& P, std::ostringstream& o, int rows) {
   }
 }
 
-}  // namespace
+// Columns read by the predicate (mask + terms) and the group keys.
+unsigned pred_key_cols(const Plan& P) {
+  unsigned m = 0;
+  if (P.mask_col >= 0) m |= 1u << P.mask_col;
+  for (int t = 0; t < P.nterms; ++t) {
+    m |= 1u << P.terms[t].lhs;
+    if (P.terms[t].rhs >= 0) m |= 1u << P.terms[t].rhs;
+  }
+  if (P.key_mode != 0)
+    for (int k = 0; k < P.nkeys; ++k) m |= 1u << P.key_col[k];
+  return m;
+}
 
-// Returns false when the plan shape is outside what the generator emits (caller uses the
-// generic kernel). `log2` is the LDS table size chosen for this launch.
-bool gen_fused_source(const Plan& P, int log2, std::string* src, size_t* lds_bytes) {
-  if (log2 < 4 || log2 > 16 || P.ncols < 1 || P.ncols > QE_MAX_COLS) return false;
-  std::ostringstream o;
-  const int S = 1 << log2, SS = S + 2;
-  o << "\nusing namespace qe;\n"
-    << "extern \"C\" __global__ void __launch_bounds__(512) qe_fused(const Plan P) {\n"
-    << "  constexpr int LOG2 = " << log2 << ", S = " << S << ", SS = " << SS << ";\n"
-    << "  __shared__ qi64 s_keys[SS];\n  __shared__ qu32 s_cst[SS];\n";
-  size_t lds = (size_t)SS * 12;
-  for (int j = 0; j < P.naggs; ++j) {
-    const DAgg& a = P.aggs[j];
-    if (a.acc != ACC_NONE) {
-      o << "  __shared__ qi64 s_acc" << j << "[SS];\n";
-      lds += 8 * SS;
-    }
-    if (a.track_nn) {
-      o << "  __shared__ qu32 s_nn" << j << "[SS];\n";
-      lds += 4 * SS;
-    }
-    if (acc_is_f64mm(a.acc)) {
-      o << "  __shared__ qu64 s_idx" << j << "[4 * SS];\n";
-      lds += 32 * SS;
-    }
-  }
-  *lds_bytes = lds;
-  // ---- init
-  o << "  for (int s = threadIdx.x; s < SS; s += blockDim.x) {\n    s_keys[s] = EMPTY_KEY;\n    s_cst[s] = 0;\n";
-  for (int j = 0; j < P.naggs; ++j) {
-    const DAgg& a = P.aggs[j];
-    if (a.acc != ACC_NONE) o << "    s_acc" << j << "[s] = " << acc_init(a.acc) << ";\n";
-    if (a.track_nn) o << "    s_nn" << j << "[s] = 0;\n";
-    if (acc_is_f64mm(a.acc))
-      o << "    for (int k = 0; k < 4; ++k) s_idx" << j << "[k * SS + s] = ~0ull;\n";
-  }
-  o << "  }\n  __syncthreads();\n"
-    << "  const int lane = threadIdx.x & 63;\n"
-    << "  const qi64 wave = (blockIdx.x * (qi64)blockDim.x + threadIdx.x) >> 6;\n"
-    << "  const qi64 stride = (((qi64)gridDim.x * blockDim.x) >> 6) * 256;\n"
-    << "  for (qi64 base = wave * 256; base < P.n; base += stride) {\n"
-    << "    const bool full = base + 256 <= P.n;\n"
-    << "    const qi64 r0 = base + 2 * lane;\n";
-  // ---- column loads: lane rows r0 + {0,1} and r0 + 128 + {0,1}
+// Column loads of one 256-row wave step (lane rows r0 + {0,1} and r0 + 128 + {0,1}) for the
+// slots in `need`: c<slot>[4] values (sign-/zero-extended), v<slot> validity bits.
+void emit_col_loads(const Plan& P, std::ostringstream& o, unsigned need) {
   for (int c = 0; c < P.ncols; ++c) {
+    if (!((need >> c) & 1u)) continue;
     const std::string cs = std::to_string(c);
     o << "    qi64 c" << cs << "[4];\n";
     const int kind = P.cols[c].kind;
@@ -240,14 +211,21 @@ bool gen_fused_source(const Plan& P, int log2, std::string* src, size_t* lds_byt
         << "      v" << cs << " = lo | (hi << 2);\n    }\n";
     }
   }
-  // ---- active rows: range, retry set, mask, predicate terms
+}
+
+// act: rows of this step inside [0, P.n), in the retry set (if any), passing mask and terms.
+void emit_active_rows(const Plan& P, std::ostringstream& o, bool retry) {
   o << "    qu32 act = 15u;\n"
-    << "    if (!full) { act = 0; for (int r = 0; r < 4; ++r) act |= (qu32)(r0 + 128 * (r >> 1) + (r & 1) < P.n) << r; }\n"
-    << "    if (P.defer_in) {\n      for (int r = 0; r < 4; ++r) { const qi64 row = r0 + 128 * (r >> 1) + (r & 1);\n"
-    << "        if (row < P.n && !((P.defer_in[row >> 5] >> (row & 31)) & 1)) act &= ~(1u << r); }\n    }\n";
+    << "    if (!full) { act = 0; for (int r = 0; r < 4; ++r) act |= (qu32)(r0 + 128 * (r >> 1) + (r & 1) < P.n) << r; }\n";
+  if (retry)
+    o << "    if (P.defer_in) {\n      for (int r = 0; r < 4; ++r) { const qi64 row = r0 + 128 * (r >> 1) + (r & 1);\n"
+      << "        if (row < P.n && !((P.defer_in[row >> 5] >> (row & 31)) & 1)) act &= ~(1u << r); }\n    }\n";
   emit_predicate(P, o, 4);
   o << "    if (act == 0) continue;\n";
-  // ---- keys
+}
+
+// key[4] (packed / canonical int64 group key) and knull (bit r: the key of row r is null).
+void emit_keys(const Plan& P, std::ostringstream& o) {
   o << "    qi64 key[4] = {0, 0, 0, 0};\n    qu32 knull = 0;\n";
   if (P.key_mode == 1) {
     const int c = P.key_col[0];
@@ -265,7 +243,47 @@ bool gen_fused_source(const Plan& P, int log2, std::string* src, size_t* lds_byt
     }
     o << "      key[r] = k;\n    }\n";
   }
-  // ---- LDS slots: first probe of the 4 rows together, collisions probe on
+}
+
+// Per-workgroup LDS table of 2^log2 (+2 special) slots: declarations and initialisation.
+void emit_lds_table(const Plan& P, std::ostringstream& o, int log2, size_t* lds_bytes) {
+  const int S = 1 << log2, SS = S + 2;
+  o << "  constexpr int LOG2 = " << log2 << ", S = " << S << ", SS = " << SS << ";\n"
+    << "  __shared__ qi64 s_keys[SS];\n  __shared__ qu32 s_cst[SS];\n";
+  size_t lds = (size_t)SS * 12;
+  for (int j = 0; j < P.naggs; ++j) {
+    const DAgg& a = P.aggs[j];
+    if (a.acc != ACC_NONE) {
+      o << "  __shared__ qi64 s_acc" << j << "[SS];\n";
+      lds += 8 * SS;
+    }
+    if (a.track_nn) {
+      o << "  __shared__ qu32 s_nn" << j << "[SS];\n";
+      lds += 4 * SS;
+    }
+    if (acc_is_f64mm(a.acc)) {
+      o << "  __shared__ qu64 s_idx" << j << "[4 * SS];\n";
+      lds += 32 * SS;
+    }
+  }
+  *lds_bytes = lds;
+  o << "  for (int s = threadIdx.x; s < SS; s += blockDim.x) {\n    s_keys[s] = EMPTY_KEY;\n    s_cst[s] = 0;\n";
+  for (int j = 0; j < P.naggs; ++j) {
+    const DAgg& a = P.aggs[j];
+    if (a.acc != ACC_NONE) o << "    s_acc" << j << "[s] = " << acc_init(a.acc) << ";\n";
+    if (a.track_nn) o << "    s_nn" << j << "[s] = 0;\n";
+    if (acc_is_f64mm(a.acc))
+      o << "    for (int k = 0; k < 4; ++k) s_idx" << j << "[k * SS + s] = ~0ull;\n";
+  }
+  o << "  }\n  __syncthreads();\n";
+}
+
+// Aggregation of the 4 active rows of a step (act, key[4], knull) into the LDS table; rows whose
+// group does not fit go to the global table, and rows the global table cannot take are deferred
+// (bit `didx` of defer_out). val[j] / ok[j]: aggregate j's input value (int64 bits) and validity
+// for row r; `row`: the row's global index (fp64 MIN/MAX order); all are C expressions of r.
+void emit_agg_rows(const Plan& P, std::ostringstream& o, const std::vector<std::string>& val,
+                   const std::vector<std::string>& ok, const std::string& row, const std::string& didx) {
   o << "    int slot[4];\n    qu32 h[4];\n    qi64 k0[4];\n"
     << "#pragma unroll\n    for (int r = 0; r < 4; ++r) { h[r] = lds_hash((qu64)key[r]) >> (32 - LOG2); k0[r] = ((act >> r) & 1) ? s_keys[h[r]] : 0; }\n"
     << "#pragma unroll\n    for (int r = 0; r < 4; ++r) slot[r] = ((knull >> r) & 1) ? S : (key[r] == EMPTY_KEY ? S + 1 : (k0[r] == key[r] ? (int)h[r] : -1));\n"
@@ -277,17 +295,14 @@ bool gen_fused_source(const Plan& P, int log2, std::string* src, size_t* lds_byt
     << "#pragma unroll\n    for (int r = 0; r < 4; ++r) glob |= (qu32)(slot[r] < 0) << r;\n"
     << "    glob &= act;\n    const qu32 loc = act & ~glob;\n"
     << "#pragma unroll\n    for (int r = 0; r < 4; ++r) if ((loc >> r) & 1) atomicAdd(&s_cst[slot[r]], 1u);\n";
-  // ---- aggregate inputs into LDS
-  std::vector<Expr> ex(P.naggs);
   for (int j = 0; j < P.naggs; ++j) {
     const DAgg& a = P.aggs[j];
     if (a.pkind == 0) continue;
-    if (!agg_expr(P, j, &ex[j])) return false;
     const std::string js = std::to_string(j);
     o << "    {\n#pragma unroll\n      for (int r = 0; r < 4; ++r) {\n"
       << "        if (!((loc >> r) & 1)) continue;\n"
-      << "        if (!(" << ex[j].ok << ")) continue;\n"
-      << "        const qi64 x = " << ex[j].v << ";\n"
+      << "        if (!(" << ok[j] << ")) continue;\n"
+      << "        const qi64 x = " << val[j] << ";\n"
       << "        const int s = slot[r];\n";
     if (a.track_nn) o << "        atomicAdd(&s_nn" << js << "[s], 1u);\n";
     switch (a.acc) {
@@ -298,36 +313,44 @@ bool gen_fused_source(const Plan& P, int log2, std::string* src, size_t* lds_byt
       case ACC_MIN_F:
       case ACC_MAX_F:
         o << "        lds_f64mm<" << (a.acc == ACC_MAX_F ? "true" : "false") << ">(s_acc" << js << ", s_idx" << js
-          << ", SS, s, x, (qu64)(P.row_base + r0 + 128 * (r >> 1) + (r & 1)));\n";
+          << ", SS, s, x, (qu64)(" << row << "));\n";
         break;
       default: break;
     }
     o << "      }\n    }\n";
   }
-  // ---- rows whose group only fits the global table (rare)
+  // rows whose group only fits the global table (rare)
   o << "    if (glob) {\n      for (int r = 0; r < 4; ++r) {\n        if (!((glob >> r) & 1)) continue;\n"
-    << "        const qi64 lr = r0 + 128 * (r >> 1) + (r & 1);\n        qu64 gs;\n"
+    << "        const qi64 lr = " << didx << ";\n        qu64 gs;\n"
     << "        if (!gtable_find(P.t, key[r], (knull >> r) & 1, gs)) {\n"
     << "          atomicOr((qu32*)&P.defer_out[lr >> 5], 1u << (lr & 31));\n"
     << "          atomicAdd(&P.t.ctl[1], 1ull);\n          continue;\n        }\n"
-    << "        gadd_cstar(P.t, gs, 1);\n        const qu64 row = (qu64)(P.row_base + lr);\n";
+    << "        gadd_cstar(P.t, gs, 1);\n        const qu64 row = (qu64)(" << row << ");\n";
   for (int j = 0; j < P.naggs; ++j) {
     const DAgg& a = P.aggs[j];
     if (a.pkind == 0) continue;
-    o << "        if (" << ex[j].ok << ") { const RowVal rv = row_partial(" << a.acc << ", " << ex[j].v
+    o << "        if (" << ok[j] << ") { const RowVal rv = row_partial(" << a.acc << ", " << val[j]
       << ", row); gcombine(P.t, " << a.acc << ", " << j << ", gs, rv.acc, 1, rv.i0, rv.i1, rv.i2, rv.i3); }\n";
   }
-  o << "      }\n    }\n  }\n";
-  // ---- flush the workgroup table into the global table (or overflow records)
+  o << "      }\n    }\n";
+}
+
+// Merge the workgroup's LDS table into the global table (or the overflow records). With
+// `mark_full`, a group that finds neither a global slot nor overflow space is flagged in s_cst
+// (bit 31) and s_fail is set: the caller then defers that group's records for a retry pass.
+void emit_flush(const Plan& P, std::ostringstream& o, bool mark_full = false) {
   o << "  __syncthreads();\n"
     << "  for (int s = threadIdx.x; s < SS; s += blockDim.x) {\n"
     << "    const qu32 c = s_cst[s];\n    if (c == 0) continue;\n"
     << "    const bool knl = s == S;\n    const qi64 key = knl ? 0 : (s == S + 1 ? EMPTY_KEY : s_keys[s]);\n"
     << "    qu64 gs;\n    const bool ok = gtable_find(P.t, key, knl, gs);\n    qu8* rec = nullptr;\n"
     << "    if (ok) {\n      gadd_cstar(P.t, gs, c);\n    } else {\n"
-    << "      const qu64 ri = atomicAdd(&P.t.ctl[2], 1ull);\n"
-    << "      if (ri >= P.ovf_cap) { atomicAdd(&P.t.ctl[3], 1ull); continue; }\n"
-    << "      rec = P.ovf + ri * (qu64)P.rec_bytes;\n      write_record_head(rec, key, knl, c);\n    }\n";
+    << "      const qu64 ri = atomicAdd(&P.t.ctl[2], 1ull);\n";
+  if (mark_full)
+    o << "      if (ri >= P.ovf_cap) { s_cst[s] = c | 0x80000000u; s_fail = 1; continue; }\n";
+  else
+    o << "      if (ri >= P.ovf_cap) { atomicAdd(&P.t.ctl[3], 1ull); continue; }\n";
+  o << "      rec = P.ovf + ri * (qu64)P.rec_bytes;\n      write_record_head(rec, key, knl, c);\n    }\n";
   int off = 24;
   for (int j = 0; j < P.naggs; ++j) {
     const DAgg& a = P.aggs[j];
@@ -346,7 +369,195 @@ bool gen_fused_source(const Plan& P, int log2, std::string* src, size_t* lds_byt
     o << " }\n    }\n";
     off += agg_rec_bytes(a.acc);
   }
-  o << "  }\n}\n";
+  o << "  }\n";
+}
+
+// Aggregate input expressions of the plan, per row r of a step.
+bool agg_inputs(const Plan& P, std::vector<Expr>* ex) {
+  ex->assign(P.naggs, Expr{"0", "1u", false});
+  for (int j = 0; j < P.naggs; ++j)
+    if (P.aggs[j].pkind != 0 && !agg_expr(P, j, &(*ex)[j])) return false;
+  return true;
+}
+
+}  // namespace
+
+// Returns false when the plan shape is outside what the generator emits (caller uses the
+// generic kernel). `log2` is the LDS table size chosen for this launch.
+bool gen_fused_source(const Plan& P, int log2, std::string* src, size_t* lds_bytes) {
+  if (log2 < 4 || log2 > 16 || P.ncols < 1 || P.ncols > QE_MAX_COLS) return false;
+  std::vector<Expr> ex;
+  if (!agg_inputs(P, &ex)) return false;
+  std::vector<std::string> val(P.naggs), ok(P.naggs);
+  for (int j = 0; j < P.naggs; ++j) {
+    val[j] = ex[j].v;
+    ok[j] = ex[j].ok;
+  }
+  std::ostringstream o;
+  o << "\nusing namespace qe;\n"
+    << "extern \"C\" __global__ void __launch_bounds__(512) qe_fused(const Plan P) {\n";
+  emit_lds_table(P, o, log2, lds_bytes);
+  o << "  const int lane = threadIdx.x & 63;\n"
+    << "  const qi64 wave = (blockIdx.x * (qi64)blockDim.x + threadIdx.x) >> 6;\n"
+    << "  const qi64 stride = (((qi64)gridDim.x * blockDim.x) >> 6) * 256;\n"
+    << "  for (qi64 base = wave * 256; base < P.n; base += stride) {\n"
+    << "    const bool full = base + 256 <= P.n;\n"
+    << "    const qi64 r0 = base + 2 * lane;\n";
+  emit_col_loads(P, o, ~0u);
+  emit_active_rows(P, o, true);
+  emit_keys(P, o);
+  emit_agg_rows(P, o, val, ok, "P.row_base + r0 + 128 * (r >> 1) + (r & 1)", "r0 + 128 * (r >> 1) + (r & 1)");
+  o << "  }\n";
+  emit_flush(P, o);
+  o << "}\n";
+  *src = std::string(kDevHeader) + o.str();
+  return true;
+}
+
+// ---- radix-partitioned aggregation (group counts beyond the LDS table) ---------------------------------
+// When the expected groups do not fit a workgroup's LDS table, every row would otherwise update
+// the global table with device-scope atomics (~30 G atomics/s chip-wide: 2 % of the HBM roofline
+// at 64K+ groups). Instead the rows are partitioned by key hash so that each workgroup of the
+// aggregation pass sees a contiguous slice of records drawn from at most two buckets, whose groups
+// fit its LDS table:
+//   qe_pcount   per (bucket, workgroup) counts of the selected rows (reads predicate + key columns)
+//   (exclusive scan of the counts, bucket-major: records of one bucket are contiguous)
+//   qe_pscatter predicate, key, aggregate inputs -> one fixed-width record per selected row at
+//               its bucket's next position (LDS cursors)
+//   qe_pagg     LDS aggregation of a contiguous record slice, then the usual flush
+// Record layout (rec_layout): key | aggregate input values | [flags: bit 0 null key, bit 1+j input j
+// valid] | [global row index, fp64 MIN/MAX only], padded to 16 bytes.
+PartLayout part_layout(const Plan& P) {
+  PartLayout L{};
+  int w = 1;
+  bool nullable = false;
+  for (int k = 0; k < P.nkeys; ++k) nullable = nullable || P.cols[P.key_col[k]].valid != nullptr;
+  for (int j = 0; j < P.naggs; ++j) {
+    L.val_word[j] = -1;
+    if (P.aggs[j].pkind == 0) continue;
+    L.val_word[j] = w++;
+    nullable = nullable || P.aggs[j].track_nn;
+    L.row = L.row || acc_is_f64mm(P.aggs[j].acc);
+  }
+  L.flags_word = nullable ? w++ : -1;
+  L.row_word = L.row ? w++ : -1;
+  L.used = w;
+  L.words = (w + 1) & ~1;
+  return L;
+}
+
+bool gen_part_source(const Plan& P, int log2p, bool scatter, std::string* src) {
+  if (P.ncols < 1 || P.ncols > QE_MAX_COLS || log2p < 1 || log2p > 13) return false;
+  std::vector<Expr> ex;
+  if (!agg_inputs(P, &ex)) return false;
+  const PartLayout L = part_layout(P);
+  unsigned need = pred_key_cols(P);
+  if (scatter) need = ~0u;
+  std::ostringstream o;
+  o << "\nusing namespace qe;\n"
+    << "extern \"C\" __global__ void __launch_bounds__(512) " << (scatter ? "qe_pscatter" : "qe_pcount")
+    << "(const Plan P) {\n"
+    << "  constexpr int LOG2P = " << log2p << ", NP = 1 << LOG2P;\n";
+  if (scatter)
+    o << "  __shared__ qu64 s_cur[NP];\n"
+      << "  for (int b = threadIdx.x; b < NP; b += blockDim.x) s_cur[b] = (qu64)P.part_off[(qi64)b * gridDim.x + blockIdx.x];\n";
+  else
+    o << "  __shared__ qu32 s_cnt[NP];\n"
+      << "  for (int b = threadIdx.x; b < NP; b += blockDim.x) s_cnt[b] = 0;\n";
+  o << "  __syncthreads();\n"
+    << "  const int lane = threadIdx.x & 63;\n"
+    << "  const qi64 lo = (qi64)blockIdx.x * P.part_tw;\n"
+    << "  const qi64 hi = lo + P.part_tw < P.n ? lo + P.part_tw : P.n;\n"
+    << "  for (qi64 base = lo + (qi64)(threadIdx.x >> 6) * 256; base < hi; base += (qi64)(blockDim.x >> 6) * 256) {\n"
+    << "    const bool full = base + 256 <= P.n;\n"
+    << "    const qi64 r0 = base + 2 * lane;\n";
+  emit_col_loads(P, o, need);
+  emit_active_rows(P, o, false);
+  emit_keys(P, o);
+  o << "#pragma unroll\n    for (int r = 0; r < 4; ++r) {\n"
+    << "      if (!((act >> r) & 1)) continue;\n"
+    << "      const qu32 b = (qu32)(fmix64((qu64)key[r]) >> (64 - LOG2P));\n";
+  if (!scatter) {
+    o << "      atomicAdd(&s_cnt[b], 1u);\n    }\n  }\n  __syncthreads();\n"
+      << "  for (int b = threadIdx.x; b < NP; b += blockDim.x) P.part_off[(qi64)b * gridDim.x + blockIdx.x] = s_cnt[b];\n}\n";
+  } else {
+    o << "      const qu64 pos = atomicAdd(&s_cur[b], 1ull);\n"
+      << "      qi64 w[" << L.words << "];\n"
+      << "      w[0] = key[r];\n";
+    if (L.used < L.words) o << "      w[" << L.words - 1 << "] = 0;\n";
+    for (int j = 0; j < P.naggs; ++j)
+      if (L.val_word[j] >= 0) o << "      w[" << L.val_word[j] << "] = " << ex[j].v << ";\n";
+    if (L.flags_word >= 0) {
+      o << "      w[" << L.flags_word << "] = (qi64)((knull >> r) & 1)";
+      for (int j = 0; j < P.naggs; ++j)
+        if (L.val_word[j] >= 0) o << " | ((qi64)((" << ex[j].ok << ") & 1u) << " << (1 + j) << ")";
+      o << ";\n";
+    }
+    if (L.row_word >= 0) o << "      w[" << L.row_word << "] = P.row_base + r0 + 128 * (r >> 1) + (r & 1);\n";
+    o << "      qi64x2* dst = (qi64x2*)(P.part_rec + pos * " << 8 * L.words << "ull);\n";
+    for (int q = 0; q < L.words / 2; ++q)
+      o << "      dst[" << q << "] = qi64x2{w[" << 2 * q << "], w[" << 2 * q + 1 << "]};\n";
+    o << "    }\n  }\n}\n";
+  }
+  *src = std::string(kDevHeader) + o.str();
+  return true;
+}
+
+bool gen_pagg_source(const Plan& P, int log2, std::string* src, size_t* lds_bytes) {
+  if (log2 < 4 || log2 > 16) return false;
+  const PartLayout L = part_layout(P);
+  std::vector<std::string> val(P.naggs), ok(P.naggs);
+  for (int j = 0; j < P.naggs; ++j) {
+    val[j] = L.val_word[j] >= 0 ? "w" + std::to_string(L.val_word[j]) + "[r]" : "0";
+    ok[j] = (L.val_word[j] >= 0 && P.aggs[j].track_nn)
+                ? "((qu32)(w" + std::to_string(L.flags_word) + "[r] >> " + std::to_string(1 + j) + ") & 1u)"
+                : "1u";
+  }
+  std::ostringstream o;
+  o << "\nusing namespace qe;\n"
+    << "extern \"C\" __global__ void __launch_bounds__(512) qe_pagg(const Plan P) {\n";
+  o << "  __shared__ int s_fail;\n  if (threadIdx.x == 0) s_fail = 0;\n";
+  emit_lds_table(P, o, log2, lds_bytes);
+  o << "  const int lane = threadIdx.x & 63;\n"
+    << "  const qi64 lo = (qi64)blockIdx.x * P.part_tw;\n"
+    << "  const qi64 hi = lo + P.part_tw < P.n ? lo + P.part_tw : P.n;\n"
+    << "  for (qi64 base = lo + (qi64)(threadIdx.x >> 6) * 256; base < hi; base += (qi64)(blockDim.x >> 6) * 256) {\n"
+    << "    qu32 act = 0, knull = 0;\n    qi64 key[4];\n";
+  for (int q = 1; q < L.words; ++q) o << "    qi64 w" << q << "[4];\n";
+  o << "#pragma unroll\n    for (int r = 0; r < 4; ++r) {\n"
+    << "      const qi64 i = base + lane + 64 * r;\n"
+    << "      bool on = i < hi;\n"
+    << "      if (on && P.defer_in) on = (P.defer_in[i >> 5] >> (i & 31)) & 1;\n"
+    << "      act |= (qu32)on << r;\n"
+    << "      const qi64x2* p = (const qi64x2*)(P.part_rec + (on ? i : 0) * " << 8 * L.words << "ull);\n";
+  for (int q = 0; q < L.words / 2; ++q) {
+    o << "      { const qi64x2 v = " << ld("qi64x2", "p + " + std::to_string(q)) << "; ";
+    o << (q == 0 ? "key[r]" : "w" + std::to_string(2 * q) + "[r]") << " = v.x; w" << 2 * q + 1 << "[r] = v.y; }\n";
+  }
+  if (L.flags_word >= 0) o << "      knull |= (qu32)(w" << L.flags_word << "[r] & 1) << r;\n";
+  o << "    }\n    if (act == 0) continue;\n";
+  emit_agg_rows(P, o, val, ok, L.row_word >= 0 ? "w" + std::to_string(L.row_word) + "[r]" : "0",
+                "base + lane + 64 * r");
+  o << "  }\n";
+  emit_flush(P, o, true);
+  // groups that found no room anywhere: defer their records (the LDS table is final, so a key is
+  // in it exactly when its records were aggregated there rather than on the global path)
+  o << "  __syncthreads();\n"
+    << "  if (s_fail) {\n"
+    << "    for (qi64 i = lo + threadIdx.x; i < hi; i += blockDim.x) {\n"
+    << "      if (P.defer_in && !((P.defer_in[i >> 5] >> (i & 31)) & 1)) continue;\n"
+    << "      const qi64* rp = (const qi64*)(P.part_rec + i * " << 8 * L.words << "ull);\n"
+    << "      const qi64 k = rp[0];\n";
+  if (L.flags_word >= 0)
+    o << "      const bool kn = rp[" << L.flags_word << "] & 1;\n";
+  else
+    o << "      const bool kn = false;\n";
+  o << "      int s = kn ? S : (k == EMPTY_KEY ? S + 1 : -1);\n"
+    << "      if (s < 0) { const qu32 hh = lds_hash((qu64)k) >> (32 - LOG2); s = s_keys[hh] == k ? (int)hh : lds_probe(s_keys, LOG2, k, hh); }\n"
+    << "      if (s >= 0 && (s_cst[s] & 0x80000000u)) {\n"
+    << "        atomicOr((qu32*)&P.defer_out[i >> 5], 1u << (i & 31));\n"
+    << "        atomicAdd(&P.t.ctl[1], 1ull);\n      }\n    }\n  }\n";
+  o << "}\n";
   *src = std::string(kDevHeader) + o.str();
   return true;
 }

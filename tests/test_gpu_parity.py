@@ -584,6 +584,65 @@ def test_hashagg_growth_from_tiny_table(agg_ctx):
     assert_groups_equal(result_dict(kk, aa), ref, [N.AGG_SUM, N.AGG_COUNT_STAR])
 
 
+def check_partitioned(ctx, st):
+    spec, note = st.last_kernel_kind()
+    if getattr(ctx, "kernel_mode", "jit") == "jit":
+        assert spec and note.startswith("radix-partitioned"), note
+
+
+@pytest.mark.parametrize("ngroups,expected", [(50_000, 50_000), (600_000, 20_000), (3, 100_000)])
+@pytest.mark.parametrize("vtype", ["i64", "f64"])
+def test_hashagg_partitioned(agg_ctx, ngroups, expected, vtype):
+    """Expected groups beyond the LDS table: rows are radix-partitioned by key hash and each
+    workgroup aggregates a record slice in LDS. Nullable keys and inputs, the EMPTY sentinel as a
+    key, fp64 MIN/MAX order ties across two batches, and far more groups than expected (records of
+    groups that find no room are retried)."""
+    rng = np.random.default_rng(ngroups + expected)
+    n = 1_000_000
+    k = rng.integers(0, ngroups, n).astype(np.int64) * 7919 - 3
+    kv = rng.random(n) > 0.01
+    k[rng.random(n) < 0.001] = -2**63
+    if vtype == "i64":
+        x = rng.integers(-2**62, 2**62, n).astype(np.int64)
+        xv = rng.random(n) > 0.1
+        t = N.TYPE_INT64
+    else:
+        x, xv = _rand(rng, n, "f64", 0.1)
+        t = N.TYPE_FLOAT64
+    st = HashAggregateState(agg_ctx, [N.TYPE_INT64], [(f, t) for f in ALL_FNS], expected)
+    half = 400_001
+    for s, e in ((0, half), (half, n)):
+        st.update([dcol(agg_ctx, N.TYPE_INT64, k[s:e], kv[s:e])], [dcol(agg_ctx, t, x[s:e], xv[s:e])] * len(ALL_FNS))
+        check_partitioned(agg_ctx, st)
+    keys, aggs = st.finalize()
+    ref = S.group_aggregate([k], [kv], [x] * 6, [xv] * 6, ALL_FNS)
+    assert_groups_equal(result_dict(keys, aggs), ref, ALL_FNS)
+
+
+@pytest.mark.parametrize("groups,threshold", [(100_000, 1 << 19), (1 << 20, 1 << 19), (100_000, 1 << 21)])
+def test_fused_c4_partitioned_vs_oracle(agg_ctx, groups, threshold):
+    """C4 query shape with k = u mod G for large G (partitioned fused path), including a predicate
+    no row passes (zero records, zero groups)."""
+    from kquery.datasource import C4_COLUMNS, ColumnSpec, generate_column
+
+    n, row0 = 3_000_001, 7
+    kspec = ColumnSpec("k", N.TYPE_INT64, N.GEN_MOD, groups, 0)
+    cols = [generate_column(kspec, n, row0, 42, agg_ctx)] + [generate_column(s, n, row0, 42, agg_ctx)
+                                                              for s in C4_COLUMNS[1:]]
+    st = HashAggregateState(agg_ctx, [N.TYPE_INT64], C4_AGGS, groups)
+    st.update_fused(cols, _c4_spec(threshold))
+    check_partitioned(agg_ctx, st)
+    kk, aa = st.finalize()
+    k, _ = gen.generate(gen.GEN_MOD, groups, 42, 0, row0, n)
+    a, _ = gen.generate(gen.GEN_MOD, 1 << 20, 42, 1, row0, n)
+    b, _ = gen.generate(gen.GEN_MOD, 1 << 20, 42, 2, row0, n)
+    ref = S.group_aggregate([k], [None], [S.arith(S.OP_ADD, a, None, b, None)[0], None, a, b], [None] * 4, C4_FNS,
+                            a > threshold)
+    assert_groups_equal(result_dict(kk, aa), ref, C4_FNS)
+    if threshold >= 1 << 20:
+        assert kk[0].length == 0
+
+
 @pytest.mark.slow
 def test_c4_full_size_properties(gpu_ctx):
     """BASELINE config 4 at full size (1B rows, one GPU): size-independent properties.
