@@ -42,6 +42,7 @@ typedef long long qi64x2 __attribute__((ext_vector_type(2)));
 typedef int qi32x2 __attribute__((ext_vector_type(2)));
 
 constexpr qi64 EMPTY_KEY = (qi64)0x8000000000000000ull;  // LDS/global slot sentinel (INT64_MIN)
+constexpr qi64 PART_EXCL = 1ll << 62;  // partition-aggregate slice flag: the slice holds its whole bucket
 constexpr qu64 NULL_SALT = 0x6A09E667F3BCC909ull;
 constexpr int HA_LDS_MAXP = 32;      // probe limit in the LDS table
 constexpr int HA_GLOBAL_MAXP = 256;  // probe limit in the global table
@@ -120,7 +121,8 @@ struct Plan {
   // radix-partitioned aggregation (high group counts, qe_jit.hip gen_part_source / gen_pagg_source)
   qu8* part_rec;   // records grouped by key-hash bucket (scatter output, partition-aggregate input)
   qi64* part_off;  // count: per (bucket, workgroup) record counts; scatter: their exclusive scan
-  qi64 part_tw;    // rows (count / scatter) or records (partition aggregate) per workgroup
+  qi64 part_tw;    // rows per workgroup (count / scatter)
+  qi64* part_slice;  // partition aggregate: [0] slice count, then (lo, hi | PART_EXCL) per slice
 };
 
 // ---- scalar helpers ---------------------------------------------------------------------------------
@@ -208,6 +210,39 @@ __device__ inline bool gtable_find(const DTable& t, qi64 key, bool knull, qu64& 
   return false;
 }
 
+// gtable_find for a workgroup flush: a new group is counted in the workgroup's LDS counter
+// `newg` (added to ctl[0] once per workgroup) instead of one device-scope add per group on the
+// same word. `*inserted` reports whether this call created the group.
+__device__ inline bool gtable_find_wg(const DTable& t, qi64 key, bool knull, qu64& slot, qu32* newg) {
+  if (knull || key == EMPTY_KEY) {
+    slot = knull ? t.cap : t.cap + 1;
+    return true;
+  }
+  qu64 h = fmix64((qu64)key) & (t.cap - 1);
+#pragma unroll 1
+  for (int p = 0; p < HA_GLOBAL_MAXP; ++p) {
+    const qi64 k = __hip_atomic_load(&t.keys[h], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (k == key) {
+      slot = h;
+      return true;
+    }
+    if (k == EMPTY_KEY) {
+      const qi64 old = (qi64)atomicCAS((qu64*)&t.keys[h], (qu64)EMPTY_KEY, (qu64)key);
+      if (old == EMPTY_KEY) {
+        atomicAdd(newg, 1u);
+        slot = h;
+        return true;
+      }
+      if (old == key) {
+        slot = h;
+        return true;
+      }
+    }
+    h = (h + 1) & (t.cap - 1);
+  }
+  return false;
+}
+
 __device__ inline void gadd_cstar(const DTable& t, qu64 slot, qu64 c) {
   const qu64 old = atomicAdd(&t.cstar[slot], c);
   if (slot >= t.cap && old == 0) atomicAdd(&t.ctl[0], 1ull);  // a special group appears
@@ -240,6 +275,44 @@ __device__ inline void gcombine(const DTable& t, int acck, int j, qu64 s, qi64 a
     if (i1 != ~0ull) atomicMin(&ix[stride + s], i1);
     if (i2 != ~0ull) atomicMin(&ix[2 * stride + s], i2);
     if (i3 != ~0ull) atomicMin(&ix[3 * stride + s], i3);
+  }
+}
+
+// Exclusive forms of gadd_cstar / gcombine: the caller is the only writer of slot `s` during this
+// launch (a radix-partitioned slice holding its bucket's every record), so plain read-modify-writes
+// replace the device-scope atomics. The table was last written by earlier launches (or not at
+// all), whose writes the launch boundary makes visible; same results as the atomic forms.
+__device__ inline void gadd_cstar_excl(const DTable& t, qu64 slot, qu64 c, qu32* newg) {
+  const qu64 old = t.cstar[slot];
+  t.cstar[slot] = old + c;
+  if (slot >= t.cap && old == 0) atomicAdd(newg, 1u);
+}
+
+__device__ inline void gcombine_excl(const DTable& t, int acck, int j, qu64 s, qi64 acc, qu64 nn, qu64 i0,
+                                     qu64 i1, qu64 i2, qu64 i3) {
+  if (nn == 0) return;
+  t.nn[j][s] += nn;
+  qi64* a = &t.acc[j][s];
+  switch (acck) {
+    case ACC_SUM_I: *a = (qi64)((qu64)*a + (qu64)acc); break;
+    case ACC_SUM_F: *a = f64_bits(bits_f64(*a) + bits_f64(acc)); break;
+    case ACC_MIN_I:
+    case ACC_MIN_F:
+      if (acc < *a) *a = acc;
+      break;
+    case ACC_MAX_I:
+    case ACC_MAX_F:
+      if (acc > *a) *a = acc;
+      break;
+    default: break;
+  }
+  if (acc_is_f64mm(acck)) {
+    const qu64 stride = t.cap + 2;
+    qu64* ix = t.idx[j] + s;
+    if (i0 < ix[0]) ix[0] = i0;
+    if (i1 < ix[stride]) ix[stride] = i1;
+    if (i2 < ix[2 * stride]) ix[2 * stride] = i2;
+    if (i3 < ix[3 * stride]) ix[3 * stride] = i3;
   }
 }
 

@@ -722,6 +722,43 @@ struct AggMeta {
   qi32 acc[QE_MAX_AGGS];
 };
 
+// Slice descriptors of the partition-aggregate pass (one workgroup). Bucket b's records are
+// [off[b * g], off[(b + 1) * g]) (bucket-major exclusive scan of the (bucket, workgroup) counts,
+// off[np * g] = total); a bucket of n records gets ceil(n / cw) slices, and a bucket that is one
+// slice is flagged PART_EXCL: its workgroup is the only one to touch its groups. out[0] = slices.
+__global__ void __launch_bounds__(1024) k_part_slices(const qi64* __restrict__ off, qi32 np, qi64 g, qi64 cw,
+                                                      qi64* __restrict__ out) {
+  __shared__ qi64 s_sum[1024];
+  const int per = (np + 1023) / 1024;
+  const int b0 = threadIdx.x * per;
+  qi64 cnt = 0;
+  for (int i = 0; i < per; ++i) {
+    const int b = b0 + i;
+    if (b < np) cnt += (off[(qi64)(b + 1) * g] - off[(qi64)b * g] + cw - 1) / cw;
+  }
+  s_sum[threadIdx.x] = cnt;
+  __syncthreads();
+  for (int d = 1; d < 1024; d <<= 1) {
+    const qi64 v = (int)threadIdx.x >= d ? s_sum[threadIdx.x - d] : 0;
+    __syncthreads();
+    s_sum[threadIdx.x] += v;
+    __syncthreads();
+  }
+  qi64 pos = s_sum[threadIdx.x] - cnt;
+  for (int i = 0; i < per; ++i) {
+    const int b = b0 + i;
+    if (b >= np) break;
+    const qi64 s = off[(qi64)b * g], e = off[(qi64)(b + 1) * g];
+    const qi64 ns = (e - s + cw - 1) / cw;
+    for (qi64 k = 0; k < ns; ++k, ++pos) {
+      const qi64 lo = s + k * cw;
+      out[2 + 2 * pos] = lo;
+      out[3 + 2 * pos] = (lo + cw < e ? lo + cw : e) | (ns == 1 ? PART_EXCL : 0);
+    }
+  }
+  if (threadIdx.x == 1023) out[0] = s_sum[1023];
+}
+
 __global__ void k_table_init(DTable t, AggMeta m) {
   const qu64 SS = t.cap + 2;
   for (qu64 s = blockIdx.x * (qu64)blockDim.x + threadIdx.x; s < SS; s += (qu64)gridDim.x * blockDim.x) {
@@ -1129,6 +1166,8 @@ struct qe_hashagg {
   size_t part_cnt_bytes = 0;
   uint8_t* part_rec = nullptr;
   size_t part_rec_bytes = 0;
+  int64_t* part_slc = nullptr;  // slice descriptors of the partition-aggregate pass
+  size_t part_slc_bytes = 0;
   // overflow records
   uint8_t* ovf = nullptr;
   uint64_t ovf_cap = 0;
@@ -1542,16 +1581,18 @@ static int partition_rows(qe_hashagg* h, Plan& P, hipFunction_t* fn, int* grid) 
   while (log2p < 13 && (((int64_t)1 << tlog2) >> 2) * ((int64_t)1 << log2p) < h->expected_groups) ++log2p;
   std::string sc, ss, sa;
   size_t jl = 0;
-  QE_CHECK(gen_part_source(P, log2p, false, &sc) && gen_part_source(P, log2p, true, &ss) &&
+  const bool staged = part_staged_ok(P, log2p);
+  QE_CHECK(gen_part_source(P, log2p, false, &sc) &&
+               (staged ? gen_pscatter_staged_source(P, log2p, &ss) : gen_part_source(P, log2p, true, &ss)) &&
                gen_pagg_source(P, tlog2, &sa, &jl),
            QE_ERR_UNSUPPORTED, "plan shape not specialisable");
   hipFunction_t fc, fs;
   int bpc = 0;
   QE_TRY(jit_kernel(ctx, sc, &fc, &bpc, "qe_pcount"));
-  QE_TRY(jit_kernel(ctx, ss, &fs, &bpc, "qe_pscatter"));
+  QE_TRY(jit_kernel(ctx, ss, &fs, &bpc, "qe_pscatter", staged ? 256 : 512));
   QE_TRY(jit_kernel(ctx, sa, fn, &bpc, "qe_pagg"));
   const int64_t n = P.n;
-  int64_t g = std::min<int64_t>((int64_t)ctx->num_cus * 2, (int64_t)div_up((uint64_t)n, 256));
+  int64_t g = std::min<int64_t>((int64_t)ctx->num_cus * 4, (int64_t)div_up((uint64_t)n, 256));
   const int64_t tw = (int64_t)div_up(div_up((uint64_t)n, (uint64_t)g), 256) * 256;
   g = (int64_t)div_up((uint64_t)n, (uint64_t)tw);
   const size_t cells = ((size_t)1 << log2p) * (size_t)g;
@@ -1585,16 +1626,27 @@ static int partition_rows(qe_hashagg* h, Plan& P, hipFunction_t* fn, int* grid) 
     QE_TRY(grow_buffer(&h->part_rec, &h->part_rec_bytes, (size_t)R * rb, ctx->stream, "partition records"));
     P.part_off = (qi64*)off;
     P.part_rec = h->part_rec;
-    QE_TRY(jit_launch(ctx, fs, (int)g, P));
+    QE_TRY(jit_launch(ctx, fs, (int)g, P, staged ? 256 : 512));
     QE_TRY(launch_check("qe_pscatter"));
   }
-  // aggregation slices of about one bucket's records each
-  const int64_t cw = std::max<int64_t>(256, (int64_t)div_up(div_up((uint64_t)std::max<int64_t>(R, 1), (uint64_t)1 << log2p), 256) * 256);
+  // aggregation slices inside bucket boundaries: one per bucket, or more (up to 8 per CU, none
+  // below ~32K records) when there are few buckets; cw is 5/4 of the even share, so a bucket of
+  // about average size is one slice, whose workgroup then owns its groups outright (plain
+  // combines, k_part_slices)
+  const int64_t target = std::max<int64_t>((int64_t)1 << log2p, std::min<int64_t>((int64_t)ctx->num_cus * 8, R >> 15));
+  const int64_t cw = std::max<int64_t>(256, (int64_t)div_up((uint64_t)std::max<int64_t>(R, 1) * 5, (uint64_t)target * 4));
+  const int64_t max_slices = ((int64_t)1 << log2p) + (int64_t)div_up((uint64_t)std::max<int64_t>(R, 1), (uint64_t)cw);
+  QE_TRY(grow_buffer(&h->part_slc, &h->part_slc_bytes, (size_t)(2 + 2 * max_slices) * 8, ctx->stream, "partition slices"));
+  hipLaunchKernelGGL(k_part_slices, dim3(1), dim3(1024), 0, ctx->stream, (const qi64*)off, (qi32)(1 << log2p), (qi64)g,
+                     (qi64)cw, (qi64*)h->part_slc);
+  QE_TRY(launch_check("k_part_slices"));
   P.n = R;
   P.part_tw = cw;
   P.part_rec = h->part_rec;
-  *grid = (int)div_up((uint64_t)std::max<int64_t>(R, 1), (uint64_t)cw);
-  h->jit_note = "radix-partitioned: " + std::to_string(1 << log2p) + " buckets, " + std::to_string(R) + " records";
+  P.part_slice = (qi64*)h->part_slc;
+  *grid = (int)max_slices;
+  h->jit_note = "radix-partitioned: " + std::to_string(1 << log2p) + " buckets, " + std::to_string(R) + " records" +
+                (staged ? ", staged scatter" : "");
   return QE_OK;
 }
 
@@ -1837,6 +1889,7 @@ int qe_hashagg_destroy(qe_hashagg* h) {
   if (h->ovf) (void)hipFree(h->ovf);
   if (h->part_cnt) (void)hipFree(h->part_cnt);
   if (h->part_rec) (void)hipFree(h->part_rec);
+  if (h->part_slc) (void)hipFree(h->part_slc);
   for (int i = 0; i < 2; ++i) {
     if (h->defer[i]) (void)hipFree(h->defer[i]);
     if (h->ev[i]) (void)hipEventDestroy(h->ev[i]);

@@ -338,13 +338,21 @@ void emit_agg_rows(const Plan& P, std::ostringstream& o, const std::vector<std::
 // Merge the workgroup's LDS table into the global table (or the overflow records). With
 // `mark_full`, a group that finds neither a global slot nor overflow space is flagged in s_cst
 // (bit 31) and s_fail is set: the caller then defers that group's records for a retry pass.
-void emit_flush(const Plan& P, std::ostringstream& o, bool mark_full = false) {
+//
+// `part` (partition aggregate): new groups are counted in the LDS word s_newg, and when the runtime
+// flag `excl` says this workgroup holds every record of its groups, the combines are plain
+// read-modify-writes (gadd_cstar_excl / gcombine_excl).
+void emit_flush(const Plan& P, std::ostringstream& o, bool mark_full = false, bool part = false) {
   o << "  __syncthreads();\n"
     << "  for (int s = threadIdx.x; s < SS; s += blockDim.x) {\n"
     << "    const qu32 c = s_cst[s];\n    if (c == 0) continue;\n"
     << "    const bool knl = s == S;\n    const qi64 key = knl ? 0 : (s == S + 1 ? EMPTY_KEY : s_keys[s]);\n"
-    << "    qu64 gs;\n    const bool ok = gtable_find(P.t, key, knl, gs);\n    qu8* rec = nullptr;\n"
-    << "    if (ok) {\n      gadd_cstar(P.t, gs, c);\n    } else {\n"
+    << "    qu64 gs;\n"
+    << (part ? "    const bool ok = gtable_find_wg(P.t, key, knl, gs, &s_newg);\n"
+             : "    const bool ok = gtable_find(P.t, key, knl, gs);\n")
+    << "    qu8* rec = nullptr;\n"
+    << (part ? "    if (ok) {\n      if (excl) gadd_cstar_excl(P.t, gs, c, &s_newg); else gadd_cstar(P.t, gs, c);\n    } else {\n"
+             : "    if (ok) {\n      gadd_cstar(P.t, gs, c);\n    } else {\n")
     << "      const qu64 ri = atomicAdd(&P.t.ctl[2], 1ull);\n";
   if (mark_full)
     o << "      if (ri >= P.ovf_cap) { s_cst[s] = c | 0x80000000u; s_fail = 1; continue; }\n";
@@ -362,7 +370,10 @@ void emit_flush(const Plan& P, std::ostringstream& o, bool mark_full = false) {
         << "[2 * SS + s], i3 = s_idx" << js << "[3 * SS + s];\n";
     else
       o << "      const qu64 i0 = ~0ull, i1 = ~0ull, i2 = ~0ull, i3 = ~0ull;\n";
-    if (a.fn != QE_AGG_COUNT_STAR)
+    if (a.fn != QE_AGG_COUNT_STAR && part)
+      o << "      if (ok) { if (excl) gcombine_excl(P.t, " << a.acc << ", " << j << ", gs, acc, nn, i0, i1, i2, i3);"
+        << " else gcombine(P.t, " << a.acc << ", " << j << ", gs, acc, nn, i0, i1, i2, i3); }\n";
+    else if (a.fn != QE_AGG_COUNT_STAR)
       o << "      if (ok) gcombine(P.t, " << a.acc << ", " << j << ", gs, acc, nn, i0, i1, i2, i3);\n";
     o << "      if (!ok) { qu64* f = (qu64*)(rec + " << off << "); f[0] = (qu64)acc; f[1] = nn;";
     if (acc_is_f64mm(a.acc)) o << " f[2] = i0; f[3] = i1; f[4] = i2; f[5] = i3;";
@@ -503,6 +514,119 @@ bool gen_part_source(const Plan& P, int log2p, bool scatter, std::string* src) {
   return true;
 }
 
+// Staged scatter (few buckets): a 256-thread workgroup takes 1024-row tiles; the tile's records
+// are counting-sorted by bucket in LDS (rank = LDS atomic on the tile histogram, one wave scans
+// it), then written out as contiguous per-bucket runs, 16 bytes per lane in record-stream order,
+// so the HBM writes coalesce instead of landing as one 2-word record per lane. Rows go to the same
+// (bucket, workgroup) ranges as the direct scatter: the records of one bucket and workgroup keep
+// a contiguous range of its bucket (their order inside it may differ run to run).
+bool part_staged_ok(const Plan& P, int log2p) {
+  return log2p <= 9 && part_layout(P).words <= 8;
+}
+
+bool gen_pscatter_staged_source(const Plan& P, int log2p, std::string* src) {
+  if (P.ncols < 1 || P.ncols > QE_MAX_COLS || log2p < 1 || !part_staged_ok(P, log2p)) return false;
+  std::vector<Expr> ex;
+  if (!agg_inputs(P, &ex)) return false;
+  const PartLayout L = part_layout(P);
+  const int W = L.words;
+  std::ostringstream o;
+  o << "\nusing namespace qe;\n"
+    << "extern \"C\" __global__ void __launch_bounds__(256) qe_pscatter(const Plan P) {\n"
+    << "  constexpr int LOG2P = " << log2p << ", NP = 1 << LOG2P, W = " << W << ", T = 1024;\n"
+    << "  __shared__ qu32 s_hist[NP];\n  __shared__ qu32 s_off[NP];\n  __shared__ qu64 s_cur[NP];\n"
+    << "  __shared__ qi64x2 s_rec[T * W / 2];\n  __shared__ unsigned short s_bkt[T];\n  __shared__ qu32 s_total;\n"
+    << "  for (int b = threadIdx.x; b < NP; b += blockDim.x) s_cur[b] = (qu64)P.part_off[(qi64)b * gridDim.x + blockIdx.x];\n"
+    << "  const int lane = threadIdx.x & 63;\n"
+    << "  const qi64 lo = (qi64)blockIdx.x * P.part_tw;\n"
+    << "  const qi64 hi = lo + P.part_tw < P.n ? lo + P.part_tw : P.n;\n"
+    << "  const qi64 woff = (qi64)(threadIdx.x >> 6) * 256;\n";
+  // register prefetch: the column loads of the next tile are issued before this tile's sort and
+  // write-out (barriers do not wait for plain loads), so HBM latency overlaps the LDS phases
+  std::ostringstream pf, cp;
+  for (int c = 0; c < P.ncols; ++c) {
+    const std::string cs = std::to_string(c);
+    o << "  qi64 n" << cs << "[4] = {0, 0, 0, 0};\n";
+    pf << "      n" << cs << "[0] = c" << cs << "[0]; n" << cs << "[1] = c" << cs << "[1]; n" << cs << "[2] = c" << cs
+       << "[2]; n" << cs << "[3] = c" << cs << "[3];\n";
+    cp << "    qi64 c" << cs << "[4] = {n" << cs << "[0], n" << cs << "[1], n" << cs << "[2], n" << cs << "[3]};\n";
+    if (P.cols[c].valid) {
+      o << "  qu32 nv" << cs << " = 0;\n";
+      pf << "      nv" << cs << " = v" << cs << ";\n";
+      cp << "    const qu32 v" << cs << " = nv" << cs << ";\n";
+    }
+  }
+  auto prefetch = [&](const std::string& nb) {
+    o << "    {\n      const qi64 base = " << nb << ";\n"
+      << "      if (base < hi) {\n      const bool full = base + 256 <= P.n;\n      const qi64 r0 = base + 2 * lane;\n";
+    emit_col_loads(P, o, ~0u);
+    o << pf.str() << "      }\n    }\n";
+  };
+  prefetch("lo + woff");
+  o << "  for (qi64 tile = lo; tile < hi; tile += T) {\n"
+    << "    for (int b = threadIdx.x; b < NP; b += blockDim.x) s_hist[b] = 0;\n"
+    << "    qu32 ract = 0, bk[4], rk[4];\n    qi64 rw[4][W];\n"
+    << "    const qi64 base = tile + woff;\n";
+  o << cp.str();
+  prefetch("tile + T + woff");
+  o << "    __syncthreads();\n"
+    << "    if (base < hi) do {\n"
+    << "    const bool full = base + 256 <= P.n;\n"
+    << "    const qi64 r0 = base + 2 * lane;\n";
+  emit_active_rows(P, o, false);
+  emit_keys(P, o);
+  o << "    ract = act;\n"
+    << "#pragma unroll\n    for (int r = 0; r < 4; ++r) {\n"
+    << "      if (!((act >> r) & 1)) continue;\n"
+    << "      bk[r] = (qu32)(fmix64((qu64)key[r]) >> (64 - LOG2P));\n"
+    << "      rk[r] = atomicAdd(&s_hist[bk[r]], 1u);\n"
+    << "      rw[r][0] = key[r];\n";
+  if (L.used < L.words) o << "      rw[r][" << W - 1 << "] = 0;\n";
+  for (int j = 0; j < P.naggs; ++j)
+    if (L.val_word[j] >= 0) o << "      rw[r][" << L.val_word[j] << "] = " << ex[j].v << ";\n";
+  if (L.flags_word >= 0) {
+    o << "      rw[r][" << L.flags_word << "] = (qi64)((knull >> r) & 1)";
+    for (int j = 0; j < P.naggs; ++j)
+      if (L.val_word[j] >= 0) o << " | ((qi64)((" << ex[j].ok << ") & 1u) << " << (1 + j) << ")";
+    o << ";\n";
+  }
+  if (L.row_word >= 0) o << "      rw[r][" << L.row_word << "] = P.row_base + r0 + 128 * (r >> 1) + (r & 1);\n";
+  o << "    }\n    } while (0);\n"
+    << "    __syncthreads();\n"
+    // exclusive scan of the tile histogram by wave 0
+    << "    if (threadIdx.x < 64) {\n"
+    << "      constexpr int PER = (NP + 63) / 64;\n"
+    << "      qu32 loc[PER], s = 0;\n"
+    << "#pragma unroll\n      for (int i = 0; i < PER; ++i) { const int b = lane * PER + i; loc[i] = b < NP ? s_hist[b] : 0u; s += loc[i]; }\n"
+    << "      qu32 x = s;\n"
+    << "#pragma unroll\n      for (int d = 1; d < 64; d <<= 1) { const qu32 y = __shfl_up(x, d); if (lane >= d) x += y; }\n"
+    << "      qu32 e = x - s;\n"
+    << "#pragma unroll\n      for (int i = 0; i < PER; ++i) { const int b = lane * PER + i; if (b < NP) s_off[b] = e; e += loc[i]; }\n"
+    << "      if (lane == 63) s_total = x;\n"
+    << "    }\n"
+    << "    __syncthreads();\n"
+    << "#pragma unroll\n    for (int r = 0; r < 4; ++r) {\n"
+    << "      if (!((ract >> r) & 1)) continue;\n"
+    << "      const qu32 pos = s_off[bk[r]] + rk[r];\n"
+    << "      s_bkt[pos] = (unsigned short)bk[r];\n"
+    << "#pragma unroll\n      for (int q = 0; q < W / 2; ++q) s_rec[pos * (W / 2) + q] = qi64x2{rw[r][2 * q], rw[r][2 * q + 1]};\n"
+    << "    }\n"
+    << "    __syncthreads();\n"
+    << "    const qu32 tot = s_total;\n"
+    << "    for (qu32 c = threadIdx.x; c < tot * (W / 2); c += blockDim.x) {\n"
+    << "      const qu32 j = c / (W / 2), q = c % (W / 2);\n"
+    << "      const qu32 b = s_bkt[j];\n"
+    << "      const qu64 dst = s_cur[b] + (j - s_off[b]);\n"
+    << "      ((qi64x2*)(P.part_rec + dst * " << 8 * W << "ull))[q] = s_rec[c];\n"
+    << "    }\n"
+    << "    __syncthreads();\n"
+    << "    for (int b = threadIdx.x; b < NP; b += blockDim.x) s_cur[b] += s_hist[b];\n"
+    << "    __syncthreads();\n"
+    << "  }\n}\n";
+  *src = std::string(kDevHeader) + o.str();
+  return true;
+}
+
 bool gen_pagg_source(const Plan& P, int log2, std::string* src, size_t* lds_bytes) {
   if (log2 < 4 || log2 > 16) return false;
   const PartLayout L = part_layout(P);
@@ -515,12 +639,15 @@ bool gen_pagg_source(const Plan& P, int log2, std::string* src, size_t* lds_byte
   }
   std::ostringstream o;
   o << "\nusing namespace qe;\n"
-    << "extern \"C\" __global__ void __launch_bounds__(512) qe_pagg(const Plan P) {\n";
-  o << "  __shared__ int s_fail;\n  if (threadIdx.x == 0) s_fail = 0;\n";
+    << "extern \"C\" __global__ void __launch_bounds__(512) qe_pagg(const Plan P) {\n"
+    << "  if ((qi64)blockIdx.x >= P.part_slice[0]) return;\n"
+    << "  const qi64 lo = P.part_slice[2 + 2 * (qi64)blockIdx.x];\n"
+    << "  const qi64 hx = P.part_slice[3 + 2 * (qi64)blockIdx.x];\n"
+    << "  const bool excl = (hx & PART_EXCL) != 0;\n"
+    << "  const qi64 hi = hx & ~PART_EXCL;\n";
+  o << "  __shared__ int s_fail;\n  __shared__ qu32 s_newg;\n  if (threadIdx.x == 0) { s_fail = 0; s_newg = 0; }\n";
   emit_lds_table(P, o, log2, lds_bytes);
   o << "  const int lane = threadIdx.x & 63;\n"
-    << "  const qi64 lo = (qi64)blockIdx.x * P.part_tw;\n"
-    << "  const qi64 hi = lo + P.part_tw < P.n ? lo + P.part_tw : P.n;\n"
     << "  for (qi64 base = lo + (qi64)(threadIdx.x >> 6) * 256; base < hi; base += (qi64)(blockDim.x >> 6) * 256) {\n"
     << "    qu32 act = 0, knull = 0;\n    qi64 key[4];\n";
   for (int q = 1; q < L.words; ++q) o << "    qi64 w" << q << "[4];\n";
@@ -539,7 +666,7 @@ bool gen_pagg_source(const Plan& P, int log2, std::string* src, size_t* lds_byte
   emit_agg_rows(P, o, val, ok, L.row_word >= 0 ? "w" + std::to_string(L.row_word) + "[r]" : "0",
                 "base + lane + 64 * r");
   o << "  }\n";
-  emit_flush(P, o, true);
+  emit_flush(P, o, true, true);
   // groups that found no room anywhere: defer their records (the LDS table is final, so a key is
   // in it exactly when its records were aggregated there rather than on the global path)
   o << "  __syncthreads();\n"
@@ -556,7 +683,8 @@ bool gen_pagg_source(const Plan& P, int log2, std::string* src, size_t* lds_byte
     << "      if (s < 0) { const qu32 hh = lds_hash((qu64)k) >> (32 - LOG2); s = s_keys[hh] == k ? (int)hh : lds_probe(s_keys, LOG2, k, hh); }\n"
     << "      if (s >= 0 && (s_cst[s] & 0x80000000u)) {\n"
     << "        atomicOr((qu32*)&P.defer_out[i >> 5], 1u << (i & 31));\n"
-    << "        atomicAdd(&P.t.ctl[1], 1ull);\n      }\n    }\n  }\n";
+    << "        atomicAdd(&P.t.ctl[1], 1ull);\n      }\n    }\n  }\n"
+    << "  if (threadIdx.x == 0 && s_newg) atomicAdd(&P.t.ctl[0], (qu64)s_newg);\n";
   o << "}\n";
   *src = std::string(kDevHeader) + o.str();
   return true;
