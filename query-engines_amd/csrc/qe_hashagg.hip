@@ -1765,6 +1765,13 @@ static int run_update(qe_hashagg* h, Plan& P) {
     out_i ^= 1;
   }
   h->row_base += rows;
+  // Adaptive: once the groups seen exceed this launch's LDS table, most rows of later batches
+  // would take the global-table path; they go through the radix-partitioned update instead,
+  // sized for the groups seen so far.
+  if (h->known_groups > 0 && ctx->jit) {
+    if (lds && h->known_groups * 5 / 4 > ((int64_t)1 << P.lds_log2)) h->lds_log2 = 0;
+    if (h->lds_log2 == 0) h->expected_groups = std::max<int64_t>(h->expected_groups, h->known_groups);
+  }
   return QE_OK;
 }
 

@@ -619,6 +619,27 @@ def test_hashagg_partitioned(agg_ctx, ngroups, expected, vtype):
     assert_groups_equal(result_dict(keys, aggs), ref, ALL_FNS)
 
 
+def test_hashagg_adapts_to_partitioned(agg_ctx):
+    """expected_groups left at its default while the batches hold 300K groups: the first batch
+    grows the global table, and the later batches switch to the partitioned update by themselves."""
+    rng = np.random.default_rng(23)
+    n, nb = 1_500_000, 3
+    k = rng.integers(0, 300_000, n).astype(np.int64) * 31 + 5
+    x = rng.integers(-1000, 1000, n).astype(np.int64)
+    fns = [N.AGG_SUM, N.AGG_COUNT_STAR, N.AGG_MIN, N.AGG_MAX]
+    st = HashAggregateState(agg_ctx, [N.TYPE_INT64], [(f, N.TYPE_INT64) for f in fns])
+    notes = []
+    for s in range(0, n, n // nb):
+        st.update([dcol(agg_ctx, N.TYPE_INT64, k[s:s + n // nb])], [dcol(agg_ctx, N.TYPE_INT64, x[s:s + n // nb])] * 4)
+        notes.append(st.last_kernel_kind()[1])
+    if agg_ctx.kernel_mode == "jit":
+        assert not notes[0].startswith("radix-partitioned"), notes
+        assert all(m.startswith("radix-partitioned") for m in notes[1:]), notes
+    kk, aa = st.finalize()
+    ref = S.group_aggregate([k], [None], [x] * 4, [None] * 4, fns)
+    assert_groups_equal(result_dict(kk, aa), ref, fns)
+
+
 @pytest.mark.parametrize("groups,threshold", [(100_000, 1 << 19), (1 << 20, 1 << 19), (100_000, 1 << 21)])
 def test_fused_c4_partitioned_vs_oracle(agg_ctx, groups, threshold):
     """C4 query shape with k = u mod G for large G (partitioned fused path), including a predicate
