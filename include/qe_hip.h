@@ -109,9 +109,14 @@ int qe_ctx_synchronize(qe_ctx* ctx);
 const char* qe_last_error(void);
 int qe_abi_version(void);
 
-/* Device memory helpers for hosts without their own allocator (JNI). */
+/* Device memory helpers for hosts without their own allocator (JNI). Blocks come from the
+ * library's caching allocator: a freed block is reused by the same ctx stream at once, by other
+ * streams once the work queued before the free has completed. (The reference never frees its
+ * allocators, K:256 / K:465 / K:635; this is the bounded equivalent.) */
 int qe_device_alloc(qe_ctx* ctx, size_t bytes, void** out);
 int qe_device_free(qe_ctx* ctx, void* ptr);
+/* Return the cached free blocks of `device` to the driver (waits for their last users). */
+int qe_release_cached_memory(int device);
 int qe_copy_to_device(qe_ctx* ctx, void* dst, const void* src, size_t bytes);   /* sync */
 int qe_copy_to_host(qe_ctx* ctx, void* dst, const void* src, size_t bytes);     /* sync */
 

@@ -250,10 +250,9 @@ int qe_batch_import(qe_ctx* ctx, const ArrowSchema* schema, const ArrowArray* ar
   qe_batch* b = new qe_batch();
   b->ctx = ctx;
   b->length = n;
-  if (hipMalloc(&b->device_block, total ? total : 256) != hipSuccess) {
-    (void)hipGetLastError();
+  if (dev_alloc(ctx, total ? total : 256, &b->device_block) != QE_OK) {
     delete b;
-    return fail(QE_ERR_OOM, "hipMalloc(%zu) for an imported batch failed", total);
+    return fail(QE_ERR_OOM, "device allocation of %zu bytes for an imported batch failed", total);
   }
   uint8_t* base = (uint8_t*)b->device_block;
   std::vector<H2DJob> jobs;
@@ -292,7 +291,7 @@ int qe_batch_import(qe_ctx* ctx, const ArrowSchema* schema, const ArrowArray* ar
   }
   const int rc = parallel_h2d(ctx, jobs);
   if (rc != QE_OK) {
-    (void)hipFree(b->device_block);
+    dev_free(ctx, b->device_block);
     delete b;
     return rc;
   }
@@ -347,8 +346,7 @@ int qe_batch_destroy(qe_batch* b) {
   if (!b) return QE_OK;
   if (b->device_block) {
     (void)hipSetDevice(b->ctx->device);
-    (void)hipStreamSynchronize(b->ctx->stream);
-    (void)hipFree(b->device_block);
+    dev_free(b->ctx, b->device_block);
   }
   delete b;
   return QE_OK;

@@ -472,10 +472,7 @@ __global__ void k_csv_copy(const uint8_t* __restrict__ data, const int64_t* __re
 }
 
 int dmalloc(qe_csv_table* t, size_t bytes, void** p) {
-  if (hipMalloc(p, bytes ? bytes : 1) != hipSuccess) {
-    (void)hipGetLastError();
-    return fail(QE_ERR_OOM, "hipMalloc(%zu) failed in CSV scan", bytes);
-  }
+  if (dev_alloc(t->ctx, bytes ? bytes : 1, p) != QE_OK) return fail(QE_ERR_OOM, "device allocation of %zu bytes failed in CSV scan", bytes);
   t->owned.push_back(*p);
   return QE_OK;
 }
@@ -648,8 +645,7 @@ int qe_csv_parse(qe_ctx* ctx, const uint8_t* data, int64_t nbytes, const qe_csv_
   t->ctx = ctx;
   const int rc = csv_parse(ctx, data, nbytes, opt, t);
   if (rc != QE_OK) {
-    (void)hipStreamSynchronize(ctx->stream);
-    for (void* q : t->owned) (void)hipFree(q);
+    for (void* q : t->owned) dev_free(ctx, q);
     delete t;
     return rc;
   }
@@ -708,8 +704,7 @@ int qe_csv_column_copy(const qe_csv_table* tc, int32_t i, qe_column* dst) {
 int qe_csv_destroy(qe_csv_table* t) {
   if (!t) return QE_OK;
   (void)hipSetDevice(t->ctx->device);
-  (void)hipStreamSynchronize(t->ctx->stream);
-  for (void* q : t->owned) (void)hipFree(q);
+  for (void* q : t->owned) dev_free(t->ctx, q);
   delete t;
   return QE_OK;
 }

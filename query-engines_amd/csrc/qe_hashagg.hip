@@ -1204,10 +1204,7 @@ static size_t table_bytes(const qe_hashagg* h, uint64_t cap) {
 
 static int table_alloc(qe_hashagg* h, uint64_t cap, void** mem, DTable* t) {
   const size_t bytes = table_bytes(h, cap);
-  if (hipMalloc(mem, bytes) != hipSuccess) {
-    (void)hipGetLastError();
-    return fail(QE_ERR_OOM, "hash table allocation of %zu bytes failed", bytes);
-  }
+  QE_TRY(dev_alloc(h->ctx, bytes, mem));
   const uint64_t SS = cap + 2;
   char* p = (char*)*mem;
   *t = DTable{};
@@ -1265,7 +1262,7 @@ static int table_grow(qe_hashagg* h, uint64_t want_cap) {
   uint64_t c[8];
   QE_TRY(read_ctl(h, c));  // synchronises: the old table can go
   QE_CHECK(c[3] == 0, QE_ERR_CAPACITY, "hash table rehash lost %llu groups", (unsigned long long)c[3]);
-  QE_HIP(hipFree(h->table_mem));
+  dev_free(h->ctx, h->table_mem);
   h->table_mem = mem;
   h->t = nt;
   return QE_OK;
@@ -1287,14 +1284,11 @@ static int ensure_defer(qe_hashagg* h, int64_t n) {
   const size_t words = (size_t)div_up((uint64_t)n, 32);
   if (words <= h->defer_words) return QE_OK;
   for (int i = 0; i < 2; ++i) {
-    if (h->defer[i]) QE_HIP(hipFree(h->defer[i]));
+    dev_free(h->ctx, h->defer[i]);
     h->defer[i] = nullptr;
   }
   for (int i = 0; i < 2; ++i) {
-    if (hipMalloc(&h->defer[i], words * 4) != hipSuccess) {
-      (void)hipGetLastError();
-      return fail(QE_ERR_OOM, "defer bitmap allocation failed");
-    }
+    QE_TRY(dev_alloc(h->ctx, words * 4, (void**)&h->defer[i]));
     QE_HIP(hipMemsetAsync(h->defer[i], 0, words * 4, h->ctx->stream));
     h->defer_dirty[i] = false;
   }
@@ -1550,18 +1544,12 @@ static int launch_hashagg(const Plan& P, int grid, size_t lds, hipStream_t st) {
 }
 
 template <typename T>
-static int grow_buffer(T** p, size_t* have, size_t need, hipStream_t st, const char* what) {
+static int grow_buffer(T** p, size_t* have, size_t need, qe_ctx* ctx, const char* what) {
   if (need <= *have) return QE_OK;
-  if (*p) {
-    QE_HIP(hipStreamSynchronize(st));
-    QE_HIP(hipFree(*p));
-  }
+  dev_free(ctx, *p);
   *p = nullptr;
   *have = 0;
-  if (hipMalloc((void**)p, need) != hipSuccess) {
-    (void)hipGetLastError();
-    return fail(QE_ERR_OOM, "%s: allocation of %zu bytes failed", what, need);
-  }
+  if (dev_alloc(ctx, need, (void**)p) != QE_OK) return fail(QE_ERR_OOM, "%s: allocation of %zu bytes failed", what, need);
   *have = need;
   return QE_OK;
 }
@@ -1596,7 +1584,7 @@ static int partition_rows(qe_hashagg* h, Plan& P, hipFunction_t* fn, int* grid) 
   const int64_t tw = (int64_t)div_up(div_up((uint64_t)n, (uint64_t)g), 256) * 256;
   g = (int64_t)div_up((uint64_t)n, (uint64_t)tw);
   const size_t cells = ((size_t)1 << log2p) * (size_t)g;
-  QE_TRY(grow_buffer(&h->part_cnt, &h->part_cnt_bytes, (2 * cells + 1) * 8, ctx->stream, "partition counts"));
+  QE_TRY(grow_buffer(&h->part_cnt, &h->part_cnt_bytes, (2 * cells + 1) * 8, ctx, "partition counts"));
   int64_t* cnt = h->part_cnt;
   int64_t* off = cnt + cells;
   P.part_tw = tw;
@@ -1613,8 +1601,8 @@ static int partition_rows(qe_hashagg* h, Plan& P, hipFunction_t* fn, int* grid) 
   if (!h->ovf || h->ovf_cap < (1ull << 20)) {
     uint8_t* ovf = nullptr;
     size_t have = 0;
-    QE_TRY(grow_buffer(&ovf, &have, (size_t)(1ull << 20) * h->rec_bytes, ctx->stream, "overflow area"));
-    if (h->ovf) (void)hipFree(h->ovf);
+    QE_TRY(grow_buffer(&ovf, &have, (size_t)(1ull << 20) * h->rec_bytes, ctx, "overflow area"));
+    dev_free(ctx, h->ovf);
     h->ovf = ovf;
     h->ovf_cap = 1ull << 20;
   }
@@ -1623,7 +1611,7 @@ static int partition_rows(qe_hashagg* h, Plan& P, hipFunction_t* fn, int* grid) 
   const PartLayout L = part_layout(P);
   const size_t rb = 8 * (size_t)L.words;
   if (R > 0) {
-    QE_TRY(grow_buffer(&h->part_rec, &h->part_rec_bytes, (size_t)R * rb, ctx->stream, "partition records"));
+    QE_TRY(grow_buffer(&h->part_rec, &h->part_rec_bytes, (size_t)R * rb, ctx, "partition records"));
     P.part_off = (qi64*)off;
     P.part_rec = h->part_rec;
     QE_TRY(jit_launch(ctx, fs, (int)g, P, staged ? 256 : 512));
@@ -1636,7 +1624,7 @@ static int partition_rows(qe_hashagg* h, Plan& P, hipFunction_t* fn, int* grid) 
   const int64_t target = std::max<int64_t>((int64_t)1 << log2p, std::min<int64_t>((int64_t)ctx->num_cus * 8, R >> 15));
   const int64_t cw = std::max<int64_t>(256, (int64_t)div_up((uint64_t)std::max<int64_t>(R, 1) * 5, (uint64_t)target * 4));
   const int64_t max_slices = ((int64_t)1 << log2p) + (int64_t)div_up((uint64_t)std::max<int64_t>(R, 1), (uint64_t)cw);
-  QE_TRY(grow_buffer(&h->part_slc, &h->part_slc_bytes, (size_t)(2 + 2 * max_slices) * 8, ctx->stream, "partition slices"));
+  QE_TRY(grow_buffer(&h->part_slc, &h->part_slc_bytes, (size_t)(2 + 2 * max_slices) * 8, ctx, "partition slices"));
   hipLaunchKernelGGL(k_part_slices, dim3(1), dim3(1024), 0, ctx->stream, (const qi64*)off, (qi32)(1 << log2p), (qi64)g,
                      (qi64)cw, (qi64*)h->part_slc);
   QE_TRY(launch_check("k_part_slices"));
@@ -1853,7 +1841,7 @@ int qe_hashagg_create(qe_ctx* ctx, int32_t nkeys, const int32_t* key_types, int3
   // control words
   if (hipEventCreate(&h->ev[0]) != hipSuccess || hipEventCreate(&h->ev[1]) != hipSuccess)
     return bail(fail(QE_ERR_DEVICE, "hipEventCreate failed"));
-  if (hipMalloc(&h->ctl, 64) != hipSuccess) return bail(fail(QE_ERR_OOM, "control allocation failed"));
+  if (dev_alloc(ctx, 64, (void**)&h->ctl) != QE_OK) return bail(fail(QE_ERR_OOM, "control allocation failed"));
   if (hipMemsetAsync(h->ctl, 0, 64, ctx->stream) != hipSuccess) return bail(fail(QE_ERR_DEVICE, "memset failed"));
   // LDS table: 2x the expected groups (load factor <= 0.5); a launch may shrink it down to
   // 1.25x (lds_log2_min) to fit the per-workgroup budget, else the launch is global-only.
@@ -1871,16 +1859,16 @@ int qe_hashagg_create(qe_ctx* ctx, int32_t nkeys, const int32_t* key_types, int3
   // overflow records: at most one per LDS slot per workgroup
   if (h->lds_log2) {
     h->ovf_cap = (uint64_t)h->grid * (((uint64_t)1 << h->lds_log2) + 2);
-    if (hipMalloc(&h->ovf, h->ovf_cap * h->rec_bytes) != hipSuccess) {
-      if (h->ctl) (void)hipFree(h->ctl);
+    if (dev_alloc(ctx, h->ovf_cap * h->rec_bytes, (void**)&h->ovf) != QE_OK) {
+      dev_free(ctx, h->ctl);
       return bail(fail(QE_ERR_OOM, "overflow area allocation failed"));
     }
   }
   // global table: 2x expected groups
   const int st = table_alloc(h, std::max<uint64_t>(1024, next_pow2((uint64_t)(2 * eg))), &h->table_mem, &h->t);
   if (st != QE_OK) {
-    if (h->ovf) (void)hipFree(h->ovf);
-    (void)hipFree(h->ctl);
+    dev_free(ctx, h->ovf);
+    dev_free(ctx, h->ctl);
     return bail(st);
   }
   *out = h;
@@ -1890,15 +1878,10 @@ int qe_hashagg_create(qe_ctx* ctx, int32_t nkeys, const int32_t* key_types, int3
 int qe_hashagg_destroy(qe_hashagg* h) {
   if (!h) return QE_OK;
   (void)hipSetDevice(h->ctx->device);
-  (void)hipStreamSynchronize(h->ctx->stream);
-  if (h->table_mem) (void)hipFree(h->table_mem);
-  if (h->ctl) (void)hipFree(h->ctl);
-  if (h->ovf) (void)hipFree(h->ovf);
-  if (h->part_cnt) (void)hipFree(h->part_cnt);
-  if (h->part_rec) (void)hipFree(h->part_rec);
-  if (h->part_slc) (void)hipFree(h->part_slc);
+  qe_ctx* ctx = h->ctx;  // blocks go back to the caching allocator behind this stream's work
+  void* bufs[] = {h->table_mem, h->ctl, h->ovf, h->part_cnt, h->part_rec, h->part_slc, h->defer[0], h->defer[1]};
+  for (void* b : bufs) dev_free(ctx, b);
   for (int i = 0; i < 2; ++i) {
-    if (h->defer[i]) (void)hipFree(h->defer[i]);
     if (h->ev[i]) (void)hipEventDestroy(h->ev[i]);
   }
   delete h;

@@ -53,6 +53,11 @@ void clear_error();
   } while (0)
 
 int ctx_enter(qe_ctx* ctx);                                   // validates + hipSetDevice
+// Caching device allocator (qe_runtime.hip): stream-ordered reuse of freed blocks.
+int dev_alloc(qe_ctx* ctx, size_t bytes, void** out);
+void dev_free(qe_ctx* ctx, void* p);
+void dev_forget_stream(qe_ctx* ctx);
+int dev_release(int device);
 int ctx_scratch(qe_ctx* ctx, size_t bytes, void** out);       // grow-only scratch
 int ctx_pinned(qe_ctx* ctx, size_t bytes, void** out);        // grow-only pinned host
 int launch_check(const char* what);                           // hipGetLastError wrapper

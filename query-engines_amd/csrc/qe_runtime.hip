@@ -3,9 +3,157 @@
 #include <stdio.h>
 #include <stdlib.h>
 
+#include <map>
+#include <mutex>
+#include <unordered_map>
+#include <vector>
+
 #include "qe_internal.hpp"
 
 namespace qe {
+
+// ---- caching device allocator ----------------------------------------------------------------------
+// Every per-object device buffer of the library (hash tables, control words, defer bitmaps,
+// partition records, dictionaries, imported batches, CSV tables) comes from here. hipMalloc /
+// hipFree cost tens of microseconds each and hipFree waits for the device, which made a small
+// query's aggregate state cost ~0.24 ms to create and destroy. Freed blocks are kept per device,
+// keyed by size class, with an event recorded on the freeing ctx's stream: the same stream may
+// reuse a block at once (stream order), any other stream once the event has completed. A failed
+// hipMalloc releases every completed cached block and retries; cached bytes above
+// QE_CACHE_LIMIT_GB (default 64) are released as blocks are freed.
+namespace {
+
+struct FreeBlk {
+  void* p;
+  size_t size;
+  hipStream_t stream;
+  hipEvent_t ev;
+};
+
+struct DevCache {
+  std::multimap<size_t, FreeBlk> free;
+  std::unordered_map<void*, size_t> live;
+  std::vector<hipEvent_t> events;
+  size_t cached = 0;
+};
+
+std::mutex g_amu;
+std::map<int, DevCache> g_dev;
+
+size_t size_class(size_t b) {
+  if (b <= 512) return 512;
+  if (b <= ((size_t)1 << 20)) {
+    size_t c = 1024;
+    while (c < b) c <<= 1;
+    return c;
+  }
+  const size_t g = (size_t)2 << 20;
+  return (b + g - 1) / g * g;
+}
+
+size_t cache_limit() {
+  static const size_t lim = [] {
+    const char* e = getenv("QE_CACHE_LIMIT_GB");
+    return (e && *e ? (size_t)atoll(e) : (size_t)64) << 30;
+  }();
+  return lim;
+}
+
+bool block_ready(const FreeBlk& b, hipStream_t s) {
+  if (b.stream && b.stream == s) return true;
+  const hipError_t e = hipEventQuery(b.ev);
+  if (e == hipSuccess) return true;
+  (void)hipGetLastError();  // hipErrorNotReady must not surface as a later launch error
+  return false;
+}
+
+// Releases cached blocks whose events have completed (all of them with `wait`). Lock held.
+void release_cached(DevCache& C, bool wait, size_t down_to) {
+  for (auto it = C.free.begin(); it != C.free.end() && C.cached > down_to;) {
+    FreeBlk& b = it->second;
+    if (wait) (void)hipEventSynchronize(b.ev);
+    if (wait || hipEventQuery(b.ev) == hipSuccess) {
+      (void)hipFree(b.p);
+      C.events.push_back(b.ev);
+      C.cached -= b.size;
+      it = C.free.erase(it);
+    } else {
+      (void)hipGetLastError();
+      ++it;
+    }
+  }
+}
+
+}  // namespace
+
+int dev_alloc(qe_ctx* ctx, size_t bytes, void** out) {
+  const size_t cls = size_class(bytes);
+  const size_t hi = cls <= ((size_t)1 << 20) ? cls : cls + cls / 4;
+  std::lock_guard<std::mutex> lk(g_amu);
+  DevCache& C = g_dev[ctx->device];
+  for (auto it = C.free.lower_bound(cls); it != C.free.end() && it->first <= hi; ++it) {
+    if (!block_ready(it->second, ctx->stream)) continue;
+    *out = it->second.p;
+    C.events.push_back(it->second.ev);
+    C.cached -= it->first;
+    C.live[*out] = it->first;
+    C.free.erase(it);
+    return QE_OK;
+  }
+  void* p = nullptr;
+  if (hipMalloc(&p, cls) != hipSuccess) {
+    (void)hipGetLastError();
+    release_cached(C, true, 0);
+    if (hipMalloc(&p, cls) != hipSuccess) {
+      (void)hipGetLastError();
+      return fail(QE_ERR_OOM, "device allocation of %zu bytes failed", bytes);
+    }
+  }
+  C.live[p] = cls;
+  *out = p;
+  return QE_OK;
+}
+
+void dev_free(qe_ctx* ctx, void* p) {
+  if (!p) return;
+  std::lock_guard<std::mutex> lk(g_amu);
+  DevCache& C = g_dev[ctx->device];
+  auto it = C.live.find(p);
+  if (it == C.live.end()) {  // not from dev_alloc
+    (void)hipFree(p);
+    return;
+  }
+  const size_t size = it->second;
+  C.live.erase(it);
+  hipEvent_t ev = nullptr;
+  if (!C.events.empty()) {
+    ev = C.events.back();
+    C.events.pop_back();
+  } else if (hipEventCreateWithFlags(&ev, hipEventDisableTiming) != hipSuccess) {
+    (void)hipGetLastError();
+    (void)hipStreamSynchronize(ctx->stream);
+    (void)hipFree(p);
+    return;
+  }
+  (void)hipEventRecord(ev, ctx->stream);
+  C.free.emplace(size, FreeBlk{p, size, ctx->stream, ev});
+  C.cached += size;
+  if (C.cached > cache_limit()) release_cached(C, false, cache_limit() / 2);
+}
+
+// A ctx going away: its stream handle may be reused, so its cached blocks wait on their events.
+void dev_forget_stream(qe_ctx* ctx) {
+  std::lock_guard<std::mutex> lk(g_amu);
+  for (auto& kv : g_dev[ctx->device].free)
+    if (kv.second.stream == ctx->stream) kv.second.stream = nullptr;
+}
+
+int dev_release(int device) {
+  std::lock_guard<std::mutex> lk(g_amu);
+  auto it = g_dev.find(device);
+  if (it != g_dev.end()) release_cached(it->second, true, 0);
+  return QE_OK;
+}
 
 static thread_local std::string g_last_error;
 
@@ -208,6 +356,7 @@ int qe_ctx_destroy(qe_ctx* ctx) {
   if (!ctx) return QE_OK;
   (void)hipSetDevice(ctx->device);
   (void)hipStreamSynchronize(ctx->stream);
+  dev_forget_stream(ctx);
   if (ctx->scratch) (void)hipFree(ctx->scratch);
   if (ctx->scan_tmp) (void)hipFree(ctx->scan_tmp);
   for (void* w : ctx->ws)
@@ -235,17 +384,18 @@ int qe_ctx_synchronize(qe_ctx* ctx) {
 int qe_device_alloc(qe_ctx* ctx, size_t bytes, void** out) {
   QE_TRY(ctx_enter(ctx));
   QE_CHECK(out != nullptr, QE_ERR_INVALID_ARG, "null out");
-  if (hipMalloc(out, bytes ? bytes : 1) != hipSuccess) {
-    (void)hipGetLastError();
-    return fail(QE_ERR_OOM, "hipMalloc(%zu) failed", bytes);
-  }
-  return QE_OK;
+  return dev_alloc(ctx, bytes, out);
 }
 
 int qe_device_free(qe_ctx* ctx, void* ptr) {
   QE_TRY(ctx_enter(ctx));
-  if (ptr) QE_HIP(hipFree(ptr));
+  dev_free(ctx, ptr);
   return QE_OK;
+}
+
+int qe_release_cached_memory(int device) {
+  QE_HIP(hipSetDevice(device));
+  return dev_release(device);
 }
 
 int qe_copy_to_device(qe_ctx* ctx, void* dst, const void* src, size_t bytes) {

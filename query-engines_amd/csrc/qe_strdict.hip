@@ -663,19 +663,18 @@ namespace {
 
 int dict_free(qe_strdict* d) {
   void* ptrs[] = {d->s_hash, d->s_code, d->code_off, d->code_len, d->code_hash, d->arena, d->ctl};
-  for (void* p : ptrs)
-    if (p) (void)hipFree(p);
+  for (void* p : ptrs) dev_free(d->ctx, p);
   return QE_OK;
 }
 
 int grow_slots(qe_strdict* d, uint64_t cap) {
   qe_ctx* ctx = d->ctx;
-  if (d->s_hash) QE_HIP(hipFree(d->s_hash));
-  if (d->s_code) QE_HIP(hipFree(d->s_code));
+  dev_free(ctx, d->s_hash);
+  dev_free(ctx, d->s_code);
   d->s_hash = nullptr;
   d->s_code = nullptr;
-  QE_HIP(hipMalloc(&d->s_hash, cap * 8));
-  QE_HIP(hipMalloc(&d->s_code, cap * 4));
+  QE_TRY(dev_alloc(ctx, cap * 8, (void**)&d->s_hash));
+  QE_TRY(dev_alloc(ctx, cap * 4, (void**)&d->s_code));
   d->cap = cap;
   QE_HIP(hipMemsetAsync(d->s_hash, 0, cap * 8, ctx->stream));
   QE_HIP(hipMemsetAsync(d->s_code, 0xFF, cap * 4, ctx->stream));
@@ -690,11 +689,10 @@ int grow_slots(qe_strdict* d, uint64_t cap) {
 template <typename T>
 int grow_array(qe_ctx* ctx, T** p, int64_t old_n, int64_t new_n) {
   T* q = nullptr;
-  QE_HIP(hipMalloc(&q, (size_t)new_n * sizeof(T)));
+  QE_TRY(dev_alloc(ctx, (size_t)new_n * sizeof(T), (void**)&q));
   if (*p) {
     if (old_n > 0) QE_HIP(hipMemcpyAsync(q, *p, (size_t)old_n * sizeof(T), hipMemcpyDeviceToDevice, ctx->stream));
-    QE_HIP(hipStreamSynchronize(ctx->stream));
-    QE_HIP(hipFree(*p));
+    dev_free(ctx, *p);
   }
   *p = q;
   return QE_OK;
@@ -756,7 +754,6 @@ int qe_strdict_create(qe_ctx* ctx, int64_t expected_distinct, qe_strdict** out) 
 int qe_strdict_destroy(qe_strdict* d) {
   if (!d) return QE_OK;
   (void)hipSetDevice(d->ctx->device);
-  (void)hipStreamSynchronize(d->ctx->stream);
   dict_free(d);
   delete d;
   return QE_OK;

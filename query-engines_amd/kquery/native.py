@@ -190,6 +190,7 @@ SIGNATURES = [
     ("qe_abi_version", C.c_int, []),
     ("qe_device_alloc", C.c_int, [_P, C.c_size_t, _PP]),
     ("qe_device_free", C.c_int, [_P, _P]),
+    ("qe_release_cached_memory", C.c_int, [C.c_int]),
     ("qe_copy_to_device", C.c_int, [_P, _P, _P, C.c_size_t]),
     ("qe_copy_to_host", C.c_int, [_P, _P, _P, C.c_size_t]),
     ("qe_generate", C.c_int, [_P, _COLP, C.c_int32, C.c_int64, C.c_uint64, C.c_uint64, C.c_int64, C.c_int32]),
