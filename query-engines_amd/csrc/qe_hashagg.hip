@@ -1577,10 +1577,16 @@ static int partition_rows(qe_hashagg* h, Plan& P, hipFunction_t* fn, int* grid) 
   hipFunction_t fc, fs;
   int bpc = 0;
   QE_TRY(jit_kernel(ctx, sc, &fc, &bpc, "qe_pcount"));
-  QE_TRY(jit_kernel(ctx, ss, &fs, &bpc, "qe_pscatter", staged ? 256 : 512));
+  QE_TRY(jit_kernel(ctx, ss, &fs, &bpc, "qe_pscatter", staged ? pscatter_block() : 512));
   QE_TRY(jit_kernel(ctx, sa, fn, &bpc, "qe_pagg"));
   const int64_t n = P.n;
-  int64_t g = std::min<int64_t>((int64_t)ctx->num_cus * 4, (int64_t)div_up((uint64_t)n, 256));
+  // count / scatter workgroups per CU (QE_PART_WG_PER_CU overrides; see pscatter_block)
+  static const int wg_per_cu = [] {
+    const char* e = getenv("QE_PART_WG_PER_CU");
+    const int v = e && *e ? atoi(e) : 2;
+    return v >= 1 && v <= 32 ? v : 2;
+  }();
+  int64_t g = std::min<int64_t>((int64_t)ctx->num_cus * wg_per_cu, (int64_t)div_up((uint64_t)n, 256));
   const int64_t tw = (int64_t)div_up(div_up((uint64_t)n, (uint64_t)g), 256) * 256;
   g = (int64_t)div_up((uint64_t)n, (uint64_t)tw);
   const size_t cells = ((size_t)1 << log2p) * (size_t)g;
@@ -1614,7 +1620,7 @@ static int partition_rows(qe_hashagg* h, Plan& P, hipFunction_t* fn, int* grid) 
     QE_TRY(grow_buffer(&h->part_rec, &h->part_rec_bytes, (size_t)R * rb, ctx, "partition records"));
     P.part_off = (qi64*)off;
     P.part_rec = h->part_rec;
-    QE_TRY(jit_launch(ctx, fs, (int)g, P, staged ? 256 : 512));
+    QE_TRY(jit_launch(ctx, fs, (int)g, P, staged ? pscatter_block() : 512));
     QE_TRY(launch_check("qe_pscatter"));
   }
   // aggregation slices inside bucket boundaries: one per bucket, or more (up to 8 per CU, none

@@ -514,14 +514,26 @@ bool gen_part_source(const Plan& P, int log2p, bool scatter, std::string* src) {
   return true;
 }
 
-// Staged scatter (few buckets): a 256-thread workgroup takes 1024-row tiles; the tile's records
+// Staged scatter (few buckets): a workgroup of B threads (512) takes 4B-row tiles; the tile's records
 // are counting-sorted by bucket in LDS (rank = LDS atomic on the tile histogram, one wave scans
 // it), then written out as contiguous per-bucket runs, 16 bytes per lane in record-stream order,
 // so the HBM writes coalesce instead of landing as one 2-word record per lane. Rows go to the same
 // (bucket, workgroup) ranges as the direct scatter: the records of one bucket and workgroup keep
 // a contiguous range of its bucket (their order inside it may differ run to run).
 bool part_staged_ok(const Plan& P, int log2p) {
-  return log2p <= 9 && part_layout(P).words <= 8;
+  return log2p <= 9 && part_layout(P).words * pscatter_block() <= 8 * 256;
+}
+
+// Workgroup size of the staged scatter (tile = 4 rows per thread); QE_PSCATTER_BLOCK overrides.
+// Measured at 200M rows, 64K / 256K groups (count + scatter + aggregate): 128 threads 4.05 /
+// 4.69 ms, 512 threads (2 per CU) 3.55 / 4.14 ms, 1024 threads 3.64 / 4.37 ms.
+int pscatter_block() {
+  static const int b = [] {
+    const char* e = getenv("QE_PSCATTER_BLOCK");
+    const int v = e && *e ? atoi(e) : 512;
+    return (v == 128 || v == 256 || v == 512 || v == 1024) ? v : 512;
+  }();
+  return b;
 }
 
 bool gen_pscatter_staged_source(const Plan& P, int log2p, std::string* src) {
@@ -532,8 +544,8 @@ bool gen_pscatter_staged_source(const Plan& P, int log2p, std::string* src) {
   const int W = L.words;
   std::ostringstream o;
   o << "\nusing namespace qe;\n"
-    << "extern \"C\" __global__ void __launch_bounds__(256) qe_pscatter(const Plan P) {\n"
-    << "  constexpr int LOG2P = " << log2p << ", NP = 1 << LOG2P, W = " << W << ", T = 1024;\n"
+    << "extern \"C\" __global__ void __launch_bounds__(" << pscatter_block() << ") qe_pscatter(const Plan P) {\n"
+    << "  constexpr int LOG2P = " << log2p << ", NP = 1 << LOG2P, W = " << W << ", T = " << 4 * pscatter_block() << ";\n"
     << "  __shared__ qu32 s_hist[NP];\n  __shared__ qu32 s_off[NP];\n  __shared__ qu64 s_cur[NP];\n"
     << "  __shared__ qi64x2 s_rec[T * W / 2];\n  __shared__ unsigned short s_bkt[T];\n  __shared__ qu32 s_total;\n"
     << "  for (int b = threadIdx.x; b < NP; b += blockDim.x) s_cur[b] = (qu64)P.part_off[(qi64)b * gridDim.x + blockIdx.x];\n"
