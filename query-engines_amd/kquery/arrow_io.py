@@ -7,7 +7,8 @@ that producer/consumer role through the same two structs.
 from __future__ import annotations
 
 import ctypes as C
-from typing import List, Optional, Sequence
+from concurrent.futures import ThreadPoolExecutor
+from typing import Iterable, Iterator, List, Optional, Sequence
 
 from . import native as N
 from .columnar import Context, DeviceColumn
@@ -110,3 +111,39 @@ def export_to_pyarrow(ctx: Context, cols: Sequence, names: Sequence[str]):
 
 def columns_from_batch(db: DeviceBatch) -> List[N.QeColumn]:
     return [c for c, _ in db.columns()]
+
+
+_IMPORT_CTX: dict = {}
+
+
+def prefetch_import(batches: Iterable, ctx: Context, import_ctx: Optional[Context] = None) -> Iterator[DeviceBatch]:
+    """Host Arrow RecordBatches -> DeviceBatches, importing one batch ahead (H2D
+    overlapped with compute). ScanExec.execute (K:569-571) hands batches to the operators one at a
+    time. While the caller's kernels for batch i run on `ctx`'s stream, a worker thread imports
+    batch i+1 through `import_ctx`. That ctx has its own HIP stream, so the import's pinned staging
+    (8 host threads) and DMA run beside the compute. ctypes releases the GIL during
+    qe_batch_import. The import has completed when a batch is yielded. A yielded batch stays
+    valid until the caller asks for the next one. Then `ctx` is synchronised and the batch is
+    closed, so its blocks are never reused while the caller's kernels still read them."""
+    import torch
+
+    if import_ctx is None:  # one import ctx (stream + pinned staging) per compute ctx, kept
+        import_ctx = _IMPORT_CTX.get(id(ctx))
+        if import_ctx is None:
+            with torch.cuda.stream(torch.cuda.Stream(device=ctx.torch_device)):
+                import_ctx = _IMPORT_CTX[id(ctx)] = Context.get(ctx.device)
+    it = iter(batches)
+    first = next(it, None)
+    if first is None:
+        return
+    with ThreadPoolExecutor(max_workers=1) as pool:
+        fut = pool.submit(DeviceBatch.from_pyarrow, first, import_ctx)
+        while fut is not None:
+            db = fut.result()
+            nxt = next(it, None)
+            fut = pool.submit(DeviceBatch.from_pyarrow, nxt, import_ctx) if nxt is not None else None
+            try:
+                yield db
+            finally:
+                ctx.synchronize()
+                db.close()
