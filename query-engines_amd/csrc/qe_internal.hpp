@@ -90,7 +90,7 @@ int compile_inputs(const qe_column* cols, int32_t ncols, int32_t mask_col, int32
 int compile_program(const qe_column* cols, int32_t ncols, const bool* col_f64, const qe_agg_program& pg, int j,
                     qe::DAgg* a, bool* is_f, bool* nullable);
 // Select-project kernel source (qe_jit.hip): R rows per thread, 256 threads.
-bool gen_selproj_source(const qe::Plan& P, const int32_t* out_kind, int nout, std::string* src);
+bool gen_selproj_source(const qe::Plan& P, const int32_t* out_kind, int nout, std::string* src, bool persistent);
 int selproj_rows_per_thread(const qe::Plan& P);
 // Exclusive scan of n int64 on the ctx stream (one block); out[n] = total. (qe_filter.hip)
 int exclusive_scan_i64(qe_ctx* ctx, const int64_t* in, int64_t* out, int64_t n);

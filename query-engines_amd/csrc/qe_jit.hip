@@ -714,9 +714,16 @@ bool gen_pagg_source(const Plan& P, int log2, std::string* src, size_t* lds_byte
 // t.cap number of tiles. out_kind[k] = byte width (8, 4, 1) | 0x100 if the output is nullable.
 // (Measured alternatives, C2 10M rows: a persistent grid pulling tiles, 73 us; a look-back
 // reading 4 windows per round trip, 87 us; this one-tile-per-workgroup, one-window form, 64 us.)
+// Non-temporal input loads once the inputs exceed the 256 MB MALL (QE_SELPROJ_NT=0/1 forces).
+bool selproj_nt(const Plan& P) {
+  const char* e = getenv("QE_SELPROJ_NT");
+  if (e && *e) return e[0] == '1';
+  return P.n > (64ll << 20);
+}
+
 int selproj_rows_per_thread(const Plan& P) { return P.ncols <= 3 ? 16 : (P.ncols <= 6 ? 8 : 4); }
 
-bool gen_selproj_source(const Plan& P, const int32_t* out_kind, int nout, std::string* src) {
+bool gen_selproj_source(const Plan& P, const int32_t* out_kind, int nout, std::string* src, bool persistent) {
   if (P.ncols < 1 || P.ncols > QE_MAX_COLS || nout < 1 || nout > QE_MAX_AGGS) return false;
   const int R = selproj_rows_per_thread(P);
   std::ostringstream o;
@@ -724,12 +731,19 @@ bool gen_selproj_source(const Plan& P, const int32_t* out_kind, int nout, std::s
     << "extern \"C\" __global__ void __launch_bounds__(256) qe_selproj(const Plan P) {\n"
     << "  constexpr int R = " << R << ";\n"
     << "  constexpr qu64 F_AGG = 1ull << 62, F_INC = 2ull << 62, VMASK = (1ull << 62) - 1;\n"
-    << "  __shared__ qu32 s_cnt[R * 4];\n  __shared__ qu64 s_base;\n  __shared__ qu32 s_tile;\n"
-    << "  const int t = threadIdx.x, lane = t & 63, w = t >> 6;\n"
-    << "  if (t == 0) s_tile = (qu32)atomicAdd((unsigned long long*)&P.t.ctl[0], 1ull);\n"
-    << "  __syncthreads();\n"
-    << "  const qu32 tile = s_tile;\n"
-    << "  const qi64 base = (qi64)tile * (R * 256);\n"
+    << "  __shared__ qu32 s_cnt[R * 4];\n  __shared__ qu64 s_base;\n  __shared__ qu32 s_tile, s_total;\n"
+    << "  __shared__ qi64 s_out[" << ((size_t)nout * R * 256 * 8 <= 64 * 1024 ? nout * R * 256 : 1) << "];\n"
+    << "  const int t = threadIdx.x, lane = t & 63, w = t >> 6;\n";
+  if (persistent) {
+    // every workgroup is resident (grid <= CUs x occupancy), so a static tile order cannot
+    // deadlock the look-back and no tile counter is needed
+    o << "  for (qu32 tile = blockIdx.x; (qu64)tile < P.t.cap; tile += gridDim.x) {\n";
+  } else {
+    o << "  {\n  if (t == 0) s_tile = (qu32)atomicAdd((unsigned long long*)&P.t.ctl[0], 1ull);\n"
+      << "  __syncthreads();\n"
+      << "  const qu32 tile = s_tile;\n";
+  }
+  o << "  const qi64 base = (qi64)tile * (R * 256);\n"
     << "  const bool full = base + R * 256 <= P.n;\n";
   for (int c = 0; c < P.ncols; ++c) {
     const std::string cs = std::to_string(c);
@@ -742,7 +756,7 @@ bool gen_selproj_source(const Plan& P, const int32_t* out_kind, int nout, std::s
     else
       // default policy: this kernel is look-back bound and C2-sized inputs stay in the MALL
       // (measured: nt 68.4 us, default 65.0 us)
-      o << "      c" << cs << "[r] = (full || row < P.n) ? (qi64)" << ld(ty, "p + row", false) << " : 0;\n";
+      o << "      c" << cs << "[r] = (full || row < P.n) ? (qi64)" << ld(ty, "p + row", selproj_nt(P)) << " : 0;\n";
     o << "    }\n  }\n";
     if (P.cols[c].valid) {
       o << "  qu32 v" << cs << " = 0;\n  {\n    const qu8* vb = P.cols[" << cs << "].valid;\n"
@@ -760,59 +774,106 @@ bool gen_selproj_source(const Plan& P, const int32_t* out_kind, int nout, std::s
     for (size_t k = body.find(from); k != std::string::npos; k = body.find(from, k)) body.replace(k, from.size(), to);
     o << body;
   }
+  // Staged output (all outputs 8 bytes wide, R x 256 x 8 B each within 64 KiB of LDS): selected
+  // rows land compacted in LDS, then the tile's output range is written with 16-byte stores, all
+  // lanes active. Direct 8-byte stores from the row registers were store-issue bound (half the
+  // lanes idle at 50 % selectivity, 16 store instructions per thread).
+  bool staged = (size_t)nout * R * 256 * 8 <= 64 * 1024;
+  for (int k = 0; k < nout; ++k) staged = staged && (out_kind[k] & 0xFF) == 8;
+  std::vector<Expr> ex(nout);
+  for (int k = 0; k < nout; ++k)
+    if (!agg_expr(P, k, &ex[k])) return false;
   o << "  qu64 bal[R];\n"
     << "#pragma unroll\n  for (int r = 0; r < R; ++r) bal[r] = __ballot((act >> r) & 1u);\n"
     << "  if (lane == 0) {\n#pragma unroll\n    for (int r = 0; r < R; ++r) s_cnt[r * 4 + w] = (qu32)__popcll(bal[r]);\n  }\n"
     << "  __syncthreads();\n"
+    << "  qu64* st = (qu64*)P.t.keys;\n"
     << "  if (w == 0) {\n"
     << "    const qu32 x = lane < R * 4 ? s_cnt[lane] : 0u;\n"
     << "    qu32 inc = x;\n"
     << "#pragma unroll\n    for (int d = 1; d < 64; d <<= 1) { const qu32 y = __shfl_up(inc, d); if (lane >= d) inc += y; }\n"
     << "    const qu64 total = (qu64)__shfl(inc, 63);\n"
     << "    if (lane < R * 4) s_cnt[lane] = inc - x;\n"
-    << "    qu64* st = (qu64*)P.t.keys;\n"
-    << "    if (lane == 0) __hip_atomic_store(&st[tile], (tile == 0 ? F_INC : F_AGG) | total, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);\n"
-    << "    qu64 excl = 0;\n"
-    << "    if (tile > 0) {\n"
-    << "      qi64 pos = (qi64)tile - 1;\n"
-    << "      for (;;) {\n"
-    << "        const qi64 idx = pos - lane;\n"
-    << "        qu64 v;\n"
-    << "        do { v = idx >= 0 ? __hip_atomic_load(&st[idx], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : F_INC; }\n"
-    << "        while (__any((v >> 62) == 0));\n"
-    << "        const qu64 incm = __ballot((v >> 62) == 2);\n"
-    << "        qu64 c = v & VMASK;\n"
-    << "        if (incm) { const int first = __ffsll((long long)incm) - 1; if (lane > first) c = 0; }\n"
-    << "#pragma unroll\n        for (int d = 32; d >= 1; d >>= 1) c += __shfl_xor(c, d);\n"
-    << "        excl += c;\n"
-    << "        if (incm) break;\n"
-    << "        pos -= 64;\n"
-    << "      }\n"
-    << "      if (lane == 0) __hip_atomic_store(&st[tile], F_INC | (excl + total), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);\n"
-    << "    }\n"
-    << "    if (lane == 0) {\n      s_base = excl;\n"
-    << "      if ((qu64)tile == P.t.cap - 1) __hip_atomic_store(&P.t.ctl[1], excl + total, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);\n    }\n"
-    << "  }\n  __syncthreads();\n"
-    << "  const qu64 tb = s_base;\n"
-    << "  const qu64 below = (1ull << lane) - 1;\n"
-    << "#pragma unroll\n  for (int r = 0; r < R; ++r) {\n"
-    << "    if (!((act >> r) & 1u)) continue;\n"
-    << "    const qu64 pos = tb + s_cnt[r * 4 + w] + (qu64)__popcll(bal[r] & below);\n";
-  for (int k = 0; k < nout; ++k) {
-    Expr e;
-    if (!agg_expr(P, k, &e)) return false;
-    const std::string ks = std::to_string(k);
-    const int width = out_kind[k] & 0xFF;
-    const bool nullable = (out_kind[k] & 0x100) != 0;
-    o << "    {\n      const qi64 x = " << e.v << ";\n";
-    if (width == 8) o << "      ((qi64*)P.t.acc[" << ks << "])[pos] = x;\n";
-    else if (width == 4) o << "      ((qi32*)P.t.acc[" << ks << "])[pos] = (qi32)x;\n";
-    else if (width == 1) o << "      ((qu8*)P.t.acc[" << ks << "])[pos] = (qu8)x;\n";
-    else return false;
-    if (nullable)
-      o << "      if (" << e.ok << ") atomicOr(&((qu32*)P.t.nn[" << ks << "])[pos >> 5], 1u << (pos & 31));\n";
-    o << "    }\n";
+    << "    if (lane == 0) { s_total = (qu32)total; __hip_atomic_store(&st[tile], (tile == 0 ? F_INC : F_AGG) | total, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }\n"
+    << "  }\n";
+  const std::string lookback =
+      "    const qu64 total = s_total;\n"
+      "    qu64 excl = 0;\n"
+      "    if (tile > 0) {\n"
+      "      qi64 pos = (qi64)tile - 1;\n"
+      "      for (;;) {\n"
+      "        const qi64 idx = pos - lane;\n"
+      "        qu64 v;\n"
+      "        do { v = idx >= 0 ? __hip_atomic_load(&st[idx], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : F_INC; }\n"
+      "        while (__any((v >> 62) == 0));\n"
+      "        const qu64 incm = __ballot((v >> 62) == 2);\n"
+      "        qu64 c = v & VMASK;\n"
+      "        if (incm) { const int first = __ffsll((long long)incm) - 1; if (lane > first) c = 0; }\n"
+      "#pragma unroll\n        for (int d = 32; d >= 1; d >>= 1) c += __shfl_xor(c, d);\n"
+      "        excl += c;\n"
+      "        if (incm) break;\n"
+      "        pos -= 64;\n"
+      "      }\n"
+      "      if (lane == 0) __hip_atomic_store(&st[tile], F_INC | (excl + total), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);\n"
+      "    }\n"
+      "    if (lane == 0) {\n      s_base = excl;\n"
+      "      if ((qu64)tile == P.t.cap - 1) __hip_atomic_store(&P.t.ctl[1], excl + total, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);\n    }\n";
+  o << "  __syncthreads();\n"
+    << "  const qu64 below = (1ull << lane) - 1;\n";
+  if (staged) {
+    // rows -> LDS at their tile-local positions (validity bits straight to the output bitmap
+    // once the tile base is known), while wave 0 then runs the look-back
+    o << "#pragma unroll\n  for (int r = 0; r < R; ++r) {\n"
+      << "    if (!((act >> r) & 1u)) continue;\n"
+      << "    const qu32 lp = s_cnt[r * 4 + w] + (qu32)__popcll(bal[r] & below);\n";
+    for (int k = 0; k < nout; ++k) o << "    s_out[" << k << " * (R * 256) + lp] = " << ex[k].v << ";\n";
+    o << "  }\n"
+      << "  if (w == 0) {\n" << lookback << "  }\n"
+      << "  __syncthreads();\n"
+      << "  {\n    const qu64 tb = s_base;\n    const qu32 tot = s_total;\n";
+    for (int k = 0; k < nout; ++k) {
+      const std::string ks = std::to_string(k);
+      o << "    {\n      qi64* out = (qi64*)P.t.acc[" << ks << "] + tb;\n"
+        << "      const qi64* so = s_out + " << ks << " * (R * 256);\n"
+        << "      const qu32 mis = (qu32)(((qu64)out >> 3) & 1), head = mis < tot ? mis : tot;  // 16-byte alignment\n"
+        << "      if (head && t == 0) out[0] = so[0];\n"
+        << "      for (qu32 i = head + 2 * t; i + 1 < tot; i += 512) *(qi64x2*)(out + i) = qi64x2{so[i], so[i + 1]};\n"
+        << "      if (t == 0 && tot > head && ((tot - head) & 1)) out[tot - 1] = so[tot - 1];\n    }\n";
+    }
+    const bool any_null = [&] { for (int k = 0; k < nout; ++k) if (out_kind[k] & 0x100) return true; return false; }();
+    if (any_null) {
+      o << "#pragma unroll\n    for (int r = 0; r < R; ++r) {\n"
+        << "      if (!((act >> r) & 1u)) continue;\n"
+        << "      const qu64 pos = tb + s_cnt[r * 4 + w] + (qu64)__popcll(bal[r] & below);\n";
+      for (int k = 0; k < nout; ++k)
+        if (out_kind[k] & 0x100)
+          o << "      if (" << ex[k].ok << ") atomicOr(&((qu32*)P.t.nn[" << k << "])[pos >> 5], 1u << (pos & 31));\n";
+      o << "    }\n";
+    }
+    o << "  }\n";
+  } else {
+    o << "  if (w == 0) {\n" << lookback << "  }\n"
+      << "  __syncthreads();\n"
+      << "  const qu64 tb = s_base;\n"
+      << "#pragma unroll\n  for (int r = 0; r < R; ++r) {\n"
+      << "    if (!((act >> r) & 1u)) continue;\n"
+      << "    const qu64 pos = tb + s_cnt[r * 4 + w] + (qu64)__popcll(bal[r] & below);\n";
+    for (int k = 0; k < nout; ++k) {
+      const std::string ks = std::to_string(k);
+      const int width = out_kind[k] & 0xFF;
+      const bool nullable = (out_kind[k] & 0x100) != 0;
+      o << "    {\n      const qi64 x = " << ex[k].v << ";\n";
+      if (width == 8) o << "      ((qi64*)P.t.acc[" << ks << "])[pos] = x;\n";
+      else if (width == 4) o << "      ((qi32*)P.t.acc[" << ks << "])[pos] = (qi32)x;\n";
+      else if (width == 1) o << "      ((qu8*)P.t.acc[" << ks << "])[pos] = (qu8)x;\n";
+      else return false;
+      if (nullable)
+        o << "      if (" << ex[k].ok << ") atomicOr(&((qu32*)P.t.nn[" << ks << "])[pos >> 5], 1u << (pos & 31));\n";
+      o << "    }\n";
+    }
+    o << "  }\n";
   }
+  if (persistent) o << "  __syncthreads();\n";  // s_cnt / s_base are reused by the next tile
   o << "  }\n}\n";
   *src = std::string(kDevHeader) + o.str();
   return true;

@@ -50,8 +50,16 @@ extern "C" int qe_select_project(qe_ctx* ctx, const qe_column* cols, int32_t nco
     P.t.nn[k] = (qu64*)outs[k].validity;
   }
   if (!ctx->jit) return fail(QE_ERR_UNSUPPORTED, "fused select-project needs kernel specialisation (jit is off)");
+  // Tile order: a persistent grid (every workgroup resident, tiles assigned statically) or one
+  // tile per workgroup with ids from a device counter in start order (QE_SELPROJ_PERSIST=0). The
+  // counter is one word every workgroup hits: ~88 returning atomics/us, a floor of 2.8 ms for
+  // 1B rows in 4096-row tiles.
+  static const bool persist = [] {
+    const char* e = getenv("QE_SELPROJ_PERSIST");
+    return !(e && e[0] == '0');
+  }();
   std::string src;
-  if (!gen_selproj_source(P, out_kind, spec->nout, &src))
+  if (!gen_selproj_source(P, out_kind, spec->nout, &src, persist))
     return fail(QE_ERR_UNSUPPORTED, "plan shape is outside the select-project generator");
   hipFunction_t fn;
   int bpc = 0;
@@ -74,7 +82,13 @@ extern "C" int qe_select_project(qe_ctx* ctx, const qe_column* cols, int32_t nco
     P.t.ctl = ctl;
     P.t.keys = (qi64*)(ctl + 2);
     P.t.cap = (qu64)tiles;
-    QE_TRY(jit_launch(ctx, fn, (int)tiles, P, 256));  // one tile per workgroup, ids in start order
+    static const int wg_cap = [] {
+      const char* e = getenv("QE_SELPROJ_WG_PER_CU");
+      return e && *e ? std::max(1, atoi(e)) : 64;
+    }();
+    const int64_t grid =
+        persist ? std::min<int64_t>(tiles, (int64_t)ctx->num_cus * std::max(1, std::min(bpc, wg_cap))) : tiles;
+    QE_TRY(jit_launch(ctx, fn, (int)grid, P, 256));
     QE_TRY(launch_check("qe_selproj"));
     void* pin;
     QE_TRY(ctx_pinned(ctx, 8, &pin));

@@ -109,6 +109,28 @@ def main():
             ms_s = timed(run_sweep)
             report(f"C2 fused, a > {sel_k}", n, 16 + 8 * cnt.value / n, ms_s, selected=cnt.value)
         del cols, out
+    if "C2L" in which:  # the C2 kernel at 1B rows: its bandwidth once launch latency is amortised
+        n = 1_000_000_000
+        cols = [generate_column(s, n, 0, 42, ctx) for s in C2_COLUMNS]
+        schema = Schema([s.field() for s in C2_COLUMNS])
+        scan = ScanExec(InMemoryDataSource(schema, [RecordBatch(schema, cols)]), ["a", "b"])
+        sel = SelectionExec(scan, GtExpression(ColumnExpression(0), LiteralLongExpression(1 << 19)))
+        proj = ProjectionExec(sel, Schema([Field("ab", N.TYPE_INT64)]),
+                              [AddExpression(ColumnExpression(0), ColumnExpression(1))])
+        fused = fuse(proj)
+        cc = (N.QeColumn * 2)(*[x.as_c() for x in cols])
+        o = DeviceColumn.empty(N.TYPE_INT64, n, False, ctx=ctx)
+        oc = (N.QeColumn * 1)(o.as_c())
+        cnt = N.C.c_int64()
+
+        def run_large():
+            oc[0].length = n
+            N.check(N.lib().qe_select_project(ctx.handle, cc, 2, N.C.byref(fused.spec), oc, N.C.byref(cnt)))
+
+        ms_l = timed(run_large)
+        report("C2 shape at 1B rows: fused select+project (qe_select_project call)", n, 16 + 8 * cnt.value / n, ms_l,
+               selected=cnt.value)
+        del cols, o
     if "C3" in which:
         n = 100_000_000
         col = generate_column(C3_COLUMNS[0], n, 0, 42, ctx)
