@@ -30,6 +30,7 @@ struct qe_csv_table {
   int64_t stride = 0;             // entries per array of the block (>= rows + 1)
   int32_t nproj = 0;
   void* block = nullptr;          // per projected column: start i64, len i64, byte start i64 [stride], quoted u8
+  uint8_t* stage_block = nullptr; // per projected column: 16 bytes per row (short unquoted values)
   std::vector<int64_t> total;     // per projected column: bytes
   std::vector<qe_column> cols;    // materialised views (qe_csv_column), built on first request
   std::vector<void*> owned;
@@ -37,6 +38,7 @@ struct qe_csv_table {
   int64_t* len(int c) { return (int64_t*)block + (size_t)(nproj + c) * stride; }
   int64_t* bstart(int c) { return (int64_t*)block + (size_t)(2 * nproj + c) * stride; }
   uint8_t* quoted(int c) { return (uint8_t*)((int64_t*)block + (size_t)3 * nproj * stride) + (size_t)c * stride; }
+  uint8_t* stage(int c) { return stage_block + (size_t)c * stride * 16; }
 };
 
 namespace qe {
@@ -256,6 +258,7 @@ struct FieldArgs {
   int64_t* start[CSV_MAX_FIELDS];     // per column: byte position of the (trimmed, unquoted) value
   int64_t* len[CSV_MAX_FIELDS];       // per column: output length (after unescaping)
   uint8_t* quoted[CSV_MAX_FIELDS];    // per column: 1 if "" sequences must be unescaped
+  uint8_t* stage[CSV_MAX_FIELDS];     // per column: 16 bytes per row, the value when unquoted and <= 16 bytes
   int32_t max_field;                  // largest projected field index
   int32_t delim;
   uint64_t low_mask;                  // bit f: field f < 64 is projected (skips the table lookup)
@@ -266,12 +269,38 @@ struct GBytes {
   const uint8_t* d;
   int64_t nbytes;
   __device__ __forceinline__ uint32_t operator[](int64_t i) const { return d[i]; }
+  __device__ __forceinline__ uint4 bytes16(int64_t s, int64_t n) const {  // bytes [s, s + n), n <= 16
+    uint64_t lo = 0, hi = 0;
+    for (int64_t k = 0; k < n; ++k) {
+      const uint64_t b = d[s + k];
+      if (k < 8) lo |= b << (8 * k);
+      else hi |= b << (8 * (k - 8));
+    }
+    return make_uint4((uint32_t)lo, (uint32_t)(lo >> 32), (uint32_t)hi, (uint32_t)(hi >> 32));
+  }
   __device__ __forceinline__ Lane16 load16(int64_t a) const { return qe::load16(d, nbytes, a); }
 };
 struct LBytes {
   const uint8_t* L;  // LDS copy of [base, base + span), base 16-byte aligned
   int64_t base;
   __device__ __forceinline__ uint32_t operator[](int64_t i) const { return L[i - base]; }
+  // bytes [s, s + n), n <= 16, zero-padded: two aligned 16-byte LDS reads and a funnel shift
+  __device__ __forceinline__ uint4 bytes16(int64_t s, int64_t n) const {
+    const int64_t o = s - base;
+    const int sh = (int)(o & 15);
+    const uint4 a = *(const uint4*)(L + (o - sh));
+    unsigned __int128 v = ((unsigned __int128)(((uint64_t)a.w << 32) | a.z) << 64) | (((uint64_t)a.y << 32) | a.x);
+    if (sh) {
+      v >>= 8 * sh;
+      if (sh + n > 16) {
+        const uint4 b = *(const uint4*)(L + (o - sh) + 16);
+        const unsigned __int128 w = ((unsigned __int128)(((uint64_t)b.w << 32) | b.z) << 64) | (((uint64_t)b.y << 32) | b.x);
+        v |= w << (128 - 8 * sh);
+      }
+    }
+    if (n < 16) v &= (((unsigned __int128)1) << (8 * n)) - 1;
+    return make_uint4((uint32_t)v, (uint32_t)(v >> 32), (uint32_t)(v >> 64), (uint32_t)(v >> 96));
+  }
   __device__ __forceinline__ Lane16 load16(int64_t a) const {  // a: 16-byte aligned, inside the copy
     const uint4 t = *(const uint4*)(L + (a - base));
     Lane16 v;
@@ -318,6 +347,9 @@ __device__ void record_field(const D& d, const FieldArgs& A, int f, int64_t s, i
   A.start[sl][row] = s;
   A.len[sl][row] = len;
   A.quoted[sl][row] = q;
+  // Short unquoted values are also staged densely, 16 bytes per row, while the line sits in LDS;
+  // the column build then reads them there instead of gathering from every line of the file.
+  if (!q && len <= 16) *(uint4*)(A.stage[sl] + row * 16) = d.bytes16(s, len);
 }
 
 // One record [s, e): the projected fields' ranges into row `r` (missing fields read as "").
@@ -366,6 +398,7 @@ __device__ __forceinline__ void stage_args(FieldArgs& S, const FieldArgs& A) {
     S.start[threadIdx.x] = A.start[threadIdx.x];
     S.len[threadIdx.x] = A.len[threadIdx.x];
     S.quoted[threadIdx.x] = A.quoted[threadIdx.x];
+    S.stage[threadIdx.x] = A.stage[threadIdx.x];
   }
   if (threadIdx.x == 0) {
     S.max_field = A.max_field;
@@ -460,9 +493,10 @@ __global__ void k_csv_offsets(const int64_t* __restrict__ starts64, int64_t n, i
 // took 132 / 95 us for tripdata's fare_amount / VendorID columns.)
 __global__ void __launch_bounds__(256) k_csv_copy_wave(const uint8_t* __restrict__ data, const int64_t* __restrict__ start,
                                                        const int64_t* __restrict__ len, const uint8_t* __restrict__ quoted,
-                                                       const int32_t* __restrict__ offs, int64_t n, uint8_t* __restrict__ out) {
+                                                       const uint8_t* __restrict__ stage, const int32_t* __restrict__ offs,
+                                                       int64_t n, uint8_t* __restrict__ out) {
   __shared__ int32_t s_o[4][65];
-  __shared__ int64_t s_s[4][64];
+  __shared__ int64_t s_s[4][64];  // source of the row's first byte: file position, or -1 - row (staged)
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int64_t nw = ((int64_t)gridDim.x * blockDim.x) >> 6;
   for (int64_t r0 = (((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6) * 64; r0 < n; r0 += nw * 64) {
@@ -488,7 +522,7 @@ __global__ void __launch_bounds__(256) k_csv_copy_wave(const uint8_t* __restrict
     }
     const int64_t rend = r0 + 64 < n ? r0 + 64 : n;
     s_o[w][lane] = in ? offs[r] : 0x7FFFFFFF;
-    s_s[w][lane] = s;
+    s_s[w][lane] = (in && len[r] <= 16) ? -1 - r : s;  // unquoted here: short values are staged
     if (lane == 0) s_o[w][64] = offs[rend];
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
@@ -508,7 +542,8 @@ __global__ void __launch_bounds__(256) k_csv_copy_wave(const uint8_t* __restrict
         const int32_t b = j + k;
         if (b >= oend) break;
         while (s_o[w][row + 1] <= b) ++row;
-        out[b] = data[s_s[w][row] + (b - s_o[w][row])];
+        const int64_t src = s_s[w][row];
+        out[b] = src < 0 ? stage[(-1 - src) * 16 + (b - s_o[w][row])] : data[src + (b - s_o[w][row])];
       }
     }
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");  // s_o / s_s are rewritten next
@@ -599,10 +634,13 @@ int csv_parse(qe_ctx* ctx, const uint8_t* data, int64_t nbytes, const qe_csv_opt
   t->stride = nlines + 1;
   QE_TRY(dmalloc(t, (size_t)nproj * (size_t)t->stride * 25 + 64, &p));
   t->block = p;
+  QE_TRY(dmalloc(t, (size_t)nproj * (size_t)t->stride * 16, &p));
+  t->stage_block = (uint8_t*)p;
   for (int c = 0; c < nproj; ++c) {
     A.start[c] = t->start(c);
     A.len[c] = t->len(c);
     A.quoted[c] = t->quoted(c);
+    A.stage[c] = t->stage(c);
   }
   int64_t rows = 0;
   if (nlines > 0) {
@@ -669,7 +707,7 @@ int build_column(qe_csv_table* t, int c, int32_t* offsets, uint8_t* values) {
   QE_TRY(launch_check("k_csv_offsets"));
   if (t->total[(size_t)c] > 0) {
     hipLaunchKernelGGL(k_csv_copy_wave, dim3(grid_for(ctx, rows)), dim3(256), 0, ctx->stream, t->data, t->start(c),
-                       t->len(c), t->quoted(c), offsets, rows, values);
+                       t->len(c), t->quoted(c), t->stage(c), offsets, rows, values);
     QE_TRY(launch_check("k_csv_copy_wave"));
   }
   return QE_OK;
