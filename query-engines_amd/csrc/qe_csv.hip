@@ -14,8 +14,9 @@
 //     with '"' (length >= 2) the quotes are removed, "" becomes ", and the result is trimmed again
 //     (K:263 calls String.trim() on every value); a missing trailing field reads as "" (K:263).
 // Pipeline (all HBM-streaming, one wave per 64 KiB segment for the byte passes):
-//   k_csv_quotes   quotes per segment                -> scan -> quote state at segment start
-//   k_csv_terms    record terminators per segment    -> scan -> terminator positions (k_csv_emit)
+//   k_csv_count2   per segment: quotes, and terminators under both starting quote states
+//                  -> scan of quotes (state at segment start) -> pick -> scan -> k_csv_terms<true>:
+//                  terminator positions
 //   k_csv_keep     per line: kept?                   -> scan -> kept-line list
 //   k_csv_fields   per kept row: projected field ranges, unescaped lengths
 //   k_csv_copy_wave per projected column: offsets (scan of lengths) + bytes
@@ -91,27 +92,6 @@ __device__ __forceinline__ bool has_byte(const Lane16& v, uint32_t b) {
     any |= (x - 0x01010101u) & ~x & 0x80808080u;
   }
   return any != 0;
-}
-
-__global__ void __launch_bounds__(256) k_csv_quotes(const uint8_t* __restrict__ data, int64_t nbytes, int64_t nseg,
-                                                    int64_t* __restrict__ seg_q) {
-  const int lane = threadIdx.x & 63;
-  const int64_t seg = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
-  if (seg >= nseg) return;
-  const int64_t base = seg * SEG;
-  int q = 0;
-  for (int step = 0; step < SEG / 1024; step += 4) {  // 4 loads in flight per lane
-    Lane16 v[4];
-#pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      const int64_t pos = base + (step + u) * 1024 + lane * 16;
-      v[u] = pos < nbytes ? load16(data, nbytes, pos) : Lane16{{0, 0, 0, 0}};
-    }
-#pragma unroll
-    for (int u = 0; u < 4; ++u) q += has_byte(v[u], '"') ? quotes16(v[u]) : 0;
-  }
-  for (int d = 32; d >= 1; d >>= 1) q += __shfl_xor(q, d);
-  if (lane == 0) seg_q[seg] = q;
 }
 
 // Terminator mask (bit k = byte k ends a record) of a lane's 16 bytes, given the quote state at
@@ -226,6 +206,77 @@ __global__ void __launch_bounds__(256) k_csv_terms(const uint8_t* __restrict__ d
     count += total;
   }
   if (!EMIT && lane == 0) seg_t[seg] = count;
+}
+
+// One read of the file for the counting pass: per segment its quote count and its terminator
+// count under both possible quote states at the segment's first byte (the state is the parity of
+// all earlier quotes, known only after a scan of the quote counts). A lane without a quote gets
+// both hypotheses from one mask: inside quotes nothing terminates. Replaces a quote pass plus a
+// terminator pass that needed the scanned quote counts (two reads of the file).
+__global__ void __launch_bounds__(256) k_csv_count2(const uint8_t* __restrict__ data, int64_t nbytes, int64_t nseg,
+                                                    int64_t* __restrict__ seg_q, int64_t* __restrict__ seg_t0,
+                                                    int64_t* __restrict__ seg_t1) {
+  const int lane = threadIdx.x & 63;
+  const int64_t seg = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  if (seg >= nseg) return;
+  const int64_t base = seg * SEG;
+  const uint64_t below = (1ull << lane) - 1;
+  uint32_t rel = 0;  // parity of this segment's quotes before the current step
+  int q = 0, c0 = 0, c1 = 0;
+  Lane16 vq[4];
+  for (int step = 0; step < SEG / 1024; ++step) {
+    const int64_t row0 = base + step * 1024;
+    if (row0 >= nbytes) break;
+    const int64_t pos = row0 + lane * 16;
+    if ((step & 3) == 0) {
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int64_t pu = pos + u * 1024;
+        vq[u] = pu < nbytes ? load16(data, nbytes, pu) : Lane16{{0, 0, 0, 0}};
+      }
+    }
+    Lane16 v;
+    switch (step & 3) {
+      case 0: v = vq[0]; break;
+      case 1: v = vq[1]; break;
+      case 2: v = vq[2]; break;
+      default: v = vq[3]; break;
+    }
+    const bool hasq = has_byte(v, '"');
+    const int nq = hasq ? quotes16(v) : 0;
+    q += nq;
+    const uint64_t par = __ballot(nq & 1);
+    const uint32_t x = rel ^ ((uint32_t)__popcll(par & below) & 1u);  // state at this lane's first byte if the segment starts outside quotes
+    uint32_t next = (uint32_t)__shfl_down((int)(v.w[0] & 0xFFu), 1);
+    if (lane == 63) next = (v.byte(15) == '\r' && pos + 16 < nbytes) ? data[pos + 16] : 0u;
+    uint32_t dummy;
+    if (nq == 0) {
+      const int m = __popc(terms16(v, next, nbytes, pos, 0u, &dummy));
+      if (x) c1 += m;
+      else c0 += m;
+    } else {
+      c0 += __popc(terms16(v, next, nbytes, pos, x, &dummy));
+      c1 += __popc(terms16(v, next, nbytes, pos, x ^ 1u, &dummy));
+    }
+    rel ^= (uint32_t)__popcll(par) & 1u;
+  }
+  for (int d = 32; d >= 1; d >>= 1) {
+    q += __shfl_xor(q, d);
+    c0 += __shfl_xor(c0, d);
+    c1 += __shfl_xor(c1, d);
+  }
+  if (lane == 0) {
+    seg_q[seg] = q;
+    seg_t0[seg] = c0;
+    seg_t1[seg] = c1;
+  }
+}
+
+// Terminator count of each segment under its actual starting quote state.
+__global__ void k_csv_pick(const int64_t* __restrict__ seg_qs, const int64_t* __restrict__ t0,
+                           const int64_t* __restrict__ t1, int64_t nseg, int64_t* __restrict__ seg_t) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < nseg; i += (int64_t)gridDim.x * blockDim.x)
+    seg_t[i] = (seg_qs[i] & 1) ? t1[i] : t0[i];
 }
 
 // Line i is [start(i), ends[i]) with start(0) = 0, start(i) = ends[i-1] + 1.
@@ -591,22 +642,24 @@ int csv_parse(qe_ctx* ctx, const uint8_t* data, int64_t nbytes, const qe_csv_opt
   // ---- record terminators
   const int64_t nseg = (int64_t)div_up((uint64_t)(nbytes > 0 ? nbytes : 1), SEG);
   void* p;
-  QE_TRY(ctx_workspace(ctx, 0, (size_t)(4 * nseg + 4) * 8, &p));
+  QE_TRY(ctx_workspace(ctx, 0, (size_t)(6 * nseg + 4) * 8, &p));
   int64_t* seg_q = (int64_t*)p;
   int64_t* seg_qs = seg_q + nseg;
   int64_t* seg_t = seg_qs + nseg + 1;
   int64_t* seg_ts = seg_t + nseg;
+  int64_t* seg_t0 = seg_ts + nseg + 1;
+  int64_t* seg_t1 = seg_t0 + nseg;
   const int wgrid = (int)div_up((uint64_t)nseg, 4);  // 4 waves per 256-thread block
   if (nbytes > 0) {
-    hipLaunchKernelGGL(k_csv_quotes, dim3(wgrid), dim3(256), 0, ctx->stream, data, nbytes, nseg, seg_q);
-    QE_TRY(launch_check("k_csv_quotes"));
+    hipLaunchKernelGGL(k_csv_count2, dim3(wgrid), dim3(256), 0, ctx->stream, data, nbytes, nseg, seg_q, seg_t0, seg_t1);
+    QE_TRY(launch_check("k_csv_count2"));
   } else {
     QE_HIP(hipMemsetAsync(seg_q, 0, 8, ctx->stream));
+    QE_HIP(hipMemsetAsync(seg_t0, 0, 16, ctx->stream));
   }
   QE_TRY(exclusive_scan_i64(ctx, seg_q, seg_qs, nseg));
-  hipLaunchKernelGGL(k_csv_terms<false>, dim3(wgrid), dim3(256), 0, ctx->stream, data, nbytes, nseg, seg_qs, seg_t,
-                     nullptr, nullptr);
-  QE_TRY(launch_check("k_csv_terms"));
+  hipLaunchKernelGGL(k_csv_pick, dim3(grid_for(ctx, nseg)), dim3(256), 0, ctx->stream, seg_qs, seg_t0, seg_t1, nseg, seg_t);
+  QE_TRY(launch_check("k_csv_pick"));
   QE_TRY(exclusive_scan_i64(ctx, seg_t, seg_ts, nseg));
   int64_t nterm = 0;
   QE_TRY(read_i64(ctx, seg_ts + nseg, &nterm));
