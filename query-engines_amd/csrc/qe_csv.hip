@@ -45,7 +45,7 @@ struct qe_csv_table {
 namespace qe {
 namespace {
 
-constexpr int SEG = 64 * 1024;  // bytes per wave-task: 64 steps x 64 lanes x 16 B
+constexpr int SEG = 16 * 1024;  // bytes per wave-task: 16 steps x 64 lanes x 16 B
 constexpr int CSV_MAX_FIELDS = 32;
 constexpr int CSV_MAX_FIELD_INDEX = 1024;
 
