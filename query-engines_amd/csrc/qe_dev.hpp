@@ -123,6 +123,9 @@ struct Plan {
   qi64* part_off;  // count: per (bucket, workgroup) record counts; scatter: their exclusive scan
   qi64 part_tw;    // rows per workgroup (count / scatter)
   qi64* part_slice;  // partition aggregate: [0] slice count, then (lo, hi | PART_EXCL) per slice
+  // multi-pass fused aggregate (groups just beyond one LDS table): pass mp_pass of mp_n keeps the
+  // rows whose key hash falls in bucket mp_pass (mp_n = 0: every row)
+  qi32 mp_n, mp_pass;
 };
 
 // ---- scalar helpers ---------------------------------------------------------------------------------

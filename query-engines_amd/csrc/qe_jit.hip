@@ -417,6 +417,10 @@ bool gen_fused_source(const Plan& P, int log2, std::string* src, size_t* lds_byt
   emit_col_loads(P, o, ~0u);
   emit_active_rows(P, o, true);
   emit_keys(P, o);
+  if (P.mp_n > 1)
+    o << "#pragma unroll\n    for (int r = 0; r < 4; ++r)\n"
+      << "      if (((act >> r) & 1) && (qu32)__umul64hi(fmix64((qu64)key[r]), (qu64)P.mp_n) != (qu32)P.mp_pass) act &= ~(1u << r);\n"
+      << "    if (act == 0) continue;\n";
   emit_agg_rows(P, o, val, ok, "P.row_base + r0 + 128 * (r >> 1) + (r & 1)", "r0 + 128 * (r >> 1) + (r & 1)");
   o << "  }\n";
   emit_flush(P, o);

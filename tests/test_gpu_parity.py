@@ -619,6 +619,57 @@ def test_hashagg_partitioned(agg_ctx, ngroups, expected, vtype):
     assert_groups_equal(result_dict(keys, aggs), ref, ALL_FNS)
 
 
+MP_I64 = [N.AGG_SUM, N.AGG_COUNT_STAR, N.AGG_MIN, N.AGG_MAX]
+MP_F64 = [N.AGG_SUM, N.AGG_COUNT, N.AGG_MAX]
+
+
+@pytest.mark.parametrize("vtype,ngroups,expected", [("i64", 2500, 2500), ("i64", 40_000, 2000),
+                                                    ("f64", 1200, 1200), ("f64", 40_000, 1200)])
+def test_hashagg_multipass(agg_ctx, vtype, ngroups, expected):
+    """Expected groups just beyond one LDS table: 2 passes of the fused kernel, each keeping one
+    bucket of key hashes (also when far more groups turn up than expected: overflow records and
+    deferred rows inside a pass). Nullable keys and inputs, fp64 MAX order across two batches."""
+    rng = np.random.default_rng(ngroups * 3 + expected)
+    n = 600_000
+    k = rng.integers(0, ngroups, n).astype(np.int64) * 104729 + 11
+    kv = rng.random(n) > 0.01
+    if vtype == "i64":
+        fns, t = MP_I64, N.TYPE_INT64  # non-nullable: the LDS table then holds 2048 slots
+        x = rng.integers(-2**62, 2**62, n).astype(np.int64)
+        xv = None
+    else:
+        fns, t = MP_F64, N.TYPE_FLOAT64
+        x, xv = _rand(rng, n, "f64", 0.1)
+    st = HashAggregateState(agg_ctx, [N.TYPE_INT64], [(f, t) for f in fns], expected)
+    for s, e in ((0, 250_001), (250_001, n)):
+        st.update([dcol(agg_ctx, N.TYPE_INT64, k[s:e], kv[s:e])],
+                  [dcol(agg_ctx, t, x[s:e], None if xv is None else xv[s:e])] * len(fns))
+        if agg_ctx.kernel_mode == "jit" and s == 0:
+            assert st.last_kernel_kind()[1].startswith("multi-pass"), st.last_kernel_kind()
+    keys, aggs = st.finalize()
+    ref = S.group_aggregate([k], [kv], [x] * len(fns), [xv] * len(fns), fns)
+    assert_groups_equal(result_dict(keys, aggs), ref, fns)
+
+
+def test_fused_c4_multipass_vs_oracle(agg_ctx):
+    from kquery.datasource import C4_COLUMNS, ColumnSpec, generate_column
+
+    n, groups = 2_000_003, 2400
+    kspec = ColumnSpec("k", N.TYPE_INT64, N.GEN_MOD, groups, 0)
+    cols = [generate_column(kspec, n, 0, 42, agg_ctx)] + [generate_column(s, n, 0, 42, agg_ctx) for s in C4_COLUMNS[1:]]
+    st = HashAggregateState(agg_ctx, [N.TYPE_INT64], C4_AGGS, groups)
+    st.update_fused(cols, _c4_spec())
+    if agg_ctx.kernel_mode == "jit":
+        assert st.last_kernel_kind()[1].startswith("multi-pass"), st.last_kernel_kind()
+    kk, aa = st.finalize()
+    k, _ = gen.generate(gen.GEN_MOD, groups, 42, 0, 0, n)
+    a, _ = gen.generate(gen.GEN_MOD, 1 << 20, 42, 1, 0, n)
+    b, _ = gen.generate(gen.GEN_MOD, 1 << 20, 42, 2, 0, n)
+    ref = S.group_aggregate([k], [None], [S.arith(S.OP_ADD, a, None, b, None)[0], None, a, b], [None] * 4, C4_FNS,
+                            a > (1 << 19))
+    assert_groups_equal(result_dict(kk, aa), ref, C4_FNS)
+
+
 def test_hashagg_adapts_to_partitioned(agg_ctx):
     """expected_groups left at its default while the batches hold 300K groups: the first batch
     grows the global table, and the later batches switch to the partitioned update by themselves."""
