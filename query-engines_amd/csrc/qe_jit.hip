@@ -735,6 +735,7 @@ bool gen_selproj_source(const Plan& P, const int32_t* out_kind, int nout, std::s
     << "extern \"C\" __global__ void __launch_bounds__(256) qe_selproj(const Plan P) {\n"
     << "  constexpr int R = " << R << ";\n"
     << "  constexpr qu64 F_AGG = 1ull << 62, F_INC = 2ull << 62, VMASK = (1ull << 62) - 1;\n"
+    << "  constexpr bool PERSIST = " << (persistent ? "true" : "false") << ";\n"
     << "  __shared__ qu32 s_cnt[R * 4];\n  __shared__ qu64 s_base;\n  __shared__ qu32 s_tile, s_total;\n"
     << "  __shared__ qi64 s_out[" << ((size_t)nout * R * 256 * 8 <= 64 * 1024 ? nout * R * 256 : 1) << "];\n"
     << "  const int t = threadIdx.x, lane = t & 63, w = t >> 6;\n";
@@ -826,8 +827,13 @@ bool gen_selproj_source(const Plan& P, const int32_t* out_kind, int nout, std::s
       "      for (;;) {\n"
       "        const qi64 idx = pos - lane;\n"
       "        qu64 v;\n"
+      "        qu32 spins = 0;\n"
       "        do { v = idx >= 0 ? __hip_atomic_load(&st[idx], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : F_INC; }\n"
-      "        while (__any((v >> 62) == 0));\n"
+      "        while (__any((v >> 62) == 0) && (!PERSIST || ++spins < (1u << 20)));\n"
+      // persistent grid only: a predecessor that never publishes means a workgroup was not
+      // resident after all; flag it (the host reruns with counter-ordered tiles) and let every
+      // wave finish instead of hanging the device
+      "        if (PERSIST && spins >= (1u << 20)) { if (lane == 0) __hip_atomic_store(&P.t.ctl[2], 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); v = F_INC; }\n"
       "        const qu64 incm = __ballot((v >> 62) == 2);\n"
       "        qu64 c = v & VMASK;\n"
       "        if (incm) { const int first = __ffsll((long long)incm) - 1; if (lane > first) c = 0; }\n"

@@ -7,6 +7,8 @@
 //
 // The kernel is generated per plan shape and compiled with hipRTC (qe_jit.hip gen_selproj_source);
 // without hipRTC the call returns QE_ERR_UNSUPPORTED and callers run the per-family operators.
+#include <stdio.h>
+
 #include "qe_internal.hpp"
 
 using namespace qe;
@@ -53,48 +55,67 @@ extern "C" int qe_select_project(qe_ctx* ctx, const qe_column* cols, int32_t nco
   // Tile order: a persistent grid (every workgroup resident, tiles assigned statically) or one
   // tile per workgroup with ids from a device counter in start order (QE_SELPROJ_PERSIST=0). The
   // counter is one word every workgroup hits: ~88 returning atomics/us, a floor of 2.8 ms for
-  // 1B rows in 4096-row tiles.
-  static const bool persist = [] {
+  // 1B rows in 4096-row tiles. Residency comes from the grid size alone, and the occupancy query
+  // is advisory (it can over-report by a block per CU), so the persistent grid keeps at most
+  // min(4, occupancy - 1) blocks per CU, and its look-back spins are bounded: a tile whose
+  // predecessor never publishes flags ctl[2], and the call reruns with counter-ordered tiles.
+  static const bool persist_env = [] {
     const char* e = getenv("QE_SELPROJ_PERSIST");
     return !(e && e[0] == '0');
   }();
-  std::string src;
-  if (!gen_selproj_source(P, out_kind, spec->nout, &src, persist))
-    return fail(QE_ERR_UNSUPPORTED, "plan shape is outside the select-project generator");
-  hipFunction_t fn;
-  int bpc = 0;
-  QE_TRY(jit_kernel(ctx, src, &fn, &bpc, "qe_selproj", 256));
+  static const int wg_cap = [] {
+    const char* e = getenv("QE_SELPROJ_WG_PER_CU");
+    return e && *e ? std::max(1, atoi(e)) : 4;
+  }();
   // validity: nullable outputs start all-null (the kernel sets bits); others all-valid
-  for (int k = 0; k < spec->nout; ++k) {
-    if (!outs[k].validity) continue;
-    const size_t vb = (size_t)div_up((uint64_t)(n > 0 ? n : 1), 32) * 4;
-    QE_HIP(hipMemsetAsync(outs[k].validity, (out_kind[k] & 0x100) ? 0 : 0xFF, vb, ctx->stream));
-  }
+  auto init_validity = [&]() -> int {
+    for (int k = 0; k < spec->nout; ++k) {
+      if (!outs[k].validity) continue;
+      const size_t vb = (size_t)div_up((uint64_t)(n > 0 ? n : 1), 32) * 4;
+      QE_HIP(hipMemsetAsync(outs[k].validity, (out_kind[k] & 0x100) ? 0 : 0xFF, vb, ctx->stream));
+    }
+    return QE_OK;
+  };
+  QE_TRY(init_validity());
   *out_count = 0;
   if (n > 0) {
     const int R = selproj_rows_per_thread(P);
     const int64_t tiles = (int64_t)div_up((uint64_t)n, (uint64_t)R * 256);
     QE_CHECK(tiles < (1ll << 31), QE_ERR_CAPACITY, "too many rows for one select-project call");
     void* s;
-    QE_TRY(ctx_scratch(ctx, (size_t)(tiles + 2) * 8, &s));
+    QE_TRY(ctx_scratch(ctx, (size_t)(tiles + 3) * 8, &s));
     qu64* ctl = (qu64*)s;
-    QE_HIP(hipMemsetAsync(s, 0, (size_t)(tiles + 2) * 8, ctx->stream));
     P.t.ctl = ctl;
-    P.t.keys = (qi64*)(ctl + 2);
+    P.t.keys = (qi64*)(ctl + 3);
     P.t.cap = (qu64)tiles;
-    static const int wg_cap = [] {
-      const char* e = getenv("QE_SELPROJ_WG_PER_CU");
-      return e && *e ? std::max(1, atoi(e)) : 64;
-    }();
-    const int64_t grid =
-        persist ? std::min<int64_t>(tiles, (int64_t)ctx->num_cus * std::max(1, std::min(bpc, wg_cap))) : tiles;
-    QE_TRY(jit_launch(ctx, fn, (int)grid, P, 256));
-    QE_TRY(launch_check("qe_selproj"));
     void* pin;
-    QE_TRY(ctx_pinned(ctx, 8, &pin));
-    QE_HIP(hipMemcpyAsync(pin, ctl + 1, 8, hipMemcpyDeviceToHost, ctx->stream));
-    QE_HIP(hipStreamSynchronize(ctx->stream));
-    *out_count = *(int64_t*)pin;
+    QE_TRY(ctx_pinned(ctx, 16, &pin));
+    for (int attempt = 0; attempt < 2; ++attempt) {
+      const bool persist = persist_env && attempt == 0;
+      std::string src;
+      if (!gen_selproj_source(P, out_kind, spec->nout, &src, persist))
+        return fail(QE_ERR_UNSUPPORTED, "plan shape is outside the select-project generator");
+      hipFunction_t fn;
+      int bpc = 0;
+      QE_TRY(jit_kernel(ctx, src, &fn, &bpc, "qe_selproj", 256));
+      QE_HIP(hipMemsetAsync(s, 0, (size_t)(tiles + 3) * 8, ctx->stream));
+      // QE_SELPROJ_OVERSUB (tests only) multiplies the persistent grid past residency, to exercise
+      // the bounded look-back and the rerun
+      const char* ov = getenv("QE_SELPROJ_OVERSUB");
+      const int oversub = ov && *ov ? std::max(1, std::min(64, atoi(ov))) : 1;
+      const int per_cu = std::max(1, std::min(wg_cap, bpc - 1));
+      const int64_t grid = persist ? std::min<int64_t>(tiles, (int64_t)ctx->num_cus * per_cu * oversub) : tiles;
+      QE_TRY(jit_launch(ctx, fn, (int)grid, P, 256));
+      QE_TRY(launch_check("qe_selproj"));
+      QE_HIP(hipMemcpyAsync(pin, ctl + 1, 16, hipMemcpyDeviceToHost, ctx->stream));
+      QE_HIP(hipStreamSynchronize(ctx->stream));
+      *out_count = ((int64_t*)pin)[0];
+      if (((int64_t*)pin)[1] == 0) break;  // else: a persistent workgroup was not resident
+      QE_CHECK(persist, QE_ERR_DEVICE, "select-project look-back did not complete");
+      fprintf(stderr, "qe: select-project persistent look-back stalled (grid %lld); rerunning with counter-ordered tiles\n",
+              (long long)grid);
+      QE_TRY(init_validity());  // the aborted launch may have set bits anywhere
+    }
   }
   for (int k = 0; k < spec->nout; ++k) outs[k].length = *out_count;
   return QE_OK;

@@ -158,3 +158,26 @@ def test_jit_off_falls_back_to_unfused(gpu_ctx):
     finally:
         N.check(N.lib().qe_ctx_set_jit(gpu_ctx.handle, 1))
     assert (got == want).all()
+
+
+def test_persistent_grid_not_resident_reruns(gpu_ctx, monkeypatch, capfd):
+    """The persistent select-project grid assumes every workgroup is resident. Oversubscribed 8x
+    on purpose (QE_SELPROJ_OVERSUB, a test knob), tiles wait on predecessors that have not
+    started; their bounded look-back flags it, the launch drains, and the call reruns with
+    counter-ordered tiles. Same bit-exact result, and no hang."""
+    from kquery import native as N
+    from kquery.datasource import C2_COLUMNS, generate_column
+
+    monkeypatch.setenv("QE_SELPROJ_OVERSUB", "8")
+    n, k = 80_000_000, 1 << 19  # >= 2 tiles per workgroup: every resident one waits on a later one
+    cols = [generate_column(s, n, 0, 42, gpu_ctx) for s in C2_COLUMNS]
+    spec = _spec(N, [(0, N.OP_GT, -1, k)], [[(N.TOK_COL, 0, None), (N.TOK_COL, 1, None), (N.TOK_ADD, 0, None)]])
+    cnt, (ab,) = _run(gpu_ctx, cols, spec, [N.TYPE_INT64])
+    a_h, _ = gen.generate(C2_COLUMNS[0].dist, C2_COLUMNS[0].param, 42, C2_COLUMNS[0].col_id, 0, n)
+    b_h, _ = gen.generate(C2_COLUMNS[1].dist, C2_COLUMNS[1].param, 42, C2_COLUMNS[1].col_id, 0, n)
+    m, mv = S.cmp(S.OP_GT, a_h, None, k, None)
+    fa, fb = S.filter_columns(m, mv, [a_h, b_h])
+    want, _ = S.arith(S.OP_ADD, fa, None, fb, None)
+    assert cnt == len(fa)
+    assert (ab.to_numpy() == want).all()
+    assert "rerunning with counter-ordered tiles" in capfd.readouterr().err
