@@ -280,8 +280,18 @@ __global__ void __launch_bounds__(ENC_THREADS) k_dict_encode(DictDev D, const in
                                                              int32_t* __restrict__ codes, uint32_t* __restrict__ retry) {
   __shared__ LdsCache C;
   __shared__ int wg_full;  // a lane of this workgroup saw the dictionary full: the batch reruns
+  // Rows whose key another wave had claimed but not yet published: kept here and resolved after
+  // this workgroup's loop, when the claimers have long published. At a batch's start every wave
+  // meets every new key at once (3 tripdata keys sent ~260K rows to a 66 us retry pass); only
+  // rows past DEF_CAP, or still unpublished then, go to the retry bitmap.
+  constexpr int DEF_CAP = 2048;
+  __shared__ int s_ndef;
+  __shared__ int64_t s_def[DEF_CAP];
   for (int k = threadIdx.x; k < LC_SLOTS; k += blockDim.x) C.state[k] = 0;
-  if (threadIdx.x == 0) wg_full = 0;
+  if (threadIdx.x == 0) {
+    wg_full = 0;
+    s_ndef = 0;
+  }
   __syncthreads();
   const int lane = threadIdx.x & 63;
   // every lane runs the same trip count so the wave-level dedup below sees whole waves
@@ -329,9 +339,35 @@ __global__ void __launch_bounds__(ENC_THREADS) k_dict_encode(DictDev D, const in
       codes[i] = (live && c >= 0) ? c : 0;
       if (live && c == R_OVERFLOW) wg_full = 1;
       if (live && c == R_RETRY) {
-        atomicOr(&retry[i >> 5], 1u << (i & 31));
-        atomicAdd(&D.flags[1], 1u);
+        const int d = atomicAdd(&s_ndef, 1);
+        if (d < DEF_CAP) {
+          s_def[d] = i;
+        } else {
+          atomicOr(&retry[i >> 5], 1u << (i & 31));
+          atomicAdd(&D.flags[1], 1u);
+        }
       }
+    }
+  }
+  __syncthreads();
+  const int nd = s_ndef < DEF_CAP ? s_ndef : DEF_CAP;
+  for (int d = threadIdx.x; d < nd; d += blockDim.x) {
+    const int64_t i = s_def[d];
+    const int32_t s0 = offs[i], len = offs[i + 1] - s0;
+    const uint8_t* p = bytes + s0;
+    const uint64_t h = str_hash(p, len);
+    int c = -1;
+    if (len <= LC_BYTES) {
+      uint64_t hd[LC_BYTES / 8];
+      head32(p, len, hd);
+      c = lc_find(C, h, len, hd);
+    }
+    if (c < 0) c = dict_find_or_insert(D, p, len, h);
+    codes[i] = c >= 0 ? c : 0;
+    if (c == R_OVERFLOW) wg_full = 1;
+    if (c == R_RETRY) {
+      atomicOr(&retry[i >> 5], 1u << (i & 31));
+      atomicAdd(&D.flags[1], 1u);
     }
   }
 }
