@@ -433,13 +433,14 @@ bool gen_fused_source(const Plan& P, int log2, std::string* src, size_t* lds_byt
 // When the expected groups do not fit a workgroup's LDS table, every row would otherwise update
 // the global table with device-scope atomics (~30 G atomics/s chip-wide: 2 % of the HBM roofline
 // at 64K+ groups). Instead the rows are partitioned by key hash so that each workgroup of the
-// aggregation pass sees a contiguous slice of records drawn from at most two buckets, whose groups
-// fit its LDS table:
+// aggregation pass sees a slice of one bucket's records, whose groups fit its LDS table:
 //   qe_pcount   per (bucket, workgroup) counts of the selected rows (reads predicate + key columns)
 //   (exclusive scan of the counts, bucket-major: records of one bucket are contiguous)
 //   qe_pscatter predicate, key, aggregate inputs -> one fixed-width record per selected row at
-//               its bucket's next position (LDS cursors)
-//   qe_pagg     LDS aggregation of a contiguous record slice, then the usual flush
+//               its bucket's next position (LDS cursors, or an LDS counting sort per tile)
+//   k_part_slices (qe_hashagg.hip) slices inside bucket boundaries; a one-slice bucket is exclusive
+//   qe_pagg     LDS aggregation of a record slice, then the flush (plain read-modify-writes when
+//               the slice is exclusive)
 // Record layout (rec_layout): key | aggregate input values | [flags: bit 0 null key, bit 1+j input j
 // valid] | [global row index, fp64 MIN/MAX only], padded to 16 bytes.
 PartLayout part_layout(const Plan& P) {
@@ -711,11 +712,14 @@ bool gen_pagg_source(const Plan& P, int log2, std::string* src, size_t* lds_byte
 // are coalesced and (stripe, wave) chunks are in row order). Per tile: predicate -> ballots ->
 // per-(stripe, wave) counts -> wave-0 exclusive scan -> decoupled look-back over the previous
 // tiles' status words (flag in bits 62-63: 1 aggregate, 2 inclusive prefix) -> each selected row
-// evaluates the projection programs and stores at its global position. Tile ids come from an
-// atomic counter, so every predecessor of a waiting tile is already running.
+// evaluates the projection programs and stores at its global position. Tile order: a persistent
+// grid of resident workgroups walking the tiles statically (bounded look-back spins; a stall sets
+// t.ctl[2] and the host reruns), or ids from an atomic counter, so that every predecessor of a
+// waiting tile is already running (qe_selproj.hip).
 // Pointers ride in the Plan's table fields: t.acc[k] output k values, t.nn[k] output k validity
 // words (nullable outputs only), t.keys tile status, t.ctl[0] tile counter, t.ctl[1] total,
-// t.cap number of tiles. out_kind[k] = byte width (8, 4, 1) | 0x100 if the output is nullable.
+// t.ctl[2] stall flag, t.cap number of tiles. out_kind[k] = byte width (8, 4, 1) | 0x100 if the
+// output is nullable.
 // (Measured alternatives, C2 10M rows: a persistent grid pulling tiles, 73 us; a look-back
 // reading 4 windows per round trip, 87 us; this one-tile-per-workgroup, one-window form, 64 us.)
 // Non-temporal input loads once the inputs exceed the 256 MB MALL (QE_SELPROJ_NT=0/1 forces).
