@@ -223,6 +223,7 @@ __global__ void __launch_bounds__(256) k_csv_count2(const uint8_t* __restrict__ 
   const uint64_t below = (1ull << lane) - 1;
   uint32_t rel = 0;  // parity of this segment's quotes before the current step
   int q = 0, c0 = 0, c1 = 0;
+  int64_t l0 = -1, l1 = -1;  // last terminator position under each hypothesis
   Lane16 vq[4];
   for (int step = 0; step < SEG / 1024; ++step) {
     const int64_t row0 = base + step * 1024;
@@ -251,12 +252,24 @@ __global__ void __launch_bounds__(256) k_csv_count2(const uint8_t* __restrict__ 
     if (lane == 63) next = (v.byte(15) == '\r' && pos + 16 < nbytes) ? data[pos + 16] : 0u;
     uint32_t dummy;
     if (nq == 0) {
-      const int m = __popc(terms16(v, next, nbytes, pos, 0u, &dummy));
-      if (x) c1 += m;
-      else c0 += m;
+      const uint32_t mm = terms16(v, next, nbytes, pos, 0u, &dummy);
+      if (mm) {
+        const int64_t last = pos + 31 - __builtin_clz(mm);
+        if (x) {
+          c1 += __popc(mm);
+          l1 = last;
+        } else {
+          c0 += __popc(mm);
+          l0 = last;
+        }
+      }
     } else {
-      c0 += __popc(terms16(v, next, nbytes, pos, x, &dummy));
-      c1 += __popc(terms16(v, next, nbytes, pos, x ^ 1u, &dummy));
+      const uint32_t m0 = terms16(v, next, nbytes, pos, x, &dummy);
+      const uint32_t m1 = terms16(v, next, nbytes, pos, x ^ 1u, &dummy);
+      c0 += __popc(m0);
+      c1 += __popc(m1);
+      if (m0) l0 = pos + 31 - __builtin_clz(m0);
+      if (m1) l1 = pos + 31 - __builtin_clz(m1);
     }
     rel ^= (uint32_t)__popcll(par) & 1u;
   }
@@ -264,20 +277,32 @@ __global__ void __launch_bounds__(256) k_csv_count2(const uint8_t* __restrict__ 
     q += __shfl_xor(q, d);
     c0 += __shfl_xor(c0, d);
     c1 += __shfl_xor(c1, d);
+    l0 = max(l0, (int64_t)__shfl_xor(l0, d));
+    l1 = max(l1, (int64_t)__shfl_xor(l1, d));
   }
   if (lane == 0) {
     seg_q[seg] = q;
     seg_t0[seg] = c0;
     seg_t1[seg] = c1;
+    seg_t0[2 * nseg + seg] = l0;  // seg_l0 / seg_l1 follow the two count arrays
+    seg_t1[2 * nseg + seg] = l1;
   }
 }
 
-// Terminator count of each segment under its actual starting quote state.
+// Terminator count of each segment under its actual starting quote state, and the file's last
+// terminator position (atomic max into *last, which starts at -1).
 __global__ void k_csv_pick(const int64_t* __restrict__ seg_qs, const int64_t* __restrict__ t0,
-                           const int64_t* __restrict__ t1, int64_t nseg, int64_t* __restrict__ seg_t) {
-  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < nseg; i += (int64_t)gridDim.x * blockDim.x)
-    seg_t[i] = (seg_qs[i] & 1) ? t1[i] : t0[i];
+                           const int64_t* __restrict__ t1, int64_t nseg, int64_t* __restrict__ seg_t,
+                           long long* __restrict__ last) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < nseg; i += (int64_t)gridDim.x * blockDim.x) {
+    const bool odd = seg_qs[i] & 1;
+    seg_t[i] = odd ? t1[i] : t0[i];
+    const int64_t l = odd ? t1[2 * nseg + i] : t0[2 * nseg + i];
+    if (l >= 0) atomicMax(last, (long long)l);
+  }
 }
+
+__global__ void k_csv_set_i64(int64_t* p, int64_t v) { *p = v; }
 
 // Line i is [start(i), ends[i]) with start(0) = 0, start(i) = ends[i-1] + 1.
 __device__ __forceinline__ int64_t line_start(const int64_t* ends, int64_t i) { return i == 0 ? 0 : ends[i - 1] + 1; }
@@ -642,13 +667,14 @@ int csv_parse(qe_ctx* ctx, const uint8_t* data, int64_t nbytes, const qe_csv_opt
   // ---- record terminators
   const int64_t nseg = (int64_t)div_up((uint64_t)(nbytes > 0 ? nbytes : 1), SEG);
   void* p;
-  QE_TRY(ctx_workspace(ctx, 0, (size_t)(6 * nseg + 4) * 8, &p));
+  QE_TRY(ctx_workspace(ctx, 0, (size_t)(8 * nseg + 6) * 8, &p));
   int64_t* seg_q = (int64_t*)p;
   int64_t* seg_qs = seg_q + nseg;
   int64_t* seg_t = seg_qs + nseg + 1;
   int64_t* seg_ts = seg_t + nseg;
-  int64_t* seg_t0 = seg_ts + nseg + 1;
+  int64_t* seg_t0 = seg_ts + nseg + 1;  // then seg_t1 [nseg], seg_l0 [nseg], seg_l1 [nseg]
   int64_t* seg_t1 = seg_t0 + nseg;
+  long long* last_term = (long long*)(seg_t0 + 4 * nseg);
   const int wgrid = (int)div_up((uint64_t)nseg, 4);  // 4 waves per 256-thread block
   if (nbytes > 0) {
     hipLaunchKernelGGL(k_csv_count2, dim3(wgrid), dim3(256), 0, ctx->stream, data, nbytes, nseg, seg_q, seg_t0, seg_t1);
@@ -656,29 +682,39 @@ int csv_parse(qe_ctx* ctx, const uint8_t* data, int64_t nbytes, const qe_csv_opt
   } else {
     QE_HIP(hipMemsetAsync(seg_q, 0, 8, ctx->stream));
     QE_HIP(hipMemsetAsync(seg_t0, 0, 16, ctx->stream));
+    QE_HIP(hipMemsetAsync(seg_t0 + 2, 0xFF, 16, ctx->stream));  // no terminator (nseg == 1)
   }
+  QE_HIP(hipMemsetAsync(last_term, 0xFF, 8, ctx->stream));
   QE_TRY(exclusive_scan_i64(ctx, seg_q, seg_qs, nseg));
-  hipLaunchKernelGGL(k_csv_pick, dim3(grid_for(ctx, nseg)), dim3(256), 0, ctx->stream, seg_qs, seg_t0, seg_t1, nseg, seg_t);
+  hipLaunchKernelGGL(k_csv_pick, dim3(grid_for(ctx, nseg)), dim3(256), 0, ctx->stream, seg_qs, seg_t0, seg_t1, nseg, seg_t,
+                     last_term);
   QE_TRY(launch_check("k_csv_pick"));
   QE_TRY(exclusive_scan_i64(ctx, seg_t, seg_ts, nseg));
-  int64_t nterm = 0;
-  QE_TRY(read_i64(ctx, seg_ts + nseg, &nterm));
+  // one read-back for the terminator count and the last terminator's position
+  int64_t nterm = 0, last_end = -1;
+  {
+    void* pin2;
+    QE_TRY(ctx_pinned(ctx, 16, &pin2));
+    QE_HIP(hipMemcpyAsync(pin2, seg_ts + nseg, 8, hipMemcpyDeviceToHost, ctx->stream));
+    QE_HIP(hipMemcpyAsync((int64_t*)pin2 + 1, last_term, 8, hipMemcpyDeviceToHost, ctx->stream));
+    QE_HIP(hipStreamSynchronize(ctx->stream));
+    nterm = ((int64_t*)pin2)[0];
+    last_end = ((int64_t*)pin2)[1];
+  }
   QE_TRY(ctx_workspace(ctx, 1, (size_t)(3 * nterm + 7) * 8, &p));
   int64_t* ends = (int64_t*)p;
   int64_t* keep = ends + nterm + 2;
   int64_t* kstart = keep + nterm + 2;
-  int64_t last_end = -1;
   if (nterm > 0) {
     hipLaunchKernelGGL(k_csv_terms<true>, dim3(wgrid), dim3(256), 0, ctx->stream, data, nbytes, nseg, seg_qs, nullptr,
                        seg_ts, ends);
     QE_TRY(launch_check("k_csv_terms<emit>"));
-    QE_TRY(read_i64(ctx, ends + nterm - 1, &last_end));
   }
   // bytes after the last terminator form a final record (also an unterminated quote at EOF)
   const int64_t nlines = nterm + (last_end + 1 < nbytes ? 1 : 0);
   if (nlines > nterm) {
-    QE_HIP(hipMemcpyAsync(ends + nterm, &nbytes, 8, hipMemcpyHostToDevice, ctx->stream));
-    QE_HIP(hipStreamSynchronize(ctx->stream));  // &nbytes is a host stack address
+    hipLaunchKernelGGL(k_csv_set_i64, dim3(1), dim3(1), 0, ctx->stream, ends + nterm, nbytes);
+    QE_TRY(launch_check("k_csv_set_i64"));
   }
   // ---- records and their projected fields
   const int64_t first = opt->has_header ? 1 : 0;
@@ -696,6 +732,7 @@ int csv_parse(qe_ctx* ctx, const uint8_t* data, int64_t nbytes, const qe_csv_opt
     A.stage[c] = t->stage(c);
   }
   int64_t rows = 0;
+  bool scanned = false;  // column sizes already known (the all-records fast path)
   if (nlines > 0) {
     // every line a record (the common case): one pass over the lines, no kept-line list
     unsigned long long* nskip = (unsigned long long*)keep;
@@ -704,10 +741,25 @@ int csv_parse(qe_ctx* ctx, const uint8_t* data, int64_t nbytes, const qe_csv_opt
     hipLaunchKernelGGL(k_csv_lines, dim3((unsigned)blocks), dim3(256), 0, ctx->stream, data, nbytes, ends, nlines, first,
                        A, nproj, nskip);
     QE_TRY(launch_check("k_csv_lines"));
-    int64_t skipped = 0;
-    QE_TRY(read_i64(ctx, (const int64_t*)nskip, &skipped));
+    // Speculatively every line a record (the common case): the columns' length scans run now, and
+    // the skipped-line count and the column sizes come back in one read.
+    const int64_t rows_all = std::max<int64_t>(0, nlines - first);
+    for (int c = 0; c < nproj && rows_all > 0; ++c) QE_TRY(exclusive_scan_i64(ctx, A.len[c], t->bstart(c), rows_all));
+    void* pin;
+    QE_TRY(ctx_pinned(ctx, (size_t)(nproj + 1) * 8, &pin));
+    QE_HIP(hipMemcpyAsync(pin, nskip, 8, hipMemcpyDeviceToHost, ctx->stream));
+    for (int c = 0; c < nproj && rows_all > 0; ++c)
+      QE_HIP(hipMemcpyAsync((int64_t*)pin + 1 + c, t->bstart(c) + rows_all, 8, hipMemcpyDeviceToHost, ctx->stream));
+    QE_HIP(hipStreamSynchronize(ctx->stream));
+    const int64_t skipped = ((int64_t*)pin)[0];
     if (skipped == 0) {
-      rows = std::max<int64_t>(0, nlines - first);
+      rows = rows_all;
+      scanned = true;
+      t->total.assign((size_t)nproj, 0);
+      for (int c = 0; c < nproj && rows > 0; ++c) {
+        t->total[(size_t)c] = ((int64_t*)pin)[1 + c];
+        QE_CHECK(t->total[(size_t)c] < (1ll << 31), QE_ERR_CAPACITY, "CSV column %d holds more than 2^31 bytes", c);
+      }
     } else {  // blank or comment lines: kept-line list, then the fields of the kept rows
       hipLaunchKernelGGL(k_csv_keep, dim3(grid_for(ctx, nlines)), dim3(256), 0, ctx->stream, data, ends, nlines, keep);
       QE_TRY(launch_check("k_csv_keep"));
@@ -730,6 +782,7 @@ int csv_parse(qe_ctx* ctx, const uint8_t* data, int64_t nbytes, const qe_csv_opt
     }
   }
   t->rows = rows;
+  if (scanned) return QE_OK;
   // ---- per column: byte positions of the values (scan of lengths) and the column's size
   t->total.assign((size_t)nproj, 0);
   for (int c = 0; c < nproj && rows > 0; ++c) QE_TRY(exclusive_scan_i64(ctx, A.len[c], t->bstart(c), rows));
