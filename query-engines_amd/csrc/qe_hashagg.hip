@@ -1639,7 +1639,8 @@ static int partition_rows(qe_hashagg* h, Plan& P, hipFunction_t* fn, int* grid) 
   P.part_rec = h->part_rec;
   P.part_slice = (qi64*)h->part_slc;
   *grid = (int)max_slices;
-  h->jit_note = "radix-partitioned: " + std::to_string(1 << log2p) + " buckets, " + std::to_string(R) + " records" +
+  h->jit_note = "radix-partitioned: " + std::to_string(1 << log2p) + " buckets, " + std::to_string(R) + " records of " +
+                std::to_string(rb) + " B (" + (L.colmode ? "column" : "value") + " words)" +
                 (staged ? ", staged scatter" : "");
   return QE_OK;
 }

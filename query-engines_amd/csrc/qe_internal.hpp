@@ -68,10 +68,13 @@ int parallel_h2d_copy(qe_ctx* ctx, void* dst, const void* src, size_t n);
 bool gen_fused_source(const qe::Plan& P, int log2, std::string* src, size_t* lds_bytes);
 // Radix-partitioned aggregation for group counts beyond the LDS table (qe_jit.hip).
 struct PartLayout {
-  int words = 0;  // record width in 8-byte words (even)
-  int used = 0;   // words holding fields (the rest is padding)
+  int words = 0;  // record width in 8-byte words
+  // colmode: the record holds the columns the aggregate programs read (col_word) and the
+  // aggregation pass evaluates the programs; otherwise it holds each program's value (val_word)
+  bool colmode = false;
   int val_word[QE_MAX_AGGS] = {};  // word of aggregate j's input value, -1 if it has none
-  int flags_word = -1;             // bit 0 null key, bit 1 + j input j valid; -1 if nothing is nullable
+  int col_word[QE_MAX_COLS] = {};  // colmode: word of column slot c, -1 if no program reads it
+  int flags_word = -1;  // bit 0 null key, bit 1 + j input j valid (colmode: column c valid); -1 if nothing is nullable
   int row_word = -1;               // global row index (fp64 MIN/MAX); -1 if not needed
   bool row = false;
 };

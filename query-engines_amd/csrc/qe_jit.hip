@@ -441,25 +441,57 @@ bool gen_fused_source(const Plan& P, int log2, std::string* src, size_t* lds_byt
 //   k_part_slices (qe_hashagg.hip) slices inside bucket boundaries; a one-slice bucket is exclusive
 //   qe_pagg     LDS aggregation of a record slice, then the flush (plain read-modify-writes when
 //               the slice is exclusive)
-// Record layout (rec_layout): key | aggregate input values | [flags: bit 0 null key, bit 1+j input j
-// valid] | [global row index, fp64 MIN/MAX only], padded to 16 bytes.
+// Record layout: key | aggregate input values, or (colmode) the columns the programs read |
+// [flags: bit 0 null key, bit 1+j input j valid (colmode: column slot c valid)] | [global row index,
+// fp64 MIN/MAX only]. Whichever of the two forms is narrower is used: C4 (SUM(a+b), MIN(a),
+// MAX(b)) stores key, a, b in 24 bytes instead of key, a+b, a, b in 32. Odd widths are written and
+// read in 8-byte words, even widths in 16-byte pairs.
 PartLayout part_layout(const Plan& P) {
   PartLayout L{};
-  int w = 1;
-  bool nullable = false;
-  for (int k = 0; k < P.nkeys; ++k) nullable = nullable || P.cols[P.key_col[k]].valid != nullptr;
+  bool knull = false, vnull = false, cnull = false;
+  for (int k = 0; k < P.nkeys; ++k) knull = knull || P.cols[P.key_col[k]].valid != nullptr;
+  int nv = 0;
+  unsigned cm = 0;
   for (int j = 0; j < P.naggs; ++j) {
-    L.val_word[j] = -1;
     if (P.aggs[j].pkind == 0) continue;
-    L.val_word[j] = w++;
-    nullable = nullable || P.aggs[j].track_nn;
+    ++nv;
+    vnull = vnull || P.aggs[j].track_nn;
     L.row = L.row || acc_is_f64mm(P.aggs[j].acc);
+    for (int t = 0; t < P.aggs[j].ntok; ++t)
+      if (P.aggs[j].tok[t].op == T_COL) cm |= 1u << P.aggs[j].tok[t].arg;
   }
-  L.flags_word = nullable ? w++ : -1;
+  for (int c = 0; c < P.ncols; ++c)
+    if ((cm >> c) & 1u) cnull = cnull || P.cols[c].valid != nullptr;
+  const int wv = 1 + nv + ((knull || vnull) ? 1 : 0);
+  const int wc = 1 + __builtin_popcount(cm) + ((knull || cnull) ? 1 : 0);
+  L.colmode = wc < wv;
+  int w = 1;
+  for (int j = 0; j < P.naggs; ++j) L.val_word[j] = (!L.colmode && P.aggs[j].pkind != 0) ? w++ : -1;
+  for (int c = 0; c < QE_MAX_COLS; ++c) L.col_word[c] = (L.colmode && ((cm >> c) & 1u)) ? w++ : -1;
+  L.flags_word = (knull || (L.colmode ? cnull : vnull)) ? w++ : -1;
   L.row_word = L.row ? w++ : -1;
-  L.used = w;
-  L.words = (w + 1) & ~1;
+  L.words = w;
   return L;
+}
+
+// Record word assignments for row r of a scatter step into `dst` (an array expression).
+void emit_record_words(const Plan& P, const PartLayout& L, const std::vector<Expr>& ex, const std::string& dst,
+                       std::ostringstream& o) {
+  o << "      " << dst << "[0] = key[r];\n";
+  for (int j = 0; j < P.naggs; ++j)
+    if (L.val_word[j] >= 0) o << "      " << dst << "[" << L.val_word[j] << "] = " << ex[j].v << ";\n";
+  for (int c = 0; c < P.ncols; ++c)
+    if (L.col_word[c] >= 0) o << "      " << dst << "[" << L.col_word[c] << "] = " << col_raw(c) << ";\n";
+  if (L.flags_word >= 0) {
+    o << "      " << dst << "[" << L.flags_word << "] = (qi64)((knull >> r) & 1)";
+    for (int j = 0; j < P.naggs; ++j)
+      if (L.val_word[j] >= 0) o << " | ((qi64)((" << ex[j].ok << ") & 1u) << " << (1 + j) << ")";
+    for (int c = 0; c < P.ncols; ++c)
+      if (L.col_word[c] >= 0 && P.cols[c].valid) o << " | ((qi64)" << col_ok(P, c) << " << " << (1 + c) << ")";
+    o << ";\n";
+  }
+  if (L.row_word >= 0)
+    o << "      " << dst << "[" << L.row_word << "] = P.row_base + r0 + 128 * (r >> 1) + (r & 1);\n";
 }
 
 bool gen_part_source(const Plan& P, int log2p, bool scatter, std::string* src) {
@@ -498,21 +530,16 @@ bool gen_part_source(const Plan& P, int log2p, bool scatter, std::string* src) {
       << "  for (int b = threadIdx.x; b < NP; b += blockDim.x) P.part_off[(qi64)b * gridDim.x + blockIdx.x] = s_cnt[b];\n}\n";
   } else {
     o << "      const qu64 pos = atomicAdd(&s_cur[b], 1ull);\n"
-      << "      qi64 w[" << L.words << "];\n"
-      << "      w[0] = key[r];\n";
-    if (L.used < L.words) o << "      w[" << L.words - 1 << "] = 0;\n";
-    for (int j = 0; j < P.naggs; ++j)
-      if (L.val_word[j] >= 0) o << "      w[" << L.val_word[j] << "] = " << ex[j].v << ";\n";
-    if (L.flags_word >= 0) {
-      o << "      w[" << L.flags_word << "] = (qi64)((knull >> r) & 1)";
-      for (int j = 0; j < P.naggs; ++j)
-        if (L.val_word[j] >= 0) o << " | ((qi64)((" << ex[j].ok << ") & 1u) << " << (1 + j) << ")";
-      o << ";\n";
+      << "      qi64 w[" << L.words << "];\n";
+    emit_record_words(P, L, ex, "w", o);
+    if (L.words % 2 == 0) {
+      o << "      qi64x2* dst = (qi64x2*)(P.part_rec + pos * " << 8 * L.words << "ull);\n";
+      for (int q = 0; q < L.words / 2; ++q)
+        o << "      dst[" << q << "] = qi64x2{w[" << 2 * q << "], w[" << 2 * q + 1 << "]};\n";
+    } else {
+      o << "      qi64* dst = (qi64*)(P.part_rec + pos * " << 8 * L.words << "ull);\n";
+      for (int q = 0; q < L.words; ++q) o << "      dst[" << q << "] = w[" << q << "];\n";
     }
-    if (L.row_word >= 0) o << "      w[" << L.row_word << "] = P.row_base + r0 + 128 * (r >> 1) + (r & 1);\n";
-    o << "      qi64x2* dst = (qi64x2*)(P.part_rec + pos * " << 8 * L.words << "ull);\n";
-    for (int q = 0; q < L.words / 2; ++q)
-      o << "      dst[" << q << "] = qi64x2{w[" << 2 * q << "], w[" << 2 * q + 1 << "]};\n";
     o << "    }\n  }\n}\n";
   }
   *src = std::string(kDevHeader) + o.str();
@@ -521,7 +548,8 @@ bool gen_part_source(const Plan& P, int log2p, bool scatter, std::string* src) {
 
 // Staged scatter (few buckets): a workgroup of B threads (512) takes 4B-row tiles; the tile's records
 // are counting-sorted by bucket in LDS (rank = LDS atomic on the tile histogram, one wave scans
-// it), then written out as contiguous per-bucket runs, 16 bytes per lane in record-stream order,
+// it), then written out as contiguous per-bucket runs, 16 bytes per lane in record-stream order
+// (8 for odd record widths),
 // so the HBM writes coalesce instead of landing as one 2-word record per lane. Rows go to the same
 // (bucket, workgroup) ranges as the direct scatter: the records of one bucket and workgroup keep
 // a contiguous range of its bucket (their order inside it may differ run to run).
@@ -546,13 +574,15 @@ bool gen_pscatter_staged_source(const Plan& P, int log2p, std::string* src) {
   std::vector<Expr> ex;
   if (!agg_inputs(P, &ex)) return false;
   const PartLayout L = part_layout(P);
-  const int W = L.words;
+  const int W = L.words, G = W % 2 ? 1 : 2;
+  const char* chunk = G == 2 ? "qi64x2" : "qi64";
   std::ostringstream o;
   o << "\nusing namespace qe;\n"
     << "extern \"C\" __global__ void __launch_bounds__(" << pscatter_block() << ") qe_pscatter(const Plan P) {\n"
     << "  constexpr int LOG2P = " << log2p << ", NP = 1 << LOG2P, W = " << W << ", T = " << 4 * pscatter_block() << ";\n"
     << "  __shared__ qu32 s_hist[NP];\n  __shared__ qu32 s_off[NP];\n  __shared__ qu64 s_cur[NP];\n"
-    << "  __shared__ qi64x2 s_rec[T * W / 2];\n  __shared__ unsigned short s_bkt[T];\n  __shared__ qu32 s_total;\n"
+    << "  constexpr int WC = " << W / G << ";  // " << chunk << " chunks per record\n"
+    << "  __shared__ " << chunk << " s_rec[T * WC];\n  __shared__ unsigned short s_bkt[T];\n  __shared__ qu32 s_total;\n"
     << "  for (int b = threadIdx.x; b < NP; b += blockDim.x) s_cur[b] = (qu64)P.part_off[(qi64)b * gridDim.x + blockIdx.x];\n"
     << "  const int lane = threadIdx.x & 63;\n"
     << "  const qi64 lo = (qi64)blockIdx.x * P.part_tw;\n"
@@ -596,18 +626,8 @@ bool gen_pscatter_staged_source(const Plan& P, int log2p, std::string* src) {
     << "#pragma unroll\n    for (int r = 0; r < 4; ++r) {\n"
     << "      if (!((act >> r) & 1)) continue;\n"
     << "      bk[r] = (qu32)(fmix64((qu64)key[r]) >> (64 - LOG2P));\n"
-    << "      rk[r] = atomicAdd(&s_hist[bk[r]], 1u);\n"
-    << "      rw[r][0] = key[r];\n";
-  if (L.used < L.words) o << "      rw[r][" << W - 1 << "] = 0;\n";
-  for (int j = 0; j < P.naggs; ++j)
-    if (L.val_word[j] >= 0) o << "      rw[r][" << L.val_word[j] << "] = " << ex[j].v << ";\n";
-  if (L.flags_word >= 0) {
-    o << "      rw[r][" << L.flags_word << "] = (qi64)((knull >> r) & 1)";
-    for (int j = 0; j < P.naggs; ++j)
-      if (L.val_word[j] >= 0) o << " | ((qi64)((" << ex[j].ok << ") & 1u) << " << (1 + j) << ")";
-    o << ";\n";
-  }
-  if (L.row_word >= 0) o << "      rw[r][" << L.row_word << "] = P.row_base + r0 + 128 * (r >> 1) + (r & 1);\n";
+    << "      rk[r] = atomicAdd(&s_hist[bk[r]], 1u);\n";
+  emit_record_words(P, L, ex, "rw[r]", o);
   o << "    }\n    } while (0);\n"
     << "    __syncthreads();\n"
     // exclusive scan of the tile histogram by wave 0
@@ -626,15 +646,15 @@ bool gen_pscatter_staged_source(const Plan& P, int log2p, std::string* src) {
     << "      if (!((ract >> r) & 1)) continue;\n"
     << "      const qu32 pos = s_off[bk[r]] + rk[r];\n"
     << "      s_bkt[pos] = (unsigned short)bk[r];\n"
-    << "#pragma unroll\n      for (int q = 0; q < W / 2; ++q) s_rec[pos * (W / 2) + q] = qi64x2{rw[r][2 * q], rw[r][2 * q + 1]};\n"
+    << "#pragma unroll\n      for (int q = 0; q < WC; ++q) s_rec[pos * WC + q] = " << (W % 2 ? "rw[r][q]" : "qi64x2{rw[r][2 * q], rw[r][2 * q + 1]}") << ";\n"
     << "    }\n"
     << "    __syncthreads();\n"
     << "    const qu32 tot = s_total;\n"
-    << "    for (qu32 c = threadIdx.x; c < tot * (W / 2); c += blockDim.x) {\n"
-    << "      const qu32 j = c / (W / 2), q = c % (W / 2);\n"
+    << "    for (qu32 c = threadIdx.x; c < tot * WC; c += blockDim.x) {\n"
+    << "      const qu32 j = c / WC, q = c % WC;\n"
     << "      const qu32 b = s_bkt[j];\n"
     << "      const qu64 dst = s_cur[b] + (j - s_off[b]);\n"
-    << "      ((qi64x2*)(P.part_rec + dst * " << 8 * W << "ull))[q] = s_rec[c];\n"
+    << "      ((" << chunk << "*)(P.part_rec + dst * " << 8 * W << "ull))[q] = s_rec[c];\n"
     << "    }\n"
     << "    __syncthreads();\n"
     << "    for (int b = threadIdx.x; b < NP; b += blockDim.x) s_cur[b] += s_hist[b];\n"
@@ -648,11 +668,21 @@ bool gen_pagg_source(const Plan& P, int log2, std::string* src, size_t* lds_byte
   if (log2 < 4 || log2 > 16) return false;
   const PartLayout L = part_layout(P);
   std::vector<std::string> val(P.naggs), ok(P.naggs);
-  for (int j = 0; j < P.naggs; ++j) {
-    val[j] = L.val_word[j] >= 0 ? "w" + std::to_string(L.val_word[j]) + "[r]" : "0";
-    ok[j] = (L.val_word[j] >= 0 && P.aggs[j].track_nn)
-                ? "((qu32)(w" + std::to_string(L.flags_word) + "[r] >> " + std::to_string(1 + j) + ") & 1u)"
-                : "1u";
+  if (L.colmode) {
+    // the programs run here, over column values read back from the record (c<slot>[r], v<slot>)
+    std::vector<Expr> ex;
+    if (!agg_inputs(P, &ex)) return false;
+    for (int j = 0; j < P.naggs; ++j) {
+      val[j] = ex[j].v;
+      ok[j] = ex[j].ok;
+    }
+  } else {
+    for (int j = 0; j < P.naggs; ++j) {
+      val[j] = L.val_word[j] >= 0 ? "w" + std::to_string(L.val_word[j]) + "[r]" : "0";
+      ok[j] = (L.val_word[j] >= 0 && P.aggs[j].track_nn)
+                  ? "((qu32)(w" + std::to_string(L.flags_word) + "[r] >> " + std::to_string(1 + j) + ") & 1u)"
+                  : "1u";
+    }
   }
   std::ostringstream o;
   o << "\nusing namespace qe;\n"
@@ -672,14 +702,29 @@ bool gen_pagg_source(const Plan& P, int log2, std::string* src, size_t* lds_byte
     << "      const qi64 i = base + lane + 64 * r;\n"
     << "      bool on = i < hi;\n"
     << "      if (on && P.defer_in) on = (P.defer_in[i >> 5] >> (i & 31)) & 1;\n"
-    << "      act |= (qu32)on << r;\n"
-    << "      const qi64x2* p = (const qi64x2*)(P.part_rec + (on ? i : 0) * " << 8 * L.words << "ull);\n";
-  for (int q = 0; q < L.words / 2; ++q) {
-    o << "      { const qi64x2 v = " << ld("qi64x2", "p + " + std::to_string(q)) << "; ";
-    o << (q == 0 ? "key[r]" : "w" + std::to_string(2 * q) + "[r]") << " = v.x; w" << 2 * q + 1 << "[r] = v.y; }\n";
+    << "      act |= (qu32)on << r;\n";
+  auto word = [](int q) { return q == 0 ? std::string("key[r]") : "w" + std::to_string(q) + "[r]"; };
+  if (L.words % 2 == 0) {
+    o << "      const qi64x2* p = (const qi64x2*)(P.part_rec + (on ? i : 0) * " << 8 * L.words << "ull);\n";
+    for (int q = 0; q < L.words / 2; ++q)
+      o << "      { const qi64x2 v = " << ld("qi64x2", "p + " + std::to_string(q)) << "; " << word(2 * q)
+        << " = v.x; " << word(2 * q + 1) << " = v.y; }\n";
+  } else {
+    o << "      const qi64* p = (const qi64*)(P.part_rec + (on ? i : 0) * " << 8 * L.words << "ull);\n";
+    for (int q = 0; q < L.words; ++q) o << "      " << word(q) << " = " << ld("qi64", "p + " + std::to_string(q)) << ";\n";
   }
   if (L.flags_word >= 0) o << "      knull |= (qu32)(w" << L.flags_word << "[r] & 1) << r;\n";
-  o << "    }\n    if (act == 0) continue;\n";
+  o << "    }\n";
+  for (int c = 0; c < P.ncols; ++c) {
+    if (L.col_word[c] < 0) continue;
+    const std::string cs = std::to_string(c);
+    o << "    qi64 (&c" << cs << ")[4] = w" << L.col_word[c] << ";\n";
+    if (P.cols[c].valid)
+      o << "    qu32 v" << cs << " = 0;\n"
+        << "#pragma unroll\n    for (int r = 0; r < 4; ++r) v" << cs << " |= ((qu32)(w" << L.flags_word << "[r] >> "
+        << (1 + c) << ") & 1u) << r;\n";
+  }
+  o << "    if (act == 0) continue;\n";
   emit_agg_rows(P, o, val, ok, L.row_word >= 0 ? "w" + std::to_string(L.row_word) + "[r]" : "0",
                 "base + lane + 64 * r");
   o << "  }\n";

@@ -715,6 +715,75 @@ def test_fused_c4_partitioned_vs_oracle(agg_ctx, groups, threshold):
         assert kk[0].length == 0
 
 
+def _colrec_case(shape, rng, n):
+    """(slot arrays, slot valids, slot types, aggs, programs, oracle inputs, predicate term)."""
+    from kquery.workloads import _prog, _tok
+
+    k = rng.integers(0, 60_000, n).astype(np.int64) * 7919 - 3
+    kv = rng.random(n) > 0.01
+    if shape == "f64":
+        x, xv = _rand(rng, n, "f64", 0.1)
+        cols, valids, types = [k, x], [kv, xv], [N.TYPE_INT64, N.TYPE_FLOAT64]
+        aggs = [(N.AGG_SUM, N.TYPE_FLOAT64), (N.AGG_MAX, N.TYPE_FLOAT64), (N.AGG_MIN, N.TYPE_FLOAT64),
+                (N.AGG_AVG, N.TYPE_FLOAT64), (N.AGG_COUNT_STAR, N.TYPE_INT64)]
+        progs = {0: [_tok(N.TOK_COL, 1), _tok(N.TOK_LIT, 0, 1.5), _tok(N.TOK_ADD)], 1: [_tok(N.TOK_COL, 1)],
+                 2: [_tok(N.TOK_COL, 1)], 3: [_tok(N.TOK_COL, 1)]}
+        s0 = S.arith(S.OP_ADD, x, xv, 1.5, None)
+        ins = [s0, (x, xv), (x, xv), (x, xv), (None, None)]
+        term, sel = N.QePredTerm(1, N.OP_GT, -1, 0, N.scalar(-50.0)), xv & (x > -50.0)
+    else:
+        a = rng.integers(-2**40, 2**40, n).astype(np.int64)
+        av = rng.random(n) > 0.1
+        c = rng.integers(-3, 4, n).astype(np.int64)
+        cv = rng.random(n) > 0.1
+        cols, valids, types = [k, a, c], [kv, av, cv], [N.TYPE_INT64] * 3
+        if shape == "odd":  # key, a, flags: 3 words (values would take 5)
+            aggs = [(N.AGG_SUM, N.TYPE_INT64), (N.AGG_MIN, N.TYPE_INT64), (N.AGG_COUNT, N.TYPE_INT64),
+                    (N.AGG_COUNT_STAR, N.TYPE_INT64)]
+            progs = {0: [_tok(N.TOK_COL, 1), _tok(N.TOK_COL, 1), _tok(N.TOK_ADD)], 1: [_tok(N.TOK_COL, 1)],
+                     2: [_tok(N.TOK_COL, 1)]}
+            ins = [S.arith(S.OP_ADD, a, av, a, av), (a, av), (a, av), (None, None)]
+        else:  # key, a, c, flags: 4 words (values would take 6); division by zero is null
+            aggs = [(N.AGG_SUM, N.TYPE_INT64), (N.AGG_MIN, N.TYPE_INT64), (N.AGG_MAX, N.TYPE_INT64),
+                    (N.AGG_SUM, N.TYPE_INT64), (N.AGG_COUNT_STAR, N.TYPE_INT64)]
+            progs = {0: [_tok(N.TOK_COL, 1), _tok(N.TOK_COL, 2), _tok(N.TOK_DIV)], 1: [_tok(N.TOK_COL, 1)],
+                     2: [_tok(N.TOK_COL, 2), _tok(N.TOK_LIT, 0, 7), _tok(N.TOK_MUL)], 3: [_tok(N.TOK_COL, 2)]}
+            ins = [S.arith(S.OP_DIV, a, av, c, cv), (a, av), S.arith(S.OP_MUL, c, cv, 7, None), (c, cv), (None, None)]
+        term, sel = N.QePredTerm(1, N.OP_GT, -1, 0, N.scalar(-(2**39))), av & (a > -(2**39))
+    return cols, valids, types, aggs, progs, ins, term, sel
+
+
+@pytest.mark.parametrize("shape,width", [("odd", 24), ("even", 32), ("f64", 32)])
+def test_fused_partitioned_column_records(agg_ctx, shape, width):
+    """Partitioned records that hold the columns the aggregate programs read, when that is narrower
+    than the programs' values: the programs are re-evaluated in the aggregation pass. Nullable key
+    and inputs, integer division by zero (null), literals, fp64 MIN/MAX row order, two batches."""
+    rng = np.random.default_rng(len(shape))
+    n = 1_000_000
+    cols, valids, types, aggs, progs, ins, term, sel = _colrec_case(shape, rng, n)
+    spec = N.QeFusedSpec()
+    spec.mask_col = -1
+    spec.nterms = 1
+    spec.terms[0] = term
+    spec.key_cols[0] = 0
+    for j, toks in progs.items():
+        p = spec.inputs[j]
+        p.ntokens = len(toks)
+        for i, t in enumerate(toks):
+            p.tokens[i] = t
+    st = HashAggregateState(agg_ctx, [N.TYPE_INT64], aggs, 60_000)
+    half = 400_001
+    for s0, e0 in ((0, half), (half, n)):
+        st.update_fused([dcol(agg_ctx, t, v[s0:e0], m[s0:e0]) for t, v, m in zip(types, cols, valids)], spec)
+        check_partitioned(agg_ctx, st)
+        if getattr(agg_ctx, "kernel_mode", "jit") == "jit":
+            assert f"records of {width} B (column words)" in st.last_kernel_kind()[1]
+    kk, aa = st.finalize()
+    fns = [f for f, _ in aggs]
+    ref = S.group_aggregate([cols[0]], [valids[0]], [v for v, _ in ins], [m for _, m in ins], fns, sel)
+    assert_groups_equal(result_dict(kk, aa), ref, fns)
+
+
 @pytest.mark.slow
 def test_c4_full_size_properties(gpu_ctx):
     """BASELINE config 4 at full size (1B rows, one GPU): size-independent properties.
