@@ -569,6 +569,16 @@ int pscatter_block() {
   return b;
 }
 
+// Tiles of column loads in flight ahead of the one being sorted (QE_PSCATTER_DEPTH, 1..4).
+int pscatter_depth() {
+  static const int d = [] {
+    const char* e = getenv("QE_PSCATTER_DEPTH");
+    const int v = e && *e ? atoi(e) : 2;
+    return std::max(1, std::min(4, v));
+  }();
+  return d;
+}
+
 bool gen_pscatter_staged_source(const Plan& P, int log2p, std::string* src) {
   if (P.ncols < 1 || P.ncols > QE_MAX_COLS || log2p < 1 || !part_staged_ok(P, log2p)) return false;
   std::vector<Expr> ex;
@@ -588,34 +598,48 @@ bool gen_pscatter_staged_source(const Plan& P, int log2p, std::string* src) {
     << "  const qi64 lo = (qi64)blockIdx.x * P.part_tw;\n"
     << "  const qi64 hi = lo + P.part_tw < P.n ? lo + P.part_tw : P.n;\n"
     << "  const qi64 woff = (qi64)(threadIdx.x >> 6) * 256;\n";
-  // register prefetch: the column loads of the next tile are issued before this tile's sort and
-  // write-out (barriers do not wait for plain loads), so HBM latency overlaps the LDS phases
-  std::ostringstream pf, cp;
+  // register prefetch: the column loads of the next D tiles are in flight during this tile's sort
+  // and write-out (barriers do not wait for plain loads), so HBM latency overlaps the LDS phases.
+  // LDS holds the workgroup to 2 per CU, so the stage registers cost no occupancy.
+  const int D = pscatter_depth();
+  auto stage = [](int d, const std::string& cs) { return "n" + std::to_string(d) + "_" + cs; };
+  std::vector<std::string> pf(D);
+  std::ostringstream cp;
   for (int c = 0; c < P.ncols; ++c) {
     const std::string cs = std::to_string(c);
-    o << "  qi64 n" << cs << "[4] = {0, 0, 0, 0};\n";
-    pf << "      n" << cs << "[0] = c" << cs << "[0]; n" << cs << "[1] = c" << cs << "[1]; n" << cs << "[2] = c" << cs
-       << "[2]; n" << cs << "[3] = c" << cs << "[3];\n";
-    cp << "    qi64 c" << cs << "[4] = {n" << cs << "[0], n" << cs << "[1], n" << cs << "[2], n" << cs << "[3]};\n";
-    if (P.cols[c].valid) {
-      o << "  qu32 nv" << cs << " = 0;\n";
-      pf << "      nv" << cs << " = v" << cs << ";\n";
-      cp << "    const qu32 v" << cs << " = nv" << cs << ";\n";
+    for (int d = 0; d < D; ++d) {
+      const std::string n = stage(d, cs);
+      o << "  qi64 " << n << "[4] = {0, 0, 0, 0};\n";
+      pf[d] += "      " + n + "[0] = c" + cs + "[0]; " + n + "[1] = c" + cs + "[1]; " + n + "[2] = c" + cs + "[2]; " + n +
+               "[3] = c" + cs + "[3];\n";
+      if (P.cols[c].valid) {
+        o << "  qu32 v" << n << " = 0;\n";
+        pf[d] += "      v" + n + " = v" + cs + ";\n";
+      }
+    }
+    const std::string n0 = stage(0, cs);
+    cp << "    qi64 c" << cs << "[4] = {" << n0 << "[0], " << n0 << "[1], " << n0 << "[2], " << n0 << "[3]};\n";
+    if (P.cols[c].valid) cp << "    const qu32 v" << cs << " = v" << n0 << ";\n";
+    for (int d = 0; d + 1 < D; ++d) {
+      const std::string x = stage(d, cs), y = stage(d + 1, cs);
+      cp << "    " << x << "[0] = " << y << "[0]; " << x << "[1] = " << y << "[1]; " << x << "[2] = " << y << "[2]; "
+         << x << "[3] = " << y << "[3];\n";
+      if (P.cols[c].valid) cp << "    v" << x << " = v" << y << ";\n";
     }
   }
-  auto prefetch = [&](const std::string& nb) {
+  auto prefetch = [&](const std::string& nb, int d) {
     o << "    {\n      const qi64 base = " << nb << ";\n"
       << "      if (base < hi) {\n      const bool full = base + 256 <= P.n;\n      const qi64 r0 = base + 2 * lane;\n";
     emit_col_loads(P, o, ~0u);
-    o << pf.str() << "      }\n    }\n";
+    o << pf[d] << "      }\n    }\n";
   };
-  prefetch("lo + woff");
+  for (int d = 0; d < D; ++d) prefetch("lo + " + std::to_string(d) + " * (qi64)T + woff", d);
   o << "  for (qi64 tile = lo; tile < hi; tile += T) {\n"
     << "    for (int b = threadIdx.x; b < NP; b += blockDim.x) s_hist[b] = 0;\n"
     << "    qu32 ract = 0, bk[4], rk[4];\n    qi64 rw[4][W];\n"
     << "    const qi64 base = tile + woff;\n";
   o << cp.str();
-  prefetch("tile + T + woff");
+  prefetch("tile + " + std::to_string(D) + " * (qi64)T + woff", D - 1);
   o << "    __syncthreads();\n"
     << "    if (base < hi) do {\n"
     << "    const bool full = base + 256 <= P.n;\n"
