@@ -715,30 +715,49 @@ bool gen_pagg_source(const Plan& P, int log2, std::string* src, size_t* lds_byte
     << "  const qi64 lo = P.part_slice[2 + 2 * (qi64)blockIdx.x];\n"
     << "  const qi64 hx = P.part_slice[3 + 2 * (qi64)blockIdx.x];\n"
     << "  const bool excl = (hx & PART_EXCL) != 0;\n"
-    << "  const qi64 hi = hx & ~PART_EXCL;\n";
+    << "  const qi64 hi = hx & ~PART_EXCL;\n"
+    << "  if (hi <= lo) return;  // (the step prefetch below reads the slice's first record)\n";
   o << "  __shared__ int s_fail;\n  __shared__ qu32 s_newg;\n  if (threadIdx.x == 0) { s_fail = 0; s_newg = 0; }\n";
   emit_lds_table(P, o, log2, lds_bytes);
+  // the records of the wave's next step are loaded into n* registers before this step's LDS work
+  auto word = [](const std::string& pre, int q) {
+    return (q == 0 ? pre + "key" : pre + "w" + std::to_string(q)) + "[r]";
+  };
+  auto load_step = [&](const std::string& pre, const std::string& nb) {
+    o << "    {\n      const qi64 nb = " << nb << ";\n      " << pre << "act = 0;\n"
+      << "#pragma unroll\n      for (int r = 0; r < 4; ++r) {\n"
+      << "        const qi64 i = nb + lane + 64 * r;\n"
+      << "        bool on = i < hi;\n"
+      << "        if (on && P.defer_in) on = (P.defer_in[i >> 5] >> (i & 31)) & 1;\n"
+      << "        " << pre << "act |= (qu32)on << r;\n";
+    if (L.words % 2 == 0) {
+      o << "        const qi64x2* p = (const qi64x2*)(P.part_rec + (on ? i : 0) * " << 8 * L.words << "ull);\n";
+      for (int q = 0; q < L.words / 2; ++q)
+        o << "        { const qi64x2 v = " << ld("qi64x2", "p + " + std::to_string(q)) << "; " << word(pre, 2 * q)
+          << " = v.x; " << word(pre, 2 * q + 1) << " = v.y; }\n";
+    } else {
+      o << "        const qi64* p = (const qi64*)(P.part_rec + (on ? i : 0) * " << 8 * L.words << "ull);\n";
+      for (int q = 0; q < L.words; ++q)
+        o << "        " << word(pre, q) << " = " << ld("qi64", "p + " + std::to_string(q)) << ";\n";
+    }
+    o << "      }\n    }\n";
+  };
   o << "  const int lane = threadIdx.x & 63;\n"
-    << "  for (qi64 base = lo + (qi64)(threadIdx.x >> 6) * 256; base < hi; base += (qi64)(blockDim.x >> 6) * 256) {\n"
-    << "    qu32 act = 0, knull = 0;\n    qi64 key[4];\n";
-  for (int q = 1; q < L.words; ++q) o << "    qi64 w" << q << "[4];\n";
-  o << "#pragma unroll\n    for (int r = 0; r < 4; ++r) {\n"
-    << "      const qi64 i = base + lane + 64 * r;\n"
-    << "      bool on = i < hi;\n"
-    << "      if (on && P.defer_in) on = (P.defer_in[i >> 5] >> (i & 31)) & 1;\n"
-    << "      act |= (qu32)on << r;\n";
-  auto word = [](int q) { return q == 0 ? std::string("key[r]") : "w" + std::to_string(q) + "[r]"; };
-  if (L.words % 2 == 0) {
-    o << "      const qi64x2* p = (const qi64x2*)(P.part_rec + (on ? i : 0) * " << 8 * L.words << "ull);\n";
-    for (int q = 0; q < L.words / 2; ++q)
-      o << "      { const qi64x2 v = " << ld("qi64x2", "p + " + std::to_string(q)) << "; " << word(2 * q)
-        << " = v.x; " << word(2 * q + 1) << " = v.y; }\n";
-  } else {
-    o << "      const qi64* p = (const qi64*)(P.part_rec + (on ? i : 0) * " << 8 * L.words << "ull);\n";
-    for (int q = 0; q < L.words; ++q) o << "      " << word(q) << " = " << ld("qi64", "p + " + std::to_string(q)) << ";\n";
-  }
-  if (L.flags_word >= 0) o << "      knull |= (qu32)(w" << L.flags_word << "[r] & 1) << r;\n";
-  o << "    }\n";
+    << "  const qi64 step = (qi64)(blockDim.x >> 6) * 256;\n"
+    << "  qu32 nact;\n  qi64 nkey[4];\n";
+  for (int q = 1; q < L.words; ++q) o << "  qi64 nw" << q << "[4];\n";
+  const char* pfe = getenv("QE_PAGG_PREFETCH");
+  const bool pf = !(pfe && pfe[0] == '0');
+  if (pf) load_step("n", "lo + (qi64)(threadIdx.x >> 6) * 256");
+  o << "  for (qi64 base = lo + (qi64)(threadIdx.x >> 6) * 256; base < hi; base += step) {\n";
+  if (!pf) load_step("n", "base");
+  o << "    const qu32 act = nact;\n    qu32 knull = 0;\n"
+    << "    qi64 key[4] = {nkey[0], nkey[1], nkey[2], nkey[3]};\n";
+  for (int q = 1; q < L.words; ++q)
+    o << "    qi64 w" << q << "[4] = {nw" << q << "[0], nw" << q << "[1], nw" << q << "[2], nw" << q << "[3]};\n";
+  if (pf) load_step("n", "base + step");
+  if (L.flags_word >= 0)
+    o << "#pragma unroll\n    for (int r = 0; r < 4; ++r) knull |= (qu32)(w" << L.flags_word << "[r] & 1) << r;\n";
   for (int c = 0; c < P.ncols; ++c) {
     if (L.col_word[c] < 0) continue;
     const std::string cs = std::to_string(c);
