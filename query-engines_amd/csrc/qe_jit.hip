@@ -598,92 +598,91 @@ bool gen_pscatter_staged_source(const Plan& P, int log2p, std::string* src) {
     << "  const qi64 lo = (qi64)blockIdx.x * P.part_tw;\n"
     << "  const qi64 hi = lo + P.part_tw < P.n ? lo + P.part_tw : P.n;\n"
     << "  const qi64 woff = (qi64)(threadIdx.x >> 6) * 256;\n";
-  // register prefetch: the column loads of the next D tiles are in flight during this tile's sort
-  // and write-out (barriers do not wait for plain loads), so HBM latency overlaps the LDS phases.
-  // LDS holds the workgroup to 2 per CU, so the stage registers cost no occupancy.
+  // Register prefetch over D rotating buffers: the tile loop is unrolled D times, and step k
+  // reads buffer k, builds its records, then reloads buffer k with the tile D steps ahead before
+  // the LDS sort and write-out. The loads then have D - 1 whole tiles plus this tile's LDS phases
+  // to land (barriers wait on LDS only; moving buffers between registers would wait on them).
+  // LDS holds the workgroup to 2 per CU, so the buffer registers cost no occupancy.
   const int D = pscatter_depth();
-  auto stage = [](int d, const std::string& cs) { return "n" + std::to_string(d) + "_" + cs; };
-  std::vector<std::string> pf(D);
-  std::ostringstream cp;
-  for (int c = 0; c < P.ncols; ++c) {
-    const std::string cs = std::to_string(c);
+  auto buf = [](int d, const std::string& cs) { return "n" + std::to_string(d) + "_" + cs; };
+  for (int c = 0; c < P.ncols; ++c)
     for (int d = 0; d < D; ++d) {
-      const std::string n = stage(d, cs);
-      o << "  qi64 " << n << "[4] = {0, 0, 0, 0};\n";
-      pf[d] += "      " + n + "[0] = c" + cs + "[0]; " + n + "[1] = c" + cs + "[1]; " + n + "[2] = c" + cs + "[2]; " + n +
-               "[3] = c" + cs + "[3];\n";
-      if (P.cols[c].valid) {
-        o << "  qu32 v" << n << " = 0;\n";
-        pf[d] += "      v" + n + " = v" + cs + ";\n";
-      }
+      o << "  qi64 " << buf(d, std::to_string(c)) << "[4] = {0, 0, 0, 0};\n";
+      if (P.cols[c].valid) o << "  qu32 v" << buf(d, std::to_string(c)) << " = 0;\n";
     }
-    const std::string n0 = stage(0, cs);
-    cp << "    qi64 c" << cs << "[4] = {" << n0 << "[0], " << n0 << "[1], " << n0 << "[2], " << n0 << "[3]};\n";
-    if (P.cols[c].valid) cp << "    const qu32 v" << cs << " = v" << n0 << ";\n";
-    for (int d = 0; d + 1 < D; ++d) {
-      const std::string x = stage(d, cs), y = stage(d + 1, cs);
-      cp << "    " << x << "[0] = " << y << "[0]; " << x << "[1] = " << y << "[1]; " << x << "[2] = " << y << "[2]; "
-         << x << "[3] = " << y << "[3];\n";
-      if (P.cols[c].valid) cp << "    v" << x << " = v" << y << ";\n";
-    }
-  }
-  auto prefetch = [&](const std::string& nb, int d) {
-    o << "    {\n      const qi64 base = " << nb << ";\n"
-      << "      if (base < hi) {\n      const bool full = base + 256 <= P.n;\n      const qi64 r0 = base + 2 * lane;\n";
+  auto load_into = [&](const std::string& nb, int d, const std::string& ind) {
+    o << ind << "{\n" << ind << "  const qi64 base = " << nb << ";\n"
+      << ind << "  if (base < hi) {\n" << ind << "  const bool full = base + 256 <= P.n;\n"
+      << ind << "  const qi64 r0 = base + 2 * lane;\n";
     emit_col_loads(P, o, ~0u);
-    o << pf[d] << "      }\n    }\n";
+    for (int c = 0; c < P.ncols; ++c) {
+      const std::string cs = std::to_string(c), n = buf(d, cs);
+      o << ind << "  " << n << "[0] = c" << cs << "[0]; " << n << "[1] = c" << cs << "[1]; " << n << "[2] = c" << cs
+        << "[2]; " << n << "[3] = c" << cs << "[3];\n";
+      if (P.cols[c].valid) o << ind << "  v" << n << " = v" << cs << ";\n";
+    }
+    o << ind << "  }\n" << ind << "}\n";
   };
-  for (int d = 0; d < D; ++d) prefetch("lo + " + std::to_string(d) + " * (qi64)T + woff", d);
-  o << "  for (qi64 tile = lo; tile < hi; tile += T) {\n"
-    << "    for (int b = threadIdx.x; b < NP; b += blockDim.x) s_hist[b] = 0;\n"
-    << "    qu32 ract = 0, bk[4], rk[4];\n    qi64 rw[4][W];\n"
-    << "    const qi64 base = tile + woff;\n";
-  o << cp.str();
-  prefetch("tile + " + std::to_string(D) + " * (qi64)T + woff", D - 1);
-  o << "    __syncthreads();\n"
-    << "    if (base < hi) do {\n"
-    << "    const bool full = base + 256 <= P.n;\n"
-    << "    const qi64 r0 = base + 2 * lane;\n";
-  emit_active_rows(P, o, false);
-  emit_keys(P, o);
-  o << "    ract = act;\n"
-    << "#pragma unroll\n    for (int r = 0; r < 4; ++r) {\n"
-    << "      if (!((act >> r) & 1)) continue;\n"
-    << "      bk[r] = (qu32)(fmix64((qu64)key[r]) >> (64 - LOG2P));\n"
-    << "      rk[r] = atomicAdd(&s_hist[bk[r]], 1u);\n";
-  emit_record_words(P, L, ex, "rw[r]", o);
-  o << "    }\n    } while (0);\n"
-    << "    __syncthreads();\n"
-    // exclusive scan of the tile histogram by wave 0
-    << "    if (threadIdx.x < 64) {\n"
-    << "      constexpr int PER = (NP + 63) / 64;\n"
-    << "      qu32 loc[PER], s = 0;\n"
-    << "#pragma unroll\n      for (int i = 0; i < PER; ++i) { const int b = lane * PER + i; loc[i] = b < NP ? s_hist[b] : 0u; s += loc[i]; }\n"
-    << "      qu32 x = s;\n"
-    << "#pragma unroll\n      for (int d = 1; d < 64; d <<= 1) { const qu32 y = __shfl_up(x, d); if (lane >= d) x += y; }\n"
-    << "      qu32 e = x - s;\n"
-    << "#pragma unroll\n      for (int i = 0; i < PER; ++i) { const int b = lane * PER + i; if (b < NP) s_off[b] = e; e += loc[i]; }\n"
-    << "      if (lane == 63) s_total = x;\n"
-    << "    }\n"
-    << "    __syncthreads();\n"
-    << "#pragma unroll\n    for (int r = 0; r < 4; ++r) {\n"
-    << "      if (!((ract >> r) & 1)) continue;\n"
-    << "      const qu32 pos = s_off[bk[r]] + rk[r];\n"
-    << "      s_bkt[pos] = (unsigned short)bk[r];\n"
-    << "#pragma unroll\n      for (int q = 0; q < WC; ++q) s_rec[pos * WC + q] = " << (W % 2 ? "rw[r][q]" : "qi64x2{rw[r][2 * q], rw[r][2 * q + 1]}") << ";\n"
-    << "    }\n"
-    << "    __syncthreads();\n"
-    << "    const qu32 tot = s_total;\n"
-    << "    for (qu32 c = threadIdx.x; c < tot * WC; c += blockDim.x) {\n"
-    << "      const qu32 j = c / WC, q = c % WC;\n"
-    << "      const qu32 b = s_bkt[j];\n"
-    << "      const qu64 dst = s_cur[b] + (j - s_off[b]);\n"
-    << "      ((" << chunk << "*)(P.part_rec + dst * " << 8 * W << "ull))[q] = s_rec[c];\n"
-    << "    }\n"
-    << "    __syncthreads();\n"
-    << "    for (int b = threadIdx.x; b < NP; b += blockDim.x) s_cur[b] += s_hist[b];\n"
-    << "    __syncthreads();\n"
-    << "  }\n}\n";
+  for (int d = 0; d < D; ++d) load_into("lo + " + std::to_string(d) + " * (qi64)T + woff", d, "  ");
+  o << "  for (qi64 t0 = lo; t0 < hi; t0 += " << D << " * (qi64)T) {\n";
+  for (int k = 0; k < D; ++k) {
+    o << "  {\n    const qi64 tile = t0 + " << k << " * (qi64)T;\n    if (tile >= hi) break;\n"
+      << "    for (int b = threadIdx.x; b < NP; b += blockDim.x) s_hist[b] = 0;\n"
+      << "    qu32 ract = 0, bk[4], rk[4];\n    qi64 rw[4][W];\n"
+      << "    const qi64 base = tile + woff;\n";
+    for (int c = 0; c < P.ncols; ++c) {
+      const std::string cs = std::to_string(c);
+      o << "    qi64 (&c" << cs << ")[4] = " << buf(k, cs) << ";\n";
+      if (P.cols[c].valid) o << "    const qu32 v" << cs << " = v" << buf(k, cs) << ";\n";
+    }
+    o << "    __syncthreads();\n"
+      << "    if (base < hi) do {\n"
+      << "    const bool full = base + 256 <= P.n;\n"
+      << "    const qi64 r0 = base + 2 * lane;\n";
+    emit_active_rows(P, o, false);
+    emit_keys(P, o);
+    o << "    ract = act;\n"
+      << "#pragma unroll\n    for (int r = 0; r < 4; ++r) {\n"
+      << "      if (!((act >> r) & 1)) continue;\n"
+      << "      bk[r] = (qu32)(fmix64((qu64)key[r]) >> (64 - LOG2P));\n"
+      << "      rk[r] = atomicAdd(&s_hist[bk[r]], 1u);\n";
+    emit_record_words(P, L, ex, "rw[r]", o);
+    o << "    }\n    } while (0);\n";
+    load_into("tile + " + std::to_string(D) + " * (qi64)T + woff", k, "    ");
+    o << "    __syncthreads();\n"
+      // exclusive scan of the tile histogram by wave 0
+      << "    if (threadIdx.x < 64) {\n"
+      << "      constexpr int PER = (NP + 63) / 64;\n"
+      << "      qu32 loc[PER], s = 0;\n"
+      << "#pragma unroll\n      for (int i = 0; i < PER; ++i) { const int b = lane * PER + i; loc[i] = b < NP ? s_hist[b] : 0u; s += loc[i]; }\n"
+      << "      qu32 x = s;\n"
+      << "#pragma unroll\n      for (int d = 1; d < 64; d <<= 1) { const qu32 y = __shfl_up(x, d); if (lane >= d) x += y; }\n"
+      << "      qu32 e = x - s;\n"
+      << "#pragma unroll\n      for (int i = 0; i < PER; ++i) { const int b = lane * PER + i; if (b < NP) s_off[b] = e; e += loc[i]; }\n"
+      << "      if (lane == 63) s_total = x;\n"
+      << "    }\n"
+      << "    __syncthreads();\n"
+      << "#pragma unroll\n    for (int r = 0; r < 4; ++r) {\n"
+      << "      if (!((ract >> r) & 1)) continue;\n"
+      << "      const qu32 pos = s_off[bk[r]] + rk[r];\n"
+      << "      s_bkt[pos] = (unsigned short)bk[r];\n"
+      << "#pragma unroll\n      for (int q = 0; q < WC; ++q) s_rec[pos * WC + q] = "
+      << (W % 2 ? "rw[r][q]" : "qi64x2{rw[r][2 * q], rw[r][2 * q + 1]}") << ";\n"
+      << "    }\n"
+      << "    __syncthreads();\n"
+      << "    const qu32 tot = s_total;\n"
+      << "    for (qu32 c = threadIdx.x; c < tot * WC; c += blockDim.x) {\n"
+      << "      const qu32 j = c / WC, q = c % WC;\n"
+      << "      const qu32 b = s_bkt[j];\n"
+      << "      const qu64 dst = s_cur[b] + (j - s_off[b]);\n"
+      << "      ((" << chunk << "*)(P.part_rec + dst * " << 8 * W << "ull))[q] = s_rec[c];\n"
+      << "    }\n"
+      << "    __syncthreads();\n"
+      << "    for (int b = threadIdx.x; b < NP; b += blockDim.x) s_cur[b] += s_hist[b];\n"
+      << "    __syncthreads();\n"
+      << "  }\n";
+  }
+  o << "  }\n}\n";
   *src = std::string(kDevHeader) + o.str();
   return true;
 }
