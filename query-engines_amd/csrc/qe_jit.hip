@@ -816,7 +816,15 @@ bool selproj_nt(const Plan& P) {
   return P.n > (64ll << 20);
 }
 
-int selproj_rows_per_thread(const Plan& P) { return P.ncols <= 3 ? 16 : (P.ncols <= 6 ? 8 : 4); }
+int selproj_rows_per_thread(const Plan& P) {
+  static const int env = [] {
+    const char* e = getenv("QE_SELPROJ_ROWS");
+    const int v = e && *e ? atoi(e) : 0;
+    return (v == 4 || v == 8 || v == 16) ? v : 0;  // (R x 4 waves) chunk counts fit one wave's scan
+  }();
+  if (env) return env;
+  return P.ncols <= 3 ? 16 : (P.ncols <= 6 ? 8 : 4);
+}
 
 bool gen_selproj_source(const Plan& P, const int32_t* out_kind, int nout, std::string* src, bool persistent) {
   if (P.ncols < 1 || P.ncols > QE_MAX_COLS || nout < 1 || nout > QE_MAX_AGGS) return false;
