@@ -826,9 +826,12 @@ int selproj_rows_per_thread(const Plan& P) {
   return P.ncols <= 3 ? 16 : (P.ncols <= 6 ? 8 : 4);
 }
 
-bool gen_selproj_source(const Plan& P, const int32_t* out_kind, int nout, std::string* src, bool persistent) {
+bool gen_selproj_source(const Plan& P, const int32_t* out_kind, int nout, std::string* src, int mode) {
   if (P.ncols < 1 || P.ncols > QE_MAX_COLS || nout < 1 || nout > QE_MAX_AGGS) return false;
   const int R = selproj_rows_per_thread(P);
+  const bool persistent = mode == SP_PERSIST;
+  // the count pass loads only the predicate's columns
+  const unsigned need = mode == SP_COUNT ? pred_key_cols(P) : ~0u;
   std::ostringstream o;
   o << "\nusing namespace qe;\n"
     << "extern \"C\" __global__ void __launch_bounds__(256) qe_selproj(const Plan P) {\n"
@@ -841,6 +844,7 @@ bool gen_selproj_source(const Plan& P, const int32_t* out_kind, int nout, std::s
   // column loads of the tile at `b` into <cp><slot>[R] / <vp><slot> (validity bits)
   auto emit_loads = [&](const std::string& cp, const std::string& vp, const std::string& b, const std::string& ind) {
     for (int c = 0; c < P.ncols; ++c) {
+      if (!((need >> c) & 1u)) continue;
       const std::string cs = std::to_string(c);
       const int kind = P.cols[c].kind;
       const char* ty = kind == K_I32 ? "qi32" : (kind == K_U8 || kind == K_BOOL) ? "qu8" : "qi64";
@@ -875,16 +879,27 @@ bool gen_selproj_source(const Plan& P, const int32_t* out_kind, int nout, std::s
     }
     emit_loads("c", "v", "base", "  ");
   } else {
-    o << "  {\n  if (t == 0) s_tile = (qu32)atomicAdd((unsigned long long*)&P.t.ctl[0], 1ull);\n"
-      << "  __syncthreads();\n"
-      << "  const qu32 tile = s_tile;\n"
-      << "  const qi64 base = (qi64)tile * (R * 256);\n"
+    if (mode == SP_COUNTER)
+      o << "  {\n  if (t == 0) s_tile = (qu32)atomicAdd((unsigned long long*)&P.t.ctl[0], 1ull);\n"
+        << "  __syncthreads();\n"
+        << "  const qu32 tile = s_tile;\n";
+    else  // two-pass: one tile per workgroup in grid order
+      o << "  {\n  const qu32 tile = blockIdx.x;\n";
+    o << "  const qi64 base = (qi64)tile * (R * 256);\n"
       << "  const bool full = base + R * 256 <= P.n;\n";
     for (int c = 0; c < P.ncols; ++c) {
+      if (!((need >> c) & 1u)) continue;
       o << "  qi64 c" << c << "[R];\n";
       if (P.cols[c].valid) o << "  qu32 v" << c << " = 0;\n";
     }
     emit_loads("c", "v", "base", "  ");
+    if (mode == SP_WRITE)
+      // this tile's base: the earlier tiles' counts, summed by the whole workgroup while its
+      // column loads are in flight
+      o << "  qu64 pre = 0;\n"
+        << "  for (qi64 i = t; i < (qi64)tile; i += 256) pre += ((const qu64*)P.t.keys)[i];\n"
+        << "#pragma unroll\n  for (int d = 32; d >= 1; d >>= 1) pre += __shfl_xor(pre, d);\n"
+        << "  __shared__ qu64 s_pre[4];\n  if (lane == 0) s_pre[w] = pre;\n";
   }
   o << "  qu32 act = 0;\n"
     << "#pragma unroll\n  for (int r = 0; r < R; ++r) act |= (qu32)(full || base + r * 256 + t < P.n) << r;\n";
@@ -895,6 +910,15 @@ bool gen_selproj_source(const Plan& P, const int32_t* out_kind, int nout, std::s
     const std::string from = "r < 16;", to = "r < R;";
     for (size_t k = body.find(from); k != std::string::npos; k = body.find(from, k)) body.replace(k, from.size(), to);
     o << body;
+  }
+  if (mode == SP_COUNT) {
+    o << "  qu32 n = __popc(act);\n"
+      << "#pragma unroll\n  for (int d = 32; d >= 1; d >>= 1) n += __shfl_xor(n, d);\n"
+      << "  if (lane == 0) s_cnt[w] = n;\n  __syncthreads();\n"
+      << "  if (t == 0) ((qu64*)P.t.keys)[tile] = (qu64)s_cnt[0] + s_cnt[1] + s_cnt[2] + s_cnt[3];\n"
+      << "  }\n}\n";
+    *src = std::string(kDevHeader) + o.str();
+    return true;
   }
   // Staged output (all outputs 8 bytes wide, R x 256 x 8 B each within 64 KiB of LDS): selected
   // rows land compacted in LDS, then the tile's output range is written with 16-byte stores, all
@@ -916,9 +940,13 @@ bool gen_selproj_source(const Plan& P, const int32_t* out_kind, int nout, std::s
     << "#pragma unroll\n    for (int d = 1; d < 64; d <<= 1) { const qu32 y = __shfl_up(inc, d); if (lane >= d) inc += y; }\n"
     << "    const qu64 total = (qu64)__shfl(inc, 63);\n"
     << "    if (lane < R * 4) s_cnt[lane] = inc - x;\n"
-    << "    if (lane == 0) { s_total = (qu32)total; __hip_atomic_store(&st[tile], (tile == 0 ? F_INC : F_AGG) | total, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }\n"
+    << (mode == SP_WRITE ? "    if (lane == 0) s_total = (qu32)total;\n"
+                         : "    if (lane == 0) { s_total = (qu32)total; __hip_atomic_store(&st[tile], (tile == 0 ? F_INC : F_AGG) | total, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }\n")
     << "  }\n";
-  const std::string lookback =
+  const std::string lookback = mode == SP_WRITE ?
+      "    const qu64 total = s_total;\n"
+      "    if (lane == 0) {\n      const qu64 excl = s_pre[0] + s_pre[1] + s_pre[2] + s_pre[3];\n      s_base = excl;\n"
+      "      if ((qu64)tile == P.t.cap - 1) P.t.ctl[1] = excl + total;\n    }\n" :
       "    const qu64 total = s_total;\n"
       "    qu64 excl = 0;\n"
       "    if (tile > 0) {\n"

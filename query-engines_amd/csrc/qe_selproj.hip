@@ -8,12 +8,80 @@
 // The kernel is generated per plan shape and compiled with hipRTC (qe_jit.hip gen_selproj_source);
 // without hipRTC the call returns QE_ERR_UNSUPPORTED and callers run the per-family operators.
 #include <stdio.h>
+#include <string.h>
+
+#include <map>
+#include <mutex>
+#include <string>
 
 #include "qe_internal.hpp"
 
 using namespace qe;
 
 namespace {
+
+// Kernel of one plan shape and pass, memoised on the plan's structure: generating the source
+// (~6 us) and looking it up in the source-keyed module cache ran on every call, two passes per
+// call. The key is the Plan with its run-time values cleared (buffer pointers reduced to
+// present / absent, literals, row count, table and partition fields), plus everything else the
+// generator reads: output kinds, pass, rows per thread, load policy, device.
+int selproj_kernel(qe_ctx* ctx, const Plan& P, const int32_t* out_kind, int nout, int mode, hipFunction_t* fn,
+                   int* bpc) {
+  struct Key {
+    Plan p;
+    int32_t out_kind[QE_MAX_AGGS];
+    int32_t nout, mode, rows, nt, nt_env, device;
+  };
+  Key k;
+  memset(&k, 0, sizeof k);
+  memcpy(&k.p, &P, sizeof P);
+  for (int c = 0; c < QE_MAX_COLS; ++c) {
+    k.p.cols[c].p = (const void*)(uintptr_t)(P.cols[c].p != nullptr);
+    k.p.cols[c].valid = (const qu8*)(uintptr_t)(P.cols[c].valid != nullptr);
+  }
+  for (int t = 0; t < QE_MAX_TERMS; ++t) k.p.terms[t].lit = 0;
+  for (int j = 0; j < QE_MAX_AGGS; ++j) {
+    k.p.aggs[j].rhs_lit = 0;
+    for (int t = 0; t < QE_MAX_TOKENS; ++t) k.p.aggs[j].tok[t].lit = 0;
+  }
+  memset(&k.p.t, 0, sizeof k.p.t);
+  k.p.n = k.p.row_base = 0;
+  k.p.defer_in = nullptr;
+  k.p.defer_out = nullptr;
+  k.p.ovf = nullptr;
+  k.p.ovf_cap = 0;
+  k.p.part_rec = nullptr;
+  k.p.part_off = nullptr;
+  k.p.part_tw = 0;
+  k.p.part_slice = nullptr;
+  for (int j = 0; j < nout; ++j) k.out_kind[j] = out_kind[j];
+  k.nout = nout;
+  k.mode = mode;
+  k.rows = selproj_rows_per_thread(P);
+  k.nt = selproj_nt(P);
+  const char* ne = getenv("QE_NT");
+  k.nt_env = !(ne && ne[0] == '0');
+  k.device = ctx->device;
+  const std::string key((const char*)&k, sizeof k);
+  static std::mutex mu;
+  static std::map<std::string, std::pair<hipFunction_t, int>> memo;
+  {
+    std::lock_guard<std::mutex> g(mu);
+    auto it = memo.find(key);
+    if (it != memo.end()) {
+      *fn = it->second.first;
+      *bpc = it->second.second;
+      return QE_OK;
+    }
+  }
+  std::string src;
+  if (!gen_selproj_source(P, out_kind, nout, &src, mode))
+    return fail(QE_ERR_UNSUPPORTED, "plan shape is outside the select-project generator");
+  QE_TRY(jit_kernel(ctx, src, fn, bpc, "qe_selproj", 256));
+  std::lock_guard<std::mutex> g(mu);
+  memo[key] = {*fn, *bpc};
+  return QE_OK;
+}
 
 // Output column type a program produces: a lone column reference keeps the column's type;
 // anything else is INT64 or FLOAT64 by promotion.
@@ -78,7 +146,41 @@ extern "C" int qe_select_project(qe_ctx* ctx, const qe_column* cols, int32_t nco
   };
   QE_TRY(init_validity());
   *out_count = 0;
-  if (n > 0) {
+  // Two passes (count per tile, then write at the sum of the earlier tiles' counts) while the
+  // predicate's columns fit the MALL, so the second pass reads them from there: no look-back
+  // round trips. QE_SELPROJ_TWOPASS=0/1 forces either way.
+  const char* tpe = getenv("QE_SELPROJ_TWOPASS");  // read per call: tests switch it
+  const int twopass_env = tpe && *tpe ? (tpe[0] == '1' ? 1 : 0) : -1;
+  unsigned pred_cols = P.mask_col >= 0 ? 1u << P.mask_col : 0u;
+  for (int t = 0; t < P.nterms; ++t)
+    pred_cols |= (1u << P.terms[t].lhs) | (P.terms[t].rhs >= 0 ? 1u << P.terms[t].rhs : 0u);
+  size_t pred_bytes = 0;
+  for (int c = 0; c < P.ncols; ++c)
+    if ((pred_cols >> c) & 1u) pred_bytes += (size_t)n * std::max(1, type_width(cols[c].type));
+  const bool twopass = twopass_env >= 0 ? twopass_env == 1 : pred_bytes <= (96ull << 20);
+  if (n > 0 && twopass) {
+    const int R = selproj_rows_per_thread(P);
+    const int64_t tiles = (int64_t)div_up((uint64_t)n, (uint64_t)R * 256);
+    QE_CHECK(tiles < (1ll << 31), QE_ERR_CAPACITY, "too many rows for one select-project call");
+    void* s;
+    QE_TRY(ctx_scratch(ctx, (size_t)(tiles + 3) * 8, &s));
+    qu64* ctl = (qu64*)s;
+    P.t.ctl = ctl;
+    P.t.keys = (qi64*)(ctl + 3);
+    P.t.cap = (qu64)tiles;
+    void* pin;
+    QE_TRY(ctx_pinned(ctx, 16, &pin));
+    for (int mode : {SP_COUNT, SP_WRITE}) {
+      hipFunction_t fn;
+      int bpc = 0;
+      QE_TRY(selproj_kernel(ctx, P, out_kind, spec->nout, mode, &fn, &bpc));
+      QE_TRY(jit_launch(ctx, fn, (int)tiles, P, 256));
+      QE_TRY(launch_check(mode == SP_COUNT ? "qe_selproj (count)" : "qe_selproj (write)"));
+    }
+    QE_HIP(hipMemcpyAsync(pin, ctl + 1, 8, hipMemcpyDeviceToHost, ctx->stream));
+    QE_HIP(hipStreamSynchronize(ctx->stream));
+    *out_count = ((int64_t*)pin)[0];
+  } else if (n > 0) {
     const int R = selproj_rows_per_thread(P);
     const int64_t tiles = (int64_t)div_up((uint64_t)n, (uint64_t)R * 256);
     QE_CHECK(tiles < (1ll << 31), QE_ERR_CAPACITY, "too many rows for one select-project call");
@@ -92,12 +194,9 @@ extern "C" int qe_select_project(qe_ctx* ctx, const qe_column* cols, int32_t nco
     QE_TRY(ctx_pinned(ctx, 16, &pin));
     for (int attempt = 0; attempt < 2; ++attempt) {
       const bool persist = persist_env && attempt == 0;
-      std::string src;
-      if (!gen_selproj_source(P, out_kind, spec->nout, &src, persist))
-        return fail(QE_ERR_UNSUPPORTED, "plan shape is outside the select-project generator");
       hipFunction_t fn;
       int bpc = 0;
-      QE_TRY(jit_kernel(ctx, src, &fn, &bpc, "qe_selproj", 256));
+      QE_TRY(selproj_kernel(ctx, P, out_kind, spec->nout, persist ? SP_PERSIST : SP_COUNTER, &fn, &bpc));
       QE_HIP(hipMemsetAsync(s, 0, (size_t)(tiles + 3) * 8, ctx->stream));
       // QE_SELPROJ_OVERSUB (tests only) multiplies the persistent grid past residency, to exercise
       // the bounded look-back and the rerun

@@ -43,9 +43,17 @@ def _run(ctx, cols, spec, out_types):
     return cnt.value, outs
 
 
+@pytest.fixture(params=["twopass", "lookback"])
+def selproj_path(request, monkeypatch):
+    """Both tile-base schemes: two passes (count, then write; the default while the predicate's
+    columns fit the MALL) and the single pass with a decoupled look-back."""
+    monkeypatch.setenv("QE_SELPROJ_TWOPASS", "1" if request.param == "twopass" else "0")
+    return request.param
+
+
 @pytest.mark.parametrize("n", [0, 1, 255, 4095, 4096, 4097, 100_003, 3_000_000])
 @pytest.mark.parametrize("k", [0, 1 << 10, 1 << 19, (1 << 20) - 1, 1 << 20])
-def test_c2_shape(gpu_ctx, n, k):
+def test_c2_shape(gpu_ctx, selproj_path, n, k):
     """C2: SELECT a + b WHERE a > k (a uniform in [0, 2^20), b full-range int64: wrap)."""
     from kquery import native as N
     from kquery.datasource import C2_COLUMNS, generate_column
@@ -66,7 +74,7 @@ def test_c2_shape(gpu_ctx, n, k):
 
 
 @pytest.mark.parametrize("n", [1000, 70_001])
-def test_nulls_division_f64_and_narrow_types(gpu_ctx, n):
+def test_nulls_division_f64_and_narrow_types(gpu_ctx, selproj_path, n):
     from kquery import native as N
     from kquery.columnar import DeviceColumn
 
@@ -169,6 +177,7 @@ def test_persistent_grid_not_resident_reruns(gpu_ctx, monkeypatch, capfd):
     from kquery.datasource import C2_COLUMNS, generate_column
 
     monkeypatch.setenv("QE_SELPROJ_OVERSUB", "8")
+    monkeypatch.setenv("QE_SELPROJ_TWOPASS", "0")
     n, k = 80_000_000, 1 << 19  # >= 2 tiles per workgroup: every resident one waits on a later one
     cols = [generate_column(s, n, 0, 42, gpu_ctx) for s in C2_COLUMNS]
     spec = _spec(N, [(0, N.OP_GT, -1, k)], [[(N.TOK_COL, 0, None), (N.TOK_COL, 1, None), (N.TOK_ADD, 0, None)]])
