@@ -157,7 +157,10 @@ extern "C" int qe_select_project(qe_ctx* ctx, const qe_column* cols, int32_t nco
   size_t pred_bytes = 0;
   for (int c = 0; c < P.ncols; ++c)
     if ((pred_cols >> c) & 1u) pred_bytes += (size_t)n * std::max(1, type_width(cols[c].type));
-  const bool twopass = twopass_env >= 0 ? twopass_env == 1 : pred_bytes <= (96ull << 20);
+  // (each write-pass tile sums all earlier tiles' counts, so the tile count is bounded too: a
+  // plan with no predicate reads nothing in the count pass but still pays the prefix sums)
+  const int64_t tiles_est = (int64_t)div_up((uint64_t)n, (uint64_t)selproj_rows_per_thread(P) * 256);
+  const bool twopass = twopass_env >= 0 ? twopass_env == 1 : (pred_bytes <= (96ull << 20) && tiles_est <= 4096);
   if (n > 0 && twopass) {
     const int R = selproj_rows_per_thread(P);
     const int64_t tiles = (int64_t)div_up((uint64_t)n, (uint64_t)R * 256);
