@@ -25,6 +25,9 @@
 // so every row is applied exactly once.
 // Roofline: HBM read. Algorithmic bytes per row = sum of the widths of the columns read
 // (24 B/row for the headline: k, a, b int64).
+#include <map>
+#include <mutex>
+
 #include "qe_internal.hpp"
 
 namespace qe {
@@ -1745,11 +1748,30 @@ static int run_update(qe_hashagg* h, Plan& P) {
     if (pfn) {
       // records of the partitioned update
     } else if (lds && ctx->jit) {
+      // kernel memoised on the plan's structure: source generation and the source-keyed module
+      // lookup ran on every update
+      static std::mutex memo_mu;
+      static std::map<std::string, std::pair<hipFunction_t, int>> memo;
+      const std::string key = plan_shape_key(ctx, P);
+      int bpc = 0;
+      bool have = false;
+      {
+        std::lock_guard<std::mutex> g(memo_mu);
+        auto it = memo.find(key);
+        if (it != memo.end()) {
+          jfn = it->second.first;
+          bpc = it->second.second;
+          have = true;
+        }
+      }
       std::string src;
       size_t jl = 0;
-      if (gen_fused_source(P, P.lds_log2, &src, &jl)) {
-        int bpc = 0;
-        if (jit_kernel(ctx, src, &jfn, &bpc) == QE_OK) {
+      if (have || gen_fused_source(P, P.lds_log2, &src, &jl)) {
+        if (have || jit_kernel(ctx, src, &jfn, &bpc) == QE_OK) {
+          if (!have) {
+            std::lock_guard<std::mutex> g(memo_mu);
+            memo[key] = {jfn, bpc};
+          }
           jgrid = (int)std::min<int64_t>(std::min<int64_t>((int64_t)ctx->num_cus * bpc, h->grid),
                                          (int64_t)div_up((uint64_t)waves, HA_THREADS / 64));
           if (jgrid < 1) jgrid = 1;

@@ -87,6 +87,11 @@ bool gen_pscatter_staged_source(const qe::Plan& P, int log2p, std::string* src);
 int jit_kernel(qe_ctx* ctx, const std::string& src, hipFunction_t* fn, int* blocks_per_cu,
                const char* name = "qe_fused", int block = 512);
 int jit_launch(qe_ctx* ctx, hipFunction_t fn, int grid, const qe::Plan& P, int block = 512);
+// Memo key of a plan's structure: the Plan bytes with run-time values cleared (buffer pointers
+// reduced to present / absent; literals, row count and base, table, defer, overflow and partition
+// fields zeroed), plus the device and the QE_NT load policy. Two plans with equal keys generate
+// the same kernel source.
+std::string plan_shape_key(const qe_ctx* ctx, const qe::Plan& P);
 // Fused-plan compilation shared by the aggregate and select-project paths (qe_hashagg.hip).
 int compile_inputs(const qe_column* cols, int32_t ncols, int32_t mask_col, int32_t nterms, const qe_pred_term* terms,
                    qe::Plan* P, bool* col_f64);

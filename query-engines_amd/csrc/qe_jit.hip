@@ -816,6 +816,33 @@ bool selproj_nt(const Plan& P) {
   return P.n > (64ll << 20);
 }
 
+std::string plan_shape_key(const qe_ctx* ctx, const Plan& P) {
+  Plan k;
+  memset(&k, 0, sizeof k);
+  memcpy(&k, &P, sizeof P);
+  for (int c = 0; c < QE_MAX_COLS; ++c) {
+    k.cols[c].p = (const void*)(uintptr_t)(P.cols[c].p != nullptr);
+    k.cols[c].valid = (const qu8*)(uintptr_t)(P.cols[c].valid != nullptr);
+  }
+  for (int t = 0; t < QE_MAX_TERMS; ++t) k.terms[t].lit = 0;
+  for (int j = 0; j < QE_MAX_AGGS; ++j) {
+    k.aggs[j].rhs_lit = 0;
+    for (int t = 0; t < QE_MAX_TOKENS; ++t) k.aggs[j].tok[t].lit = 0;
+  }
+  memset(&k.t, 0, sizeof k.t);
+  k.n = k.row_base = 0;
+  k.defer_in = nullptr;
+  k.defer_out = nullptr;
+  k.ovf = nullptr;
+  k.ovf_cap = 0;
+  k.part_rec = nullptr;
+  k.part_off = nullptr;
+  k.part_tw = 0;
+  k.part_slice = nullptr;
+  const int32_t extra[2] = {ctx->device, use_nt() ? 1 : 0};
+  return std::string((const char*)&k, sizeof k) + std::string((const char*)extra, sizeof extra);
+}
+
 int selproj_rows_per_thread(const Plan& P) {
   static const int env = [] {
     const char* e = getenv("QE_SELPROJ_ROWS");

@@ -20,49 +20,24 @@ using namespace qe;
 
 namespace {
 
-// Kernel of one plan shape and pass, memoised on the plan's structure: generating the source
-// (~6 us) and looking it up in the source-keyed module cache ran on every call, two passes per
-// call. The key is the Plan with its run-time values cleared (buffer pointers reduced to
-// present / absent, literals, row count, table and partition fields), plus everything else the
-// generator reads: output kinds, pass, rows per thread, load policy, device.
+// Kernel of one plan shape and pass, memoised on the plan's structure (plan_shape_key) plus what
+// else the generator reads: output kinds, pass, rows per thread, load policy. Generating the
+// source (~6 us) and looking it up in the source-keyed module cache ran on every call, two passes
+// per call.
 int selproj_kernel(qe_ctx* ctx, const Plan& P, const int32_t* out_kind, int nout, int mode, hipFunction_t* fn,
                    int* bpc) {
   struct Key {
-    Plan p;
     int32_t out_kind[QE_MAX_AGGS];
-    int32_t nout, mode, rows, nt, nt_env, device;
+    int32_t nout, mode, rows, nt;
   };
   Key k;
   memset(&k, 0, sizeof k);
-  memcpy(&k.p, &P, sizeof P);
-  for (int c = 0; c < QE_MAX_COLS; ++c) {
-    k.p.cols[c].p = (const void*)(uintptr_t)(P.cols[c].p != nullptr);
-    k.p.cols[c].valid = (const qu8*)(uintptr_t)(P.cols[c].valid != nullptr);
-  }
-  for (int t = 0; t < QE_MAX_TERMS; ++t) k.p.terms[t].lit = 0;
-  for (int j = 0; j < QE_MAX_AGGS; ++j) {
-    k.p.aggs[j].rhs_lit = 0;
-    for (int t = 0; t < QE_MAX_TOKENS; ++t) k.p.aggs[j].tok[t].lit = 0;
-  }
-  memset(&k.p.t, 0, sizeof k.p.t);
-  k.p.n = k.p.row_base = 0;
-  k.p.defer_in = nullptr;
-  k.p.defer_out = nullptr;
-  k.p.ovf = nullptr;
-  k.p.ovf_cap = 0;
-  k.p.part_rec = nullptr;
-  k.p.part_off = nullptr;
-  k.p.part_tw = 0;
-  k.p.part_slice = nullptr;
   for (int j = 0; j < nout; ++j) k.out_kind[j] = out_kind[j];
   k.nout = nout;
   k.mode = mode;
   k.rows = selproj_rows_per_thread(P);
   k.nt = selproj_nt(P);
-  const char* ne = getenv("QE_NT");
-  k.nt_env = !(ne && ne[0] == '0');
-  k.device = ctx->device;
-  const std::string key((const char*)&k, sizeof k);
+  const std::string key = plan_shape_key(ctx, P) + std::string((const char*)&k, sizeof k);
   static std::mutex mu;
   static std::map<std::string, std::pair<hipFunction_t, int>> memo;
   {
