@@ -54,22 +54,24 @@ def _cpu_lib():
     return lib, G
 
 
-def cpu_baseline(sample_rows: int, threads: int) -> dict:
+def cpu_baseline(sample_rows: int, threads: int):
     """Timed CPU legs (rank 0, N = 1) on bounded samples of the same rows:
     * `value`: the oracle's reference-faithful C restatement of the query (oracle/cpu_baseline.c:
       row-at-a-time Selection -> Projection -> HashMap aggregate with boxed keys and virtual
       accumulators, partition-parallel like Main.kt:1309-1325) on `threads` threads;
     * `single_thread`: the same port on one thread (SURVEY §8d: 1 thread and all threads);
     * `tuned`: a tuned C implementation (no boxing or materialisation, per-thread open-addressing
-      tables), so the GPU is also compared with a fast CPU engine."""
+      tables), so the GPU is also compared with a fast CPU engine.
+    Returns (the port's groups over the sample, key -> (SUM, COUNT, MIN, MAX); the JSON object)."""
     lib, G = _cpu_lib()
     out = (G * 2048)()
     ng = C.c_int64()
     secs = lib.qe_cpu_c4(0, sample_rows, 42, threads, 1 << 19, 1024, out, 2048, C.byref(ng))
+    groups = {int(g.key): (int(g.sum), int(g.count), int(g.min), int(g.max)) for g in out[:ng.value]}
     one_rows = min(sample_rows, 100_000_000)
     secs1 = lib.qe_cpu_c4(0, one_rows, 42, 1, 1 << 19, 1024, out, 2048, C.byref(ng))
     secs_t = lib.qe_cpu_c4_fast(0, sample_rows, 42, threads, 1 << 19, 1024, out, 2048, C.byref(ng))
-    return {"value": sample_rows / secs, "unit": "rows/s", "cores": threads, "kind": "port",
+    return groups, {"value": sample_rows / secs, "unit": "rows/s", "cores": threads, "kind": "port",
             "sample": f"rows 0..{sample_rows - 1} of the same C4 table (seed 42), {threads} threads, "
                       f"{secs:.3f} s; C restatement of the reference operator chain (oracle/cpu_baseline.c)",
             "single_thread": {"value": one_rows / secs1, "cores": 1,
@@ -183,10 +185,17 @@ def main():
         sr.append(ms.value)
     stream_gbs = rows * BYTES_PER_ROW / (sorted(sr)[2] * 1e-3) / 1e9
 
-    # sanity: every group present once across owners, COUNT(*) adds up to the filtered rows
-    groups = torch.tensor([keys[0].length, int(res[1].to_numpy().sum())], dtype=torch.int64, device="cuda")
+    # Result checks before any number is printed: every group present once across owners, and
+    # COUNT(*) adds up to the rows an independent torch kernel counts as passing the predicate.
+    a_col = cols[1].values[:rows]
+    selected = int((a_col > (1 << 19)).sum().item())
+    groups = torch.tensor([keys[0].length, int(res[1].to_numpy().sum()), selected], dtype=torch.int64, device="cuda")
     if world > 1:
         dist.all_reduce(groups)
+    n_groups, count_total, selected_total = (int(x) for x in groups.tolist())
+    if n_groups != 1024 or count_total != selected_total:
+        sys.exit(f"bench: wrong result: {n_groups} groups (want 1024), COUNT(*) total {count_total} "
+                 f"(want {selected_total})")
     ms_step = elapsed / args.steps * 1e3
     launches = sum(k for _, k in kernel_ms)
     avg_kernel_ms = sum(m for m, _ in kernel_ms) / max(1, launches)
@@ -225,11 +234,22 @@ def main():
             "bytes_per_launch": rows * BYTES_PER_ROW,
             "stream_read_ceiling_gbs": stream_gbs,
         },
-        "check": {"groups": int(groups[0].item()), "count_star_total": int(groups[1].item())},
+        "check": {"groups": n_groups, "count_star_total": count_total, "count_star_torch": selected_total},
     }
     if rank == 0 and world == 1 and not args.no_cpu:
         threads = args.cpu_threads or min(16, os.cpu_count() or 1)
-        line["cpu_baseline"] = cpu_baseline(args.cpu_sample_rows or rows, threads)
+        sample = args.cpu_sample_rows or rows
+        cpu_groups, line["cpu_baseline"] = cpu_baseline(sample, threads)
+        if sample == rows:
+            # the CPU port ran over exactly these rows: every group's SUM/COUNT/MIN/MAX must agree
+            kv = keys[0].to_numpy()
+            rv = [r.to_numpy() for r in res]
+            gpu_groups = {int(kv[i]): tuple(int(r[i]) for r in rv) for i in range(keys[0].length)}
+            if gpu_groups != cpu_groups:
+                bad = sorted(k for k in set(gpu_groups) | set(cpu_groups) if gpu_groups.get(k) != cpu_groups.get(k))
+                sys.exit(f"bench: {len(bad)} groups differ from the CPU port, e.g. key {bad[0]}: "
+                         f"gpu {gpu_groups.get(bad[0])} cpu {cpu_groups.get(bad[0])}")
+            line["check"]["cpu_port_groups_equal"] = True
     if rank == 0:
         print(json.dumps(line), flush=True)
     if dist.is_initialized():

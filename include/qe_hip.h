@@ -25,14 +25,28 @@
  * QE_ERR_UNSUPPORTED -> IllegalStateException (K:195, K:469, K:677, K:792, K:799),
  * QE_ERR_INVALID_ARG -> IllegalArgumentException (K:49), the rest -> RuntimeException.
  *
- * Threading: re-entrant. No global mutable state besides the thread-local error string;
- * each qe_ctx owns one HIP stream and its scratch memory (the reference calls the engine
- * concurrently from coroutine workers, one ExecutionContext each, K:1309-1313, K:1333).
+ * Threading: re-entrant. Each qe_ctx owns one HIP stream and its scratch memory (the
+ * reference calls the engine concurrently from coroutine workers, one ExecutionContext each,
+ * K:1309-1313, K:1333); one ctx must not be used by two threads at once. Process-wide state,
+ * each guarded by its own mutex and safe to share between ctxs and threads:
+ *   - the thread-local error string (qe_last_error);
+ *   - the device caching allocator (qe_runtime.hip dev_alloc/dev_free): freed blocks are kept
+ *     per device and size class and reused once the freeing stream's event has completed;
+ *     QE_CACHE_LIMIT_GB bounds what it keeps;
+ *   - the hipRTC module cache (qe_jit.hip): one code object per (device, plan shape), loaded
+ *     on first use and never unloaded for the life of the process, mirrored on disk in a
+ *     per-user 0700 directory;
+ *   - memo maps from plan structure to kernel (qe_selproj.hip, qe_hashagg.hip), which only
+ *     grow (one entry per distinct plan shape).
  *
  * Memory: all column buffers are DEVICE pointers on the ctx's device (hipMalloc'ed or
  * torch-allocated). Layout is the Arrow columnar format: fixed-width values buffer,
  * optional LSB-first validity bitmap (NULL = no nulls), bit-packed booleans, offset 0.
  * Results are written into caller-provided device buffers; sizes are queried first.
+ * Every OUTPUT validity or BOOL bitmap must be 4-byte aligned and padded to whole 32-bit
+ * words (ceil(rows/32)*4 bytes): kernels write bitmaps a 32-bit word at a time, and some
+ * clear the whole last word first. Arrow's recommended 64-byte buffer padding satisfies
+ * this; a minimal ceil(rows/8)-byte bitmap does not. Input bitmaps need no padding.
  */
 #ifndef QE_HIP_H
 #define QE_HIP_H

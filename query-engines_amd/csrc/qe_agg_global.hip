@@ -115,12 +115,13 @@ __global__ void __launch_bounds__(256) k_agg_global(const int64_t* __restrict__ 
       const int sh = (int)(r0 & 7);
       uint32_t inrange = full ? 3u : (uint32_t)((r0 < n) | ((r0 + 1 < n) << 1));
       uint32_t sel = inrange;
-      if (mv) {
+      // bitmaps are read only for rows < n: an input bitmap may be Arrow-minimal (ceil(n/8) B)
+      if (mv && sel) {
         uint32_t m = (uint32_t)(mv[r0 >> 3] >> sh);
         if (ml) m &= (uint32_t)(ml[r0 >> 3] >> sh);
         sel &= m;
       }
-      const uint32_t nn = valid ? (sel & (uint32_t)(valid[r0 >> 3] >> sh)) : sel;
+      const uint32_t nn = valid && sel ? (sel & (uint32_t)(valid[r0 >> 3] >> sh)) : sel;
       p.rows += __popc(sel & 3u);
 #pragma unroll
       for (int j = 0; j < 2; ++j) {

@@ -213,8 +213,9 @@ __device__ __forceinline__ void load_cols(const Plan& P, qi64 base, int lane, bo
       qu32 vv = 15u;
       if (c < P.ncols && P.cols[c].valid) {
         const qi64 r0 = base + 2 * lane;
-        const qu32 lo = (qu32)(P.cols[c].valid[r0 >> 3] >> (r0 & 7)) & 3u;
-        const qu32 hi = (qu32)(P.cols[c].valid[(r0 + 128) >> 3] >> (r0 & 7)) & 3u;
+        // bytes past ceil(n/8) are never read: an input bitmap may be Arrow-minimal
+        const qu32 lo = r0 < P.n ? (qu32)(P.cols[c].valid[r0 >> 3] >> (r0 & 7)) & 3u : 0u;
+        const qu32 hi = r0 + 128 < P.n ? (qu32)(P.cols[c].valid[(r0 + 128) >> 3] >> (r0 & 7)) & 3u : 0u;
         vv = lo | (hi << 2);
       }
       valid |= vv << (4 * c);
@@ -282,7 +283,7 @@ __device__ __forceinline__ void load_cols(const Plan& P, qi64 base, int lane, bo
       }
       R.v[4 * c + 2 * q] = a;
       R.v[4 * c + 2 * q + 1] = b;
-      const qu32 vv = col.valid ? ((qu32)(col.valid[r0 >> 3] >> (r0 & 7)) & 3u) : 3u;
+      const qu32 vv = !col.valid ? 3u : r0 < P.n ? ((qu32)(col.valid[r0 >> 3] >> (r0 & 7)) & 3u) : 0u;
       R.valid |= vv << (4 * c + 2 * q);
     }
   }
@@ -1234,12 +1235,18 @@ static int table_alloc(qe_hashagg* h, uint64_t cap, void** mem, DTable* t) {
 
 // ctl words: [0] groups, [1] deferred rows, [2] overflow records, [3] lost groups,
 // [4] largest slot count reported by the senders of an import_slots, [5] their records in total
+// ctl[3] is sticky: every path that can drop a group (k_rehash, k_import, k_import_slots, the
+// fused kernel's overflow area) adds to it and nothing but a reset clears it, so a loss in a
+// launch with no read-back of its own (qe_hashagg_import_slots queues k_import_slots and returns)
+// fails the next call that reads the counters — at the latest finalize / num_groups.
 static int read_ctl(qe_hashagg* h, uint64_t out[8]) {
   void* p;
   QE_TRY(ctx_pinned(h->ctx, 64, &p));
   QE_HIP(hipMemcpyAsync(p, h->ctl, 64, hipMemcpyDeviceToHost, h->ctx->stream));
   QE_HIP(hipStreamSynchronize(h->ctx->stream));
   memcpy(out, p, 64);
+  QE_CHECK(out[3] == 0, QE_ERR_CAPACITY, "hash aggregate lost %llu groups (probe limit or overflow area)",
+           (unsigned long long)out[3]);
   return QE_OK;
 }
 
@@ -1258,7 +1265,6 @@ static int table_grow(qe_hashagg* h, uint64_t want_cap) {
   QE_TRY(table_alloc(h, cap, &mem, &nt));
   // the group counter is recomputed by the re-insert
   QE_HIP(hipMemsetAsync(h->ctl, 0, 8, h->ctx->stream));
-  QE_HIP(hipMemsetAsync(h->ctl + 3, 0, 8, h->ctx->stream));
   const int grid = (int)std::min<uint64_t>(div_up(h->t.cap + 2, 256), 8192);
   hipLaunchKernelGGL(k_rehash, dim3(grid), dim3(256), 0, h->ctx->stream, h->t, nt, agg_meta(h));
   QE_TRY(launch_check("k_rehash"));
@@ -1813,7 +1819,6 @@ static int run_update(qe_hashagg* h, Plan& P) {
     // grow, then re-apply what could not be inserted
     QE_TRY(table_grow(h, std::max<uint64_t>(4 * h->t.cap, 2 * (groups + ovf_recs))));
     if (ovf_recs) {
-      QE_HIP(hipMemsetAsync(h->ctl + 3, 0, 8, ctx->stream));
       QE_TRY(import_records(h, h->ovf, (int64_t)ovf_recs));
     }
     if (deferred == 0) break;
@@ -2221,7 +2226,6 @@ int qe_hashagg_import_slots(qe_hashagg* h, const void* slots, int32_t nslots, in
   if (c[5] == 0) return QE_OK;
   if (2 * (c[0] + c[5]) > h->t.cap) QE_TRY(table_grow(h, 2 * (c[0] + c[5])));
   h->known_groups = -1;
-  QE_HIP(hipMemsetAsync(h->ctl + 3, 0, 8, ctx->stream));
   const int grid = (int)std::min<uint64_t>(div_up((uint64_t)nslots * slot_records, 256), 8192);
   hipLaunchKernelGGL(k_import_slots, dim3(grid), dim3(256), 0, ctx->stream, (const uint8_t*)slots, nslots,
                      (qi64)slot_records, h->rec_bytes, h->t, agg_meta(h));
@@ -2237,7 +2241,6 @@ int qe_hashagg_import(qe_hashagg* h, const void* records, int64_t nrecords) {
   uint64_t c[8];
   QE_TRY(read_ctl(h, c));
   if (2 * (c[0] + (uint64_t)nrecords) > h->t.cap) QE_TRY(table_grow(h, 2 * (c[0] + (uint64_t)nrecords)));
-  QE_HIP(hipMemsetAsync(h->ctl + 3, 0, 8, h->ctx->stream));
   return import_records(h, records, nrecords);
 }
 

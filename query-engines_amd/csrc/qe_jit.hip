@@ -16,6 +16,8 @@
 #include <hip/hiprtc.h>
 #include <stdio.h>
 #include <stdlib.h>
+#include <fcntl.h>
+#include <string.h>
 #include <sys/stat.h>
 #include <unistd.h>
 
@@ -206,7 +208,7 @@ void emit_col_loads(const Plan& P, std::ostringstream& o, unsigned need) {
     o << "    }\n";
     if (P.cols[c].valid) {
       o << "    qu32 v" << cs << ";\n    {\n      const qu8* vb = P.cols[" << cs << "].valid;\n"
-        << "      const qu32 lo = (qu32)(vb[r0 >> 3] >> (r0 & 7)) & 3u;\n"
+        << "      const qu32 lo = (full || r0 < P.n) ? ((qu32)(vb[r0 >> 3] >> (r0 & 7)) & 3u) : 0u;\n"
         << "      const qu32 hi = (full || r0 + 128 < P.n) ? ((qu32)(vb[(r0 + 128) >> 3] >> (r0 & 7)) & 3u) : 0u;\n"
         << "      v" << cs << " = lo | (hi << 2);\n    }\n";
     }
@@ -1082,30 +1084,75 @@ uint64_t fnv1a(const std::string& s) {
   return h;
 }
 
+// On-disk cache of compiled code objects. The directory is private to the effective user:
+// $QE_JIT_CACHE, else $XDG_CACHE_HOME/qe_jit, else /tmp/qe_jit_cache-<uid>; created 0700 and used
+// only while it is a real directory (not a symlink) owned by this user with no group/other
+// access. Returns "" (memory-only caching) otherwise, so no other local user can plant device
+// code that this process would load.
 std::string cache_dir() {
-  const char* d = getenv("QE_JIT_CACHE");
-  return d && *d ? std::string(d) : std::string("/tmp/qe_jit_cache");
+  static std::string dir = [] {
+    std::string d;
+    const char* e = getenv("QE_JIT_CACHE");
+    const char* x = getenv("XDG_CACHE_HOME");
+    if (e && *e) d = e;
+    else if (x && *x) d = std::string(x) + "/qe_jit";
+    else d = "/tmp/qe_jit_cache-" + std::to_string((long)geteuid());
+    mkdir(d.c_str(), 0700);
+    struct stat st;
+    if (lstat(d.c_str(), &st) != 0 || !S_ISDIR(st.st_mode) || st.st_uid != geteuid() || (st.st_mode & 077) != 0)
+      return std::string();
+    return d;
+  }();
+  return dir;
 }
 
-bool read_file(const std::string& path, std::vector<char>* out) {
-  FILE* f = fopen(path.c_str(), "rb");
-  if (!f) return false;
-  fseek(f, 0, SEEK_END);
-  const long n = ftell(f);
-  fseek(f, 0, SEEK_SET);
-  out->resize(n > 0 ? (size_t)n : 0);
-  const bool ok = n > 0 && fread(out->data(), 1, (size_t)n, f) == (size_t)n;
+// Entry file: magic | u64 key length | u64 code length | u64 fnv1a(code) | key text | code.
+// The full key text (hipRTC version, options, kernel source) is compared on load, so a name
+// collision or a stale toolchain never loads the wrong code; the code hash catches truncation.
+constexpr char kMagic[8] = {'Q', 'E', 'J', 'I', 'T', 'C', 'O', '2'};
+
+bool read_entry(const std::string& path, const std::string& key, std::vector<char>* code) {
+  const int fd = open(path.c_str(), O_RDONLY | O_NOFOLLOW | O_CLOEXEC);
+  if (fd < 0) return false;
+  FILE* f = fdopen(fd, "rb");
+  if (!f) {
+    close(fd);
+    return false;
+  }
+  struct stat st;
+  bool ok = fstat(fd, &st) == 0 && S_ISREG(st.st_mode) && st.st_uid == geteuid() && (st.st_mode & 022) == 0;
+  char magic[8];
+  uint64_t hdr[3] = {0, 0, 0};
+  ok = ok && fread(magic, 1, 8, f) == 8 && memcmp(magic, kMagic, 8) == 0 && fread(hdr, 8, 3, f) == 3 &&
+       hdr[0] == key.size() && hdr[1] > 0 && (uint64_t)st.st_size == 32 + hdr[0] + hdr[1];
+  if (ok) {
+    std::string k(hdr[0], '\0');
+    ok = fread(&k[0], 1, hdr[0], f) == hdr[0] && k == key;
+  }
+  if (ok) {
+    code->resize(hdr[1]);
+    ok = fread(code->data(), 1, hdr[1], f) == hdr[1] &&
+         fnv1a(std::string(code->data(), code->size())) == hdr[2];
+  }
   fclose(f);
   return ok;
 }
 
-void write_file(const std::string& path, const std::vector<char>& data) {
+void write_entry(const std::string& path, const std::string& key, const std::vector<char>& code) {
   const std::string tmp = path + ".tmp" + std::to_string((long)getpid());
-  FILE* f = fopen(tmp.c_str(), "wb");
-  if (!f) return;
-  const bool ok = fwrite(data.data(), 1, data.size(), f) == data.size();
-  fclose(f);
-  if (ok) rename(tmp.c_str(), path.c_str());
+  const int fd = open(tmp.c_str(), O_WRONLY | O_CREAT | O_EXCL | O_NOFOLLOW | O_CLOEXEC, 0600);
+  if (fd < 0) return;
+  FILE* f = fdopen(fd, "wb");
+  if (!f) {
+    close(fd);
+    remove(tmp.c_str());
+    return;
+  }
+  const uint64_t hdr[3] = {key.size(), code.size(), fnv1a(std::string(code.data(), code.size()))};
+  const bool ok = fwrite(kMagic, 1, 8, f) == 8 && fwrite(hdr, 8, 3, f) == 3 &&
+                  fwrite(key.data(), 1, key.size(), f) == key.size() &&
+                  fwrite(code.data(), 1, code.size(), f) == code.size();
+  if (fclose(f) == 0 && ok) rename(tmp.c_str(), path.c_str());
   else remove(tmp.c_str());
 }
 
@@ -1127,12 +1174,18 @@ int jit_kernel(qe_ctx* ctx, const std::string& src, hipFunction_t* fn, int* bloc
   const std::string opt_arch = "--offload-arch=" + arch;
   // no FMA contraction: a*b+c rounds twice, as the reference (JVM) arithmetic does
   const char* opts[] = {opt_arch.c_str(), "-O3", "-ffp-contract=off", "-munsafe-fp-atomics", "-std=c++17"};
+  int rtc_major = 0, rtc_minor = 0;
+  hiprtcVersion(&rtc_major, &rtc_minor);
+  std::string disk_key = "hiprtc " + std::to_string(rtc_major) + "." + std::to_string(rtc_minor) + " HIP " +
+                         std::to_string(HIP_VERSION) + " " + arch;
+  for (const char* o : opts) disk_key += std::string(" ") + o;
+  disk_key += "\n" + src;
   char name[64];
-  snprintf(name, sizeof(name), "%016llx", (unsigned long long)fnv1a(src + arch + " -O3 -ffp-contract=off -munsafe-fp-atomics"));
+  snprintf(name, sizeof(name), "%016llx", (unsigned long long)fnv1a(disk_key));
   const std::string dir = cache_dir();
-  const std::string path = dir + "/" + name + ".co";
+  const std::string path = dir.empty() ? std::string() : dir + "/" + name + ".co";
   std::vector<char> code;
-  if (!read_file(path, &code)) {
+  if (path.empty() || !read_entry(path, disk_key, &code)) {
     hiprtcProgram prog;
     if (hiprtcCreateProgram(&prog, src.c_str(), "qe_fused.hip", 0, nullptr, nullptr) != HIPRTC_SUCCESS)
       return fail(QE_ERR_DEVICE, "hiprtcCreateProgram failed");
@@ -1150,8 +1203,7 @@ int jit_kernel(qe_ctx* ctx, const std::string& src, hipFunction_t* fn, int* bloc
     code.resize(cs);
     hiprtcGetCode(prog, code.data());
     hiprtcDestroyProgram(&prog);
-    mkdir(dir.c_str(), 0777);
-    write_file(path, code);
+    if (!path.empty()) write_entry(path, disk_key, code);
   }
   Entry e;
   QE_HIP(hipModuleLoadData(&e.mod, code.data()));

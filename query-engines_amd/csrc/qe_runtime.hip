@@ -178,13 +178,15 @@ int ctx_enter(qe_ctx* ctx) {
 int ctx_scratch(qe_ctx* ctx, size_t bytes, void** out) {
   if (bytes == 0) bytes = 256;
   if (bytes > ctx->scratch_bytes) {
+    const size_t old = ctx->scratch_bytes;
     if (ctx->scratch) {
       QE_HIP(hipStreamSynchronize(ctx->stream));
       QE_HIP(hipFree(ctx->scratch));
       ctx->scratch = nullptr;
       ctx->scratch_bytes = 0;
     }
-    size_t want = bytes < 2 * ctx->scratch_bytes ? 2 * ctx->scratch_bytes : bytes;
+    // geometric growth: a series of slightly larger requests reallocates O(log) times
+    size_t want = bytes < 2 * old ? 2 * old : bytes;
     want = (want + 4095) & ~size_t(4095);
     if (hipMalloc(&ctx->scratch, want) != hipSuccess) {
       (void)hipGetLastError();

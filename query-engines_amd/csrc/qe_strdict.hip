@@ -886,8 +886,8 @@ int qe_strdict_encode(qe_strdict* d, const qe_column* in, qe_column* codes) {
   codes->length = n;
   if (n == 0) return QE_OK;
   if (in->validity)
-    QE_HIP(hipMemcpyAsync(codes->validity, in->validity, (size_t)div_up((uint64_t)n, 32) * 4, hipMemcpyDeviceToDevice,
-                          ctx->stream));
+    QE_HIP(hipMemcpyAsync(codes->validity, in->validity, (size_t)div_up((uint64_t)n, 8), hipMemcpyDeviceToDevice,
+                          ctx->stream));  // an input bitmap may be Arrow-minimal: ceil(n/8) bytes
   int32_t o[2] = {0, 0};
   QE_HIP(hipMemcpy(o, in->offsets + n, 4, hipMemcpyDeviceToHost));
   QE_HIP(hipMemcpy(o + 1, in->offsets, 4, hipMemcpyDeviceToHost));
@@ -1067,7 +1067,7 @@ int qe_strdict_decode(qe_strdict* d, const qe_column* codes, qe_column* out) {
                      (uint8_t*)out->values);
   QE_TRY(launch_check("k_dict_decode_copy"));
   if (codes->validity)
-    QE_HIP(hipMemcpyAsync(out->validity, codes->validity, (size_t)div_up((uint64_t)n, 32) * 4,
+    QE_HIP(hipMemcpyAsync(out->validity, codes->validity, (size_t)div_up((uint64_t)n, 8),
                           hipMemcpyDeviceToDevice, ctx->stream));
   return QE_OK;
 }

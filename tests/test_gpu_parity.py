@@ -946,3 +946,50 @@ def test_filter_utf8_columns(gpu_ctx, n):
     want = [s for s, keep in zip(strs, m) if keep]
     assert out.field(0).to_pylist() == want
     assert out.field(1).to_numpy().tolist() == np.nonzero(m)[0].tolist()
+
+
+def _unfmix64(h: int) -> int:
+    """Inverse of the murmur3 finaliser (qe_dev.hpp fmix64): a key whose table hash is `h`."""
+    m = (1 << 64) - 1
+    h ^= h >> 33
+    h = (h * pow(0xC4CEB9FE1A85EC53, -1, 1 << 64)) & m
+    h ^= h >> 33
+    h = (h * pow(0xFF51AFD7ED558CCD, -1, 1 << 64)) & m
+    h ^= h >> 33
+    return h - (1 << 64) if h >= 1 << 63 else h
+
+
+@pytest.mark.parametrize("path", ["slots", "records"])
+def test_import_probe_limit_loses_no_group_silently(gpu_ctx, path):
+    """300 keys whose global-table hash shares its low 32 bits form one probe chain longer than
+    the probe limit (HA_GLOBAL_MAXP = 256) at every table size, so an import must drop groups.
+    The loss must surface as CapacityError — on the slot path (k_import_slots runs without a
+    read-back of its own) at the latest from finalize — never as a silently short result."""
+    import torch
+
+    from oracle import records as R
+
+    keys = [_unfmix64((j << 32) | 0x1234) for j in range(1, 301)]
+    assert all(R.fmix64(k) & 0xFFFFFFFF == 0x1234 for k in keys)
+    fns = [R.AGG_SUM, R.AGG_COUNT_STAR]
+    groups = {k: (1, [(k, 1), (0, 1)]) for k in keys}
+    aggs = [(N.AGG_SUM, N.TYPE_INT64), (N.AGG_COUNT_STAR, N.TYPE_INT64)]
+    st = HashAggregateState(gpu_ctx, [N.TYPE_INT64], aggs, 1024)
+    with pytest.raises(N.CapacityError, match="lost"):
+        if path == "slots":
+            buf = R.encode_slots(groups, fns, 1, 512)
+            dev = torch.frombuffer(bytearray(buf), dtype=torch.uint8).to(gpu_ctx.torch_device)
+            assert st.import_slots(dev, 1, 512) == 300
+            st.finalize()
+        else:
+            payload, counts = R.encode(groups, fns, 1)
+            dev = torch.frombuffer(bytearray(payload), dtype=torch.uint8).to(gpu_ctx.torch_device)
+            st.import_records(dev, counts[0])
+    # the same keys spread over distinct chains import and finalise exactly
+    st2 = HashAggregateState(gpu_ctx, [N.TYPE_INT64], aggs, 1024)
+    spread = {j * 7919 + 1: (1, [(j, 1), (0, 1)]) for j in range(300)}
+    buf = R.encode_slots(spread, fns, 1, 512)
+    dev = torch.frombuffer(bytearray(buf), dtype=torch.uint8).to(gpu_ctx.torch_device)
+    assert st2.import_slots(dev, 1, 512) == 300
+    kc, res = st2.finalize()
+    assert kc[0].length == 300 and int(res[1].to_numpy().sum()) == 300
