@@ -1773,13 +1773,13 @@ static int run_update(qe_hashagg* h, Plan& P) {
       std::string src;
       size_t jl = 0;
       if (have || gen_fused_source(P, P.lds_log2, &src, &jl)) {
-        if (have || jit_kernel(ctx, src, &jfn, &bpc) == QE_OK) {
+        if (have || jit_kernel(ctx, src, &jfn, &bpc, "qe_fused", fused_block()) == QE_OK) {
           if (!have) {
             std::lock_guard<std::mutex> g(memo_mu);
             memo[key] = {jfn, bpc};
           }
-          jgrid = (int)std::min<int64_t>(std::min<int64_t>((int64_t)ctx->num_cus * bpc, h->grid),
-                                         (int64_t)div_up((uint64_t)waves, HA_THREADS / 64));
+          jgrid = (int)std::min<int64_t>(std::min<int64_t>((int64_t)ctx->num_cus * bpc, h->grid * 512 / fused_block()),
+                                         (int64_t)div_up((uint64_t)waves, fused_block() / 64));
           if (jgrid < 1) jgrid = 1;
           h->jit_note.clear();
         } else {
@@ -1794,7 +1794,7 @@ static int run_update(qe_hashagg* h, Plan& P) {
     }
     if (pass > 0 || mp > 0) QE_HIP(hipEventRecord(h->ev[0], ctx->stream));
     if (jfn) {
-      QE_TRY(jit_launch(ctx, jfn, jgrid, P));
+      QE_TRY(jit_launch(ctx, jfn, jgrid, P, pfn ? 512 : fused_block()));
     } else {
       QE_TRY(launch_hashagg(P, grid, lds, ctx->stream));
     }

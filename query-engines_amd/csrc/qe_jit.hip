@@ -131,6 +131,29 @@ bool use_nt() {
   const char* e = getenv("QE_NT");
   return !(e && e[0] == '0');
 }
+}  // namespace
+
+// Fused aggregate kernel shape knobs (read once per process).
+// QE_FUSED_PF=1: load step i+1's columns before step i's LDS work (software pipeline).
+bool fused_prefetch() {
+  static const bool v = [] {
+    const char* e = getenv("QE_FUSED_PF");
+    return e && e[0] == '1';
+  }();
+  return v;
+}
+// QE_FUSED_BLOCK: workgroup size of the fused kernel (256 / 512 / 1024).
+int fused_block() {
+  static const int v = [] {
+    const char* e = getenv("QE_FUSED_BLOCK");
+    const int b = e ? atoi(e) : 512;
+    return (b == 256 || b == 1024) ? b : 512;
+  }();
+  return v;
+}
+
+namespace {
+
 std::string ld(const std::string& type, const std::string& ptr, bool nt = true) {
   if (nt && use_nt()) return "__builtin_nontemporal_load((const " + type + "*)(" + ptr + "))";
   return "(*(const " + type + "*)(" + ptr + "))";
@@ -176,41 +199,47 @@ unsigned pred_key_cols(const Plan& P) {
 }
 
 // Column loads of one 256-row wave step (lane rows r0 + {0,1} and r0 + 128 + {0,1}) for the
-// slots in `need`: c<slot>[4] values (sign-/zero-extended), v<slot> validity bits.
-void emit_col_loads(const Plan& P, std::ostringstream& o, unsigned need) {
+// slots in `need`: c<slot>[4] values (sign-/zero-extended), v<slot> validity bits. `pre` names
+// the destination arrays (the prefetching fused kernel loads the next step into p<slot>/pv<slot>);
+// `declare` = false stores into arrays declared earlier.
+void emit_col_loads(const Plan& P, std::ostringstream& o, unsigned need, const std::string& pre = "c",
+                    bool declare = true) {
+  const std::string vpre = pre == "c" ? "v" : "p" + std::string("v");
   for (int c = 0; c < P.ncols; ++c) {
     if (!((need >> c) & 1u)) continue;
     const std::string cs = std::to_string(c);
-    o << "    qi64 c" << cs << "[4];\n";
+    const std::string dst = pre + cs;
+    if (declare) o << "    qi64 " << dst << "[4];\n";
     const int kind = P.cols[c].kind;
     const char* ty = kind == K_I32 ? "qi32" : kind == K_U8 ? "qu8" : kind == K_BOOL ? "qu8" : "qi64";
     o << "    {\n      const " << ty << "* p = (const " << ty << "*)P.cols[" << cs << "].p;\n";
     if (kind == K_BOOL) {
       o << "      for (int r = 0; r < 4; ++r) { const qi64 row = r0 + 128 * (r >> 1) + (r & 1);\n"
-        << "        c" << cs << "[r] = (full || row < P.n) ? ((p[row >> 3] >> (row & 7)) & 1) : 0; }\n";
+        << "        " << dst << "[r] = (full || row < P.n) ? ((p[row >> 3] >> (row & 7)) & 1) : 0; }\n";
     } else {
       o << "      if (full) {\n";
       if (kind == K_I64 || kind == K_F64) {
         o << "        const qi64x2 a = " << ld("qi64x2", "p + r0") << ", b = " << ld("qi64x2", "p + r0 + 128") << ";\n"
-          << "        c" << cs << "[0] = a.x; c" << cs << "[1] = a.y; c" << cs << "[2] = b.x; c" << cs << "[3] = b.y;\n";
+          << "        " << dst << "[0] = a.x; " << dst << "[1] = a.y; " << dst << "[2] = b.x; " << dst << "[3] = b.y;\n";
       } else if (kind == K_I32) {
         o << "        const qi32x2 a = " << ld("qi32x2", "p + r0") << ", b = " << ld("qi32x2", "p + r0 + 128") << ";\n"
-          << "        c" << cs << "[0] = a.x; c" << cs << "[1] = a.y; c" << cs << "[2] = b.x; c" << cs << "[3] = b.y;\n";
+          << "        " << dst << "[0] = a.x; " << dst << "[1] = a.y; " << dst << "[2] = b.x; " << dst << "[3] = b.y;\n";
       } else {  // K_U8
         o << "        const qu16 a = " << ld("qu16", "p + r0") << ", b = " << ld("qu16", "p + r0 + 128") << ";\n"
-          << "        c" << cs << "[0] = a & 0xFF; c" << cs << "[1] = a >> 8; c" << cs << "[2] = b & 0xFF; c" << cs
+          << "        " << dst << "[0] = a & 0xFF; " << dst << "[1] = a >> 8; " << dst << "[2] = b & 0xFF; " << dst
           << "[3] = b >> 8;\n";
       }
       o << "      } else {\n"
         << "        for (int r = 0; r < 4; ++r) { const qi64 row = r0 + 128 * (r >> 1) + (r & 1);\n"
-        << "          c" << cs << "[r] = row < P.n ? (qi64)p[row] : 0; }\n      }\n";
+        << "          " << dst << "[r] = row < P.n ? (qi64)p[row] : 0; }\n      }\n";
     }
     o << "    }\n";
     if (P.cols[c].valid) {
-      o << "    qu32 v" << cs << ";\n    {\n      const qu8* vb = P.cols[" << cs << "].valid;\n"
+      if (declare) o << "    qu32 " << vpre << cs << ";\n";
+      o << "    {\n      const qu8* vb = P.cols[" << cs << "].valid;\n"
         << "      const qu32 lo = (full || r0 < P.n) ? ((qu32)(vb[r0 >> 3] >> (r0 & 7)) & 3u) : 0u;\n"
         << "      const qu32 hi = (full || r0 + 128 < P.n) ? ((qu32)(vb[(r0 + 128) >> 3] >> (r0 & 7)) & 3u) : 0u;\n"
-        << "      v" << cs << " = lo | (hi << 2);\n    }\n";
+        << "      " << vpre << cs << " = lo | (hi << 2);\n    }\n";
     }
   }
 }
@@ -407,16 +436,35 @@ bool gen_fused_source(const Plan& P, int log2, std::string* src, size_t* lds_byt
     ok[j] = ex[j].ok;
   }
   std::ostringstream o;
+  const bool pf = fused_prefetch();
   o << "\nusing namespace qe;\n"
-    << "extern \"C\" __global__ void __launch_bounds__(512) qe_fused(const Plan P) {\n";
+    << "extern \"C\" __global__ void __launch_bounds__(" << fused_block() << ") qe_fused(const Plan P) {\n";
   emit_lds_table(P, o, log2, lds_bytes);
   o << "  const int lane = threadIdx.x & 63;\n"
     << "  const qi64 wave = (blockIdx.x * (qi64)blockDim.x + threadIdx.x) >> 6;\n"
-    << "  const qi64 stride = (((qi64)gridDim.x * blockDim.x) >> 6) * 256;\n"
-    << "  for (qi64 base = wave * 256; base < P.n; base += stride) {\n"
-    << "    const bool full = base + 256 <= P.n;\n"
-    << "    const qi64 r0 = base + 2 * lane;\n";
-  emit_col_loads(P, o, ~0u);
+    << "  const qi64 stride = (((qi64)gridDim.x * blockDim.x) >> 6) * 256;\n";
+  if (pf) {
+    // software pipeline: the next step's columns are loaded before this step's LDS work
+    o << "  {\n    const qi64 base = wave * 256;\n    const bool full = base + 256 <= P.n;\n"
+      << "    const qi64 r0 = base + 2 * lane;\n";
+    emit_col_loads(P, o, ~0u, "p", true);
+    o << "  for (qi64 base = wave * 256; base < P.n; base += stride) {\n"
+      << "    const bool full = base + 256 <= P.n;\n"
+      << "    const qi64 r0 = base + 2 * lane;\n";
+    for (int c = 0; c < P.ncols; ++c) {
+      o << "    qi64 c" << c << "[4] = {p" << c << "[0], p" << c << "[1], p" << c << "[2], p" << c << "[3]};\n";
+      if (P.cols[c].valid) o << "    const qu32 v" << c << " = pv" << c << ";\n";
+    }
+    o << "    if (base + stride < P.n) {\n      const qi64 nb = base + stride;\n"
+      << "      const bool full = nb + 256 <= P.n;\n      const qi64 r0 = nb + 2 * lane;\n";
+    emit_col_loads(P, o, ~0u, "p", false);
+    o << "    }\n    do {\n";
+  } else {
+    o << "  for (qi64 base = wave * 256; base < P.n; base += stride) {\n"
+      << "    const bool full = base + 256 <= P.n;\n"
+      << "    const qi64 r0 = base + 2 * lane;\n";
+    emit_col_loads(P, o, ~0u);
+  }
   emit_active_rows(P, o, true);
   emit_keys(P, o);
   if (P.mp_n > 1)
@@ -424,7 +472,7 @@ bool gen_fused_source(const Plan& P, int log2, std::string* src, size_t* lds_byt
       << "      if (((act >> r) & 1) && (qu32)__umul64hi(fmix64((qu64)key[r]), (qu64)P.mp_n) != (qu32)P.mp_pass) act &= ~(1u << r);\n"
       << "    if (act == 0) continue;\n";
   emit_agg_rows(P, o, val, ok, "P.row_base + r0 + 128 * (r >> 1) + (r & 1)", "r0 + 128 * (r >> 1) + (r & 1)");
-  o << "  }\n";
+  o << (pf ? "    } while (0);\n  }\n  }\n" : "  }\n");
   emit_flush(P, o);
   o << "}\n";
   *src = std::string(kDevHeader) + o.str();
@@ -855,100 +903,53 @@ int selproj_rows_per_thread(const Plan& P) {
   return P.ncols <= 3 ? 16 : (P.ncols <= 6 ? 8 : 4);
 }
 
-bool gen_selproj_source(const Plan& P, const int32_t* out_kind, int nout, std::string* src, int mode) {
-  if (P.ncols < 1 || P.ncols > QE_MAX_COLS || nout < 1 || nout > QE_MAX_AGGS) return false;
-  const int R = selproj_rows_per_thread(P);
-  const bool persistent = mode == SP_PERSIST;
-  // the count pass loads only the predicate's columns
-  const unsigned need = mode == SP_COUNT ? pred_key_cols(P) : ~0u;
-  std::ostringstream o;
-  o << "\nusing namespace qe;\n"
-    << "extern \"C\" __global__ void __launch_bounds__(256) qe_selproj(const Plan P) {\n"
-    << "  constexpr int R = " << R << ";\n"
-    << "  constexpr qu64 F_AGG = 1ull << 62, F_INC = 2ull << 62, VMASK = (1ull << 62) - 1;\n"
-    << "  constexpr bool PERSIST = " << (persistent ? "true" : "false") << ";\n"
-    << "  __shared__ qu32 s_cnt[R * 4];\n  __shared__ qu64 s_base;\n  __shared__ qu32 s_tile, s_total;\n"
-    << "  __shared__ qi64 s_out[" << ((size_t)nout * R * 256 * 8 <= 64 * 1024 ? nout * R * 256 : 1) << "];\n"
-    << "  const int t = threadIdx.x, lane = t & 63, w = t >> 6;\n";
-  // column loads of the tile at `b` into <cp><slot>[R] / <vp><slot> (validity bits)
-  auto emit_loads = [&](const std::string& cp, const std::string& vp, const std::string& b, const std::string& ind) {
-    for (int c = 0; c < P.ncols; ++c) {
-      if (!((need >> c) & 1u)) continue;
-      const std::string cs = std::to_string(c);
-      const int kind = P.cols[c].kind;
-      const char* ty = kind == K_I32 ? "qi32" : (kind == K_U8 || kind == K_BOOL) ? "qu8" : "qi64";
-      o << ind << "{\n" << ind << "  const qi64 lb = " << b << ";\n" << ind << "  const bool lfull = lb + R * 256 <= P.n;\n"
-        << ind << "  const " << ty << "* p = (const " << ty << "*)P.cols[" << cs << "].p;\n"
-        << "#pragma unroll\n" << ind << "  for (int r = 0; r < R; ++r) {\n" << ind << "    const qi64 row = lb + r * 256 + t;\n";
-      if (kind == K_BOOL)
-        o << ind << "    " << cp << cs << "[r] = (lfull || row < P.n) ? ((p[row >> 3] >> (row & 7)) & 1) : 0;\n";
-      else
-        // default policy below 64M rows: C2-sized inputs stay in the MALL (nt 68.4 us, default 65.0 us)
-        o << ind << "    " << cp << cs << "[r] = (lfull || row < P.n) ? (qi64)" << ld(ty, "p + row", selproj_nt(P)) << " : 0;\n";
-      o << ind << "  }\n";
-      if (P.cols[c].valid) {
-        o << ind << "  const qu8* vb = P.cols[" << cs << "].valid;\n" << ind << "  " << vp << cs << " = 0;\n"
-          << "#pragma unroll\n" << ind << "  for (int r = 0; r < R; ++r) {\n" << ind << "    const qi64 row = lb + r * 256 + t;\n"
-          << ind << "    if (lfull || row < P.n) " << vp << cs << " |= (qu32)((vb[row >> 3] >> (row & 7)) & 1) << r;\n"
-          << ind << "  }\n";
-      }
-      o << ind << "}\n";
-    }
-  };
-  if (persistent) {
-    // Every workgroup is resident (grid <= CUs x occupancy), so a static tile order cannot
-    // deadlock the look-back and no tile counter is needed. (Prefetching the next tile's columns
-    // into registers during this tile's look-back measured slower: 5.00 vs 4.67 ms at 1B rows.)
-    o << "  for (qu32 tile = blockIdx.x; (qu64)tile < P.t.cap; tile += gridDim.x) {\n"
-      << "  const qi64 base = (qi64)tile * (R * 256);\n"
-      << "  const bool full = base + R * 256 <= P.n;\n";
-    for (int c = 0; c < P.ncols; ++c) {
-      o << "  qi64 c" << c << "[R];\n";
-      if (P.cols[c].valid) o << "  qu32 v" << c << " = 0;\n";
-    }
-    emit_loads("c", "v", "base", "  ");
-  } else {
-    if (mode == SP_COUNTER)
-      o << "  {\n  if (t == 0) s_tile = (qu32)atomicAdd((unsigned long long*)&P.t.ctl[0], 1ull);\n"
-        << "  __syncthreads();\n"
-        << "  const qu32 tile = s_tile;\n";
-    else  // two-pass: one tile per workgroup in grid order
-      o << "  {\n  const qu32 tile = blockIdx.x;\n";
-    o << "  const qi64 base = (qi64)tile * (R * 256);\n"
-      << "  const bool full = base + R * 256 <= P.n;\n";
-    for (int c = 0; c < P.ncols; ++c) {
-      if (!((need >> c) & 1u)) continue;
-      o << "  qi64 c" << c << "[R];\n";
-      if (P.cols[c].valid) o << "  qu32 v" << c << " = 0;\n";
-    }
-    emit_loads("c", "v", "base", "  ");
-    if (mode == SP_WRITE)
-      // this tile's base: the earlier tiles' counts, summed by the whole workgroup while its
-      // column loads are in flight
-      o << "  qu64 pre = 0;\n"
-        << "  for (qi64 i = t; i < (qi64)tile; i += 256) pre += ((const qu64*)P.t.keys)[i];\n"
-        << "#pragma unroll\n  for (int d = 32; d >= 1; d >>= 1) pre += __shfl_xor(pre, d);\n"
-        << "  __shared__ qu64 s_pre[4];\n  if (lane == 0) s_pre[w] = pre;\n";
-  }
+// act (bit r: row base + r * 256 + t is inside [0, n) and passes the predicate) of a
+// select-project tile whose columns are loaded.
+void emit_selproj_act(const Plan& P, std::ostringstream& o) {
   o << "  qu32 act = 0;\n"
     << "#pragma unroll\n  for (int r = 0; r < R; ++r) act |= (qu32)(full || base + r * 256 + t < P.n) << r;\n";
-  {
-    std::ostringstream q;
-    emit_predicate(P, q, 16);  // emits with a fixed trip count; R <= 16 and bits >= R are clear
-    std::string body = q.str();
-    const std::string from = "r < 16;", to = "r < R;";
-    for (size_t k = body.find(from); k != std::string::npos; k = body.find(from, k)) body.replace(k, from.size(), to);
-    o << body;
+  std::ostringstream q;
+  emit_predicate(P, q, 16);  // emits with a fixed trip count; R <= 16 and bits >= R are clear
+  std::string body = q.str();
+  const std::string from = "r < 16;", to = "r < R;";
+  for (size_t k = body.find(from); k != std::string::npos; k = body.find(from, k)) body.replace(k, from.size(), to);
+  o << body;
+}
+
+// Column loads of the select-project tile at row `b` (C expression) into <cp><slot>[R] and the
+// validity bits into <vp><slot>, for the slots in `need`; `nt`: non-temporal loads.
+void emit_selproj_loads(const Plan& P, std::ostringstream& o, unsigned need, bool nt, const std::string& cp,
+                        const std::string& vp, const std::string& b, const std::string& ind) {
+  for (int c = 0; c < P.ncols; ++c) {
+    if (!((need >> c) & 1u)) continue;
+    const std::string cs = std::to_string(c);
+    const int kind = P.cols[c].kind;
+    const char* ty = kind == K_I32 ? "qi32" : (kind == K_U8 || kind == K_BOOL) ? "qu8" : "qi64";
+    o << ind << "{\n" << ind << "  const qi64 lb = " << b << ";\n" << ind << "  const bool lfull = lb + R * 256 <= P.n;\n"
+      << ind << "  const " << ty << "* p = (const " << ty << "*)P.cols[" << cs << "].p;\n"
+      << "#pragma unroll\n" << ind << "  for (int r = 0; r < R; ++r) {\n" << ind << "    const qi64 row = lb + r * 256 + t;\n";
+    if (kind == K_BOOL)
+      o << ind << "    " << cp << cs << "[r] = (lfull || row < P.n) ? ((p[row >> 3] >> (row & 7)) & 1) : 0;\n";
+    else
+      // default policy below 64M rows: C2-sized inputs stay in the MALL (nt 68.4 us, default 65.0 us)
+      o << ind << "    " << cp << cs << "[r] = (lfull || row < P.n) ? (qi64)" << ld(ty, "p + row", nt) << " : 0;\n";
+    o << ind << "  }\n";
+    if (P.cols[c].valid) {
+      o << ind << "  const qu8* vb = P.cols[" << cs << "].valid;\n" << ind << "  " << vp << cs << " = 0;\n"
+        << "#pragma unroll\n" << ind << "  for (int r = 0; r < R; ++r) {\n" << ind << "    const qi64 row = lb + r * 256 + t;\n"
+        << ind << "    if (lfull || row < P.n) " << vp << cs << " |= (qu32)((vb[row >> 3] >> (row & 7)) & 1) << r;\n"
+        << ind << "  }\n";
+    }
+    o << ind << "}\n";
   }
-  if (mode == SP_COUNT) {
-    o << "  qu32 n = __popc(act);\n"
-      << "#pragma unroll\n  for (int d = 32; d >= 1; d >>= 1) n += __shfl_xor(n, d);\n"
-      << "  if (lane == 0) s_cnt[w] = n;\n  __syncthreads();\n"
-      << "  if (t == 0) ((qu64*)P.t.keys)[tile] = (qu64)s_cnt[0] + s_cnt[1] + s_cnt[2] + s_cnt[3];\n"
-      << "  }\n}\n";
-    *src = std::string(kDevHeader) + o.str();
-    return true;
-  }
+}
+
+// Write phase of one select-project tile, after the caller's code has loaded the tile's columns
+// (c<slot>[R], v<slot>) and computed `act` (bit r: row base + r * 256 + t is selected): ballots,
+// per-(stripe, wave) counts, one wave's scan, the tile's output base (decoupled look-back or the
+// two-pass prefix), then the compacted stores.
+bool emit_selproj_write(const Plan& P, const int32_t* out_kind, int nout, int mode, std::ostringstream& o) {
+  const int R = selproj_rows_per_thread(P);
   // Staged output (all outputs 8 bytes wide, R x 256 x 8 B each within 64 KiB of LDS): selected
   // rows land compacted in LDS, then the tile's output range is written with 16-byte stores, all
   // lanes active. Direct 8-byte stores from the row registers were store-issue bound (half the
@@ -1057,6 +1058,73 @@ bool gen_selproj_source(const Plan& P, const int32_t* out_kind, int nout, std::s
     }
     o << "  }\n";
   }
+  return true;
+}
+
+bool gen_selproj_source(const Plan& P, const int32_t* out_kind, int nout, std::string* src, int mode) {
+  if (P.ncols < 1 || P.ncols > QE_MAX_COLS || nout < 1 || nout > QE_MAX_AGGS) return false;
+  const int R = selproj_rows_per_thread(P);
+  const bool persistent = mode == SP_PERSIST;
+  // the count pass loads only the predicate's columns
+  const unsigned need = mode == SP_COUNT ? pred_key_cols(P) : ~0u;
+  std::ostringstream o;
+  o << "\nusing namespace qe;\n"
+    << "extern \"C\" __global__ void __launch_bounds__(256) qe_selproj(const Plan P) {\n"
+    << "  constexpr int R = " << R << ";\n"
+    << "  constexpr qu64 F_AGG = 1ull << 62, F_INC = 2ull << 62, VMASK = (1ull << 62) - 1;\n"
+    << "  constexpr bool PERSIST = " << (persistent ? "true" : "false") << ";\n"
+    << "  __shared__ qu32 s_cnt[R * 4];\n  __shared__ qu64 s_base;\n  __shared__ qu32 s_tile, s_total;\n"
+    << "  __shared__ qi64 s_out[" << ((size_t)nout * R * 256 * 8 <= 64 * 1024 ? nout * R * 256 : 1) << "];\n"
+    << "  const int t = threadIdx.x, lane = t & 63, w = t >> 6;\n";
+  auto emit_loads = [&](const std::string& cp, const std::string& vp, const std::string& b, const std::string& ind) {
+    emit_selproj_loads(P, o, need, selproj_nt(P), cp, vp, b, ind);
+  };
+  if (persistent) {
+    // Every workgroup is resident (grid <= CUs x occupancy), so a static tile order cannot
+    // deadlock the look-back and no tile counter is needed. (Prefetching the next tile's columns
+    // into registers during this tile's look-back measured slower: 5.00 vs 4.67 ms at 1B rows.)
+    o << "  for (qu32 tile = blockIdx.x; (qu64)tile < P.t.cap; tile += gridDim.x) {\n"
+      << "  const qi64 base = (qi64)tile * (R * 256);\n"
+      << "  const bool full = base + R * 256 <= P.n;\n";
+    for (int c = 0; c < P.ncols; ++c) {
+      o << "  qi64 c" << c << "[R];\n";
+      if (P.cols[c].valid) o << "  qu32 v" << c << " = 0;\n";
+    }
+    emit_loads("c", "v", "base", "  ");
+  } else {
+    if (mode == SP_COUNTER)
+      o << "  {\n  if (t == 0) s_tile = (qu32)atomicAdd((unsigned long long*)&P.t.ctl[0], 1ull);\n"
+        << "  __syncthreads();\n"
+        << "  const qu32 tile = s_tile;\n";
+    else  // two-pass: one tile per workgroup in grid order
+      o << "  {\n  const qu32 tile = blockIdx.x;\n";
+    o << "  const qi64 base = (qi64)tile * (R * 256);\n"
+      << "  const bool full = base + R * 256 <= P.n;\n";
+    for (int c = 0; c < P.ncols; ++c) {
+      if (!((need >> c) & 1u)) continue;
+      o << "  qi64 c" << c << "[R];\n";
+      if (P.cols[c].valid) o << "  qu32 v" << c << " = 0;\n";
+    }
+    emit_loads("c", "v", "base", "  ");
+    if (mode == SP_WRITE)
+      // this tile's base: the earlier tiles' counts, summed by the whole workgroup while its
+      // column loads are in flight
+      o << "  qu64 pre = 0;\n"
+        << "  for (qi64 i = t; i < (qi64)tile; i += 256) pre += ((const qu64*)P.t.keys)[i];\n"
+        << "#pragma unroll\n  for (int d = 32; d >= 1; d >>= 1) pre += __shfl_xor(pre, d);\n"
+        << "  __shared__ qu64 s_pre[4];\n  if (lane == 0) s_pre[w] = pre;\n";
+  }
+  emit_selproj_act(P, o);
+  if (mode == SP_COUNT) {
+    o << "  qu32 n = __popc(act);\n"
+      << "#pragma unroll\n  for (int d = 32; d >= 1; d >>= 1) n += __shfl_xor(n, d);\n"
+      << "  if (lane == 0) s_cnt[w] = n;\n  __syncthreads();\n"
+      << "  if (t == 0) ((qu64*)P.t.keys)[tile] = (qu64)s_cnt[0] + s_cnt[1] + s_cnt[2] + s_cnt[3];\n"
+      << "  }\n}\n";
+    *src = std::string(kDevHeader) + o.str();
+    return true;
+  }
+  if (!emit_selproj_write(P, out_kind, nout, mode, o)) return false;
   if (persistent) o << "  __syncthreads();\n";  // s_cnt / s_base are reused by the next tile
   o << "  }\n}\n";
   *src = std::string(kDevHeader) + o.str();
@@ -1184,6 +1252,12 @@ int jit_kernel(qe_ctx* ctx, const std::string& src, hipFunction_t* fn, int* bloc
   snprintf(name, sizeof(name), "%016llx", (unsigned long long)fnv1a(disk_key));
   const std::string dir = cache_dir();
   const std::string path = dir.empty() ? std::string() : dir + "/" + name + ".co";
+  if (const char* dump = getenv("QE_JIT_DUMP")) {  // kernel sources for offline ISA inspection
+    if (FILE* f = fopen((std::string(dump) + "/" + kname + "_" + name + ".hip").c_str(), "w")) {
+      fwrite(src.data(), 1, src.size(), f);
+      fclose(f);
+    }
+  }
   std::vector<char> code;
   if (path.empty() || !read_entry(path, disk_key, &code)) {
     hiprtcProgram prog;

@@ -162,8 +162,9 @@ extern "C" int qe_select_project(qe_ctx* ctx, const qe_column* cols, int32_t nco
     const int R = selproj_rows_per_thread(P);
     const int64_t tiles = (int64_t)div_up((uint64_t)n, (uint64_t)R * 256);
     QE_CHECK(tiles < (1ll << 31), QE_ERR_CAPACITY, "too many rows for one select-project call");
+    const size_t sbytes = (size_t)(3 + tiles) * 8;  // ctl[3] | per tile a look-back status word
     void* s;
-    QE_TRY(ctx_scratch(ctx, (size_t)(tiles + 3) * 8, &s));
+    QE_TRY(ctx_scratch(ctx, sbytes, &s));
     qu64* ctl = (qu64*)s;
     P.t.ctl = ctl;
     P.t.keys = (qi64*)(ctl + 3);
@@ -172,16 +173,21 @@ extern "C" int qe_select_project(qe_ctx* ctx, const qe_column* cols, int32_t nco
     QE_TRY(ctx_pinned(ctx, 16, &pin));
     for (int attempt = 0; attempt < 2; ++attempt) {
       const bool persist = persist_env && attempt == 0;
+      const int mode = persist ? SP_PERSIST : SP_COUNTER;
       hipFunction_t fn;
       int bpc = 0;
-      QE_TRY(selproj_kernel(ctx, P, out_kind, spec->nout, persist ? SP_PERSIST : SP_COUNTER, &fn, &bpc));
-      QE_HIP(hipMemsetAsync(s, 0, (size_t)(tiles + 3) * 8, ctx->stream));
+      QE_TRY(selproj_kernel(ctx, P, out_kind, spec->nout, mode, &fn, &bpc));
       // QE_SELPROJ_OVERSUB (tests only) multiplies the persistent grid past residency, to exercise
       // the bounded look-back and the rerun
       const char* ov = getenv("QE_SELPROJ_OVERSUB");
       const int oversub = ov && *ov ? std::max(1, std::min(64, atoi(ov))) : 1;
-      const int per_cu = std::max(1, std::min(wg_cap, bpc - 1));
+      static const int margin = [] {  // QE_SELPROJ_OCC_MARGIN: blocks per CU held back from the occupancy
+        const char* e = getenv("QE_SELPROJ_OCC_MARGIN");
+        return e && *e ? std::max(0, atoi(e)) : 1;
+      }();
+      const int per_cu = std::max(1, std::min(wg_cap, bpc - margin));
       const int64_t grid = persist ? std::min<int64_t>(tiles, (int64_t)ctx->num_cus * per_cu * oversub) : tiles;
+      QE_HIP(hipMemsetAsync(s, 0, sbytes, ctx->stream));
       QE_TRY(jit_launch(ctx, fn, (int)grid, P, 256));
       QE_TRY(launch_check("qe_selproj"));
       QE_HIP(hipMemcpyAsync(pin, ctl + 1, 16, hipMemcpyDeviceToHost, ctx->stream));

@@ -1,0 +1,39 @@
+"""Generated kernel sources compile for gfx950 (CPU suite, no GPU): the select-project generator's
+every tile-order mode (qe_jit.hip gen_selproj_source) for a C2 plan
+and a nullable two-output plan, emitted by tests/native/gen_sources.cpp through the library's own
+plan compiler and compiled with hipcc as hipRTC would (same options, device code only)."""
+import pathlib
+import subprocess
+
+import pytest
+
+ROOT = pathlib.Path(__file__).resolve().parents[1]
+HIPCC = "/opt/rocm/bin/hipcc"
+
+
+@pytest.fixture(scope="module")
+def sources(tmp_path_factory):
+    if not pathlib.Path(HIPCC).exists():
+        pytest.skip("hipcc not present")
+    if not (ROOT / "query-engines_amd" / "lib" / "libqe_hip.so").exists():
+        pytest.skip("libqe_hip.so not built")
+    subprocess.run(["make", "-C", str(ROOT / "tests" / "native"), "_build/gen_sources"], check=True,
+                   capture_output=True)
+    out = tmp_path_factory.mktemp("jitsrc")
+    r = subprocess.run([str(ROOT / "tests" / "native" / "_build" / "gen_sources"), str(out)], check=True,
+                       capture_output=True, text=True)
+    return [pathlib.Path(p) for p in r.stdout.split()]
+
+
+def test_all_modes_emitted(sources):
+    names = sorted(p.name for p in sources)
+    assert names == sorted(f"{s}_m{m}.hip" for s in ("c2", "nullable") for m in range(4))
+
+
+@pytest.mark.parametrize("name", ["c2_m0", "c2_m1", "c2_m2", "c2_m3", "nullable_m1", "nullable_m3"])
+def test_compiles_for_gfx950(sources, name, tmp_path):
+    src = next(p for p in sources if p.stem == name)
+    r = subprocess.run([HIPCC, "--offload-arch=gfx950", "-O3", "-std=c++17", "-ffp-contract=off",
+                        "-munsafe-fp-atomics", "--cuda-device-only", "-include", "hip/hip_runtime.h", "-c",
+                        str(src), "-o", str(tmp_path / (name + ".o"))], capture_output=True, text=True)
+    assert r.returncode == 0, r.stderr[-2000:]
