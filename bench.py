@@ -107,6 +107,9 @@ def main():
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--exchange", action="store_true",
                     help="run the multi-GPU exchange leg even with one rank (tests the N > 1 step on one GPU)")
+    ap.add_argument("--dist-backend", default="nccl",
+                    help="torch.distributed backend (nccl = RCCL over xGMI; gloo only to rehearse N > 1 "
+                         "ranks sharing one GPU)")
     args = ap.parse_args()
 
     import torch
@@ -122,14 +125,19 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
         print(f"warning: --gpus {args.gpus} but WORLD_SIZE {world}; using WORLD_SIZE", file=sys.stderr)
-    torch.cuda.set_device(local)
+    # one rank per GPU; more ranks than GPUs only in a gloo rehearsal (ranks then share devices)
+    device = local % max(1, torch.cuda.device_count())
+    torch.cuda.set_device(device)
     if world > 1 or args.exchange:
         for k, v in (("MASTER_ADDR", "127.0.0.1"), ("MASTER_PORT", "29511"), ("RANK", "0"), ("WORLD_SIZE", "1")):
             os.environ.setdefault(k, v)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if args.dist_backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", device))
+        else:
+            dist.init_process_group(args.dist_backend)
     from kquery.exchange import exchange_partials
 
-    ctx = Context.get(local)
+    ctx = Context.get(device)
     rows = args.rows
     row0 = rank * rows
     cols = [generate_column(s, rows, row0, 42, ctx) for s in C4_COLUMNS]
@@ -148,7 +156,6 @@ def main():
         partial.set_row_base(row0)
         partial.update_fused(cols, spec)
         kernel_ms.append(partial.last_kernel_time())
-        kinds.append(partial.last_kernel_kind())
         final = partial
         if exchange:
             owner.reset()
@@ -162,6 +169,7 @@ def main():
 
     for _ in range(args.warmup):
         step()
+    kinds.append(partial.last_kernel_kind())
     kernel_ms.clear()
     barrier()
     torch.cuda.synchronize()
@@ -169,6 +177,7 @@ def main():
     for _ in range(args.steps):
         keys, res = step()
     torch.cuda.synchronize()
+    kinds.append(partial.last_kernel_kind())
     barrier()
     elapsed = time.perf_counter() - t0
     if world > 1:
@@ -219,7 +228,9 @@ def main():
             "rows_per_gpu": rows,
             "groups": 1024,
             "columns": "k, a, b int64 (Arrow, no nulls)",
-            "parallelism": f"hash-sharded partial aggregate x{world}" + (" + RCCL all-to-all" if exchange else ""),
+            "parallelism": f"hash-sharded partial aggregate x{world}" + (
+                (" + RCCL all-to-all" if args.dist_backend == "nccl" else f" + {args.dist_backend} all-to-all (rehearsal)")
+                if exchange else ""),
         },
         "roofline": {
             "bound": "hbm",

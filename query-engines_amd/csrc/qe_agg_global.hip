@@ -344,7 +344,7 @@ static int agg_global_finish(qe_ctx* ctx, const GPart* dp, int32_t type, qe_glob
   void* h;
   QE_TRY(ctx_pinned(ctx, sizeof(GPart), &h));
   QE_HIP(hipMemcpyAsync(h, dp, sizeof(GPart), hipMemcpyDeviceToHost, ctx->stream));
-  QE_HIP(hipStreamSynchronize(ctx->stream));
+  QE_TRY(ctx_sync(ctx));
   const GPart p = *(const GPart*)h;
   const bool f64 = type == QE_TYPE_FLOAT64;
   memset(out, 0, sizeof(*out));

@@ -145,7 +145,7 @@ int parallel_h2d(qe_ctx* ctx, const std::vector<H2DJob>& jobs) {
   stage_pool().run(tasks);
   for (int t = 0; t < T; ++t)
     if (rc[(size_t)t] != QE_OK) return fail(QE_ERR_DEVICE, "host-to-device staging failed");
-  QE_HIP(hipStreamSynchronize(ctx->stream));
+  QE_TRY(ctx_sync(ctx));
   return QE_OK;
 }
 

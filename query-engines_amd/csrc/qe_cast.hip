@@ -124,7 +124,7 @@ extern "C" int qe_cast_utf8_to_f64(qe_ctx* ctx, const qe_column* in, qe_column* 
   QE_TRY(launch_check("k_cast_utf8_f64"));
   uint64_t hdr[2] = {~0ull, 0};
   QE_HIP(hipMemcpyAsync(hdr, s, 16, hipMemcpyDeviceToHost, ctx->stream));
-  QE_HIP(hipStreamSynchronize(ctx->stream));
+  QE_TRY(ctx_sync(ctx));
   if (hdr[0] != ~0ull) {
     const uint64_t row = hdr[0];
     if (error_row) *error_row = (int64_t)row;

@@ -640,7 +640,7 @@ int grid_for(qe_ctx* ctx, int64_t n, int threads = 256) {
 
 int read_i64(qe_ctx* ctx, const int64_t* p, int64_t* out) {
   QE_HIP(hipMemcpyAsync(out, p, 8, hipMemcpyDeviceToHost, ctx->stream));
-  QE_HIP(hipStreamSynchronize(ctx->stream));
+  QE_TRY(ctx_sync(ctx));
   return QE_OK;
 }
 
@@ -697,7 +697,7 @@ int csv_parse(qe_ctx* ctx, const uint8_t* data, int64_t nbytes, const qe_csv_opt
     QE_TRY(ctx_pinned(ctx, 16, &pin2));
     QE_HIP(hipMemcpyAsync(pin2, seg_ts + nseg, 8, hipMemcpyDeviceToHost, ctx->stream));
     QE_HIP(hipMemcpyAsync((int64_t*)pin2 + 1, last_term, 8, hipMemcpyDeviceToHost, ctx->stream));
-    QE_HIP(hipStreamSynchronize(ctx->stream));
+    QE_TRY(ctx_sync(ctx));
     nterm = ((int64_t*)pin2)[0];
     last_end = ((int64_t*)pin2)[1];
   }
@@ -750,7 +750,7 @@ int csv_parse(qe_ctx* ctx, const uint8_t* data, int64_t nbytes, const qe_csv_opt
     QE_HIP(hipMemcpyAsync(pin, nskip, 8, hipMemcpyDeviceToHost, ctx->stream));
     for (int c = 0; c < nproj && rows_all > 0; ++c)
       QE_HIP(hipMemcpyAsync((int64_t*)pin + 1 + c, t->bstart(c) + rows_all, 8, hipMemcpyDeviceToHost, ctx->stream));
-    QE_HIP(hipStreamSynchronize(ctx->stream));
+    QE_TRY(ctx_sync(ctx));
     const int64_t skipped = ((int64_t*)pin)[0];
     if (skipped == 0) {
       rows = rows_all;
@@ -791,7 +791,7 @@ int csv_parse(qe_ctx* ctx, const uint8_t* data, int64_t nbytes, const qe_csv_opt
     QE_TRY(ctx_pinned(ctx, (size_t)nproj * 8, &pin));
     for (int c = 0; c < nproj; ++c)
       QE_HIP(hipMemcpyAsync((int64_t*)pin + c, t->bstart(c) + rows, 8, hipMemcpyDeviceToHost, ctx->stream));
-    QE_HIP(hipStreamSynchronize(ctx->stream));
+    QE_TRY(ctx_sync(ctx));
     for (int c = 0; c < nproj; ++c) {
       t->total[(size_t)c] = ((int64_t*)pin)[c];
       QE_CHECK(t->total[(size_t)c] < (1ll << 31), QE_ERR_CAPACITY, "CSV column %d holds more than 2^31 bytes", c);

@@ -338,7 +338,7 @@ int qe_eval_cmp(qe_ctx* ctx, int32_t op, const qe_operand* lhs, const qe_operand
     QE_CHECK(!c->validity || out->validity, QE_ERR_INVALID_ARG, "output validity buffer required");
     int32_t lo[2];
     QE_HIP(hipMemcpyAsync(lo, rhs->col->offsets, 8, hipMemcpyDeviceToHost, ctx->stream));
-    QE_HIP(hipStreamSynchronize(ctx->stream));
+    QE_TRY(ctx_sync(ctx));
     out->length = n;
     if (n == 0) return QE_OK;
     hipLaunchKernelGGL(k_cmp_utf8, dim3(grid_for(ctx, (n + 7) / 8)), dim3(256), 0, ctx->stream, c->offsets,

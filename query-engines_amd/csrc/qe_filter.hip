@@ -143,7 +143,7 @@ int exclusive_scan_i64(qe_ctx* ctx, const int64_t* in, int64_t* out, int64_t n) 
   const size_t need = (size_t)(2 * nb + 2) * 8;
   if (need > ctx->scan_tmp_bytes) {
     if (ctx->scan_tmp) {
-      QE_HIP(hipStreamSynchronize(ctx->stream));
+      QE_TRY(ctx_sync(ctx));
       QE_HIP(hipFree(ctx->scan_tmp));
     }
     ctx->scan_tmp = nullptr;
@@ -356,7 +356,7 @@ static int read_total(qe_ctx* ctx, const FilterPlan& fp, int64_t* total) {
   void* h;
   QE_TRY(ctx_pinned(ctx, 8, &h));
   QE_HIP(hipMemcpyAsync(h, fp.offsets + fp.ntiles, 8, hipMemcpyDeviceToHost, ctx->stream));
-  QE_HIP(hipStreamSynchronize(ctx->stream));
+  QE_TRY(ctx_sync(ctx));
   *total = *(int64_t*)h;
   return QE_OK;
 }

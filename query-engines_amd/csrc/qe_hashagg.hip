@@ -763,8 +763,9 @@ __global__ void __launch_bounds__(1024) k_part_slices(const qi64* __restrict__ o
   if (threadIdx.x == 1023) out[0] = s_sum[1023];
 }
 
-__global__ void k_table_init(DTable t, AggMeta m) {
+__global__ void k_table_init(DTable t, AggMeta m, qu64* zero_ctl) {
   const qu64 SS = t.cap + 2;
+  if (zero_ctl && blockIdx.x == 0 && threadIdx.x < 8) zero_ctl[threadIdx.x] = 0;  // reset: the control words too
   for (qu64 s = blockIdx.x * (qu64)blockDim.x + threadIdx.x; s < SS; s += (qu64)gridDim.x * blockDim.x) {
     t.keys[s] = EMPTY_KEY;
     t.cstar[s] = 0;
@@ -1027,7 +1028,10 @@ __device__ __forceinline__ void finalize_slot(const DTable& t, const AggMeta& m,
       if (out.keys[k].validity) put_bit(out.keys[k].validity, lbits, k, o, !isn);
     }
   }
-  // aggregates
+  // aggregates (a rolled loop: the kernel is one workgroup whose run time is mostly instruction
+  // fetch, so code size is what counts — unrolled over QE_MAX_AGGS it ran 16 us instead of 13)
+  const qu64 cst = t.cstar[s];
+#pragma unroll 1
   for (int j = 0; j < m.naggs; ++j) {
     const qu64 nn = t.nn[j][s];
     const qi64 acc = t.acc[j][s];
@@ -1035,7 +1039,7 @@ __device__ __forceinline__ void finalize_slot(const DTable& t, const AggMeta& m,
     bool valid = nn > 0;
     switch (m.fn[j]) {
       case QE_AGG_COUNT: val = (qi64)nn; valid = true; break;
-      case QE_AGG_COUNT_STAR: val = (qi64)t.cstar[s]; valid = true; break;
+      case QE_AGG_COUNT_STAR: val = (qi64)cst; valid = true; break;
       case QE_AGG_AVG: val = f64_bits(bits_f64(acc) / (double)nn); break;
       default:
         if (acc_is_f64mm(m.acc[j])) {
@@ -1089,10 +1093,9 @@ constexpr int FS_THREADS = 1024, FS_PER = 16, FS_WAVES = FS_THREADS / 64;
 static_assert(FS_THREADS * FS_PER / 2 / 32 <= FS_WORDS, "LDS bitmaps hold every group of a small table");
 __global__ void __launch_bounds__(FS_THREADS) k_finalize_small(DTable t, AggMeta m, KeyMeta km, OutCols out,
                                                                qi64 groups) {
-  __shared__ qi32 wcnt[FS_PER][FS_WAVES];  // set slots per (chunk, wave)
+  __shared__ qi32 wcnt[FS_PER][FS_WAVES];  // set slots per (chunk, wave), then their exclusive prefix
   __shared__ qu64 wbal[FS_PER][FS_WAVES];  // their ballots
   __shared__ qu32 lbits[(QE_MAX_KEYS + QE_MAX_AGGS) * FS_WORDS];  // validity, copied out at the end
-  __shared__ qi32 cbase[FS_PER + 1];       // rows before each chunk
   const qu64 SS = t.cap + 2;
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const qu64 lt = lane ? (~0ull >> (64 - lane)) : 0ull;
@@ -1113,20 +1116,30 @@ __global__ void __launch_bounds__(FS_THREADS) k_finalize_small(DTable t, AggMeta
     }
   }
   __syncthreads();  // also orders the LDS zeroing before any bit is set
-  if (tid == 0) {
-    qi32 run = 0;
-    for (int i = 0; i < FS_PER; ++i) {
-      cbase[i] = run;
-      for (int w = 0; w < FS_WAVES; ++w) run += wcnt[i][w];
+  // exclusive prefix of the (chunk, wave) counts in slot order, by wave 0: four per lane, then a
+  // wave scan (a serial walk by one thread was 256 dependent LDS reads, ~10 us)
+  static_assert(FS_PER * FS_WAVES == 4 * 64, "four (chunk, wave) counts per lane");
+  if (wid == 0) {
+    qi32* flat = &wcnt[0][0];
+    const qi32 c0 = flat[4 * lane], c1 = flat[4 * lane + 1], c2 = flat[4 * lane + 2], c3 = flat[4 * lane + 3];
+    const qi32 sum = c0 + c1 + c2 + c3;
+    qi32 inc = sum;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+      const qi32 y = __shfl_up(inc, d);
+      if (lane >= d) inc += y;
     }
-    cbase[FS_PER] = run;
+    const qi32 ex = inc - sum;
+    flat[4 * lane] = ex;
+    flat[4 * lane + 1] = ex + c0;
+    flat[4 * lane + 2] = ex + c0 + c1;
+    flat[4 * lane + 3] = ex + c0 + c1 + c2;
   }
   __syncthreads();
   while (occ) {
     const int i = __ffs(occ) - 1;
     occ &= occ - 1;
-    qi64 o = cbase[i] + __popcll(wbal[i][wid] & lt);
-    for (int w = 0; w < wid; ++w) o += wcnt[i][w];
+    const qi64 o = wcnt[i][wid] + __popcll(wbal[i][wid] & lt);  // wcnt now holds the prefix
     finalize_slot(t, m, km, out, (qu64)i * FS_THREADS + tid, o, lbits);
   }
   __syncthreads();
@@ -1179,6 +1192,7 @@ struct qe_hashagg {
   uint32_t* defer[2] = {nullptr, nullptr};
   size_t defer_words = 0;
   bool defer_dirty[2] = {false, false};
+  bool ctl_rows_clean = false;  // ctl[1] / ctl[2] known zero (written only by update launches)
   // HIP events around the aggregation kernel launches of the last update (measurement hook)
   hipEvent_t ev[2] = {nullptr, nullptr};
   double last_kernel_ms = 0.0;
@@ -1229,7 +1243,7 @@ static int table_alloc(qe_hashagg* h, uint64_t cap, void** mem, DTable* t) {
   t->cap = cap;
   t->ctl = h->ctl;
   const int grid = (int)std::min<uint64_t>(div_up(SS, 256), 4096);
-  hipLaunchKernelGGL(k_table_init, dim3(grid), dim3(256), 0, h->ctx->stream, *t, agg_meta(h));
+  hipLaunchKernelGGL(k_table_init, dim3(grid), dim3(256), 0, h->ctx->stream, *t, agg_meta(h), (qu64*)nullptr);
   return launch_check("k_table_init");
 }
 
@@ -1243,7 +1257,7 @@ static int read_ctl(qe_hashagg* h, uint64_t out[8]) {
   void* p;
   QE_TRY(ctx_pinned(h->ctx, 64, &p));
   QE_HIP(hipMemcpyAsync(p, h->ctl, 64, hipMemcpyDeviceToHost, h->ctx->stream));
-  QE_HIP(hipStreamSynchronize(h->ctx->stream));
+  QE_TRY(ctx_sync(h->ctx));
   memcpy(out, p, 64);
   QE_CHECK(out[3] == 0, QE_ERR_CAPACITY, "hash aggregate lost %llu groups (probe limit or overflow area)",
            (unsigned long long)out[3]);
@@ -1610,7 +1624,7 @@ static int partition_rows(qe_hashagg* h, Plan& P, hipFunction_t* fn, int* grid) 
   void* pin;
   QE_TRY(ctx_pinned(ctx, 8, &pin));
   QE_HIP(hipMemcpyAsync(pin, off + cells, 8, hipMemcpyDeviceToHost, ctx->stream));
-  QE_HIP(hipStreamSynchronize(ctx->stream));
+  QE_TRY(ctx_sync(ctx));
   const int64_t R = *(int64_t*)pin;
   // overflow records of the aggregation pass (bounded; groups beyond it retry their records)
   if (!h->ovf || h->ovf_cap < (1ull << 20)) {
@@ -1739,7 +1753,10 @@ static int run_update(qe_hashagg* h, Plan& P) {
       QE_HIP(hipMemsetAsync(h->defer[out_i], 0, h->defer_words * 4, ctx->stream));
       h->defer_dirty[out_i] = false;
     }
-    QE_HIP(hipMemsetAsync(h->ctl + 1, 0, 24, ctx->stream));
+    // deferred-row and overflow-record counters (ctl[3], lost groups, stays: only reset clears
+    // it); known zero after a reset or after a launch that read back zeros
+    if (!h->ctl_rows_clean) QE_HIP(hipMemsetAsync(h->ctl + 1, 0, 16, ctx->stream));
+    h->ctl_rows_clean = false;
     P.t = h->t;
     P.defer_in = defer_in;
     P.defer_out = h->defer[out_i];
@@ -1811,6 +1828,7 @@ static int run_update(qe_hashagg* h, Plan& P) {
     }
     QE_CHECK(c[3] == 0, QE_ERR_CAPACITY, "hash aggregate lost %llu groups (overflow area)", (unsigned long long)c[3]);
     const uint64_t groups = c[0], deferred = c[1], ovf_recs = std::min<uint64_t>(c[2], P.ovf_cap);
+    h->ctl_rows_clean = c[1] == 0 && c[2] == 0;
     if (deferred == 0 && ovf_recs == 0) {
       if (groups * 2 > h->t.cap) QE_TRY(table_grow(h, 4 * h->t.cap));
       h->known_groups = (int64_t)groups;  // saves finalize a device round trip
@@ -1984,10 +2002,10 @@ int qe_hashagg_last_kernel_time(qe_hashagg* h, double* ms, int32_t* launches) {
 int qe_hashagg_reset(qe_hashagg* h) {
   QE_CHECK(h, QE_ERR_INVALID_ARG, "null state");
   QE_TRY(ctx_enter(h->ctx));
-  QE_HIP(hipMemsetAsync(h->ctl, 0, 64, h->ctx->stream));
   const int grid = (int)std::min<uint64_t>(div_up(h->t.cap + 2, 256), 4096);
-  hipLaunchKernelGGL(k_table_init, dim3(grid), dim3(256), 0, h->ctx->stream, h->t, agg_meta(h));
+  hipLaunchKernelGGL(k_table_init, dim3(grid), dim3(256), 0, h->ctx->stream, h->t, agg_meta(h), (qu64*)h->ctl);
   QE_TRY(launch_check("k_table_init"));
+  h->ctl_rows_clean = true;
   h->row_base = 0;
   h->known_groups = 0;
   return QE_OK;
@@ -2124,7 +2142,7 @@ int qe_hashagg_finalize(qe_hashagg* h, qe_column* out_keys, qe_column* out_aggs,
     hipLaunchKernelGGL(k_finalize_small, dim3(1), dim3(FS_THREADS), 0, ctx->stream, h->t, agg_meta(h), h->km, oc,
                        (qi64)groups);
     QE_TRY(launch_check("k_finalize_small"));
-    QE_HIP(hipStreamSynchronize(ctx->stream));
+    QE_TRY(ctx_sync(ctx));
     return QE_OK;
   }
   // one 256-slot tile per workgroup: a single pass each, so the chip finalises in one wave of
@@ -2142,7 +2160,7 @@ int qe_hashagg_finalize(qe_hashagg* h, qe_column* out_keys, qe_column* out_aggs,
   hipLaunchKernelGGL(k_finalize, dim3((unsigned)ntiles), dim3(256), 0, ctx->stream, h->t, agg_meta(h), h->km, (const qi64*)offs,
                      tile_slots, oc);
   QE_TRY(launch_check("k_finalize"));
-  QE_HIP(hipStreamSynchronize(ctx->stream));
+  QE_TRY(ctx_sync(ctx));
   return QE_OK;
 }
 
@@ -2163,7 +2181,7 @@ int qe_hashagg_export_counts(qe_hashagg* h, int32_t nparts, int64_t* counts) {
   hipLaunchKernelGGL(k_export_count, dim3(grid), dim3(256), 0, ctx->stream, h->t, nparts, (unsigned long long*)s);
   QE_TRY(launch_check("k_export_count"));
   QE_HIP(hipMemcpyAsync(counts, s, (size_t)nparts * 8, hipMemcpyDeviceToHost, ctx->stream));
-  QE_HIP(hipStreamSynchronize(ctx->stream));
+  QE_TRY(ctx_sync(ctx));
   return QE_OK;
 }
 

@@ -180,7 +180,7 @@ int ctx_scratch(qe_ctx* ctx, size_t bytes, void** out) {
   if (bytes > ctx->scratch_bytes) {
     const size_t old = ctx->scratch_bytes;
     if (ctx->scratch) {
-      QE_HIP(hipStreamSynchronize(ctx->stream));
+      QE_TRY(ctx_sync(ctx));
       QE_HIP(hipFree(ctx->scratch));
       ctx->scratch = nullptr;
       ctx->scratch_bytes = 0;
@@ -195,6 +195,11 @@ int ctx_scratch(qe_ctx* ctx, size_t bytes, void** out) {
     ctx->scratch_bytes = want;
   }
   *out = ctx->scratch;
+  return QE_OK;
+}
+
+int ctx_sync(qe_ctx* ctx) {
+  QE_HIP(hipStreamSynchronize(ctx->stream));
   return QE_OK;
 }
 
@@ -213,7 +218,7 @@ int ctx_pinned(qe_ctx* ctx, size_t bytes, void** out) {
 int ctx_workspace(qe_ctx* ctx, int slot, size_t bytes, void** out) {
   if (bytes > ctx->ws_bytes[slot]) {
     if (ctx->ws[slot]) {
-      QE_HIP(hipStreamSynchronize(ctx->stream));
+      QE_TRY(ctx_sync(ctx));
       QE_HIP(hipFree(ctx->ws[slot]));
     }
     ctx->ws[slot] = nullptr;
@@ -379,7 +384,7 @@ void* qe_ctx_stream(qe_ctx* ctx) { return ctx ? (void*)ctx->stream : nullptr; }
 
 int qe_ctx_synchronize(qe_ctx* ctx) {
   QE_TRY(ctx_enter(ctx));
-  QE_HIP(hipStreamSynchronize(ctx->stream));
+  QE_TRY(ctx_sync(ctx));
   return QE_OK;
 }
 
@@ -404,14 +409,14 @@ int qe_copy_to_device(qe_ctx* ctx, void* dst, const void* src, size_t bytes) {
   QE_TRY(ctx_enter(ctx));
   if (bytes >= ((size_t)32 << 20)) return parallel_h2d_copy(ctx, dst, src, bytes);  // large: staged, 8 threads
   QE_HIP(hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, ctx->stream));
-  QE_HIP(hipStreamSynchronize(ctx->stream));
+  QE_TRY(ctx_sync(ctx));
   return QE_OK;
 }
 
 int qe_copy_to_host(qe_ctx* ctx, void* dst, const void* src, size_t bytes) {
   QE_TRY(ctx_enter(ctx));
   QE_HIP(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, ctx->stream));
-  QE_HIP(hipStreamSynchronize(ctx->stream));
+  QE_TRY(ctx_sync(ctx));
   return QE_OK;
 }
 

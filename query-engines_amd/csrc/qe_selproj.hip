@@ -156,7 +156,7 @@ extern "C" int qe_select_project(qe_ctx* ctx, const qe_column* cols, int32_t nco
       QE_TRY(launch_check(mode == SP_COUNT ? "qe_selproj (count)" : "qe_selproj (write)"));
     }
     QE_HIP(hipMemcpyAsync(pin, ctl + 1, 8, hipMemcpyDeviceToHost, ctx->stream));
-    QE_HIP(hipStreamSynchronize(ctx->stream));
+    QE_TRY(ctx_sync(ctx));
     *out_count = ((int64_t*)pin)[0];
   } else if (n > 0) {
     const int R = selproj_rows_per_thread(P);
@@ -191,7 +191,7 @@ extern "C" int qe_select_project(qe_ctx* ctx, const qe_column* cols, int32_t nco
       QE_TRY(jit_launch(ctx, fn, (int)grid, P, 256));
       QE_TRY(launch_check("qe_selproj"));
       QE_HIP(hipMemcpyAsync(pin, ctl + 1, 16, hipMemcpyDeviceToHost, ctx->stream));
-      QE_HIP(hipStreamSynchronize(ctx->stream));
+      QE_TRY(ctx_sync(ctx));
       *out_count = ((int64_t*)pin)[0];
       if (((int64_t*)pin)[1] == 0) break;  // else: a persistent workgroup was not resident
       QE_CHECK(persist, QE_ERR_DEVICE, "select-project look-back did not complete");

@@ -738,7 +738,7 @@ int grow_array(qe_ctx* ctx, T** p, int64_t old_n, int64_t new_n) {
 int read_ctl(qe_strdict* d, uint32_t* overflow, uint32_t* unresolved) {
   uint8_t h[24];
   QE_HIP(hipMemcpyAsync(h, d->ctl, 24, hipMemcpyDeviceToHost, d->ctx->stream));
-  QE_HIP(hipStreamSynchronize(d->ctx->stream));
+  QE_TRY(ctx_sync(d->ctx));
   uint32_t nc;
   uint64_t au;
   memcpy(&nc, h, 4);
@@ -757,7 +757,7 @@ int write_ctl(qe_strdict* d) {
   memcpy(h, &nc, 4);
   memcpy(h + 8, &au, 8);
   QE_HIP(hipMemcpyAsync(d->ctl, h, 24, hipMemcpyHostToDevice, d->ctx->stream));
-  QE_HIP(hipStreamSynchronize(d->ctx->stream));
+  QE_TRY(ctx_sync(d->ctx));
   return QE_OK;
 }
 
@@ -1012,7 +1012,7 @@ int qe_strdict_decode_tuple(qe_strdict* d, const qe_column* codes, int32_t nkeys
   QE_TRY(launch_check("k_tuple_decode"));
   uint32_t bad = 0;
   QE_HIP(hipMemcpyAsync(&bad, s, 4, hipMemcpyDeviceToHost, ctx->stream));
-  QE_HIP(hipStreamSynchronize(ctx->stream));
+  QE_TRY(ctx_sync(ctx));
   QE_CHECK(bad == 0, QE_ERR_INVALID_ARG, "code out of range for this dictionary");
   return QE_OK;
 }
@@ -1039,7 +1039,7 @@ int qe_strdict_decode_bytes(qe_strdict* d, const qe_column* codes, int64_t* out_
   int64_t h[2] = {0, 0};
   QE_HIP(hipMemcpyAsync(h, starts + n, 8, hipMemcpyDeviceToHost, ctx->stream));
   QE_HIP(hipMemcpyAsync(h + 1, bad, 4, hipMemcpyDeviceToHost, ctx->stream));
-  QE_HIP(hipStreamSynchronize(ctx->stream));
+  QE_TRY(ctx_sync(ctx));
   QE_CHECK((uint32_t)h[1] == 0, QE_ERR_INVALID_ARG, "code out of range for this dictionary");
   *out_bytes = h[0];
   return QE_OK;

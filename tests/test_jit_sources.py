@@ -17,11 +17,13 @@ def sources(tmp_path_factory):
         pytest.skip("hipcc not present")
     if not (ROOT / "query-engines_amd" / "lib" / "libqe_hip.so").exists():
         pytest.skip("libqe_hip.so not built")
-    subprocess.run(["make", "-C", str(ROOT / "tests" / "native"), "_build/gen_sources"], check=True,
-                   capture_output=True)
-    out = tmp_path_factory.mktemp("jitsrc")
-    r = subprocess.run([str(ROOT / "tests" / "native" / "_build" / "gen_sources"), str(out)], check=True,
-                       capture_output=True, text=True)
+    out = tmp_path_factory.mktemp("jitsrc")  # per xdist worker: no shared build output
+    csrc, lib = ROOT / "query-engines_amd" / "csrc", ROOT / "query-engines_amd" / "lib"
+    exe = out / "gen_sources"
+    subprocess.run([HIPCC, "-O1", "-std=c++17", f"-I{csrc}", f"-I{ROOT / 'include'}",
+                    str(ROOT / "tests" / "native" / "gen_sources.cpp"), f"-L{lib}", "-lqe_hip",
+                    f"-Wl,-rpath,{lib}", "-o", str(exe)], check=True, capture_output=True)
+    r = subprocess.run([str(exe), str(out)], check=True, capture_output=True, text=True)
     return [pathlib.Path(p) for p in r.stdout.split()]
 
 
