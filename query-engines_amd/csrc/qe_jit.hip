@@ -374,13 +374,13 @@ void emit_agg_rows(const Plan& P, std::ostringstream& o, const std::vector<std::
 // flag `excl` says this workgroup holds every record of its groups, the combines are plain
 // read-modify-writes (gadd_cstar_excl / gcombine_excl).
 void emit_flush(const Plan& P, std::ostringstream& o, bool mark_full = false, bool part = false) {
+  // new groups: counted in the workgroup's LDS word s_newg (the caller adds it to ctl[0] once)
   o << "  __syncthreads();\n"
     << "  for (int s = threadIdx.x; s < SS; s += blockDim.x) {\n"
     << "    const qu32 c = s_cst[s];\n    if (c == 0) continue;\n"
     << "    const bool knl = s == S;\n    const qi64 key = knl ? 0 : (s == S + 1 ? EMPTY_KEY : s_keys[s]);\n"
     << "    qu64 gs;\n"
-    << (part ? "    const bool ok = gtable_find_wg(P.t, key, knl, gs, &s_newg);\n"
-             : "    const bool ok = gtable_find(P.t, key, knl, gs);\n")
+    << "    const bool ok = gtable_find_wg(P.t, key, knl, gs, &s_newg);\n"
     << "    qu8* rec = nullptr;\n"
     << (part ? "    if (ok) {\n      if (excl) gadd_cstar_excl(P.t, gs, c, &s_newg); else gadd_cstar(P.t, gs, c);\n    } else {\n"
              : "    if (ok) {\n      gadd_cstar(P.t, gs, c);\n    } else {\n")
@@ -438,7 +438,8 @@ bool gen_fused_source(const Plan& P, int log2, std::string* src, size_t* lds_byt
   std::ostringstream o;
   const bool pf = fused_prefetch();
   o << "\nusing namespace qe;\n"
-    << "extern \"C\" __global__ void __launch_bounds__(" << fused_block() << ") qe_fused(const Plan P) {\n";
+    << "extern \"C\" __global__ void __launch_bounds__(" << fused_block() << ") qe_fused(const Plan P) {\n"
+    << "  __shared__ qu32 s_newg;\n  if (threadIdx.x == 0) s_newg = 0;\n";
   emit_lds_table(P, o, log2, lds_bytes);
   o << "  const int lane = threadIdx.x & 63;\n"
     << "  const qi64 wave = (blockIdx.x * (qi64)blockDim.x + threadIdx.x) >> 6;\n"
@@ -474,7 +475,7 @@ bool gen_fused_source(const Plan& P, int log2, std::string* src, size_t* lds_byt
   emit_agg_rows(P, o, val, ok, "P.row_base + r0 + 128 * (r >> 1) + (r & 1)", "r0 + 128 * (r >> 1) + (r & 1)");
   o << (pf ? "    } while (0);\n  }\n  }\n" : "  }\n");
   emit_flush(P, o);
-  o << "}\n";
+  o << "  __syncthreads();\n  if (threadIdx.x == 0 && s_newg) atomicAdd(&P.t.ctl[0], (qu64)s_newg);\n}\n";
   *src = std::string(kDevHeader) + o.str();
   return true;
 }
