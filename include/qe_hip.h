@@ -347,6 +347,8 @@ int qe_hashagg_num_groups(qe_hashagg* agg, int64_t* out);
 /* Materialise the single output batch (K:635-650): key columns then one column per
  * aggregate. out_keys[i]/out_aggs[j] must hold num_groups rows; validity buffers are
  * written when non-NULL (required for nullable results: any key, SUM/MIN/MAX/AVG).
+ * *out_groups is exact on return; the column contents are stream-ordered: they are written by
+ * work queued on the ctx stream (read them on that stream, or after qe_ctx_synchronize).
  * Output types: keys as declared; SUM/MIN/MAX as input type; COUNT/COUNT_STAR int64;
  * AVG fp64. */
 int qe_hashagg_finalize(qe_hashagg* agg, qe_column* out_keys, qe_column* out_aggs,
@@ -379,6 +381,14 @@ int qe_hashagg_import(qe_hashagg* agg, const void* records, int64_t nrecords);
 int qe_hashagg_export_slots(qe_hashagg* agg, int32_t nparts, int64_t slot_records, void* dst);
 int qe_hashagg_import_slots(qe_hashagg* agg, const void* slots, int32_t nslots, int64_t slot_records,
                             int64_t* max_count, int64_t* nrecords);
+
+/* Stream-ordered updates (default 0 = off). With `enable`, an update that needs one kernel launch
+ * returns once it is queued; the read-back of its counters — and, when the global table had to
+ * grow, the retry pass that re-reads the update's input columns — happens in the next call on
+ * this state (update, num_groups, finalize, export*, import*, last_kernel_time), which then also
+ * reports the update's errors. The input columns must stay valid until that call returns.
+ * qe_hashagg_reset discards a pending update; qe_hashagg_set_async(agg, 0) settles it. */
+int qe_hashagg_set_async(qe_hashagg* agg, int32_t enable);
 
 /* Offset added to row indices of the next update (for shards of one logical stream). */
 int qe_hashagg_set_row_base(qe_hashagg* agg, int64_t row_base);

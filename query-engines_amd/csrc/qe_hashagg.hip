@@ -26,6 +26,7 @@
 // Roofline: HBM read. Algorithmic bytes per row = sum of the widths of the columns read
 // (24 B/row for the headline: k, a, b int64).
 #include <map>
+#include <memory>
 #include <mutex>
 
 #include "qe_internal.hpp"
@@ -1247,6 +1248,12 @@ struct qe_hashagg {
   int last_launches = 0;
   int last_specialized = 0;  // 1: the last update ran a hipRTC-specialised kernel
   std::string jit_note;      // why the last update could not specialise (empty if it did)
+  // stream-ordered updates (qe_hashagg_set_async): the last update's launch, read back later
+  bool async = false;
+  bool pending = false;
+  std::unique_ptr<qe::Plan> pend_plan;
+  size_t pend_lds = 0;
+  int pend_out_i = 0;
 };
 
 namespace qe {
@@ -1716,8 +1723,151 @@ static int partition_rows(qe_hashagg* h, Plan& P, hipFunction_t* fn, int* grid) 
   return QE_OK;
 }
 
+// One launch of an update's aggregation kernel: pass 0 over the batch, pass > 0 over the rows
+// deferred by the previous pass (defer_in). Control counters cleared as needed, the kernel
+// chosen (plan-specialised when possible), events bracketing it (ev[0] of pass 0 / mp 0 is
+// recorded by the caller, before any partitioning work).
+static int launch_pass(qe_hashagg* h, Plan& P, size_t lds, hipFunction_t pfn, int pgrid, int pass, int mp,
+                       int out_i, const uint32_t* defer_in) {
+  qe_ctx* ctx = h->ctx;
+  const int64_t n = P.n;
+  QE_CHECK(pass < 64, QE_ERR_CAPACITY, "hash aggregate did not converge after %d passes", pass);
+  if (h->defer_dirty[out_i]) {
+    QE_HIP(hipMemsetAsync(h->defer[out_i], 0, h->defer_words * 4, ctx->stream));
+    h->defer_dirty[out_i] = false;
+  }
+  // deferred-row and overflow-record counters (ctl[3], lost groups, stays: only reset clears
+  // it); known zero after a reset or after a launch that read back zeros
+  if (!h->ctl_rows_clean) QE_HIP(hipMemsetAsync(h->ctl + 1, 0, 16, ctx->stream));
+  h->ctl_rows_clean = false;
+  P.t = h->t;
+  P.defer_in = defer_in;
+  P.defer_out = h->defer[out_i];
+  const int64_t waves = (int64_t)div_up((uint64_t)n, 256);
+  const int per_cu = lds ? std::max<int>(1, std::min<int>(8, (int)((160 * 1024) / lds))) : 8;
+  const int64_t gcap = std::min<int64_t>((int64_t)ctx->num_cus * per_cu, h->grid);
+  int grid = (int)std::min<int64_t>((int64_t)div_up((uint64_t)waves, HA_THREADS / 64), gcap);
+  if (grid < 1) grid = 1;
+  // specialised kernel for this plan shape when possible, else the generic interpreter
+  hipFunction_t jfn = pfn;
+  int jgrid = pgrid;
+  if (pfn) {
+    // records of the partitioned update
+  } else if (lds && ctx->jit) {
+    // kernel memoised on the plan's structure: source generation and the source-keyed module
+    // lookup ran on every update
+    static std::mutex memo_mu;
+    static std::map<std::string, std::pair<hipFunction_t, int>> memo;
+    const std::string key = plan_shape_key(ctx, P);
+    int bpc = 0;
+    bool have = false;
+    {
+      std::lock_guard<std::mutex> g(memo_mu);
+      auto it = memo.find(key);
+      if (it != memo.end()) {
+        jfn = it->second.first;
+        bpc = it->second.second;
+        have = true;
+      }
+    }
+    std::string src;
+    size_t jl = 0;
+    if (have || gen_fused_source(P, P.lds_log2, &src, &jl)) {
+      if (have || jit_kernel(ctx, src, &jfn, &bpc, "qe_fused", fused_block()) == QE_OK) {
+        if (!have) {
+          std::lock_guard<std::mutex> g(memo_mu);
+          memo[key] = {jfn, bpc};
+        }
+        jgrid = (int)std::min<int64_t>(std::min<int64_t>((int64_t)ctx->num_cus * bpc, h->grid * 512 / fused_block()),
+                                       (int64_t)div_up((uint64_t)waves, fused_block() / 64));
+        if (jgrid < 1) jgrid = 1;
+        h->jit_note.clear();
+      } else {
+        h->jit_note = qe_last_error();
+        jfn = nullptr;
+      }
+    } else {
+      h->jit_note = "plan shape not specialisable";
+    }
+  } else if (h->jit_note.rfind("partitioning unavailable", 0) != 0) {
+    h->jit_note = lds ? "jit disabled" : "global-only launch";
+  }
+  if (pass > 0 || mp > 0) QE_HIP(hipEventRecord(h->ev[0], ctx->stream));
+  if (jfn) {
+    QE_TRY(jit_launch(ctx, jfn, jgrid, P, pfn ? 512 : fused_block()));
+  } else {
+    QE_TRY(launch_hashagg(P, grid, lds, ctx->stream));
+  }
+  h->last_specialized = jfn ? 1 : 0;
+  QE_TRY(launch_check("k_hashagg"));
+  QE_HIP(hipEventRecord(h->ev[1], ctx->stream));
+  return QE_OK;
+}
+
+// After a launch: read the control counters back (synchronises), add the launch's time, and when
+// rows were deferred or groups went to the overflow area, grow the table, re-apply the overflow
+// records and set up the retry pass (*out_i / *defer_in). *done: nothing left to re-apply.
+static int settle_pass(qe_hashagg* h, const Plan& P, int* out_i, const uint32_t** defer_in, bool* done) {
+  uint64_t c[8];
+  QE_TRY(read_ctl(h, c));
+  {
+    float ms = 0.f;
+    QE_HIP(hipEventElapsedTime(&ms, h->ev[0], h->ev[1]));
+    h->last_kernel_ms += ms;
+    h->last_launches += 1;
+  }
+  QE_CHECK(c[3] == 0, QE_ERR_CAPACITY, "hash aggregate lost %llu groups (overflow area)", (unsigned long long)c[3]);
+  const uint64_t groups = c[0], deferred = c[1], ovf_recs = std::min<uint64_t>(c[2], P.ovf_cap);
+  h->ctl_rows_clean = c[1] == 0 && c[2] == 0;
+  *done = true;
+  if (deferred == 0 && ovf_recs == 0) {
+    if (groups * 2 > h->t.cap) QE_TRY(table_grow(h, 4 * h->t.cap));
+    h->known_groups = (int64_t)groups;  // saves finalize a device round trip
+    return QE_OK;
+  }
+  // grow, then re-apply what could not be inserted
+  QE_TRY(table_grow(h, std::max<uint64_t>(4 * h->t.cap, 2 * (groups + ovf_recs))));
+  if (ovf_recs) QE_TRY(import_records(h, h->ovf, (int64_t)ovf_recs));
+  if (deferred == 0) return QE_OK;
+  h->defer_dirty[*out_i] = true;
+  *defer_in = h->defer[*out_i];
+  *out_i ^= 1;
+  *done = false;
+  return QE_OK;
+}
+
+// Adaptive: once the groups seen exceed this launch's LDS table, most rows of later batches
+// would take the global-table path; they go through the radix-partitioned update instead,
+// sized for the groups seen so far.
+static void adapt_after_update(qe_hashagg* h, size_t lds, int lds_log2) {
+  if (h->known_groups > 0 && h->ctx->jit) {
+    if (lds && h->known_groups * 5 / 4 > ((int64_t)1 << lds_log2)) h->lds_log2 = 0;
+    if (h->lds_log2 == 0) h->expected_groups = std::max<int64_t>(h->expected_groups, h->known_groups);
+  }
+}
+
+// Stream-ordered update (qe_hashagg_set_async): the pass-0 launch is queued and the read-back of
+// its counters (with any growth / retry passes, which re-read the update's columns) is done by the
+// next call on the state. Nothing pending: no-op.
+static int settle_pending(qe_hashagg* h) {
+  if (!h->pending) return QE_OK;
+  h->pending = false;
+  Plan& P = *h->pend_plan;
+  int out_i = h->pend_out_i;
+  const uint32_t* defer_in = nullptr;
+  for (int pass = 1;; ++pass) {
+    bool done = false;
+    QE_TRY(settle_pass(h, P, &out_i, &defer_in, &done));
+    if (done) break;
+    QE_TRY(launch_pass(h, P, h->pend_lds, nullptr, 0, pass, 0, out_i, defer_in));
+  }
+  adapt_after_update(h, h->pend_lds, P.lds_log2);
+  return QE_OK;
+}
+
 static int run_update(qe_hashagg* h, Plan& P) {
   qe_ctx* ctx = h->ctx;
+  QE_TRY(settle_pending(h));
   const int64_t rows = P.n;
   if (rows == 0) return QE_OK;
   size_t lds = lds_layout(h, &P);
@@ -1790,118 +1940,31 @@ static int run_update(qe_hashagg* h, Plan& P) {
       pfn = nullptr;
     }
   }
-  const int64_t n = P.n;
   int out_i = 0;
   for (int mp = 0; mp < std::max(1, mp_n); ++mp) {
-  P.mp_pass = mp;
-  const uint32_t* defer_in = nullptr;
-  for (int pass = 0;; ++pass) {
-    QE_CHECK(pass < 64, QE_ERR_CAPACITY, "hash aggregate did not converge after %d passes", pass);
-    if (h->defer_dirty[out_i]) {
-      QE_HIP(hipMemsetAsync(h->defer[out_i], 0, h->defer_words * 4, ctx->stream));
-      h->defer_dirty[out_i] = false;
-    }
-    // deferred-row and overflow-record counters (ctl[3], lost groups, stays: only reset clears
-    // it); known zero after a reset or after a launch that read back zeros
-    if (!h->ctl_rows_clean) QE_HIP(hipMemsetAsync(h->ctl + 1, 0, 16, ctx->stream));
-    h->ctl_rows_clean = false;
-    P.t = h->t;
-    P.defer_in = defer_in;
-    P.defer_out = h->defer[out_i];
-    const int64_t waves = (int64_t)div_up((uint64_t)n, 256);
-    const int per_cu = lds ? std::max<int>(1, std::min<int>(8, (int)((160 * 1024) / lds))) : 8;
-    const int64_t gcap = std::min<int64_t>((int64_t)ctx->num_cus * per_cu, h->grid);
-    int grid = (int)std::min<int64_t>((int64_t)div_up((uint64_t)waves, HA_THREADS / 64), gcap);
-    if (grid < 1) grid = 1;
-    // specialised kernel for this plan shape when possible, else the generic interpreter
-    hipFunction_t jfn = pfn;
-    int jgrid = pgrid;
-    if (pfn) {
-      // records of the partitioned update
-    } else if (lds && ctx->jit) {
-      // kernel memoised on the plan's structure: source generation and the source-keyed module
-      // lookup ran on every update
-      static std::mutex memo_mu;
-      static std::map<std::string, std::pair<hipFunction_t, int>> memo;
-      const std::string key = plan_shape_key(ctx, P);
-      int bpc = 0;
-      bool have = false;
-      {
-        std::lock_guard<std::mutex> g(memo_mu);
-        auto it = memo.find(key);
-        if (it != memo.end()) {
-          jfn = it->second.first;
-          bpc = it->second.second;
-          have = true;
-        }
+    P.mp_pass = mp;
+    const uint32_t* defer_in = nullptr;
+    for (int pass = 0;; ++pass) {
+      QE_TRY(launch_pass(h, P, lds, pfn, pgrid, pass, mp, out_i, defer_in));
+      if (h->async && pass == 0 && mp_n == 0 && !pfn) {
+        // one plain launch: its counters are read (and anything deferred re-applied) by the
+        // next call on this state
+        if (!h->pend_plan) h->pend_plan.reset(new Plan());
+        *h->pend_plan = P;
+        h->pend_lds = lds;
+        h->pend_out_i = out_i;
+        h->pending = true;
+        h->row_base += rows;
+        return QE_OK;
       }
-      std::string src;
-      size_t jl = 0;
-      if (have || gen_fused_source(P, P.lds_log2, &src, &jl)) {
-        if (have || jit_kernel(ctx, src, &jfn, &bpc, "qe_fused", fused_block()) == QE_OK) {
-          if (!have) {
-            std::lock_guard<std::mutex> g(memo_mu);
-            memo[key] = {jfn, bpc};
-          }
-          jgrid = (int)std::min<int64_t>(std::min<int64_t>((int64_t)ctx->num_cus * bpc, h->grid * 512 / fused_block()),
-                                         (int64_t)div_up((uint64_t)waves, fused_block() / 64));
-          if (jgrid < 1) jgrid = 1;
-          h->jit_note.clear();
-        } else {
-          h->jit_note = qe_last_error();
-          jfn = nullptr;
-        }
-      } else {
-        h->jit_note = "plan shape not specialisable";
-      }
-    } else if (h->jit_note.rfind("partitioning unavailable", 0) != 0) {
-      h->jit_note = lds ? "jit disabled" : "global-only launch";
+      bool done = false;
+      QE_TRY(settle_pass(h, P, &out_i, &defer_in, &done));
+      if (done) break;
     }
-    if (pass > 0 || mp > 0) QE_HIP(hipEventRecord(h->ev[0], ctx->stream));
-    if (jfn) {
-      QE_TRY(jit_launch(ctx, jfn, jgrid, P, pfn ? 512 : fused_block()));
-    } else {
-      QE_TRY(launch_hashagg(P, grid, lds, ctx->stream));
-    }
-    h->last_specialized = jfn ? 1 : 0;
-    QE_TRY(launch_check("k_hashagg"));
-    QE_HIP(hipEventRecord(h->ev[1], ctx->stream));
-    uint64_t c[8];
-    QE_TRY(read_ctl(h, c));
-    {
-      float ms = 0.f;
-      QE_HIP(hipEventElapsedTime(&ms, h->ev[0], h->ev[1]));
-      h->last_kernel_ms += ms;
-      h->last_launches += 1;
-    }
-    QE_CHECK(c[3] == 0, QE_ERR_CAPACITY, "hash aggregate lost %llu groups (overflow area)", (unsigned long long)c[3]);
-    const uint64_t groups = c[0], deferred = c[1], ovf_recs = std::min<uint64_t>(c[2], P.ovf_cap);
-    h->ctl_rows_clean = c[1] == 0 && c[2] == 0;
-    if (deferred == 0 && ovf_recs == 0) {
-      if (groups * 2 > h->t.cap) QE_TRY(table_grow(h, 4 * h->t.cap));
-      h->known_groups = (int64_t)groups;  // saves finalize a device round trip
-      break;
-    }
-    // grow, then re-apply what could not be inserted
-    QE_TRY(table_grow(h, std::max<uint64_t>(4 * h->t.cap, 2 * (groups + ovf_recs))));
-    if (ovf_recs) {
-      QE_TRY(import_records(h, h->ovf, (int64_t)ovf_recs));
-    }
-    if (deferred == 0) break;
-    h->defer_dirty[out_i] = true;
-    defer_in = h->defer[out_i];
-    out_i ^= 1;
-  }
   }
   if (mp_n) h->jit_note = "multi-pass: " + std::to_string(mp_n) + " bucket passes";
   h->row_base += rows;
-  // Adaptive: once the groups seen exceed this launch's LDS table, most rows of later batches
-  // would take the global-table path; they go through the radix-partitioned update instead,
-  // sized for the groups seen so far.
-  if (h->known_groups > 0 && ctx->jit) {
-    if (lds && h->known_groups * 5 / 4 > ((int64_t)1 << P.lds_log2)) h->lds_log2 = 0;
-    if (h->lds_log2 == 0) h->expected_groups = std::max<int64_t>(h->expected_groups, h->known_groups);
-  }
+  adapt_after_update(h, lds, P.lds_log2);
   return QE_OK;
 }
 
@@ -2042,14 +2105,28 @@ int qe_hashagg_last_kernel_kind(qe_hashagg* h, int32_t* specialized, char* note,
 
 int qe_hashagg_last_kernel_time(qe_hashagg* h, double* ms, int32_t* launches) {
   QE_CHECK(h && ms, QE_ERR_INVALID_ARG, "null argument");
+  QE_TRY(ctx_enter(h->ctx));
+  QE_TRY(settle_pending(h));
   *ms = h->last_kernel_ms;
   if (launches) *launches = h->last_launches;
+  return QE_OK;
+}
+
+int qe_hashagg_set_async(qe_hashagg* h, int32_t enable) {
+  QE_CHECK(h, QE_ERR_INVALID_ARG, "null state");
+  QE_TRY(ctx_enter(h->ctx));
+  if (!enable) QE_TRY(settle_pending(h));
+  h->async = enable != 0;
   return QE_OK;
 }
 
 int qe_hashagg_reset(qe_hashagg* h) {
   QE_CHECK(h, QE_ERR_INVALID_ARG, "null state");
   QE_TRY(ctx_enter(h->ctx));
+  if (h->pending) {  // the table restarts: the pending launch's counters no longer matter
+    h->pending = false;
+    h->defer_dirty[h->pend_out_i] = true;
+  }
   const int grid = (int)std::min<uint64_t>(div_up(h->t.cap + 2, 256), 4096);
   hipLaunchKernelGGL(k_table_init, dim3(grid), dim3(256), 0, h->ctx->stream, h->t, agg_meta(h), (qu64*)h->ctl);
   QE_TRY(launch_check("k_table_init"));
@@ -2137,6 +2214,7 @@ int qe_hashagg_update(qe_hashagg* h, const qe_column* keys, const qe_column* agg
 int qe_hashagg_num_groups(qe_hashagg* h, int64_t* out) {
   QE_CHECK(h && out, QE_ERR_INVALID_ARG, "null argument");
   QE_TRY(ctx_enter(h->ctx));
+  QE_TRY(settle_pending(h));
   if (h->known_groups >= 0) {
     *out = h->known_groups;
     return QE_OK;
@@ -2154,6 +2232,7 @@ int qe_hashagg_finalize(qe_hashagg* h, qe_column* out_keys, qe_column* out_aggs,
   qe_ctx* ctx = h->ctx;
   int64_t groups;
   QE_TRY(qe_hashagg_num_groups(h, &groups));
+  if (out_groups) *out_groups = groups;  // also on QE_ERR_CAPACITY: callers size the outputs from it
   // small tables finalise in one workgroup that also zeroes the validity bitmaps
   const bool small = h->t.cap + 2 <= (uint64_t)FS_THREADS * FS_PER && groups <= (int64_t)FS_WORDS * 32;
   OutCols oc{};
@@ -2182,7 +2261,6 @@ int qe_hashagg_finalize(qe_hashagg* h, qe_column* out_keys, qe_column* out_aggs,
     oc.aggs[j] = c;
     if (c.validity && !small) QE_HIP(hipMemsetAsync(c.validity, 0, div_up((uint64_t)groups, 32) * 4, ctx->stream));
   }
-  if (out_groups) *out_groups = groups;
   for (int k = 0; k < h->nkeys; ++k) out_keys[k].length = groups;
   for (int j = 0; j < h->naggs; ++j) out_aggs[j].length = groups;
   if (groups == 0) return QE_OK;
@@ -2190,8 +2268,7 @@ int qe_hashagg_finalize(qe_hashagg* h, qe_column* out_keys, qe_column* out_aggs,
     hipLaunchKernelGGL(k_finalize_small, dim3(1), dim3(FS_THREADS), 0, ctx->stream, h->t, agg_meta(h), h->km, oc,
                        (qi64)groups);
     QE_TRY(launch_check("k_finalize_small"));
-    QE_TRY(ctx_sync(ctx));
-    return QE_OK;
+    return QE_OK;  // stream-ordered: the outputs are ready when the ctx stream's work is
   }
   // one 256-slot tile per workgroup: a single pass each, so the chip finalises in one wave of
   // workgroups instead of a serial walk of long tiles
@@ -2208,7 +2285,6 @@ int qe_hashagg_finalize(qe_hashagg* h, qe_column* out_keys, qe_column* out_aggs,
   hipLaunchKernelGGL(k_finalize, dim3((unsigned)ntiles), dim3(256), 0, ctx->stream, h->t, agg_meta(h), h->km, (const qi64*)offs,
                      tile_slots, oc);
   QE_TRY(launch_check("k_finalize"));
-  QE_TRY(ctx_sync(ctx));
   return QE_OK;
 }
 
@@ -2221,6 +2297,7 @@ int qe_hashagg_record_bytes(qe_hashagg* h, int64_t* out) {
 int qe_hashagg_export_counts(qe_hashagg* h, int32_t nparts, int64_t* counts) {
   QE_CHECK(h && counts && nparts >= 1, QE_ERR_INVALID_ARG, "bad arguments");
   QE_TRY(ctx_enter(h->ctx));
+  QE_TRY(settle_pending(h));
   qe_ctx* ctx = h->ctx;
   void* s;
   QE_TRY(ctx_scratch(ctx, (size_t)nparts * 8, &s));
@@ -2259,6 +2336,7 @@ int qe_hashagg_export(qe_hashagg* h, int32_t nparts, void* dst) {
 int qe_hashagg_export_slots(qe_hashagg* h, int32_t nparts, int64_t slot_records, void* dst) {
   QE_CHECK(h && nparts >= 1 && slot_records >= 1 && dst, QE_ERR_INVALID_ARG, "bad arguments");
   QE_TRY(ctx_enter(h->ctx));
+  QE_TRY(settle_pending(h));
   qe_ctx* ctx = h->ctx;
   void* s;
   QE_TRY(ctx_scratch(ctx, (size_t)nparts * 8, &s));
@@ -2278,6 +2356,7 @@ int qe_hashagg_import_slots(qe_hashagg* h, const void* slots, int32_t nslots, in
                             int64_t* max_count, int64_t* nrecords) {
   QE_CHECK(h && slots && nslots >= 1 && slot_records >= 1 && max_count, QE_ERR_INVALID_ARG, "bad arguments");
   QE_TRY(ctx_enter(h->ctx));
+  QE_TRY(settle_pending(h));
   qe_ctx* ctx = h->ctx;
   const uint64_t slot_bytes = QE_SLOT_HEADER + (uint64_t)slot_records * h->rec_bytes;
   // the senders' counts decide, identically on every rank, whether the slots held everything
@@ -2302,6 +2381,7 @@ int qe_hashagg_import_slots(qe_hashagg* h, const void* slots, int32_t nslots, in
 int qe_hashagg_import(qe_hashagg* h, const void* records, int64_t nrecords) {
   QE_CHECK(h && nrecords >= 0 && (records || nrecords == 0), QE_ERR_INVALID_ARG, "bad arguments");
   QE_TRY(ctx_enter(h->ctx));
+  QE_TRY(settle_pending(h));
   if (nrecords == 0) return QE_OK;
   h->known_groups = -1;
   uint64_t c[8];

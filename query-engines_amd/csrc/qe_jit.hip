@@ -142,12 +142,16 @@ bool fused_prefetch() {
   }();
   return v;
 }
-// QE_FUSED_BLOCK: workgroup size of the fused kernel (256 / 512 / 1024).
+// QE_FUSED_BLOCK: workgroup size of the fused kernel (256 / 512 / 1024). Default 1024: the same
+// 16 waves per CU as two 512-thread workgroups, but ONE LDS table per CU, so the end-of-kernel
+// flush into the global table does half the device-scope atomics. C4 at 1B rows, one box:
+// 1024 3.571 ms, 512 3.609 / 3.611 ms, 256 4.168 ms; QE_FUSED_PF=1 (512) 3.793 ms; four
+// interleaved pairs on another box (tools/exp_variants.sh): median 3.556 (1024) vs 3.566 ms (512).
 int fused_block() {
   static const int v = [] {
     const char* e = getenv("QE_FUSED_BLOCK");
-    const int b = e ? atoi(e) : 512;
-    return (b == 256 || b == 1024) ? b : 512;
+    const int b = e ? atoi(e) : 1024;
+    return (b == 256 || b == 512) ? b : 1024;
   }();
   return v;
 }

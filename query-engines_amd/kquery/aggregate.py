@@ -71,6 +71,24 @@ def _carve(ctx: Context, n: int, specs) -> List[DeviceColumn]:
     return out
 
 
+def _trim(c: DeviceColumn, n: int) -> DeviceColumn:
+    """The first n rows of a carved output column (views of its buffers)."""
+    from .columnar import bitmap_bytes
+
+    v = c.values[: max(n, 1)]
+    vb = c.validity[: max(bitmap_bytes(n), 4)] if c.validity is not None else None
+    return DeviceColumn(c.type, n, v, vb, None, c.ctx)
+
+
+def _order_for_reader(ctx: Context) -> None:
+    """Stream-ordered results (qe_hashagg_finalize) are read through torch on its current stream:
+    when that is not the ctx's stream, wait for the ctx's queued work first."""
+    import torch
+
+    if torch.cuda.current_stream(ctx.torch_device).cuda_stream != ctx.stream:
+        ctx.synchronize()
+
+
 def dictionary_keys(key_types) -> Optional[int]:
     """None when qe_hashagg groups by these keys directly; otherwise the number of device key
     columns the dictionaries turn them into (UTF-8 keys -> one int32 code each; a key set that
@@ -85,7 +103,10 @@ class HashAggregateState:
     """Owns one qe_hashagg. Keys: ``key_types``; aggregates: (fn, input_type) pairs."""
 
     def __init__(self, ctx: Context, key_types: Sequence[int], aggs: Sequence[Tuple[int, int]],
-                 expected_groups: int = 1024):
+                 expected_groups: int = 1024, async_update: bool = False):
+        """``async_update``: stream-ordered updates (qe_hashagg_set_async) — an update returns once
+        its kernel is queued and is checked by the next call on the state; the caller keeps the
+        update's input columns alive until then (finalize, num_groups, the next update)."""
         from .strdict import StringDictionary
 
         self.ctx = ctx
@@ -109,6 +130,9 @@ class HashAggregateState:
         N.check(N.lib().qe_hashagg_create(ctx.handle, len(self.device_key_types), kt, len(self.aggs), ad,
                                           int(expected_groups), N.C.byref(h)))
         self.handle = h
+        self._out_rows = max(1, 2 * self.expected_groups)  # finalize's first output sizing guess
+        if async_update:
+            N.check(N.lib().qe_hashagg_set_async(h, 1))
 
     def close(self) -> None:
         for d in getattr(self, "dicts", {}).values():
@@ -191,17 +215,32 @@ class HashAggregateState:
         return n.value
 
     def finalize(self) -> Tuple[List[DeviceColumn], List[DeviceColumn]]:
-        """One output batch (Main.kt:635-650): key columns, aggregate columns."""
-        g = self.num_groups()
-        cols = _carve(self.ctx, g, [(t, True) for t in self.device_key_types] +
-                      [(output_type(f, t), f not in (N.AGG_COUNT, N.AGG_COUNT_STAR)) for f, t in self.aggs])
-        keys, aggs = cols[:len(self.device_key_types)], cols[len(self.device_key_types):]
-        kc = (N.QeColumn * max(1, len(keys)))(*[k.as_c() for k in keys])
-        ac = (N.QeColumn * max(1, len(aggs)))(*[a.as_c() for a in aggs])
-        out = N.C.c_int64()
-        N.check(N.lib().qe_hashagg_finalize(self.handle, kc, ac, N.C.byref(out)))
-        for c in keys + aggs:
-            c.length = out.value
+        """One output batch (Main.kt:635-650): key columns, aggregate columns.
+
+        The outputs are carved before the call, at the size of the last result (or 2x the
+        expected groups), so that the host work is done before qe_hashagg_finalize waits for the
+        aggregation; a larger result (QE_ERR_CAPACITY, with the exact count) carves again."""
+        specs = ([(t, True) for t in self.device_key_types] +
+                 [(output_type(f, t), f not in (N.AGG_COUNT, N.AGG_COUNT_STAR)) for f, t in self.aggs])
+        nk = len(self.device_key_types)
+        out = N.C.c_int64(-1)
+        rows = self._out_rows
+        while True:
+            cols = _carve(self.ctx, rows, specs)
+            kc = (N.QeColumn * max(1, nk))(*[k.as_c() for k in cols[:nk]])
+            ac = (N.QeColumn * max(1, len(cols) - nk))(*[a.as_c() for a in cols[nk:]])
+            st = N.lib().qe_hashagg_finalize(self.handle, kc, ac, N.C.byref(out))
+            if st == N.QE_ERR_CAPACITY and out.value > rows:
+                rows = out.value
+                continue
+            N.check(st)
+            break
+        g = out.value
+        self._out_rows = max(1, g)
+        _order_for_reader(self.ctx)
+        if g != rows:
+            cols = [_trim(c, g) for c in cols]
+        keys, aggs = cols[:nk], cols[nk:]
         if self.tuple_dict is not None:
             keys = self.tuple_dict.decode_tuple(keys[0], self.member_types)
         keys = [self.dicts[i].decode(k) if i in self.dicts else k for i, k in enumerate(keys)]
