@@ -272,7 +272,10 @@ __global__ void k_agg_global_unpack(const uint8_t* __restrict__ recs, int n, GPa
   for (int i = threadIdx.x; i < n; i += blockDim.x) out[i] = *(const GPart*)(recs + (size_t)i * QE_GLOBAL_PARTIAL_BYTES);
 }
 
-__global__ void __launch_bounds__(256) k_agg_global_final(GPart* __restrict__ partials, int nparts) {
+// host_out (optional): pinned host memory that also receives the result, so the caller reads it
+// after a stream sync with no device-to-host copy launch.
+__global__ void __launch_bounds__(256) k_agg_global_final(GPart* __restrict__ partials, int nparts,
+                                                          GPart* __restrict__ host_out) {
   // Fixed-order reduction: thread t folds partials t, t+256, ...; then a fixed wave/block tree.
   GPart p;
   gpart_init(p);
@@ -285,6 +288,7 @@ __global__ void __launch_bounds__(256) k_agg_global_final(GPart* __restrict__ pa
     GPart b = wp[0];
     for (int w = 1; w < 4; ++w) gpart_merge(b, wp[w]);
     partials[nparts] = b;
+    if (host_out) *host_out = b;
   }
 }
 
@@ -303,7 +307,8 @@ using namespace qe;
 namespace qe {
 
 // The column's partial, reduced on the device into *result (a GPart in scratch).
-static int agg_global_partial(qe_ctx* ctx, const qe_column* col, const qe_column* mask, GPart** result) {
+static int agg_global_partial(qe_ctx* ctx, const qe_column* col, const qe_column* mask, GPart** result,
+                              GPart* host_out = nullptr) {
   QE_CHECK(col, QE_ERR_INVALID_ARG, "null argument");
   QE_CHECK(col->type == QE_TYPE_INT64 || col->type == QE_TYPE_FLOAT64, QE_ERR_UNSUPPORTED,
            "global aggregate over type %d not supported (int64/fp64)", col->type);
@@ -333,17 +338,19 @@ static int agg_global_partial(qe_ctx* ctx, const qe_column* col, const qe_column
     hipLaunchKernelGGL(k_agg_global<false>, dim3((unsigned)blocks), dim3(256), 0, ctx->stream,
                        (const int64_t*)col->values, col->validity, mv, ml, n, parts);
   QE_TRY(launch_check("k_agg_global"));
-  hipLaunchKernelGGL(k_agg_global_final, dim3(1), dim3(256), 0, ctx->stream, parts, (int)blocks);
+  hipLaunchKernelGGL(k_agg_global_final, dim3(1), dim3(256), 0, ctx->stream, parts, (int)blocks, host_out);
   QE_TRY(launch_check("k_agg_global_final"));
   *result = parts + blocks;
   return QE_OK;
 }
 
-// Device GPart -> qe_global_agg (synchronises).
-static int agg_global_finish(qe_ctx* ctx, const GPart* dp, int32_t type, qe_global_agg* out) {
-  void* h;
-  QE_TRY(ctx_pinned(ctx, sizeof(GPart), &h));
-  QE_HIP(hipMemcpyAsync(h, dp, sizeof(GPart), hipMemcpyDeviceToHost, ctx->stream));
+// Device GPart -> qe_global_agg (synchronises). `h`: the pinned copy the final kernel wrote (no
+// copy needed), or null.
+static int agg_global_finish(qe_ctx* ctx, const GPart* dp, int32_t type, qe_global_agg* out, void* h = nullptr) {
+  if (!h) {
+    QE_TRY(ctx_pinned(ctx, sizeof(GPart), &h));
+    QE_HIP(hipMemcpyAsync(h, dp, sizeof(GPart), hipMemcpyDeviceToHost, ctx->stream));
+  }
   QE_TRY(ctx_sync(ctx));
   const GPart p = *(const GPart*)h;
   const bool f64 = type == QE_TYPE_FLOAT64;
@@ -373,9 +380,11 @@ static int agg_global_finish(qe_ctx* ctx, const GPart* dp, int32_t type, qe_glob
 extern "C" int qe_agg_global(qe_ctx* ctx, const qe_column* col, const qe_column* mask, qe_global_agg* out) {
   QE_TRY(ctx_enter(ctx));
   QE_CHECK(out, QE_ERR_INVALID_ARG, "null argument");
+  void* h;
+  QE_TRY(ctx_pinned(ctx, sizeof(GPart), &h));
   GPart* p;
-  QE_TRY(agg_global_partial(ctx, col, mask, &p));
-  return agg_global_finish(ctx, p, col->type, out);
+  QE_TRY(agg_global_partial(ctx, col, mask, &p, (GPart*)h));
+  return agg_global_finish(ctx, p, col->type, out, h);
 }
 
 extern "C" int qe_agg_global_partial(qe_ctx* ctx, const qe_column* col, const qe_column* mask, int64_t row_base,
@@ -401,7 +410,9 @@ extern "C" int qe_agg_global_merge(qe_ctx* ctx, int32_t type, const void* partia
   hipLaunchKernelGGL(k_agg_global_unpack, dim3(1), dim3(256), 0, ctx->stream, (const uint8_t*)partials, n, parts);
   QE_TRY(launch_check("k_agg_global_unpack"));
   // fixed-order fold: the same partials give the same bits on every rank
-  hipLaunchKernelGGL(k_agg_global_final, dim3(1), dim3(256), 0, ctx->stream, parts, (int)n);
+  void* h;
+  QE_TRY(ctx_pinned(ctx, sizeof(GPart), &h));
+  hipLaunchKernelGGL(k_agg_global_final, dim3(1), dim3(256), 0, ctx->stream, parts, (int)n, (GPart*)h);
   QE_TRY(launch_check("k_agg_global_final"));
-  return agg_global_finish(ctx, parts + n, type, out);
+  return agg_global_finish(ctx, parts + n, type, out, h);
 }

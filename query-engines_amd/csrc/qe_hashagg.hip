@@ -1773,13 +1773,13 @@ static int launch_pass(qe_hashagg* h, Plan& P, size_t lds, hipFunction_t pfn, in
     std::string src;
     size_t jl = 0;
     if (have || gen_fused_source(P, P.lds_log2, &src, &jl)) {
-      if (have || jit_kernel(ctx, src, &jfn, &bpc, "qe_fused", fused_block()) == QE_OK) {
+      if (have || jit_kernel(ctx, src, &jfn, &bpc, "qe_fused", fused_block(P.lds_log2)) == QE_OK) {
         if (!have) {
           std::lock_guard<std::mutex> g(memo_mu);
           memo[key] = {jfn, bpc};
         }
-        jgrid = (int)std::min<int64_t>(std::min<int64_t>((int64_t)ctx->num_cus * bpc, h->grid * 512 / fused_block()),
-                                       (int64_t)div_up((uint64_t)waves, fused_block() / 64));
+        jgrid = (int)std::min<int64_t>(std::min<int64_t>((int64_t)ctx->num_cus * bpc, h->grid * 512 / fused_block(P.lds_log2)),
+                                       (int64_t)div_up((uint64_t)waves, fused_block(P.lds_log2) / 64));
         if (jgrid < 1) jgrid = 1;
         h->jit_note.clear();
       } else {
@@ -1794,7 +1794,7 @@ static int launch_pass(qe_hashagg* h, Plan& P, size_t lds, hipFunction_t pfn, in
   }
   if (pass > 0 || mp > 0) QE_HIP(hipEventRecord(h->ev[0], ctx->stream));
   if (jfn) {
-    QE_TRY(jit_launch(ctx, jfn, jgrid, P, pfn ? 512 : fused_block()));
+    QE_TRY(jit_launch(ctx, jfn, jgrid, P, pfn ? 512 : fused_block(P.lds_log2)));
   } else {
     QE_TRY(launch_hashagg(P, grid, lds, ctx->stream));
   }

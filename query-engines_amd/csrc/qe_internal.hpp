@@ -87,7 +87,7 @@ bool gen_pagg_source(const qe::Plan& P, int log2, std::string* src, size_t* lds_
 bool part_staged_ok(const qe::Plan& P, int log2p);
 int pscatter_block();
 bool fused_prefetch();
-int fused_block();
+int fused_block(int lds_log2);
 bool gen_pscatter_staged_source(const qe::Plan& P, int log2p, std::string* src);
 int jit_kernel(qe_ctx* ctx, const std::string& src, hipFunction_t* fn, int* blocks_per_cu,
                const char* name = "qe_fused", int block = 512);

@@ -142,18 +142,21 @@ bool fused_prefetch() {
   }();
   return v;
 }
-// QE_FUSED_BLOCK: workgroup size of the fused kernel (256 / 512 / 1024). Default 1024: the same
-// 16 waves per CU as two 512-thread workgroups, but ONE LDS table per CU, so the end-of-kernel
-// flush into the global table does half the device-scope atomics. C4 at 1B rows, one box:
-// 1024 3.571 ms, 512 3.609 / 3.611 ms, 256 4.168 ms; QE_FUSED_PF=1 (512) 3.793 ms; four
-// interleaved pairs on another box (tools/exp_variants.sh): median 3.556 (1024) vs 3.566 ms (512).
-int fused_block() {
-  static const int v = [] {
+// Workgroup size of the fused kernel for an LDS table of 2^lds_log2 slots (QE_FUSED_BLOCK = 256 /
+// 512 / 1024 overrides). Large tables (>= 1024 slots): 1024 threads — the same 16 waves per CU as
+// two 512-thread workgroups but ONE table per CU, so the end-of-kernel flush into the global table
+// does half the device-scope atomics. C4 (2048 slots) at 1B rows, one box: 1024 3.571 ms, 512
+// 3.609 / 3.611 ms, 256 4.168 ms; QE_FUSED_PF=1 (512) 3.793 ms; four interleaved pairs on another
+// box (tools/exp_variants.sh): median 3.556 (1024) vs 3.566 ms (512). Small tables: 512 threads —
+// few slots shared by more waves contend in LDS; C5 (6 groups, 16 slots): 512 7.53 ms, 1024 7.78 ms.
+int fused_block(int lds_log2) {
+  static const int env = [] {
     const char* e = getenv("QE_FUSED_BLOCK");
-    const int b = e ? atoi(e) : 1024;
-    return (b == 256 || b == 512) ? b : 1024;
+    const int b = e ? atoi(e) : 0;
+    return (b == 256 || b == 512 || b == 1024) ? b : 0;
   }();
-  return v;
+  if (env) return env;
+  return lds_log2 >= 10 ? 1024 : 512;
 }
 
 namespace {
@@ -442,7 +445,7 @@ bool gen_fused_source(const Plan& P, int log2, std::string* src, size_t* lds_byt
   std::ostringstream o;
   const bool pf = fused_prefetch();
   o << "\nusing namespace qe;\n"
-    << "extern \"C\" __global__ void __launch_bounds__(" << fused_block() << ") qe_fused(const Plan P) {\n"
+    << "extern \"C\" __global__ void __launch_bounds__(" << fused_block(log2) << ") qe_fused(const Plan P) {\n"
     << "  __shared__ qu32 s_newg;\n  if (threadIdx.x == 0) s_newg = 0;\n";
   emit_lds_table(P, o, log2, lds_bytes);
   o << "  const int lane = threadIdx.x & 63;\n"
