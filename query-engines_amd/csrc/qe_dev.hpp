@@ -116,7 +116,8 @@ struct Plan {
   qi32 key_col[QE_MAX_KEYS], key_shift[QE_MAX_KEYS], key_nullbit[QE_MAX_KEYS], pad0;
   qi64 key_fmask[QE_MAX_KEYS];
   qi32 lds_log2, off_cstar;
-  qi32 all8, pad1;  // every column slot is 8 bytes wide (straight-line loads)
+  qi32 all8;       // every column slot is 8 bytes wide (straight-line loads)
+  qi32 nn_skip;    // bit j: the table keeps aggregate j's non-null count implicit (== COUNT(*)): no nn adds
   qi32 off_acc[QE_MAX_AGGS], off_nn[QE_MAX_AGGS], off_idx[QE_MAX_AGGS];
   // radix-partitioned aggregation (high group counts, qe_jit.hip gen_part_source / gen_pagg_source)
   qu8* part_rec;   // records grouped by key-hash bucket (scatter output, partition-aggregate input)
@@ -251,11 +252,13 @@ __device__ inline void gadd_cstar(const DTable& t, qu64 slot, qu64 c) {
   if (slot >= t.cap && old == 0) atomicAdd(&t.ctl[0], 1ull);  // a special group appears
 }
 
-// Combine one aggregate's partial state into global slot `s` (device-scope atomics).
+// Combine one aggregate's partial state into global slot `s` (device-scope atomics). add_nn =
+// false while the table keeps the aggregate's non-null count implicit (every input row so far was
+// non-null: nn == COUNT(*), read from cstar; see qe_hashagg.hip nn_implicit).
 __device__ inline void gcombine(const DTable& t, int acck, int j, qu64 s, qi64 acc, qu64 nn, qu64 i0, qu64 i1,
-                                qu64 i2, qu64 i3) {
+                                qu64 i2, qu64 i3, bool add_nn = true) {
   if (nn == 0) return;
-  atomicAdd(&t.nn[j][s], nn);
+  if (add_nn) atomicAdd(&t.nn[j][s], nn);
   switch (acck) {
     case ACC_SUM_I:
       if (acc) atomicAdd((qu64*)&t.acc[j][s], (qu64)acc);

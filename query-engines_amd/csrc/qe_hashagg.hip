@@ -725,7 +725,12 @@ struct AggMeta {
   qi32 naggs;
   qi32 fn[QE_MAX_AGGS];
   qi32 acc[QE_MAX_AGGS];
+  qi32 nn_implicit;  // bit j: aggregate j's non-null count is COUNT(*) (cstar); its nn array is unused
 };
+
+__device__ __forceinline__ qu64 slot_nn(const DTable& t, const AggMeta& m, int j, qu64 s) {
+  return ((m.nn_implicit >> j) & 1) ? t.cstar[s] : t.nn[j][s];
+}
 
 // Slice descriptors of the partition-aggregate pass (one workgroup). Bucket b's records are
 // [off[b * g], off[(b + 1) * g]) (bucket-major exclusive scan of the (bucket, workgroup) counts,
@@ -779,6 +784,15 @@ __global__ void k_table_init(DTable t, AggMeta m, qu64* zero_ctl) {
   }
 }
 
+// nn[j] := cstar for the aggregates in `mask` (an implicit non-null count made explicit, before a
+// launch that adds real non-null counts: nullable inputs, imported records, the generic kernel).
+__global__ void k_nn_materialize(DTable t, qi32 mask) {
+  const qu64 SS = t.cap + 2;
+  for (qu64 s = blockIdx.x * (qu64)blockDim.x + threadIdx.x; s < SS; s += (qu64)gridDim.x * blockDim.x)
+    for (int j = 0; j < QE_MAX_AGGS; ++j)
+      if ((mask >> j) & 1) t.nn[j][s] = t.cstar[s];
+}
+
 __device__ __forceinline__ bool gslot_occupied(const DTable& t, qu64 s) {
   return s < t.cap ? t.keys[s] != EMPTY_KEY : t.cstar[s] > 0;
 }
@@ -816,7 +830,7 @@ __global__ void k_rehash(DTable src, DTable dst, AggMeta m) {
       qu64 i[4] = {~0ull, ~0ull, ~0ull, ~0ull};
       if (acc_is_f64mm(a.acc))
         for (int k = 0; k < 4; ++k) i[k] = src.idx[j][k * SS + s];
-      gcombine(dst, a.acc, j, d, src.acc[j][s], src.nn[j][s], i[0], i[1], i[2], i[3]);
+      gcombine(dst, a.acc, j, d, src.acc[j][s], slot_nn(src, m, j, s), i[0], i[1], i[2], i[3]);
     }
   }
   wg_newg_end(&newg, dst.ctl);
@@ -936,7 +950,7 @@ __device__ void write_record(qu8* rec, const DTable& t, const AggMeta& m, qu64 s
   for (int j = 0; j < m.naggs; ++j) {
     qu64* f = (qu64*)(rec + off);
     f[0] = (qu64)t.acc[j][s];
-    f[1] = t.nn[j][s];
+    f[1] = slot_nn(t, m, j, s);
     if (acc_is_f64mm(m.acc[j]))
       for (int k = 0; k < 4; ++k) f[2 + k] = t.idx[j][k * SS + s];
     off += agg_rec_bytes(m.acc[j]);
@@ -1082,7 +1096,7 @@ __device__ __forceinline__ void finalize_slot(const DTable& t, const AggMeta& m,
   const qu64 cst = t.cstar[s];
 #pragma unroll 1
   for (int j = 0; j < m.naggs; ++j) {
-    const qu64 nn = t.nn[j][s];
+    const qu64 nn = slot_nn(t, m, j, s);
     const qi64 acc = t.acc[j][s];
     qi64 val = 0;
     bool valid = nn > 0;
@@ -1216,6 +1230,7 @@ struct qe_hashagg {
   int32_t acc[QE_MAX_AGGS] = {};
   KeyMeta km{};
   int32_t rec_bytes = 0;
+  int32_t nn_implicit = 0;  // bit j: the table's non-null count of aggregate j is COUNT(*) (AggMeta)
   int64_t row_base = 0;
   int64_t known_groups = 0;  // group count as of the last update/reset; -1 = read the device counter
   // global table
@@ -1265,7 +1280,34 @@ static AggMeta agg_meta(const qe_hashagg* h) {
     m.fn[j] = h->aggs[j].fn;
     m.acc[j] = h->acc[j];
   }
+  m.nn_implicit = h->nn_implicit;
   return m;
+}
+
+// Every aggregate's non-null count starts implicit (an empty table: nn == cstar == 0). The fused
+// kernel keeps it implicit while the aggregate's input is non-nullable — its flush then skips the
+// nn atomics (3 of the C4 flush's 7 per group) — and anything that adds real counts makes it
+// explicit first.
+static int32_t all_nn_bits(const qe_hashagg* h) {
+  static const bool off = [] {  // QE_NN_IMPLICIT=0: always store the counts (A/B and debugging)
+    const char* e = getenv("QE_NN_IMPLICIT");
+    return e && e[0] == '0';
+  }();
+  if (off) return 0;
+  int32_t b = 0;
+  for (int j = 0; j < h->naggs; ++j)
+    if (h->aggs[j].fn != QE_AGG_COUNT_STAR) b |= 1 << j;
+  return b;
+}
+
+static int nn_materialize(qe_hashagg* h, int32_t mask) {
+  mask &= h->nn_implicit;
+  if (!mask) return QE_OK;
+  const int grid = (int)std::min<uint64_t>(div_up(h->t.cap + 2, 256), 4096);
+  hipLaunchKernelGGL(k_nn_materialize, dim3(grid), dim3(256), 0, h->ctx->stream, h->t, (qi32)mask);
+  QE_TRY(launch_check("k_nn_materialize"));
+  h->nn_implicit &= ~mask;
+  return QE_OK;
 }
 
 static size_t table_bytes(const qe_hashagg* h, uint64_t cap) {
@@ -1740,6 +1782,14 @@ static int launch_pass(qe_hashagg* h, Plan& P, size_t lds, hipFunction_t pfn, in
   // it); known zero after a reset or after a launch that read back zeros
   if (!h->ctl_rows_clean) QE_HIP(hipMemsetAsync(h->ctl + 1, 0, 16, ctx->stream));
   h->ctl_rows_clean = false;
+  // non-null counts: an aggregate whose input is nullable in this launch needs its real count;
+  // the others stay implicit (the specialised kernels then skip their nn atomics; the generic and
+  // partitioned kernels still add them, into an array nothing reads while the bit is set)
+  int32_t tracked = 0;
+  for (int j = 0; j < P.naggs; ++j)
+    if (P.aggs[j].track_nn) tracked |= 1 << j;
+  QE_TRY(nn_materialize(h, tracked));
+  P.nn_skip = h->nn_implicit;
   P.t = h->t;
   P.defer_in = defer_in;
   P.defer_out = h->defer[out_i];
@@ -2071,6 +2121,7 @@ int qe_hashagg_create(qe_ctx* ctx, int32_t nkeys, const int32_t* key_types, int3
   }
   // global table: 2x expected groups
   const int st = table_alloc(h, std::max<uint64_t>(1024, next_pow2((uint64_t)(2 * eg))), &h->table_mem, &h->t);
+  h->nn_implicit = all_nn_bits(h);
   if (st != QE_OK) {
     dev_free(ctx, h->ovf);
     dev_free(ctx, h->ctl);
@@ -2130,6 +2181,7 @@ int qe_hashagg_reset(qe_hashagg* h) {
   const int grid = (int)std::min<uint64_t>(div_up(h->t.cap + 2, 256), 4096);
   hipLaunchKernelGGL(k_table_init, dim3(grid), dim3(256), 0, h->ctx->stream, h->t, agg_meta(h), (qu64*)h->ctl);
   QE_TRY(launch_check("k_table_init"));
+  h->nn_implicit = all_nn_bits(h);
   h->ctl_rows_clean = true;
   h->row_base = 0;
   h->known_groups = 0;
@@ -2357,6 +2409,7 @@ int qe_hashagg_import_slots(qe_hashagg* h, const void* slots, int32_t nslots, in
   QE_CHECK(h && slots && nslots >= 1 && slot_records >= 1 && max_count, QE_ERR_INVALID_ARG, "bad arguments");
   QE_TRY(ctx_enter(h->ctx));
   QE_TRY(settle_pending(h));
+  QE_TRY(nn_materialize(h, h->nn_implicit));  // records carry real non-null counts
   qe_ctx* ctx = h->ctx;
   const uint64_t slot_bytes = QE_SLOT_HEADER + (uint64_t)slot_records * h->rec_bytes;
   // the senders' counts decide, identically on every rank, whether the slots held everything
@@ -2383,6 +2436,7 @@ int qe_hashagg_import(qe_hashagg* h, const void* records, int64_t nrecords) {
   QE_TRY(ctx_enter(h->ctx));
   QE_TRY(settle_pending(h));
   if (nrecords == 0) return QE_OK;
+  QE_TRY(nn_materialize(h, h->nn_implicit));  // records carry real non-null counts
   h->known_groups = -1;
   uint64_t c[8];
   QE_TRY(read_ctl(h, c));

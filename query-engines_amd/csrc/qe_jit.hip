@@ -368,7 +368,8 @@ void emit_agg_rows(const Plan& P, std::ostringstream& o, const std::vector<std::
     const DAgg& a = P.aggs[j];
     if (a.pkind == 0) continue;
     o << "        if (" << ok[j] << ") { const RowVal rv = row_partial(" << a.acc << ", " << val[j]
-      << ", row); gcombine(P.t, " << a.acc << ", " << j << ", gs, rv.acc, 1, rv.i0, rv.i1, rv.i2, rv.i3); }\n";
+      << ", row); gcombine(P.t, " << a.acc << ", " << j << ", gs, rv.acc, 1, rv.i0, rv.i1, rv.i2, rv.i3, "
+      << (((P.nn_skip >> j) & 1) ? "false" : "true") << "); }\n";
   }
   o << "      }\n    }\n";
 }
@@ -408,11 +409,13 @@ void emit_flush(const Plan& P, std::ostringstream& o, bool mark_full = false, bo
         << "[2 * SS + s], i3 = s_idx" << js << "[3 * SS + s];\n";
     else
       o << "      const qu64 i0 = ~0ull, i1 = ~0ull, i2 = ~0ull, i3 = ~0ull;\n";
+    const bool skip_nn = (P.nn_skip >> j) & 1;
+    const char* add_nn = skip_nn ? "false" : "true";
     if (a.fn != QE_AGG_COUNT_STAR && part)
       o << "      if (ok) { if (excl) gcombine_excl(P.t, " << a.acc << ", " << j << ", gs, acc, nn, i0, i1, i2, i3);"
-        << " else gcombine(P.t, " << a.acc << ", " << j << ", gs, acc, nn, i0, i1, i2, i3); }\n";
-    else if (a.fn != QE_AGG_COUNT_STAR)
-      o << "      if (ok) gcombine(P.t, " << a.acc << ", " << j << ", gs, acc, nn, i0, i1, i2, i3);\n";
+        << " else gcombine(P.t, " << a.acc << ", " << j << ", gs, acc, nn, i0, i1, i2, i3, " << add_nn << "); }\n";
+    else if (a.fn != QE_AGG_COUNT_STAR && !(a.acc == ACC_NONE && skip_nn))  // implicit COUNT(x): nothing to add
+      o << "      if (ok) gcombine(P.t, " << a.acc << ", " << j << ", gs, acc, nn, i0, i1, i2, i3, " << add_nn << ");\n";
     o << "      if (!ok) { qu64* f = (qu64*)(rec + " << off << "); f[0] = (qu64)acc; f[1] = nn;";
     if (acc_is_f64mm(a.acc)) o << " f[2] = i0; f[3] = i1; f[4] = i2; f[5] = i3;";
     o << " }\n    }\n";

@@ -320,6 +320,35 @@ __global__ void __launch_bounds__(512) k_stream_read(StreamCols c, unsigned long
   if ((threadIdx.x & 63) == 0 && acc == 0x5A5A5A5A5A5A5A5Aull) atomicXor(out, acc);  // practically never
 }
 
+// Row-interleaved variant (every column the same number of 16-byte chunks): each wave step reads
+// two 1 KiB slabs of EVERY column, the access pattern of the fused aggregate (one contiguous KiB
+// per load instruction, all columns' streams in flight together).
+template <bool NT>
+__global__ void __launch_bounds__(1024) k_stream_read_rows(StreamCols c, unsigned long long* out) {
+  unsigned long long acc = 0;
+  const int lane = threadIdx.x & 63;
+  const int64_t wave = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 6;
+  const int64_t nw = ((int64_t)gridDim.x * blockDim.x) >> 6;
+  const int64_t n = c.n16[0];
+  for (int64_t base = wave * 128; base < n; base += nw * 128) {
+    const int64_t i = base + lane;
+    i64x2_rt v[16];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      if (k >= c.ncols) break;
+      v[2 * k] = i < n ? ld16<NT>(c.p[k] + i) : i64x2_rt{0, 0};
+      v[2 * k + 1] = i + 64 < n ? ld16<NT>(c.p[k] + i + 64) : i64x2_rt{0, 0};
+    }
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      if (k >= c.ncols) break;
+      acc ^= (unsigned long long)(v[2 * k].x ^ v[2 * k].y ^ v[2 * k + 1].x ^ v[2 * k + 1].y);
+    }
+  }
+  for (int m = 32; m > 0; m >>= 1) acc ^= __shfl_xor(acc, m);
+  if (lane == 0 && acc == 0x5A5A5A5A5A5A5A5Aull) atomicXor(out, acc);  // practically never
+}
+
 }  // namespace qe
 
 using namespace qe;
@@ -436,8 +465,17 @@ int qe_stream_read(qe_ctx* ctx, const qe_column* cols, int32_t ncols, double* ms
   hipEvent_t e0, e1;
   QE_HIP(hipEventCreate(&e0));
   QE_HIP(hipEventCreate(&e1));
+  bool same = true;
+  for (int k = 1; k < ncols; ++k) same = same && c.n16[k] == c.n16[0];
+  const bool nt = !(getenv("QE_NT") && getenv("QE_NT")[0] == '0');  // non-temporal (default), as the fused kernels
   QE_HIP(hipEventRecord(e0, ctx->stream));
-  if (!(getenv("QE_NT") && getenv("QE_NT")[0] == '0'))  // non-temporal (default), as the fused kernels
+  if (same && nt)
+    hipLaunchKernelGGL(k_stream_read_rows<true>, dim3(ctx->num_cus), dim3(1024), 0, ctx->stream, c,
+                       (unsigned long long*)s);
+  else if (same)
+    hipLaunchKernelGGL(k_stream_read_rows<false>, dim3(ctx->num_cus), dim3(1024), 0, ctx->stream, c,
+                       (unsigned long long*)s);
+  else if (nt)
     hipLaunchKernelGGL(k_stream_read<true>, dim3(ctx->num_cus * 4), dim3(512), 0, ctx->stream, c,
                        (unsigned long long*)s);
   else
