@@ -1004,8 +1004,11 @@ __global__ void k_export_slots(DTable t, AggMeta m, qi32 nparts, qi32 rec_bytes,
   }
 }
 
+// guard (a stream-ordered update not yet read back): its deferred-row / overflow / lost counters;
+// any of them nonzero means the table is incomplete, so word 1 reports "too many" and every rank
+// takes the variable-size exchange, which settles the update first.
 __global__ void k_slot_headers(const unsigned long long* __restrict__ cursor, qi32 nparts, qu64 slot_bytes,
-                               qu8* __restrict__ dst) {
+                               qu8* __restrict__ dst, const qu64* __restrict__ guard) {
   // one wave: word 0 = this slot's count, word 1 = the largest count over all slots
   qu64 mx = 0;
   for (int p = threadIdx.x; p < nparts; p += blockDim.x) mx = cursor[p] > mx ? cursor[p] : mx;
@@ -1013,6 +1016,7 @@ __global__ void k_slot_headers(const unsigned long long* __restrict__ cursor, qi
     const qu64 o = __shfl_xor(mx, off);
     mx = o > mx ? o : mx;
   }
+  if (guard && (guard[1] | guard[2] | guard[3])) mx = 1ull << 62;
   for (int p = threadIdx.x; p < nparts; p += blockDim.x) {
     qu64* hd = (qu64*)(dst + (qu64)p * slot_bytes);
     hd[0] = cursor[p];
@@ -1269,6 +1273,9 @@ struct qe_hashagg {
   std::unique_ptr<qe::Plan> pend_plan;
   size_t pend_lds = 0;
   int pend_out_i = 0;
+  // pinned snapshot of the control words queued behind each update launch, and its event
+  uint64_t* ctl_pin = nullptr;
+  hipEvent_t ev_ctl = nullptr;
 };
 
 namespace qe {
@@ -1851,6 +1858,10 @@ static int launch_pass(qe_hashagg* h, Plan& P, size_t lds, hipFunction_t pfn, in
   h->last_specialized = jfn ? 1 : 0;
   QE_TRY(launch_check("k_hashagg"));
   QE_HIP(hipEventRecord(h->ev[1], ctx->stream));
+  // the counters' snapshot is queued right behind the launch: settling waits for this event only,
+  // not for whatever the caller queued on the stream since (an exchange, the next query's work)
+  QE_HIP(hipMemcpyAsync(h->ctl_pin, h->ctl, 64, hipMemcpyDeviceToHost, ctx->stream));
+  QE_HIP(hipEventRecord(h->ev_ctl, ctx->stream));
   return QE_OK;
 }
 
@@ -1859,7 +1870,10 @@ static int launch_pass(qe_hashagg* h, Plan& P, size_t lds, hipFunction_t pfn, in
 // records and set up the retry pass (*out_i / *defer_in). *done: nothing left to re-apply.
 static int settle_pass(qe_hashagg* h, const Plan& P, int* out_i, const uint32_t** defer_in, bool* done) {
   uint64_t c[8];
-  QE_TRY(read_ctl(h, c));
+  QE_HIP(hipEventSynchronize(h->ev_ctl));
+  memcpy(c, h->ctl_pin, 64);
+  QE_CHECK(c[3] == 0, QE_ERR_CAPACITY, "hash aggregate lost %llu groups (probe limit or overflow area)",
+           (unsigned long long)c[3]);
   {
     float ms = 0.f;
     QE_HIP(hipEventElapsedTime(&ms, h->ev[0], h->ev[1]));
@@ -2035,6 +2049,9 @@ int qe_hashagg_create(qe_ctx* ctx, int32_t nkeys, const int32_t* key_types, int3
   h->nkeys = nkeys;
   h->naggs = naggs;
   auto bail = [&](int code) {
+    for (hipEvent_t e : {h->ev[0], h->ev[1], h->ev_ctl})
+      if (e) (void)hipEventDestroy(e);
+    if (h->ctl_pin) (void)hipHostFree(h->ctl_pin);
     delete h;
     return code;
   };
@@ -2094,8 +2111,11 @@ int qe_hashagg_create(qe_ctx* ctx, int32_t nkeys, const int32_t* key_types, int3
     h->rec_bytes += agg_rec_bytes(h->acc[j]);
   }
   // control words
-  if (hipEventCreate(&h->ev[0]) != hipSuccess || hipEventCreate(&h->ev[1]) != hipSuccess)
+  if (hipEventCreate(&h->ev[0]) != hipSuccess || hipEventCreate(&h->ev[1]) != hipSuccess ||
+      hipEventCreateWithFlags(&h->ev_ctl, hipEventDisableTiming) != hipSuccess)
     return bail(fail(QE_ERR_DEVICE, "hipEventCreate failed"));
+  if (hipHostMalloc((void**)&h->ctl_pin, 64, hipHostMallocDefault) != hipSuccess)
+    return bail(fail(QE_ERR_OOM, "pinned control snapshot allocation failed"));
   if (dev_alloc(ctx, 64, (void**)&h->ctl) != QE_OK) return bail(fail(QE_ERR_OOM, "control allocation failed"));
   if (hipMemsetAsync(h->ctl, 0, 64, ctx->stream) != hipSuccess) return bail(fail(QE_ERR_DEVICE, "memset failed"));
   // LDS table: 2x the expected groups (load factor <= 0.5); a launch may shrink it down to
@@ -2139,6 +2159,11 @@ int qe_hashagg_destroy(qe_hashagg* h) {
   for (void* b : bufs) dev_free(ctx, b);
   for (int i = 0; i < 2; ++i) {
     if (h->ev[i]) (void)hipEventDestroy(h->ev[i]);
+  }
+  if (h->ev_ctl) (void)hipEventDestroy(h->ev_ctl);
+  if (h->ctl_pin) {
+    (void)hipStreamSynchronize(ctx->stream);  // a queued snapshot copy may still target it
+    (void)hipHostFree(h->ctl_pin);
   }
   delete h;
   return QE_OK;
@@ -2388,7 +2413,9 @@ int qe_hashagg_export(qe_hashagg* h, int32_t nparts, void* dst) {
 int qe_hashagg_export_slots(qe_hashagg* h, int32_t nparts, int64_t slot_records, void* dst) {
   QE_CHECK(h && nparts >= 1 && slot_records >= 1 && dst, QE_ERR_INVALID_ARG, "bad arguments");
   QE_TRY(ctx_enter(h->ctx));
-  QE_TRY(settle_pending(h));
+  // a pending update is NOT settled here: the exchange queues behind it with no host round trip,
+  // and the slot headers force the variable-size exchange if it left the table incomplete
+  const bool speculative = h->pending;
   qe_ctx* ctx = h->ctx;
   void* s;
   QE_TRY(ctx_scratch(ctx, (size_t)nparts * 8, &s));
@@ -2399,7 +2426,7 @@ int qe_hashagg_export_slots(qe_hashagg* h, int32_t nparts, int64_t slot_records,
   QE_TRY(launch_check("k_export_slots"));
   const uint64_t slot_bytes = QE_SLOT_HEADER + (uint64_t)slot_records * h->rec_bytes;
   hipLaunchKernelGGL(k_slot_headers, dim3(1), dim3(64), 0, ctx->stream, (const unsigned long long*)s, nparts,
-                     (qu64)slot_bytes, (uint8_t*)dst);
+                     (qu64)slot_bytes, (uint8_t*)dst, speculative ? (const qu64*)h->ctl : (const qu64*)nullptr);
   QE_TRY(launch_check("k_slot_headers"));
   return QE_OK;
 }

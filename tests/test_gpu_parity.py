@@ -838,10 +838,14 @@ def test_export_partition_matches_oracle(gpu_ctx):
         assert off == len(np.unique(k))
 
 
-@pytest.mark.parametrize("slot_records", [None, 10])
-def test_exchange_rccl_single_rank(gpu_ctx, slot_records):
+@pytest.mark.parametrize("slot_records,expected,async_update", [(None, 8192, False), (10, 8192, False),
+                                                                (None, 8192, True), (8192, 16, True)])
+def test_exchange_rccl_single_rank(gpu_ctx, slot_records, expected, async_update):
     """The RCCL path of kquery.exchange (backend nccl = RCCL) end to end on one rank: fixed slots
-    (None: capacity = expected groups), and slots too small for the ~4990 groups (fallback)."""
+    (None: capacity = expected groups), slots too small for the ~4990 groups (fallback), and a
+    stream-ordered partial update exported before it is read back — (8192, 16): its table
+    overflowed (deferred rows), so the slot headers must force the variable-size exchange, which
+    settles the update first."""
     import os
     import socket
 
@@ -861,9 +865,10 @@ def test_exchange_rccl_single_rank(gpu_ctx, slot_records):
         k = rng.integers(0, 5000, 200_000).astype(np.int64)
         x = rng.integers(-100, 100, 200_000).astype(np.int64)
         aggs = [(N.AGG_SUM, N.TYPE_INT64), (N.AGG_COUNT_STAR, N.TYPE_INT64)]
-        part = HashAggregateState(gpu_ctx, [N.TYPE_INT64], aggs, 8192)
+        part = HashAggregateState(gpu_ctx, [N.TYPE_INT64], aggs, expected, async_update=async_update)
         owner = HashAggregateState(gpu_ctx, [N.TYPE_INT64], aggs, 8192)
-        part.update([dcol(gpu_ctx, N.TYPE_INT64, k)], [dcol(gpu_ctx, N.TYPE_INT64, x), None])
+        K, X = dcol(gpu_ctx, N.TYPE_INT64, k), dcol(gpu_ctx, N.TYPE_INT64, x)
+        part.update([K], [X, None])
         n = exchange_partials(part, owner, slot_records=slot_records)
         assert n == len(np.unique(k))
         kk, aa = owner.finalize()
