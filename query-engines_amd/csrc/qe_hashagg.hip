@@ -870,37 +870,44 @@ __global__ void k_import(const qu8* __restrict__ recs, qi64 nrec, qi32 rec_bytes
 }
 
 // Received slots (qe_hashagg_import_slots): header word 0 = records in the slot (the sender's
-// count; may exceed the capacity), word 1 = the sender's largest count over all its slots.
-__global__ void k_slots_scan(const qu8* __restrict__ slots, qi32 nslots, qu64 slot_bytes, qu64* ctl) {
-  // one wave: ctl[4] = max over senders of their largest count, ctl[5] = records held in total
-  qu64 mx = 0, tot = 0;
-  for (int i = threadIdx.x; i < nslots; i += blockDim.x) {
-    const qu64* hd = (const qu64*)(slots + (qu64)i * slot_bytes);
-    mx = hd[1] > mx ? hd[1] : mx;
-    tot += hd[0];
-  }
-  for (int off = 32; off > 0; off >>= 1) {
-    const qu64 o = __shfl_xor(mx, off);
-    mx = o > mx ? o : mx;
-    tot += __shfl_xor(tot, off);
-  }
-  if (threadIdx.x == 0) {
-    ctl[4] = mx;
-    ctl[5] = tot;
-  }
-}
-
+// count; may exceed the capacity), word 1 = the sender's largest count over all its slots. Every
+// workgroup first reads the headers: if some sender's largest count exceeds the slot capacity
+// (the same verdict on every rank), nothing is imported; block 0 reports ctl[4] = that largest
+// count, ctl[5] = records held in total. One launch and one read-back for the whole import.
 __global__ void k_import_slots(const qu8* __restrict__ slots, qi32 nslots, qi64 slot_records, qi32 rec_bytes,
                                DTable dst, AggMeta m) {
   __shared__ qu32 newg;
-  wg_newg_begin(&newg);
+  __shared__ qi32 s_ok;
   const qu64 slot_bytes = QE_SLOT_HEADER + (qu64)slot_records * rec_bytes;
-  const qi64 total = (qi64)nslots * slot_records;
-  for (qi64 r = blockIdx.x * (qi64)blockDim.x + threadIdx.x; r < total; r += (qi64)gridDim.x * blockDim.x) {
-    const qi64 sl = r / slot_records, i = r - sl * slot_records;
-    const qu8* base = slots + (qu64)sl * slot_bytes;
-    if ((qu64)i >= ((const qu64*)base)[0]) continue;
-    import_record(base + QE_SLOT_HEADER + (qu64)i * rec_bytes, dst, m, &newg);
+  if (threadIdx.x < 64) {
+    qu64 mx = 0, tot = 0;
+    for (int i = threadIdx.x; i < nslots; i += 64) {
+      const qu64* hd = (const qu64*)(slots + (qu64)i * slot_bytes);
+      mx = hd[1] > mx ? hd[1] : mx;
+      tot += hd[0] < (qu64)slot_records ? hd[0] : (qu64)slot_records;
+    }
+    for (int off = 32; off > 0; off >>= 1) {
+      const qu64 o = __shfl_xor(mx, off);
+      mx = o > mx ? o : mx;
+      tot += __shfl_xor(tot, off);
+    }
+    if (threadIdx.x == 0) {
+      s_ok = mx <= (qu64)slot_records;
+      if (blockIdx.x == 0) {
+        dst.ctl[4] = mx;
+        dst.ctl[5] = tot;
+      }
+    }
+  }
+  wg_newg_begin(&newg);  // (its barrier also publishes s_ok)
+  if (s_ok) {
+    const qi64 total = (qi64)nslots * slot_records;
+    for (qi64 r = blockIdx.x * (qi64)blockDim.x + threadIdx.x; r < total; r += (qi64)gridDim.x * blockDim.x) {
+      const qi64 sl = r / slot_records, i = r - sl * slot_records;
+      const qu8* base = slots + (qu64)sl * slot_bytes;
+      if ((qu64)i >= ((const qu64*)base)[0]) continue;
+      import_record(base + QE_SLOT_HEADER + (qu64)i * rec_bytes, dst, m, &newg);
+    }
   }
   wg_newg_end(&newg, dst.ctl);
 }
@@ -2438,23 +2445,29 @@ int qe_hashagg_import_slots(qe_hashagg* h, const void* slots, int32_t nslots, in
   QE_TRY(settle_pending(h));
   QE_TRY(nn_materialize(h, h->nn_implicit));  // records carry real non-null counts
   qe_ctx* ctx = h->ctx;
-  const uint64_t slot_bytes = QE_SLOT_HEADER + (uint64_t)slot_records * h->rec_bytes;
-  // the senders' counts decide, identically on every rank, whether the slots held everything
-  hipLaunchKernelGGL(k_slots_scan, dim3(1), dim3(64), 0, ctx->stream, (const uint8_t*)slots, nslots,
-                     (qu64)slot_bytes, h->ctl);
-  QE_TRY(launch_check("k_slots_scan"));
-  uint64_t c[8];
-  QE_TRY(read_ctl(h, c));
-  *max_count = (int64_t)c[4];
-  if (nrecords) *nrecords = (int64_t)c[5];
-  if (c[4] > (uint64_t)slot_records) return QE_OK;  // some sender overflowed a slot: nothing imported
-  if (c[5] == 0) return QE_OK;
-  if (2 * (c[0] + c[5]) > h->t.cap) QE_TRY(table_grow(h, 2 * (c[0] + c[5])));
+  // room for every record the slots can hold (duplicates counted: an upper bound) before the
+  // launch, so the import needs no read-back of its own first; the one read-back after it gives
+  // the verdict, the records and the group count (finalize then needs none)
+  uint64_t groups_before;
+  if (h->known_groups >= 0) {
+    groups_before = (uint64_t)h->known_groups;
+  } else {
+    uint64_t c[8];
+    QE_TRY(read_ctl(h, c));
+    groups_before = c[0];
+  }
+  const uint64_t bound = groups_before + (uint64_t)nslots * (uint64_t)slot_records;
+  if (2 * bound > h->t.cap) QE_TRY(table_grow(h, 2 * bound));
   h->known_groups = -1;
   const int grid = (int)std::min<uint64_t>(div_up((uint64_t)nslots * slot_records, 256), 8192);
   hipLaunchKernelGGL(k_import_slots, dim3(grid), dim3(256), 0, ctx->stream, (const uint8_t*)slots, nslots,
                      (qi64)slot_records, h->rec_bytes, h->t, agg_meta(h));
   QE_TRY(launch_check("k_import_slots"));
+  uint64_t c[8];
+  QE_TRY(read_ctl(h, c));
+  *max_count = (int64_t)c[4];
+  if (nrecords) *nrecords = (int64_t)c[5];
+  h->known_groups = (int64_t)c[0];
   return QE_OK;
 }
 

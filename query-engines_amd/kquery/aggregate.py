@@ -85,7 +85,9 @@ def _order_for_reader(ctx: Context) -> None:
     when that is not the ctx's stream, wait for the ctx's queued work first."""
     import torch
 
-    if torch.cuda.current_stream(ctx.torch_device).cuda_stream != ctx.stream:
+    raw = getattr(torch._C, "_cuda_getCurrentRawStream", None)  # the same handle, without a Stream object
+    cur = raw(ctx.device) if raw is not None else torch.cuda.current_stream(ctx.torch_device).cuda_stream
+    if cur != ctx.stream:
         ctx.synchronize()
 
 
@@ -214,24 +216,38 @@ class HashAggregateState:
         N.check(N.lib().qe_hashagg_num_groups(self.handle, N.C.byref(n)))
         return n.value
 
-    def finalize(self) -> Tuple[List[DeviceColumn], List[DeviceColumn]]:
-        """One output batch (Main.kt:635-650): key columns, aggregate columns.
+    def prepare_output(self) -> None:
+        """Carve the next finalize's output columns now (at the last result's size), so that the
+        host work is done before a call that waits for the device (kquery.exchange calls it
+        before the import's read-back)."""
+        if getattr(self, "_stash", None) is None:
+            self._stash = self._carve_c(self._out_rows)
 
-        The outputs are carved before the call, at the size of the last result (or 2x the
-        expected groups), so that the host work is done before qe_hashagg_finalize waits for the
-        aggregation; a larger result (QE_ERR_CAPACITY, with the exact count) carves again."""
+    def _carve_c(self, rows: int):
         specs = ([(t, True) for t in self.device_key_types] +
                  [(output_type(f, t), f not in (N.AGG_COUNT, N.AGG_COUNT_STAR)) for f, t in self.aggs])
         nk = len(self.device_key_types)
+        cols = _carve(self.ctx, rows, specs)
+        kc = (N.QeColumn * max(1, nk))(*[k.as_c() for k in cols[:nk]])
+        ac = (N.QeColumn * max(1, len(cols) - nk))(*[a.as_c() for a in cols[nk:]])
+        return rows, cols, kc, ac
+
+    def finalize(self) -> Tuple[List[DeviceColumn], List[DeviceColumn]]:
+        """One output batch (Main.kt:635-650): key columns, aggregate columns.
+
+        The outputs are carved before the call (or earlier, prepare_output), at the size of the
+        last result (or 2x the expected groups), so that the host work is done before
+        qe_hashagg_finalize waits for the aggregation; a larger result (QE_ERR_CAPACITY, with the
+        exact count) carves again."""
+        nk = len(self.device_key_types)
         out = N.C.c_int64(-1)
-        rows = self._out_rows
+        stash, self._stash = getattr(self, "_stash", None), None
         while True:
-            cols = _carve(self.ctx, rows, specs)
-            kc = (N.QeColumn * max(1, nk))(*[k.as_c() for k in cols[:nk]])
-            ac = (N.QeColumn * max(1, len(cols) - nk))(*[a.as_c() for a in cols[nk:]])
+            rows, cols, kc, ac = stash if stash is not None else self._carve_c(self._out_rows)
+            stash = None
             st = N.lib().qe_hashagg_finalize(self.handle, kc, ac, N.C.byref(out))
             if st == N.QE_ERR_CAPACITY and out.value > rows:
-                rows = out.value
+                self._out_rows = out.value
                 continue
             N.check(st)
             break

@@ -167,15 +167,18 @@ def exchange_partials(partial, owner, group: Optional[dist.ProcessGroup] = None,
     key and merges what this rank receives into `owner`. Returns the records received.
 
     Fast path: fixed-capacity slots of `slot_records` groups per destination (default: the
-    state's expected_groups, the same on every rank), ONE all-to-all, no host round trip before
-    it. If any rank had more groups for one owner than a slot holds, every rank sees it in the
-    slot headers and all of them fall back to the variable-size exchange (counts all-to-all,
+    state's expected groups spread over the ranks with headroom — 1.5x an even share plus 32,
+    at most the expected groups — the same on every rank), ONE all-to-all, no host round trip
+    before it. If any rank had more groups for one owner than a slot holds, every rank sees it in
+    the slot headers and all of them fall back to the variable-size exchange (counts all-to-all,
     then records)."""
     if getattr(partial, "keyed_by_dictionary", False):
         return exchange_keyed_partials(partial, owner, group)
     world = dist.get_world_size(group)
-    cap = int(slot_records or partial.expected_groups)
+    eg = int(partial.expected_groups)
+    cap = int(slot_records or min(eg, -(-3 * eg // (2 * world)) + 32))
     recv = all_to_all_slots(partial.export_slots(world, cap), group)
+    owner.prepare_output()  # host work of the owner's finalize, before the import's read-back
     n = owner.import_slots(recv, world, cap)
     if n is not None:
         return n
