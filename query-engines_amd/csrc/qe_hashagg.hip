@@ -1842,7 +1842,12 @@ static int launch_pass(qe_hashagg* h, Plan& P, size_t lds, hipFunction_t pfn, in
           std::lock_guard<std::mutex> g(memo_mu);
           memo[key] = {jfn, bpc};
         }
-        jgrid = (int)std::min<int64_t>(std::min<int64_t>((int64_t)ctx->num_cus * bpc, h->grid * 512 / fused_block(P.lds_log2)),
+        static const int wg_env = [] {  // QE_FUSED_WG_PER_CU: workgroups per CU (default: the state's)
+          const char* e = getenv("QE_FUSED_WG_PER_CU");
+          return e && *e ? std::max(1, atoi(e)) : 0;
+        }();
+        const int64_t per_state = wg_env ? (int64_t)ctx->num_cus * wg_env : h->grid * 512 / fused_block(P.lds_log2);
+        jgrid = (int)std::min<int64_t>(std::min<int64_t>((int64_t)ctx->num_cus * bpc, per_state),
                                        (int64_t)div_up((uint64_t)waves, fused_block(P.lds_log2) / 64));
         if (jgrid < 1) jgrid = 1;
         h->jit_note.clear();

@@ -142,21 +142,21 @@ bool fused_prefetch() {
   }();
   return v;
 }
-// Workgroup size of the fused kernel for an LDS table of 2^lds_log2 slots (QE_FUSED_BLOCK = 256 /
-// 512 / 1024 overrides). Large tables (>= 1024 slots): 1024 threads — the same 16 waves per CU as
-// two 512-thread workgroups but ONE table per CU, so the end-of-kernel flush into the global table
-// does half the device-scope atomics. C4 (2048 slots) at 1B rows, one box: 1024 3.571 ms, 512
-// 3.609 / 3.611 ms, 256 4.168 ms; QE_FUSED_PF=1 (512) 3.793 ms; four interleaved pairs on another
-// box (tools/exp_variants.sh): median 3.556 (1024) vs 3.566 ms (512). Small tables: 512 threads —
-// few slots shared by more waves contend in LDS; C5 (6 groups, 16 slots): 512 7.53 ms, 1024 7.78 ms.
+// Workgroup size of the fused kernel (QE_FUSED_BLOCK = 256 / 512 / 1024 overrides; the LDS table
+// size is an argument so that a shape-dependent rule can come back). 1024 threads: the same 16
+// waves per CU as two 512-thread workgroups but ONE LDS table per CU, so the end-of-kernel flush
+// into the global table does half the device-scope atomics. Interleaved A/B on one box each:
+// C4 (2048-slot table) 3.556 (1024) vs 3.566 ms (512); C5 (16-slot table) 7.28-7.29 (1024) vs
+// 7.55-7.58 ms (512), 1024 with 4 workgroups per CU 7.31 ms. (An earlier, non-interleaved pair
+// had C5 the other way round and briefly made small tables use 512.)
 int fused_block(int lds_log2) {
+  (void)lds_log2;
   static const int env = [] {
     const char* e = getenv("QE_FUSED_BLOCK");
     const int b = e ? atoi(e) : 0;
     return (b == 256 || b == 512 || b == 1024) ? b : 0;
   }();
-  if (env) return env;
-  return lds_log2 >= 10 ? 1024 : 512;
+  return env ? env : 1024;
 }
 
 namespace {
