@@ -102,12 +102,13 @@ int compile_inputs(const qe_column* cols, int32_t ncols, int32_t mask_col, int32
                    qe::Plan* P, bool* col_f64);
 int compile_program(const qe_column* cols, int32_t ncols, const bool* col_f64, const qe_agg_program& pg, int j,
                     qe::DAgg* a, bool* is_f, bool* nullable);
-// Select-project kernel source (qe_jit.hip): R rows per thread, 256 threads.
+// Select-project kernel source (qe_jit.hip): R rows per thread, selproj_block() threads.
 // Select-project tile order / pass: SP_COUNTER (tile ids from a device counter, look-back),
 // SP_PERSIST (persistent grid, look-back), SP_COUNT (two-pass, first pass: selected rows per tile
 // into t.keys), SP_WRITE (two-pass, second pass: each tile's base = sum of the earlier tiles' counts).
 enum { SP_COUNTER = 0, SP_PERSIST = 1, SP_COUNT = 2, SP_WRITE = 3 };
 bool gen_selproj_source(const qe::Plan& P, const int32_t* out_kind, int nout, std::string* src, int mode);
+int selproj_block();                                  // select-project workgroup size
 int selproj_rows_per_thread(const qe::Plan& P);
 bool selproj_nt(const qe::Plan& P);  // non-temporal input loads (large inputs)
 // Exclusive scan of n int64 on the ctx stream (one block); out[n] = total. (qe_filter.hip)

@@ -904,21 +904,32 @@ std::string plan_shape_key(const qe_ctx* ctx, const Plan& P) {
   return std::string((const char*)&k, sizeof k) + std::string((const char*)extra, sizeof extra);
 }
 
+// Select-project workgroup size (QE_SELPROJ_BLOCK = 256 / 512 / 1024).
+int selproj_block() {
+  static const int v = [] {
+    const char* e = getenv("QE_SELPROJ_BLOCK");
+    const int b = e && *e ? atoi(e) : 256;
+    return (b == 512 || b == 1024) ? b : 256;
+  }();
+  return v;
+}
+
 int selproj_rows_per_thread(const Plan& P) {
   static const int env = [] {
     const char* e = getenv("QE_SELPROJ_ROWS");
     const int v = e && *e ? atoi(e) : 0;
-    return (v == 4 || v == 8 || v == 16) ? v : 0;  // (R x 4 waves) chunk counts fit one wave's scan
+    return (v == 2 || v == 4 || v == 8 || v == 16) ? v : 0;
   }();
-  if (env) return env;
-  return P.ncols <= 3 ? 16 : (P.ncols <= 6 ? 8 : 4);
+  const int by_cols = env ? env : (P.ncols <= 3 ? 16 : (P.ncols <= 6 ? 8 : 4));
+  // (R x waves) per-(stripe, wave) counts fit one wave's scan
+  return std::min(by_cols, 64 / (selproj_block() / 64));
 }
 
-// act (bit r: row base + r * 256 + t is inside [0, n) and passes the predicate) of a
+// act (bit r: row base + r * BT + t is inside [0, n) and passes the predicate) of a
 // select-project tile whose columns are loaded.
 void emit_selproj_act(const Plan& P, std::ostringstream& o) {
   o << "  qu32 act = 0;\n"
-    << "#pragma unroll\n  for (int r = 0; r < R; ++r) act |= (qu32)(full || base + r * 256 + t < P.n) << r;\n";
+    << "#pragma unroll\n  for (int r = 0; r < R; ++r) act |= (qu32)(full || base + r * BT + t < P.n) << r;\n";
   std::ostringstream q;
   emit_predicate(P, q, 16);  // emits with a fixed trip count; R <= 16 and bits >= R are clear
   std::string body = q.str();
@@ -936,9 +947,9 @@ void emit_selproj_loads(const Plan& P, std::ostringstream& o, unsigned need, boo
     const std::string cs = std::to_string(c);
     const int kind = P.cols[c].kind;
     const char* ty = kind == K_I32 ? "qi32" : (kind == K_U8 || kind == K_BOOL) ? "qu8" : "qi64";
-    o << ind << "{\n" << ind << "  const qi64 lb = " << b << ";\n" << ind << "  const bool lfull = lb + R * 256 <= P.n;\n"
+    o << ind << "{\n" << ind << "  const qi64 lb = " << b << ";\n" << ind << "  const bool lfull = lb + R * BT <= P.n;\n"
       << ind << "  const " << ty << "* p = (const " << ty << "*)P.cols[" << cs << "].p;\n"
-      << "#pragma unroll\n" << ind << "  for (int r = 0; r < R; ++r) {\n" << ind << "    const qi64 row = lb + r * 256 + t;\n";
+      << "#pragma unroll\n" << ind << "  for (int r = 0; r < R; ++r) {\n" << ind << "    const qi64 row = lb + r * BT + t;\n";
     if (kind == K_BOOL)
       o << ind << "    " << cp << cs << "[r] = (lfull || row < P.n) ? ((p[row >> 3] >> (row & 7)) & 1) : 0;\n";
     else
@@ -947,7 +958,7 @@ void emit_selproj_loads(const Plan& P, std::ostringstream& o, unsigned need, boo
     o << ind << "  }\n";
     if (P.cols[c].valid) {
       o << ind << "  const qu8* vb = P.cols[" << cs << "].valid;\n" << ind << "  " << vp << cs << " = 0;\n"
-        << "#pragma unroll\n" << ind << "  for (int r = 0; r < R; ++r) {\n" << ind << "    const qi64 row = lb + r * 256 + t;\n"
+        << "#pragma unroll\n" << ind << "  for (int r = 0; r < R; ++r) {\n" << ind << "    const qi64 row = lb + r * BT + t;\n"
         << ind << "    if (lfull || row < P.n) " << vp << cs << " |= (qu32)((vb[row >> 3] >> (row & 7)) & 1) << r;\n"
         << ind << "  }\n";
     }
@@ -956,37 +967,37 @@ void emit_selproj_loads(const Plan& P, std::ostringstream& o, unsigned need, boo
 }
 
 // Write phase of one select-project tile, after the caller's code has loaded the tile's columns
-// (c<slot>[R], v<slot>) and computed `act` (bit r: row base + r * 256 + t is selected): ballots,
+// (c<slot>[R], v<slot>) and computed `act` (bit r: row base + r * BT + t is selected): ballots,
 // per-(stripe, wave) counts, one wave's scan, the tile's output base (decoupled look-back or the
 // two-pass prefix), then the compacted stores.
 bool emit_selproj_write(const Plan& P, const int32_t* out_kind, int nout, int mode, std::ostringstream& o) {
   const int R = selproj_rows_per_thread(P);
-  // Staged output (all outputs 8 bytes wide, R x 256 x 8 B each within 64 KiB of LDS): selected
+  // Staged output (all outputs 8 bytes wide, R x BT x 8 B each within 64 KiB of LDS): selected
   // rows land compacted in LDS, then the tile's output range is written with 16-byte stores, all
   // lanes active. Direct 8-byte stores from the row registers were store-issue bound (half the
   // lanes idle at 50 % selectivity, 16 store instructions per thread).
-  bool staged = (size_t)nout * R * 256 * 8 <= 64 * 1024;
+  bool staged = (size_t)nout * R * selproj_block() * 8 <= 64 * 1024;
   for (int k = 0; k < nout; ++k) staged = staged && (out_kind[k] & 0xFF) == 8;
   std::vector<Expr> ex(nout);
   for (int k = 0; k < nout; ++k)
     if (!agg_expr(P, k, &ex[k])) return false;
   o << "  qu64 bal[R];\n"
     << "#pragma unroll\n  for (int r = 0; r < R; ++r) bal[r] = __ballot((act >> r) & 1u);\n"
-    << "  if (lane == 0) {\n#pragma unroll\n    for (int r = 0; r < R; ++r) s_cnt[r * 4 + w] = (qu32)__popcll(bal[r]);\n  }\n"
+    << "  if (lane == 0) {\n#pragma unroll\n    for (int r = 0; r < R; ++r) s_cnt[r * W + w] = (qu32)__popcll(bal[r]);\n  }\n"
     << "  __syncthreads();\n"
     << "  qu64* st = (qu64*)P.t.keys;\n"
     << "  if (w == 0) {\n"
-    << "    const qu32 x = lane < R * 4 ? s_cnt[lane] : 0u;\n"
+    << "    const qu32 x = lane < R * W ? s_cnt[lane] : 0u;\n"
     << "    qu32 inc = x;\n"
     << "#pragma unroll\n    for (int d = 1; d < 64; d <<= 1) { const qu32 y = __shfl_up(inc, d); if (lane >= d) inc += y; }\n"
     << "    const qu64 total = (qu64)__shfl(inc, 63);\n"
-    << "    if (lane < R * 4) s_cnt[lane] = inc - x;\n"
+    << "    if (lane < R * W) s_cnt[lane] = inc - x;\n"
     << (mode == SP_WRITE ? "    if (lane == 0) s_total = (qu32)total;\n"
                          : "    if (lane == 0) { s_total = (qu32)total; __hip_atomic_store(&st[tile], (tile == 0 ? F_INC : F_AGG) | total, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }\n")
     << "  }\n";
   const std::string lookback = mode == SP_WRITE ?
       "    const qu64 total = s_total;\n"
-      "    if (lane == 0) {\n      const qu64 excl = s_pre[0] + s_pre[1] + s_pre[2] + s_pre[3];\n      s_base = excl;\n"
+      "    if (lane == 0) {\n      qu64 excl = 0;\n      for (int q = 0; q < W; ++q) excl += s_pre[q];\n      s_base = excl;\n"
       "      if ((qu64)tile == P.t.cap - 1) P.t.ctl[1] = excl + total;\n    }\n" :
       "    const qu64 total = s_total;\n"
       "    qu64 excl = 0;\n"
@@ -1021,8 +1032,8 @@ bool emit_selproj_write(const Plan& P, const int32_t* out_kind, int nout, int mo
     // once the tile base is known), while wave 0 then runs the look-back
     o << "#pragma unroll\n  for (int r = 0; r < R; ++r) {\n"
       << "    if (!((act >> r) & 1u)) continue;\n"
-      << "    const qu32 lp = s_cnt[r * 4 + w] + (qu32)__popcll(bal[r] & below);\n";
-    for (int k = 0; k < nout; ++k) o << "    s_out[" << k << " * (R * 256) + lp] = " << ex[k].v << ";\n";
+      << "    const qu32 lp = s_cnt[r * W + w] + (qu32)__popcll(bal[r] & below);\n";
+    for (int k = 0; k < nout; ++k) o << "    s_out[" << k << " * (R * BT) + lp] = " << ex[k].v << ";\n";
     o << "  }\n"
       << "  if (w == 0) {\n" << lookback << "  }\n"
       << "  __syncthreads();\n"
@@ -1030,17 +1041,17 @@ bool emit_selproj_write(const Plan& P, const int32_t* out_kind, int nout, int mo
     for (int k = 0; k < nout; ++k) {
       const std::string ks = std::to_string(k);
       o << "    {\n      qi64* out = (qi64*)P.t.acc[" << ks << "] + tb;\n"
-        << "      const qi64* so = s_out + " << ks << " * (R * 256);\n"
+        << "      const qi64* so = s_out + " << ks << " * (R * BT);\n"
         << "      const qu32 mis = (qu32)(((qu64)out >> 3) & 1), head = mis < tot ? mis : tot;  // 16-byte alignment\n"
         << "      if (head && t == 0) out[0] = so[0];\n"
-        << "      for (qu32 i = head + 2 * t; i + 1 < tot; i += 512) *(qi64x2*)(out + i) = qi64x2{so[i], so[i + 1]};\n"
+        << "      for (qu32 i = head + 2 * t; i + 1 < tot; i += 2 * BT) *(qi64x2*)(out + i) = qi64x2{so[i], so[i + 1]};\n"
         << "      if (t == 0 && tot > head && ((tot - head) & 1)) out[tot - 1] = so[tot - 1];\n    }\n";
     }
     const bool any_null = [&] { for (int k = 0; k < nout; ++k) if (out_kind[k] & 0x100) return true; return false; }();
     if (any_null) {
       o << "#pragma unroll\n    for (int r = 0; r < R; ++r) {\n"
         << "      if (!((act >> r) & 1u)) continue;\n"
-        << "      const qu64 pos = tb + s_cnt[r * 4 + w] + (qu64)__popcll(bal[r] & below);\n";
+        << "      const qu64 pos = tb + s_cnt[r * W + w] + (qu64)__popcll(bal[r] & below);\n";
       for (int k = 0; k < nout; ++k)
         if (out_kind[k] & 0x100)
           o << "      if (" << ex[k].ok << ") atomicOr(&((qu32*)P.t.nn[" << k << "])[pos >> 5], 1u << (pos & 31));\n";
@@ -1053,7 +1064,7 @@ bool emit_selproj_write(const Plan& P, const int32_t* out_kind, int nout, int mo
       << "  const qu64 tb = s_base;\n"
       << "#pragma unroll\n  for (int r = 0; r < R; ++r) {\n"
       << "    if (!((act >> r) & 1u)) continue;\n"
-      << "    const qu64 pos = tb + s_cnt[r * 4 + w] + (qu64)__popcll(bal[r] & below);\n";
+      << "    const qu64 pos = tb + s_cnt[r * W + w] + (qu64)__popcll(bal[r] & below);\n";
     for (int k = 0; k < nout; ++k) {
       const std::string ks = std::to_string(k);
       const int width = out_kind[k] & 0xFF;
@@ -1080,12 +1091,12 @@ bool gen_selproj_source(const Plan& P, const int32_t* out_kind, int nout, std::s
   const unsigned need = mode == SP_COUNT ? pred_key_cols(P) : ~0u;
   std::ostringstream o;
   o << "\nusing namespace qe;\n"
-    << "extern \"C\" __global__ void __launch_bounds__(256) qe_selproj(const Plan P) {\n"
-    << "  constexpr int R = " << R << ";\n"
+    << "extern \"C\" __global__ void __launch_bounds__(" << selproj_block() << ") qe_selproj(const Plan P) {\n"
+    << "  constexpr int R = " << R << ", BT = " << selproj_block() << ", W = BT / 64;\n"
     << "  constexpr qu64 F_AGG = 1ull << 62, F_INC = 2ull << 62, VMASK = (1ull << 62) - 1;\n"
     << "  constexpr bool PERSIST = " << (persistent ? "true" : "false") << ";\n"
-    << "  __shared__ qu32 s_cnt[R * 4];\n  __shared__ qu64 s_base;\n  __shared__ qu32 s_tile, s_total;\n"
-    << "  __shared__ qi64 s_out[" << ((size_t)nout * R * 256 * 8 <= 64 * 1024 ? nout * R * 256 : 1) << "];\n"
+    << "  __shared__ qu32 s_cnt[R * W];\n  __shared__ qu64 s_base;\n  __shared__ qu32 s_tile, s_total;\n"
+    << "  __shared__ qi64 s_out[" << ((size_t)nout * R * selproj_block() * 8 <= 64 * 1024 ? nout * R * selproj_block() : 1) << "];\n"
     << "  const int t = threadIdx.x, lane = t & 63, w = t >> 6;\n";
   auto emit_loads = [&](const std::string& cp, const std::string& vp, const std::string& b, const std::string& ind) {
     emit_selproj_loads(P, o, need, selproj_nt(P), cp, vp, b, ind);
@@ -1095,8 +1106,8 @@ bool gen_selproj_source(const Plan& P, const int32_t* out_kind, int nout, std::s
     // deadlock the look-back and no tile counter is needed. (Prefetching the next tile's columns
     // into registers during this tile's look-back measured slower: 5.00 vs 4.67 ms at 1B rows.)
     o << "  for (qu32 tile = blockIdx.x; (qu64)tile < P.t.cap; tile += gridDim.x) {\n"
-      << "  const qi64 base = (qi64)tile * (R * 256);\n"
-      << "  const bool full = base + R * 256 <= P.n;\n";
+      << "  const qi64 base = (qi64)tile * (R * BT);\n"
+      << "  const bool full = base + R * BT <= P.n;\n";
     for (int c = 0; c < P.ncols; ++c) {
       o << "  qi64 c" << c << "[R];\n";
       if (P.cols[c].valid) o << "  qu32 v" << c << " = 0;\n";
@@ -1109,8 +1120,8 @@ bool gen_selproj_source(const Plan& P, const int32_t* out_kind, int nout, std::s
         << "  const qu32 tile = s_tile;\n";
     else  // two-pass: one tile per workgroup in grid order
       o << "  {\n  const qu32 tile = blockIdx.x;\n";
-    o << "  const qi64 base = (qi64)tile * (R * 256);\n"
-      << "  const bool full = base + R * 256 <= P.n;\n";
+    o << "  const qi64 base = (qi64)tile * (R * BT);\n"
+      << "  const bool full = base + R * BT <= P.n;\n";
     for (int c = 0; c < P.ncols; ++c) {
       if (!((need >> c) & 1u)) continue;
       o << "  qi64 c" << c << "[R];\n";
@@ -1121,16 +1132,16 @@ bool gen_selproj_source(const Plan& P, const int32_t* out_kind, int nout, std::s
       // this tile's base: the earlier tiles' counts, summed by the whole workgroup while its
       // column loads are in flight
       o << "  qu64 pre = 0;\n"
-        << "  for (qi64 i = t; i < (qi64)tile; i += 256) pre += ((const qu64*)P.t.keys)[i];\n"
+        << "  for (qi64 i = t; i < (qi64)tile; i += BT) pre += ((const qu64*)P.t.keys)[i];\n"
         << "#pragma unroll\n  for (int d = 32; d >= 1; d >>= 1) pre += __shfl_xor(pre, d);\n"
-        << "  __shared__ qu64 s_pre[4];\n  if (lane == 0) s_pre[w] = pre;\n";
+        << "  __shared__ qu64 s_pre[W];\n  if (lane == 0) s_pre[w] = pre;\n";
   }
   emit_selproj_act(P, o);
   if (mode == SP_COUNT) {
     o << "  qu32 n = __popc(act);\n"
       << "#pragma unroll\n  for (int d = 32; d >= 1; d >>= 1) n += __shfl_xor(n, d);\n"
       << "  if (lane == 0) s_cnt[w] = n;\n  __syncthreads();\n"
-      << "  if (t == 0) ((qu64*)P.t.keys)[tile] = (qu64)s_cnt[0] + s_cnt[1] + s_cnt[2] + s_cnt[3];\n"
+      << "  if (t == 0) { qu64 c = 0; for (int q = 0; q < W; ++q) c += s_cnt[q]; ((qu64*)P.t.keys)[tile] = c; }\n"
       << "  }\n}\n";
     *src = std::string(kDevHeader) + o.str();
     return true;

@@ -52,7 +52,7 @@ int selproj_kernel(qe_ctx* ctx, const Plan& P, const int32_t* out_kind, int nout
   std::string src;
   if (!gen_selproj_source(P, out_kind, nout, &src, mode))
     return fail(QE_ERR_UNSUPPORTED, "plan shape is outside the select-project generator");
-  QE_TRY(jit_kernel(ctx, src, fn, bpc, "qe_selproj", 256));
+  QE_TRY(jit_kernel(ctx, src, fn, bpc, "qe_selproj", selproj_block()));
   std::lock_guard<std::mutex> g(mu);
   memo[key] = {*fn, *bpc};
   return QE_OK;
@@ -134,11 +134,11 @@ extern "C" int qe_select_project(qe_ctx* ctx, const qe_column* cols, int32_t nco
     if ((pred_cols >> c) & 1u) pred_bytes += (size_t)n * std::max(1, type_width(cols[c].type));
   // (each write-pass tile sums all earlier tiles' counts, so the tile count is bounded too: a
   // plan with no predicate reads nothing in the count pass but still pays the prefix sums)
-  const int64_t tiles_est = (int64_t)div_up((uint64_t)n, (uint64_t)selproj_rows_per_thread(P) * 256);
+  const int64_t tiles_est = (int64_t)div_up((uint64_t)n, (uint64_t)selproj_rows_per_thread(P) * selproj_block());
   const bool twopass = twopass_env >= 0 ? twopass_env == 1 : (pred_bytes <= (96ull << 20) && tiles_est <= 4096);
   if (n > 0 && twopass) {
     const int R = selproj_rows_per_thread(P);
-    const int64_t tiles = (int64_t)div_up((uint64_t)n, (uint64_t)R * 256);
+    const int64_t tiles = (int64_t)div_up((uint64_t)n, (uint64_t)R * selproj_block());
     QE_CHECK(tiles < (1ll << 31), QE_ERR_CAPACITY, "too many rows for one select-project call");
     void* s;
     QE_TRY(ctx_scratch(ctx, (size_t)(tiles + 3) * 8, &s));
@@ -152,7 +152,7 @@ extern "C" int qe_select_project(qe_ctx* ctx, const qe_column* cols, int32_t nco
       hipFunction_t fn;
       int bpc = 0;
       QE_TRY(selproj_kernel(ctx, P, out_kind, spec->nout, mode, &fn, &bpc));
-      QE_TRY(jit_launch(ctx, fn, (int)tiles, P, 256));
+      QE_TRY(jit_launch(ctx, fn, (int)tiles, P, selproj_block()));
       QE_TRY(launch_check(mode == SP_COUNT ? "qe_selproj (count)" : "qe_selproj (write)"));
     }
     QE_HIP(hipMemcpyAsync(pin, ctl + 1, 8, hipMemcpyDeviceToHost, ctx->stream));
@@ -160,7 +160,7 @@ extern "C" int qe_select_project(qe_ctx* ctx, const qe_column* cols, int32_t nco
     *out_count = ((int64_t*)pin)[0];
   } else if (n > 0) {
     const int R = selproj_rows_per_thread(P);
-    const int64_t tiles = (int64_t)div_up((uint64_t)n, (uint64_t)R * 256);
+    const int64_t tiles = (int64_t)div_up((uint64_t)n, (uint64_t)R * selproj_block());
     QE_CHECK(tiles < (1ll << 31), QE_ERR_CAPACITY, "too many rows for one select-project call");
     const size_t sbytes = (size_t)(3 + tiles) * 8;  // ctl[3] | per tile a look-back status word
     void* s;
@@ -188,7 +188,7 @@ extern "C" int qe_select_project(qe_ctx* ctx, const qe_column* cols, int32_t nco
       const int per_cu = std::max(1, std::min(wg_cap, bpc - margin));
       const int64_t grid = persist ? std::min<int64_t>(tiles, (int64_t)ctx->num_cus * per_cu * oversub) : tiles;
       QE_HIP(hipMemsetAsync(s, 0, sbytes, ctx->stream));
-      QE_TRY(jit_launch(ctx, fn, (int)grid, P, 256));
+      QE_TRY(jit_launch(ctx, fn, (int)grid, P, selproj_block()));
       QE_TRY(launch_check("qe_selproj"));
       QE_HIP(hipMemcpyAsync(pin, ctl + 1, 16, hipMemcpyDeviceToHost, ctx->stream));
       QE_TRY(ctx_sync(ctx));
