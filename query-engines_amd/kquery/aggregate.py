@@ -107,8 +107,9 @@ class HashAggregateState:
     def __init__(self, ctx: Context, key_types: Sequence[int], aggs: Sequence[Tuple[int, int]],
                  expected_groups: int = 1024, async_update: bool = False):
         """``async_update``: stream-ordered updates (qe_hashagg_set_async) — an update returns once
-        its kernel is queued and is checked by the next call on the state; the caller keeps the
-        update's input columns alive until then (finalize, num_groups, the next update)."""
+        its kernel is queued and is checked by the next call on the state (finalize, num_groups,
+        the next update), which may re-read the update's columns; the state holds a reference to
+        them until the next update or reset."""
         from .strdict import StringDictionary
 
         self.ctx = ctx
@@ -133,6 +134,8 @@ class HashAggregateState:
                                           int(expected_groups), N.C.byref(h)))
         self.handle = h
         self._out_rows = max(1, 2 * self.expected_groups)  # finalize's first output sizing guess
+        self.async_update = bool(async_update)
+        self._held = None  # async: the last update's columns, alive until the state settles it
         if async_update:
             N.check(N.lib().qe_hashagg_set_async(h, 1))
 
@@ -169,6 +172,8 @@ class HashAggregateState:
             *[(x.as_c() if x is not None else N.QeColumn()) for x in inputs])
         mc = mask.as_c() if mask is not None else None
         N.check(N.lib().qe_hashagg_update(self.handle, kc, ic, N.C.byref(mc) if mc is not None else None))
+        if self.async_update:  # a pending update may re-read its columns when it is settled
+            self._held = (keys, inputs, mask)
 
     def update_fused(self, cols: Sequence[DeviceColumn], spec: N.QeFusedSpec,
                      key_cols: Optional[Sequence[DeviceColumn]] = None) -> None:
@@ -189,6 +194,8 @@ class HashAggregateState:
             cols += codes
         cc = (N.QeColumn * len(cols))(*[c.as_c() for c in cols])
         N.check(N.lib().qe_hashagg_update_fused(self.handle, cc, len(cols), N.C.byref(spec)))
+        if self.async_update:  # a pending update may re-read its columns when it is settled
+            self._held = cols
 
     def set_row_base(self, row_base: int) -> None:
         N.check(N.lib().qe_hashagg_set_row_base(self.handle, int(row_base)))
@@ -209,6 +216,7 @@ class HashAggregateState:
 
     def reset(self) -> None:
         N.check(N.lib().qe_hashagg_reset(self.handle))
+        self._held = None
 
     # ---- results ----------------------------------------------------------------------------------
     def num_groups(self) -> int:
