@@ -185,7 +185,7 @@ class HashAggregateExec(PhysicalPlan):
                     present[0].ctx, [k.type for k in keys],
                     [(a.fn, (i.type if i is not None and a.fn != N.AGG_COUNT_STAR else N.TYPE_INT64))
                      for a, i in zip(self.aggregateExpr, inputs)],
-                    self.expected_groups)
+                    self.expected_groups, async_update=True)
             state.update(keys, inputs)
         self.state = state
         return state
@@ -243,7 +243,9 @@ class FusedHashAggregateExec(PhysicalPlan):
             cols = [batch.field(i) for i in self.slots]
             key_cols = [batch.field(i) for i in self.key_scan] if self.key_scan is not None else None
             if state is None:
-                state = HashAggregateState((cols or key_cols)[0].ctx, self.key_types, self.aggs, self.expected_groups)
+                # stream-ordered updates: the host prepares batch i + 1 while batch i's kernel runs
+                state = HashAggregateState((cols or key_cols)[0].ctx, self.key_types, self.aggs, self.expected_groups,
+                                           async_update=True)
             state.update_fused(cols, self.spec, key_cols)
         self.state = state
         return state
