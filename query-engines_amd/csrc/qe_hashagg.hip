@@ -2063,7 +2063,7 @@ int qe_hashagg_create(qe_ctx* ctx, int32_t nkeys, const int32_t* key_types, int3
   auto bail = [&](int code) {
     for (hipEvent_t e : {h->ev[0], h->ev[1], h->ev_ctl})
       if (e) (void)hipEventDestroy(e);
-    if (h->ctl_pin) (void)hipHostFree(h->ctl_pin);
+    if (h->ctl_pin) pinned_slot_free(h->ctl_pin, h->ctx->stream);
     delete h;
     return code;
   };
@@ -2126,8 +2126,7 @@ int qe_hashagg_create(qe_ctx* ctx, int32_t nkeys, const int32_t* key_types, int3
   if (hipEventCreate(&h->ev[0]) != hipSuccess || hipEventCreate(&h->ev[1]) != hipSuccess ||
       hipEventCreateWithFlags(&h->ev_ctl, hipEventDisableTiming) != hipSuccess)
     return bail(fail(QE_ERR_DEVICE, "hipEventCreate failed"));
-  if (hipHostMalloc((void**)&h->ctl_pin, 64, hipHostMallocDefault) != hipSuccess)
-    return bail(fail(QE_ERR_OOM, "pinned control snapshot allocation failed"));
+  if (pinned_slot_alloc(&h->ctl_pin) != QE_OK) return bail(QE_ERR_OOM);
   if (dev_alloc(ctx, 64, (void**)&h->ctl) != QE_OK) return bail(fail(QE_ERR_OOM, "control allocation failed"));
   if (hipMemsetAsync(h->ctl, 0, 64, ctx->stream) != hipSuccess) return bail(fail(QE_ERR_DEVICE, "memset failed"));
   // LDS table: 2x the expected groups (load factor <= 0.5); a launch may shrink it down to
@@ -2173,10 +2172,7 @@ int qe_hashagg_destroy(qe_hashagg* h) {
     if (h->ev[i]) (void)hipEventDestroy(h->ev[i]);
   }
   if (h->ev_ctl) (void)hipEventDestroy(h->ev_ctl);
-  if (h->ctl_pin) {
-    (void)hipStreamSynchronize(ctx->stream);  // a queued snapshot copy may still target it
-    (void)hipHostFree(h->ctl_pin);
-  }
+  pinned_slot_free(h->ctl_pin, ctx->stream);  // a queued snapshot copy may still target it
   delete h;
   return QE_OK;
 }

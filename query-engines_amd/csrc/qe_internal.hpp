@@ -60,6 +60,8 @@ void dev_forget_stream(qe_ctx* ctx);
 int dev_release(int device);
 int ctx_scratch(qe_ctx* ctx, size_t bytes, void** out);       // grow-only scratch
 int ctx_pinned(qe_ctx* ctx, size_t bytes, void** out);        // grow-only pinned host
+int pinned_slot_alloc(uint64_t** out);                        // 64 pinned bytes (pooled)
+void pinned_slot_free(uint64_t* p, hipStream_t stream);       // reusable once `stream`'s work is done
 // Wait for everything queued on the ctx stream (blocking; polling an event from this thread
 // measured 15 us slower per finalize).
 int ctx_sync(qe_ctx* ctx);

@@ -155,6 +155,59 @@ int dev_release(int device) {
   return QE_OK;
 }
 
+// ---- pinned 64-byte slots (hash-aggregate control snapshots) ------------------------------------------
+// hipHostMalloc costs tens of microseconds (and hipHostFree waits for the device), too much per
+// aggregate state: slots come from 64 KiB pinned chunks that are never released, and a freed slot
+// is reused only once the work queued on its stream before the free has completed.
+namespace {
+struct PinSlot {
+  uint64_t* p;
+  hipEvent_t ev;
+};
+std::mutex g_pmu;
+std::vector<PinSlot> g_pfree;
+std::vector<uint64_t*> g_pnew;  // never-used slots of the current chunk
+}  // namespace
+
+int pinned_slot_alloc(uint64_t** out) {
+  std::lock_guard<std::mutex> lk(g_pmu);
+  for (size_t i = 0; i < g_pfree.size(); ++i) {
+    const hipError_t e = hipEventQuery(g_pfree[i].ev);
+    if (e != hipSuccess) {
+      (void)hipGetLastError();  // hipErrorNotReady must not surface later
+      continue;
+    }
+    *out = g_pfree[i].p;
+    (void)hipEventDestroy(g_pfree[i].ev);
+    g_pfree[i] = g_pfree.back();
+    g_pfree.pop_back();
+    return QE_OK;
+  }
+  if (g_pnew.empty()) {
+    void* chunk = nullptr;
+    QE_HIP(hipHostMalloc(&chunk, 65536, hipHostMallocDefault));
+    for (int i = 1023; i >= 0; --i) g_pnew.push_back((uint64_t*)chunk + 8 * i);
+  }
+  *out = g_pnew.back();
+  g_pnew.pop_back();
+  return QE_OK;
+}
+
+void pinned_slot_free(uint64_t* p, hipStream_t stream) {
+  if (!p) return;
+  hipEvent_t ev = nullptr;
+  if (hipEventCreateWithFlags(&ev, hipEventDisableTiming) != hipSuccess || hipEventRecord(ev, stream) != hipSuccess) {
+    (void)hipGetLastError();
+    (void)hipStreamSynchronize(stream);
+    if (ev) (void)hipEventDestroy(ev);
+    std::lock_guard<std::mutex> lk(g_pmu);
+    g_pnew.push_back(p);
+    return;
+  }
+  std::lock_guard<std::mutex> lk(g_pmu);
+  g_pfree.push_back({p, ev});
+}
+
 static thread_local std::string g_last_error;
 
 int fail(int code, const char* fmt, ...) {
