@@ -1629,13 +1629,27 @@ static size_t lds_layout_at(const qe_hashagg* h, Plan* P, int log2) {
   return off;
 }
 
+// LDS bytes a workgroup's table may take. The generic kernel runs two 512-thread workgroups per
+// CU (80 KiB each). The specialised kernel's 1024-thread workgroups run one per CU, so its table
+// may take nearly all of the CU's 160 KiB: twice the groups in one pass (C4 shape: up to ~2.5K
+// groups in a 4096-slot table instead of ~1.3K in 2048 slots). QE_LDS_BUDGET_KB overrides.
+static size_t lds_budget(const qe_ctx* ctx) {
+  static const size_t env = [] {
+    const char* e = getenv("QE_LDS_BUDGET_KB");
+    return e && *e ? (size_t)std::max(16, std::min(156, atoi(e))) * 1024 : (size_t)0;
+  }();
+  if (env) return env;
+  return (ctx->jit && fused_block(0) == 1024) ? (size_t)152 * 1024 : HA_LDS_BUDGET;
+}
+
 // Largest LDS table in [lds_log2_min, lds_log2] that fits the per-workgroup budget; 0 bytes =>
 // global-only launch (the expected groups do not fit on chip).
 static size_t lds_layout(const qe_hashagg* h, Plan* P) {
   if (h->lds_log2 == 0) return 0;
+  const size_t budget = lds_budget(h->ctx);
   for (int log2 = h->lds_log2; log2 >= h->lds_log2_min; --log2) {
     const size_t b = lds_layout_at(h, P, log2);
-    if (b <= HA_LDS_BUDGET) return b;
+    if (b <= budget) return b;
   }
   P->lds_log2 = 0;
   return 0;
@@ -1846,7 +1860,8 @@ static int launch_pass(qe_hashagg* h, Plan& P, size_t lds, hipFunction_t pfn, in
           const char* e = getenv("QE_FUSED_WG_PER_CU");
           return e && *e ? std::max(1, atoi(e)) : 0;
         }();
-        const int64_t per_state = wg_env ? (int64_t)ctx->num_cus * wg_env : h->grid * 512 / fused_block(P.lds_log2);
+        const int64_t per_state = wg_env ? (int64_t)ctx->num_cus * wg_env
+                                         : std::max<int64_t>(ctx->num_cus, h->grid * 512 / fused_block(P.lds_log2));
         jgrid = (int)std::min<int64_t>(std::min<int64_t>((int64_t)ctx->num_cus * bpc, per_state),
                                        (int64_t)div_up((uint64_t)waves, fused_block(P.lds_log2) / 64));
         if (jgrid < 1) jgrid = 1;
@@ -1969,10 +1984,14 @@ static int run_update(qe_hashagg* h, Plan& P) {
   if (!lds && ctx->jit && h->expected_groups > 0) {
     int tlog2 = 16;
     Plan T = P;
-    while (tlog2 >= 8 && lds_layout_at(h, &T, tlog2) > HA_LDS_BUDGET) --tlog2;
+    while (tlog2 >= 8 && lds_layout_at(h, &T, tlog2) > lds_budget(ctx)) --tlog2;
     const int64_t per_pass = (((int64_t)1 << tlog2) * 5) / 8;
     const int64_t np = tlog2 >= 8 ? (h->expected_groups + per_pass - 1) / per_pass : 0;
-    if (np == 2) {
+    static const int64_t mp_max = [] {  // QE_MP_MAX: most bucket passes before partitioning
+      const char* e = getenv("QE_MP_MAX");
+      return (int64_t)(e && *e ? std::max(2, std::min(8, atoi(e))) : 2);
+    }();
+    if (np >= 2 && np <= mp_max) {
       T.mp_n = (qi32)np;
       T.mp_pass = 0;
       lds_mp = lds_layout_at(h, &T, tlog2);
@@ -2136,8 +2155,9 @@ int qe_hashagg_create(qe_ctx* ctx, int32_t nkeys, const int32_t* key_types, int3
   int log2 = 8, log2_min = 8;
   while (log2 < 16 && ((int64_t)1 << log2) < 2 * eg) ++log2;
   while (log2_min < 16 && ((int64_t)1 << log2_min) < (5 * eg + 3) / 4) ++log2_min;
-  while (log2 > log2_min && lds_bytes_min(h, log2) > HA_LDS_BUDGET) --log2;
-  h->lds_log2 = lds_bytes_min(h, log2) <= HA_LDS_BUDGET ? log2 : 0;
+  const size_t budget = lds_budget(ctx);
+  while (log2 > log2_min && lds_bytes_min(h, log2) > budget) --log2;
+  h->lds_log2 = lds_bytes_min(h, log2) <= budget ? log2 : 0;
   h->lds_log2_min = log2_min;
   // workgroups per CU: as many as the smallest layout of the LDS table allows (max 8)
   const int per_cu = h->lds_log2 ? std::max<int>(1, std::min<int>(8, (int)((160 * 1024) / lds_bytes_min(h, h->lds_log2)))) : 8;

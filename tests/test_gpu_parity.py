@@ -623,18 +623,20 @@ MP_I64 = [N.AGG_SUM, N.AGG_COUNT_STAR, N.AGG_MIN, N.AGG_MAX]
 MP_F64 = [N.AGG_SUM, N.AGG_COUNT, N.AGG_MAX]
 
 
-@pytest.mark.parametrize("vtype,ngroups,expected", [("i64", 2500, 2500), ("i64", 40_000, 2000),
-                                                    ("f64", 1200, 1200), ("f64", 40_000, 1200)])
+@pytest.mark.parametrize("vtype,ngroups,expected", [("i64", 4500, 4500), ("i64", 40_000, 4000),
+                                                    ("f64", 2400, 2400), ("f64", 40_000, 2400)])
 def test_hashagg_multipass(agg_ctx, vtype, ngroups, expected):
-    """Expected groups just beyond one LDS table: 2 passes of the fused kernel, each keeping one
-    bucket of key hashes (also when far more groups turn up than expected: overflow records and
-    deferred rows inside a pass). Nullable keys and inputs, fp64 MAX order across two batches."""
+    """Expected groups just beyond one LDS table (the specialised kernel's table takes up to
+    152 KiB: ~2.5K groups of the i64 shape, ~1.3K of the f64 one): 2 passes of the fused kernel,
+    each keeping one bucket of key hashes (also when far more groups turn up than expected:
+    overflow records and deferred rows inside a pass). Nullable keys and inputs, fp64 MAX order
+    across two batches."""
     rng = np.random.default_rng(ngroups * 3 + expected)
     n = 600_000
     k = rng.integers(0, ngroups, n).astype(np.int64) * 104729 + 11
     kv = rng.random(n) > 0.01
     if vtype == "i64":
-        fns, t = MP_I64, N.TYPE_INT64  # non-nullable: the LDS table then holds 2048 slots
+        fns, t = MP_I64, N.TYPE_INT64  # non-nullable: the LDS table then holds 4096 slots
         x = rng.integers(-2**62, 2**62, n).astype(np.int64)
         xv = None
     else:
@@ -651,10 +653,31 @@ def test_hashagg_multipass(agg_ctx, vtype, ngroups, expected):
     assert_groups_equal(result_dict(keys, aggs), ref, fns)
 
 
+def test_fused_c4_one_pass_large_table(agg_ctx):
+    """2400 groups of the C4 shape: one pass of the specialised kernel over a 4096-slot table
+    (152 KiB LDS budget of its 1024-thread workgroups); the generic kernel (80 KiB) partitions."""
+    from kquery.datasource import C4_COLUMNS, ColumnSpec, generate_column
+
+    n, groups = 1_000_003, 2400
+    kspec = ColumnSpec("k", N.TYPE_INT64, N.GEN_MOD, groups, 0)
+    cols = [generate_column(kspec, n, 0, 42, agg_ctx)] + [generate_column(s, n, 0, 42, agg_ctx) for s in C4_COLUMNS[1:]]
+    st = HashAggregateState(agg_ctx, [N.TYPE_INT64], C4_AGGS, groups)
+    st.update_fused(cols, _c4_spec())
+    if agg_ctx.kernel_mode == "jit":
+        assert st.last_kernel_kind() == (True, ""), st.last_kernel_kind()
+    kk, aa = st.finalize()
+    k, _ = gen.generate(gen.GEN_MOD, groups, 42, 0, 0, n)
+    a, _ = gen.generate(gen.GEN_MOD, 1 << 20, 42, 1, 0, n)
+    b, _ = gen.generate(gen.GEN_MOD, 1 << 20, 42, 2, 0, n)
+    ref = S.group_aggregate([k], [None], [S.arith(S.OP_ADD, a, None, b, None)[0], None, a, b], [None] * 4, C4_FNS,
+                            a > (1 << 19))
+    assert_groups_equal(result_dict(kk, aa), ref, C4_FNS)
+
+
 def test_fused_c4_multipass_vs_oracle(agg_ctx):
     from kquery.datasource import C4_COLUMNS, ColumnSpec, generate_column
 
-    n, groups = 2_000_003, 2400
+    n, groups = 2_000_003, 4000
     kspec = ColumnSpec("k", N.TYPE_INT64, N.GEN_MOD, groups, 0)
     cols = [generate_column(kspec, n, 0, 42, agg_ctx)] + [generate_column(s, n, 0, 42, agg_ctx) for s in C4_COLUMNS[1:]]
     st = HashAggregateState(agg_ctx, [N.TYPE_INT64], C4_AGGS, groups)
