@@ -107,6 +107,9 @@ def main():
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--exchange", action="store_true",
                     help="run the multi-GPU exchange leg even with one rank (tests the N > 1 step on one GPU)")
+    ap.add_argument("--exchange-impl", default="torch", choices=["torch", "native"],
+                    help="torch: all-to-all through torch.distributed (default); native: the C ABI's own "
+                         "RCCL communicator (qe_hashagg_exchange)")
     ap.add_argument("--dist-backend", default="nccl",
                     help="torch.distributed backend (nccl = RCCL over xGMI; gloo only to rehearse N > 1 "
                          "ranks sharing one GPU)")
@@ -135,7 +138,7 @@ def main():
             dist.init_process_group("nccl", device_id=torch.device("cuda", device))
         else:
             dist.init_process_group(args.dist_backend)
-    from kquery.exchange import exchange_partials
+    from kquery.exchange import NativeComm, exchange_partials, exchange_partials_native
 
     ctx = Context.get(device)
     rows = args.rows
@@ -149,6 +152,7 @@ def main():
     partial = HashAggregateState(ctx, [N.TYPE_INT64], aggs, 1024, async_update=True)
     exchange = world > 1 or args.exchange
     owner = HashAggregateState(ctx, [N.TYPE_INT64], aggs, 1024) if exchange else None
+    comm = NativeComm(ctx) if exchange and args.exchange_impl == "native" else None
     spec = c4_spec(N)
     kernel_ms = []
     kinds = []
@@ -160,7 +164,10 @@ def main():
         final = partial
         if exchange:
             owner.reset()
-            exchange_partials(partial, owner)
+            if comm is not None:
+                exchange_partials_native(partial, owner, comm)
+            else:
+                exchange_partials(partial, owner)
             final = owner
         out = final.finalize()
         kernel_ms.append(partial.last_kernel_time())
@@ -232,7 +239,8 @@ def main():
             "groups": 1024,
             "columns": "k, a, b int64 (Arrow, no nulls)",
             "parallelism": f"hash-sharded partial aggregate x{world}" + (
-                (" + RCCL all-to-all" if args.dist_backend == "nccl" else f" + {args.dist_backend} all-to-all (rehearsal)")
+                (" + RCCL send/recv (qe_hashagg_exchange)" if comm is not None else
+                 " + RCCL all-to-all" if args.dist_backend == "nccl" else f" + {args.dist_backend} all-to-all (rehearsal)")
                 if exchange else ""),
         },
         "roofline": {
@@ -266,6 +274,8 @@ def main():
             line["check"]["cpu_port_groups_equal"] = True
     if rank == 0:
         print(json.dumps(line), flush=True)
+    if comm is not None:
+        comm.close()
     if dist.is_initialized():
         dist.destroy_process_group()
 

@@ -67,6 +67,7 @@ extern "C" {
 #define QE_ERR_OOM (-3)
 #define QE_ERR_DEVICE (-4)       /* HIP runtime error */
 #define QE_ERR_CAPACITY (-5)     /* output buffer too small */
+#define QE_ERR_COMM (-6)         /* RCCL communicator / collective failure */
 
 /* ---- types ------------------------------------------------------------------------------ */
 /* Arrow type ids used by this kernel. The reference knows only Float8 (fp64) and Utf8
@@ -389,6 +390,26 @@ int qe_hashagg_import_slots(qe_hashagg* agg, const void* slots, int32_t nslots, 
  * reports the update's errors. The input columns must stay valid until that call returns.
  * qe_hashagg_reset discards a pending update; qe_hashagg_set_async(agg, 0) settles it. */
 int qe_hashagg_set_async(qe_hashagg* agg, int32_t enable);
+
+/* ---- multi-GPU exchange over RCCL without a host framework (JNI) ---------------------------
+ * One qe_comm per GPU (rank), all on the ctx whose stream runs the aggregation. Rank 0 calls
+ * qe_comm_unique_id and the host hands the 128 bytes to every rank (its own transport), then
+ * every rank calls qe_comm_create (collective). RCCL is loaded at run time (librccl.so.1);
+ * QE_ERR_COMM when it is missing or a call fails. */
+#define QE_COMM_ID_BYTES 128
+typedef struct qe_comm qe_comm;
+int qe_comm_unique_id(void* id /* QE_COMM_ID_BYTES */);
+int qe_comm_create(qe_ctx* ctx, int32_t world, int32_t rank, const void* id, qe_comm** out);
+int qe_comm_destroy(qe_comm* comm);
+/* Every rank: move each group of `partial` to the rank that owns its key (hash(key) mod world,
+ * as qe_hashagg_export) and merge what this rank receives into `owner` (K:1309-1325 across GPUs).
+ * Fixed slots of `slot_records` groups per destination (<= 0: the expected groups spread over the
+ * ranks with headroom), one grouped send/recv on the ctx stream, one read-back; if a partition
+ * overflowed its slot on any rank, every rank falls back to counts + records. A stream-ordered
+ * (qe_hashagg_set_async) partial is exported without a host wait. *nrecords (optional) = records
+ * this rank merged. partial, owner and comm must share the ctx. */
+int qe_hashagg_exchange(qe_comm* comm, qe_hashagg* partial, qe_hashagg* owner, int64_t slot_records,
+                        int64_t* nrecords);
 
 /* Offset added to row indices of the next update (for shards of one logical stream). */
 int qe_hashagg_set_row_base(qe_hashagg* agg, int64_t row_base);

@@ -1287,6 +1287,14 @@ struct qe_hashagg {
 
 namespace qe {
 
+int hashagg_expected_groups(const qe_hashagg* h, int64_t* out) {
+  QE_CHECK(h && out, QE_ERR_INVALID_ARG, "null argument");
+  *out = h->expected_groups;
+  return QE_OK;
+}
+
+qe_ctx* hashagg_ctx(const qe_hashagg* h) { return h ? h->ctx : nullptr; }
+
 static AggMeta agg_meta(const qe_hashagg* h) {
   AggMeta m{};
   m.naggs = h->naggs;

@@ -188,6 +188,54 @@ def exchange_partials(partial, owner, group: Optional[dist.ProcessGroup] = None,
     return n
 
 
+class NativeComm:
+    """An RCCL communicator owned by the C library (qe_comm_*): the exchange a JNI host would use,
+    with no torch.distributed collective on the data path. Rank 0's unique id reaches the other
+    ranks through the process group's object broadcast (a JNI host would use its own transport)."""
+
+    def __init__(self, ctx, group: Optional[dist.ProcessGroup] = None):
+        from . import native as N
+
+        world = dist.get_world_size(group) if dist.is_initialized() else 1
+        rank = dist.get_rank(group) if dist.is_initialized() else 0
+        uid = (N.C.c_char * N.COMM_ID_BYTES)()
+        if rank == 0:
+            N.check(N.lib().qe_comm_unique_id(uid))
+        if world > 1:
+            box = [bytes(uid)]
+            dist.broadcast_object_list(box, src=0, group=group)
+            uid = (N.C.c_char * N.COMM_ID_BYTES).from_buffer_copy(box[0])
+        h = N.C.c_void_p()
+        N.check(N.lib().qe_comm_create(ctx.handle, world, rank, uid, N.C.byref(h)))
+        self.handle, self.ctx, self.world, self.rank = h, ctx, world, rank
+
+    def close(self) -> None:
+        from . import native as N
+
+        if getattr(self, "handle", None) is not None:
+            N.lib().qe_comm_destroy(self.handle)
+            self.handle = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def exchange_partials_native(partial, owner, comm: NativeComm, slot_records: int = 0) -> int:
+    """exchange_partials through the C ABI (qe_hashagg_exchange): export slots, one grouped RCCL
+    send/recv on the ctx stream, import with one read-back; same fallback rule. Returns the records
+    this rank merged."""
+    from . import native as N
+
+    partial._check_exportable()
+    owner.prepare_output()  # host work of the owner's finalize, before the import's read-back
+    n = N.C.c_int64()
+    N.check(N.lib().qe_hashagg_exchange(comm.handle, partial.handle, owner.handle, int(slot_records), N.C.byref(n)))
+    return n.value
+
+
 def global_aggregate(col, mask=None, row_base: int = 0, group: Optional[dist.ProcessGroup] = None):
     """SUM/MIN/MAX/COUNT/AVG without GROUP BY over a column whose rows are split across ranks
     (SURVEY §8e "global aggregate: one exchange"): this rank's 128-byte partial

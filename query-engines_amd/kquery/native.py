@@ -24,6 +24,8 @@ QE_ERR_UNSUPPORTED = -2
 QE_ERR_OOM = -3
 QE_ERR_DEVICE = -4
 QE_ERR_CAPACITY = -5
+QE_ERR_COMM = -6
+COMM_ID_BYTES = 128
 
 TYPE_INT64 = 1
 TYPE_FLOAT64 = 2
@@ -79,10 +81,15 @@ class DeviceError(QueryEngineError):
     """QE_ERR_DEVICE / QE_ERR_OOM."""
 
 
+class CommError(QueryEngineError):
+    """QE_ERR_COMM: RCCL missing or a collective failed."""
+
+
 _ERR_CLASS = {
     QE_ERR_UNSUPPORTED: IllegalStateException,
     QE_ERR_INVALID_ARG: IllegalArgumentException,
     QE_ERR_CAPACITY: CapacityError,
+    QE_ERR_COMM: CommError,
 }
 
 
@@ -218,6 +225,10 @@ SIGNATURES = [
     ("qe_hashagg_import", C.c_int, [_P, _P, C.c_int64]),
     ("qe_hashagg_export_slots", C.c_int, [_P, C.c_int32, C.c_int64, _P]),
     ("qe_hashagg_import_slots", C.c_int, [_P, _P, C.c_int32, C.c_int64, _I64P, _I64P]),
+    ("qe_comm_unique_id", C.c_int, [_P]),
+    ("qe_comm_create", C.c_int, [_P, C.c_int32, C.c_int32, _P, C.POINTER(C.c_void_p)]),
+    ("qe_comm_destroy", C.c_int, [_P]),
+    ("qe_hashagg_exchange", C.c_int, [_P, _P, _P, C.c_int64, _I64P]),
     ("qe_hashagg_set_row_base", C.c_int, [_P, C.c_int64]),
     ("qe_hashagg_set_async", C.c_int, [_P, C.c_int32]),
     ("qe_hashagg_last_kernel_time", C.c_int, [_P, C.POINTER(C.c_double), C.POINTER(C.c_int32)]),
