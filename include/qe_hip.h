@@ -377,7 +377,11 @@ int qe_hashagg_import(qe_hashagg* agg, const void* records, int64_t nrecords);
  * every sender's word 1, so all ranks get the same value). If *max_count > slot_records some
  * sender's groups did not fit: NOTHING is imported, and every rank should exchange again with
  * qe_hashagg_export / qe_hashagg_import. *nrecords (optional) = records the slots hold.
- * import_slots synchronises once (to read the headers); export_slots does not. */
+ * export_slots does not synchronise, not even to settle a pending stream-ordered update: if that
+ * update left the table incomplete (deferred rows, overflow), word 1 reports 2^62 so that every
+ * rank takes the variable-size exchange, which settles it. import_slots is one launch (each
+ * workgroup checks the headers itself) and one read-back; it grows the table beforehand from an
+ * upper bound (groups so far + nslots * slot_records). */
 #define QE_SLOT_HEADER 64
 int qe_hashagg_export_slots(qe_hashagg* agg, int32_t nparts, int64_t slot_records, void* dst);
 int qe_hashagg_import_slots(qe_hashagg* agg, const void* slots, int32_t nslots, int64_t slot_records,
