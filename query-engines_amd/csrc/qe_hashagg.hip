@@ -1718,7 +1718,8 @@ static int partition_rows(qe_hashagg* h, Plan& P, hipFunction_t* fn, int* grid) 
   qe_ctx* ctx = h->ctx;
   // aggregation-pass LDS table: the largest that fits the per-workgroup budget
   int tlog2 = 16;
-  while (tlog2 >= 8 && lds_layout_at(h, &P, tlog2) > HA_LDS_BUDGET) --tlog2;
+  const size_t pbudget = pagg_block() == 1024 ? (size_t)152 * 1024 : HA_LDS_BUDGET;
+  while (tlog2 >= 8 && lds_layout_at(h, &P, tlog2) > pbudget) --tlog2;
   QE_CHECK(tlog2 >= 8, QE_ERR_UNSUPPORTED, "aggregate state too wide for a partitioned LDS table");
   // buckets: about a quarter of the table's slots in groups per bucket (a slice spans <= 2 buckets)
   int log2p = 1;
@@ -1734,7 +1735,7 @@ static int partition_rows(qe_hashagg* h, Plan& P, hipFunction_t* fn, int* grid) 
   int bpc = 0;
   QE_TRY(jit_kernel(ctx, sc, &fc, &bpc, "qe_pcount"));
   QE_TRY(jit_kernel(ctx, ss, &fs, &bpc, "qe_pscatter", staged ? pscatter_block() : 512));
-  QE_TRY(jit_kernel(ctx, sa, fn, &bpc, "qe_pagg"));
+  QE_TRY(jit_kernel(ctx, sa, fn, &bpc, "qe_pagg", pagg_block()));
   const int64_t n = P.n;
   // count / scatter workgroups per CU (QE_PART_WG_PER_CU overrides; see pscatter_block)
   static const int wg_per_cu = [] {
@@ -1886,7 +1887,7 @@ static int launch_pass(qe_hashagg* h, Plan& P, size_t lds, hipFunction_t pfn, in
   }
   if (pass > 0 || mp > 0) QE_HIP(hipEventRecord(h->ev[0], ctx->stream));
   if (jfn) {
-    QE_TRY(jit_launch(ctx, jfn, jgrid, P, pfn ? 512 : fused_block(P.lds_log2)));
+    QE_TRY(jit_launch(ctx, jfn, jgrid, P, pfn ? pagg_block() : fused_block(P.lds_log2)));
   } else {
     QE_TRY(launch_hashagg(P, grid, lds, ctx->stream));
   }

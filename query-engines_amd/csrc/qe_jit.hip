@@ -630,6 +630,18 @@ int pscatter_block() {
   return b;
 }
 
+// Workgroup size of the partition-aggregate pass (QE_PAGG_BLOCK = 512 / 1024, default 1024). 1024
+// threads run one workgroup per CU with up to 152 KiB of LDS table, so the radix pass needs half the
+// buckets of 512-thread tables (76 KiB). 1B rows, C4 shape, interleaved A/B (512 -> 1024, ms):
+// 65536 groups 14.52 -> 13.93, 262144 18.32 -> 16.50, 1048576 20.4 -> 20.4, 4194304 24.5 -> 22.0.
+int pagg_block() {
+  static const int b = [] {
+    const char* e = getenv("QE_PAGG_BLOCK");
+    return e && *e && atoi(e) == 512 ? 512 : 1024;
+  }();
+  return b;
+}
+
 // Tiles of column loads in flight ahead of the one being sorted (QE_PSCATTER_DEPTH, 1..4).
 int pscatter_depth() {
   static const int d = [] {
@@ -770,7 +782,7 @@ bool gen_pagg_source(const Plan& P, int log2, std::string* src, size_t* lds_byte
   }
   std::ostringstream o;
   o << "\nusing namespace qe;\n"
-    << "extern \"C\" __global__ void __launch_bounds__(512) qe_pagg(const Plan P) {\n"
+    << "extern \"C\" __global__ void __launch_bounds__(" << pagg_block() << ") qe_pagg(const Plan P) {\n"
     << "  if ((qi64)blockIdx.x >= P.part_slice[0]) return;\n"
     << "  const qi64 lo = P.part_slice[2 + 2 * (qi64)blockIdx.x];\n"
     << "  const qi64 hx = P.part_slice[3 + 2 * (qi64)blockIdx.x];\n"
