@@ -88,6 +88,8 @@ bool gen_part_source(const qe::Plan& P, int log2p, bool scatter, std::string* sr
 bool gen_pagg_source(const qe::Plan& P, int log2, std::string* src, size_t* lds_bytes);
 bool part_staged_ok(const qe::Plan& P, int log2p);
 int pscatter_block();
+bool pscatter_wide();
+int pscatter_block_for(int log2p);
 int pagg_block();
 bool fused_prefetch();
 int fused_block(int lds_log2);

@@ -615,8 +615,22 @@ bool gen_part_source(const Plan& P, int log2p, bool scatter, std::string* src) {
 // (bucket, workgroup) ranges as the direct scatter: the records of one bucket and workgroup keep
 // a contiguous range of its bucket (their order inside it may differ run to run).
 bool part_staged_ok(const Plan& P, int log2p) {
+  if (log2p == 10) return pscatter_wide() && part_layout(P).words <= 3;
   return log2p <= 9 && part_layout(P).words * pscatter_block() <= 8 * 256;
 }
+
+// QE_PSCATTER_WIDE=1: 1024 buckets staged by 1024-thread workgroups (4096-row tiles, records of
+// <= 3 words: 96 KiB of LDS records + 16 KiB of bucket cursors), one per CU. Off: 1B rows, 1M
+// groups (1024 buckets) took 22.6 ms staged this way against 19.3 ms with the direct scatter.
+bool pscatter_wide() {
+  static const bool w = [] {
+    const char* e = getenv("QE_PSCATTER_WIDE");
+    return e && *e && atoi(e) == 1;
+  }();
+  return w;
+}
+
+int pscatter_block_for(int log2p) { return log2p == 10 ? 1024 : pscatter_block(); }
 
 // Workgroup size of the staged scatter (tile = 4 rows per thread); QE_PSCATTER_BLOCK overrides.
 // Measured at 200M rows, 64K / 256K groups (count + scatter + aggregate): 128 threads 4.05 /
@@ -661,8 +675,8 @@ bool gen_pscatter_staged_source(const Plan& P, int log2p, std::string* src) {
   const char* chunk = G == 2 ? "qi64x2" : "qi64";
   std::ostringstream o;
   o << "\nusing namespace qe;\n"
-    << "extern \"C\" __global__ void __launch_bounds__(" << pscatter_block() << ") qe_pscatter(const Plan P) {\n"
-    << "  constexpr int LOG2P = " << log2p << ", NP = 1 << LOG2P, W = " << W << ", T = " << 4 * pscatter_block() << ";\n"
+    << "extern \"C\" __global__ void __launch_bounds__(" << pscatter_block_for(log2p) << ") qe_pscatter(const Plan P) {\n"
+    << "  constexpr int LOG2P = " << log2p << ", NP = 1 << LOG2P, W = " << W << ", T = " << 4 * pscatter_block_for(log2p) << ";\n"
     << "  __shared__ qu32 s_hist[NP];\n  __shared__ qu32 s_off[NP];\n  __shared__ qu64 s_cur[NP];\n"
     << "  constexpr int WC = " << W / G << ";  // " << chunk << " chunks per record\n"
     << "  __shared__ " << chunk << " s_rec[T * WC];\n  __shared__ unsigned short s_bkt[T];\n  __shared__ qu32 s_total;\n"
