@@ -113,8 +113,9 @@ int compile_program(const qe_column* cols, int32_t ncols, const bool* col_f64, c
 // Select-project kernel source (qe_jit.hip): R rows per thread, selproj_block() threads.
 // Select-project tile order / pass: SP_COUNTER (tile ids from a device counter, look-back),
 // SP_PERSIST (persistent grid, look-back), SP_COUNT (two-pass, first pass: selected rows per tile
-// into t.keys), SP_WRITE (two-pass, second pass: each tile's base = sum of the earlier tiles' counts).
-enum { SP_COUNTER = 0, SP_PERSIST = 1, SP_COUNT = 2, SP_WRITE = 3 };
+// into t.keys), SP_WRITE (two-pass, second pass: each tile's base = sum of the earlier tiles' counts),
+// SP_WRITE_SCAN (second pass after a device scan of the counts: each tile's base = t.keys[tile]).
+enum { SP_COUNTER = 0, SP_PERSIST = 1, SP_COUNT = 2, SP_WRITE = 3, SP_WRITE_SCAN = 4 };
 bool gen_selproj_source(const qe::Plan& P, const int32_t* out_kind, int nout, std::string* src, int mode);
 int selproj_block();                                  // select-project workgroup size
 int selproj_rows_per_thread(const qe::Plan& P);

@@ -1018,10 +1018,10 @@ bool emit_selproj_write(const Plan& P, const int32_t* out_kind, int nout, int mo
     << "#pragma unroll\n    for (int d = 1; d < 64; d <<= 1) { const qu32 y = __shfl_up(inc, d); if (lane >= d) inc += y; }\n"
     << "    const qu64 total = (qu64)__shfl(inc, 63);\n"
     << "    if (lane < R * W) s_cnt[lane] = inc - x;\n"
-    << (mode == SP_WRITE ? "    if (lane == 0) s_total = (qu32)total;\n"
+    << (mode == SP_WRITE || mode == SP_WRITE_SCAN ? "    if (lane == 0) s_total = (qu32)total;\n"
                          : "    if (lane == 0) { s_total = (qu32)total; __hip_atomic_store(&st[tile], (tile == 0 ? F_INC : F_AGG) | total, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }\n")
     << "  }\n";
-  const std::string lookback = mode == SP_WRITE ?
+  const std::string lookback = mode == SP_WRITE || mode == SP_WRITE_SCAN ?
       "    const qu64 total = s_total;\n"
       "    if (lane == 0) {\n      qu64 excl = 0;\n      for (int q = 0; q < W; ++q) excl += s_pre[q];\n      s_base = excl;\n"
       "      if ((qu64)tile == P.t.cap - 1) P.t.ctl[1] = excl + total;\n    }\n" :
@@ -1161,6 +1161,9 @@ bool gen_selproj_source(const Plan& P, const int32_t* out_kind, int nout, std::s
         << "  for (qi64 i = t; i < (qi64)tile; i += BT) pre += ((const qu64*)P.t.keys)[i];\n"
         << "#pragma unroll\n  for (int d = 32; d >= 1; d >>= 1) pre += __shfl_xor(pre, d);\n"
         << "  __shared__ qu64 s_pre[W];\n  if (lane == 0) s_pre[w] = pre;\n";
+    else if (mode == SP_WRITE_SCAN)  // base from the scanned counts
+      o << "  __shared__ qu64 s_pre[W];\n"
+        << "  if (lane == 0) s_pre[w] = w == 0 ? ((const qu64*)P.t.keys)[tile] : 0ull;\n";
   }
   emit_selproj_act(P, o);
   if (mode == SP_COUNT) {

@@ -125,7 +125,7 @@ extern "C" int qe_select_project(qe_ctx* ctx, const qe_column* cols, int32_t nco
   // predicate's columns fit the MALL, so the second pass reads them from there: no look-back
   // round trips. QE_SELPROJ_TWOPASS=0/1 forces either way.
   const char* tpe = getenv("QE_SELPROJ_TWOPASS");  // read per call: tests switch it
-  const int twopass_env = tpe && *tpe ? (tpe[0] == '1' ? 1 : 0) : -1;
+  const int twopass_env = tpe && *tpe ? (tpe[0] == '1' ? 1 : tpe[0] == '2' ? 2 : 0) : -1;
   unsigned pred_cols = P.mask_col >= 0 ? 1u << P.mask_col : 0u;
   for (int t = 0; t < P.nterms; ++t)
     pred_cols |= (1u << P.terms[t].lhs) | (P.terms[t].rhs >= 0 ? 1u << P.terms[t].rhs : 0u);
@@ -136,7 +136,38 @@ extern "C" int qe_select_project(qe_ctx* ctx, const qe_column* cols, int32_t nco
   // plan with no predicate reads nothing in the count pass but still pays the prefix sums)
   const int64_t tiles_est = (int64_t)div_up((uint64_t)n, (uint64_t)selproj_rows_per_thread(P) * selproj_block());
   const bool twopass = twopass_env >= 0 ? twopass_env == 1 : (pred_bytes <= (96ull << 20) && tiles_est <= 4096);
-  if (n > 0 && twopass) {
+  // Scanned two passes (QE_SELPROJ_TWOPASS=2): count pass, a device scan of the tile counts, then
+  // the write pass reads its tile's base — no look-back chain and no per-tile prefix sums, at the
+  // price of reading the predicate's columns twice.
+  const bool scanned = twopass_env == 2;
+  if (n > 0 && scanned) {
+    const int R = selproj_rows_per_thread(P);
+    const int64_t tiles = (int64_t)div_up((uint64_t)n, (uint64_t)R * selproj_block());
+    QE_CHECK(tiles < (1ll << 31), QE_ERR_CAPACITY, "too many rows for one select-project call");
+    void* s;
+    QE_TRY(ctx_scratch(ctx, (size_t)(2 * tiles + 4) * 8, &s));
+    qu64* ctl = (qu64*)s;
+    qu64* cnt = ctl + 3;
+    qu64* offs = cnt + tiles;  // tiles + 1 words
+    P.t.ctl = ctl;
+    P.t.cap = (qu64)tiles;
+    void* pin;
+    QE_TRY(ctx_pinned(ctx, 16, &pin));
+    hipFunction_t fn;
+    int bpc = 0;
+    P.t.keys = (qi64*)cnt;
+    QE_TRY(selproj_kernel(ctx, P, out_kind, spec->nout, SP_COUNT, &fn, &bpc));
+    QE_TRY(jit_launch(ctx, fn, (int)tiles, P, selproj_block()));
+    QE_TRY(launch_check("qe_selproj (count)"));
+    QE_TRY(exclusive_scan_i64(ctx, (const int64_t*)cnt, (int64_t*)offs, tiles));
+    P.t.keys = (qi64*)offs;
+    QE_TRY(selproj_kernel(ctx, P, out_kind, spec->nout, SP_WRITE_SCAN, &fn, &bpc));
+    QE_TRY(jit_launch(ctx, fn, (int)tiles, P, selproj_block()));
+    QE_TRY(launch_check("qe_selproj (write)"));
+    QE_HIP(hipMemcpyAsync(pin, offs + tiles, 8, hipMemcpyDeviceToHost, ctx->stream));
+    QE_TRY(ctx_sync(ctx));
+    *out_count = ((int64_t*)pin)[0];
+  } else if (n > 0 && twopass) {
     const int R = selproj_rows_per_thread(P);
     const int64_t tiles = (int64_t)div_up((uint64_t)n, (uint64_t)R * selproj_block());
     QE_CHECK(tiles < (1ll << 31), QE_ERR_CAPACITY, "too many rows for one select-project call");

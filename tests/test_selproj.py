@@ -43,11 +43,12 @@ def _run(ctx, cols, spec, out_types):
     return cnt.value, outs
 
 
-@pytest.fixture(params=["twopass", "lookback"])
+@pytest.fixture(params=["twopass", "lookback", "scanned"])
 def selproj_path(request, monkeypatch):
-    """Both tile-base schemes: two passes (count, then write; the default while the predicate's
-    columns fit the MALL) and the single pass with a decoupled look-back."""
-    monkeypatch.setenv("QE_SELPROJ_TWOPASS", "1" if request.param == "twopass" else "0")
+    """Every tile-base scheme: two passes (count, then write; the default while the predicate's
+    columns fit the MALL), the single pass with a decoupled look-back, and two passes with a device
+    scan of the tile counts between them."""
+    monkeypatch.setenv("QE_SELPROJ_TWOPASS", {"twopass": "1", "lookback": "0", "scanned": "2"}[request.param])
     return request.param
 
 
