@@ -677,10 +677,12 @@ bool gen_pscatter_staged_source(const Plan& P, int log2p, std::string* src) {
   o << "\nusing namespace qe;\n"
     << "extern \"C\" __global__ void __launch_bounds__(" << pscatter_block_for(log2p) << ") qe_pscatter(const Plan P) {\n"
     << "  constexpr int LOG2P = " << log2p << ", NP = 1 << LOG2P, W = " << W << ", T = " << 4 * pscatter_block_for(log2p) << ";\n"
-    << "  __shared__ qu32 s_hist[NP];\n  __shared__ qu32 s_off[NP];\n  __shared__ qu64 s_cur[NP];\n"
+    << "  __shared__ qu32 s_hist[NP];\n  __shared__ qu32 s_off[NP];\n  __shared__ qu64 s_cur[NP];\n  __shared__ qu64 s_dst[NP];\n"
     << "  constexpr int WC = " << W / G << ";  // " << chunk << " chunks per record\n"
     << "  __shared__ " << chunk << " s_rec[T * WC];\n  __shared__ unsigned short s_bkt[T];\n  __shared__ qu32 s_total;\n"
-    << "  for (int b = threadIdx.x; b < NP; b += blockDim.x) s_cur[b] = (qu64)P.part_off[(qi64)b * gridDim.x + blockIdx.x];\n"
+    << "  for (int b = threadIdx.x; b < NP; b += blockDim.x) {\n"
+    << "    s_cur[b] = (qu64)P.part_off[(qi64)b * gridDim.x + blockIdx.x];\n    s_hist[b] = 0;\n  }\n"
+    << "  __syncthreads();\n"
     << "  const int lane = threadIdx.x & 63;\n"
     << "  const qi64 lo = (qi64)blockIdx.x * P.part_tw;\n"
     << "  const qi64 hi = lo + P.part_tw < P.n ? lo + P.part_tw : P.n;\n"
@@ -713,8 +715,11 @@ bool gen_pscatter_staged_source(const Plan& P, int log2p, std::string* src) {
   for (int d = 0; d < D; ++d) load_into("lo + " + std::to_string(d) + " * (qi64)T + woff", d, "  ");
   o << "  for (qi64 t0 = lo; t0 < hi; t0 += " << D << " * (qi64)T) {\n";
   for (int k = 0; k < D; ++k) {
+    // Three barriers per tile: (A) the tile histogram is complete (and the previous tile's
+    // write-out has finished with s_dst / s_rec); (B) wave 0 has scanned it into s_off, the tile's
+    // per-bucket destination bases s_dst, and advanced s_cur; (C) the records sit sorted in LDS
+    // and s_hist is cleared for the next tile. The write-out then runs without a barrier behind it.
     o << "  {\n    const qi64 tile = t0 + " << k << " * (qi64)T;\n    if (tile >= hi) break;\n"
-      << "    for (int b = threadIdx.x; b < NP; b += blockDim.x) s_hist[b] = 0;\n"
       << "    qu32 ract = 0, bk[4], rk[4];\n    qi64 rw[4][W];\n"
       << "    const qi64 base = tile + woff;\n";
     for (int c = 0; c < P.ncols; ++c) {
@@ -722,8 +727,7 @@ bool gen_pscatter_staged_source(const Plan& P, int log2p, std::string* src) {
       o << "    qi64 (&c" << cs << ")[4] = " << buf(k, cs) << ";\n";
       if (P.cols[c].valid) o << "    const qu32 v" << cs << " = v" << buf(k, cs) << ";\n";
     }
-    o << "    __syncthreads();\n"
-      << "    if (base < hi) do {\n"
+    o << "    if (base < hi) do {\n"
       << "    const bool full = base + 256 <= P.n;\n"
       << "    const qi64 r0 = base + 2 * lane;\n";
     emit_active_rows(P, o, false);
@@ -745,10 +749,14 @@ bool gen_pscatter_staged_source(const Plan& P, int log2p, std::string* src) {
       << "      qu32 x = s;\n"
       << "#pragma unroll\n      for (int d = 1; d < 64; d <<= 1) { const qu32 y = __shfl_up(x, d); if (lane >= d) x += y; }\n"
       << "      qu32 e = x - s;\n"
-      << "#pragma unroll\n      for (int i = 0; i < PER; ++i) { const int b = lane * PER + i; if (b < NP) s_off[b] = e; e += loc[i]; }\n"
+      << "#pragma unroll\n      for (int i = 0; i < PER; ++i) {\n"
+      << "        const int b = lane * PER + i;\n"
+      << "        if (b < NP) { s_off[b] = e; const qu64 c = s_cur[b]; s_dst[b] = c - e; s_cur[b] = c + loc[i]; }\n"
+      << "        e += loc[i];\n      }\n"
       << "      if (lane == 63) s_total = x;\n"
       << "    }\n"
       << "    __syncthreads();\n"
+      << "    for (int b = threadIdx.x; b < NP; b += blockDim.x) s_hist[b] = 0;\n"
       << "#pragma unroll\n    for (int r = 0; r < 4; ++r) {\n"
       << "      if (!((ract >> r) & 1)) continue;\n"
       << "      const qu32 pos = s_off[bk[r]] + rk[r];\n"
@@ -760,13 +768,9 @@ bool gen_pscatter_staged_source(const Plan& P, int log2p, std::string* src) {
       << "    const qu32 tot = s_total;\n"
       << "    for (qu32 c = threadIdx.x; c < tot * WC; c += blockDim.x) {\n"
       << "      const qu32 j = c / WC, q = c % WC;\n"
-      << "      const qu32 b = s_bkt[j];\n"
-      << "      const qu64 dst = s_cur[b] + (j - s_off[b]);\n"
+      << "      const qu64 dst = s_dst[s_bkt[j]] + j;\n"
       << "      ((" << chunk << "*)(P.part_rec + dst * " << 8 * W << "ull))[q] = s_rec[c];\n"
       << "    }\n"
-      << "    __syncthreads();\n"
-      << "    for (int b = threadIdx.x; b < NP; b += blockDim.x) s_cur[b] += s_hist[b];\n"
-      << "    __syncthreads();\n"
       << "  }\n";
   }
   o << "  }\n}\n";

@@ -263,7 +263,8 @@ def load_library(path: os.PathLike | str | None = None) -> C.CDLL:
     global _lib
     if _lib is not None and path is None:
         return _lib
-    p = pathlib.Path(path) if path else LIB_PATH
+    # QE_LIB: another build of the library (experiments: A/B of two builds on one box)
+    p = pathlib.Path(path) if path else pathlib.Path(os.environ.get("QE_LIB") or LIB_PATH)
     if not p.exists():
         raise ImportError(
             f"libqe_hip.so not found at {p}: build it with `python -c 'import __graft_entry__ as g; g.build()'` "
