@@ -1,7 +1,13 @@
 #!/bin/bash
-# Kernel trace of tools/bench_groups.py (partitioned GROUP BY kernels), on the GPU box.
+# PMC passes over the partitioned GROUP BY kernels (bench_groups.py ROWS G), one run per pass.
+#   bash tools/prof_groups.sh OUTDIR ROWS G
 set -o pipefail
 export TMPDIR=/tmp
-OUT=${GRAFT_REPO_ROOT:-$PWD}/gpurun_out/pgrp
-rm -rf $OUT && mkdir -p $OUT
-timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/trace -o run -- python3 tools/bench_groups.py ${ROWS:-200000000} ${GROUPS_LIST:-65536 262144 1048576} > $OUT/log 2>&1
+OUT=$1; ROWS=$2; G=$3
+mkdir -p "$OUT"
+B="python3 tools/bench_groups.py $ROWS $G"
+timeout -k 10 200 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/trace -o run -- $B > $OUT/trace.log 2>&1 || exit 1
+timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $OUT/fetch -o run -- $B > $OUT/fetch.log 2>&1 || exit 1
+timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $OUT/write -o run -- $B > $OUT/write.log 2>&1 || exit 1
+timeout -s KILL 120 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_SALU SQ_WAIT_INST_LDS --output-format csv -d $OUT/sq -o run -- $B > $OUT/sq.log 2>&1 || exit 1
+timeout -s KILL 120 rocprofv3 --pmc SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE GRBM_GUI_ACTIVE --output-format csv -d $OUT/lds -o run -- $B > $OUT/lds.log 2>&1 || exit 1
