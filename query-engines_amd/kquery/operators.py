@@ -282,7 +282,7 @@ class FusedSelectProjectExec(PhysicalPlan):
         cols = [batch.field(i) for i in self.slots]
         ctx = cols[0].ctx
         n = cols[0].length
-        outs = [DeviceColumn.empty(t, n, True, ctx=ctx) for t in self.out_types]
+        outs = [DeviceColumn.empty(t, n, self._may_be_null(k, cols), ctx=ctx) for k, t in enumerate(self.out_types)]
         cc = (N.QeColumn * len(cols))(*[c.as_c() for c in cols])
         oc = (N.QeColumn * len(outs))(*[o.as_c() for o in outs])
         cnt = N.C.c_int64()
@@ -293,6 +293,20 @@ class FusedSelectProjectExec(PhysicalPlan):
         for o in outs:
             o.length = cnt.value
         return RecordBatch(self._schema, outs)
+
+    def _may_be_null(self, k: int, cols: Sequence[DeviceColumn]) -> bool:
+        """Whether output k can hold a null, as compile_program decides it (qe_hashagg.hip): a
+        referenced column with a validity bitmap, a null literal, or a division (int64 x / 0 ->
+        null). Only such outputs get a validity bitmap: allocating and filling one for the C2
+        output cost ~10 us of a ~73 us operator call (tools/selproj_op_overhead.py)."""
+        pg = self.spec.outputs[k]
+        for i in range(pg.ntokens):
+            tk = pg.tokens[i]
+            if tk.op == N.TOK_COL and cols[tk.arg].validity is not None:
+                return True
+            if (tk.op == N.TOK_LIT and tk.lit.is_null) or tk.op == N.TOK_DIV:
+                return True
+        return False
 
     def execute(self) -> Iterator[RecordBatch]:
         for batch in self.scan.execute():
