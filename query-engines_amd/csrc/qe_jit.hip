@@ -838,29 +838,55 @@ bool gen_pagg_source(const Plan& P, int log2, std::string* src, size_t* lds_byte
   for (int q = 1; q < L.words; ++q) o << "  qi64 nw" << q << "[4];\n";
   const char* pfe = getenv("QE_PAGG_PREFETCH");
   const bool pf = !(pfe && pfe[0] == '0');
-  if (pf) load_step("n", "lo + (qi64)(threadIdx.x >> 6) * 256");
-  o << "  for (qi64 base = lo + (qi64)(threadIdx.x >> 6) * 256; base < hi; base += step) {\n";
-  if (!pf) load_step("n", "base");
-  o << "    const qu32 act = nact;\n    qu32 knull = 0;\n"
-    << "    qi64 key[4] = {nkey[0], nkey[1], nkey[2], nkey[3]};\n";
-  for (int q = 1; q < L.words; ++q)
-    o << "    qi64 w" << q << "[4] = {nw" << q << "[0], nw" << q << "[1], nw" << q << "[2], nw" << q << "[3]};\n";
-  if (pf) load_step("n", "base + step");
-  if (L.flags_word >= 0)
-    o << "#pragma unroll\n    for (int r = 0; r < 4; ++r) knull |= (qu32)(w" << L.flags_word << "[r] & 1) << r;\n";
-  for (int c = 0; c < P.ncols; ++c) {
-    if (L.col_word[c] < 0) continue;
-    const std::string cs = std::to_string(c);
-    o << "    qi64 (&c" << cs << ")[4] = w" << L.col_word[c] << ";\n";
-    if (P.cols[c].valid)
-      o << "    qu32 v" << cs << " = 0;\n"
-        << "#pragma unroll\n    for (int r = 0; r < 4; ++r) v" << cs << " |= ((qu32)(w" << L.flags_word << "[r] >> "
-        << (1 + c) << ") & 1u) << r;\n";
+  // QE_PAGG_DEPTH = 2: two record buffers (n*, m*) in rotation, the loop unrolled twice, so each
+  // buffer is reloaded two steps ahead (copying one buffer into the other would wait on its loads)
+  const char* pde = getenv("QE_PAGG_DEPTH");
+  const int depth = pf && pde && pde[0] == '2' ? 2 : 1;
+  if (depth == 2) {
+    o << "  qu32 mact;\n  qi64 mkey[4];\n";
+    for (int q = 1; q < L.words; ++q) o << "  qi64 mw" << q << "[4];\n";
   }
-  o << "    if (act == 0) continue;\n";
-  emit_agg_rows(P, o, val, ok, L.row_word >= 0 ? "w" + std::to_string(L.row_word) + "[r]" : "0",
-                "base + lane + 64 * r");
-  o << "  }\n";
+  // one step over the records of buffer `pre` at row `b`, reloading that buffer with row `nb`
+  auto body = [&](const std::string& pre, const std::string& b, const std::string& nb) {
+    o << "    {\n    const qi64 sbase = " << b << ";\n"
+      << "    const qu32 act = " << pre << "act;\n    qu32 knull = 0;\n"
+      << "    qi64 key[4] = {" << pre << "key[0], " << pre << "key[1], " << pre << "key[2], " << pre << "key[3]};\n";
+    for (int q = 1; q < L.words; ++q)
+      o << "    qi64 w" << q << "[4] = {" << pre << "w" << q << "[0], " << pre << "w" << q << "[1], " << pre << "w" << q
+        << "[2], " << pre << "w" << q << "[3]};\n";
+    if (!nb.empty()) load_step(pre, nb);
+    if (L.flags_word >= 0)
+      o << "#pragma unroll\n    for (int r = 0; r < 4; ++r) knull |= (qu32)(w" << L.flags_word << "[r] & 1) << r;\n";
+    for (int c = 0; c < P.ncols; ++c) {
+      if (L.col_word[c] < 0) continue;
+      const std::string cs = std::to_string(c);
+      o << "    qi64 (&c" << cs << ")[4] = w" << L.col_word[c] << ";\n";
+      if (P.cols[c].valid)
+        o << "    qu32 v" << cs << " = 0;\n"
+          << "#pragma unroll\n    for (int r = 0; r < 4; ++r) v" << cs << " |= ((qu32)(w" << L.flags_word << "[r] >> "
+          << (1 + c) << ") & 1u) << r;\n";
+    }
+    o << "    if (act != 0) {\n";
+    emit_agg_rows(P, o, val, ok, L.row_word >= 0 ? "w" + std::to_string(L.row_word) + "[r]" : "0",
+                  "sbase + lane + 64 * r");
+    o << "    }\n    }\n";
+  };
+  const std::string first = "lo + (qi64)(threadIdx.x >> 6) * 256";
+  if (depth == 2) {
+    load_step("n", first);
+    load_step("m", first + " + step");
+    o << "  for (qi64 base = " << first << "; base < hi; base += 2 * step) {\n";
+    body("n", "base", "base + 2 * step");
+    o << "    if (base + step >= hi) break;\n";
+    body("m", "base + step", "base + 3 * step");
+    o << "  }\n";
+  } else {
+    if (pf) load_step("n", first);
+    o << "  for (qi64 base = " << first << "; base < hi; base += step) {\n";
+    if (!pf) load_step("n", "base");
+    body("n", "base", pf ? "base + step" : "");
+    o << "  }\n";
+  }
   emit_flush(P, o, true, true);
   // groups that found no room anywhere: defer their records (the LDS table is final, so a key is
   // in it exactly when its records were aggregated there rather than on the global path)
