@@ -40,7 +40,7 @@ static int emit(const char* dir, const char* name, const qe_column* cols, int nc
     }
     out_kind[k] = (is_f ? 8 : 8) | (nullable ? 0x100 : 0);
   }
-  const int modes[] = {SP_COUNTER, SP_PERSIST, SP_COUNT, SP_WRITE};
+  const int modes[] = {SP_COUNTER, SP_PERSIST, SP_COUNT, SP_WRITE, SP_WRITE_SCAN};
   for (int m : modes) {
     std::string src;
     if (!gen_selproj_source(P, out_kind, nout, &src, m)) {

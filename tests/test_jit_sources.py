@@ -29,10 +29,11 @@ def sources(tmp_path_factory):
 
 def test_all_modes_emitted(sources):
     names = sorted(p.name for p in sources)
-    assert names == sorted(f"{s}_m{m}.hip" for s in ("c2", "nullable") for m in range(4))
+    assert names == sorted(f"{s}_m{m}.hip" for s in ("c2", "nullable") for m in range(5))
 
 
-@pytest.mark.parametrize("name", ["c2_m0", "c2_m1", "c2_m2", "c2_m3", "nullable_m1", "nullable_m3"])
+@pytest.mark.parametrize("name", ["c2_m0", "c2_m1", "c2_m2", "c2_m3", "c2_m4", "nullable_m1", "nullable_m3",
+                                  "nullable_m4"])
 def test_compiles_for_gfx950(sources, name, tmp_path):
     src = next(p for p in sources if p.stem == name)
     r = subprocess.run([HIPCC, "--offload-arch=gfx950", "-O3", "-std=c++17", "-ffp-contract=off",
