@@ -43,6 +43,7 @@ typedef int qi32x2 __attribute__((ext_vector_type(2)));
 
 constexpr qi64 EMPTY_KEY = (qi64)0x8000000000000000ull;  // LDS/global slot sentinel (INT64_MIN)
 constexpr qi64 PART_EXCL = 1ll << 62;  // partition-aggregate slice flag: the slice holds its whole bucket
+constexpr qi64 PART_CH = 2048;          // records per chunk of the chunked scatter (>= its 2048-row tiles)
 constexpr qu64 NULL_SALT = 0x6A09E667F3BCC909ull;
 constexpr int HA_LDS_MAXP = 32;      // probe limit in the LDS table
 constexpr int HA_GLOBAL_MAXP = 256;  // probe limit in the global table
@@ -124,6 +125,11 @@ struct Plan {
   qi64* part_off;  // count: per (bucket, workgroup) record counts; scatter: their exclusive scan
   qi64 part_tw;    // rows per workgroup (count / scatter)
   qi64* part_slice;  // partition aggregate: [0] slice count, then (lo, hi | PART_EXCL) per slice
+  // chunked scatter (no count pass): part_chunk[0] = chunks claimed, part_chunk[1 + c] =
+  // (bucket << 32) | records in chunk c (PART_CH record slots each); part_sorted: chunk ids
+  // grouped by bucket; slices are then (first, end | PART_EXCL) ranges of part_sorted
+  qi64* part_chunk;
+  qi32* part_sorted;
   // multi-pass fused aggregate (groups just beyond one LDS table): pass mp_pass of mp_n keeps the
   // rows whose key hash falls in bucket mp_pass (mp_n = 0: every row)
   qi32 mp_n, mp_pass;

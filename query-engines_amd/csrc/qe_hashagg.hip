@@ -769,6 +769,64 @@ __global__ void __launch_bounds__(1024) k_part_slices(const qi64* __restrict__ o
   if (threadIdx.x == 1023) out[0] = s_sum[1023];
 }
 
+// Chunked scatter -> aggregation slices (one workgroup): counts the claimed chunks and their
+// records per bucket, groups the chunk ids by bucket into `sorted` (order inside a bucket is
+// arbitrary) and cuts each bucket's chunk list into slices of at most cpc chunks, cpc chosen like
+// k_part_slices' cw: 5/4 of an even share of `target` slices, target = max(buckets, min(tmax,
+// records / 32K)). A bucket that is one slice is flagged exclusive. out[0] = slices (at most
+// tmax + buckets).
+constexpr int CHUNK_PLAN_MAXB = 512;  // buckets of the staged scatter
+__global__ void __launch_bounds__(1024) k_chunk_plan(const qi64* __restrict__ meta, qi32 np, qi64 tmax,
+                                                     qi64* __restrict__ out, qi32* __restrict__ sorted) {
+  __shared__ qu32 s_cnt[CHUNK_PLAN_MAXB], s_base[CHUNK_PLAN_MAXB], s_cur[CHUNK_PLAN_MAXB], s_sl[CHUNK_PLAN_MAXB];
+  __shared__ unsigned long long s_rec[CHUNK_PLAN_MAXB];
+  __shared__ qi64 s_cpc;
+  const qi64 C = meta[0];
+  for (int b = threadIdx.x; b < np; b += blockDim.x) {
+    s_cnt[b] = 0;
+    s_cur[b] = 0;
+    s_rec[b] = 0;
+  }
+  __syncthreads();
+  for (qi64 c = threadIdx.x; c < C; c += blockDim.x) {
+    const qi64 w = meta[1 + c];
+    const int b = (int)(w >> 32);
+    atomicAdd(&s_cnt[b], 1u);
+    atomicAdd(&s_rec[b], (unsigned long long)(w & 0xFFFFFFFFll));
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    qi64 R = 0;
+    for (int b = 0; b < np; ++b) R += (qi64)s_rec[b];
+    const qi64 target = max((qi64)np, min(tmax, R >> 15));
+    const qi64 cpc = max((qi64)1, (5 * C + 4 * target - 1) / (4 * target));
+    qu32 base = 0, sl = 0;
+    for (int b = 0; b < np; ++b) {
+      s_base[b] = base;
+      s_sl[b] = sl;
+      base += s_cnt[b];
+      sl += (qu32)((s_cnt[b] + cpc - 1) / cpc);
+    }
+    s_cpc = cpc;
+    out[0] = sl;
+  }
+  __syncthreads();
+  const qi64 cpc = s_cpc;
+  for (int b = threadIdx.x; b < np; b += blockDim.x) {
+    const qi64 s0 = s_base[b], e0 = s0 + s_cnt[b];
+    const qi64 ns = (s_cnt[b] + cpc - 1) / cpc;
+    for (qi64 k = 0; k < ns; ++k) {
+      const qi64 lo = s0 + k * cpc;
+      out[2 + 2 * (s_sl[b] + k)] = lo;
+      out[3 + 2 * (s_sl[b] + k)] = (lo + cpc < e0 ? lo + cpc : e0) | (ns == 1 ? PART_EXCL : 0);
+    }
+  }
+  for (qi64 c = threadIdx.x; c < C; c += blockDim.x) {
+    const int b = (int)(meta[1 + c] >> 32);
+    sorted[s_base[b] + atomicAdd(&s_cur[b], 1u)] = (qi32)c;
+  }
+}
+
 __global__ void k_table_init(DTable t, AggMeta m, qu64* zero_ctl) {
   const qu64 SS = t.cap + 2;
   if (zero_ctl && blockIdx.x == 0 && threadIdx.x < 8) zero_ctl[threadIdx.x] = 0;  // reset: the control words too
@@ -1741,16 +1799,7 @@ static int partition_rows(qe_hashagg* h, Plan& P, hipFunction_t* fn, int* grid) 
   std::string sc, ss, sa;
   size_t jl = 0;
   const bool staged = part_staged_ok(P, log2p);
-  QE_CHECK(gen_part_source(P, log2p, false, &sc) &&
-               (staged ? gen_pscatter_staged_source(P, log2p, &ss) : gen_part_source(P, log2p, true, &ss)) &&
-               gen_pagg_source(P, tlog2, &sa, &jl),
-           QE_ERR_UNSUPPORTED, "plan shape not specialisable");
-  hipFunction_t fc, fs;
-  int bpc = 0;
-  QE_TRY(jit_kernel(ctx, sc, &fc, &bpc, "qe_pcount"));
   const int sblock = staged ? pscatter_block_for(log2p) : 512;
-  QE_TRY(jit_kernel(ctx, ss, &fs, &bpc, "qe_pscatter", sblock));
-  QE_TRY(jit_kernel(ctx, sa, fn, &bpc, "qe_pagg", pagg_block()));
   const int64_t n = P.n;
   // count / scatter workgroups per CU (QE_PART_WG_PER_CU overrides; see pscatter_block)
   static const int wg_per_cu = [] {
@@ -1760,8 +1809,74 @@ static int partition_rows(qe_hashagg* h, Plan& P, hipFunction_t* fn, int* grid) 
   }();
   // (one 1024-thread staged workgroup fits a CU)
   int64_t g = std::min<int64_t>((int64_t)ctx->num_cus * (sblock == 1024 ? 1 : wg_per_cu), (int64_t)div_up((uint64_t)n, 256));
+  const PartLayout L = part_layout(P);
+  const size_t rb = 8 * (size_t)L.words;
+  // Chunked scatter (staged buckets): no count pass and no read-back of the record count;
+  // workgroups claim PART_CH-record chunks per bucket from a device counter. Record space: every
+  // selected row in a full chunk plus one open chunk per (workgroup, bucket) — at most
+  // n / PART_CH + g x buckets chunks — so it is taken while the open chunks' slots do not exceed
+  // the batch's rows (large batches). QE_PART_CHUNKED (read per call): 0 never, 1 whenever the
+  // scatter is staged, unset: by that rule.
+  // (forced on a small batch, the scatter runs fewer workgroups so that the open chunks stay
+  // within 4x the rows: tests exercise the chunked path at their sizes)
+  const char* ce = getenv("QE_PART_CHUNKED");
+  const int chunk_env = ce && *ce ? (ce[0] == '0' ? 0 : 1) : -1;
+  const int64_t np_all = (int64_t)1 << log2p;
+  if (chunk_env == 1 && staged && g * np_all * PART_CH > 4 * n)
+    g = std::max<int64_t>(1, 4 * n / (np_all * PART_CH));
   const int64_t tw = (int64_t)div_up(div_up((uint64_t)n, (uint64_t)g), 256) * 256;
   g = (int64_t)div_up((uint64_t)n, (uint64_t)tw);
+  const int64_t open_slots = g * np_all * PART_CH;
+  const int64_t cmax = (int64_t)div_up((uint64_t)n, (uint64_t)PART_CH) + g * np_all + 1;
+  const bool chunked = chunk_env != 0 && staged && np_all <= CHUNK_PLAN_MAXB &&
+                       (chunk_env == 1 || open_slots <= n) && (uint64_t)cmax * PART_CH * rb <= (96ull << 30);
+  QE_CHECK((chunked || gen_part_source(P, log2p, false, &sc)) &&
+               (staged ? gen_pscatter_staged_source(P, log2p, &ss, chunked) : gen_part_source(P, log2p, true, &ss)) &&
+               gen_pagg_source(P, tlog2, &sa, &jl, chunked),
+           QE_ERR_UNSUPPORTED, "plan shape not specialisable");
+  hipFunction_t fc = nullptr, fs;
+  int bpc = 0;
+  if (!chunked) QE_TRY(jit_kernel(ctx, sc, &fc, &bpc, "qe_pcount"));
+  QE_TRY(jit_kernel(ctx, ss, &fs, &bpc, "qe_pscatter", sblock));
+  QE_TRY(jit_kernel(ctx, sa, fn, &bpc, "qe_pagg", pagg_block()));
+  if (chunked) {
+    const int64_t np = (int64_t)1 << log2p;
+    // [0] chunks claimed | per chunk (bucket << 32 | records) | chunk ids by bucket (int32)
+    QE_TRY(grow_buffer(&h->part_cnt, &h->part_cnt_bytes, (size_t)(1 + cmax) * 8 + (size_t)cmax * 4, ctx, "chunk table"));
+    qi64* meta = (qi64*)h->part_cnt;
+    qi32* sorted = (qi32*)(meta + 1 + cmax);
+    QE_TRY(grow_buffer(&h->part_rec, &h->part_rec_bytes, (size_t)cmax * PART_CH * rb, ctx, "partition records"));
+    const int64_t tmax = (int64_t)ctx->num_cus * 8;
+    const int64_t max_slices = tmax + np;
+    QE_TRY(grow_buffer(&h->part_slc, &h->part_slc_bytes, (size_t)(2 + 2 * max_slices) * 8, ctx, "partition slices"));
+    if (!h->ovf || h->ovf_cap < (1ull << 20)) {
+      uint8_t* ovf = nullptr;
+      size_t have = 0;
+      QE_TRY(grow_buffer(&ovf, &have, (size_t)(1ull << 20) * h->rec_bytes, ctx, "overflow area"));
+      dev_free(ctx, h->ovf);
+      h->ovf = ovf;
+      h->ovf_cap = 1ull << 20;
+    }
+    QE_TRY(ensure_defer(h, cmax * PART_CH));  // the retry bitmaps index record slots
+    P.ovf = h->ovf;
+    P.ovf_cap = h->ovf_cap;
+    QE_HIP(hipMemsetAsync(meta, 0, 8, ctx->stream));
+    P.part_tw = tw;
+    P.part_rec = h->part_rec;
+    P.part_chunk = meta;
+    QE_TRY(jit_launch(ctx, fs, (int)g, P, sblock));
+    QE_TRY(launch_check("qe_pscatter"));
+    hipLaunchKernelGGL(k_chunk_plan, dim3(1), dim3(1024), 0, ctx->stream, (const qi64*)meta, (qi32)np, (qi64)tmax,
+                       (qi64*)h->part_slc, sorted);
+    QE_TRY(launch_check("k_chunk_plan"));
+    P.n = cmax * PART_CH;
+    P.part_slice = (qi64*)h->part_slc;
+    P.part_sorted = sorted;
+    *grid = (int)max_slices;
+    h->jit_note = "radix-partitioned: " + std::to_string(np) + " buckets, chunked records of " + std::to_string(rb) +
+                  " B (" + (L.colmode ? "column" : "value") + " words), staged scatter";
+    return QE_OK;
+  }
   const size_t cells = ((size_t)1 << log2p) * (size_t)g;
   QE_TRY(grow_buffer(&h->part_cnt, &h->part_cnt_bytes, (2 * cells + 1) * 8, ctx, "partition counts"));
   int64_t* cnt = h->part_cnt;
@@ -1787,8 +1902,6 @@ static int partition_rows(qe_hashagg* h, Plan& P, hipFunction_t* fn, int* grid) 
   }
   P.ovf = h->ovf;
   P.ovf_cap = h->ovf_cap;
-  const PartLayout L = part_layout(P);
-  const size_t rb = 8 * (size_t)L.words;
   if (R > 0) {
     QE_TRY(grow_buffer(&h->part_rec, &h->part_rec_bytes, (size_t)R * rb, ctx, "partition records"));
     P.part_off = (qi64*)off;

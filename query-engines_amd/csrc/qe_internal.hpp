@@ -85,7 +85,7 @@ struct PartLayout {
 };
 PartLayout part_layout(const qe::Plan& P);
 bool gen_part_source(const qe::Plan& P, int log2p, bool scatter, std::string* src);
-bool gen_pagg_source(const qe::Plan& P, int log2, std::string* src, size_t* lds_bytes);
+bool gen_pagg_source(const qe::Plan& P, int log2, std::string* src, size_t* lds_bytes, bool chunked = false);
 bool part_staged_ok(const qe::Plan& P, int log2p);
 int pscatter_block();
 bool pscatter_wide();
@@ -96,7 +96,7 @@ int fused_block(int lds_log2);
 // hash-aggregate state accessors for other translation units (qe_comm.hip)
 int hashagg_expected_groups(const qe_hashagg* h, int64_t* out);
 qe_ctx* hashagg_ctx(const qe_hashagg* h);
-bool gen_pscatter_staged_source(const qe::Plan& P, int log2p, std::string* src);
+bool gen_pscatter_staged_source(const qe::Plan& P, int log2p, std::string* src, bool chunked = false);
 int jit_kernel(qe_ctx* ctx, const std::string& src, hipFunction_t* fn, int* blocks_per_cu,
                const char* name = "qe_fused", int block = 512);
 int jit_launch(qe_ctx* ctx, hipFunction_t fn, int grid, const qe::Plan& P, int block = 512);

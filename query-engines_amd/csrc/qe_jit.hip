@@ -666,7 +666,7 @@ int pscatter_depth() {
   return d;
 }
 
-bool gen_pscatter_staged_source(const Plan& P, int log2p, std::string* src) {
+bool gen_pscatter_staged_source(const Plan& P, int log2p, std::string* src, bool chunked) {
   if (P.ncols < 1 || P.ncols > QE_MAX_COLS || log2p < 1 || !part_staged_ok(P, log2p)) return false;
   std::vector<Expr> ex;
   if (!agg_inputs(P, &ex)) return false;
@@ -679,10 +679,18 @@ bool gen_pscatter_staged_source(const Plan& P, int log2p, std::string* src) {
     << "  constexpr int LOG2P = " << log2p << ", NP = 1 << LOG2P, W = " << W << ", T = " << 4 * pscatter_block_for(log2p) << ";\n"
     << "  __shared__ qu32 s_hist[NP];\n  __shared__ qu32 s_off[NP];\n  __shared__ qu64 s_cur[NP];\n  __shared__ qu64 s_dst[NP];\n"
     << "  constexpr int WC = " << W / G << ";  // " << chunk << " chunks per record\n"
-    << "  __shared__ " << chunk << " s_rec[T * WC];\n  __shared__ unsigned short s_bkt[T];\n  __shared__ qu32 s_total;\n"
-    << "  for (int b = threadIdx.x; b < NP; b += blockDim.x) {\n"
-    << "    s_cur[b] = (qu64)P.part_off[(qi64)b * gridDim.x + blockIdx.x];\n    s_hist[b] = 0;\n  }\n"
-    << "  __syncthreads();\n"
+    << "  __shared__ " << chunk << " s_rec[T * WC];\n  __shared__ unsigned short s_bkt[T];\n  __shared__ qu32 s_total;\n";
+  if (chunked)
+    // per bucket: the open chunk (-1: none) and its end, the tile's second destination base (for
+    // the records past the open chunk's room) and the tile-local index where that part starts
+    o << "  __shared__ qu64 s_end[NP];\n  __shared__ qu64 s_dst2[NP];\n  __shared__ qu32 s_lim[NP];\n"
+      << "  __shared__ qi32 s_chunk[NP];\n"
+      << "  for (int b = threadIdx.x; b < NP; b += blockDim.x) {\n"
+      << "    s_cur[b] = 0;\n    s_end[b] = 0;\n    s_chunk[b] = -1;\n    s_hist[b] = 0;\n  }\n";
+  else
+    o << "  for (int b = threadIdx.x; b < NP; b += blockDim.x) {\n"
+      << "    s_cur[b] = (qu64)P.part_off[(qi64)b * gridDim.x + blockIdx.x];\n    s_hist[b] = 0;\n  }\n";
+  o << "  __syncthreads();\n"
     << "  const int lane = threadIdx.x & 63;\n"
     << "  const qi64 lo = (qi64)blockIdx.x * P.part_tw;\n"
     << "  const qi64 hi = lo + P.part_tw < P.n ? lo + P.part_tw : P.n;\n"
@@ -750,9 +758,22 @@ bool gen_pscatter_staged_source(const Plan& P, int log2p, std::string* src) {
       << "#pragma unroll\n      for (int d = 1; d < 64; d <<= 1) { const qu32 y = __shfl_up(x, d); if (lane >= d) x += y; }\n"
       << "      qu32 e = x - s;\n"
       << "#pragma unroll\n      for (int i = 0; i < PER; ++i) {\n"
-      << "        const int b = lane * PER + i;\n"
-      << "        if (b < NP) { s_off[b] = e; const qu64 c = s_cur[b]; s_dst[b] = c - e; s_cur[b] = c + loc[i]; }\n"
-      << "        e += loc[i];\n      }\n"
+      << "        const int b = lane * PER + i;\n";
+    if (chunked)
+      // a run longer than the open chunk's room fills it, and the rest starts a new chunk
+      o << "        if (b < NP) {\n"
+        << "          s_off[b] = e;\n          const qu64 c = s_cur[b], room = s_end[b] - c;\n          s_dst[b] = c - e;\n"
+        << "          if (loc[i] > room) {\n"
+        << "            if (s_chunk[b] >= 0) P.part_chunk[1 + s_chunk[b]] = ((qi64)b << 32) | PART_CH;\n"
+        << "            const qi64 id = (qi64)atomicAdd((unsigned long long*)P.part_chunk, 1ull);\n"
+        << "            const qu64 nb = (qu64)id * PART_CH;\n"
+        << "            s_lim[b] = e + (qu32)room;\n            s_dst2[b] = nb - (e + room);\n"
+        << "            s_cur[b] = nb + (loc[i] - room);\n            s_end[b] = nb + PART_CH;\n            s_chunk[b] = (qi32)id;\n"
+        << "          } else {\n            s_lim[b] = e + loc[i];\n            s_cur[b] = c + loc[i];\n          }\n"
+        << "        }\n";
+    else
+      o << "        if (b < NP) { s_off[b] = e; const qu64 c = s_cur[b]; s_dst[b] = c - e; s_cur[b] = c + loc[i]; }\n";
+    o << "        e += loc[i];\n      }\n"
       << "      if (lane == 63) s_total = x;\n"
       << "    }\n"
       << "    __syncthreads();\n"
@@ -768,17 +789,23 @@ bool gen_pscatter_staged_source(const Plan& P, int log2p, std::string* src) {
       << "    const qu32 tot = s_total;\n"
       << "    for (qu32 c = threadIdx.x; c < tot * WC; c += blockDim.x) {\n"
       << "      const qu32 j = c / WC, q = c % WC;\n"
-      << "      const qu64 dst = s_dst[s_bkt[j]] + j;\n"
+      << (chunked ? "      const qu32 b = s_bkt[j];\n      const qu64 dst = (j < s_lim[b] ? s_dst[b] : s_dst2[b]) + j;\n"
+                  : "      const qu64 dst = s_dst[s_bkt[j]] + j;\n")
       << "      ((" << chunk << "*)(P.part_rec + dst * " << 8 * W << "ull))[q] = s_rec[c];\n"
       << "    }\n"
       << "  }\n";
   }
-  o << "  }\n}\n";
+  o << "  }\n";
+  if (chunked)  // close the open chunks (their last tile's scan is behind a barrier every thread passed)
+    o << "  __syncthreads();\n"
+      << "  for (int b = threadIdx.x; b < NP; b += blockDim.x)\n"
+      << "    if (s_chunk[b] >= 0) P.part_chunk[1 + s_chunk[b]] = ((qi64)b << 32) | (qi64)(s_cur[b] - (qu64)s_chunk[b] * PART_CH);\n";
+  o << "}\n";
   *src = std::string(kDevHeader) + o.str();
   return true;
 }
 
-bool gen_pagg_source(const Plan& P, int log2, std::string* src, size_t* lds_bytes) {
+bool gen_pagg_source(const Plan& P, int log2, std::string* src, size_t* lds_bytes, bool chunked) {
   if (log2 < 4 || log2 > 16) return false;
   const PartLayout L = part_layout(P);
   std::vector<std::string> val(P.naggs), ok(P.naggs);
@@ -801,12 +828,20 @@ bool gen_pagg_source(const Plan& P, int log2, std::string* src, size_t* lds_byte
   std::ostringstream o;
   o << "\nusing namespace qe;\n"
     << "extern \"C\" __global__ void __launch_bounds__(" << pagg_block() << ") qe_pagg(const Plan P) {\n"
-    << "  if ((qi64)blockIdx.x >= P.part_slice[0]) return;\n"
-    << "  const qi64 lo = P.part_slice[2 + 2 * (qi64)blockIdx.x];\n"
-    << "  const qi64 hx = P.part_slice[3 + 2 * (qi64)blockIdx.x];\n"
-    << "  const bool excl = (hx & PART_EXCL) != 0;\n"
-    << "  const qi64 hi = hx & ~PART_EXCL;\n"
-    << "  if (hi <= lo) return;  // (the step prefetch below reads the slice's first record)\n";
+    << "  if ((qi64)blockIdx.x >= P.part_slice[0]) return;\n";
+  if (chunked)
+    // the slice is a range [clo, chi) of the bucket-grouped chunk list; rows lo..hi index its
+    // chunks' record slots (PART_CH per chunk, the tail of a partly filled chunk inactive)
+    o << "  const qi64 clo = P.part_slice[2 + 2 * (qi64)blockIdx.x];\n"
+      << "  const qi64 hx = P.part_slice[3 + 2 * (qi64)blockIdx.x];\n"
+      << "  const bool excl = (hx & PART_EXCL) != 0;\n"
+      << "  const qi64 lo = 0, hi = ((hx & ~PART_EXCL) - clo) * PART_CH;\n";
+  else
+    o << "  const qi64 lo = P.part_slice[2 + 2 * (qi64)blockIdx.x];\n"
+      << "  const qi64 hx = P.part_slice[3 + 2 * (qi64)blockIdx.x];\n"
+      << "  const bool excl = (hx & PART_EXCL) != 0;\n"
+      << "  const qi64 hi = hx & ~PART_EXCL;\n";
+  o << "  if (hi <= lo) return;  // (the step prefetch below reads the slice's first record)\n";
   o << "  __shared__ int s_fail;\n  __shared__ qu32 s_newg;\n  if (threadIdx.x == 0) { s_fail = 0; s_newg = 0; }\n";
   emit_lds_table(P, o, log2, lds_bytes);
   // the records of the wave's next step are loaded into n* registers before this step's LDS work
@@ -814,10 +849,18 @@ bool gen_pagg_source(const Plan& P, int log2, std::string* src, size_t* lds_byte
     return (q == 0 ? pre + "key" : pre + "w" + std::to_string(q)) + "[r]";
   };
   auto load_step = [&](const std::string& pre, const std::string& nb) {
-    o << "    {\n      const qi64 nb = " << nb << ";\n      " << pre << "act = 0;\n"
-      << "#pragma unroll\n      for (int r = 0; r < 4; ++r) {\n"
-      << "        const qi64 i = nb + lane + 64 * r;\n"
-      << "        bool on = i < hi;\n"
+    o << "    {\n      const qi64 nb = " << nb << ";\n      " << pre << "act = 0;\n";
+    if (chunked)
+      o << "      qi64 cfill = 0;\n      " << pre << "pb = 0;\n"
+        << "      if (nb < hi) {\n"
+        << "        const qi64 id = P.part_sorted[clo + nb / PART_CH], ko = nb % PART_CH;\n"
+        << "        " << pre << "pb = id * PART_CH + ko;\n"
+        << "        cfill = (P.part_chunk[1 + id] & 0xFFFFFFFFll) - ko;\n      }\n";
+    else
+      o << "      " << pre << "pb = nb;\n";
+    o << "#pragma unroll\n      for (int r = 0; r < 4; ++r) {\n"
+      << "        const qi64 i = " << pre << "pb + lane + 64 * r;\n"
+      << (chunked ? "        bool on = lane + 64 * r < cfill;\n" : "        bool on = i < hi;\n")
       << "        if (on && P.defer_in) on = (P.defer_in[i >> 5] >> (i & 31)) & 1;\n"
       << "        " << pre << "act |= (qu32)on << r;\n";
     if (L.words % 2 == 0) {
@@ -834,7 +877,7 @@ bool gen_pagg_source(const Plan& P, int log2, std::string* src, size_t* lds_byte
   };
   o << "  const int lane = threadIdx.x & 63;\n"
     << "  const qi64 step = (qi64)(blockDim.x >> 6) * 256;\n"
-    << "  qu32 nact;\n  qi64 nkey[4];\n";
+    << "  qu32 nact;\n  qi64 nkey[4], npb;\n";
   for (int q = 1; q < L.words; ++q) o << "  qi64 nw" << q << "[4];\n";
   const char* pfe = getenv("QE_PAGG_PREFETCH");
   const bool pf = !(pfe && pfe[0] == '0');
@@ -843,12 +886,13 @@ bool gen_pagg_source(const Plan& P, int log2, std::string* src, size_t* lds_byte
   const char* pde = getenv("QE_PAGG_DEPTH");
   const int depth = pf && pde && pde[0] == '2' ? 2 : 1;
   if (depth == 2) {
-    o << "  qu32 mact;\n  qi64 mkey[4];\n";
+    o << "  qu32 mact;\n  qi64 mkey[4], mpb;\n";
     for (int q = 1; q < L.words; ++q) o << "  qi64 mw" << q << "[4];\n";
   }
   // one step over the records of buffer `pre` at row `b`, reloading that buffer with row `nb`
   auto body = [&](const std::string& pre, const std::string& b, const std::string& nb) {
-    o << "    {\n    const qi64 sbase = " << b << ";\n"
+    (void)b;  // the step's first record slot is the buffer's pb (= its row for unchunked slices)
+    o << "    {\n    const qi64 sbase = " << pre << "pb;\n"
       << "    const qu32 act = " << pre << "act;\n    qu32 knull = 0;\n"
       << "    qi64 key[4] = {" << pre << "key[0], " << pre << "key[1], " << pre << "key[2], " << pre << "key[3]};\n";
     for (int q = 1; q < L.words; ++q)
@@ -892,7 +936,11 @@ bool gen_pagg_source(const Plan& P, int log2, std::string* src, size_t* lds_byte
   // in it exactly when its records were aggregated there rather than on the global path)
   o << "  __syncthreads();\n"
     << "  if (s_fail) {\n"
-    << "    for (qi64 i = lo + threadIdx.x; i < hi; i += blockDim.x) {\n"
+    << (chunked ? "    for (qi64 v = threadIdx.x; v < hi; v += blockDim.x) {\n"
+                  "      const qi64 id = P.part_sorted[clo + v / PART_CH], ko = v % PART_CH;\n"
+                  "      if (ko >= (P.part_chunk[1 + id] & 0xFFFFFFFFll)) continue;\n"
+                  "      const qi64 i = id * PART_CH + ko;\n"
+                : "    for (qi64 i = lo + threadIdx.x; i < hi; i += blockDim.x) {\n")
     << "      if (P.defer_in && !((P.defer_in[i >> 5] >> (i & 31)) & 1)) continue;\n"
     << "      const qi64* rp = (const qi64*)(P.part_rec + i * " << 8 * L.words << "ull);\n"
     << "      const qi64 k = rp[0];\n";
@@ -956,6 +1004,8 @@ std::string plan_shape_key(const qe_ctx* ctx, const Plan& P) {
   k.part_off = nullptr;
   k.part_tw = 0;
   k.part_slice = nullptr;
+  k.part_chunk = nullptr;
+  k.part_sorted = nullptr;
   const int32_t extra[2] = {ctx->device, use_nt() ? 1 : 0};
   return std::string((const char*)&k, sizeof k) + std::string((const char*)extra, sizeof extra);
 }

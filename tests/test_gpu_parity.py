@@ -590,9 +590,18 @@ def check_partitioned(ctx, st):
         assert spec and note.startswith("radix-partitioned"), note
 
 
+@pytest.fixture(params=["auto", "chunked", "counted"])
+def part_mode(request, monkeypatch):
+    """Both record placements of the partitioned update: chunks claimed from a device counter (the
+    default for large batches; forced here at test sizes) and exact offsets from a count pass."""
+    if request.param != "auto":
+        monkeypatch.setenv("QE_PART_CHUNKED", "1" if request.param == "chunked" else "0")
+    return request.param
+
+
 @pytest.mark.parametrize("ngroups,expected", [(50_000, 50_000), (600_000, 20_000), (3, 100_000)])
 @pytest.mark.parametrize("vtype", ["i64", "f64"])
-def test_hashagg_partitioned(agg_ctx, ngroups, expected, vtype):
+def test_hashagg_partitioned(agg_ctx, part_mode, ngroups, expected, vtype):
     """Expected groups beyond the LDS table: rows are radix-partitioned by key hash and each
     workgroup aggregates a record slice in LDS. Nullable keys and inputs, the EMPTY sentinel as a
     key, fp64 MIN/MAX order ties across two batches, and far more groups than expected (records of
@@ -693,7 +702,7 @@ def test_fused_c4_multipass_vs_oracle(agg_ctx):
     assert_groups_equal(result_dict(kk, aa), ref, C4_FNS)
 
 
-def test_hashagg_adapts_to_partitioned(agg_ctx):
+def test_hashagg_adapts_to_partitioned(agg_ctx, part_mode):
     """expected_groups left at its default while the batches hold 300K groups: the first batch
     grows the global table, and the later batches switch to the partitioned update by themselves."""
     rng = np.random.default_rng(23)
@@ -715,7 +724,7 @@ def test_hashagg_adapts_to_partitioned(agg_ctx):
 
 
 @pytest.mark.parametrize("groups,threshold", [(100_000, 1 << 19), (1 << 20, 1 << 19), (100_000, 1 << 21)])
-def test_fused_c4_partitioned_vs_oracle(agg_ctx, groups, threshold):
+def test_fused_c4_partitioned_vs_oracle(agg_ctx, part_mode, groups, threshold):
     """C4 query shape with k = u mod G for large G (partitioned fused path), including a predicate
     no row passes (zero records, zero groups)."""
     from kquery.datasource import C4_COLUMNS, ColumnSpec, generate_column
@@ -780,7 +789,7 @@ def _colrec_case(shape, rng, n):
 
 
 @pytest.mark.parametrize("shape,width", [("odd", 24), ("even", 32), ("f64", 32)])
-def test_fused_partitioned_column_records(agg_ctx, shape, width):
+def test_fused_partitioned_column_records(agg_ctx, part_mode, shape, width):
     """Partitioned records that hold the columns the aggregate programs read, when that is narrower
     than the programs' values: the programs are re-evaluated in the aggregation pass. Nullable key
     and inputs, integer division by zero (null), literals, fp64 MIN/MAX row order, two batches."""
