@@ -133,6 +133,8 @@ struct Plan {
   // multi-pass fused aggregate (groups just beyond one LDS table): pass mp_pass of mp_n keeps the
   // rows whose key hash falls in bucket mp_pass (mp_n = 0: every row)
   qi32 mp_n, mp_pass;
+  // spilling first pass (spill_update): rows with fmix64(key) >> 32 >= mp_keep are spilled as records
+  qu64 mp_keep;
 };
 
 // ---- scalar helpers ---------------------------------------------------------------------------------

@@ -827,6 +827,27 @@ __global__ void __launch_bounds__(1024) k_chunk_plan(const qi64* __restrict__ me
   }
 }
 
+// Slices of the spilled bucket (spill_update): one bucket, so the chunk list is the identity
+// (sorted[c] = c) and slices are ranges of at most cpc chunks, about min(tmax, records / 32K) of
+// them; a single slice is exclusive. Grid: enough threads for every chunk id; k_chunk_plan's one
+// workgroup took 0.32 ms over the ~122K chunks of 1B rows.
+__global__ void k_spill_plan(const qi64* __restrict__ meta, qi64 tmax, qi64* __restrict__ out, qi32* __restrict__ sorted) {
+  const qi64 C = meta[0];
+  const qi64 c = (qi64)blockIdx.x * blockDim.x + threadIdx.x;
+  if (c < C) sorted[c] = (qi32)c;
+  if (blockIdx.x != 0) return;
+  qi64 target = (C * PART_CH) >> 15;
+  target = target < 1 ? 1 : (target > tmax ? tmax : target);
+  const qi64 cpc = (C + target - 1) / target > 0 ? (C + target - 1) / target : 1;
+  const qi64 ns = (C + cpc - 1) / cpc;
+  for (qi64 k = threadIdx.x; k < ns; k += blockDim.x) {
+    const qi64 lo = k * cpc;
+    out[2 + 2 * k] = lo;
+    out[3 + 2 * k] = (lo + cpc < C ? lo + cpc : C) | (ns == 1 ? PART_EXCL : 0);
+  }
+  if (threadIdx.x == 0) out[0] = ns;
+}
+
 __global__ void k_table_init(DTable t, AggMeta m, qu64* zero_ctl) {
   const qu64 SS = t.cap + 2;
   if (zero_ctl && blockIdx.x == 0 && threadIdx.x < 8) zero_ctl[threadIdx.x] = 0;  // reset: the control words too
@@ -1936,7 +1957,7 @@ static int partition_rows(qe_hashagg* h, Plan& P, hipFunction_t* fn, int* grid) 
 // chosen (plan-specialised when possible), events bracketing it (ev[0] of pass 0 / mp 0 is
 // recorded by the caller, before any partitioning work).
 static int launch_pass(qe_hashagg* h, Plan& P, size_t lds, hipFunction_t pfn, int pgrid, int pass, int mp,
-                       int out_i, const uint32_t* defer_in) {
+                       int out_i, const uint32_t* defer_in, int pblock = 0) {
   qe_ctx* ctx = h->ctx;
   const int64_t n = P.n;
   QE_CHECK(pass < 64, QE_ERR_CAPACITY, "hash aggregate did not converge after %d passes", pass);
@@ -2016,7 +2037,7 @@ static int launch_pass(qe_hashagg* h, Plan& P, size_t lds, hipFunction_t pfn, in
   }
   if (pass > 0 || mp > 0) QE_HIP(hipEventRecord(h->ev[0], ctx->stream));
   if (jfn) {
-    QE_TRY(jit_launch(ctx, jfn, jgrid, P, pfn ? pagg_block() : fused_block(P.lds_log2)));
+    QE_TRY(jit_launch(ctx, jfn, jgrid, P, pfn ? (pblock ? pblock : pagg_block()) : fused_block(P.lds_log2)));
   } else {
     QE_TRY(launch_hashagg(P, grid, lds, ctx->stream));
   }
@@ -2094,6 +2115,87 @@ static int settle_pending(qe_hashagg* h) {
   return QE_OK;
 }
 
+// Two key-hash buckets (groups just beyond one LDS table; QE_MP_SPILL, read per call, 0 = two
+// fused passes): pass 0 of the fused kernel keeps bucket 0 in its LDS tables and appends the other
+// bucket's selected rows as partition records (part_layout, chunk-columnar) in per-wave chunks;
+// k_spill_plan slices them (at most a slice per CU) and one chunked qe_pagg pass aggregates bucket 1. The columns are read once: C4 shape
+// 24 B/row + 2 x 24 B per spilled record (~36 GB at 1B rows) instead of 48 B/row for two passes.
+// *used = false: not applicable here (the caller runs the fused passes).
+static int spill_update(qe_hashagg* h, Plan& P, size_t lds, int64_t rows, bool* used) {
+  qe_ctx* ctx = h->ctx;
+  *used = false;
+  const char* e = getenv("QE_MP_SPILL");
+  if ((e && e[0] == '0') || P.mp_n != 2) return QE_OK;
+  const PartLayout L = part_layout(P);
+  const size_t rb = 8 * (size_t)L.words;
+  if ((uint64_t)rows * rb > (96ull << 30)) return QE_OK;
+  Plan Q = P;
+  Q.mp_n = 0;
+  Q.mp_pass = 0;
+  int tlog2 = 16;
+  const size_t pbudget = pagg_block() == 1024 ? (size_t)152 * 1024 : HA_LDS_BUDGET;
+  while (tlog2 >= 8 && lds_layout_at(h, &Q, tlog2) > pbudget) --tlog2;
+  if (tlog2 < 8) return QE_OK;
+  std::string ss, sa;
+  size_t jl = 0;
+  if (!gen_fused_source(P, P.lds_log2, &ss, &jl, true) || !gen_pagg_source(Q, tlog2, &sa, &jl, true, true)) return QE_OK;
+  hipFunction_t fs = nullptr, fa = nullptr;
+  int bpc = 0, bpc_a = 0;
+  const int sblock = fused_block(P.lds_log2);
+  QE_TRY(jit_kernel(ctx, ss, &fs, &bpc, "qe_fused", sblock));
+  QE_TRY(jit_kernel(ctx, sa, &fa, &bpc_a, "qe_pagg", pagg_block()));
+  const int64_t waves = (int64_t)div_up((uint64_t)rows, 256);
+  const int sgrid = (int)std::max<int64_t>(
+      1, std::min<int64_t>((int64_t)ctx->num_cus * std::max(1, bpc), (int64_t)div_up((uint64_t)waves, sblock / 64)));
+  // chunks: the full ones plus one open chunk per wave of the grid
+  const int64_t cmax = (int64_t)div_up((uint64_t)rows, (uint64_t)PART_CH) + (int64_t)sgrid * (sblock / 64) + 1;
+  QE_TRY(grow_buffer(&h->part_rec, &h->part_rec_bytes, (size_t)cmax * PART_CH * rb, ctx, "spill records"));
+  QE_TRY(grow_buffer(&h->part_cnt, &h->part_cnt_bytes, (size_t)(1 + cmax) * 8 + (size_t)cmax * 4, ctx, "chunk table"));
+  qi64* meta = (qi64*)h->part_cnt;
+  qi32* sorted = (qi32*)(meta + 1 + cmax);
+  const int64_t tmax = ctx->num_cus;  // aggregation slices of the spilled bucket
+  QE_TRY(grow_buffer(&h->part_slc, &h->part_slc_bytes, (size_t)(2 + 2 * (tmax + 1)) * 8, ctx, "spill slices"));
+  QE_TRY(ensure_defer(h, cmax * PART_CH));  // the aggregation pass's retry bitmaps index record slots
+  *used = true;
+  QE_HIP(hipMemsetAsync(meta, 0, 8, ctx->stream));
+  // kept share: as many groups as one LDS table holds at the multi-pass load (5/8), the rest spilled
+  // (4096 expected groups of the C4 shape: 62.5 % kept, so 3/4 of the records of an even split)
+  const double keep = std::min(1.0, (double)(((int64_t)1 << P.lds_log2) * 5 / 8) / (double)std::max<int64_t>(1, h->expected_groups));
+  P.mp_keep = (qu64)(keep * 4294967296.0);
+  P.part_rec = h->part_rec;
+  P.part_chunk = meta;
+  int out_i = 0;
+  const uint32_t* defer_in = nullptr;
+  // retry passes re-run the spill kernel over deferred rows only: those are bucket-0 rows, so
+  // nothing is spilled twice
+  for (int pass = 0;; ++pass) {
+    QE_TRY(launch_pass(h, P, lds, fs, sgrid, pass, 0, out_i, defer_in, sblock));
+    bool done = false;
+    QE_TRY(settle_pass(h, P, &out_i, &defer_in, &done));
+    if (done) break;
+  }
+  hipLaunchKernelGGL(k_spill_plan, dim3((unsigned)div_up((uint64_t)cmax, 256)), dim3(256), 0, ctx->stream,
+                     (const qi64*)meta, (qi64)tmax, (qi64*)h->part_slc, sorted);
+  QE_TRY(launch_check("k_spill_plan"));
+  Q.n = cmax * PART_CH;  // record slots (the retry bitmaps index them)
+  Q.part_rec = h->part_rec;
+  Q.part_chunk = meta;
+  Q.part_sorted = sorted;
+  Q.part_slice = (qi64*)h->part_slc;
+  Q.ovf = h->ovf;
+  Q.ovf_cap = h->ovf_cap;
+  defer_in = nullptr;
+  for (int pass = 0;; ++pass) {
+    QE_TRY(launch_pass(h, Q, lds, fa, (int)(tmax + 1), pass, 1, out_i, defer_in));
+    bool done = false;
+    QE_TRY(settle_pass(h, Q, &out_i, &defer_in, &done));
+    if (done) break;
+  }
+  h->jit_note = "multi-pass: 2 buckets, bucket 1 spilled as " + std::to_string(rb) + " B records (" +
+                (L.colmode ? "column" : "value") + " words)";
+  return QE_OK;
+}
+
 static int run_update(qe_hashagg* h, Plan& P) {
   qe_ctx* ctx = h->ctx;
   QE_TRY(settle_pending(h));
@@ -2151,6 +2253,15 @@ static int run_update(qe_hashagg* h, Plan& P) {
         P = T;
         lds = lds_mp;
       }
+    }
+  }
+  if (mp_n == 2) {
+    bool used = false;
+    QE_TRY(spill_update(h, P, lds, rows, &used));
+    if (used) {
+      h->row_base += rows;
+      adapt_after_update(h, lds, P.lds_log2);
+      return QE_OK;
     }
   }
   if (!lds && mp_n == 0 && ctx->jit && h->expected_groups > 0) {

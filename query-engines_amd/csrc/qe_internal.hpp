@@ -70,7 +70,7 @@ int ctx_workspace(qe_ctx* ctx, int slot, size_t bytes, void** out);  // grow-onl
 // Host (pageable) -> device through pinned staging with 8 host threads; synchronous (qe_arrow.hip).
 int parallel_h2d_copy(qe_ctx* ctx, void* dst, const void* src, size_t n);
 // Per-plan kernel specialisation (qe_jit.hip).
-bool gen_fused_source(const qe::Plan& P, int log2, std::string* src, size_t* lds_bytes);
+bool gen_fused_source(const qe::Plan& P, int log2, std::string* src, size_t* lds_bytes, bool spill = false);
 // Radix-partitioned aggregation for group counts beyond the LDS table (qe_jit.hip).
 struct PartLayout {
   int words = 0;  // record width in 8-byte words
@@ -85,7 +85,8 @@ struct PartLayout {
 };
 PartLayout part_layout(const qe::Plan& P);
 bool gen_part_source(const qe::Plan& P, int log2p, bool scatter, std::string* src);
-bool gen_pagg_source(const qe::Plan& P, int log2, std::string* src, size_t* lds_bytes, bool chunked = false);
+bool gen_pagg_source(const qe::Plan& P, int log2, std::string* src, size_t* lds_bytes, bool chunked = false,
+                     bool soa = false);
 bool part_staged_ok(const qe::Plan& P, int log2p);
 int pscatter_block();
 bool pscatter_wide();

@@ -434,10 +434,25 @@ bool agg_inputs(const Plan& P, std::vector<Expr>* ex) {
 
 }  // namespace
 
+void emit_record_words(const Plan& P, const PartLayout& L, const std::vector<Expr>& ex, const std::string& dst,
+                       std::ostringstream& o);
+
 // Returns false when the plan shape is outside what the generator emits (caller uses the
 // generic kernel). `log2` is the LDS table size chosen for this launch.
-bool gen_fused_source(const Plan& P, int log2, std::string* src, size_t* lds_bytes) {
+//
+// `spill` (with P.mp_n > 1): rows whose key hash is at or above P.mp_keep (the kept share sized
+// to fill the LDS table) are not dropped but appended as
+// partition records (part_layout) for one chunked qe_pagg pass afterwards: the columns are read
+// once, and only the spilled rows' records are written and re-read. Each wave fills its own
+// PART_CH-record chunks, claimed from P.part_chunk[0] (one device atomic per 2048 records; one per
+// wave step on a single cursor serialised the kernel: 49 ms at 1B rows); in a step the spilling
+// lanes take consecutive slots (ballot + popcount among the lanes still in the step). Chunk c's
+// fill goes to P.part_chunk[1 + c] (bucket 0), as the chunked scatter leaves it. Records are stored
+// chunk-columnar (word q of a chunk's records together; gen_pagg_source `soa`): a step's spilling
+// lanes then write whole 512-byte runs per word instead of 8 bytes every 24.
+bool gen_fused_source(const Plan& P, int log2, std::string* src, size_t* lds_bytes, bool spill) {
   if (log2 < 4 || log2 > 16 || P.ncols < 1 || P.ncols > QE_MAX_COLS) return false;
+  if (spill && P.mp_n < 2) return false;
   std::vector<Expr> ex;
   if (!agg_inputs(P, &ex)) return false;
   std::vector<std::string> val(P.naggs), ok(P.naggs);
@@ -450,6 +465,9 @@ bool gen_fused_source(const Plan& P, int log2, std::string* src, size_t* lds_byt
   o << "\nusing namespace qe;\n"
     << "extern \"C\" __global__ void __launch_bounds__(" << fused_block(log2) << ") qe_fused(const Plan P) {\n"
     << "  __shared__ qu32 s_newg;\n  if (threadIdx.x == 0) s_newg = 0;\n";
+  if (spill)
+    o << "  __shared__ qi64 s_spc[16];\n  __shared__ qu32 s_spf[16];\n"
+      << "  if (threadIdx.x < 16) { s_spc[threadIdx.x] = -1; s_spf[threadIdx.x] = 0; }\n";
   emit_lds_table(P, o, log2, lds_bytes);
   o << "  const int lane = threadIdx.x & 63;\n"
     << "  const qi64 wave = (blockIdx.x * (qi64)blockDim.x + threadIdx.x) >> 6;\n"
@@ -478,12 +496,58 @@ bool gen_fused_source(const Plan& P, int log2, std::string* src, size_t* lds_byt
   }
   emit_active_rows(P, o, true);
   emit_keys(P, o);
-  if (P.mp_n > 1)
+  if (spill) {
+    const PartLayout L = part_layout(P);
+    // per wave: the open record chunk (PART_CH slots claimed from the chunk counter P.part_chunk[0])
+    // and its fill, in LDS so that every lane still in the step sees the current values (the same
+    // state in registers, with every lane running the block, measured 6.40 against 6.19 ms)
+    o << "    qu32 sp = 0;\n"
+      << "#pragma unroll\n    for (int r = 0; r < 4; ++r)\n"
+      << "      if (((act >> r) & 1) && (fmix64((qu64)key[r]) >> 32) >= P.mp_keep) sp |= 1u << r;\n"
+      << "    act &= ~sp;\n"
+      << "    {\n      qu64 bal[4];\n      qu32 tot = 0;\n"
+      << "#pragma unroll\n      for (int r = 0; r < 4; ++r) { bal[r] = __ballot((sp >> r) & 1u); tot += (qu32)__popcll(bal[r]); }\n"
+      << "      if (tot) {\n"
+      << "        const int leader = __ffsll((long long)__ballot(1)) - 1;\n"
+      << "        const int wv = threadIdx.x >> 6;\n"
+      << "        const qi64 cid = s_spc[wv];\n"
+      << "        const qu32 fill = s_spf[wv];\n"
+      << "        const qu32 room = cid >= 0 ? (qu32)PART_CH - fill : 0u;\n"
+      << "        qi64 nid = cid;\n"
+      << "        if (tot > room) {\n"
+      << "          qi64 id = 0;\n"
+      << "          if (lane == leader) {\n"
+      << "            if (cid >= 0) P.part_chunk[1 + cid] = PART_CH;\n"
+      << "            id = (qi64)atomicAdd((qu64*)P.part_chunk, 1ull);\n"
+      << "          }\n"
+      << "          nid = __shfl(id, leader);\n"
+      << "        }\n"
+      << "        if (lane == leader) {\n"
+      << "          if (tot > room) { s_spc[wv] = nid; s_spf[wv] = tot - room; } else s_spf[wv] = fill + tot;\n"
+      << "        }\n"
+      << "        const qu64 below = (1ull << lane) - 1;\n"
+      << "        qu32 kb = 0;\n"
+      << "#pragma unroll\n        for (int r = 0; r < 4; ++r) {\n"
+      << "          if ((sp >> r) & 1) {\n"
+      << "            const qu32 k = kb + (qu32)__popcll(bal[r] & below);\n"
+      << "            const qu64 pos = k < room ? (qu64)cid * PART_CH + fill + k : (qu64)nid * PART_CH + (k - room);\n"
+      << "            qi64 w[" << L.words << "];\n";
+    emit_record_words(P, L, ex, "w", o);
+    // chunk-columnar: word q of slot `pos` at ((chunk * W + q) * PART_CH + pos % PART_CH) * 8, so the
+    // lanes of one row position store consecutive 8-byte words
+    o << "            qi64* dst = (qi64*)P.part_rec + (pos / PART_CH) * (" << L.words << " * PART_CH) + pos % PART_CH;\n";
+    for (int q = 0; q < L.words; ++q) o << "            dst[" << q << " * PART_CH] = w[" << q << "];\n";
+    o << "          }\n          kb += (qu32)__popcll(bal[r]);\n        }\n      }\n    }\n"
+      << "    if (act == 0) continue;\n";
+  } else if (P.mp_n > 1)
     o << "#pragma unroll\n    for (int r = 0; r < 4; ++r)\n"
       << "      if (((act >> r) & 1) && (qu32)__umul64hi(fmix64((qu64)key[r]), (qu64)P.mp_n) != (qu32)P.mp_pass) act &= ~(1u << r);\n"
       << "    if (act == 0) continue;\n";
   emit_agg_rows(P, o, val, ok, "P.row_base + r0 + 128 * (r >> 1) + (r & 1)", "r0 + 128 * (r >> 1) + (r & 1)");
   o << (pf ? "    } while (0);\n  }\n  }\n" : "  }\n");
+  if (spill)  // each wave's open chunk: its fill (a wave's LDS writes are seen by its own later reads)
+    o << "  if ((threadIdx.x & 63) == 0 && s_spc[threadIdx.x >> 6] >= 0)\n"
+      << "    P.part_chunk[1 + s_spc[threadIdx.x >> 6]] = (qi64)s_spf[threadIdx.x >> 6];\n";
   emit_flush(P, o);
   o << "  __syncthreads();\n  if (threadIdx.x == 0 && s_newg) atomicAdd(&P.t.ctl[0], (qu64)s_newg);\n}\n";
   *src = std::string(kDevHeader) + o.str();
@@ -805,8 +869,10 @@ bool gen_pscatter_staged_source(const Plan& P, int log2p, std::string* src, bool
   return true;
 }
 
-bool gen_pagg_source(const Plan& P, int log2, std::string* src, size_t* lds_bytes, bool chunked) {
-  if (log2 < 4 || log2 > 16) return false;
+// `soa` (chunked only): records stored chunk-columnar, word q of slot i at
+// ((i / PART_CH) * W + q) * PART_CH + i % PART_CH (the spilling fused pass writes them so).
+bool gen_pagg_source(const Plan& P, int log2, std::string* src, size_t* lds_bytes, bool chunked, bool soa) {
+  if (log2 < 4 || log2 > 16 || (soa && !chunked)) return false;
   const PartLayout L = part_layout(P);
   std::vector<std::string> val(P.naggs), ok(P.naggs);
   if (L.colmode) {
@@ -863,7 +929,12 @@ bool gen_pagg_source(const Plan& P, int log2, std::string* src, size_t* lds_byte
       << (chunked ? "        bool on = lane + 64 * r < cfill;\n" : "        bool on = i < hi;\n")
       << "        if (on && P.defer_in) on = (P.defer_in[i >> 5] >> (i & 31)) & 1;\n"
       << "        " << pre << "act |= (qu32)on << r;\n";
-    if (L.words % 2 == 0) {
+    if (soa) {
+      o << "        const qi64* p = (const qi64*)P.part_rec + (on ? (i / PART_CH) * (" << L.words
+        << " * PART_CH) + i % PART_CH : 0);\n";
+      for (int q = 0; q < L.words; ++q)
+        o << "        " << word(pre, q) << " = " << ld("qi64", "p + " + std::to_string(q) + " * PART_CH") << ";\n";
+    } else if (L.words % 2 == 0) {
       o << "        const qi64x2* p = (const qi64x2*)(P.part_rec + (on ? i : 0) * " << 8 * L.words << "ull);\n";
       for (int q = 0; q < L.words / 2; ++q)
         o << "        { const qi64x2 v = " << ld("qi64x2", "p + " + std::to_string(q)) << "; " << word(pre, 2 * q)
@@ -942,10 +1013,12 @@ bool gen_pagg_source(const Plan& P, int log2, std::string* src, size_t* lds_byte
                   "      const qi64 i = id * PART_CH + ko;\n"
                 : "    for (qi64 i = lo + threadIdx.x; i < hi; i += blockDim.x) {\n")
     << "      if (P.defer_in && !((P.defer_in[i >> 5] >> (i & 31)) & 1)) continue;\n"
-    << "      const qi64* rp = (const qi64*)(P.part_rec + i * " << 8 * L.words << "ull);\n"
+    << (soa ? "      const qi64* rp = (const qi64*)P.part_rec + (i / PART_CH) * (" + std::to_string(L.words) +
+                  " * PART_CH) + i % PART_CH;\n"
+            : "      const qi64* rp = (const qi64*)(P.part_rec + i * " + std::to_string(8 * L.words) + "ull);\n")
     << "      const qi64 k = rp[0];\n";
   if (L.flags_word >= 0)
-    o << "      const bool kn = rp[" << L.flags_word << "] & 1;\n";
+    o << "      const bool kn = rp[" << L.flags_word << (soa ? " * PART_CH" : "") << "] & 1;\n";
   else
     o << "      const bool kn = false;\n";
   o << "      int s = kn ? S : (k == EMPTY_KEY ? S + 1 : -1);\n"
@@ -1006,6 +1079,7 @@ std::string plan_shape_key(const qe_ctx* ctx, const Plan& P) {
   k.part_slice = nullptr;
   k.part_chunk = nullptr;
   k.part_sorted = nullptr;
+  k.mp_keep = 0;
   const int32_t extra[2] = {ctx->device, use_nt() ? 1 : 0};
   return std::string((const char*)&k, sizeof k) + std::string((const char*)extra, sizeof extra);
 }

@@ -57,6 +57,60 @@ static int emit(const char* dir, const char* name, const qe_column* cols, int nc
   return 0;
 }
 
+static int write_src(const char* dir, const std::string& name, const std::string& src) {
+  const std::string path = std::string(dir) + "/" + name + ".hip";
+  FILE* f = fopen(path.c_str(), "w");
+  if (!f) return 1;
+  fwrite(src.data(), 1, src.size(), f);
+  fclose(f);
+  printf("%s\n", path.c_str());
+  return 0;
+}
+
+// Fused GROUP BY plan (key in slot 0; aggregates given as (fn, acc, program)) with two key-hash
+// buckets: the two-pass fused kernel, the spilling first pass (spill_update) and the qe_pagg pass
+// over its records.
+struct AggIn {
+  int fn, acc;
+  const qe_agg_program* prog;  // null: COUNT(*)
+};
+static int emit_agg(const char* dir, const char* name, const qe_column* cols, int ncols, const qe_pred_term* terms,
+                    int nterms, const AggIn* aggs, int naggs, int log2) {
+  Plan P;
+  bool col_f64[QE_MAX_COLS];
+  if (compile_inputs(cols, ncols, -1, nterms, terms, &P, col_f64) != QE_OK) {
+    fprintf(stderr, "%s: compile_inputs: %s\n", name, qe_last_error());
+    return 1;
+  }
+  P.key_mode = 1;
+  P.nkeys = 1;
+  P.key_col[0] = 0;
+  P.key_f64 = 0;
+  P.naggs = naggs;
+  for (int j = 0; j < naggs; ++j) {
+    memset(&P.aggs[j], 0, sizeof P.aggs[j]);
+    bool is_f = false, nullable = false;
+    if (aggs[j].prog && compile_program(cols, ncols, col_f64, *aggs[j].prog, j, &P.aggs[j], &is_f, &nullable) != QE_OK) {
+      fprintf(stderr, "%s: compile_program: %s\n", name, qe_last_error());
+      return 1;
+    }
+    P.aggs[j].fn = aggs[j].fn;
+    P.aggs[j].acc = aggs[j].acc;
+    P.aggs[j].track_nn = nullable ? 1 : 0;
+  }
+  P.mp_n = 2;
+  P.mp_pass = 0;
+  std::string a, b, c;
+  size_t lds = 0;
+  if (!gen_fused_source(P, log2, &a, &lds, false) || !gen_fused_source(P, log2, &b, &lds, true) ||
+      !gen_pagg_source(P, log2, &c, &lds, true, true)) {
+    fprintf(stderr, "%s: fused / spill / pagg source not generated\n", name);
+    return 1;
+  }
+  return write_src(dir, std::string(name) + "_fused", a) | write_src(dir, std::string(name) + "_spill", b) |
+         write_src(dir, std::string(name) + "_pagg", c);
+}
+
 int main(int argc, char** argv) {
   if (argc < 2) return 2;
   static int64_t dummy[64];
@@ -89,5 +143,28 @@ int main(int argc, char** argv) {
   outs[1].tokens[0].op = QE_TOK_COL;
   outs[1].tokens[0].arg = 2;
   rc |= emit(argv[1], "nullable", cols, 3, t2, 2, outs, 2);
+  // C4: SELECT k, SUM(a+b), COUNT(*), MIN(a), MAX(b) WHERE a > 2^19 GROUP BY k (slots k, a, b)
+  cols[1].validity = nullptr;
+  qe_pred_term t4 = term(1, QE_OP_GT, 1 << 19);
+  qe_agg_program ab = add, pa, pb;
+  ab.tokens[0].arg = 1;
+  ab.tokens[1].arg = 2;
+  memset(&pa, 0, sizeof pa);
+  pa.ntokens = 1;
+  pa.tokens[0].op = QE_TOK_COL;
+  pa.tokens[0].arg = 1;
+  pb = pa;
+  pb.tokens[0].arg = 2;
+  const AggIn c4[4] = {{QE_AGG_SUM, ACC_SUM_I, &ab}, {QE_AGG_COUNT_STAR, ACC_NONE, nullptr},
+                       {QE_AGG_MIN, ACC_MIN_I, &pa}, {QE_AGG_MAX, ACC_MAX_I, &pb}};
+  rc |= emit_agg(argv[1], "c4", cols, 3, &t4, 1, c4, 4, 12);
+  // nullable key and an fp64 MAX (records carry flags and the global row index)
+  static double fdummy[64];
+  cols[0].validity = vdummy;
+  cols[2].type = QE_TYPE_FLOAT64;
+  cols[2].values = fdummy;
+  cols[2].validity = vdummy;
+  const AggIn fx[2] = {{QE_AGG_MAX, ACC_MAX_F, &pb}, {QE_AGG_COUNT_STAR, ACC_NONE, nullptr}};
+  rc |= emit_agg(argv[1], "f64max", cols, 3, &t4, 1, fx, 2, 11);
   return rc;
 }

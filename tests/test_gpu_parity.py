@@ -628,13 +628,29 @@ def test_hashagg_partitioned(agg_ctx, part_mode, ngroups, expected, vtype):
     assert_groups_equal(result_dict(keys, aggs), ref, ALL_FNS)
 
 
+@pytest.fixture(params=["spill", "twopass"])
+def mp_mode(request, monkeypatch):
+    """Both two-bucket updates: one fused pass that spills the second bucket's rows as records for a
+    partition-aggregate pass (default), and two fused passes (QE_MP_SPILL=0)."""
+    monkeypatch.setenv("QE_MP_SPILL", "1" if request.param == "spill" else "0")
+    return request.param
+
+
+def check_multipass(ctx, st, mode, buckets=2):
+    note = st.last_kernel_kind()[1]
+    if getattr(ctx, "kernel_mode", "jit") == "jit":
+        assert note.startswith("multi-pass"), note
+        if buckets == 2:
+            assert ("spilled" in note) == (mode == "spill"), note
+
+
 MP_I64 = [N.AGG_SUM, N.AGG_COUNT_STAR, N.AGG_MIN, N.AGG_MAX]
 MP_F64 = [N.AGG_SUM, N.AGG_COUNT, N.AGG_MAX]
 
 
 @pytest.mark.parametrize("vtype,ngroups,expected", [("i64", 4500, 4500), ("i64", 40_000, 4000),
                                                     ("f64", 2400, 2400), ("f64", 40_000, 2400)])
-def test_hashagg_multipass(agg_ctx, vtype, ngroups, expected):
+def test_hashagg_multipass(agg_ctx, mp_mode, vtype, ngroups, expected):
     """Expected groups just beyond one LDS table (the specialised kernel's table takes up to
     152 KiB: ~2.5K groups of the i64 shape, ~1.3K of the f64 one): 2 passes of the fused kernel,
     each keeping one bucket of key hashes (also when far more groups turn up than expected:
@@ -655,8 +671,8 @@ def test_hashagg_multipass(agg_ctx, vtype, ngroups, expected):
     for s, e in ((0, 250_001), (250_001, n)):
         st.update([dcol(agg_ctx, N.TYPE_INT64, k[s:e], kv[s:e])],
                   [dcol(agg_ctx, t, x[s:e], None if xv is None else xv[s:e])] * len(fns))
-        if agg_ctx.kernel_mode == "jit" and s == 0:
-            assert st.last_kernel_kind()[1].startswith("multi-pass"), st.last_kernel_kind()
+        if s == 0:
+            check_multipass(agg_ctx, st, mp_mode)
     keys, aggs = st.finalize()
     ref = S.group_aggregate([k], [kv], [x] * len(fns), [xv] * len(fns), fns)
     assert_groups_equal(result_dict(keys, aggs), ref, fns)
@@ -683,7 +699,7 @@ def test_fused_c4_one_pass_large_table(agg_ctx):
     assert_groups_equal(result_dict(kk, aa), ref, C4_FNS)
 
 
-def test_fused_c4_multipass_vs_oracle(agg_ctx):
+def test_fused_c4_multipass_vs_oracle(agg_ctx, mp_mode):
     from kquery.datasource import C4_COLUMNS, ColumnSpec, generate_column
 
     n, groups = 2_000_003, 4000
@@ -691,8 +707,7 @@ def test_fused_c4_multipass_vs_oracle(agg_ctx):
     cols = [generate_column(kspec, n, 0, 42, agg_ctx)] + [generate_column(s, n, 0, 42, agg_ctx) for s in C4_COLUMNS[1:]]
     st = HashAggregateState(agg_ctx, [N.TYPE_INT64], C4_AGGS, groups)
     st.update_fused(cols, _c4_spec())
-    if agg_ctx.kernel_mode == "jit":
-        assert st.last_kernel_kind()[1].startswith("multi-pass"), st.last_kernel_kind()
+    check_multipass(agg_ctx, st, mp_mode)
     kk, aa = st.finalize()
     k, _ = gen.generate(gen.GEN_MOD, groups, 42, 0, 0, n)
     a, _ = gen.generate(gen.GEN_MOD, 1 << 20, 42, 1, 0, n)
