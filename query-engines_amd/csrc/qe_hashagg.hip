@@ -769,68 +769,119 @@ __global__ void __launch_bounds__(1024) k_part_slices(const qi64* __restrict__ o
   if (threadIdx.x == 1023) out[0] = s_sum[1023];
 }
 
-// Chunked scatter -> aggregation slices (one workgroup): counts the claimed chunks and their
-// records per bucket, groups the chunk ids by bucket into `sorted` (order inside a bucket is
-// arbitrary) and cuts each bucket's chunk list into slices of at most cpc chunks, cpc chosen like
-// k_part_slices' cw: 5/4 of an even share of `target` slices, target = max(buckets, min(tmax,
-// records / 32K)). A bucket that is one slice is flagged exclusive. out[0] = slices (at most
-// tmax + buckets).
+// Chunked scatter -> aggregation slices, in three launches over the chunk table meta (meta[0] =
+// chunks C, meta[1 + c] = bucket << 32 | records). One workgroup doing all of it took 250-355 us
+// per update at 1B rows (~250K chunks, LDS atomics on a few counters).
+//   k_chunk_hist   per-workgroup LDS histograms of chunks and records per bucket, added to cnt / rec
+//   k_chunk_slices one workgroup: bucket bases (exclusive scan of cnt) and slices: each bucket's
+//                  chunk list is cut into slices of at most cpc chunks, cpc = 5/4 of an even share
+//                  of target = max(buckets, min(tmax, records / 32K)) slices; a bucket that is one
+//                  slice is flagged exclusive; out[0] = slices (at most tmax + buckets)
+//   k_chunk_place  chunk ids grouped by bucket into `sorted` (per-workgroup LDS ranks, one global
+//                  atomic per (workgroup, bucket) on cur; order inside a bucket is arbitrary)
+// cnt, rec and cur are zeroed by the caller.
 constexpr int CHUNK_PLAN_MAXB = 512;  // buckets of the staged scatter
-__global__ void __launch_bounds__(1024) k_chunk_plan(const qi64* __restrict__ meta, qi32 np, qi64 tmax,
-                                                     qi64* __restrict__ out, qi32* __restrict__ sorted) {
-  __shared__ qu32 s_cnt[CHUNK_PLAN_MAXB], s_base[CHUNK_PLAN_MAXB], s_cur[CHUNK_PLAN_MAXB], s_sl[CHUNK_PLAN_MAXB];
+constexpr int CHUNK_PER_WG = 1024;    // chunks per workgroup of k_chunk_hist / k_chunk_place
+__global__ void __launch_bounds__(256) k_chunk_hist(const qi64* __restrict__ meta, qi32 np, qu32* __restrict__ cnt,
+                                                   unsigned long long* __restrict__ rec) {
+  __shared__ qu32 s_cnt[CHUNK_PLAN_MAXB];
   __shared__ unsigned long long s_rec[CHUNK_PLAN_MAXB];
-  __shared__ qi64 s_cpc;
-  const qi64 C = meta[0];
+  const qi64 C = meta[0], lo = (qi64)blockIdx.x * CHUNK_PER_WG;
+  if (lo >= C) return;
+  const qi64 hi = lo + CHUNK_PER_WG < C ? lo + CHUNK_PER_WG : C;
   for (int b = threadIdx.x; b < np; b += blockDim.x) {
     s_cnt[b] = 0;
-    s_cur[b] = 0;
     s_rec[b] = 0;
   }
   __syncthreads();
-  for (qi64 c = threadIdx.x; c < C; c += blockDim.x) {
+  for (qi64 c = lo + threadIdx.x; c < hi; c += blockDim.x) {
     const qi64 w = meta[1 + c];
     const int b = (int)(w >> 32);
     atomicAdd(&s_cnt[b], 1u);
     atomicAdd(&s_rec[b], (unsigned long long)(w & 0xFFFFFFFFll));
   }
   __syncthreads();
-  if (threadIdx.x == 0) {
-    qi64 R = 0;
-    for (int b = 0; b < np; ++b) R += (qi64)s_rec[b];
-    const qi64 target = max((qi64)np, min(tmax, R >> 15));
-    const qi64 cpc = max((qi64)1, (5 * C + 4 * target - 1) / (4 * target));
-    qu32 base = 0, sl = 0;
-    for (int b = 0; b < np; ++b) {
-      s_base[b] = base;
-      s_sl[b] = sl;
-      base += s_cnt[b];
-      sl += (qu32)((s_cnt[b] + cpc - 1) / cpc);
+  for (int b = threadIdx.x; b < np; b += blockDim.x)
+    if (s_cnt[b]) {
+      atomicAdd(&cnt[b], s_cnt[b]);
+      atomicAdd(&rec[b], s_rec[b]);
     }
-    s_cpc = cpc;
-    out[0] = sl;
-  }
+}
+
+__global__ void __launch_bounds__(1024) k_chunk_slices(const qi64* __restrict__ meta, qi32 np, qi64 tmax,
+                                                      const qu32* __restrict__ cnt,
+                                                      const unsigned long long* __restrict__ rec,
+                                                      qi64* __restrict__ out, qu32* __restrict__ base) {
+  // one thread per bucket (np <= 1024): a tree reduction of the records, then Hillis-Steele scans of
+  // the chunk counts and slice counts (a serial loop over the buckets' global counters took 60 us)
+  __shared__ qu32 s_a[1024], s_b[1024];
+  __shared__ unsigned long long s_r[1024];
+  const int t = threadIdx.x;
+  const qu32 c = t < np ? cnt[t] : 0u;
+  s_r[t] = t < np ? rec[t] : 0ull;
   __syncthreads();
-  const qi64 cpc = s_cpc;
-  for (int b = threadIdx.x; b < np; b += blockDim.x) {
-    const qi64 s0 = s_base[b], e0 = s0 + s_cnt[b];
-    const qi64 ns = (s_cnt[b] + cpc - 1) / cpc;
+  for (int d = 512; d > 0; d >>= 1) {
+    if (t < d) s_r[t] += s_r[t + d];
+    __syncthreads();
+  }
+  const qi64 C = meta[0], R = (qi64)s_r[0];
+  const qi64 target = max((qi64)np, min(tmax, R >> 15));
+  const qi64 cpc = max((qi64)1, (5 * C + 4 * target - 1) / (4 * target));
+  const qu32 ns = (qu32)((c + cpc - 1) / cpc);
+  s_a[t] = c;
+  s_b[t] = ns;
+  __syncthreads();
+  for (int d = 1; d < 1024; d <<= 1) {
+    const qu32 xa = t >= d ? s_a[t - d] : 0u, xb = t >= d ? s_b[t - d] : 0u;
+    __syncthreads();
+    s_a[t] += xa;
+    s_b[t] += xb;
+    __syncthreads();
+  }
+  if (t < np) {
+    const qi64 s0 = s_a[t] - c, e0 = s0 + c, sl = s_b[t] - ns;
+    base[t] = (qu32)s0;
     for (qi64 k = 0; k < ns; ++k) {
       const qi64 lo = s0 + k * cpc;
-      out[2 + 2 * (s_sl[b] + k)] = lo;
-      out[3 + 2 * (s_sl[b] + k)] = (lo + cpc < e0 ? lo + cpc : e0) | (ns == 1 ? PART_EXCL : 0);
+      out[2 + 2 * (sl + k)] = lo;
+      out[3 + 2 * (sl + k)] = (lo + cpc < e0 ? lo + cpc : e0) | (ns == 1 ? PART_EXCL : 0);
     }
   }
-  for (qi64 c = threadIdx.x; c < C; c += blockDim.x) {
-    const int b = (int)(meta[1 + c] >> 32);
-    sorted[s_base[b] + atomicAdd(&s_cur[b], 1u)] = (qi32)c;
+  if (t == 1023) out[0] = s_b[1023];
+}
+
+__global__ void __launch_bounds__(256) k_chunk_place(const qi64* __restrict__ meta, qi32 np,
+                                                    const qu32* __restrict__ base, qu32* __restrict__ cur,
+                                                    qi32* __restrict__ sorted) {
+  constexpr int PER = CHUNK_PER_WG / 256;
+  __shared__ qu32 s_cnt[CHUNK_PLAN_MAXB];
+  const qi64 C = meta[0], lo = (qi64)blockIdx.x * CHUNK_PER_WG;
+  if (lo >= C) return;
+  for (int b = threadIdx.x; b < np; b += blockDim.x) s_cnt[b] = 0;
+  __syncthreads();
+  int bk[PER];
+  qu32 rk[PER];
+#pragma unroll
+  for (int i = 0; i < PER; ++i) {
+    const qi64 c = lo + threadIdx.x + 256 * i;
+    bk[i] = -1;
+    if (c < C) {
+      bk[i] = (int)(meta[1 + c] >> 32);
+      rk[i] = atomicAdd(&s_cnt[bk[i]], 1u);
+    }
   }
+  __syncthreads();
+  for (int b = threadIdx.x; b < np; b += blockDim.x)
+    if (s_cnt[b]) s_cnt[b] = base[b] + atomicAdd(&cur[b], s_cnt[b]);
+  __syncthreads();
+#pragma unroll
+  for (int i = 0; i < PER; ++i)
+    if (bk[i] >= 0) sorted[s_cnt[bk[i]] + rk[i]] = (qi32)(lo + threadIdx.x + 256 * i);
 }
 
 // Slices of the spilled bucket (spill_update): one bucket, so the chunk list is the identity
 // (sorted[c] = c) and slices are ranges of at most cpc chunks, about min(tmax, records / 32K) of
-// them; a single slice is exclusive. Grid: enough threads for every chunk id; k_chunk_plan's one
-// workgroup took 0.32 ms over the ~122K chunks of 1B rows.
+// them; a single slice is exclusive. Grid: enough threads for every chunk id.
 __global__ void k_spill_plan(const qi64* __restrict__ meta, qi64 tmax, qi64* __restrict__ out, qi32* __restrict__ sorted) {
   const qi64 C = meta[0];
   const qi64 c = (qi64)blockIdx.x * blockDim.x + threadIdx.x;
@@ -1863,9 +1914,15 @@ static int partition_rows(qe_hashagg* h, Plan& P, hipFunction_t* fn, int* grid) 
   if (chunked) {
     const int64_t np = (int64_t)1 << log2p;
     // [0] chunks claimed | per chunk (bucket << 32 | records) | chunk ids by bucket (int32)
-    QE_TRY(grow_buffer(&h->part_cnt, &h->part_cnt_bytes, (size_t)(1 + cmax) * 8 + (size_t)cmax * 4, ctx, "chunk table"));
+    // chunk table | sorted chunk ids | plan scratch: cnt u32[np], cur u32[np], base u32[np], rec u64[np]
+    const size_t tbl = ((size_t)(1 + cmax) * 8 + (size_t)cmax * 4 + 7) & ~(size_t)7;
+    QE_TRY(grow_buffer(&h->part_cnt, &h->part_cnt_bytes, tbl + (size_t)np * 20, ctx, "chunk table"));
     qi64* meta = (qi64*)h->part_cnt;
     qi32* sorted = (qi32*)(meta + 1 + cmax);
+    unsigned long long* prec = (unsigned long long*)((uint8_t*)h->part_cnt + tbl);
+    qu32* pcnt = (qu32*)(prec + np);
+    qu32* pcur = pcnt + np;
+    qu32* pbase = pcur + np;
     QE_TRY(grow_buffer(&h->part_rec, &h->part_rec_bytes, (size_t)cmax * PART_CH * rb, ctx, "partition records"));
     const int64_t tmax = (int64_t)ctx->num_cus * 8;
     const int64_t max_slices = tmax + np;
@@ -1882,14 +1939,21 @@ static int partition_rows(qe_hashagg* h, Plan& P, hipFunction_t* fn, int* grid) 
     P.ovf = h->ovf;
     P.ovf_cap = h->ovf_cap;
     QE_HIP(hipMemsetAsync(meta, 0, 8, ctx->stream));
+    QE_HIP(hipMemsetAsync(prec, 0, (size_t)np * 16, ctx->stream));  // rec, cnt, cur
     P.part_tw = tw;
     P.part_rec = h->part_rec;
     P.part_chunk = meta;
     QE_TRY(jit_launch(ctx, fs, (int)g, P, sblock));
     QE_TRY(launch_check("qe_pscatter"));
-    hipLaunchKernelGGL(k_chunk_plan, dim3(1), dim3(1024), 0, ctx->stream, (const qi64*)meta, (qi32)np, (qi64)tmax,
-                       (qi64*)h->part_slc, sorted);
-    QE_TRY(launch_check("k_chunk_plan"));
+    const unsigned pg = (unsigned)div_up((uint64_t)cmax, CHUNK_PER_WG);
+    hipLaunchKernelGGL(k_chunk_hist, dim3(pg), dim3(256), 0, ctx->stream, (const qi64*)meta, (qi32)np, pcnt, prec);
+    QE_TRY(launch_check("k_chunk_hist"));
+    hipLaunchKernelGGL(k_chunk_slices, dim3(1), dim3(1024), 0, ctx->stream, (const qi64*)meta, (qi32)np, (qi64)tmax,
+                       (const qu32*)pcnt, (const unsigned long long*)prec, (qi64*)h->part_slc, pbase);
+    QE_TRY(launch_check("k_chunk_slices"));
+    hipLaunchKernelGGL(k_chunk_place, dim3(pg), dim3(256), 0, ctx->stream, (const qi64*)meta, (qi32)np,
+                       (const qu32*)pbase, pcur, sorted);
+    QE_TRY(launch_check("k_chunk_place"));
     P.n = cmax * PART_CH;
     P.part_slice = (qi64*)h->part_slc;
     P.part_sorted = sorted;
