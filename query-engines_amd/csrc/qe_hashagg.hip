@@ -2222,9 +2222,13 @@ static int spill_update(qe_hashagg* h, Plan& P, size_t lds, int64_t rows, bool* 
   QE_TRY(ensure_defer(h, cmax * PART_CH));  // the aggregation pass's retry bitmaps index record slots
   *used = true;
   QE_HIP(hipMemsetAsync(meta, 0, 8, ctx->stream));
-  // kept share: as many groups as one LDS table holds at the multi-pass load (5/8), the rest spilled
-  // (4096 expected groups of the C4 shape: 62.5 % kept, so 3/4 of the records of an even split)
-  const double keep = std::min(1.0, (double)(((int64_t)1 << P.lds_log2) * 5 / 8) / (double)std::max<int64_t>(1, h->expected_groups));
+  // kept share: as many groups as one LDS table holds at a 6/8 load, the rest spilled (4096
+  // expected groups of the C4 shape: 75 % kept, half the records of an even split). QE_SPILL_LOAD
+  // (eighths, 4..7, read per call); 1B rows, 4096 / 5000 groups: 5/8 7.27 / 8.12 ms, 6/8 6.56 /
+  // 7.85, 7/8 6.62 / 10.79
+  const char* le = getenv("QE_SPILL_LOAD");
+  const int load8 = le && *le ? std::max(4, std::min(7, atoi(le))) : 6;
+  const double keep = std::min(1.0, (double)(((int64_t)1 << P.lds_log2) * load8 / 8) / (double)std::max<int64_t>(1, h->expected_groups));
   P.mp_keep = (qu64)(keep * 4294967296.0);
   P.part_rec = h->part_rec;
   P.part_chunk = meta;
