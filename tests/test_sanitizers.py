@@ -11,6 +11,7 @@ UndefinedBehaviorSanitizer, on the CPU.
 A sanitizer report makes the driver exit non-zero (-fno-sanitize-recover for UBSan), which fails
 the test. GPU code is not sanitized (no GPU ASan on this pool); the device paths get the
 run-to-run determinism check in test_determinism.py instead."""
+import fcntl
 import os
 import pathlib
 import random
@@ -30,7 +31,12 @@ ENV = dict(os.environ, ASAN_OPTIONS="detect_leaks=1:abort_on_error=0:exitcode=23
 
 @pytest.fixture(scope="module")
 def drivers():
-    r = subprocess.run(["make", "-s", "-C", str(NATIVE), "san"], capture_output=True, text=True)
+    # one build at a time: under pytest-xdist another worker may be running the binaries that a
+    # concurrent make would relink ("Text file busy")
+    (NATIVE / "_build").mkdir(exist_ok=True)
+    with open(NATIVE / "_build" / ".lock", "w") as lock:
+        fcntl.flock(lock, fcntl.LOCK_EX)
+        r = subprocess.run(["make", "-s", "-C", str(NATIVE), "san"], capture_output=True, text=True)
     if r.returncode != 0:
         pytest.skip("sanitizer build unavailable: " + r.stderr[-400:])
     return NATIVE / "_build" / "san_cast", NATIVE / "_build" / "san_oracle"
