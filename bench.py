@@ -54,12 +54,35 @@ def _cpu_lib():
     return lib, G
 
 
+def cpu_model() -> str:
+    """The host CPU's model name (what `lscpu` prints as "Model name"), from /proc/cpuinfo."""
+    try:
+        for ln in open("/proc/cpuinfo"):
+            if ln.lower().startswith("model name"):
+                return ln.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def cgroup_cpus():
+    """CPUs the cgroup quota allows (cpu.max), or None when unlimited / unreadable."""
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        return None if q == "max" else round(int(q) / int(per), 2)
+    except (OSError, ValueError):
+        return None
+
+
 def cpu_baseline(sample_rows: int, threads: int):
     """Timed CPU legs (rank 0, N = 1) on bounded samples of the same rows:
-    * `value`: the oracle's reference-faithful C restatement of the query (oracle/cpu_baseline.c:
-      row-at-a-time Selection -> Projection -> HashMap aggregate with boxed keys and virtual
-      accumulators, partition-parallel like Main.kt:1309-1325) on `threads` threads;
-    * `single_thread`: the same port on one thread (SURVEY §8d: 1 thread and all threads);
+    * `value`: the oracle's C restatement of the reference operator chain (oracle/cpu_baseline.c:
+      row-at-a-time Selection -> Projection -> HashMap aggregate whose keys are per-row List +
+      boxed Long objects from a per-thread bump allocator, boxed accumulator inputs through virtual
+      accumulators, partition-parallel like Main.kt:1309-1325) on `threads` threads — every core
+      this process may run on (os.sched_getaffinity);
+    * `threads_16`: the same at 16 threads (the GPU box's CPU share per GPU);
+    * `single_thread`: the same on one thread (SURVEY §8d: 1 thread and all threads);
     * `tuned`: a tuned C implementation (no boxing or materialisation, per-thread open-addressing
       tables), so the GPU is also compared with a fast CPU engine.
     Returns (the port's groups over the sample, key -> (SUM, COUNT, MIN, MAX); the JSON object)."""
@@ -70,10 +93,14 @@ def cpu_baseline(sample_rows: int, threads: int):
     groups = {int(g.key): (int(g.sum), int(g.count), int(g.min), int(g.max)) for g in out[:ng.value]}
     one_rows = min(sample_rows, 100_000_000)
     secs1 = lib.qe_cpu_c4(0, one_rows, 42, 1, 1 << 19, 1024, out, 2048, C.byref(ng))
+    secs16 = lib.qe_cpu_c4(0, sample_rows, 42, 16, 1 << 19, 1024, out, 2048, C.byref(ng)) if threads != 16 else secs
     secs_t = lib.qe_cpu_c4_fast(0, sample_rows, 42, threads, 1 << 19, 1024, out, 2048, C.byref(ng))
     return groups, {"value": sample_rows / secs, "unit": "rows/s", "cores": threads, "kind": "port",
-            "sample": f"rows 0..{sample_rows - 1} of the same C4 table (seed 42), {threads} threads, "
-                      f"{secs:.3f} s; C restatement of the reference operator chain (oracle/cpu_baseline.c)",
+            "cpu_model": cpu_model(), "cgroup_cpus": cgroup_cpus(),
+            "sample": f"rows 0..{sample_rows - 1} of the same C4 table (seed 42), {threads} threads "
+                      f"(all of sched_getaffinity), {secs:.3f} s; C restatement of the reference operator chain "
+                      "with per-row boxed key List / Long objects (oracle/cpu_baseline.c)",
+            "threads_16": {"value": sample_rows / secs16, "cores": 16, "sample": f"same rows, 16 threads, {secs16:.3f} s"},
             "single_thread": {"value": one_rows / secs1, "cores": 1,
                               "sample": f"rows 0..{one_rows - 1}, 1 thread, {secs1:.3f} s"},
             "tuned": ({"value": sample_rows / secs_t, "cores": threads,
@@ -81,19 +108,68 @@ def cpu_baseline(sample_rows: int, threads: int):
                                  "per-thread open-addressing tables (qe_cpu_c4_fast)"} if secs_t > 0 else None)}
 
 
+# sources the specialised C4 kernel is generated from (qe_jit.hip emits it, including qe_dev.hpp;
+# qe_hashagg.hip sizes the table and the launch): profiles/traffic.json is valid for these bytes only
+TRAFFIC_SOURCES = ("query-engines_amd/csrc/qe_jit.hip", "query-engines_amd/csrc/qe_dev.hpp",
+                   "query-engines_amd/csrc/qe_hashagg.hip")
+
+
+def kernel_source_hash() -> str:
+    import hashlib
+
+    h = hashlib.sha256()
+    for rel in TRAFFIC_SOURCES:
+        h.update(rel.encode() + b"\0" + (ROOT / rel).read_bytes() + b"\0")
+    return h.hexdigest()[:16]
+
+
 def load_traffic(rows: int):
-    """HBM bytes per fused-kernel launch from the committed rocprofv3 PMC summary (profiles/),
-    FETCH_SIZE doubled per MI355X_MICROARCH.md §HBM (gfx950 counts half of wide streaming reads)."""
+    """HBM bytes per fused-kernel launch from the committed rocprofv3 PMC summary
+    (profiles/traffic.json, written by profiles/summarize.py; FETCH_SIZE doubled per
+    MI355X_MICROARCH.md §HBM: gfx950 counts half of wide streaming reads). Used only when it was
+    measured at these rows on kernel sources identical to this tree's (kernel_source_hash): a
+    kernel change leaves `traffic` null until the PMC passes are re-run. Returns (bytes, note)."""
     p = ROOT / "profiles" / "traffic.json"
     if not p.exists():
-        return None
+        return None, "no profiles/traffic.json"
     try:
         t = json.loads(p.read_text())
-        if int(t.get("rows", -1)) == rows:
-            return float(t["hbm_bytes_per_launch"])
-    except Exception:
-        return None
-    return None
+    except ValueError:
+        return None, "unreadable profiles/traffic.json"
+    if int(t.get("rows", -1)) != rows:
+        return None, f"profiles/traffic.json is for {t.get('rows')} rows"
+    have, want = t.get("kernel_source_hash"), kernel_source_hash()
+    if have != want:
+        return None, f"stale: profiles/traffic.json measured on kernel sources {have}, tree has {want}"
+    return float(t["hbm_bytes_per_launch"]), (f"profiles/traffic.json (rocprofv3 FETCH_SIZE x2 + WRITE_SIZE, "
+                                              f"sources {have}, git {t.get('git_head', '?')})")
+
+
+def launch_ranks(args) -> int:
+    """`bench.py --gpus N` without a launcher: start N ranks with torch.distributed.run as a child
+    process (this process never touches the GPU, so no exec after GPU init), pass rank 0's JSON
+    line through, and return the child's exit code. With nccl (RCCL) each rank needs its own GPU:
+    fewer visible GPUs than N is an error, never a silent 1-rank run. gloo may rehearse N ranks on
+    fewer GPUs (ranks then share devices)."""
+    import socket
+    import subprocess
+
+    if args.dist_backend == "nccl":
+        import torch  # device_count() does not initialise HIP on this image
+
+        have = torch.cuda.device_count()
+        if have < args.gpus:
+            print(f"bench: --gpus {args.gpus} needs {args.gpus} visible GPUs for one RCCL rank each, found {have} "
+                  "(--dist-backend gloo rehearses more ranks than GPUs)", file=sys.stderr)
+            return 2
+    with socket.socket() as so:
+        so.bind(("127.0.0.1", 0))
+        port = so.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+           "--master-addr=127.0.0.1", f"--master-port={port}", str(pathlib.Path(__file__).resolve())] + sys.argv[1:]
+    env = dict(os.environ)
+    env.setdefault("OMP_NUM_THREADS", "4")
+    return subprocess.run(cmd, env=env).returncode
 
 
 def main():
@@ -101,7 +177,7 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--rows", type=int, default=1_000_000_000, help="rows per GPU")
+    ap.add_argument("--rows", type=lambda v: int(float(v)), default=1_000_000_000, help="rows per GPU (1e9 ok)")
     ap.add_argument("--cpu-sample-rows", type=int, default=0, help="default: the same rows as one GPU")
     ap.add_argument("--cpu-threads", type=int, default=0)
     ap.add_argument("--no-cpu", action="store_true")
@@ -113,7 +189,16 @@ def main():
     ap.add_argument("--dist-backend", default="nccl",
                     help="torch.distributed backend (nccl = RCCL over xGMI; gloo only to rehearse N > 1 "
                          "ranks sharing one GPU)")
+    ap.add_argument("--slot-records", type=int, default=0,
+                    help="N > 1: records per exchange slot (0: qe_hashagg_slot_capacity); a small value forces "
+                         "the variable-size fallback")
+    ap.add_argument("--verify-cpu", action="store_true",
+                    help="N > 1: rank 0 checks every owner's groups against the CPU port over all ranks' rows")
     args = ap.parse_args()
+
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        # one process per GPU: this process only launches them (no torch, no GPU call here)
+        return launch_ranks(args)
 
     import torch
     import torch.distributed as dist
@@ -128,8 +213,11 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
         print(f"warning: --gpus {args.gpus} but WORLD_SIZE {world}; using WORLD_SIZE", file=sys.stderr)
+    ndev = torch.cuda.device_count()
+    if world > 1 and args.dist_backend == "nccl" and ndev < world:
+        sys.exit(f"bench: {world} RCCL ranks need {world} visible GPUs, found {ndev}")
     # one rank per GPU; more ranks than GPUs only in a gloo rehearsal (ranks then share devices)
-    device = local % max(1, torch.cuda.device_count())
+    device = local % max(1, ndev)
     torch.cuda.set_device(device)
     if world > 1 or args.exchange:
         for k, v in (("MASTER_ADDR", "127.0.0.1"), ("MASTER_PORT", "29511"), ("RANK", "0"), ("WORLD_SIZE", "1")):
@@ -138,6 +226,8 @@ def main():
             dist.init_process_group("nccl", device_id=torch.device("cuda", device))
         else:
             dist.init_process_group(args.dist_backend)
+        world = dist.get_world_size()
+        rank = dist.get_rank()
     from kquery.exchange import NativeComm, exchange_partials, exchange_partials_native
 
     ctx = Context.get(device)
@@ -155,7 +245,9 @@ def main():
     comm = NativeComm(ctx) if exchange and args.exchange_impl == "native" else None
     spec = c4_spec(N)
     kernel_ms = []
+    exch_ev = []  # (after the update is queued, after the owner's import) per timed step
     kinds = []
+    timing = [False]
 
     def step():
         partial.reset()
@@ -163,11 +255,17 @@ def main():
         partial.update_fused(cols, spec)
         final = partial
         if exchange:
+            if timing[0]:
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record()
             owner.reset()
             if comm is not None:
-                exchange_partials_native(partial, owner, comm)
+                exchange_partials_native(partial, owner, comm, args.slot_records)
             else:
-                exchange_partials(partial, owner)
+                exchange_partials(partial, owner, slot_records=args.slot_records or None)
+            if timing[0]:
+                e1.record()
+                exch_ev.append((e0, e1))
             final = owner
         out = final.finalize()
         kernel_ms.append(partial.last_kernel_time())
@@ -183,6 +281,7 @@ def main():
     kernel_ms.clear()
     barrier()
     torch.cuda.synchronize()
+    timing[0] = True
     t0 = time.perf_counter()
     for _ in range(args.steps):
         keys, res = step()
@@ -190,19 +289,27 @@ def main():
     kinds.append(partial.last_kernel_kind())
     barrier()
     elapsed = time.perf_counter() - t0
+    timing[0] = False
+    launches = sum(k for _, k in kernel_ms)
+    avg_kernel_ms = sum(m for m, _ in kernel_ms) / max(1, launches)
+    # exchange leg on the device timeline: from the aggregation kernel's queue position to the end
+    # of the owner's import (waits for the slowest peer's kernel inside the all-to-all)
+    avg_exch_ms = (sum(a.elapsed_time(b) for a, b in exch_ev) / len(exch_ev)) if exch_ev else None
     if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+        t = torch.tensor([elapsed, avg_kernel_ms, avg_exch_ms or 0.0], dtype=torch.float64, device="cuda")
+        if args.dist_backend == "gloo":
+            t = t.cpu()
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+        elapsed, max_kernel_ms, avg_exch_ms = (float(x) for x in t.tolist())
+    else:
+        max_kernel_ms = avg_kernel_ms
 
-    # stream-read ceiling over the same 24 B/row (k, a, b), median of 5
+    # stream-read ceiling over the same 24 B/row (k, a, b): best launch shape, median of 5 each
     cc = (N.QeColumn * 3)(*[c.as_c() for c in cols])
-    sr = []
-    for _ in range(5):
-        ms = C.c_double()
-        N.check(N.lib().qe_stream_read(ctx.handle, cc, 3, C.byref(ms)))
-        sr.append(ms.value)
-    stream_gbs = rows * BYTES_PER_ROW / (sorted(sr)[2] * 1e-3) / 1e9
+    ms = C.c_double()
+    shape = C.create_string_buffer(128)
+    N.check(N.lib().qe_stream_read_best(ctx.handle, cc, 3, 5, C.byref(ms), shape, 128))
+    stream_gbs = rows * BYTES_PER_ROW / (ms.value * 1e-3) / 1e9
 
     # Result checks before any number is printed: every group present once across owners, and
     # COUNT(*) adds up to the rows an independent torch kernel counts as passing the predicate.
@@ -210,24 +317,52 @@ def main():
     selected = int((a_col > (1 << 19)).sum().item())
     groups = torch.tensor([keys[0].length, int(res[1].to_numpy().sum()), selected], dtype=torch.int64, device="cuda")
     if world > 1:
+        if args.dist_backend == "gloo":
+            groups = groups.cpu()
         dist.all_reduce(groups)
     n_groups, count_total, selected_total = (int(x) for x in groups.tolist())
     if n_groups != 1024 or count_total != selected_total:
         sys.exit(f"bench: wrong result: {n_groups} groups (want 1024), COUNT(*) total {count_total} "
                  f"(want {selected_total})")
+    kv = keys[0].to_numpy()
+    rv = [r.to_numpy() for r in res]
+    my_groups = {int(kv[i]): tuple(int(r[i]) for r in rv) for i in range(keys[0].length)}
+    check = {"groups": n_groups, "count_star_total": count_total, "count_star_torch": selected_total}
+    if world > 1 and args.verify_cpu:
+        # union of the owners' groups == the CPU port over every rank's rows (rows 0 .. world*rows)
+        everyone = [None] * world
+        dist.all_gather_object(everyone, my_groups)
+        if rank == 0:
+            union = {}
+            for g in everyone:
+                for k, v in g.items():
+                    if k in union:
+                        sys.exit(f"bench: group {k} owned by two ranks")
+                    union[k] = v
+            lib, G = _cpu_lib()
+            out = (G * 2048)()
+            ng = C.c_int64()
+            lib.qe_cpu_c4(0, world * rows, 42, len(os.sched_getaffinity(0)), 1 << 19, 1024, out, 2048, C.byref(ng))
+            want = {int(g.key): (int(g.sum), int(g.count), int(g.min), int(g.max)) for g in out[:ng.value]}
+            if union != want:
+                bad = sorted(k for k in set(union) | set(want) if union.get(k) != want.get(k))
+                sys.exit(f"bench: {len(bad)} groups differ from the CPU port over all ranks' rows, e.g. key {bad[0]}: "
+                         f"gpu {union.get(bad[0])} cpu {want.get(bad[0])}")
+            check["cpu_port_groups_equal_all_ranks"] = True
     ms_step = elapsed / args.steps * 1e3
-    launches = sum(k for _, k in kernel_ms)
-    avg_kernel_ms = sum(m for m, _ in kernel_ms) / max(1, launches)
     achieved = rows * BYTES_PER_ROW / (avg_kernel_ms * 1e-3) / 1e9
-    traffic = load_traffic(rows)
+    traffic, traffic_note = load_traffic(rows)
     line = {
         "metric": METRIC,
         "value": world * rows / (ms_step * 1e-3),
         "unit": "rows/s",
         "n_gpus": world,
+        "world_size": world,
         "steps": args.steps,
         "warmup": args.warmup,
         "ms_per_step": ms_step,
+        "kernel_ms": max_kernel_ms,
+        "exchange_ms": avg_exch_ms,
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
@@ -250,27 +385,26 @@ def main():
             "unit": "GB/s",
             "frac": achieved / HBM_PEAK_GBS,
             "traffic": traffic,
+            "traffic_source": traffic_note,
             "kernel": ("qe_fused (hipRTC plan-specialised filter+project+LDS hash aggregate)" if kinds[-1][0]
                        else f"k_hashagg generic interpreter ({kinds[-1][1]})"),
             "avg_kernel_ms": avg_kernel_ms,
             "bytes_per_launch": rows * BYTES_PER_ROW,
             "stream_read_ceiling_gbs": stream_gbs,
+            "stream_read_ceiling_shape": shape.value.decode(),
         },
-        "check": {"groups": n_groups, "count_star_total": count_total, "count_star_torch": selected_total},
+        "check": check,
     }
     if rank == 0 and world == 1 and not args.no_cpu:
-        threads = args.cpu_threads or min(16, os.cpu_count() or 1)
+        threads = args.cpu_threads or len(os.sched_getaffinity(0))
         sample = args.cpu_sample_rows or rows
         cpu_groups, line["cpu_baseline"] = cpu_baseline(sample, threads)
         if sample == rows:
             # the CPU port ran over exactly these rows: every group's SUM/COUNT/MIN/MAX must agree
-            kv = keys[0].to_numpy()
-            rv = [r.to_numpy() for r in res]
-            gpu_groups = {int(kv[i]): tuple(int(r[i]) for r in rv) for i in range(keys[0].length)}
-            if gpu_groups != cpu_groups:
-                bad = sorted(k for k in set(gpu_groups) | set(cpu_groups) if gpu_groups.get(k) != cpu_groups.get(k))
+            if my_groups != cpu_groups:
+                bad = sorted(k for k in set(my_groups) | set(cpu_groups) if my_groups.get(k) != cpu_groups.get(k))
                 sys.exit(f"bench: {len(bad)} groups differ from the CPU port, e.g. key {bad[0]}: "
-                         f"gpu {gpu_groups.get(bad[0])} cpu {cpu_groups.get(bad[0])}")
+                         f"gpu {my_groups.get(bad[0])} cpu {cpu_groups.get(bad[0])}")
             line["check"]["cpu_port_groups_equal"] = True
     if rank == 0:
         print(json.dumps(line), flush=True)
@@ -278,7 +412,8 @@ def main():
         comm.close()
     if dist.is_initialized():
         dist.destroy_process_group()
+    return 0
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main())

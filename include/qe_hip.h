@@ -155,6 +155,12 @@ int qe_generate(qe_ctx* ctx, qe_column* out, int32_t dist, int64_t param, uint64
  * fixed-width columns with 16-B loads — the achievable stream-read ceiling for the bytes a
  * query scans (reported next to the roofline). */
 int qe_stream_read(qe_ctx* ctx, const qe_column* cols, int32_t ncols, double* ms);
+/* The same ceiling taken over several launch shapes (row-interleaved or column-serial, 1-4 slabs
+ * per step, 256-1024 threads, 1-8 workgroups per CU, non-temporal or cached loads): `reps` launches
+ * per shape, the best shape's median in *ms and its description in `shape`. This is the bound
+ * bench.py reports beside the fused kernel. */
+int qe_stream_read_best(qe_ctx* ctx, const qe_column* cols, int32_t ncols, int32_t reps, double* ms,
+                        char* shape, int32_t shape_len);
 
 /* ---- vectorised expressions: Expression.evaluate (K:448-450) ---------------------------- */
 #define QE_OP_ADD 1
@@ -342,6 +348,16 @@ typedef struct qe_select_spec {
 } qe_select_spec;
 int qe_select_project(qe_ctx* ctx, const qe_column* cols, int32_t ncols, const qe_select_spec* spec,
                       qe_column* outs, int64_t* out_count);
+/* Stream-ordered form (a pipelined SelectionExec -> ProjectionExec over a Sequence<RecordBatch>,
+ * K:589-594): queues the kernels and the copy of the row count into pinned memory, and returns
+ * without waiting. *pending must be passed to qe_select_pending_wait exactly once (it frees it);
+ * that call waits for this select-project's kernels only — not for work queued behind them, such
+ * as the next batch's select-project — and returns the row count. The inputs must stay valid and
+ * the outputs unread until then. qe_select_project = async + wait. */
+typedef struct qe_select_pending qe_select_pending;
+int qe_select_project_async(qe_ctx* ctx, const qe_column* cols, int32_t ncols, const qe_select_spec* spec,
+                            qe_column* outs, qe_select_pending** pending);
+int qe_select_pending_wait(qe_select_pending* pending, int64_t* out_count);
 
 /* Number of groups so far (synchronises). */
 int qe_hashagg_num_groups(qe_hashagg* agg, int64_t* out);
@@ -386,6 +402,10 @@ int qe_hashagg_import(qe_hashagg* agg, const void* records, int64_t nrecords);
 int qe_hashagg_export_slots(qe_hashagg* agg, int32_t nparts, int64_t slot_records, void* dst);
 int qe_hashagg_import_slots(qe_hashagg* agg, const void* slots, int32_t nslots, int64_t slot_records,
                             int64_t* max_count, int64_t* nrecords);
+/* Default slot capacity for a `world`-rank exchange: the expected groups given to
+ * qe_hashagg_create (never the sizing hint a rank's own data raised) spread over the ranks with
+ * headroom — min(eg, ceil(3 eg / 2 world) + 32) — so every rank computes the same slot size. */
+int qe_hashagg_slot_capacity(qe_hashagg* agg, int32_t world, int64_t* slot_records);
 
 /* Stream-ordered updates (default 0 = off). With `enable`, an update that needs one kernel launch
  * returns once it is queued; the read-back of its counters — and, when the global table had to

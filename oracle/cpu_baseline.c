@@ -6,9 +6,11 @@
  * as the reference's operator chain would execute it (folkol/query-engines kquerydiy/src/Main.kt):
  *   - per input batch, SelectionExec materialises the selected rows (build-defined operator),
  *   - ProjectionExec evaluates a+b into a new column (K:589-594),
- *   - HashAggregateExec.execute loops row at a time (K:620), looks the key tuple up in a chained
- *     hash map (java.util.HashMap, K:616/K:627: boxed key, bucket array, node per group) and calls
- *     each Accumulator through a virtual interface (K:519-522, K:628-631) with boxed values.
+ *   - HashAggregateExec.execute loops row at a time (K:620): it builds the row's key as a List of
+ *     boxed values (K:621-626; ArrayList + Object[] + java.lang.Long from a per-thread bump
+ *     allocator that is collected after each batch), looks it up in a chained hash map
+ *     (java.util.HashMap, K:616/K:627: List.hashCode / List.equals, node per group) and calls each
+ *     Accumulator through a virtual interface (K:519-522, K:628-631) with a boxed Long per input.
  *   - partition parallelism mirrors main() (K:1309-1325): T partitions aggregated concurrently,
  *     then a final merge of the partial maps.
  * The synthetic columns are regenerated here bit-for-bit (splitmix64, oracle/gen.py) before the
@@ -30,36 +32,98 @@ static uint64_t gen_u64(uint64_t seed, uint64_t col, uint64_t row) {
   return splitmix64(seed ^ (col * 0x9E3779B97F4A7C15ull) ^ row);
 }
 
-/* ---- boxed values and the Accumulator interface (K:519-522) ------------------------------ */
+/* ---- JVM object model the reference's row loop allocates (K:620-631) ----------------------------
+ * Per selected row the reference builds the group key as a Kotlin List of boxed values
+ * (`groupKeys.map { it.getValue(rowIndex) }`, K:621-626: an ArrayList plus its Object[] plus a
+ * java.lang.Long per key value), and passes every aggregate input to its Accumulator boxed
+ * (`aggrInputValues[i].getValue(rowIndex)`, K:628-631). Those objects come from the thread's
+ * allocation buffer (bump pointer) and die young: here a per-thread arena that is reset after
+ * every input batch (a minor collection whose survivors are only the map's keys, copied out on
+ * insert). Long.valueOf's cache of -128..127 is modelled (no allocation for those values). */
 typedef struct {
-  int is_null;
+  uint64_t hdr; /* mark + class words of a JVM object header, compressed */
   int64_t v;
-} boxed;
+} jlong_box; /* java.lang.Long */
 
+typedef struct {
+  uint64_t hdr;
+  int32_t len, pad;
+  jlong_box* e[1];
+} jarray1; /* Object[1] */
+
+typedef struct {
+  uint64_t hdr;
+  int32_t size, modcount;
+  jarray1* data;
+} jlist; /* java.util.ArrayList of one key */
+
+typedef struct {
+  char* base;
+  size_t off, cap;
+} arena;
+
+static jlong_box g_long_cache[256]; /* Long.valueOf cache, -128..127 */
+static pthread_once_t g_cache_once = PTHREAD_ONCE_INIT;
+static void init_long_cache(void) {
+  for (int i = 0; i < 256; ++i) g_long_cache[i] = (jlong_box){0x1ull, (int64_t)i - 128};
+}
+
+static void* arena_alloc(arena* a, size_t n) {
+  n = (n + 7) & ~(size_t)7;
+  if (a->off + n > a->cap) { /* eden full mid-batch: a collection (nothing of earlier rows is live) */
+    a->off = 0;
+  }
+  void* p = a->base + a->off;
+  a->off += n;
+  return p;
+}
+
+static jlong_box* box_long(arena* a, int64_t v) { /* Long.valueOf */
+  if (v >= -128 && v <= 127) return &g_long_cache[v + 128];
+  jlong_box* b = (jlong_box*)arena_alloc(a, sizeof(jlong_box));
+  b->hdr = 0x1ull;
+  b->v = v;
+  return b;
+}
+
+static jlist* key_list(arena* a, jlong_box* k) { /* listOf(boxed key) built by map { } */
+  jarray1* arr = (jarray1*)arena_alloc(a, sizeof(jarray1));
+  arr->hdr = 0x1ull;
+  arr->len = 1;
+  arr->e[0] = k;
+  jlist* l = (jlist*)arena_alloc(a, sizeof(jlist));
+  l->hdr = 0x1ull;
+  l->size = 1;
+  l->modcount = 0;
+  l->data = arr;
+  return l;
+}
+
+/* ---- the Accumulator interface (K:519-522), inputs boxed (null = NULL pointer) --------------- */
 typedef struct accumulator accumulator;
 struct accumulator {
-  void (*accumulate)(accumulator*, const boxed*);
+  void (*accumulate)(accumulator*, const jlong_box*);
   int has;
   int64_t value;
 };
 
-static void sum_acc(accumulator* a, const boxed* x) {
-  if (x->is_null) return;
+static void sum_acc(accumulator* a, const jlong_box* x) {
+  if (!x) return;
   a->value = (int64_t)((uint64_t)a->value + (uint64_t)x->v);
   a->has = 1;
 }
-static void count_acc(accumulator* a, const boxed* x) {
+static void count_acc(accumulator* a, const jlong_box* x) {
   (void)x;
   a->value += 1;
   a->has = 1;
 }
-static void min_acc(accumulator* a, const boxed* x) {
-  if (x->is_null) return;
+static void min_acc(accumulator* a, const jlong_box* x) {
+  if (!x) return;
   if (!a->has || x->v < a->value) a->value = x->v;
   a->has = 1;
 }
-static void max_acc(accumulator* a, const boxed* x) { /* MaxAccumulator K:540-557 */
-  if (x->is_null) return;
+static void max_acc(accumulator* a, const jlong_box* x) { /* MaxAccumulator K:540-557 */
+  if (!x) return;
   if (!a->has) {
     a->value = x->v;
     a->has = 1;
@@ -68,9 +132,9 @@ static void max_acc(accumulator* a, const boxed* x) { /* MaxAccumulator K:540-55
   }
 }
 
-/* ---- java.util.HashMap-like chained map keyed by the boxed key tuple (K:616, K:627) --------- */
+/* ---- java.util.HashMap<List<Any?>, List<Accumulator>> (K:616, K:627) --------------------------- */
 typedef struct node {
-  boxed key;
+  jlist* key; /* survivor copy of the row's key list */
   uint32_t hash;
   struct node* next;
   accumulator acc[4];
@@ -82,9 +146,37 @@ typedef struct {
   size_t size;
 } hashmap;
 
-static uint32_t box_hash(const boxed* k) { /* Long.hashCode + HashMap.hash spreading */
-  uint32_t h = k->is_null ? 0u : (uint32_t)(k->v ^ ((uint64_t)k->v >> 32));
+static uint32_t list_hash(const jlist* k) { /* List.hashCode (31 * 1 + Long.hashCode) + HashMap.hash */
+  uint32_t h = 1;
+  for (int32_t i = 0; i < k->size; ++i) {
+    const jlong_box* e = k->data->e[i];
+    h = 31u * h + (e ? (uint32_t)(e->v ^ ((uint64_t)e->v >> 32)) : 0u);
+  }
   return h ^ (h >> 16);
+}
+
+static int list_equals(const jlist* x, const jlist* y) { /* List.equals -> Long.equals per element */
+  if (x->size != y->size) return 0;
+  for (int32_t i = 0; i < x->size; ++i) {
+    const jlong_box *a = x->data->e[i], *b = y->data->e[i];
+    if ((a == NULL) != (b == NULL)) return 0;
+    if (a && a->v != b->v) return 0;
+  }
+  return 1;
+}
+
+static jlist* list_survivor(const jlist* k) { /* the key object outlives the batch: copy it out */
+  jlist* l = (jlist*)malloc(sizeof(jlist) + sizeof(jarray1) + sizeof(jlong_box));
+  jarray1* arr = (jarray1*)(l + 1);
+  jlong_box* b = (jlong_box*)(arr + 1);
+  *l = *k;
+  l->data = arr;
+  *arr = *k->data;
+  if (k->data->e[0]) {
+    *b = *k->data->e[0];
+    arr->e[0] = b;
+  }
+  return l;
 }
 
 static void map_init(hashmap* m) {
@@ -111,13 +203,13 @@ static void map_grow(hashmap* m) {
   m->nbuckets = nb;
 }
 
-static node* map_get_or_put(hashmap* m, const boxed* key) {
-  uint32_t h = box_hash(key);
+static node* map_get_or_put(hashmap* m, const jlist* key) {
+  uint32_t h = list_hash(key);
   node* n = m->buckets[h & (m->nbuckets - 1)];
   for (; n; n = n->next)
-    if (n->hash == h && n->key.is_null == key->is_null && (key->is_null || n->key.v == key->v)) return n;
+    if (n->hash == h && list_equals(n->key, key)) return n;
   n = (node*)calloc(1, sizeof(node));
-  n->key = *key;
+  n->key = list_survivor(key);
   n->hash = h;
   n->acc[0].accumulate = sum_acc;
   n->acc[1].accumulate = count_acc;
@@ -135,6 +227,7 @@ static void map_free(hashmap* m) {
     node* n = m->buckets[i];
     while (n) {
       node* nx = n->next;
+      free(n->key);
       free(n);
       n = nx;
     }
@@ -142,8 +235,11 @@ static void map_free(hashmap* m) {
   free(m->buckets);
 }
 
+static int64_t key_of(const node* n) { return n->key->data->e[0]->v; }
+
 /* ---- one partition: batches of BATCH rows through Selection -> Projection -> HashAggregate ---- */
 #define BATCH 65536
+#define EDEN_BYTES ((size_t)16 << 20)
 
 typedef struct {
   const int64_t *k, *a, *b;
@@ -152,10 +248,12 @@ typedef struct {
 } part;
 
 static void run_partition(part* p) {
+  pthread_once(&g_cache_once, init_long_cache);
   int64_t* sk = (int64_t*)malloc(BATCH * sizeof(int64_t));
   int64_t* sa = (int64_t*)malloc(BATCH * sizeof(int64_t));
   int64_t* sb = (int64_t*)malloc(BATCH * sizeof(int64_t));
   int64_t* proj = (int64_t*)malloc(BATCH * sizeof(int64_t));
+  arena eden = {(char*)malloc(EDEN_BYTES), 0, EDEN_BYTES};
   map_init(&p->map);
   for (int64_t s = 0; s < p->n; s += BATCH) {
     const int64_t m = p->n - s < BATCH ? p->n - s : BATCH;
@@ -171,17 +269,18 @@ static void run_partition(part* p) {
     }
     /* ProjectionExec: a + b (JVM Long wrap) */
     for (int64_t i = 0; i < c; ++i) proj[i] = (int64_t)((uint64_t)sa[i] + (uint64_t)sb[i]);
-    /* HashAggregateExec row loop (K:620-631) */
+    /* HashAggregateExec row loop (K:620-631): boxed key list, getOrPut, boxed accumulator inputs */
     for (int64_t i = 0; i < c; ++i) {
-      boxed key = {0, sk[i]};
-      node* n = map_get_or_put(&p->map, &key);
-      boxed in0 = {0, proj[i]}, in1 = {0, 1}, in2 = {0, sa[i]}, in3 = {0, sb[i]};
-      n->acc[0].accumulate(&n->acc[0], &in0);
-      n->acc[1].accumulate(&n->acc[1], &in1);
-      n->acc[2].accumulate(&n->acc[2], &in2);
-      n->acc[3].accumulate(&n->acc[3], &in3);
+      jlist* key = key_list(&eden, box_long(&eden, sk[i]));
+      node* n = map_get_or_put(&p->map, key);
+      n->acc[0].accumulate(&n->acc[0], box_long(&eden, proj[i]));
+      n->acc[1].accumulate(&n->acc[1], box_long(&eden, 1));
+      n->acc[2].accumulate(&n->acc[2], box_long(&eden, sa[i]));
+      n->acc[3].accumulate(&n->acc[3], box_long(&eden, sb[i]));
     }
+    eden.off = 0; /* minor collection: this batch's row objects are dead */
   }
+  free(eden.base);
   free(sk);
   free(sa);
   free(sb);
@@ -257,13 +356,13 @@ double qe_cpu_c4(int64_t row0, int64_t rows, uint64_t seed, int threads, int64_t
   for (int t = 0; t < threads; ++t) {
     for (size_t i = 0; i < parts[t].map.nbuckets; ++i) {
       for (node* n = parts[t].map.buckets[i]; n; n = n->next) {
-        node* f = map_get_or_put(&fin, &n->key);
-        boxed s0 = {0, n->acc[0].value}, s2 = {!n->acc[2].has, n->acc[2].value}, s3 = {!n->acc[3].has, n->acc[3].value};
+        node* f = map_get_or_put(&fin, n->key);
+        jlong_box s0 = {1, n->acc[0].value}, s2 = {1, n->acc[2].value}, s3 = {1, n->acc[3].value};
         f->acc[0].accumulate(&f->acc[0], &s0);
         f->acc[1].value += n->acc[1].value;
         f->acc[1].has = 1;
-        f->acc[2].accumulate(&f->acc[2], &s2);
-        f->acc[3].accumulate(&f->acc[3], &s3);
+        f->acc[2].accumulate(&f->acc[2], n->acc[2].has ? &s2 : NULL);
+        f->acc[3].accumulate(&f->acc[3], n->acc[3].has ? &s3 : NULL);
       }
     }
   }
@@ -272,7 +371,7 @@ double qe_cpu_c4(int64_t row0, int64_t rows, uint64_t seed, int threads, int64_t
   for (size_t i = 0; i < fin.nbuckets; ++i) {
     for (node* n = fin.buckets[i]; n; n = n->next) {
       if (g < cap && out) {
-        out[g].key = n->key.v;
+        out[g].key = key_of(n);
         out[g].sum = n->acc[0].value;
         out[g].count = n->acc[1].value;
         out[g].min = n->acc[2].value;

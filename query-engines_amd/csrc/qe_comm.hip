@@ -162,20 +162,29 @@ int qe_comm_destroy(qe_comm* c) {
   return QE_OK;
 }
 
+int qe_hashagg_slot_capacity(qe_hashagg* h, int32_t world, int64_t* cap) {
+  QE_CHECK(h && cap && world >= 1, QE_ERR_INVALID_ARG, "bad arguments");
+  // the create-time expected groups spread over the ranks with headroom: 1.5x an even share plus
+  // 32, at most the expected groups. It depends on nothing a rank's own data changes, so every
+  // rank computes the same slot size (the all-to-all's slots must be equal).
+  int64_t eg = 0;
+  QE_TRY(hashagg_expected_groups(h, &eg));
+  eg = std::max<int64_t>(eg, 1);
+  *cap = std::min<int64_t>(eg, (3 * eg + 2 * world - 1) / (2 * world) + 32);
+  return QE_OK;
+}
+
 int qe_hashagg_exchange(qe_comm* c, qe_hashagg* partial, qe_hashagg* owner, int64_t slot_records,
                         int64_t* nrecords) {
   QE_CHECK(c && partial && owner, QE_ERR_INVALID_ARG, "null argument");
   QE_TRY(ctx_enter(c->ctx));
   const int world = c->world;
-  int64_t rb = 0, eg = 0;
+  int64_t rb = 0;
   QE_TRY(qe_hashagg_record_bytes(partial, &rb));
-  QE_TRY(hashagg_expected_groups(partial, &eg));
   QE_CHECK(hashagg_ctx(partial) == c->ctx && hashagg_ctx(owner) == c->ctx, QE_ERR_INVALID_ARG,
            "partial, owner and communicator must share one qe_ctx (one stream)");
-  // default capacity: the expected groups spread over the ranks with headroom (the same on every
-  // rank: it must be, the slots are equal-sized)
-  const int64_t cap = slot_records > 0 ? slot_records
-                                       : std::min<int64_t>(std::max<int64_t>(eg, 1), (3 * eg + 2 * world - 1) / (2 * world) + 32);
+  int64_t cap = slot_records;
+  if (cap <= 0) QE_TRY(qe_hashagg_slot_capacity(partial, world, &cap));
   const size_t slot_bytes = (size_t)QE_SLOT_HEADER + (size_t)cap * (size_t)rb;
   QE_TRY(comm_buffer(c, 2 * (size_t)world * slot_bytes));
   uint8_t* send = c->buf;

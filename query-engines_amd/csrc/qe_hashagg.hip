@@ -1381,7 +1381,8 @@ struct qe_hashagg {
   // LDS sizing
   int32_t lds_log2 = 0;  // largest LDS table (log2 slots); 0 => global-only mode
   int32_t lds_log2_min = 0;
-  int64_t expected_groups = 0;
+  int64_t expected_groups = 0;  // sizing hint; raised by adapt_after_update once the LDS table is outgrown
+  int64_t create_groups = 0;    // qe_hashagg_create's expected groups, never changed (exchange slot sizing)
   int grid = 0;          // workgroups per launch (cap)
   // radix-partitioned updates (expected groups beyond the LDS table): counts / offsets, records
   int64_t* part_cnt = nullptr;
@@ -1413,13 +1414,19 @@ struct qe_hashagg {
   // pinned snapshot of the control words queued behind each update launch, and its event
   uint64_t* ctl_pin = nullptr;
   hipEvent_t ev_ctl = nullptr;
+  // a stream-ordered update whose settling failed leaves an incomplete table: every later call
+  // that reads the state fails with this status until qe_hashagg_reset
+  int poisoned = 0;
+  std::string poison_msg;
 };
 
 namespace qe {
 
 int hashagg_expected_groups(const qe_hashagg* h, int64_t* out) {
   QE_CHECK(h && out, QE_ERR_INVALID_ARG, "null argument");
-  *out = h->expected_groups;
+  // the create-time value: the exchange sizes equal slots from it, so it must be the same on every
+  // rank whatever each rank's own data did to the sizing hint (adapt_after_update)
+  *out = h->create_groups;
   return QE_OK;
 }
 
@@ -2020,7 +2027,7 @@ static int partition_rows(qe_hashagg* h, Plan& P, hipFunction_t* fn, int* grid) 
 // deferred by the previous pass (defer_in). Control counters cleared as needed, the kernel
 // chosen (plan-specialised when possible), events bracketing it (ev[0] of pass 0 / mp 0 is
 // recorded by the caller, before any partitioning work).
-static int launch_pass(qe_hashagg* h, Plan& P, size_t lds, hipFunction_t pfn, int pgrid, int pass, int mp,
+static int launch_pass(qe_hashagg* h, Plan& P, size_t& lds, hipFunction_t pfn, int pgrid, int pass, int mp,
                        int out_i, const uint32_t* defer_in, int pblock = 0) {
   qe_ctx* ctx = h->ctx;
   const int64_t n = P.n;
@@ -2099,6 +2106,22 @@ static int launch_pass(qe_hashagg* h, Plan& P, size_t lds, hipFunction_t pfn, in
   } else if (h->jit_note.rfind("partitioning unavailable", 0) != 0) {
     h->jit_note = lds ? "jit disabled" : "global-only launch";
   }
+  if (!jfn && lds > HA_LDS_BUDGET) {
+    // the 152 KiB budget is for the specialised 1024-thread kernel (one per CU); the generic
+    // 512-thread kernel runs two per CU, so its table is re-laid out within HA_LDS_BUDGET
+    size_t b = 0;
+    int log2 = P.lds_log2;
+    while (log2 >= h->lds_log2_min && (b = lds_layout_at(h, &P, log2)) > HA_LDS_BUDGET) --log2;
+    if (log2 < h->lds_log2_min || log2 < 8) {
+      P.lds_log2 = 0;
+      lds = 0;
+    } else {
+      lds = b;
+    }
+    const int pc = lds ? std::max<int>(1, std::min<int>(8, (int)((160 * 1024) / lds))) : 8;
+    grid = (int)std::max<int64_t>(1, std::min<int64_t>((int64_t)div_up((uint64_t)waves, HA_THREADS / 64),
+                                                       std::min<int64_t>((int64_t)ctx->num_cus * pc, h->grid)));
+  }
   if (pass > 0 || mp > 0) QE_HIP(hipEventRecord(h->ev[0], ctx->stream));
   if (jfn) {
     QE_TRY(jit_launch(ctx, jfn, jgrid, P, pfn ? (pblock ? pblock : pagg_block()) : fused_block(P.lds_log2)));
@@ -2163,9 +2186,7 @@ static void adapt_after_update(qe_hashagg* h, size_t lds, int lds_log2) {
 // Stream-ordered update (qe_hashagg_set_async): the pass-0 launch is queued and the read-back of
 // its counters (with any growth / retry passes, which re-read the update's columns) is done by the
 // next call on the state. Nothing pending: no-op.
-static int settle_pending(qe_hashagg* h) {
-  if (!h->pending) return QE_OK;
-  h->pending = false;
+static int settle_body(qe_hashagg* h) {
   Plan& P = *h->pend_plan;
   int out_i = h->pend_out_i;
   const uint32_t* defer_in = nullptr;
@@ -2177,6 +2198,19 @@ static int settle_pending(qe_hashagg* h) {
   }
   adapt_after_update(h, h->pend_lds, P.lds_log2);
   return QE_OK;
+}
+
+static int settle_pending(qe_hashagg* h) {
+  if (h->poisoned)
+    return fail(h->poisoned, "an earlier stream-ordered update failed (%s); reset the state", h->poison_msg.c_str());
+  if (!h->pending) return QE_OK;
+  h->pending = false;
+  const int st = settle_body(h);
+  if (st != QE_OK) {  // the table is incomplete: keep failing, not just this once
+    h->poisoned = st;
+    h->poison_msg = qe_last_error();
+  }
+  return st;
 }
 
 // Two key-hash buckets (groups just beyond one LDS table; QE_MP_SPILL, read per call, 0 = two
@@ -2469,6 +2503,7 @@ int qe_hashagg_create(qe_ctx* ctx, int32_t nkeys, const int32_t* key_types, int3
   // 1.25x (lds_log2_min) to fit the per-workgroup budget, else the launch is global-only.
   const int64_t eg = expected_groups > 0 ? expected_groups : 1024;
   h->expected_groups = eg;
+  h->create_groups = eg;
   int log2 = 8, log2_min = 8;
   while (log2 < 16 && ((int64_t)1 << log2) < 2 * eg) ++log2;
   while (log2_min < 16 && ((int64_t)1 << log2_min) < (5 * eg + 3) / 4) ++log2_min;
@@ -2548,6 +2583,8 @@ int qe_hashagg_reset(qe_hashagg* h) {
     h->pending = false;
     h->defer_dirty[h->pend_out_i] = true;
   }
+  h->poisoned = 0;
+  h->poison_msg.clear();
   const int grid = (int)std::min<uint64_t>(div_up(h->t.cap + 2, 256), 4096);
   hipLaunchKernelGGL(k_table_init, dim3(grid), dim3(256), 0, h->ctx->stream, h->t, agg_meta(h), (qu64*)h->ctl);
   QE_TRY(launch_check("k_table_init"));

@@ -3,6 +3,7 @@
 #include <stdio.h>
 #include <stdlib.h>
 
+#include <algorithm>
 #include <map>
 #include <mutex>
 #include <unordered_map>
@@ -374,32 +375,77 @@ __global__ void __launch_bounds__(512) k_stream_read(StreamCols c, unsigned long
 }
 
 // Row-interleaved variant (every column the same number of 16-byte chunks): each wave step reads
-// two 1 KiB slabs of EVERY column, the access pattern of the fused aggregate (one contiguous KiB
-// per load instruction, all columns' streams in flight together).
-template <bool NT>
+// SLABS 1 KiB slabs of EVERY column, the access pattern of the fused aggregate (one contiguous KiB
+// per load instruction, all columns' streams in flight together). NC: columns compiled for (the
+// loop stops at c.ncols), so a 3-column read keeps its loads in registers at any occupancy.
+template <bool NT, int SLABS, int NC>
 __global__ void __launch_bounds__(1024) k_stream_read_rows(StreamCols c, unsigned long long* out) {
   unsigned long long acc = 0;
   const int lane = threadIdx.x & 63;
   const int64_t wave = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 6;
   const int64_t nw = ((int64_t)gridDim.x * blockDim.x) >> 6;
   const int64_t n = c.n16[0];
-  for (int64_t base = wave * 128; base < n; base += nw * 128) {
+  for (int64_t base = wave * (64 * SLABS); base < n; base += nw * (64 * SLABS)) {
     const int64_t i = base + lane;
-    i64x2_rt v[16];
+    i64x2_rt v[NC * SLABS];
 #pragma unroll
-    for (int k = 0; k < 8; ++k) {
+    for (int k = 0; k < NC; ++k) {
       if (k >= c.ncols) break;
-      v[2 * k] = i < n ? ld16<NT>(c.p[k] + i) : i64x2_rt{0, 0};
-      v[2 * k + 1] = i + 64 < n ? ld16<NT>(c.p[k] + i + 64) : i64x2_rt{0, 0};
+#pragma unroll
+      for (int s = 0; s < SLABS; ++s)
+        v[SLABS * k + s] = i + 64 * s < n ? ld16<NT>(c.p[k] + i + 64 * s) : i64x2_rt{0, 0};
     }
 #pragma unroll
-    for (int k = 0; k < 8; ++k) {
+    for (int k = 0; k < NC; ++k) {
       if (k >= c.ncols) break;
-      acc ^= (unsigned long long)(v[2 * k].x ^ v[2 * k].y ^ v[2 * k + 1].x ^ v[2 * k + 1].y);
+#pragma unroll
+      for (int s = 0; s < SLABS; ++s) acc ^= (unsigned long long)(v[SLABS * k + s].x ^ v[SLABS * k + s].y);
     }
   }
   for (int m = 32; m > 0; m >>= 1) acc ^= __shfl_xor(acc, m);
   if (lane == 0 && acc == 0x5A5A5A5A5A5A5A5Aull) atomicXor(out, acc);  // practically never
+}
+
+// Launch shapes the ceiling is taken over (qe_stream_read_best): the best of them is the bound a
+// streaming kernel of this access pattern can reach on this part, whatever its occupancy.
+struct StreamShape {
+  int rows;     // 1: row-interleaved (all columns per step), 0: one column after another
+  int nt;       // non-temporal loads
+  int slabs;    // 1 KiB slabs per column per wave step (rows only)
+  int block;    // threads per workgroup
+  int per_cu;   // workgroups per CU
+};
+static const StreamShape kStreamShapes[] = {
+    {1, 1, 2, 1024, 1}, {1, 1, 2, 1024, 2}, {1, 1, 2, 512, 4}, {1, 1, 1, 256, 8}, {1, 1, 4, 256, 4},
+    {1, 1, 2, 256, 8},  {1, 0, 2, 1024, 2}, {0, 1, 0, 512, 4}, {0, 1, 0, 512, 8}, {0, 0, 0, 512, 4},
+};
+constexpr int kNumStreamShapes = (int)(sizeof(kStreamShapes) / sizeof(kStreamShapes[0]));
+
+template <bool NT, int SLABS>
+static void launch_rows(const StreamCols& c, int grid, int block, hipStream_t st, unsigned long long* out) {
+  if (c.ncols <= 3)
+    hipLaunchKernelGGL((k_stream_read_rows<NT, SLABS, 3>), dim3(grid), dim3(block), 0, st, c, out);
+  else
+    hipLaunchKernelGGL((k_stream_read_rows<NT, SLABS, 8>), dim3(grid), dim3(block), 0, st, c, out);
+}
+
+static void launch_stream_shape(const StreamShape& sh, const StreamCols& c, int cus, hipStream_t st,
+                                unsigned long long* out) {
+  const int grid = cus * sh.per_cu;
+  if (!sh.rows) {
+    if (sh.nt)
+      hipLaunchKernelGGL(k_stream_read<true>, dim3(grid), dim3(sh.block), 0, st, c, out);
+    else
+      hipLaunchKernelGGL(k_stream_read<false>, dim3(grid), dim3(sh.block), 0, st, c, out);
+    return;
+  }
+  if (sh.nt) {
+    if (sh.slabs == 1) launch_rows<true, 1>(c, grid, sh.block, st, out);
+    else if (sh.slabs == 4) launch_rows<true, 4>(c, grid, sh.block, st, out);
+    else launch_rows<true, 2>(c, grid, sh.block, st, out);
+  } else {
+    launch_rows<false, 2>(c, grid, sh.block, st, out);
+  }
 }
 
 }  // namespace qe
@@ -502,38 +548,30 @@ int qe_copy_to_host(qe_ctx* ctx, void* dst, const void* src, size_t bytes) {
   return QE_OK;
 }
 
-int qe_stream_read(qe_ctx* ctx, const qe_column* cols, int32_t ncols, double* ms) {
-  QE_TRY(ctx_enter(ctx));
-  QE_CHECK(cols && ncols >= 1 && ncols <= 8 && ms, QE_ERR_INVALID_ARG, "1..8 columns");
-  StreamCols c{};
-  c.ncols = ncols;
+static int stream_cols(const qe_column* cols, int32_t ncols, StreamCols* c, bool* same) {
+  QE_CHECK(cols && ncols >= 1 && ncols <= 8, QE_ERR_INVALID_ARG, "1..8 columns");
+  *c = StreamCols{};
+  c->ncols = ncols;
   for (int k = 0; k < ncols; ++k) {
     QE_CHECK(is_fixed(cols[k].type), QE_ERR_UNSUPPORTED, "fixed-width columns only");
     QE_CHECK(((uintptr_t)cols[k].values & 15) == 0, QE_ERR_INVALID_ARG, "16-byte aligned columns only");
-    c.p[k] = (const i64x2_rt*)cols[k].values;
-    c.n16[k] = cols[k].length * type_width(cols[k].type) / 16;
+    c->p[k] = (const i64x2_rt*)cols[k].values;
+    c->n16[k] = cols[k].length * type_width(cols[k].type) / 16;
   }
+  *same = true;
+  for (int k = 1; k < ncols; ++k) *same = *same && c->n16[k] == c->n16[0];
+  return QE_OK;
+}
+
+// Device time of one launch of shape `sh` (events on the ctx stream).
+static int stream_time(qe_ctx* ctx, const StreamShape& sh, const StreamCols& c, double* ms) {
   void* s;
   QE_TRY(ctx_scratch(ctx, 64, &s));
   hipEvent_t e0, e1;
   QE_HIP(hipEventCreate(&e0));
   QE_HIP(hipEventCreate(&e1));
-  bool same = true;
-  for (int k = 1; k < ncols; ++k) same = same && c.n16[k] == c.n16[0];
-  const bool nt = !(getenv("QE_NT") && getenv("QE_NT")[0] == '0');  // non-temporal (default), as the fused kernels
   QE_HIP(hipEventRecord(e0, ctx->stream));
-  if (same && nt)
-    hipLaunchKernelGGL(k_stream_read_rows<true>, dim3(ctx->num_cus), dim3(1024), 0, ctx->stream, c,
-                       (unsigned long long*)s);
-  else if (same)
-    hipLaunchKernelGGL(k_stream_read_rows<false>, dim3(ctx->num_cus), dim3(1024), 0, ctx->stream, c,
-                       (unsigned long long*)s);
-  else if (nt)
-    hipLaunchKernelGGL(k_stream_read<true>, dim3(ctx->num_cus * 4), dim3(512), 0, ctx->stream, c,
-                       (unsigned long long*)s);
-  else
-    hipLaunchKernelGGL(k_stream_read<false>, dim3(ctx->num_cus * 4), dim3(512), 0, ctx->stream, c,
-                       (unsigned long long*)s);
+  launch_stream_shape(sh, c, ctx->num_cus, ctx->stream, (unsigned long long*)s);
   QE_HIP(hipEventRecord(e1, ctx->stream));
   QE_HIP(hipEventSynchronize(e1));
   float f = 0.f;
@@ -542,6 +580,47 @@ int qe_stream_read(qe_ctx* ctx, const qe_column* cols, int32_t ncols, double* ms
   (void)hipEventDestroy(e0);
   (void)hipEventDestroy(e1);
   return launch_check("k_stream_read");
+}
+
+int qe_stream_read(qe_ctx* ctx, const qe_column* cols, int32_t ncols, double* ms) {
+  QE_TRY(ctx_enter(ctx));
+  QE_CHECK(ms, QE_ERR_INVALID_ARG, "null ms");
+  StreamCols c;
+  bool same = false;
+  QE_TRY(stream_cols(cols, ncols, &c, &same));
+  const bool nt = !(getenv("QE_NT") && getenv("QE_NT")[0] == '0');  // non-temporal (default), as the fused kernels
+  const StreamShape sh = same ? StreamShape{1, nt ? 1 : 0, 2, 1024, 1} : StreamShape{0, nt ? 1 : 0, 0, 512, 4};
+  return stream_time(ctx, sh, c, ms);
+}
+
+int qe_stream_read_best(qe_ctx* ctx, const qe_column* cols, int32_t ncols, int32_t reps, double* ms,
+                        char* shape, int32_t shape_len) {
+  QE_TRY(ctx_enter(ctx));
+  QE_CHECK(ms && reps >= 1 && reps <= 64, QE_ERR_INVALID_ARG, "bad arguments");
+  StreamCols c;
+  bool same = false;
+  QE_TRY(stream_cols(cols, ncols, &c, &same));
+  double best = 0.0;
+  int bi = -1;
+  for (int i = 0; i < kNumStreamShapes; ++i) {
+    const StreamShape& sh = kStreamShapes[i];
+    if (sh.rows && !same) continue;
+    std::vector<double> t((size_t)reps);
+    for (int r = 0; r < reps; ++r) QE_TRY(stream_time(ctx, sh, c, &t[(size_t)r]));
+    std::sort(t.begin(), t.end());
+    const double med = t[(size_t)reps / 2];
+    if (bi < 0 || med < best) {
+      best = med;
+      bi = i;
+    }
+  }
+  *ms = best;
+  if (shape && shape_len > 0) {
+    const StreamShape& sh = kStreamShapes[bi];
+    snprintf(shape, (size_t)shape_len, "%s%s, %d slab(s), %d threads x %d per CU", sh.rows ? "row-interleaved" : "column-serial",
+             sh.nt ? " nt" : "", sh.slabs, sh.block, sh.per_cu);
+  }
+  return QE_OK;
 }
 
 int qe_generate(qe_ctx* ctx, qe_column* out, int32_t dist, int64_t param, uint64_t seed, uint64_t col,

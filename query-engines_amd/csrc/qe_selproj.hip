@@ -11,6 +11,7 @@
 #include <string.h>
 
 #include <map>
+#include <memory>
 #include <mutex>
 #include <string>
 
@@ -67,34 +68,43 @@ int32_t program_type(const qe_column* cols, const DAgg& a, bool is_f) {
 
 }  // namespace
 
-extern "C" int qe_select_project(qe_ctx* ctx, const qe_column* cols, int32_t ncols, const qe_select_spec* spec,
-                                 qe_column* outs, int64_t* out_count) {
-  QE_TRY(ctx_enter(ctx));
-  QE_CHECK(cols && spec && outs && out_count, QE_ERR_INVALID_ARG, "null argument");
-  QE_CHECK(spec->nout >= 1 && spec->nout <= QE_MAX_AGGS, QE_ERR_UNSUPPORTED, "select-project takes 1..%d outputs",
-           QE_MAX_AGGS);
+// A queued select-project call (qe_select_project_async): the plan and outputs, and where its
+// count (and the persistent look-back's stall flag) land in pinned memory behind an event.
+struct qe_select_pending {
+  qe_ctx* ctx = nullptr;
   Plan P;
-  bool col_f64[QE_MAX_COLS];
-  QE_TRY(compile_inputs(cols, ncols, spec->mask_col, spec->nterms, spec->terms, &P, col_f64));
-  const int64_t n = P.n;
-  int32_t out_kind[QE_MAX_AGGS];
-  bool nullable[QE_MAX_AGGS];
-  P.naggs = spec->nout;
-  for (int k = 0; k < spec->nout; ++k) {
-    bool is_f = false;
-    DAgg& a = P.aggs[k];
-    QE_TRY(compile_program(cols, ncols, col_f64, spec->outputs[k], k, &a, &is_f, &nullable[k]));
-    const int32_t t = program_type(cols, a, is_f);
-    QE_CHECK(t != QE_TYPE_BOOL, QE_ERR_UNSUPPORTED, "output %d: BOOL pass-through is not fused", k);
-    QE_CHECK(outs[k].type == t, QE_ERR_INVALID_ARG, "output %d: column type %d, expression yields %d", k, outs[k].type,
-             t);
-    QE_CHECK(outs[k].length >= n && (outs[k].values || n == 0), QE_ERR_CAPACITY,
-             "output %d: capacity %lld rows, input has %lld", k, (long long)outs[k].length, (long long)n);
-    out_kind[k] = type_width(t) | ((nullable[k] && outs[k].validity) ? 0x100 : 0);
-    P.t.acc[k] = (qi64*)outs[k].values;
-    P.t.nn[k] = (qu64*)outs[k].validity;
+  int32_t out_kind[QE_MAX_AGGS] = {};
+  int32_t nout = 0;
+  qe_column outs[QE_MAX_AGGS] = {};
+  uint64_t* pin = nullptr;  // [0] count, [1] stall flag (persistent look-back)
+  hipEvent_t ev = nullptr;
+  bool persist = false;     // the launch was the persistent look-back grid (a stall reruns it)
+  int32_t col_width[QE_MAX_COLS] = {};
+};
+
+namespace {
+
+// validity: nullable outputs start all-null (the kernel sets bits); others all-valid
+int init_validity(qe_ctx* ctx, const qe_column* outs, const int32_t* out_kind, int nout, int64_t n) {
+  for (int k = 0; k < nout; ++k) {
+    if (!outs[k].validity) continue;
+    const size_t vb = (size_t)div_up((uint64_t)(n > 0 ? n : 1), 32) * 4;
+    QE_HIP(hipMemsetAsync(outs[k].validity, (out_kind[k] & 0x100) ? 0 : 0xFF, vb, ctx->stream));
   }
-  if (!ctx->jit) return fail(QE_ERR_UNSUPPORTED, "fused select-project needs kernel specialisation (jit is off)");
+  return QE_OK;
+}
+
+// Queues the kernels of one select-project over P (validity already initialised) and the copy of
+// its count into pin[0] (pin[1]: 1 if a persistent look-back tile never saw its predecessor).
+// `persist_ok` = false forces counter-ordered tiles (the rerun after a stall).
+int launch_select(qe_ctx* ctx, Plan& P, const int32_t* col_width, const int32_t* out_kind, int nout, bool persist_ok,
+                  uint64_t* pin, bool* persist_used) {
+  *persist_used = false;
+  const int64_t n = P.n;
+  if (n == 0) {
+    QE_HIP(hipMemsetAsync(pin, 0, 16, ctx->stream));  // (pinned: a stream-ordered write of zeros)
+    return QE_OK;
+  }
   // Tile order: a persistent grid (every workgroup resident, tiles assigned statically) or one
   // tile per workgroup with ids from a device counter in start order (QE_SELPROJ_PERSIST=0). The
   // counter is one word every workgroup hits: ~88 returning atomics/us, a floor of 2.8 ms for
@@ -110,17 +120,6 @@ extern "C" int qe_select_project(qe_ctx* ctx, const qe_column* cols, int32_t nco
     const char* e = getenv("QE_SELPROJ_WG_PER_CU");
     return e && *e ? std::max(1, atoi(e)) : 4;
   }();
-  // validity: nullable outputs start all-null (the kernel sets bits); others all-valid
-  auto init_validity = [&]() -> int {
-    for (int k = 0; k < spec->nout; ++k) {
-      if (!outs[k].validity) continue;
-      const size_t vb = (size_t)div_up((uint64_t)(n > 0 ? n : 1), 32) * 4;
-      QE_HIP(hipMemsetAsync(outs[k].validity, (out_kind[k] & 0x100) ? 0 : 0xFF, vb, ctx->stream));
-    }
-    return QE_OK;
-  };
-  QE_TRY(init_validity());
-  *out_count = 0;
   // Two passes (count per tile, then write at the sum of the earlier tiles' counts) while the
   // predicate's columns fit the MALL, so the second pass reads them from there: no look-back
   // round trips. QE_SELPROJ_TWOPASS=0/1 forces either way.
@@ -131,19 +130,20 @@ extern "C" int qe_select_project(qe_ctx* ctx, const qe_column* cols, int32_t nco
     pred_cols |= (1u << P.terms[t].lhs) | (P.terms[t].rhs >= 0 ? 1u << P.terms[t].rhs : 0u);
   size_t pred_bytes = 0;
   for (int c = 0; c < P.ncols; ++c)
-    if ((pred_cols >> c) & 1u) pred_bytes += (size_t)n * std::max(1, type_width(cols[c].type));
+    if ((pred_cols >> c) & 1u) pred_bytes += (size_t)n * std::max(1, col_width[c]);
   // (each write-pass tile sums all earlier tiles' counts, so the tile count is bounded too: a
   // plan with no predicate reads nothing in the count pass but still pays the prefix sums)
-  const int64_t tiles_est = (int64_t)div_up((uint64_t)n, (uint64_t)selproj_rows_per_thread(P) * selproj_block());
-  const bool twopass = twopass_env >= 0 ? twopass_env == 1 : (pred_bytes <= (96ull << 20) && tiles_est <= 4096);
+  const int R = selproj_rows_per_thread(P);
+  const int64_t tiles = (int64_t)div_up((uint64_t)n, (uint64_t)R * selproj_block());
+  QE_CHECK(tiles < (1ll << 31), QE_ERR_CAPACITY, "too many rows for one select-project call");
+  const bool twopass = twopass_env >= 0 ? twopass_env == 1 : (pred_bytes <= (96ull << 20) && tiles <= 4096);
   // Scanned two passes (QE_SELPROJ_TWOPASS=2): count pass, a device scan of the tile counts, then
   // the write pass reads its tile's base — no look-back chain and no per-tile prefix sums, at the
   // price of reading the predicate's columns twice.
   const bool scanned = twopass_env == 2;
-  if (n > 0 && scanned) {
-    const int R = selproj_rows_per_thread(P);
-    const int64_t tiles = (int64_t)div_up((uint64_t)n, (uint64_t)R * selproj_block());
-    QE_CHECK(tiles < (1ll << 31), QE_ERR_CAPACITY, "too many rows for one select-project call");
+  hipFunction_t fn;
+  int bpc = 0;
+  if (scanned) {
     void* s;
     QE_TRY(ctx_scratch(ctx, (size_t)(2 * tiles + 4) * 8, &s));
     qu64* ctl = (qu64*)s;
@@ -151,86 +151,152 @@ extern "C" int qe_select_project(qe_ctx* ctx, const qe_column* cols, int32_t nco
     qu64* offs = cnt + tiles;  // tiles + 1 words
     P.t.ctl = ctl;
     P.t.cap = (qu64)tiles;
-    void* pin;
-    QE_TRY(ctx_pinned(ctx, 16, &pin));
-    hipFunction_t fn;
-    int bpc = 0;
     P.t.keys = (qi64*)cnt;
-    QE_TRY(selproj_kernel(ctx, P, out_kind, spec->nout, SP_COUNT, &fn, &bpc));
+    QE_TRY(selproj_kernel(ctx, P, out_kind, nout, SP_COUNT, &fn, &bpc));
     QE_TRY(jit_launch(ctx, fn, (int)tiles, P, selproj_block()));
     QE_TRY(launch_check("qe_selproj (count)"));
     QE_TRY(exclusive_scan_i64(ctx, (const int64_t*)cnt, (int64_t*)offs, tiles));
     P.t.keys = (qi64*)offs;
-    QE_TRY(selproj_kernel(ctx, P, out_kind, spec->nout, SP_WRITE_SCAN, &fn, &bpc));
+    QE_TRY(selproj_kernel(ctx, P, out_kind, nout, SP_WRITE_SCAN, &fn, &bpc));
     QE_TRY(jit_launch(ctx, fn, (int)tiles, P, selproj_block()));
     QE_TRY(launch_check("qe_selproj (write)"));
+    QE_HIP(hipMemsetAsync(pin + 1, 0, 8, ctx->stream));
     QE_HIP(hipMemcpyAsync(pin, offs + tiles, 8, hipMemcpyDeviceToHost, ctx->stream));
-    QE_TRY(ctx_sync(ctx));
-    *out_count = ((int64_t*)pin)[0];
-  } else if (n > 0 && twopass) {
-    const int R = selproj_rows_per_thread(P);
-    const int64_t tiles = (int64_t)div_up((uint64_t)n, (uint64_t)R * selproj_block());
-    QE_CHECK(tiles < (1ll << 31), QE_ERR_CAPACITY, "too many rows for one select-project call");
+    return QE_OK;
+  }
+  if (twopass) {
     void* s;
     QE_TRY(ctx_scratch(ctx, (size_t)(tiles + 3) * 8, &s));
     qu64* ctl = (qu64*)s;
     P.t.ctl = ctl;
     P.t.keys = (qi64*)(ctl + 3);
     P.t.cap = (qu64)tiles;
-    void* pin;
-    QE_TRY(ctx_pinned(ctx, 16, &pin));
     for (int mode : {SP_COUNT, SP_WRITE}) {
-      hipFunction_t fn;
-      int bpc = 0;
-      QE_TRY(selproj_kernel(ctx, P, out_kind, spec->nout, mode, &fn, &bpc));
+      QE_TRY(selproj_kernel(ctx, P, out_kind, nout, mode, &fn, &bpc));
       QE_TRY(jit_launch(ctx, fn, (int)tiles, P, selproj_block()));
       QE_TRY(launch_check(mode == SP_COUNT ? "qe_selproj (count)" : "qe_selproj (write)"));
     }
+    QE_HIP(hipMemsetAsync(pin + 1, 0, 8, ctx->stream));
     QE_HIP(hipMemcpyAsync(pin, ctl + 1, 8, hipMemcpyDeviceToHost, ctx->stream));
-    QE_TRY(ctx_sync(ctx));
-    *out_count = ((int64_t*)pin)[0];
-  } else if (n > 0) {
-    const int R = selproj_rows_per_thread(P);
-    const int64_t tiles = (int64_t)div_up((uint64_t)n, (uint64_t)R * selproj_block());
-    QE_CHECK(tiles < (1ll << 31), QE_ERR_CAPACITY, "too many rows for one select-project call");
-    const size_t sbytes = (size_t)(3 + tiles) * 8;  // ctl[3] | per tile a look-back status word
-    void* s;
-    QE_TRY(ctx_scratch(ctx, sbytes, &s));
-    qu64* ctl = (qu64*)s;
-    P.t.ctl = ctl;
-    P.t.keys = (qi64*)(ctl + 3);
-    P.t.cap = (qu64)tiles;
-    void* pin;
-    QE_TRY(ctx_pinned(ctx, 16, &pin));
-    for (int attempt = 0; attempt < 2; ++attempt) {
-      const bool persist = persist_env && attempt == 0;
-      const int mode = persist ? SP_PERSIST : SP_COUNTER;
-      hipFunction_t fn;
-      int bpc = 0;
-      QE_TRY(selproj_kernel(ctx, P, out_kind, spec->nout, mode, &fn, &bpc));
-      // QE_SELPROJ_OVERSUB (tests only) multiplies the persistent grid past residency, to exercise
-      // the bounded look-back and the rerun
-      const char* ov = getenv("QE_SELPROJ_OVERSUB");
-      const int oversub = ov && *ov ? std::max(1, std::min(64, atoi(ov))) : 1;
-      static const int margin = [] {  // QE_SELPROJ_OCC_MARGIN: blocks per CU held back from the occupancy
-        const char* e = getenv("QE_SELPROJ_OCC_MARGIN");
-        return e && *e ? std::max(0, atoi(e)) : 1;
-      }();
-      const int per_cu = std::max(1, std::min(wg_cap, bpc - margin));
-      const int64_t grid = persist ? std::min<int64_t>(tiles, (int64_t)ctx->num_cus * per_cu * oversub) : tiles;
-      QE_HIP(hipMemsetAsync(s, 0, sbytes, ctx->stream));
-      QE_TRY(jit_launch(ctx, fn, (int)grid, P, selproj_block()));
-      QE_TRY(launch_check("qe_selproj"));
-      QE_HIP(hipMemcpyAsync(pin, ctl + 1, 16, hipMemcpyDeviceToHost, ctx->stream));
-      QE_TRY(ctx_sync(ctx));
-      *out_count = ((int64_t*)pin)[0];
-      if (((int64_t*)pin)[1] == 0) break;  // else: a persistent workgroup was not resident
-      QE_CHECK(persist, QE_ERR_DEVICE, "select-project look-back did not complete");
-      fprintf(stderr, "qe: select-project persistent look-back stalled (grid %lld); rerunning with counter-ordered tiles\n",
-              (long long)grid);
-      QE_TRY(init_validity());  // the aborted launch may have set bits anywhere
+    return QE_OK;
+  }
+  const size_t sbytes = (size_t)(3 + tiles) * 8;  // ctl[3] | per tile a look-back status word
+  void* s;
+  QE_TRY(ctx_scratch(ctx, sbytes, &s));
+  qu64* ctl = (qu64*)s;
+  P.t.ctl = ctl;
+  P.t.keys = (qi64*)(ctl + 3);
+  P.t.cap = (qu64)tiles;
+  const bool persist = persist_env && persist_ok;
+  const int mode = persist ? SP_PERSIST : SP_COUNTER;
+  QE_TRY(selproj_kernel(ctx, P, out_kind, nout, mode, &fn, &bpc));
+  // QE_SELPROJ_OVERSUB (tests only) multiplies the persistent grid past residency, to exercise
+  // the bounded look-back and the rerun
+  const char* ov = getenv("QE_SELPROJ_OVERSUB");
+  const int oversub = ov && *ov ? std::max(1, std::min(64, atoi(ov))) : 1;
+  static const int margin = [] {  // QE_SELPROJ_OCC_MARGIN: blocks per CU held back from the occupancy
+    const char* e = getenv("QE_SELPROJ_OCC_MARGIN");
+    return e && *e ? std::max(0, atoi(e)) : 1;
+  }();
+  const int per_cu = std::max(1, std::min(wg_cap, bpc - margin));
+  const int64_t grid = persist ? std::min<int64_t>(tiles, (int64_t)ctx->num_cus * per_cu * oversub) : tiles;
+  QE_HIP(hipMemsetAsync(s, 0, sbytes, ctx->stream));
+  QE_TRY(jit_launch(ctx, fn, (int)grid, P, selproj_block()));
+  QE_TRY(launch_check("qe_selproj"));
+  QE_HIP(hipMemcpyAsync(pin, ctl + 1, 16, hipMemcpyDeviceToHost, ctx->stream));
+  *persist_used = persist;
+  return QE_OK;
+}
+
+void pending_free(qe_select_pending* r) {
+  if (!r) return;
+  if (r->ev) (void)hipEventDestroy(r->ev);
+  if (r->pin) pinned_slot_free(r->pin, r->ctx->stream);
+  delete r;
+}
+
+}  // namespace
+
+extern "C" {
+
+int qe_select_project_async(qe_ctx* ctx, const qe_column* cols, int32_t ncols, const qe_select_spec* spec,
+                            qe_column* outs, qe_select_pending** pending) {
+  QE_TRY(ctx_enter(ctx));
+  QE_CHECK(cols && spec && outs && pending, QE_ERR_INVALID_ARG, "null argument");
+  *pending = nullptr;
+  QE_CHECK(spec->nout >= 1 && spec->nout <= QE_MAX_AGGS, QE_ERR_UNSUPPORTED, "select-project takes 1..%d outputs",
+           QE_MAX_AGGS);
+  std::unique_ptr<qe_select_pending> r(new qe_select_pending());
+  r->ctx = ctx;
+  Plan& P = r->P;
+  bool col_f64[QE_MAX_COLS];
+  QE_TRY(compile_inputs(cols, ncols, spec->mask_col, spec->nterms, spec->terms, &P, col_f64));
+  const int64_t n = P.n;
+  for (int c = 0; c < ncols && c < QE_MAX_COLS; ++c) r->col_width[c] = type_width(cols[c].type);
+  bool nullable[QE_MAX_AGGS];
+  P.naggs = spec->nout;
+  r->nout = spec->nout;
+  for (int k = 0; k < spec->nout; ++k) {
+    bool is_f = false;
+    DAgg& a = P.aggs[k];
+    QE_TRY(compile_program(cols, ncols, col_f64, spec->outputs[k], k, &a, &is_f, &nullable[k]));
+    const int32_t t = program_type(cols, a, is_f);
+    QE_CHECK(t != QE_TYPE_BOOL, QE_ERR_UNSUPPORTED, "output %d: BOOL pass-through is not fused", k);
+    QE_CHECK(outs[k].type == t, QE_ERR_INVALID_ARG, "output %d: column type %d, expression yields %d", k, outs[k].type,
+             t);
+    QE_CHECK(outs[k].length >= n && (outs[k].values || n == 0), QE_ERR_CAPACITY,
+             "output %d: capacity %lld rows, input has %lld", k, (long long)outs[k].length, (long long)n);
+    r->out_kind[k] = type_width(t) | ((nullable[k] && outs[k].validity) ? 0x100 : 0);
+    P.t.acc[k] = (qi64*)outs[k].values;
+    P.t.nn[k] = (qu64*)outs[k].validity;
+    r->outs[k] = outs[k];
+  }
+  if (!ctx->jit) return fail(QE_ERR_UNSUPPORTED, "fused select-project needs kernel specialisation (jit is off)");
+  QE_TRY(pinned_slot_alloc(&r->pin));
+  QE_HIP(hipEventCreateWithFlags(&r->ev, hipEventDisableTiming));
+  QE_TRY(init_validity(ctx, outs, r->out_kind, r->nout, n));
+  const int st = launch_select(ctx, P, r->col_width, r->out_kind, r->nout, true, r->pin, &r->persist);
+  if (st != QE_OK) {
+    pending_free(r.release());
+    return st;
+  }
+  QE_HIP(hipEventRecord(r->ev, ctx->stream));
+  *pending = r.release();
+  return QE_OK;
+}
+
+int qe_select_pending_wait(qe_select_pending* r, int64_t* out_count) {
+  QE_CHECK(r && out_count, QE_ERR_INVALID_ARG, "null argument");
+  qe_ctx* ctx = r->ctx;
+  int st = ctx_enter(ctx);
+  if (st == QE_OK && hipEventSynchronize(r->ev) != hipSuccess) st = fail(QE_ERR_DEVICE, "select-project event wait failed");
+  if (st == QE_OK && r->pin[1] != 0) {
+    // a persistent workgroup was not resident: every wave drained; rerun with counter-ordered tiles
+    if (!r->persist) {
+      st = fail(QE_ERR_DEVICE, "select-project look-back did not complete");
+    } else {
+      fprintf(stderr, "qe: select-project persistent look-back stalled; rerunning with counter-ordered tiles\n");
+      bool used = false;
+      st = init_validity(ctx, r->outs, r->out_kind, r->nout, r->P.n);  // the aborted launch may have set bits anywhere
+      if (st == QE_OK) st = launch_select(ctx, r->P, r->col_width, r->out_kind, r->nout, false, r->pin, &used);
+      if (st == QE_OK) st = ctx_sync(ctx);
+      if (st == QE_OK && r->pin[1] != 0) st = fail(QE_ERR_DEVICE, "select-project look-back did not complete");
     }
   }
+  if (st == QE_OK) *out_count = (int64_t)r->pin[0];
+  pending_free(r);
+  return st;
+}
+
+int qe_select_project(qe_ctx* ctx, const qe_column* cols, int32_t ncols, const qe_select_spec* spec,
+                      qe_column* outs, int64_t* out_count) {
+  QE_CHECK(out_count, QE_ERR_INVALID_ARG, "null argument");
+  *out_count = 0;
+  qe_select_pending* r = nullptr;
+  QE_TRY(qe_select_project_async(ctx, cols, ncols, spec, outs, &r));
+  QE_TRY(qe_select_pending_wait(r, out_count));
   for (int k = 0; k < spec->nout; ++k) outs[k].length = *out_count;
   return QE_OK;
 }
+
+}  // extern "C"

@@ -197,6 +197,12 @@ class HashAggregateState:
         if self.async_update:  # a pending update may re-read its columns when it is settled
             self._held = cols
 
+    def slot_capacity(self, world: int) -> int:
+        """Default records per slot of a `world`-rank exchange (qe_hashagg_slot_capacity)."""
+        cap = N.C.c_int64()
+        N.check(N.lib().qe_hashagg_slot_capacity(self.handle, int(world), N.C.byref(cap)))
+        return cap.value
+
     def set_row_base(self, row_base: int) -> None:
         N.check(N.lib().qe_hashagg_set_row_base(self.handle, int(row_base)))
 
@@ -216,7 +222,8 @@ class HashAggregateState:
 
     def reset(self) -> None:
         N.check(N.lib().qe_hashagg_reset(self.handle))
-        self._held = None
+        # _held stays: the discarded update's kernel may still be reading those columns on the
+        # ctx stream. The next update replaces it after queueing behind that kernel.
 
     # ---- results ----------------------------------------------------------------------------------
     def num_groups(self) -> int:

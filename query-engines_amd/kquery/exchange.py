@@ -166,17 +166,17 @@ def exchange_partials(partial, owner, group: Optional[dist.ProcessGroup] = None,
     """Moves every group of `partial` (this rank's HashAggregateState) to the rank that owns its
     key and merges what this rank receives into `owner`. Returns the records received.
 
-    Fast path: fixed-capacity slots of `slot_records` groups per destination (default: the
-    state's expected groups spread over the ranks with headroom — 1.5x an even share plus 32,
-    at most the expected groups — the same on every rank), ONE all-to-all, no host round trip
+    Fast path: fixed-capacity slots of `slot_records` groups per destination (default:
+    qe_hashagg_slot_capacity — the create-time expected groups spread over the ranks with
+    headroom, 1.5x an even share plus 32, at most the expected groups — the same on every rank
+    whatever groups each rank's data produced), ONE all-to-all, no host round trip
     before it. If any rank had more groups for one owner than a slot holds, every rank sees it in
     the slot headers and all of them fall back to the variable-size exchange (counts all-to-all,
     then records)."""
     if getattr(partial, "keyed_by_dictionary", False):
         return exchange_keyed_partials(partial, owner, group)
     world = dist.get_world_size(group)
-    eg = int(partial.expected_groups)
-    cap = int(slot_records or min(eg, -(-3 * eg // (2 * world)) + 32))
+    cap = int(slot_records or partial.slot_capacity(world))
     recv = all_to_all_slots(partial.export_slots(world, cap), group)
     owner.prepare_output()  # host work of the owner's finalize, before the import's read-back
     n = owner.import_slots(recv, world, cap)

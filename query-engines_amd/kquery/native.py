@@ -202,6 +202,7 @@ SIGNATURES = [
     ("qe_copy_to_host", C.c_int, [_P, _P, _P, C.c_size_t]),
     ("qe_generate", C.c_int, [_P, _COLP, C.c_int32, C.c_int64, C.c_uint64, C.c_uint64, C.c_int64, C.c_int32]),
     ("qe_stream_read", C.c_int, [_P, _COLP, C.c_int32, C.POINTER(C.c_double)]),
+    ("qe_stream_read_best", C.c_int, [_P, _COLP, C.c_int32, C.c_int32, C.POINTER(C.c_double), C.c_char_p, C.c_int32]),
     ("qe_eval_arith", C.c_int, [_P, C.c_int32, _OPP, _OPP, _COLP]),
     ("qe_eval_cmp", C.c_int, [_P, C.c_int32, _OPP, _OPP, _COLP]),
     ("qe_eval_bool", C.c_int, [_P, C.c_int32, _COLP, _COLP, _COLP]),
@@ -225,6 +226,7 @@ SIGNATURES = [
     ("qe_hashagg_import", C.c_int, [_P, _P, C.c_int64]),
     ("qe_hashagg_export_slots", C.c_int, [_P, C.c_int32, C.c_int64, _P]),
     ("qe_hashagg_import_slots", C.c_int, [_P, _P, C.c_int32, C.c_int64, _I64P, _I64P]),
+    ("qe_hashagg_slot_capacity", C.c_int, [_P, C.c_int32, _I64P]),
     ("qe_comm_unique_id", C.c_int, [_P]),
     ("qe_comm_create", C.c_int, [_P, C.c_int32, C.c_int32, _P, C.POINTER(C.c_void_p)]),
     ("qe_comm_destroy", C.c_int, [_P]),
@@ -243,6 +245,8 @@ SIGNATURES = [
     ("qe_strdict_decode_tuple", C.c_int, [_P, _COLP, C.c_int32, _COLP]),
     ("qe_hash_partition", C.c_int, [_P, _COLP, C.c_int32, C.c_int32, _P]),
     ("qe_select_project", C.c_int, [_P, _COLP, C.c_int32, C.POINTER(QeSelectSpec), _COLP, _I64P]),
+    ("qe_select_project_async", C.c_int, [_P, _COLP, C.c_int32, C.POINTER(QeSelectSpec), _COLP, C.POINTER(_P)]),
+    ("qe_select_pending_wait", C.c_int, [_P, _I64P]),
     ("qe_csv_parse", C.c_int, [_P, _P, C.c_int64, C.POINTER(QeCsvOptions), _PP]),
     ("qe_csv_rows", C.c_int, [_P, _I64P]),
     ("qe_csv_column", C.c_int, [_P, C.c_int32, _COLP]),

@@ -278,21 +278,35 @@ class FusedSelectProjectExec(PhysicalPlan):
     def children(self) -> List[PhysicalPlan]:
         return [self.scan]
 
-    def run_batch(self, batch: RecordBatch) -> Optional[RecordBatch]:
+    def launch_batch(self, batch: RecordBatch):
+        """Queues the select-project of one batch (qe_select_project_async) and returns
+        (outputs, pending), or None when the kernel cannot take the plan."""
         cols = [batch.field(i) for i in self.slots]
         ctx = cols[0].ctx
         n = cols[0].length
         outs = [DeviceColumn.empty(t, n, self._may_be_null(k, cols), ctx=ctx) for k, t in enumerate(self.out_types)]
         cc = (N.QeColumn * len(cols))(*[c.as_c() for c in cols])
         oc = (N.QeColumn * len(outs))(*[o.as_c() for o in outs])
-        cnt = N.C.c_int64()
-        st = N.lib().qe_select_project(ctx.handle, cc, len(cols), N.C.byref(self.spec), oc, N.C.byref(cnt))
+        pending = N.C.c_void_p()
+        st = N.lib().qe_select_project_async(ctx.handle, cc, len(cols), N.C.byref(self.spec), oc, N.C.byref(pending))
         if st == N.QE_ERR_UNSUPPORTED:
             return None
         N.check(st)
+        return outs, pending, cols
+
+    def finish_batch(self, launched) -> RecordBatch:
+        """Waits for that batch's kernels only (not for what was queued behind them) and sets the
+        output row count."""
+        outs, pending, _cols = launched
+        cnt = N.C.c_int64()
+        N.check(N.lib().qe_select_pending_wait(pending, N.C.byref(cnt)))
         for o in outs:
             o.length = cnt.value
         return RecordBatch(self._schema, outs)
+
+    def run_batch(self, batch: RecordBatch) -> Optional[RecordBatch]:
+        launched = self.launch_batch(batch)
+        return None if launched is None else self.finish_batch(launched)
 
     def _may_be_null(self, k: int, cols: Sequence[DeviceColumn]) -> bool:
         """Whether output k can hold a null, as compile_program decides it (qe_hashagg.hip): a
@@ -309,12 +323,21 @@ class FusedSelectProjectExec(PhysicalPlan):
         return False
 
     def execute(self) -> Iterator[RecordBatch]:
+        """Pipelined one batch ahead: batch i+1's kernels are queued before batch i's row count is
+        read back, so the host wait for batch i overlaps batch i+1 on the device and the stream
+        never drains between batches. Batches come out in input order (row order preserved)."""
+        ahead = None
         for batch in self.scan.execute():
-            out = self.run_batch(batch)
-            if out is None:  # kernel specialisation unavailable: per-family operators
+            launched = self.launch_batch(batch)
+            if ahead is not None:
+                yield self.finish_batch(ahead)
+                ahead = None
+            if launched is None:  # kernel specialisation unavailable: per-family operators
                 yield from _replay(self.unfused, batch)
             else:
-                yield out
+                ahead = launched
+        if ahead is not None:
+            yield self.finish_batch(ahead)
 
     def __repr__(self) -> str:
         return f"FusedSelectProjectExec: slots={self.slots}, outputs={self.out_types}"

@@ -191,3 +191,36 @@ def test_persistent_grid_not_resident_reruns(gpu_ctx, monkeypatch, capfd):
     assert cnt == len(fa)
     assert (ab.to_numpy() == want).all()
     assert "rerunning with counter-ordered tiles" in capfd.readouterr().err
+
+
+def test_async_calls_queued_back_to_back(gpu_ctx, selproj_path):
+    """qe_select_project_async: several calls queued before any count is read back (the pipelined
+    FusedSelectProjectExec); each pending result is waited once and returns its own count, and the
+    outputs equal the synchronous call's."""
+    from kquery import native as N
+    from kquery.columnar import DeviceColumn
+    from kquery.datasource import C2_COLUMNS, generate_column
+
+    spec = None
+    pend, outs, wants = [], [], []
+    for i, (n, k) in enumerate([(100_003, 1 << 19), (4096, 0), (0, 5), (300_001, (1 << 20) - 7), (77, 1 << 10)]):
+        cols = [generate_column(s, n, 1000 * i, 42, gpu_ctx) for s in C2_COLUMNS]
+        spec = _spec(N, [(0, N.OP_GT, -1, k)], [[(N.TOK_COL, 0, None), (N.TOK_COL, 1, None), (N.TOK_ADD, 0, None)]])
+        o = DeviceColumn.empty(N.TYPE_INT64, n, True, ctx=gpu_ctx)
+        cc = (N.QeColumn * 2)(*[c.as_c() for c in cols])
+        oc = (N.QeColumn * 1)(o.as_c())
+        p = N.C.c_void_p()
+        N.check(N.lib().qe_select_project_async(gpu_ctx.handle, cc, 2, N.C.byref(spec), oc, N.C.byref(p)))
+        pend.append((p, cols, cc, oc))
+        outs.append(o)
+        a_h, _ = gen.generate(C2_COLUMNS[0].dist, C2_COLUMNS[0].param, 42, C2_COLUMNS[0].col_id, 1000 * i, n)
+        b_h, _ = gen.generate(C2_COLUMNS[1].dist, C2_COLUMNS[1].param, 42, C2_COLUMNS[1].col_id, 1000 * i, n)
+        m, mv = S.cmp(S.OP_GT, a_h, None, k, None)
+        fa, fb = S.filter_columns(m, mv, [a_h, b_h])
+        wants.append(S.arith(S.OP_ADD, fa, None, fb, None)[0])
+    for (p, _, _, _), o, want in zip(pend, outs, wants):
+        cnt = N.C.c_int64(-1)
+        N.check(N.lib().qe_select_pending_wait(p, N.C.byref(cnt)))
+        assert cnt.value == len(want)
+        o.length = cnt.value
+        assert (o.to_numpy() == want).all()

@@ -98,6 +98,36 @@ def main():
         report("C2 fused select+project (qe_select_project), 10M int64", n, 16 + 8 * sel_rows / n, ms_f,
                selected=sel_rows, call_ms=ms_k, call_gbs=n * (16 + 8 * sel_rows / n) / (ms_k * 1e-3) / 1e9,
                path="one hipRTC-specialised kernel: predicate, look-back compaction, projection")
+        # stream-ordered calls (qe_select_project_async): call i+1 is queued before call i's count
+        # is read back, as the pipelined FusedSelectProjectExec does batch to batch
+        def run_pipelined(k=20):
+            prev = None
+            for _ in range(k):
+                oc[0].length = n
+                pend = N.C.c_void_p()
+                N.check(N.lib().qe_select_project_async(ctx.handle, cc, 2, N.C.byref(fused.spec), oc, N.C.byref(pend)))
+                if prev is not None:
+                    N.check(N.lib().qe_select_pending_wait(prev, N.C.byref(cnt)))
+                prev = pend
+            N.check(N.lib().qe_select_pending_wait(prev, N.C.byref(cnt)))
+
+        ms_p = timed(run_pipelined, reps=5, warmup=1) / 20
+        report("C2 fused select+project, stream-ordered calls back to back (qe_select_project_async), 10M int64", n,
+               16 + 8 * sel_rows / n, ms_p, selected=sel_rows, path="20 async calls, each count read while the next runs")
+        # the pipelined operator over a Sequence of 8 batches of 10M rows
+        batches = [RecordBatch(schema, [generate_column(s, n, i * n, 42, ctx) for s in C2_COLUMNS]) for i in range(8)]
+        fused8 = fuse(ProjectionExec(SelectionExec(ScanExec(InMemoryDataSource(schema, batches), ["a", "b"]),
+                                                   GtExpression(ColumnExpression(0), LiteralLongExpression(1 << 19))),
+                                     Schema([Field("ab", N.TYPE_INT64)]),
+                                     [AddExpression(ColumnExpression(0), ColumnExpression(1))]))
+
+        def run_op8():
+            out["n8"] = sum(b.rowCount() for b in fused8.execute())
+
+        ms_o = timed(run_op8, reps=5, warmup=1) / 8
+        report("C2 pipelined FusedSelectProjectExec over 8 batches of 10M rows (per batch)", n,
+               16 + 8 * (out["n8"] / 8) / n, ms_o, selected=out["n8"])
+        del batches, fused8
         for sel_k in (1 << 13, (1 << 20) - (1 << 13)):  # ~1 % / ~99 % selectivity sweep
             spec2 = N.QeSelectSpec.from_buffer_copy(fused.spec)
             spec2.terms[0].lit = N.scalar(sel_k, N.TYPE_INT64)
