@@ -274,6 +274,16 @@ typedef struct qe_hashagg qe_hashagg;
 
 int qe_hashagg_create(qe_ctx* ctx, int32_t nkeys, const int32_t* key_types, int32_t naggs,
                       const qe_agg_desc* aggs, int64_t expected_groups, qe_hashagg** out);
+/* qe_hashagg_create with options. QE_HASHAGG_DETERMINISTIC: fp64 SUM / AVG accumulate in exact
+ * fixed point (32-bit limbs, least significant bit 2^-64, integer adds) instead of fp64 atomics, so
+ * their results are bit-identical whatever order rows, workgroups, batches or ranks combine in —
+ * as the reference's sequential row loop and ordered partition merge are (K:617-631, K:1314-1325).
+ * The sum is exact up to rounding each input to a multiple of 2^-64 and is then rounded once to
+ * double; inputs must be finite with |x| < 2^63 (else the update fails with
+ * QE_ERR_UNSUPPORTED). Costs three extra LDS words and atomics per fp64 SUM and slot. */
+#define QE_HASHAGG_DETERMINISTIC 1
+int qe_hashagg_create_ex(qe_ctx* ctx, int32_t nkeys, const int32_t* key_types, int32_t naggs,
+                         const qe_agg_desc* aggs, int64_t expected_groups, int32_t flags, qe_hashagg** out);
 int qe_hashagg_destroy(qe_hashagg* agg);
 /* Forget all groups (keeps allocations). */
 int qe_hashagg_reset(qe_hashagg* agg);

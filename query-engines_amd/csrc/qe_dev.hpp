@@ -50,7 +50,11 @@ constexpr int HA_GLOBAL_MAXP = 256;  // probe limit in the global table
 
 // Operand kinds understood by the device loaders (uniform per launch).
 enum SrcKind : int { K_LIT = 0, K_I64 = 1, K_F64 = 2, K_I32 = 3, K_U8 = 4, K_BOOL = 5 };
-enum AccKind : int { ACC_NONE = 0, ACC_SUM_I = 1, ACC_SUM_F = 2, ACC_MIN_I = 3, ACC_MAX_I = 4, ACC_MIN_F = 5, ACC_MAX_F = 6 };
+// ACC_SUM_X: fp64 SUM / AVG of a deterministic state (qe_hashagg_create_ex, QE_HASHAGG_DETERMINISTIC):
+// exact fixed-point accumulation in 32-bit limbs (fx_* below), so the result does not depend on the
+// order rows, workgroups, passes or ranks are combined in.
+enum AccKind : int { ACC_NONE = 0, ACC_SUM_I = 1, ACC_SUM_F = 2, ACC_MIN_I = 3, ACC_MAX_I = 4, ACC_MIN_F = 5, ACC_MAX_F = 6,
+                     ACC_SUM_X = 7 };
 enum TokOp : int {
   T_COL = 1, T_LIT, T_I2F0, T_I2F1,
   T_ADD_I, T_SUB_I, T_MUL_I, T_DIV_I,
@@ -173,6 +177,119 @@ __device__ inline qi64 idiv(qi64 a, qi64 b) {
 }
 
 __host__ __device__ inline bool acc_is_f64mm(int acc) { return acc == ACC_MIN_F || acc == ACC_MAX_F; }
+// Aggregates with four extra 64-bit words per slot (the idx arrays): fp64 MIN/MAX keep first-row
+// indices there, ACC_SUM_X its upper limbs and out-of-range count.
+__host__ __device__ inline bool acc_has_idx(int acc) { return acc_is_f64mm(acc) || acc == ACC_SUM_X; }
+__host__ __device__ inline qu64 idx_identity(int acc) { return acc_is_f64mm(acc) ? ~0ull : 0ull; }
+
+// ---- exact fixed-point fp64 sums (ACC_SUM_X) ---------------------------------------------------------
+// value = sum_k limb_k * 2^(32k - FX_LSB), k = 0..3, limbs int64 (two's complement sums of 32-bit
+// chunks; limb 3 carries the sign). Limb 0 lives in the slot's acc word, limbs 1..3 in idx words
+// 0..2, and idx word 3 counts inputs outside the representable range (NaN, +-Inf, |x| >= 2^63).
+// A row adds the chunks of its exactly scaled value; values below 2^-64 are rounded to the nearest
+// multiple of 2^-64 (ties to even). Integer adds are associative, so any combine order gives the
+// same limbs: deterministic, and exact up to that rounding. Sums stay exact while |sum| < 2^95.
+constexpr int FX_LSB = 64;
+__host__ __device__ inline int fx_clz64(qu64 x) {
+  int n = 0;
+  for (int b = 32; b; b >>= 1)
+    if (!(x >> (64 - b))) {
+      n += b;
+      x <<= b;
+    }
+  return x ? n : 64;
+}
+
+// Chunks of one value: c[0..3] limbs, c[4] = 1 if out of range (then the limbs are 0).
+__host__ __device__ inline void fx_split(qi64 bits, qi64 c[5]) {
+  c[0] = c[1] = c[2] = c[3] = c[4] = 0;
+  const qu64 b = (qu64)bits;
+  const bool neg = b >> 63;
+  const int ex = (int)((b >> 52) & 0x7FF);
+  qu64 m = b & ((1ull << 52) - 1);
+  if (ex == 0x7FF) {
+    c[4] = 1;
+    return;
+  }
+  int e = -1074;
+  if (ex) {
+    m |= 1ull << 52;
+    e = ex - 1075;
+  }
+  if (m == 0) return;
+  int p = e + FX_LSB;  // bit position of m's lowest bit in the fixed-point number
+  if (p < 0) {
+    const int sh = -p;
+    if (sh > 54) return;  // m < 2^53 <= half of 2^sh: rounds to 0
+    const qu64 q = m >> sh, rem = m & ((1ull << sh) - 1), half = 1ull << (sh - 1);
+    m = q + ((rem > half || (rem == half && (q & 1))) ? 1 : 0);
+    p = 0;
+    if (m == 0) return;
+  }
+  if (p + (64 - fx_clz64(m)) > 127) {  // |x| >= 2^63
+    c[4] = 1;
+    return;
+  }
+  const int L = p >> 5, q = p & 31;
+  const qu64 lo = m << q, hi = q ? (m >> (64 - q)) : 0ull;
+  const qi64 ch[3] = {(qi64)(lo & 0xFFFFFFFFull), (qi64)(lo >> 32), (qi64)hi};
+  for (int k = 0; k < 3; ++k)
+    if (L + k < 4) c[L + k] = neg ? -ch[k] : ch[k];
+}
+
+// Carry-propagate so limbs 0..2 are in [0, 2^32) and limb 3 holds the rest (signed).
+__host__ __device__ inline void fx_norm(qi64& l0, qi64& l1, qi64& l2, qi64& l3) {
+  qi64 c = l0 >> 32;
+  l0 -= c * 4294967296ll;
+  l1 += c;
+  c = l1 >> 32;
+  l1 -= c * 4294967296ll;
+  l2 += c;
+  c = l2 >> 32;
+  l2 -= c * 4294967296ll;
+  l3 += c;
+}
+
+// Correctly rounded double of the limbs (ties to even).
+__host__ __device__ inline double fx_to_double(qi64 l0, qi64 l1, qi64 l2, qi64 l3) {
+  fx_norm(l0, l1, l2, l3);
+  // 32-bit words of the 160-bit two's complement value (limb 3 split in two)
+  qu64 w[5] = {(qu64)l0, (qu64)l1, (qu64)l2, (qu64)l3 & 0xFFFFFFFFull, ((qu64)l3 >> 32) & 0xFFFFFFFFull};
+  const bool neg = l3 < 0;
+  if (neg) {  // magnitude: invert and add one
+    qu64 carry = 1;
+    for (int k = 0; k < 5; ++k) {
+      const qu64 v = ((~w[k]) & 0xFFFFFFFFull) + carry;
+      w[k] = v & 0xFFFFFFFFull;
+      carry = v >> 32;
+    }
+  }
+  int top = 4;
+  while (top >= 0 && w[top] == 0) --top;
+  if (top < 0) return 0.0;
+  // the top 64 bits below and including the leading one, plus a sticky bit for the rest
+  const int lz = fx_clz64(w[top]) - 32;  // leading zeros within the 32-bit word
+  const int msb = 32 * top + 31 - lz;    // bit index of the leading one
+  qu64 win = 0;
+  bool sticky = false;
+  for (int bit = 0; bit < 64; ++bit) {
+    const int i = msb - bit;
+    if (i < 0) break;
+    win |= ((w[i >> 5] >> (i & 31)) & 1ull) << (63 - bit);
+  }
+  for (int i = msb - 64; i >= 0 && !sticky; --i) sticky = (w[i >> 5] >> (i & 31)) & 1ull;
+  qu64 mant = win >> 11;  // 53 bits
+  const qu64 rem = win & 0x7FFull;
+  if (rem > 0x400 || (rem == 0x400 && (sticky || (mant & 1)))) ++mant;
+  int ex = msb - 52 - FX_LSB;  // exponent of the mantissa's lowest bit
+  if (mant >> 53) {
+    mant >>= 1;
+    ++ex;
+  }
+  // exact scaling by 2^ex: msb < 160, so -117 <= ex <= 44, a normal power of two
+  const double d = (double)mant * bits_f64((qi64)((qu64)(1023 + ex) << 52));
+  return neg ? -d : d;
+}
 __host__ __device__ inline qi64 acc_identity(int acc) {
   switch (acc) {
     case ACC_MIN_I:
@@ -185,7 +302,7 @@ __host__ __device__ inline qi64 acc_identity(int acc) {
 
 // Record layout (export/import/overflow):
 // [0] key  [8] flags (bit0 null key)  [16] cstar  then per aggregate: acc, nn, (4 x idx if fp64 MIN/MAX)
-__host__ __device__ inline int agg_rec_bytes(int acc) { return 16 + (acc_is_f64mm(acc) ? 32 : 0); }
+__host__ __device__ inline int agg_rec_bytes(int acc) { return 16 + (acc_has_idx(acc) ? 32 : 0); }
 
 // ---- global table -------------------------------------------------------------------------------------
 __device__ inline bool gtable_find(const DTable& t, qi64 key, bool knull, qu64& slot) {
@@ -272,6 +389,9 @@ __device__ inline void gcombine(const DTable& t, int acck, int j, qu64 s, qi64 a
       if (acc) atomicAdd((qu64*)&t.acc[j][s], (qu64)acc);
       break;
     case ACC_SUM_F: atomicAdd((double*)&t.acc[j][s], bits_f64(acc)); break;
+    case ACC_SUM_X:
+      if (acc) atomicAdd((qu64*)&t.acc[j][s], (qu64)acc);
+      break;
     case ACC_MIN_I:
     case ACC_MIN_F:
       if (acc != 0x7FFFFFFFFFFFFFFFll) atomicMin(&t.acc[j][s], acc);
@@ -289,6 +409,16 @@ __device__ inline void gcombine(const DTable& t, int acck, int j, qu64 s, qi64 a
     if (i1 != ~0ull) atomicMin(&ix[stride + s], i1);
     if (i2 != ~0ull) atomicMin(&ix[2 * stride + s], i2);
     if (i3 != ~0ull) atomicMin(&ix[3 * stride + s], i3);
+  } else if (acck == ACC_SUM_X) {  // upper limbs and the out-of-range count: plain integer adds
+    const qu64 stride = t.cap + 2;
+    qu64* ix = t.idx[j];
+    if (i0) atomicAdd(&ix[s], i0);
+    if (i1) atomicAdd(&ix[stride + s], i1);
+    if (i2) atomicAdd(&ix[2 * stride + s], i2);
+    if (i3) {  // inputs the fixed point could not hold: the update reports them (ctl[6])
+      atomicAdd(&ix[3 * stride + s], i3);
+      atomicAdd(&t.ctl[6], i3);
+    }
   }
 }
 
@@ -310,6 +440,7 @@ __device__ inline void gcombine_excl(const DTable& t, int acck, int j, qu64 s, q
   switch (acck) {
     case ACC_SUM_I: *a = (qi64)((qu64)*a + (qu64)acc); break;
     case ACC_SUM_F: *a = f64_bits(bits_f64(*a) + bits_f64(acc)); break;
+    case ACC_SUM_X: *a = (qi64)((qu64)*a + (qu64)acc); break;
     case ACC_MIN_I:
     case ACC_MIN_F:
       if (acc < *a) *a = acc;
@@ -327,6 +458,13 @@ __device__ inline void gcombine_excl(const DTable& t, int acck, int j, qu64 s, q
     if (i1 < ix[stride]) ix[stride] = i1;
     if (i2 < ix[2 * stride]) ix[2 * stride] = i2;
     if (i3 < ix[3 * stride]) ix[3 * stride] = i3;
+  } else if (acck == ACC_SUM_X) {
+    const qu64 stride = t.cap + 2;
+    qu64* ix = t.idx[j] + s;
+    ix[0] += i0;
+    ix[stride] += i1;
+    ix[2 * stride] += i2;
+    ix[3 * stride] += i3;
   }
 }
 
@@ -343,6 +481,16 @@ __device__ inline RowVal row_partial(int acck, qi64 x, qu64 row) {
     case ACC_SUM_F:
     case ACC_MIN_I:
     case ACC_MAX_I: r.acc = x; break;
+    case ACC_SUM_X: {
+      qi64 c[5];
+      fx_split(x, c);
+      r.acc = c[0];
+      r.i0 = (qu64)c[1];
+      r.i1 = (qu64)c[2];
+      r.i2 = (qu64)c[3];
+      r.i3 = (qu64)c[4];
+      break;
+    }
     case ACC_MIN_F:
     case ACC_MAX_F: {
       const double d = bits_f64(x);
@@ -385,6 +533,22 @@ __device__ inline int lds_probe(qi64* keys, int log2, qi64 key, qu32 h) {
     h = (h + 1) & mask;
   }
   return -1;
+}
+
+// ACC_SUM_X row into LDS limbs (acc[s] = limb 0, idx[k * SS + s] = limb k + 1, idx[3 SS + s] =
+// out-of-range count). Returns false for an out-of-range input (the caller flags the launch).
+__device__ inline bool lds_fx_add(qi64* acc, qu64* idx, int SS, int s, qi64 x) {
+  qi64 c[5];
+  fx_split(x, c);
+  if (c[0]) atomicAdd((qu64*)&acc[s], (qu64)c[0]);
+  if (c[1]) atomicAdd(&idx[s], (qu64)c[1]);
+  if (c[2]) atomicAdd(&idx[SS + s], (qu64)c[2]);
+  if (c[3]) atomicAdd(&idx[2 * SS + s], (qu64)c[3]);
+  if (c[4]) {
+    atomicAdd(&idx[3 * SS + s], 1ull);
+    return false;
+  }
+  return true;
 }
 
 // fp64 MIN/MAX row into LDS accumulators (MaxAccumulator order semantics, Main.kt:538-561).

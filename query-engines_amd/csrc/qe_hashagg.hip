@@ -60,9 +60,10 @@ __device__ __forceinline__ void lds_init(const Plan& P, char* smem) {
       qu32* nn = (qu32*)(smem + P.off_nn[j]);
       for (int s = threadIdx.x; s < SS; s += blockDim.x) nn[s] = 0;
     }
-    if (acc_is_f64mm(a.acc)) {
+    if (acc_has_idx(a.acc)) {
       qu64* ix = (qu64*)(smem + P.off_idx[j]);
-      for (int s = threadIdx.x; s < 4 * SS; s += blockDim.x) ix[s] = ~0ull;
+      const qu64 id = idx_identity(a.acc);
+      for (int s = threadIdx.x; s < 4 * SS; s += blockDim.x) ix[s] = id;
     }
   }
 }
@@ -84,6 +85,9 @@ __device__ __forceinline__ void lds_accum(const Plan& P, char* smem, int j, int 
   switch (a.acc) {
     case ACC_SUM_I: atomicAdd((unsigned long long*)&acc[s], (unsigned long long)x); break;
     case ACC_SUM_F: atomicAdd((double*)&acc[s], bits_f64(x)); break;
+    case ACC_SUM_X:  // (an out-of-range input is counted in the slot; the flush reports it)
+      (void)lds_fx_add(acc, (qu64*)(smem + P.off_idx[j]), (1 << P.lds_log2) + 2, s, x);
+      break;
     case ACC_MIN_I: atomicMin((long long*)&acc[s], (long long)x); break;
     case ACC_MAX_I: atomicMax((long long*)&acc[s], (long long)x); break;
     case ACC_MIN_F:
@@ -136,23 +140,24 @@ __device__ __forceinline__ void lds_flush(const Plan& P, char* smem) {
     for (int j = 0; j < QE_MAX_AGGS; ++j) {
       if (j >= P.naggs) break;
       const DAgg& a = P.aggs[j];
-      const qi64 acc = a.acc != ACC_NONE ? ((const qi64*)(smem + P.off_acc[j]))[s] : 0;
+      qi64 acc = a.acc != ACC_NONE ? ((const qi64*)(smem + P.off_acc[j]))[s] : 0;
       const qu64 nn = a.track_nn ? ((const qu32*)(smem + P.off_nn[j]))[s] : c;
       qu64 i0 = ~0ull, i1 = ~0ull, i2 = ~0ull, i3 = ~0ull;
-      if (acc_is_f64mm(a.acc)) {
+      if (acc_has_idx(a.acc)) {
         const qu64* ix = (const qu64*)(smem + P.off_idx[j]);
         i0 = ix[s];
         i1 = ix[SS + s];
         i2 = ix[2 * SS + s];
         i3 = ix[3 * SS + s];
       }
+      if (a.acc == ACC_SUM_X) fx_norm(acc, (qi64&)i0, (qi64&)i1, (qi64&)i2);
       if (ok) {
         if (a.fn != QE_AGG_COUNT_STAR) gcombine(P.t, a.acc, j, gs, acc, nn, i0, i1, i2, i3);
       } else {
         qu64* f = (qu64*)(rec + off);
         f[0] = (qu64)acc;
         f[1] = nn;
-        if (acc_is_f64mm(a.acc)) {
+        if (acc_has_idx(a.acc)) {
           f[2] = i0;
           f[3] = i1;
           f[4] = i2;
@@ -507,6 +512,7 @@ __device__ __forceinline__ void lds_accum4(const Plan& P, char* smem, int j, con
       break;
     case ACC_MIN_F:
     case ACC_MAX_F:
+    case ACC_SUM_X:
 #pragma unroll
       for (int r = 0; r < 4; ++r)
         if ((m >> r) & 1) lds_accum(P, smem, j, slot[r], x[r], true, (qu64)(row0 + row_of(0, lane, r)));
@@ -908,8 +914,8 @@ __global__ void k_table_init(DTable t, AggMeta m, qu64* zero_ctl) {
     for (int j = 0; j < m.naggs; ++j) {
       t.acc[j][s] = acc_identity(m.acc[j]);
       t.nn[j][s] = 0;
-      if (acc_is_f64mm(m.acc[j]))
-        for (int k = 0; k < 4; ++k) t.idx[j][k * SS + s] = ~0ull;
+      if (acc_has_idx(m.acc[j]))
+        for (int k = 0; k < 4; ++k) t.idx[j][k * SS + s] = idx_identity(m.acc[j]);
     }
   }
 }
@@ -958,7 +964,7 @@ __global__ void k_rehash(DTable src, DTable dst, AggMeta m) {
       a.fn = m.fn[j];
       a.acc = m.acc[j];
       qu64 i[4] = {~0ull, ~0ull, ~0ull, ~0ull};
-      if (acc_is_f64mm(a.acc))
+      if (acc_has_idx(a.acc))
         for (int k = 0; k < 4; ++k) i[k] = src.idx[j][k * SS + s];
       gcombine(dst, a.acc, j, d, src.acc[j][s], slot_nn(src, m, j, s), i[0], i[1], i[2], i[3]);
     }
@@ -984,7 +990,7 @@ __device__ void import_record(const qu8* __restrict__ rec, DTable& dst, const Ag
     a.acc = m.acc[j];
     const qu64* f = (const qu64*)(rec + off);
     if (a.fn != QE_AGG_COUNT_STAR) {
-      if (acc_is_f64mm(a.acc)) gcombine(dst, a.acc, j, d, (qi64)f[0], f[1], f[2], f[3], f[4], f[5]);
+      if (acc_has_idx(a.acc)) gcombine(dst, a.acc, j, d, (qi64)f[0], f[1], f[2], f[3], f[4], f[5]);
       else gcombine(dst, a.acc, j, d, (qi64)f[0], f[1], ~0ull, ~0ull, ~0ull, ~0ull);
     }
     off += agg_rec_bytes(a.acc);
@@ -1088,7 +1094,7 @@ __device__ void write_record(qu8* rec, const DTable& t, const AggMeta& m, qu64 s
     qu64* f = (qu64*)(rec + off);
     f[0] = (qu64)t.acc[j][s];
     f[1] = slot_nn(t, m, j, s);
-    if (acc_is_f64mm(m.acc[j]))
+    if (acc_has_idx(m.acc[j]))
       for (int k = 0; k < 4; ++k) f[2 + k] = t.idx[j][k * SS + s];
     off += agg_rec_bytes(m.acc[j]);
   }
@@ -1214,6 +1220,15 @@ __device__ __forceinline__ void put_bit(qu8* gbm, qu32* lbits, int col, qi64 o, 
   else set_bit(gbm, o, true);
 }
 
+// An ACC_SUM_X slot's value (limb 0 = acc, limbs 1..3 and the out-of-range count in idx); NaN if an
+// input could not be represented (the update reported it as an error already).
+__device__ __forceinline__ double fx_sum(const DTable& t, int j, qu64 s, qi64 acc) {
+  const qu64 SS = t.cap + 2;
+  const qu64* ix = t.idx[j];
+  if (ix[3 * SS + s]) return bits_f64(0x7FF8000000000000ll);
+  return fx_to_double(acc, (qi64)ix[s], (qi64)ix[SS + s], (qi64)ix[2 * SS + s]);
+}
+
 __device__ __forceinline__ void finalize_slot(const DTable& t, const AggMeta& m, const KeyMeta& km,
                                               const OutCols& out, qu64 s, qi64 o, qu32* lbits = nullptr) {
   const qu64 SS = t.cap + 2;
@@ -1244,9 +1259,16 @@ __device__ __forceinline__ void finalize_slot(const DTable& t, const AggMeta& m,
     switch (m.fn[j]) {
       case QE_AGG_COUNT: val = (qi64)nn; valid = true; break;
       case QE_AGG_COUNT_STAR: val = (qi64)cst; valid = true; break;
-      case QE_AGG_AVG: val = f64_bits(bits_f64(acc) / (double)nn); break;
+      case QE_AGG_AVG:
+        if (m.acc[j] == ACC_SUM_X)
+          val = f64_bits(fx_sum(t, j, s, acc) / (double)nn);
+        else
+          val = f64_bits(bits_f64(acc) / (double)nn);
+        break;
       default:
-        if (acc_is_f64mm(m.acc[j])) {
+        if (m.acc[j] == ACC_SUM_X) {
+          val = f64_bits(fx_sum(t, j, s, acc));
+        } else if (acc_is_f64mm(m.acc[j])) {
           const qu64 i0 = t.idx[j][s], i1 = t.idx[j][SS + s];
           const qu64 i2 = t.idx[j][2 * SS + s], i3 = t.idx[j][3 * SS + s];
           if (i1 != ~0ull && i1 == i0) {
@@ -1472,7 +1494,7 @@ static int nn_materialize(qe_hashagg* h, int32_t mask) {
 static size_t table_bytes(const qe_hashagg* h, uint64_t cap) {
   const uint64_t SS = cap + 2;
   size_t b = 16 * SS;
-  for (int j = 0; j < h->naggs; ++j) b += (16 + (acc_is_f64mm(h->acc[j]) ? 32 : 0)) * SS;
+  for (int j = 0; j < h->naggs; ++j) b += (16 + (acc_has_idx(h->acc[j]) ? 32 : 0)) * SS;
   return b;
 }
 
@@ -1491,7 +1513,7 @@ static int table_alloc(qe_hashagg* h, uint64_t cap, void** mem, DTable* t) {
     p += 8 * SS;
     t->nn[j] = (qu64*)p;
     p += 8 * SS;
-    if (acc_is_f64mm(h->acc[j])) {
+    if (acc_has_idx(h->acc[j])) {
       t->idx[j] = (qu64*)p;
       p += 32 * SS;
     }
@@ -1504,7 +1526,8 @@ static int table_alloc(qe_hashagg* h, uint64_t cap, void** mem, DTable* t) {
 }
 
 // ctl words: [0] groups, [1] deferred rows, [2] overflow records, [3] lost groups,
-// [4] largest slot count reported by the senders of an import_slots, [5] their records in total
+// [4] largest slot count reported by the senders of an import_slots, [5] their records in total,
+// [6] fp64 SUM inputs a deterministic state could not represent (NaN, +-Inf, |x| >= 2^63)
 // ctl[3] is sticky: every path that can drop a group (k_rehash, k_import, k_import_slots, the
 // fused kernel's overflow area) adds to it and nothing but a reset clears it, so a loss in a
 // launch with no read-back of its own (qe_hashagg_import_slots queues k_import_slots and returns)
@@ -1765,7 +1788,7 @@ static size_t lds_layout_at(const qe_hashagg* h, Plan* P, int log2) {
       off += 4 * SS;
       off = (off + 15) & ~size_t(15);
     }
-    if (acc_is_f64mm(a.acc)) {
+    if (acc_has_idx(a.acc)) {
       P->off_idx[j] = (int32_t)off;
       off += 32 * SS;
     }
@@ -1806,7 +1829,7 @@ static size_t lds_bytes_min(const qe_hashagg* h, int log2) {
   size_t b = 12 * SS + 16;
   for (int j = 0; j < h->naggs; ++j) {
     if (h->acc[j] != ACC_NONE) b += 8 * SS;
-    if (acc_is_f64mm(h->acc[j])) b += 32 * SS;
+    if (acc_has_idx(h->acc[j])) b += 32 * SS;
   }
   return b;
 }
@@ -2154,6 +2177,9 @@ static int settle_pass(qe_hashagg* h, const Plan& P, int* out_i, const uint32_t*
     h->last_launches += 1;
   }
   QE_CHECK(c[3] == 0, QE_ERR_CAPACITY, "hash aggregate lost %llu groups (overflow area)", (unsigned long long)c[3]);
+  QE_CHECK(c[6] == 0, QE_ERR_UNSUPPORTED,
+           "deterministic fp64 SUM: %llu inputs outside the exact fixed-point range (NaN, +-Inf or |x| >= 2^63)",
+           (unsigned long long)c[6]);
   const uint64_t groups = c[0], deferred = c[1], ovf_recs = std::min<uint64_t>(c[2], P.ovf_cap);
   h->ctl_rows_clean = c[1] == 0 && c[2] == 0;
   *done = true;
@@ -2420,7 +2446,14 @@ extern "C" {
 
 int qe_hashagg_create(qe_ctx* ctx, int32_t nkeys, const int32_t* key_types, int32_t naggs, const qe_agg_desc* aggs,
                       int64_t expected_groups, qe_hashagg** out) {
+  return qe_hashagg_create_ex(ctx, nkeys, key_types, naggs, aggs, expected_groups, 0, out);
+}
+
+int qe_hashagg_create_ex(qe_ctx* ctx, int32_t nkeys, const int32_t* key_types, int32_t naggs, const qe_agg_desc* aggs,
+                         int64_t expected_groups, int32_t flags, qe_hashagg** out) {
   QE_TRY(ctx_enter(ctx));
+  QE_CHECK((flags & ~QE_HASHAGG_DETERMINISTIC) == 0, QE_ERR_INVALID_ARG, "unknown flags 0x%x", flags);
+  const bool det = (flags & QE_HASHAGG_DETERMINISTIC) != 0;
   QE_CHECK(out, QE_ERR_INVALID_ARG, "null out");
   QE_CHECK(nkeys >= 0 && nkeys <= QE_MAX_KEYS, QE_ERR_UNSUPPORTED, "0..%d group keys supported", QE_MAX_KEYS);
   QE_CHECK(naggs >= 0 && naggs <= QE_MAX_AGGS, QE_ERR_UNSUPPORTED, "0..%d aggregates supported", QE_MAX_AGGS);
@@ -2482,10 +2515,10 @@ int qe_hashagg_create(qe_ctx* ctx, int32_t nkeys, const int32_t* key_types, int3
       return bail(fail(QE_ERR_UNSUPPORTED, "aggregate %d: input type %d (int64/int32/date32/uint8/fp64 only)", j,
                        d.input_type));
     switch (d.fn) {
-      case QE_AGG_SUM: h->acc[j] = f ? ACC_SUM_F : ACC_SUM_I; break;
+      case QE_AGG_SUM: h->acc[j] = f ? (det ? ACC_SUM_X : ACC_SUM_F) : ACC_SUM_I; break;
       case QE_AGG_MIN: h->acc[j] = f ? ACC_MIN_F : ACC_MIN_I; break;
       case QE_AGG_MAX: h->acc[j] = f ? ACC_MAX_F : ACC_MAX_I; break;
-      case QE_AGG_AVG: h->acc[j] = ACC_SUM_F; break;
+      case QE_AGG_AVG: h->acc[j] = det ? ACC_SUM_X : ACC_SUM_F; break;
       case QE_AGG_COUNT:
       case QE_AGG_COUNT_STAR: h->acc[j] = ACC_NONE; break;
       default: return bail(fail(QE_ERR_UNSUPPORTED, "aggregate %d: unknown function %d", j, d.fn));

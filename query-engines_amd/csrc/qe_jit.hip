@@ -299,7 +299,7 @@ void emit_lds_table(const Plan& P, std::ostringstream& o, int log2, size_t* lds_
       o << "  __shared__ qu32 s_nn" << j << "[SS];\n";
       lds += 4 * SS;
     }
-    if (acc_is_f64mm(a.acc)) {
+    if (acc_has_idx(a.acc)) {
       o << "  __shared__ qu64 s_idx" << j << "[4 * SS];\n";
       lds += 32 * SS;
     }
@@ -310,8 +310,9 @@ void emit_lds_table(const Plan& P, std::ostringstream& o, int log2, size_t* lds_
     const DAgg& a = P.aggs[j];
     if (a.acc != ACC_NONE) o << "    s_acc" << j << "[s] = " << acc_init(a.acc) << ";\n";
     if (a.track_nn) o << "    s_nn" << j << "[s] = 0;\n";
-    if (acc_is_f64mm(a.acc))
-      o << "    for (int k = 0; k < 4; ++k) s_idx" << j << "[k * SS + s] = ~0ull;\n";
+    if (acc_has_idx(a.acc))
+      o << "    for (int k = 0; k < 4; ++k) s_idx" << j << "[k * SS + s] = " << (acc_is_f64mm(a.acc) ? "~0ull" : "0ull")
+        << ";\n";
   }
   o << "  }\n  __syncthreads();\n";
 }
@@ -346,6 +347,7 @@ void emit_agg_rows(const Plan& P, std::ostringstream& o, const std::vector<std::
     switch (a.acc) {
       case ACC_SUM_I: o << "        atomicAdd((qu64*)&s_acc" << js << "[s], (qu64)x);\n"; break;
       case ACC_SUM_F: o << "        atomicAdd((double*)&s_acc" << js << "[s], bits_f64(x));\n"; break;
+      case ACC_SUM_X: o << "        (void)lds_fx_add(s_acc" << js << ", s_idx" << js << ", SS, s, x);\n"; break;
       case ACC_MIN_I: o << "        atomicMin(&s_acc" << js << "[s], x);\n"; break;
       case ACC_MAX_I: o << "        atomicMax(&s_acc" << js << "[s], x);\n"; break;
       case ACC_MIN_F:
@@ -402,13 +404,14 @@ void emit_flush(const Plan& P, std::ostringstream& o, bool mark_full = false, bo
   for (int j = 0; j < P.naggs; ++j) {
     const DAgg& a = P.aggs[j];
     const std::string js = std::to_string(j);
-    o << "    {\n      const qi64 acc = " << (a.acc != ACC_NONE ? "s_acc" + js + "[s]" : std::string("0")) << ";\n"
+    o << "    {\n      qi64 acc = " << (a.acc != ACC_NONE ? "s_acc" + js + "[s]" : std::string("0")) << ";\n"
       << "      const qu64 nn = " << (a.track_nn ? "s_nn" + js + "[s]" : std::string("c")) << ";\n";
-    if (acc_is_f64mm(a.acc))
-      o << "      const qu64 i0 = s_idx" << js << "[s], i1 = s_idx" << js << "[SS + s], i2 = s_idx" << js
+    if (acc_has_idx(a.acc))
+      o << "      qu64 i0 = s_idx" << js << "[s], i1 = s_idx" << js << "[SS + s], i2 = s_idx" << js
         << "[2 * SS + s], i3 = s_idx" << js << "[3 * SS + s];\n";
     else
       o << "      const qu64 i0 = ~0ull, i1 = ~0ull, i2 = ~0ull, i3 = ~0ull;\n";
+    if (a.acc == ACC_SUM_X) o << "      fx_norm(acc, (qi64&)i0, (qi64&)i1, (qi64&)i2);\n";
     const bool skip_nn = (P.nn_skip >> j) & 1;
     const char* add_nn = skip_nn ? "false" : "true";
     if (a.fn != QE_AGG_COUNT_STAR && part)
@@ -417,7 +420,7 @@ void emit_flush(const Plan& P, std::ostringstream& o, bool mark_full = false, bo
     else if (a.fn != QE_AGG_COUNT_STAR && !(a.acc == ACC_NONE && skip_nn))  // implicit COUNT(x): nothing to add
       o << "      if (ok) gcombine(P.t, " << a.acc << ", " << j << ", gs, acc, nn, i0, i1, i2, i3, " << add_nn << ");\n";
     o << "      if (!ok) { qu64* f = (qu64*)(rec + " << off << "); f[0] = (qu64)acc; f[1] = nn;";
-    if (acc_is_f64mm(a.acc)) o << " f[2] = i0; f[3] = i1; f[4] = i2; f[5] = i3;";
+    if (acc_has_idx(a.acc)) o << " f[2] = i0; f[3] = i1; f[4] = i2; f[5] = i3;";
     o << " }\n    }\n";
     off += agg_rec_bytes(a.acc);
   }

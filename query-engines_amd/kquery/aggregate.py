@@ -105,11 +105,13 @@ class HashAggregateState:
     """Owns one qe_hashagg. Keys: ``key_types``; aggregates: (fn, input_type) pairs."""
 
     def __init__(self, ctx: Context, key_types: Sequence[int], aggs: Sequence[Tuple[int, int]],
-                 expected_groups: int = 1024, async_update: bool = False):
+                 expected_groups: int = 1024, async_update: bool = False, deterministic: bool = False):
         """``async_update``: stream-ordered updates (qe_hashagg_set_async) — an update returns once
         its kernel is queued and is checked by the next call on the state (finalize, num_groups,
         the next update), which may re-read the update's columns; the state holds a reference to
-        them until the next update or reset."""
+        them until the next update or reset.
+        ``deterministic``: fp64 SUM / AVG in exact fixed point (QE_HASHAGG_DETERMINISTIC): results
+        are bit-identical run to run, like the reference's ordered row loop and merge."""
         from .strdict import StringDictionary
 
         self.ctx = ctx
@@ -130,8 +132,10 @@ class HashAggregateState:
         kt = (N.C.c_int32 * max(1, len(self.device_key_types)))(*self.device_key_types)
         ad = (N.QeAggDesc * max(1, len(self.aggs)))(*[N.QeAggDesc(f, t) for f, t in self.aggs])
         h = N.C.c_void_p()
-        N.check(N.lib().qe_hashagg_create(ctx.handle, len(self.device_key_types), kt, len(self.aggs), ad,
-                                          int(expected_groups), N.C.byref(h)))
+        N.check(N.lib().qe_hashagg_create_ex(ctx.handle, len(self.device_key_types), kt, len(self.aggs), ad,
+                                             int(expected_groups), N.HASHAGG_DETERMINISTIC if deterministic else 0,
+                                             N.C.byref(h)))
+        self.deterministic = bool(deterministic)
         self.handle = h
         self._out_rows = max(1, 2 * self.expected_groups)  # finalize's first output sizing guess
         self.async_update = bool(async_update)

@@ -178,6 +178,7 @@ class QeSelectSpec(C.Structure):
 _lib = None
 
 # (name, restype, argtypes) for every entry point declared in include/qe_hip.h
+HASHAGG_DETERMINISTIC = 1  # qe_hashagg_create_ex flag
 _P = C.c_void_p
 _PP = C.POINTER(C.c_void_p)
 _I64P = C.POINTER(C.c_int64)
@@ -214,6 +215,8 @@ SIGNATURES = [
     ("qe_agg_global_merge", C.c_int, [_P, C.c_int32, _P, C.c_int32, C.POINTER(QeGlobalAgg)]),
     ("qe_hashagg_create", C.c_int,
      [_P, C.c_int32, C.POINTER(C.c_int32), C.c_int32, C.POINTER(QeAggDesc), C.c_int64, _PP]),
+    ("qe_hashagg_create_ex", C.c_int,
+     [_P, C.c_int32, C.POINTER(C.c_int32), C.c_int32, C.POINTER(QeAggDesc), C.c_int64, C.c_int32, _PP]),
     ("qe_hashagg_destroy", C.c_int, [_P]),
     ("qe_hashagg_reset", C.c_int, [_P]),
     ("qe_hashagg_update", C.c_int, [_P, _COLP, _COLP, _COLP]),

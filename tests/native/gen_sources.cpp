@@ -97,6 +97,7 @@ static int emit_agg(const char* dir, const char* name, const qe_column* cols, in
     P.aggs[j].fn = aggs[j].fn;
     P.aggs[j].acc = aggs[j].acc;
     P.aggs[j].track_nn = nullable ? 1 : 0;
+    P.aggs[j].pkind = aggs[j].prog ? 2 : 0;  // token program (compile_plan's general form)
   }
   P.mp_n = 2;
   P.mp_pass = 0;
@@ -166,5 +167,8 @@ int main(int argc, char** argv) {
   cols[2].validity = vdummy;
   const AggIn fx[2] = {{QE_AGG_MAX, ACC_MAX_F, &pb}, {QE_AGG_COUNT_STAR, ACC_NONE, nullptr}};
   rc |= emit_agg(argv[1], "f64max", cols, 3, &t4, 1, fx, 2, 11);
+  // deterministic state: fp64 SUM and AVG in exact fixed point (ACC_SUM_X)
+  const AggIn dx[3] = {{QE_AGG_SUM, ACC_SUM_X, &pb}, {QE_AGG_AVG, ACC_SUM_X, &pb}, {QE_AGG_COUNT_STAR, ACC_NONE, nullptr}};
+  rc |= emit_agg(argv[1], "det", cols, 3, &t4, 1, dx, 3, 10);
   return rc;
 }

@@ -8,7 +8,9 @@ design documents otherwise:
 * hash-aggregate fp64 SUM / AVG: the per-group sums combine workgroup partials with fp64 atomics,
   so their rounding depends on arrival order. Run to run they must agree within 1e-13 × Σ|x| of
   the group (a condition-aware bound: cancelling sums amplify the relative spread; the parity
-  contract of 1e-9 against the oracle holds either way) — DESIGN.md "Determinism".
+  contract of 1e-9 against the oracle holds either way) — DESIGN.md "Determinism";
+* a deterministic state (QE_HASHAGG_DETERMINISTIC) sums fp64 in exact fixed point: bit-identical
+  across runs, streams, batchings and kernel paths, and equal to math.fsum of each group.
 Group ORDER is unspecified (HashMap iteration order, K:639), so groups are compared as maps."""
 import numpy as np
 import pytest
@@ -145,3 +147,71 @@ def test_csv_cast_string_keys(gpu_ctx, tmp_path):
         groups = dict(zip(keys[0].to_pylist(), zip(*[v.to_pylist() for v in vals])))
         outs.append((_bits(b.field(0)), _bits(fs), _bits(out), groups))
     assert all(o == outs[0] for o in outs[1:])
+
+
+@pytest.mark.parametrize("groups,expected,path", [(37, 64, "lds"), (4500, 4500, "two-bucket"),
+                                                   (50_000, 50_000, "partitioned"), (300, 64, "generic")])
+def test_deterministic_fp64_group_sums(gpu_ctx, groups, expected, path):
+    """QE_HASHAGG_DETERMINISTIC: fp64 SUM / AVG in exact fixed point. Every run — default stream,
+    second context, two batches instead of one — gives the same bits, and they equal the correctly
+    rounded exact sum (math.fsum) of each group, as the reference's ordered row loop would give
+    with exact arithmetic. Values here have no bits below 2^-64, so the fixed point is exact."""
+    import math
+
+    from kquery import native as N
+    from kquery.aggregate import HashAggregateState
+    from kquery.columnar import DeviceColumn
+
+    rng = np.random.default_rng(groups)
+    n = 3_000_000
+    k = rng.integers(0, groups, n).astype(np.int64)
+    x = rng.normal(size=n) * np.exp2(rng.integers(-20, 30, n))  # wide range: fp64 atomics would wobble
+    x = np.round(x * 2.0 ** 60) * 2.0 ** -60  # multiples of 2^-60: held exactly by the fixed point
+    xv = rng.random(n) > 0.05
+    aggs = [(N.AGG_SUM, N.TYPE_FLOAT64), (N.AGG_AVG, N.TYPE_FLOAT64), (N.AGG_COUNT_STAR, N.TYPE_INT64)]
+    runs = []
+    for i, ctx in enumerate(_runs(gpu_ctx)):
+        if path == "generic":
+            N.check(N.lib().qe_ctx_set_jit(ctx.handle, 0))
+        try:
+            st = HashAggregateState(ctx, [N.TYPE_INT64], aggs, expected, deterministic=True)
+            cuts = [0, n] if i % 2 == 0 else [0, n // 3, n]  # one batch, or two
+            for lo, hi in zip(cuts[:-1], cuts[1:]):
+                kc = DeviceColumn.from_numpy(N.TYPE_INT64, k[lo:hi], None, ctx=ctx)
+                xc = DeviceColumn.from_numpy(N.TYPE_FLOAT64, x[lo:hi], xv[lo:hi], ctx=ctx)
+                st.update([kc], [xc, xc, None])
+            keys, vals = st.finalize()
+            ctx.synchronize()
+        finally:
+            N.check(N.lib().qe_ctx_set_jit(ctx.handle, 1))
+        cols = [v.to_numpy() for v in vals]
+        kv = keys[0].to_numpy()
+        runs.append({int(kv[g]): (cols[0][g].tobytes(), cols[1][g].tobytes(), int(cols[2][g])) for g in range(len(kv))})
+    assert all(r == runs[0] for r in runs[1:])
+    order = np.argsort(k, kind="stable")
+    ks, xs, vs = k[order], x[order], xv[order]
+    bounds = np.searchsorted(ks, np.arange(groups + 1))
+    for g in range(groups):
+        lo, hi = bounds[g], bounds[g + 1]
+        vals_g = xs[lo:hi][vs[lo:hi]]
+        want = math.fsum(vals_g.tolist())
+        got_sum, got_avg, cstar = runs[0][g]
+        assert cstar == hi - lo
+        assert np.frombuffer(got_sum, np.float64)[0] == want, g
+        assert np.frombuffer(got_avg, np.float64)[0] == want / len(vals_g), g
+
+
+def test_deterministic_rejects_unrepresentable(gpu_ctx):
+    """NaN / Inf / |x| >= 2^63 cannot be held by the fixed point: the update fails loudly."""
+    from kquery import native as N
+    from kquery.aggregate import HashAggregateState
+    from kquery.columnar import DeviceColumn
+
+    for bad in (np.nan, np.inf, 2.0 ** 70):
+        x = np.ones(1000)
+        x[500] = bad
+        st = HashAggregateState(gpu_ctx, [N.TYPE_INT64], [(N.AGG_SUM, N.TYPE_FLOAT64)], 16, deterministic=True)
+        kc = DeviceColumn.from_numpy(N.TYPE_INT64, np.arange(1000, dtype=np.int64) % 7, None, ctx=gpu_ctx)
+        with pytest.raises(Exception, match="fixed-point range"):
+            st.update([kc], [DeviceColumn.from_numpy(N.TYPE_FLOAT64, x, None, ctx=gpu_ctx)])
+            st.finalize()
