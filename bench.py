@@ -74,13 +74,23 @@ def cgroup_cpus():
         return None
 
 
+def usable_cpus() -> int:
+    """CPUs this process can actually run on: its affinity set, capped by the cgroup CPU quota
+    (on the GPU box the affinity lists the whole machine while the quota grants a share of it;
+    threads beyond the quota only time-slice)."""
+    n = len(os.sched_getaffinity(0))
+    q = cgroup_cpus()
+    return max(1, min(n, int(-(-q // 1)))) if q else n
+
+
 def cpu_baseline(sample_rows: int, threads: int):
     """Timed CPU legs (rank 0, N = 1) on bounded samples of the same rows:
     * `value`: the oracle's C restatement of the reference operator chain (oracle/cpu_baseline.c:
       row-at-a-time Selection -> Projection -> HashMap aggregate whose keys are per-row List +
       boxed Long objects from a per-thread bump allocator, boxed accumulator inputs through virtual
-      accumulators, partition-parallel like Main.kt:1309-1325) on `threads` threads — every core
-      this process may run on (os.sched_getaffinity);
+      accumulators, partition-parallel like Main.kt:1309-1325) on `threads` threads — every CPU
+      this process may use (usable_cpus: the affinity set capped by the cgroup quota);
+    * `threads_affinity`: the same with one thread per CPU of the affinity set;
     * `threads_16`: the same at 16 threads (the GPU box's CPU share per GPU);
     * `single_thread`: the same on one thread (SURVEY §8d: 1 thread and all threads);
     * `tuned`: a tuned C implementation (no boxing or materialisation, per-thread open-addressing
@@ -94,13 +104,19 @@ def cpu_baseline(sample_rows: int, threads: int):
     one_rows = min(sample_rows, 100_000_000)
     secs1 = lib.qe_cpu_c4(0, one_rows, 42, 1, 1 << 19, 1024, out, 2048, C.byref(ng))
     secs16 = lib.qe_cpu_c4(0, sample_rows, 42, 16, 1 << 19, 1024, out, 2048, C.byref(ng)) if threads != 16 else secs
+    naff = len(os.sched_getaffinity(0))
+    secs_aff = (lib.qe_cpu_c4(0, sample_rows, 42, naff, 1 << 19, 1024, out, 2048, C.byref(ng))
+                if naff != threads else secs)
     secs_t = lib.qe_cpu_c4_fast(0, sample_rows, 42, threads, 1 << 19, 1024, out, 2048, C.byref(ng))
     return groups, {"value": sample_rows / secs, "unit": "rows/s", "cores": threads, "kind": "port",
-            "cpu_model": cpu_model(), "cgroup_cpus": cgroup_cpus(),
+            "cpu_model": cpu_model(), "cgroup_cpus": cgroup_cpus(), "affinity_cpus": naff,
             "sample": f"rows 0..{sample_rows - 1} of the same C4 table (seed 42), {threads} threads "
-                      f"(all of sched_getaffinity), {secs:.3f} s; C restatement of the reference operator chain "
-                      "with per-row boxed key List / Long objects (oracle/cpu_baseline.c)",
+                      f"(every usable CPU: sched_getaffinity {naff}, cgroup quota {cgroup_cpus()}), {secs:.3f} s; "
+                      "C restatement of the reference operator chain with per-row boxed key List / Long objects "
+                      "(oracle/cpu_baseline.c)",
             "threads_16": {"value": sample_rows / secs16, "cores": 16, "sample": f"same rows, 16 threads, {secs16:.3f} s"},
+            "threads_affinity": {"value": sample_rows / secs_aff, "cores": naff,
+                                 "sample": f"same rows, one thread per CPU of sched_getaffinity, {secs_aff:.3f} s"},
             "single_thread": {"value": one_rows / secs1, "cores": 1,
                               "sample": f"rows 0..{one_rows - 1}, 1 thread, {secs1:.3f} s"},
             "tuned": ({"value": sample_rows / secs_t, "cores": threads,
@@ -396,7 +412,7 @@ def main():
         "check": check,
     }
     if rank == 0 and world == 1 and not args.no_cpu:
-        threads = args.cpu_threads or len(os.sched_getaffinity(0))
+        threads = args.cpu_threads or usable_cpus()
         sample = args.cpu_sample_rows or rows
         cpu_groups, line["cpu_baseline"] = cpu_baseline(sample, threads)
         if sample == rows:

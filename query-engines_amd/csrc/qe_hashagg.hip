@@ -76,11 +76,9 @@ __device__ __forceinline__ int lds_find(const Plan& P, char* smem, qi64 key, boo
   return lds_probe(lds_keys(smem), P.lds_log2, key, lds_hash((qu64)key) >> (32 - P.lds_log2));
 }
 
-__device__ __forceinline__ void lds_accum(const Plan& P, char* smem, int j, int s, qi64 x, bool valid,
-                                          qu64 row) {
+// The accumulator part of one row (the non-null count is the caller's: lds_accum / lds_accum4).
+__device__ __forceinline__ void lds_accum_value(const Plan& P, char* smem, int j, int s, qi64 x, qu64 row) {
   const DAgg& a = P.aggs[j];
-  if (!valid) return;
-  if (a.track_nn) atomicAdd((qu32*)(smem + P.off_nn[j]) + s, 1u);
   qi64* acc = (qi64*)(smem + P.off_acc[j]);
   switch (a.acc) {
     case ACC_SUM_I: atomicAdd((unsigned long long*)&acc[s], (unsigned long long)x); break;
@@ -108,6 +106,13 @@ __device__ __forceinline__ void lds_accum(const Plan& P, char* smem, int j, int 
     }
     default: break;
   }
+}
+
+__device__ __forceinline__ void lds_accum(const Plan& P, char* smem, int j, int s, qi64 x, bool valid,
+                                          qu64 row) {
+  if (!valid) return;
+  if (P.aggs[j].track_nn) atomicAdd((qu32*)(smem + P.off_nn[j]) + s, 1u);
+  lds_accum_value(P, smem, j, s, x, row);
 }
 
 // Merge the workgroup's LDS table into the global table (or the overflow records).
@@ -515,7 +520,7 @@ __device__ __forceinline__ void lds_accum4(const Plan& P, char* smem, int j, con
     case ACC_SUM_X:
 #pragma unroll
       for (int r = 0; r < 4; ++r)
-        if ((m >> r) & 1) lds_accum(P, smem, j, slot[r], x[r], true, (qu64)(row0 + row_of(0, lane, r)));
+        if ((m >> r) & 1) lds_accum_value(P, smem, j, slot[r], x[r], (qu64)(row0 + row_of(0, lane, r)));
       break;
     default: break;
   }

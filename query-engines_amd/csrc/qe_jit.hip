@@ -1108,11 +1108,28 @@ int selproj_rows_per_thread(const Plan& P) {
   return std::min(by_cols, 64 / (selproj_block() / 64));
 }
 
+// Row of (thread, r) inside a select-project tile. Stripe map (QE_SELPROJ_MAP=stripe): stripe r is
+// BT consecutive rows, thread t row t of it. Wave map (default): each wave owns R x 64 consecutive
+// rows, lane l row 64 r + l of them, so a thread's R loads of a column share one base address
+// (immediate offsets 512 B apart) instead of R address registers: fewer VGPRs, more resident
+// workgroups. The (stripe, wave) count slot follows the row order of the map.
+bool selproj_wave_map() {
+  static const bool v = [] {
+    const char* e = getenv("QE_SELPROJ_MAP");
+    return !(e && strcmp(e, "stripe") == 0);
+  }();
+  return v;
+}
+static std::string sp_row(const std::string& b) {
+  return selproj_wave_map() ? b + " + w * (R * 64) + r * 64 + lane" : b + " + r * BT + t";
+}
+static const char* sp_cnt_idx() { return selproj_wave_map() ? "w * R + r" : "r * W + w"; }
+
 // act (bit r: row base + r * BT + t is inside [0, n) and passes the predicate) of a
 // select-project tile whose columns are loaded.
 void emit_selproj_act(const Plan& P, std::ostringstream& o) {
   o << "  qu32 act = 0;\n"
-    << "#pragma unroll\n  for (int r = 0; r < R; ++r) act |= (qu32)(full || base + r * BT + t < P.n) << r;\n";
+    << "#pragma unroll\n  for (int r = 0; r < R; ++r) act |= (qu32)(full || " << sp_row("base") << " < P.n) << r;\n";
   std::ostringstream q;
   emit_predicate(P, q, 16);  // emits with a fixed trip count; R <= 16 and bits >= R are clear
   std::string body = q.str();
@@ -1132,7 +1149,7 @@ void emit_selproj_loads(const Plan& P, std::ostringstream& o, unsigned need, boo
     const char* ty = kind == K_I32 ? "qi32" : (kind == K_U8 || kind == K_BOOL) ? "qu8" : "qi64";
     o << ind << "{\n" << ind << "  const qi64 lb = " << b << ";\n" << ind << "  const bool lfull = lb + R * BT <= P.n;\n"
       << ind << "  const " << ty << "* p = (const " << ty << "*)P.cols[" << cs << "].p;\n"
-      << "#pragma unroll\n" << ind << "  for (int r = 0; r < R; ++r) {\n" << ind << "    const qi64 row = lb + r * BT + t;\n";
+      << "#pragma unroll\n" << ind << "  for (int r = 0; r < R; ++r) {\n" << ind << "    const qi64 row = " << sp_row("lb") << ";\n";
     if (kind == K_BOOL)
       o << ind << "    " << cp << cs << "[r] = (lfull || row < P.n) ? ((p[row >> 3] >> (row & 7)) & 1) : 0;\n";
     else
@@ -1141,7 +1158,7 @@ void emit_selproj_loads(const Plan& P, std::ostringstream& o, unsigned need, boo
     o << ind << "  }\n";
     if (P.cols[c].valid) {
       o << ind << "  const qu8* vb = P.cols[" << cs << "].valid;\n" << ind << "  " << vp << cs << " = 0;\n"
-        << "#pragma unroll\n" << ind << "  for (int r = 0; r < R; ++r) {\n" << ind << "    const qi64 row = lb + r * BT + t;\n"
+        << "#pragma unroll\n" << ind << "  for (int r = 0; r < R; ++r) {\n" << ind << "    const qi64 row = " << sp_row("lb") << ";\n"
         << ind << "    if (lfull || row < P.n) " << vp << cs << " |= (qu32)((vb[row >> 3] >> (row & 7)) & 1) << r;\n"
         << ind << "  }\n";
     }
@@ -1166,7 +1183,7 @@ bool emit_selproj_write(const Plan& P, const int32_t* out_kind, int nout, int mo
     if (!agg_expr(P, k, &ex[k])) return false;
   o << "  qu64 bal[R];\n"
     << "#pragma unroll\n  for (int r = 0; r < R; ++r) bal[r] = __ballot((act >> r) & 1u);\n"
-    << "  if (lane == 0) {\n#pragma unroll\n    for (int r = 0; r < R; ++r) s_cnt[r * W + w] = (qu32)__popcll(bal[r]);\n  }\n"
+    << "  if (lane == 0) {\n#pragma unroll\n    for (int r = 0; r < R; ++r) s_cnt[" << sp_cnt_idx() << "] = (qu32)__popcll(bal[r]);\n  }\n"
     << "  __syncthreads();\n"
     << "  qu64* st = (qu64*)P.t.keys;\n"
     << "  if (w == 0) {\n"
@@ -1215,7 +1232,7 @@ bool emit_selproj_write(const Plan& P, const int32_t* out_kind, int nout, int mo
     // once the tile base is known), while wave 0 then runs the look-back
     o << "#pragma unroll\n  for (int r = 0; r < R; ++r) {\n"
       << "    if (!((act >> r) & 1u)) continue;\n"
-      << "    const qu32 lp = s_cnt[r * W + w] + (qu32)__popcll(bal[r] & below);\n";
+      << "    const qu32 lp = s_cnt[" << sp_cnt_idx() << "] + (qu32)__popcll(bal[r] & below);\n";
     for (int k = 0; k < nout; ++k) o << "    s_out[" << k << " * (R * BT) + lp] = " << ex[k].v << ";\n";
     o << "  }\n"
       << "  if (w == 0) {\n" << lookback << "  }\n"
@@ -1234,7 +1251,7 @@ bool emit_selproj_write(const Plan& P, const int32_t* out_kind, int nout, int mo
     if (any_null) {
       o << "#pragma unroll\n    for (int r = 0; r < R; ++r) {\n"
         << "      if (!((act >> r) & 1u)) continue;\n"
-        << "      const qu64 pos = tb + s_cnt[r * W + w] + (qu64)__popcll(bal[r] & below);\n";
+        << "      const qu64 pos = tb + s_cnt[" << sp_cnt_idx() << "] + (qu64)__popcll(bal[r] & below);\n";
       for (int k = 0; k < nout; ++k)
         if (out_kind[k] & 0x100)
           o << "      if (" << ex[k].ok << ") atomicOr(&((qu32*)P.t.nn[" << k << "])[pos >> 5], 1u << (pos & 31));\n";
@@ -1247,7 +1264,7 @@ bool emit_selproj_write(const Plan& P, const int32_t* out_kind, int nout, int mo
       << "  const qu64 tb = s_base;\n"
       << "#pragma unroll\n  for (int r = 0; r < R; ++r) {\n"
       << "    if (!((act >> r) & 1u)) continue;\n"
-      << "    const qu64 pos = tb + s_cnt[r * W + w] + (qu64)__popcll(bal[r] & below);\n";
+      << "    const qu64 pos = tb + s_cnt[" << sp_cnt_idx() << "] + (qu64)__popcll(bal[r] & below);\n";
     for (int k = 0; k < nout; ++k) {
       const std::string ks = std::to_string(k);
       const int width = out_kind[k] & 0xFF;

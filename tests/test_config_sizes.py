@@ -175,7 +175,10 @@ def test_c5_full_size_slice(gpu_ctx):
         ms.append(_eval(gpu_ctx, "qe_eval_cmp", op, cols[col], lit, DeviceColumn.empty(N.TYPE_BOOL, n, False, ctx=gpu_ctx)))
     mask = ms[0]
     for m in ms[1:]:
-        mask = _eval(gpu_ctx, "qe_eval_bool", N.OP_AND, mask, m, DeviceColumn.empty(N.TYPE_BOOL, n, False, ctx=gpu_ctx))
+        out = DeviceColumn.empty(N.TYPE_BOOL, n, False, ctx=gpu_ctx)
+        ac, bc, oc = mask.as_c(), m.as_c(), out.as_c()
+        N.check(N.lib().qe_eval_bool(gpu_ctx.handle, N.OP_AND, N.C.byref(ac), N.C.byref(bc), N.C.byref(oc)))
+        mask = out
     del ms
     sel = _count(gpu_ctx, mask)
     assert int(cstar.sum()) == sel
