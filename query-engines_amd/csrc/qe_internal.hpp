@@ -120,6 +120,8 @@ enum { SP_COUNTER = 0, SP_PERSIST = 1, SP_COUNT = 2, SP_WRITE = 3, SP_WRITE_SCAN
 bool gen_selproj_source(const qe::Plan& P, const int32_t* out_kind, int nout, std::string* src, int mode);
 int selproj_block();                                  // select-project workgroup size
 int selproj_rows_per_thread(const qe::Plan& P);
+bool selproj_pipelined();  // look-back modes load the next tile while this one is compacted
+int selproj_rows(const qe::Plan& P, int mode);  // rows per thread of `mode`'s tiles
 bool selproj_nt(const qe::Plan& P);  // non-temporal input loads (large inputs)
 // Exclusive scan of n int64 on the ctx stream (one block); out[n] = total. (qe_filter.hip)
 int exclusive_scan_i64(qe_ctx* ctx, const int64_t* in, int64_t* out, int64_t n);

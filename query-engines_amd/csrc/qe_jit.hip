@@ -1108,15 +1108,34 @@ int selproj_rows_per_thread(const Plan& P) {
   return std::min(by_cols, 64 / (selproj_block() / 64));
 }
 
-// Row of (thread, r) inside a select-project tile. Stripe map (QE_SELPROJ_MAP=stripe): stripe r is
-// BT consecutive rows, thread t row t of it. Wave map (default): each wave owns R x 64 consecutive
+// Software-pipelined look-back tiles (QE_SELPROJ_PIPE, default on): right after a tile's
+// predicate and projections are evaluated into registers, the workgroup issues the loads of its
+// next tile, which are in flight during this tile's count scan, look-back and stores. With 8 rows
+// per thread the two register sets fit 4 workgroups per CU.
+bool selproj_pipelined() {
+  static const bool v = [] {
+    const char* e = getenv("QE_SELPROJ_PIPE");
+    return !(e && e[0] == '0');
+  }();
+  return v;
+}
+
+int selproj_rows(const Plan& P, int mode) {
+  const int r = selproj_rows_per_thread(P);
+  static const bool forced = getenv("QE_SELPROJ_ROWS") && *getenv("QE_SELPROJ_ROWS");
+  return (!forced && selproj_pipelined() && (mode == SP_PERSIST || mode == SP_COUNTER)) ? std::min(r, 8) : r;
+}
+
+// Row of (thread, r) inside a select-project tile. Stripe map (default): stripe r is BT consecutive
+// rows, thread t row t of it. Wave map (QE_SELPROJ_MAP=wave): each wave owns R x 64 consecutive
 // rows, lane l row 64 r + l of them, so a thread's R loads of a column share one base address
-// (immediate offsets 512 B apart) instead of R address registers: fewer VGPRs, more resident
-// workgroups. The (stripe, wave) count slot follows the row order of the map.
+// (immediate offsets 512 B apart): 127 instead of 141 VGPRs for C2, but 1B rows took 5.20 ms
+// against 4.86 ms for the stripe map (one box, same build). The (stripe, wave) count slot follows
+// the row order of the map.
 bool selproj_wave_map() {
   static const bool v = [] {
     const char* e = getenv("QE_SELPROJ_MAP");
-    return !(e && strcmp(e, "stripe") == 0);
+    return e && strcmp(e, "wave") == 0;
   }();
   return v;
 }
@@ -1170,8 +1189,9 @@ void emit_selproj_loads(const Plan& P, std::ostringstream& o, unsigned need, boo
 // (c<slot>[R], v<slot>) and computed `act` (bit r: row base + r * BT + t is selected): ballots,
 // per-(stripe, wave) counts, one wave's scan, the tile's output base (decoupled look-back or the
 // two-pass prefix), then the compacted stores.
-bool emit_selproj_write(const Plan& P, const int32_t* out_kind, int nout, int mode, std::ostringstream& o) {
-  const int R = selproj_rows_per_thread(P);
+bool emit_selproj_write(const Plan& P, const int32_t* out_kind, int nout, int mode, std::ostringstream& o,
+                        bool regs = false) {
+  const int R = selproj_rows(P, mode);
   // Staged output (all outputs 8 bytes wide, R x BT x 8 B each within 64 KiB of LDS): selected
   // rows land compacted in LDS, then the tile's output range is written with 16-byte stores, all
   // lanes active. Direct 8-byte stores from the row registers were store-issue bound (half the
@@ -1179,8 +1199,13 @@ bool emit_selproj_write(const Plan& P, const int32_t* out_kind, int nout, int mo
   bool staged = (size_t)nout * R * selproj_block() * 8 <= 64 * 1024;
   for (int k = 0; k < nout; ++k) staged = staged && (out_kind[k] & 0xFF) == 8;
   std::vector<Expr> ex(nout);
-  for (int k = 0; k < nout; ++k)
+  for (int k = 0; k < nout; ++k) {
     if (!agg_expr(P, k, &ex[k])) return false;
+    if (regs) {  // pipelined: values and validity were evaluated into o<k>[R] / ok<k> before the prefetch
+      ex[k].v = "o" + std::to_string(k) + "[r]";
+      ex[k].ok = "((ok" + std::to_string(k) + " >> r) & 1u)";
+    }
+  }
   o << "  qu64 bal[R];\n"
     << "#pragma unroll\n  for (int r = 0; r < R; ++r) bal[r] = __ballot((act >> r) & 1u);\n"
     << "  if (lane == 0) {\n#pragma unroll\n    for (int r = 0; r < R; ++r) s_cnt[" << sp_cnt_idx() << "] = (qu32)__popcll(bal[r]);\n  }\n"
@@ -1285,8 +1310,9 @@ bool emit_selproj_write(const Plan& P, const int32_t* out_kind, int nout, int mo
 
 bool gen_selproj_source(const Plan& P, const int32_t* out_kind, int nout, std::string* src, int mode) {
   if (P.ncols < 1 || P.ncols > QE_MAX_COLS || nout < 1 || nout > QE_MAX_AGGS) return false;
-  const int R = selproj_rows_per_thread(P);
+  const int R = selproj_rows(P, mode);
   const bool persistent = mode == SP_PERSIST;
+  const bool pipe = persistent && selproj_pipelined();
   // the count pass loads only the predicate's columns
   const unsigned need = mode == SP_COUNT ? pred_key_cols(P) : ~0u;
   std::ostringstream o;
@@ -1301,6 +1327,40 @@ bool gen_selproj_source(const Plan& P, const int32_t* out_kind, int nout, std::s
   auto emit_loads = [&](const std::string& cp, const std::string& vp, const std::string& b, const std::string& ind) {
     emit_selproj_loads(P, o, need, selproj_nt(P), cp, vp, b, ind);
   };
+  if (pipe) {
+    // Persistent grid, software-pipelined: tile i+1's loads are issued once tile i's predicate
+    // and projections sit in registers (o<k>[R], ok<k>), and are in flight during tile i's count
+    // scan, look-back and stores. The asm fence keeps the compiler from sinking the projections
+    // below the loads (which would hold both tiles' columns live).
+    for (int c = 0; c < P.ncols; ++c) {
+      o << "  qi64 c" << c << "[R];\n";
+      if (P.cols[c].valid) o << "  qu32 v" << c << " = 0;\n";
+    }
+    o << "  qu32 tile = blockIdx.x;\n  if ((qu64)tile < P.t.cap) {\n    const qi64 base0 = (qi64)tile * (R * BT);\n";
+    emit_loads("c", "v", "base0", "    ");
+    o << "  }\n  while ((qu64)tile < P.t.cap) {\n"
+      << "  const qu32 next = tile + gridDim.x;\n"
+      << "  const qi64 base = (qi64)tile * (R * BT);\n"
+      << "  const bool full = base + R * BT <= P.n;\n";
+    emit_selproj_act(P, o);
+    std::vector<Expr> ex(nout);
+    for (int k = 0; k < nout; ++k)
+      if (!agg_expr(P, k, &ex[k])) return false;
+    for (int k = 0; k < nout; ++k) {
+      const std::string ks = std::to_string(k);
+      o << "  qi64 o" << ks << "[R];\n  qu32 ok" << ks << " = 0;\n"
+        << "#pragma unroll\n  for (int r = 0; r < R; ++r) { o" << ks << "[r] = " << ex[k].v << "; ok" << ks
+        << " |= (qu32)(" << ex[k].ok << ") << r; }\n"
+        << "#pragma unroll\n  for (int r = 0; r < R; ++r) asm volatile(\"\" :: \"v\"(o" << ks << "[r]) : \"memory\");\n";
+    }
+    o << "  if ((qu64)next < P.t.cap) {\n    const qi64 nbase = (qi64)next * (R * BT);\n";
+    emit_loads("c", "v", "nbase", "    ");
+    o << "  }\n";
+    if (!emit_selproj_write(P, out_kind, nout, mode, o, true)) return false;
+    o << "  __syncthreads();\n  tile = next;\n  }\n}\n";
+    *src = std::string(kDevHeader) + o.str();
+    return true;
+  }
   if (persistent) {
     // Every workgroup is resident (grid <= CUs x occupancy), so a static tile order cannot
     // deadlock the look-back and no tile counter is needed. (Prefetching the next tile's columns

@@ -36,7 +36,7 @@ int selproj_kernel(qe_ctx* ctx, const Plan& P, const int32_t* out_kind, int nout
   for (int j = 0; j < nout; ++j) k.out_kind[j] = out_kind[j];
   k.nout = nout;
   k.mode = mode;
-  k.rows = selproj_rows_per_thread(P);
+  k.rows = selproj_rows(P, mode);
   k.nt = selproj_nt(P);
   const std::string key = plan_shape_key(ctx, P) + std::string((const char*)&k, sizeof k);
   static std::mutex mu;
@@ -133,10 +133,13 @@ int launch_select(qe_ctx* ctx, Plan& P, const int32_t* col_width, const int32_t*
     if ((pred_cols >> c) & 1u) pred_bytes += (size_t)n * std::max(1, col_width[c]);
   // (each write-pass tile sums all earlier tiles' counts, so the tile count is bounded too: a
   // plan with no predicate reads nothing in the count pass but still pays the prefix sums)
-  const int R = selproj_rows_per_thread(P);
+  const int R2 = selproj_rows(P, SP_COUNT);  // two-pass tiles
+  const int64_t tiles2 = (int64_t)div_up((uint64_t)n, (uint64_t)R2 * selproj_block());
+  const bool twopass = twopass_env >= 0 ? twopass_env == 1 : (pred_bytes <= (96ull << 20) && tiles2 <= 4096);
+  // the look-back modes (persistent and its counter-ordered rerun) share one tile size
+  const int R = (twopass || twopass_env == 2) ? R2 : selproj_rows(P, SP_PERSIST);
   const int64_t tiles = (int64_t)div_up((uint64_t)n, (uint64_t)R * selproj_block());
   QE_CHECK(tiles < (1ll << 31), QE_ERR_CAPACITY, "too many rows for one select-project call");
-  const bool twopass = twopass_env >= 0 ? twopass_env == 1 : (pred_bytes <= (96ull << 20) && tiles <= 4096);
   // Scanned two passes (QE_SELPROJ_TWOPASS=2): count pass, a device scan of the tile counts, then
   // the write pass reads its tile's base — no look-back chain and no per-tile prefix sums, at the
   // price of reading the predicate's columns twice.

@@ -9,9 +9,10 @@ run() {  # name, env...
   env "$@" timeout -k 10 120 python3 tools/bench_configs.py C2L > $OUT/$name.json 2> $OUT/$name.err || return 1
   echo "$name $(cat $OUT/$name.json)"
 }
-run wave && \
-run stripe QE_SELPROJ_MAP=stripe && \
-run wave_wg6 QE_SELPROJ_WG_PER_CU=6 QE_SELPROJ_OCC_MARGIN=0 && \
-run stripe_wg6 QE_SELPROJ_MAP=stripe QE_SELPROJ_WG_PER_CU=6 QE_SELPROJ_OCC_MARGIN=0 && \
-run wave_counter QE_SELPROJ_PERSIST=0 && \
-run wave_r8_wg8 QE_SELPROJ_ROWS=8 QE_SELPROJ_WG_PER_CU=8 QE_SELPROJ_OCC_MARGIN=0
+run pipe && \
+run pipe_wg6 QE_SELPROJ_WG_PER_CU=6 QE_SELPROJ_OCC_MARGIN=0 && \
+run pipe_wg8 QE_SELPROJ_WG_PER_CU=8 QE_SELPROJ_OCC_MARGIN=0 && \
+run pipe_wave QE_SELPROJ_MAP=wave && \
+run pipe_r16 QE_SELPROJ_ROWS=16 && \
+run nopipe_wg6 QE_SELPROJ_PIPE=0 QE_SELPROJ_WG_PER_CU=6 QE_SELPROJ_OCC_MARGIN=0 && \
+run nopipe QE_SELPROJ_PIPE=0
