@@ -124,27 +124,14 @@ def cpu_baseline(sample_rows: int, threads: int):
                                  "per-thread open-addressing tables (qe_cpu_c4_fast)"} if secs_t > 0 else None)}
 
 
-# sources the specialised C4 kernel is generated from (qe_jit.hip emits it, including qe_dev.hpp;
-# qe_hashagg.hip sizes the table and the launch): profiles/traffic.json is valid for these bytes only
-TRAFFIC_SOURCES = ("query-engines_amd/csrc/qe_jit.hip", "query-engines_amd/csrc/qe_dev.hpp",
-                   "query-engines_amd/csrc/qe_hashagg.hip")
-
-
-def kernel_source_hash() -> str:
-    import hashlib
-
-    h = hashlib.sha256()
-    for rel in TRAFFIC_SOURCES:
-        h.update(rel.encode() + b"\0" + (ROOT / rel).read_bytes() + b"\0")
-    return h.hexdigest()[:16]
-
-
-def load_traffic(rows: int):
+def load_traffic(rows: int, signature: str):
     """HBM bytes per fused-kernel launch from the committed rocprofv3 PMC summary
     (profiles/traffic.json, written by profiles/summarize.py; FETCH_SIZE doubled per
     MI355X_MICROARCH.md §HBM: gfx950 counts half of wide streaming reads). Used only when it was
-    measured at these rows on kernel sources identical to this tree's (kernel_source_hash): a
-    kernel change leaves `traffic` null until the PMC passes are re-run. Returns (bytes, note)."""
+    measured at these rows on the identical kernel and launch: `signature` is this run's
+    qe_hashagg_last_kernel_signature (hash of the specialised kernel's compile key — toolchain,
+    options, generated source — and its launch shape). Any kernel change leaves `traffic` null
+    until the PMC passes are re-run. Returns (bytes, note)."""
     p = ROOT / "profiles" / "traffic.json"
     if not p.exists():
         return None, "no profiles/traffic.json"
@@ -154,11 +141,11 @@ def load_traffic(rows: int):
         return None, "unreadable profiles/traffic.json"
     if int(t.get("rows", -1)) != rows:
         return None, f"profiles/traffic.json is for {t.get('rows')} rows"
-    have, want = t.get("kernel_source_hash"), kernel_source_hash()
-    if have != want:
-        return None, f"stale: profiles/traffic.json measured on kernel sources {have}, tree has {want}"
-    return float(t["hbm_bytes_per_launch"]), (f"profiles/traffic.json (rocprofv3 FETCH_SIZE x2 + WRITE_SIZE, "
-                                              f"sources {have}, git {t.get('git_head', '?')})")
+    have = t.get("kernel_signature")
+    if have != signature:
+        return None, f"stale: profiles/traffic.json measured kernel {have}, this run launched {signature}"
+    return float(t["hbm_bytes_per_launch"]), (f"profiles/traffic.json (rocprofv3 FETCH_SIZE x2 + WRITE_SIZE of this "
+                                              f"kernel {have}, git {t.get('git_head', '?')})")
 
 
 def launch_ranks(args) -> int:
@@ -367,7 +354,8 @@ def main():
             check["cpu_port_groups_equal_all_ranks"] = True
     ms_step = elapsed / args.steps * 1e3
     achieved = rows * BYTES_PER_ROW / (avg_kernel_ms * 1e-3) / 1e9
-    traffic, traffic_note = load_traffic(rows)
+    signature = partial.last_kernel_signature()
+    traffic, traffic_note = load_traffic(rows, signature)
     line = {
         "metric": METRIC,
         "value": world * rows / (ms_step * 1e-3),
@@ -402,6 +390,7 @@ def main():
             "frac": achieved / HBM_PEAK_GBS,
             "traffic": traffic,
             "traffic_source": traffic_note,
+            "kernel_signature": signature,
             "kernel": ("qe_fused (hipRTC plan-specialised filter+project+LDS hash aggregate)" if kinds[-1][0]
                        else f"k_hashagg generic interpreter ({kinds[-1][1]})"),
             "avg_kernel_ms": avg_kernel_ms,

@@ -452,6 +452,11 @@ int qe_hashagg_set_row_base(qe_hashagg* agg, int64_t row_base);
  * launches made by the last update call, and how many launches it took (1 unless the table
  * had to grow and deferred rows were re-applied). */
 int qe_hashagg_last_kernel_time(qe_hashagg* agg, double* ms, int32_t* launches);
+/* Measurement hook: a signature of what the last update launched — a hash of the specialised
+ * kernel's compile key (hipRTC / HIP versions, options, generated source) and its launch shape —
+ * so that counters recorded for one build (bench.py's profiles/traffic.json) are only reused for
+ * the identical kernel and launch. */
+int qe_hashagg_last_kernel_signature(qe_hashagg* agg, uint64_t* sig);
 /* Whether the last update ran a plan-specialised kernel (1) or the generic one (0), and why
  * not (NUL-terminated note, may be NULL). */
 int qe_hashagg_last_kernel_kind(qe_hashagg* agg, int32_t* specialized, char* note, int32_t note_len);

@@ -1,9 +1,10 @@
 """Summarise a rocprofv3 run of bench.py (profiles/run_profile.sh output) into profiles/.
 
 Writes profiles/<round>_kernel_stats.csv (copy of the kernel-trace --stats summary),
-profiles/<round>_summary.md and profiles/traffic.json (tagged with bench.kernel_source_hash() of the
-kernel sources in this tree — run it on the tree that was profiled — and the git head; bench.py
-ignores traffic.json once those sources change; HBM bytes per fused-kernel launch from the
+profiles/<round>_summary.md and profiles/traffic.json (tagged with the kernel signature the profiled
+bench run printed — qe_hashagg_last_kernel_signature: the specialised kernel's compile key and launch
+shape — and the git head; bench.py ignores traffic.json for any other kernel; HBM bytes per
+fused-kernel launch from the
 FETCH_SIZE / WRITE_SIZE passes; FETCH_SIZE doubled per MI355X_MICROARCH.md §HBM: on gfx950 it counts
 half the bytes of wide coalesced streaming reads; both counters are in KiB)."""
 import csv
@@ -42,17 +43,18 @@ def main():
     if fetch:
         f = sum(fetch) / len(fetch) * 1024 * 2  # KiB -> B, x2 gfx950 correction
         w = (sum(write) / len(write) * 1024) if write else 0.0
-        sys.path.insert(0, str(ROOT))
         import subprocess
 
-        import bench
-
+        sig = None  # the profiled bench run's line (trace pass) names the kernel it launched
+        for ln in open(SRC / "trace.log", errors="replace"):
+            if ln.startswith("{") and '"kernel_signature"' in ln:
+                sig = json.loads(ln)["roofline"]["kernel_signature"]
         try:
             head = subprocess.run(["git", "-C", str(ROOT), "rev-parse", "--short", "HEAD"], capture_output=True,
                                   text=True).stdout.strip()
         except OSError:
             head = ""
-        out = {"rows": 1_000_000_000, "kernel_source_hash": bench.kernel_source_hash(), "git_head": head,
+        out = {"rows": 1_000_000_000, "kernel_signature": sig, "git_head": head,
                "hbm_bytes_per_launch": f + w, "fetch_bytes_corrected": f, "write_bytes": w,
                "algorithmic_bytes": 24_000_000_000, "kernel": fused[0]["Name"] if fused else "",
                "avg_kernel_ms": float(fused[0]["AverageNs"]) / 1e6 if fused else None,

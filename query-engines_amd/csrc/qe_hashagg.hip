@@ -1431,6 +1431,7 @@ struct qe_hashagg {
   double last_kernel_ms = 0.0;
   int last_launches = 0;
   int last_specialized = 0;  // 1: the last update ran a hipRTC-specialised kernel
+  uint64_t last_sig = 0;     // signature of the last aggregation launch (kernel compile key + shape)
   std::string jit_note;      // why the last update could not specialise (empty if it did)
   // stream-ordered updates (qe_hashagg_set_async): the last update's launch, read back later
   bool async = false;
@@ -2157,6 +2158,12 @@ static int launch_pass(qe_hashagg* h, Plan& P, size_t& lds, hipFunction_t pfn, i
     QE_TRY(launch_hashagg(P, grid, lds, ctx->stream));
   }
   h->last_specialized = jfn ? 1 : 0;
+  {  // what ran: the kernel's compile key and its launch shape (measurement hook)
+    const uint64_t k = jfn ? jit_kernel_signature(jfn) : 0x6E65726963ull;  // "generic"
+    const uint64_t shape = jfn ? ((uint64_t)jgrid << 20) ^ (uint64_t)(pfn ? (pblock ? pblock : pagg_block()) : fused_block(P.lds_log2))
+                               : ((uint64_t)grid << 20) ^ (uint64_t)lds;
+    h->last_sig = fmix64(k ^ fmix64(shape));
+  }
   QE_TRY(launch_check("k_hashagg"));
   QE_HIP(hipEventRecord(h->ev[1], ctx->stream));
   // the counters' snapshot is queued right behind the launch: settling waits for this event only,
@@ -2594,6 +2601,12 @@ int qe_hashagg_last_kernel_kind(qe_hashagg* h, int32_t* specialized, char* note,
     strncpy(note, h->jit_note.c_str(), (size_t)note_len - 1);
     note[note_len - 1] = 0;
   }
+  return QE_OK;
+}
+
+int qe_hashagg_last_kernel_signature(qe_hashagg* h, uint64_t* sig) {
+  QE_CHECK(h && sig, QE_ERR_INVALID_ARG, "null argument");
+  *sig = h->last_sig;
   return QE_OK;
 }
 

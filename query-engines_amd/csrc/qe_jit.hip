@@ -1427,6 +1427,7 @@ struct Entry {
 
 std::mutex g_mu;
 std::map<std::pair<int, std::string>, Entry> g_cache;
+std::map<hipFunction_t, uint64_t> g_sig;  // kernel -> fnv1a of its compile key (toolchain, options, source)
 
 uint64_t fnv1a(const std::string& s) {
   uint64_t h = 1469598103934665603ull;
@@ -1571,9 +1572,16 @@ int jit_kernel(qe_ctx* ctx, const std::string& src, hipFunction_t* fn, int* bloc
   QE_HIP(hipModuleOccupancyMaxActiveBlocksPerMultiprocessor(&nb, e.fn, block, 0));
   e.blocks_per_cu = nb > 0 ? nb : 1;
   g_cache[key] = e;
+  g_sig[e.fn] = fnv1a(disk_key);
   *fn = e.fn;
   *blocks_per_cu = e.blocks_per_cu;
   return QE_OK;
+}
+
+uint64_t jit_kernel_signature(hipFunction_t fn) {
+  std::lock_guard<std::mutex> lk(g_mu);
+  auto it = g_sig.find(fn);
+  return it == g_sig.end() ? 0 : it->second;
 }
 
 int jit_launch(qe_ctx* ctx, hipFunction_t fn, int grid, const Plan& P, int block) {

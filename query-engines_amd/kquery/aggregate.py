@@ -217,6 +217,12 @@ class HashAggregateState:
         N.check(N.lib().qe_hashagg_last_kernel_time(self.handle, N.C.byref(ms), N.C.byref(k)))
         return ms.value, k.value
 
+    def last_kernel_signature(self) -> str:
+        """Hex signature of the last update's aggregation launch (kernel compile key + shape)."""
+        sig = N.C.c_uint64()
+        N.check(N.lib().qe_hashagg_last_kernel_signature(self.handle, N.C.byref(sig)))
+        return f"{sig.value:016x}"
+
     def last_kernel_kind(self):
         """(specialized: bool, note) for the last update's aggregation kernel."""
         k = N.C.c_int32()

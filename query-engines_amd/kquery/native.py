@@ -237,6 +237,7 @@ SIGNATURES = [
     ("qe_hashagg_set_row_base", C.c_int, [_P, C.c_int64]),
     ("qe_hashagg_set_async", C.c_int, [_P, C.c_int32]),
     ("qe_hashagg_last_kernel_time", C.c_int, [_P, C.POINTER(C.c_double), C.POINTER(C.c_int32)]),
+    ("qe_hashagg_last_kernel_signature", C.c_int, [_P, C.POINTER(C.c_uint64)]),
     ("qe_hashagg_last_kernel_kind", C.c_int, [_P, C.POINTER(C.c_int32), C.c_char_p, C.c_int32]),
     ("qe_strdict_create", C.c_int, [_P, C.c_int64, _PP]),
     ("qe_strdict_destroy", C.c_int, [_P]),
