@@ -1104,18 +1104,22 @@ int selproj_rows_per_thread(const Plan& P) {
     return (v == 2 || v == 4 || v == 8 || v == 16) ? v : 0;
   }();
   const int by_cols = env ? env : (P.ncols <= 3 ? 16 : (P.ncols <= 6 ? 8 : 4));
-  // (R x waves) per-(stripe, wave) counts fit one wave's scan
-  return std::min(by_cols, 64 / (selproj_block() / 64));
+  // (R x waves) per-(stripe, wave) counts: at most 4 per lane of the one-wave scan
+  return std::min(by_cols, 256 / (selproj_block() / 64));
 }
 
-// Software-pipelined look-back tiles (QE_SELPROJ_PIPE, default on): right after a tile's
+// Software-pipelined look-back tiles (QE_SELPROJ_PIPE=1; off by default): right after a tile's
 // predicate and projections are evaluated into registers, the workgroup issues the loads of its
-// next tile, which are in flight during this tile's count scan, look-back and stores. With 8 rows
-// per thread the two register sets fit 4 workgroups per CU.
+// next tile, which are in flight during this tile's count scan, look-back and stores (8 rows per
+// thread, so the two register sets fit 4-5 workgroups per CU). Measured slower at 1B rows: 5.49-
+// 5.71 ms against 4.67-4.89 ms unpipelined (same box). The loads sit in front of the look-back's
+// status reads in the wave's in-order load counter, so each tile publishes its prefix one memory
+// latency later — and the tiles' prefix chain, not the loads, sets the pace: the inclusive
+// prefix advances one look-back window (64 tiles) per status round trip.
 bool selproj_pipelined() {
   static const bool v = [] {
     const char* e = getenv("QE_SELPROJ_PIPE");
-    return !(e && e[0] == '0');
+    return e && e[0] == '1';
   }();
   return v;
 }
@@ -1212,11 +1216,15 @@ bool emit_selproj_write(const Plan& P, const int32_t* out_kind, int nout, int mo
     << "  __syncthreads();\n"
     << "  qu64* st = (qu64*)P.t.keys;\n"
     << "  if (w == 0) {\n"
-    << "    const qu32 x = lane < R * W ? s_cnt[lane] : 0u;\n"
+    // R x W (stripe, wave) counts, E = ceil(R W / 64) consecutive ones per lane
+    << "    constexpr int E = (R * W + 63) / 64;\n"
+    << "    qu32 xs[E];\n    qu32 x = 0;\n"
+    << "#pragma unroll\n    for (int e = 0; e < E; ++e) { xs[e] = lane * E + e < R * W ? s_cnt[lane * E + e] : 0u; x += xs[e]; }\n"
     << "    qu32 inc = x;\n"
     << "#pragma unroll\n    for (int d = 1; d < 64; d <<= 1) { const qu32 y = __shfl_up(inc, d); if (lane >= d) inc += y; }\n"
     << "    const qu64 total = (qu64)__shfl(inc, 63);\n"
-    << "    if (lane < R * W) s_cnt[lane] = inc - x;\n"
+    << "    qu32 ex = inc - x;\n"
+    << "#pragma unroll\n    for (int e = 0; e < E; ++e) { if (lane * E + e < R * W) s_cnt[lane * E + e] = ex; ex += xs[e]; }\n"
     << (mode == SP_WRITE || mode == SP_WRITE_SCAN ? "    if (lane == 0) s_total = (qu32)total;\n"
                          : "    if (lane == 0) { s_total = (qu32)total; __hip_atomic_store(&st[tile], (tile == 0 ? F_INC : F_AGG) | total, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }\n")
     << "  }\n";

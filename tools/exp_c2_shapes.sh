@@ -9,10 +9,9 @@ run() {  # name, env...
   env "$@" timeout -k 10 120 python3 tools/bench_configs.py C2L > $OUT/$name.json 2> $OUT/$name.err || return 1
   echo "$name $(cat $OUT/$name.json)"
 }
-run pipe && \
-run pipe_wg6 QE_SELPROJ_WG_PER_CU=6 QE_SELPROJ_OCC_MARGIN=0 && \
-run pipe_wg8 QE_SELPROJ_WG_PER_CU=8 QE_SELPROJ_OCC_MARGIN=0 && \
-run pipe_wave QE_SELPROJ_MAP=wave && \
-run pipe_r16 QE_SELPROJ_ROWS=16 && \
-run nopipe_wg6 QE_SELPROJ_PIPE=0 QE_SELPROJ_WG_PER_CU=6 QE_SELPROJ_OCC_MARGIN=0 && \
-run nopipe QE_SELPROJ_PIPE=0
+run dflt && \
+run b512 QE_SELPROJ_BLOCK=512 && \
+run b512_r8 QE_SELPROJ_BLOCK=512 QE_SELPROJ_ROWS=8 && \
+run b1024 QE_SELPROJ_BLOCK=1024 && \
+run b1024_r8 QE_SELPROJ_BLOCK=1024 QE_SELPROJ_ROWS=8 && \
+run margin1 QE_SELPROJ_OCC_MARGIN=1
