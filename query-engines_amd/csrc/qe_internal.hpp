@@ -118,8 +118,8 @@ int compile_program(const qe_column* cols, int32_t ncols, const bool* col_f64, c
 // SP_WRITE_SCAN (second pass after a device scan of the counts: each tile's base = t.keys[tile]).
 enum { SP_COUNTER = 0, SP_PERSIST = 1, SP_COUNT = 2, SP_WRITE = 3, SP_WRITE_SCAN = 4 };
 bool gen_selproj_source(const qe::Plan& P, const int32_t* out_kind, int nout, std::string* src, int mode);
-int selproj_block();                                  // select-project workgroup size
-int selproj_rows_per_thread(const qe::Plan& P);
+int selproj_block(int mode);  // select-project workgroup size of a mode (SP_*)
+int selproj_rows_per_thread(const qe::Plan& P, int mode);
 uint64_t jit_kernel_signature(hipFunction_t fn);  // hash of a specialised kernel's compile key (0: unknown)
 bool selproj_pipelined();  // look-back modes load the next tile while this one is compacted
 int selproj_rows(const qe::Plan& P, int mode);  // rows per thread of `mode`'s tiles

@@ -1087,17 +1087,31 @@ std::string plan_shape_key(const qe_ctx* ctx, const Plan& P) {
   return std::string((const char*)&k, sizeof k) + std::string((const char*)extra, sizeof extra);
 }
 
-// Select-project workgroup size (QE_SELPROJ_BLOCK = 256 / 512 / 1024).
-int selproj_block() {
-  static const int v = [] {
+// Select-project workgroup size per mode. QE_SELPROJ_BLOCK (256 / 512 / 1024) sets every mode;
+// QE_SELPROJ_LB_BLOCK the look-back modes alone (persistent grid and its counter-ordered rerun),
+// whose pace is set by the tiles' prefix chain — one look-back window of 64 tiles per status round
+// trip — so that larger tiles move more rows per round trip (1B rows: 256 threads 4.66 ms, 512
+// 4.51, 1024 4.40 with the output unstaged).
+int selproj_block(int mode) {
+  static const int all = [] {
     const char* e = getenv("QE_SELPROJ_BLOCK");
+    const int b = e && *e ? atoi(e) : 0;
+    return (b == 256 || b == 512 || b == 1024) ? b : 0;
+  }();
+  static const int lb = [] {
+    const char* e = getenv("QE_SELPROJ_LB_BLOCK");
     const int b = e && *e ? atoi(e) : 256;
     return (b == 512 || b == 1024) ? b : 256;
   }();
-  return v;
+  if (all) return all;
+  return (mode == SP_PERSIST || mode == SP_COUNTER) ? lb : 256;
 }
 
-int selproj_rows_per_thread(const Plan& P) {
+// LDS the staged select-project output may take (a 1024-thread tile of 16 rows per thread, one
+// 8-byte output: 128 KiB, one workgroup per CU)
+constexpr size_t kSelprojStageBytes = 128 * 1024;
+
+int selproj_rows_per_thread(const Plan& P, int mode) {
   static const int env = [] {
     const char* e = getenv("QE_SELPROJ_ROWS");
     const int v = e && *e ? atoi(e) : 0;
@@ -1105,7 +1119,7 @@ int selproj_rows_per_thread(const Plan& P) {
   }();
   const int by_cols = env ? env : (P.ncols <= 3 ? 16 : (P.ncols <= 6 ? 8 : 4));
   // (R x waves) per-(stripe, wave) counts: at most 4 per lane of the one-wave scan
-  return std::min(by_cols, 256 / (selproj_block() / 64));
+  return std::min(by_cols, 256 / (selproj_block(mode) / 64));
 }
 
 // Software-pipelined look-back tiles (QE_SELPROJ_PIPE=1; off by default): right after a tile's
@@ -1125,7 +1139,7 @@ bool selproj_pipelined() {
 }
 
 int selproj_rows(const Plan& P, int mode) {
-  const int r = selproj_rows_per_thread(P);
+  const int r = selproj_rows_per_thread(P, mode);
   static const bool forced = getenv("QE_SELPROJ_ROWS") && *getenv("QE_SELPROJ_ROWS");
   return (!forced && selproj_pipelined() && (mode == SP_PERSIST || mode == SP_COUNTER)) ? std::min(r, 8) : r;
 }
@@ -1200,7 +1214,7 @@ bool emit_selproj_write(const Plan& P, const int32_t* out_kind, int nout, int mo
   // rows land compacted in LDS, then the tile's output range is written with 16-byte stores, all
   // lanes active. Direct 8-byte stores from the row registers were store-issue bound (half the
   // lanes idle at 50 % selectivity, 16 store instructions per thread).
-  bool staged = (size_t)nout * R * selproj_block() * 8 <= 64 * 1024;
+  bool staged = (size_t)nout * R * selproj_block(mode) * 8 <= kSelprojStageBytes;
   for (int k = 0; k < nout; ++k) staged = staged && (out_kind[k] & 0xFF) == 8;
   std::vector<Expr> ex(nout);
   for (int k = 0; k < nout; ++k) {
@@ -1325,12 +1339,12 @@ bool gen_selproj_source(const Plan& P, const int32_t* out_kind, int nout, std::s
   const unsigned need = mode == SP_COUNT ? pred_key_cols(P) : ~0u;
   std::ostringstream o;
   o << "\nusing namespace qe;\n"
-    << "extern \"C\" __global__ void __launch_bounds__(" << selproj_block() << ") qe_selproj(const Plan P) {\n"
-    << "  constexpr int R = " << R << ", BT = " << selproj_block() << ", W = BT / 64;\n"
+    << "extern \"C\" __global__ void __launch_bounds__(" << selproj_block(mode) << ") qe_selproj(const Plan P) {\n"
+    << "  constexpr int R = " << R << ", BT = " << selproj_block(mode) << ", W = BT / 64;\n"
     << "  constexpr qu64 F_AGG = 1ull << 62, F_INC = 2ull << 62, VMASK = (1ull << 62) - 1;\n"
     << "  constexpr bool PERSIST = " << (persistent ? "true" : "false") << ";\n"
     << "  __shared__ qu32 s_cnt[R * W];\n  __shared__ qu64 s_base;\n  __shared__ qu32 s_tile, s_total;\n"
-    << "  __shared__ qi64 s_out[" << ((size_t)nout * R * selproj_block() * 8 <= 64 * 1024 ? nout * R * selproj_block() : 1) << "];\n"
+    << "  __shared__ qi64 s_out[" << ((size_t)nout * R * selproj_block(mode) * 8 <= kSelprojStageBytes ? nout * R * selproj_block(mode) : 1) << "];\n"
     << "  const int t = threadIdx.x, lane = t & 63, w = t >> 6;\n";
   auto emit_loads = [&](const std::string& cp, const std::string& vp, const std::string& b, const std::string& ind) {
     emit_selproj_loads(P, o, need, selproj_nt(P), cp, vp, b, ind);

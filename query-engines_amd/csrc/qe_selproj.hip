@@ -53,7 +53,7 @@ int selproj_kernel(qe_ctx* ctx, const Plan& P, const int32_t* out_kind, int nout
   std::string src;
   if (!gen_selproj_source(P, out_kind, nout, &src, mode))
     return fail(QE_ERR_UNSUPPORTED, "plan shape is outside the select-project generator");
-  QE_TRY(jit_kernel(ctx, src, fn, bpc, "qe_selproj", selproj_block()));
+  QE_TRY(jit_kernel(ctx, src, fn, bpc, "qe_selproj", selproj_block(mode)));
   std::lock_guard<std::mutex> g(mu);
   memo[key] = {*fn, *bpc};
   return QE_OK;
@@ -134,11 +134,13 @@ int launch_select(qe_ctx* ctx, Plan& P, const int32_t* col_width, const int32_t*
   // (each write-pass tile sums all earlier tiles' counts, so the tile count is bounded too: a
   // plan with no predicate reads nothing in the count pass but still pays the prefix sums)
   const int R2 = selproj_rows(P, SP_COUNT);  // two-pass tiles
-  const int64_t tiles2 = (int64_t)div_up((uint64_t)n, (uint64_t)R2 * selproj_block());
+  const int64_t tiles2 = (int64_t)div_up((uint64_t)n, (uint64_t)R2 * selproj_block(SP_COUNT));
   const bool twopass = twopass_env >= 0 ? twopass_env == 1 : (pred_bytes <= (96ull << 20) && tiles2 <= 4096);
   // the look-back modes (persistent and its counter-ordered rerun) share one tile size
-  const int R = (twopass || twopass_env == 2) ? R2 : selproj_rows(P, SP_PERSIST);
-  const int64_t tiles = (int64_t)div_up((uint64_t)n, (uint64_t)R * selproj_block());
+  const bool two = twopass || twopass_env == 2;
+  const int R = two ? R2 : selproj_rows(P, SP_PERSIST);
+  const int BT = selproj_block(two ? SP_COUNT : SP_PERSIST);  // (SP_COUNTER shares SP_PERSIST's)
+  const int64_t tiles = (int64_t)div_up((uint64_t)n, (uint64_t)R * BT);
   QE_CHECK(tiles < (1ll << 31), QE_ERR_CAPACITY, "too many rows for one select-project call");
   // Scanned two passes (QE_SELPROJ_TWOPASS=2): count pass, a device scan of the tile counts, then
   // the write pass reads its tile's base — no look-back chain and no per-tile prefix sums, at the
@@ -156,12 +158,12 @@ int launch_select(qe_ctx* ctx, Plan& P, const int32_t* col_width, const int32_t*
     P.t.cap = (qu64)tiles;
     P.t.keys = (qi64*)cnt;
     QE_TRY(selproj_kernel(ctx, P, out_kind, nout, SP_COUNT, &fn, &bpc));
-    QE_TRY(jit_launch(ctx, fn, (int)tiles, P, selproj_block()));
+    QE_TRY(jit_launch(ctx, fn, (int)tiles, P, BT));
     QE_TRY(launch_check("qe_selproj (count)"));
     QE_TRY(exclusive_scan_i64(ctx, (const int64_t*)cnt, (int64_t*)offs, tiles));
     P.t.keys = (qi64*)offs;
     QE_TRY(selproj_kernel(ctx, P, out_kind, nout, SP_WRITE_SCAN, &fn, &bpc));
-    QE_TRY(jit_launch(ctx, fn, (int)tiles, P, selproj_block()));
+    QE_TRY(jit_launch(ctx, fn, (int)tiles, P, BT));
     QE_TRY(launch_check("qe_selproj (write)"));
     QE_HIP(hipMemsetAsync(pin + 1, 0, 8, ctx->stream));
     QE_HIP(hipMemcpyAsync(pin, offs + tiles, 8, hipMemcpyDeviceToHost, ctx->stream));
@@ -176,7 +178,7 @@ int launch_select(qe_ctx* ctx, Plan& P, const int32_t* col_width, const int32_t*
     P.t.cap = (qu64)tiles;
     for (int mode : {SP_COUNT, SP_WRITE}) {
       QE_TRY(selproj_kernel(ctx, P, out_kind, nout, mode, &fn, &bpc));
-      QE_TRY(jit_launch(ctx, fn, (int)tiles, P, selproj_block()));
+      QE_TRY(jit_launch(ctx, fn, (int)tiles, P, BT));
       QE_TRY(launch_check(mode == SP_COUNT ? "qe_selproj (count)" : "qe_selproj (write)"));
     }
     QE_HIP(hipMemsetAsync(pin + 1, 0, 8, ctx->stream));
@@ -207,7 +209,7 @@ int launch_select(qe_ctx* ctx, Plan& P, const int32_t* col_width, const int32_t*
   const int per_cu = std::max(1, std::min(wg_cap, bpc - margin));
   const int64_t grid = persist ? std::min<int64_t>(tiles, (int64_t)ctx->num_cus * per_cu * oversub) : tiles;
   QE_HIP(hipMemsetAsync(s, 0, sbytes, ctx->stream));
-  QE_TRY(jit_launch(ctx, fn, (int)grid, P, selproj_block()));
+  QE_TRY(jit_launch(ctx, fn, (int)grid, P, BT));
   QE_TRY(launch_check("qe_selproj"));
   QE_HIP(hipMemcpyAsync(pin, ctl + 1, 16, hipMemcpyDeviceToHost, ctx->stream));
   *persist_used = persist;

@@ -10,8 +10,7 @@ run() {  # name, env...
   echo "$name $(cat $OUT/$name.json)"
 }
 run dflt && \
-run b512 QE_SELPROJ_BLOCK=512 && \
-run b512_r8 QE_SELPROJ_BLOCK=512 QE_SELPROJ_ROWS=8 && \
-run b1024 QE_SELPROJ_BLOCK=1024 && \
-run b1024_r8 QE_SELPROJ_BLOCK=1024 QE_SELPROJ_ROWS=8 && \
-run margin1 QE_SELPROJ_OCC_MARGIN=1
+run lb512 QE_SELPROJ_LB_BLOCK=512 && \
+run lb1024 QE_SELPROJ_LB_BLOCK=1024 && \
+run lb1024_nt0 QE_SELPROJ_LB_BLOCK=1024 QE_SELPROJ_NT=0 && \
+run lb1024_r8 QE_SELPROJ_LB_BLOCK=1024 QE_SELPROJ_ROWS=8
