@@ -1107,6 +1107,16 @@ int selproj_block(int mode) {
   return (mode == SP_PERSIST || mode == SP_COUNTER) ? lb : 256;
 }
 
+// Look-back window per status round trip, in units of 64 predecessors (QE_SELPROJ_LBW = 1 / 2 / 4).
+int selproj_lbw() {
+  static const int v = [] {
+    const char* e = getenv("QE_SELPROJ_LBW");
+    const int k = e && *e ? atoi(e) : 1;
+    return (k == 2 || k == 4) ? k : 1;
+  }();
+  return v;
+}
+
 // LDS the staged select-project output may take (a 1024-thread tile of 16 rows per thread, one
 // 8-byte output: 128 KiB, one workgroup per CU)
 constexpr size_t kSelprojStageBytes = 128 * 1024;
@@ -1250,23 +1260,35 @@ bool emit_selproj_write(const Plan& P, const int32_t* out_kind, int nout, int mo
       "    qu64 excl = 0;\n"
       "    if (tile > 0) {\n"
       "      qi64 pos = (qi64)tile - 1;\n"
+      // window of 64 x LBW predecessors per round trip: lane l reads tiles pos - (l LBW + k)
       "      for (;;) {\n"
-      "        const qi64 idx = pos - lane;\n"
-      "        qu64 v;\n"
+      "        qu64 v[LBW];\n"
       "        qu32 spins = 0;\n"
-      "        do { v = idx >= 0 ? __hip_atomic_load(&st[idx], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : F_INC; }\n"
-      "        while (__any((v >> 62) == 0) && (!PERSIST || ++spins < (1u << 20)));\n"
+      "        bool pend;\n"
+      "        do {\n"
+      "          pend = false;\n"
+      "#pragma unroll\n"
+      "          for (int k = 0; k < LBW; ++k) {\n"
+      "            const qi64 idx = pos - (qi64)(lane * LBW + k);\n"
+      "            v[k] = idx >= 0 ? __hip_atomic_load(&st[idx], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : F_INC;\n"
+      "            pend = pend || (v[k] >> 62) == 0;\n"
+      "          }\n"
+      "        } while (__any(pend) && (!PERSIST || ++spins < (1u << 20)));\n"
       // persistent grid only: a predecessor that never publishes means a workgroup was not
       // resident after all; flag it (the host reruns with counter-ordered tiles) and let every
       // wave finish instead of hanging the device
-      "        if (PERSIST && spins >= (1u << 20)) { if (lane == 0) __hip_atomic_store(&P.t.ctl[2], 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); v = F_INC; }\n"
-      "        const qu64 incm = __ballot((v >> 62) == 2);\n"
-      "        qu64 c = v & VMASK;\n"
-      "        if (incm) { const int first = __ffsll((long long)incm) - 1; if (lane > first) c = 0; }\n"
+      "        if (PERSIST && spins >= (1u << 20)) { if (lane == 0) __hip_atomic_store(&P.t.ctl[2], 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);\n"
+      "#pragma unroll\n          for (int k = 0; k < LBW; ++k) v[k] = F_INC; }\n"
+      "        int kp = LBW;\n"
+      "#pragma unroll\n        for (int k = LBW - 1; k >= 0; --k) if ((v[k] >> 62) == 2) kp = k;\n"
+      "        const qu64 incm = __ballot(kp < LBW);\n"
+      "        const int first = incm ? __ffsll((long long)incm) - 1 : 64;\n"
+      "        qu64 c = 0;\n"
+      "#pragma unroll\n        for (int k = 0; k < LBW; ++k) if (lane < first || (lane == first && k <= kp)) c += v[k] & VMASK;\n"
       "#pragma unroll\n        for (int d = 32; d >= 1; d >>= 1) c += __shfl_xor(c, d);\n"
       "        excl += c;\n"
       "        if (incm) break;\n"
-      "        pos -= 64;\n"
+      "        pos -= 64 * LBW;\n"
       "      }\n"
       "      if (lane == 0) __hip_atomic_store(&st[tile], F_INC | (excl + total), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);\n"
       "    }\n"
@@ -1340,7 +1362,7 @@ bool gen_selproj_source(const Plan& P, const int32_t* out_kind, int nout, std::s
   std::ostringstream o;
   o << "\nusing namespace qe;\n"
     << "extern \"C\" __global__ void __launch_bounds__(" << selproj_block(mode) << ") qe_selproj(const Plan P) {\n"
-    << "  constexpr int R = " << R << ", BT = " << selproj_block(mode) << ", W = BT / 64;\n"
+    << "  constexpr int R = " << R << ", BT = " << selproj_block(mode) << ", W = BT / 64, LBW = " << selproj_lbw() << ";\n"
     << "  constexpr qu64 F_AGG = 1ull << 62, F_INC = 2ull << 62, VMASK = (1ull << 62) - 1;\n"
     << "  constexpr bool PERSIST = " << (persistent ? "true" : "false") << ";\n"
     << "  __shared__ qu32 s_cnt[R * W];\n  __shared__ qu64 s_base;\n  __shared__ qu32 s_tile, s_total;\n"

@@ -9,8 +9,8 @@ run() {  # name, env...
   env "$@" timeout -k 10 120 python3 tools/bench_configs.py C2L > $OUT/$name.json 2> $OUT/$name.err || return 1
   echo "$name $(cat $OUT/$name.json)"
 }
-run dflt && \
-run lb512 QE_SELPROJ_LB_BLOCK=512 && \
 run lb1024 QE_SELPROJ_LB_BLOCK=1024 && \
-run lb1024_nt0 QE_SELPROJ_LB_BLOCK=1024 QE_SELPROJ_NT=0 && \
-run lb1024_r8 QE_SELPROJ_LB_BLOCK=1024 QE_SELPROJ_ROWS=8
+run lb1024_w2 QE_SELPROJ_LB_BLOCK=1024 QE_SELPROJ_LBW=2 && \
+run lb1024_w4 QE_SELPROJ_LB_BLOCK=1024 QE_SELPROJ_LBW=4 && \
+run lb256_w4 QE_SELPROJ_LBW=4 && \
+run lb512_w4 QE_SELPROJ_LB_BLOCK=512 QE_SELPROJ_LBW=4
