@@ -1089,9 +1089,11 @@ std::string plan_shape_key(const qe_ctx* ctx, const Plan& P) {
 
 // Select-project workgroup size per mode. QE_SELPROJ_BLOCK (256 / 512 / 1024) sets every mode;
 // QE_SELPROJ_LB_BLOCK the look-back modes alone (persistent grid and its counter-ordered rerun),
-// whose pace is set by the tiles' prefix chain — one look-back window of 64 tiles per status round
-// trip — so that larger tiles move more rows per round trip (1B rows: 256 threads 4.66 ms, 512
-// 4.51, 1024 4.40 with the output unstaged).
+// default 1024: one tile of 16K rows per workgroup step, one workgroup per CU (its staged output
+// takes 128 KiB of LDS), so the whole 1B-row input is a quarter of the look-backs of 256-thread
+// tiles. 1B rows, C2 shape: 256 threads 4.66-4.71 ms, 512 4.51-4.66, 1024 4.07-4.35 (two boxes);
+// a look-back window of 128 or 256 predecessors per round trip was slower (1024 threads: 4.22 /
+// 4.39 ms against 4.07; every entry of the window must have published before the sum is taken).
 int selproj_block(int mode) {
   static const int all = [] {
     const char* e = getenv("QE_SELPROJ_BLOCK");
@@ -1100,14 +1102,15 @@ int selproj_block(int mode) {
   }();
   static const int lb = [] {
     const char* e = getenv("QE_SELPROJ_LB_BLOCK");
-    const int b = e && *e ? atoi(e) : 256;
-    return (b == 512 || b == 1024) ? b : 256;
+    const int b = e && *e ? atoi(e) : 1024;
+    return (b == 256 || b == 512) ? b : 1024;
   }();
   if (all) return all;
   return (mode == SP_PERSIST || mode == SP_COUNTER) ? lb : 256;
 }
 
-// Look-back window per status round trip, in units of 64 predecessors (QE_SELPROJ_LBW = 1 / 2 / 4).
+// Look-back window per status round trip, in units of 64 predecessors (QE_SELPROJ_LBW = 1 / 2 / 4;
+// default 1, the widest measured slowest).
 int selproj_lbw() {
   static const int v = [] {
     const char* e = getenv("QE_SELPROJ_LBW");
