@@ -139,6 +139,9 @@ struct Plan {
   qi32 mp_n, mp_pass;
   // spilling first pass (spill_update): rows with fmix64(key) >> 32 >= mp_keep are spilled as records
   qu64 mp_keep;
+  // select-project: pinned host words the kernel writes its results to ([0] rows written, [1] the
+  // persistent look-back's stall flag), so no copy command follows the kernel (null: device only)
+  qu64* host_ctl;
 };
 
 // ---- scalar helpers ---------------------------------------------------------------------------------

@@ -1083,6 +1083,7 @@ std::string plan_shape_key(const qe_ctx* ctx, const Plan& P) {
   k.part_chunk = nullptr;
   k.part_sorted = nullptr;
   k.mp_keep = 0;
+  k.host_ctl = nullptr;
   const int32_t extra[2] = {ctx->device, use_nt() ? 1 : 0};
   return std::string((const char*)&k, sizeof k) + std::string((const char*)extra, sizeof extra);
 }
@@ -1258,7 +1259,7 @@ bool emit_selproj_write(const Plan& P, const int32_t* out_kind, int nout, int mo
   const std::string lookback = mode == SP_WRITE || mode == SP_WRITE_SCAN ?
       "    const qu64 total = s_total;\n"
       "    if (lane == 0) {\n      qu64 excl = 0;\n      for (int q = 0; q < W; ++q) excl += s_pre[q];\n      s_base = excl;\n"
-      "      if ((qu64)tile == P.t.cap - 1) P.t.ctl[1] = excl + total;\n    }\n" :
+      "      if ((qu64)tile == P.t.cap - 1) { P.t.ctl[1] = excl + total; if (P.host_ctl) __hip_atomic_store(&P.host_ctl[0], excl + total, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM); }\n    }\n" :
       "    const qu64 total = s_total;\n"
       "    qu64 excl = 0;\n"
       "    if (tile > 0) {\n"
@@ -1280,7 +1281,7 @@ bool emit_selproj_write(const Plan& P, const int32_t* out_kind, int nout, int mo
       // persistent grid only: a predecessor that never publishes means a workgroup was not
       // resident after all; flag it (the host reruns with counter-ordered tiles) and let every
       // wave finish instead of hanging the device
-      "        if (PERSIST && spins >= (1u << 20)) { if (lane == 0) __hip_atomic_store(&P.t.ctl[2], 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);\n"
+      "        if (PERSIST && spins >= (1u << 20)) { if (lane == 0) { __hip_atomic_store(&P.t.ctl[2], 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); if (P.host_ctl) __hip_atomic_store(&P.host_ctl[1], 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM); }\n"
       "#pragma unroll\n          for (int k = 0; k < LBW; ++k) v[k] = F_INC; }\n"
       "        int kp = LBW;\n"
       "#pragma unroll\n        for (int k = LBW - 1; k >= 0; --k) if ((v[k] >> 62) == 2) kp = k;\n"
@@ -1296,7 +1297,7 @@ bool emit_selproj_write(const Plan& P, const int32_t* out_kind, int nout, int mo
       "      if (lane == 0) __hip_atomic_store(&st[tile], F_INC | (excl + total), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);\n"
       "    }\n"
       "    if (lane == 0) {\n      s_base = excl;\n"
-      "      if ((qu64)tile == P.t.cap - 1) __hip_atomic_store(&P.t.ctl[1], excl + total, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);\n    }\n";
+      "      if ((qu64)tile == P.t.cap - 1) { __hip_atomic_store(&P.t.ctl[1], excl + total, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); if (P.host_ctl) __hip_atomic_store(&P.host_ctl[0], excl + total, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM); }\n    }\n";
   o << "  __syncthreads();\n"
     << "  const qu64 below = (1ull << lane) - 1;\n";
   if (staged) {

@@ -14,6 +14,7 @@
 #include <memory>
 #include <mutex>
 #include <string>
+#include <vector>
 
 #include "qe_internal.hpp"
 
@@ -101,10 +102,7 @@ int launch_select(qe_ctx* ctx, Plan& P, const int32_t* col_width, const int32_t*
                   uint64_t* pin, bool* persist_used) {
   *persist_used = false;
   const int64_t n = P.n;
-  if (n == 0) {
-    QE_HIP(hipMemsetAsync(pin, 0, 16, ctx->stream));  // (pinned: a stream-ordered write of zeros)
-    return QE_OK;
-  }
+  if (n == 0) return QE_OK;  // pin[] was zeroed by the caller
   // Tile order: a persistent grid (every workgroup resident, tiles assigned statically) or one
   // tile per workgroup with ids from a device counter in start order (QE_SELPROJ_PERSIST=0). The
   // counter is one word every workgroup hits: ~88 returning atomics/us, a floor of 2.8 ms for
@@ -165,10 +163,12 @@ int launch_select(qe_ctx* ctx, Plan& P, const int32_t* col_width, const int32_t*
     QE_TRY(selproj_kernel(ctx, P, out_kind, nout, SP_WRITE_SCAN, &fn, &bpc));
     QE_TRY(jit_launch(ctx, fn, (int)tiles, P, BT));
     QE_TRY(launch_check("qe_selproj (write)"));
-    QE_HIP(hipMemsetAsync(pin + 1, 0, 8, ctx->stream));
     QE_HIP(hipMemcpyAsync(pin, offs + tiles, 8, hipMemcpyDeviceToHost, ctx->stream));
     return QE_OK;
   }
+  // the kernels write the count (and the stall flag) straight into the pinned words: no copy
+  // command behind them on the stream
+  P.host_ctl = (qu64*)pin;
   if (twopass) {
     void* s;
     QE_TRY(ctx_scratch(ctx, (size_t)(tiles + 3) * 8, &s));
@@ -181,8 +181,6 @@ int launch_select(qe_ctx* ctx, Plan& P, const int32_t* col_width, const int32_t*
       QE_TRY(jit_launch(ctx, fn, (int)tiles, P, BT));
       QE_TRY(launch_check(mode == SP_COUNT ? "qe_selproj (count)" : "qe_selproj (write)"));
     }
-    QE_HIP(hipMemsetAsync(pin + 1, 0, 8, ctx->stream));
-    QE_HIP(hipMemcpyAsync(pin, ctl + 1, 8, hipMemcpyDeviceToHost, ctx->stream));
     return QE_OK;
   }
   const size_t sbytes = (size_t)(3 + tiles) * 8;  // ctl[3] | per tile a look-back status word
@@ -211,14 +209,42 @@ int launch_select(qe_ctx* ctx, Plan& P, const int32_t* col_width, const int32_t*
   QE_HIP(hipMemsetAsync(s, 0, sbytes, ctx->stream));
   QE_TRY(jit_launch(ctx, fn, (int)grid, P, BT));
   QE_TRY(launch_check("qe_selproj"));
-  QE_HIP(hipMemcpyAsync(pin, ctl + 1, 16, hipMemcpyDeviceToHost, ctx->stream));
   *persist_used = persist;
   return QE_OK;
 }
 
-void pending_free(qe_select_pending* r) {
+// Completion events of select-project calls, reused (hipEventCreate per call cost a few us of
+// host time on every batch). A returned event has been synchronised on, so it is idle.
+std::mutex g_ev_mu;
+std::vector<hipEvent_t> g_ev_free;
+
+int event_alloc(hipEvent_t* ev) {
+  {
+    std::lock_guard<std::mutex> g(g_ev_mu);
+    if (!g_ev_free.empty()) {
+      *ev = g_ev_free.back();
+      g_ev_free.pop_back();
+      return QE_OK;
+    }
+  }
+  QE_HIP(hipEventCreateWithFlags(ev, hipEventDisableTiming));
+  return QE_OK;
+}
+
+void event_release(hipEvent_t ev, bool idle) {
+  if (!ev) return;
+  if (!idle) {  // never waited on (a failed launch): let the runtime retire it
+    (void)hipEventDestroy(ev);
+    return;
+  }
+  std::lock_guard<std::mutex> g(g_ev_mu);
+  if (g_ev_free.size() < 64) g_ev_free.push_back(ev);
+  else (void)hipEventDestroy(ev);
+}
+
+void pending_free(qe_select_pending* r, bool waited = false) {
   if (!r) return;
-  if (r->ev) (void)hipEventDestroy(r->ev);
+  event_release(r->ev, waited);
   if (r->pin) pinned_slot_free(r->pin, r->ctx->stream);
   delete r;
 }
@@ -261,7 +287,8 @@ int qe_select_project_async(qe_ctx* ctx, const qe_column* cols, int32_t ncols, c
   }
   if (!ctx->jit) return fail(QE_ERR_UNSUPPORTED, "fused select-project needs kernel specialisation (jit is off)");
   QE_TRY(pinned_slot_alloc(&r->pin));
-  QE_HIP(hipEventCreateWithFlags(&r->ev, hipEventDisableTiming));
+  r->pin[0] = r->pin[1] = 0;  // the slot's previous user is done with it (pinned_slot_alloc)
+  QE_TRY(event_alloc(&r->ev));
   QE_TRY(init_validity(ctx, outs, r->out_kind, r->nout, n));
   const int st = launch_select(ctx, P, r->col_width, r->out_kind, r->nout, true, r->pin, &r->persist);
   if (st != QE_OK) {
@@ -285,6 +312,7 @@ int qe_select_pending_wait(qe_select_pending* r, int64_t* out_count) {
     } else {
       fprintf(stderr, "qe: select-project persistent look-back stalled; rerunning with counter-ordered tiles\n");
       bool used = false;
+      r->pin[0] = r->pin[1] = 0;  // (the aborted launch has drained: the event completed)
       st = init_validity(ctx, r->outs, r->out_kind, r->nout, r->P.n);  // the aborted launch may have set bits anywhere
       if (st == QE_OK) st = launch_select(ctx, r->P, r->col_width, r->out_kind, r->nout, false, r->pin, &used);
       if (st == QE_OK) st = ctx_sync(ctx);
@@ -292,7 +320,7 @@ int qe_select_pending_wait(qe_select_pending* r, int64_t* out_count) {
     }
   }
   if (st == QE_OK) *out_count = (int64_t)r->pin[0];
-  pending_free(r);
+  pending_free(r, st == QE_OK);
   return st;
 }
 

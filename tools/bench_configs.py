@@ -171,7 +171,12 @@ def main():
             N.check(N.lib().qe_agg_global(ctx.handle, N.C.byref(c), None, N.C.byref(r)))
 
         ms = timed(run)
-        report("C3 SUM/MIN/MAX/COUNT/AVG global aggregate, 100M fp64", n, 8, ms, path="k_agg_global + final")
+        cc = (N.QeColumn * 1)(col.as_c())
+        sms = N.C.c_double()
+        shape = N.C.create_string_buffer(128)
+        N.check(N.lib().qe_stream_read_best(ctx.handle, cc, 1, 5, N.C.byref(sms), shape, 128))
+        report("C3 SUM/MIN/MAX/COUNT/AVG global aggregate, 100M fp64", n, 8, ms, path="k_agg_global + final",
+               stream_read_ceiling_gbs=n * 8 / (sms.value * 1e-3) / 1e9, stream_read_shape=shape.value.decode())
         del col
     for cfg, specs, rows, aggs, keys, spec, bpr, ng in (
             ("C4", C4_COLUMNS, 1_000_000_000, C4_AGGS, [N.TYPE_INT64], c4_spec(), 24, 1024),
@@ -193,8 +198,14 @@ def main():
         kmed = statistics.median(kms[-10:])
         name = ("C4 SELECT k,SUM(a+b),COUNT(*),MIN(a),MAX(b) WHERE a>2^19 GROUP BY k, 1B int64" if cfg == "C4" else
                 "C5 lineitem Q1-like (3 predicates, GROUP BY returnflag,linestatus, 4 SUM+AVG+COUNT), 1.25B rows/GPU")
+        # streaming-read ceiling over the same columns (best launch shape, qe_stream_read_best)
+        cc = (N.QeColumn * len(cols))(*[c.as_c() for c in cols])
+        sms = N.C.c_double()
+        shape = N.C.create_string_buffer(128)
+        N.check(N.lib().qe_stream_read_best(ctx.handle, cc, len(cols), 5, N.C.byref(sms), shape, 128))
         report(name, rows, bpr, ms, kernel_ms=kmed, kernel_gbs=rows * bpr / (kmed * 1e-3) / 1e9,
-               specialised=kind[0], note=kind[1], groups=st.num_groups())
+               specialised=kind[0], note=kind[1], groups=st.num_groups(),
+               stream_read_ceiling_gbs=rows * bpr / (sms.value * 1e-3) / 1e9, stream_read_shape=shape.value.decode())
         del cols, st
 
 
