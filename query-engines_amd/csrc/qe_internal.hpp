@@ -62,6 +62,7 @@ int ctx_scratch(qe_ctx* ctx, size_t bytes, void** out);       // grow-only scrat
 int ctx_pinned(qe_ctx* ctx, size_t bytes, void** out);        // grow-only pinned host
 int pinned_slot_alloc(uint64_t** out);                        // 64 pinned bytes (pooled)
 void pinned_slot_free(uint64_t* p, hipStream_t stream);       // reusable once `stream`'s work is done
+void pinned_slot_free_idle(uint64_t* p);                        // no device access pending: reusable now
 // Wait for everything queued on the ctx stream (blocking; polling an event from this thread
 // measured 15 us slower per finalize).
 int ctx_sync(qe_ctx* ctx);

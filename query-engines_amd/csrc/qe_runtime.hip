@@ -209,6 +209,13 @@ void pinned_slot_free(uint64_t* p, hipStream_t stream) {
   g_pfree.push_back({p, ev});
 }
 
+// A slot whose last device access is known complete (the caller waited for it): reusable at once.
+void pinned_slot_free_idle(uint64_t* p) {
+  if (!p) return;
+  std::lock_guard<std::mutex> lk(g_pmu);
+  g_pnew.push_back(p);
+}
+
 static thread_local std::string g_last_error;
 
 int fail(int code, const char* fmt, ...) {

@@ -245,7 +245,10 @@ void event_release(hipEvent_t ev, bool idle) {
 void pending_free(qe_select_pending* r, bool waited = false) {
   if (!r) return;
   event_release(r->ev, waited);
-  if (r->pin) pinned_slot_free(r->pin, r->ctx->stream);
+  if (r->pin) {  // waited: the kernels that write it have completed
+    if (waited) pinned_slot_free_idle(r->pin);
+    else pinned_slot_free(r->pin, r->ctx->stream);
+  }
   delete r;
 }
 
