@@ -108,6 +108,43 @@ def main():
                                          [False, True, False])
             ok = len(got) == len(want) and all(got[key[0]] == w for key, w in want.items())
             results[mode] = {"ok": ok, "groups": len(got)}
+    # deterministic fp64 SUM / AVG across ranks: the exchanged partials carry exact fixed-point
+    # limbs, so every group equals math.fsum over both ranks' rows bit for bit
+    import math
+
+    rng = np.random.default_rng(700 + rank)
+    n = 60_000 + 5000 * rank
+    k = rng.integers(0, 900, n).astype(np.int64)
+    x = np.round(rng.normal(size=n) * np.exp2(rng.integers(-10, 25, n)) * 2.0 ** 50) * 2.0 ** -50
+    aggs = [(N.AGG_SUM, N.TYPE_FLOAT64), (N.AGG_AVG, N.TYPE_FLOAT64), (N.AGG_COUNT_STAR, N.TYPE_INT64)]
+    partial = HashAggregateState(ctx, [N.TYPE_INT64], aggs, 1024, deterministic=True)
+    owner = HashAggregateState(ctx, [N.TYPE_INT64], aggs, 1024, deterministic=True)
+    partial.set_row_base(rank * 10_000_000)
+    partial.update([DeviceColumn.from_numpy(N.TYPE_INT64, k, ctx=ctx)],
+                   [DeviceColumn.from_numpy(N.TYPE_FLOAT64, x, ctx=ctx)] * 2 + [None])
+    exchange_partials(partial, owner)
+    ko, ao = owner.finalize()
+    mine = [(int(a), float(b), float(c), int(d)) for a, b, c, d in
+            zip(ko[0].to_numpy(), ao[0].to_numpy(), ao[1].to_numpy(), ao[2].to_numpy())]
+    allrows = [None] * world
+    dist.all_gather_object(allrows, mine)
+    if rank == 0:
+        got = {r[0]: r[1:] for rows in allrows for r in rows}
+        kk, xs = [], []
+        for q in range(world):
+            g = np.random.default_rng(700 + q)
+            n2 = 60_000 + 5000 * q
+            k2 = g.integers(0, 900, n2).astype(np.int64)
+            x2 = np.round(g.normal(size=n2) * np.exp2(g.integers(-10, 25, n2)) * 2.0 ** 50) * 2.0 ** -50
+            kk.append(k2)
+            xs.append(x2)
+        kk, xs = np.concatenate(kk), np.concatenate(xs)
+        ok = len(got) == len(np.unique(kk))
+        for key in np.unique(kk):
+            v = xs[kk == key].tolist()
+            s_, a_, c_ = got[int(key)]
+            ok = ok and s_ == math.fsum(v) and a_ == math.fsum(v) / len(v) and c_ == len(v)
+        results["deterministic"] = {"ok": bool(ok), "groups": len(got)}
     # global aggregate over rank shards: one all-gather of partials, identical merge on every rank
     from kquery.exchange import global_aggregate
 

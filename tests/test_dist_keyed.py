@@ -1,5 +1,6 @@
 """Partials across ranks: dictionary-keyed (exchange_keyed_partials) and numeric keys through the
-fixed-capacity slot exchange and its overflow fallback. Two processes on the one GPU, gloo
+fixed-capacity slot exchange and its overflow fallback, and deterministic (fixed-point) fp64 sums
+that must equal math.fsum over both ranks' rows after the exchange. Two processes on the one GPU, gloo
 backend (RCCL cannot put two ranks on one device); see tests/dist_keyed_worker.py."""
 import json
 import os
@@ -29,4 +30,4 @@ def test_keyed_exchange_two_ranks():
     line = [ln for ln in r.stdout.splitlines() if ln.startswith("RESULT ")]
     assert line, r.stdout[-2000:] + r.stderr[-2000:]
     res = json.loads(line[0][len("RESULT "):])
-    assert all(res[m]["ok"] for m in ("utf8", "tuple", "slots", "slots_overflow", "global")), res
+    assert all(res[m]["ok"] for m in ("utf8", "tuple", "slots", "slots_overflow", "deterministic", "global")), res
