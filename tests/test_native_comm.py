@@ -78,3 +78,23 @@ def test_comm_rejects_bad_arguments(gpu_ctx):
     h = N.C.c_void_p()
     assert N.lib().qe_comm_create(gpu_ctx.handle, 2, 5, uid, N.C.byref(h)) == N.QE_ERR_INVALID_ARG
     assert N.lib().qe_hashagg_exchange(None, None, None, 0, None) == N.QE_ERR_INVALID_ARG
+
+
+def test_slot_capacity_ignores_the_ranks_own_groups(gpu_ctx):
+    """the exchange's slot size must be the same on every rank. It comes from the
+    expected groups given at create time (qe_hashagg_slot_capacity), not from the sizing hint an
+    update raises once this rank's own groups outgrow the LDS table."""
+    import numpy as np
+
+    from kquery import native as N
+    from kquery.aggregate import HashAggregateState
+    from kquery.columnar import DeviceColumn
+
+    st = HashAggregateState(gpu_ctx, [N.TYPE_INT64], [(N.AGG_COUNT_STAR, N.TYPE_INT64)], 1024)
+    before = [st.slot_capacity(w) for w in (1, 2, 8)]
+    assert before == [1024, min(1024, -(-3 * 1024 // 4) + 32), min(1024, -(-3 * 1024 // 16) + 32)]
+    k = np.random.default_rng(3).integers(0, 60_000, 400_000).astype(np.int64)
+    for _ in range(2):  # the second batch runs with the state adapted to ~60K groups
+        st.update([DeviceColumn.from_numpy(N.TYPE_INT64, k, ctx=gpu_ctx)], [None])
+    assert st.num_groups() == len(np.unique(k))
+    assert [st.slot_capacity(w) for w in (1, 2, 8)] == before
