@@ -1939,8 +1939,9 @@ static int partition_rows(qe_hashagg* h, Plan& P, hipFunction_t* fn, int* grid) 
   const bool chunked = chunk_env != 0 && staged && np_all <= CHUNK_PLAN_MAXB &&
                        (chunk_env == 1 || open_slots <= n) && (uint64_t)cmax * PART_CH * rb <= (96ull << 30);
   QE_CHECK((chunked || gen_part_source(P, log2p, false, &sc)) &&
-               (staged ? gen_pscatter_staged_source(P, log2p, &ss, chunked) : gen_part_source(P, log2p, true, &ss)) &&
-               gen_pagg_source(P, tlog2, &sa, &jl, chunked),
+               (staged ? gen_pscatter_staged_source(P, log2p, &ss, chunked, chunked && part_soa())
+                       : gen_part_source(P, log2p, true, &ss)) &&
+               gen_pagg_source(P, tlog2, &sa, &jl, chunked, chunked && part_soa()),
            QE_ERR_UNSUPPORTED, "plan shape not specialisable");
   hipFunction_t fc = nullptr, fs;
   int bpc = 0;

@@ -98,7 +98,8 @@ int fused_block(int lds_log2);
 // hash-aggregate state accessors for other translation units (qe_comm.hip)
 int hashagg_expected_groups(const qe_hashagg* h, int64_t* out);
 qe_ctx* hashagg_ctx(const qe_hashagg* h);
-bool gen_pscatter_staged_source(const qe::Plan& P, int log2p, std::string* src, bool chunked = false);
+bool gen_pscatter_staged_source(const qe::Plan& P, int log2p, std::string* src, bool chunked = false, bool soa = false);
+bool part_soa();  // chunked partition records stored chunk-columnar (QE_PART_SOA)
 int jit_kernel(qe_ctx* ctx, const std::string& src, hipFunction_t* fn, int* blocks_per_cu,
                const char* name = "qe_fused", int block = 512);
 int jit_launch(qe_ctx* ctx, hipFunction_t fn, int grid, const qe::Plan& P, int block = 512);

@@ -733,7 +733,20 @@ int pscatter_depth() {
   return d;
 }
 
-bool gen_pscatter_staged_source(const Plan& P, int log2p, std::string* src, bool chunked) {
+// Chunked partition records chunk-columnar (QE_PART_SOA=1): word q of a chunk's records together,
+// as the spilling pass writes them, so the aggregation pass loads each word as one contiguous
+// 512-byte run per wave instead of 8-byte words 8 x W bytes apart; the scatter's write-out then
+// writes each word of a bucket's run separately.
+bool part_soa() {
+  static const bool v = [] {
+    const char* e = getenv("QE_PART_SOA");
+    return e && e[0] == '1';
+  }();
+  return v;
+}
+
+bool gen_pscatter_staged_source(const Plan& P, int log2p, std::string* src, bool chunked, bool soa) {
+  if (soa && !chunked) return false;
   if (P.ncols < 1 || P.ncols > QE_MAX_COLS || log2p < 1 || !part_staged_ok(P, log2p)) return false;
   std::vector<Expr> ex;
   if (!agg_inputs(P, &ex)) return false;
@@ -853,13 +866,22 @@ bool gen_pscatter_staged_source(const Plan& P, int log2p, std::string* src, bool
       << (W % 2 ? "rw[r][q]" : "qi64x2{rw[r][2 * q], rw[r][2 * q + 1]}") << ";\n"
       << "    }\n"
       << "    __syncthreads();\n"
-      << "    const qu32 tot = s_total;\n"
-      << "    for (qu32 c = threadIdx.x; c < tot * WC; c += blockDim.x) {\n"
-      << "      const qu32 j = c / WC, q = c % WC;\n"
-      << (chunked ? "      const qu32 b = s_bkt[j];\n      const qu64 dst = (j < s_lim[b] ? s_dst[b] : s_dst2[b]) + j;\n"
-                  : "      const qu64 dst = s_dst[s_bkt[j]] + j;\n")
-      << "      ((" << chunk << "*)(P.part_rec + dst * " << 8 * W << "ull))[q] = s_rec[c];\n"
-      << "    }\n"
+      << "    const qu32 tot = s_total;\n";
+    if (soa)
+      // word-major: consecutive threads write consecutive records' word q (one run per word)
+      o << "    for (qu32 c = threadIdx.x; c < tot * W; c += blockDim.x) {\n"
+        << "      const qu32 q = c / tot, j = c - q * tot;\n"
+        << "      const qu32 b = s_bkt[j];\n      const qu64 dst = (j < s_lim[b] ? s_dst[b] : s_dst2[b]) + j;\n"
+        << "      ((qi64*)P.part_rec)[(dst / PART_CH) * (W * PART_CH) + q * PART_CH + dst % PART_CH] = ((const qi64*)s_rec)[j * W + q];\n"
+        << "    }\n";
+    else
+      o << "    for (qu32 c = threadIdx.x; c < tot * WC; c += blockDim.x) {\n"
+        << "      const qu32 j = c / WC, q = c % WC;\n"
+        << (chunked ? "      const qu32 b = s_bkt[j];\n      const qu64 dst = (j < s_lim[b] ? s_dst[b] : s_dst2[b]) + j;\n"
+                    : "      const qu64 dst = s_dst[s_bkt[j]] + j;\n")
+        << "      ((" << chunk << "*)(P.part_rec + dst * " << 8 * W << "ull))[q] = s_rec[c];\n"
+        << "    }\n";
+    o
       << "  }\n";
   }
   o << "  }\n";

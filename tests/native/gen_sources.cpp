@@ -108,8 +108,18 @@ static int emit_agg(const char* dir, const char* name, const qe_column* cols, in
     fprintf(stderr, "%s: fused / spill / pagg source not generated\n", name);
     return 1;
   }
+  // radix-partitioned path: staged chunked scatter over 64 buckets, records row-major and
+  // chunk-columnar (QE_PART_SOA), and the chunk-columnar aggregation pass
+  std::string d, e, f;
+  P.mp_n = 0;
+  if (!gen_pscatter_staged_source(P, 6, &d, true, false) || !gen_pscatter_staged_source(P, 6, &e, true, true) ||
+      !gen_pagg_source(P, log2, &f, &lds, true, false)) {
+    fprintf(stderr, "%s: partition sources not generated\n", name);
+    return 1;
+  }
   return write_src(dir, std::string(name) + "_fused", a) | write_src(dir, std::string(name) + "_spill", b) |
-         write_src(dir, std::string(name) + "_pagg", c);
+         write_src(dir, std::string(name) + "_pagg", c) | write_src(dir, std::string(name) + "_pscatter", d) |
+         write_src(dir, std::string(name) + "_pscatter_soa", e) | write_src(dir, std::string(name) + "_pagg_rows", f);
 }
 
 int main(int argc, char** argv) {

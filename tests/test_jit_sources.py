@@ -31,12 +31,14 @@ def sources(tmp_path_factory):
 def test_all_modes_emitted(sources):
     names = sorted(p.name for p in sources)
     assert names == sorted([f"{s}_m{m}.hip" for s in ("c2", "nullable") for m in range(5)] +
-                           [f"{s}_{k}.hip" for s in ("c4", "f64max", "det") for k in ("fused", "spill", "pagg")])
+                           [f"{s}_{k}.hip" for s in ("c4", "f64max", "det")
+                            for k in ("fused", "spill", "pagg", "pscatter", "pscatter_soa", "pagg_rows")])
 
 
 @pytest.mark.parametrize("name", ["c2_m0", "c2_m1", "c2_m2", "c2_m3", "c2_m4", "nullable_m1", "nullable_m3",
                                   "nullable_m4", "c4_fused", "c4_spill", "c4_pagg", "f64max_spill",
-                                  "f64max_pagg", "det_fused", "det_spill", "det_pagg"])
+                                  "f64max_pagg", "det_fused", "det_spill", "det_pagg", "c4_pscatter",
+                                  "c4_pscatter_soa", "c4_pagg_rows", "det_pscatter_soa", "f64max_pscatter_soa"])
 def test_compiles_for_gfx950(sources, name, tmp_path):
     src = next(p for p in sources if p.stem == name)
     r = subprocess.run([HIPCC, "--offload-arch=gfx950", "-O3", "-std=c++17", "-ffp-contract=off",
