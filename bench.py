@@ -172,7 +172,13 @@ def launch_ranks(args) -> int:
            "--master-addr=127.0.0.1", f"--master-port={port}", str(pathlib.Path(__file__).resolve())] + sys.argv[1:]
     env = dict(os.environ)
     env.setdefault("OMP_NUM_THREADS", "4")
-    return subprocess.run(cmd, env=env).returncode
+    # stdout carries rank 0's JSON line only: anything else the ranks print there (gloo's
+    # connection lines, library notices) goes to stderr
+    proc = subprocess.Popen(cmd, env=env, stdout=subprocess.PIPE, text=True, bufsize=1)
+    for line in proc.stdout:
+        (sys.stdout if line.startswith("{") else sys.stderr).write(line)
+    sys.stdout.flush()
+    return proc.wait()
 
 
 def main():
