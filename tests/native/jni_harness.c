@@ -1,0 +1,840 @@
+/*
+ * Drives the JNI shim (query-engines_amd/jni/qe_jni.c) the way the Kotlin classes of
+ * NativeOperators.kt do, without a JVM: a fake JNIEnv (tests/native/jnistub/jni.h) whose Java
+ * arrays, strings, direct buffers and exceptions are host structs. Self-checking: every case
+ * computes its expected answer on the host and prints "ok <case>" or "FAIL <case>: ...";
+ * exit status 0 iff all cases pass.
+ *
+ *   jni_harness cpu   argument checking and exception mapping (no GPU needed)
+ *   jni_harness gpu   end to end on device 0: the reference's operator chain (K:582-660) through
+ *                     the shim — unfused and fused GROUP BY, two-phase merge, deterministic fp64
+ *                     sums, pipelined select-project, CAST, global aggregate, Arrow C Data in /
+ *                     out, Utf8 keys, CSV scan, and the exceptions K: throws.
+ *
+ * The shim is compiled into this translation unit so that every call is type-checked.
+ */
+#include <math.h>
+#include <stdarg.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include "../../query-engines_amd/jni/qe_jni.c"
+
+/* ---- fake JVM objects --------------------------------------------------------------------- */
+
+enum { K_LONGS = 1, K_INTS, K_BYTES, K_DOUBLES, K_STRING, K_OBJS, K_CLASS, K_BUF };
+struct _jobject {
+  int kind;
+  jsize len;
+  void* data;
+};
+
+static char g_exc[128], g_msg[512];
+static int g_pending;
+
+static jobject obj_new(int kind, jsize len, size_t elem) {
+  jobject o = (jobject)calloc(1, sizeof(struct _jobject));
+  o->kind = kind;
+  o->len = len;
+  o->data = calloc((size_t)(len > 0 ? len : 1), elem ? elem : 1);
+  return o;
+}
+
+static void jraise(const char* cls, const char* msg) {
+  if (g_pending) return;
+  g_pending = 1;
+  snprintf(g_exc, sizeof g_exc, "%s", cls);
+  snprintf(g_msg, sizeof g_msg, "%s", msg ? msg : "");
+}
+
+static jclass f_FindClass(JNIEnv* env, const char* name) {
+  (void)env;
+  jobject o = obj_new(K_CLASS, (jsize)strlen(name) + 1, 1);
+  memcpy(o->data, name, strlen(name) + 1);
+  return o;
+}
+static jint f_ThrowNew(JNIEnv* env, jclass c, const char* msg) {
+  (void)env;
+  jraise((const char*)c->data, msg);
+  return 0;
+}
+static jboolean f_ExceptionCheck(JNIEnv* env) {
+  (void)env;
+  return (jboolean)g_pending;
+}
+static void f_DeleteLocalRef(JNIEnv* env, jobject o) { (void)env, (void)o; }
+static jsize f_GetArrayLength(JNIEnv* env, jarray a) {
+  (void)env;
+  return a->len;
+}
+static jobject f_GetObjectArrayElement(JNIEnv* env, jobjectArray a, jsize i) {
+  (void)env;
+  if (i < 0 || i >= a->len) {
+    jraise("java/lang/ArrayIndexOutOfBoundsException", "index");
+    return NULL;
+  }
+  return ((jobject*)a->data)[i];
+}
+static jbyteArray f_NewByteArray(JNIEnv* env, jsize n) {
+  (void)env;
+  return obj_new(K_BYTES, n, 1);
+}
+static jintArray f_NewIntArray(JNIEnv* env, jsize n) {
+  (void)env;
+  return obj_new(K_INTS, n, 4);
+}
+static jlongArray f_NewLongArray(JNIEnv* env, jsize n) {
+  (void)env;
+  return obj_new(K_LONGS, n, 8);
+}
+static int region_ok(jarray a, int kind, jsize s, jsize n) {
+  if (!a || a->kind != kind) {
+    jraise("java/lang/ClassCastException", "array kind");
+    return 0;
+  }
+  if (s < 0 || n < 0 || s + n > a->len) {
+    jraise("java/lang/ArrayIndexOutOfBoundsException", "region");
+    return 0;
+  }
+  return 1;
+}
+#define REGION(NAME, KIND, T, ES)                                                         \
+  static void f_Get##NAME(JNIEnv* env, jarray a, jsize s, jsize n, T* buf) {             \
+    (void)env;                                                                            \
+    if (region_ok(a, KIND, s, n)) memcpy(buf, (char*)a->data + (size_t)s * ES, (size_t)n * ES); \
+  }                                                                                       \
+  static void f_Set##NAME(JNIEnv* env, jarray a, jsize s, jsize n, const T* buf) {       \
+    (void)env;                                                                            \
+    if (region_ok(a, KIND, s, n)) memcpy((char*)a->data + (size_t)s * ES, buf, (size_t)n * ES); \
+  }
+REGION(ByteArrayRegion, K_BYTES, jbyte, 1)
+REGION(IntArrayRegion, K_INTS, jint, 4)
+REGION(LongArrayRegion, K_LONGS, jlong, 8)
+REGION(DoubleArrayRegion, K_DOUBLES, jdouble, 8)
+static jstring f_NewStringUTF(JNIEnv* env, const char* s) {
+  (void)env;
+  jobject o = obj_new(K_STRING, (jsize)strlen(s) + 1, 1);
+  memcpy(o->data, s, strlen(s) + 1);
+  return o;
+}
+static const char* f_GetStringUTFChars(JNIEnv* env, jstring s, jboolean* copy) {
+  (void)env;
+  if (copy) *copy = 0;
+  return (const char*)s->data;
+}
+static void f_ReleaseStringUTFChars(JNIEnv* env, jstring s, const char* c) { (void)env, (void)s, (void)c; }
+static void* f_GetDirectBufferAddress(JNIEnv* env, jobject b) {
+  (void)env;
+  return b && b->kind == K_BUF ? b->data : NULL;
+}
+static jlong f_GetDirectBufferCapacity(JNIEnv* env, jobject b) {
+  (void)env;
+  return b && b->kind == K_BUF ? b->len : -1;
+}
+
+static const struct JNINativeInterface_ g_table = {
+    f_FindClass, f_ThrowNew, f_ExceptionCheck, f_DeleteLocalRef, f_GetArrayLength, f_GetObjectArrayElement,
+    f_NewByteArray, f_NewIntArray, f_NewLongArray, f_GetByteArrayRegion, f_GetIntArrayRegion,
+    f_GetLongArrayRegion, f_GetDoubleArrayRegion, f_SetByteArrayRegion, f_SetIntArrayRegion,
+    f_SetLongArrayRegion, f_SetDoubleArrayRegion, f_NewStringUTF, f_GetStringUTFChars,
+    f_ReleaseStringUTFChars, f_GetDirectBufferAddress, f_GetDirectBufferCapacity,
+};
+static JNIEnv g_envp = &g_table;
+static JNIEnv* E = &g_envp;
+#define K NULL /* the jclass of the static `external fun`s (unused by the shim) */
+
+/* Java-side constructors */
+static jlongArray JL(const int64_t* v, jsize n) {
+  jobject o = obj_new(K_LONGS, n, 8);
+  if (n) memcpy(o->data, v, (size_t)n * 8);
+  return o;
+}
+static jintArray JI(const int32_t* v, jsize n) {
+  jobject o = obj_new(K_INTS, n, 4);
+  if (n) memcpy(o->data, v, (size_t)n * 4);
+  return o;
+}
+static jdoubleArray JD(const double* v, jsize n) {
+  jobject o = obj_new(K_DOUBLES, n, 8);
+  if (n) memcpy(o->data, v, (size_t)n * 8);
+  return o;
+}
+static jbyteArray JB(const uint8_t* v, jsize n) {
+  jobject o = obj_new(K_BYTES, n, 1);
+  if (n) memcpy(o->data, v, (size_t)n);
+  return o;
+}
+static jobjectArray JO(jobject* v, jsize n) {
+  jobject o = obj_new(K_OBJS, n, sizeof(jobject));
+  memcpy(o->data, v, (size_t)n * sizeof(jobject));
+  return o;
+}
+#define LONGS(...) JL((const int64_t[]){__VA_ARGS__}, (jsize)(sizeof((const int64_t[]){__VA_ARGS__}) / 8))
+#define INTS(...) JI((const int32_t[]){__VA_ARGS__}, (jsize)(sizeof((const int32_t[]){__VA_ARGS__}) / 4))
+#define NOINTS JI(NULL, 0)
+#define NOLONGS JL(NULL, 0)
+
+/* ---- checking ----------------------------------------------------------------------------- */
+
+static int g_fail;
+static const char* g_case = "";
+
+static void fail(const char* fmt, ...) __attribute__((format(printf, 1, 2)));
+static void fail(const char* fmt, ...) {
+  char m[512];
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(m, sizeof m, fmt, ap);
+  va_end(ap);
+  printf("FAIL %s: %s\n", g_case, m);
+  fflush(stdout);
+  ++g_fail;
+}
+
+/* evaluate `expr` expecting no Java exception */
+#define OK(expr)                                                              \
+  ({                                                                          \
+    g_pending = 0;                                                            \
+    __typeof__(expr) r_ = (expr);                                             \
+    if (g_pending) fail("%s threw %s: %s", #expr, g_exc, g_msg);              \
+    r_;                                                                       \
+  })
+#define OKV(expr)                                                             \
+  do {                                                                        \
+    g_pending = 0;                                                            \
+    expr;                                                                     \
+    if (g_pending) fail("%s threw %s: %s", #expr, g_exc, g_msg);              \
+  } while (0)
+/* evaluate `expr` expecting exception class `cls` */
+#define THROWS(cls, expr)                                                     \
+  do {                                                                        \
+    g_pending = 0;                                                            \
+    expr;                                                                     \
+    if (!g_pending) fail("%s did not throw (expected %s)", #expr, cls);       \
+    else if (strcmp(g_exc, cls)) fail("%s threw %s (%s), expected %s", #expr, g_exc, g_msg, cls); \
+    g_pending = 0;                                                            \
+  } while (0)
+#define CHECK(cond, ...) \
+  do {                   \
+    if (!(cond)) fail(__VA_ARGS__); \
+  } while (0)
+
+static void begin(const char* name) { g_case = name; }
+static void end(int fails_before) {
+  if (g_fail == fails_before) printf("ok %s\n", g_case);
+  fflush(stdout);
+}
+
+static const int64_t* LV(jlongArray a) { return (const int64_t*)a->data; }
+
+/* host copy of a fixed-width column as int64 + validity (1 = valid) */
+static int64_t* fetch_longs(jlong ctx, jlong col, uint8_t** valid) {
+  const jlong n = OK(Java_NativeEngine_columnLength(E, K, col));
+  jlongArray a = obj_new(K_LONGS, (jsize)n, 8);
+  OKV(Java_NativeEngine_columnToLongs(E, K, ctx, col, a));
+  jbyteArray v = OK(Java_NativeEngine_columnValidity(E, K, ctx, col));
+  *valid = (uint8_t*)calloc((size_t)(n ? n : 1), 1);
+  for (jlong i = 0; i < n; ++i) (*valid)[i] = v ? (((uint8_t*)v->data)[i >> 3] >> (i & 7)) & 1 : 1;
+  return (int64_t*)a->data;
+}
+static double* fetch_doubles(jlong ctx, jlong col, uint8_t** valid) {
+  const jlong n = OK(Java_NativeEngine_columnLength(E, K, col));
+  jdoubleArray a = obj_new(K_DOUBLES, (jsize)n, 8);
+  OKV(Java_NativeEngine_columnToDoubles(E, K, ctx, col, a));
+  jbyteArray v = OK(Java_NativeEngine_columnValidity(E, K, ctx, col));
+  *valid = (uint8_t*)calloc((size_t)(n ? n : 1), 1);
+  for (jlong i = 0; i < n; ++i) (*valid)[i] = v ? (((uint8_t*)v->data)[i >> 3] >> (i & 7)) & 1 : 1;
+  return (double*)a->data;
+}
+/* UTF8 column -> NUL-separated host strings (strs[i] points into one buffer; NULL = null row) */
+static char** fetch_strings(jlong ctx, jlong col, jlong* n_out) {
+  const jlong n = OK(Java_NativeEngine_columnLength(E, K, col));
+  jintArray off = OK(Java_NativeEngine_columnUtf8Offsets(E, K, ctx, col));
+  jbyteArray bytes = OK(Java_NativeEngine_columnUtf8Bytes(E, K, ctx, col));
+  jbyteArray v = OK(Java_NativeEngine_columnValidity(E, K, ctx, col));
+  char** s = (char**)calloc((size_t)(n ? n : 1), sizeof(char*));
+  for (jlong i = 0; off && bytes && i < n; ++i) {
+    const int32_t* o = (const int32_t*)off->data;
+    if (v && !((((uint8_t*)v->data)[i >> 3] >> (i & 7)) & 1)) continue;
+    s[i] = (char*)calloc((size_t)(o[i + 1] - o[i] + 1), 1);
+    memcpy(s[i], (char*)bytes->data + o[i], (size_t)(o[i + 1] - o[i]));
+  }
+  *n_out = n;
+  return s;
+}
+static jlong utf8_col(jlong ctx, const char* const* s, int n) {
+  int32_t* off = (int32_t*)calloc((size_t)n + 1, 4);
+  uint8_t valid[16] = {0};
+  size_t tot = 0;
+  for (int i = 0; i < n; ++i) tot += s[i] ? strlen(s[i]) : 0;
+  uint8_t* b = (uint8_t*)calloc(tot + 1, 1);
+  for (int i = 0; i < n; ++i) {
+    const size_t l = s[i] ? strlen(s[i]) : 0;
+    memcpy(b + off[i], s[i] ? s[i] : "", l);
+    off[i + 1] = off[i] + (int32_t)l;
+    if (s[i]) valid[i >> 3] |= (uint8_t)(1u << (i & 7));
+  }
+  const jlong h = OK(Java_NativeEngine_columnFromUtf8(E, K, ctx, JI(off, n + 1), JB(b, (jsize)tot), JB(valid, (n + 7) / 8)));
+  free(off);
+  free(b);
+  return h;
+}
+
+/* ---- CPU cases: argument checks and exception mapping ------------------------------------- */
+
+static void cpu_cases(void) {
+  int f0;
+  begin("abi_version");
+  f0 = g_fail;
+  CHECK(OK(Java_NativeEngine_abiVersion(E, K)) == QE_ABI_VERSION, "abi version");
+  end(f0);
+
+  begin("ctx_without_gpu_throws");
+  f0 = g_fail;
+  THROWS("java/lang/RuntimeException", Java_NativeEngine_ctxCreate(E, K, 0));
+  end(f0);
+
+  begin("null_handles");
+  f0 = g_fail;
+  THROWS("java/lang/IllegalArgumentException", Java_NativeEngine_columnLength(E, K, 0));
+  THROWS("java/lang/IllegalArgumentException", Java_NativeEngine_aggNumGroups(E, K, 0));
+  THROWS("java/lang/IllegalArgumentException", Java_NativeEngine_evalArith(E, K, 0, QE_OP_ADD, 0, 0, QE_TYPE_INT64, 1, 0));
+  OKV(Java_NativeEngine_columnFree(E, K, 0));
+  OKV(Java_NativeEngine_aggDestroy(E, K, 0));
+  OKV(Java_NativeEngine_specFree(E, K, 0));
+  end(f0);
+
+  begin("spec_validation");
+  f0 = g_fail;
+  /* a valid C4-shaped plan: keys slot 0, SUM(a + b), COUNT(*), MIN(a), MAX(b) where a > 2^19 */
+  jlong fs = OK(Java_NativeEngine_fusedSpec(E, K, -1, INTS(1), INTS(QE_OP_GT), INTS(-1), INTS(QE_TYPE_INT64), LONGS(1 << 19),
+                                            INTS(0), INTS(3, 0, 1, 1),
+                                            INTS(QE_TOK_COL, QE_TOK_COL, QE_TOK_ADD, QE_TOK_COL, QE_TOK_COL),
+                                            INTS(1, 2, 0, 1, 2), INTS(0, 0, 0, 0, 0), LONGS(0, 0, 0, 0, 0)));
+  CHECK(fs != 0, "valid fused spec");
+  if (fs) CHECK(((qj_spec*)(intptr_t)fs)->ncols_min == 3, "columns read: %d", ((qj_spec*)(intptr_t)fs)->ncols_min);
+  /* nine terms: more than QE_MAX_TERMS */
+  THROWS("java/lang/IllegalArgumentException",
+         Java_NativeEngine_fusedSpec(E, K, -1, INTS(1, 1, 1, 1, 1, 1, 1, 1, 1), NOINTS, NOINTS, NOINTS, NOLONGS, INTS(0),
+                                     NOINTS, NOINTS, NOINTS, NOINTS, NOLONGS));
+  /* term arrays of different lengths */
+  THROWS("java/lang/IllegalArgumentException",
+         Java_NativeEngine_fusedSpec(E, K, -1, INTS(1, 2), INTS(QE_OP_GT), INTS(-1), INTS(1), LONGS(0), INTS(0), NOINTS,
+                                     NOINTS, NOINTS, NOINTS, NOLONGS));
+  /* not a comparison */
+  THROWS("java/lang/IllegalArgumentException",
+         Java_NativeEngine_fusedSpec(E, K, -1, INTS(1), INTS(QE_OP_ADD), INTS(-1), INTS(1), LONGS(0), INTS(0), NOINTS,
+                                     NOINTS, NOINTS, NOINTS, NOLONGS));
+  /* "a +" is not a postfix expression */
+  THROWS("java/lang/IllegalArgumentException",
+         Java_NativeEngine_selectSpec(E, K, -1, NOINTS, NOINTS, NOINTS, NOINTS, NOLONGS, INTS(2), INTS(QE_TOK_COL, QE_TOK_ADD),
+                                      INTS(0, 0), INTS(0, 0), LONGS(0, 0)));
+  /* "a b" leaves two values */
+  THROWS("java/lang/IllegalArgumentException",
+         Java_NativeEngine_selectSpec(E, K, -1, NOINTS, NOINTS, NOINTS, NOINTS, NOLONGS, INTS(2), INTS(QE_TOK_COL, QE_TOK_COL),
+                                      INTS(0, 1), INTS(0, 0), LONGS(0, 0)));
+  /* unknown token, column slot out of range, token count != sum(progLen) */
+  THROWS("java/lang/IllegalArgumentException",
+         Java_NativeEngine_selectSpec(E, K, -1, NOINTS, NOINTS, NOINTS, NOINTS, NOLONGS, INTS(1), INTS(99), INTS(0), INTS(0),
+                                      LONGS(0)));
+  THROWS("java/lang/IllegalArgumentException",
+         Java_NativeEngine_selectSpec(E, K, -1, NOINTS, NOINTS, NOINTS, NOINTS, NOLONGS, INTS(1), INTS(QE_TOK_COL), INTS(8),
+                                      INTS(0), LONGS(0)));
+  THROWS("java/lang/IllegalArgumentException",
+         Java_NativeEngine_selectSpec(E, K, -1, NOINTS, NOINTS, NOINTS, NOINTS, NOLONGS, INTS(2), INTS(QE_TOK_COL), INTS(0),
+                                      INTS(0), LONGS(0)));
+  /* no outputs; an empty output program */
+  THROWS("java/lang/IllegalArgumentException",
+         Java_NativeEngine_selectSpec(E, K, -1, NOINTS, NOINTS, NOINTS, NOINTS, NOLONGS, NOINTS, NOINTS, NOINTS, NOINTS, NOLONGS));
+  THROWS("java/lang/IllegalArgumentException",
+         Java_NativeEngine_selectSpec(E, K, -1, NOINTS, NOINTS, NOINTS, NOINTS, NOLONGS, INTS(0), NOINTS, NOINTS, NOINTS, NOLONGS));
+  /* key slot out of range; mask slot out of range */
+  THROWS("java/lang/IllegalArgumentException",
+         Java_NativeEngine_fusedSpec(E, K, -1, NOINTS, NOINTS, NOINTS, NOINTS, NOLONGS, INTS(9), NOINTS, NOINTS, NOINTS, NOINTS,
+                                     NOLONGS));
+  THROWS("java/lang/IllegalArgumentException",
+         Java_NativeEngine_fusedSpec(E, K, 8, NOINTS, NOINTS, NOINTS, NOINTS, NOLONGS, INTS(0), NOINTS, NOINTS, NOINTS, NOINTS,
+                                     NOLONGS));
+  /* a fused spec where a select spec is expected (the handle tag is checked before the ctx is used) */
+  if (fs) THROWS("java/lang/IllegalArgumentException", Java_NativeEngine_selectAllocateOutputs(E, K, 1, fs, NOLONGS));
+  OKV(Java_NativeEngine_specFree(E, K, fs));
+  end(f0);
+
+  begin("array_limits");
+  f0 = g_fail;
+  /* nine filter inputs (QE_MAX_COLS = 8) are refused before anything touches the device */
+  THROWS("java/lang/IllegalArgumentException",
+         Java_NativeEngine_filter(E, K, 1, 1, LONGS(1, 2, 3, 4, 5, 6, 7, 8, 9)));
+  end(f0);
+}
+
+/* ---- GPU cases ---------------------------------------------------------------------------- */
+
+/* producer-side release callbacks of the harness's static Arrow structs (nothing to free) */
+static void rel_schema(struct ArrowSchema* s) { s->release = NULL; }
+static void rel_array(struct ArrowArray* a) { a->release = NULL; }
+
+static uint64_t splitmix(uint64_t x) {
+  x += 0x9E3779B97F4A7C15ull;
+  x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ull;
+  x = (x ^ (x >> 27)) * 0x94D049BB133111EBull;
+  return x ^ (x >> 31);
+}
+
+enum { NR = 100003, NK = 61 };
+static int64_t hk[NR], ha[NR], hb[NR];
+static uint8_t hbv[(NR + 7) / 8];
+static int b_valid(int i) { return (hbv[i >> 3] >> (i & 7)) & 1; }
+
+typedef struct {
+  int present;
+  int64_t sum, cstar, mina, maxb, cntb;
+} Exp;
+static Exp g_exp[NK];
+
+static void make_data(void) {
+  for (int i = 0; i < NR; ++i) {
+    hk[i] = (int64_t)(splitmix((uint64_t)i) % NK);
+    ha[i] = (int64_t)(splitmix((uint64_t)i ^ 0x1000) % (1u << 20));
+    hb[i] = (int64_t)(splitmix((uint64_t)i ^ 0x2000) % (1u << 20));
+    if (splitmix((uint64_t)i ^ 0x3000) % 13) hbv[i >> 3] |= (uint8_t)(1u << (i & 7));
+  }
+  for (int i = 0; i < NR; ++i) {
+    if (ha[i] <= (1 << 19)) continue;
+    Exp* e = &g_exp[hk[i]];
+    if (!e->present) e->mina = INT64_MAX, e->maxb = INT64_MIN;
+    e->present = 1;
+    e->cstar++;
+    if (ha[i] < e->mina) e->mina = ha[i];
+    if (b_valid(i)) {
+      e->sum += ha[i] + hb[i];
+      e->cntb++;
+      if (hb[i] > e->maxb) e->maxb = hb[i];
+    }
+  }
+}
+
+/* finalize handles [key, SUM(a+b), COUNT(*), MIN(a), MAX(b), COUNT(b)] against g_exp */
+static void check_groups(jlong ctx, jlongArray outs) {
+  if (!outs || outs->len != 6) {
+    fail("finalize returned %d columns", outs ? outs->len : -1);
+    return;
+  }
+  const int64_t* h = LV(outs);
+  uint8_t* v[6];
+  int64_t* c[6];
+  for (int j = 0; j < 6; ++j) c[j] = fetch_longs(ctx, h[j], &v[j]);
+  const jlong g = OK(Java_NativeEngine_columnLength(E, K, h[0]));
+  int want = 0;
+  for (int k = 0; k < NK; ++k) want += g_exp[k].present;
+  CHECK(g == want, "groups %lld, expected %d", (long long)g, want);
+  for (jlong r = 0; r < g; ++r) {
+    const int64_t key = c[0][r];
+    if (!v[0][r] || key < 0 || key >= NK || !g_exp[key].present) {
+      fail("unexpected group key %lld", (long long)key);
+      continue;
+    }
+    const Exp* e = &g_exp[key];
+    CHECK(v[1][r] == (e->cntb > 0) && (!v[1][r] || c[1][r] == e->sum), "key %lld SUM %lld vs %lld", (long long)key,
+          (long long)c[1][r], (long long)e->sum);
+    CHECK(c[2][r] == e->cstar, "key %lld COUNT(*) %lld vs %lld", (long long)key, (long long)c[2][r], (long long)e->cstar);
+    CHECK(v[3][r] && c[3][r] == e->mina, "key %lld MIN(a)", (long long)key);
+    CHECK(v[4][r] == (e->cntb > 0) && (!v[4][r] || c[4][r] == e->maxb), "key %lld MAX(b)", (long long)key);
+    CHECK(c[5][r] == e->cntb, "key %lld COUNT(b) %lld vs %lld", (long long)key, (long long)c[5][r], (long long)e->cntb);
+  }
+  for (int j = 0; j < 6; ++j) OKV(Java_NativeEngine_columnFree(E, K, h[j]));
+}
+
+static jlong c4_fused_spec(void) {
+  return OK(Java_NativeEngine_fusedSpec(
+      E, K, -1, INTS(1), INTS(QE_OP_GT), INTS(-1), INTS(QE_TYPE_INT64), LONGS(1 << 19), INTS(0), INTS(3, 0, 1, 1, 1),
+      INTS(QE_TOK_COL, QE_TOK_COL, QE_TOK_ADD, QE_TOK_COL, QE_TOK_COL, QE_TOK_COL), INTS(1, 2, 0, 1, 2, 2),
+      INTS(0, 0, 0, 0, 0, 0), LONGS(0, 0, 0, 0, 0, 0)));
+}
+static jlong c4_agg(jlong ctx, jint flags) {
+  return OK(Java_NativeEngine_aggCreate(E, K, ctx, INTS(QE_TYPE_INT64),
+                                        INTS(QE_AGG_SUM, QE_AGG_COUNT_STAR, QE_AGG_MIN, QE_AGG_MAX, QE_AGG_COUNT),
+                                        INTS(QE_TYPE_INT64, 0, QE_TYPE_INT64, QE_TYPE_INT64, QE_TYPE_INT64), 0, flags));
+}
+
+static void gpu_cases(void) {
+  int f0;
+  make_data();
+  begin("ctx_create");
+  f0 = g_fail;
+  const jlong ctx = OK(Java_NativeEngine_ctxCreate(E, K, 0));
+  end(f0);
+  if (!ctx) return;
+  jbyteArray bval = JB(hbv, (NR + 7) / 8);
+  const jlong ck = OK(Java_NativeEngine_columnFromLongs(E, K, ctx, QE_TYPE_INT64, JL(hk, NR), NULL));
+  const jlong ca = OK(Java_NativeEngine_columnFromLongs(E, K, ctx, QE_TYPE_INT64, JL(ha, NR), NULL));
+  const jlong cb = OK(Java_NativeEngine_columnFromLongs(E, K, ctx, QE_TYPE_INT64, JL(hb, NR), bval));
+
+  begin("roundtrip_columns");
+  f0 = g_fail;
+  {
+    uint8_t* v;
+    int64_t* b = fetch_longs(ctx, cb, &v);
+    int bad = 0;
+    for (int i = 0; i < NR; ++i) bad += v[i] != b_valid(i) || (v[i] && b[i] != hb[i]);
+    CHECK(!bad, "%d rows differ after upload + download", bad);
+    CHECK(OK(Java_NativeEngine_columnNullable(E, K, cb)) && !OK(Java_NativeEngine_columnNullable(E, K, ca)), "nullability");
+  }
+  end(f0);
+
+  /* SelectionExec -> ProjectionExec -> HashAggregateExec, one operator at a time (K:582-660) */
+  begin("unfused_group_by");
+  f0 = g_fail;
+  {
+    const jlong mask = OK(Java_NativeEngine_evalCmp(E, K, ctx, QE_OP_GT, ca, 0, QE_TYPE_INT64, 1 << 19, 0));
+    CHECK(OK(Java_NativeEngine_filterCount(E, K, ctx, mask)) > 0, "filter count");
+    jlongArray sel = OK(Java_NativeEngine_filter(E, K, ctx, mask, LONGS(ck, ca, cb)));
+    const int64_t* s = LV(sel);
+    const jlong sum = OK(Java_NativeEngine_evalArith(E, K, ctx, QE_OP_ADD, s[1], s[2], 0, 0, 0));
+    const jlong agg = c4_agg(ctx, 0);
+    OKV(Java_NativeEngine_aggUpdate(E, K, agg, LONGS(s[0]), LONGS(sum, 0, s[1], s[2], s[2]), 0));
+    check_groups(ctx, OK(Java_NativeEngine_aggFinalize(E, K, agg)));
+    OKV(Java_NativeEngine_aggDestroy(E, K, agg));
+    for (int i = 0; i < 3; ++i) OKV(Java_NativeEngine_columnFree(E, K, s[i]));
+    OKV(Java_NativeEngine_columnFree(E, K, sum));
+    OKV(Java_NativeEngine_columnFree(E, K, mask));
+  }
+  end(f0);
+
+  begin("fused_group_by");
+  f0 = g_fail;
+  const jlong fs = c4_fused_spec();
+  {
+    const jlong agg = c4_agg(ctx, 0);
+    OKV(Java_NativeEngine_aggUpdateFused(E, K, agg, LONGS(ck, ca, cb), fs));
+    CHECK(OK(Java_NativeEngine_aggLastKernelMs(E, K, agg)) > 0.0, "kernel time");
+    check_groups(ctx, OK(Java_NativeEngine_aggFinalize(E, K, agg)));
+    THROWS("java/lang/IllegalArgumentException", Java_NativeEngine_aggUpdateFused(E, K, agg, LONGS(ck, ca), fs));
+    OKV(Java_NativeEngine_aggDestroy(E, K, agg));
+  }
+  end(f0);
+
+  /* main(): partials per partition, merged into one state (K:1309-1325) */
+  begin("two_phase_merge");
+  f0 = g_fail;
+  {
+    const int h = NR / 3;
+    jlong p[2], parts[2][3];
+    for (int q = 0; q < 2; ++q) {
+      const int lo = q ? h : 0, n = q ? NR - h : h;
+      uint8_t* bits = (uint8_t*)calloc((size_t)(n + 7) / 8, 1);
+      for (int i = 0; i < n; ++i)
+        if (b_valid(lo + i)) bits[i >> 3] |= (uint8_t)(1u << (i & 7));
+      parts[q][0] = OK(Java_NativeEngine_columnFromLongs(E, K, ctx, QE_TYPE_INT64, JL(hk + lo, n), NULL));
+      parts[q][1] = OK(Java_NativeEngine_columnFromLongs(E, K, ctx, QE_TYPE_INT64, JL(ha + lo, n), NULL));
+      parts[q][2] = OK(Java_NativeEngine_columnFromLongs(E, K, ctx, QE_TYPE_INT64, JL(hb + lo, n), JB(bits, (n + 7) / 8)));
+      free(bits);
+      p[q] = c4_agg(ctx, 0);
+      OKV(Java_NativeEngine_aggSetAsync(E, K, p[q], 1));
+      OKV(Java_NativeEngine_aggSetRowBase(E, K, p[q], lo));
+      OKV(Java_NativeEngine_aggUpdateFused(E, K, p[q], LONGS(parts[q][0], parts[q][1], parts[q][2]), fs));
+    }
+    const jlong owner = c4_agg(ctx, 0);
+    OKV(Java_NativeEngine_aggMergeInto(E, K, owner, p[1]));
+    OKV(Java_NativeEngine_aggMergeInto(E, K, owner, p[0]));
+    check_groups(ctx, OK(Java_NativeEngine_aggFinalize(E, K, owner)));
+    OKV(Java_NativeEngine_aggDestroy(E, K, owner));
+    for (int q = 0; q < 2; ++q) {
+      OKV(Java_NativeEngine_aggDestroy(E, K, p[q]));
+      for (int i = 0; i < 3; ++i) OKV(Java_NativeEngine_columnFree(E, K, parts[q][i]));
+    }
+  }
+  end(f0);
+
+  /* fp64 SUM / AVG with QE_HASHAGG_DETERMINISTIC: bit-identical whatever the batch split, and the
+   * exact sum rounded once (the values are multiples of 2^-42, so the exact sum is an integer of
+   * 2^-42 units) */
+  begin("deterministic_fp64_sums");
+  f0 = g_fail;
+  {
+    double* v = (double*)malloc(sizeof(double) * NR);
+    __int128 exact[NK] = {0};
+    int64_t cnt[NK] = {0};
+    for (int i = 0; i < NR; ++i) {
+      const int64_t u = (int64_t)(splitmix((uint64_t)i ^ 0x4000) >> 11);
+      v[i] = ldexp((double)u, -42) - 1024.0;
+      exact[hk[i]] += (__int128)u - ((__int128)1024 << 42);
+      cnt[hk[i]]++;
+    }
+    double got[2][NK];
+    for (int split = 0; split < 2; ++split) {
+      const jlong agg = OK(Java_NativeEngine_aggCreate(E, K, ctx, INTS(QE_TYPE_INT64), INTS(QE_AGG_SUM, QE_AGG_AVG),
+                                                       INTS(QE_TYPE_FLOAT64, QE_TYPE_FLOAT64), 0, QE_HASHAGG_DETERMINISTIC));
+      const int cut = split ? 7919 : NR;
+      for (int lo = 0; lo < NR; lo += cut) {
+        const int n = lo + cut > NR ? NR - lo : cut;
+        const jlong kc = OK(Java_NativeEngine_columnFromLongs(E, K, ctx, QE_TYPE_INT64, JL(hk + lo, n), NULL));
+        const jlong vc = OK(Java_NativeEngine_columnFromDoubles(E, K, ctx, JD(v + lo, n), NULL));
+        OKV(Java_NativeEngine_aggUpdate(E, K, agg, LONGS(kc), LONGS(vc, vc), 0));
+        OKV(Java_NativeEngine_columnFree(E, K, kc));
+        OKV(Java_NativeEngine_columnFree(E, K, vc));
+      }
+      jlongArray outs = OK(Java_NativeEngine_aggFinalize(E, K, agg));
+      if (!outs) break;
+      uint8_t *vk, *vs, *va;
+      int64_t* keys = fetch_longs(ctx, LV(outs)[0], &vk);
+      double* sums = fetch_doubles(ctx, LV(outs)[1], &vs);
+      double* avgs = fetch_doubles(ctx, LV(outs)[2], &va);
+      const jlong g = OK(Java_NativeEngine_columnLength(E, K, LV(outs)[0]));
+      CHECK(g == NK, "groups %lld", (long long)g);
+      for (jlong r = 0; r < g; ++r) {
+        const int64_t key = keys[r];
+        if (key < 0 || key >= NK) {
+          fail("key %lld", (long long)key);
+          continue;
+        }
+        const double want = ldexp((double)exact[key], -42);
+        got[split][key] = sums[r];
+        CHECK(sums[r] == want, "key %lld sum %.17g, exact-rounded %.17g", (long long)key, sums[r], want);
+        CHECK(fabs(avgs[r] - want / (double)cnt[key]) <= 1e-15 * fabs(want / (double)cnt[key]), "key %lld avg", (long long)key);
+      }
+      for (int j = 0; j < 3; ++j) OKV(Java_NativeEngine_columnFree(E, K, LV(outs)[j]));
+      OKV(Java_NativeEngine_aggDestroy(E, K, agg));
+    }
+    CHECK(!memcmp(got[0], got[1], sizeof got[0]), "sums differ between batch splits");
+    /* an unrepresentable input (|x| >= 2^63) fails the update loudly */
+    const jlong agg = OK(Java_NativeEngine_aggCreate(E, K, ctx, INTS(QE_TYPE_INT64), INTS(QE_AGG_SUM), INTS(QE_TYPE_FLOAT64), 0,
+                                                     QE_HASHAGG_DETERMINISTIC));
+    const jlong kc = OK(Java_NativeEngine_columnFromLongs(E, K, ctx, QE_TYPE_INT64, LONGS(1, 2), NULL));
+    const jlong vc = OK(Java_NativeEngine_columnFromDoubles(E, K, ctx, JD((const double[]){1.0, 1e30}, 2), NULL));
+    THROWS("java/lang/IllegalStateException", {
+      Java_NativeEngine_aggUpdate(E, K, agg, LONGS(kc), LONGS(vc), 0);
+      if (!g_pending) Java_NativeEngine_aggNumGroups(E, K, agg);
+    });
+    OKV(Java_NativeEngine_aggDestroy(E, K, agg));
+    OKV(Java_NativeEngine_columnFree(E, K, kc));
+    OKV(Java_NativeEngine_columnFree(E, K, vc));
+    free(v);
+  }
+  end(f0);
+
+  /* Projection(Selection(Scan)) as one pipelined select-project per batch (K:582-603) */
+  begin("select_project_pipelined");
+  f0 = g_fail;
+  {
+    const jlong ss = OK(Java_NativeEngine_selectSpec(E, K, -1, INTS(1), INTS(QE_OP_GT), INTS(-1), INTS(QE_TYPE_INT64),
+                                                     LONGS(1 << 19), INTS(3, 1), INTS(QE_TOK_COL, QE_TOK_COL, QE_TOK_ADD, QE_TOK_COL),
+                                                     INTS(1, 2, 0, 0), INTS(0, 0, 0, 0), LONGS(0, 0, 0, 0)));
+    jlongArray cols = LONGS(ck, ca, cb);
+    jlongArray o1 = OK(Java_NativeEngine_selectAllocateOutputs(E, K, ctx, ss, cols));
+    jlongArray o2 = OK(Java_NativeEngine_selectAllocateOutputs(E, K, ctx, ss, cols));
+    /* two batches in flight: the second is queued before the first's count is read */
+    const jlong p1 = OK(Java_NativeEngine_selectProjectAsync(E, K, ctx, cols, ss, o1));
+    const jlong p2 = OK(Java_NativeEngine_selectProjectAsync(E, K, ctx, cols, ss, o2));
+    const jlong r1 = OK(Java_NativeEngine_selectProjectWait(E, K, p1, o1));
+    const jlong r2 = OK(Java_NativeEngine_selectProjectWait(E, K, p2, o2));
+    int64_t want = 0;
+    for (int i = 0; i < NR; ++i) want += ha[i] > (1 << 19);
+    CHECK(r1 == want && r2 == want, "rows %lld / %lld, expected %lld", (long long)r1, (long long)r2, (long long)want);
+    if (o1 && o2) {
+      uint8_t *v0, *v1;
+      int64_t* s0 = fetch_longs(ctx, LV(o2)[0], &v0);
+      int64_t* s1 = fetch_longs(ctx, LV(o2)[1], &v1);
+      int64_t j = 0, bad = 0;
+      for (int i = 0; i < NR; ++i) {
+        if (ha[i] <= (1 << 19)) continue;
+        bad += v0[j] != b_valid(i) || (v0[j] && s0[j] != ha[i] + hb[i]) || !v1[j] || s1[j] != hk[i];
+        ++j;
+      }
+      CHECK(!bad, "%lld output rows differ (order-preserving compaction)", (long long)bad);
+      for (int k = 0; k < 2; ++k) {
+        OKV(Java_NativeEngine_columnFree(E, K, LV(o1)[k]));
+        OKV(Java_NativeEngine_columnFree(E, K, LV(o2)[k]));
+      }
+    }
+    OKV(Java_NativeEngine_specFree(E, K, ss));
+  }
+  end(f0);
+
+  /* CastExpression (K:772-805): Double.parseDouble grammar; a bad string -> NumberFormatException */
+  begin("cast_to_double");
+  f0 = g_fail;
+  {
+    const char* s[] = {"1.5", " -2e3 ", "NaN", NULL, "0x1p4", "7d"};
+    const jlong c = utf8_col(ctx, s, 6);
+    const jlong d = OK(Java_NativeEngine_castToDouble(E, K, ctx, c));
+    uint8_t* v;
+    double* x = d ? fetch_doubles(ctx, d, &v) : NULL;
+    if (x)
+      CHECK(x[0] == 1.5 && x[1] == -2000.0 && isnan(x[2]) && !v[3] && v[0] && x[4] == 16.0 && x[5] == 7.0,
+            "cast values %g %g %g %d %g %g", x[0], x[1], x[2], v[3], x[4], x[5]);
+    const char* bad[] = {"1.0", "abc"};
+    const jlong cb2 = utf8_col(ctx, bad, 2);
+    THROWS("java/lang/NumberFormatException", Java_NativeEngine_castToDouble(E, K, ctx, cb2));
+    OKV(Java_NativeEngine_columnFree(E, K, c));
+    OKV(Java_NativeEngine_columnFree(E, K, d));
+    OKV(Java_NativeEngine_columnFree(E, K, cb2));
+  }
+  end(f0);
+
+  begin("global_aggregate");
+  f0 = g_fail;
+  {
+    jlongArray r = OK(Java_NativeEngine_aggGlobal(E, K, ctx, ca, 0));
+    int64_t sum = 0, mn = INT64_MAX, mx = INT64_MIN;
+    for (int i = 0; i < NR; ++i) {
+      sum += ha[i];
+      mn = ha[i] < mn ? ha[i] : mn;
+      mx = ha[i] > mx ? ha[i] : mx;
+    }
+    if (r) CHECK(LV(r)[0] == NR && LV(r)[1] == NR && LV(r)[3] == 1 && LV(r)[4] == sum && LV(r)[5] == mn && LV(r)[6] == mx,
+                 "global aggregate");
+    jlongArray rb = OK(Java_NativeEngine_aggGlobal(E, K, ctx, cb, 0));
+    int64_t nb = 0;
+    for (int i = 0; i < NR; ++i) nb += b_valid(i);
+    if (rb) CHECK(LV(rb)[0] == NR && LV(rb)[1] == nb, "COUNT(b) skips nulls");
+  }
+  end(f0);
+
+  /* RecordBatch in / out over the Arrow C Data Interface (what Arrow Java exports / imports) */
+  begin("arrow_c_data");
+  f0 = g_fail;
+  {
+    static int64_t xv[5] = {10, 20, 30, 40, 50};
+    static double yv[5] = {0.5, -1.5, 2.25, 1e300, -0.0};
+    static uint8_t xbits[1] = {0x1B}; /* row 2 null */
+    static const void* xb[2] = {xbits, xv};
+    static const void* yb[2] = {NULL, yv};
+    static const void* sb[1] = {NULL};
+    struct ArrowSchema sx = {"l", "x", NULL, ARROW_FLAG_NULLABLE, 0, NULL, NULL, rel_schema, NULL};
+    struct ArrowSchema sy = {"g", "y", NULL, ARROW_FLAG_NULLABLE, 0, NULL, NULL, rel_schema, NULL};
+    struct ArrowSchema* sch[2] = {&sx, &sy};
+    struct ArrowSchema ss = {"+s", "", NULL, 0, 2, sch, NULL, rel_schema, NULL};
+    struct ArrowArray ax = {5, 1, 0, 2, 0, xb, NULL, NULL, rel_array, NULL};
+    struct ArrowArray ay = {5, 0, 0, 2, 0, yb, NULL, NULL, rel_array, NULL};
+    struct ArrowArray* arr[2] = {&ax, &ay};
+    struct ArrowArray as = {5, 0, 0, 1, 2, sb, arr, NULL, rel_array, NULL};
+    const jlong b = OK(Java_NativeEngine_importBatch(E, K, ctx, (jlong)(intptr_t)&ss, (jlong)(intptr_t)&as));
+    if (b) {
+      CHECK(OK(Java_NativeEngine_batchNumColumns(E, K, b)) == 2, "columns");
+      jstring nm = OK(Java_NativeEngine_batchColumnName(E, K, b, 1));
+      CHECK(nm && !strcmp((const char*)nm->data, "y"), "column name");
+      const jlong x = OK(Java_NativeEngine_batchColumn(E, K, b, 0));
+      const jlong y = OK(Java_NativeEngine_batchColumn(E, K, b, 1));
+      jlongArray g = OK(Java_NativeEngine_aggGlobal(E, K, ctx, x, 0));
+      if (g) CHECK(LV(g)[1] == 4 && LV(g)[4] == 120, "SUM(x) over the imported batch");
+      struct ArrowSchema os;
+      struct ArrowArray oa;
+      memset(&os, 0, sizeof os);
+      memset(&oa, 0, sizeof oa);
+      jobject names[2] = {f_NewStringUTF(E, "x2"), f_NewStringUTF(E, "y2")};
+      OKV(Java_NativeEngine_exportColumns(E, K, ctx, LONGS(x, y), JO(names, 2), (jlong)(intptr_t)&os, (jlong)(intptr_t)&oa));
+      if (oa.release) {
+        CHECK(oa.length == 5 && oa.n_children == 2 && !strcmp(os.children[0]->name, "x2"), "exported shape");
+        const int64_t* ox = (const int64_t*)oa.children[0]->buffers[1];
+        const uint8_t* ov = (const uint8_t*)oa.children[0]->buffers[0];
+        const double* oy = (const double*)oa.children[1]->buffers[1];
+        CHECK(ox[0] == 10 && ox[4] == 50 && ov && !((ov[0] >> 2) & 1) && (ov[0] & 1), "exported int64 child");
+        CHECK(!memcmp(oy, yv, sizeof yv), "exported fp64 child (bits)");
+        oa.release(&oa);
+        os.release(&os);
+      } else {
+        fail("nothing exported");
+      }
+      OKV(Java_NativeEngine_columnFree(E, K, x));
+      OKV(Java_NativeEngine_columnFree(E, K, y));
+      OKV(Java_NativeEngine_batchDestroy(E, K, b));
+    }
+    /* an unsupported Arrow format is the IllegalStateException of K:195 */
+    struct ArrowSchema sh = {"e", "h", NULL, ARROW_FLAG_NULLABLE, 0, NULL, NULL, rel_schema, NULL};
+    struct ArrowSchema* sch2[1] = {&sh};
+    struct ArrowSchema ss2 = {"+s", "", NULL, 0, 1, sch2, NULL, rel_schema, NULL};
+    struct ArrowArray* arr2[1] = {&ax};
+    struct ArrowArray as2 = {5, 0, 0, 1, 1, sb, arr2, NULL, rel_array, NULL};
+    THROWS("java/lang/IllegalStateException",
+           Java_NativeEngine_importBatch(E, K, ctx, (jlong)(intptr_t)&ss2, (jlong)(intptr_t)&as2));
+  }
+  end(f0);
+
+  /* GROUP BY a Utf8 key (K:620-627): string dictionary codes, decoded at finalize */
+  begin("utf8_group_keys");
+  f0 = g_fail;
+  {
+    const char* s[] = {"CA", "NY", "CA", "TX", "NY", "CA", NULL};
+    const jlong c = utf8_col(ctx, s, 7);
+    const jlong d = OK(Java_NativeEngine_dictCreate(E, K, ctx, 0));
+    const jlong codes = OK(Java_NativeEngine_dictEncode(E, K, ctx, d, c));
+    const jlong agg = OK(Java_NativeEngine_aggCreate(E, K, ctx, INTS(QE_TYPE_INT32), INTS(QE_AGG_COUNT_STAR), INTS(0), 0, 0));
+    OKV(Java_NativeEngine_aggUpdate(E, K, agg, LONGS(codes), LONGS(0), 0));
+    jlongArray outs = OK(Java_NativeEngine_aggFinalize(E, K, agg));
+    if (outs) {
+      const jlong keys = OK(Java_NativeEngine_dictDecode(E, K, ctx, d, LV(outs)[0]));
+      jlong n = 0;
+      char** ks = fetch_strings(ctx, keys, &n);
+      uint8_t* v;
+      int64_t* cnt = fetch_longs(ctx, LV(outs)[1], &v);
+      int seen = 0;
+      for (jlong r = 0; r < n; ++r) {
+        const int64_t want = !ks[r] ? 1 : !strcmp(ks[r], "CA") ? 3 : !strcmp(ks[r], "NY") ? 2 : !strcmp(ks[r], "TX") ? 1 : -1;
+        CHECK(cnt[r] == want, "group %s: %lld", ks[r] ? ks[r] : "null", (long long)cnt[r]);
+        ++seen;
+      }
+      CHECK(seen == 4, "%d groups (CA, NY, TX, null)", seen);
+      OKV(Java_NativeEngine_columnFree(E, K, keys));
+      OKV(Java_NativeEngine_columnFree(E, K, LV(outs)[0]));
+      OKV(Java_NativeEngine_columnFree(E, K, LV(outs)[1]));
+    }
+    OKV(Java_NativeEngine_aggDestroy(E, K, agg));
+    OKV(Java_NativeEngine_columnFree(E, K, codes));
+    OKV(Java_NativeEngine_dictDestroy(E, K, d));
+    OKV(Java_NativeEngine_columnFree(E, K, c));
+  }
+  end(f0);
+
+  /* CsvDataSource.scan on the device (K:276-357), the file handed over as a direct ByteBuffer */
+  begin("csv_scan");
+  f0 = g_fail;
+  {
+    const char* text = "state,name\nCA, Ann\n# comment\nNY,\"B, \"\"Bo\"\"\"\n";
+    jobject buf = obj_new(K_BUF, (jsize)strlen(text), 1);
+    memcpy(buf->data, text, strlen(text));
+    const jlong t = OK(Java_NativeEngine_csvParse(E, K, ctx, buf, (jlong)strlen(text), ',', 1, INTS(1, 0)));
+    if (t) {
+      CHECK(OK(Java_NativeEngine_csvRows(E, K, t)) == 2, "rows");
+      const jlong c0 = OK(Java_NativeEngine_csvColumn(E, K, t, 0));
+      jlong n = 0;
+      char** s = fetch_strings(ctx, c0, &n);
+      CHECK(n == 2 && s[0] && s[1] && !strcmp(s[0], "Ann") && !strcmp(s[1], "B, \"Bo\""), "name column: [%s] [%s]",
+            n > 0 && s[0] ? s[0] : "?", n > 1 && s[1] ? s[1] : "?");
+      OKV(Java_NativeEngine_columnFree(E, K, c0));
+      OKV(Java_NativeEngine_csvDestroy(E, K, t));
+    }
+  }
+  end(f0);
+
+  /* the exceptions the reference throws for bad arguments */
+  begin("exception_mapping");
+  f0 = g_fail;
+  THROWS("java/lang/IllegalArgumentException", Java_NativeEngine_evalArith(E, K, ctx, 99, ca, 0, QE_TYPE_INT64, 1, 0));
+  {
+    const jlong agg = c4_agg(ctx, 0);
+    THROWS("java/lang/IllegalArgumentException",
+           Java_NativeEngine_aggUpdate(E, K, agg, LONGS(ck, ck), LONGS(ca, 0, ca, cb, cb), 0));
+    OKV(Java_NativeEngine_aggDestroy(E, K, agg));
+  }
+  THROWS("java/lang/IllegalArgumentException",
+         Java_NativeEngine_columnFromUtf8(E, K, ctx, INTS(0, 5), JB((const uint8_t*)"abc", 3), NULL));
+  end(f0);
+
+  OKV(Java_NativeEngine_specFree(E, K, fs));
+  OKV(Java_NativeEngine_columnFree(E, K, ck));
+  OKV(Java_NativeEngine_columnFree(E, K, ca));
+  OKV(Java_NativeEngine_columnFree(E, K, cb));
+  OKV(Java_NativeEngine_ctxDestroy(E, K, ctx));
+}
+
+int main(int argc, char** argv) {
+  const char* mode = argc > 1 ? argv[1] : "cpu";
+  if (!strcmp(mode, "gpu"))
+    gpu_cases();
+  else
+    cpu_cases();
+  printf("%s: %d failure(s)\n", g_fail ? "FAILED" : "ALL OK", g_fail);
+  return g_fail ? 1 : 0;
+}
