@@ -1180,6 +1180,22 @@ int selproj_rows(const Plan& P, int mode) {
   return (!forced && selproj_pipelined() && (mode == SP_PERSIST || mode == SP_COUNTER)) ? std::min(r, 8) : r;
 }
 
+// Persistent look-back tiles that load the next tile while this one's look-back and stores run
+// (QE_SELPROJ_PREFETCH, default on; 0 = off): only with staged outputs (all 8 bytes wide, so the
+// column registers are dead once the rows sit in LDS) and no nullable output (whose validity bits
+// are written from the column registers after the look-back).
+bool selproj_prefetch_ok(const Plan& P, const int32_t* out_kind, int nout, int mode) {
+  static const bool on = [] {
+    const char* e = getenv("QE_SELPROJ_PREFETCH");
+    return !(e && e[0] == '0');
+  }();
+  if (!on || mode != SP_PERSIST || selproj_pipelined()) return false;
+  if ((size_t)nout * selproj_rows(P, mode) * selproj_block(mode) * 8 > kSelprojStageBytes) return false;
+  for (int k = 0; k < nout; ++k)
+    if ((out_kind[k] & 0xFF) != 8 || (out_kind[k] & 0x100)) return false;
+  return true;
+}
+
 // Row of (thread, r) inside a select-project tile. Stripe map (default): stripe r is BT consecutive
 // rows, thread t row t of it. Wave map (QE_SELPROJ_MAP=wave): each wave owns R x 64 consecutive
 // rows, lane l row 64 r + l of them, so a thread's R loads of a column share one base address
@@ -1222,13 +1238,20 @@ void emit_selproj_loads(const Plan& P, std::ostringstream& o, unsigned need, boo
     const char* ty = kind == K_I32 ? "qi32" : (kind == K_U8 || kind == K_BOOL) ? "qu8" : "qi64";
     o << ind << "{\n" << ind << "  const qi64 lb = " << b << ";\n" << ind << "  const bool lfull = lb + R * BT <= P.n;\n"
       << ind << "  const " << ty << "* p = (const " << ty << "*)P.cols[" << cs << "].p;\n"
-      << "#pragma unroll\n" << ind << "  for (int r = 0; r < R; ++r) {\n" << ind << "    const qi64 row = " << sp_row("lb") << ";\n";
+      << ind << "  if (lfull) {\n"  // whole tile: R loads back to back, no per-row exec branches
+      << "#pragma unroll\n" << ind << "    for (int r = 0; r < R; ++r) {\n" << ind << "      const qi64 row = " << sp_row("lb") << ";\n";
     if (kind == K_BOOL)
-      o << ind << "    " << cp << cs << "[r] = (lfull || row < P.n) ? ((p[row >> 3] >> (row & 7)) & 1) : 0;\n";
+      o << ind << "      " << cp << cs << "[r] = (p[row >> 3] >> (row & 7)) & 1;\n";
     else
       // default policy below 64M rows: C2-sized inputs stay in the MALL (nt 68.4 us, default 65.0 us)
-      o << ind << "    " << cp << cs << "[r] = (lfull || row < P.n) ? (qi64)" << ld(ty, "p + row", nt) << " : 0;\n";
-    o << ind << "  }\n";
+      o << ind << "      " << cp << cs << "[r] = (qi64)" << ld(ty, "p + row", nt) << ";\n";
+    o << ind << "    }\n" << ind << "  } else {\n"
+      << "#pragma unroll\n" << ind << "    for (int r = 0; r < R; ++r) {\n" << ind << "      const qi64 row = " << sp_row("lb") << ";\n";
+    if (kind == K_BOOL)
+      o << ind << "      " << cp << cs << "[r] = row < P.n ? ((p[row >> 3] >> (row & 7)) & 1) : 0;\n";
+    else
+      o << ind << "      " << cp << cs << "[r] = row < P.n ? (qi64)" << ld(ty, "p + row", nt) << " : 0;\n";
+    o << ind << "    }\n" << ind << "  }\n";
     if (P.cols[c].valid) {
       o << ind << "  const qu8* vb = P.cols[" << cs << "].valid;\n" << ind << "  " << vp << cs << " = 0;\n"
         << "#pragma unroll\n" << ind << "  for (int r = 0; r < R; ++r) {\n" << ind << "    const qi64 row = " << sp_row("lb") << ";\n"
@@ -1244,7 +1267,7 @@ void emit_selproj_loads(const Plan& P, std::ostringstream& o, unsigned need, boo
 // per-(stripe, wave) counts, one wave's scan, the tile's output base (decoupled look-back or the
 // two-pass prefix), then the compacted stores.
 bool emit_selproj_write(const Plan& P, const int32_t* out_kind, int nout, int mode, std::ostringstream& o,
-                        bool regs = false) {
+                        bool regs = false, const std::string& prefetch = std::string()) {
   const int R = selproj_rows(P, mode);
   // Staged output (all outputs 8 bytes wide, R x BT x 8 B each within 64 KiB of LDS): selected
   // rows land compacted in LDS, then the tile's output range is written with 16-byte stores, all
@@ -1329,9 +1352,16 @@ bool emit_selproj_write(const Plan& P, const int32_t* out_kind, int nout, int mo
       << "    if (!((act >> r) & 1u)) continue;\n"
       << "    const qu32 lp = s_cnt[" << sp_cnt_idx() << "] + (qu32)__popcll(bal[r] & below);\n";
     for (int k = 0; k < nout; ++k) o << "    s_out[" << k << " * (R * BT) + lp] = " << ex[k].v << ";\n";
-    o << "  }\n"
-      << "  if (w == 0) {\n" << lookback << "  }\n"
-      << "  __syncthreads();\n"
+    o << "  }\n";
+    if (!prefetch.empty())
+      // the tile's rows are in LDS, so its column registers are free: the next tile's loads go
+      // out now and are in flight during the look-back and the stores (wave 0 issues its share
+      // after the look-back, so its in-order load counter never holds the status reads back)
+      o << "  asm volatile(\"\" ::: \"memory\");\n"
+        << "  if (w != 0) {\n" << prefetch << "  } else {\n" << lookback << prefetch << "  }\n";
+    else
+      o << "  if (w == 0) {\n" << lookback << "  }\n";
+    o << "  __syncthreads();\n"
       << "  {\n    const qu64 tb = s_base;\n    const qu32 tot = s_total;\n";
     for (int k = 0; k < nout; ++k) {
       const std::string ks = std::to_string(k);
@@ -1431,10 +1461,35 @@ bool gen_selproj_source(const Plan& P, const int32_t* out_kind, int nout, std::s
     *src = std::string(kDevHeader) + o.str();
     return true;
   }
+  if (persistent && selproj_prefetch_ok(P, out_kind, nout, mode)) {
+    // Persistent grid, next tile's columns loaded into the (then free) column registers once this
+    // tile's rows are staged in LDS (emit_selproj_write): with one 1024-thread workgroup per CU
+    // nothing else on the CU would keep HBM busy during the look-back and the stores.
+    for (int c = 0; c < P.ncols; ++c) {
+      o << "  qi64 c" << c << "[R];\n";
+      if (P.cols[c].valid) o << "  qu32 v" << c << " = 0;\n";
+    }
+    o << "  qu32 tile = blockIdx.x;\n  if ((qu64)tile < P.t.cap) {\n    const qi64 base0 = (qi64)tile * (R * BT);\n";
+    emit_loads("c", "v", "base0", "    ");
+    o << "  }\n  while ((qu64)tile < P.t.cap) {\n"
+      << "  const qu32 next = tile + gridDim.x;\n"
+      << "  const qi64 base = (qi64)tile * (R * BT);\n"
+      << "  const bool full = base + R * BT <= P.n;\n";
+    emit_selproj_act(P, o);
+    std::ostringstream pf;
+    pf << "    if ((qu64)next < P.t.cap) {\n      const qi64 nbase = (qi64)next * (R * BT);\n";
+    emit_selproj_loads(P, pf, need, selproj_nt(P), "c", "v", "nbase", "      ");
+    pf << "    }\n";
+    if (!emit_selproj_write(P, out_kind, nout, mode, o, false, pf.str())) return false;
+    o << "  __syncthreads();\n  tile = next;\n  }\n}\n";
+    *src = std::string(kDevHeader) + o.str();
+    return true;
+  }
   if (persistent) {
     // Every workgroup is resident (grid <= CUs x occupancy), so a static tile order cannot
     // deadlock the look-back and no tile counter is needed. (Prefetching the next tile's columns
-    // into registers during this tile's look-back measured slower: 5.00 vs 4.67 ms at 1B rows.)
+    // into registers during this tile's look-back measured slower with 256-thread workgroups,
+    // 4 per CU: 5.00 vs 4.67 ms at 1B rows; see selproj_prefetch_ok for 1024-thread ones.)
     o << "  for (qu32 tile = blockIdx.x; (qu64)tile < P.t.cap; tile += gridDim.x) {\n"
       << "  const qi64 base = (qi64)tile * (R * BT);\n"
       << "  const bool full = base + R * BT <= P.n;\n";
