@@ -184,8 +184,8 @@ def launch_ranks(args) -> int:
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--rows", type=lambda v: int(float(v)), default=1_000_000_000, help="rows per GPU (1e9 ok)")
     ap.add_argument("--cpu-sample-rows", type=int, default=0, help="default: the same rows as one GPU")
     ap.add_argument("--cpu-threads", type=int, default=0)
