@@ -6,7 +6,7 @@
  * exit status 0 iff all cases pass.
  *
  *   jni_harness cpu   argument checking and exception mapping (no GPU needed)
- *   jni_harness gpu   end to end on device 0: the reference's operator chain (K:582-660) through
+ *   jni_harness gpu [employee.csv]  end to end on device 0: the reference's operator chain (K:582-660) through
  *                     the shim — unfused and fused GROUP BY, two-phase merge, deterministic fp64
  *                     sums, pipelined select-project, CAST, global aggregate, Arrow C Data in /
  *                     out, Utf8 keys, CSV scan, and the exceptions K: throws.
@@ -178,6 +178,7 @@ static jobjectArray JO(jobject* v, jsize n) {
 /* ---- checking ----------------------------------------------------------------------------- */
 
 static int g_fail;
+static const char* g_employee; /* gpu mode: path of the reference's employee.csv fixture */
 static const char* g_case = "";
 
 static void fail(const char* fmt, ...) __attribute__((format(printf, 1, 2)));
@@ -808,6 +809,78 @@ static void gpu_cases(void) {
   }
   end(f0);
 
+  /* the reference's own fixture and query shape (kquerydiy employee.csv, K:1336): scan on the
+   * device, CAST(salary AS double), GROUP BY state MAX, and the filters state = 'CA' / 'Uppsala';
+   * expected values are the reference-held answers in tests/golden/employee_kat.json */
+  if (g_employee) {
+    begin("employee_reference_query");
+    f0 = g_fail;
+    FILE* fp = fopen(g_employee, "rb");
+    char text[4096];
+    const size_t nb = fp ? fread(text, 1, sizeof text, fp) : 0;
+    if (fp) fclose(fp);
+    CHECK(nb > 0, "cannot read %s", g_employee);
+    jobject buf = obj_new(K_BUF, (jsize)nb, 1);
+    memcpy(buf->data, text, nb);
+    /* header: id,first_name,last_name,state,job_title,salary -> project id (0), state (3), salary (5) */
+    const jlong t = nb ? OK(Java_NativeEngine_csvParse(E, K, ctx, buf, (jlong)nb, ',', 1, INTS(0, 3, 5))) : 0;
+    if (t) {
+      CHECK(OK(Java_NativeEngine_csvRows(E, K, t)) == 3, "rows");
+      const jlong id = OK(Java_NativeEngine_csvColumn(E, K, t, 0));
+      const jlong state = OK(Java_NativeEngine_csvColumn(E, K, t, 1));
+      const jlong salary = OK(Java_NativeEngine_csvColumn(E, K, t, 2));
+      const jlong sal = OK(Java_NativeEngine_castToDouble(E, K, ctx, salary));
+      const jlong d = OK(Java_NativeEngine_dictCreate(E, K, ctx, 0));
+      const jlong codes = OK(Java_NativeEngine_dictEncode(E, K, ctx, d, state));
+      const jlong agg = OK(Java_NativeEngine_aggCreate(E, K, ctx, INTS(QE_TYPE_INT32), INTS(QE_AGG_MAX), INTS(QE_TYPE_FLOAT64), 0, 0));
+      OKV(Java_NativeEngine_aggUpdate(E, K, agg, LONGS(codes), LONGS(sal), 0));
+      jlongArray outs = OK(Java_NativeEngine_aggFinalize(E, K, agg));
+      if (outs) {
+        const jlong keys = OK(Java_NativeEngine_dictDecode(E, K, ctx, d, LV(outs)[0]));
+        jlong n = 0;
+        char** ks = fetch_strings(ctx, keys, &n);
+        uint8_t* v;
+        double* mx = fetch_doubles(ctx, LV(outs)[1], &v);
+        int seen = 0;
+        for (jlong r = 0; r < n; ++r) {
+          if (ks[r] && !strcmp(ks[r], "Uppsala")) {
+            ++seen;
+            CHECK(v[r] && mx[r] == 1337.0, "MAX(salary) Uppsala %g", mx[r]);
+          } else if (ks[r] && !strcmp(ks[r], "Sthlm")) {
+            ++seen;
+            CHECK(v[r] && mx[r] == 0.0, "MAX(salary) Sthlm %g", mx[r]);
+          } else {
+            fail("unexpected group %s", ks[r] ? ks[r] : "null");
+          }
+        }
+        CHECK(seen == 2 && n == 2, "groups %lld", (long long)n);
+        OKV(Java_NativeEngine_columnFree(E, K, keys));
+        OKV(Java_NativeEngine_columnFree(E, K, LV(outs)[0]));
+        OKV(Java_NativeEngine_columnFree(E, K, LV(outs)[1]));
+      }
+      /* WHERE state = 'CA' -> no rows; WHERE state = 'Uppsala' -> ids 1, 2 */
+      const char* ca[] = {"CA"};
+      const char* up[] = {"Uppsala"};
+      const jlong lca = utf8_col(ctx, ca, 1), lup = utf8_col(ctx, up, 1);
+      const jlong mca = OK(Java_NativeEngine_evalCmp(E, K, ctx, QE_OP_EQ, state, lca, 0, 0, 0));
+      const jlong mup = OK(Java_NativeEngine_evalCmp(E, K, ctx, QE_OP_EQ, state, lup, 0, 0, 0));
+      CHECK(OK(Java_NativeEngine_filterCount(E, K, ctx, mca)) == 0, "state = 'CA' selects rows");
+      jlongArray sel = OK(Java_NativeEngine_filter(E, K, ctx, mup, LONGS(id)));
+      if (sel) {
+        jlong n = 0;
+        char** ids = fetch_strings(ctx, LV(sel)[0], &n);
+        CHECK(n == 2 && ids[0] && ids[1] && !strcmp(ids[0], "1") && !strcmp(ids[1], "2"), "Uppsala ids");
+        OKV(Java_NativeEngine_columnFree(E, K, LV(sel)[0]));
+      }
+      const jlong tmp[] = {mca, mup, lca, lup, id, state, salary, sal, codes};
+      for (int i = 0; i < 9; ++i) OKV(Java_NativeEngine_columnFree(E, K, tmp[i]));
+      OKV(Java_NativeEngine_aggDestroy(E, K, agg));
+      OKV(Java_NativeEngine_dictDestroy(E, K, d));
+      OKV(Java_NativeEngine_csvDestroy(E, K, t));
+    }
+    end(f0);
+  }
+
   /* the exceptions the reference throws for bad arguments */
   begin("exception_mapping");
   f0 = g_fail;
@@ -831,6 +904,7 @@ static void gpu_cases(void) {
 
 int main(int argc, char** argv) {
   const char* mode = argc > 1 ? argv[1] : "cpu";
+  g_employee = argc > 2 ? argv[2] : NULL;
   if (!strcmp(mode, "gpu"))
     gpu_cases();
   else

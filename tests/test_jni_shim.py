@@ -6,7 +6,9 @@ result against answers it computes on the host. CPU: argument validation and the
 classes the reference throws (K:49, K:195, K:791). GPU: the reference's operator chain through
 the shim end to end — SelectionExec / ProjectionExec / HashAggregateExec (K:582-660), fused and
 unfused, the two-phase merge of main() (K:1309-1325), deterministic fp64 sums, pipelined
-select-project, CastExpression (K:772-805), Arrow C Data in and out, Utf8 keys, CSV scan."""
+select-project, CastExpression (K:772-805), Arrow C Data in and out, Utf8 keys, CSV scan, and the
+reference's own fixture (employee.csv: GROUP BY state MAX(CAST(salary AS double)), state = 'CA' /
+'Uppsala') against its reference-held answers (tests/golden/employee_kat.json)."""
 import pathlib
 import subprocess
 
@@ -17,8 +19,8 @@ NATIVE = ROOT / "tests" / "native"
 HARNESS = NATIVE / "_build" / "jni_harness"
 
 
-def _run(mode: str) -> str:
-    r = subprocess.run([str(HARNESS), mode], capture_output=True, text=True, timeout=110)
+def _run(mode: str, *args: str) -> str:
+    r = subprocess.run([str(HARNESS), mode, *args], capture_output=True, text=True, timeout=110)
     out = r.stdout + r.stderr
     assert r.returncode == 0 and "ALL OK" in r.stdout, out[-4000:]
     return r.stdout
@@ -44,8 +46,8 @@ def test_real_shim_build_is_gated():
 def test_shim_gpu_cases():
     # built beforehand by __graft_entry__.build() (no compilation on the GPU box)
     assert HARNESS.exists(), "tests/native/_build/jni_harness missing: run __graft_entry__.build() first"
-    out = _run("gpu")
-    for case in ("roundtrip_columns", "unfused_group_by", "fused_group_by", "two_phase_merge",
+    out = _run("gpu", str(ROOT / "tests" / "golden" / "employee.csv"))
+    for case in ("employee_reference_query", "roundtrip_columns", "unfused_group_by", "fused_group_by", "two_phase_merge",
                  "deterministic_fp64_sums", "select_project_pipelined", "cast_to_double", "global_aggregate",
                  "arrow_c_data", "utf8_group_keys", "csv_scan", "exception_mapping"):
         assert f"ok {case}" in out, out[-4000:]
