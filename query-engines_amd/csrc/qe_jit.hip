@@ -1209,6 +1209,15 @@ bool selproj_wave_map() {
   }();
   return v;
 }
+// Full tiles of 8-byte columns load through a per-tile buffer descriptor (QE_SELPROJ_BUFLD, default
+// 1; stripe map only): one shared 32-bit lane offset register instead of a 64-bit address per load.
+bool selproj_buffer_loads() {
+  static const bool v = [] {
+    const char* e = getenv("QE_SELPROJ_BUFLD");
+    return !(e && e[0] == '0');
+  }();
+  return v && !selproj_wave_map();
+}
 static std::string sp_row(const std::string& b) {
   return selproj_wave_map() ? b + " + w * (R * 64) + r * 64 + lane" : b + " + r * BT + t";
 }
@@ -1238,10 +1247,19 @@ void emit_selproj_loads(const Plan& P, std::ostringstream& o, unsigned need, boo
     const char* ty = kind == K_I32 ? "qi32" : (kind == K_U8 || kind == K_BOOL) ? "qu8" : "qi64";
     o << ind << "{\n" << ind << "  const qi64 lb = " << b << ";\n" << ind << "  const bool lfull = lb + R * BT <= P.n;\n"
       << ind << "  const " << ty << "* p = (const " << ty << "*)P.cols[" << cs << "].p;\n"
-      << ind << "  if (lfull) {\n"  // whole tile: R loads back to back, no per-row exec branches
+      << ind << "  if (lfull) {\n";  // whole tile: R loads back to back, no per-row exec branches
+    if (std::string(ty) == "qi64" && kind != K_BOOL && selproj_buffer_loads())
+      o << ind << "    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc((void*)(p + lb), (short)0, "
+        << "(int)(R * BT * 8), 0x00020000);\n";
+    o
       << "#pragma unroll\n" << ind << "    for (int r = 0; r < R; ++r) {\n" << ind << "      const qi64 row = " << sp_row("lb") << ";\n";
     if (kind == K_BOOL)
       o << ind << "      " << cp << cs << "[r] = (p[row >> 3] >> (row & 7)) & 1;\n";
+    else if (std::string(ty) == "qi64" && selproj_buffer_loads())
+      // 8-byte column, stripe map: buffer loads off a per-tile descriptor (tile base in SGPRs), so
+      // all R loads share one 32-bit lane offset instead of a 64-bit address register each
+      o << ind << "      const auto v = __builtin_amdgcn_raw_buffer_load_b64(rs, (int)t * 8, r * BT * 8, " << (nt ? 2 : 0)
+        << ");\n" << ind << "      " << cp << cs << "[r] = (qi64)(((qu64)v[1] << 32) | (qu64)v[0]);\n";
     else
       // default policy below 64M rows: C2-sized inputs stay in the MALL (nt 68.4 us, default 65.0 us)
       o << ind << "      " << cp << cs << "[r] = (qi64)" << ld(ty, "p + row", nt) << ";\n";
