@@ -1155,7 +1155,11 @@ int selproj_rows_per_thread(const Plan& P, int mode) {
   }();
   const int by_cols = env ? env : (P.ncols <= 3 ? 16 : (P.ncols <= 6 ? 8 : 4));
   // (R x waves) per-(stripe, wave) counts: at most 4 per lane of the one-wave scan
-  return std::min(by_cols, 256 / (selproj_block(mode) / 64));
+  int r = std::min(by_cols, 256 / (selproj_block(mode) / 64));
+  // fewer rows per thread rather than losing the LDS-staged output (unstaged, every selected row
+  // stores 8 bytes from its lane and sets its validity bit with a device-scope atomic)
+  while (!env && r > 4 && (size_t)std::max(1, (int)P.naggs) * r * selproj_block(mode) * 8 > kSelprojStageBytes) r /= 2;
+  return r;
 }
 
 // Software-pipelined look-back tiles (QE_SELPROJ_PIPE=1; off by default): right after a tile's
@@ -1182,8 +1186,7 @@ int selproj_rows(const Plan& P, int mode) {
 
 // Persistent look-back tiles that load the next tile while this one's look-back and stores run
 // (QE_SELPROJ_PREFETCH, default on; 0 = off): only with staged outputs (all 8 bytes wide, so the
-// column registers are dead once the rows sit in LDS) and no nullable output (whose validity bits
-// are written from the column registers after the look-back).
+// column registers are dead once the rows — and nullable outputs' validity bits — sit in LDS).
 bool selproj_prefetch_ok(const Plan& P, const int32_t* out_kind, int nout, int mode) {
   static const bool on = [] {
     const char* e = getenv("QE_SELPROJ_PREFETCH");
@@ -1192,7 +1195,7 @@ bool selproj_prefetch_ok(const Plan& P, const int32_t* out_kind, int nout, int m
   if (!on || mode != SP_PERSIST || selproj_pipelined()) return false;
   if ((size_t)nout * selproj_rows(P, mode) * selproj_block(mode) * 8 > kSelprojStageBytes) return false;
   for (int k = 0; k < nout; ++k)
-    if ((out_kind[k] & 0xFF) != 8 || (out_kind[k] & 0x100)) return false;
+    if ((out_kind[k] & 0xFF) != 8) return false;
   return true;
 }
 
@@ -1301,6 +1304,14 @@ bool emit_selproj_write(const Plan& P, const int32_t* out_kind, int nout, int mo
       ex[k].ok = "((ok" + std::to_string(k) + " >> r) & 1u)";
     }
   }
+  const bool any_null = [&] { for (int k = 0; k < nout; ++k) if (out_kind[k] & 0x100) return true; return false; }();
+  if (staged && any_null)
+    // the tile's output validity bits, in tile-local order (bit = compacted position), zeroed
+    // behind the previous tile's last barrier
+    for (int k = 0; k < nout; ++k)
+      if (out_kind[k] & 0x100)
+        o << "  __shared__ qu32 s_vb" << k << "[R * BT / 32 + 2];\n"
+          << "  for (int i = t; i < R * BT / 32 + 2; i += BT) s_vb" << k << "[i] = 0u;\n";
   o << "  qu64 bal[R];\n"
     << "#pragma unroll\n  for (int r = 0; r < R; ++r) bal[r] = __ballot((act >> r) & 1u);\n"
     << "  if (lane == 0) {\n#pragma unroll\n    for (int r = 0; r < R; ++r) s_cnt[" << sp_cnt_idx() << "] = (qu32)__popcll(bal[r]);\n  }\n"
@@ -1370,6 +1381,8 @@ bool emit_selproj_write(const Plan& P, const int32_t* out_kind, int nout, int mo
       << "    if (!((act >> r) & 1u)) continue;\n"
       << "    const qu32 lp = s_cnt[" << sp_cnt_idx() << "] + (qu32)__popcll(bal[r] & below);\n";
     for (int k = 0; k < nout; ++k) o << "    s_out[" << k << " * (R * BT) + lp] = " << ex[k].v << ";\n";
+    for (int k = 0; k < nout; ++k)
+      if (out_kind[k] & 0x100) o << "    if (" << ex[k].ok << ") atomicOr(&s_vb" << k << "[lp >> 5], 1u << (lp & 31));\n";
     o << "  }\n";
     if (!prefetch.empty())
       // the tile's rows are in LDS, so its column registers are free: the next tile's loads go
@@ -1390,14 +1403,25 @@ bool emit_selproj_write(const Plan& P, const int32_t* out_kind, int nout, int mo
         << "      for (qu32 i = head + 2 * t; i + 1 < tot; i += 2 * BT) *(qi64x2*)(out + i) = qi64x2{so[i], so[i + 1]};\n"
         << "      if (t == 0 && tot > head && ((tot - head) & 1)) out[tot - 1] = so[tot - 1];\n    }\n";
     }
-    const bool any_null = [&] { for (int k = 0; k < nout; ++k) if (out_kind[k] & 0x100) return true; return false; }();
     if (any_null) {
-      o << "#pragma unroll\n    for (int r = 0; r < R; ++r) {\n"
-        << "      if (!((act >> r) & 1u)) continue;\n"
-        << "      const qu64 pos = tb + s_cnt[" << sp_cnt_idx() << "] + (qu64)__popcll(bal[r] & below);\n";
-      for (int k = 0; k < nout; ++k)
-        if (out_kind[k] & 0x100)
-          o << "      if (" << ex[k].ok << ") atomicOr(&((qu32*)P.t.nn[" << k << "])[pos >> 5], 1u << (pos & 31));\n";
+      // validity words of the output range [tb, tb + tot): the words inside it belong to this tile
+      // alone (plain stores); the first and last may share bits with the neighbouring tiles
+      // (atomicOr into the zero-initialised bitmap)
+      o << "    const qu64 w0 = tb >> 5;\n"
+        << "    const qu32 nw = tot ? (qu32)(((tb + tot - 1) >> 5) - w0 + 1) : 0u;\n"
+        << "    for (qu32 i = t; i < nw; i += BT) {\n"
+        << "      const qi64 l0 = (qi64)((w0 + i) << 5) - (qi64)tb;  // tile-local bit of the word's bit 0\n"
+        << "      const bool whole = l0 >= 0 && l0 + 32 <= (qi64)tot;\n";
+      for (int k = 0; k < nout; ++k) {
+        if (!(out_kind[k] & 0x100)) continue;
+        const std::string ks = std::to_string(k);
+        o << "      {\n        qu32 v;\n"
+          << "        if (l0 < 0) v = s_vb" << ks << "[0] << (qu32)(-l0);\n"
+          << "        else { const qu32 q = (qu32)l0 >> 5, sh = (qu32)l0 & 31u;\n"
+          << "               v = sh ? (s_vb" << ks << "[q] >> sh) | (s_vb" << ks << "[q + 1] << (32u - sh)) : s_vb" << ks << "[q]; }\n"
+          << "        qu32* vw = (qu32*)P.t.nn[" << ks << "] + (w0 + i);\n"
+          << "        if (whole) *vw = v; else if (v) atomicOr(vw, v);\n      }\n";
+      }
       o << "    }\n";
     }
     o << "  }\n";

@@ -22,8 +22,8 @@ import torch  # noqa: E402
 from kquery import native as N  # noqa: E402
 from kquery.aggregate import HashAggregateState  # noqa: E402
 from kquery.columnar import Context, DeviceColumn, Field, RecordBatch, Schema  # noqa: E402
-from kquery.datasource import (C2_COLUMNS, C3_COLUMNS, C4_COLUMNS, C5_COLUMNS, InMemoryDataSource,  # noqa: E402
-                               generate_column)
+from kquery.datasource import (C2_COLUMNS, C3_COLUMNS, C4_COLUMNS, C5_COLUMNS, ColumnSpec,  # noqa: E402
+                               InMemoryDataSource, generate_column)
 from kquery.expressions import (AddExpression, ColumnExpression, GtExpression,  # noqa: E402
                                 LiteralLongExpression)
 from kquery.operators import ProjectionExec, ScanExec, SelectionExec, fuse  # noqa: E402
@@ -159,6 +159,30 @@ def main():
 
         ms_l = timed(run_large)
         report("C2 shape at 1B rows: fused select+project (qe_select_project call)", n, 16 + 8 * cnt.value / n, ms_l,
+               selected=cnt.value)
+        del cols, o
+    if "C2LN" in which:  # the C2 shape at 1B rows with 1 % nulls in b: a nullable output (a + b)
+        n = 1_000_000_000
+        specs = [C2_COLUMNS[0], ColumnSpec("b", N.TYPE_INT64, N.GEN_RAW, 0, 2, null_permille=10)]
+        cols = [generate_column(s, n, 0, 42, ctx) for s in specs]
+        schema = Schema([s.field() for s in specs])
+        scan = ScanExec(InMemoryDataSource(schema, [RecordBatch(schema, cols)]), ["a", "b"])
+        sel = SelectionExec(scan, GtExpression(ColumnExpression(0), LiteralLongExpression(1 << 19)))
+        proj = ProjectionExec(sel, Schema([Field("ab", N.TYPE_INT64)]),
+                              [AddExpression(ColumnExpression(0), ColumnExpression(1))])
+        fused = fuse(proj)
+        cc = (N.QeColumn * 2)(*[x.as_c() for x in cols])
+        o = DeviceColumn.empty(N.TYPE_INT64, n, True, ctx=ctx)
+        oc = (N.QeColumn * 1)(o.as_c())
+        cnt = N.C.c_int64()
+
+        def run_nullable():
+            oc[0].length = n
+            N.check(N.lib().qe_select_project(ctx.handle, cc, 2, N.C.byref(fused.spec), oc, N.C.byref(cnt)))
+
+        ms_n = timed(run_nullable)
+        # a, b, b's validity bits in; a+b and its validity bits out for the selected rows
+        report("C2 shape at 1B rows, b 1 % null (nullable output)", n, 16 + 1 / 8 + (8 + 1 / 8) * cnt.value / n, ms_n,
                selected=cnt.value)
         del cols, o
     if "C3" in which:
