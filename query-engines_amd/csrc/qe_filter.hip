@@ -165,7 +165,7 @@ struct GatherCol {
   const void* in;
   const uint8_t* in_valid;
   void* out;
-  uint32_t* out_valid;  // zeroed by the host; bits set with atomicOr
+  uint32_t* out_valid;  // zeroed by the host; whole words from the tile's LDS bitmap (atomicOr at its edges)
   int32_t width;        // 8, 4 or 1; 0 = UTF-8 (out = int64 {src offset, length} per selected row)
   int32_t pad;
   const int32_t* in_offs;  // UTF-8 input offsets
@@ -178,7 +178,7 @@ struct GatherArgs {
 };
 
 __device__ __forceinline__ void gather_store(const GatherCol& c, int64_t row0, int nsel_mask, int64_t pos0,
-                                             const int (&rank)[4], bool full) {
+                                             const int (&rank)[4], bool full, uint32_t* lbits, int64_t tb) {
   // Loads the lane's 4 rows (vectorised when the tile is full) and stores the selected ones.
   if (c.width == 0) {  // UTF-8: record (source byte offset, length); bytes are copied after the scan
 #pragma unroll
@@ -211,15 +211,36 @@ __device__ __forceinline__ void gather_store(const GatherCol& c, int64_t row0, i
     for (int j = 0; j < 4; ++j)
       if ((nsel_mask >> j) & 1) ((uint8_t*)c.out)[pos0 + rank[j]] = ((const uint8_t*)c.in)[row0 + j];
   }
-  if (c.out_valid) {
+  if (c.out_valid) {  // validity bits at tile-local output positions in LDS (written out per tile)
     const uint8_t vb = c.in_valid ? (uint8_t)(c.in_valid[row0 >> 3] >> (row0 & 7)) : (uint8_t)0xF;
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       if (((nsel_mask >> j) & 1) && ((vb >> j) & 1)) {
-        const int64_t p = pos0 + rank[j];
-        atomicOr(&c.out_valid[p >> 5], 1u << (p & 31));
+        const int p = (int)(pos0 + rank[j] - tb);
+        atomicOr(&lbits[p >> 5], 1u << (p & 31));
       }
     }
+  }
+}
+
+// A tile's validity bits (LDS, tile-local compacted order) -> the output bitmap words of its range
+// [tb, tb + total): words inside the range are this tile's alone (plain stores), the first and last
+// may share bits with the neighbouring tiles (atomicOr into the zeroed bitmap).
+__device__ __forceinline__ void flush_valid_bits(uint32_t* out_valid, const uint32_t* lbits, int64_t tb, int64_t total) {
+  const int64_t w0 = tb >> 5;
+  const int64_t nw = total ? ((tb + total - 1) >> 5) - w0 + 1 : 0;
+  for (int64_t i = threadIdx.x; i < nw; i += blockDim.x) {
+    const int64_t l0 = ((w0 + i) << 5) - tb;  // tile-local bit of the word's bit 0
+    uint32_t v;
+    if (l0 < 0) {
+      v = lbits[0] << (uint32_t)(-l0);
+    } else {
+      const uint32_t q = (uint32_t)(l0 >> 5), sh = (uint32_t)(l0 & 31);
+      v = sh ? (lbits[q] >> sh) | (lbits[q + 1] << (32u - sh)) : lbits[q];
+    }
+    uint32_t* dst = out_valid + (w0 + i);
+    if (l0 >= 0 && l0 + 32 <= total) *dst = v;
+    else if (v) atomicOr(dst, v);
   }
 }
 
@@ -227,9 +248,15 @@ __global__ void __launch_bounds__(FT_THREADS) k_compact(const uint8_t* __restric
                                                         int64_t n, const int64_t* __restrict__ tile_offsets,
                                                         GatherArgs args) {
   __shared__ int wtot[FT_THREADS / 64];
+  constexpr int VW = (int)(FT_TILE / 32) + 1;  // a tile's output validity words (+1: shifted reads)
+  __shared__ uint32_t s_vb[FT_MAX_COLS][VW];
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   const int64_t tile = blockIdx.x;
   int64_t base = tile_offsets[tile];
+  const int64_t tb = base;
+  for (int k = 0; k < args.ncols; ++k)
+    if (args.cols[k].out_valid)
+      for (int i = threadIdx.x; i < VW; i += FT_THREADS) s_vb[k][i] = 0u;
   const uint64_t lt = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
   for (int it = 0; it < FT_ITERS; ++it) {
     const int64_t row0 = tile * FT_TILE + (int64_t)it * (FT_THREADS * FT_ROWS_PER_LANE) +
@@ -259,11 +286,13 @@ __global__ void __launch_bounds__(FT_THREADS) k_compact(const uint8_t* __restric
       }
       const int64_t pos0 = base + woff + prefix;
       const bool full = row0 + 4 <= n;
-      for (int k = 0; k < args.ncols; ++k) gather_store(args.cols[k], row0, sel, pos0, rank, full);
+      for (int k = 0; k < args.ncols; ++k) gather_store(args.cols[k], row0, sel, pos0, rank, full, s_vb[k], tb);
     }
     base += btot;
     __syncthreads();
   }
+  for (int k = 0; k < args.ncols; ++k)
+    if (args.cols[k].out_valid) flush_valid_bits(args.cols[k].out_valid, s_vb[k], tb, base - tb);
 }
 
 // ---- UTF-8 gather: (src, len) pairs -> offsets (device-wide exclusive scan) -> bytes ------------
