@@ -74,6 +74,33 @@ def test_c2_shape(gpu_ctx, selproj_path, n, k):
     assert ab.valid_mask().all()
 
 
+@pytest.mark.parametrize("n", [1, 4097, 100_003, 3_000_017])
+@pytest.mark.parametrize("nout", [1, 2])
+def test_nullable_wide_outputs(gpu_ctx, selproj_path, n, nout):
+    """8-byte outputs that can be null (b has nulls): the tile's validity bits are staged in LDS in
+    compacted order and written as whole words, shared words at tile edges by atomicOr. Checks every
+    output bit and value against the oracle, across many tiles whose output ranges start at
+    arbitrary bit offsets."""
+    from kquery import native as N
+    from kquery.datasource import C2_COLUMNS, ColumnSpec, generate_column
+
+    specs = [C2_COLUMNS[0], ColumnSpec("b", N.TYPE_INT64, N.GEN_RAW, 0, 2, null_permille=100)]
+    cols = [generate_column(s, n, 0, 42, gpu_ctx) for s in specs]
+    progs = [[(N.TOK_COL, 0, None), (N.TOK_COL, 1, None), (N.TOK_ADD, 0, None)], [(N.TOK_COL, 1, None)]][:nout]
+    spec = _spec(N, [(0, N.OP_GT, -1, 1 << 19)], progs)
+    cnt, outs = _run(gpu_ctx, cols, spec, [N.TYPE_INT64] * nout)
+    a_h, _ = gen.generate(specs[0].dist, specs[0].param, 42, specs[0].col_id, 0, n)
+    b_h, bv = gen.generate(specs[1].dist, specs[1].param, 42, specs[1].col_id, 0, n, 100)
+    m, mv = S.cmp(S.OP_GT, a_h, None, 1 << 19, None)
+    sel = S.select_mask(m, mv)
+    assert cnt == int(sel.sum())
+    ab, abv = S.arith(S.OP_ADD, a_h, None, b_h, bv)
+    for out, (val, valid) in zip(outs, [(ab, abv), (b_h, bv)]):
+        got_v = out.valid_mask()
+        assert (got_v == valid[sel]).all()
+        assert (out.to_numpy()[got_v] == val[sel][valid[sel]]).all()
+
+
 @pytest.mark.parametrize("n", [1000, 70_001])
 def test_nulls_division_f64_and_narrow_types(gpu_ctx, selproj_path, n):
     from kquery import native as N
