@@ -6,7 +6,10 @@ UndefinedBehaviorSanitizer, on the CPU.
   exact-size heap copy, so a read past a string's end is a report; the results must equal the
   oracle (Double.parseDouble) bit for bit;
 * the oracle's C restatement (oracle/cpu_baseline.c, the bench's CPU baseline) multi-threaded
-  under the same sanitizers, checked against the Python oracle.
+  under the same sanitizers, checked against the Python oracle;
+* the JNI shim (query-engines_amd/jni/qe_jni.c) driven through its argument-checking and
+  exception paths by tests/native/jni_harness.c (test-double JNIEnv; leak detection off: the
+  harness keeps its fake Java objects for the process lifetime, as a JVM's GC would own them).
 
 A sanitizer report makes the driver exit non-zero (-fno-sanitize-recover for UBSan), which fails
 the test. GPU code is not sanitized (no GPU ASan on this pool); the device paths get the
@@ -99,3 +102,17 @@ def test_cpu_baseline_asan_ubsan(drivers, threads, row0, rows):
     want = S.group_aggregate([k], [None], [S.arith(S.OP_ADD, a, None, b, None)[0], None, a, b], [None] * 4,
                              [S.AGG_SUM, S.AGG_COUNT_STAR, S.AGG_MIN, S.AGG_MAX], a > (1 << 19))
     assert got == want
+
+
+def test_jni_shim_host_paths_under_asan_ubsan():
+    (NATIVE / "_build").mkdir(exist_ok=True)
+    with open(NATIVE / "_build" / ".lock", "w") as lock:
+        fcntl.flock(lock, fcntl.LOCK_EX)
+        r = subprocess.run(["make", "-s", "-C", str(NATIVE), "_build/san_jni_harness"], capture_output=True, text=True)
+    if r.returncode != 0:
+        pytest.skip("sanitizer build unavailable: " + r.stderr[-400:])
+    env = dict(ENV, ASAN_OPTIONS="detect_leaks=0:abort_on_error=0:exitcode=23")
+    p = subprocess.run([str(NATIVE / "_build" / "san_jni_harness"), "cpu"], capture_output=True, text=True, env=env,
+                       timeout=300)
+    assert p.returncode == 0 and "ALL OK" in p.stdout, (p.returncode, p.stdout[-2000:], p.stderr[-3000:])
+    assert "runtime error" not in p.stderr and "AddressSanitizer" not in p.stderr, p.stderr[-3000:]
