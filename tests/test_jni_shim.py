@@ -35,6 +35,16 @@ def test_shim_cpu_cases():
         assert f"ok {case}" in out
 
 
+def test_kotlin_declarations_match_the_shim():
+    """Every `external fun` of NativeEngine.kt has its Java_NativeEngine_* in qe_jni.c and back."""
+    import re
+
+    jni = ROOT / "query-engines_amd" / "jni"
+    c_names = set(re.findall(r"JNICALL Java_NativeEngine_(\w+)\(", (jni / "qe_jni.c").read_text()))
+    kt_names = set(re.findall(r"@JvmStatic external fun (\w+)\(", (jni / "NativeEngine.kt").read_text()))
+    assert c_names and c_names == kt_names, (sorted(c_names - kt_names), sorted(kt_names - c_names))
+
+
 def test_real_shim_build_is_gated():
     """Without a JDK the shim's own Makefile says so and succeeds (nothing half-built)."""
     r = subprocess.run(["make", "-C", str(ROOT / "query-engines_amd" / "jni")], capture_output=True, text=True,
