@@ -45,6 +45,34 @@ def test_kotlin_declarations_match_the_shim():
     assert c_names and c_names == kt_names, (sorted(c_names - kt_names), sorted(kt_names - c_names))
 
 
+_KT_TO_JNI = {"Long": "jlong", "Int": "jint", "Boolean": "jboolean", "Double": "jdouble", "LongArray": "jlongArray",
+              "IntArray": "jintArray", "ByteArray": "jbyteArray", "DoubleArray": "jdoubleArray",
+              "Array<String>": "jobjectArray", "java.nio.ByteBuffer": "jobject", "String": "jstring", "Unit": "void"}
+
+
+def test_kotlin_signatures_match_the_shim():
+    """Parameter and return types of every external fun map to the C function's JNI types (the
+    JVM binds by name only, so a mismatch would corrupt arguments at run time, not fail to link)."""
+    import re
+
+    jni = ROOT / "query-engines_amd" / "jni"
+    csrc = (jni / "qe_jni.c").read_text()
+    c_sig = {}
+    for m in re.finditer(r"JNIEXPORT (\w+) JNICALL Java_NativeEngine_(\w+)\(([^)]*)\)", csrc):
+        params = [" ".join(p.split()[:-1]) for p in m.group(3).replace("\n", " ").split(",")]
+        assert params[:2] == ["JNIEnv*", "jclass"], m.group(2)
+        c_sig[m.group(2)] = (m.group(1), params[2:])
+    kt = re.sub(r"\s+", " ", (jni / "NativeEngine.kt").read_text())
+    n = 0
+    for m in re.finditer(r"@JvmStatic external fun (\w+)\(([^)]*)\)(?:: ([\w.<>?]+))?", kt):
+        name, params, ret = m.group(1), m.group(2), m.group(3) or "Unit"
+        types = [p.split(":", 1)[1].strip().rstrip("?") for p in params.split(",") if p.strip()]
+        want = (_KT_TO_JNI[ret.rstrip("?")], [_KT_TO_JNI[t] for t in types])
+        assert c_sig[name] == want, (name, c_sig[name], want)
+        n += 1
+    assert n == len(c_sig) == 60
+
+
 def test_real_shim_build_is_gated():
     """Without a JDK the shim's own Makefile says so and succeeds (nothing half-built)."""
     r = subprocess.run(["make", "-C", str(ROOT / "query-engines_amd" / "jni")], capture_output=True, text=True,
