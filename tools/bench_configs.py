@@ -95,8 +95,24 @@ def main():
             N.check(N.lib().qe_select_project(ctx.handle, cc, 2, N.C.byref(fused.spec), oc, N.C.byref(cnt)))
 
         ms_k = timed(run_kernel)
+        # the same call with the input evicted from the 256 MB MALL first (a 1 GiB write between
+        # calls, outside the timed region): what one 10M batch costs from HBM
+        flush = torch.empty(1 << 30, dtype=torch.uint8, device=ctx.torch_device)
+        cold = []
+        for it in range(13):
+            flush.fill_(it & 0xFF)
+            s_ev, e_ev = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            s_ev.record()
+            run_kernel()
+            e_ev.record()
+            e_ev.synchronize()
+            if it >= 3:
+                cold.append(s_ev.elapsed_time(e_ev))
+        ms_cold = statistics.median(cold)
+        del flush
         report("C2 fused select+project (qe_select_project), 10M int64", n, 16 + 8 * sel_rows / n, ms_f,
                selected=sel_rows, call_ms=ms_k, call_gbs=n * (16 + 8 * sel_rows / n) / (ms_k * 1e-3) / 1e9,
+               call_cold_ms=ms_cold, call_cold_gbs=n * (16 + 8 * sel_rows / n) / (ms_cold * 1e-3) / 1e9,
                path="one hipRTC-specialised kernel: predicate, look-back compaction, projection")
         # stream-ordered calls (qe_select_project_async): call i+1 is queued before call i's count
         # is read back, as the pipelined FusedSelectProjectExec does batch to batch
