@@ -179,3 +179,66 @@ def test_random_plan(gpu_ctx, seed):
             for j, (g, x) in enumerate(zip(got[ck], w)):
                 rel = REL if fns[j] in (1, 6) and isinstance(x, float) else 0.0
                 assert S.rows_equal(g, x, rel), (type(p).__name__, seed, k, j, g, x)
+
+
+@pytest.mark.parametrize("seed", range(60))
+def test_random_select_project(gpu_ctx, monkeypatch, seed):
+    """Random Projection(Selection(Scan)) plans (the same random columns, predicates and projection
+    arithmetic): the fused select-project kernel (tile-base mode by seed: two passes, look-back,
+    scanned; nullable and narrow outputs, staged validity words) and the unfused operators must
+    both return the oracle's rows, in input order."""
+    from kquery import expressions as E
+    from kquery import native as N
+    from kquery.columnar import DeviceColumn, Field, RecordBatch, Schema
+    from kquery.datasource import InMemoryDataSource
+    from kquery.operators import ProjectionExec, ScanExec, SelectionExec, fuse
+
+    monkeypatch.setenv("QE_SELPROJ_TWOPASS", ("1", "0", "2")[seed % 3])
+    n, types, cols, keys, terms, aggs = _plan(seed + 1000)
+    keys = [k for k in keys if k < 5]  # fixed-width outputs (UTF-8 projections take the unfused path)
+    qtypes = [_qe_type(N, t) for t in types]
+    schema = Schema([Field(f"c{i}", qtypes[i]) for i in range(5)])
+    batch = RecordBatch(schema, [DeviceColumn.from_numpy(qtypes[i], cols[i][0], cols[i][1], ctx=gpu_ctx)
+                                 for i in range(5)])
+    scan = ScanExec(InMemoryDataSource(schema, [batch]), [f"c{i}" for i in range(5)])
+    cmp_cls = {10: E.EqExpression, 11: E.NeqExpression, 12: E.LtExpression, 13: E.LtEqExpression,
+               14: E.GtExpression, 15: E.GtEqExpression}
+    pred = None
+    sel = np.ones(n, dtype=bool)
+    for c, op, rc, lit in terms:
+        rhs = E.ColumnExpression(rc) if rc is not None else (
+            E.LiteralDoubleExpression(lit) if isinstance(lit, float) else E.LiteralLongExpression(lit))
+        t = cmp_cls[op](E.ColumnExpression(c), rhs)
+        pred = t if pred is None else E.AndExpression(pred, t)
+        a = cols[c][0].astype(np.float64 if types[c] == "f64" else np.int64)
+        if rc is not None:
+            b, bv = cols[rc][0].astype(np.float64 if types[rc] == "f64" else np.int64), cols[rc][1]
+        else:
+            b, bv = lit, None
+        m, mv = S.cmp(op, a, cols[c][1], b, bv)
+        sel &= S.select_mask(m, mv)
+    if pred is None:
+        pred = E.GtEqExpression(E.ColumnExpression(0), E.LiteralLongExpression(-2**62))
+        m, mv = S.cmp(15, cols[0][0].astype(np.float64 if types[0] == "f64" else np.int64), cols[0][1], -2**62, None)
+        sel &= S.select_mask(m, mv)
+    exprs = [E.ColumnExpression(k) for k in keys] + [_expr(E, sh, a, b) for _, sh, a, b in aggs]
+    want = [(cols[k][0], cols[k][1]) for k in keys] + [_oracle_expr(sh, a, b, cols, types) for _, sh, a, b in aggs]
+    out_types = [qtypes[k] for k in keys]
+    for _, sh, a, b in aggs:
+        is_f = types[a] == "f64" or (sh in ("add", "mul") and types[b] == "f64")
+        out_types.append(N.TYPE_FLOAT64 if is_f else (qtypes[a] if sh == "col" else N.TYPE_INT64))
+    plan = ProjectionExec(SelectionExec(scan, pred), Schema([Field(f"o{j}", t) for j, t in enumerate(out_types)]),
+                          exprs)
+    fused = fuse(plan)
+    assert type(fused).__name__ == "FusedSelectProjectExec", fused
+    for p in (fused, plan):
+        rows = [b for b in p.execute()]
+        got = [[] for _ in exprs]
+        for b in rows:
+            for j in range(len(exprs)):
+                got[j].extend(b.field(j).to_pylist())
+        for j, (v, vv) in enumerate(want):
+            exp = [None if vv is not None and not vv[i] else v[i].item() for i in np.nonzero(sel)[0]]
+            assert len(got[j]) == len(exp), (type(p).__name__, seed, j, len(got[j]), len(exp))
+            for g, x in zip(got[j], exp):
+                assert S.rows_equal(g, x, 0.0), (type(p).__name__, seed, j, g, x)
