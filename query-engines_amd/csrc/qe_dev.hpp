@@ -137,6 +137,9 @@ struct Plan {
   // multi-pass fused aggregate (groups just beyond one LDS table): pass mp_pass of mp_n keeps the
   // rows whose key hash falls in bucket mp_pass (mp_n = 0: every row)
   qi32 mp_n, mp_pass;
+  // radix-partitioned records in 32-bit words when the plan's words are integral (part_layout):
+  // the scatter sets t.ctl[7] if a value did not fit, and the aggregation pass then does nothing
+  qi32 part_narrow, pad1;
   // spilling first pass (spill_update): rows with fmix64(key) >> 32 >= mp_keep are spilled as records
   qu64 mp_keep;
   // select-project: pinned host words the kernel writes its results to ([0] rows written, [1] the

@@ -1418,6 +1418,9 @@ struct qe_hashagg {
   size_t part_rec_bytes = 0;
   int64_t* part_slc = nullptr;  // slice descriptors of the partition-aggregate pass
   size_t part_slc_bytes = 0;
+  // 32-bit partition records (Plan.part_narrow): off for good once a value did not fit
+  bool part_wide = false;
+  bool narrow_failed = false;  // the last settled launch saw ctl[7] set
   // overflow records
   uint8_t* ovf = nullptr;
   uint64_t ovf_cap = 0;
@@ -1880,8 +1883,21 @@ static int grow_buffer(T** p, size_t* have, size_t need, qe_ctx* ctx, const char
 // selected rows per (key-hash bucket, workgroup), scan, scatter one record per selected row into
 // its bucket. On return P describes the aggregation pass over the records (P.n = records,
 // P.part_tw = records per workgroup) and *fn / *grid its kernel.
+// Narrow records (QE_PART_NARROW, default 1): integral record words are stored as 32 bits while
+// every value of the update fits (sign-extended); the scatter flags ctl[7] otherwise, the
+// aggregation pass then does nothing and run_update repeats the update with 64-bit words.
+static bool part_narrow_env() {
+  static const bool v = [] {
+    const char* e = getenv("QE_PART_NARROW");
+    return !(e && e[0] == '0');
+  }();
+  return v;
+}
+
 static int partition_rows(qe_hashagg* h, Plan& P, hipFunction_t* fn, int* grid) {
   qe_ctx* ctx = h->ctx;
+  P.part_narrow = (!h->part_wide && part_narrow_env() && !part_soa()) ? 1 : 0;
+  P.t = h->t;  // the scatter's fit flag (t.ctl[7])
   // aggregation-pass LDS table: the largest that fits the per-workgroup budget
   int tlog2 = 16;
   const size_t pbudget = pagg_block() == 1024 ? (size_t)152 * 1024 : HA_LDS_BUDGET;
@@ -1918,7 +1934,8 @@ static int partition_rows(qe_hashagg* h, Plan& P, hipFunction_t* fn, int* grid) 
   // (one 1024-thread staged workgroup fits a CU)
   int64_t g = std::min<int64_t>((int64_t)ctx->num_cus * (sblock == 1024 ? 1 : wg_per_cu), (int64_t)div_up((uint64_t)n, 256));
   const PartLayout L = part_layout(P);
-  const size_t rb = 8 * (size_t)L.words;
+  const size_t rb = (size_t)L.bytes();
+  if (L.narrow) QE_HIP(hipMemsetAsync(h->ctl + 7, 0, 8, ctx->stream));
   // Chunked scatter (staged buckets): no count pass and no read-back of the record count;
   // workgroups claim PART_CH-record chunks per bucket from a device counter. Record space: every
   // selected row in a full chunk plus one open chunk per (workgroup, bucket) — at most
@@ -1996,7 +2013,7 @@ static int partition_rows(qe_hashagg* h, Plan& P, hipFunction_t* fn, int* grid) 
     P.part_sorted = sorted;
     *grid = (int)max_slices;
     h->jit_note = "radix-partitioned: " + std::to_string(np) + " buckets, chunked records of " + std::to_string(rb) +
-                  " B (" + (L.colmode ? "column" : "value") + " words), staged scatter";
+                  " B (" + (L.colmode ? "column" : "value") + (L.narrow ? " words, 32-bit" : " words") + "), staged scatter";
     return QE_OK;
   }
   const size_t cells = ((size_t)1 << log2p) * (size_t)g;
@@ -2048,7 +2065,7 @@ static int partition_rows(qe_hashagg* h, Plan& P, hipFunction_t* fn, int* grid) 
   P.part_slice = (qi64*)h->part_slc;
   *grid = (int)max_slices;
   h->jit_note = "radix-partitioned: " + std::to_string(1 << log2p) + " buckets, " + std::to_string(R) + " records of " +
-                std::to_string(rb) + " B (" + (L.colmode ? "column" : "value") + " words)" +
+                std::to_string(rb) + " B (" + (L.colmode ? "column" : "value") + (L.narrow ? " words, 32-bit)" : " words)") +
                 (staged ? ", staged scatter" : "");
   return QE_OK;
 }
@@ -2193,6 +2210,7 @@ static int settle_pass(qe_hashagg* h, const Plan& P, int* out_i, const uint32_t*
   QE_CHECK(c[6] == 0, QE_ERR_UNSUPPORTED,
            "deterministic fp64 SUM: %llu inputs outside the exact fixed-point range (NaN, +-Inf or |x| >= 2^63)",
            (unsigned long long)c[6]);
+  h->narrow_failed = P.part_narrow && c[7] != 0;
   const uint64_t groups = c[0], deferred = c[1], ovf_recs = std::min<uint64_t>(c[2], P.ovf_cap);
   h->ctl_rows_clean = c[1] == 0 && c[2] == 0;
   *done = true;
@@ -2405,6 +2423,8 @@ static int run_update(qe_hashagg* h, Plan& P) {
       return QE_OK;
     }
   }
+  const Plan P_rows = P;  // the batch's plan, for a partitioned update repeated with 64-bit records
+  for (;;) {
   if (!lds && mp_n == 0 && ctx->jit && h->expected_groups > 0) {
     Plan Q = P;
     if (partition_rows(h, Q, &pfn, &pgrid) == QE_OK) {
@@ -2446,6 +2466,17 @@ static int run_update(qe_hashagg* h, Plan& P) {
       QE_TRY(settle_pass(h, P, &out_i, &defer_in, &done));
       if (done) break;
     }
+  }
+  if (pfn && h->narrow_failed) {
+    // a value did not fit the 32-bit records (the aggregation pass left the table untouched):
+    // this state's partitioned updates use 64-bit words from now on
+    h->narrow_failed = false;
+    h->part_wide = true;
+    P = P_rows;
+    pfn = nullptr;
+    continue;
+  }
+  break;
   }
   if (mp_n) h->jit_note = "multi-pass: " + std::to_string(mp_n) + " bucket passes";
   h->row_base += rows;

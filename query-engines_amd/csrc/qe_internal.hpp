@@ -83,6 +83,9 @@ struct PartLayout {
   int flags_word = -1;  // bit 0 null key, bit 1 + j input j valid (colmode: column c valid); -1 if nothing is nullable
   int row_word = -1;               // global row index (fp64 MIN/MAX); -1 if not needed
   bool row = false;
+  // every word stored as 32 bits (sign-extended on load): Plan.part_narrow and integral words only
+  bool narrow = false;
+  int bytes() const { return (narrow ? 4 : 8) * words; }
 };
 PartLayout part_layout(const qe::Plan& P);
 bool gen_part_source(const qe::Plan& P, int log2p, bool scatter, std::string* src);

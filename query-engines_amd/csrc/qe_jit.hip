@@ -599,7 +599,32 @@ PartLayout part_layout(const Plan& P) {
   L.flags_word = (knull || (L.colmode ? cnull : vnull)) ? w++ : -1;
   L.row_word = L.row ? w++ : -1;
   L.words = w;
+  // 32-bit words: every word integral (no fp64 key, value or column, no row index); whether the
+  // values fit is checked by the scatter (Plan.part_narrow)
+  if (P.part_narrow && !L.row && !P.key_f64) {
+    bool ok = true;
+    for (int c = 0; c < P.ncols; ++c)
+      if (L.col_word[c] >= 0 && P.cols[c].kind == K_F64) ok = false;
+    for (int j = 0; j < P.naggs; ++j)
+      if (L.val_word[j] >= 0 && P.aggs[j].acc != ACC_SUM_I && P.aggs[j].acc != ACC_MIN_I && P.aggs[j].acc != ACC_MAX_I)
+        ok = false;
+    L.narrow = ok;
+  }
   return L;
+}
+
+// Narrow records: the statements that fold `w`'s words (qi64 array expression) into `nfit` (set when
+// one does not survive the round trip through 32 bits).
+static void emit_fit_check(const PartLayout& L, const std::string& w, std::ostringstream& o) {
+  if (!L.narrow) return;
+  for (int q = 0; q < L.words; ++q)
+    o << "      nfit |= (qu32)(" << w << "[" << q << "] != (qi64)(qi32)" << w << "[" << q << "]);\n";
+}
+
+// Narrow records: chunk value q of a record whose words are `w` (G = 1: one word, G = 2: a pair).
+static std::string narrow_chunk(const std::string& w, int G, const std::string& q) {
+  if (G == 1) return "(qu32)" + w + "[" + q + "]";
+  return "((qu64)(qu32)" + w + "[2 * (" + q + ")] | ((qu64)(qu32)" + w + "[2 * (" + q + ") + 1] << 32))";
 }
 
 // Record word assignments for row r of a scatter step into `dst` (an array expression).
@@ -642,6 +667,7 @@ bool gen_part_source(const Plan& P, int log2p, bool scatter, std::string* src) {
       << "  for (int b = threadIdx.x; b < NP; b += blockDim.x) s_cnt[b] = 0;\n";
   o << "  __syncthreads();\n"
     << "  const int lane = threadIdx.x & 63;\n"
+    << "  qu32 nfit = 0;\n"
     << "  const qi64 lo = (qi64)blockIdx.x * P.part_tw;\n"
     << "  const qi64 hi = lo + P.part_tw < P.n ? lo + P.part_tw : P.n;\n"
     << "  for (qi64 base = lo + (qi64)(threadIdx.x >> 6) * 256; base < hi; base += (qi64)(blockDim.x >> 6) * 256) {\n"
@@ -660,7 +686,14 @@ bool gen_part_source(const Plan& P, int log2p, bool scatter, std::string* src) {
     o << "      const qu64 pos = atomicAdd(&s_cur[b], 1ull);\n"
       << "      qi64 w[" << L.words << "];\n";
     emit_record_words(P, L, ex, "w", o);
-    if (L.words % 2 == 0) {
+    emit_fit_check(L, "w", o);
+    if (L.narrow) {
+      const int G = L.words % 2 ? 1 : 2;
+      const char* ct = G == 2 ? "qu64" : "qu32";
+      o << "      " << ct << "* dst = (" << ct << "*)(P.part_rec + pos * " << L.bytes() << "ull);\n";
+      for (int q = 0; q < L.words / G; ++q)
+        o << "      dst[" << q << "] = " << narrow_chunk("w", G, std::to_string(q)) << ";\n";
+    } else if (L.words % 2 == 0) {
       o << "      qi64x2* dst = (qi64x2*)(P.part_rec + pos * " << 8 * L.words << "ull);\n";
       for (int q = 0; q < L.words / 2; ++q)
         o << "      dst[" << q << "] = qi64x2{w[" << 2 * q << "], w[" << 2 * q + 1 << "]};\n";
@@ -668,7 +701,9 @@ bool gen_part_source(const Plan& P, int log2p, bool scatter, std::string* src) {
       o << "      qi64* dst = (qi64*)(P.part_rec + pos * " << 8 * L.words << "ull);\n";
       for (int q = 0; q < L.words; ++q) o << "      dst[" << q << "] = w[" << q << "];\n";
     }
-    o << "    }\n  }\n}\n";
+    o << "    }\n  }\n";
+    if (L.narrow) o << "  if (nfit) atomicOr(&P.t.ctl[7], 1ull);\n";
+    o << "}\n";
   }
   *src = std::string(kDevHeader) + o.str();
   return true;
@@ -751,8 +786,9 @@ bool gen_pscatter_staged_source(const Plan& P, int log2p, std::string* src, bool
   std::vector<Expr> ex;
   if (!agg_inputs(P, &ex)) return false;
   const PartLayout L = part_layout(P);
+  if (soa && L.narrow) return false;
   const int W = L.words, G = W % 2 ? 1 : 2;
-  const char* chunk = G == 2 ? "qi64x2" : "qi64";
+  const char* chunk = L.narrow ? (G == 2 ? "qu64" : "qu32") : (G == 2 ? "qi64x2" : "qi64");
   std::ostringstream o;
   o << "\nusing namespace qe;\n"
     << "extern \"C\" __global__ void __launch_bounds__(" << pscatter_block_for(log2p) << ") qe_pscatter(const Plan P) {\n"
@@ -772,6 +808,7 @@ bool gen_pscatter_staged_source(const Plan& P, int log2p, std::string* src, bool
       << "    s_cur[b] = (qu64)P.part_off[(qi64)b * gridDim.x + blockIdx.x];\n    s_hist[b] = 0;\n  }\n";
   o << "  __syncthreads();\n"
     << "  const int lane = threadIdx.x & 63;\n"
+    << "  qu32 nfit = 0;\n"
     << "  const qi64 lo = (qi64)blockIdx.x * P.part_tw;\n"
     << "  const qi64 hi = lo + P.part_tw < P.n ? lo + P.part_tw : P.n;\n"
     << "  const qi64 woff = (qi64)(threadIdx.x >> 6) * 256;\n";
@@ -826,6 +863,7 @@ bool gen_pscatter_staged_source(const Plan& P, int log2p, std::string* src, bool
       << "      bk[r] = (qu32)(fmix64((qu64)key[r]) >> (64 - LOG2P));\n"
       << "      rk[r] = atomicAdd(&s_hist[bk[r]], 1u);\n";
     emit_record_words(P, L, ex, "rw[r]", o);
+    emit_fit_check(L, "rw[r]", o);
     o << "    }\n    } while (0);\n";
     load_into("tile + " + std::to_string(D) + " * (qi64)T + woff", k, "    ");
     o << "    __syncthreads();\n"
@@ -863,7 +901,7 @@ bool gen_pscatter_staged_source(const Plan& P, int log2p, std::string* src, bool
       << "      const qu32 pos = s_off[bk[r]] + rk[r];\n"
       << "      s_bkt[pos] = (unsigned short)bk[r];\n"
       << "#pragma unroll\n      for (int q = 0; q < WC; ++q) s_rec[pos * WC + q] = "
-      << (W % 2 ? "rw[r][q]" : "qi64x2{rw[r][2 * q], rw[r][2 * q + 1]}") << ";\n"
+      << (L.narrow ? narrow_chunk("rw[r]", G, "q") : W % 2 ? "rw[r][q]" : "qi64x2{rw[r][2 * q], rw[r][2 * q + 1]}") << ";\n"
       << "    }\n"
       << "    __syncthreads();\n"
       << "    const qu32 tot = s_total;\n";
@@ -879,7 +917,7 @@ bool gen_pscatter_staged_source(const Plan& P, int log2p, std::string* src, bool
         << "      const qu32 j = c / WC, q = c % WC;\n"
         << (chunked ? "      const qu32 b = s_bkt[j];\n      const qu64 dst = (j < s_lim[b] ? s_dst[b] : s_dst2[b]) + j;\n"
                     : "      const qu64 dst = s_dst[s_bkt[j]] + j;\n")
-        << "      ((" << chunk << "*)(P.part_rec + dst * " << 8 * W << "ull))[q] = s_rec[c];\n"
+        << "      ((" << chunk << "*)(P.part_rec + dst * " << L.bytes() << "ull))[q] = s_rec[c];\n"
         << "    }\n";
     o
       << "  }\n";
@@ -889,6 +927,7 @@ bool gen_pscatter_staged_source(const Plan& P, int log2p, std::string* src, bool
     o << "  __syncthreads();\n"
       << "  for (int b = threadIdx.x; b < NP; b += blockDim.x)\n"
       << "    if (s_chunk[b] >= 0) P.part_chunk[1 + s_chunk[b]] = ((qi64)b << 32) | (qi64)(s_cur[b] - (qu64)s_chunk[b] * PART_CH);\n";
+  if (L.narrow) o << "  if (nfit) atomicOr(&P.t.ctl[7], 1ull);\n";
   o << "}\n";
   *src = std::string(kDevHeader) + o.str();
   return true;
@@ -899,6 +938,7 @@ bool gen_pscatter_staged_source(const Plan& P, int log2p, std::string* src, bool
 bool gen_pagg_source(const Plan& P, int log2, std::string* src, size_t* lds_bytes, bool chunked, bool soa) {
   if (log2 < 4 || log2 > 16 || (soa && !chunked)) return false;
   const PartLayout L = part_layout(P);
+  if (soa && L.narrow) return false;
   std::vector<std::string> val(P.naggs), ok(P.naggs);
   if (L.colmode) {
     // the programs run here, over column values read back from the record (c<slot>[r], v<slot>)
@@ -933,6 +973,7 @@ bool gen_pagg_source(const Plan& P, int log2, std::string* src, size_t* lds_byte
       << "  const bool excl = (hx & PART_EXCL) != 0;\n"
       << "  const qi64 hi = hx & ~PART_EXCL;\n";
   o << "  if (hi <= lo) return;  // (the step prefetch below reads the slice's first record)\n";
+  if (L.narrow) o << "  if (P.t.ctl[7]) return;  // a value did not fit the 32-bit records: the update reruns wide\n";
   o << "  __shared__ int s_fail;\n  __shared__ qu32 s_newg;\n  if (threadIdx.x == 0) { s_fail = 0; s_newg = 0; }\n";
   emit_lds_table(P, o, log2, lds_bytes);
   // the records of the wave's next step are loaded into n* registers before this step's LDS work
@@ -954,7 +995,19 @@ bool gen_pagg_source(const Plan& P, int log2, std::string* src, size_t* lds_byte
       << (chunked ? "        bool on = lane + 64 * r < cfill;\n" : "        bool on = i < hi;\n")
       << "        if (on && P.defer_in) on = (P.defer_in[i >> 5] >> (i & 31)) & 1;\n"
       << "        " << pre << "act |= (qu32)on << r;\n";
-    if (soa) {
+    if (L.narrow) {
+      // 32-bit words, sign-extended (pairs loaded as one 8-byte word when the width is even)
+      const int G = L.words % 2 ? 1 : 2;
+      const char* ct = G == 2 ? "qu64" : "qu32";
+      o << "        const " << ct << "* p = (const " << ct << "*)(P.part_rec + (on ? i : 0) * " << L.bytes() << "ull);\n";
+      for (int q = 0; q < L.words / G; ++q) {
+        o << "        { const " << ct << " v = " << ld(ct, "p + " + std::to_string(q)) << "; ";
+        if (G == 1)
+          o << word(pre, q) << " = (qi64)(qi32)v; }\n";
+        else
+          o << word(pre, 2 * q) << " = (qi64)(qi32)(qu32)v; " << word(pre, 2 * q + 1) << " = (qi64)(qi32)(qu32)(v >> 32); }\n";
+      }
+    } else if (soa) {
       o << "        const qi64* p = (const qi64*)P.part_rec + (on ? (i / PART_CH) * (" << L.words
         << " * PART_CH) + i % PART_CH : 0);\n";
       for (int q = 0; q < L.words; ++q)
@@ -1038,7 +1091,8 @@ bool gen_pagg_source(const Plan& P, int log2, std::string* src, size_t* lds_byte
                   "      const qi64 i = id * PART_CH + ko;\n"
                 : "    for (qi64 i = lo + threadIdx.x; i < hi; i += blockDim.x) {\n")
     << "      if (P.defer_in && !((P.defer_in[i >> 5] >> (i & 31)) & 1)) continue;\n"
-    << (soa ? "      const qi64* rp = (const qi64*)P.part_rec + (i / PART_CH) * (" + std::to_string(L.words) +
+    << (L.narrow ? "      const qi32* rp = (const qi32*)(P.part_rec + i * " + std::to_string(L.bytes()) + "ull);\n"
+        : soa ? "      const qi64* rp = (const qi64*)P.part_rec + (i / PART_CH) * (" + std::to_string(L.words) +
                   " * PART_CH) + i % PART_CH;\n"
             : "      const qi64* rp = (const qi64*)(P.part_rec + i * " + std::to_string(8 * L.words) + "ull);\n")
     << "      const qi64 k = rp[0];\n";

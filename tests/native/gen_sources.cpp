@@ -117,9 +117,21 @@ static int emit_agg(const char* dir, const char* name, const qe_column* cols, in
     fprintf(stderr, "%s: partition sources not generated\n", name);
     return 1;
   }
+  // 32-bit records (Plan.part_narrow; wide again where a word is fp64 or a row index): staged
+  // chunked and direct scatters, chunked and unchunked aggregation passes
+  std::string g, h, i, j;
+  P.part_narrow = 1;
+  if (!gen_pscatter_staged_source(P, 6, &g, true, false) || !gen_part_source(P, 10, true, &h) ||
+      !gen_pagg_source(P, log2, &i, &lds, true, false) || !gen_pagg_source(P, log2, &j, &lds, false, false)) {
+    fprintf(stderr, "%s: narrow partition sources not generated\n", name);
+    return 1;
+  }
   return write_src(dir, std::string(name) + "_fused", a) | write_src(dir, std::string(name) + "_spill", b) |
          write_src(dir, std::string(name) + "_pagg", c) | write_src(dir, std::string(name) + "_pscatter", d) |
-         write_src(dir, std::string(name) + "_pscatter_soa", e) | write_src(dir, std::string(name) + "_pagg_rows", f);
+         write_src(dir, std::string(name) + "_pscatter_soa", e) | write_src(dir, std::string(name) + "_pagg_rows", f) |
+         write_src(dir, std::string(name) + "_pscatter_n32", g) |
+         write_src(dir, std::string(name) + "_pdirect_n32", h) | write_src(dir, std::string(name) + "_pagg_n32", i) |
+         write_src(dir, std::string(name) + "_pagg_unchunked_n32", j);
 }
 
 int main(int argc, char** argv) {

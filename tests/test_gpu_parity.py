@@ -765,6 +765,80 @@ def test_fused_c4_partitioned_vs_oracle(agg_ctx, part_mode, groups, threshold):
         assert kk[0].length == 0
 
 
+NARROW_FNS = [N.AGG_SUM, N.AGG_COUNT_STAR, N.AGG_MIN, N.AGG_MAX]
+
+
+@pytest.mark.parametrize("case", ["fits", "edges", "wide_first", "wide_later"])
+def test_partitioned_narrow_records(agg_ctx, part_mode, case):
+    """Partitioned records in 32-bit words (Plan.part_narrow): integral words are stored narrow while
+    every value of the update survives int32 (sign-extended, INT32_MIN / INT32_MAX included); one
+    value outside it (here a single row, key or input) makes the scatter flag the update, the
+    aggregation pass leaves the table alone and the update reruns with 64-bit words, which the state
+    then keeps. Three batches; results equal the oracle either way."""
+    rng = np.random.default_rng(len(case) * 7)
+    n, groups = 900_000, 80_000
+    k = (rng.integers(0, groups, n).astype(np.int64) - groups // 2) * 20011
+    x = rng.integers(-2**31, 2**31, n).astype(np.int64)
+    if case == "edges":
+        x[::1000] = -2**31
+        x[1::1000] = 2**31 - 1
+        k[5] = 2**31 - 1
+        k[6] = -2**31
+    elif case == "wide_first":
+        x[17] = 2**31  # one row of batch 0
+    elif case == "wide_later":
+        k[2 * n // 3 + 5] = -2**31 - 1  # one key of batch 2
+    st = HashAggregateState(agg_ctx, [N.TYPE_INT64], [(f, N.TYPE_INT64) for f in NARROW_FNS], groups)
+    notes = []
+    for s in range(0, n, n // 3):
+        st.update([dcol(agg_ctx, N.TYPE_INT64, k[s:s + n // 3])], [dcol(agg_ctx, N.TYPE_INT64, x[s:s + n // 3])] * 4)
+        check_partitioned(agg_ctx, st)
+        notes.append(st.last_kernel_kind()[1])
+    if getattr(agg_ctx, "kernel_mode", "jit") == "jit":
+        narrow = ["32-bit" in m for m in notes]
+        assert narrow == {"fits": [True] * 3, "edges": [True] * 3, "wide_first": [False] * 3,
+                          "wide_later": [True, True, False]}[case], notes
+        if narrow[0]:
+            assert "records of 8 B (column words, 32-bit)" in notes[0], notes  # key, x
+    kk, aa = st.finalize()
+    ref = S.group_aggregate([k], [None], [x] * 4, [None] * 4, NARROW_FNS)
+    assert_groups_equal(result_dict(kk, aa), ref, NARROW_FNS)
+
+
+_NARROW_OFF_CHILD = """
+import sys
+sys.path[:0] = [sys.argv[1], sys.argv[1] + "/query-engines_amd"]
+import numpy as np
+from kquery import native as N
+from kquery.aggregate import HashAggregateState
+from kquery.columnar import Context, DeviceColumn
+ctx = Context.get(0)
+k = np.arange(300000, dtype=np.int64) % 100000
+st = HashAggregateState(ctx, [N.TYPE_INT64], [(N.AGG_SUM, N.TYPE_INT64)], 100000)
+st.update([DeviceColumn.from_numpy(N.TYPE_INT64, k, ctx=ctx)], [DeviceColumn.from_numpy(N.TYPE_INT64, 3 * k, ctx=ctx)])
+note = st.last_kernel_kind()[1]
+kk, aa = st.finalize()
+got = dict(zip(kk[0].to_numpy().tolist(), aa[0].to_numpy().tolist()))
+assert note.startswith("radix-partitioned") and "32-bit" not in note, note
+assert got == {i: 9 * i for i in range(100000)}
+print("ok")
+"""
+
+
+def test_partitioned_narrow_off():
+    """QE_PART_NARROW=0 (read once per process, so run in a child process): 64-bit records."""
+    import os
+    import pathlib
+    import subprocess
+    import sys
+
+    root = pathlib.Path(__file__).resolve().parents[1]
+    env = dict(os.environ, QE_PART_NARROW="0")
+    r = subprocess.run([sys.executable, "-c", _NARROW_OFF_CHILD, str(root)], cwd=str(root), env=env,
+                       capture_output=True, text=True, timeout=110)
+    assert r.returncode == 0 and "ok" in r.stdout, r.stderr[-3000:]
+
+
 def _colrec_case(shape, rng, n):
     """(slot arrays, slot valids, slot types, aggs, programs, oracle inputs, predicate term)."""
     from kquery.workloads import _prog, _tok
