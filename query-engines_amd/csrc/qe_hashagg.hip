@@ -2281,8 +2281,10 @@ static int spill_update(qe_hashagg* h, Plan& P, size_t lds, int64_t rows, bool* 
   *used = false;
   const char* e = getenv("QE_MP_SPILL");
   if ((e && e[0] == '0') || P.mp_n != 2) return QE_OK;
+  P.part_narrow = (!h->part_wide && part_narrow_env()) ? 1 : 0;  // 32-bit record words while values fit
+  P.t = h->t;
   const PartLayout L = part_layout(P);
-  const size_t rb = 8 * (size_t)L.words;
+  const size_t rb = (size_t)L.bytes();
   if ((uint64_t)rows * rb > (96ull << 30)) return QE_OK;
   Plan Q = P;
   Q.mp_n = 0;
@@ -2313,6 +2315,7 @@ static int spill_update(qe_hashagg* h, Plan& P, size_t lds, int64_t rows, bool* 
   QE_TRY(ensure_defer(h, cmax * PART_CH));  // the aggregation pass's retry bitmaps index record slots
   *used = true;
   QE_HIP(hipMemsetAsync(meta, 0, 8, ctx->stream));
+  if (L.narrow) QE_HIP(hipMemsetAsync(h->ctl + 7, 0, 8, ctx->stream));
   // kept share: as many groups as one LDS table holds at a 6/8 load, the rest spilled (4096
   // expected groups of the C4 shape: 75 % kept, half the records of an even split). QE_SPILL_LOAD
   // (eighths, 4..7, read per call); 1B rows, 4096 / 5000 groups: 5/8 7.27 / 8.12 ms, 6/8 6.56 /
@@ -2327,11 +2330,34 @@ static int spill_update(qe_hashagg* h, Plan& P, size_t lds, int64_t rows, bool* 
   const uint32_t* defer_in = nullptr;
   // retry passes re-run the spill kernel over deferred rows only: those are bucket-0 rows, so
   // nothing is spilled twice
+  bool misfit = false;
   for (int pass = 0;; ++pass) {
     QE_TRY(launch_pass(h, P, lds, fs, sgrid, pass, 0, out_i, defer_in, sblock));
     bool done = false;
     QE_TRY(settle_pass(h, P, &out_i, &defer_in, &done));
+    misfit = misfit || h->narrow_failed;
     if (done) break;
+  }
+  if (misfit) {
+    // a spilled value did not fit the 32-bit records: the kept rows are aggregated, the records
+    // are not usable. The spilled rows (key hash >= mp_keep) go through one more fused pass over
+    // the columns instead (mp_pass -1), and this state's records are 64-bit from now on.
+    h->narrow_failed = false;
+    h->part_wide = true;
+    Plan R = P;
+    R.part_narrow = 0;
+    R.mp_pass = -1;
+    h->defer_dirty[0] = h->defer_dirty[1] = true;
+    out_i = 0;
+    defer_in = nullptr;
+    for (int pass = 0;; ++pass) {
+      QE_TRY(launch_pass(h, R, lds, nullptr, 0, pass, 1, out_i, defer_in));
+      bool done = false;
+      QE_TRY(settle_pass(h, R, &out_i, &defer_in, &done));
+      if (done) break;
+    }
+    h->jit_note = "multi-pass: 2 buckets, bucket 1 spilled, then re-read (a value outside the 32-bit records)";
+    return QE_OK;
   }
   hipLaunchKernelGGL(k_spill_plan, dim3((unsigned)div_up((uint64_t)cmax, 256)), dim3(256), 0, ctx->stream,
                      (const qi64*)meta, (qi64)tmax, (qi64*)h->part_slc, sorted);
@@ -2351,7 +2377,7 @@ static int spill_update(qe_hashagg* h, Plan& P, size_t lds, int64_t rows, bool* 
     if (done) break;
   }
   h->jit_note = "multi-pass: 2 buckets, bucket 1 spilled as " + std::to_string(rb) + " B records (" +
-                (L.colmode ? "column" : "value") + " words)";
+                (L.colmode ? "column" : "value") + (L.narrow ? " words, 32-bit)" : " words)");
   return QE_OK;
 }
 

@@ -439,6 +439,7 @@ bool agg_inputs(const Plan& P, std::vector<Expr>* ex) {
 
 void emit_record_words(const Plan& P, const PartLayout& L, const std::vector<Expr>& ex, const std::string& dst,
                        std::ostringstream& o);
+static void emit_fit_check(const PartLayout& L, const std::string& w, std::ostringstream& o);
 
 // Returns false when the plan shape is outside what the generator emits (caller uses the
 // generic kernel). `log2` is the LDS table size chosen for this launch.
@@ -469,7 +470,7 @@ bool gen_fused_source(const Plan& P, int log2, std::string* src, size_t* lds_byt
     << "extern \"C\" __global__ void __launch_bounds__(" << fused_block(log2) << ") qe_fused(const Plan P) {\n"
     << "  __shared__ qu32 s_newg;\n  if (threadIdx.x == 0) s_newg = 0;\n";
   if (spill)
-    o << "  __shared__ qi64 s_spc[16];\n  __shared__ qu32 s_spf[16];\n"
+    o << "  __shared__ qi64 s_spc[16];\n  __shared__ qu32 s_spf[16];\n  qu32 nfit = 0;\n"
       << "  if (threadIdx.x < 16) { s_spc[threadIdx.x] = -1; s_spf[threadIdx.x] = 0; }\n";
   emit_lds_table(P, o, log2, lds_bytes);
   o << "  const int lane = threadIdx.x & 63;\n"
@@ -536,21 +537,27 @@ bool gen_fused_source(const Plan& P, int log2, std::string* src, size_t* lds_byt
       << "            const qu64 pos = k < room ? (qu64)cid * PART_CH + fill + k : (qu64)nid * PART_CH + (k - room);\n"
       << "            qi64 w[" << L.words << "];\n";
     emit_record_words(P, L, ex, "w", o);
-    // chunk-columnar: word q of slot `pos` at ((chunk * W + q) * PART_CH + pos % PART_CH) * 8, so the
-    // lanes of one row position store consecutive 8-byte words
-    o << "            qi64* dst = (qi64*)P.part_rec + (pos / PART_CH) * (" << L.words << " * PART_CH) + pos % PART_CH;\n";
-    for (int q = 0; q < L.words; ++q) o << "            dst[" << q << " * PART_CH] = w[" << q << "];\n";
+    emit_fit_check(L, "w", o);
+    // chunk-columnar: word q of slot `pos` at ((chunk * W + q) * PART_CH + pos % PART_CH) * 8 (4 for
+    // 32-bit words), so the lanes of one row position store consecutive words
+    const char* wt = L.narrow ? "qi32" : "qi64";
+    o << "            " << wt << "* dst = (" << wt << "*)P.part_rec + (pos / PART_CH) * (" << L.words << " * PART_CH) + pos % PART_CH;\n";
+    for (int q = 0; q < L.words; ++q)
+      o << "            dst[" << q << " * PART_CH] = " << (L.narrow ? "(qi32)" : "") << "w[" << q << "];\n";
     o << "          }\n          kb += (qu32)__popcll(bal[r]);\n        }\n      }\n    }\n"
       << "    if (act == 0) continue;\n";
   } else if (P.mp_n > 1)
     o << "#pragma unroll\n    for (int r = 0; r < 4; ++r)\n"
-      << "      if (((act >> r) & 1) && (qu32)__umul64hi(fmix64((qu64)key[r]), (qu64)P.mp_n) != (qu32)P.mp_pass) act &= ~(1u << r);\n"
+      << "      if (((act >> r) & 1) && (P.mp_pass < 0 ? (fmix64((qu64)key[r]) >> 32) < P.mp_keep\n"
+      << "                                              : (qu32)__umul64hi(fmix64((qu64)key[r]), (qu64)P.mp_n) != (qu32)P.mp_pass))\n"
+      << "        act &= ~(1u << r);\n"
       << "    if (act == 0) continue;\n";
   emit_agg_rows(P, o, val, ok, "P.row_base + r0 + 128 * (r >> 1) + (r & 1)", "r0 + 128 * (r >> 1) + (r & 1)");
   o << (pf ? "    } while (0);\n  }\n  }\n" : "  }\n");
   if (spill)  // each wave's open chunk: its fill (a wave's LDS writes are seen by its own later reads)
     o << "  if ((threadIdx.x & 63) == 0 && s_spc[threadIdx.x >> 6] >= 0)\n"
-      << "    P.part_chunk[1 + s_spc[threadIdx.x >> 6]] = (qi64)s_spf[threadIdx.x >> 6];\n";
+      << "    P.part_chunk[1 + s_spc[threadIdx.x >> 6]] = (qi64)s_spf[threadIdx.x >> 6];\n"
+      << "  if (nfit) atomicOr(&P.t.ctl[7], 1ull);\n";
   emit_flush(P, o);
   o << "  __syncthreads();\n  if (threadIdx.x == 0 && s_newg) atomicAdd(&P.t.ctl[0], (qu64)s_newg);\n}\n";
   *src = std::string(kDevHeader) + o.str();
@@ -938,7 +945,6 @@ bool gen_pscatter_staged_source(const Plan& P, int log2p, std::string* src, bool
 bool gen_pagg_source(const Plan& P, int log2, std::string* src, size_t* lds_bytes, bool chunked, bool soa) {
   if (log2 < 4 || log2 > 16 || (soa && !chunked)) return false;
   const PartLayout L = part_layout(P);
-  if (soa && L.narrow) return false;
   std::vector<std::string> val(P.naggs), ok(P.naggs);
   if (L.colmode) {
     // the programs run here, over column values read back from the record (c<slot>[r], v<slot>)
@@ -995,7 +1001,12 @@ bool gen_pagg_source(const Plan& P, int log2, std::string* src, size_t* lds_byte
       << (chunked ? "        bool on = lane + 64 * r < cfill;\n" : "        bool on = i < hi;\n")
       << "        if (on && P.defer_in) on = (P.defer_in[i >> 5] >> (i & 31)) & 1;\n"
       << "        " << pre << "act |= (qu32)on << r;\n";
-    if (L.narrow) {
+    if (L.narrow && soa) {
+      o << "        const qi32* p = (const qi32*)P.part_rec + (on ? (i / PART_CH) * (" << L.words
+        << " * PART_CH) + i % PART_CH : 0);\n";
+      for (int q = 0; q < L.words; ++q)
+        o << "        " << word(pre, q) << " = (qi64)" << ld("qi32", "p + " + std::to_string(q) + " * PART_CH") << ";\n";
+    } else if (L.narrow) {
       // 32-bit words, sign-extended (pairs loaded as one 8-byte word when the width is even)
       const int G = L.words % 2 ? 1 : 2;
       const char* ct = G == 2 ? "qu64" : "qu32";
@@ -1091,7 +1102,9 @@ bool gen_pagg_source(const Plan& P, int log2, std::string* src, size_t* lds_byte
                   "      const qi64 i = id * PART_CH + ko;\n"
                 : "    for (qi64 i = lo + threadIdx.x; i < hi; i += blockDim.x) {\n")
     << "      if (P.defer_in && !((P.defer_in[i >> 5] >> (i & 31)) & 1)) continue;\n"
-    << (L.narrow ? "      const qi32* rp = (const qi32*)(P.part_rec + i * " + std::to_string(L.bytes()) + "ull);\n"
+    << (L.narrow && soa ? "      const qi32* rp = (const qi32*)P.part_rec + (i / PART_CH) * (" + std::to_string(L.words) +
+                              " * PART_CH) + i % PART_CH;\n"
+        : L.narrow ? "      const qi32* rp = (const qi32*)(P.part_rec + i * " + std::to_string(L.bytes()) + "ull);\n"
         : soa ? "      const qi64* rp = (const qi64*)P.part_rec + (i / PART_CH) * (" + std::to_string(L.words) +
                   " * PART_CH) + i % PART_CH;\n"
             : "      const qi64* rp = (const qi64*)(P.part_rec + i * " + std::to_string(8 * L.words) + "ull);\n")

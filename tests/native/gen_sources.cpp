@@ -126,12 +126,20 @@ static int emit_agg(const char* dir, const char* name, const qe_column* cols, in
     fprintf(stderr, "%s: narrow partition sources not generated\n", name);
     return 1;
   }
+  // 32-bit chunk-columnar records of the spilling pass and their aggregation pass
+  std::string k, l;
+  P.mp_n = 2;
+  if (!gen_fused_source(P, log2, &k, &lds, true) || !gen_pagg_source(P, log2, &l, &lds, true, true)) {
+    fprintf(stderr, "%s: narrow spill sources not generated\n", name);
+    return 1;
+  }
   return write_src(dir, std::string(name) + "_fused", a) | write_src(dir, std::string(name) + "_spill", b) |
          write_src(dir, std::string(name) + "_pagg", c) | write_src(dir, std::string(name) + "_pscatter", d) |
          write_src(dir, std::string(name) + "_pscatter_soa", e) | write_src(dir, std::string(name) + "_pagg_rows", f) |
          write_src(dir, std::string(name) + "_pscatter_n32", g) |
          write_src(dir, std::string(name) + "_pdirect_n32", h) | write_src(dir, std::string(name) + "_pagg_n32", i) |
-         write_src(dir, std::string(name) + "_pagg_unchunked_n32", j);
+         write_src(dir, std::string(name) + "_pagg_unchunked_n32", j) |
+         write_src(dir, std::string(name) + "_spill_n32", k) | write_src(dir, std::string(name) + "_pagg_soa_n32", l);
 }
 
 int main(int argc, char** argv) {

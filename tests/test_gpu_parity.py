@@ -678,6 +678,37 @@ def test_hashagg_multipass(agg_ctx, mp_mode, vtype, ngroups, expected):
     assert_groups_equal(result_dict(keys, aggs), ref, fns)
 
 
+@pytest.mark.parametrize("case", ["fits", "wide_first", "wide_later"])
+def test_multipass_spill_narrow_records(agg_ctx, monkeypatch, case):
+    """The spilling first pass writes its records in 32-bit words while the spilled values fit int32;
+    when one does not, the kept rows stand, the records are dropped, and the spilled rows (key hash
+    at or above the kept share) are aggregated by one more fused pass over the columns; the state's
+    records are 64-bit afterwards. Two batches; results equal the oracle."""
+    monkeypatch.setenv("QE_MP_SPILL", "1")
+    rng = np.random.default_rng(len(case) + 99)
+    n, groups = 600_000, 4000
+    k = rng.integers(0, groups, n).astype(np.int64) * 104729 + 11
+    x = rng.integers(-2**31, 2**31, n).astype(np.int64)
+    half = 250_001
+    if case == "wide_first":
+        x[:half:50] = 2**40  # every 50th row of batch 0: some of them are spilled
+    elif case == "wide_later":
+        x[half::50] = -2**40
+    st = HashAggregateState(agg_ctx, [N.TYPE_INT64], [(f, N.TYPE_INT64) for f in MP_I64], groups)
+    notes = []
+    for s, e in ((0, half), (half, n)):
+        st.update([dcol(agg_ctx, N.TYPE_INT64, k[s:e])], [dcol(agg_ctx, N.TYPE_INT64, x[s:e])] * len(MP_I64))
+        notes.append(st.last_kernel_kind()[1])
+    if getattr(agg_ctx, "kernel_mode", "jit") == "jit":
+        narrow = "spilled as 8 B records (column words, 32-bit)"
+        wide = "spilled as 16 B records (column words)"
+        expect = {"fits": [narrow, narrow], "wide_first": ["re-read", wide], "wide_later": [narrow, "re-read"]}[case]
+        assert all(x in m for x, m in zip(expect, notes)), notes
+    keys, aggs = st.finalize()
+    ref = S.group_aggregate([k], [None], [x] * len(MP_I64), [None] * len(MP_I64), MP_I64)
+    assert_groups_equal(result_dict(keys, aggs), ref, MP_I64)
+
+
 def test_fused_c4_one_pass_large_table(agg_ctx):
     """2400 groups of the C4 shape: one pass of the specialised kernel over a 4096-slot table
     (152 KiB LDS budget of its 1024-thread workgroups); the generic kernel (80 KiB) partitions."""
