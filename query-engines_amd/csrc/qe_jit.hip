@@ -826,21 +826,58 @@ bool gen_pscatter_staged_source(const Plan& P, int log2p, std::string* src, bool
   // LDS holds the workgroup to 2 per CU, so the buffer registers cost no occupancy.
   const int D = pscatter_depth();
   auto buf = [](int d, const std::string& cs) { return "n" + std::to_string(d) + "_" + cs; };
+  // 8-byte columns are buffered as two 16-byte vectors, loaded straight into them on both the
+  // full-tile and the tail path: with a 4 x int64 buffer filled from a per-load temporary, the
+  // compiler merged the two paths with register moves that waited for each load right after it
+  // was issued (s_waitcnt vmcnt(0) per column), which serialised the prefetch
+  // (QE_PSCATTER_VEC=0 restores that form)
+  static const bool vec = [] {
+    const char* e = getenv("QE_PSCATTER_VEC");
+    return !(e && e[0] == '0');
+  }();
+  auto wide8 = [&](int c) { return vec && (P.cols[c].kind == K_I64 || P.cols[c].kind == K_F64); };
   for (int c = 0; c < P.ncols; ++c)
     for (int d = 0; d < D; ++d) {
-      o << "  qi64 " << buf(d, std::to_string(c)) << "[4] = {0, 0, 0, 0};\n";
+      if (wide8(c))
+        o << "  qi64x2 " << buf(d, std::to_string(c)) << "[2] = {qi64x2{0, 0}, qi64x2{0, 0}};\n";
+      else
+        o << "  qi64 " << buf(d, std::to_string(c)) << "[4] = {0, 0, 0, 0};\n";
       if (P.cols[c].valid) o << "  qu32 v" << buf(d, std::to_string(c)) << " = 0;\n";
     }
   auto load_into = [&](const std::string& nb, int d, const std::string& ind) {
     o << ind << "{\n" << ind << "  const qi64 base = " << nb << ";\n"
       << ind << "  if (base < hi) {\n" << ind << "  const bool full = base + 256 <= P.n;\n"
       << ind << "  const qi64 r0 = base + 2 * lane;\n";
-    emit_col_loads(P, o, ~0u);
+    unsigned rest = 0;
     for (int c = 0; c < P.ncols; ++c) {
+      if (!wide8(c)) {
+        rest |= 1u << c;
+        continue;
+      }
       const std::string cs = std::to_string(c), n = buf(d, cs);
-      o << ind << "  " << n << "[0] = c" << cs << "[0]; " << n << "[1] = c" << cs << "[1]; " << n << "[2] = c" << cs
-        << "[2]; " << n << "[3] = c" << cs << "[3];\n";
-      if (P.cols[c].valid) o << ind << "  v" << n << " = v" << cs << ";\n";
+      o << ind << "  {\n" << ind << "    const qi64* p = (const qi64*)P.cols[" << cs << "].p;\n"
+        << ind << "    if (full) {\n"
+        << ind << "      " << n << "[0] = " << ld("qi64x2", "p + r0") << ";\n"
+        << ind << "      " << n << "[1] = " << ld("qi64x2", "p + r0 + 128") << ";\n"
+        << ind << "    } else {\n"
+        << ind << "      " << n << "[0] = qi64x2{r0 < P.n ? p[r0] : 0, r0 + 1 < P.n ? p[r0 + 1] : 0};\n"
+        << ind << "      " << n << "[1] = qi64x2{r0 + 128 < P.n ? p[r0 + 128] : 0, r0 + 129 < P.n ? p[r0 + 129] : 0};\n"
+        << ind << "    }\n" << ind << "  }\n";
+      if (P.cols[c].valid)
+        o << ind << "  {\n" << ind << "    const qu8* vb = P.cols[" << cs << "].valid;\n"
+          << ind << "    const qu32 lo = (full || r0 < P.n) ? ((qu32)(vb[r0 >> 3] >> (r0 & 7)) & 3u) : 0u;\n"
+          << ind << "    const qu32 hi = (full || r0 + 128 < P.n) ? ((qu32)(vb[(r0 + 128) >> 3] >> (r0 & 7)) & 3u) : 0u;\n"
+          << ind << "    v" << n << " = lo | (hi << 2);\n" << ind << "  }\n";
+    }
+    if (rest) {
+      emit_col_loads(P, o, rest);
+      for (int c = 0; c < P.ncols; ++c) {
+        if (!((rest >> c) & 1u)) continue;
+        const std::string cs = std::to_string(c), n = buf(d, cs);
+        o << ind << "  " << n << "[0] = c" << cs << "[0]; " << n << "[1] = c" << cs << "[1]; " << n << "[2] = c" << cs
+          << "[2]; " << n << "[3] = c" << cs << "[3];\n";
+        if (P.cols[c].valid) o << ind << "  v" << n << " = v" << cs << ";\n";
+      }
     }
     o << ind << "  }\n" << ind << "}\n";
   };
@@ -855,9 +892,12 @@ bool gen_pscatter_staged_source(const Plan& P, int log2p, std::string* src, bool
       << "    qu32 ract = 0, bk[4], rk[4];\n    qi64 rw[4][W];\n"
       << "    const qi64 base = tile + woff;\n";
     for (int c = 0; c < P.ncols; ++c) {
-      const std::string cs = std::to_string(c);
-      o << "    qi64 (&c" << cs << ")[4] = " << buf(k, cs) << ";\n";
-      if (P.cols[c].valid) o << "    const qu32 v" << cs << " = v" << buf(k, cs) << ";\n";
+      const std::string cs = std::to_string(c), n = buf(k, cs);
+      if (wide8(c))
+        o << "    qi64 c" << cs << "[4] = {" << n << "[0].x, " << n << "[0].y, " << n << "[1].x, " << n << "[1].y};\n";
+      else
+        o << "    qi64 (&c" << cs << ")[4] = " << n << ";\n";
+      if (P.cols[c].valid) o << "    const qu32 v" << cs << " = v" << n << ";\n";
     }
     o << "    if (base < hi) do {\n"
       << "    const bool full = base + 256 <= P.n;\n"
@@ -989,11 +1029,14 @@ bool gen_pagg_source(const Plan& P, int log2, std::string* src, size_t* lds_byte
   auto load_step = [&](const std::string& pre, const std::string& nb) {
     o << "    {\n      const qi64 nb = " << nb << ";\n      " << pre << "act = 0;\n";
     if (chunked)
+      // the wave's current chunk (slice index, id, fill) is fetched when a step enters a new one
       o << "      qi64 cfill = 0;\n      " << pre << "pb = 0;\n"
         << "      if (nb < hi) {\n"
-        << "        const qi64 id = P.part_sorted[clo + nb / PART_CH], ko = nb % PART_CH;\n"
-        << "        " << pre << "pb = id * PART_CH + ko;\n"
-        << "        cfill = (P.part_chunk[1 + id] & 0xFFFFFFFFll) - ko;\n      }\n";
+        << "        const qi64 cix = nb / PART_CH, ko = nb % PART_CH;\n"
+        << "        if (cix != mcix) {\n          mcix = cix;\n          mid = P.part_sorted[clo + cix];\n"
+        << "          mfill = P.part_chunk[1 + mid] & 0xFFFFFFFFll;\n        }\n"
+        << "        " << pre << "pb = mid * PART_CH + ko;\n"
+        << "        cfill = mfill - ko;\n      }\n";
     else
       o << "      " << pre << "pb = nb;\n";
     o << "#pragma unroll\n      for (int r = 0; r < 4; ++r) {\n"
@@ -1038,6 +1081,9 @@ bool gen_pagg_source(const Plan& P, int log2, std::string* src, size_t* lds_byte
   o << "  const int lane = threadIdx.x & 63;\n"
     << "  const qi64 step = (qi64)(blockDim.x >> 6) * 256;\n"
     << "  qu32 nact;\n  qi64 nkey[4], npb;\n";
+  if (chunked)
+    o << "  const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), nwv = blockDim.x >> 6;\n"
+      << "  qi64 mcix = -1, mid = 0, mfill = 0;\n";
   for (int q = 1; q < L.words; ++q) o << "  qi64 nw" << q << "[4];\n";
   const char* pfe = getenv("QE_PAGG_PREFETCH");
   const bool pf = !(pfe && pfe[0] == '0');
@@ -1076,7 +1122,22 @@ bool gen_pagg_source(const Plan& P, int log2, std::string* src, size_t* lds_byte
     o << "    }\n    }\n";
   };
   const std::string first = "lo + (qi64)(threadIdx.x >> 6) * 256";
-  if (depth == 2) {
+  // chunk-major walk (chunked slices, one-step prefetch; QE_PAGG_WALK=0: step-major): wave w takes
+  // the slice's chunks w, w + waves, ..., each as PART_CH / 256 consecutive steps, so the chunk
+  // list and fill are read once per 8 steps instead of every step (each such read waited for all
+  // of the wave's outstanding record loads)
+  const char* wke = getenv("QE_PAGG_WALK");
+  const bool walk = chunked && pf && depth == 1 && !(wke && wke[0] == '0');
+  auto NB = [](const std::string& t) {
+    return "((qi64)(wv + ((" + t + ") >> 3) * nwv) * PART_CH + (qi64)((" + t + ") & 7) * 256)";
+  };
+  if (walk) {
+    static_assert(PART_CH == 8 * 256, "chunk-major walk: 8 steps of 256 records per chunk");
+    load_step("n", NB("0"));
+    o << "  for (int t = 0;; ++t) {\n    const qi64 base = " << NB("t") << ";\n    if (base >= hi) break;\n";
+    body("n", "base", NB("t + 1"));
+    o << "  }\n";
+  } else if (depth == 2) {
     load_step("n", first);
     load_step("m", first + " + step");
     o << "  for (qi64 base = " << first << "; base < hi; base += 2 * step) {\n";
