@@ -807,6 +807,7 @@ __global__ void __launch_bounds__(256) k_chunk_hist(const qi64* __restrict__ met
   __syncthreads();
   for (qi64 c = lo + threadIdx.x; c < hi; c += blockDim.x) {
     const qi64 w = meta[1 + c];
+    if (w < 0) continue;  // an unused id of a workgroup's range (part_static)
     const int b = (int)(w >> 32);
     atomicAdd(&s_cnt[b], 1u);
     atomicAdd(&s_rec[b], (unsigned long long)(w & 0xFFFFFFFFll));
@@ -830,12 +831,19 @@ __global__ void __launch_bounds__(1024) k_chunk_slices(const qi64* __restrict__ 
   const int t = threadIdx.x;
   const qu32 c = t < np ? cnt[t] : 0u;
   s_r[t] = t < np ? rec[t] : 0ull;
+  s_a[t] = c;
   __syncthreads();
   for (int d = 512; d > 0; d >>= 1) {
-    if (t < d) s_r[t] += s_r[t + d];
+    if (t < d) {
+      s_r[t] += s_r[t + d];
+      s_a[t] += s_a[t + d];
+    }
     __syncthreads();
   }
-  const qi64 C = meta[0], R = (qi64)s_r[0];
+  // chunks in use (meta[0] may also count unused ids of the workgroups' ranges)
+  const qi64 C = (qi64)s_a[0], R = (qi64)s_r[0];
+  (void)meta;
+  __syncthreads();
   const qi64 target = max((qi64)np, min(tmax, R >> 15));
   const qi64 cpc = max((qi64)1, (5 * C + 4 * target - 1) / (4 * target));
   const qu32 ns = (qu32)((c + cpc - 1) / cpc);
@@ -876,7 +884,7 @@ __global__ void __launch_bounds__(256) k_chunk_place(const qi64* __restrict__ me
   for (int i = 0; i < PER; ++i) {
     const qi64 c = lo + threadIdx.x + 256 * i;
     bk[i] = -1;
-    if (c < C) {
+    if (c < C && meta[1 + c] >= 0) {
       bk[i] = (int)(meta[1 + c] >> 32);
       rk[i] = atomicAdd(&s_cnt[bk[i]], 1u);
     }
@@ -1952,7 +1960,9 @@ static int partition_rows(qe_hashagg* h, Plan& P, hipFunction_t* fn, int* grid) 
   const int64_t tw = (int64_t)div_up(div_up((uint64_t)n, (uint64_t)g), 256) * 256;
   g = (int64_t)div_up((uint64_t)n, (uint64_t)tw);
   const int64_t open_slots = g * np_all * PART_CH;
-  const int64_t cmax = (int64_t)div_up((uint64_t)n, (uint64_t)PART_CH) + g * np_all + 1;
+  // chunk ids: every claim of a device-wide counter, or each workgroup's own range (part_static)
+  const int64_t cmax = std::max<int64_t>((int64_t)div_up((uint64_t)n, (uint64_t)PART_CH) + g * np_all + 1,
+                                         g * ((int64_t)div_up((uint64_t)tw, (uint64_t)PART_CH) + np_all));
   const bool chunked = chunk_env != 0 && staged && np_all <= CHUNK_PLAN_MAXB &&
                        (chunk_env == 1 || open_slots <= n) && (uint64_t)cmax * PART_CH * rb <= (96ull << 30);
   QE_CHECK((chunked || gen_part_source(P, log2p, false, &sc)) &&

@@ -102,6 +102,7 @@ int fused_block(int lds_log2);
 int hashagg_expected_groups(const qe_hashagg* h, int64_t* out);
 qe_ctx* hashagg_ctx(const qe_hashagg* h);
 bool gen_pscatter_staged_source(const qe::Plan& P, int log2p, std::string* src, bool chunked = false, bool soa = false);
+bool part_static();  // chunked staged scatter: per-workgroup chunk id ranges (QE_PART_STATIC)
 bool part_soa();  // chunked partition records stored chunk-columnar (QE_PART_SOA)
 int jit_kernel(qe_ctx* ctx, const std::string& src, hipFunction_t* fn, int* blocks_per_cu,
                const char* name = "qe_fused", int block = 512);

@@ -724,6 +724,7 @@ bool gen_part_source(const Plan& P, int log2p, bool scatter, std::string* src) {
 // (bucket, workgroup) ranges as the direct scatter: the records of one bucket and workgroup keep
 // a contiguous range of its bucket (their order inside it may differ run to run).
 bool part_staged_ok(const Plan& P, int log2p) {
+  if (P.n < 2) return false;  // (the staged scatter's prefetch loads row pairs clamped to n - 2)
   if (log2p == 10) return pscatter_wide() && part_layout(P).words <= 3;
   return log2p <= 9 && part_layout(P).words * pscatter_block() <= 8 * 256;
 }
@@ -787,6 +788,20 @@ bool part_soa() {
   return v;
 }
 
+// Chunk ids of the chunked staged scatter (QE_PART_STATIC, default 1): each workgroup owns the
+// range [blockIdx.x * cpw, (blockIdx.x + 1) * cpw), cpw = its rows / PART_CH rounded up + buckets
+// (every closed chunk is full, so a workgroup never needs more), and claims from it with an LDS
+// counter; unused ids are marked -1 (skipped by the chunk planning). 0: one device-wide counter
+// (a device atomic with a return value per claim, which waits for every load the claiming wave
+// has in flight).
+bool part_static() {
+  static const bool v = [] {
+    const char* e = getenv("QE_PART_STATIC");
+    return !(e && e[0] == '0');
+  }();
+  return v;
+}
+
 bool gen_pscatter_staged_source(const Plan& P, int log2p, std::string* src, bool chunked, bool soa) {
   if (soa && !chunked) return false;
   if (P.ncols < 1 || P.ncols > QE_MAX_COLS || log2p < 1 || !part_staged_ok(P, log2p)) return false;
@@ -809,7 +824,10 @@ bool gen_pscatter_staged_source(const Plan& P, int log2p, std::string* src, bool
     o << "  __shared__ qu64 s_end[NP];\n  __shared__ qu64 s_dst2[NP];\n  __shared__ qu32 s_lim[NP];\n"
       << "  __shared__ qi32 s_chunk[NP];\n"
       << "  for (int b = threadIdx.x; b < NP; b += blockDim.x) {\n"
-      << "    s_cur[b] = 0;\n    s_end[b] = 0;\n    s_chunk[b] = -1;\n    s_hist[b] = 0;\n  }\n";
+      << "    s_cur[b] = 0;\n    s_end[b] = 0;\n    s_chunk[b] = -1;\n    s_hist[b] = 0;\n  }\n"
+      << (part_static() ? "  __shared__ qu32 s_cnext;\n  if (threadIdx.x == 0) s_cnext = 0;\n"
+                          "  const qi64 cpw = (P.part_tw + PART_CH - 1) / PART_CH + NP, cbase = (qi64)blockIdx.x * cpw;\n"
+                        : "");
   else
     o << "  for (int b = threadIdx.x; b < NP; b += blockDim.x) {\n"
       << "    s_cur[b] = (qu64)P.part_off[(qi64)b * gridDim.x + blockIdx.x];\n    s_hist[b] = 0;\n  }\n";
@@ -831,9 +849,11 @@ bool gen_pscatter_staged_source(const Plan& P, int log2p, std::string* src, bool
   // compiler merged the two paths with register moves that waited for each load right after it
   // was issued (s_waitcnt vmcnt(0) per column), which serialised the prefetch
   // (QE_PSCATTER_VEC=0 restores that form)
-  static const bool vec = [] {
+  // (QE_PSCATTER_VEC=1: vector buffers loaded under the full-tile / in-range branches, = 2 default:
+  // loaded unconditionally, below)
+  static const int vec = [] {
     const char* e = getenv("QE_PSCATTER_VEC");
-    return !(e && e[0] == '0');
+    return e && *e ? std::max(0, std::min(2, atoi(e))) : 2;
   }();
   auto wide8 = [&](int c) { return vec && (P.cols[c].kind == K_I64 || P.cols[c].kind == K_F64); };
   for (int c = 0; c < P.ncols; ++c)
@@ -846,8 +866,13 @@ bool gen_pscatter_staged_source(const Plan& P, int log2p, std::string* src, bool
     }
   auto load_into = [&](const std::string& nb, int d, const std::string& ind) {
     o << ind << "{\n" << ind << "  const qi64 base = " << nb << ";\n"
-      << ind << "  if (base < hi) {\n" << ind << "  const bool full = base + 256 <= P.n;\n"
       << ind << "  const qi64 r0 = base + 2 * lane;\n";
+    // Vector buffers load unconditionally, from row indices clamped to [0, n - 2] (the staged
+    // scatter runs only when n >= 2; rows at or past n are masked by act when the tile is used,
+    // and a tile past the workgroup's range is never used): the same load instructions issue on
+    // every path, so the wait before a buffer is consumed can leave the later buffers' loads in
+    // flight (a load under a branch left the in-order count unknown, and the compiler waited for
+    // every outstanding load)
     unsigned rest = 0;
     for (int c = 0; c < P.ncols; ++c) {
       if (!wide8(c)) {
@@ -855,20 +880,29 @@ bool gen_pscatter_staged_source(const Plan& P, int log2p, std::string* src, bool
         continue;
       }
       const std::string cs = std::to_string(c), n = buf(d, cs);
-      o << ind << "  {\n" << ind << "    const qi64* p = (const qi64*)P.cols[" << cs << "].p;\n"
-        << ind << "    if (full) {\n"
-        << ind << "      " << n << "[0] = " << ld("qi64x2", "p + r0") << ";\n"
-        << ind << "      " << n << "[1] = " << ld("qi64x2", "p + r0 + 128") << ";\n"
-        << ind << "    } else {\n"
-        << ind << "      " << n << "[0] = qi64x2{r0 < P.n ? p[r0] : 0, r0 + 1 < P.n ? p[r0 + 1] : 0};\n"
-        << ind << "      " << n << "[1] = qi64x2{r0 + 128 < P.n ? p[r0 + 128] : 0, r0 + 129 < P.n ? p[r0 + 129] : 0};\n"
-        << ind << "    }\n" << ind << "  }\n";
+      if (vec == 1)
+        o << ind << "  if (base < hi) {\n" << ind << "    const qi64* p = (const qi64*)P.cols[" << cs << "].p;\n"
+          << ind << "    if (base + 256 <= P.n) {\n"
+          << ind << "      " << n << "[0] = " << ld("qi64x2", "p + r0") << ";\n"
+          << ind << "      " << n << "[1] = " << ld("qi64x2", "p + r0 + 128") << ";\n"
+          << ind << "    } else {\n"
+          << ind << "      " << n << "[0] = qi64x2{r0 < P.n ? p[r0] : 0, r0 + 1 < P.n ? p[r0 + 1] : 0};\n"
+          << ind << "      " << n << "[1] = qi64x2{r0 + 128 < P.n ? p[r0 + 128] : 0, r0 + 129 < P.n ? p[r0 + 129] : 0};\n"
+          << ind << "    }\n" << ind << "  }\n";
+      else
+        o << ind << "  {\n" << ind << "    const qi64* p = (const qi64*)P.cols[" << cs << "].p;\n"
+          << ind << "    const qi64 lim = P.n - 2, i0 = r0 < lim ? r0 : lim, i1 = r0 + 128 < lim ? r0 + 128 : lim;\n"
+          << ind << "    " << n << "[0] = " << ld("qi64x2", "p + i0") << ";\n"
+          << ind << "    " << n << "[1] = " << ld("qi64x2", "p + i1") << ";\n"
+          << ind << "  }\n";
       if (P.cols[c].valid)
         o << ind << "  {\n" << ind << "    const qu8* vb = P.cols[" << cs << "].valid;\n"
-          << ind << "    const qu32 lo = (full || r0 < P.n) ? ((qu32)(vb[r0 >> 3] >> (r0 & 7)) & 3u) : 0u;\n"
-          << ind << "    const qu32 hi = (full || r0 + 128 < P.n) ? ((qu32)(vb[(r0 + 128) >> 3] >> (r0 & 7)) & 3u) : 0u;\n"
+          << ind << "    const qi64 lim = P.n - 1, i0 = r0 < lim ? r0 : lim, i1 = r0 + 128 < lim ? r0 + 128 : lim;\n"
+          << ind << "    const qu32 lo = (qu32)(vb[i0 >> 3] >> (r0 & 7)) & 3u;\n"
+          << ind << "    const qu32 hi = (qu32)(vb[i1 >> 3] >> (r0 & 7)) & 3u;\n"
           << ind << "    v" << n << " = lo | (hi << 2);\n" << ind << "  }\n";
     }
+    o << ind << "  if (base < hi) {\n" << ind << "  const bool full = base + 256 <= P.n;\n";
     if (rest) {
       emit_col_loads(P, o, rest);
       for (int c = 0; c < P.ncols; ++c) {
@@ -893,7 +927,10 @@ bool gen_pscatter_staged_source(const Plan& P, int log2p, std::string* src, bool
       << "    const qi64 base = tile + woff;\n";
     for (int c = 0; c < P.ncols; ++c) {
       const std::string cs = std::to_string(c), n = buf(k, cs);
-      if (wide8(c))
+      if (wide8(c) && vec == 2)  // (a pair clamped at the column's end holds the last row in .y)
+        o << "    qi64 c" << cs << "[4] = {base + 2 * lane + 1 < P.n ? " << n << "[0].x : " << n << "[0].y, " << n
+          << "[0].y, base + 2 * lane + 129 < P.n ? " << n << "[1].x : " << n << "[1].y, " << n << "[1].y};\n";
+      else if (wide8(c))
         o << "    qi64 c" << cs << "[4] = {" << n << "[0].x, " << n << "[0].y, " << n << "[1].x, " << n << "[1].y};\n";
       else
         o << "    qi64 (&c" << cs << ")[4] = " << n << ";\n";
@@ -912,7 +949,15 @@ bool gen_pscatter_staged_source(const Plan& P, int log2p, std::string* src, bool
     emit_record_words(P, L, ex, "rw[r]", o);
     emit_fit_check(L, "rw[r]", o);
     o << "    }\n    } while (0);\n";
-    load_into("tile + " + std::to_string(D) + " * (qi64)T + woff", k, "    ");
+    // QE_PSCATTER_RELOAD=1 (default): the buffer is reloaded after the scan, whose chunk claims
+    // (a device atomic with a return value) would otherwise wait for wave 0's just-issued loads
+    // (in-order vmcnt); 0: reloaded before the scan
+    static const bool late = [] {
+      const char* e = getenv("QE_PSCATTER_RELOAD");
+      return !(e && e[0] == '0');
+    }();
+    const std::string reload_at = "tile + " + std::to_string(D) + " * (qi64)T + woff";
+    if (!(late && chunked)) load_into(reload_at, k, "    ");
     o << "    __syncthreads();\n"
       // exclusive scan of the tile histogram by wave 0
       << "    if (threadIdx.x < 64) {\n"
@@ -930,7 +975,8 @@ bool gen_pscatter_staged_source(const Plan& P, int log2p, std::string* src, bool
         << "          s_off[b] = e;\n          const qu64 c = s_cur[b], room = s_end[b] - c;\n          s_dst[b] = c - e;\n"
         << "          if (loc[i] > room) {\n"
         << "            if (s_chunk[b] >= 0) P.part_chunk[1 + s_chunk[b]] = ((qi64)b << 32) | PART_CH;\n"
-        << "            const qi64 id = (qi64)atomicAdd((unsigned long long*)P.part_chunk, 1ull);\n"
+        << (part_static() ? "            const qi64 id = cbase + (qi64)atomicAdd(&s_cnext, 1u);\n"
+                          : "            const qi64 id = (qi64)atomicAdd((unsigned long long*)P.part_chunk, 1ull);\n")
         << "            const qu64 nb = (qu64)id * PART_CH;\n"
         << "            s_lim[b] = e + (qu32)room;\n            s_dst2[b] = nb - (e + room);\n"
         << "            s_cur[b] = nb + (loc[i] - room);\n            s_end[b] = nb + PART_CH;\n            s_chunk[b] = (qi32)id;\n"
@@ -941,8 +987,9 @@ bool gen_pscatter_staged_source(const Plan& P, int log2p, std::string* src, bool
     o << "        e += loc[i];\n      }\n"
       << "      if (lane == 63) s_total = x;\n"
       << "    }\n"
-      << "    __syncthreads();\n"
-      << "    for (int b = threadIdx.x; b < NP; b += blockDim.x) s_hist[b] = 0;\n"
+      << "    __syncthreads();\n";
+    if (late && chunked) load_into(reload_at, k, "    ");
+    o << "    for (int b = threadIdx.x; b < NP; b += blockDim.x) s_hist[b] = 0;\n"
       << "#pragma unroll\n    for (int r = 0; r < 4; ++r) {\n"
       << "      if (!((ract >> r) & 1)) continue;\n"
       << "      const qu32 pos = s_off[bk[r]] + rk[r];\n"
@@ -974,6 +1021,9 @@ bool gen_pscatter_staged_source(const Plan& P, int log2p, std::string* src, bool
     o << "  __syncthreads();\n"
       << "  for (int b = threadIdx.x; b < NP; b += blockDim.x)\n"
       << "    if (s_chunk[b] >= 0) P.part_chunk[1 + s_chunk[b]] = ((qi64)b << 32) | (qi64)(s_cur[b] - (qu64)s_chunk[b] * PART_CH);\n";
+  if (chunked && part_static())  // the range's unused chunk ids are marked empty; block 0 writes the id count
+    o << "  for (qi64 c = (qi64)s_cnext + threadIdx.x; c < cpw; c += blockDim.x) P.part_chunk[1 + cbase + c] = -1;\n"
+      << "  if (blockIdx.x == 0 && threadIdx.x == 0) P.part_chunk[0] = (qi64)gridDim.x * cpw;\n";
   if (L.narrow) o << "  if (nfit) atomicOr(&P.t.ctl[7], 1ull);\n";
   o << "}\n";
   *src = std::string(kDevHeader) + o.str();

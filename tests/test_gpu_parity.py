@@ -836,6 +836,23 @@ def test_partitioned_narrow_records(agg_ctx, part_mode, case):
     assert_groups_equal(result_dict(kk, aa), ref, NARROW_FNS)
 
 
+@pytest.mark.parametrize("n", [1, 2, 3, 255, 257, 4097])
+def test_partitioned_tiny_batches(agg_ctx, part_mode, n):
+    """Partitioned updates of a few rows: the staged scatter's prefetch loads row pairs clamped to
+    the column's last pair (n >= 2; one row goes to the direct scatter), so the odd last row of a
+    batch must come from the pair's upper half. Every row selected, nullable key."""
+    rng = np.random.default_rng(n)
+    k = rng.integers(-2**30, 2**30, n).astype(np.int64)
+    kv = rng.random(n) > 0.1
+    x = rng.integers(-2**20, 2**20, n).astype(np.int64)
+    st = HashAggregateState(agg_ctx, [N.TYPE_INT64], [(f, N.TYPE_INT64) for f in NARROW_FNS], 100_000)
+    st.update([dcol(agg_ctx, N.TYPE_INT64, k, kv)], [dcol(agg_ctx, N.TYPE_INT64, x)] * 4)
+    check_partitioned(agg_ctx, st)
+    kk, aa = st.finalize()
+    ref = S.group_aggregate([k], [kv], [x] * 4, [None] * 4, NARROW_FNS)
+    assert_groups_equal(result_dict(kk, aa), ref, NARROW_FNS)
+
+
 _NARROW_OFF_CHILD = """
 import sys
 sys.path[:0] = [sys.argv[1], sys.argv[1] + "/query-engines_amd"]
