@@ -1177,12 +1177,49 @@ bool gen_pagg_source(const Plan& P, int log2, std::string* src, size_t* lds_byte
   // list and fill are read once per 8 steps instead of every step (each such read waited for all
   // of the wave's outstanding record loads)
   const char* wke = getenv("QE_PAGG_WALK");
-  const bool walk = chunked && pf && depth == 1 && !(wke && wke[0] == '0');
+  const int walk_lvl = wke && *wke ? atoi(wke) : 2;
+  const bool walk = chunked && pf && depth == 1 && walk_lvl >= 1;
   auto NB = [](const std::string& t) {
     return "((qi64)(wv + ((" + t + ") >> 3) * nwv) * PART_CH + (qi64)((" + t + ") & 7) * 256)";
   };
-  if (walk) {
+  // QE_PAGG_WALK=2 (default): two record buffers, each consumed in place and reloaded only after
+  // its step's LDS work. With one buffer the step first copied the buffer out (so that the next
+  // step's loads could target it), and every copy waited for all of the wave's outstanding loads
+  // (in-order vmcnt): four serialised load round trips per step.
+  auto body2 = [&](const std::string& pre, const std::string& nb) {
+    o << "    {\n    const qi64 sbase = " << pre << "pb;\n"
+      << "    const qu32 act = " << pre << "act;\n    qu32 knull = 0;\n"
+      << "    qi64 (&key)[4] = " << pre << "key;\n";
+    for (int q = 1; q < L.words; ++q) o << "    qi64 (&w" << q << ")[4] = " << pre << "w" << q << ";\n";
+    if (L.flags_word >= 0)
+      o << "#pragma unroll\n    for (int r = 0; r < 4; ++r) knull |= (qu32)(w" << L.flags_word << "[r] & 1) << r;\n";
+    for (int c = 0; c < P.ncols; ++c) {
+      if (L.col_word[c] < 0) continue;
+      const std::string cs = std::to_string(c);
+      o << "    qi64 (&c" << cs << ")[4] = w" << L.col_word[c] << ";\n";
+      if (P.cols[c].valid)
+        o << "    qu32 v" << cs << " = 0;\n"
+          << "#pragma unroll\n    for (int r = 0; r < 4; ++r) v" << cs << " |= ((qu32)(w" << L.flags_word << "[r] >> "
+          << (1 + c) << ") & 1u) << r;\n";
+    }
+    o << "    if (act != 0) {\n";
+    emit_agg_rows(P, o, val, ok, L.row_word >= 0 ? "w" + std::to_string(L.row_word) + "[r]" : "0",
+                  "sbase + lane + 64 * r");
+    o << "    }\n    }\n";
+    load_step(pre, nb);
+  };
+  if (walk && walk_lvl >= 2) {
     static_assert(PART_CH == 8 * 256, "chunk-major walk: 8 steps of 256 records per chunk");
+    o << "  qu32 mact;\n  qi64 mkey[4], mpb;\n";
+    for (int q = 1; q < L.words; ++q) o << "  qi64 mw" << q << "[4];\n";
+    load_step("n", NB("0"));
+    load_step("m", NB("1"));
+    o << "  for (int t = 0;; t += 2) {\n    if (" << NB("t") << " >= hi) break;\n";
+    body2("n", NB("t + 2"));
+    o << "    if (" << NB("t + 1") << " >= hi) break;\n";
+    body2("m", NB("t + 3"));
+    o << "  }\n";
+  } else if (walk) {
     load_step("n", NB("0"));
     o << "  for (int t = 0;; ++t) {\n    const qi64 base = " << NB("t") << ";\n    if (base >= hi) break;\n";
     body("n", "base", NB("t + 1"));
