@@ -1177,15 +1177,16 @@ bool gen_pagg_source(const Plan& P, int log2, std::string* src, size_t* lds_byte
   // list and fill are read once per 8 steps instead of every step (each such read waited for all
   // of the wave's outstanding record loads)
   const char* wke = getenv("QE_PAGG_WALK");
-  const int walk_lvl = wke && *wke ? atoi(wke) : 2;
+  const int walk_lvl = wke && *wke ? atoi(wke) : 1;
   const bool walk = chunked && pf && depth == 1 && walk_lvl >= 1;
   auto NB = [](const std::string& t) {
     return "((qi64)(wv + ((" + t + ") >> 3) * nwv) * PART_CH + (qi64)((" + t + ") & 7) * 256)";
   };
-  // QE_PAGG_WALK=2 (default): two record buffers, each consumed in place and reloaded only after
-  // its step's LDS work. With one buffer the step first copied the buffer out (so that the next
-  // step's loads could target it), and every copy waited for all of the wave's outstanding loads
-  // (in-order vmcnt): four serialised load round trips per step.
+  // QE_PAGG_WALK=2: two record buffers, each consumed in place and reloaded only after its step's
+  // LDS work. With one buffer (default) the step first copies the buffer out so that the next
+  // step's loads can target it, and the ISA shows each copy waiting for all of the wave's
+  // outstanding loads (in-order vmcnt). Measured anyway (1B rows, 8K / 64K / 1M groups, one box):
+  // two buffers 8.07 / 8.68 / 14.23 ms, one 7.98 / 8.57 / 14.04: sixteen waves per CU hide it.
   auto body2 = [&](const std::string& pre, const std::string& nb) {
     o << "    {\n    const qi64 sbase = " << pre << "pb;\n"
       << "    const qu32 act = " << pre << "act;\n    qu32 knull = 0;\n"

@@ -6,7 +6,7 @@ set -o pipefail
 export TMPDIR=/tmp
 OUT=gpurun_out/vec
 mkdir -p $OUT
-timeout -k 10 300 python -u -m pytest tests/test_gpu_parity.py -x -q --timeout 200 --timeout-method thread -k "partitioned or multipass or narrow or spill or tiny or adapts" > $OUT/tests.log 2>&1 || { tail -40 $OUT/tests.log; exit 1; }
+timeout -k 10 700 python -u -m pytest tests/test_gpu_parity.py -x -q --timeout 200 --timeout-method thread -k "partitioned or multipass or narrow or spill or tiny or adapts" > $OUT/tests.log 2>&1 || { tail -40 $OUT/tests.log; exit 1; }
 tail -2 $OUT/tests.log
 run() {  # name, env...
   local name=$1; shift
