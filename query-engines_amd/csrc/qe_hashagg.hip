@@ -1988,7 +1988,15 @@ static int partition_rows(qe_hashagg* h, Plan& P, hipFunction_t* fn, int* grid) 
     qu32* pcur = pcnt + np;
     qu32* pbase = pcur + np;
     QE_TRY(grow_buffer(&h->part_rec, &h->part_rec_bytes, (size_t)cmax * PART_CH * rb, ctx, "partition records"));
-    const int64_t tmax = (int64_t)ctx->num_cus * 8;
+    // aggregation slices: at most QE_PAGG_SLICES_PER_CU (default 8) per CU. One 1024-thread
+    // workgroup runs per CU either way; more slices balance better, fewer flush less (each slice
+    // of a bucket flushes every group it saw with device-scope atomics)
+    static const int spc = [] {
+      const char* e = getenv("QE_PAGG_SLICES_PER_CU");
+      const int v = e && *e ? atoi(e) : 8;
+      return v >= 1 && v <= 64 ? v : 8;
+    }();
+    const int64_t tmax = (int64_t)ctx->num_cus * spc;
     const int64_t max_slices = tmax + np;
     QE_TRY(grow_buffer(&h->part_slc, &h->part_slc_bytes, (size_t)(2 + 2 * max_slices) * 8, ctx, "partition slices"));
     if (!h->ovf || h->ovf_cap < (1ull << 20)) {
