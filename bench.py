@@ -181,6 +181,19 @@ def launch_ranks(args) -> int:
     return proc.wait()
 
 
+def rank_plan(world: int, rank: int, local: int, backend: str, ndev: int, exchange: bool) -> dict:
+    """This rank's device and process-group plan from the launcher environment. One RCCL rank per
+    GPU: rank `local` drives cuda:`local` and binds its communicator to it (device_id); more ranks
+    than GPUs only in a gloo rehearsal (ranks then share devices, no device_id)."""
+    plan = {"world_size": world, "rank": rank, "local_rank": local, "backend": backend, "visible_gpus": ndev,
+            "device": local % max(1, ndev), "device_id": None, "process_group": world > 1 or exchange}
+    if world > 1 and backend == "nccl" and ndev < world:
+        plan["error"] = f"bench: {world} RCCL ranks need {world} visible GPUs, found {ndev}"
+    if plan["process_group"] and backend == "nccl":
+        plan["device_id"] = f"cuda:{plan['device']}"
+    return plan
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -202,7 +215,12 @@ def main():
                     help="N > 1: records per exchange slot (0: qe_hashagg_slot_capacity); a small value forces "
                          "the variable-size fallback")
     ap.add_argument("--verify-cpu", action="store_true",
-                    help="N > 1: rank 0 checks every owner's groups against the CPU port over all ranks' rows")
+                    help="check every owner's groups against the CPU port over all ranks' rows (default for N > 1)")
+    ap.add_argument("--no-verify-cpu", action="store_true", help="N > 1: skip that check")
+    ap.add_argument("--dry-run", action="store_true",
+                    help="print this rank's device plan (backend, device, device_id) as JSON and exit before any "
+                         "GPU or process-group call (launcher-environment check)")
+    ap.add_argument("--assume-gpus", type=int, default=-1, help="--dry-run only: visible GPU count to plan for")
     args = ap.parse_args()
 
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
@@ -222,19 +240,22 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
         print(f"warning: --gpus {args.gpus} but WORLD_SIZE {world}; using WORLD_SIZE", file=sys.stderr)
-    ndev = torch.cuda.device_count()
-    if world > 1 and args.dist_backend == "nccl" and ndev < world:
-        sys.exit(f"bench: {world} RCCL ranks need {world} visible GPUs, found {ndev}")
-    # one rank per GPU; more ranks than GPUs only in a gloo rehearsal (ranks then share devices)
-    device = local % max(1, ndev)
+    ndev = args.assume_gpus if args.dry_run and args.assume_gpus >= 0 else torch.cuda.device_count()
+    plan = rank_plan(world, rank, local, args.dist_backend, ndev, args.exchange)
+    if args.dry_run:
+        print(json.dumps(plan), flush=True)
+        return 0 if "error" not in plan else 2
+    if "error" in plan:
+        sys.exit(plan["error"])
+    device = plan["device"]
     torch.cuda.set_device(device)
-    if world > 1 or args.exchange:
+    if plan["process_group"]:
         for k, v in (("MASTER_ADDR", "127.0.0.1"), ("MASTER_PORT", "29511"), ("RANK", "0"), ("WORLD_SIZE", "1")):
             os.environ.setdefault(k, v)
-        if args.dist_backend == "nccl":
-            dist.init_process_group("nccl", device_id=torch.device("cuda", device))
+        if plan["device_id"] is not None:
+            dist.init_process_group(plan["backend"], device_id=torch.device(plan["device_id"]))
         else:
-            dist.init_process_group(args.dist_backend)
+            dist.init_process_group(plan["backend"])
         world = dist.get_world_size()
         rank = dist.get_rank()
     from kquery.exchange import NativeComm, exchange_partials, exchange_partials_native
@@ -337,7 +358,7 @@ def main():
     rv = [r.to_numpy() for r in res]
     my_groups = {int(kv[i]): tuple(int(r[i]) for r in rv) for i in range(keys[0].length)}
     check = {"groups": n_groups, "count_star_total": count_total, "count_star_torch": selected_total}
-    if world > 1 and args.verify_cpu:
+    if world > 1 and (args.verify_cpu or not args.no_verify_cpu):
         # union of the owners' groups == the CPU port over every rank's rows (rows 0 .. world*rows)
         everyone = [None] * world
         dist.all_gather_object(everyone, my_groups)
@@ -351,7 +372,9 @@ def main():
             lib, G = _cpu_lib()
             out = (G * 2048)()
             ng = C.c_int64()
-            lib.qe_cpu_c4(0, world * rows, 42, len(os.sched_getaffinity(0)), 1 << 19, 1024, out, 2048, C.byref(ng))
+            # the tuned CPU leg (per-thread open-addressing tables, oracle/cpu_baseline.c), after the
+            # timed region: 8 ranks x 1B rows take seconds, not minutes
+            lib.qe_cpu_c4_fast(0, world * rows, 42, usable_cpus(), 1 << 19, 1024, out, 2048, C.byref(ng))
             want = {int(g.key): (int(g.sum), int(g.count), int(g.min), int(g.max)) for g in out[:ng.value]}
             if union != want:
                 bad = sorted(k for k in set(union) | set(want) if union.get(k) != want.get(k))
@@ -406,6 +429,10 @@ def main():
         },
         "check": check,
     }
+    if world > 1 or exchange:
+        line["comm"] = {"backend": args.dist_backend, "impl": args.exchange_impl,
+                        "rccl_version": (".".join(str(x) for x in torch.cuda.nccl.version())
+                                         if args.dist_backend == "nccl" else None)}
     if rank == 0 and world == 1 and not args.no_cpu:
         threads = args.cpu_threads or usable_cpus()
         sample = args.cpu_sample_rows or rows

@@ -587,6 +587,12 @@ int qe_csv_column(const qe_csv_table* table, int32_t i, qe_column* out);
 int qe_csv_column_bytes(const qe_csv_table* table, int32_t i, int64_t* nbytes);
 int qe_csv_column_copy(const qe_csv_table* table, int32_t i, qe_column* dst);
 int qe_csv_destroy(qe_csv_table* table);
+/* Streaming a file larger than one device batch (ReaderIterator's batches, K:239-252): host bytes
+ * data[0, nbytes) that start at a record boundary are cut after their last complete record.
+ * *cut = the end of the last record terminator outside quotes (a '\r' at the very end does not
+ * count: a '\n' may follow), 0 if there is none (the caller reads more), nbytes when eof != 0.
+ * Host only; the bytes [*cut, nbytes) begin the next chunk. */
+int qe_csv_record_end(const uint8_t* data, int64_t nbytes, int32_t eof, int64_t* cut);
 
 #ifdef __cplusplus
 }

@@ -898,4 +898,31 @@ int qe_csv_destroy(qe_csv_table* t) {
   return QE_OK;
 }
 
+int qe_csv_record_end(const uint8_t* data, int64_t nbytes, int32_t eof, int64_t* cut) {
+  QE_CHECK(cut && nbytes >= 0 && (data || nbytes == 0), QE_ERR_INVALID_ARG, "bad arguments");
+  *cut = 0;
+  if (eof) {
+    *cut = nbytes;
+    return QE_OK;
+  }
+  // quote parity of the whole buffer (it starts at a record boundary, outside quotes; '"' toggles
+  // the quoted state anywhere, oracle/csv_ref.py split_records), then a walk back from the end to
+  // the last terminator outside quotes: '\n', or a '\r' whose next byte is known not to be '\n'
+  int64_t q = 0;
+  for (int64_t i = 0; i < nbytes; ++i) q += data[i] == 0x22;
+  for (int64_t i = nbytes - 1; i >= 0; --i) {
+    const uint8_t c = data[i];
+    if (c == 0x22) {
+      --q;  // q = quotes in [0, i)
+      continue;
+    }
+    if (q & 1) continue;  // inside a quoted field
+    if (c == 0x0A || (c == 0x0D && i + 1 < nbytes && data[i + 1] != 0x0A)) {
+      *cut = i + 1;
+      return QE_OK;
+    }
+  }
+  return QE_OK;
+}
+
 }  // extern "C"

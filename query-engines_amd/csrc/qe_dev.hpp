@@ -191,10 +191,19 @@ __host__ __device__ inline qu64 idx_identity(int acc) { return acc_is_f64mm(acc)
 // ---- exact fixed-point fp64 sums (ACC_SUM_X) ---------------------------------------------------------
 // value = sum_k limb_k * 2^(32k - FX_LSB), k = 0..3, limbs int64 (two's complement sums of 32-bit
 // chunks; limb 3 carries the sign). Limb 0 lives in the slot's acc word, limbs 1..3 in idx words
-// 0..2, and idx word 3 counts inputs outside the representable range (NaN, +-Inf, |x| >= 2^63).
-// A row adds the chunks of its exactly scaled value; values below 2^-64 are rounded to the nearest
-// multiple of 2^-64 (ties to even). Integer adds are associative, so any combine order gives the
-// same limbs: deterministic, and exact up to that rounding. Sums stay exact while |sum| < 2^95.
+// 0..2, and idx word 3 is the slot's status word (FX_* below): how many inputs were rounded, how
+// many could not be represented at all (NaN, +-Inf, |x| >= 2^63) and the net number of times limb 3
+// wrapped. A row adds the chunks of its exactly scaled value; a value with bits below 2^-64 is
+// rounded to the nearest multiple of 2^-64 (ties to even) and counted as inexact. Integer adds are
+// associative, so any combine order gives the same limbs and the same status word: deterministic.
+// The result is the correctly rounded exact sum when no input was rounded; otherwise it is off by
+// at most inexact x 2^-65, and finalize reports an error when that bound exceeds 1e-9 of the
+// result (FX_REL_TOL). Unrepresentable inputs fail the update (ctl[6]); a limb-3 wrap that does
+// not cancel (|sum| >= 2^95) fails finalize.
+constexpr qu64 FX_BAD = 1ull << 48;          // status: one unrepresentable input
+constexpr qu64 FX_WRAP = 1ull << 56;         // status: one net wrap of limb 3 (signed)
+constexpr qu64 FX_INEXACT_MASK = FX_BAD - 1;  // status bits 0..47: inputs rounded to 2^-64 units
+constexpr double FX_REL_TOL = 1e-9;
 constexpr int FX_LSB = 64;
 __host__ __device__ inline int fx_clz64(qu64 x) {
   int n = 0;
@@ -206,7 +215,8 @@ __host__ __device__ inline int fx_clz64(qu64 x) {
   return x ? n : 64;
 }
 
-// Chunks of one value: c[0..3] limbs, c[4] = 1 if out of range (then the limbs are 0).
+// Chunks of one value: c[0..3] limbs, c[4] = the status word's share: FX_BAD if out of range (then
+// the limbs are 0), 1 if the value was rounded, else 0.
 __host__ __device__ inline void fx_split(qi64 bits, qi64 c[5]) {
   c[0] = c[1] = c[2] = c[3] = c[4] = 0;
   const qu64 b = (qu64)bits;
@@ -214,7 +224,7 @@ __host__ __device__ inline void fx_split(qi64 bits, qi64 c[5]) {
   const int ex = (int)((b >> 52) & 0x7FF);
   qu64 m = b & ((1ull << 52) - 1);
   if (ex == 0x7FF) {
-    c[4] = 1;
+    c[4] = (qi64)FX_BAD;
     return;
   }
   int e = -1074;
@@ -226,14 +236,16 @@ __host__ __device__ inline void fx_split(qi64 bits, qi64 c[5]) {
   int p = e + FX_LSB;  // bit position of m's lowest bit in the fixed-point number
   if (p < 0) {
     const int sh = -p;
+    c[4] = 1;  // bits below 2^-64 (m != 0): rounded, unless every dropped bit is zero (below)
     if (sh > 54) return;  // m < 2^53 <= half of 2^sh: rounds to 0
     const qu64 q = m >> sh, rem = m & ((1ull << sh) - 1), half = 1ull << (sh - 1);
+    if (rem == 0) c[4] = 0;
     m = q + ((rem > half || (rem == half && (q & 1))) ? 1 : 0);
     p = 0;
     if (m == 0) return;
   }
   if (p + (64 - fx_clz64(m)) > 127) {  // |x| >= 2^63
-    c[4] = 1;
+    c[4] = (qi64)FX_BAD;
     return;
   }
   const int L = p >> 5, q = p & 31;
@@ -242,6 +254,17 @@ __host__ __device__ inline void fx_split(qi64 bits, qi64 c[5]) {
   for (int k = 0; k < 3; ++k)
     if (L + k < 4) c[L + k] = neg ? -ch[k] : ch[k];
 }
+
+// Status-word delta when limb 3 goes from `old` to old + add (two's complement): +-FX_WRAP on a
+// signed overflow. Net wraps cancel exactly when the true limb-3 sum is back in range.
+__host__ __device__ inline qu64 fx_wrap(qu64 old, qu64 add) {
+  const qi64 o = (qi64)old, a = (qi64)add, n = (qi64)(old + add);
+  if (((o ^ n) & (a ^ n)) >= 0) return 0;
+  return n < 0 ? FX_WRAP : (qu64)0 - FX_WRAP;
+}
+
+// Unrepresentable inputs recorded in a status word (what an update reports through ctl[6]).
+__host__ __device__ inline qu64 fx_bad_count(qu64 status) { return (status >> 48) & 0xFF; }
 
 // Carry-propagate so limbs 0..2 are in [0, 2^32) and limb 3 holds the rest (signed).
 __host__ __device__ inline void fx_norm(qi64& l0, qi64& l1, qi64& l2, qi64& l3) {
@@ -420,10 +443,10 @@ __device__ inline void gcombine(const DTable& t, int acck, int j, qu64 s, qi64 a
     qu64* ix = t.idx[j];
     if (i0) atomicAdd(&ix[s], i0);
     if (i1) atomicAdd(&ix[stride + s], i1);
-    if (i2) atomicAdd(&ix[2 * stride + s], i2);
-    if (i3) {  // inputs the fixed point could not hold: the update reports them (ctl[6])
+    if (i2) i3 += fx_wrap(atomicAdd(&ix[2 * stride + s], i2), i2);
+    if (i3) {  // status: rounded / unrepresentable inputs (the update reports the latter, ctl[6]), wraps
       atomicAdd(&ix[3 * stride + s], i3);
-      atomicAdd(&t.ctl[6], i3);
+      if (fx_bad_count(i3)) atomicAdd(&t.ctl[6], fx_bad_count(i3));
     }
   }
 }
@@ -469,8 +492,10 @@ __device__ inline void gcombine_excl(const DTable& t, int acck, int j, qu64 s, q
     qu64* ix = t.idx[j] + s;
     ix[0] += i0;
     ix[stride] += i1;
+    i3 += fx_wrap(ix[2 * stride], i2);
     ix[2 * stride] += i2;
     ix[3 * stride] += i3;
+    if (fx_bad_count(i3)) atomicAdd(&t.ctl[6], fx_bad_count(i3));  // as gcombine: the update fails
   }
 }
 
@@ -542,7 +567,7 @@ __device__ inline int lds_probe(qi64* keys, int log2, qi64 key, qu32 h) {
 }
 
 // ACC_SUM_X row into LDS limbs (acc[s] = limb 0, idx[k * SS + s] = limb k + 1, idx[3 SS + s] =
-// out-of-range count). Returns false for an out-of-range input (the caller flags the launch).
+// status word). Returns false for an out-of-range input (the flush reports it through ctl[6]).
 __device__ inline bool lds_fx_add(qi64* acc, qu64* idx, int SS, int s, qi64 x) {
   qi64 c[5];
   fx_split(x, c);
@@ -551,8 +576,8 @@ __device__ inline bool lds_fx_add(qi64* acc, qu64* idx, int SS, int s, qi64 x) {
   if (c[2]) atomicAdd(&idx[SS + s], (qu64)c[2]);
   if (c[3]) atomicAdd(&idx[2 * SS + s], (qu64)c[3]);
   if (c[4]) {
-    atomicAdd(&idx[3 * SS + s], 1ull);
-    return false;
+    atomicAdd(&idx[3 * SS + s], (qu64)c[4]);
+    return (qu64)c[4] < FX_BAD;
   }
   return true;
 }

@@ -602,6 +602,17 @@ __device__ __forceinline__ void process_step(const Plan& P, char* smem, const Co
       }
     }
   }
+  // multi-pass (groups beyond one LDS table, run_update): this pass keeps the rows whose key hash
+  // falls in bucket mp_pass of mp_n (mp_pass < 0: the share at or above mp_keep), as qe_fused does
+  if (P.mp_n > 1) {
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const qu64 hk = fmix64((qu64)key[r]);
+      const bool other = P.mp_pass < 0 ? (hk >> 32) < P.mp_keep : (qu32)__umul64hi(hk, (qu64)P.mp_n) != (qu32)P.mp_pass;
+      if (other) act &= ~(1u << r);
+    }
+    if (act == 0) return;
+  }
   // ---- slots: first LDS probe of all 4 rows issued together; collisions (rare) probe on
   int slot[4] = {-1, -1, -1, -1};
   if (USE_LDS) {
@@ -1233,13 +1244,23 @@ __device__ __forceinline__ void put_bit(qu8* gbm, qu32* lbits, int col, qi64 o, 
   else set_bit(gbm, o, true);
 }
 
-// An ACC_SUM_X slot's value (limb 0 = acc, limbs 1..3 and the out-of-range count in idx); NaN if an
-// input could not be represented (the update reported it as an error already).
+// An ACC_SUM_X slot's value (limb 0 = acc, limbs 1..3 and the status word in idx). NaN, counted in
+// ctl[6] for finalize to report, when the slot cannot give a sum within FX_REL_TOL of the exact
+// one: an unrepresentable input (the update reported it already), a limb-3 wrap that did not
+// cancel (|sum| >= 2^95), or more rounded inputs than the result's size allows (each rounding to
+// a multiple of 2^-64 is off by at most 2^-65).
 __device__ __forceinline__ double fx_sum(const DTable& t, int j, qu64 s, qi64 acc) {
   const qu64 SS = t.cap + 2;
   const qu64* ix = t.idx[j];
-  if (ix[3 * SS + s]) return bits_f64(0x7FF8000000000000ll);
-  return fx_to_double(acc, (qi64)ix[s], (qi64)ix[SS + s], (qi64)ix[2 * SS + s]);
+  const qu64 st = ix[3 * SS + s];
+  double v = bits_f64(0x7FF8000000000000ll);
+  if ((st & ~FX_INEXACT_MASK) == 0) {
+    v = fx_to_double(acc, (qi64)ix[s], (qi64)ix[SS + s], (qi64)ix[2 * SS + s]);
+    const qu64 inexact = st & FX_INEXACT_MASK;
+    if (inexact && (double)inexact * 0x1p-65 > FX_REL_TOL * __builtin_fabs(v)) v = bits_f64(0x7FF8000000000000ll);
+  }
+  if (v != v) atomicAdd(&t.ctl[6], 1ull);
+  return v;
 }
 
 __device__ __forceinline__ void finalize_slot(const DTable& t, const AggMeta& m, const KeyMeta& km,
@@ -2187,6 +2208,11 @@ static int launch_pass(qe_hashagg* h, Plan& P, size_t& lds, hipFunction_t pfn, i
     grid = (int)std::max<int64_t>(1, std::min<int64_t>((int64_t)div_up((uint64_t)waves, HA_THREADS / 64),
                                                        std::min<int64_t>((int64_t)ctx->num_cus * pc, h->grid)));
   }
+  if (!jfn) {  // what the generic kernel got: its LDS table and how many of its workgroups share a CU
+    const int pcu = lds ? std::max<int>(1, std::min<int>(2048 / HA_THREADS, (int)((160 * 1024) / lds))) : 2048 / HA_THREADS;
+    h->jit_note += std::string(h->jit_note.empty() ? "" : "; ") + "generic kernel: " + std::to_string(lds / 1024) +
+                   " KiB LDS table, " + std::to_string(pcu) + " workgroups per CU";
+  }
   if (pass > 0 || mp > 0) QE_HIP(hipEventRecord(h->ev[0], ctx->stream));
   if (jfn) {
     QE_TRY(jit_launch(ctx, jfn, jgrid, P, pfn ? (pblock ? pblock : pagg_block()) : fused_block(P.lds_log2)));
@@ -2424,17 +2450,20 @@ static int run_update(qe_hashagg* h, Plan& P) {
   // their edge (3000 groups 2.88 ms, 3800 groups 3.44 ms against 3.09 ms partitioned).
   size_t lds_mp = 0;
   int mp_n = 0;
-  if (!lds && ctx->jit && h->expected_groups > 0) {
+  // The generic kernel (JIT off, or no specialised kernel) passes too, with its own 80 KiB budget:
+  // it has no partitioned path to fall back on, and global-only rows cost a device atomic each.
+  if (!lds && h->expected_groups > 0) {
     int tlog2 = 16;
     Plan T = P;
-    while (tlog2 >= 8 && lds_layout_at(h, &T, tlog2) > lds_budget(ctx)) --tlog2;
+    const size_t mbudget = ctx->jit ? lds_budget(ctx) : HA_LDS_BUDGET;
+    while (tlog2 >= 8 && lds_layout_at(h, &T, tlog2) > mbudget) --tlog2;
     const int64_t per_pass = (((int64_t)1 << tlog2) * 5) / 8;
     const int64_t np = tlog2 >= 8 ? (h->expected_groups + per_pass - 1) / per_pass : 0;
     static const int64_t mp_max = [] {  // QE_MP_MAX: most bucket passes before partitioning
       const char* e = getenv("QE_MP_MAX");
       return (int64_t)(e && *e ? std::max(2, std::min(8, atoi(e))) : 2);
     }();
-    if (np >= 2 && np <= mp_max) {
+    if (np >= 2 && np <= (ctx->jit ? mp_max : 8)) {
       T.mp_n = (qi32)np;
       T.mp_pass = 0;
       lds_mp = lds_layout_at(h, &T, tlog2);
@@ -2442,7 +2471,7 @@ static int run_update(qe_hashagg* h, Plan& P) {
       size_t jl = 0;
       // overflow records: a workgroup flushes at most its table's slots
       const uint64_t need = (uint64_t)ctx->num_cus * 8 * (((uint64_t)1 << tlog2) + 2);
-      if (lds_mp && gen_fused_source(T, T.lds_log2, &src, &jl)) {
+      if (lds_mp && (!ctx->jit || gen_fused_source(T, T.lds_log2, &src, &jl))) {
         if (h->ovf_cap < need) {
           dev_free(ctx, h->ovf);
           h->ovf = nullptr;
@@ -2458,7 +2487,7 @@ static int run_update(qe_hashagg* h, Plan& P) {
       }
     }
   }
-  if (mp_n == 2) {
+  if (mp_n == 2 && ctx->jit) {
     bool used = false;
     QE_TRY(spill_update(h, P, lds, rows, &used));
     if (used) {
@@ -2518,11 +2547,14 @@ static int run_update(qe_hashagg* h, Plan& P) {
     h->part_wide = true;
     P = P_rows;
     pfn = nullptr;
+    // the repeat is timed from here: the attempt just settled is already in last_kernel_ms once
+    QE_HIP(hipEventRecord(h->ev[0], ctx->stream));
     continue;
   }
   break;
   }
-  if (mp_n) h->jit_note = "multi-pass: " + std::to_string(mp_n) + " bucket passes";
+  if (mp_n)
+    h->jit_note = "multi-pass: " + std::to_string(mp_n) + " bucket passes" + (h->last_specialized ? "" : "; " + h->jit_note);
   h->row_base += rows;
   adapt_after_update(h, lds, P.lds_log2);
   return QE_OK;
@@ -2812,6 +2844,18 @@ int qe_hashagg_num_groups(qe_hashagg* h, int64_t* out) {
   return QE_OK;
 }
 
+// Deterministic states: finalize waits for its kernel and fails when a group's fixed-point sum
+// could not be given within FX_REL_TOL of the exact sum (fx_sum counted such groups in ctl[6]).
+static int check_fx_final(qe_hashagg* h) {
+  uint64_t c[8];
+  QE_TRY(read_ctl(h, c));
+  QE_CHECK(c[6] == 0, QE_ERR_UNSUPPORTED,
+           "deterministic fp64 SUM: %llu group results not exact to 1e-9 (inputs outside the fixed-point range "
+           "[2^-64, 2^63) or |sum| >= 2^95)",
+           (unsigned long long)c[6]);
+  return QE_OK;
+}
+
 int qe_hashagg_finalize(qe_hashagg* h, qe_column* out_keys, qe_column* out_aggs, int64_t* out_groups) {
   QE_CHECK(h, QE_ERR_INVALID_ARG, "null state");
   QE_TRY(ctx_enter(h->ctx));
@@ -2850,11 +2894,13 @@ int qe_hashagg_finalize(qe_hashagg* h, qe_column* out_keys, qe_column* out_aggs,
   for (int k = 0; k < h->nkeys; ++k) out_keys[k].length = groups;
   for (int j = 0; j < h->naggs; ++j) out_aggs[j].length = groups;
   if (groups == 0) return QE_OK;
+  bool det = false;
+  for (int j = 0; j < h->naggs; ++j) det = det || h->acc[j] == ACC_SUM_X;
   if (small) {
     hipLaunchKernelGGL(k_finalize_small, dim3(1), dim3(FS_THREADS), 0, ctx->stream, h->t, agg_meta(h), h->km, oc,
                        (qi64)groups);
     QE_TRY(launch_check("k_finalize_small"));
-    return QE_OK;  // stream-ordered: the outputs are ready when the ctx stream's work is
+    return det ? check_fx_final(h) : QE_OK;  // stream-ordered: the outputs are ready when the ctx stream's work is
   }
   // one 256-slot tile per workgroup: a single pass each, so the chip finalises in one wave of
   // workgroups instead of a serial walk of long tiles
@@ -2871,7 +2917,7 @@ int qe_hashagg_finalize(qe_hashagg* h, qe_column* out_keys, qe_column* out_aggs,
   hipLaunchKernelGGL(k_finalize, dim3((unsigned)ntiles), dim3(256), 0, ctx->stream, h->t, agg_meta(h), h->km, (const qi64*)offs,
                      tile_slots, oc);
   QE_TRY(launch_check("k_finalize"));
-  return QE_OK;
+  return det ? check_fx_final(h) : QE_OK;
 }
 
 int qe_hashagg_record_bytes(qe_hashagg* h, int64_t* out) {

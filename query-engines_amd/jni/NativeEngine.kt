@@ -117,6 +117,7 @@ object NativeEngine {
     // CsvDataSource.scan on the device (K:276-357)
     @JvmStatic external fun csvParse(ctx: Long, data: java.nio.ByteBuffer, nbytes: Long, delimiter: Int, hasHeader: Boolean,
                                      fields: IntArray): Long
+    @JvmStatic external fun csvRecordEnd(data: java.nio.ByteBuffer, nbytes: Long, eof: Boolean): Long
     @JvmStatic external fun csvRows(table: Long): Long
     @JvmStatic external fun csvColumn(table: Long, i: Int): Long
     @JvmStatic external fun csvDestroy(table: Long)

@@ -146,8 +146,11 @@ private class NativeBinaryExpression(
 
 // HashAggregateExec (K:605-660) on the device: every input batch is one aggregate update (Utf8
 // keys through a string dictionary), then ONE output batch (K:649-650). MAX follows
-// MaxAccumulator (K:538-561); a MAX over an input the reference rejects (Utf8) fails with
-// IllegalStateException where the reference throws UnsupportedOperationException (K:548).
+// MaxAccumulator (K:538-561). A MAX over a Utf8 column is the reference's own operator: its
+// accumulator keeps the first String of a group with no type check and throws
+// UnsupportedOperationException at the second (K:541-550), row-order behaviour the device has no
+// use for; that row loop reads these batches through NativeColumnVector.getValue. (Called
+// directly, aggCreate throws the same UnsupportedOperationException for a Utf8 MAX input.)
 private class NativeHashAggregateExec(
     private val input: PhysicalPlan,
     private val groupExpr: List<Expression>,
@@ -157,6 +160,11 @@ private class NativeHashAggregateExec(
     override fun schema() = schema
 
     override fun execute(): Sequence<RecordBatch> {
+        val inSchema = input.schema()
+        if (aggregateExpr.any { e ->
+                val x = e.inputExpression()
+                e is MaxExpression && x is ColumnExpression && inSchema.fields[x.i].dataType == ArrowTypes.StringType
+            }) return HashAggregateExec(input, groupExpr, aggregateExpr, schema).execute() // K:615-651
         val ctx = Native.ctx()
         val fns = IntArray(aggregateExpr.size) { i ->
             when (aggregateExpr[i]) {
@@ -236,12 +244,17 @@ private class NativeSelectProjectExec(
     override fun children() = listOf1(input)
 }
 
-// CsvDataSource (K:276-357) scanned on the device: the file goes to HBM once and is tokenised,
-// trimmed and unquoted there. The header and delimiter come from the reference's own
-// CsvDataSource (univocity detection, K:290-297, K:332-356); one batch holds the whole file
-// (its columns are zero-copy views of the parsed table).
+// CsvDataSource (K:276-357) scanned on the device: the file goes to HBM in chunks of whole records
+// and is tokenised, trimmed and unquoted there. The header and delimiter come from the reference's
+// own CsvDataSource (univocity detection, K:290-297, K:332-356). Like ReaderIterator (K:239-252)
+// the scan streams: a chunk of up to chunkBytes is cut after its last complete record
+// (csvRecordEnd, quote-aware), parsed on the device as one batch, and its tail begins the next
+// chunk; sizes are Long, so files past 2 GiB stream (the reference's monthly tripdata, K:1335).
+// A record longer than the buffer doubles it. Each batch's columns are zero-copy views of its
+// chunk's parsed table.
 private class NativeCsvDataSource(private val filename: String, private val hasHeaders: Boolean) : DataSource {
     private val host = CsvDataSource(filename, hasHeaders, 1000, null)
+    private val chunkBytes = 256 shl 20
 
     override fun schema(): Schema = host.schema()
 
@@ -251,12 +264,34 @@ private class NativeCsvDataSource(private val filename: String, private val hasH
         val readSchema = if (projection.isNotEmpty()) schema().select(projection) else schema()
         val fields = readSchema.fields.map { f -> schema().fields.indexOfFirst { it.name == f.name } }.toIntArray()
         val delimiter = detectDelimiter(file)
-        val bytes = java.nio.channels.FileChannel.open(file.toPath(), java.nio.file.StandardOpenOption.READ).use { ch ->
-            java.nio.ByteBuffer.allocateDirect(ch.size().toInt()).also { while (it.hasRemaining() && ch.read(it) >= 0) {} }
+        return sequence {
+            java.nio.channels.FileChannel.open(file.toPath(), java.nio.file.StandardOpenOption.READ).use { ch ->
+                var buf = java.nio.ByteBuffer.allocateDirect(chunkBytes)
+                var header = hasHeaders // the header record is in the first chunk
+                var eof = false
+                while (true) {
+                    while (!eof && buf.hasRemaining()) if (ch.read(buf) < 0) eof = true
+                    val have = buf.position().toLong()
+                    if (have == 0L) break
+                    val cut = NativeEngine.csvRecordEnd(buf, have, eof)
+                    if (cut == 0L) { // one record longer than the buffer
+                        val bigger = java.nio.ByteBuffer.allocateDirect(Math.multiplyExact(buf.capacity(), 2))
+                        buf.flip()
+                        bigger.put(buf)
+                        buf = bigger
+                        continue
+                    }
+                    val table = CsvTable(NativeEngine.csvParse(Native.ctx(), buf, cut, delimiter.code, header, fields))
+                    header = false
+                    if (NativeEngine.csvRows(table.handle) > 0) {
+                        yield(RecordBatch(readSchema, fields.indices.map { table.column(it) }))
+                    }
+                    buf.limit(have.toInt()) // the bytes past the cut begin the next chunk
+                    buf.position(cut.toInt())
+                    buf.compact()
+                }
+            }
         }
-        val table = CsvTable(NativeEngine.csvParse(Native.ctx(), bytes, bytes.capacity().toLong(), delimiter.code,
-                                                   hasHeaders, fields))
-        return sequenceOf(RecordBatch(readSchema, fields.indices.map { table.column(it) }))
     }
 
     private fun detectDelimiter(file: File): Char {

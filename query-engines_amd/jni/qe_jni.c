@@ -1013,6 +1013,15 @@ JNIEXPORT jlong JNICALL Java_NativeEngine_aggCreate(JNIEnv* env, jclass k, jlong
   for (int j = 0; j < a.naggs; ++j) {
     a.aggs[j].fn = f[j];
     a.aggs[j].input_type = t[j];
+    if (t[j] == QE_TYPE_UTF8 && f[j] != QE_AGG_COUNT && f[j] != QE_AGG_COUNT_STAR) {
+      /* MaxAccumulator.accumulate (K:545-550): a String value takes `else -> throw
+       * UnsupportedOperationException("MAX is not implemented for data type ${value.javaClass.name}")` */
+      char msg[96];
+      snprintf(msg, sizeof msg, "%s is not implemented for data type java.lang.String",
+               f[j] == QE_AGG_MAX ? "MAX" : f[j] == QE_AGG_MIN ? "MIN" : f[j] == QE_AGG_SUM ? "SUM" : "AVG");
+      throw_class(env, "java/lang/UnsupportedOperationException", msg);
+      return 0;
+    }
   }
   QJ_TRY(env,
          qe_hashagg_create_ex(a.ctx, a.nkeys, a.key_types, a.naggs, a.aggs, expectedGroups > 0 ? expectedGroups : 1024,
@@ -1334,6 +1343,19 @@ JNIEXPORT jlong JNICALL Java_NativeEngine_csvParse(JNIEnv* env, jclass k, jlong 
     return 0;
   }
   return (jlong)(intptr_t)t;
+}
+
+/* Streaming scan (ReaderIterator's batches, K:239-252): the end of the last complete record in the
+ * direct buffer's first nbytes (quote-aware; nbytes when eof; 0 when none is complete yet). */
+JNIEXPORT jlong JNICALL Java_NativeEngine_csvRecordEnd(JNIEnv* env, jclass k, jobject data, jlong nbytes, jboolean eof) {
+  (void)k;
+  QJ_NEED(env, data, "null data", 0);
+  const void* host = (*env)->GetDirectBufferAddress(env, data);
+  const jlong cap = (*env)->GetDirectBufferCapacity(env, data);
+  QJ_NEED(env, host && nbytes >= 0 && nbytes <= cap, "csvRecordEnd needs a direct ByteBuffer of at least nbytes", 0);
+  int64_t cut = 0;
+  QJ_TRY(env, qe_csv_record_end((const uint8_t*)host, nbytes, eof ? 1 : 0, &cut), 0);
+  return cut;
 }
 
 JNIEXPORT jlong JNICALL Java_NativeEngine_csvRows(JNIEnv* env, jclass k, jlong table) {

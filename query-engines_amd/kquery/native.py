@@ -257,6 +257,7 @@ SIGNATURES = [
     ("qe_csv_column_bytes", C.c_int, [_P, C.c_int32, _I64P]),
     ("qe_csv_column_copy", C.c_int, [_P, C.c_int32, _COLP]),
     ("qe_csv_destroy", C.c_int, [_P]),
+    ("qe_csv_record_end", C.c_int, [_P, C.c_int64, C.c_int32, _I64P]),
     ("qe_batch_import", C.c_int, [_P, _P, _P, _PP]),
     ("qe_batch_import_device", C.c_int, [_P, _P, _P, _PP]),
     ("qe_batch_destroy", C.c_int, [_P]),

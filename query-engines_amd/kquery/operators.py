@@ -326,18 +326,24 @@ class FusedSelectProjectExec(PhysicalPlan):
         """Pipelined one batch ahead: batch i+1's kernels are queued before batch i's row count is
         read back, so the host wait for batch i overlaps batch i+1 on the device and the stream
         never drains between batches. Batches come out in input order (row order preserved)."""
-        ahead = None
-        for batch in self.scan.execute():
-            launched = self.launch_batch(batch)
-            if ahead is not None:
-                yield self.finish_batch(ahead)
-                ahead = None
-            if launched is None:  # kernel specialisation unavailable: per-family operators
-                yield from _replay(self.unfused, batch)
-            else:
-                ahead = launched
-        if ahead is not None:
-            yield self.finish_batch(ahead)
+        inflight = []  # launched, not yet waited on (at most two: this batch and the one ahead)
+        try:
+            for batch in self.scan.execute():
+                launched = self.launch_batch(batch)
+                if launched is not None:
+                    inflight.append(launched)
+                if len(inflight) > 1 or (launched is None and inflight):
+                    yield self.finish_batch(inflight.pop(0))
+                if launched is None:  # kernel specialisation unavailable: per-family operators
+                    yield from _replay(self.unfused, batch)
+            while inflight:
+                yield self.finish_batch(inflight.pop(0))
+        finally:
+            # the consumer stopped early, or a scan / launch raised: every queued call is still
+            # waited on once, which frees its pinned slot and event and runs its look-back stall
+            # check (qe_select_pending_wait); an error here must not mask the one propagating
+            for _outs, pending, _cols in inflight:
+                N.lib().qe_select_pending_wait(pending, N.C.byref(N.C.c_int64()))
 
     def __repr__(self) -> str:
         return f"FusedSelectProjectExec: slots={self.slots}, outputs={self.out_types}"

@@ -362,6 +362,47 @@ static void cpu_cases(void) {
   OKV(Java_NativeEngine_specFree(E, K, fs));
   end(f0);
 
+  begin("csv_record_end");
+  f0 = g_fail;
+  {
+    /* a chunk boundary inside a quoted field: the chunk is cut after the last record that ends
+     * outside quotes (the header here), and the field's bytes begin the next chunk */
+    static const struct {
+      const char* text;
+      int eof;
+      jlong cut;
+    } cases[] = {
+        {"a,b\n1,\"x\ny", 0, 4},      /* the newline inside the open quote is not a record end */
+        {"a,b\n1,\"x\ny\"\n2", 0, 12}, /* closed quote: the newline after it is */
+        {"a,b\n1,\"x\"\"\n", 0, 4},     /* "" escape still inside the field */
+        {"a\rb", 0, 2},                 /* a lone \r ends a record */
+        {"a\r", 0, 0},                  /* \r at the end: a \n may follow */
+        {"abc", 0, 0},                   /* no complete record */
+        {"abc", 1, 3},                   /* eof: everything */
+        {"a\r\nb", 0, 3},
+    };
+    for (size_t i = 0; i < sizeof cases / sizeof cases[0]; ++i) {
+      const jsize n = (jsize)strlen(cases[i].text);
+      jobject buf = obj_new(K_BUF, n, 1);
+      memcpy(buf->data, cases[i].text, (size_t)n);
+      const jlong cut = OK(Java_NativeEngine_csvRecordEnd(E, K, buf, n, (jboolean)cases[i].eof));
+      CHECK(cut == cases[i].cut, "case %zu: cut %lld, expected %lld", i, (long long)cut, (long long)cases[i].cut);
+    }
+    jobject b1 = obj_new(K_BUF, 4, 1);
+    THROWS("java/lang/IllegalArgumentException", Java_NativeEngine_csvRecordEnd(E, K, b1, 5, 0));
+  }
+  end(f0);
+
+  begin("max_over_utf8_unsupported");
+  f0 = g_fail;
+  /* MAX of a String column: the reference's MaxAccumulator throws UnsupportedOperationException
+   * (K:545-550); refused before the (fake, non-null) ctx handle is used */
+  THROWS("java/lang/UnsupportedOperationException",
+         Java_NativeEngine_aggCreate(E, K, 1, INTS(QE_TYPE_INT64), INTS(QE_AGG_MAX), INTS(QE_TYPE_UTF8), 0, 0));
+  CHECK(strstr(g_msg, "MAX is not implemented for data type java.lang.String") != NULL, "message: %s", g_msg);
+  g_msg[0] = 0;
+  end(f0);
+
   begin("array_limits");
   f0 = g_fail;
   /* nine filter inputs (QE_MAX_COLS = 8) are refused before anything touches the device */
@@ -806,6 +847,46 @@ static void gpu_cases(void) {
       OKV(Java_NativeEngine_columnFree(E, K, c0));
       OKV(Java_NativeEngine_csvDestroy(E, K, t));
     }
+  }
+  end(f0);
+
+  /* the streaming scan's chunks (NativeCsvDataSource.scan): the same file cut at csvRecordEnd of
+   * 7-byte windows (boundaries inside quoted fields and between \r and \n) gives the same rows */
+  begin("csv_scan_chunked");
+  f0 = g_fail;
+  {
+    const char* text = "state,name\nCA, Ann\n# comment\nNY,\"B,\n \"\"Bo\"\"\"\r\nTX,\"C\r\"\rWA,Dee";
+    const char* want[] = {"Ann", "B,\n \"Bo\"", "C", "Dee"};
+    const jsize total = (jsize)strlen(text);
+    jsize start = 0, got = 0, window = 7;
+    int header = 1;
+    while (start < total && got < 8) {
+      jsize have = start + window < total ? window : total - start;
+      const int eof = start + have == total;
+      jobject buf = obj_new(K_BUF, have, 1);
+      memcpy(buf->data, text + start, (size_t)have);
+      const jlong cut = OK(Java_NativeEngine_csvRecordEnd(E, K, buf, have, (jboolean)eof));
+      if (cut == 0) {  /* one record longer than the window: grow it */
+        window *= 2;
+        continue;
+      }
+      const jlong t = OK(Java_NativeEngine_csvParse(E, K, ctx, buf, cut, ',', (jboolean)header, INTS(1)));
+      header = 0;
+      if (!t) break;
+      const jlong rows = OK(Java_NativeEngine_csvRows(E, K, t));
+      if (rows > 0) {
+        const jlong c0 = OK(Java_NativeEngine_csvColumn(E, K, t, 0));
+        jlong n = 0;
+        char** s = fetch_strings(ctx, c0, &n);
+        for (jlong r = 0; r < n; ++r, ++got)
+          CHECK(got < 4 && s[r] && !strcmp(s[r], want[got]), "row %d: [%s]", (int)got, s[r] ? s[r] : "?");
+        OKV(Java_NativeEngine_columnFree(E, K, c0));
+      }
+      OKV(Java_NativeEngine_csvDestroy(E, K, t));
+      start += (jsize)cut;
+      window = 7;
+    }
+    CHECK(got == 4, "rows over all chunks: %d", (int)got);
   }
   end(f0);
 

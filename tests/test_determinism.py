@@ -201,17 +201,61 @@ def test_deterministic_fp64_group_sums(gpu_ctx, groups, expected, path):
         assert np.frombuffer(got_avg, np.float64)[0] == want / len(vals_g), g
 
 
-def test_deterministic_rejects_unrepresentable(gpu_ctx):
-    """NaN / Inf / |x| >= 2^63 cannot be held by the fixed point: the update fails loudly."""
+@pytest.mark.parametrize("expected", [16, 4500, 50_000])
+def test_deterministic_rejects_unrepresentable(gpu_ctx, expected):
+    """NaN / Inf / |x| >= 2^63 cannot be held by the fixed point: the update fails loudly, on the
+    LDS, two-bucket and radix-partitioned paths alike (the partitioned flush of an exclusive slice
+    reports it too)."""
     from kquery import native as N
     from kquery.aggregate import HashAggregateState
     from kquery.columnar import DeviceColumn
 
+    n = 200_000
     for bad in (np.nan, np.inf, 2.0 ** 70):
-        x = np.ones(1000)
-        x[500] = bad
-        st = HashAggregateState(gpu_ctx, [N.TYPE_INT64], [(N.AGG_SUM, N.TYPE_FLOAT64)], 16, deterministic=True)
-        kc = DeviceColumn.from_numpy(N.TYPE_INT64, np.arange(1000, dtype=np.int64) % 7, None, ctx=gpu_ctx)
+        x = np.ones(n)
+        x[n // 2] = bad
+        st = HashAggregateState(gpu_ctx, [N.TYPE_INT64], [(N.AGG_SUM, N.TYPE_FLOAT64)], expected, deterministic=True)
+        kc = DeviceColumn.from_numpy(N.TYPE_INT64, np.arange(n, dtype=np.int64) % max(7, expected), None, ctx=gpu_ctx)
         with pytest.raises(Exception, match="fixed-point range"):
             st.update([kc], [DeviceColumn.from_numpy(N.TYPE_FLOAT64, x, None, ctx=gpu_ctx)])
             st.finalize()
+
+
+def test_deterministic_inexact_bound(gpu_ctx):
+    """Values with bits below 2^-64 are rounded to multiples of 2^-64 and counted. A group whose
+    sum is large enough that the rounding (at most 2^-65 per input) stays within 1e-9 relative is
+    returned, deterministic and within 1e-9 of math.fsum; a group of values around 1e-25 (every
+    one rounded to 0) cannot be, and finalize fails instead of returning a wrong sum."""
+    import math
+
+    from kquery import native as N
+    from kquery.aggregate import HashAggregateState
+    from kquery.columnar import DeviceColumn
+
+    rng = np.random.default_rng(3)
+    n = 100_000
+    k = rng.integers(0, 50, n).astype(np.int64)
+    x = rng.random(n) * 10.0 + rng.random(n) * 1e-4  # low bits well below 2^-64 on the small terms
+    x[::7] = 3.7e-5  # full-mantissa values under 2^-11: inexact
+    outs = []
+    for ctx in _runs(gpu_ctx):
+        st = HashAggregateState(ctx, [N.TYPE_INT64], [(N.AGG_SUM, N.TYPE_FLOAT64)], 64, deterministic=True)
+        st.update([DeviceColumn.from_numpy(N.TYPE_INT64, k, None, ctx=ctx)],
+                  [DeviceColumn.from_numpy(N.TYPE_FLOAT64, x, None, ctx=ctx)])
+        keys, vals = st.finalize()
+        ctx.synchronize()
+        kv, sv = keys[0].to_numpy(), vals[0].to_numpy()
+        outs.append({int(kv[i]): sv[i].tobytes() for i in range(len(kv))})
+    assert all(o == outs[0] for o in outs[1:])
+    for g, b in outs[0].items():
+        want = math.fsum(x[k == g].tolist())
+        got = float(np.frombuffer(b, np.float64)[0])
+        assert abs(got - want) <= 1e-9 * abs(want), (g, got, want)
+    # every value of group 1 is ~1e-25: its fixed-point sum is 0, off by 100 % of the exact sum
+    k2 = np.array([0, 1, 1, 1, 0], dtype=np.int64)
+    x2 = np.array([1.0, 1.1e-25, 0.9e-25, 1.3e-25, 2.0])
+    st = HashAggregateState(gpu_ctx, [N.TYPE_INT64], [(N.AGG_SUM, N.TYPE_FLOAT64)], 16, deterministic=True)
+    st.update([DeviceColumn.from_numpy(N.TYPE_INT64, k2, None, ctx=gpu_ctx)],
+              [DeviceColumn.from_numpy(N.TYPE_FLOAT64, x2, None, ctx=gpu_ctx)])
+    with pytest.raises(Exception, match="not exact to 1e-9"):
+        st.finalize()

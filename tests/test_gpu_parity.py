@@ -58,7 +58,7 @@ def check_kernel_kind(ctx, st, lds_mode=True):
     spec, note = st.last_kernel_kind()
     if getattr(ctx, "kernel_mode", "jit") == "jit" and lds_mode:
         # plans whose on-chip table does not fit the LDS budget run global-only (generic kernel)
-        assert spec or note == "global-only launch", f"expected the specialised kernel: {note}"
+        assert spec or note.startswith("global-only launch"), f"expected the specialised kernel: {note}"
     elif getattr(ctx, "kernel_mode", "jit") == "generic":
         assert not spec
 
@@ -1170,3 +1170,33 @@ def test_import_probe_limit_loses_no_group_silently(gpu_ctx, path):
     assert st2.import_slots(dev, 1, 512) == 300
     kc, res = st2.finalize()
     assert kc[0].length == 300 and int(res[1].to_numpy().sum()) == 300
+
+
+def test_generic_kernel_lds_budget(gpu_ctx):
+    """The 152 KiB LDS table budget belongs to the specialised 1024-thread kernel (one workgroup
+    per CU). A state created with JIT on whose update then runs the generic 512-thread kernel (JIT
+    switched off after create, as after a failed hipRTC compile) gets its table re-laid out within
+    the 80 KiB budget: two workgroups per CU, not one, and the same results."""
+    rng = np.random.default_rng(7)
+    n = 400_000
+    k = rng.integers(0, 2000, n).astype(np.int64)
+    v = rng.integers(-1000, 1000, n).astype(np.int64)
+    aggs = [(N.AGG_SUM, N.TYPE_INT64), (N.AGG_COUNT_STAR, N.TYPE_INT64), (N.AGG_MIN, N.TYPE_INT64),
+            (N.AGG_MAX, N.TYPE_INT64)]
+    st = HashAggregateState(gpu_ctx, [N.TYPE_INT64], aggs, 2000)
+    kc, vc = dcol(gpu_ctx, N.TYPE_INT64, k), dcol(gpu_ctx, N.TYPE_INT64, v)
+    N.check(N.lib().qe_ctx_set_jit(gpu_ctx.handle, 0))
+    try:
+        st.update([kc], [vc, None, vc, vc])
+        spec, note = st.last_kernel_kind()
+        keys, vals = st.finalize()
+        gpu_ctx.synchronize()
+    finally:
+        N.check(N.lib().qe_ctx_set_jit(gpu_ctx.handle, 1))
+    assert not spec and "2 workgroups per CU" in note, note
+    ref = S.group_aggregate([k], [None], [v, None, v, v], [None] * 4,
+                            [S.AGG_SUM, S.AGG_COUNT_STAR, S.AGG_MIN, S.AGG_MAX], None)
+    kv = keys[0].to_numpy()
+    cols = [c.to_numpy() for c in vals]
+    got = {(int(kv[i]),): [int(c[i]) for c in cols] for i in range(len(kv))}
+    assert got == ref

@@ -70,7 +70,7 @@ def test_kotlin_signatures_match_the_shim():
         want = (_KT_TO_JNI[ret.rstrip("?")], [_KT_TO_JNI[t] for t in types])
         assert c_sig[name] == want, (name, c_sig[name], want)
         n += 1
-    assert n == len(c_sig) == 60
+    assert n == len(c_sig) == 61
 
 
 def test_real_shim_build_is_gated():

@@ -1,0 +1,7 @@
+#!/bin/bash
+# Full GPU test suite (pytest -m gpu) with a per-test timeout; output under gpurun_out/$1.
+set -o pipefail
+export TMPDIR=/tmp
+OUT=gpurun_out/${1:-tests_r04}
+mkdir -p $OUT
+timeout -k 10 1100 python3 -u -m pytest tests -x -v --timeout 300 --timeout-method thread -m gpu > $OUT/tests.txt 2>&1
