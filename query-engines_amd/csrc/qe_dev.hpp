@@ -40,6 +40,7 @@ typedef unsigned short qu16;
 typedef unsigned char qu8;
 typedef long long qi64x2 __attribute__((ext_vector_type(2)));
 typedef int qi32x2 __attribute__((ext_vector_type(2)));
+typedef unsigned int qu32x4 __attribute__((ext_vector_type(4)));
 
 constexpr qi64 EMPTY_KEY = (qi64)0x8000000000000000ull;  // LDS/global slot sentinel (INT64_MIN)
 constexpr qi64 PART_EXCL = 1ll << 62;  // partition-aggregate slice flag: the slice holds its whole bucket
@@ -560,6 +561,24 @@ __device__ inline int lds_probe(qi64* keys, int log2, qi64 key, qu32 h) {
     if (k == EMPTY_KEY) {
       const qi64 old = (qi64)atomicCAS((qu64*)&keys[h], (qu64)EMPTY_KEY, (qu64)key);
       if (old == EMPTY_KEY || old == key) return (int)h;
+    }
+    h = (h + 1) & mask;
+  }
+  return -1;
+}
+
+// lds_probe for the 32-bit key tables of the fast aggregation pass (qe_jit.hip gen_pagg_fast_source):
+// empty slots hold EMPTY_KEY32 (INT32_MIN; that key itself lives in special slot S + 1).
+constexpr qi32 EMPTY_KEY32 = (qi32)0x80000000u;
+__device__ inline int lds_probe32(qi32* keys, int log2, qi32 key, qu32 h) {
+  const qu32 mask = (1u << log2) - 1;
+#pragma unroll 1
+  for (int p = 0; p < HA_LDS_MAXP; ++p) {
+    const qi32 k = keys[h];
+    if (k == key) return (int)h;
+    if (k == EMPTY_KEY32) {
+      const qi32 old = atomicCAS(&keys[h], EMPTY_KEY32, key);
+      if (old == EMPTY_KEY32 || old == key) return (int)h;
     }
     h = (h + 1) & mask;
   }

@@ -802,6 +802,14 @@ bool part_static() {
   return v;
 }
 
+static bool pscatter_fast_env() {
+  static const bool v = [] {
+    const char* e = getenv("QE_PSCATTER_FAST");
+    return !(e && e[0] == '0');
+  }();
+  return v;
+}
+
 bool gen_pscatter_staged_source(const Plan& P, int log2p, std::string* src, bool chunked, bool soa) {
   if (soa && !chunked) return false;
   if (P.ncols < 1 || P.ncols > QE_MAX_COLS || log2p < 1 || !part_staged_ok(P, log2p)) return false;
@@ -811,13 +819,22 @@ bool gen_pscatter_staged_source(const Plan& P, int log2p, std::string* src, bool
   if (soa && L.narrow) return false;
   const int W = L.words, G = W % 2 ? 1 : 2;
   const char* chunk = L.narrow ? (G == 2 ? "qu64" : "qu32") : (G == 2 ? "qi64x2" : "qi64");
+  // fast form (chunked 32-bit records, QE_PSCATTER_FAST default 1): each row writes its record
+  // words to LDS right away (word-major, double-buffered by tile, slot wave*256 + 64r + lane) and
+  // after the scan only its 2-byte index to the sorted position; the write-out then moves whole
+  // records (W dwords per lane). The records' registers are dead before the first barrier.
+  const bool fast = chunked && !soa && L.narrow && pscatter_fast_env();
   std::ostringstream o;
   o << "\nusing namespace qe;\n"
     << "extern \"C\" __global__ void __launch_bounds__(" << pscatter_block_for(log2p) << ") qe_pscatter(const Plan P) {\n"
     << "  constexpr int LOG2P = " << log2p << ", NP = 1 << LOG2P, W = " << W << ", T = " << 4 * pscatter_block_for(log2p) << ";\n"
     << "  __shared__ qu32 s_hist[NP];\n  __shared__ qu32 s_off[NP];\n  __shared__ qu64 s_cur[NP];\n  __shared__ qu64 s_dst[NP];\n"
-    << "  constexpr int WC = " << W / G << ";  // " << chunk << " chunks per record\n"
-    << "  __shared__ " << chunk << " s_rec[T * WC];\n  __shared__ unsigned short s_bkt[T];\n  __shared__ qu32 s_total;\n";
+    << "  constexpr int WC = " << W / G << ";  // " << chunk << " chunks per record\n";
+  if (fast)
+    o << "  __shared__ qu32 s_w[2][" << W << "][T];\n  __shared__ unsigned short s_perm[T];\n";
+  else
+    o << "  __shared__ " << chunk << " s_rec[T * WC];\n";
+  o << "  __shared__ unsigned short s_bkt[T];\n  __shared__ qu32 s_total;\n";
   if (chunked)
     // per bucket: the open chunk (-1: none) and its end, the tile's second destination base (for
     // the records past the open chunk's room) and the tile-local index where that part starts
@@ -923,7 +940,7 @@ bool gen_pscatter_staged_source(const Plan& P, int log2p, std::string* src, bool
     // per-bucket destination bases s_dst, and advanced s_cur; (C) the records sit sorted in LDS
     // and s_hist is cleared for the next tile. The write-out then runs without a barrier behind it.
     o << "  {\n    const qi64 tile = t0 + " << k << " * (qi64)T;\n    if (tile >= hi) break;\n"
-      << "    qu32 ract = 0, bk[4], rk[4];\n    qi64 rw[4][W];\n"
+      << "    qu32 ract = 0, bk[4], rk[4];\n" << (fast ? "    const int sb = (int)((tile - lo) / T) & 1;\n" : "    qi64 rw[4][W];\n")
       << "    const qi64 base = tile + woff;\n";
     for (int c = 0; c < P.ncols; ++c) {
       const std::string cs = std::to_string(c), n = buf(k, cs);
@@ -946,8 +963,16 @@ bool gen_pscatter_staged_source(const Plan& P, int log2p, std::string* src, bool
       << "      if (!((act >> r) & 1)) continue;\n"
       << "      bk[r] = (qu32)(fmix64((qu64)key[r]) >> (64 - LOG2P));\n"
       << "      rk[r] = atomicAdd(&s_hist[bk[r]], 1u);\n";
-    emit_record_words(P, L, ex, "rw[r]", o);
-    emit_fit_check(L, "rw[r]", o);
+    if (fast) {
+      o << "      {\n      qi64 w[W];\n";
+      emit_record_words(P, L, ex, "w", o);
+      emit_fit_check(L, "w", o);
+      o << "      const int slot = (int)woff + 64 * r + lane;\n"
+        << "#pragma unroll\n      for (int q = 0; q < W; ++q) s_w[sb][q][slot] = (qu32)w[q];\n      }\n";
+    } else {
+      emit_record_words(P, L, ex, "rw[r]", o);
+      emit_fit_check(L, "rw[r]", o);
+    }
     o << "    }\n    } while (0);\n";
     // QE_PSCATTER_RELOAD=1 (default): the buffer is reloaded after the scan, whose chunk claims
     // (a device atomic with a return value) would otherwise wait for wave 0's just-issued loads
@@ -993,13 +1018,23 @@ bool gen_pscatter_staged_source(const Plan& P, int log2p, std::string* src, bool
       << "#pragma unroll\n    for (int r = 0; r < 4; ++r) {\n"
       << "      if (!((ract >> r) & 1)) continue;\n"
       << "      const qu32 pos = s_off[bk[r]] + rk[r];\n"
-      << "      s_bkt[pos] = (unsigned short)bk[r];\n"
-      << "#pragma unroll\n      for (int q = 0; q < WC; ++q) s_rec[pos * WC + q] = "
-      << (L.narrow ? narrow_chunk("rw[r]", G, "q") : W % 2 ? "rw[r][q]" : "qi64x2{rw[r][2 * q], rw[r][2 * q + 1]}") << ";\n"
-      << "    }\n"
+      << "      s_bkt[pos] = (unsigned short)bk[r];\n";
+    if (fast)
+      o << "      s_perm[pos] = (unsigned short)((int)woff + 64 * r + lane);\n";
+    else
+      o << "#pragma unroll\n      for (int q = 0; q < WC; ++q) s_rec[pos * WC + q] = "
+        << (L.narrow ? narrow_chunk("rw[r]", G, "q") : W % 2 ? "rw[r][q]" : "qi64x2{rw[r][2 * q], rw[r][2 * q + 1]}") << ";\n";
+    o << "    }\n"
       << "    __syncthreads();\n"
       << "    const qu32 tot = s_total;\n";
-    if (soa)
+    if (fast)
+      o << "    for (qu32 j = threadIdx.x; j < tot; j += blockDim.x) {\n"
+        << "      const qu32 b = s_bkt[j], src = s_perm[j];\n"
+        << "      const qu64 dst = (j < s_lim[b] ? s_dst[b] : s_dst2[b]) + j;\n"
+        << "      qu32* d = (qu32*)(P.part_rec + dst * " << L.bytes() << "ull);\n"
+        << "#pragma unroll\n      for (int q = 0; q < W; ++q) d[q] = s_w[sb][q][src];\n"
+        << "    }\n";
+    else if (soa)
       // word-major: consecutive threads write consecutive records' word q (one run per word)
       o << "    for (qu32 c = threadIdx.x; c < tot * W; c += blockDim.x) {\n"
         << "      const qu32 q = c / tot, j = c - q * tot;\n"
@@ -1030,11 +1065,285 @@ bool gen_pscatter_staged_source(const Plan& P, int log2p, std::string* src, bool
   return true;
 }
 
+// Aggregation pass for chunked 32-bit records (QE_PAGG_FAST, default 1; the general form below
+// otherwise). Same walk (a wave takes whole chunks, one step of 256 records in flight ahead), but:
+//   * each lane takes 4 CONSECUTIVE records of the step and loads them as W 16-byte vectors (4 x W
+//     32-bit words, 16-byte aligned: a chunk is PART_CH x 4W bytes), instead of 4W strided 4-byte
+//     loads whose per-lane addresses each cost 64-bit arithmetic;
+//   * the LDS table keeps 32-bit keys (every key of a 32-bit record fits; EMPTY_KEY32 = INT32_MIN,
+//     that key itself in special slot S + 1) and 32-bit MIN / MAX accumulators where the input is a
+//     32-bit word (a value word, or a bare column), so those atomics move half the bytes;
+//   * the per-row LDS updates are branch-free: a row that is inactive, goes to the global table or
+//     has a null input adds into a sink slot (index SS, never flushed) instead of running under a
+//     per-row, per-aggregate exec-mask branch (the SALU half of the general pass's instructions).
+constexpr int PAGG_CHCAP = 2048;  // chunk-list entries a fast aggregation slice stages in LDS
+// record buffers of the fast aggregation pass in rotation (QE_PAGG_FAST_DEPTH, 2 or 4)
+static int pagg_fast_depth() {
+  static const int d = [] {
+    const char* e = getenv("QE_PAGG_FAST_DEPTH");
+    const int v = e && *e ? atoi(e) : 2;
+    return v == 4 ? 4 : 2;  // (a divisor of the 8 steps per chunk)
+  }();
+  return d;
+}
+static bool pagg_fast_env() {
+  static const bool v = [] {
+    const char* e = getenv("QE_PAGG_FAST");
+    return !(e && e[0] == '0');
+  }();
+  return v;
+}
+
+static bool gen_pagg_fast_source(const Plan& P, const PartLayout& L, int log2, std::string* src, size_t* lds_bytes) {
+  if (!L.narrow || L.row_word >= 0 || P.key_f64) return false;
+  const int W = L.words;
+  std::vector<std::string> val(P.naggs), ok(P.naggs);
+  std::vector<bool> acc32(P.naggs, false);
+  std::vector<Expr> ex;
+  if (L.colmode && !agg_inputs(P, &ex)) return false;
+  for (int j = 0; j < P.naggs; ++j) {
+    const DAgg& a = P.aggs[j];
+    if (a.acc != ACC_NONE && a.acc != ACC_SUM_I && a.acc != ACC_MIN_I && a.acc != ACC_MAX_I) return false;
+    if (L.colmode) {
+      val[j] = ex[j].v;
+      ok[j] = ex[j].ok;
+    } else {
+      val[j] = L.val_word[j] >= 0 ? "w" + std::to_string(L.val_word[j]) + "[r]" : "0";
+      ok[j] = (L.val_word[j] >= 0 && a.track_nn)
+                  ? "((qu32)(w" + std::to_string(L.flags_word) + "[r] >> " + std::to_string(1 + j) + ") & 1u)"
+                  : "1u";
+    }
+    const bool bare = L.colmode ? (a.ntok == 1 && a.tok[0].op == T_COL) : L.val_word[j] >= 0;
+    acc32[j] = (a.acc == ACC_MIN_I || a.acc == ACC_MAX_I) && bare;
+  }
+  const int S = 1 << log2, SS = S + 2;
+  // QE_PAGG_EXP=1: timing experiment, no LDS work (never for results)
+  static const int exp = [] {
+    const char* e = getenv("QE_PAGG_EXP");
+    return e && *e ? atoi(e) : 0;
+  }();
+  std::ostringstream o;
+  o << "\nusing namespace qe;\n"
+    << "extern \"C\" __global__ void __launch_bounds__(" << pagg_block() << ") qe_pagg(const Plan P) {\n"
+    << "  if ((qi64)blockIdx.x >= P.part_slice[0]) return;\n"
+    << "  const qi64 clo = P.part_slice[2 + 2 * (qi64)blockIdx.x];\n"
+    << "  const qi64 hx = P.part_slice[3 + 2 * (qi64)blockIdx.x];\n"
+    << "  const bool excl = (hx & PART_EXCL) != 0;\n"
+    << "  const qi64 hi = ((hx & ~PART_EXCL) - clo) * PART_CH;\n"
+    << "  if (hi <= 0) return;\n"
+    << "  if (P.t.ctl[7]) return;  // a value did not fit the 32-bit records: the update reruns wide\n"
+    << "  __shared__ int s_fail;\n  __shared__ qu32 s_newg;\n  if (threadIdx.x == 0) { s_fail = 0; s_newg = 0; }\n"
+    << "  constexpr int LOG2 = " << log2 << ", S = " << S << ", SS = " << SS << ", SINK = SS;\n"
+    << "  __shared__ qi32 s_keys[SS + 1];\n  __shared__ qu32 s_cst[SS + 1];\n";
+  size_t lds = (size_t)(SS + 1) * 8;
+  for (int j = 0; j < P.naggs; ++j) {
+    const DAgg& a = P.aggs[j];
+    if (a.acc != ACC_NONE) {
+      o << "  __shared__ " << (acc32[j] ? "qi32" : "qi64") << " s_acc" << j << "[SS + 1];\n";
+      lds += (size_t)(SS + 1) * (acc32[j] ? 4 : 8);
+    }
+    if (a.track_nn) {
+      o << "  __shared__ qu32 s_nn" << j << "[SS + 1];\n";
+      lds += (size_t)(SS + 1) * 4;
+    }
+  }
+  *lds_bytes = lds;
+  auto init32 = [](int acc) {
+    return acc == ACC_MIN_I ? std::string("0x7FFFFFFF") : acc == ACC_MAX_I ? std::string("(qi32)0x80000000u") : "0";
+  };
+  o << "  for (int s = threadIdx.x; s < SS + 1; s += blockDim.x) {\n    s_keys[s] = EMPTY_KEY32;\n    s_cst[s] = 0;\n";
+  for (int j = 0; j < P.naggs; ++j) {
+    const DAgg& a = P.aggs[j];
+    if (a.acc != ACC_NONE) o << "    s_acc" << j << "[s] = " << (acc32[j] ? init32(a.acc) : acc_init(a.acc)) << ";\n";
+    if (a.track_nn) o << "    s_nn" << j << "[s] = 0;\n";
+  }
+  // the slice's chunk list (id, fill) staged in LDS, CHCAP chunks per round: the walk's per-step
+  // lookups are then LDS reads, off the in-order vector-memory counter the record loads wait on
+  // (a global lookup under a branch made the compiler wait for every outstanding load there)
+  o << "  }\n"
+    << "  constexpr int CHCAP = " << PAGG_CHCAP << ";\n  __shared__ qu64 s_ch[CHCAP];\n"
+    << "  const qi64 nch = hi / PART_CH;\n"
+    << "  const int lane = threadIdx.x & 63;\n"
+    << "  const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), nwv = blockDim.x >> 6;\n"
+    ;
+  lds += (size_t)PAGG_CHCAP * 8;
+  // D rotating record buffers: step t consumes buffer t % D in place and reloads it with step t + D,
+  // so each step's loads have the next D - 1 steps' work to land (one buffer copied forward made
+  // the loop's back edge wait for the loads it had just issued)
+  const int D = pagg_fast_depth();
+  o << "  qu64 xacc = 0;\n";
+  for (int k = 0; k < D; ++k) {
+    o << "  qu32 b" << k << "_act;\n  qi64 b" << k << "_pb;\n";
+    for (int v = 0; v < W; ++v) o << "  qu32x4 b" << k << "_v" << v << ";\n";
+  }
+  auto NB = [](const std::string& t) {
+    return "((qi64)(wv + ((" + t + ") >> 3) * nwv) * PART_CH + (qi64)((" + t + ") & 7) * 256)";
+  };
+  auto load_step = [&](int k, const std::string& nb) {
+    const std::string B = "b" + std::to_string(k) + "_";
+    // branch-free (a step past the wave's last one loads a real chunk's slots, all inactive)
+    o << "    {\n      const qi64 nb = " << nb << ";\n      const bool in = nb < rhi;\n"
+      << "      const qu64 m = s_ch[in ? (int)(nb >> 11) : 0];\n"
+      << "      const qi32 ko = (qi32)(nb & (PART_CH - 1));\n"
+      << "      const qi64 npb = (qi64)(qi32)(qu32)m * PART_CH + ko;\n      const qi32 cfill = in ? (qi32)(m >> 32) - ko : 0;\n"
+      << "      const qu32x4* p = (const qu32x4*)(P.part_rec + (qu64)(npb + 4 * lane) * " << L.bytes() << "ull);\n";
+    for (int v = 0; v < W; ++v) o << "      " << B << "v" << v << " = " << ld("qu32x4", "p + " + std::to_string(v)) << ";\n";
+    o << "      " << B << "pb = npb;\n      qu32 nact = 0;\n"
+      << "#pragma unroll\n      for (int r = 0; r < 4; ++r) nact |= (qu32)(4 * lane + r < cfill) << r;\n"
+      << "      if (P.defer_in) {  // (uniform: retry passes only)\n"
+      << "        for (int r = 0; r < 4; ++r) { const qi64 i = npb + 4 * lane + r; if (!((P.defer_in[i >> 5] >> (i & 31)) & 1)) nact &= ~(1u << r); }\n"
+      << "      }\n      " << B << "act = nact;\n    }\n";
+  };
+  o << "  for (qi64 c0 = 0; c0 < nch; c0 += CHCAP) {\n"
+    << "  const qi64 rch = nch - c0 < CHCAP ? nch - c0 : CHCAP, rhi = rch * PART_CH;\n"
+    << "  if (c0) __syncthreads();  // every wave is done with the previous round's list\n"
+    << "  for (qi64 c = threadIdx.x; c < rch; c += blockDim.x) {\n"
+    << "    const qi32 id = P.part_sorted[clo + c0 + c];\n"
+    << "    s_ch[c] = (qu64)(qu32)id | ((qu64)P.part_chunk[1 + id] << 32);\n  }\n"
+    << "  __syncthreads();\n";
+  for (int k = 0; k < D; ++k) load_step(k, NB(std::to_string(k)));
+  // the wave's steps: 8 per chunk it takes (wv, wv + nwv, ...), a multiple of D, so the unrolled
+  // loop has no exit between a buffer's reload and its use
+  o << "  const int nsteps = wv < rch ? (int)((rch - 1 - wv) / nwv + 1) * 8 : 0;\n"
+    << "  for (int t = 0; t < nsteps; t += " << D << ") {\n";
+  for (int k = 0; k < D; ++k) {
+  const std::string B = "b" + std::to_string(k) + "_";
+  o << "  {\n"
+    << "    const qi64 sbase = " << B << "pb;\n    const qu32 act = " << B << "act;\n"
+    << "    const qu32 d[" << 4 * W << "] = {";
+  for (int v = 0; v < W; ++v)
+    o << (v ? ", " : "") << B << "v" << v << ".x, " << B << "v" << v << ".y, " << B << "v" << v << ".z, " << B << "v" << v << ".w";
+  o << "};\n"
+    << "    qi64 key[4];\n";
+  for (int q = 1; q < W; ++q) o << "    qi64 w" << q << "[4];\n";
+  o << "#pragma unroll\n    for (int r = 0; r < 4; ++r) {\n      key[r] = (qi64)(qi32)d[r * " << W << "];\n";
+  for (int q = 1; q < W; ++q) o << "      w" << q << "[r] = (qi64)(qi32)d[r * " << W << " + " << q << "];\n";
+  o << "    }\n    qu32 knull = 0;\n";
+  if (L.flags_word >= 0)
+    o << "#pragma unroll\n    for (int r = 0; r < 4; ++r) knull |= (qu32)(w" << L.flags_word << "[r] & 1) << r;\n";
+  for (int c = 0; c < P.ncols; ++c) {
+    if (L.col_word[c] < 0) continue;
+    const std::string cs = std::to_string(c);
+    o << "    qi64 (&c" << cs << ")[4] = w" << L.col_word[c] << ";\n";
+    if (P.cols[c].valid)
+      o << "    qu32 v" << cs << " = 0;\n"
+        << "#pragma unroll\n    for (int r = 0; r < 4; ++r) v" << cs << " |= ((qu32)(w" << L.flags_word << "[r] >> "
+        << (1 + c) << ") & 1u) << r;\n";
+  }
+  // slots: the first probe of all 4 rows together; collisions (rare) probe on
+  if (exp == 1) {  // timing experiment: the records' walk and loads only (wrong results)
+    o << "#pragma unroll\n    for (int r = 0; r < 4; ++r) xacc ^= (qu64)key[r]";
+    for (int q = 1; q < W; ++q) o << " ^ (qu64)w" << q << "[r]";
+    o << " ^ act;\n  }\n";
+    load_step(k, NB("t + " + std::to_string(k + D)));
+    continue;
+  }
+  o << "    int slot[4];\n    qu32 h[4];\n    qi32 k0[4];\n"
+    << "#pragma unroll\n    for (int r = 0; r < 4; ++r) { h[r] = lds_hash((qu64)key[r]) >> (32 - LOG2); k0[r] = s_keys[h[r]]; }\n"
+    << "#pragma unroll\n    for (int r = 0; r < 4; ++r) slot[r] = ((knull >> r) & 1) ? S : ((qi32)key[r] == EMPTY_KEY32 ? S + 1 : (k0[r] == (qi32)key[r] ? (int)h[r] : -1));\n"
+    << "    qu32 miss = 0;\n"
+    << "#pragma unroll\n    for (int r = 0; r < 4; ++r) miss |= (qu32)(slot[r] < 0) << r;\n"
+    << "    miss &= act;\n"
+    << "    if (miss) {\n      for (int r = 0; r < 4; ++r) if ((miss >> r) & 1) slot[r] = lds_probe32(s_keys, LOG2, (qi32)key[r], h[r]);\n    }\n"
+    << "    qu32 glob = 0;\n"
+    << "#pragma unroll\n    for (int r = 0; r < 4; ++r) glob |= (qu32)(slot[r] < 0) << r;\n"
+    << "    glob &= act;\n    const qu32 loc = act & ~glob;\n"
+    << "    int sl[4];\n"
+    << "#pragma unroll\n    for (int r = 0; r < 4; ++r) sl[r] = ((loc >> r) & 1) ? slot[r] : SINK;\n"
+    << "#pragma unroll\n    for (int r = 0; r < 4; ++r) atomicAdd(&s_cst[sl[r]], 1u);\n";
+  for (int j = 0; j < P.naggs; ++j) {
+    const DAgg& a = P.aggs[j];
+    if (a.pkind == 0) continue;
+    const std::string js = std::to_string(j);
+    o << "#pragma unroll\n    for (int r = 0; r < 4; ++r) {\n"
+      << "      const int s = (" << ok[j] << ") ? sl[r] : SINK;\n"
+      << "      const qi64 x = " << val[j] << ";\n";
+    if (a.track_nn) o << "      atomicAdd(&s_nn" << js << "[s], 1u);\n";
+    switch (a.acc) {
+      case ACC_SUM_I: o << "      atomicAdd((qu64*)&s_acc" << js << "[s], (qu64)x);\n"; break;
+      case ACC_MIN_I:
+        o << "      atomicMin(&s_acc" << js << "[s], " << (acc32[j] ? "(qi32)x" : "x") << ");\n";
+        break;
+      case ACC_MAX_I:
+        o << "      atomicMax(&s_acc" << js << "[s], " << (acc32[j] ? "(qi32)x" : "x") << ");\n";
+        break;
+      default: break;
+    }
+    o << "    }\n";
+  }
+  // rows whose group only fits the global table (rare)
+  o << "    if (glob) {\n      for (int r = 0; r < 4; ++r) {\n        if (!((glob >> r) & 1)) continue;\n"
+    << "        const qi64 lr = sbase + 4 * lane + r;\n        qu64 gs;\n"
+    << "        if (!gtable_find(P.t, key[r], (knull >> r) & 1, gs)) {\n"
+    << "          atomicOr((qu32*)&P.defer_out[lr >> 5], 1u << (lr & 31));\n"
+    << "          atomicAdd(&P.t.ctl[1], 1ull);\n          continue;\n        }\n"
+    << "        gadd_cstar(P.t, gs, 1);\n";
+  for (int j = 0; j < P.naggs; ++j) {
+    const DAgg& a = P.aggs[j];
+    if (a.pkind == 0) continue;
+    o << "        if (" << ok[j] << ") { const RowVal rv = row_partial(" << a.acc << ", " << val[j]
+      << ", 0); gcombine(P.t, " << a.acc << ", " << j << ", gs, rv.acc, 1, rv.i0, rv.i1, rv.i2, rv.i3, "
+      << (((P.nn_skip >> j) & 1) ? "false" : "true") << "); }\n";
+  }
+  o << "      }\n    }\n  }\n";
+  load_step(k, NB("t + " + std::to_string(k + D)));
+  }  // buffers
+  o << "  }\n  }\n";
+  // flush (exclusive slices: plain read-modify-writes), as emit_flush with 32-bit keys / accumulators
+  o << "  if (xacc == 0x9E3779B97F4A7C15ull) s_fail = 3;  // (keeps the experiment's loads live)\n"
+    << "  __syncthreads();\n"
+    << "  for (int s = threadIdx.x; s < SS; s += blockDim.x) {\n"
+    << "    const qu32 c = s_cst[s];\n    if (c == 0) continue;\n"
+    << "    const bool knl = s == S;\n    const qi64 key = knl ? 0 : (s == S + 1 ? (qi64)EMPTY_KEY32 : (qi64)s_keys[s]);\n"
+    << "    qu64 gs;\n"
+    << "    const bool ok = gtable_find_wg(P.t, key, knl, gs, &s_newg);\n"
+    << "    qu8* rec = nullptr;\n"
+    << "    if (ok) {\n      if (excl) gadd_cstar_excl(P.t, gs, c, &s_newg); else gadd_cstar(P.t, gs, c);\n    } else {\n"
+    << "      const qu64 ri = atomicAdd(&P.t.ctl[2], 1ull);\n"
+    << "      if (ri >= P.ovf_cap) { s_cst[s] = c | 0x80000000u; s_fail = 1; continue; }\n"
+    << "      rec = P.ovf + ri * (qu64)P.rec_bytes;\n      write_record_head(rec, key, knl, c);\n    }\n";
+  int off = 24;
+  for (int j = 0; j < P.naggs; ++j) {
+    const DAgg& a = P.aggs[j];
+    const std::string js = std::to_string(j);
+    o << "    {\n      const qi64 acc = " << (a.acc != ACC_NONE ? "(qi64)s_acc" + js + "[s]" : std::string("0")) << ";\n"
+      << "      const qu64 nn = " << (a.track_nn ? "s_nn" + js + "[s]" : std::string("c")) << ";\n";
+    const bool skip_nn = (P.nn_skip >> j) & 1;
+    if (a.fn != QE_AGG_COUNT_STAR)
+      o << "      if (ok) { if (excl) gcombine_excl(P.t, " << a.acc << ", " << j << ", gs, acc, nn, ~0ull, ~0ull, ~0ull, ~0ull);"
+        << " else gcombine(P.t, " << a.acc << ", " << j << ", gs, acc, nn, ~0ull, ~0ull, ~0ull, ~0ull, "
+        << (skip_nn ? "false" : "true") << "); }\n";
+    o << "      if (!ok) { qu64* f = (qu64*)(rec + " << off << "); f[0] = (qu64)acc; f[1] = nn; }\n    }\n";
+    off += agg_rec_bytes(a.acc);
+  }
+  o << "  }\n";
+  // groups that found no room anywhere: defer their records (the table is final)
+  o << "  __syncthreads();\n"
+    << "  if (s_fail) {\n"
+    << "    for (qi64 v = threadIdx.x; v < hi; v += blockDim.x) {\n"
+    << "      const qi64 id = P.part_sorted[clo + v / PART_CH], ko = v % PART_CH;\n"
+    << "      if (ko >= (P.part_chunk[1 + id] & 0xFFFFFFFFll)) continue;\n"
+    << "      const qi64 i = id * PART_CH + ko;\n"
+    << "      if (P.defer_in && !((P.defer_in[i >> 5] >> (i & 31)) & 1)) continue;\n"
+    << "      const qi32* rp = (const qi32*)(P.part_rec + i * " << L.bytes() << "ull);\n"
+    << "      const qi32 k = rp[0];\n"
+    << "      const bool kn = " << (L.flags_word >= 0 ? "rp[" + std::to_string(L.flags_word) + "] & 1" : std::string("false")) << ";\n"
+    << "      int s = kn ? S : (k == EMPTY_KEY32 ? S + 1 : -1);\n"
+    << "      if (s < 0) { const qu32 hh = lds_hash((qu64)(qi64)k) >> (32 - LOG2); s = s_keys[hh] == k ? (int)hh : lds_probe32(s_keys, LOG2, k, hh); }\n"
+    << "      if (s >= 0 && (s_cst[s] & 0x80000000u)) {\n"
+    << "        atomicOr((qu32*)&P.defer_out[i >> 5], 1u << (i & 31));\n"
+    << "        atomicAdd(&P.t.ctl[1], 1ull);\n      }\n    }\n  }\n"
+    << "  if (threadIdx.x == 0 && s_newg) atomicAdd(&P.t.ctl[0], (qu64)s_newg);\n}\n";
+  *src = std::string(kDevHeader) + o.str();
+  return true;
+}
+
 // `soa` (chunked only): records stored chunk-columnar, word q of slot i at
 // ((i / PART_CH) * W + q) * PART_CH + i % PART_CH (the spilling fused pass writes them so).
 bool gen_pagg_source(const Plan& P, int log2, std::string* src, size_t* lds_bytes, bool chunked, bool soa) {
   if (log2 < 4 || log2 > 16 || (soa && !chunked)) return false;
   const PartLayout L = part_layout(P);
+  if (chunked && !soa && pagg_fast_env() && gen_pagg_fast_source(P, L, log2, src, lds_bytes)) return true;
   std::vector<std::string> val(P.naggs), ok(P.naggs);
   if (L.colmode) {
     // the programs run here, over column values read back from the record (c<slot>[r], v<slot>)

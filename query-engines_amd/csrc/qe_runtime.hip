@@ -421,19 +421,32 @@ struct StreamShape {
   int slabs;    // 1 KiB slabs per column per wave step (rows only)
   int block;    // threads per workgroup
   int per_cu;   // workgroups per CU
+  int lds_kb;   // dynamic LDS per workgroup (unused by the kernel): holds the grid to per_cu per CU
 };
+// The pinned shapes (lds_kb > 0) place workgroups the way the LDS-table kernels are placed: the
+// fused aggregate's 147 KiB table admits exactly one 1024-thread workgroup per CU, while a kernel
+// with no LDS may be dealt two workgroups on one CU and none on another (round 3 measured the
+// fused kernel slightly above the best unpinned shape: 6.70 vs 6.65 TB/s).
 static const StreamShape kStreamShapes[] = {
-    {1, 1, 2, 1024, 1}, {1, 1, 2, 1024, 2}, {1, 1, 2, 512, 4}, {1, 1, 1, 256, 8}, {1, 1, 4, 256, 4},
-    {1, 1, 2, 256, 8},  {1, 0, 2, 1024, 2}, {0, 1, 0, 512, 4}, {0, 1, 0, 512, 8}, {0, 0, 0, 512, 4},
+    {1, 1, 2, 1024, 1, 0}, {1, 1, 2, 1024, 2, 0}, {1, 1, 2, 512, 4, 0}, {1, 1, 1, 256, 8, 0}, {1, 1, 4, 256, 4, 0},
+    {1, 1, 2, 256, 8, 0},  {1, 0, 2, 1024, 2, 0}, {0, 1, 0, 512, 4, 0}, {0, 1, 0, 512, 8, 0}, {0, 0, 0, 512, 4, 0},
+    {1, 1, 2, 1024, 1, 96}, {1, 1, 4, 1024, 1, 96}, {1, 1, 2, 512, 2, 64}, {1, 1, 4, 512, 2, 64},
 };
 constexpr int kNumStreamShapes = (int)(sizeof(kStreamShapes) / sizeof(kStreamShapes[0]));
 
 template <bool NT, int SLABS>
-static void launch_rows(const StreamCols& c, int grid, int block, hipStream_t st, unsigned long long* out) {
+static void launch_rows(const StreamCols& c, int grid, int block, hipStream_t st, unsigned long long* out,
+                        size_t lds = 0) {
+  if (lds > 0) {  // (above 64 KiB a kernel must opt in to its dynamic LDS)
+    (void)hipFuncSetAttribute((const void*)k_stream_read_rows<NT, SLABS, 3>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              (int)lds);
+    (void)hipFuncSetAttribute((const void*)k_stream_read_rows<NT, SLABS, 8>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              (int)lds);
+  }
   if (c.ncols <= 3)
-    hipLaunchKernelGGL((k_stream_read_rows<NT, SLABS, 3>), dim3(grid), dim3(block), 0, st, c, out);
+    hipLaunchKernelGGL((k_stream_read_rows<NT, SLABS, 3>), dim3(grid), dim3(block), lds, st, c, out);
   else
-    hipLaunchKernelGGL((k_stream_read_rows<NT, SLABS, 8>), dim3(grid), dim3(block), 0, st, c, out);
+    hipLaunchKernelGGL((k_stream_read_rows<NT, SLABS, 8>), dim3(grid), dim3(block), lds, st, c, out);
 }
 
 static void launch_stream_shape(const StreamShape& sh, const StreamCols& c, int cus, hipStream_t st,
@@ -446,10 +459,11 @@ static void launch_stream_shape(const StreamShape& sh, const StreamCols& c, int 
       hipLaunchKernelGGL(k_stream_read<false>, dim3(grid), dim3(sh.block), 0, st, c, out);
     return;
   }
+  const size_t lds = (size_t)sh.lds_kb * 1024;
   if (sh.nt) {
-    if (sh.slabs == 1) launch_rows<true, 1>(c, grid, sh.block, st, out);
-    else if (sh.slabs == 4) launch_rows<true, 4>(c, grid, sh.block, st, out);
-    else launch_rows<true, 2>(c, grid, sh.block, st, out);
+    if (sh.slabs == 1) launch_rows<true, 1>(c, grid, sh.block, st, out, lds);
+    else if (sh.slabs == 4) launch_rows<true, 4>(c, grid, sh.block, st, out, lds);
+    else launch_rows<true, 2>(c, grid, sh.block, st, out, lds);
   } else {
     launch_rows<false, 2>(c, grid, sh.block, st, out);
   }
@@ -596,7 +610,7 @@ int qe_stream_read(qe_ctx* ctx, const qe_column* cols, int32_t ncols, double* ms
   bool same = false;
   QE_TRY(stream_cols(cols, ncols, &c, &same));
   const bool nt = !(getenv("QE_NT") && getenv("QE_NT")[0] == '0');  // non-temporal (default), as the fused kernels
-  const StreamShape sh = same ? StreamShape{1, nt ? 1 : 0, 2, 1024, 1} : StreamShape{0, nt ? 1 : 0, 0, 512, 4};
+  const StreamShape sh = same ? StreamShape{1, nt ? 1 : 0, 2, 1024, 1, 96} : StreamShape{0, nt ? 1 : 0, 0, 512, 4, 0};
   return stream_time(ctx, sh, c, ms);
 }
 
@@ -624,8 +638,8 @@ int qe_stream_read_best(qe_ctx* ctx, const qe_column* cols, int32_t ncols, int32
   *ms = best;
   if (shape && shape_len > 0) {
     const StreamShape& sh = kStreamShapes[bi];
-    snprintf(shape, (size_t)shape_len, "%s%s, %d slab(s), %d threads x %d per CU", sh.rows ? "row-interleaved" : "column-serial",
-             sh.nt ? " nt" : "", sh.slabs, sh.block, sh.per_cu);
+    snprintf(shape, (size_t)shape_len, "%s%s, %d slab(s), %d threads x %d per CU%s", sh.rows ? "row-interleaved" : "column-serial",
+             sh.nt ? " nt" : "", sh.slabs, sh.block, sh.per_cu, sh.lds_kb ? " (LDS-pinned)" : "");
   }
   return QE_OK;
 }
