@@ -140,7 +140,10 @@ struct Plan {
   qi32 mp_n, mp_pass;
   // radix-partitioned records in 32-bit words when the plan's words are integral (part_layout):
   // the scatter sets t.ctl[7] if a value did not fit, and the aggregation pass then does nothing
-  qi32 part_narrow, pad1;
+  qi32 part_narrow;
+  // fused aggregate with a compact LDS table (qe_jit.hip compact_*): this many slots of 32-bit keys
+  // (and 32-bit MIN / MAX where the input is a bare column), 0 = the regular 2^lds_log2 table
+  qi32 lds_compact;
   // spilling first pass (spill_update): rows with fmix64(key) >> 32 >= mp_keep are spilled as records
   qu64 mp_keep;
   // select-project: pinned host words the kernel writes its results to ([0] rows written, [1] the
@@ -581,6 +584,57 @@ __device__ inline int lds_probe32(qi32* keys, int log2, qi32 key, qu32 h) {
       if (old == EMPTY_KEY32 || old == key) return (int)h;
     }
     h = (h + 1) & mask;
+  }
+  return -1;
+}
+
+// Tables of 32-bit keys in 4-slot buckets (16-byte aligned; the fast aggregation pass and the
+// compact fused table): a key lives in its home bucket or, if that filled up first, a later one,
+// so a lookup is one 16-byte LDS read and four compares (a home bucket of four slots at <= 65 %
+// load almost never overflows). Slots fill in order and are never emptied, so a lookup may stop
+// at a bucket with an empty slot. Continues from home bucket b; returns the slot, -1 at the limit.
+__device__ inline int lds_probe4(qi32* keys, qu32 nb, qi32 key, qu32 b) {
+#pragma unroll 1
+  for (int p = 0; p < HA_LDS_MAXP; ++p) {
+    const qu32x4 q = *(const volatile qu32x4*)(keys + 4 * b);
+    const qi32 kk[4] = {(qi32)q.x, (qi32)q.y, (qi32)q.z, (qi32)q.w};
+#pragma unroll 1
+    for (int i = 0; i < 4; ++i) {
+      if (kk[i] == key) return (int)(4 * b) + i;
+      if (kk[i] == EMPTY_KEY32) {
+        const qi32 old = atomicCAS(&keys[4 * b + i], EMPTY_KEY32, key);
+        if (old == EMPTY_KEY32 || old == key) return (int)(4 * b) + i;
+        // another key took it: the later slots of the snapshot are still candidates
+      }
+    }
+    b = b + 1 == nb ? 0 : b + 1;
+  }
+  return -1;
+}
+
+// Slot of `kk` among the 8 slots of bucket b and the bucket b2 after it (their 16-byte snapshots q,
+// q2), or -1: the hit test of the 4-slot-bucket tables without a branch. Keys that lds_probe4
+// placed one bucket past their own are found here too (at a half-full table ~4 % of the keys;
+// the home bucket alone sent nearly every 256-record step down the serial probe loop).
+__device__ inline int bucket2_hit(qu32x4 q, qu32x4 q2, qu32 kk, qu32 b, qu32 b2) {
+  const qu32 m = (qu32)(q.x == kk) | ((qu32)(q.y == kk) << 1) | ((qu32)(q.z == kk) << 2) | ((qu32)(q.w == kk) << 3) |
+                 ((qu32)(q2.x == kk) << 4) | ((qu32)(q2.y == kk) << 5) | ((qu32)(q2.z == kk) << 6) |
+                 ((qu32)(q2.w == kk) << 7);
+  const int i = __builtin_ctz(m | 0x100u);
+  return i < 4 ? (int)(4 * b) + i : (i < 8 ? (int)(4 * b2) + i - 4 : -1);
+}
+
+// lds_probe32 over a table of `nsl` slots (any count: the compact fused table).
+__device__ inline int lds_probe32n(qi32* keys, qu32 nsl, qi32 key, qu32 h) {
+#pragma unroll 1
+  for (int p = 0; p < HA_LDS_MAXP; ++p) {
+    const qi32 k = keys[h];
+    if (k == key) return (int)h;
+    if (k == EMPTY_KEY32) {
+      const qi32 old = atomicCAS(&keys[h], EMPTY_KEY32, key);
+      if (old == EMPTY_KEY32 || old == key) return (int)h;
+    }
+    h = h + 1 == nsl ? 0 : h + 1;
   }
   return -1;
 }

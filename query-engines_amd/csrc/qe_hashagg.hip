@@ -1450,6 +1450,7 @@ struct qe_hashagg {
   // 32-bit partition records (Plan.part_narrow): off for good once a value did not fit
   bool part_wide = false;
   bool narrow_failed = false;  // the last settled launch saw ctl[7] set
+  bool compact_off = false;    // a value did not fit the compact fused table (ctl[7] bit 1): not again
   // overflow records
   uint8_t* ovf = nullptr;
   uint64_t ovf_cap = 0;
@@ -1989,7 +1990,8 @@ static int partition_rows(qe_hashagg* h, Plan& P, hipFunction_t* fn, int* grid) 
   QE_CHECK((chunked || gen_part_source(P, log2p, false, &sc)) &&
                (staged ? gen_pscatter_staged_source(P, log2p, &ss, chunked, chunked && part_soa())
                        : gen_part_source(P, log2p, true, &ss)) &&
-               gen_pagg_source(P, tlog2, &sa, &jl, chunked, chunked && part_soa()),
+               gen_pagg_source(P, tlog2, &sa, &jl, chunked, chunked && part_soa(),
+                               (int64_t)(h->expected_groups >> log2p) + 1),
            QE_ERR_UNSUPPORTED, "plan shape not specialisable");
   hipFunction_t fc = nullptr, fs;
   int bpc = 0;
@@ -2182,6 +2184,7 @@ static int launch_pass(qe_hashagg* h, Plan& P, size_t& lds, hipFunction_t pfn, i
                                        (int64_t)div_up((uint64_t)waves, fused_block(P.lds_log2) / 64));
         if (jgrid < 1) jgrid = 1;
         h->jit_note.clear();
+        if (P.lds_compact) h->jit_note = "compact LDS table: " + std::to_string(P.lds_compact) + " slots";
       } else {
         h->jit_note = qe_last_error();
         jfn = nullptr;
@@ -2254,7 +2257,8 @@ static int settle_pass(qe_hashagg* h, const Plan& P, int* out_i, const uint32_t*
   QE_CHECK(c[6] == 0, QE_ERR_UNSUPPORTED,
            "deterministic fp64 SUM: %llu inputs outside the exact fixed-point range (NaN, +-Inf or |x| >= 2^63)",
            (unsigned long long)c[6]);
-  h->narrow_failed = P.part_narrow && c[7] != 0;
+  h->narrow_failed = P.part_narrow && (c[7] & 1) != 0;
+  if (P.lds_compact && (c[7] & 2)) h->compact_off = true;
   const uint64_t groups = c[0], deferred = c[1], ovf_recs = std::min<uint64_t>(c[2], P.ovf_cap);
   h->ctl_rows_clean = c[1] == 0 && c[2] == 0;
   *done = true;
@@ -2450,6 +2454,38 @@ static int run_update(qe_hashagg* h, Plan& P) {
   // their edge (3000 groups 2.88 ms, 3800 groups 3.44 ms against 3.09 ms partitioned).
   size_t lds_mp = 0;
   int mp_n = 0;
+  // Groups just past the regular LDS table: one pass with the compact table (qe_jit.hip
+  // compact_*, 32-bit keys, <= 80 % load) when the plan shape and the expected groups allow it
+  // (QE_LDS_COMPACT=0: never; read per call), before key-hash passes / spilling.
+  const char* ce = getenv("QE_LDS_COMPACT");
+  if (!lds && ctx->jit && h->expected_groups > 0 && !h->compact_off && !(ce && ce[0] == '0') && compact_ok(P)) {
+    Plan T = P;
+    T.lds_log2 = 16;  // (unused by the compact kernel; keeps adapt_after_update from resizing)
+    const size_t bps = compact_slot_bytes(T);
+    const int64_t nsl = ((int64_t)((lds_budget(ctx) - 512) / bps) - 66) & ~(int64_t)63;  // (+2 special, 64 sinks)
+    if (nsl >= 512 && nsl >= (h->expected_groups * 5 + 3) / 4) {
+      T.lds_compact = (qi32)nsl;
+      std::string src;
+      size_t jl = 0;
+      hipFunction_t f = nullptr;
+      int bpc = 0;
+      if (gen_fused_source(T, T.lds_log2, &src, &jl) && jit_kernel(ctx, src, &f, &bpc, "qe_fused", fused_block(16)) == QE_OK) {
+        const uint64_t need = (uint64_t)ctx->num_cus * 8 * ((uint64_t)nsl + 2);
+        if (h->ovf_cap < need) {
+          dev_free(ctx, h->ovf);
+          h->ovf = nullptr;
+          h->ovf_cap = 0;
+          QE_TRY(dev_alloc(ctx, need * h->rec_bytes, (void**)&h->ovf));
+          h->ovf_cap = need;
+        }
+        T.ovf = h->ovf;
+        T.ovf_cap = h->ovf_cap;
+        QE_HIP(hipMemsetAsync(h->ctl + 7, 0, 8, ctx->stream));
+        P = T;
+        lds = jl;
+      }
+    }
+  }
   // The generic kernel (JIT off, or no specialised kernel) passes too, with its own 80 KiB budget:
   // it has no partitioned path to fall back on, and global-only rows cost a device atomic each.
   if (!lds && h->expected_groups > 0) {

@@ -72,6 +72,10 @@ int ctx_workspace(qe_ctx* ctx, int slot, size_t bytes, void** out);  // grow-onl
 int parallel_h2d_copy(qe_ctx* ctx, void* dst, const void* src, size_t n);
 // Per-plan kernel specialisation (qe_jit.hip).
 bool gen_fused_source(const qe::Plan& P, int log2, std::string* src, size_t* lds_bytes, bool spill = false);
+// compact fused LDS table (Plan.lds_compact): plan shapes it supports, bytes per slot, 32-bit MIN/MAX
+bool compact_ok(const qe::Plan& P);
+size_t compact_slot_bytes(const qe::Plan& P);
+bool compact_acc32(const qe::Plan& P, int j);
 // Radix-partitioned aggregation for group counts beyond the LDS table (qe_jit.hip).
 struct PartLayout {
   int words = 0;  // record width in 8-byte words
@@ -89,8 +93,9 @@ struct PartLayout {
 };
 PartLayout part_layout(const qe::Plan& P);
 bool gen_part_source(const qe::Plan& P, int log2p, bool scatter, std::string* src);
+// bucket_groups: expected groups per bucket (0: unknown), which sizes the fast pass's table
 bool gen_pagg_source(const qe::Plan& P, int log2, std::string* src, size_t* lds_bytes, bool chunked = false,
-                     bool soa = false);
+                     bool soa = false, int64_t bucket_groups = 0);
 bool part_staged_ok(const qe::Plan& P, int log2p);
 int pscatter_block();
 bool pscatter_wide();

@@ -427,6 +427,133 @@ void emit_flush(const Plan& P, std::ostringstream& o, bool mark_full = false, bo
   o << "  }\n";
 }
 
+// ---- compact LDS table of the fused aggregate (Plan.lds_compact slots) --------------------------------
+// Groups just past the regular table (~2.5K for the C4 shape) used to take two key-hash passes or
+// a spilling pass. A slot of 32-bit key + COUNT(*) + per aggregate a 64-bit SUM or a 32-bit MIN /
+// MAX (bare column inputs) is 24 B for C4 instead of 36, so one 152 KiB table holds ~6.2K slots:
+// up to ~5K groups in one pass at <= 80 % load. The slot count is any number (multiply-shift
+// slot hash). Speculative like the 32-bit records: a row whose key or 32-bit accumulator input
+// does not fit 32 bits goes to the global table directly (correct, slow) and sets ctl[7] bit 1,
+// after which the state no longer uses the compact table.
+namespace {
+
+void emit_lds_table_c(const Plan& P, std::ostringstream& o, size_t* lds_bytes) {
+  const int NSL = P.lds_compact;
+  o << "  constexpr qu32 NSL = " << NSL << ", NBK = NSL / 4;\n  constexpr int S = " << NSL << ", SS = " << NSL + 2 << ", SINK = SS;\n"
+    << "  __shared__ __attribute__((aligned(16))) qi32 s_keys[SS + 64];\n  __shared__ qu32 s_cst[SS + 64];\n";
+  for (int j = 0; j < P.naggs; ++j) {
+    const DAgg& a = P.aggs[j];
+    if (a.acc != ACC_NONE) o << "  __shared__ " << (compact_acc32(P, j) ? "qi32" : "qi64") << " s_acc" << j << "[SS + 64];\n";
+    if (a.track_nn) o << "  __shared__ qu32 s_nn" << j << "[SS + 64];\n";
+  }
+  *lds_bytes = (size_t)(NSL + 66) * compact_slot_bytes(P);
+  o << "  for (int s = threadIdx.x; s < SS + 64; s += blockDim.x) {\n    s_keys[s] = EMPTY_KEY32;\n    s_cst[s] = 0;\n";
+  for (int j = 0; j < P.naggs; ++j) {
+    const DAgg& a = P.aggs[j];
+    if (a.acc != ACC_NONE)
+      o << "    s_acc" << j << "[s] = "
+        << (compact_acc32(P, j) ? (a.acc == ACC_MIN_I ? std::string("0x7FFFFFFF") : std::string("(qi32)0x80000000u"))
+                                : acc_init(a.acc))
+        << ";\n";
+    if (a.track_nn) o << "    s_nn" << j << "[s] = 0;\n";
+  }
+  o << "  }\n  __syncthreads();\n";
+}
+
+void emit_agg_rows_c(const Plan& P, std::ostringstream& o, const std::vector<std::string>& val,
+                     const std::vector<std::string>& ok, const std::string& row, const std::string& didx) {
+  // rows whose key and 32-bit accumulator inputs fit 32 bits
+  o << "    qu32 fit = 0;\n"
+    << "#pragma unroll\n    for (int r = 0; r < 4; ++r) {\n      bool f = key[r] == (qi64)(qi32)key[r];\n";
+  for (int j = 0; j < P.naggs; ++j)
+    if (P.aggs[j].pkind != 0 && compact_acc32(P, j))
+      o << "      { const qi64 x = " << val[j] << "; f = f && (!(" << ok[j] << ") || x == (qi64)(qi32)x); }\n";
+  o << "      fit |= (qu32)f << r;\n    }\n"
+    << "    if (act & ~fit) atomicOr(&P.t.ctl[7], 2ull);\n"
+    << "    int slot[4];\n    qu32 h[4];\n    qu32x4 q[4];\n"
+    << "    qu32 h2[4];\n    qu32x4 q2[4];\n"
+    << "#pragma unroll\n    for (int r = 0; r < 4; ++r) {\n"
+    << "      h[r] = (qu32)(((qu64)lds_hash((qu64)key[r]) * NBK) >> 32); h2[r] = h[r] + 1 == NBK ? 0u : h[r] + 1;\n"
+    << "      q[r] = ((const qu32x4*)s_keys)[h[r]]; q2[r] = ((const qu32x4*)s_keys)[h2[r]];\n    }\n"
+    << "#pragma unroll\n    for (int r = 0; r < 4; ++r) {\n"
+    << "      const qu32 kk = (qu32)key[r];\n"
+    << "      const int hs = bucket2_hit(q[r], q2[r], kk, h[r], h2[r]);\n"
+    << "      slot[r] = ((knull >> r) & 1) ? S : ((qi32)kk == EMPTY_KEY32 ? S + 1 : hs);\n"
+    << "    }\n"
+    << "    qu32 miss = 0;\n"
+    << "#pragma unroll\n    for (int r = 0; r < 4; ++r) miss |= (qu32)(slot[r] < 0) << r;\n"
+    << "    miss &= act & fit;\n"
+    << "    if (miss) {\n      for (int r = 0; r < 4; ++r) if ((miss >> r) & 1) slot[r] = lds_probe4(s_keys, NBK, (qi32)key[r], h[r]);\n    }\n"
+    << "    qu32 glob = ~fit;\n"
+    << "#pragma unroll\n    for (int r = 0; r < 4; ++r) glob |= (qu32)(slot[r] < 0) << r;\n"
+    << "    glob &= act;\n    const qu32 loc = act & ~glob;\n"
+    << "    int sl[4];\n"
+    << "#pragma unroll\n    for (int r = 0; r < 4; ++r) sl[r] = ((loc >> r) & 1) ? slot[r] : SINK + lane;\n"
+    << "#pragma unroll\n    for (int r = 0; r < 4; ++r) atomicAdd(&s_cst[sl[r]], 1u);\n";
+  for (int j = 0; j < P.naggs; ++j) {
+    const DAgg& a = P.aggs[j];
+    if (a.pkind == 0) continue;
+    const std::string js = std::to_string(j);
+    const bool a32 = compact_acc32(P, j);
+    o << "#pragma unroll\n    for (int r = 0; r < 4; ++r) {\n"
+      << "      const int s = (" << ok[j] << ") ? sl[r] : SINK + lane;\n"
+      << "      const qi64 x = " << val[j] << ";\n";
+    if (a.track_nn) o << "      atomicAdd(&s_nn" << js << "[s], 1u);\n";
+    switch (a.acc) {
+      case ACC_SUM_I: o << "      atomicAdd((qu64*)&s_acc" << js << "[s], (qu64)x);\n"; break;
+      case ACC_MIN_I: o << "      atomicMin(&s_acc" << js << "[s], " << (a32 ? "(qi32)x" : "x") << ");\n"; break;
+      case ACC_MAX_I: o << "      atomicMax(&s_acc" << js << "[s], " << (a32 ? "(qi32)x" : "x") << ");\n"; break;
+      default: break;
+    }
+    o << "    }\n";
+  }
+  // rows for the global table: no room in LDS, or a value that does not fit the compact slots
+  o << "    if (glob) {\n      for (int r = 0; r < 4; ++r) {\n        if (!((glob >> r) & 1)) continue;\n"
+    << "        const qi64 lr = " << didx << ";\n        qu64 gs;\n"
+    << "        if (!gtable_find(P.t, key[r], (knull >> r) & 1, gs)) {\n"
+    << "          atomicOr((qu32*)&P.defer_out[lr >> 5], 1u << (lr & 31));\n"
+    << "          atomicAdd(&P.t.ctl[1], 1ull);\n          continue;\n        }\n"
+    << "        gadd_cstar(P.t, gs, 1);\n        const qu64 row = (qu64)(" << row << ");\n";
+  for (int j = 0; j < P.naggs; ++j) {
+    const DAgg& a = P.aggs[j];
+    if (a.pkind == 0) continue;
+    o << "        if (" << ok[j] << ") { const RowVal rv = row_partial(" << a.acc << ", " << val[j]
+      << ", row); gcombine(P.t, " << a.acc << ", " << j << ", gs, rv.acc, 1, rv.i0, rv.i1, rv.i2, rv.i3, "
+      << (((P.nn_skip >> j) & 1) ? "false" : "true") << "); }\n";
+  }
+  o << "      }\n    }\n";
+}
+
+void emit_flush_c(const Plan& P, std::ostringstream& o) {
+  o << "  __syncthreads();\n"
+    << "  for (int s = threadIdx.x; s < SS; s += blockDim.x) {\n"
+    << "    const qu32 c = s_cst[s];\n    if (c == 0) continue;\n"
+    << "    const bool knl = s == S;\n    const qi64 key = knl ? 0 : (s == S + 1 ? (qi64)EMPTY_KEY32 : (qi64)s_keys[s]);\n"
+    << "    qu64 gs;\n"
+    << "    const bool ok = gtable_find_wg(P.t, key, knl, gs, &s_newg);\n"
+    << "    qu8* rec = nullptr;\n"
+    << "    if (ok) {\n      gadd_cstar(P.t, gs, c);\n    } else {\n"
+    << "      const qu64 ri = atomicAdd(&P.t.ctl[2], 1ull);\n"
+    << "      if (ri >= P.ovf_cap) { atomicAdd(&P.t.ctl[3], 1ull); continue; }\n"
+    << "      rec = P.ovf + ri * (qu64)P.rec_bytes;\n      write_record_head(rec, key, knl, c);\n    }\n";
+  int off = 24;
+  for (int j = 0; j < P.naggs; ++j) {
+    const DAgg& a = P.aggs[j];
+    const std::string js = std::to_string(j);
+    o << "    {\n      const qi64 acc = " << (a.acc != ACC_NONE ? "(qi64)s_acc" + js + "[s]" : std::string("0")) << ";\n"
+      << "      const qu64 nn = " << (a.track_nn ? "s_nn" + js + "[s]" : std::string("c")) << ";\n";
+    const bool skip_nn = (P.nn_skip >> j) & 1;
+    if (a.fn != QE_AGG_COUNT_STAR && !(a.acc == ACC_NONE && skip_nn))
+      o << "      if (ok) gcombine(P.t, " << a.acc << ", " << j << ", gs, acc, nn, ~0ull, ~0ull, ~0ull, ~0ull, "
+        << (skip_nn ? "false" : "true") << ");\n";
+    o << "      if (!ok) { qu64* f = (qu64*)(rec + " << off << "); f[0] = (qu64)acc; f[1] = nn; }\n    }\n";
+    off += agg_rec_bytes(a.acc);
+  }
+  o << "  }\n";
+}
+
+}  // namespace
+
 // Aggregate input expressions of the plan, per row r of a step.
 bool agg_inputs(const Plan& P, std::vector<Expr>* ex) {
   ex->assign(P.naggs, Expr{"0", "1u", false});
@@ -454,9 +581,37 @@ static void emit_fit_check(const PartLayout& L, const std::string& w, std::ostri
 // fill goes to P.part_chunk[1 + c] (bucket 0), as the chunked scatter leaves it. Records are stored
 // chunk-columnar (word q of a chunk's records together; gen_pagg_source `soa`): a step's spilling
 // lanes then write whole 512-byte runs per word instead of 8 bytes every 24.
+bool compact_acc32(const Plan& P, int j) {
+  const DAgg& a = P.aggs[j];
+  if (a.acc != ACC_MIN_I && a.acc != ACC_MAX_I) return false;
+  if (a.ntok != 1 || a.tok[0].op != T_COL) return false;
+  const int k = P.cols[a.tok[0].arg].kind;
+  return k == K_I64 || k == K_I32 || k == K_U8 || k == K_BOOL;
+}
+
+bool compact_ok(const Plan& P) {
+  if (P.key_f64 || P.key_mode == 0) return false;
+  for (int j = 0; j < P.naggs; ++j) {
+    const int acc = P.aggs[j].acc;
+    if (acc != ACC_NONE && acc != ACC_SUM_I && acc != ACC_MIN_I && acc != ACC_MAX_I) return false;
+  }
+  return true;
+}
+
+size_t compact_slot_bytes(const Plan& P) {
+  size_t b = 8;  // key, COUNT(*)
+  for (int j = 0; j < P.naggs; ++j) {
+    if (P.aggs[j].acc != ACC_NONE) b += compact_acc32(P, j) ? 4 : 8;
+    if (P.aggs[j].track_nn) b += 4;
+  }
+  return b;
+}
+
 bool gen_fused_source(const Plan& P, int log2, std::string* src, size_t* lds_bytes, bool spill) {
   if (log2 < 4 || log2 > 16 || P.ncols < 1 || P.ncols > QE_MAX_COLS) return false;
   if (spill && P.mp_n < 2) return false;
+  const bool compact = P.lds_compact > 0;
+  if (compact && (spill || !compact_ok(P))) return false;
   std::vector<Expr> ex;
   if (!agg_inputs(P, &ex)) return false;
   std::vector<std::string> val(P.naggs), ok(P.naggs);
@@ -472,7 +627,8 @@ bool gen_fused_source(const Plan& P, int log2, std::string* src, size_t* lds_byt
   if (spill)
     o << "  __shared__ qi64 s_spc[16];\n  __shared__ qu32 s_spf[16];\n  qu32 nfit = 0;\n"
       << "  if (threadIdx.x < 16) { s_spc[threadIdx.x] = -1; s_spf[threadIdx.x] = 0; }\n";
-  emit_lds_table(P, o, log2, lds_bytes);
+  if (compact) emit_lds_table_c(P, o, lds_bytes);
+  else emit_lds_table(P, o, log2, lds_bytes);
   o << "  const int lane = threadIdx.x & 63;\n"
     << "  const qi64 wave = (blockIdx.x * (qi64)blockDim.x + threadIdx.x) >> 6;\n"
     << "  const qi64 stride = (((qi64)gridDim.x * blockDim.x) >> 6) * 256;\n";
@@ -552,13 +708,17 @@ bool gen_fused_source(const Plan& P, int log2, std::string* src, size_t* lds_byt
       << "                                              : (qu32)__umul64hi(fmix64((qu64)key[r]), (qu64)P.mp_n) != (qu32)P.mp_pass))\n"
       << "        act &= ~(1u << r);\n"
       << "    if (act == 0) continue;\n";
-  emit_agg_rows(P, o, val, ok, "P.row_base + r0 + 128 * (r >> 1) + (r & 1)", "r0 + 128 * (r >> 1) + (r & 1)");
+  if (compact)
+    emit_agg_rows_c(P, o, val, ok, "P.row_base + r0 + 128 * (r >> 1) + (r & 1)", "r0 + 128 * (r >> 1) + (r & 1)");
+  else
+    emit_agg_rows(P, o, val, ok, "P.row_base + r0 + 128 * (r >> 1) + (r & 1)", "r0 + 128 * (r >> 1) + (r & 1)");
   o << (pf ? "    } while (0);\n  }\n  }\n" : "  }\n");
   if (spill)  // each wave's open chunk: its fill (a wave's LDS writes are seen by its own later reads)
     o << "  if ((threadIdx.x & 63) == 0 && s_spc[threadIdx.x >> 6] >= 0)\n"
       << "    P.part_chunk[1 + s_spc[threadIdx.x >> 6]] = (qi64)s_spf[threadIdx.x >> 6];\n"
       << "  if (nfit) atomicOr(&P.t.ctl[7], 1ull);\n";
-  emit_flush(P, o);
+  if (compact) emit_flush_c(P, o);
+  else emit_flush(P, o);
   o << "  __syncthreads();\n  if (threadIdx.x == 0 && s_newg) atomicAdd(&P.t.ctl[0], (qu64)s_newg);\n}\n";
   *src = std::string(kDevHeader) + o.str();
   return true;
@@ -802,13 +962,17 @@ bool part_static() {
   return v;
 }
 
+// (QE_PSCATTER_FAST=1, off by default: 1B rows, same box, 64K / 1M groups 6.41 / 9.00 ms against
+// 5.93 / 8.90 for the per-lane chunk write-out)
 static bool pscatter_fast_env() {
   static const bool v = [] {
     const char* e = getenv("QE_PSCATTER_FAST");
-    return !(e && e[0] == '0');
+    return e && e[0] == '1';
   }();
   return v;
 }
+
+bool part_blk64(const Plan& P, const PartLayout& L);
 
 bool gen_pscatter_staged_source(const Plan& P, int log2p, std::string* src, bool chunked, bool soa) {
   if (soa && !chunked) return false;
@@ -819,11 +983,12 @@ bool gen_pscatter_staged_source(const Plan& P, int log2p, std::string* src, bool
   if (soa && L.narrow) return false;
   const int W = L.words, G = W % 2 ? 1 : 2;
   const char* chunk = L.narrow ? (G == 2 ? "qu64" : "qu32") : (G == 2 ? "qi64x2" : "qi64");
-  // fast form (chunked 32-bit records, QE_PSCATTER_FAST default 1): each row writes its record
+  // fast form (chunked 32-bit records, QE_PSCATTER_FAST=1, opt-in): each row writes its record
   // words to LDS right away (word-major, double-buffered by tile, slot wave*256 + 64r + lane) and
   // after the scan only its 2-byte index to the sorted position; the write-out then moves whole
   // records (W dwords per lane). The records' registers are dead before the first barrier.
   const bool fast = chunked && !soa && L.narrow && pscatter_fast_env();
+  const bool blk = fast && part_blk64(P, L);
   std::ostringstream o;
   o << "\nusing namespace qe;\n"
     << "extern \"C\" __global__ void __launch_bounds__(" << pscatter_block_for(log2p) << ") qe_pscatter(const Plan P) {\n"
@@ -1031,8 +1196,10 @@ bool gen_pscatter_staged_source(const Plan& P, int log2p, std::string* src, bool
       o << "    for (qu32 j = threadIdx.x; j < tot; j += blockDim.x) {\n"
         << "      const qu32 b = s_bkt[j], src = s_perm[j];\n"
         << "      const qu64 dst = (j < s_lim[b] ? s_dst[b] : s_dst2[b]) + j;\n"
-        << "      qu32* d = (qu32*)(P.part_rec + dst * " << L.bytes() << "ull);\n"
-        << "#pragma unroll\n      for (int q = 0; q < W; ++q) d[q] = s_w[sb][q][src];\n"
+        << (blk ? "      qu32* d = (qu32*)P.part_rec + (dst >> 6) * " + std::to_string(64 * W) + "ull + (dst & 63);  // (blocks of 64, part_blk64)\n"
+                  "#pragma unroll\n      for (int q = 0; q < W; ++q) d[64 * q] = s_w[sb][q][src];\n"
+                : "      qu32* d = (qu32*)(P.part_rec + dst * " + std::to_string(L.bytes()) + "ull);\n"
+                  "#pragma unroll\n      for (int q = 0; q < W; ++q) d[q] = s_w[sb][q][src];\n")
         << "    }\n";
     else if (soa)
       // word-major: consecutive threads write consecutive records' word q (one run per word)
@@ -1075,7 +1242,8 @@ bool gen_pscatter_staged_source(const Plan& P, int log2p, std::string* src, bool
 //     32-bit word (a value word, or a bare column), so those atomics move half the bytes;
 //   * the per-row LDS updates are branch-free: a row that is inactive, goes to the global table or
 //     has a null input adds into a sink slot (index SS, never flushed) instead of running under a
-//     per-row, per-aggregate exec-mask branch (the SALU half of the general pass's instructions).
+//     per-row, per-aggregate exec-mask branch (the SALU half of the general pass's instructions);
+//     one sink slot per lane (SS + lane), so inactive lanes never pile onto one LDS address.
 constexpr int PAGG_CHCAP = 2048;  // chunk-list entries a fast aggregation slice stages in LDS
 // record buffers of the fast aggregation pass in rotation (QE_PAGG_FAST_DEPTH, 2 or 4)
 static int pagg_fast_depth() {
@@ -1094,8 +1262,36 @@ static bool pagg_fast_env() {
   return v;
 }
 
-static bool gen_pagg_fast_source(const Plan& P, const PartLayout& L, int log2, std::string* src, size_t* lds_bytes) {
+// Plans the fast aggregation pass takes: 32-bit integral records, integer accumulators.
+static bool pagg_fast_ok(const Plan& P, const PartLayout& L) {
   if (!L.narrow || L.row_word >= 0 || P.key_f64) return false;
+  for (int j = 0; j < P.naggs; ++j) {
+    const int acc = P.aggs[j].acc;
+    if (acc != ACC_NONE && acc != ACC_SUM_I && acc != ACC_MIN_I && acc != ACC_MAX_I) return false;
+  }
+  std::vector<Expr> ex;
+  return !L.colmode || agg_inputs(P, &ex);
+}
+
+// Chunked 32-bit records in blocks of 64 (word q of the block's 64 records contiguous: record slot
+// p's word q at dword (p / 64) * 64W + 64q + p % 64), written by the fast staged scatter and read
+// by the fast aggregation pass: a load instruction there takes 4 x 256 contiguous bytes (16 lanes
+// x 4 records of one word per block) instead of 16 bytes every 48 (record-major). Measured on the
+// records' walk alone (QE_PAGG_EXP 1 vs 4, 1B rows, 64K groups): 1.70 vs 1.26 ms.
+// (QE_PART_BLK64=1; off: the scatter's write-out then stores each record's words 256 B apart and
+// took 8.5 instead of 6.5 ms at 64K groups, more than the reads gain)
+bool part_blk64(const Plan& P, const PartLayout& L) {
+  static const bool on = [] {
+    const char* e = getenv("QE_PART_BLK64");
+    return e && e[0] == '1';
+  }();
+  return on && pscatter_fast_env() && pagg_fast_env() && pagg_fast_ok(P, L);
+}
+
+static bool gen_pagg_fast_source(const Plan& P, const PartLayout& L, int log2, int64_t bucket_groups, std::string* src,
+                                 size_t* lds_bytes) {
+  if (!pagg_fast_ok(P, L)) return false;
+  const bool blk = part_blk64(P, L);
   const int W = L.words;
   std::vector<std::string> val(P.naggs), ok(P.naggs);
   std::vector<bool> acc32(P.naggs, false);
@@ -1116,12 +1312,40 @@ static bool gen_pagg_fast_source(const Plan& P, const PartLayout& L, int log2, s
     const bool bare = L.colmode ? (a.ntok == 1 && a.tok[0].op == T_COL) : L.val_word[j] >= 0;
     acc32[j] = (a.acc == ACC_MIN_I || a.acc == ACC_MAX_I) && bare;
   }
-  const int S = 1 << log2, SS = S + 2;
-  // QE_PAGG_EXP=1: timing experiment, no LDS work (never for results)
+  // QE_PAGG_EXP: timing experiments (never for results): 1 no LDS work, 2 the same reading each
+  // slice's chunks as one contiguous range, 3 no flush, 4 as 1 with each
+  // load instruction reading one contiguous KiB
   static const int exp = [] {
     const char* e = getenv("QE_PAGG_EXP");
     return e && *e ? atoi(e) : 0;
   }();
+  // Table size: as many 4-slot buckets as the LDS holds beside the chunk list (and the per-wave
+  // regrouping area, when that is used), not the power of two of the general pass's 36-byte slots:
+  // with C4's 24-byte slots ~6K slots instead of 4096, so the half-full tables of 128+ buckets
+  // run about a third full. Regrouped loads (QE_PAGG_TRANSPOSE, 48 KiB for C4) only while the
+  // table they leave is at most a quarter full: at 1B rows and 262K / 1M groups (2048 groups per
+  // bucket) a half-full 4096-slot table spent 5.5 / 6.4 ms in the aggregation pass (general pass:
+  // 4.1 / 4.8), the keys displaced past the two-bucket window taking the serial probe loop.
+  static const bool tr_env = [] {
+    const char* e = getenv("QE_PAGG_TRANSPOSE");
+    return !(e && e[0] == '0');
+  }();
+  size_t bps = 8;  // key + COUNT(*)
+  for (int j = 0; j < P.naggs; ++j) {
+    if (P.aggs[j].acc != ACC_NONE) bps += acc32[j] ? 4 : 8;
+    if (P.aggs[j].track_nn) bps += 4;
+  }
+  constexpr size_t kBudget = 160 * 1024 - 256;  // (s_fail, s_newg, alignment)
+  const size_t tr_bytes = (size_t)(pagg_block() / 64) * W * 1024;
+  auto slots_for = [&](size_t fixed) -> int {
+    const int64_t s = fixed < kBudget ? ((int64_t)((kBudget - fixed) / bps) - 66) & ~(int64_t)63 : 0;
+    return (int)std::min<int64_t>(s, 1 << 14);
+  };
+  const int s_tr = slots_for((size_t)1024 * 8 + tr_bytes), s_plain = slots_for((size_t)PAGG_CHCAP * 8);
+  const bool tr = !blk && tr_env && exp == 0 && s_tr >= 256 && (bucket_groups <= 0 || 4 * bucket_groups <= s_tr);
+  const int S = tr ? s_tr : s_plain, SS = S + 2;
+  if (S < 256) return false;
+  (void)log2;
   std::ostringstream o;
   o << "\nusing namespace qe;\n"
     << "extern \"C\" __global__ void __launch_bounds__(" << pagg_block() << ") qe_pagg(const Plan P) {\n"
@@ -1133,25 +1357,32 @@ static bool gen_pagg_fast_source(const Plan& P, const PartLayout& L, int log2, s
     << "  if (hi <= 0) return;\n"
     << "  if (P.t.ctl[7]) return;  // a value did not fit the 32-bit records: the update reruns wide\n"
     << "  __shared__ int s_fail;\n  __shared__ qu32 s_newg;\n  if (threadIdx.x == 0) { s_fail = 0; s_newg = 0; }\n"
-    << "  constexpr int LOG2 = " << log2 << ", S = " << S << ", SS = " << SS << ", SINK = SS;\n"
-    << "  __shared__ qi32 s_keys[SS + 1];\n  __shared__ qu32 s_cst[SS + 1];\n";
-  size_t lds = (size_t)(SS + 1) * 8;
+    << "  constexpr int S = " << S << ", SS = " << SS << ", SINK = SS;\n"
+    << "  constexpr qu32 NBK = S / 4;\n"
+    << "  __shared__ __attribute__((aligned(16))) qi32 s_keys[SS + 64];\n  __shared__ qu32 s_cst[SS + 64];\n";
+  size_t lds = (size_t)(SS + 64) * 8;
   for (int j = 0; j < P.naggs; ++j) {
     const DAgg& a = P.aggs[j];
     if (a.acc != ACC_NONE) {
-      o << "  __shared__ " << (acc32[j] ? "qi32" : "qi64") << " s_acc" << j << "[SS + 1];\n";
-      lds += (size_t)(SS + 1) * (acc32[j] ? 4 : 8);
+      o << "  __shared__ " << (acc32[j] ? "qi32" : "qi64") << " s_acc" << j << "[SS + 64];\n";
+      lds += (size_t)(SS + 64) * (acc32[j] ? 4 : 8);
     }
     if (a.track_nn) {
-      o << "  __shared__ qu32 s_nn" << j << "[SS + 1];\n";
-      lds += (size_t)(SS + 1) * 4;
+      o << "  __shared__ qu32 s_nn" << j << "[SS + 64];\n";
+      lds += (size_t)(SS + 64) * 4;
     }
   }
+  // record-major records loaded as contiguous KiB per load instruction and regrouped per lane
+  // through a per-wave LDS staging area (W KiB per wave; `tr` above): each lane then holds 4
+  // consecutive records as before. Measured on the walk alone (QE_PAGG_EXP 1 vs 4, 1B rows, 64K
+  // groups): 1.70 vs 1.26 ms. (QE_PAGG_TRANSPOSE=0: direct 48-byte lane loads)
+  const int chcap = 1024;
+  if (tr) lds += tr_bytes;
   *lds_bytes = lds;
   auto init32 = [](int acc) {
     return acc == ACC_MIN_I ? std::string("0x7FFFFFFF") : acc == ACC_MAX_I ? std::string("(qi32)0x80000000u") : "0";
   };
-  o << "  for (int s = threadIdx.x; s < SS + 1; s += blockDim.x) {\n    s_keys[s] = EMPTY_KEY32;\n    s_cst[s] = 0;\n";
+  o << "  for (int s = threadIdx.x; s < SS + 64; s += blockDim.x) {\n    s_keys[s] = EMPTY_KEY32;\n    s_cst[s] = 0;\n";
   for (int j = 0; j < P.naggs; ++j) {
     const DAgg& a = P.aggs[j];
     if (a.acc != ACC_NONE) o << "    s_acc" << j << "[s] = " << (acc32[j] ? init32(a.acc) : acc_init(a.acc)) << ";\n";
@@ -1161,12 +1392,14 @@ static bool gen_pagg_fast_source(const Plan& P, const PartLayout& L, int log2, s
   // lookups are then LDS reads, off the in-order vector-memory counter the record loads wait on
   // (a global lookup under a branch made the compiler wait for every outstanding load there)
   o << "  }\n"
-    << "  constexpr int CHCAP = " << PAGG_CHCAP << ";\n  __shared__ qu64 s_ch[CHCAP];\n"
+    << "  constexpr int CHCAP = " << (tr ? chcap : PAGG_CHCAP) << ";\n  __shared__ qu64 s_ch[CHCAP];\n"
+    << (tr ? "  __shared__ qu32x4 s_tr[" + std::to_string(pagg_block() / 64) + "][" + std::to_string(64 * W) + "];\n" : std::string())
     << "  const qi64 nch = hi / PART_CH;\n"
     << "  const int lane = threadIdx.x & 63;\n"
+    << "  const int ro = " << (blk ? "64 * (lane >> 4) + 4 * (lane & 15)" : "4 * lane") << ";  // the lane's first record of a step\n"
     << "  const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), nwv = blockDim.x >> 6;\n"
     ;
-  lds += (size_t)PAGG_CHCAP * 8;
+  lds += (size_t)(tr ? chcap : PAGG_CHCAP) * 8;
   // D rotating record buffers: step t consumes buffer t % D in place and reloads it with step t + D,
   // so each step's loads have the next D - 1 steps' work to land (one buffer copied forward made
   // the loop's back edge wait for the loads it had just issued)
@@ -1185,13 +1418,31 @@ static bool gen_pagg_fast_source(const Plan& P, const PartLayout& L, int log2, s
     o << "    {\n      const qi64 nb = " << nb << ";\n      const bool in = nb < rhi;\n"
       << "      const qu64 m = s_ch[in ? (int)(nb >> 11) : 0];\n"
       << "      const qi32 ko = (qi32)(nb & (PART_CH - 1));\n"
-      << "      const qi64 npb = (qi64)(qi32)(qu32)m * PART_CH + ko;\n      const qi32 cfill = in ? (qi32)(m >> 32) - ko : 0;\n"
-      << "      const qu32x4* p = (const qu32x4*)(P.part_rec + (qu64)(npb + 4 * lane) * " << L.bytes() << "ull);\n";
+      << (exp == 2 ? "      const qi64 npb = ((qi64)blockIdx.x * nch + c0 + (nb >> 11)) % (P.n / PART_CH) * PART_CH + ko;  // (experiment: slices contiguous)\n"
+                   : "      const qi64 npb = (qi64)(qi32)(qu32)m * PART_CH + ko;\n")
+      << "      const qi32 cfill = in ? (qi32)(m >> 32) - ko : 0;\n"
+      // (lanes whose records lie past the chunk's fill read the step's first block instead: the
+      // unfilled tail of a chunk is never fetched)
+      << (blk ? "      const qu32x4* p = (const qu32x4*)((const qu32*)P.part_rec + ((npb >> 6) + (ro < cfill ? (lane >> 4) : 0)) * " +
+                    std::to_string(64 * W) + "ull + 4 * (lane & 15));\n"
+              : "      const qu32x4* p = (const qu32x4*)(P.part_rec + (qu64)(npb + 4 * lane) * " + std::to_string(L.bytes()) + "ull);\n");
+    if (blk && exp != 4) {
+      for (int v = 0; v < W; ++v) o << "      " << B << "v" << v << " = " << ld("qu32x4", "p + 16 * " + std::to_string(v)) << ";\n";
+    } else if (exp == 4) {  // (experiment: each load instruction one contiguous KiB of the step's records)
+      o << "      const qu32x4* pc = (const qu32x4*)(P.part_rec + (qu64)npb * " << L.bytes() << "ull) + lane;\n";
+      for (int v = 0; v < W; ++v) o << "      " << B << "v" << v << " = " << ld("qu32x4", "pc + 64 * " + std::to_string(v)) << ";\n";
+    } else if (tr) {  // contiguous KiB per load; a piece past the chunk's fill re-reads the step's first
+      o << "      const qu32x4* pc = (const qu32x4*)(P.part_rec + (qu64)npb * " << L.bytes() << "ull);\n";
+      for (int v = 0; v < W; ++v)
+        o << "      " << B << "v" << v << " = " << ld("qu32x4", "pc + ((" + std::to_string(64 * v) + " + lane) * 16 < cfill * " +
+                                                        std::to_string(L.bytes()) + " ? " + std::to_string(64 * v) + " + lane : lane)")
+          << ";\n";
+    } else
     for (int v = 0; v < W; ++v) o << "      " << B << "v" << v << " = " << ld("qu32x4", "p + " + std::to_string(v)) << ";\n";
     o << "      " << B << "pb = npb;\n      qu32 nact = 0;\n"
-      << "#pragma unroll\n      for (int r = 0; r < 4; ++r) nact |= (qu32)(4 * lane + r < cfill) << r;\n"
+      << "#pragma unroll\n      for (int r = 0; r < 4; ++r) nact |= (qu32)(ro + r < cfill) << r;\n"
       << "      if (P.defer_in) {  // (uniform: retry passes only)\n"
-      << "        for (int r = 0; r < 4; ++r) { const qi64 i = npb + 4 * lane + r; if (!((P.defer_in[i >> 5] >> (i & 31)) & 1)) nact &= ~(1u << r); }\n"
+      << "        for (int r = 0; r < 4; ++r) { const qi64 i = npb + ro + r; if (!((P.defer_in[i >> 5] >> (i & 31)) & 1)) nact &= ~(1u << r); }\n"
       << "      }\n      " << B << "act = nact;\n    }\n";
   };
   o << "  for (qi64 c0 = 0; c0 < nch; c0 += CHCAP) {\n"
@@ -1210,10 +1461,29 @@ static bool gen_pagg_fast_source(const Plan& P, const PartLayout& L, int log2, s
   const std::string B = "b" + std::to_string(k) + "_";
   o << "  {\n"
     << "    const qi64 sbase = " << B << "pb;\n    const qu32 act = " << B << "act;\n"
-    << "    const qu32 d[" << 4 * W << "] = {";
-  for (int v = 0; v < W; ++v)
-    o << (v ? ", " : "") << B << "v" << v << ".x, " << B << "v" << v << ".y, " << B << "v" << v << ".z, " << B << "v" << v << ".w";
-  o << "};\n"
+    << "    qu32 d[" << 4 * W << "] = {";
+  if (blk) {  // vector v holds word v of the lane's 4 records: d[r * W + q] = word q of record r
+    const char* el[4] = {".x", ".y", ".z", ".w"};
+    for (int r = 0; r < 4; ++r)
+      for (int q = 0; q < W; ++q) o << (r || q ? ", " : "") << B << "v" << q << el[r];
+  } else if (tr) {  // through the wave's staging area: piece v of lane l in, the lane's own 4 records out
+    // (lanes exchange data through LDS: wave-scope fences keep the compiler from moving a read of
+    // another lane's piece above the write that stores it, or the next step's writes above it)
+    o << "0};\n    {\n      qu32x4* st = s_tr[threadIdx.x >> 6];\n"
+      << "      __builtin_amdgcn_fence(__ATOMIC_RELEASE, \"wavefront\");\n      __builtin_amdgcn_wave_barrier();\n";
+    for (int v = 0; v < W; ++v) o << "      st[" << 64 * v << " + lane] = " << B << "v" << v << ";\n";
+    o << "      __builtin_amdgcn_fence(__ATOMIC_RELEASE, \"wavefront\");\n      __builtin_amdgcn_wave_barrier();\n"
+      << "      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, \"wavefront\");\n";
+    for (int v = 0; v < W; ++v)
+      o << "      { const qu32x4 t = st[lane * " << W << " + " << v << "]; d[" << 4 * v << "] = t.x; d[" << 4 * v + 1
+        << "] = t.y; d[" << 4 * v + 2 << "] = t.z; d[" << 4 * v + 3 << "] = t.w; }\n";
+    o << "    }\n";
+  } else {
+    for (int v = 0; v < W; ++v)
+      o << (v ? ", " : "") << B << "v" << v << ".x, " << B << "v" << v << ".y, " << B << "v" << v << ".z, " << B << "v" << v << ".w";
+  }
+  if (!tr) o << "};\n";
+  o << ""
     << "    qi64 key[4];\n";
   for (int q = 1; q < W; ++q) o << "    qi64 w" << q << "[4];\n";
   o << "#pragma unroll\n    for (int r = 0; r < 4; ++r) {\n      key[r] = (qi64)(qi32)d[r * " << W << "];\n";
@@ -1231,32 +1501,39 @@ static bool gen_pagg_fast_source(const Plan& P, const PartLayout& L, int log2, s
         << (1 + c) << ") & 1u) << r;\n";
   }
   // slots: the first probe of all 4 rows together; collisions (rare) probe on
-  if (exp == 1) {  // timing experiment: the records' walk and loads only (wrong results)
+  if (exp == 1 || exp == 2 || exp == 4) {  // timing experiments: the records' walk and loads only (wrong results)
     o << "#pragma unroll\n    for (int r = 0; r < 4; ++r) xacc ^= (qu64)key[r]";
     for (int q = 1; q < W; ++q) o << " ^ (qu64)w" << q << "[r]";
     o << " ^ act;\n  }\n";
     load_step(k, NB("t + " + std::to_string(k + D)));
     continue;
   }
-  o << "    int slot[4];\n    qu32 h[4];\n    qi32 k0[4];\n"
-    << "#pragma unroll\n    for (int r = 0; r < 4; ++r) { h[r] = lds_hash((qu64)key[r]) >> (32 - LOG2); k0[r] = s_keys[h[r]]; }\n"
-    << "#pragma unroll\n    for (int r = 0; r < 4; ++r) slot[r] = ((knull >> r) & 1) ? S : ((qi32)key[r] == EMPTY_KEY32 ? S + 1 : (k0[r] == (qi32)key[r] ? (int)h[r] : -1));\n"
+  o << "    int slot[4];\n    qu32 h[4];\n    qu32x4 q[4];\n"
+    << "    qu32 h2[4];\n    qu32x4 q2[4];\n"
+    << "#pragma unroll\n    for (int r = 0; r < 4; ++r) {\n"
+    << "      h[r] = (qu32)(((qu64)lds_hash((qu64)key[r]) * NBK) >> 32); h2[r] = h[r] + 1 == NBK ? 0u : h[r] + 1;\n"
+    << "      q[r] = ((const qu32x4*)s_keys)[h[r]]; q2[r] = ((const qu32x4*)s_keys)[h2[r]];\n    }\n"
+    << "#pragma unroll\n    for (int r = 0; r < 4; ++r) {\n"
+    << "      const qu32 kk = (qu32)key[r];\n"
+    << "      const int hs = bucket2_hit(q[r], q2[r], kk, h[r], h2[r]);\n"
+    << "      slot[r] = ((knull >> r) & 1) ? S : ((qi32)kk == EMPTY_KEY32 ? S + 1 : hs);\n"
+    << "    }\n"
     << "    qu32 miss = 0;\n"
     << "#pragma unroll\n    for (int r = 0; r < 4; ++r) miss |= (qu32)(slot[r] < 0) << r;\n"
     << "    miss &= act;\n"
-    << "    if (miss) {\n      for (int r = 0; r < 4; ++r) if ((miss >> r) & 1) slot[r] = lds_probe32(s_keys, LOG2, (qi32)key[r], h[r]);\n    }\n"
+    << "    if (miss) {\n      for (int r = 0; r < 4; ++r) if ((miss >> r) & 1) slot[r] = lds_probe4(s_keys, NBK, (qi32)key[r], h[r]);\n    }\n"
     << "    qu32 glob = 0;\n"
     << "#pragma unroll\n    for (int r = 0; r < 4; ++r) glob |= (qu32)(slot[r] < 0) << r;\n"
     << "    glob &= act;\n    const qu32 loc = act & ~glob;\n"
     << "    int sl[4];\n"
-    << "#pragma unroll\n    for (int r = 0; r < 4; ++r) sl[r] = ((loc >> r) & 1) ? slot[r] : SINK;\n"
+    << "#pragma unroll\n    for (int r = 0; r < 4; ++r) sl[r] = ((loc >> r) & 1) ? slot[r] : SINK + lane;\n"
     << "#pragma unroll\n    for (int r = 0; r < 4; ++r) atomicAdd(&s_cst[sl[r]], 1u);\n";
   for (int j = 0; j < P.naggs; ++j) {
     const DAgg& a = P.aggs[j];
     if (a.pkind == 0) continue;
     const std::string js = std::to_string(j);
     o << "#pragma unroll\n    for (int r = 0; r < 4; ++r) {\n"
-      << "      const int s = (" << ok[j] << ") ? sl[r] : SINK;\n"
+      << "      const int s = (" << ok[j] << ") ? sl[r] : SINK + lane;\n"
       << "      const qi64 x = " << val[j] << ";\n";
     if (a.track_nn) o << "      atomicAdd(&s_nn" << js << "[s], 1u);\n";
     switch (a.acc) {
@@ -1273,7 +1550,7 @@ static bool gen_pagg_fast_source(const Plan& P, const PartLayout& L, int log2, s
   }
   // rows whose group only fits the global table (rare)
   o << "    if (glob) {\n      for (int r = 0; r < 4; ++r) {\n        if (!((glob >> r) & 1)) continue;\n"
-    << "        const qi64 lr = sbase + 4 * lane + r;\n        qu64 gs;\n"
+    << "        const qi64 lr = sbase + ro + r;\n        qu64 gs;\n"
     << "        if (!gtable_find(P.t, key[r], (knull >> r) & 1, gs)) {\n"
     << "          atomicOr((qu32*)&P.defer_out[lr >> 5], 1u << (lr & 31));\n"
     << "          atomicAdd(&P.t.ctl[1], 1ull);\n          continue;\n        }\n"
@@ -1292,6 +1569,7 @@ static bool gen_pagg_fast_source(const Plan& P, const PartLayout& L, int log2, s
   // flush (exclusive slices: plain read-modify-writes), as emit_flush with 32-bit keys / accumulators
   o << "  if (xacc == 0x9E3779B97F4A7C15ull) s_fail = 3;  // (keeps the experiment's loads live)\n"
     << "  __syncthreads();\n"
+    << (exp == 3 ? "  if (s_cst[0] != 0x7FFFFFFFu) return;  // (experiment: no flush)\n" : "")
     << "  for (int s = threadIdx.x; s < SS; s += blockDim.x) {\n"
     << "    const qu32 c = s_cst[s];\n    if (c == 0) continue;\n"
     << "    const bool knl = s == S;\n    const qi64 key = knl ? 0 : (s == S + 1 ? (qi64)EMPTY_KEY32 : (qi64)s_keys[s]);\n"
@@ -1325,11 +1603,12 @@ static bool gen_pagg_fast_source(const Plan& P, const PartLayout& L, int log2, s
     << "      if (ko >= (P.part_chunk[1 + id] & 0xFFFFFFFFll)) continue;\n"
     << "      const qi64 i = id * PART_CH + ko;\n"
     << "      if (P.defer_in && !((P.defer_in[i >> 5] >> (i & 31)) & 1)) continue;\n"
-    << "      const qi32* rp = (const qi32*)(P.part_rec + i * " << L.bytes() << "ull);\n"
+    << (blk ? "      const qi32* rp = (const qi32*)P.part_rec + (i >> 6) * " + std::to_string(64 * W) + "ll + (i & 63);\n"
+            : "      const qi32* rp = (const qi32*)(P.part_rec + i * " + std::to_string(L.bytes()) + "ull);\n")
     << "      const qi32 k = rp[0];\n"
-    << "      const bool kn = " << (L.flags_word >= 0 ? "rp[" + std::to_string(L.flags_word) + "] & 1" : std::string("false")) << ";\n"
+    << "      const bool kn = " << (L.flags_word >= 0 ? "rp[" + std::to_string(L.flags_word * (blk ? 64 : 1)) + "] & 1" : std::string("false")) << ";\n"
     << "      int s = kn ? S : (k == EMPTY_KEY32 ? S + 1 : -1);\n"
-    << "      if (s < 0) { const qu32 hh = lds_hash((qu64)(qi64)k) >> (32 - LOG2); s = s_keys[hh] == k ? (int)hh : lds_probe32(s_keys, LOG2, k, hh); }\n"
+    << "      if (s < 0) s = lds_probe4(s_keys, NBK, k, (qu32)(((qu64)lds_hash((qu64)(qi64)k) * NBK) >> 32));\n"
     << "      if (s >= 0 && (s_cst[s] & 0x80000000u)) {\n"
     << "        atomicOr((qu32*)&P.defer_out[i >> 5], 1u << (i & 31));\n"
     << "        atomicAdd(&P.t.ctl[1], 1ull);\n      }\n    }\n  }\n"
@@ -1340,10 +1619,11 @@ static bool gen_pagg_fast_source(const Plan& P, const PartLayout& L, int log2, s
 
 // `soa` (chunked only): records stored chunk-columnar, word q of slot i at
 // ((i / PART_CH) * W + q) * PART_CH + i % PART_CH (the spilling fused pass writes them so).
-bool gen_pagg_source(const Plan& P, int log2, std::string* src, size_t* lds_bytes, bool chunked, bool soa) {
+bool gen_pagg_source(const Plan& P, int log2, std::string* src, size_t* lds_bytes, bool chunked, bool soa,
+                     int64_t bucket_groups) {
   if (log2 < 4 || log2 > 16 || (soa && !chunked)) return false;
   const PartLayout L = part_layout(P);
-  if (chunked && !soa && pagg_fast_env() && gen_pagg_fast_source(P, L, log2, src, lds_bytes)) return true;
+  if (chunked && !soa && pagg_fast_env() && gen_pagg_fast_source(P, L, log2, bucket_groups, src, lds_bytes)) return true;
   std::vector<std::string> val(P.naggs), ok(P.naggs);
   if (L.colmode) {
     // the programs run here, over column values read back from the record (c<slot>[r], v<slot>)
@@ -1858,7 +2138,9 @@ bool emit_selproj_write(const Plan& P, const int32_t* out_kind, int nout, int mo
   const std::string lookback = mode == SP_WRITE || mode == SP_WRITE_SCAN ?
       "    const qu64 total = s_total;\n"
       "    if (lane == 0) {\n      qu64 excl = 0;\n      for (int q = 0; q < W; ++q) excl += s_pre[q];\n      s_base = excl;\n"
-      "      if ((qu64)tile == P.t.cap - 1) { P.t.ctl[1] = excl + total; if (P.host_ctl) __hip_atomic_store(&P.host_ctl[0], excl + total, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM); }\n    }\n" :
+      // (host_ctl[2]: the count has landed — the host polls it instead of waiting for the
+      // kernel's completion signal, ~6 us sooner)
+      "      if ((qu64)tile == P.t.cap - 1) { P.t.ctl[1] = excl + total; if (P.host_ctl) { __hip_atomic_store(&P.host_ctl[0], excl + total, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM); __hip_atomic_store(&P.host_ctl[2], 1ull, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM); } }\n    }\n" :
       "    const qu64 total = s_total;\n"
       "    qu64 excl = 0;\n"
       "    if (tile > 0) {\n"

@@ -10,6 +10,8 @@
 #include <stdio.h>
 #include <string.h>
 
+#include <atomic>
+#include <chrono>
 #include <map>
 #include <memory>
 #include <mutex>
@@ -80,6 +82,7 @@ struct qe_select_pending {
   uint64_t* pin = nullptr;  // [0] count, [1] stall flag (persistent look-back)
   hipEvent_t ev = nullptr;
   bool persist = false;     // the launch was the persistent look-back grid (a stall reruns it)
+  bool poll = false;        // two passes: the write pass sets pin[2] once the count is in pin[0]
   int32_t col_width[QE_MAX_COLS] = {};
 };
 
@@ -99,8 +102,9 @@ int init_validity(qe_ctx* ctx, const qe_column* outs, const int32_t* out_kind, i
 // its count into pin[0] (pin[1]: 1 if a persistent look-back tile never saw its predecessor).
 // `persist_ok` = false forces counter-ordered tiles (the rerun after a stall).
 int launch_select(qe_ctx* ctx, Plan& P, const int32_t* col_width, const int32_t* out_kind, int nout, bool persist_ok,
-                  uint64_t* pin, bool* persist_used) {
+                  uint64_t* pin, bool* persist_used, bool* poll) {
   *persist_used = false;
+  *poll = false;
   const int64_t n = P.n;
   if (n == 0) return QE_OK;  // pin[] was zeroed by the caller
   // Tile order: a persistent grid (every workgroup resident, tiles assigned statically) or one
@@ -181,6 +185,7 @@ int launch_select(qe_ctx* ctx, Plan& P, const int32_t* col_width, const int32_t*
       QE_TRY(jit_launch(ctx, fn, (int)tiles, P, BT));
       QE_TRY(launch_check(mode == SP_COUNT ? "qe_selproj (count)" : "qe_selproj (write)"));
     }
+    *poll = true;
     return QE_OK;
   }
   const size_t sbytes = (size_t)(3 + tiles) * 8;  // ctl[3] | per tile a look-back status word
@@ -215,8 +220,11 @@ int launch_select(qe_ctx* ctx, Plan& P, const int32_t* col_width, const int32_t*
 
 // Completion events of select-project calls, reused (hipEventCreate per call cost a few us of
 // host time on every batch). A returned event has been synchronised on, so it is idle.
+// Events of calls that returned on the polled count (their kernels may still be finishing) retire
+// to g_ev_busy and are reused once hipEventQuery reports them complete.
 std::mutex g_ev_mu;
 std::vector<hipEvent_t> g_ev_free;
+std::vector<hipEvent_t> g_ev_busy;
 
 int event_alloc(hipEvent_t* ev) {
   {
@@ -226,25 +234,34 @@ int event_alloc(hipEvent_t* ev) {
       g_ev_free.pop_back();
       return QE_OK;
     }
+    for (size_t i = 0; i < g_ev_busy.size(); ++i) {
+      if (hipEventQuery(g_ev_busy[i]) != hipSuccess) {
+        (void)hipGetLastError();  // hipErrorNotReady must not surface later
+        continue;
+      }
+      *ev = g_ev_busy[i];
+      g_ev_busy[i] = g_ev_busy.back();
+      g_ev_busy.pop_back();
+      return QE_OK;
+    }
   }
   QE_HIP(hipEventCreateWithFlags(ev, hipEventDisableTiming));
   return QE_OK;
 }
 
-void event_release(hipEvent_t ev, bool idle) {
+// idle: waited on (complete). busy: recorded, possibly still pending (polled calls). Neither: a
+// failed launch, whose event the runtime retires.
+void event_release(hipEvent_t ev, bool idle, bool busy = false) {
   if (!ev) return;
-  if (!idle) {  // never waited on (a failed launch): let the runtime retire it
-    (void)hipEventDestroy(ev);
-    return;
-  }
   std::lock_guard<std::mutex> g(g_ev_mu);
-  if (g_ev_free.size() < 64) g_ev_free.push_back(ev);
+  if (idle && g_ev_free.size() < 64) g_ev_free.push_back(ev);
+  else if (busy && g_ev_busy.size() < 64) g_ev_busy.push_back(ev);
   else (void)hipEventDestroy(ev);
 }
 
-void pending_free(qe_select_pending* r, bool waited = false) {
+void pending_free(qe_select_pending* r, bool waited = false, bool polled = false) {
   if (!r) return;
-  event_release(r->ev, waited);
+  event_release(r->ev, waited && !polled, polled);
   if (r->pin) {  // waited: the kernels that write it have completed
     if (waited) pinned_slot_free_idle(r->pin);
     else pinned_slot_free(r->pin, r->ctx->stream);
@@ -290,10 +307,10 @@ int qe_select_project_async(qe_ctx* ctx, const qe_column* cols, int32_t ncols, c
   }
   if (!ctx->jit) return fail(QE_ERR_UNSUPPORTED, "fused select-project needs kernel specialisation (jit is off)");
   QE_TRY(pinned_slot_alloc(&r->pin));
-  r->pin[0] = r->pin[1] = 0;  // the slot's previous user is done with it (pinned_slot_alloc)
+  r->pin[0] = r->pin[1] = r->pin[2] = 0;  // the slot's previous user is done with it (pinned_slot_alloc)
   QE_TRY(event_alloc(&r->ev));
   QE_TRY(init_validity(ctx, outs, r->out_kind, r->nout, n));
-  const int st = launch_select(ctx, P, r->col_width, r->out_kind, r->nout, true, r->pin, &r->persist);
+  const int st = launch_select(ctx, P, r->col_width, r->out_kind, r->nout, true, r->pin, &r->persist, &r->poll);
   if (st != QE_OK) {
     pending_free(r.release());
     return st;
@@ -307,6 +324,36 @@ int qe_select_pending_wait(qe_select_pending* r, int64_t* out_count) {
   QE_CHECK(r && out_count, QE_ERR_INVALID_ARG, "null argument");
   qe_ctx* ctx = r->ctx;
   int st = ctx_enter(ctx);
+  if (st == QE_OK && r->poll) {
+    // Two passes: the write pass's last tile stores the count, then pin[2]. Polling that word
+    // returns ~6 us before the kernel's completion signal would (one launch + event wait: 12.6 us,
+    // + a polled pinned word instead: 6.7 us; tools/exp_sync_latency.hip). The outputs are then
+    // complete in the ctx stream's order (what every later call on the ctx, and a synchronisation
+    // of its stream, sees); the event is checked every ~50 us, so a failed kernel still ends the
+    // wait.
+    volatile uint64_t* pv = r->pin;
+    auto t0 = std::chrono::steady_clock::now();
+    for (uint32_t i = 1; pv[2] == 0; ++i) {
+      if ((i & 1023) != 0) continue;
+      if (std::chrono::steady_clock::now() - t0 < std::chrono::microseconds(50)) continue;
+      t0 = std::chrono::steady_clock::now();
+      const hipError_t e = hipEventQuery(r->ev);
+      if (e == hipSuccess) {
+        if (pv[2] == 0) st = fail(QE_ERR_DEVICE, "select-project finished without publishing its row count");
+        break;
+      }
+      if (e != hipErrorNotReady) {
+        st = fail(QE_ERR_DEVICE, "select-project kernel failed: %s", hipGetErrorString(e));
+        break;
+      }
+      (void)hipGetLastError();
+    }
+    std::atomic_thread_fence(std::memory_order_acquire);
+    if (st == QE_OK) *out_count = (int64_t)pv[0];
+    // the slot's last device write (pin[2]) has landed: reusable at once; the event may be pending
+    pending_free(r, st == QE_OK, true);
+    return st;
+  }
   if (st == QE_OK && hipEventSynchronize(r->ev) != hipSuccess) st = fail(QE_ERR_DEVICE, "select-project event wait failed");
   if (st == QE_OK && r->pin[1] != 0) {
     // a persistent workgroup was not resident: every wave drained; rerun with counter-ordered tiles
@@ -317,7 +364,8 @@ int qe_select_pending_wait(qe_select_pending* r, int64_t* out_count) {
       bool used = false;
       r->pin[0] = r->pin[1] = 0;  // (the aborted launch has drained: the event completed)
       st = init_validity(ctx, r->outs, r->out_kind, r->nout, r->P.n);  // the aborted launch may have set bits anywhere
-      if (st == QE_OK) st = launch_select(ctx, r->P, r->col_width, r->out_kind, r->nout, false, r->pin, &used);
+      bool poll = false;
+      if (st == QE_OK) st = launch_select(ctx, r->P, r->col_width, r->out_kind, r->nout, false, r->pin, &used, &poll);
       if (st == QE_OK) st = ctx_sync(ctx);
       if (st == QE_OK && r->pin[1] != 0) st = fail(QE_ERR_DEVICE, "select-project look-back did not complete");
     }

@@ -119,10 +119,12 @@ static int emit_agg(const char* dir, const char* name, const qe_column* cols, in
   }
   // 32-bit records (Plan.part_narrow; wide again where a word is fp64 or a row index): staged
   // chunked and direct scatters, chunked and unchunked aggregation passes
-  std::string g, h, i, j;
+  std::string g, h, i, j, i2;
   P.part_narrow = 1;
+  // (i2: the fast aggregation pass with 2048 groups per bucket: its largest table, no regrouping)
   if (!gen_pscatter_staged_source(P, 6, &g, true, false) || !gen_part_source(P, 10, true, &h) ||
-      !gen_pagg_source(P, log2, &i, &lds, true, false) || !gen_pagg_source(P, log2, &j, &lds, false, false)) {
+      !gen_pagg_source(P, log2, &i, &lds, true, false) || !gen_pagg_source(P, log2, &j, &lds, false, false) ||
+      !gen_pagg_source(P, log2, &i2, &lds, true, false, 2048)) {
     fprintf(stderr, "%s: narrow partition sources not generated\n", name);
     return 1;
   }
@@ -133,12 +135,25 @@ static int emit_agg(const char* dir, const char* name, const qe_column* cols, in
     fprintf(stderr, "%s: narrow spill sources not generated\n", name);
     return 1;
   }
+  // compact LDS table (Plan.lds_compact) where the plan shape allows it
+  P.mp_n = 0;
+  P.part_narrow = 0;
+  P.lds_compact = 6080;
+  std::string m;
+  if (compact_ok(P)) {
+    if (!gen_fused_source(P, log2, &m, &lds, false) || write_src(dir, std::string(name) + "_fused_compact", m)) {
+      fprintf(stderr, "%s: compact fused source not generated\n", name);
+      return 1;
+    }
+  }
+  P.lds_compact = 0;
   return write_src(dir, std::string(name) + "_fused", a) | write_src(dir, std::string(name) + "_spill", b) |
          write_src(dir, std::string(name) + "_pagg", c) | write_src(dir, std::string(name) + "_pscatter", d) |
          write_src(dir, std::string(name) + "_pscatter_soa", e) | write_src(dir, std::string(name) + "_pagg_rows", f) |
          write_src(dir, std::string(name) + "_pscatter_n32", g) |
          write_src(dir, std::string(name) + "_pdirect_n32", h) | write_src(dir, std::string(name) + "_pagg_n32", i) |
          write_src(dir, std::string(name) + "_pagg_unchunked_n32", j) |
+         write_src(dir, std::string(name) + "_pagg_big_n32", i2) |
          write_src(dir, std::string(name) + "_spill_n32", k) | write_src(dir, std::string(name) + "_pagg_soa_n32", l);
 }
 

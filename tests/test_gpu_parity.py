@@ -633,6 +633,7 @@ def mp_mode(request, monkeypatch):
     """Both two-bucket updates: one fused pass that spills the second bucket's rows as records for a
     partition-aggregate pass (default), and two fused passes (QE_MP_SPILL=0)."""
     monkeypatch.setenv("QE_MP_SPILL", "1" if request.param == "spill" else "0")
+    monkeypatch.setenv("QE_LDS_COMPACT", "0")  # (the compact one-pass table has tests of its own)
     return request.param
 
 
@@ -685,6 +686,7 @@ def test_multipass_spill_narrow_records(agg_ctx, monkeypatch, case):
     at or above the kept share) are aggregated by one more fused pass over the columns; the state's
     records are 64-bit afterwards. Two batches; results equal the oracle."""
     monkeypatch.setenv("QE_MP_SPILL", "1")
+    monkeypatch.setenv("QE_LDS_COMPACT", "0")
     rng = np.random.default_rng(len(case) + 99)
     n, groups = 600_000, 4000
     k = rng.integers(0, groups, n).astype(np.int64) * 104729 + 11
@@ -728,6 +730,68 @@ def test_fused_c4_one_pass_large_table(agg_ctx):
     ref = S.group_aggregate([k], [None], [S.arith(S.OP_ADD, a, None, b, None)[0], None, a, b], [None] * 4, C4_FNS,
                             a > (1 << 19))
     assert_groups_equal(result_dict(kk, aa), ref, C4_FNS)
+
+
+@pytest.mark.parametrize("groups", [3500, 4096, 5000])
+def test_fused_c4_compact_vs_oracle(agg_ctx, groups):
+    """Groups just past the regular LDS table: ONE fused pass over a compact table (32-bit keys,
+    32-bit MIN / MAX of bare columns, ~6.4K slots in 152 KiB) instead of key-hash passes."""
+    from kquery.datasource import C4_COLUMNS, ColumnSpec, generate_column
+
+    n, row0 = 2_000_003, 5
+    kspec = ColumnSpec("k", N.TYPE_INT64, N.GEN_MOD, groups, 0)
+    cols = [generate_column(kspec, n, row0, 42, agg_ctx)] + [generate_column(s, n, row0, 42, agg_ctx)
+                                                              for s in C4_COLUMNS[1:]]
+    st = HashAggregateState(agg_ctx, [N.TYPE_INT64], C4_AGGS, groups)
+    st.update_fused(cols, _c4_spec())
+    if agg_ctx.kernel_mode == "jit":
+        spec, note = st.last_kernel_kind()
+        assert spec and note.startswith("compact LDS table"), note
+    kk, aa = st.finalize()
+    k, _ = gen.generate(gen.GEN_MOD, groups, 42, 0, row0, n)
+    a, _ = gen.generate(gen.GEN_MOD, 1 << 20, 42, 1, row0, n)
+    b, _ = gen.generate(gen.GEN_MOD, 1 << 20, 42, 2, row0, n)
+    ref = S.group_aggregate([k], [None], [S.arith(S.OP_ADD, a, None, b, None)[0], None, a, b], [None] * 4, C4_FNS,
+                            a > (1 << 19))
+    assert_groups_equal(result_dict(kk, aa), ref, C4_FNS)
+
+
+@pytest.mark.parametrize("case", ["fits", "key_wide", "value_wide", "nullable"])
+def test_compact_table_speculation(agg_ctx, case):
+    """The compact table speculates that keys and MIN / MAX inputs fit 32 bits. A batch where one
+    does not is still exact (those rows go to the global table) and the state's later batches take
+    the bucket passes instead; null keys, INT32_MIN keys and nullable inputs keep their semantics."""
+    rng = np.random.default_rng(len(case) * 7)
+    # (nullable inputs add a non-null count per aggregate to the slot: fewer slots, fewer groups)
+    n, groups = 400_000, 2600 if case == "nullable" else 4200
+    k = (rng.integers(0, groups, n).astype(np.int64) - groups // 2) * 1021
+    k[::997] = -2**31  # the 32-bit table's empty marker is a real key here
+    x = rng.integers(-2**31, 2**31, n).astype(np.int64)
+    kv = xv = None
+    half = n // 2
+    if case == "key_wide":
+        k[:half:5000] = 2**40 + 3
+    elif case == "value_wide":
+        x[:half:3000] = -2**45
+    elif case == "nullable":
+        kv = rng.random(n) > 0.02
+        xv = rng.random(n) > 0.1
+    fns = [N.AGG_SUM, N.AGG_COUNT_STAR, N.AGG_MIN, N.AGG_MAX, N.AGG_COUNT]
+    st = HashAggregateState(agg_ctx, [N.TYPE_INT64], [(f, N.TYPE_INT64) for f in fns], groups)
+    notes = []
+    for s, e in ((0, half), (half, n)):
+        st.update([dcol(agg_ctx, N.TYPE_INT64, k[s:e], None if kv is None else kv[s:e])],
+                  [dcol(agg_ctx, N.TYPE_INT64, x[s:e], None if xv is None else xv[s:e])] * len(fns))
+        notes.append(st.last_kernel_kind()[1])
+    if agg_ctx.kernel_mode == "jit":
+        assert notes[0].startswith("compact LDS table"), notes
+        if case in ("key_wide", "value_wide"):
+            assert not notes[1].startswith("compact LDS table"), notes
+        else:
+            assert notes[1].startswith("compact LDS table"), notes
+    kk, aa = st.finalize()
+    ref = S.group_aggregate([k], [kv], [x] * len(fns), [xv] * len(fns), fns)
+    assert_groups_equal(result_dict(kk, aa), ref, fns)
 
 
 def test_fused_c4_multipass_vs_oracle(agg_ctx, mp_mode):
@@ -883,6 +947,66 @@ def test_partitioned_narrow_off():
     root = pathlib.Path(__file__).resolve().parents[1]
     env = dict(os.environ, QE_PART_NARROW="0")
     r = subprocess.run([sys.executable, "-c", _NARROW_OFF_CHILD, str(root)], cwd=str(root), env=env,
+                       capture_output=True, text=True, timeout=110)
+    assert r.returncode == 0 and "ok" in r.stdout, r.stderr[-3000:]
+
+
+_KNOB_CHILD = """
+import sys
+sys.path[:0] = [sys.argv[1], sys.argv[1] + "/query-engines_amd"]
+import numpy as np
+from kquery import native as N
+from kquery.aggregate import HashAggregateState
+from kquery.columnar import Context, DeviceColumn
+from oracle import semantics as S
+ctx = Context.get(0)
+fns = [N.AGG_SUM, N.AGG_MIN, N.AGG_MAX, N.AGG_COUNT, N.AGG_COUNT_STAR]
+rng = np.random.default_rng(7)
+n = 700_001
+k = rng.integers(0, 90_000, n).astype(np.int64) * 7919 - 3
+kv = rng.random(n) > 0.01
+k[rng.random(n) < 0.001] = -2**31  # the 32-bit EMPTY sentinel as a key
+x = rng.integers(-2**31, 2**31, n).astype(np.int64)
+xv = rng.random(n) > 0.1
+st = HashAggregateState(ctx, [N.TYPE_INT64], [(f, N.TYPE_INT64) for f in fns], 100_000)
+for s, e in ((0, 300_001), (300_001, n)):
+    st.update([DeviceColumn.from_numpy(N.TYPE_INT64, k[s:e], kv[s:e], ctx=ctx)],
+              [DeviceColumn.from_numpy(N.TYPE_INT64, x[s:e], xv[s:e], ctx=ctx)] * len(fns))
+    note = st.last_kernel_kind()[1]
+    assert note.startswith("radix-partitioned") and "32-bit" in note, note
+kk, aa = st.finalize()
+ref = S.group_aggregate([k], [kv], [x] * len(fns), [xv] * len(fns), fns)
+got = {}
+kl, avs = kk[0].to_pylist(), [a.to_pylist() for a in aa]
+for i, key in enumerate(kl):
+    got[(key,)] = tuple(a[i] for a in avs)
+assert len(got) == len(ref), (len(got), len(ref))
+for key, want in ref.items():
+    assert tuple(got[key]) == tuple(want), (key, got[key], want)
+print("ok")
+"""
+
+
+@pytest.mark.parametrize("knobs", [
+    {"QE_PSCATTER_FAST": "1"},
+    {"QE_PSCATTER_FAST": "1", "QE_PART_BLK64": "1"},
+    {"QE_PAGG_TRANSPOSE": "0"},
+    {"QE_PAGG_FAST_DEPTH": "4"},
+    {"QE_PAGG_FAST": "0"},
+], ids=lambda d: ",".join(f"{k}={v}" for k, v in d.items()))
+def test_partitioned_layout_knobs(knobs):
+    """The partitioned path's opt-in and opt-out layouts (knobs read once per process, so each in a
+    child process): the record-regrouping scatter, 64-record blocks, direct lane loads in the fast
+    aggregation pass, its 4-deep buffer rotation, and the general aggregation pass — chunked 32-bit
+    records, nullable keys and inputs, INT32_MIN keys, two batches; bit-exact vs the oracle."""
+    import os
+    import pathlib
+    import subprocess
+    import sys
+
+    root = pathlib.Path(__file__).resolve().parents[1]
+    env = dict(os.environ, QE_PART_CHUNKED="1", **knobs)
+    r = subprocess.run([sys.executable, "-c", _KNOB_CHILD, str(root)], cwd=str(root), env=env,
                        capture_output=True, text=True, timeout=110)
     assert r.returncode == 0 and "ok" in r.stdout, r.stderr[-3000:]
 

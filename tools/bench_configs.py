@@ -12,6 +12,7 @@ HBM bytes / time against the 8 TB/s peak. Writes one JSON object per config to s
 import json
 import pathlib
 import statistics
+import time
 import sys
 
 ROOT = pathlib.Path(__file__).resolve().parents[1]
@@ -95,8 +96,28 @@ def main():
             N.check(N.lib().qe_select_project(ctx.handle, cc, 2, N.C.byref(fused.spec), oc, N.C.byref(cnt)))
 
         ms_k = timed(run_kernel)
+
+        def wall(fn, reps=30, warmup=5, before=None):
+            """Host wall time of a synchronous call (what a caller waits), median; `before` runs
+            untimed ahead of each call, followed by a stream synchronisation."""
+            ts = []
+            for it in range(warmup + reps):
+                if before is not None:
+                    before(it)
+                torch.cuda.synchronize()
+                t0 = time.perf_counter()
+                fn()
+                t1 = time.perf_counter()
+                if it >= warmup:
+                    ts.append((t1 - t0) * 1e3)
+            torch.cuda.synchronize()
+            return statistics.median(ts)
+
+        ms_wall = wall(run_kernel)
         # the same call with the input evicted from the 256 MB MALL first (a 1 GiB write between
-        # calls, outside the timed region): what one 10M batch costs from HBM
+        # calls, outside the timed region): what one 10M batch costs from HBM. The write leaves the
+        # MALL full of dirty lines, so the call's reads also pay their write-back; "clean" evicts
+        # with a 1 GiB READ instead (MALL holding clean lines of another buffer)
         flush = torch.empty(1 << 30, dtype=torch.uint8, device=ctx.torch_device)
         cold = []
         for it in range(13):
@@ -109,10 +130,16 @@ def main():
             if it >= 3:
                 cold.append(s_ev.elapsed_time(e_ev))
         ms_cold = statistics.median(cold)
-        del flush
+        ms_cold_wall = wall(run_kernel, reps=10, warmup=3, before=lambda it: flush.fill_(it & 0xFF))
+        fl64 = flush.view(torch.int64)
+        fl64.fill_(1)
+        ms_clean_wall = wall(run_kernel, reps=10, warmup=3, before=lambda it: fl64.max())
+        del flush, fl64
         report("C2 fused select+project (qe_select_project), 10M int64", n, 16 + 8 * sel_rows / n, ms_f,
                selected=sel_rows, call_ms=ms_k, call_gbs=n * (16 + 8 * sel_rows / n) / (ms_k * 1e-3) / 1e9,
                call_cold_ms=ms_cold, call_cold_gbs=n * (16 + 8 * sel_rows / n) / (ms_cold * 1e-3) / 1e9,
+               call_wall_ms=ms_wall, call_cold_wall_ms=ms_cold_wall, call_cold_clean_wall_ms=ms_clean_wall,
+               call_cold_clean_frac=n * (16 + 8 * sel_rows / n) / (ms_clean_wall * 1e-3) / 8e12,
                path="one hipRTC-specialised kernel: predicate, look-back compaction, projection")
         # stream-ordered calls (qe_select_project_async): call i+1 is queued before call i's count
         # is read back, as the pipelined FusedSelectProjectExec does batch to batch
