@@ -624,6 +624,13 @@ __device__ inline int bucket2_hit(qu32x4 q, qu32x4 q2, qu32 kk, qu32 b, qu32 b2)
   return i < 4 ? (int)(4 * b) + i : (i < 8 ? (int)(4 * b2) + i - 4 : -1);
 }
 
+// bucket2_hit over three consecutive buckets (b, b2, b3): fuller tables (QE_PAGG_WINDOW=3)
+__device__ inline int bucket3_hit(qu32x4 q, qu32x4 q2, qu32x4 q3, qu32 kk, qu32 b, qu32 b2, qu32 b3) {
+  const int i = bucket2_hit(q, q2, kk, b, b2);
+  const qu32 m = (qu32)(q3.x == kk) | ((qu32)(q3.y == kk) << 1) | ((qu32)(q3.z == kk) << 2) | ((qu32)(q3.w == kk) << 3);
+  return i >= 0 ? i : (m ? (int)(4 * b3) + __builtin_ctz(m) : -1);
+}
+
 // lds_probe32 over a table of `nsl` slots (any count: the compact fused table).
 __device__ inline int lds_probe32n(qi32* keys, qu32 nsl, qi32 key, qu32 h) {
 #pragma unroll 1

@@ -1950,6 +1950,21 @@ static int partition_rows(qe_hashagg* h, Plan& P, hipFunction_t* fn, int* grid) 
   };
   int log2p = fill_env ? buckets_log2(fill_env) : buckets_log2(2);
   if (!fill_env && log2p > 6) log2p = buckets_log2(1);
+  // QE_PART_FAST_FILL (percent): buckets for the fast aggregation pass's own (larger) table, each
+  // bucket's expected groups at most that share of its slots (fewer buckets: longer scatter runs)
+  static const int fast_fill = [] {
+    const char* e = getenv("QE_PART_FAST_FILL");
+    const int v = e && *e ? atoi(e) : 0;
+    return v >= 10 && v <= 90 ? v : 0;
+  }();
+  if (!fill_env && fast_fill) {
+    const int64_t fs = (int64_t)pagg_fast_slots(P) * fast_fill / 100;
+    if (fs > 0) {
+      int l = 1;
+      while (l < 13 && fs * ((int64_t)1 << l) < h->expected_groups) ++l;
+      log2p = l;
+    }
+  }
   std::string sc, ss, sa;
   size_t jl = 0;
   const bool staged = part_staged_ok(P, log2p);

@@ -26,6 +26,8 @@ struct qe_ctx {
   size_t scan_tmp_bytes = 0;
   void* ws[8] = {};              // grow-only workspace slots (CSV scan intermediates)
   size_t ws_bytes[8] = {};
+  void* sp_status = nullptr;     // per-workgroup counts of the register-resident select-project
+  uint32_t sp_epoch = 0;         // (epoch-tagged, so no memset per call; qe_selproj.hip)
 };
 
 namespace qe {
@@ -93,6 +95,8 @@ struct PartLayout {
 };
 PartLayout part_layout(const qe::Plan& P);
 bool gen_part_source(const qe::Plan& P, int log2p, bool scatter, std::string* src);
+// fast aggregation pass's largest table in slots (0: the plan does not take that pass)
+int pagg_fast_slots(const qe::Plan& P);
 // bucket_groups: expected groups per bucket (0: unknown), which sizes the fast pass's table
 bool gen_pagg_source(const qe::Plan& P, int log2, std::string* src, size_t* lds_bytes, bool chunked = false,
                      bool soa = false, int64_t bucket_groups = 0);
@@ -127,7 +131,13 @@ int compile_program(const qe_column* cols, int32_t ncols, const bool* col_f64, c
 // SP_PERSIST (persistent grid, look-back), SP_COUNT (two-pass, first pass: selected rows per tile
 // into t.keys), SP_WRITE (two-pass, second pass: each tile's base = sum of the earlier tiles' counts),
 // SP_WRITE_SCAN (second pass after a device scan of the counts: each tile's base = t.keys[tile]).
-enum { SP_COUNTER = 0, SP_PERSIST = 1, SP_COUNT = 2, SP_WRITE = 3, SP_WRITE_SCAN = 4 };
+// SP_RESIDENT: one pass whose workgroups each hold their whole row range's predicate columns in
+// registers (gen_selproj_resident_source).
+enum { SP_COUNTER = 0, SP_PERSIST = 1, SP_COUNT = 2, SP_WRITE = 3, SP_WRITE_SCAN = 4, SP_RESIDENT = 5 };
+// rows per thread of the resident pass for n rows on `cus` CUs, or 0 when the plan or size does
+// not take it
+int selproj_resident_rows(const qe::Plan& P, const int32_t* out_kind, int nout, int64_t n, int cus);
+bool gen_selproj_resident_source(const qe::Plan& P, const int32_t* out_kind, int nout, int R, std::string* src);
 bool gen_selproj_source(const qe::Plan& P, const int32_t* out_kind, int nout, std::string* src, int mode);
 int selproj_block(int mode);  // select-project workgroup size of a mode (SP_*)
 int selproj_rows_per_thread(const qe::Plan& P, int mode);

@@ -1262,6 +1262,23 @@ static bool pagg_fast_env() {
   return v;
 }
 
+// Fast-pass LDS slot: 32-bit key, COUNT(*), per aggregate a 64-bit SUM or 32-bit MIN / MAX (a bare
+// 32-bit word), a 32-bit non-null count where tracked.
+static size_t pagg_fast_slot_bytes(const Plan& P, const std::vector<bool>& acc32) {
+  size_t bps = 8;
+  for (int j = 0; j < P.naggs; ++j) {
+    if (P.aggs[j].acc != ACC_NONE) bps += acc32[j] ? 4 : 8;
+    if (P.aggs[j].track_nn) bps += 4;
+  }
+  return bps;
+}
+// Slots (multiple of 64, + 2 special + 64 sinks) beside `fixed` bytes of other LDS
+static int pagg_fast_slots_for(size_t bps, size_t fixed) {
+  constexpr size_t kBudget = 160 * 1024 - 256;  // (s_fail, s_newg, alignment)
+  const int64_t s = fixed < kBudget ? ((int64_t)((kBudget - fixed) / bps) - 66) & ~(int64_t)63 : 0;
+  return (int)std::min<int64_t>(s, 1 << 14);
+}
+
 // Plans the fast aggregation pass takes: 32-bit integral records, integer accumulators.
 static bool pagg_fast_ok(const Plan& P, const PartLayout& L) {
   if (!L.narrow || L.row_word >= 0 || P.key_f64) return false;
@@ -1330,21 +1347,18 @@ static bool gen_pagg_fast_source(const Plan& P, const PartLayout& L, int log2, i
     const char* e = getenv("QE_PAGG_TRANSPOSE");
     return !(e && e[0] == '0');
   }();
-  size_t bps = 8;  // key + COUNT(*)
-  for (int j = 0; j < P.naggs; ++j) {
-    if (P.aggs[j].acc != ACC_NONE) bps += acc32[j] ? 4 : 8;
-    if (P.aggs[j].track_nn) bps += 4;
-  }
-  constexpr size_t kBudget = 160 * 1024 - 256;  // (s_fail, s_newg, alignment)
+  const size_t bps = pagg_fast_slot_bytes(P, acc32);
   const size_t tr_bytes = (size_t)(pagg_block() / 64) * W * 1024;
-  auto slots_for = [&](size_t fixed) -> int {
-    const int64_t s = fixed < kBudget ? ((int64_t)((kBudget - fixed) / bps) - 66) & ~(int64_t)63 : 0;
-    return (int)std::min<int64_t>(s, 1 << 14);
-  };
-  const int s_tr = slots_for((size_t)1024 * 8 + tr_bytes), s_plain = slots_for((size_t)PAGG_CHCAP * 8);
+  const int s_tr = pagg_fast_slots_for(bps, (size_t)1024 * 8 + tr_bytes);
+  const int s_plain = pagg_fast_slots_for(bps, (size_t)PAGG_CHCAP * 8);
   const bool tr = !blk && tr_env && exp == 0 && s_tr >= 256 && (bucket_groups <= 0 || 4 * bucket_groups <= s_tr);
   const int S = tr ? s_tr : s_plain, SS = S + 2;
   if (S < 256) return false;
+  // hit window: 2 buckets (default) or 3 (QE_PAGG_WINDOW=3, for fuller tables)
+  static const bool win3 = [] {
+    const char* e = getenv("QE_PAGG_WINDOW");
+    return e && e[0] == '3';
+  }();
   (void)log2;
   std::ostringstream o;
   o << "\nusing namespace qe;\n"
@@ -1509,13 +1523,16 @@ static bool gen_pagg_fast_source(const Plan& P, const PartLayout& L, int log2, i
     continue;
   }
   o << "    int slot[4];\n    qu32 h[4];\n    qu32x4 q[4];\n"
-    << "    qu32 h2[4];\n    qu32x4 q2[4];\n"
+    << "    qu32 h2[4];\n    qu32x4 q2[4];\n" << (win3 ? "    qu32 h3[4];\n    qu32x4 q3[4];\n" : "")
     << "#pragma unroll\n    for (int r = 0; r < 4; ++r) {\n"
     << "      h[r] = (qu32)(((qu64)lds_hash((qu64)key[r]) * NBK) >> 32); h2[r] = h[r] + 1 == NBK ? 0u : h[r] + 1;\n"
-    << "      q[r] = ((const qu32x4*)s_keys)[h[r]]; q2[r] = ((const qu32x4*)s_keys)[h2[r]];\n    }\n"
+    << "      q[r] = ((const qu32x4*)s_keys)[h[r]]; q2[r] = ((const qu32x4*)s_keys)[h2[r]];\n"
+    << (win3 ? "      h3[r] = h2[r] + 1 == NBK ? 0u : h2[r] + 1; q3[r] = ((const qu32x4*)s_keys)[h3[r]];\n" : "")
+    << "    }\n"
     << "#pragma unroll\n    for (int r = 0; r < 4; ++r) {\n"
     << "      const qu32 kk = (qu32)key[r];\n"
-    << "      const int hs = bucket2_hit(q[r], q2[r], kk, h[r], h2[r]);\n"
+    << (win3 ? "      const int hs = bucket3_hit(q[r], q2[r], q3[r], kk, h[r], h2[r], h3[r]);\n"
+             : "      const int hs = bucket2_hit(q[r], q2[r], kk, h[r], h2[r]);\n")
     << "      slot[r] = ((knull >> r) & 1) ? S : ((qi32)kk == EMPTY_KEY32 ? S + 1 : hs);\n"
     << "    }\n"
     << "    qu32 miss = 0;\n"
@@ -1615,6 +1632,20 @@ static bool gen_pagg_fast_source(const Plan& P, const PartLayout& L, int log2, i
     << "  if (threadIdx.x == 0 && s_newg) atomicAdd(&P.t.ctl[0], (qu64)s_newg);\n}\n";
   *src = std::string(kDevHeader) + o.str();
   return true;
+}
+
+// Largest table of the fast aggregation pass without the regrouping area (0: the plan does not take
+// the fast pass), for the bucket count of the partitioned update.
+int pagg_fast_slots(const Plan& P) {
+  const PartLayout L = part_layout(P);
+  if (!pagg_fast_env() || !pagg_fast_ok(P, L)) return 0;
+  std::vector<bool> acc32(P.naggs, false);
+  for (int j = 0; j < P.naggs; ++j) {
+    const DAgg& a = P.aggs[j];
+    const bool bare = L.colmode ? (a.ntok == 1 && a.tok[0].op == T_COL) : L.val_word[j] >= 0;
+    acc32[j] = (a.acc == ACC_MIN_I || a.acc == ACC_MAX_I) && bare;
+  }
+  return pagg_fast_slots_for(pagg_fast_slot_bytes(P, acc32), (size_t)PAGG_CHCAP * 8);
 }
 
 // `soa` (chunked only): records stored chunk-columnar, word q of slot i at
@@ -2386,6 +2417,210 @@ bool gen_selproj_source(const Plan& P, const int32_t* out_kind, int nout, std::s
   if (!emit_selproj_write(P, out_kind, nout, mode, o)) return false;
   if (persistent) o << "  __syncthreads();\n";  // s_cnt / s_base are reused by the next tile
   o << "  }\n}\n";
+  *src = std::string(kDevHeader) + o.str();
+  return true;
+}
+
+// ---- register-resident select-project (SP_RESIDENT) ---------------------------------------------------
+// One pass for batches up to ~10M rows per predicate column (C2: filter(a > 2^19) + project(a + b),
+// 10M int64, K:589-594). Workgroup w of at most one per CU owns rows [w R BT, (w + 1) R BT): it loads
+// its predicate columns (R values per thread, stripe map: row = base + r BT + t) and keeps them in
+// registers, counts its selected rows per (stripe, wave), publishes its total, and sums the totals
+// of the workgroups before it (epoch-tagged status words, so the buffer needs no memset per call).
+// Only then does it load the columns the outputs alone read, stage each group of GS stripes'
+// compacted outputs in LDS and write them with 16-byte stores. Against the two passes it replaces
+// (count pass over the predicate's columns, then the write pass re-reading them from the MALL) the
+// predicate columns cross HBM once and there is one launch. A workgroup waits only for lower ids,
+// which the in-order dispatcher placed first, so nothing depends on every workgroup being resident.
+namespace {
+constexpr int kResBlock = 1024, kResMaxRegs = 96;  // predicate values held: <= 96 VGPRs per thread
+bool sp_resident_env() {
+  static const bool v = [] {
+    const char* e = getenv("QE_SELPROJ_RESIDENT");
+    return !(e && e[0] == '0');
+  }();
+  return v;
+}
+// slots read by the outputs' programs
+unsigned out_cols(const Plan& P, int nout) {
+  unsigned m = 0;
+  for (int k = 0; k < nout; ++k)
+    for (int t = 0; t < P.aggs[k].ntok; ++t)
+      if (P.aggs[k].tok[t].op == T_COL) m |= 1u << P.aggs[k].tok[t].arg;
+  return m;
+}
+}  // namespace
+
+int selproj_resident_rows(const Plan& P, const int32_t* out_kind, int nout, int64_t n, int cus) {
+  if (!sp_resident_env() || selproj_wave_map() || n <= 0 || cus <= 0 || nout < 1 || nout > 2) return 0;
+  const unsigned pred = pred_key_cols(P), used = pred | out_cols(P, nout);
+  int npred = 0;
+  for (int c = 0; c < P.ncols; ++c) {
+    if (!((used >> c) & 1u)) continue;
+    if (P.cols[c].valid) return 0;  // (nullable inputs: the look-back and two-pass kernels)
+    const int k = P.cols[c].kind;
+    if (k != K_I64 && k != K_F64 && k != K_I32) return 0;
+    if ((pred >> c) & 1u) ++npred;
+  }
+  for (int k = 0; k < nout; ++k)
+    if ((out_kind[k] & 0x100) || (out_kind[k] & 0xFF) != 8) return 0;
+  const int64_t per = (int64_t)cus * kResBlock;
+  int R = (int)((n + per - 1) / per);
+  R = (R + 3) & ~3;  // (a few kernel shapes cover every size)
+  if (R > 48 || (int64_t)std::max(1, npred) * R * 2 > kResMaxRegs) return 0;
+  return R;
+}
+
+// Polls the status words sw[0, bid) (4 per lane, in v0..v3) until all carry this call's tag;
+// `flag` = true if it gave up (bounded spins). Scalars, not an array: an array passed to a helper
+// went to scratch.
+static std::string poll_code(const std::string& sw, const std::string& flag) {
+  std::string o;
+  o += "    {\n";
+  for (int k = 0; k < 4; ++k)
+    o += "      v" + std::to_string(k) + " = lane + " + std::to_string(64 * k) + " < bid ? 0ull : tag;\n";
+  o += "      " + flag + " = false;\n";
+  o += "      for (qu32 spins = 0;; ++spins) {\n        bool pend = false;\n";
+  for (int k = 0; k < 4; ++k) {
+    const std::string v = "v" + std::to_string(k);
+    o += "        if ((" + v + " & ~VMASK) != tag) { " + v + " = __hip_atomic_load(&" + sw + "[lane + " + std::to_string(64 * k) +
+         "], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); pend = pend || (" + v + " & ~VMASK) != tag; }\n";
+  }
+  o += "        if (!__any(pend)) break;\n";
+  o += "        if (spins >= (1u << 22)) { " + flag + " = true; break; }  // (bounded: see the host's stall check)\n";
+  o += "        __builtin_amdgcn_s_sleep(1);\n      }\n    }\n";
+  return o;
+}
+
+bool gen_selproj_resident_source(const Plan& P, const int32_t* out_kind, int nout, int R, std::string* src) {
+  if (R < 4 || R > 48 || (R & 3)) return false;
+  const unsigned pred = pred_key_cols(P), rest = out_cols(P, nout) & ~pred;
+  std::vector<Expr> ex(nout);
+  for (int k = 0; k < nout; ++k)
+    if (!agg_expr(P, k, &ex[k])) return false;
+  const int GS = std::min(R, 8);  // stripes per staged output group (<= 128 KiB of LDS; their loads in flight)
+  std::ostringstream o;
+  o << "\nusing namespace qe;\n"
+    << "extern \"C\" __global__ void __launch_bounds__(" << kResBlock << ") qe_selproj(const Plan P) {\n"
+    << "  constexpr int R = " << R << ", BT = " << kResBlock << ", W = BT / 64, GS = " << GS << ";\n"
+    << "  constexpr qu64 VMASK = (1ull << 40) - 1;\n"
+    << "  __shared__ qu32 s_cnt[R * W + 1];\n  __shared__ qu64 s_base;\n  __shared__ qu32 s_total;\n"
+    << "  __shared__ __attribute__((aligned(16))) qi64 s_out[" << nout << " * GS * BT];\n"
+    << "  const int t = threadIdx.x, lane = t & 63, w = t >> 6;\n"
+    << "  const qi64 base = (qi64)blockIdx.x * (R * BT);\n"
+    << "  const bool full = base + R * BT <= P.n;\n";
+  auto loads = [&](unsigned need, const std::string& r0, const std::string& r1, const std::string& ind) {
+    for (int c = 0; c < P.ncols; ++c) {
+      if (!((need >> c) & 1u)) continue;
+      const std::string cs = std::to_string(c);
+      const bool i32 = P.cols[c].kind == K_I32;
+      const char* ty = i32 ? "qi32" : "qi64";
+      const int wd = i32 ? 4 : 8;
+      // buffer loads off a per-workgroup descriptor whose size is the workgroup's rows: the stripe
+      // offset sits in the instruction's scalar offset (a global load's 13-bit immediate cannot
+      // reach r * 8 KiB, so each of the R loads in flight would hold a 64-bit address: spilled),
+      // and rows past the batch's end read as 0 (the hardware range check; `act` masks them)
+      o << ind << "{\n"
+        << ind << "  const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc((void*)((const " << ty
+        << "*)P.cols[" << cs << "].p + base), (short)0, nrec * " << wd << ", 0x00020000);\n"
+        << "#pragma unroll\n" << ind << "  for (int r = " << r0 << "; r < " << r1 << "; ++r) {\n";
+      if (i32)
+        o << ind << "    c" << cs << "[r] = (qi64)(qi32)__builtin_amdgcn_raw_buffer_load_b32(rs, (int)t * 4, r * BT * 4, 0);\n";
+      else
+        o << ind << "    const auto v = __builtin_amdgcn_raw_buffer_load_b64(rs, (int)t * 8, r * BT * 8, 0);\n"
+          << ind << "    c" << cs << "[r] = (qi64)(((qu64)v[1] << 32) | (qu64)v[0]);\n";
+      o << ind << "  }\n" << ind << "}\n";
+    }
+  };
+  o << "  const int nrec = (int)(P.n - base < (qi64)(R * BT) ? P.n - base : (qi64)(R * BT));  // rows of this workgroup\n";
+  for (int c = 0; c < P.ncols; ++c)
+    if (((pred | rest) >> c) & 1u) o << "  qi64 c" << c << "[R];\n";
+  loads(pred, "0", "R", "  ");
+  // act: bit r = row base + r BT + t is in range and selected (64-bit: R may exceed 32)
+  {
+    std::ostringstream q;
+    emit_predicate(P, q, 16);
+    std::string body = q.str();
+    auto repl = [&](const std::string& from, const std::string& to) {
+      for (size_t k = body.find(from); k != std::string::npos; k = body.find(from, k + to.size())) body.replace(k, from.size(), to);
+    };
+    repl("r < 16;", "r < R;");
+    repl("~(1u << r)", "~(1ull << r)");
+    o << "  qu64 act = 0;\n"
+      << "#pragma unroll\n  for (int r = 0; r < R; ++r) act |= (qu64)(full || base + r * BT + t < P.n) << r;\n"
+      << body;
+  }
+  o << "#pragma unroll\n  for (int r = 0; r < R; ++r) {\n"
+    << "    const qu64 b = __ballot((act >> r) & 1u);\n    if (lane == 0) s_cnt[r * W + w] = (qu32)__popcll(b);\n  }\n"
+    << "  __syncthreads();\n"
+    // wave 0: exclusive scan of the R x W counts (stripe-major: row order), the workgroup's total,
+    // its status word, and the sum of the lower workgroups' totals
+    << "  if (w == 0) {\n"
+    << "    constexpr int E = (R * W + 63) / 64;\n"
+    // (the lane's E counts are read twice from LDS rather than held: this kernel has no registers to spare)
+    << "    qu32 x = 0;\n"
+    << "#pragma unroll\n    for (int e = 0; e < E; ++e) x += lane * E + e < R * W ? s_cnt[lane * E + e] : 0u;\n"
+    << "    qu32 inc = x;\n"
+    << "#pragma unroll\n    for (int d = 1; d < 64; d <<= 1) { const qu32 y = __shfl_up(inc, d); if (lane >= d) inc += y; }\n"
+    << "    const qu64 total = (qu64)__shfl(inc, 63);\n"
+    << "    qu32 ex = inc - x;\n"
+    << "#pragma unroll\n    for (int e = 0; e < E; ++e) { if (lane * E + e < R * W) { const qu32 c = s_cnt[lane * E + e]; s_cnt[lane * E + e] = ex; ex += c; } }\n"
+    << "    if (lane == 0) s_cnt[R * W] = (qu32)total;\n"
+    << "    qu64* st = (qu64*)P.t.keys;  // [0, 256): totals; [256, 512): prefix taken (bit 0: a stall)\n"
+    << "    const qu64 tag = P.mp_keep << 40;  // this call's epoch\n"
+    << "    const qu32 bid = blockIdx.x;\n"
+    << "    if (lane == 0) __hip_atomic_store(&st[bid], tag | total, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);\n"
+    // the lower workgroups' status words, 4 per lane, polled together (one far round trip when
+    // they are all there)
+    << "    qu64 v0, v1, v2, v3;\n"
+    << "    bool stalled;\n"
+    << poll_code("st", "stalled")
+    << "    qu64 pre = 0;\n"
+    << "    pre += (lane < bid ? (v0 & VMASK) : 0ull) + (lane + 64 < bid ? (v1 & VMASK) : 0ull) + (lane + 128 < bid ? (v2 & VMASK) : 0ull) + (lane + 192 < bid ? (v3 & VMASK) : 0ull);\n"
+    << "#pragma unroll\n    for (int d = 32; d >= 1; d >>= 1) pre += __shfl_xor(pre, d);\n"
+    << "    if (lane == 0) __hip_atomic_store(&st[256 + bid], tag | (stalled ? 1ull : 0ull), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);\n"
+    << "    if (lane == 0) { s_base = pre; s_total = (qu32)total; }\n"
+    // the last workgroup publishes the row count once every workgroup has taken its prefix, with
+    // the stall flag first if any gave up waiting (its rows would be misplaced: the host reruns)
+    << "    if (bid == gridDim.x - 1) {\n"
+    << "      bool bad;\n" << poll_code("(st + 256)", "bad")
+    << "      bad = bad || (lane < bid && (v0 & 1)) || (lane + 64 < bid && (v1 & 1)) || (lane + 128 < bid && (v2 & 1)) || (lane + 192 < bid && (v3 & 1));\n"
+    << "      bad = __any(bad) || stalled;\n"
+    << "      if (lane == 0) {\n"
+    << "        if (bad) { __hip_atomic_store(&P.t.ctl[2], 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); if (P.host_ctl) __hip_atomic_store(&P.host_ctl[1], 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM); }\n"
+    << "        P.t.ctl[1] = pre + total;\n"
+    << "        if (P.host_ctl) { __hip_atomic_store(&P.host_ctl[0], pre + total, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM); "
+    << "__hip_atomic_store(&P.host_ctl[2], 1ull, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM); }\n"
+    << "      }\n    }\n  }\n"
+    << "  __syncthreads();\n"
+    << "  const qu64 tb = s_base;\n  const qu64 below = (1ull << lane) - 1;\n";
+  // output groups of GS stripes: load the outputs' other columns, stage compacted, store
+  for (int g0 = 0; g0 < R; g0 += GS) {
+    const int g1 = std::min(R, g0 + GS);
+    const std::string G0 = std::to_string(g0), G1 = std::to_string(g1);
+    o << "  {\n";
+    loads(rest, G0, G1, "    ");
+    o << "    const qu32 gb = s_cnt[" << g0 << " * W];\n"
+      << "    const qu32 ge = " << (g1 < R ? "s_cnt[" + G1 + " * W]" : std::string("s_total")) << ";\n"
+      << "#pragma unroll\n    for (int r = " << g0 << "; r < " << g1 << "; ++r) {\n"
+      << "      const qu64 b = __ballot((act >> r) & 1u);\n"
+      << "      if (!((act >> r) & 1u)) continue;\n"
+      << "      const qu32 lp = s_cnt[r * W + w] - gb + (qu32)__popcll(b & below);\n";
+    for (int k = 0; k < nout; ++k) o << "      s_out[" << k << " * GS * BT + lp] = " << ex[k].v << ";\n";
+    o << "    }\n    __syncthreads();\n"
+      << "    const qu32 tot = ge - gb;\n";
+    for (int k = 0; k < nout; ++k) {
+      const std::string ks = std::to_string(k);
+      o << "    {\n      qi64* out = (qi64*)P.t.acc[" << ks << "] + tb + gb;\n"
+        << "      const qi64* so = s_out + " << ks << " * GS * BT;\n"
+        << "      const qu32 mis = (qu32)(((qu64)out >> 3) & 1), head = mis < tot ? mis : tot;  // 16-byte alignment\n"
+        << "      if (head && t == 0) out[0] = so[0];\n"
+        << "      for (qu32 i = head + 2 * t; i + 1 < tot; i += 2 * BT) *(qi64x2*)(out + i) = qi64x2{so[i], so[i + 1]};\n"
+        << "      if (t == 0 && tot > head && ((tot - head) & 1)) out[tot - 1] = so[tot - 1];\n    }\n";
+    }
+    o << "    __syncthreads();\n  }\n";
+  }
+  o << "}\n";
   *src = std::string(kDevHeader) + o.str();
   return true;
 }

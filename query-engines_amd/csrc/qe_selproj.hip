@@ -29,7 +29,7 @@ namespace {
 // source (~6 us) and looking it up in the source-keyed module cache ran on every call, two passes
 // per call.
 int selproj_kernel(qe_ctx* ctx, const Plan& P, const int32_t* out_kind, int nout, int mode, hipFunction_t* fn,
-                   int* bpc) {
+                   int* bpc, int rows = 0) {
   struct Key {
     int32_t out_kind[QE_MAX_AGGS];
     int32_t nout, mode, rows, nt;
@@ -39,7 +39,7 @@ int selproj_kernel(qe_ctx* ctx, const Plan& P, const int32_t* out_kind, int nout
   for (int j = 0; j < nout; ++j) k.out_kind[j] = out_kind[j];
   k.nout = nout;
   k.mode = mode;
-  k.rows = selproj_rows(P, mode);
+  k.rows = rows ? rows : selproj_rows(P, mode);
   k.nt = selproj_nt(P);
   const std::string key = plan_shape_key(ctx, P) + std::string((const char*)&k, sizeof k);
   static std::mutex mu;
@@ -54,9 +54,10 @@ int selproj_kernel(qe_ctx* ctx, const Plan& P, const int32_t* out_kind, int nout
     }
   }
   std::string src;
-  if (!gen_selproj_source(P, out_kind, nout, &src, mode))
+  if (mode == SP_RESIDENT ? !gen_selproj_resident_source(P, out_kind, nout, rows, &src)
+                          : !gen_selproj_source(P, out_kind, nout, &src, mode))
     return fail(QE_ERR_UNSUPPORTED, "plan shape is outside the select-project generator");
-  QE_TRY(jit_kernel(ctx, src, fn, bpc, "qe_selproj", selproj_block(mode)));
+  QE_TRY(jit_kernel(ctx, src, fn, bpc, "qe_selproj", mode == SP_RESIDENT ? 1024 : selproj_block(mode)));
   std::lock_guard<std::mutex> g(mu);
   memo[key] = {*fn, *bpc};
   return QE_OK;
@@ -102,11 +103,41 @@ int init_validity(qe_ctx* ctx, const qe_column* outs, const int32_t* out_kind, i
 // its count into pin[0] (pin[1]: 1 if a persistent look-back tile never saw its predecessor).
 // `persist_ok` = false forces counter-ordered tiles (the rerun after a stall).
 int launch_select(qe_ctx* ctx, Plan& P, const int32_t* col_width, const int32_t* out_kind, int nout, bool persist_ok,
-                  uint64_t* pin, bool* persist_used, bool* poll) {
+                  uint64_t* pin, bool* persist_used, bool* poll, bool resident_ok = true) {
   *persist_used = false;
   *poll = false;
   const int64_t n = P.n;
   if (n == 0) return QE_OK;  // pin[] was zeroed by the caller
+  // One register-resident pass (SP_RESIDENT, qe_jit.hip gen_selproj_resident_source) while every
+  // workgroup's predicate columns fit its registers: ~10M rows of one 8-byte predicate column.
+  // QE_SELPROJ_TWOPASS (any value) picks the other modes, QE_SELPROJ_RESIDENT=0 turns it off.
+  const char* tpe0 = getenv("QE_SELPROJ_TWOPASS");
+  const int rres = (resident_ok && !(tpe0 && *tpe0)) ? selproj_resident_rows(P, out_kind, nout, n, ctx->num_cus) : 0;
+  const int64_t rgrid = rres ? (int64_t)div_up((uint64_t)n, (uint64_t)rres * 1024) : 0;
+  if (rres && rgrid <= 256) {
+    if (!ctx->sp_status) {
+      QE_HIP(hipMalloc(&ctx->sp_status, 512 * 8));
+      QE_HIP(hipMemsetAsync(ctx->sp_status, 0, 512 * 8, ctx->stream));
+    }
+    if (++ctx->sp_epoch >= (1u << 24)) {  // epoch tags are 24 bits: clear the words once per 16M calls
+      QE_HIP(hipMemsetAsync(ctx->sp_status, 0, 512 * 8, ctx->stream));
+      ctx->sp_epoch = 1;
+    }
+    void* s;
+    QE_TRY(ctx_scratch(ctx, 3 * 8, &s));
+    P.t.ctl = (qu64*)s;
+    P.t.keys = (qi64*)ctx->sp_status;
+    P.t.cap = (qu64)rgrid;
+    P.mp_keep = ctx->sp_epoch;
+    P.host_ctl = (qu64*)pin;
+    hipFunction_t fn;
+    int bpc = 0;
+    QE_TRY(selproj_kernel(ctx, P, out_kind, nout, SP_RESIDENT, &fn, &bpc, rres));
+    QE_TRY(jit_launch(ctx, fn, (int)rgrid, P, 1024));
+    QE_TRY(launch_check("qe_selproj (resident)"));
+    *poll = true;
+    return QE_OK;
+  }
   // Tile order: a persistent grid (every workgroup resident, tiles assigned statically) or one
   // tile per workgroup with ids from a device counter in start order (QE_SELPROJ_PERSIST=0). The
   // counter is one word every workgroup hits: ~88 returning atomics/us, a floor of 2.8 ms for
@@ -349,6 +380,19 @@ int qe_select_pending_wait(qe_select_pending* r, int64_t* out_count) {
       (void)hipGetLastError();
     }
     std::atomic_thread_fence(std::memory_order_acquire);
+    if (st == QE_OK && pv[1] != 0) {
+      // a resident-pass workgroup gave up waiting for a lower one's count (only if its dispatch
+      // was held back for seconds): its rows may be misplaced; rerun without the resident pass
+      fprintf(stderr, "qe: select-project resident pass stalled; rerunning with two passes\n");
+      bool used = false, poll = false;
+      st = ctx_sync(ctx);
+      if (st == QE_OK) {
+        r->pin[0] = r->pin[1] = r->pin[2] = 0;
+        st = launch_select(ctx, r->P, r->col_width, r->out_kind, r->nout, true, r->pin, &used, &poll, false);
+      }
+      if (st == QE_OK) st = ctx_sync(ctx);
+      if (st == QE_OK && r->pin[1] != 0) st = fail(QE_ERR_DEVICE, "select-project look-back did not complete");
+    }
     if (st == QE_OK) *out_count = (int64_t)pv[0];
     // the slot's last device write (pin[2]) has landed: reusable at once; the event may be pending
     pending_free(r, st == QE_OK, true);

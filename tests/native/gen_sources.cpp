@@ -54,6 +54,21 @@ static int emit(const char* dir, const char* name, const qe_column* cols, int nc
     fclose(f);
     printf("%s\n", path.c_str());
   }
+  // register-resident one-pass kernel (SP_RESIDENT) at 40 rows per thread, where the plan takes it
+  const int R = selproj_resident_rows(P, out_kind, nout, 10000000, 256);
+  if (R > 0) {
+    std::string src;
+    if (!gen_selproj_resident_source(P, out_kind, nout, R, &src)) {
+      fprintf(stderr, "%s: resident mode not generated\n", name);
+      return 1;
+    }
+    const std::string path = std::string(dir) + "/" + name + "_m" + std::to_string(SP_RESIDENT) + ".hip";
+    FILE* f = fopen(path.c_str(), "w");
+    if (!f) return 1;
+    fwrite(src.data(), 1, src.size(), f);
+    fclose(f);
+    printf("%s\n", path.c_str());
+  }
   return 0;
 }
 

@@ -43,12 +43,16 @@ def _run(ctx, cols, spec, out_types):
     return cnt.value, outs
 
 
-@pytest.fixture(params=["twopass", "lookback", "scanned"])
+@pytest.fixture(params=["default", "twopass", "lookback", "scanned"])
 def selproj_path(request, monkeypatch):
-    """Every tile-base scheme: two passes (count, then write; the default while the predicate's
-    columns fit the MALL), the single pass with a decoupled look-back, and two passes with a device
-    scan of the tile counts between them."""
-    monkeypatch.setenv("QE_SELPROJ_TWOPASS", {"twopass": "1", "lookback": "0", "scanned": "2"}[request.param])
+    """Every tile-base scheme: the default (one register-resident pass while each workgroup's
+    predicate columns fit its registers, ~12M rows of one 8-byte column and non-nullable columns;
+    else two passes), two passes (count, then write), the single pass with a decoupled look-back,
+    and two passes with a device scan of the tile counts between them."""
+    if request.param == "default":
+        monkeypatch.delenv("QE_SELPROJ_TWOPASS", raising=False)
+    else:
+        monkeypatch.setenv("QE_SELPROJ_TWOPASS", {"twopass": "1", "lookback": "0", "scanned": "2"}[request.param])
     return request.param
 
 
@@ -72,6 +76,28 @@ def test_c2_shape(gpu_ctx, selproj_path, n, k):
     assert (ab.to_numpy() == want).all()
     assert (b.to_numpy() == fb).all()
     assert ab.valid_mask().all()
+
+
+@pytest.mark.parametrize("n", [10_000_000, 10_485_761, 12_582_912, 12_582_913])
+def test_c2_resident_limits(gpu_ctx, monkeypatch, n):
+    """The register-resident pass at C2's size and its limits on 256 CUs: 40 rows per thread
+    (10M), 44 (just past 10,485,760 = 256 x 1024 x 40), 48 (12,582,912, the largest), and one row
+    more (two passes again). Bit-exact vs the oracle; the count arrives through the polled word."""
+    from kquery import native as N
+    from kquery.datasource import C2_COLUMNS, generate_column
+
+    monkeypatch.delenv("QE_SELPROJ_TWOPASS", raising=False)
+    k = 1 << 19
+    cols = [generate_column(s, n, 0, 42, gpu_ctx) for s in C2_COLUMNS]
+    spec = _spec(N, [(0, N.OP_GT, -1, k)], [[(N.TOK_COL, 0, None), (N.TOK_COL, 1, None), (N.TOK_ADD, 0, None)]])
+    a_h, _ = gen.generate(C2_COLUMNS[0].dist, C2_COLUMNS[0].param, 42, C2_COLUMNS[0].col_id, 0, n)
+    b_h, _ = gen.generate(C2_COLUMNS[1].dist, C2_COLUMNS[1].param, 42, C2_COLUMNS[1].col_id, 0, n)
+    m = a_h > k
+    want = (a_h[m].astype(np.uint64) + b_h[m].astype(np.uint64)).astype(np.int64)
+    for _ in range(2):  # (a second call: new epoch tags over the same status words)
+        cnt, (ab,) = _run(gpu_ctx, cols, spec, [N.TYPE_INT64])
+        assert cnt == int(m.sum())
+        assert (ab.to_numpy() == want).all()
 
 
 @pytest.mark.parametrize("n", [1, 4097, 100_003, 3_000_017])

@@ -114,6 +114,21 @@ def main():
             return statistics.median(ts)
 
         ms_wall = wall(run_kernel)
+        # host split of one call: enqueue (qe_select_project_async) and wait (qe_select_pending_wait)
+        enq, wt = [], []
+        for it in range(35):
+            torch.cuda.synchronize()
+            oc[0].length = n
+            pend = N.C.c_void_p()
+            t0 = time.perf_counter()
+            N.check(N.lib().qe_select_project_async(ctx.handle, cc, 2, N.C.byref(fused.spec), oc, N.C.byref(pend)))
+            t1 = time.perf_counter()
+            N.check(N.lib().qe_select_pending_wait(pend, N.C.byref(cnt)))
+            t2 = time.perf_counter()
+            if it >= 5:
+                enq.append((t1 - t0) * 1e3)
+                wt.append((t2 - t1) * 1e3)
+        ms_enq, ms_wait = statistics.median(enq), statistics.median(wt)
         # the same call with the input evicted from the 256 MB MALL first (a 1 GiB write between
         # calls, outside the timed region): what one 10M batch costs from HBM. The write leaves the
         # MALL full of dirty lines, so the call's reads also pay their write-back; "clean" evicts
@@ -138,7 +153,8 @@ def main():
         report("C2 fused select+project (qe_select_project), 10M int64", n, 16 + 8 * sel_rows / n, ms_f,
                selected=sel_rows, call_ms=ms_k, call_gbs=n * (16 + 8 * sel_rows / n) / (ms_k * 1e-3) / 1e9,
                call_cold_ms=ms_cold, call_cold_gbs=n * (16 + 8 * sel_rows / n) / (ms_cold * 1e-3) / 1e9,
-               call_wall_ms=ms_wall, call_cold_wall_ms=ms_cold_wall, call_cold_clean_wall_ms=ms_clean_wall,
+               call_wall_ms=ms_wall, call_enqueue_ms=ms_enq, call_wait_ms=ms_wait,
+               call_cold_wall_ms=ms_cold_wall, call_cold_clean_wall_ms=ms_clean_wall,
                call_cold_clean_frac=n * (16 + 8 * sel_rows / n) / (ms_clean_wall * 1e-3) / 8e12,
                path="one hipRTC-specialised kernel: predicate, look-back compaction, projection")
         # stream-ordered calls (qe_select_project_async): call i+1 is queued before call i's count
