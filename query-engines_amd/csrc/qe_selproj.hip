@@ -24,6 +24,32 @@ using namespace qe;
 
 namespace {
 
+// QE_HOST_PROFILE=1: per-stage host time of qe_select_project_async, printed at exit (tools only)
+struct HostProf {
+  double sum[8] = {};
+  long n = 0;
+  bool on = [] {
+    const char* e = getenv("QE_HOST_PROFILE");
+    return e && e[0] == '1';
+  }();
+  ~HostProf() {
+    if (!on || !n) return;
+    fprintf(stderr, "{\"select_project_host_us\": {\"compile\": %.2f, \"alloc\": %.2f, \"kernel_lookup\": %.2f, "
+            "\"launch\": %.2f, \"event\": %.2f, \"calls\": %ld}}\n", sum[1] / n, sum[2] / n, sum[3] / n, sum[4] / n, sum[5] / n, n);
+  }
+};
+HostProf g_hprof;
+inline double now_us() {
+  return std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+double g_hp_t = 0;
+inline void hprof(int stage) {
+  if (!g_hprof.on) return;
+  const double t = now_us();
+  if (stage > 0) g_hprof.sum[stage] += t - g_hp_t;
+  g_hp_t = t;
+}
+
 // Kernel of one plan shape and pass, memoised on the plan's structure (plan_shape_key) plus what
 // else the generator reads: output kinds, pass, rows per thread, load policy. Generating the
 // source (~6 us) and looking it up in the source-keyed module cache ran on every call, two passes
@@ -132,8 +158,11 @@ int launch_select(qe_ctx* ctx, Plan& P, const int32_t* col_width, const int32_t*
     P.host_ctl = (qu64*)pin;
     hipFunction_t fn;
     int bpc = 0;
+    hprof(0);
     QE_TRY(selproj_kernel(ctx, P, out_kind, nout, SP_RESIDENT, &fn, &bpc, rres));
+    hprof(3);
     QE_TRY(jit_launch(ctx, fn, (int)rgrid, P, 1024));
+    hprof(4);
     QE_TRY(launch_check("qe_selproj (resident)"));
     *poll = true;
     return QE_OK;
@@ -309,6 +338,7 @@ int qe_select_project_async(qe_ctx* ctx, const qe_column* cols, int32_t ncols, c
   QE_TRY(ctx_enter(ctx));
   QE_CHECK(cols && spec && outs && pending, QE_ERR_INVALID_ARG, "null argument");
   *pending = nullptr;
+  hprof(0);
   QE_CHECK(spec->nout >= 1 && spec->nout <= QE_MAX_AGGS, QE_ERR_UNSUPPORTED, "select-project takes 1..%d outputs",
            QE_MAX_AGGS);
   std::unique_ptr<qe_select_pending> r(new qe_select_pending());
@@ -337,16 +367,25 @@ int qe_select_project_async(qe_ctx* ctx, const qe_column* cols, int32_t ncols, c
     r->outs[k] = outs[k];
   }
   if (!ctx->jit) return fail(QE_ERR_UNSUPPORTED, "fused select-project needs kernel specialisation (jit is off)");
+  hprof(1);
   QE_TRY(pinned_slot_alloc(&r->pin));
   r->pin[0] = r->pin[1] = r->pin[2] = 0;  // the slot's previous user is done with it (pinned_slot_alloc)
-  QE_TRY(event_alloc(&r->ev));
   QE_TRY(init_validity(ctx, outs, r->out_kind, r->nout, n));
+  hprof(2);
   const int st = launch_select(ctx, P, r->col_width, r->out_kind, r->nout, true, r->pin, &r->persist, &r->poll);
   if (st != QE_OK) {
     pending_free(r.release());
     return st;
   }
-  QE_HIP(hipEventRecord(r->ev, ctx->stream));
+  hprof(0);
+  // polled calls need no completion event (the wait spins on pin[2] and, as a fallback, queries the
+  // stream): one runtime call less per batch
+  if (!r->poll) {
+    QE_TRY(event_alloc(&r->ev));
+    QE_HIP(hipEventRecord(r->ev, ctx->stream));
+  }
+  hprof(5);
+  if (g_hprof.on) ++g_hprof.n;
   *pending = r.release();
   return QE_OK;
 }
@@ -368,7 +407,7 @@ int qe_select_pending_wait(qe_select_pending* r, int64_t* out_count) {
       if ((i & 1023) != 0) continue;
       if (std::chrono::steady_clock::now() - t0 < std::chrono::microseconds(50)) continue;
       t0 = std::chrono::steady_clock::now();
-      const hipError_t e = hipEventQuery(r->ev);
+      const hipError_t e = r->ev ? hipEventQuery(r->ev) : hipStreamQuery(ctx->stream);
       if (e == hipSuccess) {
         if (pv[2] == 0) st = fail(QE_ERR_DEVICE, "select-project finished without publishing its row count");
         break;
@@ -398,7 +437,8 @@ int qe_select_pending_wait(qe_select_pending* r, int64_t* out_count) {
     pending_free(r, st == QE_OK, true);
     return st;
   }
-  if (st == QE_OK && hipEventSynchronize(r->ev) != hipSuccess) st = fail(QE_ERR_DEVICE, "select-project event wait failed");
+  if (st == QE_OK && (r->ev ? hipEventSynchronize(r->ev) : hipStreamSynchronize(ctx->stream)) != hipSuccess)
+    st = fail(QE_ERR_DEVICE, "select-project event wait failed");
   if (st == QE_OK && r->pin[1] != 0) {
     // a persistent workgroup was not resident: every wave drained; rerun with counter-ordered tiles
     if (!r->persist) {

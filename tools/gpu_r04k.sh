@@ -17,3 +17,4 @@ run fill68w3 QE_PART_FAST_FILL=68 QE_PAGG_WINDOW=3 || exit 1
 run fill80w3 QE_PART_FAST_FILL=80 QE_PAGG_WINDOW=3 || exit 1
 run wg3 QE_PART_WG_PER_CU=3 || exit 1
 run wg4 QE_PART_WG_PER_CU=4 || exit 1
+QE_HOST_PROFILE=1 timeout -k 10 200 python3 tools/bench_configs.py C2 > $OUT/c2_hostprof.jsonl 2> $OUT/c2_hostprof.err || exit 1
