@@ -631,6 +631,60 @@ __device__ inline int bucket3_hit(qu32x4 q, qu32x4 q2, qu32x4 q3, qu32 kk, qu32 
   return i >= 0 ? i : (m ? (int)(4 * b3) + __builtin_ctz(m) : -1);
 }
 
+// lds_probe4 for up to four rows of a lane at once (bit r of pm: row r pending; key k_r, home bucket
+// h_r; its slot, or -1, into s_r). Each iteration advances the lowest pending row of EVERY lane by
+// one bucket, so a wave spends about the longest lane's total probe length instead of, row after
+// row, the longest probe of that row. Same probe order and insert rule as lds_probe4 (the first
+// EMPTY slot from the home bucket on), so keys are never duplicated.
+__device__ inline void lds_probe4_rows(qi32* keys, qu32 nb, qu32 pm, qi32 k0, qi32 k1, qi32 k2, qi32 k3, qu32 h0,
+                                       qu32 h1, qu32 h2, qu32 h3, int& s0, int& s1, int& s2, int& s3) {
+  const qu32 pm0 = pm;
+  int r = pm ? __builtin_ctz(pm) : 0;
+  qu32 b = r == 0 ? h0 : r == 1 ? h1 : r == 2 ? h2 : h3;
+  int probes = 0;
+  qu64 res = 0;
+#pragma unroll 1
+  while (pm) {
+    const qi32 kk = r == 0 ? k0 : r == 1 ? k1 : r == 2 ? k2 : k3;
+    const qu32x4 q = *(const volatile qu32x4*)(keys + 4 * b);
+    const qu32 m = (qu32)(q.x == (qu32)kk) | ((qu32)(q.y == (qu32)kk) << 1) | ((qu32)(q.z == (qu32)kk) << 2) |
+                   ((qu32)(q.w == (qu32)kk) << 3);
+    const qu32 e = (qu32)(q.x == (qu32)EMPTY_KEY32) | ((qu32)(q.y == (qu32)EMPTY_KEY32) << 1) |
+                   ((qu32)(q.z == (qu32)EMPTY_KEY32) << 2) | ((qu32)(q.w == (qu32)EMPTY_KEY32) << 3);
+    int found = -2;  // -2: keep probing
+    if (m) {
+      found = (int)(4 * b) + __builtin_ctz(m);
+    } else if (e) {
+      const int i = __builtin_ctz(e);
+      const qi32 old = atomicCAS(&keys[4 * b + i], EMPTY_KEY32, kk);
+      if (old == EMPTY_KEY32 || old == kk) found = (int)(4 * b) + i;
+      // else another key took that slot: read the same bucket again
+    } else if (++probes >= HA_LDS_MAXP) {
+      found = -1;
+    } else {
+      b = b + 1 == nb ? 0 : b + 1;
+    }
+    if (found != -2) {
+      // (results packed 16 bits per row: a row-indexed write would put s0..s3 in scratch)
+      res = (res & ~(0xFFFFull << (16 * r))) | ((qu64)(qu32)(found & 0xFFFF) << (16 * r));
+      pm &= pm - 1;
+      if (pm) {
+        r = __builtin_ctz(pm);
+        b = r == 0 ? h0 : r == 1 ? h1 : r == 2 ? h2 : h3;
+        probes = 0;
+      }
+    }
+  }
+  auto unpack = [&](int q, int& dst) {
+    const qu32 v = (qu32)(res >> (16 * q)) & 0xFFFFu;
+    if ((pm0 >> q) & 1) dst = v == 0xFFFFu ? -1 : (int)v;
+  };
+  unpack(0, s0);
+  unpack(1, s1);
+  unpack(2, s2);
+  unpack(3, s3);
+}
+
 // lds_probe32 over a table of `nsl` slots (any count: the compact fused table).
 __device__ inline int lds_probe32n(qi32* keys, qu32 nsl, qi32 key, qu32 h) {
 #pragma unroll 1

@@ -483,7 +483,9 @@ void emit_agg_rows_c(const Plan& P, std::ostringstream& o, const std::vector<std
     << "    qu32 miss = 0;\n"
     << "#pragma unroll\n    for (int r = 0; r < 4; ++r) miss |= (qu32)(slot[r] < 0) << r;\n"
     << "    miss &= act & fit;\n"
-    << "    if (miss) {\n      for (int r = 0; r < 4; ++r) if ((miss >> r) & 1) slot[r] = lds_probe4(s_keys, NBK, (qi32)key[r], h[r]);\n    }\n"
+    << "    if (miss) {\n      int t0 = slot[0], t1 = slot[1], t2 = slot[2], t3 = slot[3];\n"
+    << "      lds_probe4_rows(s_keys, NBK, miss, (qi32)key[0], (qi32)key[1], (qi32)key[2], (qi32)key[3], h[0], h[1], h[2], h[3], t0, t1, t2, t3);\n"
+    << "      slot[0] = t0; slot[1] = t1; slot[2] = t2; slot[3] = t3;\n    }\n"
     << "    qu32 glob = ~fit;\n"
     << "#pragma unroll\n    for (int r = 0; r < 4; ++r) glob |= (qu32)(slot[r] < 0) << r;\n"
     << "    glob &= act;\n    const qu32 loc = act & ~glob;\n"
@@ -1538,7 +1540,9 @@ static bool gen_pagg_fast_source(const Plan& P, const PartLayout& L, int log2, i
     << "    qu32 miss = 0;\n"
     << "#pragma unroll\n    for (int r = 0; r < 4; ++r) miss |= (qu32)(slot[r] < 0) << r;\n"
     << "    miss &= act;\n"
-    << "    if (miss) {\n      for (int r = 0; r < 4; ++r) if ((miss >> r) & 1) slot[r] = lds_probe4(s_keys, NBK, (qi32)key[r], h[r]);\n    }\n"
+    << "    if (miss) {\n      int t0 = slot[0], t1 = slot[1], t2 = slot[2], t3 = slot[3];\n"
+    << "      lds_probe4_rows(s_keys, NBK, miss, (qi32)key[0], (qi32)key[1], (qi32)key[2], (qi32)key[3], h[0], h[1], h[2], h[3], t0, t1, t2, t3);\n"
+    << "      slot[0] = t0; slot[1] = t1; slot[2] = t2; slot[3] = t3;\n    }\n"
     << "    qu32 glob = 0;\n"
     << "#pragma unroll\n    for (int r = 0; r < 4; ++r) glob |= (qu32)(slot[r] < 0) << r;\n"
     << "    glob &= act;\n    const qu32 loc = act & ~glob;\n"
