@@ -26,7 +26,8 @@ struct qe_ctx {
   size_t scan_tmp_bytes = 0;
   void* ws[8] = {};              // grow-only workspace slots (CSV scan intermediates)
   size_t ws_bytes[8] = {};
-  void* sp_status = nullptr;     // per-workgroup counts of the register-resident select-project
+  void* sp_status = nullptr;     // per-tile counts of the register-resident select-project
+  size_t sp_status_bytes = 0;
   uint32_t sp_epoch = 0;         // (epoch-tagged, so no memset per call; qe_selproj.hip)
 };
 

@@ -2471,24 +2471,34 @@ int selproj_resident_rows(const Plan& P, const int32_t* out_kind, int nout, int6
   const int64_t per = (int64_t)cus * kResBlock;
   int R = (int)((n + per - 1) / per);
   R = (R + 3) & ~3;  // (a few kernel shapes cover every size)
+  // larger batches: several rounds of tiles (QE_SELPROJ_RESIDENT_ROUNDS=1; opt-in)
+  static const bool rounds = [] {
+    const char* e = getenv("QE_SELPROJ_RESIDENT_ROUNDS");
+    return e && e[0] == '1';
+  }();
+  if (R > 48 && rounds) R = 32;
   if (R > 48 || (int64_t)std::max(1, npred) * R * 2 > kResMaxRegs) return 0;
   return R;
 }
 
-// Polls the status words sw[0, bid) (4 per lane, in v0..v3) until all carry this call's tag;
-// `flag` = true if it gave up (bounded spins). Scalars, not an array: an array passed to a helper
-// went to scratch.
-static std::string poll_code(const std::string& sw, const std::string& flag) {
+// Polls status words (4 per lane, in v0..v3: word i = lane + 64 k is `addr(i)`, taking part when
+// `part(i)`; "@" stands for i) until all carry this call's tag; `flag` = true if it gave up (bounded
+// spins). Scalars, not an array: an array passed to a helper went to scratch.
+static std::string poll_code(const std::string& addr, const std::string& part, const std::string& flag) {
+  auto sub = [](std::string e, int k) {
+    const std::string i = "(lane + " + std::to_string(64 * k) + ")";
+    for (size_t p = e.find('@'); p != std::string::npos; p = e.find('@', p + i.size())) e.replace(p, 1, i);
+    return e;
+  };
   std::string o;
   o += "    {\n";
-  for (int k = 0; k < 4; ++k)
-    o += "      v" + std::to_string(k) + " = lane + " + std::to_string(64 * k) + " < bid ? 0ull : tag;\n";
+  for (int k = 0; k < 4; ++k) o += "      v" + std::to_string(k) + " = (" + sub(part, k) + ") ? 0ull : tag;\n";
   o += "      " + flag + " = false;\n";
   o += "      for (qu32 spins = 0;; ++spins) {\n        bool pend = false;\n";
   for (int k = 0; k < 4; ++k) {
     const std::string v = "v" + std::to_string(k);
-    o += "        if ((" + v + " & ~VMASK) != tag) { " + v + " = __hip_atomic_load(&" + sw + "[lane + " + std::to_string(64 * k) +
-         "], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); pend = pend || (" + v + " & ~VMASK) != tag; }\n";
+    o += "        if ((" + v + " & ~VMASK) != tag) { " + v + " = __hip_atomic_load(&" + sub(addr, k) +
+         ", __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); pend = pend || (" + v + " & ~VMASK) != tag; }\n";
   }
   o += "        if (!__any(pend)) break;\n";
   o += "        if (spins >= (1u << 22)) { " + flag + " = true; break; }  // (bounded: see the host's stall check)\n";
@@ -2496,7 +2506,10 @@ static std::string poll_code(const std::string& sw, const std::string& flag) {
   return o;
 }
 
-bool gen_selproj_resident_source(const Plan& P, const int32_t* out_kind, int nout, int R, std::string* src) {
+bool gen_selproj_resident_source(const Plan& P, const int32_t* out_kind, int nout, int rows, std::string* src) {
+  // rows: R (rows per thread) | 0x100 when the workgroups walk several rounds of tiles
+  const int R = rows & 0xFF;
+  const bool multi = (rows & 0x100) != 0;
   if (R < 4 || R > 48 || (R & 3)) return false;
   const unsigned pred = pred_key_cols(P), rest = out_cols(P, nout) & ~pred;
   std::vector<Expr> ex(nout);
@@ -2511,7 +2524,16 @@ bool gen_selproj_resident_source(const Plan& P, const int32_t* out_kind, int nou
     << "  __shared__ qu32 s_cnt[R * W + 1];\n  __shared__ qu64 s_base;\n  __shared__ qu32 s_total;\n"
     << "  __shared__ __attribute__((aligned(16))) qi64 s_out[" << nout << " * GS * BT];\n"
     << "  const int t = threadIdx.x, lane = t & 63, w = t >> 6;\n"
-    << "  const qi64 base = (qi64)blockIdx.x * (R * BT);\n"
+    << "  const qu64 tag = P.mp_keep << 40;  // this call's epoch\n"
+    << "  qu64* st = (qu64*)P.t.keys;  // [0, 256): per workgroup, its tiles' prefixes taken (bit 0: a stall); [256, ...): tile totals\n"
+    << "  const qu32 bid = blockIdx.x, G = gridDim.x;\n"
+    << "  const qu64 ntiles = P.t.cap;\n"
+    << "  qu64 pre_prev = 0;  // (wave 0) this workgroup's previous tile's prefix\n"
+    << "  bool stalled_any = false;\n"
+    // tile T = round * G + workgroup; its prefix = the same workgroup's previous tile's prefix + the
+    // totals of the G tiles just before T (one far round trip when they are all there)
+    << (multi ? "  for (qu32 T = bid; T < ntiles; T += G) {\n" : "  {\n  const qu32 T = bid;\n")
+    << "  const qi64 base = (qi64)T * (R * BT);\n"
     << "  const bool full = base + R * BT <= P.n;\n";
   auto loads = [&](unsigned need, const std::string& r0, const std::string& r1, const std::string& ind) {
     for (int c = 0; c < P.ncols; ++c) {
@@ -2570,26 +2592,26 @@ bool gen_selproj_resident_source(const Plan& P, const int32_t* out_kind, int nou
     << "    qu32 ex = inc - x;\n"
     << "#pragma unroll\n    for (int e = 0; e < E; ++e) { if (lane * E + e < R * W) { const qu32 c = s_cnt[lane * E + e]; s_cnt[lane * E + e] = ex; ex += c; } }\n"
     << "    if (lane == 0) s_cnt[R * W] = (qu32)total;\n"
-    << "    qu64* st = (qu64*)P.t.keys;  // [0, 256): totals; [256, 512): prefix taken (bit 0: a stall)\n"
-    << "    const qu64 tag = P.mp_keep << 40;  // this call's epoch\n"
-    << "    const qu32 bid = blockIdx.x;\n"
-    << "    if (lane == 0) __hip_atomic_store(&st[bid], tag | total, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);\n"
-    // the lower workgroups' status words, 4 per lane, polled together (one far round trip when
-    // they are all there)
+    << "    if (lane == 0) __hip_atomic_store(&st[256 + T], tag | total, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);\n"
+    // the G tiles before T (window word i: tile T - G + i), 4 per lane, polled together
+    << "    const qi64 w0 = (qi64)T - (qi64)G;\n"
     << "    qu64 v0, v1, v2, v3;\n"
     << "    bool stalled;\n"
-    << poll_code("st", "stalled")
+    << poll_code("st[256 + w0 + @]", "@ < G && w0 + @ >= 0", "stalled")
     << "    qu64 pre = 0;\n"
-    << "    pre += (lane < bid ? (v0 & VMASK) : 0ull) + (lane + 64 < bid ? (v1 & VMASK) : 0ull) + (lane + 128 < bid ? (v2 & VMASK) : 0ull) + (lane + 192 < bid ? (v3 & VMASK) : 0ull);\n"
+    << "    pre += (lane < G && w0 + lane >= 0 ? (v0 & VMASK) : 0ull) + (lane + 64 < G && w0 + lane + 64 >= 0 ? (v1 & VMASK) : 0ull) +\n"
+    << "           (lane + 128 < G && w0 + lane + 128 >= 0 ? (v2 & VMASK) : 0ull) + (lane + 192 < G && w0 + lane + 192 >= 0 ? (v3 & VMASK) : 0ull);\n"
     << "#pragma unroll\n    for (int d = 32; d >= 1; d >>= 1) pre += __shfl_xor(pre, d);\n"
-    << "    if (lane == 0) __hip_atomic_store(&st[256 + bid], tag | (stalled ? 1ull : 0ull), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);\n"
+    << "    pre += pre_prev;\n    pre_prev = pre;\n"
+    << "    stalled_any = stalled_any || __any(stalled);\n"
     << "    if (lane == 0) { s_base = pre; s_total = (qu32)total; }\n"
-    // the last workgroup publishes the row count once every workgroup has taken its prefix, with
-    // the stall flag first if any gave up waiting (its rows would be misplaced: the host reruns)
-    << "    if (bid == gridDim.x - 1) {\n"
-    << "      bool bad;\n" << poll_code("(st + 256)", "bad")
-    << "      bad = bad || (lane < bid && (v0 & 1)) || (lane + 64 < bid && (v1 & 1)) || (lane + 128 < bid && (v2 & 1)) || (lane + 192 < bid && (v3 & 1));\n"
-    << "      bad = __any(bad) || stalled;\n"
+    // the last tile publishes the row count once every other workgroup has taken all its tiles'
+    // prefixes, with the stall flag first if any gave up waiting (rows misplaced: the host reruns)
+    << "    if (T == ntiles - 1) {\n"
+    << "      bool bad;\n" << poll_code("st[@]", "@ < G && @ != bid", "bad")
+    << "      bad = bad || (lane < G && lane != bid && (v0 & 1)) || (lane + 64 < G && lane + 64 != bid && (v1 & 1)) ||\n"
+    << "            (lane + 128 < G && lane + 128 != bid && (v2 & 1)) || (lane + 192 < G && lane + 192 != bid && (v3 & 1));\n"
+    << "      bad = __any(bad) || stalled_any;\n"
     << "      if (lane == 0) {\n"
     << "        if (bad) { __hip_atomic_store(&P.t.ctl[2], 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); if (P.host_ctl) __hip_atomic_store(&P.host_ctl[1], 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM); }\n"
     << "        P.t.ctl[1] = pre + total;\n"
@@ -2624,7 +2646,9 @@ bool gen_selproj_resident_source(const Plan& P, const int32_t* out_kind, int nou
     }
     o << "    __syncthreads();\n  }\n";
   }
-  o << "}\n";
+  o << "  }  // tiles\n"
+    << "  if (t == 0) __hip_atomic_store(&st[bid], tag | (stalled_any ? 1ull : 0ull), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);\n"
+    << "}\n";
   *src = std::string(kDevHeader) + o.str();
   return true;
 }

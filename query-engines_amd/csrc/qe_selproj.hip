@@ -139,27 +139,39 @@ int launch_select(qe_ctx* ctx, Plan& P, const int32_t* col_width, const int32_t*
   // QE_SELPROJ_TWOPASS (any value) picks the other modes, QE_SELPROJ_RESIDENT=0 turns it off.
   const char* tpe0 = getenv("QE_SELPROJ_TWOPASS");
   const int rres = (resident_ok && !(tpe0 && *tpe0)) ? selproj_resident_rows(P, out_kind, nout, n, ctx->num_cus) : 0;
-  const int64_t rgrid = rres ? (int64_t)div_up((uint64_t)n, (uint64_t)rres * 1024) : 0;
+  // tiles of R x 1024 rows, one workgroup per CU walking them in rounds (one round up to ~12M rows)
+  const int64_t rtiles = rres ? (int64_t)div_up((uint64_t)n, (uint64_t)rres * 1024) : 0;
+  const int64_t rgrid = std::min<int64_t>(rtiles, ctx->num_cus);
   if (rres && rgrid <= 256) {
-    if (!ctx->sp_status) {
-      QE_HIP(hipMalloc(&ctx->sp_status, 512 * 8));
-      QE_HIP(hipMemsetAsync(ctx->sp_status, 0, 512 * 8, ctx->stream));
+    // status words: 256 per-workgroup "prefixes taken" + one total per tile, epoch-tagged
+    const size_t need = (size_t)(256 + rtiles) * 8;
+    if (need > ctx->sp_status_bytes) {
+      if (ctx->sp_status) {
+        QE_HIP(hipStreamSynchronize(ctx->stream));  // (an earlier call may still read the old words)
+        (void)hipFree(ctx->sp_status);
+        ctx->sp_status = nullptr;
+        ctx->sp_status_bytes = 0;
+      }
+      const size_t bytes = std::max<size_t>(need, 512 * 8);
+      QE_HIP(hipMalloc(&ctx->sp_status, bytes));
+      QE_HIP(hipMemsetAsync(ctx->sp_status, 0, bytes, ctx->stream));
+      ctx->sp_status_bytes = bytes;
     }
     if (++ctx->sp_epoch >= (1u << 24)) {  // epoch tags are 24 bits: clear the words once per 16M calls
-      QE_HIP(hipMemsetAsync(ctx->sp_status, 0, 512 * 8, ctx->stream));
+      QE_HIP(hipMemsetAsync(ctx->sp_status, 0, ctx->sp_status_bytes, ctx->stream));
       ctx->sp_epoch = 1;
     }
     void* s;
     QE_TRY(ctx_scratch(ctx, 3 * 8, &s));
     P.t.ctl = (qu64*)s;
     P.t.keys = (qi64*)ctx->sp_status;
-    P.t.cap = (qu64)rgrid;
+    P.t.cap = (qu64)rtiles;
     P.mp_keep = ctx->sp_epoch;
     P.host_ctl = (qu64*)pin;
     hipFunction_t fn;
     int bpc = 0;
     hprof(0);
-    QE_TRY(selproj_kernel(ctx, P, out_kind, nout, SP_RESIDENT, &fn, &bpc, rres));
+    QE_TRY(selproj_kernel(ctx, P, out_kind, nout, SP_RESIDENT, &fn, &bpc, rres | (rtiles > rgrid ? 0x100 : 0)));
     hprof(3);
     QE_TRY(jit_launch(ctx, fn, (int)rgrid, P, 1024));
     hprof(4);

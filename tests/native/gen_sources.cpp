@@ -55,14 +55,15 @@ static int emit(const char* dir, const char* name, const qe_column* cols, int nc
     printf("%s\n", path.c_str());
   }
   // register-resident one-pass kernel (SP_RESIDENT) at 40 rows per thread, where the plan takes it
+  // (and its several-rounds form, file suffix _m6)
   const int R = selproj_resident_rows(P, out_kind, nout, 10000000, 256);
-  if (R > 0) {
+  for (int multi = 0; R > 0 && multi < 2; ++multi) {
     std::string src;
-    if (!gen_selproj_resident_source(P, out_kind, nout, R, &src)) {
+    if (!gen_selproj_resident_source(P, out_kind, nout, R | (multi ? 0x100 : 0), &src)) {
       fprintf(stderr, "%s: resident mode not generated\n", name);
       return 1;
     }
-    const std::string path = std::string(dir) + "/" + name + "_m" + std::to_string(SP_RESIDENT) + ".hip";
+    const std::string path = std::string(dir) + "/" + name + "_m" + std::to_string(SP_RESIDENT + multi) + ".hip";
     FILE* f = fopen(path.c_str(), "w");
     if (!f) return 1;
     fwrite(src.data(), 1, src.size(), f);

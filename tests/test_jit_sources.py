@@ -30,14 +30,14 @@ def sources(tmp_path_factory):
 
 def test_all_modes_emitted(sources):
     names = sorted(p.name for p in sources)
-    assert names == sorted([f"{s}_m{m}.hip" for s in ("c2", "nullable") for m in range(5)] + ["c2_m5.hip"] +
+    assert names == sorted([f"{s}_m{m}.hip" for s in ("c2", "nullable") for m in range(5)] + ["c2_m5.hip", "c2_m6.hip"] +
                            [f"{s}_{k}.hip" for s in ("c4", "f64max", "det")
                             for k in ("fused", "spill", "pagg", "pscatter", "pscatter_soa", "pagg_rows",
                                       "pscatter_n32", "pdirect_n32", "pagg_n32", "pagg_unchunked_n32", "spill_n32",
                                       "pagg_soa_n32", "pagg_big_n32")] + ["c4_fused_compact.hip"])
 
 
-@pytest.mark.parametrize("name", ["c2_m0", "c2_m1", "c2_m2", "c2_m3", "c2_m4", "c2_m5", "nullable_m1", "nullable_m3",
+@pytest.mark.parametrize("name", ["c2_m0", "c2_m1", "c2_m2", "c2_m3", "c2_m4", "c2_m5", "c2_m6", "nullable_m1", "nullable_m3",
                                   "nullable_m4", "c4_fused", "c4_spill", "c4_pagg", "f64max_spill",
                                   "f64max_pagg", "det_fused", "det_spill", "det_pagg", "c4_pscatter",
                                   "c4_pscatter_soa", "c4_pagg_rows", "det_pscatter_soa", "f64max_pscatter_soa",
