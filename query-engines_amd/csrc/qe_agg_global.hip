@@ -10,6 +10,8 @@
 // instruction of a wave reads one contiguous KiB. Per-block partials are reduced by a second
 // single-block kernel in fixed order: bit-reproducible run to run.
 // Roofline: HBM read, 8 B/row (+1/8 B validity, +1/8 B mask).
+#include <atomic>
+#include <chrono>
 #include "qe_internal.hpp"
 
 namespace qe {
@@ -274,8 +276,10 @@ __global__ void k_agg_global_unpack(const uint8_t* __restrict__ recs, int n, GPa
 
 // host_out (optional): pinned host memory that also receives the result, so the caller reads it
 // after a stream sync with no device-to-host copy launch.
+// host_flag (optional): set once host_out is written, for a host polling it (release, system scope).
 __global__ void __launch_bounds__(256) k_agg_global_final(GPart* __restrict__ partials, int nparts,
-                                                          GPart* __restrict__ host_out) {
+                                                          GPart* __restrict__ host_out,
+                                                          unsigned long long* __restrict__ host_flag) {
   // Fixed-order reduction: thread t folds partials t, t+256, ...; then a fixed wave/block tree.
   GPart p;
   gpart_init(p);
@@ -289,6 +293,7 @@ __global__ void __launch_bounds__(256) k_agg_global_final(GPart* __restrict__ pa
     for (int w = 1; w < 4; ++w) gpart_merge(b, wp[w]);
     partials[nparts] = b;
     if (host_out) *host_out = b;
+    if (host_flag) __hip_atomic_store(host_flag, 1ull, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
   }
 }
 
@@ -308,7 +313,7 @@ namespace qe {
 
 // The column's partial, reduced on the device into *result (a GPart in scratch).
 static int agg_global_partial(qe_ctx* ctx, const qe_column* col, const qe_column* mask, GPart** result,
-                              GPart* host_out = nullptr) {
+                              GPart* host_out = nullptr, unsigned long long* host_flag = nullptr) {
   QE_CHECK(col, QE_ERR_INVALID_ARG, "null argument");
   QE_CHECK(col->type == QE_TYPE_INT64 || col->type == QE_TYPE_FLOAT64, QE_ERR_UNSUPPORTED,
            "global aggregate over type %d not supported (int64/fp64)", col->type);
@@ -338,7 +343,7 @@ static int agg_global_partial(qe_ctx* ctx, const qe_column* col, const qe_column
     hipLaunchKernelGGL(k_agg_global<false>, dim3((unsigned)blocks), dim3(256), 0, ctx->stream,
                        (const int64_t*)col->values, col->validity, mv, ml, n, parts);
   QE_TRY(launch_check("k_agg_global"));
-  hipLaunchKernelGGL(k_agg_global_final, dim3(1), dim3(256), 0, ctx->stream, parts, (int)blocks, host_out);
+  hipLaunchKernelGGL(k_agg_global_final, dim3(1), dim3(256), 0, ctx->stream, parts, (int)blocks, host_out, host_flag);
   QE_TRY(launch_check("k_agg_global_final"));
   *result = parts + blocks;
   return QE_OK;
@@ -346,12 +351,33 @@ static int agg_global_partial(qe_ctx* ctx, const qe_column* col, const qe_column
 
 // Device GPart -> qe_global_agg (synchronises). `h`: the pinned copy the final kernel wrote (no
 // copy needed), or null.
-static int agg_global_finish(qe_ctx* ctx, const GPart* dp, int32_t type, qe_global_agg* out, void* h = nullptr) {
+// `flag`: the final kernel sets it once h is written; polled instead of synchronising the stream
+// (~6 us sooner per call: tools/exp_sync_latency.hip), with a stream query every 50 us so a failed
+// kernel still ends the wait. The result is then complete; later work on the stream is ordered
+// after the kernel as usual.
+static int agg_global_finish(qe_ctx* ctx, const GPart* dp, int32_t type, qe_global_agg* out, void* h = nullptr,
+                             volatile unsigned long long* flag = nullptr) {
   if (!h) {
     QE_TRY(ctx_pinned(ctx, sizeof(GPart), &h));
     QE_HIP(hipMemcpyAsync(h, dp, sizeof(GPart), hipMemcpyDeviceToHost, ctx->stream));
   }
-  QE_TRY(ctx_sync(ctx));
+  if (flag) {
+    auto t0 = std::chrono::steady_clock::now();
+    for (uint32_t i = 1; *flag == 0; ++i) {
+      if ((i & 1023) != 0 || std::chrono::steady_clock::now() - t0 < std::chrono::microseconds(50)) continue;
+      t0 = std::chrono::steady_clock::now();
+      const hipError_t e = hipStreamQuery(ctx->stream);
+      if (e == hipSuccess) {
+        QE_CHECK(*flag != 0, QE_ERR_DEVICE, "global aggregate finished without publishing its result");
+        break;
+      }
+      if (e != hipErrorNotReady) return fail(QE_ERR_DEVICE, "global aggregate kernel failed: %s", hipGetErrorString(e));
+      (void)hipGetLastError();
+    }
+    std::atomic_thread_fence(std::memory_order_acquire);
+  } else {
+    QE_TRY(ctx_sync(ctx));
+  }
   const GPart p = *(const GPart*)h;
   const bool f64 = type == QE_TYPE_FLOAT64;
   memset(out, 0, sizeof(*out));
@@ -381,10 +407,13 @@ extern "C" int qe_agg_global(qe_ctx* ctx, const qe_column* col, const qe_column*
   QE_TRY(ctx_enter(ctx));
   QE_CHECK(out, QE_ERR_INVALID_ARG, "null argument");
   void* h;
-  QE_TRY(ctx_pinned(ctx, sizeof(GPart), &h));
+  constexpr size_t kFlagOff = (sizeof(GPart) + 63) & ~(size_t)63;
+  QE_TRY(ctx_pinned(ctx, kFlagOff + 64, &h));
+  unsigned long long* flag = (unsigned long long*)((uint8_t*)h + kFlagOff);
+  *(volatile unsigned long long*)flag = 0;  // (the previous call on this ctx has returned: its kernels wrote it)
   GPart* p;
-  QE_TRY(agg_global_partial(ctx, col, mask, &p, (GPart*)h));
-  return agg_global_finish(ctx, p, col->type, out, h);
+  QE_TRY(agg_global_partial(ctx, col, mask, &p, (GPart*)h, flag));
+  return agg_global_finish(ctx, p, col->type, out, h, flag);
 }
 
 extern "C" int qe_agg_global_partial(qe_ctx* ctx, const qe_column* col, const qe_column* mask, int64_t row_base,
@@ -412,7 +441,8 @@ extern "C" int qe_agg_global_merge(qe_ctx* ctx, int32_t type, const void* partia
   // fixed-order fold: the same partials give the same bits on every rank
   void* h;
   QE_TRY(ctx_pinned(ctx, sizeof(GPart), &h));
-  hipLaunchKernelGGL(k_agg_global_final, dim3(1), dim3(256), 0, ctx->stream, parts, (int)n, (GPart*)h);
+  hipLaunchKernelGGL(k_agg_global_final, dim3(1), dim3(256), 0, ctx->stream, parts, (int)n, (GPart*)h,
+                     (unsigned long long*)nullptr);
   QE_TRY(launch_check("k_agg_global_final"));
   return agg_global_finish(ctx, parts + n, type, out, h);
 }

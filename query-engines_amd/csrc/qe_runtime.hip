@@ -271,7 +271,8 @@ int ctx_pinned(qe_ctx* ctx, size_t bytes, void** out) {
     if (ctx->pinned) QE_HIP(hipHostFree(ctx->pinned));
     ctx->pinned = nullptr;
     size_t want = bytes < 4096 ? 4096 : bytes;
-    QE_HIP(hipHostMalloc(&ctx->pinned, want, hipHostMallocDefault));
+    // fine-grained: a kernel's system-scope stores are visible to a polling host (qe_agg_global)
+    QE_HIP(hipHostMalloc(&ctx->pinned, want, hipHostMallocCoherent | hipHostMallocMapped));
     ctx->pinned_bytes = want;
   }
   *out = ctx->pinned;
