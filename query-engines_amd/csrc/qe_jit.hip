@@ -2605,6 +2605,9 @@ bool gen_selproj_resident_source(const Plan& P, const int32_t* out_kind, int nou
     << "    pre += pre_prev;\n    pre_prev = pre;\n"
     << "    stalled_any = stalled_any || __any(stalled);\n"
     << "    if (lane == 0) { s_base = pre; s_total = (qu32)total; }\n"
+    // this workgroup's last tile has its prefix: say so now, not after its stores, so the last tile
+    // can publish the count as soon as every workgroup is past its prefix
+    << "    if (lane == 0 && (qu64)T + G >= ntiles) __hip_atomic_store(&st[bid], tag | (stalled_any ? 1ull : 0ull), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);\n"
     // the last tile publishes the row count once every other workgroup has taken all its tiles'
     // prefixes, with the stall flag first if any gave up waiting (rows misplaced: the host reruns)
     << "    if (T == ntiles - 1) {\n"
@@ -2647,7 +2650,6 @@ bool gen_selproj_resident_source(const Plan& P, const int32_t* out_kind, int nou
     o << "    __syncthreads();\n  }\n";
   }
   o << "  }  // tiles\n"
-    << "  if (t == 0) __hip_atomic_store(&st[bid], tag | (stalled_any ? 1ull : 0ull), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);\n"
     << "}\n";
   *src = std::string(kDevHeader) + o.str();
   return true;
