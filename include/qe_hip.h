@@ -361,9 +361,13 @@ int qe_select_project(qe_ctx* ctx, const qe_column* cols, int32_t ncols, const q
 /* Stream-ordered form (a pipelined SelectionExec -> ProjectionExec over a Sequence<RecordBatch>,
  * K:589-594): queues the kernels and the copy of the row count into pinned memory, and returns
  * without waiting. *pending must be passed to qe_select_pending_wait exactly once (it frees it);
- * that call waits for this select-project's kernels only — not for work queued behind them, such
- * as the next batch's select-project — and returns the row count. The inputs must stay valid and
- * the outputs unread until then. qe_select_project = async + wait. */
+ * that call waits for this select-project's row count only — not for work queued behind it, such
+ * as the next batch's select-project — and returns it. Where the kernel publishes the count itself
+ * (the register-resident pass and the two-pass write kernel) the wait polls that word in pinned
+ * memory and may return while the kernel's last stores drain: the outputs are then complete for
+ * every later operation on ctx's stream (and after a synchronisation of it), as for any
+ * stream-ordered call. The inputs must stay valid until the wait returns.
+ * qe_select_project = async + wait. */
 typedef struct qe_select_pending qe_select_pending;
 int qe_select_project_async(qe_ctx* ctx, const qe_column* cols, int32_t ncols, const qe_select_spec* spec,
                             qe_column* outs, qe_select_pending** pending);
