@@ -2445,6 +2445,15 @@ bool sp_resident_env() {
   }();
   return v;
 }
+// QE_SELPROJ_RESIDENT_TEST_STALL=1 (tests only): the last tile reports a stall, so the host's
+// rerun path runs (tests/test_selproj.py::test_resident_stall_reruns)
+bool sp_resident_test_stall() {
+  static const bool v = [] {
+    const char* e = getenv("QE_SELPROJ_RESIDENT_TEST_STALL");
+    return e && e[0] == '1';
+  }();
+  return v;
+}
 // slots read by the outputs' programs
 unsigned out_cols(const Plan& P, int nout) {
   unsigned m = 0;
@@ -2614,7 +2623,7 @@ bool gen_selproj_resident_source(const Plan& P, const int32_t* out_kind, int nou
     << "      bool bad;\n" << poll_code("st[@]", "@ < G && @ != bid", "bad")
     << "      bad = bad || (lane < G && lane != bid && (v0 & 1)) || (lane + 64 < G && lane + 64 != bid && (v1 & 1)) ||\n"
     << "            (lane + 128 < G && lane + 128 != bid && (v2 & 1)) || (lane + 192 < G && lane + 192 != bid && (v3 & 1));\n"
-    << "      bad = __any(bad) || stalled_any;\n"
+    << "      bad = __any(bad) || stalled_any" << (sp_resident_test_stall() ? " || true" : "") << ";\n"
     << "      if (lane == 0) {\n"
     << "        if (bad) { __hip_atomic_store(&P.t.ctl[2], 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); if (P.host_ctl) __hip_atomic_store(&P.host_ctl[1], 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM); }\n"
     << "        P.t.ctl[1] = pre + total;\n"

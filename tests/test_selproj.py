@@ -128,6 +128,47 @@ print("ok")
 """
 
 
+_STALL_CHILD = """
+import sys
+sys.path[:0] = [sys.argv[1], sys.argv[1] + "/query-engines_amd"]
+import numpy as np
+from kquery import native as N
+from kquery.columnar import Context
+from kquery.datasource import C2_COLUMNS, generate_column
+from oracle import gen
+sys.path.insert(0, sys.argv[1] + "/tests")
+from test_selproj import _spec, _run
+ctx = Context.get(0)
+n, k = 3_000_017, 1 << 19
+cols = [generate_column(s, n, 0, 42, ctx) for s in C2_COLUMNS]
+spec = _spec(N, [(0, N.OP_GT, -1, k)], [[(N.TOK_COL, 0, None), (N.TOK_COL, 1, None), (N.TOK_ADD, 0, None)]])
+a_h, _ = gen.generate(C2_COLUMNS[0].dist, C2_COLUMNS[0].param, 42, C2_COLUMNS[0].col_id, 0, n)
+b_h, _ = gen.generate(C2_COLUMNS[1].dist, C2_COLUMNS[1].param, 42, C2_COLUMNS[1].col_id, 0, n)
+m = a_h > k
+want = (a_h[m].astype(np.uint64) + b_h[m].astype(np.uint64)).astype(np.int64)
+cnt, (ab,) = _run(ctx, cols, spec, [N.TYPE_INT64])
+assert cnt == int(m.sum()) and (ab.to_numpy() == want).all()
+print("ok")
+"""
+
+
+def test_resident_stall_reruns():
+    """A resident-pass call whose last tile reports a stall (forced by a test-only knob, in a child
+    process) is rerun with two passes: bit-exact result and the rerun notice on stderr."""
+    import os
+    import pathlib
+    import subprocess
+    import sys
+
+    root = pathlib.Path(__file__).resolve().parents[1]
+    env = dict(os.environ, QE_SELPROJ_RESIDENT_TEST_STALL="1")
+    env.pop("QE_SELPROJ_TWOPASS", None)
+    r = subprocess.run([sys.executable, "-c", _STALL_CHILD, str(root)], cwd=str(root), env=env,
+                       capture_output=True, text=True, timeout=200)
+    assert r.returncode == 0 and "ok" in r.stdout, r.stderr[-3000:]
+    assert "resident pass stalled; rerunning with two passes" in r.stderr
+
+
 def test_c2_resident_rounds():
     """The resident pass walking several rounds of tiles (QE_SELPROJ_RESIDENT_ROUNDS=1, read once
     per process, so in a child process): 2, 3 and 4 rounds of 32-row-per-thread tiles, two
