@@ -2352,6 +2352,7 @@ static int spill_update(qe_hashagg* h, Plan& P, size_t lds, int64_t rows, bool* 
   Plan Q = P;
   Q.mp_n = 0;
   Q.mp_pass = 0;
+  Q.lds_compact = 0;  // (the spilled records' pass keeps the regular table)
   int tlog2 = 16;
   const size_t pbudget = pagg_block() == 1024 ? (size_t)152 * 1024 : HA_LDS_BUDGET;
   while (tlog2 >= 8 && lds_layout_at(h, &Q, tlog2) > pbudget) --tlog2;
@@ -2385,7 +2386,8 @@ static int spill_update(qe_hashagg* h, Plan& P, size_t lds, int64_t rows, bool* 
   // 7.85, 7/8 6.62 / 10.79
   const char* le = getenv("QE_SPILL_LOAD");
   const int load8 = le && *le ? std::max(4, std::min(7, atoi(le))) : 6;
-  const double keep = std::min(1.0, (double)(((int64_t)1 << P.lds_log2) * load8 / 8) / (double)std::max<int64_t>(1, h->expected_groups));
+  const int64_t kept_cap = P.lds_compact ? (int64_t)P.lds_compact : ((int64_t)1 << P.lds_log2);  // kept table's slots
+  const double keep = std::min(1.0, (double)(kept_cap * load8 / 8) / (double)std::max<int64_t>(1, h->expected_groups));
   P.mp_keep = (qu64)(keep * 4294967296.0);
   P.part_rec = h->part_rec;
   P.part_chunk = meta;
@@ -2439,8 +2441,9 @@ static int spill_update(qe_hashagg* h, Plan& P, size_t lds, int64_t rows, bool* 
     QE_TRY(settle_pass(h, Q, &out_i, &defer_in, &done));
     if (done) break;
   }
-  h->jit_note = "multi-pass: 2 buckets, bucket 1 spilled as " + std::to_string(rb) + " B records (" +
-                (L.colmode ? "column" : "value") + (L.narrow ? " words, 32-bit)" : " words)");
+  h->jit_note = std::string("multi-pass: 2 buckets") + (P.lds_compact ? " (compact kept table)" : "") +
+                ", bucket 1 spilled as " + std::to_string(rb) + " B records (" + (L.colmode ? "column" : "value") +
+                (L.narrow ? " words, 32-bit)" : " words)");
   return QE_OK;
 }
 
@@ -2498,6 +2501,47 @@ static int run_update(qe_hashagg* h, Plan& P) {
         QE_HIP(hipMemsetAsync(h->ctl + 7, 0, 8, ctx->stream));
         P = T;
         lds = jl;
+      }
+    }
+  }
+  // Past the compact table (~5K groups for C4) and up to ~1.5 tables' worth: ONE spilling pass
+  // whose kept share (key hashes below mp_keep, 6/8 of the compact table's slots) stays in the
+  // compact table and whose other rows are written as records for one aggregation pass
+  // (spill_update), instead of the 8-bucket partitioned path (QE_COMPACT_SPILL=0: off).
+  if (!lds && ctx->jit && h->expected_groups > 0 && !h->compact_off && !(ce && ce[0] == '0') && compact_ok(P)) {
+    static const bool cs_env = [] {
+      const char* e = getenv("QE_COMPACT_SPILL");
+      return !(e && e[0] == '0');
+    }();
+    Plan T = P;
+    T.lds_log2 = 16;
+    const size_t bps = compact_slot_bytes(T);
+    const int64_t nsl = ((int64_t)((lds_budget(ctx) - 512 - 256) / bps) - 66) & ~(int64_t)63;  // (+ spill chunk state)
+    if (cs_env && nsl >= 512 && h->expected_groups <= nsl * 3 / 2) {
+      T.lds_compact = (qi32)nsl;
+      T.mp_n = 2;
+      T.mp_pass = 0;
+      std::string src;
+      size_t jl = 0;
+      if (gen_fused_source(T, T.lds_log2, &src, &jl, true)) {
+        const uint64_t need = (uint64_t)ctx->num_cus * 8 * ((uint64_t)nsl + 2);
+        if (h->ovf_cap < need) {
+          dev_free(ctx, h->ovf);
+          h->ovf = nullptr;
+          h->ovf_cap = 0;
+          QE_TRY(dev_alloc(ctx, need * h->rec_bytes, (void**)&h->ovf));
+          h->ovf_cap = need;
+        }
+        T.ovf = h->ovf;
+        T.ovf_cap = h->ovf_cap;
+        QE_HIP(hipMemsetAsync(h->ctl + 7, 0, 8, ctx->stream));
+        bool used = false;
+        QE_TRY(spill_update(h, T, jl, rows, &used));
+        if (used) {
+          h->row_base += rows;
+          adapt_after_update(h, jl, T.lds_log2);
+          return QE_OK;
+        }
       }
     }
   }

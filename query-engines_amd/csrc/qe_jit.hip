@@ -613,7 +613,7 @@ bool gen_fused_source(const Plan& P, int log2, std::string* src, size_t* lds_byt
   if (log2 < 4 || log2 > 16 || P.ncols < 1 || P.ncols > QE_MAX_COLS) return false;
   if (spill && P.mp_n < 2) return false;
   const bool compact = P.lds_compact > 0;
-  if (compact && (spill || !compact_ok(P))) return false;
+  if (compact && !compact_ok(P)) return false;
   std::vector<Expr> ex;
   if (!agg_inputs(P, &ex)) return false;
   std::vector<std::string> val(P.naggs), ok(P.naggs);

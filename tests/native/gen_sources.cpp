@@ -155,12 +155,20 @@ static int emit_agg(const char* dir, const char* name, const qe_column* cols, in
   P.mp_n = 0;
   P.part_narrow = 0;
   P.lds_compact = 6080;
-  std::string m;
+  std::string m, m2;
   if (compact_ok(P)) {
     if (!gen_fused_source(P, log2, &m, &lds, false) || write_src(dir, std::string(name) + "_fused_compact", m)) {
       fprintf(stderr, "%s: compact fused source not generated\n", name);
       return 1;
     }
+    // the spilling pass over a compact kept table (32-bit spill records)
+    P.mp_n = 2;
+    P.part_narrow = 1;
+    if (!gen_fused_source(P, log2, &m2, &lds, true) || write_src(dir, std::string(name) + "_spill_compact", m2)) {
+      fprintf(stderr, "%s: compact spill source not generated\n", name);
+      return 1;
+    }
+    P.mp_n = 0;
   }
   P.lds_compact = 0;
   return write_src(dir, std::string(name) + "_fused", a) | write_src(dir, std::string(name) + "_spill", b) |
