@@ -2517,7 +2517,18 @@ static int run_update(qe_hashagg* h, Plan& P) {
     T.lds_log2 = 16;
     const size_t bps = compact_slot_bytes(T);
     const int64_t nsl = ((int64_t)((lds_budget(ctx) - 512 - 256) / bps) - 66) & ~(int64_t)63;  // (+ spill chunk state)
-    if (cs_env && nsl >= 512 && h->expected_groups <= nsl * 3 / 2) {
+    // the spilled share goes through the regular aggregation table: at most half of it (1B rows:
+    // 5,500 / 6,500 groups 5.95 / 6.59 ms against 8.23 / 8.25 partitioned; 8,192 groups, whose
+    // ~3.4K spilled groups fill 84 % of a 4096-slot table, 11.0 against 8.1 ms)
+    int tl = 16;
+    {
+      Plan Q = T;
+      Q.lds_compact = 0;
+      Q.mp_n = 0;
+      const size_t pbudget = pagg_block() == 1024 ? (size_t)152 * 1024 : HA_LDS_BUDGET;
+      while (tl >= 8 && lds_layout_at(h, &Q, tl) > pbudget) --tl;
+    }
+    if (cs_env && nsl >= 512 && tl >= 8 && h->expected_groups <= nsl * 3 / 4 + ((int64_t)1 << tl) / 2) {
       T.lds_compact = (qi32)nsl;
       T.mp_n = 2;
       T.mp_pass = 0;
