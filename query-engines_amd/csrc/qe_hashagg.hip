@@ -2556,6 +2556,45 @@ static int run_update(qe_hashagg* h, Plan& P) {
       }
     }
   }
+  // Beyond the compact spill (~6.75K–10K groups for C4): two key-hash passes over the columns,
+  // each keeping half the groups in the compact table (QE_COMPACT_SPILL=0 turns this off too).
+  bool no_spill = false;
+  if (!lds && ctx->jit && h->expected_groups > 0 && !h->compact_off && !(ce && ce[0] == '0') && compact_ok(P)) {
+    static const bool c2_env = [] {
+      const char* e = getenv("QE_COMPACT_SPILL");
+      return !(e && e[0] == '0');
+    }();
+    Plan T = P;
+    T.lds_log2 = 16;
+    const size_t bps = compact_slot_bytes(T);
+    const int64_t nsl = ((int64_t)((lds_budget(ctx) - 512) / bps) - 66) & ~(int64_t)63;
+    if (c2_env && nsl >= 512 && h->expected_groups <= nsl * 8 / 5) {
+      T.lds_compact = (qi32)nsl;
+      T.mp_n = 2;
+      T.mp_pass = 0;
+      std::string src;
+      size_t jl = 0;
+      hipFunction_t f = nullptr;
+      int bpc = 0;
+      if (gen_fused_source(T, T.lds_log2, &src, &jl) && jit_kernel(ctx, src, &f, &bpc, "qe_fused", fused_block(16)) == QE_OK) {
+        const uint64_t need = (uint64_t)ctx->num_cus * 8 * ((uint64_t)nsl + 2);
+        if (h->ovf_cap < need) {
+          dev_free(ctx, h->ovf);
+          h->ovf = nullptr;
+          h->ovf_cap = 0;
+          QE_TRY(dev_alloc(ctx, need * h->rec_bytes, (void**)&h->ovf));
+          h->ovf_cap = need;
+        }
+        T.ovf = h->ovf;
+        T.ovf_cap = h->ovf_cap;
+        QE_HIP(hipMemsetAsync(h->ctl + 7, 0, 8, ctx->stream));
+        P = T;
+        lds = jl;
+        mp_n = 2;
+        no_spill = true;
+      }
+    }
+  }
   // The generic kernel (JIT off, or no specialised kernel) passes too, with its own 80 KiB budget:
   // it has no partitioned path to fall back on, and global-only rows cost a device atomic each.
   if (!lds && h->expected_groups > 0) {
@@ -2593,7 +2632,7 @@ static int run_update(qe_hashagg* h, Plan& P) {
       }
     }
   }
-  if (mp_n == 2 && ctx->jit) {
+  if (mp_n == 2 && ctx->jit && !no_spill) {
     bool used = false;
     QE_TRY(spill_update(h, P, lds, rows, &used));
     if (used) {
@@ -2660,7 +2699,8 @@ static int run_update(qe_hashagg* h, Plan& P) {
   break;
   }
   if (mp_n)
-    h->jit_note = "multi-pass: " + std::to_string(mp_n) + " bucket passes" + (h->last_specialized ? "" : "; " + h->jit_note);
+    h->jit_note = "multi-pass: " + std::to_string(mp_n) + " bucket passes" + (P.lds_compact ? " (compact table)" : "") +
+                  (h->last_specialized ? "" : "; " + h->jit_note);
   h->row_base += rows;
   adapt_after_update(h, lds, P.lds_log2);
   return QE_OK;
