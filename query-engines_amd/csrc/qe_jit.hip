@@ -1371,7 +1371,7 @@ static bool gen_pagg_fast_source(const Plan& P, const PartLayout& L, int log2, i
     << "  const bool excl = (hx & PART_EXCL) != 0;\n"
     << "  const qi64 hi = ((hx & ~PART_EXCL) - clo) * PART_CH;\n"
     << "  if (hi <= 0) return;\n"
-    << "  if (P.t.ctl[7]) return;  // a value did not fit the 32-bit records: the update reruns wide\n"
+    << "  if (P.t.ctl[7] & 1) return;  // a value did not fit the 32-bit records: the update reruns wide (bit 1: a compact-table misfit, not ours)\n"
     << "  __shared__ int s_fail;\n  __shared__ qu32 s_newg;\n  if (threadIdx.x == 0) { s_fail = 0; s_newg = 0; }\n"
     << "  constexpr int S = " << S << ", SS = " << SS << ", SINK = SS;\n"
     << "  constexpr qu32 NBK = S / 4;\n"
@@ -1693,7 +1693,7 @@ bool gen_pagg_source(const Plan& P, int log2, std::string* src, size_t* lds_byte
       << "  const bool excl = (hx & PART_EXCL) != 0;\n"
       << "  const qi64 hi = hx & ~PART_EXCL;\n";
   o << "  if (hi <= lo) return;  // (the step prefetch below reads the slice's first record)\n";
-  if (L.narrow) o << "  if (P.t.ctl[7]) return;  // a value did not fit the 32-bit records: the update reruns wide\n";
+  if (L.narrow) o << "  if (P.t.ctl[7] & 1) return;  // a value did not fit the 32-bit records: the update reruns wide (bit 1: a compact-table misfit)\n";
   o << "  __shared__ int s_fail;\n  __shared__ qu32 s_newg;\n  if (threadIdx.x == 0) { s_fail = 0; s_newg = 0; }\n";
   emit_lds_table(P, o, log2, lds_bytes);
   // the records of the wave's next step are loaded into n* registers before this step's LDS work
