@@ -408,7 +408,7 @@ extern "C" int qe_agg_global(qe_ctx* ctx, const qe_column* col, const qe_column*
   QE_CHECK(out, QE_ERR_INVALID_ARG, "null argument");
   void* h;
   constexpr size_t kFlagOff = (sizeof(GPart) + 63) & ~(size_t)63;
-  QE_TRY(ctx_pinned(ctx, kFlagOff + 64, &h));
+  QE_TRY(ctx_pinned_coherent(ctx, kFlagOff + 64, &h));
   unsigned long long* flag = (unsigned long long*)((uint8_t*)h + kFlagOff);
   *(volatile unsigned long long*)flag = 0;  // (the previous call on this ctx has returned: its kernels wrote it)
   GPart* p;

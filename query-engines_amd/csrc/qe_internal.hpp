@@ -21,6 +21,8 @@ struct qe_ctx {
   size_t scratch_bytes = 0;
   void* pinned = nullptr;        // small pinned host buffer for read-backs
   size_t pinned_bytes = 0;
+  void* pinned_fg = nullptr;     // fine-grained pinned words a host polls (ctx_pinned_coherent)
+  size_t pinned_fg_bytes = 0;
   int jit = 1;                   // specialise fused plans with hipRTC (qe_jit.hip)
   void* scan_tmp = nullptr;      // block sums of exclusive_scan_i64 (never aliases `scratch`)
   size_t scan_tmp_bytes = 0;
@@ -63,6 +65,7 @@ void dev_forget_stream(qe_ctx* ctx);
 int dev_release(int device);
 int ctx_scratch(qe_ctx* ctx, size_t bytes, void** out);       // grow-only scratch
 int ctx_pinned(qe_ctx* ctx, size_t bytes, void** out);        // grow-only pinned host
+int ctx_pinned_coherent(qe_ctx* ctx, size_t bytes, void** out);  // grow-only fine-grained pinned host (polled words)
 int pinned_slot_alloc(uint64_t** out);                        // 64 pinned bytes (pooled)
 void pinned_slot_free(uint64_t* p, hipStream_t stream);       // reusable once `stream`'s work is done
 void pinned_slot_free_idle(uint64_t* p);                        // no device access pending: reusable now

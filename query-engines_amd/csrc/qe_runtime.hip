@@ -271,11 +271,25 @@ int ctx_pinned(qe_ctx* ctx, size_t bytes, void** out) {
     if (ctx->pinned) QE_HIP(hipHostFree(ctx->pinned));
     ctx->pinned = nullptr;
     size_t want = bytes < 4096 ? 4096 : bytes;
-    // fine-grained: a kernel's system-scope stores are visible to a polling host (qe_agg_global)
-    QE_HIP(hipHostMalloc(&ctx->pinned, want, hipHostMallocCoherent | hipHostMallocMapped));
+    QE_HIP(hipHostMalloc(&ctx->pinned, want, hipHostMallocDefault));
     ctx->pinned_bytes = want;
   }
   *out = ctx->pinned;
+  return QE_OK;
+}
+
+// Small fine-grained pinned buffer: a kernel's system-scope stores into it are visible to a host
+// polling it while the kernel runs (qe_agg_global's result). Kept apart from ctx_pinned, whose
+// large staging buffers feed DMA copies.
+int ctx_pinned_coherent(qe_ctx* ctx, size_t bytes, void** out) {
+  if (bytes > ctx->pinned_fg_bytes) {
+    if (ctx->pinned_fg) QE_HIP(hipHostFree(ctx->pinned_fg));
+    ctx->pinned_fg = nullptr;
+    const size_t want = bytes < 4096 ? 4096 : bytes;
+    QE_HIP(hipHostMalloc(&ctx->pinned_fg, want, hipHostMallocCoherent | hipHostMallocMapped));
+    ctx->pinned_fg_bytes = want;
+  }
+  *out = ctx->pinned_fg;
   return QE_OK;
 }
 
@@ -522,6 +536,7 @@ int qe_ctx_destroy(qe_ctx* ctx) {
   for (void* w : ctx->ws)
     if (w) (void)hipFree(w);
   if (ctx->pinned) (void)hipHostFree(ctx->pinned);
+  if (ctx->pinned_fg) (void)hipHostFree(ctx->pinned_fg);
   if (ctx->own_stream) (void)hipStreamDestroy(ctx->stream);
   delete ctx;
   return QE_OK;
