@@ -24,7 +24,8 @@ using namespace qe;
 
 namespace {
 
-// QE_HOST_PROFILE=1: per-stage host time of qe_select_project_async, printed at exit (tools only)
+// QE_HOST_PROFILE=1: per-stage host time of qe_select_project_async, printed at exit (tools only;
+// one calling thread: the stage clock is a plain global)
 struct HostProf {
   double sum[8] = {};
   long n = 0;
