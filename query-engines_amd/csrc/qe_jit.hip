@@ -1425,7 +1425,15 @@ static bool gen_pagg_fast_source(const Plan& P, const PartLayout& L, int log2, i
     o << "  qu32 b" << k << "_act;\n  qi64 b" << k << "_pb;\n";
     for (int v = 0; v < W; ++v) o << "  qu32x4 b" << k << "_v" << v << ";\n";
   }
+  // Step order (QE_PAGG_INTERLEAVE=1): wave w takes steps w, w + nwv, ... of the slice's chunk list
+  // (8 per chunk) instead of whole chunks, so a slice of ~150 chunks splits over 16 waves to within
+  // one step rather than one chunk (the chunk list is in LDS, so a step's lookup is cheap either way)
+  static const bool ilv = [] {
+    const char* e = getenv("QE_PAGG_INTERLEAVE");
+    return e && e[0] == '1';
+  }();
   auto NB = [](const std::string& t) {
+    if (ilv) return "((qi64)((wv + (" + t + ") * nwv) >> 3) * PART_CH + (qi64)((wv + (" + t + ") * nwv) & 7) * 256)";
     return "((qi64)(wv + ((" + t + ") >> 3) * nwv) * PART_CH + (qi64)((" + t + ") & 7) * 256)";
   };
   auto load_step = [&](int k, const std::string& nb) {
@@ -1471,8 +1479,11 @@ static bool gen_pagg_fast_source(const Plan& P, const PartLayout& L, int log2, i
   for (int k = 0; k < D; ++k) load_step(k, NB(std::to_string(k)));
   // the wave's steps: 8 per chunk it takes (wv, wv + nwv, ...), a multiple of D, so the unrolled
   // loop has no exit between a buffer's reload and its use
-  o << "  const int nsteps = wv < rch ? (int)((rch - 1 - wv) / nwv + 1) * 8 : 0;\n"
-    << "  for (int t = 0; t < nsteps; t += " << D << ") {\n";
+  if (ilv)
+    o << "  const int nsteps = wv < rch * 8 ? (((int)((rch * 8 - 1 - wv) / nwv) + 1 + " << D - 1 << ") / " << D << ") * " << D << " : 0;\n";
+  else
+    o << "  const int nsteps = wv < rch ? (int)((rch - 1 - wv) / nwv + 1) * 8 : 0;\n";
+  o << "  for (int t = 0; t < nsteps; t += " << D << ") {\n";
   for (int k = 0; k < D; ++k) {
   const std::string B = "b" + std::to_string(k) + "_";
   o << "  {\n"

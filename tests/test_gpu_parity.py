@@ -1001,6 +1001,7 @@ print("ok")
     {"QE_PSCATTER_FAST": "1", "QE_PART_BLK64": "1"},
     {"QE_PAGG_TRANSPOSE": "0"},
     {"QE_PAGG_FAST_DEPTH": "4"},
+    {"QE_PAGG_INTERLEAVE": "1"},
     {"QE_PAGG_FAST": "0"},
 ], ids=lambda d: ",".join(f"{k}={v}" for k, v in d.items()))
 def test_partitioned_layout_knobs(knobs):
