@@ -748,7 +748,7 @@ def test_fused_c4_compact_vs_oracle(agg_ctx, groups):
     st.update_fused(cols, _c4_spec())
     if agg_ctx.kernel_mode == "jit":
         spec, note = st.last_kernel_kind()
-        want = ("compact LDS table" if groups <= 5000 else "multi-pass: 2 buckets (compact kept table)"
+        want = ("compact LDS table" if groups <= 5500 else "multi-pass: 2 buckets (compact kept table)"
                 if groups <= 6500 else "radix-partitioned")
         assert spec and note.startswith(want), note
     kk, aa = st.finalize()
@@ -766,11 +766,11 @@ def test_compact_table_speculation(agg_ctx, case, spill):
     """The compact table speculates that keys and MIN / MAX inputs fit 32 bits. A batch where one
     does not is still exact (those rows go to the global table) and the state's later batches take
     the bucket passes instead; null keys, INT32_MIN keys and nullable inputs keep their semantics.
-    `spill`: 5,600 groups, past the one-pass table: the spilling pass over the compact kept table,
+    `spill`: 6,300 groups, past the one-pass table: the spilling pass over the compact kept table,
     where a wide key or value in the spilled share also makes its 32-bit records misfit."""
     rng = np.random.default_rng(len(case) * 7 + spill)
     # (nullable inputs add a non-null count per aggregate to the slot: fewer slots, fewer groups)
-    n, groups = 400_000, 2600 if case == "nullable" else (5600 if spill else 4200)
+    n, groups = 400_000, 2600 if case == "nullable" else (6300 if spill else 4200)
     k = (rng.integers(0, groups, n).astype(np.int64) - groups // 2) * 1021
     k[::997] = -2**31  # the 32-bit table's empty marker is a real key here
     x = rng.integers(-2**31, 2**31, n).astype(np.int64)
