@@ -2475,7 +2475,7 @@ static int run_update(qe_hashagg* h, Plan& P) {
   size_t lds_mp = 0;
   int mp_n = 0;
   // Groups just past the regular LDS table: one pass with the compact table (qe_jit.hip
-  // compact_*, 32-bit keys, <= 80 % load) when the plan shape and the expected groups allow it
+  // compact_*, 32-bit keys, <= 92 % load) when the plan shape and the expected groups allow it
   // (QE_LDS_COMPACT=0: never; read per call), before key-hash passes / spilling.
   const char* ce = getenv("QE_LDS_COMPACT");
   if (!lds && ctx->jit && h->expected_groups > 0 && !h->compact_off && !(ce && ce[0] == '0') && compact_ok(P)) {

@@ -431,7 +431,7 @@ void emit_flush(const Plan& P, std::ostringstream& o, bool mark_full = false, bo
 // Groups just past the regular table (~2.5K for the C4 shape) used to take two key-hash passes or
 // a spilling pass. A slot of 32-bit key + COUNT(*) + per aggregate a 64-bit SUM or a 32-bit MIN /
 // MAX (bare column inputs) is 24 B for C4 instead of 36, so one 152 KiB table holds ~6.2K slots:
-// up to ~5K groups in one pass at <= 80 % load. The slot count is any number (multiply-shift
+// up to ~5.8K groups in one pass at <= 92 % load. The slot count is any number (multiply-shift
 // slot hash). Speculative like the 32-bit records: a row whose key or 32-bit accumulator input
 // does not fit 32 bits goes to the global table directly (correct, slow) and sets ctl[7] bit 1,
 // after which the state no longer uses the compact table.
