@@ -274,14 +274,23 @@ typedef struct qe_hashagg qe_hashagg;
 
 int qe_hashagg_create(qe_ctx* ctx, int32_t nkeys, const int32_t* key_types, int32_t naggs,
                       const qe_agg_desc* aggs, int64_t expected_groups, qe_hashagg** out);
-/* qe_hashagg_create with options. QE_HASHAGG_DETERMINISTIC: fp64 SUM / AVG accumulate in exact
- * fixed point (32-bit limbs, least significant bit 2^-64, integer adds) instead of fp64 atomics, so
- * their results are bit-identical whatever order rows, workgroups, batches or ranks combine in —
- * as the reference's sequential row loop and ordered partition merge are (K:617-631, K:1314-1325).
- * The sum is exact up to rounding each input to a multiple of 2^-64 and is then rounded once to
- * double; inputs must be finite with |x| < 2^63 (else the update fails with
- * QE_ERR_UNSUPPORTED). Costs three extra LDS words and atomics per fp64 SUM and slot. */
+/* qe_hashagg_create with options.
+ * fp64 SUM / AVG guarantee (within 1e-9 relative of the exact sum). By default they
+ * accumulate exactly, in 256-bit fixed point (least significant bit 2^-128, integer adds: a 192-bit
+ * window per LDS slot for |x| in [2^-44, 2^62), the global table's full words for every other
+ * input), and finalize rounds the exact sum once to double: the result is the correctly rounded
+ * exact sum, bit-identical whatever order rows, workgroups, batches or ranks combine in — what the
+ * reference's sequential row loop and ordered partition merge give with exact arithmetic
+ * (K:617-631, K:1314-1325). NaN / +-Inf inputs give NaN / the infinity, as IEEE addition does.
+ * finalize fails with QE_ERR_UNSUPPORTED instead of returning a group's sum when that group had
+ * an input of magnitude 2^126 or more, or inputs with bits below 2^-128 whose rounding (half a
+ * unit each) could exceed 1e-9 of the result. A state with exact sums synchronises in finalize to
+ * check that (the outputs are complete when it returns).
+ * QE_HASHAGG_DETERMINISTIC: the default (kept for callers that name it).
+ * QE_HASHAGG_FAST_FP64: plain fp64 atomics instead (one LDS atomic per row and aggregate); their
+ * rounding depends on arrival order, and a group whose terms cancel can miss the 1e-9 contract. */
 #define QE_HASHAGG_DETERMINISTIC 1
+#define QE_HASHAGG_FAST_FP64 2
 int qe_hashagg_create_ex(qe_ctx* ctx, int32_t nkeys, const int32_t* key_types, int32_t naggs,
                          const qe_agg_desc* aggs, int64_t expected_groups, int32_t flags, qe_hashagg** out);
 int qe_hashagg_destroy(qe_hashagg* agg);

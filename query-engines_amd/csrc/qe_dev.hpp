@@ -193,124 +193,245 @@ __host__ __device__ inline bool acc_has_idx(int acc) { return acc_is_f64mm(acc) 
 __host__ __device__ inline qu64 idx_identity(int acc) { return acc_is_f64mm(acc) ? ~0ull : 0ull; }
 
 // ---- exact fixed-point fp64 sums (ACC_SUM_X) ---------------------------------------------------------
-// value = sum_k limb_k * 2^(32k - FX_LSB), k = 0..3, limbs int64 (two's complement sums of 32-bit
-// chunks; limb 3 carries the sign). Limb 0 lives in the slot's acc word, limbs 1..3 in idx words
-// 0..2, and idx word 3 is the slot's status word (FX_* below): how many inputs were rounded, how
-// many could not be represented at all (NaN, +-Inf, |x| >= 2^63) and the net number of times limb 3
-// wrapped. A row adds the chunks of its exactly scaled value; a value with bits below 2^-64 is
-// rounded to the nearest multiple of 2^-64 (ties to even) and counted as inexact. Integer adds are
-// associative, so any combine order gives the same limbs and the same status word: deterministic.
-// The result is the correctly rounded exact sum when no input was rounded; otherwise it is off by
-// at most inexact x 2^-65, and finalize reports an error when that bound exceeds 1e-9 of the
-// result (FX_REL_TOL). Unrepresentable inputs fail the update (ctl[6]); a limb-3 wrap that does
-// not cancel (|sum| >= 2^95) fails finalize.
-constexpr qu64 FX_BAD = 1ull << 48;          // status: one unrepresentable input
-constexpr qu64 FX_WRAP = 1ull << 56;         // status: one net wrap of limb 3 (signed)
-constexpr qu64 FX_INEXACT_MASK = FX_BAD - 1;  // status bits 0..47: inputs rounded to 2^-64 units
+// A slot's fp64 SUM is a 256-bit two's complement integer W in units of 2^-128 (sum = W * 2^-128):
+// four 64-bit words w0..w3, w3 the signed top, plus a status word. Words live in acc (w0) and idx
+// words 0..2 (w1..w3); idx word 3 is the status:
+//   bits 0..7   flags, OR-ed: a NaN input, a +Inf input, a -Inf input, an input with |x| >= 2^126,
+//               an input with bits below 2^-128 (rounded to the nearest multiple, ties to even)
+//   bits 8..63  signed count of net wraps of W: the exact sum is (W + wraps * 2^256) * 2^-128
+// A row adds its value's (at most 117-bit) two's complement image to the two words its mantissa
+// spans, with integer atomics that return the old word; only a carry out of the second word or a
+// change of the running sum's sign moves on to the next word. Integer adds are associative, so any
+// order of rows, workgroups, passes, batches or ranks gives the same words: the result is the
+// correctly rounded exact sum, bit-identical run to run. NaN / +-Inf inputs give the IEEE result
+// of the sum (NaN, or the infinity); an input of 2^126 or more, or rounded inputs whose error bound
+// (non-null count x 2^-129) exceeds FX_REL_TOL of the result, make finalize fail (qe_hashagg.hip).
+constexpr qu64 FX_NAN = 1, FX_PINF = 2, FX_NINF = 4, FX_HUGE = 8, FX_INEXACT = 16, FX_FLAGS = 0xFF;
+constexpr qu64 FX_WRAP = 1ull << 8;  // one net wrap of W (signed count in bits 8..63)
 constexpr double FX_REL_TOL = 1e-9;
-constexpr int FX_LSB = 64;
-__host__ __device__ inline int fx_clz64(qu64 x) {
-  int n = 0;
-  for (int b = 32; b; b >>= 1)
-    if (!(x >> (64 - b))) {
-      n += b;
-      x <<= b;
-    }
-  return x ? n : 64;
-}
+constexpr int FX_LSB = 128;
 
-// Chunks of one value: c[0..3] limbs, c[4] = the status word's share: FX_BAD if out of range (then
-// the limbs are 0), 1 if the value was rounded, else 0.
-__host__ __device__ inline void fx_split(qi64 bits, qi64 c[5]) {
-  c[0] = c[1] = c[2] = c[3] = c[4] = 0;
+// One input's image: (hi:lo) two's complement at words k, k+1 (k < 0: nothing to add), sign
+// extended above; st = its status flags.
+struct FxRow {
+  qu64 lo, hi, st;
+  int k;
+  bool neg;
+};
+__host__ __device__ inline FxRow fx_row(qi64 bits) {
+  FxRow r{0ull, 0ull, 0ull, -1, false};
   const qu64 b = (qu64)bits;
-  const bool neg = b >> 63;
+  r.neg = b >> 63;
   const int ex = (int)((b >> 52) & 0x7FF);
   qu64 m = b & ((1ull << 52) - 1);
   if (ex == 0x7FF) {
-    c[4] = (qi64)FX_BAD;
-    return;
+    r.st = m ? FX_NAN : (r.neg ? FX_NINF : FX_PINF);
+    return r;
   }
-  int e = -1074;
+  int p = -1074 + FX_LSB;  // bit position of m's lowest bit in W
   if (ex) {
     m |= 1ull << 52;
-    e = ex - 1075;
+    p = ex - 1075 + FX_LSB;
   }
-  if (m == 0) return;
-  int p = e + FX_LSB;  // bit position of m's lowest bit in the fixed-point number
-  if (p < 0) {
+  if (m == 0) return r;
+  if (p < 0) {  // bits below 2^-128: round to the nearest multiple, ties to even
     const int sh = -p;
-    c[4] = 1;  // bits below 2^-64 (m != 0): rounded, unless every dropped bit is zero (below)
-    if (sh > 54) return;  // m < 2^53 <= half of 2^sh: rounds to 0
+    r.st = FX_INEXACT;
+    if (sh > 54) return r;  // m < 2^53 < half a unit: 0
     const qu64 q = m >> sh, rem = m & ((1ull << sh) - 1), half = 1ull << (sh - 1);
-    if (rem == 0) c[4] = 0;
+    if (rem == 0) r.st = 0;
     m = q + ((rem > half || (rem == half && (q & 1))) ? 1 : 0);
     p = 0;
-    if (m == 0) return;
+    if (m == 0) return r;
   }
-  if (p + (64 - fx_clz64(m)) > 127) {  // |x| >= 2^63
-    c[4] = (qi64)FX_BAD;
-    return;
+  if (p + 64 - __builtin_clzll(m) > 254) {  // |x| >= 2^126: beyond the words' headroom
+    r.st |= FX_HUGE;
+    return r;
   }
-  const int L = p >> 5, q = p & 31;
-  const qu64 lo = m << q, hi = q ? (m >> (64 - q)) : 0ull;
-  const qi64 ch[3] = {(qi64)(lo & 0xFFFFFFFFull), (qi64)(lo >> 32), (qi64)hi};
-  for (int k = 0; k < 3; ++k)
-    if (L + k < 4) c[L + k] = neg ? -ch[k] : ch[k];
+  r.k = p >> 6;
+  const int q = p & 63;
+  qu64 lo = m << q, hi = q ? (m >> (64 - q)) : 0ull;
+  if (r.neg) {
+    lo = 0ull - lo;
+    hi = ~hi + (lo == 0 ? 1ull : 0ull);
+  }
+  r.lo = lo;
+  r.hi = hi;
+  return r;
 }
 
-// Status-word delta when limb 3 goes from `old` to old + add (two's complement): +-FX_WRAP on a
-// signed overflow. Net wraps cancel exactly when the true limb-3 sum is back in range.
+// Status-word delta when the top word goes from `old` to old + add (signed): +-FX_WRAP on an
+// overflow. Net wraps cancel exactly when the true sum is back in range.
 __host__ __device__ inline qu64 fx_wrap(qu64 old, qu64 add) {
   const qi64 o = (qi64)old, a = (qi64)add, n = (qi64)(old + add);
   if (((o ^ n) & (a ^ n)) >= 0) return 0;
   return n < 0 ? FX_WRAP : (qu64)0 - FX_WRAP;
 }
 
-// Unrepresentable inputs recorded in a status word (what an update reports through ctl[6]).
-__host__ __device__ inline qu64 fx_bad_count(qu64 status) { return (status >> 48) & 0xFF; }
-
-// Carry-propagate so limbs 0..2 are in [0, 2^32) and limb 3 holds the rest (signed).
-__host__ __device__ inline void fx_norm(qi64& l0, qi64& l1, qi64& l2, qi64& l3) {
-  qi64 c = l0 >> 32;
-  l0 -= c * 4294967296ll;
-  l1 += c;
-  c = l1 >> 32;
-  l1 -= c * 4294967296ll;
-  l2 += c;
-  c = l2 >> 32;
-  l2 -= c * 4294967296ll;
-  l3 += c;
+// Word add that returns the old word: an LDS / device-scope atomic, or a plain read-modify-write
+// for a slot the caller owns alone (also the host build of the CPU algorithm test,
+// tests/native/fx_host.hip, which instantiates only the plain form).
+template <bool ATOMIC>
+__host__ __device__ inline qu64 fx_xadd(qu64* p, qu64 v) {
+  if constexpr (ATOMIC) {
+    return atomicAdd(p, v);
+  } else {
+    const qu64 o = *p;
+    *p = o + v;
+    return o;
+  }
+}
+template <bool ATOMIC>
+__host__ __device__ inline void fx_status(qu64* st, qu64 v) {
+  if (!v) return;
+  if constexpr (ATOMIC) {
+    if (v & FX_FLAGS) atomicOr(st, v & FX_FLAGS);
+    if (v & ~FX_FLAGS) atomicAdd(st, v & ~FX_FLAGS);
+  } else {
+    *st = ((*st & ~FX_FLAGS) + (v & ~FX_FLAGS)) | ((*st | v) & FX_FLAGS);
+  }
 }
 
-// Correctly rounded double of the limbs (ties to even).
-__host__ __device__ inline double fx_to_double(qi64 l0, qi64 l1, qi64 l2, qi64 l3) {
-  fx_norm(l0, l1, l2, l3);
-  // 32-bit words of the 160-bit two's complement value (limb 3 split in two)
-  qu64 w[5] = {(qu64)l0, (qu64)l1, (qu64)l2, (qu64)l3 & 0xFFFFFFFFull, ((qu64)l3 >> 32) & 0xFFFFFFFFull};
-  const bool neg = l3 < 0;
+// One row into a slot whose word w is at wp(w).
+template <bool ATOMIC, class WP>
+__host__ __device__ inline void fx_add_row(WP wp, const FxRow& r, qu64* st) {
+  qu64 sd = r.st;
+  if (r.k >= 0) {
+    int w = r.k;
+    qu64 old = fx_xadd<ATOMIC>(wp(w), r.lo);
+    if (w == 3) {
+      sd += fx_wrap(old, r.lo);
+    } else {
+      const qu64 t = r.hi + (old + r.lo < old ? 1ull : 0ull);
+      ++w;
+      old = fx_xadd<ATOMIC>(wp(w), t);
+      if (w == 3) {
+        sd += fx_wrap(old, t);
+      } else {
+        // carry out of word w and the image's sign extension: -1, 0 or +1 for the next word
+        qi64 d = (qi64)((t < r.hi ? 1 : 0) + (old + t < old ? 1 : 0)) - (r.neg ? 1 : 0);
+#pragma unroll 1
+        while (d != 0 && ++w <= 3) {
+          old = fx_xadd<ATOMIC>(wp(w), (qu64)d);
+          if (w == 3) {
+            sd += fx_wrap(old, (qu64)d);
+            break;
+          }
+          d = d > 0 ? (old == ~0ull ? 1 : 0) : (old != 0 ? 0 : -1);
+        }
+      }
+    }
+  }
+  fx_status<ATOMIC>(st, sd);
+}
+
+// A whole partial (words v0..v3, status vst) into a slot.
+template <bool ATOMIC, class WP>
+__host__ __device__ inline void fx_add_words(WP wp, qu64 v0, qu64 v1, qu64 v2, qu64 v3, qu64 vst, qu64* st) {
+  const qu64 v[3] = {v0, v1, v2};
+  qu64 c = 0;
+#pragma unroll
+  for (int w = 0; w < 3; ++w) {
+    const qu64 t = v[w] + c;
+    qu64 cb = 0;
+    if (t) {
+      const qu64 old = fx_xadd<ATOMIC>(wp(w), t);
+      cb = old + t < old ? 1ull : 0ull;
+    }
+    c = (t < v[w] ? 1ull : 0ull) + cb;
+  }
+  qu64 sd = vst;
+  if (c && v3 == 0x7FFFFFFFFFFFFFFFull) sd += FX_WRAP;  // v3 + 1 = 2^63: -2^63 and one wrap
+  const qu64 t = v3 + c;
+  if (t) sd += fx_wrap(fx_xadd<ATOMIC>(wp(3), t), t);
+  fx_status<ATOMIC>(st, sd);
+}
+
+// ---- the per-workgroup LDS window of an exact fp64 SUM (plan-specialised kernels) -------------------
+// 192-bit two's complement in units of 2^-96: words u0 (2^-96), u1 (2^-32) and u2 (2^32, the signed
+// top), 24 bytes per LDS slot instead of the global slot's 40. A row whose value is +-0 or has
+// |x| in [2^-44, 2^62) (exponent field 979..1084) adds here exactly: its mantissa lies inside the
+// window, and a workgroup's partial stays below 2^62 x 2^31 rows = 2^93, so the top word never
+// overflows and needs no status. Every other row (NaN, +-Inf, subnormal, tinier or larger values:
+// fx_rare) goes to the global table's full accumulator like a row whose group has no LDS slot.
+constexpr int FXW_LSB = 96;
+constexpr int FXW_EX_LO = 979, FXW_EX_HI = 1085;  // exponent fields [2^-44, 2^62)
+__host__ __device__ inline bool fx_rare(qi64 bits) {
+  const qu32 ex = (qu32)((qu64)bits >> 52) & 0x7FFu;
+  return (ex - (qu32)FXW_EX_LO) >= (qu32)(FXW_EX_HI - FXW_EX_LO) && ((qu64)bits << 1) != 0;
+}
+
+// One row (!fx_rare) into a window whose word w is at wp(w): two LDS atomics that return the old
+// word (the carry out of the first feeds the second); a third, rare, when the carry out of u1 and
+// the row's sign extension do not cancel (the running sum changed sign).
+template <bool ATOMIC = true, class WP>
+__host__ __device__ inline void fxw_add(WP wp, qi64 bits) {
+  const qu64 b = (qu64)bits;
+  const int ex = (int)((b >> 52) & 0x7FF);
+  if (ex == 0) return;  // +-0 (a subnormal is an fx_rare row)
+  const qu64 m = (b & ((1ull << 52) - 1)) | (1ull << 52);
+  const int p = ex - FXW_EX_LO, k = p >> 6, q = p & 63;
+  qu64 lo = m << q, hi = q ? (m >> (64 - q)) : 0ull;
+  const bool neg = b >> 63;
+  if (neg) {
+    lo = 0ull - lo;
+    hi = ~hi + (lo == 0 ? 1ull : 0ull);
+  }
+  const qu64 o0 = fx_xadd<ATOMIC>(wp(k), lo);
+  const qu64 t = hi + (o0 + lo < o0 ? 1ull : 0ull);
+  const qu64 o1 = fx_xadd<ATOMIC>(wp(k + 1), t);  // k == 1: the top word, whose carry out is dropped
+  if (k == 0) {
+    const qi64 d = (qi64)((t < hi ? 1 : 0) + (o1 + t < o1 ? 1 : 0)) - (neg ? 1 : 0);
+    if (d) fx_xadd<ATOMIC>(wp(2), (qu64)d);
+  }
+}
+
+// A window as a partial of the global accumulator (units 2^-128: shifted up 32 bits): v[0..3].
+__host__ __device__ inline void fxw_words(qu64 u0, qu64 u1, qu64 u2, qu64 v[4]) {
+  v[0] = u0 << 32;
+  v[1] = (u0 >> 32) | (u1 << 32);
+  v[2] = (u1 >> 32) | (u2 << 32);
+  v[3] = (qu64)((qi64)u2 >> 32);
+}
+
+// The words of one input alone (RowVal form: the global-table and record paths).
+__host__ __device__ inline void fx_row_words(qi64 bits, qu64 w[5]) {
+  const FxRow r = fx_row(bits);
+  for (int i = 0; i < 4; ++i) w[i] = (r.k >= 0 && i > r.k + 1 && r.neg) ? ~0ull : 0ull;
+  if (r.k >= 0) {
+    w[r.k] = r.lo;
+    if (r.k < 3) w[r.k + 1] = r.hi;
+  }
+  w[4] = r.st;
+}
+
+// Correctly rounded double of (w0..w3 + wraps * 2^256) * 2^-128 (ties to even).
+__host__ __device__ inline double fx_to_double(qu64 w0, qu64 w1, qu64 w2, qu64 w3, qi64 wraps) {
+  qu64 w[5] = {w0, w1, w2, w3, (qu64)(wraps + ((qi64)w3 >> 63))};
+  const bool neg = (qi64)w[4] < 0;
   if (neg) {  // magnitude: invert and add one
     qu64 carry = 1;
     for (int k = 0; k < 5; ++k) {
-      const qu64 v = ((~w[k]) & 0xFFFFFFFFull) + carry;
-      w[k] = v & 0xFFFFFFFFull;
-      carry = v >> 32;
+      w[k] = ~w[k] + carry;
+      carry = (carry && w[k] == 0) ? 1ull : 0ull;
     }
   }
   int top = 4;
   while (top >= 0 && w[top] == 0) --top;
   if (top < 0) return 0.0;
-  // the top 64 bits below and including the leading one, plus a sticky bit for the rest
-  const int lz = fx_clz64(w[top]) - 32;  // leading zeros within the 32-bit word
-  const int msb = 32 * top + 31 - lz;    // bit index of the leading one
-  qu64 win = 0;
+  const int msb = 64 * top + 63 - __builtin_clzll(w[top]);
+  // the 64 bits ending at the leading one, plus a sticky bit for the rest
+  qu64 win;
   bool sticky = false;
-  for (int bit = 0; bit < 64; ++bit) {
-    const int i = msb - bit;
-    if (i < 0) break;
-    win |= ((w[i >> 5] >> (i & 31)) & 1ull) << (63 - bit);
+  const int lowpos = msb - 63;
+  if (lowpos <= 0) {
+    win = w[0] << (-lowpos);
+  } else {
+    const int a = lowpos >> 6, sh = lowpos & 63;
+    win = sh ? ((w[a] >> sh) | (w[a + 1] << (64 - sh))) : w[a];
+    sticky = sh && (w[a] & ((1ull << sh) - 1)) != 0;
+    for (int i = 0; i < a && !sticky; ++i) sticky = w[i] != 0;
   }
-  for (int i = msb - 64; i >= 0 && !sticky; --i) sticky = (w[i >> 5] >> (i & 31)) & 1ull;
   qu64 mant = win >> 11;  // 53 bits
   const qu64 rem = win & 0x7FFull;
   if (rem > 0x400 || (rem == 0x400 && (sticky || (mant & 1)))) ++mant;
@@ -319,9 +440,30 @@ __host__ __device__ inline double fx_to_double(qi64 l0, qi64 l1, qi64 l2, qi64 l
     mant >>= 1;
     ++ex;
   }
-  // exact scaling by 2^ex: msb < 160, so -117 <= ex <= 44, a normal power of two
+  // exact scaling by 2^ex: msb < 320, so -180 <= ex <= 140, a normal power of two
   const double d = (double)mant * bits_f64((qi64)((qu64)(1023 + ex) << 52));
   return neg ? -d : d;
+}
+
+// The SUM of a slot (`nn` non-null inputs). *err: the sum cannot be given within FX_REL_TOL of the
+// exact one (an input >= 2^126, or more rounding than the result's size allows).
+__host__ __device__ inline double fx_result(qu64 w0, qu64 w1, qu64 w2, qu64 w3, qu64 st, qu64 nn, bool* err) {
+  *err = false;
+  const qu64 f = st & FX_FLAGS;
+  if ((f & FX_NAN) || ((f & FX_PINF) && (f & FX_NINF))) return bits_f64(0x7FF8000000000000ll);
+  if (f & FX_PINF) return bits_f64(0x7FF0000000000000ll);
+  if (f & FX_NINF) return bits_f64((qi64)0xFFF0000000000000ull);
+  if (f & FX_HUGE) {
+    *err = true;
+    return bits_f64(0x7FF8000000000000ll);
+  }
+  const double v = fx_to_double(w0, w1, w2, w3, (qi64)st >> 8);
+  // every rounded input is off by at most half a unit (2^-129)
+  if ((f & FX_INEXACT) && (double)nn * 0x1p-129 > FX_REL_TOL * (v < 0 ? -v : v)) {
+    *err = true;
+    return bits_f64(0x7FF8000000000000ll);
+  }
+  return v;
 }
 __host__ __device__ inline qi64 acc_identity(int acc) {
   switch (acc) {
@@ -413,18 +555,17 @@ __device__ inline void gadd_cstar(const DTable& t, qu64 slot, qu64 c) {
 // Combine one aggregate's partial state into global slot `s` (device-scope atomics). add_nn =
 // false while the table keeps the aggregate's non-null count implicit (every input row so far was
 // non-null: nn == COUNT(*), read from cstar; see qe_hashagg.hip nn_implicit).
+// An exact fp64 SUM partial may carry words with nn == 0: a rare input whose row was counted in an
+// LDS slot (fx_rare_global).
 __device__ inline void gcombine(const DTable& t, int acck, int j, qu64 s, qi64 acc, qu64 nn, qu64 i0, qu64 i1,
                                 qu64 i2, qu64 i3, bool add_nn = true) {
-  if (nn == 0) return;
-  if (add_nn) atomicAdd(&t.nn[j][s], nn);
+  if (nn == 0 && acck != ACC_SUM_X) return;
+  if (add_nn && nn) atomicAdd(&t.nn[j][s], nn);
   switch (acck) {
     case ACC_SUM_I:
       if (acc) atomicAdd((qu64*)&t.acc[j][s], (qu64)acc);
       break;
     case ACC_SUM_F: atomicAdd((double*)&t.acc[j][s], bits_f64(acc)); break;
-    case ACC_SUM_X:
-      if (acc) atomicAdd((qu64*)&t.acc[j][s], (qu64)acc);
-      break;
     case ACC_MIN_I:
     case ACC_MIN_F:
       if (acc != 0x7FFFFFFFFFFFFFFFll) atomicMin(&t.acc[j][s], acc);
@@ -442,16 +583,11 @@ __device__ inline void gcombine(const DTable& t, int acck, int j, qu64 s, qi64 a
     if (i1 != ~0ull) atomicMin(&ix[stride + s], i1);
     if (i2 != ~0ull) atomicMin(&ix[2 * stride + s], i2);
     if (i3 != ~0ull) atomicMin(&ix[3 * stride + s], i3);
-  } else if (acck == ACC_SUM_X) {  // upper limbs and the out-of-range count: plain integer adds
+  } else if (acck == ACC_SUM_X) {  // 256-bit add with carries (words: acc, idx 0..2; status idx 3)
     const qu64 stride = t.cap + 2;
     qu64* ix = t.idx[j];
-    if (i0) atomicAdd(&ix[s], i0);
-    if (i1) atomicAdd(&ix[stride + s], i1);
-    if (i2) i3 += fx_wrap(atomicAdd(&ix[2 * stride + s], i2), i2);
-    if (i3) {  // status: rounded / unrepresentable inputs (the update reports the latter, ctl[6]), wraps
-      atomicAdd(&ix[3 * stride + s], i3);
-      if (fx_bad_count(i3)) atomicAdd(&t.ctl[6], fx_bad_count(i3));
-    }
+    fx_add_words<true>([&](int w) { return w == 0 ? (qu64*)&t.acc[j][s] : &ix[(w - 1) * stride + s]; }, (qu64)acc,
+                       i0, i1, i2, i3, &ix[3 * stride + s]);
   }
 }
 
@@ -467,13 +603,12 @@ __device__ inline void gadd_cstar_excl(const DTable& t, qu64 slot, qu64 c, qu32*
 
 __device__ inline void gcombine_excl(const DTable& t, int acck, int j, qu64 s, qi64 acc, qu64 nn, qu64 i0,
                                      qu64 i1, qu64 i2, qu64 i3) {
-  if (nn == 0) return;
+  if (nn == 0 && acck != ACC_SUM_X) return;
   t.nn[j][s] += nn;
   qi64* a = &t.acc[j][s];
   switch (acck) {
     case ACC_SUM_I: *a = (qi64)((qu64)*a + (qu64)acc); break;
     case ACC_SUM_F: *a = f64_bits(bits_f64(*a) + bits_f64(acc)); break;
-    case ACC_SUM_X: *a = (qi64)((qu64)*a + (qu64)acc); break;
     case ACC_MIN_I:
     case ACC_MIN_F:
       if (acc < *a) *a = acc;
@@ -494,12 +629,8 @@ __device__ inline void gcombine_excl(const DTable& t, int acck, int j, qu64 s, q
   } else if (acck == ACC_SUM_X) {
     const qu64 stride = t.cap + 2;
     qu64* ix = t.idx[j] + s;
-    ix[0] += i0;
-    ix[stride] += i1;
-    i3 += fx_wrap(ix[2 * stride], i2);
-    ix[2 * stride] += i2;
-    ix[3 * stride] += i3;
-    if (fx_bad_count(i3)) atomicAdd(&t.ctl[6], fx_bad_count(i3));  // as gcombine: the update fails
+    fx_add_words<false>([&](int w) { return w == 0 ? (qu64*)a : &ix[(w - 1) * stride]; }, (qu64)acc, i0, i1, i2, i3,
+                        &ix[3 * stride]);
   }
 }
 
@@ -517,13 +648,13 @@ __device__ inline RowVal row_partial(int acck, qi64 x, qu64 row) {
     case ACC_MIN_I:
     case ACC_MAX_I: r.acc = x; break;
     case ACC_SUM_X: {
-      qi64 c[5];
-      fx_split(x, c);
-      r.acc = c[0];
-      r.i0 = (qu64)c[1];
-      r.i1 = (qu64)c[2];
-      r.i2 = (qu64)c[3];
-      r.i3 = (qu64)c[4];
+      qu64 w[5];
+      fx_row_words(x, w);
+      r.acc = (qi64)w[0];
+      r.i0 = w[1];
+      r.i1 = w[2];
+      r.i2 = w[3];
+      r.i3 = w[4];
       break;
     }
     case ACC_MIN_F:
@@ -550,6 +681,38 @@ __device__ inline void write_record_head(qu8* rec, qi64 key, bool knull, qu64 cs
   ((qi64*)rec)[0] = key;
   ((qu64*)rec)[1] = knull ? 1ull : 0ull;
   ((qu64*)rec)[2] = cstar;
+}
+
+// A queued exact-SUM input of aggregate j outside the LDS window (fx_rare; the specialised fused
+// kernel's fx queue): straight into its group's global slot — the row's COUNT(*) and non-null
+// count stay in the LDS slot, which the flush merges later — or, while the global table has no room
+// for the group, as an overflow record (COUNT(*) 0, identity partials but j) merged after the table
+// grows, like the flush's own records.
+__device__ inline void fx_rare_global(const Plan& P, int j, qi64 key, bool knull, qi64 x) {
+  qu64 w[5];
+  fx_row_words(x, w);
+  qu64 gs;
+  if (gtable_find(P.t, key, knull, gs)) {
+    gcombine(P.t, ACC_SUM_X, j, gs, (qi64)w[0], 0, w[1], w[2], w[3], w[4], false);
+    return;
+  }
+  const qu64 ri = atomicAdd(&P.t.ctl[2], 1ull);
+  if (ri >= P.ovf_cap) {
+    atomicAdd(&P.t.ctl[3], 1ull);
+    return;
+  }
+  qu8* rec = P.ovf + ri * (qu64)P.rec_bytes;
+  write_record_head(rec, key, knull, 0);
+  int off = 24;
+  for (int a = 0; a < P.naggs; ++a) {
+    qu64* f = (qu64*)(rec + off);
+    const int acc = P.aggs[a].acc;
+    f[0] = a == j ? w[0] : (qu64)acc_identity(acc);
+    f[1] = 0;
+    if (acc_has_idx(acc))
+      for (int i = 0; i < 4; ++i) f[2 + i] = a == j ? w[1 + i] : idx_identity(acc);
+    off += agg_rec_bytes(acc);
+  }
 }
 
 // ---- LDS table helpers ----------------------------------------------------------------------------------
@@ -700,20 +863,17 @@ __device__ inline int lds_probe32n(qi32* keys, qu32 nsl, qi32 key, qu32 h) {
   return -1;
 }
 
-// ACC_SUM_X row into LDS limbs (acc[s] = limb 0, idx[k * SS + s] = limb k + 1, idx[3 SS + s] =
-// status word). Returns false for an out-of-range input (the flush reports it through ctl[6]).
-__device__ inline bool lds_fx_add(qi64* acc, qu64* idx, int SS, int s, qi64 x) {
-  qi64 c[5];
-  fx_split(x, c);
-  if (c[0]) atomicAdd((qu64*)&acc[s], (qu64)c[0]);
-  if (c[1]) atomicAdd(&idx[s], (qu64)c[1]);
-  if (c[2]) atomicAdd(&idx[SS + s], (qu64)c[2]);
-  if (c[3]) atomicAdd(&idx[2 * SS + s], (qu64)c[3]);
-  if (c[4]) {
-    atomicAdd(&idx[3 * SS + s], (qu64)c[4]);
-    return (qu64)c[4] < FX_BAD;
-  }
-  return true;
+// ACC_SUM_X row into an LDS window (acc[s] = u0, idx[s] = u1, idx[SS + s] = u2): plan-specialised
+// kernels, rows that are not fx_rare.
+__device__ inline void lds_fxw_add(qi64* acc, qu64* idx, int SS, int s, qi64 x) {
+  fxw_add([&](int w) { return w == 0 ? (qu64*)&acc[s] : &idx[(w - 1) * SS + s]; }, x);
+}
+
+// ACC_SUM_X row into a full LDS slot (acc[s] = word 0, idx[k * SS + s] = word k + 1, idx[3 SS + s] =
+// status word).
+__device__ inline void lds_fx_add(qi64* acc, qu64* idx, int SS, int s, qi64 x) {
+  const FxRow r = fx_row(x);
+  fx_add_row<true>([&](int w) { return w == 0 ? (qu64*)&acc[s] : &idx[(w - 1) * SS + s]; }, r, &idx[3 * SS + s]);
 }
 
 // fp64 MIN/MAX row into LDS accumulators (MaxAccumulator order semantics, Main.kt:538-561).

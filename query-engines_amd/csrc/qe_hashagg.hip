@@ -83,9 +83,7 @@ __device__ __forceinline__ void lds_accum_value(const Plan& P, char* smem, int j
   switch (a.acc) {
     case ACC_SUM_I: atomicAdd((unsigned long long*)&acc[s], (unsigned long long)x); break;
     case ACC_SUM_F: atomicAdd((double*)&acc[s], bits_f64(x)); break;
-    case ACC_SUM_X:  // (an out-of-range input is counted in the slot; the flush reports it)
-      (void)lds_fx_add(acc, (qu64*)(smem + P.off_idx[j]), (1 << P.lds_log2) + 2, s, x);
-      break;
+    case ACC_SUM_X: lds_fx_add(acc, (qu64*)(smem + P.off_idx[j]), (1 << P.lds_log2) + 2, s, x); break;
     case ACC_MIN_I: atomicMin((long long*)&acc[s], (long long)x); break;
     case ACC_MAX_I: atomicMax((long long*)&acc[s], (long long)x); break;
     case ACC_MIN_F:
@@ -155,7 +153,6 @@ __device__ __forceinline__ void lds_flush(const Plan& P, char* smem) {
         i2 = ix[2 * SS + s];
         i3 = ix[3 * SS + s];
       }
-      if (a.acc == ACC_SUM_X) fx_norm(acc, (qi64&)i0, (qi64&)i1, (qi64&)i2);
       if (ok) {
         if (a.fn != QE_AGG_COUNT_STAR) gcombine(P.t, a.acc, j, gs, acc, nn, i0, i1, i2, i3);
       } else {
@@ -1244,22 +1241,16 @@ __device__ __forceinline__ void put_bit(qu8* gbm, qu32* lbits, int col, qi64 o, 
   else set_bit(gbm, o, true);
 }
 
-// An ACC_SUM_X slot's value (limb 0 = acc, limbs 1..3 and the status word in idx). NaN, counted in
-// ctl[6] for finalize to report, when the slot cannot give a sum within FX_REL_TOL of the exact
-// one: an unrepresentable input (the update reported it already), a limb-3 wrap that did not
-// cancel (|sum| >= 2^95), or more rounded inputs than the result's size allows (each rounding to
-// a multiple of 2^-64 is off by at most 2^-65).
-__device__ __forceinline__ double fx_sum(const DTable& t, int j, qu64 s, qi64 acc) {
+// An ACC_SUM_X slot's value (word 0 = acc, words 1..3 and the status word in idx; qe_dev.hpp
+// fx_result). A slot that cannot give its sum within FX_REL_TOL of the exact one (an input of
+// 2^126 or more, or rounded inputs whose error bound is too large for the result) is counted in
+// ctl[6], which finalize zeroes beforehand and reports.
+__device__ __forceinline__ double fx_sum(const DTable& t, int j, qu64 s, qi64 acc, qu64 nn) {
   const qu64 SS = t.cap + 2;
   const qu64* ix = t.idx[j];
-  const qu64 st = ix[3 * SS + s];
-  double v = bits_f64(0x7FF8000000000000ll);
-  if ((st & ~FX_INEXACT_MASK) == 0) {
-    v = fx_to_double(acc, (qi64)ix[s], (qi64)ix[SS + s], (qi64)ix[2 * SS + s]);
-    const qu64 inexact = st & FX_INEXACT_MASK;
-    if (inexact && (double)inexact * 0x1p-65 > FX_REL_TOL * __builtin_fabs(v)) v = bits_f64(0x7FF8000000000000ll);
-  }
-  if (v != v) atomicAdd(&t.ctl[6], 1ull);
+  bool err;
+  const double v = fx_result((qu64)acc, ix[s], ix[SS + s], ix[2 * SS + s], ix[3 * SS + s], nn, &err);
+  if (err) atomicAdd(&t.ctl[6], 1ull);
   return v;
 }
 
@@ -1295,13 +1286,13 @@ __device__ __forceinline__ void finalize_slot(const DTable& t, const AggMeta& m,
       case QE_AGG_COUNT_STAR: val = (qi64)cst; valid = true; break;
       case QE_AGG_AVG:
         if (m.acc[j] == ACC_SUM_X)
-          val = f64_bits(fx_sum(t, j, s, acc) / (double)nn);
+          val = f64_bits(fx_sum(t, j, s, acc, nn) / (double)nn);
         else
           val = f64_bits(bits_f64(acc) / (double)nn);
         break;
       default:
         if (m.acc[j] == ACC_SUM_X) {
-          val = f64_bits(fx_sum(t, j, s, acc));
+          val = f64_bits(fx_sum(t, j, s, acc, nn));
         } else if (acc_is_f64mm(m.acc[j])) {
           const qu64 i0 = t.idx[j][s], i1 = t.idx[j][SS + s];
           const qu64 i2 = t.idx[j][2 * SS + s], i3 = t.idx[j][3 * SS + s];
@@ -1566,7 +1557,7 @@ static int table_alloc(qe_hashagg* h, uint64_t cap, void** mem, DTable* t) {
 
 // ctl words: [0] groups, [1] deferred rows, [2] overflow records, [3] lost groups,
 // [4] largest slot count reported by the senders of an import_slots, [5] their records in total,
-// [6] fp64 SUM inputs a deterministic state could not represent (NaN, +-Inf, |x| >= 2^63)
+// [6] finalize: exact fp64 SUM groups that cannot be given within 1e-9 (zeroed before each finalize)
 // ctl[3] is sticky: every path that can drop a group (k_rehash, k_import, k_import_slots, the
 // fused kernel's overflow area) adds to it and nothing but a reset clears it, so a loss in a
 // launch with no read-back of its own (qe_hashagg_import_slots queues k_import_slots and returns)
@@ -1810,7 +1801,13 @@ static int compile_plan(qe_hashagg* h, const qe_column* cols, int32_t ncols, con
 }
 
 // LDS layout for a table of 2^log2 slots under this launch's aggregates. Returns bytes.
-static size_t lds_layout_at(const qe_hashagg* h, Plan* P, int log2) {
+// LDS words per slot beyond acc of an aggregate with idx arrays: fp64 MIN / MAX keep 4 row
+// indices; an exact fp64 SUM keeps 4 more words (256-bit + status) in the generic kernel but only
+// 2 in the plan-specialised kernels' 192-bit window (qe_dev.hpp fxw_add; rare rows go global).
+static size_t idx_words(int acc, bool generic) { return acc == ACC_SUM_X && !generic ? 2 : 4; }
+
+static size_t lds_layout_at(const qe_hashagg* h, Plan* P, int log2, bool generic = false) {
+  generic = generic || !h->ctx->jit;
   const size_t SS = ((size_t)1 << log2) + 2;
   size_t off = 8 * SS;  // keys
   P->off_cstar = (int32_t)off;
@@ -1829,7 +1826,7 @@ static size_t lds_layout_at(const qe_hashagg* h, Plan* P, int log2) {
     }
     if (acc_has_idx(a.acc)) {
       P->off_idx[j] = (int32_t)off;
-      off += 32 * SS;
+      off += 8 * idx_words(a.acc, generic) * SS;
     }
   }
   P->lds_log2 = log2;
@@ -1868,7 +1865,7 @@ static size_t lds_bytes_min(const qe_hashagg* h, int log2) {
   size_t b = 12 * SS + 16;
   for (int j = 0; j < h->naggs; ++j) {
     if (h->acc[j] != ACC_NONE) b += 8 * SS;
-    if (acc_has_idx(h->acc[j])) b += 32 * SS;
+    if (acc_has_idx(h->acc[j])) b += 8 * idx_words(h->acc[j], !h->ctx->jit) * SS;
   }
   return b;
 }
@@ -2210,12 +2207,15 @@ static int launch_pass(qe_hashagg* h, Plan& P, size_t& lds, hipFunction_t pfn, i
   } else if (h->jit_note.rfind("partitioning unavailable", 0) != 0) {
     h->jit_note = lds ? "jit disabled" : "global-only launch";
   }
-  if (!jfn && lds > HA_LDS_BUDGET) {
+  bool sum_x = false;
+  for (int j = 0; j < h->naggs; ++j) sum_x = sum_x || h->acc[j] == ACC_SUM_X;
+  if (!jfn && lds && (lds > HA_LDS_BUDGET || (sum_x && ctx->jit))) {
     // the 152 KiB budget is for the specialised 1024-thread kernel (one per CU); the generic
-    // 512-thread kernel runs two per CU, so its table is re-laid out within HA_LDS_BUDGET
+    // 512-thread kernel runs two per CU, so its table is re-laid out within HA_LDS_BUDGET (and with
+    // the generic kernel's full exact-SUM slots)
     size_t b = 0;
     int log2 = P.lds_log2;
-    while (log2 >= h->lds_log2_min && (b = lds_layout_at(h, &P, log2)) > HA_LDS_BUDGET) --log2;
+    while (log2 >= h->lds_log2_min && (b = lds_layout_at(h, &P, log2, true)) > HA_LDS_BUDGET) --log2;
     if (log2 < h->lds_log2_min || log2 < 8) {
       P.lds_log2 = 0;
       lds = 0;
@@ -2269,9 +2269,6 @@ static int settle_pass(qe_hashagg* h, const Plan& P, int* out_i, const uint32_t*
     h->last_launches += 1;
   }
   QE_CHECK(c[3] == 0, QE_ERR_CAPACITY, "hash aggregate lost %llu groups (overflow area)", (unsigned long long)c[3]);
-  QE_CHECK(c[6] == 0, QE_ERR_UNSUPPORTED,
-           "deterministic fp64 SUM: %llu inputs outside the exact fixed-point range (NaN, +-Inf or |x| >= 2^63)",
-           (unsigned long long)c[6]);
   h->narrow_failed = P.part_narrow && (c[7] & 1) != 0;
   if (P.lds_compact && (c[7] & 2)) h->compact_off = true;
   const uint64_t groups = c[0], deferred = c[1], ovf_recs = std::min<uint64_t>(c[2], P.ovf_cap);
@@ -2730,8 +2727,12 @@ int qe_hashagg_create(qe_ctx* ctx, int32_t nkeys, const int32_t* key_types, int3
 int qe_hashagg_create_ex(qe_ctx* ctx, int32_t nkeys, const int32_t* key_types, int32_t naggs, const qe_agg_desc* aggs,
                          int64_t expected_groups, int32_t flags, qe_hashagg** out) {
   QE_TRY(ctx_enter(ctx));
-  QE_CHECK((flags & ~QE_HASHAGG_DETERMINISTIC) == 0, QE_ERR_INVALID_ARG, "unknown flags 0x%x", flags);
-  const bool det = (flags & QE_HASHAGG_DETERMINISTIC) != 0;
+  QE_CHECK((flags & ~(QE_HASHAGG_DETERMINISTIC | QE_HASHAGG_FAST_FP64)) == 0, QE_ERR_INVALID_ARG, "unknown flags 0x%x",
+           flags);
+  QE_CHECK((flags & QE_HASHAGG_DETERMINISTIC) == 0 || (flags & QE_HASHAGG_FAST_FP64) == 0, QE_ERR_INVALID_ARG,
+           "QE_HASHAGG_DETERMINISTIC and QE_HASHAGG_FAST_FP64 exclude each other");
+  // fp64 SUM / AVG: exact (ACC_SUM_X) unless the caller opts into plain fp64 atomics
+  const bool det = (flags & QE_HASHAGG_FAST_FP64) == 0;
   QE_CHECK(out, QE_ERR_INVALID_ARG, "null out");
   QE_CHECK(nkeys >= 0 && nkeys <= QE_MAX_KEYS, QE_ERR_UNSUPPORTED, "0..%d group keys supported", QE_MAX_KEYS);
   QE_CHECK(naggs >= 0 && naggs <= QE_MAX_AGGS, QE_ERR_UNSUPPORTED, "0..%d aggregates supported", QE_MAX_AGGS);
@@ -3002,14 +3003,15 @@ int qe_hashagg_num_groups(qe_hashagg* h, int64_t* out) {
   return QE_OK;
 }
 
-// Deterministic states: finalize waits for its kernel and fails when a group's fixed-point sum
-// could not be given within FX_REL_TOL of the exact sum (fx_sum counted such groups in ctl[6]).
+// States with exact fp64 sums: finalize waits for its kernel and fails when a group's sum could not
+// be given within FX_REL_TOL of the exact sum (fx_sum counted such groups in ctl[6], zeroed before
+// the finalize kernel, so a failed finalize does not leak into later calls).
 static int check_fx_final(qe_hashagg* h) {
   uint64_t c[8];
   QE_TRY(read_ctl(h, c));
   QE_CHECK(c[6] == 0, QE_ERR_UNSUPPORTED,
-           "deterministic fp64 SUM: %llu group results not exact to 1e-9 (inputs outside the fixed-point range "
-           "[2^-64, 2^63) or |sum| >= 2^95)",
+           "fp64 SUM: %llu group results not exact to 1e-9 (an input of magnitude >= 2^126, or inputs with bits "
+           "below 2^-128 whose rounding is too large for the result)",
            (unsigned long long)c[6]);
   return QE_OK;
 }
@@ -3054,6 +3056,7 @@ int qe_hashagg_finalize(qe_hashagg* h, qe_column* out_keys, qe_column* out_aggs,
   if (groups == 0) return QE_OK;
   bool det = false;
   for (int j = 0; j < h->naggs; ++j) det = det || h->acc[j] == ACC_SUM_X;
+  if (det) QE_HIP(hipMemsetAsync(h->ctl + 6, 0, 8, ctx->stream));
   if (small) {
     hipLaunchKernelGGL(k_finalize_small, dim3(1), dim3(FS_THREADS), 0, ctx->stream, h->t, agg_meta(h), h->km, oc,
                        (qi64)groups);

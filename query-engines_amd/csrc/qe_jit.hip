@@ -252,14 +252,14 @@ void emit_col_loads(const Plan& P, std::ostringstream& o, unsigned need, const s
 }
 
 // act: rows of this step inside [0, P.n), in the retry set (if any), passing mask and terms.
-void emit_active_rows(const Plan& P, std::ostringstream& o, bool retry) {
+void emit_active_rows(const Plan& P, std::ostringstream& o, bool retry, bool skip_idle = true) {
   o << "    qu32 act = 15u;\n"
     << "    if (!full) { act = 0; for (int r = 0; r < 4; ++r) act |= (qu32)(r0 + 128 * (r >> 1) + (r & 1) < P.n) << r; }\n";
   if (retry)
     o << "    if (P.defer_in) {\n      for (int r = 0; r < 4; ++r) { const qi64 row = r0 + 128 * (r >> 1) + (r & 1);\n"
       << "        if (row < P.n && !((P.defer_in[row >> 5] >> (row & 31)) & 1)) act &= ~(1u << r); }\n    }\n";
   emit_predicate(P, o, 4);
-  o << "    if (act == 0) continue;\n";
+  if (skip_idle) o << "    if (act == 0) continue;\n";
 }
 
 // key[4] (packed / canonical int64 group key) and knull (bit r: the key of row r is null).
@@ -299,9 +299,10 @@ void emit_lds_table(const Plan& P, std::ostringstream& o, int log2, size_t* lds_
       o << "  __shared__ qu32 s_nn" << j << "[SS];\n";
       lds += 4 * SS;
     }
-    if (acc_has_idx(a.acc)) {
-      o << "  __shared__ qu64 s_idx" << j << "[4 * SS];\n";
-      lds += 32 * SS;
+    if (acc_has_idx(a.acc)) {  // fp64 MIN / MAX: 4 row indices; exact SUM: window words u1, u2
+      const int nw = a.acc == ACC_SUM_X ? 2 : 4;
+      o << "  __shared__ qu64 s_idx" << j << "[" << nw << " * SS];\n";
+      lds += 8 * nw * SS;
     }
   }
   *lds_bytes = lds;
@@ -311,10 +312,114 @@ void emit_lds_table(const Plan& P, std::ostringstream& o, int log2, size_t* lds_
     if (a.acc != ACC_NONE) o << "    s_acc" << j << "[s] = " << acc_init(a.acc) << ";\n";
     if (a.track_nn) o << "    s_nn" << j << "[s] = 0;\n";
     if (acc_has_idx(a.acc))
-      o << "    for (int k = 0; k < 4; ++k) s_idx" << j << "[k * SS + s] = " << (acc_is_f64mm(a.acc) ? "~0ull" : "0ull")
-        << ";\n";
+      o << "    for (int k = 0; k < " << (a.acc == ACC_SUM_X ? 2 : 4) << "; ++k) s_idx" << j << "[k * SS + s] = "
+        << (acc_is_f64mm(a.acc) ? "~0ull" : "0ull") << ";\n";
   }
   o << "  }\n  __syncthreads();\n";
+}
+
+// ---- exact fp64 SUM rows through a per-wave queue (fx queue) -----------------------------------------
+// An exact fp64 SUM (ACC_SUM_X) costs a row about 30 VALU instructions and two LDS atomics that
+// return (qe_dev.hpp fx_row / fx_add_row). Issued per row position of a step, a wave pays that for
+// all 64 lanes however few rows passed the predicate (C5: ~12 %). Instead, every row bound for the
+// LDS table appends (slot | input validity bits << 24, the SUM inputs) to its wave's ring of 128
+// entries in LDS, and whenever 64 are queued the wave adds them with every lane busy. Only the
+// SUM_X adds are queued; COUNT(*), non-null counts and the other aggregates stay direct. The
+// kernel's step loop must then be convergent at the append points (no per-lane `continue`).
+// Wave-private: a wave's LDS operations complete in order, so its lanes read what other lanes of
+// the same wave wrote before (the fences keep the compiler from reordering them).
+constexpr int FXQ_CAP = 128;
+
+std::vector<int> fx_queue_aggs(const Plan& P) {
+  std::vector<int> q;
+  for (int j = 0; j < P.naggs; ++j)
+    if (P.aggs[j].pkind != 0 && P.aggs[j].acc == ACC_SUM_X) q.push_back(j);
+  return q;
+}
+
+bool fx_queue_enabled() {
+  static const bool v = [] {
+    const char* e = getenv("QE_FX_QUEUE");
+    return !(e && e[0] == '0');
+  }();
+  return v;
+}
+
+size_t fx_queue_bytes(const Plan& P, int block) {
+  const size_t nq = fx_queue_aggs(P).size();
+  return nq ? (size_t)(block / 64) * FXQ_CAP * (4 + 8 * nq) : 0;
+}
+
+void emit_fx_queue_decl(const Plan& P, std::ostringstream& o, int block) {
+  const std::vector<int> q = fx_queue_aggs(P);
+  o << "  __shared__ qu32 q_slot[" << (block / 64) * FXQ_CAP << "];\n";
+  for (size_t k = 0; k < q.size(); ++k) o << "  __shared__ qi64 q_x" << k << "[" << (block / 64) * FXQ_CAP << "];\n";
+  o << "  const qu32 q_base = (threadIdx.x >> 6) * " << FXQ_CAP << "u;\n  qu32 q_head = 0, q_n = 0;\n";
+}
+
+// Adds the `m` entries at the head of the wave's ring (m <= 64: one per lane). The window adds of all
+// queued aggregates go out phase by phase (first words, then second words) so that their LDS round
+// trips overlap; an input outside the window (fx_rare) goes to the group's global slot.
+void emit_fx_queue_run(const Plan& P, std::ostringstream& o, const std::string& m) {
+  const std::vector<int> q = fx_queue_aggs(P);
+  const int nq = (int)q.size();
+  o << "      __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, \"wavefront\");\n"
+    << "      if ((qu32)lane < " << m << ") {\n"
+    << "        const qu32 qp = q_base + ((q_head + (qu32)lane) & " << FXQ_CAP - 1 << "u);\n"
+    << "        const qu32 qe = q_slot[qp];\n        const int s = (int)(qe & 0xFFFFFFu);\n"
+    << "        qi64 qx[" << nq << "];\n        qu32 rare = 0;\n";
+  for (int k = 0; k < nq; ++k)
+    o << "        qx[" << k << "] = ((qe >> " << 24 + k << ") & 1u) ? q_x" << k << "[qp] : 0ll;\n"
+      << "        if (fx_rare(qx[" << k << "])) { rare |= 1u << " << k << "; qx[" << k << "] = 0; }\n";
+  o << "        qu64* wp0[" << nq << "];\n        qu64* wp1[" << nq << "];\n        qu64 lo[" << nq << "], hi[" << nq
+    << "];\n        bool ng[" << nq << "], k0[" << nq << "];\n";
+  for (int k = 0; k < nq; ++k) {
+    const std::string j = std::to_string(q[k]), ks = std::to_string(k);
+    o << "        {\n          const qu64 b = (qu64)qx[" << ks << "];\n          const int ex = (int)((b >> 52) & 0x7FF);\n"
+      << "          const qu64 mm = ex ? ((b & ((1ull << 52) - 1)) | (1ull << 52)) : 0ull;\n"
+      << "          const int p = ex ? ex - FXW_EX_LO : 0, kk = p >> 6, qq = p & 63;\n"
+      << "          qu64 l = mm << qq, h = qq ? (mm >> (64 - qq)) : 0ull;\n"
+      << "          ng[" << ks << "] = ex && (b >> 63);  // (-0.0 adds nothing, like +0.0)\n"
+      << "          if (ng[" << ks << "]) { l = 0ull - l; h = ~h + (l == 0 ? 1ull : 0ull); }\n"
+      << "          lo[" << ks << "] = l; hi[" << ks << "] = h; k0[" << ks << "] = kk == 0;\n"
+      << "          wp0[" << ks << "] = kk ? &s_idx" << j << "[s] : (qu64*)&s_acc" << j << "[s];\n"
+      << "          wp1[" << ks << "] = &s_idx" << j << "[kk * SS + s];\n        }\n";
+  }
+  o << "        qu64 o0[" << nq << "], t[" << nq << "], o1[" << nq << "];\n";
+  for (int k = 0; k < nq; ++k) o << "        o0[" << k << "] = atomicAdd(wp0[" << k << "], lo[" << k << "]);\n";
+  for (int k = 0; k < nq; ++k)
+    o << "        t[" << k << "] = hi[" << k << "] + (o0[" << k << "] + lo[" << k << "] < o0[" << k << "] ? 1ull : 0ull);\n";
+  for (int k = 0; k < nq; ++k) o << "        o1[" << k << "] = atomicAdd(wp1[" << k << "], t[" << k << "]);\n";
+  for (int k = 0; k < nq; ++k) {
+    const std::string j = std::to_string(q[k]), ks = std::to_string(k);
+    o << "        if (k0[" << ks << "]) {\n          const qi64 d = (qi64)((t[" << ks << "] < hi[" << ks << "] ? 1 : 0) + (o1[" << ks
+      << "] + t[" << ks << "] < o1[" << ks << "] ? 1 : 0)) - (ng[" << ks << "] ? 1 : 0);\n"
+      << "          if (d) atomicAdd(&s_idx" << j << "[SS + s], (qu64)d);\n        }\n";
+  }
+  o << "        if (rare) {\n          const bool knl = s == S;\n"
+    << "          const qi64 key = knl ? 0 : (s == S + 1 ? EMPTY_KEY : s_keys[s]);\n";
+  for (int k = 0; k < nq; ++k)
+    o << "          if ((rare >> " << k << ") & 1u) fx_rare_global(P, " << q[k] << ", key, knl, q_x" << k << "[qp]);\n";
+  o << "        }\n      }\n      __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, \"wavefront\");\n";
+}
+
+void emit_fx_queue_append(const Plan& P, std::ostringstream& o, const std::vector<std::string>& val,
+                          const std::vector<std::string>& ok) {
+  const std::vector<int> q = fx_queue_aggs(P);
+  o << "    {\n      const qu64 below = (1ull << lane) - 1;\n"
+    << "#pragma unroll\n      for (int r = 0; r < 4; ++r) {\n"
+    << "        const bool qa = (loc >> r) & 1;\n        const qu64 bq = __ballot(qa);\n"
+    << "        if (qa) {\n"
+    << "          const qu32 qp = q_base + ((q_head + q_n + (qu32)__popcll(bq & below)) & " << FXQ_CAP - 1 << "u);\n"
+    << "          qu32 qe = (qu32)slot[r];\n";
+  for (size_t k = 0; k < q.size(); ++k)
+    o << "          qe |= (" << ok[q[k]] << " ? 1u : 0u) << " << 24 + k << ";\n          q_x" << k << "[qp] = " << val[q[k]]
+      << ";\n";
+  o << "          q_slot[qp] = qe;\n        }\n"
+    << "        q_n += (qu32)__popcll(bq);\n"
+    << "        if (q_n >= 64u) {\n";
+  emit_fx_queue_run(P, o, "64u");
+  o << "          q_head = (q_head + 64u) & " << FXQ_CAP - 1 << "u;\n          q_n -= 64u;\n        }\n      }\n    }\n";
 }
 
 // Aggregation of the 4 active rows of a step (act, key[4], knull) into the LDS table; rows whose
@@ -322,7 +427,8 @@ void emit_lds_table(const Plan& P, std::ostringstream& o, int log2, size_t* lds_
 // (bit `didx` of defer_out). val[j] / ok[j]: aggregate j's input value (int64 bits) and validity
 // for row r; `row`: the row's global index (fp64 MIN/MAX order); all are C expressions of r.
 void emit_agg_rows(const Plan& P, std::ostringstream& o, const std::vector<std::string>& val,
-                   const std::vector<std::string>& ok, const std::string& row, const std::string& didx) {
+                   const std::vector<std::string>& ok, const std::string& row, const std::string& didx,
+                   bool fx_queue = false) {
   o << "    int slot[4];\n    qu32 h[4];\n    qi64 k0[4];\n"
     << "#pragma unroll\n    for (int r = 0; r < 4; ++r) { h[r] = lds_hash((qu64)key[r]) >> (32 - LOG2); k0[r] = ((act >> r) & 1) ? s_keys[h[r]] : 0; }\n"
     << "#pragma unroll\n    for (int r = 0; r < 4; ++r) slot[r] = ((knull >> r) & 1) ? S : (key[r] == EMPTY_KEY ? S + 1 : (k0[r] == key[r] ? (int)h[r] : -1));\n"
@@ -331,8 +437,19 @@ void emit_agg_rows(const Plan& P, std::ostringstream& o, const std::vector<std::
     << "    miss &= act;\n"
     << "    if (miss) {\n      for (int r = 0; r < 4; ++r) if ((miss >> r) & 1) slot[r] = lds_probe(s_keys, LOG2, key[r], h[r]);\n    }\n"
     << "    qu32 glob = 0;\n"
-    << "#pragma unroll\n    for (int r = 0; r < 4; ++r) glob |= (qu32)(slot[r] < 0) << r;\n"
-    << "    glob &= act;\n    const qu32 loc = act & ~glob;\n"
+    << "#pragma unroll\n    for (int r = 0; r < 4; ++r) glob |= (qu32)(slot[r] < 0) << r;\n";
+  // rows with an exact fp64 SUM input outside the LDS window: the global table's full accumulator
+  // (with the fx queue the check happens when the queue is drained: fx_rare_global)
+  bool any_x = false;
+  for (int j = 0; j < P.naggs; ++j) any_x = any_x || (P.aggs[j].pkind != 0 && P.aggs[j].acc == ACC_SUM_X);
+  if (any_x && !fx_queue) {
+    o << "#pragma unroll\n    for (int r = 0; r < 4; ++r) {\n      bool rare = false;\n";
+    for (int j = 0; j < P.naggs; ++j)
+      if (P.aggs[j].pkind != 0 && P.aggs[j].acc == ACC_SUM_X)
+        o << "      rare = rare || ((" << ok[j] << ") && fx_rare(" << val[j] << "));\n";
+    o << "      glob |= (qu32)rare << r;\n    }\n";
+  }
+  o << "    glob &= act;\n    const qu32 loc = act & ~glob;\n"
     << "#pragma unroll\n    for (int r = 0; r < 4; ++r) if ((loc >> r) & 1) atomicAdd(&s_cst[slot[r]], 1u);\n";
   for (int j = 0; j < P.naggs; ++j) {
     const DAgg& a = P.aggs[j];
@@ -347,7 +464,10 @@ void emit_agg_rows(const Plan& P, std::ostringstream& o, const std::vector<std::
     switch (a.acc) {
       case ACC_SUM_I: o << "        atomicAdd((qu64*)&s_acc" << js << "[s], (qu64)x);\n"; break;
       case ACC_SUM_F: o << "        atomicAdd((double*)&s_acc" << js << "[s], bits_f64(x));\n"; break;
-      case ACC_SUM_X: o << "        (void)lds_fx_add(s_acc" << js << ", s_idx" << js << ", SS, s, x);\n"; break;
+      case ACC_SUM_X:
+        if (!fx_queue) o << "        lds_fxw_add(s_acc" << js << ", s_idx" << js << ", SS, s, x);\n";
+        else o << "        (void)x; (void)s;\n";
+        break;
       case ACC_MIN_I: o << "        atomicMin(&s_acc" << js << "[s], x);\n"; break;
       case ACC_MAX_I: o << "        atomicMax(&s_acc" << js << "[s], x);\n"; break;
       case ACC_MIN_F:
@@ -374,6 +494,7 @@ void emit_agg_rows(const Plan& P, std::ostringstream& o, const std::vector<std::
       << (((P.nn_skip >> j) & 1) ? "false" : "true") << "); }\n";
   }
   o << "      }\n    }\n";
+  if (fx_queue) emit_fx_queue_append(P, o, val, ok);
 }
 
 // Merge the workgroup's LDS table into the global table (or the overflow records). With
@@ -406,12 +527,14 @@ void emit_flush(const Plan& P, std::ostringstream& o, bool mark_full = false, bo
     const std::string js = std::to_string(j);
     o << "    {\n      qi64 acc = " << (a.acc != ACC_NONE ? "s_acc" + js + "[s]" : std::string("0")) << ";\n"
       << "      const qu64 nn = " << (a.track_nn ? "s_nn" + js + "[s]" : std::string("c")) << ";\n";
-    if (acc_has_idx(a.acc))
+    if (a.acc == ACC_SUM_X)  // the LDS window as a global partial (status 0: rare rows went global)
+      o << "      qu64 i0, i1, i2;\n      const qu64 i3 = 0;\n      {\n        qu64 v[4];\n        fxw_words((qu64)acc, s_idx" << js
+        << "[s], s_idx" << js << "[SS + s], v);\n        acc = (qi64)v[0]; i0 = v[1]; i1 = v[2]; i2 = v[3];\n      }\n";
+    else if (acc_has_idx(a.acc))
       o << "      qu64 i0 = s_idx" << js << "[s], i1 = s_idx" << js << "[SS + s], i2 = s_idx" << js
         << "[2 * SS + s], i3 = s_idx" << js << "[3 * SS + s];\n";
     else
       o << "      const qu64 i0 = ~0ull, i1 = ~0ull, i2 = ~0ull, i3 = ~0ull;\n";
-    if (a.acc == ACC_SUM_X) o << "      fx_norm(acc, (qi64&)i0, (qi64&)i1, (qi64&)i2);\n";
     const bool skip_nn = (P.nn_skip >> j) & 1;
     const char* add_nn = skip_nn ? "false" : "true";
     if (a.fn != QE_AGG_COUNT_STAR && part)
@@ -631,6 +754,15 @@ bool gen_fused_source(const Plan& P, int log2, std::string* src, size_t* lds_byt
       << "  if (threadIdx.x < 16) { s_spc[threadIdx.x] = -1; s_spf[threadIdx.x] = 0; }\n";
   if (compact) emit_lds_table_c(P, o, lds_bytes);
   else emit_lds_table(P, o, log2, lds_bytes);
+  // exact fp64 SUMs through the per-wave queue when the plan's step loop allows it and it fits
+  const int block = fused_block(log2);
+  const bool fxq = !compact && !spill && P.mp_n <= 1 && fx_queue_enabled() && !fx_queue_aggs(P).empty() &&
+                   fx_queue_aggs(P).size() <= 8 && (1 << log2) + 2 < (1 << 24) &&
+                   *lds_bytes + fx_queue_bytes(P, block) <= (size_t)152 * 1024;
+  if (fxq) {
+    emit_fx_queue_decl(P, o, block);
+    *lds_bytes += fx_queue_bytes(P, block);
+  }
   o << "  const int lane = threadIdx.x & 63;\n"
     << "  const qi64 wave = (blockIdx.x * (qi64)blockDim.x + threadIdx.x) >> 6;\n"
     << "  const qi64 stride = (((qi64)gridDim.x * blockDim.x) >> 6) * 256;\n";
@@ -656,7 +788,7 @@ bool gen_fused_source(const Plan& P, int log2, std::string* src, size_t* lds_byt
       << "    const qi64 r0 = base + 2 * lane;\n";
     emit_col_loads(P, o, ~0u);
   }
-  emit_active_rows(P, o, true);
+  emit_active_rows(P, o, true, !fxq);
   emit_keys(P, o);
   if (spill) {
     const PartLayout L = part_layout(P);
@@ -713,8 +845,13 @@ bool gen_fused_source(const Plan& P, int log2, std::string* src, size_t* lds_byt
   if (compact)
     emit_agg_rows_c(P, o, val, ok, "P.row_base + r0 + 128 * (r >> 1) + (r & 1)", "r0 + 128 * (r >> 1) + (r & 1)");
   else
-    emit_agg_rows(P, o, val, ok, "P.row_base + r0 + 128 * (r >> 1) + (r & 1)", "r0 + 128 * (r >> 1) + (r & 1)");
+    emit_agg_rows(P, o, val, ok, "P.row_base + r0 + 128 * (r >> 1) + (r & 1)", "r0 + 128 * (r >> 1) + (r & 1)", fxq);
   o << (pf ? "    } while (0);\n  }\n  }\n" : "  }\n");
+  if (fxq) {  // the rest of the wave's queue
+    o << "  if (q_n) {\n";
+    emit_fx_queue_run(P, o, "q_n");
+    o << "  }\n";
+  }
   if (spill)  // each wave's open chunk: its fill (a wave's LDS writes are seen by its own later reads)
     o << "  if ((threadIdx.x & 63) == 0 && s_spc[threadIdx.x >> 6] >= 0)\n"
       << "    P.part_chunk[1 + s_spc[threadIdx.x >> 6]] = (qi64)s_spf[threadIdx.x >> 6];\n"

@@ -105,13 +105,16 @@ class HashAggregateState:
     """Owns one qe_hashagg. Keys: ``key_types``; aggregates: (fn, input_type) pairs."""
 
     def __init__(self, ctx: Context, key_types: Sequence[int], aggs: Sequence[Tuple[int, int]],
-                 expected_groups: int = 1024, async_update: bool = False, deterministic: bool = False):
+                 expected_groups: int = 1024, async_update: bool = False, deterministic: bool = False,
+                 fast_fp64: bool = False):
         """``async_update``: stream-ordered updates (qe_hashagg_set_async) — an update returns once
         its kernel is queued and is checked by the next call on the state (finalize, num_groups,
         the next update), which may re-read the update's columns; the state holds a reference to
         them until the next update or reset.
-        ``deterministic``: fp64 SUM / AVG in exact fixed point (QE_HASHAGG_DETERMINISTIC): results
-        are bit-identical run to run, like the reference's ordered row loop and merge."""
+        fp64 SUM / AVG are exact by default (the correctly rounded exact sum, bit-identical run to
+        run, like the reference's ordered row loop with exact arithmetic); ``deterministic`` names
+        that default (QE_HASHAGG_DETERMINISTIC). ``fast_fp64``: plain fp64 atomics instead
+        (QE_HASHAGG_FAST_FP64), without the 1e-9 guarantee for cancelling groups."""
         from .strdict import StringDictionary
 
         self.ctx = ctx
@@ -133,9 +136,11 @@ class HashAggregateState:
         ad = (N.QeAggDesc * max(1, len(self.aggs)))(*[N.QeAggDesc(f, t) for f, t in self.aggs])
         h = N.C.c_void_p()
         N.check(N.lib().qe_hashagg_create_ex(ctx.handle, len(self.device_key_types), kt, len(self.aggs), ad,
-                                             int(expected_groups), N.HASHAGG_DETERMINISTIC if deterministic else 0,
+                                             int(expected_groups),
+                                             (N.HASHAGG_DETERMINISTIC if deterministic else 0) |
+                                             (N.HASHAGG_FAST_FP64 if fast_fp64 else 0),
                                              N.C.byref(h)))
-        self.deterministic = bool(deterministic)
+        self.deterministic = not fast_fp64
         self.handle = h
         self._out_rows = max(1, 2 * self.expected_groups)  # finalize's first output sizing guess
         self.async_update = bool(async_update)

@@ -178,7 +178,8 @@ class QeSelectSpec(C.Structure):
 _lib = None
 
 # (name, restype, argtypes) for every entry point declared in include/qe_hip.h
-HASHAGG_DETERMINISTIC = 1  # qe_hashagg_create_ex flag
+HASHAGG_DETERMINISTIC = 1  # qe_hashagg_create_ex flags
+HASHAGG_FAST_FP64 = 2
 _P = C.c_void_p
 _PP = C.POINTER(C.c_void_p)
 _I64P = C.POINTER(C.c_int64)

@@ -171,6 +171,12 @@ static int emit_agg(const char* dir, const char* name, const qe_column* cols, in
     P.mp_n = 0;
   }
   P.lds_compact = 0;
+  // single-pass fused kernel (mp_n = 0): exact fp64 SUM plans add through the per-wave fx queue
+  std::string q1;
+  if (!gen_fused_source(P, log2, &q1, &lds, false) || write_src(dir, std::string(name) + "_fused1", q1)) {
+    fprintf(stderr, "%s: single-pass fused source not generated\n", name);
+    return 1;
+  }
   return write_src(dir, std::string(name) + "_fused", a) | write_src(dir, std::string(name) + "_spill", b) |
          write_src(dir, std::string(name) + "_pagg", c) | write_src(dir, std::string(name) + "_pscatter", d) |
          write_src(dir, std::string(name) + "_pscatter_soa", e) | write_src(dir, std::string(name) + "_pagg_rows", f) |

@@ -5,12 +5,11 @@ design documents otherwise:
 
 * compaction (filter, select-project), CAST, CSV scan, global aggregate (per-block partials and a
   fixed-order final pass), and every integer / MIN / MAX / COUNT group result: bit-identical;
-* hash-aggregate fp64 SUM / AVG: the per-group sums combine workgroup partials with fp64 atomics,
-  so their rounding depends on arrival order. Run to run they must agree within 1e-13 × Σ|x| of
-  the group (a condition-aware bound: cancelling sums amplify the relative spread; the parity
-  contract of 1e-9 against the oracle holds either way) — DESIGN.md "Determinism";
-* a deterministic state (QE_HASHAGG_DETERMINISTIC) sums fp64 in exact fixed point: bit-identical
-  across runs, streams, batchings and kernel paths, and equal to math.fsum of each group.
+* hash-aggregate fp64 SUM / AVG: exact fixed point by default (qe_dev.hpp fx_*): bit-identical
+  across runs, streams, batchings and kernel paths, and equal to math.fsum of each group;
+* with QE_HASHAGG_FAST_FP64 (opt-in fp64 atomics) the per-group sums combine in arrival order:
+  run to run they agree within 1e-13 × Σ|x| of the group (a condition-aware bound; this mode does
+  not promise the 1e-9 contract for groups whose terms cancel — DESIGN.md "fp64 SUM").
 Group ORDER is unspecified (HashMap iteration order, K:639), so groups are compared as maps."""
 import numpy as np
 import pytest
@@ -97,28 +96,32 @@ def test_hash_aggregate(gpu_ctx):
             (N.AGG_MAX, N.TYPE_FLOAT64), (N.AGG_SUM, N.TYPE_INT64), (N.AGG_COUNT, N.TYPE_INT64),
             (N.AGG_MIN, N.TYPE_INT64)]
     yv = rng.random(n) > 0.2
-    runs = []
-    for ctx in _runs(gpu_ctx):
-        kc = DeviceColumn.from_numpy(N.TYPE_INT64, k, None, ctx=ctx)
-        xc = DeviceColumn.from_numpy(N.TYPE_FLOAT64, x, None, ctx=ctx)
-        yc = DeviceColumn.from_numpy(N.TYPE_INT64, y, yv, ctx=ctx)
-        st = HashAggregateState(ctx, [N.TYPE_INT64], aggs, 1024)
-        st.update([kc], [xc, xc, xc, xc, yc, yc, yc])
-        keys, vals = st.finalize()
-        ctx.synchronize()
-        cols = [v.to_pylist() for v in vals]
-        runs.append({kk: [c[i] for c in cols] for i, kk in enumerate(keys[0].to_pylist())})
-    absum = np.bincount(k, weights=np.abs(x))
-    cnt = np.bincount(k)
-    base = runs[0]
-    for r in runs[1:]:
-        assert r.keys() == base.keys()
-        for kk, v in r.items():
-            b = base[kk]
-            assert v[2:] == b[2:], kk  # MIN/MAX fp64 and every integer result: bit-identical
-            bound = 1e-13 * absum[kk]  # fp64 SUM / AVG: atomic arrival order
-            assert abs(v[0] - b[0]) <= bound, (kk, v[0], b[0])
-            assert abs(v[1] - b[1]) <= bound / cnt[kk], (kk, v[1], b[1])
+    for fast in (False, True):
+        runs = []
+        for ctx in _runs(gpu_ctx):
+            kc = DeviceColumn.from_numpy(N.TYPE_INT64, k, None, ctx=ctx)
+            xc = DeviceColumn.from_numpy(N.TYPE_FLOAT64, x, None, ctx=ctx)
+            yc = DeviceColumn.from_numpy(N.TYPE_INT64, y, yv, ctx=ctx)
+            st = HashAggregateState(ctx, [N.TYPE_INT64], aggs, 1024, fast_fp64=fast)
+            st.update([kc], [xc, xc, xc, xc, yc, yc, yc])
+            keys, vals = st.finalize()
+            ctx.synchronize()
+            cols = [v.to_pylist() for v in vals]
+            runs.append({kk: [c[i] for c in cols] for i, kk in enumerate(keys[0].to_pylist())})
+        absum = np.bincount(k, weights=np.abs(x))
+        cnt = np.bincount(k)
+        base = runs[0]
+        for r in runs[1:]:
+            assert r.keys() == base.keys()
+            for kk, v in r.items():
+                b = base[kk]
+                if not fast:
+                    assert v == b, kk  # exact fp64 sums too: bit-identical
+                    continue
+                assert v[2:] == b[2:], kk  # MIN/MAX fp64 and every integer result: bit-identical
+                bound = 1e-13 * absum[kk]  # fast fp64 SUM / AVG: atomic arrival order
+                assert abs(v[0] - b[0]) <= bound, (kk, v[0], b[0])
+                assert abs(v[1] - b[1]) <= bound / cnt[kk], (kk, v[1], b[1])
 
 
 def test_csv_cast_string_keys(gpu_ctx, tmp_path):
@@ -152,10 +155,11 @@ def test_csv_cast_string_keys(gpu_ctx, tmp_path):
 @pytest.mark.parametrize("groups,expected,path", [(37, 64, "lds"), (4500, 4500, "two-bucket"),
                                                    (50_000, 50_000, "partitioned"), (300, 64, "generic")])
 def test_deterministic_fp64_group_sums(gpu_ctx, groups, expected, path):
-    """QE_HASHAGG_DETERMINISTIC: fp64 SUM / AVG in exact fixed point. Every run — default stream,
-    second context, two batches instead of one — gives the same bits, and they equal the correctly
-    rounded exact sum (math.fsum) of each group, as the reference's ordered row loop would give
-    with exact arithmetic. Values here have no bits below 2^-64, so the fixed point is exact."""
+    """fp64 SUM / AVG in exact fixed point (the default; QE_HASHAGG_DETERMINISTIC names it). Every
+    run — default stream, second context, two batches instead of one — gives the same bits, and
+    they equal the correctly rounded exact sum (math.fsum) of each group, as the reference's
+    ordered row loop would give with exact arithmetic. Values span 2^-80 .. 2^30: some take the LDS
+    window, some (below 2^-44) the global table's full accumulator."""
     import math
 
     from kquery import native as N
@@ -165,8 +169,7 @@ def test_deterministic_fp64_group_sums(gpu_ctx, groups, expected, path):
     rng = np.random.default_rng(groups)
     n = 3_000_000
     k = rng.integers(0, groups, n).astype(np.int64)
-    x = rng.normal(size=n) * np.exp2(rng.integers(-20, 30, n))  # wide range: fp64 atomics would wobble
-    x = np.round(x * 2.0 ** 60) * 2.0 ** -60  # multiples of 2^-60: held exactly by the fixed point
+    x = rng.normal(size=n) * np.exp2(rng.integers(-80, 30, n))  # wide range: fp64 atomics would wobble
     xv = rng.random(n) > 0.05
     aggs = [(N.AGG_SUM, N.TYPE_FLOAT64), (N.AGG_AVG, N.TYPE_FLOAT64), (N.AGG_COUNT_STAR, N.TYPE_INT64)]
     runs = []
@@ -202,30 +205,47 @@ def test_deterministic_fp64_group_sums(gpu_ctx, groups, expected, path):
 
 
 @pytest.mark.parametrize("expected", [16, 4500, 50_000])
-def test_deterministic_rejects_unrepresentable(gpu_ctx, expected):
-    """NaN / Inf / |x| >= 2^63 cannot be held by the fixed point: the update fails loudly, on the
-    LDS, two-bucket and radix-partitioned paths alike (the partitioned flush of an exclusive slice
-    reports it too)."""
+def test_exact_sum_specials(gpu_ctx, expected):
+    """IEEE specials and large inputs on the LDS, two-bucket and radix-partitioned paths: NaN and
+    +-Inf give the IEEE result of the sum in their group only; 2^70 (outside the LDS window, in the
+    global accumulator) is summed exactly; an input of 2^127 cannot be, and finalize reports it."""
+    import math
+
     from kquery import native as N
     from kquery.aggregate import HashAggregateState
     from kquery.columnar import DeviceColumn
 
     n = 200_000
-    for bad in (np.nan, np.inf, 2.0 ** 70):
+    ng = max(7, expected)
+    kv = np.arange(n, dtype=np.int64) % ng
+    for bad, want in ((np.nan, math.nan), (np.inf, math.inf), (-np.inf, -math.inf), (2.0 ** 70, None)):
         x = np.ones(n)
         x[n // 2] = bad
-        st = HashAggregateState(gpu_ctx, [N.TYPE_INT64], [(N.AGG_SUM, N.TYPE_FLOAT64)], expected, deterministic=True)
-        kc = DeviceColumn.from_numpy(N.TYPE_INT64, np.arange(n, dtype=np.int64) % max(7, expected), None, ctx=gpu_ctx)
-        with pytest.raises(Exception, match="fixed-point range"):
-            st.update([kc], [DeviceColumn.from_numpy(N.TYPE_FLOAT64, x, None, ctx=gpu_ctx)])
-            st.finalize()
+        st = HashAggregateState(gpu_ctx, [N.TYPE_INT64], [(N.AGG_SUM, N.TYPE_FLOAT64)], expected)
+        st.update([DeviceColumn.from_numpy(N.TYPE_INT64, kv, None, ctx=gpu_ctx)],
+                  [DeviceColumn.from_numpy(N.TYPE_FLOAT64, x, None, ctx=gpu_ctx)])
+        keys, vals = st.finalize()
+        got = dict(zip(keys[0].to_pylist(), vals[0].to_pylist()))
+        g = int(kv[n // 2])
+        for kk, v in got.items():
+            ref = math.fsum(x[kv == kk].tolist()) if kk != g or want is None else want
+            assert (math.isnan(v) and math.isnan(ref)) or v == ref, (bad, kk, v, ref)
+    x = np.ones(n)
+    x[n // 2] = 2.0 ** 127
+    st = HashAggregateState(gpu_ctx, [N.TYPE_INT64], [(N.AGG_SUM, N.TYPE_FLOAT64)], expected)
+    st.update([DeviceColumn.from_numpy(N.TYPE_INT64, kv, None, ctx=gpu_ctx)],
+              [DeviceColumn.from_numpy(N.TYPE_FLOAT64, x, None, ctx=gpu_ctx)])
+    with pytest.raises(Exception, match="not exact to 1e-9"):
+        st.finalize()
 
 
-def test_deterministic_inexact_bound(gpu_ctx):
-    """Values with bits below 2^-64 are rounded to multiples of 2^-64 and counted. A group whose
-    sum is large enough that the rounding (at most 2^-65 per input) stays within 1e-9 relative is
-    returned, deterministic and within 1e-9 of math.fsum; a group of values around 1e-25 (every
-    one rounded to 0) cannot be, and finalize fails instead of returning a wrong sum."""
+def test_exact_sum_inexact_bound(gpu_ctx):
+    """Values with bits below 2^-128 are rounded to multiples of 2^-128 (the group remembers that
+    one was). A group whose sum is large enough that the rounding (at most 2^-129 per input) stays
+    within 1e-9 relative is returned, deterministic and within 1e-9 of math.fsum — even a group of
+    values around 1e-25 alone; values that cancel exactly give exactly 0 (the old
+    2^-64 fixed point failed {3.7e-5, -3.7e-5}); a group of values around 1e-40 (each rounded to 0
+    or 2^-128) cannot be given to 1e-9, and finalize fails instead of returning a wrong sum."""
     import math
 
     from kquery import native as N
@@ -239,7 +259,7 @@ def test_deterministic_inexact_bound(gpu_ctx):
     x[::7] = 3.7e-5  # full-mantissa values under 2^-11: inexact
     outs = []
     for ctx in _runs(gpu_ctx):
-        st = HashAggregateState(ctx, [N.TYPE_INT64], [(N.AGG_SUM, N.TYPE_FLOAT64)], 64, deterministic=True)
+        st = HashAggregateState(ctx, [N.TYPE_INT64], [(N.AGG_SUM, N.TYPE_FLOAT64)], 64)
         st.update([DeviceColumn.from_numpy(N.TYPE_INT64, k, None, ctx=ctx)],
                   [DeviceColumn.from_numpy(N.TYPE_FLOAT64, x, None, ctx=ctx)])
         keys, vals = st.finalize()
@@ -251,11 +271,19 @@ def test_deterministic_inexact_bound(gpu_ctx):
         want = math.fsum(x[k == g].tolist())
         got = float(np.frombuffer(b, np.float64)[0])
         assert abs(got - want) <= 1e-9 * abs(want), (g, got, want)
-    # every value of group 1 is ~1e-25: its fixed-point sum is 0, off by 100 % of the exact sum
-    k2 = np.array([0, 1, 1, 1, 0], dtype=np.int64)
-    x2 = np.array([1.0, 1.1e-25, 0.9e-25, 1.3e-25, 2.0])
-    st = HashAggregateState(gpu_ctx, [N.TYPE_INT64], [(N.AGG_SUM, N.TYPE_FLOAT64)], 16, deterministic=True)
+    k2 = np.array([0, 1, 1, 1, 0, 2, 2], dtype=np.int64)
+    x2 = np.array([1.0, 1.1e-25, 0.9e-25, 1.3e-25, 2.0, 3.7e-5, -3.7e-5])
+    st = HashAggregateState(gpu_ctx, [N.TYPE_INT64], [(N.AGG_SUM, N.TYPE_FLOAT64)], 16)
     st.update([DeviceColumn.from_numpy(N.TYPE_INT64, k2, None, ctx=gpu_ctx)],
+              [DeviceColumn.from_numpy(N.TYPE_FLOAT64, x2, None, ctx=gpu_ctx)])
+    keys, vals = st.finalize()
+    got = dict(zip(keys[0].to_pylist(), vals[0].to_pylist()))
+    assert got[0] == 3.0 and got[2] == 0.0
+    assert abs(got[1] - math.fsum(x2[1:4].tolist())) <= 1e-9 * math.fsum(x2[1:4].tolist())
+    # every value of group 1 is ~1e-40: rounded to 0 or 2^-128 each, not within 1e-9 of the exact sum
+    x2 = np.array([1.0, 1.1e-40, 0.9e-40, 1.3e-40, 2.0])
+    st = HashAggregateState(gpu_ctx, [N.TYPE_INT64], [(N.AGG_SUM, N.TYPE_FLOAT64)], 16)
+    st.update([DeviceColumn.from_numpy(N.TYPE_INT64, k2[:5], None, ctx=gpu_ctx)],
               [DeviceColumn.from_numpy(N.TYPE_FLOAT64, x2, None, ctx=gpu_ctx)])
     with pytest.raises(Exception, match="not exact to 1e-9"):
         st.finalize()
