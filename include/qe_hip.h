@@ -283,7 +283,7 @@ int qe_hashagg_create(qe_ctx* ctx, int32_t nkeys, const int32_t* key_types, int3
  * reference's sequential row loop and ordered partition merge give with exact arithmetic
  * (K:617-631, K:1314-1325). NaN / +-Inf inputs give NaN / the infinity, as IEEE addition does.
  * finalize fails with QE_ERR_UNSUPPORTED instead of returning a group's sum when that group had
- * an input of magnitude 2^126 or more, or inputs with bits below 2^-128 whose rounding (half a
+ * an input of magnitude 2^182 (6e54) or more, or inputs with bits below 2^-128 whose rounding (half a
  * unit each) could exceed 1e-9 of the result. A state with exact sums synchronises in finalize to
  * check that (the outputs are complete when it returns).
  * QE_HASHAGG_DETERMINISTIC: the default (kept for callers that name it).

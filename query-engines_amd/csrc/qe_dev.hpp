@@ -81,6 +81,9 @@ struct DAgg {
   qi32 rhs;       // pkind 3: rhs slot, or -1 => literal
   qi32 rhs_null;  // pkind 3: literal is null
   qi64 rhs_lit;   // pkind 3: literal bits
+  qi32 share;     // i + 1: same input and accumulator as aggregate i (SUM / AVG of one expression);
+                  // the plan-specialised kernels keep one LDS accumulator for both (0: own)
+  qi32 pad;
   DTok tok[QE_MAX_TOKENS];
 };
 
@@ -196,7 +199,7 @@ __host__ __device__ inline qu64 idx_identity(int acc) { return acc_is_f64mm(acc)
 // A slot's fp64 SUM is a 256-bit two's complement integer W in units of 2^-128 (sum = W * 2^-128):
 // four 64-bit words w0..w3, w3 the signed top, plus a status word. Words live in acc (w0) and idx
 // words 0..2 (w1..w3); idx word 3 is the status:
-//   bits 0..7   flags, OR-ed: a NaN input, a +Inf input, a -Inf input, an input with |x| >= 2^126,
+//   bits 0..7   flags, OR-ed: a NaN input, a +Inf input, a -Inf input, an input with |x| >= 2^182,
 //               an input with bits below 2^-128 (rounded to the nearest multiple, ties to even)
 //   bits 8..63  signed count of net wraps of W: the exact sum is (W + wraps * 2^256) * 2^-128
 // A row adds its value's (at most 117-bit) two's complement image to the two words its mantissa
@@ -204,22 +207,32 @@ __host__ __device__ inline qu64 idx_identity(int acc) { return acc_is_f64mm(acc)
 // change of the running sum's sign moves on to the next word. Integer adds are associative, so any
 // order of rows, workgroups, passes, batches or ranks gives the same words: the result is the
 // correctly rounded exact sum, bit-identical run to run. NaN / +-Inf inputs give the IEEE result
-// of the sum (NaN, or the infinity); an input of 2^126 or more, or rounded inputs whose error bound
+// of the sum (NaN, or the infinity). An input in [2^126, 2^182) is exact too: its bits above the
+// words go straight into the wrap count (fx_row_words). An input of 2^182 or more, or rounded
+// inputs whose error bound
 // (non-null count x 2^-129) exceeds FX_REL_TOL of the result, make finalize fail (qe_hashagg.hip).
 constexpr qu64 FX_NAN = 1, FX_PINF = 2, FX_NINF = 4, FX_HUGE = 8, FX_INEXACT = 16, FX_FLAGS = 0xFF;
 constexpr qu64 FX_WRAP = 1ull << 8;  // one net wrap of W (signed count in bits 8..63)
 constexpr double FX_REL_TOL = 1e-9;
+// rare-path helpers of the exact sums: out of line unless a generated kernel asks otherwise
+#ifdef QE_FX_INLINE
+#define QE_FX_OUTLINE inline
+#else
+#define QE_FX_OUTLINE __attribute__((noinline))
+#endif
 constexpr int FX_LSB = 128;
 
-// One input's image: (hi:lo) two's complement at words k, k+1 (k < 0: nothing to add), sign
-// extended above; st = its status flags.
+// One input's image: (hi:lo) two's complement at words k, k+1 (k == -1: nothing to add; k == -2:
+// |x| in [2^126, 2^182), added as a whole partial, fx_row_words), sign extended above; st = its
+// status flags.
 struct FxRow {
   qu64 lo, hi, st;
   int k;
   bool neg;
+  qi64 bits;
 };
 __host__ __device__ inline FxRow fx_row(qi64 bits) {
-  FxRow r{0ull, 0ull, 0ull, -1, false};
+  FxRow r{0ull, 0ull, 0ull, -1, false, bits};
   const qu64 b = (qu64)bits;
   r.neg = b >> 63;
   const int ex = (int)((b >> 52) & 0x7FF);
@@ -245,7 +258,8 @@ __host__ __device__ inline FxRow fx_row(qi64 bits) {
     if (m == 0) return r;
   }
   if (p + 64 - __builtin_clzll(m) > 254) {  // |x| >= 2^126: beyond the words' headroom
-    r.st |= FX_HUGE;
+    if (p + 64 - __builtin_clzll(m) > 310) r.st |= FX_HUGE;  // >= 2^182: beyond the wrap count too
+    else r.k = -2;
     return r;
   }
   r.k = p >> 6;
@@ -294,7 +308,17 @@ __host__ __device__ inline void fx_status(qu64* st, qu64 v) {
 
 // One row into a slot whose word w is at wp(w).
 template <bool ATOMIC, class WP>
+__host__ __device__ inline void fx_add_words(WP wp, qu64 v0, qu64 v1, qu64 v2, qu64 v3, qu64 vst, qu64* st);
+__host__ __device__ inline void fx_row_words(qi64 bits, qu64 w[5]);
+
+template <bool ATOMIC, class WP>
 __host__ __device__ inline void fx_add_row(WP wp, const FxRow& r, qu64* st) {
+  if (r.k == -2) {  // [2^126, 2^182): the whole 320-bit image
+    qu64 w[5];
+    fx_row_words(r.bits, w);
+    fx_add_words<ATOMIC>(wp, w[0], w[1], w[2], w[3], w[4], st);
+    return;
+  }
   qu64 sd = r.st;
   if (r.k >= 0) {
     int w = r.k;
@@ -394,14 +418,33 @@ __host__ __device__ inline void fxw_words(qu64 u0, qu64 u1, qu64 u2, qu64 v[4]) 
   v[3] = (qu64)((qi64)u2 >> 32);
 }
 
-// The words of one input alone (RowVal form: the global-table and record paths).
+// The words of one input alone (RowVal form: the global-table and record paths): w[0..3] and the
+// status word (flags, and for |x| in [2^126, 2^182) the bits above the words as a wrap count).
 __host__ __device__ inline void fx_row_words(qi64 bits, qu64 w[5]) {
   const FxRow r = fx_row(bits);
-  for (int i = 0; i < 4; ++i) w[i] = (r.k >= 0 && i > r.k + 1 && r.neg) ? ~0ull : 0ull;
-  if (r.k >= 0) {
-    w[r.k] = r.lo;
-    if (r.k < 3) w[r.k + 1] = r.hi;
+  if (r.k == -2) {  // 320-bit image of m << p, p = exponent position in units of 2^-128
+    const qu64 b = (qu64)bits;
+    const qu64 m = (b & ((1ull << 52) - 1)) | (1ull << 52);
+    const int p = (int)((b >> 52) & 0x7FF) - 1075 + FX_LSB, a = p >> 6, sh = p & 63;
+    qu64 v[5];
+#pragma unroll
+    for (int i = 0; i < 5; ++i)  // (selects, not a dynamic index: the array stays in registers)
+      v[i] = i == a ? m << sh : (i == a + 1 && sh ? m >> (64 - sh) : 0ull);
+    if (r.neg) {
+      qu64 c = 1;
+      for (int i = 0; i < 5; ++i) {
+        v[i] = ~v[i] + c;
+        c = (c && v[i] == 0) ? 1ull : 0ull;
+      }
+    }
+    for (int i = 0; i < 4; ++i) w[i] = v[i];
+    const qi64 wraps = (qi64)v[4] + (qi64)(v[3] >> 63);  // with W's top word read as signed
+    w[4] = (qu64)wraps * FX_WRAP;
+    return;
   }
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+    w[i] = r.k < 0 ? 0ull : i == r.k ? r.lo : i == r.k + 1 ? r.hi : (i > r.k + 1 && r.neg) ? ~0ull : 0ull;
   w[4] = r.st;
 }
 
@@ -446,7 +489,7 @@ __host__ __device__ inline double fx_to_double(qu64 w0, qu64 w1, qu64 w2, qu64 w
 }
 
 // The SUM of a slot (`nn` non-null inputs). *err: the sum cannot be given within FX_REL_TOL of the
-// exact one (an input >= 2^126, or more rounding than the result's size allows).
+// exact one (an input >= 2^182, or more rounding than the result's size allows).
 __host__ __device__ inline double fx_result(qu64 w0, qu64 w1, qu64 w2, qu64 w3, qu64 st, qu64 nn, bool* err) {
   *err = false;
   const qu64 f = st & FX_FLAGS;
@@ -555,6 +598,25 @@ __device__ inline void gadd_cstar(const DTable& t, qu64 slot, qu64 c) {
 // Combine one aggregate's partial state into global slot `s` (device-scope atomics). add_nn =
 // false while the table keeps the aggregate's non-null count implicit (every input row so far was
 // non-null: nn == COUNT(*), read from cstar; see qe_hashagg.hip nn_implicit).
+// An exact fp64 SUM partial into global slot s (device-scope atomics). Out of line: the kernels call
+// it from their flush and from rare rows, and inlined copies of its carry chain at every such site
+// made the C5 fused kernel 8x larger than the instruction cache.
+static __device__ QE_FX_OUTLINE void gcombine_fx(const DTable& t, int j, qu64 s, qu64 w0, qu64 w1,
+                                                             qu64 w2, qu64 w3, qu64 st) {
+  const qu64 stride = t.cap + 2;
+  qu64* ix = t.idx[j];
+  fx_add_words<true>([&](int w) { return w == 0 ? (qu64*)&t.acc[j][s] : &ix[(w - 1) * stride + s]; }, w0, w1, w2, w3,
+                     st, &ix[3 * stride + s]);
+}
+
+// One row's exact fp64 SUM input into global slot s (rows whose group has no LDS slot), out of line.
+static __device__ QE_FX_OUTLINE void gcombine_fx_row(const DTable& t, int j, qu64 s, qi64 x, bool add_nn) {
+  qu64 w[5];
+  fx_row_words(x, w);
+  if (add_nn) atomicAdd(&t.nn[j][s], 1ull);
+  gcombine_fx(t, j, s, w[0], w[1], w[2], w[3], w[4]);
+}
+
 // An exact fp64 SUM partial may carry words with nn == 0: a rare input whose row was counted in an
 // LDS slot (fx_rare_global).
 __device__ inline void gcombine(const DTable& t, int acck, int j, qu64 s, qi64 acc, qu64 nn, qu64 i0, qu64 i1,
@@ -584,10 +646,7 @@ __device__ inline void gcombine(const DTable& t, int acck, int j, qu64 s, qi64 a
     if (i2 != ~0ull) atomicMin(&ix[2 * stride + s], i2);
     if (i3 != ~0ull) atomicMin(&ix[3 * stride + s], i3);
   } else if (acck == ACC_SUM_X) {  // 256-bit add with carries (words: acc, idx 0..2; status idx 3)
-    const qu64 stride = t.cap + 2;
-    qu64* ix = t.idx[j];
-    fx_add_words<true>([&](int w) { return w == 0 ? (qu64*)&t.acc[j][s] : &ix[(w - 1) * stride + s]; }, (qu64)acc,
-                       i0, i1, i2, i3, &ix[3 * stride + s]);
+    gcombine_fx(t, j, s, (qu64)acc, i0, i1, i2, i3);
   }
 }
 
@@ -683,17 +742,20 @@ __device__ inline void write_record_head(qu8* rec, qi64 key, bool knull, qu64 cs
   ((qu64*)rec)[2] = cstar;
 }
 
-// A queued exact-SUM input of aggregate j outside the LDS window (fx_rare; the specialised fused
-// kernel's fx queue): straight into its group's global slot — the row's COUNT(*) and non-null
-// count stay in the LDS slot, which the flush merges later — or, while the global table has no room
-// for the group, as an overflow record (COUNT(*) 0, identity partials but j) merged after the table
-// grows, like the flush's own records.
-__device__ inline void fx_rare_global(const Plan& P, int j, qi64 key, bool knull, qi64 x) {
+// A queued exact-SUM input outside the LDS window (fx_rare; the specialised fused kernel's fx queue)
+// for the aggregates in `jmask` (one, or several sharing one LDS accumulator: DAgg.share): straight
+// into its group's global slot — the row's COUNT(*) and non-null counts stay in the LDS slot, which
+// the flush merges later — or, while the global table has no room for the group, as an overflow
+// record (COUNT(*) 0, identity partials but those aggregates) merged after the table grows, like
+// the flush's own records.
+static __device__ QE_FX_OUTLINE void fx_rare_global(const Plan& P, qu32 jmask, qi64 key, bool knull,
+                                                                qi64 x) {
   qu64 w[5];
   fx_row_words(x, w);
   qu64 gs;
   if (gtable_find(P.t, key, knull, gs)) {
-    gcombine(P.t, ACC_SUM_X, j, gs, (qi64)w[0], 0, w[1], w[2], w[3], w[4], false);
+    for (int j = 0; j < P.naggs; ++j)
+      if ((jmask >> j) & 1) gcombine(P.t, ACC_SUM_X, j, gs, (qi64)w[0], 0, w[1], w[2], w[3], w[4], false);
     return;
   }
   const qu64 ri = atomicAdd(&P.t.ctl[2], 1ull);
@@ -707,10 +769,11 @@ __device__ inline void fx_rare_global(const Plan& P, int j, qi64 key, bool knull
   for (int a = 0; a < P.naggs; ++a) {
     qu64* f = (qu64*)(rec + off);
     const int acc = P.aggs[a].acc;
-    f[0] = a == j ? w[0] : (qu64)acc_identity(acc);
+    const bool mine = (jmask >> a) & 1;
+    f[0] = mine ? w[0] : (qu64)acc_identity(acc);
     f[1] = 0;
     if (acc_has_idx(acc))
-      for (int i = 0; i < 4; ++i) f[2 + i] = a == j ? w[1 + i] : idx_identity(acc);
+      for (int i = 0; i < 4; ++i) f[2 + i] = mine ? w[1 + i] : idx_identity(acc);
     off += agg_rec_bytes(acc);
   }
 }

@@ -1243,7 +1243,7 @@ __device__ __forceinline__ void put_bit(qu8* gbm, qu32* lbits, int col, qi64 o, 
 
 // An ACC_SUM_X slot's value (word 0 = acc, words 1..3 and the status word in idx; qe_dev.hpp
 // fx_result). A slot that cannot give its sum within FX_REL_TOL of the exact one (an input of
-// 2^126 or more, or rounded inputs whose error bound is too large for the result) is counted in
+// 2^182 or more, or rounded inputs whose error bound is too large for the result) is counted in
 // ctl[6], which finalize zeroes beforehand and reports.
 __device__ __forceinline__ double fx_sum(const DTable& t, int j, qu64 s, qi64 acc, qu64 nn) {
   const qu64 SS = t.cap + 2;
@@ -1796,6 +1796,22 @@ static int compile_plan(qe_hashagg* h, const qe_column* cols, int32_t ncols, con
       a.pkind = 2;
     }
   }
+  // aggregates that sum the same expression into the same kind of accumulator (TPC-H Q1's
+  // SUM(l_extendedprice) and AVG(l_extendedprice)) share one LDS accumulator in the specialised
+  // kernels; the global table and the output keep one per aggregate
+  for (int j = 0; j < h->naggs; ++j) {
+    DAgg& b = P->aggs[j];
+    if (b.pkind == 0 || (b.acc != ACC_SUM_I && b.acc != ACC_SUM_F && b.acc != ACC_SUM_X)) continue;
+    for (int i = 0; i < j; ++i) {
+      const DAgg& a = P->aggs[i];
+      if (a.share || a.acc != b.acc || a.pkind != b.pkind || a.track_nn != b.track_nn || a.col != b.col ||
+          a.cvt_i2f != b.cvt_i2f || a.ntok != b.ntok || a.bop != b.bop || a.rhs != b.rhs || a.rhs_null != b.rhs_null ||
+          a.rhs_lit != b.rhs_lit || memcmp(a.tok, b.tok, sizeof(DTok) * (size_t)a.ntok) != 0)
+        continue;
+      b.share = i + 1;
+      break;
+    }
+  }
   P->rec_bytes = h->rec_bytes;
   return QE_OK;
 }
@@ -1815,6 +1831,7 @@ static size_t lds_layout_at(const qe_hashagg* h, Plan* P, int log2, bool generic
   off = (off + 15) & ~size_t(15);
   for (int j = 0; j < h->naggs; ++j) {
     const DAgg& a = P->aggs[j];
+    if (!generic && a.share) continue;  // the specialised kernels read the shared accumulator
     if (a.acc != ACC_NONE) {
       P->off_acc[j] = (int32_t)off;
       off += 8 * SS;
@@ -2207,9 +2224,9 @@ static int launch_pass(qe_hashagg* h, Plan& P, size_t& lds, hipFunction_t pfn, i
   } else if (h->jit_note.rfind("partitioning unavailable", 0) != 0) {
     h->jit_note = lds ? "jit disabled" : "global-only launch";
   }
-  bool sum_x = false;
-  for (int j = 0; j < h->naggs; ++j) sum_x = sum_x || h->acc[j] == ACC_SUM_X;
-  if (!jfn && lds && (lds > HA_LDS_BUDGET || (sum_x && ctx->jit))) {
+  bool own_layout = false;  // the specialised kernels' LDS layout differs from the generic kernel's
+  for (int j = 0; j < h->naggs; ++j) own_layout = own_layout || h->acc[j] == ACC_SUM_X || P.aggs[j].share;
+  if (!jfn && lds && (lds > HA_LDS_BUDGET || (own_layout && ctx->jit))) {
     // the 152 KiB budget is for the specialised 1024-thread kernel (one per CU); the generic
     // 512-thread kernel runs two per CU, so its table is re-laid out within HA_LDS_BUDGET (and with
     // the generic kernel's full exact-SUM slots)
@@ -3010,7 +3027,7 @@ static int check_fx_final(qe_hashagg* h) {
   uint64_t c[8];
   QE_TRY(read_ctl(h, c));
   QE_CHECK(c[6] == 0, QE_ERR_UNSUPPORTED,
-           "fp64 SUM: %llu group results not exact to 1e-9 (an input of magnitude >= 2^126, or inputs with bits "
+           "fp64 SUM: %llu group results not exact to 1e-9 (an input of magnitude >= 2^182, or inputs with bits "
            "below 2^-128 whose rounding is too large for the result)",
            (unsigned long long)c[6]);
   return QE_OK;

@@ -291,6 +291,13 @@ void emit_lds_table(const Plan& P, std::ostringstream& o, int log2, size_t* lds_
   size_t lds = (size_t)SS * 12;
   for (int j = 0; j < P.naggs; ++j) {
     const DAgg& a = P.aggs[j];
+    if (a.share) {  // the accumulator of aggregate share - 1 (same input, same kind)
+      const int i = a.share - 1;
+      if (a.acc != ACC_NONE) o << "  qi64* const s_acc" << j << " = s_acc" << i << ";\n";
+      if (a.track_nn) o << "  qu32* const s_nn" << j << " = s_nn" << i << ";\n";
+      if (acc_has_idx(a.acc)) o << "  qu64* const s_idx" << j << " = s_idx" << i << ";\n";
+      continue;
+    }
     if (a.acc != ACC_NONE) {
       o << "  __shared__ qi64 s_acc" << j << "[SS];\n";
       lds += 8 * SS;
@@ -309,6 +316,7 @@ void emit_lds_table(const Plan& P, std::ostringstream& o, int log2, size_t* lds_
   o << "  for (int s = threadIdx.x; s < SS; s += blockDim.x) {\n    s_keys[s] = EMPTY_KEY;\n    s_cst[s] = 0;\n";
   for (int j = 0; j < P.naggs; ++j) {
     const DAgg& a = P.aggs[j];
+    if (a.share) continue;
     if (a.acc != ACC_NONE) o << "    s_acc" << j << "[s] = " << acc_init(a.acc) << ";\n";
     if (a.track_nn) o << "    s_nn" << j << "[s] = 0;\n";
     if (acc_has_idx(a.acc))
@@ -333,7 +341,7 @@ constexpr int FXQ_CAP = 128;
 std::vector<int> fx_queue_aggs(const Plan& P) {
   std::vector<int> q;
   for (int j = 0; j < P.naggs; ++j)
-    if (P.aggs[j].pkind != 0 && P.aggs[j].acc == ACC_SUM_X) q.push_back(j);
+    if (P.aggs[j].pkind != 0 && P.aggs[j].acc == ACC_SUM_X && !P.aggs[j].share) q.push_back(j);
   return q;
 }
 
@@ -398,24 +406,42 @@ void emit_fx_queue_run(const Plan& P, std::ostringstream& o, const std::string& 
   }
   o << "        if (rare) {\n          const bool knl = s == S;\n"
     << "          const qi64 key = knl ? 0 : (s == S + 1 ? EMPTY_KEY : s_keys[s]);\n";
-  for (int k = 0; k < nq; ++k)
-    o << "          if ((rare >> " << k << ") & 1u) fx_rare_global(P, " << q[k] << ", key, knl, q_x" << k << "[qp]);\n";
+  for (int k = 0; k < nq; ++k) {
+    unsigned jm = 1u << q[k];  // and every aggregate sharing its accumulator (their own global sums)
+    for (int j = 0; j < P.naggs; ++j)
+      if (P.aggs[j].share == q[k] + 1) jm |= 1u << j;
+    o << "          if ((rare >> " << k << ") & 1u) fx_rare_global(P, " << jm << "u, key, knl, q_x" << k << "[qp]);\n";
+  }
   o << "        }\n      }\n      __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, \"wavefront\");\n";
 }
 
 void emit_fx_queue_append(const Plan& P, std::ostringstream& o, const std::vector<std::string>& val,
                           const std::vector<std::string>& ok) {
   const std::vector<int> q = fx_queue_aggs(P);
-  o << "    {\n      const qu64 below = (1ull << lane) - 1;\n"
-    << "#pragma unroll\n      for (int r = 0; r < 4; ++r) {\n"
+  const int nq = (int)q.size();
+  // the 4 rows' entries in registers first (constant row indices), then ONE rolled loop over the
+  // rows appends them and drains full queues: an unrolled loop held 4 copies of the drain
+  // (QE_FXQ_ROLL=0: unrolled)
+  static const bool roll = [] {
+    const char* e = getenv("QE_FXQ_ROLL");
+    return !(e && e[0] == '0');
+  }();
+  o << "    {\n      qu32 qe4[4];\n";
+  for (int k = 0; k < nq; ++k) o << "      qi64 qx4_" << k << "[4];\n";
+  o << "#pragma unroll\n      for (int r = 0; r < 4; ++r) {\n        qu32 e = (qu32)slot[r];\n";
+  for (int k = 0; k < nq; ++k)
+    o << "        e |= (" << ok[q[k]] << " ? 1u : 0u) << " << 24 + k << ";\n        qx4_" << k << "[r] = " << val[q[k]] << ";\n";
+  o << "        qe4[r] = e;\n      }\n"
+    << "      const qu64 below = (1ull << lane) - 1;\n"
+    << "#pragma unroll " << (roll ? 1 : 4) << "\n      for (int r = 0; r < 4; ++r) {\n"
     << "        const bool qa = (loc >> r) & 1;\n        const qu64 bq = __ballot(qa);\n"
     << "        if (qa) {\n"
     << "          const qu32 qp = q_base + ((q_head + q_n + (qu32)__popcll(bq & below)) & " << FXQ_CAP - 1 << "u);\n"
-    << "          qu32 qe = (qu32)slot[r];\n";
-  for (size_t k = 0; k < q.size(); ++k)
-    o << "          qe |= (" << ok[q[k]] << " ? 1u : 0u) << " << 24 + k << ";\n          q_x" << k << "[qp] = " << val[q[k]]
-      << ";\n";
-  o << "          q_slot[qp] = qe;\n        }\n"
+    << "          q_slot[qp] = r == 0 ? qe4[0] : r == 1 ? qe4[1] : r == 2 ? qe4[2] : qe4[3];\n";
+  for (int k = 0; k < nq; ++k)
+    o << "          q_x" << k << "[qp] = r == 0 ? qx4_" << k << "[0] : r == 1 ? qx4_" << k << "[1] : r == 2 ? qx4_" << k
+      << "[2] : qx4_" << k << "[3];\n";
+  o << "        }\n"
     << "        q_n += (qu32)__popcll(bq);\n"
     << "        if (q_n >= 64u) {\n";
   emit_fx_queue_run(P, o, "64u");
@@ -453,7 +479,7 @@ void emit_agg_rows(const Plan& P, std::ostringstream& o, const std::vector<std::
     << "#pragma unroll\n    for (int r = 0; r < 4; ++r) if ((loc >> r) & 1) atomicAdd(&s_cst[slot[r]], 1u);\n";
   for (int j = 0; j < P.naggs; ++j) {
     const DAgg& a = P.aggs[j];
-    if (a.pkind == 0) continue;
+    if (a.pkind == 0 || a.share) continue;  // (a shared accumulator takes the row once)
     const std::string js = std::to_string(j);
     o << "    {\n#pragma unroll\n      for (int r = 0; r < 4; ++r) {\n"
       << "        if (!((loc >> r) & 1)) continue;\n"
@@ -489,9 +515,13 @@ void emit_agg_rows(const Plan& P, std::ostringstream& o, const std::vector<std::
   for (int j = 0; j < P.naggs; ++j) {
     const DAgg& a = P.aggs[j];
     if (a.pkind == 0) continue;
-    o << "        if (" << ok[j] << ") { const RowVal rv = row_partial(" << a.acc << ", " << val[j]
-      << ", row); gcombine(P.t, " << a.acc << ", " << j << ", gs, rv.acc, 1, rv.i0, rv.i1, rv.i2, rv.i3, "
-      << (((P.nn_skip >> j) & 1) ? "false" : "true") << "); }\n";
+    if (a.acc == ACC_SUM_X)  // (out of line: a rare path)
+      o << "        if (" << ok[j] << ") gcombine_fx_row(P.t, " << j << ", gs, " << val[j] << ", "
+        << (((P.nn_skip >> j) & 1) ? "false" : "true") << ");\n";
+    else
+      o << "        if (" << ok[j] << ") { const RowVal rv = row_partial(" << a.acc << ", " << val[j]
+        << ", row); gcombine(P.t, " << a.acc << ", " << j << ", gs, rv.acc, 1, rv.i0, rv.i1, rv.i2, rv.i3, "
+        << (((P.nn_skip >> j) & 1) ? "false" : "true") << "); }\n";
   }
   o << "      }\n    }\n";
   if (fx_queue) emit_fx_queue_append(P, o, val, ok);
@@ -859,7 +889,11 @@ bool gen_fused_source(const Plan& P, int log2, std::string* src, size_t* lds_byt
   if (compact) emit_flush_c(P, o);
   else emit_flush(P, o);
   o << "  __syncthreads();\n  if (threadIdx.x == 0 && s_newg) atomicAdd(&P.t.ctl[0], (qu64)s_newg);\n}\n";
-  *src = std::string(kDevHeader) + o.str();
+  static const bool fx_inline = [] {  // QE_FX_INLINE=1: the exact sums' rare paths inline (A/B knob)
+    const char* e = getenv("QE_FX_INLINE");
+    return e && e[0] == '1';
+  }();
+  *src = std::string(fx_inline ? "#define QE_FX_INLINE 1\n" : "") + kDevHeader + o.str();
   return true;
 }
 

@@ -115,6 +115,10 @@ static int emit_agg(const char* dir, const char* name, const qe_column* cols, in
     P.aggs[j].track_nn = nullable ? 1 : 0;
     P.aggs[j].pkind = aggs[j].prog ? 2 : 0;  // token program (compile_plan's general form)
   }
+  // the same input summed twice (SUM and AVG of one column): one shared LDS accumulator, as
+  // compile_plan marks it
+  for (int j = 1; j < naggs; ++j)
+    if (aggs[j].prog && aggs[j].prog == aggs[0].prog && aggs[j].acc == aggs[0].acc) P.aggs[j].share = 1;
   P.mp_n = 2;
   P.mp_pass = 0;
   std::string a, b, c;
@@ -187,6 +191,92 @@ static int emit_agg(const char* dir, const char* name, const qe_column* cols, in
          write_src(dir, std::string(name) + "_spill_n32", k) | write_src(dir, std::string(name) + "_pagg_soa_n32", l);
 }
 
+// The C5 plan (BASELINE configs[4], kquery/workloads.py c5_spec): 7 columns, 4 predicate terms, two
+// packed uint8 keys, SUM(qty) int64, 3 exact fp64 SUMs and an AVG sharing the first one's
+// accumulator, COUNT(*); single pass over a 256-slot table (the fx queue path).
+static int emit_c5(const char* dir) {
+  static int64_t i64d[64];
+  static double f64d[64];
+  static uint8_t u8d[64];
+  static int32_t i32d[64];
+  qe_column cols[7];
+  memset(cols, 0, sizeof cols);
+  const int32_t types[7] = {QE_TYPE_INT64, QE_TYPE_FLOAT64, QE_TYPE_FLOAT64, QE_TYPE_FLOAT64, QE_TYPE_UINT8,
+                            QE_TYPE_UINT8, QE_TYPE_DATE32};
+  void* vals[7] = {i64d, f64d, f64d, f64d, u8d, u8d, i32d};
+  for (int c = 0; c < 7; ++c) {
+    cols[c].type = types[c];
+    cols[c].length = 1000;
+    cols[c].values = vals[c];
+  }
+  qe_pred_term t[4] = {term(6, QE_OP_LE, 2400), term(2, QE_OP_GE, 0), term(2, QE_OP_LE, 0), term(0, QE_OP_LT, 24)};
+  for (int i = 1; i <= 2; ++i) {
+    t[i].lit.type = QE_TYPE_FLOAT64;
+    const double d = i == 1 ? 0.05 : 0.07;
+    memcpy(&t[i].lit.bits, &d, 8);
+  }
+  Plan P;
+  bool col_f64[QE_MAX_COLS];
+  if (compile_inputs(cols, 7, -1, 4, t, &P, col_f64) != QE_OK) return 1;
+  P.key_mode = 2;
+  P.nkeys = 2;
+  P.key_col[0] = 4;
+  P.key_col[1] = 5;
+  P.key_shift[0] = 0;
+  P.key_fmask[0] = 0xFF;
+  P.key_nullbit[0] = 8;
+  P.key_shift[1] = 9;
+  P.key_fmask[1] = 0xFF;
+  P.key_nullbit[1] = 17;
+  auto tok = [](int op, int arg, double lit) {
+    qe_token k;
+    memset(&k, 0, sizeof k);
+    k.op = op;
+    k.arg = arg;
+    if (op == QE_TOK_LIT) {
+      k.lit.type = QE_TYPE_FLOAT64;
+      memcpy(&k.lit.bits, &lit, 8);
+    }
+    return k;
+  };
+  qe_agg_program pr[5];
+  memset(pr, 0, sizeof pr);
+  pr[0].ntokens = 1;
+  pr[0].tokens[0] = tok(QE_TOK_COL, 0, 0);
+  pr[1].ntokens = 1;
+  pr[1].tokens[0] = tok(QE_TOK_COL, 1, 0);
+  const qe_token dp[5] = {tok(QE_TOK_COL, 1, 0), tok(QE_TOK_LIT, 0, 1.0), tok(QE_TOK_COL, 2, 0), tok(QE_TOK_SUB, 0, 0),
+                          tok(QE_TOK_MUL, 0, 0)};
+  pr[2].ntokens = 5;
+  for (int i = 0; i < 5; ++i) pr[2].tokens[i] = dp[i];
+  pr[3] = pr[2];
+  pr[3].ntokens = 9;
+  pr[3].tokens[5] = tok(QE_TOK_LIT, 0, 1.0);
+  pr[3].tokens[6] = tok(QE_TOK_COL, 3, 0);
+  pr[3].tokens[7] = tok(QE_TOK_ADD, 0, 0);
+  pr[3].tokens[8] = tok(QE_TOK_MUL, 0, 0);
+  pr[4] = pr[1];
+  const int fns[6] = {QE_AGG_SUM, QE_AGG_SUM, QE_AGG_SUM, QE_AGG_SUM, QE_AGG_AVG, QE_AGG_COUNT_STAR};
+  const int accs[6] = {ACC_SUM_I, ACC_SUM_X, ACC_SUM_X, ACC_SUM_X, ACC_SUM_X, ACC_NONE};
+  P.naggs = 6;
+  for (int j = 0; j < 6; ++j) {
+    memset(&P.aggs[j], 0, sizeof P.aggs[j]);
+    if (j < 5) {
+      bool is_f = false, nullable = false;
+      if (compile_program(cols, 7, col_f64, pr[j], j, &P.aggs[j], &is_f, &nullable) != QE_OK) return 1;
+      P.aggs[j].pkind = P.aggs[j].ntok == 1 ? 1 : 2;
+      P.aggs[j].col = P.aggs[j].tok[0].arg;
+    }
+    P.aggs[j].fn = fns[j];
+    P.aggs[j].acc = accs[j];
+  }
+  P.aggs[4].share = 2;  // AVG(l_extendedprice) reads SUM(l_extendedprice)'s accumulator
+  std::string src;
+  size_t lds = 0;
+  if (!gen_fused_source(P, 8, &src, &lds, false)) return 1;
+  return write_src(dir, "c5_fused1", src);
+}
+
 int main(int argc, char** argv) {
   if (argc < 2) return 2;
   static int64_t dummy[64];
@@ -245,5 +335,6 @@ int main(int argc, char** argv) {
   // deterministic state: fp64 SUM and AVG in exact fixed point (ACC_SUM_X)
   const AggIn dx[3] = {{QE_AGG_SUM, ACC_SUM_X, &pb}, {QE_AGG_AVG, ACC_SUM_X, &pb}, {QE_AGG_COUNT_STAR, ACC_NONE, nullptr}};
   rc |= emit_agg(argv[1], "det", cols, 3, &t4, 1, dx, 3, 10);
+  rc |= emit_c5(argv[1]);
   return rc;
 }

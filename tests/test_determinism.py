@@ -207,8 +207,9 @@ def test_deterministic_fp64_group_sums(gpu_ctx, groups, expected, path):
 @pytest.mark.parametrize("expected", [16, 4500, 50_000])
 def test_exact_sum_specials(gpu_ctx, expected):
     """IEEE specials and large inputs on the LDS, two-bucket and radix-partitioned paths: NaN and
-    +-Inf give the IEEE result of the sum in their group only; 2^70 (outside the LDS window, in the
-    global accumulator) is summed exactly; an input of 2^127 cannot be, and finalize reports it."""
+    +-Inf give the IEEE result of the sum in their group only; 2^70 and 2^150 (outside the LDS
+    window, in the global accumulator) are summed exactly; an input of 2^190 cannot be, and finalize
+    reports it."""
     import math
 
     from kquery import native as N
@@ -218,7 +219,8 @@ def test_exact_sum_specials(gpu_ctx, expected):
     n = 200_000
     ng = max(7, expected)
     kv = np.arange(n, dtype=np.int64) % ng
-    for bad, want in ((np.nan, math.nan), (np.inf, math.inf), (-np.inf, -math.inf), (2.0 ** 70, None)):
+    for bad, want in ((np.nan, math.nan), (np.inf, math.inf), (-np.inf, -math.inf), (2.0 ** 70, None),
+                      (2.0 ** 150, None)):
         x = np.ones(n)
         x[n // 2] = bad
         st = HashAggregateState(gpu_ctx, [N.TYPE_INT64], [(N.AGG_SUM, N.TYPE_FLOAT64)], expected)
@@ -231,7 +233,7 @@ def test_exact_sum_specials(gpu_ctx, expected):
             ref = math.fsum(x[kv == kk].tolist()) if kk != g or want is None else want
             assert (math.isnan(v) and math.isnan(ref)) or v == ref, (bad, kk, v, ref)
     x = np.ones(n)
-    x[n // 2] = 2.0 ** 127
+    x[n // 2] = 2.0 ** 190
     st = HashAggregateState(gpu_ctx, [N.TYPE_INT64], [(N.AGG_SUM, N.TYPE_FLOAT64)], expected)
     st.update([DeviceColumn.from_numpy(N.TYPE_INT64, kv, None, ctx=gpu_ctx)],
               [DeviceColumn.from_numpy(N.TYPE_FLOAT64, x, None, ctx=gpu_ctx)])

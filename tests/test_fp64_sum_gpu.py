@@ -103,7 +103,7 @@ def test_fp64_sum_adversarial(gpu_ctx, groups, expected, path, deterministic):
 
 
 def test_fp64_sum_finalize_errors_do_not_stick(gpu_ctx):
-    """An input of 2^126 or more cannot be summed exactly: finalize reports it (never a silently
+    """An input of 2^182 or more cannot be summed exactly: finalize reports it (never a silently
     wrong sum). The failure does not leak into the state's later calls: more updates still run,
     and after a reset the state is clean (the old ctl[6] count was never cleared)."""
     from kquery import native as N
@@ -113,7 +113,7 @@ def test_fp64_sum_finalize_errors_do_not_stick(gpu_ctx):
     st = HashAggregateState(gpu_ctx, [N.TYPE_INT64], [(N.AGG_SUM, N.TYPE_FLOAT64)], 16)
     k = np.arange(1000, dtype=np.int64) % 7
     x = np.ones(1000)
-    x[500] = 2.0 ** 127
+    x[500] = 2.0 ** 200
     st.update([DeviceColumn.from_numpy(N.TYPE_INT64, k, None, ctx=gpu_ctx)],
               [DeviceColumn.from_numpy(N.TYPE_FLOAT64, x, None, ctx=gpu_ctx)])
     with pytest.raises(Exception, match="not exact to 1e-9"):

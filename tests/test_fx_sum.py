@@ -126,10 +126,12 @@ def test_ieee_specials(fx):
     assert fx([1.0, -inf])[0] == -inf
     v, err, _ = fx([inf, -inf, 1.0])
     assert math.isnan(v) and not err
-    v, err, _ = fx([2.0 ** 126, 1.0])  # beyond the words' headroom: reported, not approximated
+    for big in ([2.0 ** 126, 1.0], [2.0 ** 125, 1.0], [-(2.0 ** 181) * 1.5, 3.0, 2.0 ** 140, -1e-20],
+                [1e50, -1e50, 7.0], [2.0 ** 181, 2.0 ** 181, -(2.0 ** 170)]):
+        v, err, _ = fx(big, 2)  # up to 2^182: the bits above the words go to the wrap count
+        assert not err and same(v, exact(big)), big
+    v, err, _ = fx([2.0 ** 182, 1.0])  # beyond the wrap count too: reported, not approximated
     assert err
-    v, err, _ = fx([2.0 ** 125, 1.0])
-    assert not err and same(v, exact([2.0 ** 125, 1.0]))
     v, err, _ = fx([np.finfo(np.float64).max])
     assert err
 

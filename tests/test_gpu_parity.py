@@ -650,10 +650,10 @@ MP_F64 = [N.AGG_SUM, N.AGG_COUNT, N.AGG_MAX]
 
 
 @pytest.mark.parametrize("vtype,ngroups,expected", [("i64", 4500, 4500), ("i64", 40_000, 4000),
-                                                    ("f64", 1600, 1600), ("f64", 40_000, 1600)])
+                                                    ("f64", 1200, 1200), ("f64", 40_000, 1200)])
 def test_hashagg_multipass(agg_ctx, mp_mode, vtype, ngroups, expected):
     """Expected groups just beyond one LDS table (the specialised kernel's table takes up to
-    152 KiB: ~2.5K groups of the i64 shape, ~0.8K of the f64 one, whose exact SUM keeps a 24-byte
+    152 KiB: ~2.5K groups of the i64 shape, ~0.6K of the f64 one, whose exact SUM keeps a 24-byte
     window per slot): 2 passes of the fused kernel,
     each keeping one bucket of key hashes (also when far more groups turn up than expected:
     overflow records and deferred rows inside a pass). Nullable keys and inputs, fp64 MAX order
