@@ -373,10 +373,12 @@ int qe_select_project(qe_ctx* ctx, const qe_column* cols, int32_t ncols, const q
  * that call waits for this select-project's row count only — not for work queued behind it, such
  * as the next batch's select-project — and returns it. Where the kernel publishes the count itself
  * (the register-resident pass and the two-pass write kernel) the wait polls that word in pinned
- * memory and may return while the kernel's last stores drain: the outputs are then complete for
- * every later operation on ctx's stream (and after a synchronisation of it), as for any
- * stream-ordered call. The inputs must stay valid until the wait returns.
- * qe_select_project = async + wait. */
+ * memory and may return while the kernel still reads its inputs and writes its outputs. So, as for
+ * any stream-ordered call: the outputs are complete for every later operation on ctx's stream, and
+ * for other streams or the host only after ctx's stream work has completed (qe_ctx_synchronize);
+ * the inputs must stay valid until then too — not merely until the wait returns.
+ * qe_select_project = async + wait + a synchronisation of ctx's stream: when it returns, the
+ * kernels have completed (inputs may be released, outputs read anywhere). */
 typedef struct qe_select_pending qe_select_pending;
 int qe_select_project_async(qe_ctx* ctx, const qe_column* cols, int32_t ncols, const qe_select_spec* spec,
                             qe_column* outs, qe_select_pending** pending);
@@ -448,6 +450,14 @@ typedef struct qe_comm qe_comm;
 int qe_comm_unique_id(void* id /* QE_COMM_ID_BYTES */);
 int qe_comm_create(qe_ctx* ctx, int32_t world, int32_t rank, const void* id, qe_comm** out);
 int qe_comm_destroy(qe_comm* comm);
+/* In-process transport: `world` ranks that are threads of one process, each with its own qe_ctx
+ * (one GPU, or several), share a hub; qe_hashagg_exchange then runs its usual export -> grouped
+ * send/recv -> import with device copies in place of RCCL (every rank must call it concurrently,
+ * as with RCCL). For hosts that run several partitions in one process and for the multi-rank tests
+ * on a one-GPU box (RCCL refuses two ranks on one device). The hub outlives its communicators. */
+int qe_comm_loopback_hub_create(int32_t world, void** hub);
+int qe_comm_loopback_hub_destroy(void* hub);
+int qe_comm_create_loopback(qe_ctx* ctx, int32_t world, int32_t rank, void* hub, qe_comm** out);
 /* Every rank: move each group of `partial` to the rank that owns its key (hash(key) mod world,
  * as qe_hashagg_export) and merge what this rank receives into `owner` (K:1309-1325 across GPUs).
  * Fixed slots of `slot_records` groups per destination (<= 0: the expected groups spread over the

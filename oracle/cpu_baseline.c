@@ -16,6 +16,7 @@
  * The synthetic columns are regenerated here bit-for-bit (splitmix64, oracle/gen.py) before the
  * timed region starts.
  */
+#include <math.h>
 #include <pthread.h>
 #include <stdint.h>
 #include <stdlib.h>
@@ -517,5 +518,113 @@ double qe_cpu_c4_fast(int64_t row0, int64_t rows, uint64_t seed, int threads, in
   free(k);
   free(a);
   free(b);
+  return bad ? -1.0 : t1 - t0;
+}
+
+/* ---- C5 (BASELINE configs[4]) with exact fp64 sums: the full-size per-group check's oracle ----------
+ * SELECT l_returnflag, l_linestatus, SUM(l_quantity), SUM(l_extendedprice),
+ *        SUM(l_extendedprice * (1 - l_discount)), SUM(l_extendedprice * (1 - l_discount) * (1 + l_tax)),
+ *        AVG(l_extendedprice), COUNT(*)
+ * WHERE l_shipdate <= 2400 AND l_discount >= 0.05 AND l_discount <= 0.07 AND l_quantity < 24
+ * GROUP BY l_returnflag, l_linestatus          (kquery/workloads.py c5_spec; columns datasource.py)
+ * Rows are regenerated bit for bit (generator column ids 10..16). Each fp64 value is added EXACTLY:
+ * as an integer in units of 2^-80 (every value of this data is a multiple of that, checked; the
+ * per-group totals stay below 2^125), so the sums are the exact sums of the rows' fp64 values —
+ * the reference's sequential loop with exact arithmetic. The caller rounds them once (Python
+ * Fraction -> float). out[g * 8 + ...], g = returnflag * 2 + linestatus:
+ *   [0] COUNT(*)  [1] SUM(quantity) (int64, wraps)  [2..3] SUM(price)  [4..5] SUM(price*(1-d))
+ *   [6..7] SUM(price*(1-d)*(1+t)); each exact sum as (signed high 64 bits, low 64 bits).
+ * Returns seconds, or -1 if a value was not a multiple of 2^-80. */
+typedef struct {
+  int64_t row0, n;
+  uint64_t seed;
+  int64_t cnt[6], sq[6];
+  __int128 s[3][6];
+  int bad;
+} c5_job;
+
+static int c5_fixed(double v, __int128* out) { /* v * 2^80 as an exact integer */
+  if (v == 0.0) {
+    *out = 0;
+    return 1;
+  }
+  int e;
+  const double m = frexp(v, &e);              /* v = m * 2^e, 0.5 <= |m| < 1 */
+  const int64_t M = (int64_t)ldexp(m, 53);    /* exact: 53-bit mantissa */
+  const int sh = e - 53 + 80;
+  if (sh >= 0) {
+    if (sh > 70) return 0;
+    *out = (__int128)M << sh;
+    return 1;
+  }
+  if (-sh >= 63 || (M & ((1ll << -sh) - 1)) != 0) return 0;
+  *out = (__int128)(M >> -sh);
+  return 1;
+}
+
+static void* c5_main(void* arg) {
+  c5_job* j = (c5_job*)arg;
+  for (int64_t i = 0; i < j->n; ++i) {
+    const uint64_t r = (uint64_t)(j->row0 + i);
+    const int64_t qty = (int64_t)(gen_u64(j->seed, 10, r) % 50ull);
+    const double price = (double)(gen_u64(j->seed, 11, r) % 10000000ull) * 0.01;
+    const double disc = (double)(gen_u64(j->seed, 12, r) % 11ull) * 0.01;
+    const double tax = (double)(gen_u64(j->seed, 13, r) % 9ull) * 0.01;
+    const int flag = (int)(gen_u64(j->seed, 14, r) % 3ull);
+    const int status = (int)(gen_u64(j->seed, 15, r) % 2ull);
+    const int32_t ship = (int32_t)(gen_u64(j->seed, 16, r) % 2557ull);
+    if (!(ship <= 2400 && disc >= 0.05 && disc <= 0.07 && qty < 24)) continue;
+    const double dp = price * (1.0 - disc);
+    const double dpt = dp * (1.0 + tax);
+    const int g = flag * 2 + status;
+    __int128 a, b, c;
+    if (!c5_fixed(price, &a) || !c5_fixed(dp, &b) || !c5_fixed(dpt, &c)) {
+      j->bad = 1;
+      continue;
+    }
+    j->cnt[g] += 1;
+    j->sq[g] = (int64_t)((uint64_t)j->sq[g] + (uint64_t)qty);
+    j->s[0][g] += a;
+    j->s[1][g] += b;
+    j->s[2][g] += c;
+  }
+  return NULL;
+}
+
+double qe_cpu_c5_exact(int64_t row0, int64_t rows, uint64_t seed, int threads, int64_t* out) {
+  if (threads < 1) threads = 1;
+  c5_job* jobs = (c5_job*)calloc(threads, sizeof(c5_job));
+  pthread_t* tid = (pthread_t*)calloc(threads, sizeof(pthread_t));
+  const int64_t per = (rows + threads - 1) / threads;
+  const double t0 = now_s();
+  for (int t = 0; t < threads; ++t) {
+    const int64_t s = t * per, e = (s + per < rows) ? s + per : rows;
+    jobs[t].row0 = row0 + s;
+    jobs[t].n = e > s ? e - s : 0;
+    jobs[t].seed = seed;
+    pthread_create(&tid[t], NULL, c5_main, &jobs[t]);
+  }
+  for (int t = 0; t < threads; ++t) pthread_join(tid[t], NULL);
+  int bad = 0;
+  for (int g = 0; g < 6; ++g) {
+    int64_t cnt = 0;
+    uint64_t sq = 0;
+    __int128 s[3] = {0, 0, 0};
+    for (int t = 0; t < threads; ++t) {
+      bad |= jobs[t].bad;
+      cnt += jobs[t].cnt[g];
+      sq += (uint64_t)jobs[t].sq[g];
+      for (int k = 0; k < 3; ++k) s[k] += jobs[t].s[k][g];
+    }
+    out[g * 8 + 0] = cnt;
+    out[g * 8 + 1] = (int64_t)sq;
+    for (int k = 0; k < 3; ++k) {
+      out[g * 8 + 2 + 2 * k] = (int64_t)(s[k] >> 64);
+      out[g * 8 + 3 + 2 * k] = (int64_t)(uint64_t)s[k];
+    }
+  }
+  const double t1 = now_s();
+  free(jobs);
+  free(tid);
   return bad ? -1.0 : t1 - t0;
 }

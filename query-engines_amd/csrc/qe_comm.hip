@@ -17,6 +17,7 @@
 #include <rccl/rccl.h>
 #include <string.h>
 
+#include <condition_variable>
 #include <mutex>
 #include <string>
 #include <type_traits>
@@ -81,9 +82,36 @@ const Rccl& rccl() {
 
 }  // namespace
 
+// In-process transport (qe_comm_create_loopback): the ranks are threads of one process, each with
+// its own qe_ctx; a grouped send/recv becomes "publish my send buffers, wait for every rank, copy
+// what the peers address to me, wait again". The hash-aggregate exchange above it is the same code
+// as over RCCL — what a single-GPU box can run of the multi-rank path (RCCL refuses two ranks on
+// one device).
+struct qe_loop_hub {
+  int32_t world = 0;
+  std::mutex mu;
+  std::condition_variable cv;
+  int32_t arrived = 0;
+  uint64_t generation = 0;
+  std::vector<const uint8_t*> send;
+  std::vector<const size_t*> soff, sbytes;
+  void barrier() {
+    std::unique_lock<std::mutex> g(mu);
+    const uint64_t gen = generation;
+    if (++arrived == world) {
+      arrived = 0;
+      ++generation;
+      cv.notify_all();
+    } else {
+      cv.wait(g, [&] { return generation != gen; });
+    }
+  }
+};
+
 struct qe_comm {
   qe_ctx* ctx = nullptr;
   ncclComm_t comm = nullptr;
+  qe_loop_hub* hub = nullptr;  // in-process transport instead of RCCL
   int32_t world = 0, rank = 0;
   uint8_t* buf = nullptr;  // send | recv slots (device), grown as needed
   size_t buf_bytes = 0;
@@ -106,6 +134,26 @@ int comm_buffer(qe_comm* c, size_t bytes) {
 // Grouped point-to-point: rank p gets send + soff[p] (sbytes[p] bytes) into recv + roff[p].
 int exchange_bytes(qe_comm* c, const uint8_t* send, const size_t* soff, const size_t* sbytes, uint8_t* recv,
                    const size_t* roff, const size_t* rbytes) {
+  if (c->hub) {  // in-process ranks: publish, wait, copy what the peers address to this rank, wait
+    qe_loop_hub* h = c->hub;
+    QE_TRY(ctx_sync(c->ctx));  // the send buffers are complete
+    h->send[c->rank] = send;
+    h->soff[c->rank] = soff;
+    h->sbytes[c->rank] = sbytes;
+    h->barrier();
+    int st = QE_OK;
+    for (int p = 0; p < c->world && st == QE_OK; ++p) {
+      if (h->sbytes[p][c->rank] != rbytes[p])
+        st = fail(QE_ERR_COMM, "loopback exchange: rank %d sends %zu bytes to rank %d, which expects %zu", p,
+                  h->sbytes[p][c->rank], c->rank, rbytes[p]);
+      else if (rbytes[p] && hipMemcpyAsync(recv + roff[p], h->send[p] + h->soff[p][c->rank], rbytes[p],
+                                           hipMemcpyDeviceToDevice, c->ctx->stream) != hipSuccess)
+        st = fail(QE_ERR_DEVICE, "loopback exchange: copy from rank %d failed", p);
+    }
+    if (st == QE_OK) st = ctx_sync(c->ctx);
+    h->barrier();  // every rank has copied out of every send buffer before any is reused
+    return st;
+  }
   const Rccl& R = rccl();
   QE_NCCL(R.group_start());
   ncclResult_t r = ncclSuccess;
@@ -159,6 +207,35 @@ int qe_comm_destroy(qe_comm* c) {
   dev_free(c->ctx, c->buf);
   if (c->comm) (void)rccl().comm_destroy(c->comm);
   delete c;
+  return QE_OK;
+}
+
+int qe_comm_loopback_hub_create(int32_t world, void** hub) {
+  QE_CHECK(hub && world >= 1, QE_ERR_INVALID_ARG, "bad arguments");
+  qe_loop_hub* h = new qe_loop_hub();
+  h->world = world;
+  h->send.assign(world, nullptr);
+  h->soff.assign(world, nullptr);
+  h->sbytes.assign(world, nullptr);
+  *hub = h;
+  return QE_OK;
+}
+
+int qe_comm_loopback_hub_destroy(void* hub) {
+  delete (qe_loop_hub*)hub;
+  return QE_OK;
+}
+
+int qe_comm_create_loopback(qe_ctx* ctx, int32_t world, int32_t rank, void* hub, qe_comm** out) {
+  QE_TRY(ctx_enter(ctx));
+  qe_loop_hub* h = (qe_loop_hub*)hub;
+  QE_CHECK(out && h && world == h->world && rank >= 0 && rank < world, QE_ERR_INVALID_ARG, "bad arguments");
+  qe_comm* c = new qe_comm();
+  c->ctx = ctx;
+  c->hub = h;
+  c->world = world;
+  c->rank = rank;
+  *out = c;
   return QE_OK;
 }
 

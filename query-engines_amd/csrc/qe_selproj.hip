@@ -479,6 +479,11 @@ int qe_select_project(qe_ctx* ctx, const qe_column* cols, int32_t ncols, const q
   qe_select_pending* r = nullptr;
   QE_TRY(qe_select_project_async(ctx, cols, ncols, spec, outs, &r));
   QE_TRY(qe_select_pending_wait(r, out_count));
+  // the count can be published before the kernel's last loads and stores retire (the resident
+  // pass publishes after its final prefix; the two-pass write kernel's last tile before the
+  // others finish): a synchronous call returns only once the kernels have completed, so its inputs
+  // may be released and its outputs read from any stream
+  QE_TRY(ctx_sync(ctx));
   for (int k = 0; k < spec->nout; ++k) outs[k].length = *out_count;
   return QE_OK;
 }

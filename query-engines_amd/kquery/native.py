@@ -234,6 +234,9 @@ SIGNATURES = [
     ("qe_comm_unique_id", C.c_int, [_P]),
     ("qe_comm_create", C.c_int, [_P, C.c_int32, C.c_int32, _P, C.POINTER(C.c_void_p)]),
     ("qe_comm_destroy", C.c_int, [_P]),
+    ("qe_comm_loopback_hub_create", C.c_int, [C.c_int32, C.POINTER(C.c_void_p)]),
+    ("qe_comm_loopback_hub_destroy", C.c_int, [_P]),
+    ("qe_comm_create_loopback", C.c_int, [_P, C.c_int32, C.c_int32, _P, C.POINTER(C.c_void_p)]),
     ("qe_hashagg_exchange", C.c_int, [_P, _P, _P, C.c_int64, _I64P]),
     ("qe_hashagg_set_row_base", C.c_int, [_P, C.c_int64]),
     ("qe_hashagg_set_async", C.c_int, [_P, C.c_int32]),

@@ -113,8 +113,9 @@ def main():
             torch.cuda.synchronize()
             return statistics.median(ts)
 
-        ms_wall = wall(run_kernel)
-        # host split of one call: enqueue (qe_select_project_async) and wait (qe_select_pending_wait)
+        ms_wall = wall(run_kernel)  # synchronous call: returns once the kernels have completed
+        # host split of one stream-ordered call: enqueue (qe_select_project_async) and the time to
+        # the row count (qe_select_pending_wait; the kernel's last stores may still be in flight)
         enq, wt = [], []
         for it in range(35):
             torch.cuda.synchronize()
@@ -153,7 +154,8 @@ def main():
         report("C2 fused select+project (qe_select_project), 10M int64", n, 16 + 8 * sel_rows / n, ms_f,
                selected=sel_rows, call_ms=ms_k, call_gbs=n * (16 + 8 * sel_rows / n) / (ms_k * 1e-3) / 1e9,
                call_cold_ms=ms_cold, call_cold_gbs=n * (16 + 8 * sel_rows / n) / (ms_cold * 1e-3) / 1e9,
-               call_wall_ms=ms_wall, call_enqueue_ms=ms_enq, call_wait_ms=ms_wait,
+               call_wall_ms=ms_wall, call_wall_gbs=n * (16 + 8 * sel_rows / n) / (ms_wall * 1e-3) / 1e9,
+               call_enqueue_ms=ms_enq, call_time_to_count_ms=ms_wait,
                call_cold_wall_ms=ms_cold_wall, call_cold_clean_wall_ms=ms_clean_wall,
                call_cold_clean_frac=n * (16 + 8 * sel_rows / n) / (ms_clean_wall * 1e-3) / 8e12,
                path="one hipRTC-specialised kernel: predicate, look-back compaction, projection")
