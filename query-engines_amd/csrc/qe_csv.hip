@@ -556,6 +556,143 @@ __global__ void __launch_bounds__(256) k_csv_lines(const uint8_t* __restrict__ d
   }
 }
 
+// Terminator and delimiter masks of a lane's 16 bytes whose first byte has quote state `inq` (the
+// per-byte walk of a lane holding a quote; lanes without one use SWAR compares).
+__device__ __forceinline__ void bounds16_quoted(const Lane16& v, uint32_t next, int64_t nbytes, int64_t pos, uint32_t inq,
+                                                uint32_t delim, uint32_t* tm, uint32_t* dm) {
+  uint32_t t = 0, d = 0;
+#pragma unroll
+  for (int k = 0; k < 16; ++k) {
+    const uint32_t c = v.byte(k);
+    if (pos + k >= nbytes) break;
+    if (c == '"') {
+      inq ^= 1u;
+    } else if (!inq) {
+      if (c == '\n') {
+        t |= 1u << k;
+      } else if (c == '\r') {
+        const uint32_t nx = k < 15 ? v.byte(k + 1) : (pos + 16 < nbytes ? next : 0u);
+        if (pos + k + 1 >= nbytes || nx != '\n') t |= 1u << k;
+      } else if (c == delim) {
+        d |= 1u << k;
+      }
+    }
+  }
+  *tm = t;
+  *dm = d;
+}
+
+// The projected fields of every record, one wave per 16 KiB segment, straight from the file bytes and
+// the count pass's per-segment quote / terminator prefixes — no line-end list and no per-line walk
+// (round 4's k_csv_terms<true> + k_csv_lines, 160 + 283 us on tripdata). A wave owns the lines that
+// START in its segment (after each of its terminators; line 0 in segment 0) and runs past the
+// segment's end until the last of them ends. Per 1 KiB step, each lane has terminator and delimiter
+// masks of its 16 bytes (outside quotes); a wave prefix of (terminators, delimiters) per lane gives
+// the line and field ordinal at the lane's first byte (the field ordinal restarts at the last lane
+// holding a terminator), and each lane walks its boundaries in order, recording the projected
+// fields of its lines. Lines that may not be records — no delimiter at all (blank, or one field) or
+// '#' first — are counted in *suspect: the host then takes the kept-line path, which decides
+// exactly. Requires a delimiter above 0x20 (a blank line then has no delimiter).
+__global__ void __launch_bounds__(256) k_csv_seg_fields(const uint8_t* __restrict__ data, int64_t nbytes, int64_t nseg,
+                                                        const int64_t* __restrict__ seg_qs,
+                                                        const int64_t* __restrict__ seg_ts, int64_t nlines,
+                                                        int64_t first, FieldArgs Ag,
+                                                        unsigned long long* __restrict__ suspect) {
+  __shared__ FieldArgs A;
+  stage_args(A, Ag);
+  const int lane = threadIdx.x & 63;
+  const int64_t seg = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  if (seg >= nseg) return;
+  const uint64_t below = (1ull << lane) - 1;
+  const int64_t first_own = seg == 0 ? 0 : seg_ts[seg] + 1;
+  const int64_t last_own = min(seg_ts[seg + 1], nlines - 1);
+  if (first_own > last_own) return;
+  const GBytes G{data, nbytes};
+  const uint32_t delim = (uint32_t)A.delim;
+  uint32_t qcarry = (uint32_t)(seg_qs[seg] & 1);
+  int64_t row_c = seg == 0 ? 0 : seg_ts[seg];  // line holding the segment's first byte
+  int32_t f_c = 0;
+  int64_t fs_c = seg * SEG;
+  unsigned long long sus = 0;
+  if (seg == 0 && lane == 0 && nbytes > 0 && data[0] == '#') sus = 1;
+  for (int64_t p0 = seg * SEG; p0 < nbytes; p0 += 1024) {
+    const int64_t pos = p0 + lane * 16;
+    const Lane16 v = pos < nbytes ? load16(data, nbytes, pos) : Lane16{{0, 0, 0, 0}};
+    const bool hasq = has_byte(v, '"') && eq16(v, '"') != 0;
+    const uint32_t qodd = hasq ? (uint32_t)(quotes16(v) & 1) : 0u;
+    const uint64_t par = __ballot(qodd);
+    const uint32_t inq0 = qcarry ^ ((uint32_t)__popcll(par & below) & 1u);
+    qcarry ^= (uint32_t)__popcll(par) & 1u;
+    uint32_t next = (uint32_t)__shfl_down((int)(v.w[0] & 0xFFu), 1);
+    if (lane == 63) next = (v.byte(15) == '\r' && pos + 16 < nbytes) ? data[pos + 16] : 0u;
+    uint32_t T = 0, D = 0;
+    if (pos < nbytes) {
+      if (hasq) {
+        bounds16_quoted(v, next, nbytes, pos, inq0, delim, &T, &D);
+      } else if (!inq0) {
+        uint32_t dummy;
+        T = terms16(v, next, nbytes, pos, 0u, &dummy);
+        const uint32_t valid = pos + 16 <= nbytes ? 0xFFFFu : ((1u << (nbytes - pos)) - 1u);
+        D = has_byte(v, delim) ? (eq16(v, delim) & valid) : 0u;
+      }
+    }
+    // line and field ordinal at this lane's first byte
+    const uint32_t tc = (uint32_t)__popc(T), dc = (uint32_t)__popc(D);
+    const uint32_t cnt = (tc << 16) | dc;
+    uint32_t incl = cnt;
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+      const uint32_t y = (uint32_t)__shfl_up((int)incl, off);
+      if (lane >= off) incl += y;
+    }
+    const uint32_t excl = incl - cnt;
+    const uint64_t hasT = __ballot(T != 0), hasB = __ballot((T | D) != 0);
+    const int lastT = T ? 31 - __builtin_clz(T) : -1;
+    const int dtail = T ? __popc(D >> lastT) : 0;  // delimiters after the lane's last terminator
+    const int lastB = (T | D) ? 31 - __builtin_clz(T | D) : -1;
+    const uint64_t mt = hasT & below, mb = hasB & below;
+    const int pt = mt ? 63 - __builtin_clzll(mt) : 0;
+    const int pb = mb ? 63 - __builtin_clzll(mb) : 0;
+    const int dtail_p = __shfl(dtail, pt);
+    const uint32_t dincl_p = (uint32_t)__shfl((int)(incl & 0xFFFFu), pt);
+    const int lastB_p = __shfl(lastB, pb);
+    int64_t row = row_c + (int64_t)(excl >> 16);
+    int32_t f = mt ? dtail_p + (int32_t)((excl & 0xFFFFu) - dincl_p) : f_c + (int32_t)(excl & 0xFFFFu);
+    int64_t fs = mb ? (p0 + pb * 16 + lastB_p + 1) : fs_c;
+    // this lane's boundaries, in order
+    uint32_t bm = T | D;
+    while (bm) {
+      const int k = __builtin_ctz(bm);
+      bm &= bm - 1;
+      const int64_t pb_ = pos + k;
+      const bool is_t = (T >> k) & 1;
+      const bool own = row >= first_own && row <= last_own;
+      if (own && row >= first) record_field(G, A, f, fs, pb_, row - first);
+      if (is_t) {
+        if (own && f == 0) sus += 1;  // no delimiter: blank, comment or a one-field line?
+        ++row;
+        f = 0;
+        fs = pb_ + 1;
+        if (row >= first_own && row <= last_own && fs < nbytes && data[fs] == '#') sus += 1;
+      } else {
+        ++f;
+        fs = pb_ + 1;
+      }
+    }
+    row_c = __shfl(row, 63);
+    f_c = __shfl(f, 63);
+    fs_c = __shfl(fs, 63);
+    if (row_c > last_own) break;  // the last line that started in this segment has ended
+  }
+  // a final line without a terminator ends at the end of the file
+  if (lane == 0 && row_c == nlines - 1 && row_c >= first_own && row_c <= last_own && fs_c <= nbytes) {
+    if (row_c >= first) record_field(G, A, f_c, fs_c, nbytes, row_c - first);
+    if (f_c == 0) sus += 1;
+  }
+  for (int d = 32; d >= 1; d >>= 1) sus += __shfl_xor(sus, d);
+  if (lane == 0 && sus) atomicAdd(suspect, sus);
+}
+
 __global__ void k_csv_offsets(const int64_t* __restrict__ starts64, int64_t n, int32_t* __restrict__ offs) {
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i <= n; i += (int64_t)gridDim.x * blockDim.x)
     offs[i] = (int32_t)starts64[i];
@@ -705,18 +842,8 @@ int csv_parse(qe_ctx* ctx, const uint8_t* data, int64_t nbytes, const qe_csv_opt
   int64_t* ends = (int64_t*)p;
   int64_t* keep = ends + nterm + 2;
   int64_t* kstart = keep + nterm + 2;
-  if (nterm > 0) {
-    hipLaunchKernelGGL(k_csv_terms<true>, dim3(wgrid), dim3(256), 0, ctx->stream, data, nbytes, nseg, seg_qs, nullptr,
-                       seg_ts, ends);
-    QE_TRY(launch_check("k_csv_terms<emit>"));
-  }
   // bytes after the last terminator form a final record (also an unterminated quote at EOF)
   const int64_t nlines = nterm + (last_end + 1 < nbytes ? 1 : 0);
-  if (nlines > nterm) {
-    hipLaunchKernelGGL(k_csv_set_i64, dim3(1), dim3(1), 0, ctx->stream, ends + nterm, nbytes);
-    QE_TRY(launch_check("k_csv_set_i64"));
-  }
-  // ---- records and their projected fields
   const int64_t first = opt->has_header ? 1 : 0;
   t->nproj = nproj;
   t->data = data;
@@ -733,6 +860,49 @@ int csv_parse(qe_ctx* ctx, const uint8_t* data, int64_t nbytes, const qe_csv_opt
   }
   int64_t rows = 0;
   bool scanned = false;  // column sizes already known (the all-records fast path)
+  // ---- the segment-parallel field pass (k_csv_seg_fields): every line a record, no line-end list
+  static const bool seg_env = [] {
+    const char* e = getenv("QE_CSV_SEGFIELDS");
+    return !(e && e[0] == '0');
+  }();
+  const int64_t rows_all = std::max<int64_t>(0, nlines - first);
+  if (seg_env && nlines > 0 && A.delim > 0x20) {
+    // fields a record does not have read as "" (K:263): lengths and quote flags start at zero
+    QE_HIP(hipMemsetAsync(t->len(0), 0, (size_t)nproj * (size_t)t->stride * 8, ctx->stream));
+    QE_HIP(hipMemsetAsync(t->quoted(0), 0, (size_t)nproj * (size_t)t->stride, ctx->stream));
+    unsigned long long* suspect = (unsigned long long*)keep;
+    QE_HIP(hipMemsetAsync(suspect, 0, 8, ctx->stream));
+    hipLaunchKernelGGL(k_csv_seg_fields, dim3(wgrid), dim3(256), 0, ctx->stream, data, nbytes, nseg, seg_qs, seg_ts,
+                       nlines, first, A, suspect);
+    QE_TRY(launch_check("k_csv_seg_fields"));
+    for (int c = 0; c < nproj && rows_all > 0; ++c) QE_TRY(exclusive_scan_i64(ctx, A.len[c], t->bstart(c), rows_all));
+    void* pin;
+    QE_TRY(ctx_pinned(ctx, (size_t)(nproj + 1) * 8, &pin));
+    QE_HIP(hipMemcpyAsync(pin, suspect, 8, hipMemcpyDeviceToHost, ctx->stream));
+    for (int c = 0; c < nproj && rows_all > 0; ++c)
+      QE_HIP(hipMemcpyAsync((int64_t*)pin + 1 + c, t->bstart(c) + rows_all, 8, hipMemcpyDeviceToHost, ctx->stream));
+    QE_TRY(ctx_sync(ctx));
+    if (((int64_t*)pin)[0] == 0) {
+      t->rows = rows_all;
+      t->total.assign((size_t)nproj, 0);
+      for (int c = 0; c < nproj && rows_all > 0; ++c) {
+        t->total[(size_t)c] = ((int64_t*)pin)[1 + c];
+        QE_CHECK(t->total[(size_t)c] < (1ll << 31), QE_ERR_CAPACITY, "CSV column %d holds more than 2^31 bytes", c);
+      }
+      return QE_OK;
+    }
+    // a line that may not be a record: the line-end list and the kept-line path below decide
+  }
+  if (nterm > 0) {
+    hipLaunchKernelGGL(k_csv_terms<true>, dim3(wgrid), dim3(256), 0, ctx->stream, data, nbytes, nseg, seg_qs, nullptr,
+                       seg_ts, ends);
+    QE_TRY(launch_check("k_csv_terms<emit>"));
+  }
+  if (nlines > nterm) {
+    hipLaunchKernelGGL(k_csv_set_i64, dim3(1), dim3(1), 0, ctx->stream, ends + nterm, nbytes);
+    QE_TRY(launch_check("k_csv_set_i64"));
+  }
+  // ---- records and their projected fields
   if (nlines > 0) {
     // every line a record (the common case): one pass over the lines, no kept-line list
     unsigned long long* nskip = (unsigned long long*)keep;
@@ -743,7 +913,6 @@ int csv_parse(qe_ctx* ctx, const uint8_t* data, int64_t nbytes, const qe_csv_opt
     QE_TRY(launch_check("k_csv_lines"));
     // Speculatively every line a record (the common case): the columns' length scans run now, and
     // the skipped-line count and the column sizes come back in one read.
-    const int64_t rows_all = std::max<int64_t>(0, nlines - first);
     for (int c = 0; c < nproj && rows_all > 0; ++c) QE_TRY(exclusive_scan_i64(ctx, A.len[c], t->bstart(c), rows_all));
     void* pin;
     QE_TRY(ctx_pinned(ctx, (size_t)(nproj + 1) * 8, &pin));

@@ -274,85 +274,142 @@ __device__ __forceinline__ void head32(const uint8_t* p, int len, uint64_t (&h)[
   }
 }
 
-__global__ void __launch_bounds__(ENC_THREADS) k_dict_encode(DictDev D, const int32_t* __restrict__ offs,
-                                                             const uint8_t* __restrict__ bytes,
-                                                             const uint8_t* __restrict__ valid, int64_t n,
-                                                             int32_t* __restrict__ codes, uint32_t* __restrict__ retry) {
-  __shared__ LdsCache C;
-  __shared__ int wg_full;  // a lane of this workgroup saw the dictionary full: the batch reruns
-  // Rows whose key another wave had claimed but not yet published: kept here and resolved after
-  // this workgroup's loop, when the claimers have long published. At a batch's start every wave
-  // meets every new key at once (3 tripdata keys sent ~260K rows to a 66 us retry pass); only
-  // rows past DEF_CAP, or still unpublished then, go to the retry bitmap.
-  constexpr int DEF_CAP = 2048;
-  __shared__ int s_ndef;
-  __shared__ int64_t s_def[DEF_CAP];
-  for (int k = threadIdx.x; k < LC_SLOTS; k += blockDim.x) C.state[k] = 0;
-  if (threadIdx.x == 0) {
-    wg_full = 0;
-    s_ndef = 0;
+// One row's full lookup (LDS cache, then the wave's leaders on the global table, inserting new keys),
+// for every lane of the converged wave at once; a row another wave has claimed but not published is
+// deferred (s_def) or marked for the retry pass. The slow path of k_dict_encode's steps.
+struct EncShared {
+  LdsCache C;
+  int wg_full;  // a lane of this workgroup saw the dictionary full: the batch reruns
+  int ndef;
+  int64_t def[2048];
+};
+constexpr int DEF_CAP = 2048;
+
+__device__ __forceinline__ void encode_lookup(const DictDev& D, EncShared& S, const int32_t* __restrict__ offs,
+                                              const uint8_t* __restrict__ bytes, int64_t n, int64_t i, bool live,
+                                              int32_t* __restrict__ codes, uint32_t* __restrict__ retry, int lane) {
+  int32_t len = 0;
+  const uint8_t* p = bytes;
+  uint64_t h = 0;
+  uint64_t hd[LC_BYTES / 8] = {0, 0, 0, 0, 0};
+  int c = -1;
+  if (live) {
+    const int32_t s0 = offs[i];
+    len = offs[i + 1] - s0;
+    p = bytes + s0;
+    h = str_hash(p, len);
+    head32(p, len, hd);
+    if (len <= LC_BYTES) c = lc_find(S.C, h, len, hd);
   }
-  __syncthreads();
-  const int lane = threadIdx.x & 63;
-  // every lane runs the same trip count so the wave-level dedup below sees whole waves
-  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
-  const int64_t start = blockIdx.x * (int64_t)blockDim.x + threadIdx.x - lane;  // wave's first row
-  for (int64_t i0 = start; i0 < n; i0 += stride) {
-    if (*(volatile int*)&wg_full) break;  // uniform per wave (LDS)
-    const int64_t i = i0 + lane;
-    const bool live = i < n && (!valid || ((valid[i >> 3] >> (i & 7)) & 1));
-    int32_t len = 0;
-    const uint8_t* p = bytes;
-    uint64_t h = 0;
-    uint64_t hd[LC_BYTES / 8] = {0, 0, 0, 0, 0};
-    int c = -1;
-    if (live) {
-      const int32_t s0 = offs[i];
-      len = offs[i + 1] - s0;
-      p = bytes + s0;
-      h = str_hash(p, len);
-      head32(p, len, hd);
-      if (len <= LC_BYTES) c = lc_find(C, h, len, hd);
-    }
-    // misses: the first lane of each distinct key in the wave looks it up, all leaders at once
-    // (keys over 40 bytes: every lane for itself); the other lanes take their leader's code
-    const bool miss = live && c < 0;
-    if (__ballot(miss)) {
-      const int leader = wave_leader(miss, len <= LC_BYTES, h, len, hd, lane);
-      const bool lead = miss && leader == lane;
-      int code = 0;
-      uint64_t gslot = 0;
-      if (lead)
-        code = dict_probe(
-            D, h, [&](int cc) { return D.code_len[cc] == len && bytes_equal(D.arena + D.code_off[cc], p, len); },
-            &gslot);
-      const bool claim = lead && code == R_CLAIMED;
-      const int pc = dict_insert_wave(D, claim, gslot, h, len, [&](uint8_t* dst) {
-        for (int k = 0; k < len; ++k) dst[k] = p[k];
-      }, lane);
-      if (claim) code = pc;
-      if (lead && code >= 0 && len <= LC_BYTES) lc_insert(C, h, len, hd, code);
-      code = __shfl(code, leader);
-      if (miss) c = code;
-    }
-    if (i < n) {
-      codes[i] = (live && c >= 0) ? c : 0;
-      if (live && c == R_OVERFLOW) wg_full = 1;
-      if (live && c == R_RETRY) {
-        const int d = atomicAdd(&s_ndef, 1);
-        if (d < DEF_CAP) {
-          s_def[d] = i;
-        } else {
-          atomicOr(&retry[i >> 5], 1u << (i & 31));
-          atomicAdd(&D.flags[1], 1u);
-        }
+  // misses: the first lane of each distinct key in the wave looks it up, all leaders at once
+  // (keys over 40 bytes: every lane for itself); the other lanes take their leader's code
+  const bool miss = live && c < 0;
+  if (__ballot(miss)) {
+    const int leader = wave_leader(miss, len <= LC_BYTES, h, len, hd, lane);
+    const bool lead = miss && leader == lane;
+    int code = 0;
+    uint64_t gslot = 0;
+    if (lead)
+      code = dict_probe(
+          D, h, [&](int cc) { return D.code_len[cc] == len && bytes_equal(D.arena + D.code_off[cc], p, len); },
+          &gslot);
+    const bool claim = lead && code == R_CLAIMED;
+    const int pc = dict_insert_wave(D, claim, gslot, h, len, [&](uint8_t* dst) {
+      for (int k = 0; k < len; ++k) dst[k] = p[k];
+    }, lane);
+    if (claim) code = pc;
+    if (lead && code >= 0 && len <= LC_BYTES) lc_insert(S.C, h, len, hd, code);
+    code = __shfl(code, leader);
+    if (miss) c = code;
+  }
+  if (i < n) {
+    codes[i] = (live && c >= 0) ? c : 0;
+    if (live && c == R_OVERFLOW) S.wg_full = 1;
+    if (live && c == R_RETRY) {
+      const int d = atomicAdd(&S.ndef, 1);
+      if (d < DEF_CAP) {
+        S.def[d] = i;
+      } else {
+        atomicOr(&retry[i >> 5], 1u << (i & 31));
+        atomicAdd(&D.flags[1], 1u);
       }
     }
   }
+}
+
+// str_hash of a key of at most 8 bytes held in one word (what str_hash computes for it).
+__device__ __forceinline__ uint64_t str_hash_short(uint64_t w, int len) {
+  uint64_t h = 0x9E3779B97F4A7C15ull ^ ((uint64_t)len * 0xC2B2AE3D27D4EB4Full);
+  if (len == 8) h = fmix64(h ^ w) + 0x165667B19E3779F9ull;
+  else if (len > 0) h = fmix64(h ^ w ^ ((uint64_t)len << 59));
+  h = fmix64(h);
+  return h ? h : 1;
+}
+
+// 1024-thread workgroups, one per CU (one LDS cache per CU, warmed once; 16 waves to hide the
+// offset -> byte -> cache latency chain). A wave step takes 256 rows, 4 per lane (rows
+// base + 64 r + lane): their offsets and key words load together, then each key of at most 8 bytes
+// is looked up in the LDS cache by its one word; every other row (longer keys, cache misses while
+// the cache warms) takes encode_lookup. Round 4 ran one row per lane per step, 8 waves per CU:
+// 112 us for tripdata's 4M VendorIDs.
+constexpr int ENC_BLOCK = 1024;
+__global__ void __launch_bounds__(ENC_BLOCK) k_dict_encode(DictDev D, const int32_t* __restrict__ offs,
+                                                           const uint8_t* __restrict__ bytes,
+                                                           const uint8_t* __restrict__ valid, int64_t n,
+                                                           int32_t* __restrict__ codes, uint32_t* __restrict__ retry) {
+  __shared__ EncShared S;
+  for (int k = threadIdx.x; k < LC_SLOTS; k += blockDim.x) S.C.state[k] = 0;
+  if (threadIdx.x == 0) {
+    S.wg_full = 0;
+    S.ndef = 0;
+  }
   __syncthreads();
-  const int nd = s_ndef < DEF_CAP ? s_ndef : DEF_CAP;
+  const int lane = threadIdx.x & 63;
+  const int64_t wstride = ((int64_t)gridDim.x * blockDim.x >> 6) * 256;
+  for (int64_t base = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x - lane) * 4; base < n; base += wstride) {
+    if (*(volatile int*)&S.wg_full) break;  // uniform per wave (LDS)
+    int64_t row[4];
+    bool live[4];
+    int32_t s0[4], len[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      row[r] = base + 64 * r + lane;
+      live[r] = row[r] < n && (!valid || ((valid[row[r] >> 3] >> (row[r] & 7)) & 1));
+      s0[r] = live[r] ? offs[row[r]] : 0;
+      len[r] = live[r] ? offs[row[r] + 1] : 0;
+    }
+    uint64_t w[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      len[r] -= s0[r];
+      w[r] = (live[r] && len[r] <= 8) ? load_u64_unaligned(bytes + s0[r], len[r]) : 0ull;
+    }
+    qu32 slow = 0;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      int c = -1;
+      if (live[r] && len[r] <= 8) {
+        const uint64_t h = str_hash_short(w[r], len[r]);
+        const uint64_t hd[LC_BYTES / 8] = {w[r], 0, 0, 0, 0};
+        c = lc_find(S.C, h, len[r], hd);
+      }
+      if (live[r] && c < 0) slow |= 1u << r;
+      else if (row[r] < n) codes[row[r]] = live[r] ? c : 0;
+    }
+    // rows the cache did not answer: the full lookup, one row position at a time (rolled: its
+    // code is large and runs only while the cache warms or for long keys)
+#pragma unroll 1
+    for (int r = 0; r < 4; ++r) {
+      const bool sl = (slow >> r) & 1;
+      if (!__ballot(sl)) continue;
+      const int64_t i = base + 64 * r + lane;
+      encode_lookup(D, S, offs, bytes, n, i, sl, codes, retry, lane);
+    }
+  }
+  __syncthreads();
+  const int nd = S.ndef < DEF_CAP ? S.ndef : DEF_CAP;
   for (int d = threadIdx.x; d < nd; d += blockDim.x) {
-    const int64_t i = s_def[d];
+    const int64_t i = S.def[d];
     const int32_t s0 = offs[i], len = offs[i + 1] - s0;
     const uint8_t* p = bytes + s0;
     const uint64_t h = str_hash(p, len);
@@ -360,11 +417,11 @@ __global__ void __launch_bounds__(ENC_THREADS) k_dict_encode(DictDev D, const in
     if (len <= LC_BYTES) {
       uint64_t hd[LC_BYTES / 8];
       head32(p, len, hd);
-      c = lc_find(C, h, len, hd);
+      c = lc_find(S.C, h, len, hd);
     }
     if (c < 0) c = dict_find_or_insert(D, p, len, h);
     codes[i] = c >= 0 ? c : 0;
-    if (c == R_OVERFLOW) wg_full = 1;
+    if (c == R_OVERFLOW) S.wg_full = 1;
     if (c == R_RETRY) {
       atomicOr(&retry[i >> 5], 1u << (i & 31));
       atomicAdd(&D.flags[1], 1u);
@@ -888,17 +945,25 @@ int qe_strdict_encode(qe_strdict* d, const qe_column* in, qe_column* codes) {
   if (in->validity)
     QE_HIP(hipMemcpyAsync(codes->validity, in->validity, (size_t)div_up((uint64_t)n, 8), hipMemcpyDeviceToDevice,
                           ctx->stream));  // an input bitmap may be Arrow-minimal: ceil(n/8) bytes
+  // the column's byte span (arena sizing): two words read back on the ctx stream (a blocking
+  // hipMemcpy would wait for the whole device and add a second round trip)
   int32_t o[2] = {0, 0};
-  QE_HIP(hipMemcpy(o, in->offsets + n, 4, hipMemcpyDeviceToHost));
-  QE_HIP(hipMemcpy(o + 1, in->offsets, 4, hipMemcpyDeviceToHost));
+  {
+    void* pin;
+    QE_TRY(ctx_pinned(ctx, 8, &pin));
+    QE_HIP(hipMemcpyAsync(pin, in->offsets + n, 4, hipMemcpyDeviceToHost, ctx->stream));
+    QE_HIP(hipMemcpyAsync((int32_t*)pin + 1, in->offsets, 4, hipMemcpyDeviceToHost, ctx->stream));
+    QE_TRY(ctx_sync(ctx));
+    memcpy(o, pin, 8);
+  }
   // 2 workgroups per CU: every workgroup warms its LDS cache once, so fewer, longer-lived
   // workgroups send fewer lookups of the hot keys to the global table (4M rows: 3 keys 0.31 ms
   // at 2/CU vs 0.45 at 16/CU; 1M keys 18.9 vs 20.8 ms)
-  const int grid = (int)std::min<int64_t>((int64_t)div_up((uint64_t)n, ENC_THREADS), (int64_t)ctx->num_cus * 2);
+  const int grid = (int)std::min<int64_t>((int64_t)div_up((uint64_t)n, 4 * ENC_BLOCK), (int64_t)ctx->num_cus);
   return encode_loop(
       d, n, (int64_t)o[0] - o[1],
       [&](uint32_t* retry) {
-        hipLaunchKernelGGL(k_dict_encode, dim3(grid), dim3(ENC_THREADS), 0, ctx->stream, d->dev(), in->offsets,
+        hipLaunchKernelGGL(k_dict_encode, dim3(grid), dim3(ENC_BLOCK), 0, ctx->stream, d->dev(), in->offsets,
                            (const uint8_t*)in->values, in->validity, n, (int32_t*)codes->values, retry);
         return launch_check("k_dict_encode");
       },
@@ -944,7 +1009,7 @@ int qe_strdict_encode_tuple(qe_strdict* d, const qe_column* keys, int32_t nkeys,
   if (n == 0) return QE_OK;
   if (codes->validity)  // a tuple with null members is still a (non-null) group key
     QE_HIP(hipMemsetAsync(codes->validity, 0xFF, (size_t)div_up((uint64_t)n, 32) * 4, ctx->stream));
-  const int grid = (int)std::min<int64_t>((int64_t)div_up((uint64_t)n, ENC_THREADS), (int64_t)ctx->num_cus * 2);
+  const int grid = (int)std::min<int64_t>((int64_t)div_up((uint64_t)n, 4 * ENC_BLOCK), (int64_t)ctx->num_cus);
   return encode_loop(
       d, n, 8 * TW * std::min<int64_t>(n, 1 << 20),
       [&](uint32_t* retry) {
