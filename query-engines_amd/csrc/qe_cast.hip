@@ -27,6 +27,22 @@ using namespace castp;
 constexpr int CAST_THREADS = 256;
 constexpr int SLOW_THREADS = 64;
 
+// Bytes [p, p + n) of a value of at most 16 bytes as two little-endian words: independent byte
+// loads issued together (parse_fast walks its bytes one dependent load at a time).
+__device__ __forceinline__ void load16_words(const uint8_t* p, int n, uint64_t* w0, uint64_t* w1) {
+  uint64_t a = 0, b = 0;
+#pragma unroll
+  for (int k = 0; k < 16; ++k)
+    if (k < n) {
+      const uint64_t c = p[k];
+      if (k < 8) a |= c << (8 * k);
+      else b |= c << (8 * (k - 8));
+    }
+  *w0 = a;
+  *w1 = b;
+}
+
+
 // 8 rows per thread: one validity byte in; one validity byte and one slow-bitmap byte out.
 // One thread per row (a wave = 64 consecutive rows = 8 bitmap bytes): the rows' parses run side
 // by side instead of 8 after one another per thread. The output validity and slow-path bitmaps
@@ -50,14 +66,20 @@ __global__ void __launch_bounds__(CAST_THREADS) k_cast_utf8_f64(const int32_t* _
     bool ok = false, sl = false;
     if (live) {
       const int32_t s0 = offs[i], s1 = offs[i + 1];
-      DecScan ds;
-      const int r = parse_fast(bytes + s0, s1 - s0, &v, &ds);
-      if (r == P_ERR) {
-        atomicMin(err_row, (unsigned long long)i);
-        v = 0.0;
-      } else {
+      uint64_t w0 = 0, w1 = 0;
+      if (s1 - s0 <= 16) load16_words(bytes + s0, s1 - s0, &w0, &w1);
+      if (s1 - s0 <= 16 && fast_decimal(w0, w1, s1 - s0, &v)) {
         ok = true;
-        sl = r == P_SLOW;
+      } else {
+        DecScan ds;
+        const int r = parse_fast(bytes + s0, s1 - s0, &v, &ds);
+        if (r == P_ERR) {
+          atomicMin(err_row, (unsigned long long)i);
+          v = 0.0;
+        } else {
+          ok = true;
+          sl = r == P_SLOW;
+        }
       }
     }
     if (in) out[i] = v;

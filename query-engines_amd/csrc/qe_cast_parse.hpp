@@ -66,6 +66,39 @@ QE_HD double round_binary(uint64_t H, int e2, bool sticky) {
   return ldexp((double)q, e2 + drop);
 }
 
+// The common decimal form from registers: [+-] digits [. digits] (at least one digit, at most 15
+// in all, no other byte) is m / 10^k with m < 2^53 and k <= 15, both exact doubles, so the one
+// IEEE division is the correctly rounded value — what Double.parseDouble returns (K:791). Anything
+// else (whitespace, exponent, suffix, NaN / Infinity, hex, more digits) -> false: parse_fast.
+QE_HD inline bool fast_decimal(uint64_t w0, uint64_t w1, int n, double* out) {
+  if (n <= 0 || n > 16) return false;
+  int i = 0;
+  uint32_t c0 = (uint32_t)(w0 & 0xFF);
+  const bool neg = c0 == '-';
+  if (c0 == '-' || c0 == '+') i = 1;
+  uint64_t m = 0;
+  int digits = 0, frac = -1;
+  for (; i < n; ++i) {
+    const uint32_t c = (uint32_t)((i < 8 ? w0 >> (8 * i) : w1 >> (8 * (i - 8))) & 0xFF);
+    if (c >= '0' && c <= '9') {
+      m = m * 10 + (c - '0');
+      ++digits;
+      if (frac >= 0) ++frac;
+    } else if (c == '.' && frac < 0) {
+      frac = 0;
+    } else {
+      return false;
+    }
+  }
+  if (digits == 0 || digits > 15) return false;
+  double p10 = 1.0;  // 10^frac, exact (<= 10^15) and built without a table (a dynamically indexed
+  for (int k = 0; k < frac; ++k) p10 *= 10.0;  // local array would live in scratch memory)
+  double v = (double)m;
+  if (frac > 0) v = v / p10;
+  *out = neg ? -v : v;
+  return true;
+}
+
 // Syntax + every case except the exact decimal path. Returns P_ERR, P_DONE (*out set) or P_SLOW
 // (*ds filled, *out = a guess of |value| within a few ulps).
 QE_HD int parse_fast(const uint8_t* s, int len, double* out, DecScan* ds) {

@@ -308,3 +308,44 @@ def test_cast_expression_operator(gpu_ctx):
     assert CastExpression(ColumnExpression(0), N.TYPE_FLOAT64).evaluate(nulls).to_pylist() == [None, None]
     with pytest.raises(N.IllegalStateException, match="not supported"):
         CastExpression(ColumnExpression(0), N.TYPE_INT64).evaluate(batch)
+
+
+def test_register_fast_path_on_host(host_parser):
+    """The CAST kernel's register fast path (qe_cast_parse.hpp fast_decimal: [+-]digits[.digits],
+    at most 15 digits, one exact division) returns exactly what the full parser returns wherever it
+    applies, declines everything else, and agrees with every JDK known answer it takes."""
+    import ctypes
+    import random
+
+    d = pathlib.Path(__file__).resolve().parent / "native"
+    fast = ctypes.CDLL(str(d / "_build" / "libqe_cast_host.so")).qe_cast_host_fast
+    fast.restype = ctypes.c_int
+    fast.argtypes = [ctypes.c_char_p, ctypes.c_int, ctypes.POINTER(ctypes.c_double)]
+
+    def f(s):
+        out = ctypes.c_double()
+        return out.value if fast(s.encode(), len(s.encode()), ctypes.byref(out)) else None
+
+    rng = random.Random(5)
+    taken = 0
+    for _ in range(20000):
+        a = "".join(rng.choice("0123456789") for _ in range(rng.randint(0, 9)))
+        b = "".join(rng.choice("0123456789") for _ in range(rng.randint(0, 8)))
+        dot = rng.random() < 0.7
+        s = rng.choice(["", "-", "+"]) + a + (("." + b) if dot else "")
+        digits = a + (b if dot else "")
+        v = f(s)
+        if v is not None:
+            taken += 1
+            want = R.parse_java_double(s)
+            assert R.same_f64(v, want), (s, v, want)
+            assert R.same_f64(v, host_parser(s)[0]), s
+        elif digits:
+            assert len(digits) > 15 or len(s) > 16, s  # declined only beyond its range
+    assert taken > 15000
+    for s in ["", ".", "-", "+", "1e5", " 1", "1 ", "NaN", "0x1p3", "1d", "1.2.3", "12345678901234567", "1_0"]:
+        assert f(s) is None, s
+    for e in KAT:
+        v = f(e["in"])
+        if v is not None:
+            assert e["out"] != "NFE" and np.float64(v).view(np.uint64) == int(e["out"], 16), e["in"]
