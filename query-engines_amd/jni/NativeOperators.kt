@@ -281,7 +281,7 @@ private class NativeCsvDataSource(private val filename: String, private val hasH
                         buf = bigger
                         continue
                     }
-                    val table = CsvTable(NativeEngine.csvParse(Native.ctx(), buf, cut, delimiter.code, header, fields))
+                    val table = parseChunk(buf, cut, delimiter.code, header, fields)
                     header = false
                     if (NativeEngine.csvRows(table.handle) > 0) {
                         yield(RecordBatch(readSchema, fields.indices.map { table.column(it) }))
@@ -299,13 +299,39 @@ private class NativeCsvDataSource(private val filename: String, private val hasH
         return listOf(',', ';', '\t', '|').firstOrNull { head.contains(it) } ?: ','
     }
 
-    private class CsvTable(val handle: Long) {
+    // A chunk's table lives until its batch's columns are unreachable (a consumer may keep batches,
+    // as toList() does), so only the Cleaner may free it. The JVM side of a table is a few objects,
+    // so the heap alone need not trigger a collection while the device holds GBs of parsed chunks:
+    // the device bytes of tables not yet freed are counted, and a scan that finds more than two
+    // chunks' worth still held asks for a collection before parsing the next chunk; a device OOM
+    // collects, waits for the Cleaner, and retries once. A streaming consumer thus stays at about
+    // two chunks of device memory (ADVICE r04).
+    private fun parseChunk(buf: java.nio.ByteBuffer, cut: Long, delim: Int, header: Boolean, fields: IntArray): CsvTable {
+        if (CsvTable.held.get() > 2L * chunkBytes) System.gc()
+        val h = try {
+            NativeEngine.csvParse(Native.ctx(), buf, cut, delim, header, fields)
+        } catch (e: OutOfMemoryError) {
+            System.gc()
+            val deadline = System.nanoTime() + 2_000_000_000L
+            val before = CsvTable.held.get()
+            while (CsvTable.held.get() >= before && before > 0 && System.nanoTime() < deadline) Thread.sleep(10)
+            NativeEngine.csvParse(Native.ctx(), buf, cut, delim, header, fields)
+        }
+        return CsvTable(h, cut)
+    }
+
+    private class CsvTable(val handle: Long, bytes: Long) {
         init {
             val h = handle
-            Native.cleaner.register(this) { NativeEngine.csvDestroy(h) }
+            held.addAndGet(bytes)
+            Native.cleaner.register(this) { NativeEngine.csvDestroy(h); held.addAndGet(-bytes) }
         }
 
         fun column(i: Int) = NativeColumnVector(NativeEngine.csvColumn(handle, i), this)
+
+        companion object {
+            val held = java.util.concurrent.atomic.AtomicLong() // device bytes of tables not yet freed
+        }
     }
 }
 
