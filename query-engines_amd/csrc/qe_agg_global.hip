@@ -5,7 +5,11 @@
 //     a NaN seed is sticky, a later NaN never wins, and among +0.0/-0.0 ties the earliest row
 //     wins. In parallel this is a reduction of (non-NaN ordered key, first-non-null row,
 //     first-NaN row, first -0.0 row, first +0.0 row), each a commutative min/max.
-//   * int64 SUM wraps (JVM Long); fp64 SUM is a Neumaier-compensated tree sum.
+//   * int64 SUM wraps (JVM Long); fp64 SUM is a Neumaier-compensated tree sum whose error is
+//     bounded at the end (sum_certified: the partials also carry sum |x| and the infinite-input
+//     count); a sum the bound cannot place within 1e-9 of the exact one (heavy cancellation) is
+//     recomputed exactly by a second pass (k_agg_global_fx, qe_dev.hpp fixed point) in
+//     qe_agg_global, or fails loudly in qe_agg_global_merge (its rows are elsewhere).
 // Layout: lane handles rows base + 128q + 2*lane + {0,1} (q = 0..3) so every 16-B load
 // instruction of a wave reads one contiguous KiB. Per-block partials are reduced by a second
 // single-block kernel in fixed order: bit-reproducible run to run.
@@ -20,6 +24,8 @@ struct GPart {
   int64_t rows, count;
   int64_t isum, imin, imax;  // integral input
   double s, c;               // Neumaier sum (both input kinds; AVG of int64 uses it)
+  double a;                  // sum of |x| (fp64 inputs, plain adds): the error bound's condition term
+  int64_t ninf;              // infinite fp64 inputs
   int64_t kmin, kmax;        // ordered keys of non-NaN fp64
   uint64_t first_nn, first_nan, first_negz, first_posz;
 };
@@ -30,6 +36,8 @@ __device__ __forceinline__ void gpart_init(GPart& p) {
   p.imin = INT64_MAX;
   p.imax = INT64_MIN;
   p.s = p.c = 0.0;
+  p.a = 0.0;
+  p.ninf = 0;
   p.kmin = INT64_MAX;
   p.kmax = INT64_MIN;
   p.first_nn = p.first_nan = p.first_negz = p.first_posz = UINT64_MAX;
@@ -49,6 +57,8 @@ __device__ __forceinline__ void gpart_merge(GPart& a, const GPart& b) {
   a.imax = max(a.imax, b.imax);
   a.c += b.c;
   neumaier_add(a.s, a.c, b.s);
+  a.a += b.a;
+  a.ninf += b.ninf;
   a.kmin = min(a.kmin, b.kmin);
   a.kmax = max(a.kmax, b.kmax);
   a.first_nn = min(a.first_nn, b.first_nn);
@@ -72,6 +82,8 @@ __device__ __forceinline__ void gpart_wave_reduce(GPart& p) {
     o.imax = shfl_x(p.imax, m);
     o.s = shfl_x(p.s, m);
     o.c = shfl_x(p.c, m);
+    o.a = shfl_x(p.a, m);
+    o.ninf = shfl_x(p.ninf, m);
     o.kmin = shfl_x(p.kmin, m);
     o.kmax = shfl_x(p.kmax, m);
     o.first_nn = (uint64_t)shfl_x((int64_t)p.first_nn, m);
@@ -135,6 +147,8 @@ __global__ void __launch_bounds__(256) k_agg_global(const int64_t* __restrict__ 
         if (IS_F64) {
           const double d = bits_f64(x);
           neumaier_add(p.s, p.c, d);
+          p.a += fabs(d);
+          if (__builtin_isinf(d)) p.ninf += 1;
           if (d != d) {
             p.first_nan = min(p.first_nan, row);
           } else {
@@ -175,12 +189,13 @@ __global__ void __launch_bounds__(256) k_agg_global_f64_dense(const int64_t* __r
   const int lane = threadIdx.x & 63;
   const int64_t wave = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 6;
   const int64_t nwaves = ((int64_t)gridDim.x * blockDim.x) >> 6;
-  double s[8], c[8];
+  double s[8], c[8], a = 0.0;
 #pragma unroll
   for (int k = 0; k < 8; ++k) s[k] = c[k] = 0.0;
   double mn = __builtin_inf(), mx = -__builtin_inf();
   int64_t count = 0;
   uint64_t first_nn = UINT64_MAX, first_nan = UINT64_MAX, first_negz = UINT64_MAX, first_posz = UINT64_MAX;
+  int64_t ninf = 0;
   for (int64_t base = wave * 512; base < n; base += nwaves * 512) {
     const bool full = base + 512 <= n;
     double d[8];
@@ -211,13 +226,15 @@ __global__ void __launch_bounds__(256) k_agg_global_f64_dense(const int64_t* __r
       const double dm = in ? d[k] : __builtin_nan("");  // fmin/fmax ignore NaN
       mn = fmin(mn, dm);
       mx = fmax(mx, dm);
-      special |= (d[k] != d[k]) | (d[k] == 0.0);
+      a += fabs(d[k]);
+      special |= ((d[k] - d[k]) != 0.0) | (d[k] == 0.0);  // NaN, +-Inf or a zero
     }
-    if (special) {  // NaN or a zero among these 8 rows (rare): exact first-occurrence bookkeeping
+    if (special) {  // NaN, an infinity or a zero among these 8 rows (rare): exact first-occurrence bookkeeping
 #pragma unroll
       for (int k = 0; k < 8; ++k) {
         const int64_t row = base + 128 * (k >> 1) + 2 * lane + (k & 1);
         if (row >= n) continue;
+        if (__builtin_isinf(d[k])) ++ninf;
         if (d[k] != d[k]) first_nan = min(first_nan, (uint64_t)row);
         else if (d[k] == 0.0) {
           if (f64_bits(d[k]) < 0) first_negz = min(first_negz, (uint64_t)row);
@@ -233,6 +250,8 @@ __global__ void __launch_bounds__(256) k_agg_global_f64_dense(const int64_t* __r
   p.first_nan = first_nan;
   p.first_negz = first_negz;
   p.first_posz = first_posz;
+  p.a = a;
+  p.ninf = ninf;
 #pragma unroll
   for (int k = 0; k < 8; ++k) {  // fixed fold order
     p.c += c[k];
@@ -274,6 +293,41 @@ __global__ void k_agg_global_unpack(const uint8_t* __restrict__ recs, int n, GPa
   for (int i = threadIdx.x; i < n; i += blockDim.x) out[i] = *(const GPart*)(recs + (size_t)i * QE_GLOBAL_PARTIAL_BYTES);
 }
 
+// Exact fp64 SUM of the selected non-null rows (the fallback when the compensated sum cannot be
+// certified): every thread adds its rows into its own 256-bit fixed-point accumulator in LDS
+// (qe_dev.hpp fx_*, plain read-modify-writes), the workgroup folds them in a fixed tree, and one
+// thread per workgroup adds the result into out[0..4] (w0..w3, status) with device atomics; integer
+// adds are associative, so the words are the exact sum whatever the order. Rare by construction, so
+// it is simple rather than fast.
+__global__ void __launch_bounds__(256) k_agg_global_fx(const int64_t* __restrict__ vals, const uint8_t* __restrict__ valid,
+                                                       const uint8_t* __restrict__ mv, const uint8_t* __restrict__ ml,
+                                                       int64_t n, qu64* __restrict__ out) {
+  __shared__ qu64 t[256 * 5];
+  qu64* my = t + threadIdx.x * 5;
+  for (int w = 0; w < 5; ++w) my[w] = 0;
+  auto wp = [&](int w) { return &my[w]; };
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
+    const int sh = (int)(i & 7);
+    if (mv) {
+      uint32_t m = (uint32_t)(mv[i >> 3] >> sh);
+      if (ml) m &= (uint32_t)(ml[i >> 3] >> sh);
+      if (!(m & 1u)) continue;
+    }
+    if (valid && !((valid[i >> 3] >> sh) & 1)) continue;
+    fx_add_row<false>(wp, fx_row(vals[i]), &my[4]);
+  }
+  __syncthreads();
+  for (int h = 128; h > 0; h >>= 1) {
+    if ((int)threadIdx.x < h) {
+      const qu64* o = t + (threadIdx.x + h) * 5;
+      fx_add_words<false>(wp, o[0], o[1], o[2], o[3], o[4], &my[4]);
+    }
+    __syncthreads();
+  }
+  if (threadIdx.x == 0)
+    fx_add_words<true>([&](int w) { return &out[w]; }, my[0], my[1], my[2], my[3], my[4], &out[4]);
+}
+
 // host_out (optional): pinned host memory that also receives the result, so the caller reads it
 // after a stream sync with no device-to-host copy launch.
 // host_flag (optional): set once host_out is written, for a host polling it (release, system scope).
@@ -295,6 +349,21 @@ __global__ void __launch_bounds__(256) k_agg_global_final(GPart* __restrict__ pa
     if (host_out) *host_out = b;
     if (host_flag) __hip_atomic_store(host_flag, 1ull, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
   }
+}
+
+// Whether the compensated fp64 sum R = s + c of a partial is within FX_REL_TOL (1e-9) of the exact
+// sum. Every s update is an exact two-sum, so exact = s + sum of the error terms e_i, and c is the
+// plain-float sum of those terms: |e_i| <= u |t_i| (t_i the intermediate sums, each input inside at
+// most n of them) and summing them costs at most gamma_n of their total, so
+// |R - exact| <= u |R| + (1 + 2nu)^2 (nu)^2 sum|x| (u = 2^-53, n = the non-null count, which bounds
+// every chain depth). NaN inputs or infinities make R the IEEE result of the exact sum (certified);
+// an overflowed partial (non-finite R or sum|x| from finite inputs) is not.
+static bool sum_certified(const GPart& p, double r) {
+  if (p.count == 0 || p.first_nan != UINT64_MAX || p.ninf > 0) return true;
+  if (!std::isfinite(r) || !std::isfinite(p.a)) return false;
+  const double u = 0x1p-53, nu = (double)p.count * u, g = (1.0 + 2.0 * nu);
+  const double bound = 1.01 * (u * std::fabs(r) + g * g * nu * nu * p.a);
+  return bound <= FX_REL_TOL * std::fabs(r) || p.a == 0.0;
 }
 
 // Host-side finalisation of MIN/MAX for fp64 (MaxAccumulator order semantics).
@@ -355,8 +424,8 @@ static int agg_global_partial(qe_ctx* ctx, const qe_column* col, const qe_column
 // (~6 us sooner per call: tools/exp_sync_latency.hip), with a stream query every 50 us so a failed
 // kernel still ends the wait. The result is then complete; later work on the stream is ordered
 // after the kernel as usual.
-static int agg_global_finish(qe_ctx* ctx, const GPart* dp, int32_t type, qe_global_agg* out, void* h = nullptr,
-                             volatile unsigned long long* flag = nullptr) {
+static int agg_global_finish(qe_ctx* ctx, const GPart* dp, int32_t type, qe_global_agg* out, bool* certified,
+                             void* h = nullptr, volatile unsigned long long* flag = nullptr) {
   if (!h) {
     QE_TRY(ctx_pinned(ctx, sizeof(GPart), &h));
     QE_HIP(hipMemcpyAsync(h, dp, sizeof(GPart), hipMemcpyDeviceToHost, ctx->stream));
@@ -386,6 +455,7 @@ static int agg_global_finish(qe_ctx* ctx, const GPart* dp, int32_t type, qe_glob
   out->type = type;
   out->valid = p.count > 0 ? 1 : 0;
   const double fsum = std::isfinite(p.s) ? p.s + p.c : p.s;
+  *certified = !f64 || sum_certified(p, fsum);
   if (p.count > 0) {
     if (f64) {
       out->sum = f64_bits(fsum);
@@ -413,7 +483,33 @@ extern "C" int qe_agg_global(qe_ctx* ctx, const qe_column* col, const qe_column*
   *(volatile unsigned long long*)flag = 0;  // (the previous call on this ctx has returned: its kernels wrote it)
   GPart* p;
   QE_TRY(agg_global_partial(ctx, col, mask, &p, (GPart*)h, flag));
-  return agg_global_finish(ctx, p, col->type, out, h, flag);
+  bool certified = true;
+  QE_TRY(agg_global_finish(ctx, p, col->type, out, &certified, h, flag));
+  if (certified) return QE_OK;
+  // heavy cancellation: the exact sum from a second pass over the column
+  void* s;
+  QE_TRY(ctx_scratch(ctx, 5 * sizeof(qu64), &s));
+  QE_HIP(hipMemsetAsync(s, 0, 5 * sizeof(qu64), ctx->stream));
+  const int64_t n = col->length;
+  const unsigned blocks = (unsigned)std::max<int64_t>(1, std::min<int64_t>((int64_t)div_up((uint64_t)n, 256),
+                                                                             (int64_t)ctx->num_cus * 4));
+  hipLaunchKernelGGL(k_agg_global_fx, dim3(blocks), dim3(256), 0, ctx->stream, (const int64_t*)col->values,
+                     col->validity, mask ? (const uint8_t*)mask->values : nullptr, mask ? mask->validity : nullptr, n,
+                     (qu64*)s);
+  QE_TRY(launch_check("k_agg_global_fx"));
+  void* hw;
+  QE_TRY(ctx_pinned(ctx, 5 * sizeof(qu64), &hw));
+  QE_HIP(hipMemcpyAsync(hw, s, 5 * sizeof(qu64), hipMemcpyDeviceToHost, ctx->stream));
+  QE_TRY(ctx_sync(ctx));
+  const qu64* w = (const qu64*)hw;
+  bool err = false;
+  const double v = fx_result(w[0], w[1], w[2], w[3], w[4], (qu64)out->count, &err);
+  QE_CHECK(!err, QE_ERR_UNSUPPORTED,
+           "global fp64 SUM not exact to 1e-9 (an input of 2^182 or more, or inputs below 2^-128 rounded "
+           "beyond the bound)");
+  out->sum = f64_bits(v);
+  out->avg = v / (double)out->count;
+  return QE_OK;
 }
 
 extern "C" int qe_agg_global_partial(qe_ctx* ctx, const qe_column* col, const qe_column* mask, int64_t row_base,
@@ -444,5 +540,10 @@ extern "C" int qe_agg_global_merge(qe_ctx* ctx, int32_t type, const void* partia
   hipLaunchKernelGGL(k_agg_global_final, dim3(1), dim3(256), 0, ctx->stream, parts, (int)n, (GPart*)h,
                      (unsigned long long*)nullptr);
   QE_TRY(launch_check("k_agg_global_final"));
-  return agg_global_finish(ctx, parts + n, type, out, h);
+  bool certified = true;
+  QE_TRY(agg_global_finish(ctx, parts + n, type, out, &certified, h));
+  QE_CHECK(certified, QE_ERR_UNSUPPORTED,
+           "global fp64 SUM over %d partials cannot be certified within 1e-9 of the exact sum (the shards' "
+           "sums cancel); run qe_agg_global over the whole column for the exact sum", (int)n);
+  return QE_OK;
 }
