@@ -227,7 +227,12 @@ int qe_filter_apply(qe_ctx* ctx, const qe_column* mask, const qe_column* inputs,
 /* Global (no GROUP BY) aggregate of one column (K4a), all functions in one pass.
  * min/max follow MaxAccumulator (K:538-561): nulls skipped; the first non-null value
  * seeds; replaced only on strictly greater (less) => a NaN seed is sticky, a later NaN
- * never wins, +0.0/-0.0 ties keep the earliest. `valid` = 1 iff count > 0. */
+ * never wins, +0.0/-0.0 ties keep the earliest. `valid` = 1 iff count > 0.
+ * fp64 sum / avg: within 1e-9 of the exact sum or an error. The compensated sum is certified by
+ * an error bound; when the bound cannot place it within 1e-9 (heavy cancellation), a second,
+ * exact fixed-point pass gives the correctly rounded exact sum (QE_ERR_UNSUPPORTED for an input of
+ * 2^182 or more). qe_agg_global_merge cannot go back to the rows: an uncertifiable merge returns
+ * QE_ERR_UNSUPPORTED. int64 sum wraps; int64 avg is the compensated fp64 mean. */
 typedef struct qe_global_agg {
   int64_t rows;   /* COUNT(*) over rows passing the mask */
   int64_t count;  /* COUNT(x) */

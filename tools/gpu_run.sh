@@ -16,6 +16,7 @@
 #   profile            profiles/run_profile.sh (bench kernel trace + PMC traffic)
 #   prof_trip          tools/prof_tripdata.sh (tripdata kernel trace)
 #   prof_fp64          tools/prof_fp64_sum.sh (C5 trace + SQ / LDS counters per mode)
+#   fxq                tools/exp_fxq.sh (exact-sum kernel code-shape A/B on C5)
 #   env:NAME=VALUE     set an environment variable for the following steps
 set -o pipefail
 export TMPDIR=/tmp
@@ -46,6 +47,7 @@ for s in "$@"; do
     profile) step profile 600 bash profiles/run_profile.sh ;;
     prof_trip) step prof_trip 500 env ROWS=4000000 bash tools/prof_tripdata.sh ;;
     prof_fp64) step prof_fp64 600 bash tools/prof_fp64_sum.sh ;;
+    fxq) step fxq 900 bash tools/exp_fxq.sh ;;
     *) echo "unknown step $s" >> "$OUT/steps.log"; exit 2 ;;
   esac
 done
