@@ -106,6 +106,24 @@ def main():
 
     ms_agg, (keys, vals) = timed(ctx, agg)
     got = dict(zip(keys[0].to_pylist(), vals[0].to_pylist()))
+
+    # where the aggregate stage's time goes: host wall per call, each call followed by a device sync
+    def wall(fn):
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        r = fn()
+        torch.cuda.synchronize()
+        return (time.perf_counter() - t0) * 1e3, r
+
+    parts = {}
+    for _ in range(3):
+        t_create, st = wall(lambda: HashAggregateState(ctx, [N.TYPE_UTF8], [(N.AGG_MAX, N.TYPE_FLOAT64)], 16))
+        t_enc, codes = wall(lambda: st.dicts[0].encode(vendor))
+        t_upd, _ = wall(lambda: N.check(N.lib().qe_hashagg_update(
+            st.handle, (N.QeColumn * 1)(codes.as_c()), (N.QeColumn * 1)(fare.as_c()), None)))
+        t_fin, _ = wall(st.finalize)
+        parts = {"create": t_create, "encode": t_enc, "update": t_upd, "finalize_decode": t_fin}
+        st.close()
     n = vendor.length
     check = None
     try:
@@ -130,6 +148,7 @@ def main():
         "rows": n, "csv_bytes": nbytes, "groups": got, "check_vs_pandas": check,
         "ms": {"upload_pcie": ms_up, "scan": ms_scan, "cast": ms_cast, "agg": ms_agg, "device_total": device_ms,
                "file_to_device_columns_wall": ms_file},
+        "agg_parts_wall_ms": parts,
         "rows_per_s_device": n / (device_ms * 1e-3), "csv_GBps_device": nbytes / (device_ms * 1e-3) / 1e9,
         "csv_GBps_scan": nbytes / (ms_scan * 1e-3) / 1e9, "pcie_GBps": nbytes / (ms_up * 1e-3) / 1e9,
     }))
