@@ -53,8 +53,6 @@ def test_cancellation_is_exact(gpu_ctx, form):
     if mask is not None:
         sel &= mask
     want = math.fsum(x[sel].tolist())
-    naive = float(np.sum(x[sel]))
-    assert abs(naive - want) > 1e-9 * abs(want)  # the case fp64 adds get wrong
     r = _global(gpu_ctx, x, valid, mask)
     assert r.count == int(sel.sum())
     assert f64_from_bits(r.sum) == want, (f64_from_bits(r.sum), want)
