@@ -388,6 +388,32 @@ struct LBytes {
   }
 };
 
+// Bytes by global position from a wave's 2 KiB LDS ring holding the last two 1 KiB steps of its
+// segment walk (positions [lo, hi)); anything outside comes from HBM (fields longer than a step).
+struct RBytes {
+  const uint8_t* R;  // ring: position i at R[i & 2047]
+  int64_t lo, hi;
+  const uint8_t* d;
+  __device__ __forceinline__ uint32_t operator[](int64_t i) const { return (i >= lo && i < hi) ? R[i & 2047] : d[i]; }
+  __device__ __forceinline__ uint4 bytes16(int64_t s, int64_t n) const {  // bytes [s, s + n), n <= 16
+    if (s < lo || s + n > hi) return GBytes{d, hi}.bytes16(s, n);
+    const int64_t a = s & ~(int64_t)15;
+    const int sh = (int)(s & 15);
+    const uint4 x = *(const uint4*)(R + (a & 2047));
+    unsigned __int128 v = ((unsigned __int128)(((uint64_t)x.w << 32) | x.z) << 64) | (((uint64_t)x.y << 32) | x.x);
+    if (sh) {
+      v >>= 8 * sh;
+      if (sh + n > 16) {
+        const uint4 y = *(const uint4*)(R + ((a + 16) & 2047));
+        const unsigned __int128 w = ((unsigned __int128)(((uint64_t)y.w << 32) | y.z) << 64) | (((uint64_t)y.y << 32) | y.x);
+        v |= w << (128 - 8 * sh);
+      }
+    }
+    if (n < 16) v &= (((unsigned __int128)1) << (8 * n)) - 1;
+    return make_uint4((uint32_t)v, (uint32_t)(v >> 32), (uint32_t)(v >> 64), (uint32_t)(v >> 96));
+  }
+};
+
 template <typename D>
 __device__ __forceinline__ void trim(const D& d, int64_t& s, int64_t& e) {
   while (s < e && d[s] <= 0x20) ++s;
@@ -599,8 +625,10 @@ __global__ void __launch_bounds__(256) k_csv_seg_fields(const uint8_t* __restric
                                                         int64_t first, FieldArgs Ag,
                                                         unsigned long long* __restrict__ suspect) {
   __shared__ FieldArgs A;
+  __shared__ __attribute__((aligned(16))) uint8_t ring[4][2048];
   stage_args(A, Ag);
   const int lane = threadIdx.x & 63;
+  uint8_t* const R = ring[threadIdx.x >> 6];
   const int64_t seg = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
   if (seg >= nseg) return;
   const uint64_t below = (1ull << lane) - 1;
@@ -618,6 +646,12 @@ __global__ void __launch_bounds__(256) k_csv_seg_fields(const uint8_t* __restric
   for (int64_t p0 = seg * SEG; p0 < nbytes; p0 += 1024) {
     const int64_t pos = p0 + lane * 16;
     const Lane16 v = pos < nbytes ? load16(data, nbytes, pos) : Lane16{{0, 0, 0, 0}};
+    // the step's bytes into the ring (the step before stays there): field bytes are read from LDS
+    *(uint4*)(R + (pos & 2047)) = make_uint4(v.w[0], v.w[1], v.w[2], v.w[3]);
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    const RBytes Rb{R, p0 == seg * SEG ? p0 : p0 - 1024, min(p0 + 1024, nbytes), data};
     const bool hasq = has_byte(v, '"') && eq16(v, '"') != 0;
     const uint32_t qodd = hasq ? (uint32_t)(quotes16(v) & 1) : 0u;
     const uint64_t par = __ballot(qodd);
@@ -667,13 +701,13 @@ __global__ void __launch_bounds__(256) k_csv_seg_fields(const uint8_t* __restric
       const int64_t pb_ = pos + k;
       const bool is_t = (T >> k) & 1;
       const bool own = row >= first_own && row <= last_own;
-      if (own && row >= first) record_field(G, A, f, fs, pb_, row - first);
+      if (own && row >= first) record_field(Rb, A, f, fs, pb_, row - first);
       if (is_t) {
         if (own && f == 0) sus += 1;  // no delimiter: blank, comment or a one-field line?
         ++row;
         f = 0;
         fs = pb_ + 1;
-        if (row >= first_own && row <= last_own && fs < nbytes && data[fs] == '#') sus += 1;
+        if (row >= first_own && row <= last_own && fs < nbytes && Rb[fs] == '#') sus += 1;
       } else {
         ++f;
         fs = pb_ + 1;
@@ -682,6 +716,8 @@ __global__ void __launch_bounds__(256) k_csv_seg_fields(const uint8_t* __restric
     row_c = __shfl(row, 63);
     f_c = __shfl(f, 63);
     fs_c = __shfl(fs, 63);
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");  // the ring's older half is rewritten next step
+    __builtin_amdgcn_wave_barrier();
     if (row_c > last_own) break;  // the last line that started in this segment has ended
   }
   // a final line without a terminator ends at the end of the file

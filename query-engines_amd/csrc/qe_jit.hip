@@ -889,9 +889,13 @@ bool gen_fused_source(const Plan& P, int log2, std::string* src, size_t* lds_byt
   if (compact) emit_flush_c(P, o);
   else emit_flush(P, o);
   o << "  __syncthreads();\n  if (threadIdx.x == 0 && s_newg) atomicAdd(&P.t.ctl[0], (qu64)s_newg);\n}\n";
-  static const bool fx_inline = [] {  // QE_FX_INLINE=1: the exact sums' rare paths inline (A/B knob)
+  // The exact sums' rare paths inline in the generated kernels (QE_FX_INLINE=0: out of line). C5,
+  // one box (tools/exp_fxq.sh): queue + inline 8.79-8.84 ms, queue + out of line 11.5-11.8 ms,
+  // no queue 10.9 (inline) / 14.0 ms (out of line); fp64 atomics 7.25 ms. The out-of-line calls sit
+  // in the hot loop, and the call boundary costs the whole kernel registers.
+  static const bool fx_inline = [] {
     const char* e = getenv("QE_FX_INLINE");
-    return e && e[0] == '1';
+    return !(e && e[0] == '0');
   }();
   *src = std::string(fx_inline ? "#define QE_FX_INLINE 1\n" : "") + kDevHeader + o.str();
   return true;

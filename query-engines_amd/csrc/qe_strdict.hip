@@ -318,6 +318,21 @@ __device__ __forceinline__ void encode_lookup(const DictDev& D, EncShared& S, co
       for (int k = 0; k < len; ++k) dst[k] = p[k];
     }, lane);
     if (claim) code = pc;
+    // a key another wave has claimed but not yet published: its insert is a few stores away (every
+    // workgroup is resident and the claimer waits for nobody), so wait a little for it rather than
+    // defer the row (at a batch's start every wave of the grid meets the new keys at once). After
+    // this wave's own inserts, so a claimer in this wave has published.
+    if (lead && code == R_RETRY) {
+      auto eq = [&](int cc) { return D.code_len[cc] == len && bytes_equal(D.arena + D.code_off[cc], p, len); };
+      for (int t = 0; t < 64 && code == R_RETRY; ++t) {
+        __builtin_amdgcn_s_sleep(2);
+        code = dict_probe(D, h, eq, &gslot);
+      }
+      if (code == R_CLAIMED)  // (a hash collision past the claimed slot) this lane inserts alone
+        code = dict_insert_one(D, gslot, h, len, [&](uint8_t* dst) {
+          for (int k = 0; k < len; ++k) dst[k] = p[k];
+        });
+    }
     if (lead && code >= 0 && len <= LC_BYTES) lc_insert(S.C, h, len, hd, code);
     code = __shfl(code, leader);
     if (miss) c = code;
