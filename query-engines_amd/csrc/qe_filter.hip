@@ -50,96 +50,99 @@ __global__ void __launch_bounds__(FT_THREADS) k_tile_count(const uint8_t* __rest
   }
 }
 
-// Exclusive scan of `n` int64 counts with one 1024-thread block; writes total to out[n].
-__global__ void __launch_bounds__(1024) k_scan(const int64_t* __restrict__ in, int64_t* __restrict__ out,
-                                               int64_t n) {
-  // each thread a contiguous chunk: its sum, one block-wide scan of the 1024 sums, then the chunk's
-  // prefixes (two reads of the input, which sits in L2; round 4 stepped 1024 elements at a time with
-  // three barriers per step: 17 us for the CSV scan's 23.5K segment counts)
-  __shared__ int64_t wsum[16];
-  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-  const int64_t per = (n + 1023) / 1024;
-  const int64_t lo = (int64_t)threadIdx.x * per, hi = lo + per < n ? lo + per : n;
-  int64_t t = 0;
-  for (int64_t i = lo; i < hi; ++i) t += in[i];
-  int64_t x = t;  // inclusive wave scan of the chunk sums
-  for (int off = 1; off < 64; off <<= 1) {
-    const int64_t y = __shfl_up(x, off);
-    if (lane >= off) x += y;
-  }
-  if (lane == 63) wsum[wid] = x;
-  __syncthreads();
-  int64_t run = x - t;
-  for (int w = 0; w < wid; ++w) run += wsum[w];
-  for (int64_t i = lo; i < hi; ++i) {
-    const int64_t v = in[i];
-    out[i] = run;
-    run += v;
-  }
-  if (threadIdx.x == 1023) {
-    int64_t total = 0;
-    for (int w = 0; w < 16; ++w) total += wsum[w];
-    out[n] = total;
-  }
-}
-
-// Device-wide scan for large inputs: per-8192-element block sums -> one-block scan of the sums
-// -> per-block scan with the block's offset (3 launches, 2 passes over the input).
+// Device-wide int64 exclusive scans. A 1024-thread block takes tiles of 8192 elements; wave w of
+// the block holds elements 512 w + 64 k + lane (k < 8) of a tile, so every load and store
+// instruction moves one contiguous 512-byte row (round 4 gave each thread 8 consecutive elements:
+// 64-byte lane strides, and the one-block scan walked its chunks serially: 16.6 us per call for
+// the CSV scan's 23.5K segment counts, 54 us for a 4M-row length column).
 constexpr int GS_THREADS = 1024, GS_PER = 8;
 constexpr int64_t GS_TILE = (int64_t)GS_THREADS * GS_PER;
 
-__device__ __forceinline__ int64_t block_excl_scan(int64_t v, int64_t* wsum, int64_t* total) {
+__device__ __forceinline__ void tile_load(const int64_t* __restrict__ in, int64_t n, int64_t b0, int64_t (&v)[GS_PER]) {
+  const int64_t e0 = b0 + (int64_t)(threadIdx.x >> 6) * 512 + (threadIdx.x & 63);
+#pragma unroll
+  for (int k = 0; k < GS_PER; ++k) v[k] = e0 + 64 * k < n ? in[e0 + 64 * k] : 0;
+}
+
+// Exclusive prefixes of a loaded tile (+ carry) stored to out; returns the tile's total.
+__device__ __forceinline__ int64_t tile_scan_store(const int64_t (&v)[GS_PER], int64_t* __restrict__ out, int64_t n,
+                                                   int64_t b0, int64_t carry, int64_t* wsum) {
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-  int64_t x = v;
-  for (int off = 1; off < 64; off <<= 1) {
-    const int64_t y = __shfl_up(x, off);
-    if (lane >= off) x += y;
+  int64_t run = 0, ex[GS_PER];
+#pragma unroll
+  for (int k = 0; k < GS_PER; ++k) {  // row k of the wave: inclusive lane scan, then the rows before
+    int64_t x = v[k];
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+      const int64_t y = __shfl_up(x, off);
+      if (lane >= off) x += y;
+    }
+    ex[k] = run + x - v[k];
+    run += __shfl(x, 63);
   }
-  if (lane == 63) wsum[wid] = x;
+  if (lane == 0) wsum[wid] = run;
   __syncthreads();
   int64_t wprefix = 0, all = 0;
+#pragma unroll
   for (int w = 0; w < GS_THREADS / 64; ++w) {
     if (w < wid) wprefix += wsum[w];
     all += wsum[w];
   }
-  *total = all;
-  return wprefix + x - v;
+  __syncthreads();  // wsum is rewritten by the next tile
+  const int64_t e0 = b0 + (int64_t)wid * 512 + lane;
+#pragma unroll
+  for (int k = 0; k < GS_PER; ++k)
+    if (e0 + 64 * k < n) out[e0 + 64 * k] = carry + wprefix + ex[k];
+  return all;
+}
+
+// One block, any n (writes the total to out[n]): KS_TILES tiles' loads are issued before the first
+// of them is scanned, so up to KS_TILES tiles the block waits for memory once.
+constexpr int KS_TILES = 4;
+__global__ void __launch_bounds__(1024) k_scan(const int64_t* __restrict__ in, int64_t* __restrict__ out,
+                                               int64_t n) {
+  __shared__ int64_t wsum[16];
+  int64_t carry = 0;
+  for (int64_t g0 = 0; g0 < n; g0 += KS_TILES * GS_TILE) {
+    int64_t v[KS_TILES][GS_PER];
+#pragma unroll
+    for (int t = 0; t < KS_TILES; ++t) tile_load(in, n, g0 + t * GS_TILE, v[t]);
+#pragma unroll
+    for (int t = 0; t < KS_TILES; ++t)
+      if (g0 + t * GS_TILE < n) carry += tile_scan_store(v[t], out, n, g0 + t * GS_TILE, carry, wsum);
+  }
+  if (threadIdx.x == 0) out[n] = carry;
 }
 
 __global__ void __launch_bounds__(GS_THREADS) k_scan_reduce(const int64_t* __restrict__ in, int64_t n,
                                                              int64_t* __restrict__ sums) {
   __shared__ int64_t wsum[GS_THREADS / 64];
-  const int64_t i0 = blockIdx.x * GS_TILE + (int64_t)threadIdx.x * GS_PER;
+  int64_t v[GS_PER];
+  tile_load(in, n, blockIdx.x * GS_TILE, v);
   int64_t t = 0;
 #pragma unroll
-  for (int k = 0; k < GS_PER; ++k) t += (i0 + k < n) ? in[i0 + k] : 0;
-  int64_t total;
-  (void)block_excl_scan(t, wsum, &total);
-  if (threadIdx.x == 0) sums[blockIdx.x] = total;
+  for (int k = 0; k < GS_PER; ++k) t += v[k];
+  for (int off = 32; off > 0; off >>= 1) t += __shfl_xor(t, off);
+  if ((threadIdx.x & 63) == 0) wsum[threadIdx.x >> 6] = t;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    int64_t all = 0;
+    for (int w = 0; w < GS_THREADS / 64; ++w) all += wsum[w];
+    sums[blockIdx.x] = all;
+  }
 }
 
 __global__ void __launch_bounds__(GS_THREADS) k_scan_apply(const int64_t* __restrict__ in, int64_t* __restrict__ out,
                                                             int64_t n, const int64_t* __restrict__ offs, int64_t nb) {
   __shared__ int64_t wsum[GS_THREADS / 64];
-  const int64_t i0 = blockIdx.x * GS_TILE + (int64_t)threadIdx.x * GS_PER;
-  int64_t v[GS_PER], t = 0;
-#pragma unroll
-  for (int k = 0; k < GS_PER; ++k) {
-    v[k] = (i0 + k < n) ? in[i0 + k] : 0;
-    t += v[k];
-  }
-  int64_t total;
-  int64_t run = offs[blockIdx.x] + block_excl_scan(t, wsum, &total);
-#pragma unroll
-  for (int k = 0; k < GS_PER; ++k) {
-    if (i0 + k < n) out[i0 + k] = run;
-    run += v[k];
-  }
+  int64_t v[GS_PER];
+  tile_load(in, n, blockIdx.x * GS_TILE, v);
+  (void)tile_scan_store(v, out, n, blockIdx.x * GS_TILE, offs[blockIdx.x], wsum);
   if (blockIdx.x == nb - 1 && threadIdx.x == 0) out[n] = offs[nb];
 }
 
 int exclusive_scan_i64(qe_ctx* ctx, const int64_t* in, int64_t* out, int64_t n) {
-  if (n <= 4 * GS_TILE) {
+  if (n <= KS_TILES * GS_TILE) {
     hipLaunchKernelGGL(k_scan, dim3(1), dim3(1024), 0, ctx->stream, in, out, n);
     return launch_check("k_scan");
   }
