@@ -98,7 +98,7 @@ __device__ __forceinline__ int64_t tile_scan_store(const int64_t (&v)[GS_PER], i
 
 // One block, any n (writes the total to out[n]): KS_TILES tiles' loads are issued before the first
 // of them is scanned, so up to KS_TILES tiles the block waits for memory once.
-constexpr int KS_TILES = 4;
+constexpr int KS_TILES = 1;
 __global__ void __launch_bounds__(1024) k_scan(const int64_t* __restrict__ in, int64_t* __restrict__ out,
                                                int64_t n) {
   __shared__ int64_t wsum[16];

@@ -17,7 +17,9 @@
 #   prof_trip          tools/prof_tripdata.sh (tripdata kernel trace)
 #   prof_fp64          tools/prof_fp64_sum.sh (C5 trace + SQ / LDS counters per mode)
 #   fxq                tools/exp_fxq.sh (exact-sum kernel code-shape A/B on C5)
-#   env:NAME=VALUE     set an environment variable for the following steps
+#   csvpmc             tools/prof_csv_pmc.sh (SQ / LDS counters of the tripdata kernels, 4M rows)
+#   env:NAME=VALUE     set an environment variable for the following steps (env:TAG=x suffixes the
+#                      output files of tripdata / configs / fp64 with _x)
 set -o pipefail
 export TMPDIR=/tmp
 OUT=${GRAFT_REPO_ROOT:-$PWD}/gpurun_out/${1:?usage: gpu_run.sh OUT STEP...}
@@ -40,10 +42,11 @@ for s in "$@"; do
     tests:*) step tests 1000 bash -c "python3 -u -m pytest tests -q -m gpu --timeout 280 --timeout-method thread -k '${s#tests:}' > '$OUT/tests.txt' 2>&1" ;;
     smoke) step smoke 180 bash -c "python3 -c 'import __graft_entry__ as g; g.smoke()' > '$OUT/smoke.txt' 2>&1" ;;
     bench) step bench 300 bash -c "python3 bench.py > '$OUT/bench.json' 2> '$OUT/bench.err'" ;;
-    configs) step configs 600 bash -c "python3 tools/bench_configs.py C2 C2L C2LN C3 C4 C5 > '$OUT/configs.jsonl' 2> '$OUT/configs.err'" ;;
+    configs) step configs 600 bash -c "python3 tools/bench_configs.py C2 C2L C2LN C3 C4 C5 > '$OUT/configs${TAG:+_$TAG}.jsonl' 2> '$OUT/configs${TAG:+_$TAG}.err'" ;;
     groups) step groups 600 bash -c "python3 tools/bench_groups.py 1000000000 1024 4096 5800 8192 65536 1048576 > '$OUT/groups.jsonl' 2> '$OUT/groups.err'" ;;
-    tripdata) step tripdata 300 bash -c "python3 tools/bench_tripdata.py > '$OUT/tripdata.json' 2> '$OUT/tripdata.err'" ;;
-    fp64) step fp64 300 bash -c "python3 tools/exp_fp64_sum.py C5 C4 --rounds 3 > '$OUT/fp64.jsonl' 2>&1" ;;
+    tripdata) step tripdata 300 bash -c "python3 tools/bench_tripdata.py > '$OUT/tripdata${TAG:+_$TAG}.json' 2> '$OUT/tripdata${TAG:+_$TAG}.err'" ;;
+    fp64) step fp64 300 bash -c "python3 tools/exp_fp64_sum.py C5 C4 --rounds 3 > '$OUT/fp64${TAG:+_$TAG}.jsonl' 2>&1" ;;
+    csvpmc) step csvpmc 700 env ROWS=4000000 bash tools/prof_csv_pmc.sh ;;
     profile) step profile 600 bash profiles/run_profile.sh ;;
     prof_trip) step prof_trip 500 env ROWS=4000000 bash tools/prof_tripdata.sh ;;
     prof_fp64) step prof_fp64 600 bash tools/prof_fp64_sum.sh ;;
