@@ -500,7 +500,13 @@ int qe_strdict_destroy(qe_strdict* dict);
 /* Number of distinct strings inserted so far. */
 int qe_strdict_size(qe_strdict* dict, int64_t* out);
 /* codes (INT32, capacity >= in->length; validity required iff `in` has one, copied from it):
- * the code of every non-null row of the UTF8 column `in`, inserting new strings. */
+ * the code of every non-null row of the UTF8 column `in`, inserting new strings.
+ * An INT64 codes column asks for WIDE codes: a string of at most 7 bytes is its own code (its
+ * bytes little-endian in bits 0..55, its length in bits 56..58) and is not inserted; a longer one
+ * is 2^62 | its dictionary code. Equal strings get equal codes, bit 63 is never set, and
+ * qe_strdict_decode / _decode_bytes take either code width (qe_strdict_size counts the long
+ * strings only). A hash aggregate over wide codes groups by an INT64 key with no dictionary
+ * traffic for short keys (the reference's VendorID, K:1336). */
 int qe_strdict_encode(qe_strdict* dict, const qe_column* in, qe_column* codes);
 /* Total bytes of the strings the non-null rows of `codes` (INT32) decode to. */
 int qe_strdict_decode_bytes(qe_strdict* dict, const qe_column* codes, int64_t* out_bytes);

@@ -189,12 +189,27 @@ __device__ int dict_find_or_insert(const DictDev& D, const uint8_t* p, int len, 
 
 constexpr int ENC_THREADS = 256;
 
+// Wide (int64) key codes (qe_strdict_encode64): a key of at most 7 bytes IS its code — its bytes in
+// bits 0..55 (little-endian) and its length in bits 56..58 — and never touches the dictionary; a
+// longer key is WIDE_DICT | its dictionary code. Equal strings get equal codes either way, a short
+// and a long string never collide, and bit 63 stays clear (the hash aggregate's empty key is
+// INT64_MIN).
+constexpr int WIDE_MAX = 7;
+constexpr uint64_t WIDE_DICT = 1ull << 62;
+__device__ __forceinline__ int64_t wide_pack(uint64_t w, int len) {
+  return (int64_t)((w & ((1ull << 56) - 1)) | ((uint64_t)len << 56));
+}
+__device__ __forceinline__ void put_code(int32_t* codes, int64_t* codes64, int64_t i, int c) {
+  if (codes64) codes64[i] = c >= 0 ? (int64_t)(WIDE_DICT | (uint64_t)c) : 0;
+  else codes[i] = c >= 0 ? c : 0;
+}
+
 __device__ __forceinline__ void encode_row(const DictDev& D, const int32_t* offs, const uint8_t* bytes, int64_t i,
-                                           int32_t* codes, uint32_t* retry) {
+                                           int32_t* codes, int64_t* codes64, uint32_t* retry) {
   const int32_t s0 = offs[i], len = offs[i + 1] - s0;
   const uint8_t* p = bytes + s0;
   const int c = dict_find_or_insert(D, p, len, str_hash(p, len));
-  codes[i] = c >= 0 ? c : 0;
+  put_code(codes, codes64, i, c);
   if (c == R_RETRY) {
     atomicOr(&retry[i >> 5], 1u << (i & 31));
     atomicAdd(&D.flags[1], 1u);
@@ -287,7 +302,8 @@ constexpr int DEF_CAP = 2048;
 
 __device__ __forceinline__ void encode_lookup(const DictDev& D, EncShared& S, const int32_t* __restrict__ offs,
                                               const uint8_t* __restrict__ bytes, int64_t n, int64_t i, bool live,
-                                              int32_t* __restrict__ codes, uint32_t* __restrict__ retry, int lane) {
+                                              int32_t* __restrict__ codes, int64_t* __restrict__ codes64,
+                                              uint32_t* __restrict__ retry, int lane) {
   int32_t len = 0;
   const uint8_t* p = bytes;
   uint64_t h = 0;
@@ -338,7 +354,7 @@ __device__ __forceinline__ void encode_lookup(const DictDev& D, EncShared& S, co
     if (miss) c = code;
   }
   if (i < n) {
-    codes[i] = (live && c >= 0) ? c : 0;
+    put_code(codes, codes64, i, live ? c : -1);
     if (live && c == R_OVERFLOW) S.wg_full = 1;
     if (live && c == R_RETRY) {
       const int d = atomicAdd(&S.ndef, 1);
@@ -367,11 +383,14 @@ __device__ __forceinline__ uint64_t str_hash_short(uint64_t w, int len) {
 // is looked up in the LDS cache by its one word; every other row (longer keys, cache misses while
 // the cache warms) takes encode_lookup. Round 4 ran one row per lane per step, 8 waves per CU:
 // 112 us for tripdata's 4M VendorIDs.
+// WIDE (int64 codes): keys of at most 7 bytes are packed in place, only longer keys look up.
 constexpr int ENC_BLOCK = 1024;
+template <bool WIDE>
 __global__ void __launch_bounds__(ENC_BLOCK) k_dict_encode(DictDev D, const int32_t* __restrict__ offs,
                                                            const uint8_t* __restrict__ bytes,
                                                            const uint8_t* __restrict__ valid, int64_t n,
-                                                           int32_t* __restrict__ codes, uint32_t* __restrict__ retry) {
+                                                           int32_t* __restrict__ codes, int64_t* __restrict__ codes64,
+                                                           uint32_t* __restrict__ retry) {
   __shared__ EncShared S;
   for (int k = threadIdx.x; k < LC_SLOTS; k += blockDim.x) S.C.state[k] = 0;
   if (threadIdx.x == 0) {
@@ -400,16 +419,24 @@ __global__ void __launch_bounds__(ENC_BLOCK) k_dict_encode(DictDev D, const int3
       w[r] = (live[r] && len[r] <= 8) ? load_u64_unaligned(bytes + s0[r], len[r]) : 0ull;
     }
     qu32 slow = 0;
+    if (WIDE) {
 #pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      int c = -1;
-      if (live[r] && len[r] <= 8) {
-        const uint64_t h = str_hash_short(w[r], len[r]);
-        const uint64_t hd[LC_BYTES / 8] = {w[r], 0, 0, 0, 0};
-        c = lc_find(S.C, h, len[r], hd);
+      for (int r = 0; r < 4; ++r) {
+        if (live[r] && len[r] > WIDE_MAX) slow |= 1u << r;
+        else if (row[r] < n) codes64[row[r]] = live[r] ? wide_pack(w[r], len[r]) : 0;
       }
-      if (live[r] && c < 0) slow |= 1u << r;
-      else if (row[r] < n) codes[row[r]] = live[r] ? c : 0;
+    } else {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        int c = -1;
+        if (live[r] && len[r] <= 8) {
+          const uint64_t h = str_hash_short(w[r], len[r]);
+          const uint64_t hd[LC_BYTES / 8] = {w[r], 0, 0, 0, 0};
+          c = lc_find(S.C, h, len[r], hd);
+        }
+        if (live[r] && c < 0) slow |= 1u << r;
+        else if (row[r] < n) codes[row[r]] = live[r] ? c : 0;
+      }
     }
     // rows the cache did not answer: the full lookup, one row position at a time (rolled: its
     // code is large and runs only while the cache warms or for long keys)
@@ -418,7 +445,7 @@ __global__ void __launch_bounds__(ENC_BLOCK) k_dict_encode(DictDev D, const int3
       const bool sl = (slow >> r) & 1;
       if (!__ballot(sl)) continue;
       const int64_t i = base + 64 * r + lane;
-      encode_lookup(D, S, offs, bytes, n, i, sl, codes, retry, lane);
+      encode_lookup(D, S, offs, bytes, n, i, sl, codes, WIDE ? codes64 : nullptr, retry, lane);
     }
   }
   __syncthreads();
@@ -435,7 +462,7 @@ __global__ void __launch_bounds__(ENC_BLOCK) k_dict_encode(DictDev D, const int3
       c = lc_find(S.C, h, len, hd);
     }
     if (c < 0) c = dict_find_or_insert(D, p, len, h);
-    codes[i] = c >= 0 ? c : 0;
+    put_code(codes, WIDE ? codes64 : nullptr, i, c);
     if (c == R_OVERFLOW) S.wg_full = 1;
     if (c == R_RETRY) {
       atomicOr(&retry[i >> 5], 1u << (i & 31));
@@ -448,6 +475,7 @@ __global__ void __launch_bounds__(ENC_BLOCK) k_dict_encode(DictDev D, const int3
 __global__ void __launch_bounds__(ENC_THREADS) k_dict_encode_retry(DictDev D, const int32_t* __restrict__ offs,
                                                                    const uint8_t* __restrict__ bytes, int64_t n,
                                                                    int32_t* __restrict__ codes,
+                                                                   int64_t* __restrict__ codes64,
                                                                    const uint32_t* __restrict__ retry_in,
                                                                    uint32_t* __restrict__ retry_out) {
   const int64_t words = (n + 31) >> 5;
@@ -456,7 +484,7 @@ __global__ void __launch_bounds__(ENC_THREADS) k_dict_encode_retry(DictDev D, co
     while (bits) {
       const int j = __builtin_ctz(bits);
       bits &= bits - 1;
-      encode_row(D, offs, bytes, (w << 5) + j, codes, retry_out);
+      encode_row(D, offs, bytes, (w << 5) + j, codes, codes64, retry_out);
     }
   }
 }
@@ -705,32 +733,68 @@ __global__ void k_dict_rebuild(DictDev D, int64_t ncodes) {
   }
 }
 
-__global__ void k_dict_decode_len(const int32_t* __restrict__ codes, const uint8_t* __restrict__ valid, int64_t n,
+// Code i of a codes column: int32 (WIDE false) or a wide int64 code; *len its key's length, *c its
+// dictionary code (-1: packed in the wide code itself), false if out of range.
+template <bool WIDE>
+__device__ __forceinline__ bool code_at(const void* codes, int64_t i, const int32_t* code_len, int64_t ncodes,
+                                        int64_t* len, int64_t* c, uint64_t* packed) {
+  if (WIDE) {
+    const uint64_t x = (uint64_t)((const int64_t*)codes)[i];
+    if (!(x & WIDE_DICT)) {
+      *len = (int64_t)((x >> 56) & 0xFF);
+      *c = -1;
+      *packed = x;
+      return (x >> 59) == 0 && *len <= WIDE_MAX;
+    }
+    const uint64_t d = x & ~WIDE_DICT;
+    if (d >= (uint64_t)ncodes) return false;
+    *c = (int64_t)d;
+  } else {
+    const int32_t d = ((const int32_t*)codes)[i];
+    if (d < 0 || d >= ncodes) return false;
+    *c = d;
+  }
+  *len = code_len[*c];
+  return true;
+}
+
+template <bool WIDE>
+__global__ void k_dict_decode_len(const void* __restrict__ codes, const uint8_t* __restrict__ valid, int64_t n,
                                   const int32_t* __restrict__ code_len, int64_t ncodes, int64_t* __restrict__ lens,
                                   unsigned int* __restrict__ bad) {
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
     int64_t l = 0;
     if (!valid || ((valid[i >> 3] >> (i & 7)) & 1)) {
-      const int32_t c = codes[i];
-      if (c < 0 || c >= ncodes) atomicOr(bad, 1u);
-      else l = code_len[c];
+      int64_t c;
+      uint64_t packed;
+      if (!code_at<WIDE>(codes, i, code_len, ncodes, &l, &c, &packed)) {
+        atomicOr(bad, 1u);
+        l = 0;
+      }
     }
     lens[i] = l;
   }
 }
 
-__global__ void k_dict_decode_copy(const int32_t* __restrict__ codes, const uint8_t* __restrict__ valid, int64_t n,
+template <bool WIDE>
+__global__ void k_dict_decode_copy(const void* __restrict__ codes, const uint8_t* __restrict__ valid, int64_t n,
                                    const int64_t* __restrict__ code_off, const int32_t* __restrict__ code_len,
-                                   const uint8_t* __restrict__ arena, const int64_t* __restrict__ starts,
+                                   int64_t ncodes, const uint8_t* __restrict__ arena, const int64_t* __restrict__ starts,
                                    int32_t* __restrict__ out_offs, uint8_t* __restrict__ out_bytes) {
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i <= n; i += (int64_t)gridDim.x * blockDim.x) {
     out_offs[i] = (int32_t)starts[i];
     if (i == n) continue;
     if (valid && !((valid[i >> 3] >> (i & 7)) & 1)) continue;
-    const int32_t c = codes[i];
-    const uint8_t* src = arena + code_off[c];
+    int64_t l, c;
+    uint64_t packed = 0;
+    if (!code_at<WIDE>(codes, i, code_len, ncodes, &l, &c, &packed)) continue;  // (reported by decode_len)
     uint8_t* dst = out_bytes + starts[i];
-    for (int k = 0; k < code_len[c]; ++k) dst[k] = src[k];
+    if (c < 0) {
+      for (int k = 0; k < l; ++k) dst[k] = (uint8_t)(packed >> (8 * k));
+    } else {
+      const uint8_t* src = arena + code_off[c];
+      for (int64_t k = 0; k < l; ++k) dst[k] = src[k];
+    }
   }
 }
 
@@ -850,10 +914,15 @@ int qe_strdict_create(qe_ctx* ctx, int64_t expected_distinct, qe_strdict** out) 
   int st = QE_OK;
   if ((st = grow_array(ctx, &d->code_off, 0, d->ccap)) != QE_OK || (st = grow_array(ctx, &d->code_len, 0, d->ccap)) ||
       (st = grow_array(ctx, &d->code_hash, 0, d->ccap)) || (st = grow_array(ctx, &d->arena, 0, d->acap)) ||
-      (st = grow_array(ctx, &d->ctl, 0, 24)) || (st = grow_slots(d, (uint64_t)d->ccap * 2)) || (st = write_ctl(d))) {
+      (st = grow_array(ctx, &d->ctl, 0, 24)) || (st = grow_slots(d, (uint64_t)d->ccap * 2))) {
     dict_free(d);
     delete d;
     return st;
+  }
+  if (hipMemsetAsync(d->ctl, 0, 24, ctx->stream) != hipSuccess) {  // ncodes, arena_used, flags = 0: no host copy
+    dict_free(d);
+    delete d;
+    return fail(QE_ERR_DEVICE, "strdict control block init failed");
   }
   *out = d;
   return QE_OK;
@@ -950,7 +1019,11 @@ int qe_strdict_encode(qe_strdict* d, const qe_column* in, qe_column* codes) {
   QE_TRY(ctx_enter(ctx));
   QE_CHECK(in->type == QE_TYPE_UTF8 && in->offsets, QE_ERR_UNSUPPORTED, "string dictionary input must be UTF8");
   QE_CHECK(d->mode != 2, QE_ERR_INVALID_ARG, "dictionary holds key tuples, not strings");
-  QE_CHECK(codes->type == QE_TYPE_INT32, QE_ERR_INVALID_ARG, "codes column must be INT32");
+  QE_CHECK(codes->type == QE_TYPE_INT32 || codes->type == QE_TYPE_INT64, QE_ERR_INVALID_ARG,
+           "codes column must be INT32 (dictionary codes) or INT64 (wide codes)");
+  const bool wide = codes->type == QE_TYPE_INT64;
+  int32_t* c32 = wide ? nullptr : (int32_t*)codes->values;
+  int64_t* c64 = wide ? (int64_t*)codes->values : nullptr;
   const int64_t n = in->length;
   QE_CHECK(codes->length >= n && (codes->values || n == 0), QE_ERR_CAPACITY, "codes column too small");
   QE_CHECK(!in->validity || codes->validity, QE_ERR_INVALID_ARG, "codes validity buffer required");
@@ -978,14 +1051,18 @@ int qe_strdict_encode(qe_strdict* d, const qe_column* in, qe_column* codes) {
   return encode_loop(
       d, n, (int64_t)o[0] - o[1],
       [&](uint32_t* retry) {
-        hipLaunchKernelGGL(k_dict_encode, dim3(grid), dim3(ENC_BLOCK), 0, ctx->stream, d->dev(), in->offsets,
-                           (const uint8_t*)in->values, in->validity, n, (int32_t*)codes->values, retry);
+        if (wide)
+          hipLaunchKernelGGL(k_dict_encode<true>, dim3(grid), dim3(ENC_BLOCK), 0, ctx->stream, d->dev(), in->offsets,
+                             (const uint8_t*)in->values, in->validity, n, c32, c64, retry);
+        else
+          hipLaunchKernelGGL(k_dict_encode<false>, dim3(grid), dim3(ENC_BLOCK), 0, ctx->stream, d->dev(), in->offsets,
+                             (const uint8_t*)in->values, in->validity, n, c32, c64, retry);
         return launch_check("k_dict_encode");
       },
       [&](const uint32_t* rin, uint32_t* rout, int64_t words) {
         const int g2 = (int)std::min<int64_t>((int64_t)div_up((uint64_t)words, 256), (int64_t)ctx->num_cus * 4);
         hipLaunchKernelGGL(k_dict_encode_retry, dim3(g2), dim3(256), 0, ctx->stream, d->dev(), in->offsets,
-                           (const uint8_t*)in->values, n, (int32_t*)codes->values, rin, rout);
+                           (const uint8_t*)in->values, n, c32, c64, rin, rout);
         return launch_check("k_dict_encode_retry");
       });
 }
@@ -1101,7 +1178,8 @@ int qe_strdict_decode_bytes(qe_strdict* d, const qe_column* codes, int64_t* out_
   QE_CHECK(d && codes && out_bytes, QE_ERR_INVALID_ARG, "null argument");
   qe_ctx* ctx = d->ctx;
   QE_TRY(ctx_enter(ctx));
-  QE_CHECK(codes->type == QE_TYPE_INT32, QE_ERR_INVALID_ARG, "codes column must be INT32");
+  QE_CHECK(codes->type == QE_TYPE_INT32 || codes->type == QE_TYPE_INT64, QE_ERR_INVALID_ARG,
+           "codes column must be INT32 or INT64 (wide codes)");
   const int64_t n = codes->length;
   *out_bytes = 0;
   if (n == 0) return QE_OK;
@@ -1112,8 +1190,12 @@ int qe_strdict_decode_bytes(qe_strdict* d, const qe_column* codes, int64_t* out_
   unsigned int* bad = (unsigned int*)(starts + n + 1);
   QE_HIP(hipMemsetAsync(bad, 0, 4, ctx->stream));
   const int grid = (int)std::min<int64_t>((int64_t)div_up((uint64_t)n, 256), (int64_t)ctx->num_cus * 8);
-  hipLaunchKernelGGL(k_dict_decode_len, dim3(grid), dim3(256), 0, ctx->stream, (const int32_t*)codes->values,
-                     codes->validity, n, d->code_len, d->ncodes, lens, bad);
+  if (codes->type == QE_TYPE_INT64)
+    hipLaunchKernelGGL(k_dict_decode_len<true>, dim3(grid), dim3(256), 0, ctx->stream, codes->values, codes->validity,
+                       n, d->code_len, d->ncodes, lens, bad);
+  else
+    hipLaunchKernelGGL(k_dict_decode_len<false>, dim3(grid), dim3(256), 0, ctx->stream, codes->values,
+                       codes->validity, n, d->code_len, d->ncodes, lens, bad);
   QE_TRY(launch_check("k_dict_decode_len"));
   QE_TRY(exclusive_scan_i64(ctx, lens, starts, n));
   int64_t h[2] = {0, 0};
@@ -1142,9 +1224,13 @@ int qe_strdict_decode(qe_strdict* d, const qe_column* codes, qe_column* out) {
   QE_CHECK(out->values || total == 0, QE_ERR_CAPACITY, "output values buffer required");
   const int64_t* starts = (const int64_t*)ctx->scratch + n;
   const int grid = (int)std::min<int64_t>((int64_t)div_up((uint64_t)n + 1, 256), (int64_t)ctx->num_cus * 8);
-  hipLaunchKernelGGL(k_dict_decode_copy, dim3(grid), dim3(256), 0, ctx->stream, (const int32_t*)codes->values,
-                     codes->validity, n, d->code_off, d->code_len, d->arena, starts, out->offsets,
-                     (uint8_t*)out->values);
+  if (codes->type == QE_TYPE_INT64)
+    hipLaunchKernelGGL(k_dict_decode_copy<true>, dim3(grid), dim3(256), 0, ctx->stream, codes->values, codes->validity,
+                       n, d->code_off, d->code_len, d->ncodes, d->arena, starts, out->offsets, (uint8_t*)out->values);
+  else
+    hipLaunchKernelGGL(k_dict_decode_copy<false>, dim3(grid), dim3(256), 0, ctx->stream, codes->values,
+                       codes->validity, n, d->code_off, d->code_len, d->ncodes, d->arena, starts, out->offsets,
+                       (uint8_t*)out->values);
   QE_TRY(launch_check("k_dict_decode_copy"));
   if (codes->validity)
     QE_HIP(hipMemcpyAsync(out->validity, codes->validity, (size_t)div_up((uint64_t)n, 8),

@@ -27,7 +27,8 @@ def _device_column(ctx, type_id: int, vals, valid) -> DeviceColumn:
     from .columnar import bitmap_bytes
 
     n = vals.numel()
-    dt = {N.TYPE_INT32: torch.int32, N.TYPE_DATE32: torch.int32, N.TYPE_UINT8: torch.uint8}[type_id]
+    dt = {N.TYPE_INT32: torch.int32, N.TYPE_DATE32: torch.int32, N.TYPE_UINT8: torch.uint8,
+          N.TYPE_INT64: torch.int64}[type_id]
     v = vals.to(dt).contiguous() if n else torch.zeros(1, dtype=dt, device=vals.device)
     bits = torch.zeros(max(bitmap_bytes(n), 4) * 8, dtype=torch.uint8, device=vals.device)
     bits[:n] = valid.to(torch.uint8)
@@ -121,10 +122,13 @@ class HashAggregateState:
         self.expected_groups = int(expected_groups)
         self.key_types = list(key_types)
         self.aggs = [(int(f), int(t)) for f, t in aggs]
-        # UTF-8 keys: grouped by their dictionary code (INT32), decoded in finalize
-        self.dicts = {i: StringDictionary(ctx, expected_groups) for i, t in enumerate(self.key_types)
+        # UTF-8 keys: grouped by their dictionary code, decoded in finalize. A lone UTF-8 key takes
+        # wide INT64 codes (keys of up to 7 bytes packed in place, no dictionary traffic); in a
+        # key set, INT32 codes keep the set packable into 63 bits
+        wide = len(self.key_types) == 1
+        self.dicts = {i: StringDictionary(ctx, expected_groups, wide=wide) for i, t in enumerate(self.key_types)
                       if t == N.TYPE_UTF8}
-        self.member_types = [N.TYPE_INT32 if t == N.TYPE_UTF8 else t for t in self.key_types]
+        self.member_types = [self.dicts[i].code_type if t == N.TYPE_UTF8 else t for i, t in enumerate(self.key_types)]
         # key sets that do not pack into 63 bits group by one code per distinct key tuple
         self.tuple_dict = None
         if not packable(self.member_types):
@@ -309,8 +313,15 @@ class HashAggregateState:
     def keyed_by_dictionary(self) -> bool:
         return bool(self.dicts) or self.tuple_dict is not None
 
+    def _wide_key(self) -> bool:
+        """One INT64 device key (a lone UTF-8 key's wide codes): records carry it whole, with the
+        null group flagged in the record's second word, instead of packed narrow keys."""
+        return self.device_key_types == [N.TYPE_INT64]
+
     def _packing(self):
         """(shift, nullbit, width) per device key, as qe_hashagg_create packs narrow keys."""
+        if self._wide_key():
+            return []
         out, bit = [], 0
         for t in self.device_key_types:
             w = _KEY_BITS[t]
@@ -327,6 +338,8 @@ class HashAggregateState:
         rec = records[: n * self.record_bytes()].view(torch.int64).view(n, -1)
         packed = rec[:, 0]
         members = []
+        if self._wide_key():  # one INT64 key (wide string codes): the key word and the null flag
+            members.append(_device_column(self.ctx, N.TYPE_INT64, packed, rec[:, 1] == 0))
         for (shift, nullbit, w), t in zip(self._packing(), self.device_key_types):
             vals = (packed >> shift) & ((1 << w) - 1)
             valid = ((packed >> nullbit) & 1) == 0
@@ -348,8 +361,8 @@ class HashAggregateState:
         return out
 
     def packed_keys(self, key_cols: Sequence[DeviceColumn]):
-        """int64 packed device keys of rows given as original key columns (encodes new strings /
-        tuples into this state's dictionaries)."""
+        """(int64 device key words, null-group flags) of rows given as original key columns
+        (encodes new strings / tuples into this state's dictionaries)."""
         import torch
 
         members = [self.dicts[i].encode(k) if i in self.dicts else k for i, k in enumerate(key_cols)]
@@ -357,11 +370,17 @@ class HashAggregateState:
             members = [self.tuple_dict.encode_tuple(members)]
         n = members[0].length
         packed = torch.zeros(n, dtype=torch.int64, device=self.ctx.torch_device)
+        knull = torch.zeros(n, dtype=torch.int64, device=self.ctx.torch_device)
+        if self._wide_key():
+            m = members[0]
+            valid = torch.from_numpy(m.valid_mask()).to(self.ctx.torch_device)
+            packed = torch.where(valid, m.values[:n].to(torch.int64), packed)
+            knull = (~valid).to(torch.int64)
         for (shift, nullbit, w), m in zip(self._packing(), members):
             vals = m.values[:n].to(torch.int64) & ((1 << w) - 1)
             valid = torch.from_numpy(m.valid_mask()).to(self.ctx.torch_device)
             packed |= torch.where(valid, vals << shift, torch.zeros_like(vals)) | ((~valid).to(torch.int64) << nullbit)
-        return packed
+        return packed, knull
 
     def import_keyed(self, records, n: int, key_cols: Sequence[DeviceColumn]) -> None:
         """Import records whose keys come from another state: rewrite their key field from the
@@ -371,8 +390,7 @@ class HashAggregateState:
         if n == 0:
             return
         rec = records[: n * self.record_bytes()].view(torch.int64).view(n, -1)
-        rec[:, 0] = self.packed_keys(key_cols)
-        rec[:, 1] = 0  # narrow packed keys never use the null-key slot
+        rec[:, 0], rec[:, 1] = self.packed_keys(key_cols)  # (narrow packed keys: null flag 0)
         N.check(N.lib().qe_hashagg_import(self.handle, N.C.c_void_p(records.data_ptr()), int(n)))
 
     def export_all(self):

@@ -2,7 +2,9 @@
 
 The reference keys its HashMap by ``String(bytes)`` (Main.kt:620-627) and compares keys by
 content. Here every distinct byte string gets a dense int32 code on the device; the hash
-aggregate groups by codes and finalize decodes them back to strings.
+aggregate groups by codes and finalize decodes them back to strings. A ``wide`` dictionary gives
+int64 codes instead: a key of at most 7 bytes is packed into its own code (no dictionary work —
+the reference's VendorID keys), longer keys get 2^62 | their dictionary code.
 """
 from __future__ import annotations
 
@@ -11,8 +13,10 @@ from .columnar import Context, DeviceColumn
 
 
 class StringDictionary:
-    def __init__(self, ctx: Context, expected_distinct: int = 1024):
+    def __init__(self, ctx: Context, expected_distinct: int = 1024, wide: bool = False):
         self.ctx = ctx
+        self.wide = bool(wide)
+        self.code_type = N.TYPE_INT64 if self.wide else N.TYPE_INT32
         h = N.C.c_void_p()
         N.check(N.lib().qe_strdict_create(ctx.handle, int(expected_distinct), N.C.byref(h)))
         self.handle = h
@@ -34,16 +38,16 @@ class StringDictionary:
         return n.value
 
     def encode(self, col: DeviceColumn) -> DeviceColumn:
-        """UTF8 column -> INT32 codes (nulls stay null)."""
+        """UTF8 column -> INT32 codes, or wide INT64 codes (nulls stay null)."""
         if col.type != N.TYPE_UTF8:
             raise N.IllegalStateException(N.QE_ERR_UNSUPPORTED, f"string dictionary input type {col.type}")
-        out = DeviceColumn.empty(N.TYPE_INT32, col.length, col.nullable, ctx=self.ctx)
+        out = DeviceColumn.empty(self.code_type, col.length, col.nullable, ctx=self.ctx)
         ic, oc = col.as_c(), out.as_c()
         N.check(N.lib().qe_strdict_encode(self.handle, N.C.byref(ic), N.C.byref(oc)))
         return out
 
     def decode(self, codes: DeviceColumn) -> DeviceColumn:
-        """INT32 codes -> UTF8 column."""
+        """INT32 / wide INT64 codes -> UTF8 column."""
         import torch
 
         cc = codes.as_c()

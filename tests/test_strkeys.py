@@ -75,6 +75,65 @@ def test_strdict_roundtrip(gpu_ctx, n, distinct, expected):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("n,distinct", [(1, 1), (1000, 3), (100_003, 500), (300_000, 120_000)])
+def test_strdict_wide_codes_roundtrip(gpu_ctx, n, distinct):
+    """Wide (INT64) codes: keys of at most 7 bytes are their own code (bytes + length, no
+    dictionary entry), longer keys 2^62 | a dense dictionary code. Same string -> same code,
+    different strings -> different codes (incl. 'a' vs 'a\\0', 7 vs 8 bytes, ''), decode restores."""
+    from kquery import native as N
+    from kquery.columnar import DeviceColumn
+    from kquery.strdict import StringDictionary
+
+    rng = random.Random(n * 7 + distinct)
+    strings, pool = _random_strings(rng, n, distinct)
+    edge = ["", "a", "a\0", "\0", "abcdefg", "abcdefgh", "åäö", "1", "2", "4"]
+    strings = edge + [None if rng.random() < 0.03 else s for s in strings]
+    d = StringDictionary(gpu_ctx, 16, wide=True)
+    codes = d.encode(DeviceColumn.from_strings(strings, ctx=gpu_ctx))
+    assert codes.type == N.TYPE_INT64
+    c = codes.to_numpy()
+    valid = codes.valid_mask()
+    assert valid.tolist() == [s is not None for s in strings]
+    seen = {}
+    for s, code, v in zip(strings, c, valid):
+        if not v:
+            continue
+        b = s.encode()
+        assert seen.setdefault(s, int(code)) == int(code)
+        if len(b) <= 7:  # packed: bytes little-endian, length in bits 56..58
+            assert int(code) == int.from_bytes(b, "little") | (len(b) << 56)
+        else:
+            assert int(code) >> 62 == 1
+    assert len(set(seen.values())) == len(seen)
+    long_keys = {s for s in seen if len(s.encode()) > 7}
+    assert d.size() == len(long_keys)  # only long keys enter the dictionary
+    assert sorted(seen[s] & ((1 << 62) - 1) for s in long_keys) == list(range(len(long_keys)))
+    assert d.decode(codes).to_pylist() == strings
+
+
+@pytest.mark.gpu
+def test_group_by_lone_utf8_key_wide_codes(gpu_ctx):
+    """A lone UTF-8 group key takes wide codes: short and long keys, nulls and empty strings
+    group by content against the oracle's HashAggregateExec loop."""
+    from kquery import native as N
+    from kquery.aggregate import HashAggregateState
+    from kquery.columnar import DeviceColumn
+
+    rng = random.Random(5)
+    keys = [rng.choice(["", "1", "2", "4", "abcdefg", "abcdefgh", "a-much-longer-vendor-id", None]) for _ in range(50_000)]
+    vals = [rng.random() * 100 for _ in keys]
+    st = HashAggregateState(gpu_ctx, [N.TYPE_UTF8], [(N.AGG_MAX, N.TYPE_FLOAT64), (N.AGG_COUNT_STAR, N.TYPE_INT64)], 16)
+    assert st.device_key_types == [N.TYPE_INT64]
+    for a, b in ((0, 20_000), (20_000, 50_000)):  # two batches: codes stable across updates
+        st.update([DeviceColumn.from_strings(keys[a:b], ctx=gpu_ctx)],
+                  [DeviceColumn.from_numpy(N.TYPE_FLOAT64, np.array(vals[a:b]), ctx=gpu_ctx), None])
+    k, v = st.finalize()
+    got = {kk: (m, c) for kk, m, c in zip(k[0].to_pylist(), v[0].to_pylist(), v[1].to_pylist())}
+    want = S.hash_aggregate_rows([keys], [vals, [1.0] * len(keys)], [S.AGG_MAX, S.AGG_COUNT_STAR], [True, True])
+    assert {kk[0]: (w[0], w[1]) for kk, w in want.items()} == got
+
+
+@pytest.mark.gpu
 def test_strdict_rejects_foreign_codes(gpu_ctx):
     from kquery import native as N
     from kquery.columnar import DeviceColumn
