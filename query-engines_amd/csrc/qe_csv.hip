@@ -896,10 +896,14 @@ int csv_parse(qe_ctx* ctx, const uint8_t* data, int64_t nbytes, const qe_csv_opt
   }
   int64_t rows = 0;
   bool scanned = false;  // column sizes already known (the all-records fast path)
-  // ---- the segment-parallel field pass (k_csv_seg_fields): every line a record, no line-end list
+  // ---- the segment-parallel field pass (k_csv_seg_fields, QE_CSV_SEGFIELDS=1): every line a record,
+  // no line-end list. Opt-in: tripdata (4M rows, one box) scanned in 1.15 ms with it against 0.90 ms
+  // for the line-end list + per-line walk below (k_csv_seg_fields 635 us vs k_csv_terms<emit> 160 +
+  // k_csv_lines 283 us): a wave walks its 16 KiB segment step by step, each lane's boundaries in a
+  // serial loop, where the line pass runs 64 independent lines per wave.
   static const bool seg_env = [] {
     const char* e = getenv("QE_CSV_SEGFIELDS");
-    return !(e && e[0] == '0');
+    return e && e[0] == '1';
   }();
   const int64_t rows_all = std::max<int64_t>(0, nlines - first);
   if (seg_env && nlines > 0 && A.delim > 0x20) {
