@@ -196,3 +196,45 @@ def test_gpu_csv_long_lines_and_blank_lines(gpu_ctx, tmp_path):
         onames, _, rows = R.parse(data)
         assert names == onames
         assert cols == R.project(rows, range(len(onames)))
+
+
+_SEG_CHILD = r'''
+import pathlib, random, sys, tempfile
+root = pathlib.Path(sys.argv[1])
+sys.path[:0] = [str(root), str(root / "query-engines_amd"), str(root / "tests")]
+from kquery.columnar import Context
+from oracle import csv_ref as R
+import test_csv as T
+ctx = Context.get(0)
+tmp = pathlib.Path(tempfile.mkdtemp())
+for seed in range(8):
+    rng = random.Random(100 + seed)
+    delim = rng.choice([",", ";", "|"])
+    data = T.random_csv(rng, rng.choice([1, 300, 5000]), rng.randint(1, 7), delim, rng.choice(["\n", "\r\n", "mixed"]))
+    names, proj, cols, _ = T._gpu_scan(ctx, tmp, data)
+    onames, _, rows = R.parse(data)
+    assert names == onames and cols == R.project(rows, range(len(onames))), seed
+body = [f"{i % 97},{i},\"q,{i}\",{i * 0.5}" for i in range(200_000)]
+data = ("k,v,q,f\n" + "\n".join(body) + "\n").encode()
+names, proj, cols, _ = T._gpu_scan(ctx, tmp, data)
+onames, _, rows = R.parse(data)
+assert cols == R.project(rows, range(4))
+print("ok")
+'''
+
+
+@pytest.mark.gpu
+def test_gpu_csv_segment_field_pass(tmp_path):
+    """The opt-in segment field pass (QE_CSV_SEGFIELDS=1, read once per process: a child process)
+    against the oracle: random files (blank / comment lines take the kept-line path), and a large
+    all-records file with quoted fields, which it handles itself."""
+    import os
+    import pathlib
+    import subprocess
+    import sys
+
+    root = pathlib.Path(__file__).resolve().parents[1]
+    env = dict(os.environ, QE_CSV_SEGFIELDS="1")
+    r = subprocess.run([sys.executable, "-c", _SEG_CHILD, str(root)], cwd=str(root), env=env, capture_output=True,
+                       text=True, timeout=240)
+    assert r.returncode == 0 and "ok" in r.stdout, r.stdout[-2000:] + r.stderr[-3000:]
