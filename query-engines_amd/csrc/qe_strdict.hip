@@ -946,10 +946,26 @@ int qe_strdict_size(qe_strdict* d, int64_t* n) {
 
 namespace {
 
+// Bytes spanned by a UTF8 column's values (offsets[n] - offsets[0]; one read-back on the ctx stream).
+int column_span(qe_ctx* ctx, const qe_column* in, int64_t* out) {
+  void* pin;
+  QE_TRY(ctx_pinned(ctx, 8, &pin));
+  QE_HIP(hipMemcpyAsync(pin, in->offsets + in->length, 4, hipMemcpyDeviceToHost, ctx->stream));
+  QE_HIP(hipMemcpyAsync((int32_t*)pin + 1, in->offsets, 4, hipMemcpyDeviceToHost, ctx->stream));
+  QE_TRY(ctx_sync(ctx));
+  int32_t o[2];
+  memcpy(o, pin, 8);
+  *out = (int64_t)o[0] - o[1];
+  return QE_OK;
+}
+
 // Pass 1 over all rows, retry passes until every row resolved; on overflow grow the code arrays /
 // arena, rebuild the slots and run the batch again (re-encoding is idempotent).
 template <typename Pass1, typename Retry>
-int encode_loop(qe_strdict* d, int64_t n, int64_t batch_bytes, Pass1 pass1, Retry retry_pass) {
+int encode_loop(qe_strdict* d, int64_t n, int64_t batch_bytes, Pass1 pass1, Retry retry_pass,
+                const qe_column* span_col = nullptr) {
+  // batch_bytes < 0: the bytes of UTF8 column `span_col`, read back only if the arena has to grow
+  // (the common batch skips that host round trip)
   qe_ctx* ctx = d->ctx;
   const int64_t words = (int64_t)div_up((uint64_t)n, 32);
   void* s;
@@ -976,6 +992,7 @@ int encode_loop(qe_strdict* d, int64_t n, int64_t batch_bytes, Pass1 pass1, Retr
     while (bound < d->ncodes + n && bound < (1ll << 31)) bound <<= 1;
     const int64_t new_ccap = d->ncodes * 2 >= d->ccap ? std::max(d->ccap, std::min(d->ccap * 16, bound)) : d->ccap;
     const int64_t used = std::min<int64_t>(d->arena_used, d->acap);
+    if (batch_bytes < 0 && d->arena_used + 64 > d->acap) QE_TRY(column_span(ctx, span_col, &batch_bytes));
     const int64_t new_acap = d->arena_used + 64 > d->acap ? std::max<int64_t>(d->acap * 2, used * 2 + batch_bytes)
                                                            : d->acap;
     QE_CHECK(new_ccap <= (1ll << 31), QE_ERR_CAPACITY, "more than 2^31 distinct keys");
@@ -1033,23 +1050,11 @@ int qe_strdict_encode(qe_strdict* d, const qe_column* in, qe_column* codes) {
   if (in->validity)
     QE_HIP(hipMemcpyAsync(codes->validity, in->validity, (size_t)div_up((uint64_t)n, 8), hipMemcpyDeviceToDevice,
                           ctx->stream));  // an input bitmap may be Arrow-minimal: ceil(n/8) bytes
-  // the column's byte span (arena sizing): two words read back on the ctx stream (a blocking
-  // hipMemcpy would wait for the whole device and add a second round trip)
-  int32_t o[2] = {0, 0};
-  {
-    void* pin;
-    QE_TRY(ctx_pinned(ctx, 8, &pin));
-    QE_HIP(hipMemcpyAsync(pin, in->offsets + n, 4, hipMemcpyDeviceToHost, ctx->stream));
-    QE_HIP(hipMemcpyAsync((int32_t*)pin + 1, in->offsets, 4, hipMemcpyDeviceToHost, ctx->stream));
-    QE_TRY(ctx_sync(ctx));
-    memcpy(o, pin, 8);
-  }
-  // 2 workgroups per CU: every workgroup warms its LDS cache once, so fewer, longer-lived
-  // workgroups send fewer lookups of the hot keys to the global table (4M rows: 3 keys 0.31 ms
-  // at 2/CU vs 0.45 at 16/CU; 1M keys 18.9 vs 20.8 ms)
+  // one 1024-thread workgroup per CU: every workgroup warms its LDS cache once, so few, long-lived
+  // workgroups send few lookups of the hot keys to the global table
   const int grid = (int)std::min<int64_t>((int64_t)div_up((uint64_t)n, 4 * ENC_BLOCK), (int64_t)ctx->num_cus);
   return encode_loop(
-      d, n, (int64_t)o[0] - o[1],
+      d, n, -1,
       [&](uint32_t* retry) {
         if (wide)
           hipLaunchKernelGGL(k_dict_encode<true>, dim3(grid), dim3(ENC_BLOCK), 0, ctx->stream, d->dev(), in->offsets,
@@ -1064,7 +1069,8 @@ int qe_strdict_encode(qe_strdict* d, const qe_column* in, qe_column* codes) {
         hipLaunchKernelGGL(k_dict_encode_retry, dim3(g2), dim3(256), 0, ctx->stream, d->dev(), in->offsets,
                            (const uint8_t*)in->values, n, c32, c64, rin, rout);
         return launch_check("k_dict_encode_retry");
-      });
+      },
+      in);
 }
 
 int qe_strdict_encode_tuple(qe_strdict* d, const qe_column* keys, int32_t nkeys, qe_column* codes) {
