@@ -353,10 +353,10 @@ __device__ __forceinline__ void encode_lookup(const DictDev& D, EncShared& S, co
     code = __shfl(code, leader);
     if (miss) c = code;
   }
-  if (i < n) {
-    put_code(codes, codes64, i, live ? c : -1);
-    if (live && c == R_OVERFLOW) S.wg_full = 1;
-    if (live && c == R_RETRY) {
+  if (live && i < n) {  // (the other lanes' rows are not this call's: the caller wrote them)
+    put_code(codes, codes64, i, c);
+    if (c == R_OVERFLOW) S.wg_full = 1;
+    if (c == R_RETRY) {
       const int d = atomicAdd(&S.ndef, 1);
       if (d < DEF_CAP) {
         S.def[d] = i;
