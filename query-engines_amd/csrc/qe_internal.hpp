@@ -19,6 +19,7 @@ struct qe_ctx {
   int num_cus = 256;
   void* scratch = nullptr;       // grow-only device scratch
   size_t scratch_bytes = 0;
+  uint64_t scratch_epoch = 0;    // bumped by every ctx_scratch call (a user's contents may be gone)
   void* pinned = nullptr;        // small pinned host buffer for read-backs
   size_t pinned_bytes = 0;
   void* pinned_fg = nullptr;     // fine-grained pinned words a host polls (ctx_pinned_coherent)

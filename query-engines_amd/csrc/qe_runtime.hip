@@ -239,6 +239,7 @@ int ctx_enter(qe_ctx* ctx) {
 }
 
 int ctx_scratch(qe_ctx* ctx, size_t bytes, void** out) {
+  ++ctx->scratch_epoch;
   if (bytes == 0) bytes = 256;
   if (bytes > ctx->scratch_bytes) {
     const size_t old = ctx->scratch_bytes;

@@ -819,6 +819,12 @@ struct qe_strdict {
   int64_t ncodes = 0;
   int64_t arena_used = 0;
   int32_t mode = 0;  // 0 unused, 1 strings, 2 key tuples (kinds below)
+  // the last qe_strdict_decode_bytes: its string starts stay in ctx scratch until the next
+  // ctx_scratch call, so a qe_strdict_decode of the same codes right after reuses them
+  const void* dec_codes = nullptr;
+  const uint8_t* dec_valid = nullptr;
+  int64_t dec_n = -1, dec_total = 0;
+  uint64_t dec_epoch = 0;
   int32_t tuple_nkeys = 0;
   int32_t tuple_type[QE_MAX_KEYS] = {0, 0, 0, 0};
 
@@ -1210,6 +1216,11 @@ int qe_strdict_decode_bytes(qe_strdict* d, const qe_column* codes, int64_t* out_
   QE_TRY(ctx_sync(ctx));
   QE_CHECK((uint32_t)h[1] == 0, QE_ERR_INVALID_ARG, "code out of range for this dictionary");
   *out_bytes = h[0];
+  d->dec_codes = codes->values;
+  d->dec_valid = codes->validity;
+  d->dec_n = n;
+  d->dec_total = h[0];
+  d->dec_epoch = ctx->scratch_epoch;
   return QE_OK;
 }
 
@@ -1220,7 +1231,13 @@ int qe_strdict_decode(qe_strdict* d, const qe_column* codes, qe_column* out) {
   const int64_t n = codes->length;
   QE_CHECK(!codes->validity || out->validity, QE_ERR_INVALID_ARG, "output validity buffer required");
   int64_t total = 0;
-  QE_TRY(qe_strdict_decode_bytes(d, codes, &total));  // leaves starts in scratch
+  if (d->dec_codes == codes->values && d->dec_valid == codes->validity && d->dec_n == n && n > 0 &&
+      d->dec_epoch == ctx->scratch_epoch) {
+    total = d->dec_total;  // qe_strdict_decode_bytes of these codes just ran: its starts are in scratch
+  } else {
+    QE_TRY(qe_strdict_decode_bytes(d, codes, &total));  // leaves starts in scratch
+  }
+  d->dec_codes = nullptr;
   QE_CHECK(total < (1ll << 31), QE_ERR_CAPACITY, "decoded strings exceed 2^31 bytes");
   out->length = n;
   if (n == 0) {

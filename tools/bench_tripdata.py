@@ -99,8 +99,8 @@ def main():
 
     ms_cast, fare = timed(ctx, cast)
 
-    def agg():
-        st = HashAggregateState(ctx, [N.TYPE_UTF8], [(N.AGG_MAX, N.TYPE_FLOAT64)], 16)
+    def agg():  # as HashAggregateExec runs it (kquery/operators.py): stream-ordered updates
+        st = HashAggregateState(ctx, [N.TYPE_UTF8], [(N.AGG_MAX, N.TYPE_FLOAT64)], 16, async_update=True)
         st.update([vendor], [fare])
         return st.finalize()
 
@@ -117,7 +117,8 @@ def main():
 
     parts = {}
     for _ in range(3):
-        t_create, st = wall(lambda: HashAggregateState(ctx, [N.TYPE_UTF8], [(N.AGG_MAX, N.TYPE_FLOAT64)], 16))
+        t_create, st = wall(lambda: HashAggregateState(ctx, [N.TYPE_UTF8], [(N.AGG_MAX, N.TYPE_FLOAT64)], 16,
+                                                       async_update=True))
         t_enc, codes = wall(lambda: st.dicts[0].encode(vendor))
         t_upd, _ = wall(lambda: N.check(N.lib().qe_hashagg_update(
             st.handle, (N.QeColumn * 1)(codes.as_c()), (N.QeColumn * 1)(fare.as_c()), None)))
