@@ -3,7 +3,7 @@
 columns): HashAggregateState create / update / finalize / close, wall time per phase with a device
 sync after each, median of 20.
 
-  python tools/agg_breakdown.py [rows]
+  python tools/agg_breakdown.py [rows] [--profile]   (--profile: cProfile of 20 iterations, top calls)
 """
 import pathlib
 import statistics
@@ -22,7 +22,8 @@ from kquery.columnar import Context, DeviceColumn  # noqa: E402
 
 
 def main():
-    rows = int(sys.argv[1]) if len(sys.argv) > 1 else 4_000_000
+    args = [a for a in sys.argv[1:] if not a.startswith("--")]
+    rows = int(args[0]) if args else 4_000_000
     ctx = Context.get(0)
     rng = np.random.default_rng(1)
     keys = np.array(["1", "2", "4"], dtype=object)[rng.integers(0, 3, rows)]
@@ -49,6 +50,21 @@ def main():
                              ("total", t4 - t0)):
                 phases[name].append(dt * 1e3)
     print({k: round(statistics.median(v), 4) for k, v in phases.items()})
+    if "--profile" in sys.argv:
+        import cProfile
+        import pstats
+
+        def run():
+            for _ in range(20):
+                st = HashAggregateState(ctx, [N.TYPE_UTF8], [(N.AGG_MAX, N.TYPE_FLOAT64)], 16, async_update=True)
+                st.update([vendor], [fare])
+                st.finalize()
+                st.close()
+            ctx.synchronize()
+
+        pr = cProfile.Profile()
+        pr.runcall(run)
+        pstats.Stats(pr).sort_stats("tottime").print_stats(25)
 
 
 if __name__ == "__main__":
