@@ -134,6 +134,10 @@ int qe_device_free(qe_ctx* ctx, void* ptr);
 int qe_release_cached_memory(int device);
 int qe_copy_to_device(qe_ctx* ctx, void* dst, const void* src, size_t bytes);   /* sync */
 int qe_copy_to_host(qe_ctx* ctx, void* dst, const void* src, size_t bytes);     /* sync */
+/* `bytes` of the file `path` from `offset` straight into device memory `dst` (sync): the staging
+ * threads pread() into pinned buffers and DMA them, so the file is never mapped (CsvDataSource's
+ * file -> HBM leg, K:306-316). QE_ERR_INVALID_ARG if the file cannot be read that far. */
+int qe_file_to_device(qe_ctx* ctx, const char* path, int64_t offset, int64_t bytes, void* dst);
 
 /* ---- synthetic RecordBatch generator (measurement harness) ------------------------------ */
 /* Counter-based: u = splitmix64(seed ^ col*0x9E3779B97F4A7C15 ^ row), row = row0 + i.

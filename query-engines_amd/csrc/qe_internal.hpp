@@ -77,6 +77,7 @@ int launch_check(const char* what);                           // hipGetLastError
 int ctx_workspace(qe_ctx* ctx, int slot, size_t bytes, void** out);  // grow-only, contents not kept
 // Host (pageable) -> device through pinned staging with 8 host threads; synchronous (qe_arrow.hip).
 int parallel_h2d_copy(qe_ctx* ctx, void* dst, const void* src, size_t n);
+int parallel_h2d_file(qe_ctx* ctx, void* dst, int fd, int64_t off, size_t n);
 // Per-plan kernel specialisation (qe_jit.hip).
 bool gen_fused_source(const qe::Plan& P, int log2, std::string* src, size_t* lds_bytes, bool spill = false);
 // compact fused LDS table (Plan.lds_compact): plan shapes it supports, bytes per slot, 32-bit MIN/MAX

@@ -111,11 +111,9 @@ class CsvDataSource(DataSource):
         ctx = self.ctx or Context.get(0)
         size = os.path.getsize(self.filename)
         dev = torch.empty(max(1, size), dtype=torch.uint8, device=ctx.torch_device)
-        if size:  # file -> HBM: mapped pages go through the library's pinned multi-threaded staging,
-            raw = np.memmap(self.filename, dtype=np.uint8, mode="r")  # so the page reads run in parallel
-            N.check(N.lib().qe_copy_to_device(ctx.handle, N.C.c_void_p(dev.data_ptr()),
-                                              N.C.c_void_p(raw.ctypes.data), size))
-            del raw
+        if size:  # file -> HBM: the library's staging threads pread() into pinned buffers and DMA them
+            N.check(N.lib().qe_file_to_device(ctx.handle, os.fsencode(self.filename), 0, size,
+                                              N.C.c_void_p(dev.data_ptr())))
         cols = self._parse(ctx, dev, size, idx)
         n = cols[0].length if cols else 0
         step = self.batchSize if self.batchSize and self.batchSize > 0 else max(n, 1)

@@ -201,6 +201,7 @@ SIGNATURES = [
     ("qe_device_free", C.c_int, [_P, _P]),
     ("qe_release_cached_memory", C.c_int, [C.c_int]),
     ("qe_copy_to_device", C.c_int, [_P, _P, _P, C.c_size_t]),
+    ("qe_file_to_device", C.c_int, [_P, C.c_char_p, C.c_int64, C.c_int64, _P]),
     ("qe_copy_to_host", C.c_int, [_P, _P, _P, C.c_size_t]),
     ("qe_generate", C.c_int, [_P, _COLP, C.c_int32, C.c_int64, C.c_uint64, C.c_uint64, C.c_int64, C.c_int32]),
     ("qe_stream_read", C.c_int, [_P, _COLP, C.c_int32, C.POINTER(C.c_double)]),
