@@ -112,9 +112,16 @@ StagePool& stage_pool() {
 int parallel_h2d(qe_ctx* ctx, const std::vector<H2DJob>& jobs) {
   std::vector<H2DJob> chunks;
   const size_t PSTAGE = stage_chunk();
+  // The first chunk of every thread is small: the link idles until some thread has filled its first
+  // pinned half, so a 16 MiB first round (~2-3 ms of memcpy / pread per thread) would be pure
+  // pipeline fill; later chunks are large (per-chunk DMA + event costs).
+  const size_t RAMP = std::min<size_t>(PSTAGE, (size_t)2 << 20);
   for (const H2DJob& j : jobs)
-    for (size_t o = 0; o < j.n; o += PSTAGE)
-      chunks.push_back({j.dst + o, j.src ? j.src + o : nullptr, std::min(PSTAGE, j.n - o), j.fd, j.foff + (int64_t)o});
+    for (size_t o = 0; o < j.n;) {
+      const size_t c = std::min(chunks.size() < (size_t)PTHREADS ? RAMP : PSTAGE, j.n - o);
+      chunks.push_back({j.dst + o, j.src ? j.src + o : nullptr, c, j.fd, j.foff + (int64_t)o});
+      o += c;
+    }
   if (chunks.empty()) return QE_OK;
   const int T = (int)std::min<size_t>(PTHREADS, chunks.size());
   void* pin;
