@@ -609,13 +609,21 @@ typedef struct qe_csv_options {
   int32_t delimiter;          /* field delimiter byte (the reference detects it; the host passes it) */
   int32_t has_header;         /* 1: the first kept record is the header and yields no row */
   int32_t nfields;            /* number of projected fields (1..32) */
-  int32_t reserved;
+  int32_t flags;              /* QE_CSV_PARTIAL_TAIL: more of the file follows these bytes */
   const int32_t* field_index; /* host array of nfields 0-based field positions (< 1024) */
 } qe_csv_options;
+/* flags: the bytes after the last record terminator are the start of a record that continues
+ * past `nbytes` (a chunk of a larger file): they are not parsed, and qe_csv_consumed reports where
+ * the next chunk must start (0: no complete record yet; extend the chunk). A chunk that ends
+ * between a '\r' and its '\n' reads the '\r' as the terminator and the next chunk's leading
+ * '\n' as a blank line, which is skipped: the records are the same as one parse of the file. */
+#define QE_CSV_PARTIAL_TAIL 1
 typedef struct qe_csv_table qe_csv_table;
 int qe_csv_parse(qe_ctx* ctx, const uint8_t* data, int64_t nbytes, const qe_csv_options* opt,
                  qe_csv_table** out);
 int qe_csv_rows(const qe_csv_table* table, int64_t* rows);
+/* Bytes of the input covered by the parsed records (== nbytes without QE_CSV_PARTIAL_TAIL). */
+int qe_csv_consumed(const qe_csv_table* table, int64_t* bytes);
 /* `data` must stay valid until every wanted column has been built (column_copy / column).
  * View of projected column i (UTF8, no validity), built into table-owned memory on first request
  * and valid while the table lives. */

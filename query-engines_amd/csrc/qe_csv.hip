@@ -28,6 +28,7 @@ struct qe_csv_table {
   qe_ctx* ctx = nullptr;
   const uint8_t* data = nullptr;  // the file bytes (the caller keeps them until the columns are built)
   int64_t rows = 0;
+  int64_t consumed = 0;           // bytes up to and including the last record (all of them unless QE_CSV_PARTIAL_TAIL)
   int64_t stride = 0;             // entries per array of the block (>= rows + 1)
   int32_t nproj = 0;
   void* block = nullptr;          // per projected column: start i64, len i64, byte start i64 [stride], quoted u8
@@ -878,8 +879,11 @@ int csv_parse(qe_ctx* ctx, const uint8_t* data, int64_t nbytes, const qe_csv_opt
   int64_t* ends = (int64_t*)p;
   int64_t* keep = ends + nterm + 2;
   int64_t* kstart = keep + nterm + 2;
-  // bytes after the last terminator form a final record (also an unterminated quote at EOF)
-  const int64_t nlines = nterm + (last_end + 1 < nbytes ? 1 : 0);
+  // bytes after the last terminator form a final record (also an unterminated quote at EOF), unless
+  // the caller says more of the file follows (QE_CSV_PARTIAL_TAIL: they start its next chunk)
+  const bool partial = (opt->flags & QE_CSV_PARTIAL_TAIL) != 0;
+  const int64_t nlines = nterm + (!partial && last_end + 1 < nbytes ? 1 : 0);
+  t->consumed = partial ? last_end + 1 : nbytes;
   const int64_t first = opt->has_header ? 1 : 0;
   t->nproj = nproj;
   t->data = data;
@@ -1054,6 +1058,12 @@ int qe_csv_parse(qe_ctx* ctx, const uint8_t* data, int64_t nbytes, const qe_csv_
 int qe_csv_rows(const qe_csv_table* t, int64_t* rows) {
   QE_CHECK(t && rows, QE_ERR_INVALID_ARG, "null argument");
   *rows = t->rows;
+  return QE_OK;
+}
+
+int qe_csv_consumed(const qe_csv_table* t, int64_t* bytes) {
+  QE_CHECK(t && bytes, QE_ERR_INVALID_ARG, "null argument");
+  *bytes = t->consumed;
   return QE_OK;
 }
 

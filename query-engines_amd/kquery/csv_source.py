@@ -65,6 +65,26 @@ def _head(filename: str, limit: int = 1 << 20) -> Tuple[bytes, bool]:
         return data, len(data) < limit
 
 
+_UPLOAD_CTX: dict = {}
+
+
+def _upload_ctx(device: int) -> Context:
+    """The overlapped scan's upload context: its own stream, and kept, so its pinned staging
+    buffers are allocated once per process (one scan at a time uses it: the scan joins its thread)."""
+    if device not in _UPLOAD_CTX:
+        import torch
+
+        s = torch.cuda.Stream(torch.device("cuda", device))
+        _UPLOAD_CTX[device] = (s, Context(device, s.cuda_stream))
+    return _UPLOAD_CTX[device][1]
+
+
+def _chunk_bytes() -> int:
+    """Chunk size of the overlapped scan of large files (QE_CSV_CHUNK_MB, default 128; 0: off)."""
+    v = os.environ.get("QE_CSV_CHUNK_MB")
+    return (int(v) if v else 128) << 20
+
+
 class CsvDataSource(DataSource):
     def __init__(self, filename: str, hasHeaders: bool = True, batchSize: int = 0,  # noqa: N803
                  schema: Optional[Schema] = None, ctx: Optional[Context] = None):
@@ -110,6 +130,10 @@ class CsvDataSource(DataSource):
         idx = [names.index(f.name) for f in read_schema.fields]
         ctx = self.ctx or Context.get(0)
         size = os.path.getsize(self.filename)
+        chunk = _chunk_bytes()
+        if (not self.batchSize or self.batchSize <= 0) and chunk and size >= 2 * chunk:
+            yield from self._scan_chunked(ctx, read_schema, idx, size, chunk)
+            return
         dev = torch.empty(max(1, size), dtype=torch.uint8, device=ctx.torch_device)
         if size:  # file -> HBM: the library's staging threads pread() into pinned buffers and DMA them
             N.check(N.lib().qe_file_to_device(ctx.handle, os.fsencode(self.filename), 0, size,
@@ -122,20 +146,84 @@ class CsvDataSource(DataSource):
             yield RecordBatch(read_schema, [DeviceColumn(N.TYPE_UTF8, m, c.values, None, c.offsets[s:s + m + 1], ctx)
                                             for c in cols])
 
+    def _scan_chunked(self, ctx: Context, read_schema: Schema, idx: List[int], size: int,
+                      chunk: int) -> Iterator[RecordBatch]:
+        """A large file in chunks of about `chunk` bytes, one batch each (like the JNI scan,
+        NativeOperators.kt): a host thread uploads chunk k + 1 (qe_file_to_device on its own
+        stream) while chunk k is parsed and its batch consumed, so the PCIe copy — the bound of a
+        cold file scan — hides the device work. Chunk k is parsed from where chunk k - 1's last
+        record ended (QE_CSV_PARTIAL_TAIL), so the records are exactly those of one parse."""
+        import threading
+
+        import torch
+
+        dev = torch.empty(size, dtype=torch.uint8, device=ctx.torch_device)
+        bounds = list(range(0, size, chunk)) + [size]
+        if bounds[-1] - bounds[-2] < chunk // 2 and len(bounds) > 2:
+            del bounds[-2]  # no small last chunk
+        nchunks = len(bounds) - 1
+        ready = [threading.Event() for _ in range(nchunks)]
+        err: list = []
+        up = _upload_ctx(ctx.device)
+        path = os.fsencode(self.filename)
+
+        def upload():
+            try:
+                for k in range(nchunks):
+                    a, b = bounds[k], bounds[k + 1]
+                    N.check(N.lib().qe_file_to_device(up.handle, path, a, b - a, N.C.c_void_p(dev.data_ptr() + a)))
+                    ready[k].set()
+            except BaseException as e:  # noqa: BLE001 - re-raised by the consumer
+                err.append(e)
+                for r in ready:
+                    r.set()
+
+        th = threading.Thread(target=upload, daemon=True)
+        th.start()
+        try:
+            start, header = 0, self.hasHeaders
+            for k in range(nchunks):
+                ready[k].wait()
+                if err:
+                    raise err[0]
+                end, last = bounds[k + 1], k == nchunks - 1
+                cols, consumed = self._parse_region(ctx, dev, end - start, idx, offset=start, header=header,
+                                                    partial=not last)
+                if consumed == 0:  # no complete record in [start, end): the next chunk extends it
+                    continue
+                header = False
+                start += consumed
+                n = cols[0].length if cols else 0
+                if n:
+                    yield RecordBatch(read_schema, cols)
+        finally:
+            th.join()
+
     def _parse(self, ctx: Context, dev, nbytes: int, idx: List[int]) -> List[DeviceColumn]:
+        return self._parse_region(ctx, dev, nbytes, idx)[0]
+
+    def _parse_region(self, ctx: Context, dev, nbytes: int, idx: List[int], offset: int = 0,
+                      header: Optional[bool] = None, partial: bool = False):
+        """(columns of the projected fields of dev[offset, offset + nbytes), bytes consumed): with
+        `partial` the records end at the last terminator and the rest continues in the next chunk."""
         import torch
 
         out: List[DeviceColumn] = []
+        consumed = nbytes
+        hdr = self.hasHeaders if header is None else header
         for s in range(0, len(idx), 32):  # qe_csv_parse projects up to 32 fields per call
             part = idx[s:s + 32]
             fi = (N.C.c_int32 * len(part))(*part)
-            opt = N.QeCsvOptions(self._delim, 1 if self.hasHeaders else 0, len(part), 0, fi)
+            opt = N.QeCsvOptions(self._delim, 1 if hdr else 0, len(part), N.CSV_PARTIAL_TAIL if partial else 0, fi)
             h = N.C.c_void_p()
-            N.check(N.lib().qe_csv_parse(ctx.handle, N.C.c_void_p(dev.data_ptr()), nbytes, N.C.byref(opt),
+            N.check(N.lib().qe_csv_parse(ctx.handle, N.C.c_void_p(dev.data_ptr() + offset), nbytes, N.C.byref(opt),
                                          N.C.byref(h)))
             try:
                 rows = N.C.c_int64()
                 N.check(N.lib().qe_csv_rows(h, N.C.byref(rows)))
+                used = N.C.c_int64()
+                N.check(N.lib().qe_csv_consumed(h, N.C.byref(used)))
+                consumed = used.value
                 for c in range(len(part)):
                     nb = N.C.c_int64()
                     N.check(N.lib().qe_csv_column_bytes(h, c, N.C.byref(nb)))
@@ -148,4 +236,4 @@ class CsvDataSource(DataSource):
                 ctx.synchronize()
             finally:
                 N.lib().qe_csv_destroy(h)
-        return out
+        return out, consumed

@@ -160,7 +160,10 @@ class QeFusedSpec(C.Structure):
 
 class QeCsvOptions(C.Structure):
     _fields_ = [("delimiter", C.c_int32), ("has_header", C.c_int32), ("nfields", C.c_int32),
-                ("reserved", C.c_int32), ("field_index", C.POINTER(C.c_int32))]
+                ("flags", C.c_int32), ("field_index", C.POINTER(C.c_int32))]
+
+
+CSV_PARTIAL_TAIL = 1  # QE_CSV_PARTIAL_TAIL
 
 
 class QeSelectSpec(C.Structure):
@@ -258,6 +261,7 @@ SIGNATURES = [
     ("qe_select_pending_wait", C.c_int, [_P, _I64P]),
     ("qe_csv_parse", C.c_int, [_P, _P, C.c_int64, C.POINTER(QeCsvOptions), _PP]),
     ("qe_csv_rows", C.c_int, [_P, _I64P]),
+    ("qe_csv_consumed", C.c_int, [_P, _I64P]),
     ("qe_csv_column", C.c_int, [_P, C.c_int32, _COLP]),
     ("qe_csv_column_bytes", C.c_int, [_P, C.c_int32, _I64P]),
     ("qe_csv_column_copy", C.c_int, [_P, C.c_int32, _COLP]),

@@ -238,3 +238,31 @@ def test_gpu_csv_segment_field_pass(tmp_path):
     r = subprocess.run([sys.executable, "-c", _SEG_CHILD, str(root)], cwd=str(root), env=env, capture_output=True,
                        text=True, timeout=240)
     assert r.returncode == 0 and "ok" in r.stdout, r.stdout[-2000:] + r.stderr[-3000:]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("newline", ["\n", "\r\n"])
+def test_gpu_csv_chunked_overlapped_scan(gpu_ctx, tmp_path, monkeypatch, newline):
+    """A large file scans in chunks (QE_CSV_CHUNK_MB; 1 MiB here), the next chunk uploading while
+    this one parses: chunk boundaries land inside quoted fields with embedded newlines and
+    delimiters, between '\\r' and '\\n', and in blank / comment lines; the concatenated batches equal
+    one parse of the file (oracle), and there is more than one batch."""
+    monkeypatch.setenv("QE_CSV_CHUNK_MB", "1")
+    rng = random.Random(11 + len(newline))
+    body = []
+    for i in range(60_000):
+        r = rng.random()
+        if r < 0.01:
+            body.append("")
+        elif r < 0.02:
+            body.append("#c,o,m")
+        else:
+            q = '"%s"' % ("a,b" + newline * rng.randint(0, 2) + 'x""y') if i % 5 == 0 else str(i)
+            body.append(f"{i % 13},{q},{rng.random():.5f}")
+    data = ("k,v,f" + newline + newline.join(body) + newline).encode()
+    assert len(data) > 3 << 20
+    names, proj, cols, batches = _gpu_scan(gpu_ctx, tmp_path, data)
+    onames, _, rows = R.parse(data)
+    assert names == onames
+    assert len(batches) > 1
+    assert cols == R.project(rows, range(3))
