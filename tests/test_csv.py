@@ -250,7 +250,7 @@ def test_gpu_csv_chunked_overlapped_scan(gpu_ctx, tmp_path, monkeypatch, newline
     monkeypatch.setenv("QE_CSV_CHUNK_MB", "1")
     rng = random.Random(11 + len(newline))
     body = []
-    for i in range(60_000):
+    for i in range(200_000):
         r = rng.random()
         if r < 0.01:
             body.append("")
@@ -260,7 +260,7 @@ def test_gpu_csv_chunked_overlapped_scan(gpu_ctx, tmp_path, monkeypatch, newline
             q = '"%s"' % ("a,b" + newline * rng.randint(0, 2) + 'x""y') if i % 5 == 0 else str(i)
             body.append(f"{i % 13},{q},{rng.random():.5f}")
     data = ("k,v,f" + newline + newline.join(body) + newline).encode()
-    assert len(data) > 3 << 20
+    assert len(data) > 3 << 20  # three 1 MiB chunks at least
     names, proj, cols, batches = _gpu_scan(gpu_ctx, tmp_path, data)
     onames, _, rows = R.parse(data)
     assert names == onames
