@@ -418,6 +418,75 @@ __host__ __device__ inline void fxw_words(qu64 u0, qu64 u1, qu64 u2, qu64 v[4]) 
   v[3] = (qu64)((qi64)u2 >> 32);
 }
 
+// ---- the per-workgroup LDS limb window (plan-specialised kernels, default) --------------------------
+// Six signed 64-bit words W0..W5 per slot: word i holds a sum of signed 32-bit limbs of weight
+// 2^(32 i), in units of 2^-96, so the slot's value is sum_i W_i 2^(32 i - 96). A row that is not
+// fx_rare (|x| in [2^-44, 2^62), or +-0) adds its 53-bit mantissa, shifted to its exponent, as
+// three limbs (bits 0-31, 32-63, 64-84 of the shifted mantissa) negated for x < 0, with three LDS
+// atomics that return nothing: no carries, so no round trip, no divergence and no queue. Every
+// |limb| is below 2^32 and a workgroup adds fewer than 2^31 rows to a slot in one launch, so no
+// word can overflow. The flush folds the words into a global partial (fxl_partial).
+constexpr int FXL_WORDS = 6;
+__host__ __device__ inline void fxl_limbs(qi64 bits, int* k, qu64* l0, qu64* l1, qu64* l2) {
+  const qu64 b = (qu64)bits;
+  const int ex = (int)((b >> 52) & 0x7FF);
+  const qu64 m = ex ? ((b & ((1ull << 52) - 1)) | (1ull << 52)) : 0ull;  // ex 0: +-0 (subnormals are rare)
+  const int p = ex ? ex - FXW_EX_LO : 0, q = p & 31;
+  *k = p >> 5;
+  const qu64 lo = m << q, hi = q ? (m >> (64 - q)) : 0ull;
+  qu64 a = lo & 0xFFFFFFFFull, c = lo >> 32, d = hi;
+  if (b >> 63) {  // two's complement of each limb: the words are signed sums
+    a = 0ull - a;
+    c = 0ull - c;
+    d = 0ull - d;
+  }
+  *l0 = a;
+  *l1 = c;
+  *l2 = d;
+}
+template <bool ATOMIC = true, class WP>
+__host__ __device__ inline void fxl_add(WP wp, qi64 bits) {
+  int k;
+  qu64 a, c, d;
+  fxl_limbs(bits, &k, &a, &c, &d);
+  if constexpr (ATOMIC) {
+    atomicAdd(wp(k), a);
+    atomicAdd(wp(k + 1), c);
+    atomicAdd(wp(k + 2), d);
+  } else {
+    *wp(k) += a;
+    *wp(k + 1) += c;
+    *wp(k + 2) += d;
+  }
+}
+// The words W0..W5 as a global partial (units 2^-128: W_i at bit 32 (i + 1)): v[0..3] and the
+// status word (the wrap count above the 256 bits; zero for any workgroup's window).
+__host__ __device__ inline void fxl_partial(qu64 w0, qu64 w1, qu64 w2, qu64 w3, qu64 w4, qu64 w5, qu64 v[4],
+                                            qu64* st) {
+  const qu64 W[FXL_WORDS] = {w0, w1, w2, w3, w4, w5};
+  qu64 a[5] = {0, 0, 0, 0, 0};
+#pragma unroll
+  for (int i = 0; i < FXL_WORDS; ++i) {
+    const int bit = 32 * (i + 1), wi = bit >> 6, sh = bit & 63;  // sh: 0 or 32
+    const qu64 x = W[i], ext = ((qi64)x < 0) ? ~0ull : 0ull;
+    qu64 c = 0;
+#pragma unroll
+    for (int q = 0; q < 5; ++q) {
+      const qu64 t = q < wi ? 0ull
+                     : q == wi ? (sh ? (x << sh) : x)
+                     : q == wi + 1 ? (sh ? ((x >> (64 - sh)) | (ext << sh)) : ext)
+                                   : ext;
+      const qu64 s1 = a[q] + t, c1 = s1 < t ? 1ull : 0ull;
+      const qu64 s2 = s1 + c, c2 = s2 < s1 ? 1ull : 0ull;
+      a[q] = s2;
+      c = c1 | c2;
+    }
+  }
+#pragma unroll
+  for (int q = 0; q < 4; ++q) v[q] = a[q];
+  *st = (qu64)((qi64)a[4] + (qi64)(a[3] >> 63)) * FX_WRAP;
+}
+
 // The words of one input alone (RowVal form: the global-table and record paths): w[0..3] and the
 // status word (flags, and for |x| in [2^126, 2^182) the bits above the words as a wrap count).
 __host__ __device__ inline void fx_row_words(qi64 bits, qu64 w[5]) {
@@ -930,6 +999,12 @@ __device__ inline int lds_probe32n(qi32* keys, qu32 nsl, qi32 key, qu32 h) {
 // kernels, rows that are not fx_rare.
 __device__ inline void lds_fxw_add(qi64* acc, qu64* idx, int SS, int s, qi64 x) {
   fxw_add([&](int w) { return w == 0 ? (qu64*)&acc[s] : &idx[(w - 1) * SS + s]; }, x);
+}
+
+// ACC_SUM_X row into an LDS limb window (acc[s] = W0, idx[(k - 1) SS + s] = Wk): plan-specialised
+// kernels, rows that are not fx_rare.
+__device__ inline void lds_fxl_add(qi64* acc, qu64* idx, int SS, int s, qi64 x) {
+  fxl_add([&](int w) { return w == 0 ? (qu64*)&acc[s] : &idx[(w - 1) * SS + s]; }, x);
 }
 
 // ACC_SUM_X row into a full LDS slot (acc[s] = word 0, idx[k * SS + s] = word k + 1, idx[3 SS + s] =

@@ -1818,9 +1818,12 @@ static int compile_plan(qe_hashagg* h, const qe_column* cols, int32_t ncols, con
 
 // LDS layout for a table of 2^log2 slots under this launch's aggregates. Returns bytes.
 // LDS words per slot beyond acc of an aggregate with idx arrays: fp64 MIN / MAX keep 4 row
-// indices; an exact fp64 SUM keeps 4 more words (256-bit + status) in the generic kernel but only
-// 2 in the plan-specialised kernels' 192-bit window (qe_dev.hpp fxw_add; rare rows go global).
-static size_t idx_words(int acc, bool generic) { return acc == ACC_SUM_X && !generic ? 2 : 4; }
+// indices; an exact fp64 SUM keeps 4 more words (256-bit + status) in the generic kernel, and in
+// the plan-specialised kernels 5 (limb window, qe_dev.hpp fxl_add) or 2 (192-bit window, fxw_add);
+// rare rows go global.
+static size_t idx_words(int acc, bool generic) {
+  return acc == ACC_SUM_X && !generic ? (size_t)fx_window_idx_words() : 4;
+}
 
 static size_t lds_layout_at(const qe_hashagg* h, Plan* P, int log2, bool generic = false) {
   generic = generic || !h->ctx->jit;

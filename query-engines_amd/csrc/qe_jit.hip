@@ -306,8 +306,8 @@ void emit_lds_table(const Plan& P, std::ostringstream& o, int log2, size_t* lds_
       o << "  __shared__ qu32 s_nn" << j << "[SS];\n";
       lds += 4 * SS;
     }
-    if (acc_has_idx(a.acc)) {  // fp64 MIN / MAX: 4 row indices; exact SUM: window words u1, u2
-      const int nw = a.acc == ACC_SUM_X ? 2 : 4;
+    if (acc_has_idx(a.acc)) {  // fp64 MIN / MAX: 4 row indices; exact SUM: window words 1..
+      const int nw = a.acc == ACC_SUM_X ? fx_window_idx_words() : 4;
       o << "  __shared__ qu64 s_idx" << j << "[" << nw << " * SS];\n";
       lds += 8 * nw * SS;
     }
@@ -320,7 +320,7 @@ void emit_lds_table(const Plan& P, std::ostringstream& o, int log2, size_t* lds_
     if (a.acc != ACC_NONE) o << "    s_acc" << j << "[s] = " << acc_init(a.acc) << ";\n";
     if (a.track_nn) o << "    s_nn" << j << "[s] = 0;\n";
     if (acc_has_idx(a.acc))
-      o << "    for (int k = 0; k < " << (a.acc == ACC_SUM_X ? 2 : 4) << "; ++k) s_idx" << j << "[k * SS + s] = "
+      o << "    for (int k = 0; k < " << (a.acc == ACC_SUM_X ? fx_window_idx_words() : 4) << "; ++k) s_idx" << j << "[k * SS + s] = "
         << (acc_is_f64mm(a.acc) ? "~0ull" : "0ull") << ";\n";
   }
   o << "  }\n  __syncthreads();\n";
@@ -338,6 +338,19 @@ void emit_lds_table(const Plan& P, std::ostringstream& o, int log2, size_t* lds_
 // the same wave wrote before (the fences keep the compiler from reordering them).
 constexpr int FXQ_CAP = 128;
 
+}  // namespace
+
+// The limb window (default; QE_FX_LIMBS=0: the 192-bit window + queue). C5, one box: see DESIGN.md.
+bool fx_limbs() {
+  static const bool v = [] {
+    const char* e = getenv("QE_FX_LIMBS");
+    return !(e && e[0] == '0');
+  }();
+  return v;
+}
+
+namespace {
+
 std::vector<int> fx_queue_aggs(const Plan& P) {
   std::vector<int> q;
   for (int j = 0; j < P.naggs; ++j)
@@ -345,12 +358,12 @@ std::vector<int> fx_queue_aggs(const Plan& P) {
   return q;
 }
 
-bool fx_queue_enabled() {
+bool fx_queue_enabled() {  // (the limb window needs no queue: its adds have no carries)
   static const bool v = [] {
     const char* e = getenv("QE_FX_QUEUE");
     return !(e && e[0] == '0');
   }();
-  return v;
+  return v && !fx_limbs();
 }
 
 size_t fx_queue_bytes(const Plan& P, int block) {
@@ -491,7 +504,8 @@ void emit_agg_rows(const Plan& P, std::ostringstream& o, const std::vector<std::
       case ACC_SUM_I: o << "        atomicAdd((qu64*)&s_acc" << js << "[s], (qu64)x);\n"; break;
       case ACC_SUM_F: o << "        atomicAdd((double*)&s_acc" << js << "[s], bits_f64(x));\n"; break;
       case ACC_SUM_X:
-        if (!fx_queue) o << "        lds_fxw_add(s_acc" << js << ", s_idx" << js << ", SS, s, x);\n";
+        if (fx_limbs()) o << "        lds_fxl_add(s_acc" << js << ", s_idx" << js << ", SS, s, x);\n";
+        else if (!fx_queue) o << "        lds_fxw_add(s_acc" << js << ", s_idx" << js << ", SS, s, x);\n";
         else o << "        (void)x; (void)s;\n";
         break;
       case ACC_MIN_I: o << "        atomicMin(&s_acc" << js << "[s], x);\n"; break;
@@ -557,7 +571,11 @@ void emit_flush(const Plan& P, std::ostringstream& o, bool mark_full = false, bo
     const std::string js = std::to_string(j);
     o << "    {\n      qi64 acc = " << (a.acc != ACC_NONE ? "s_acc" + js + "[s]" : std::string("0")) << ";\n"
       << "      const qu64 nn = " << (a.track_nn ? "s_nn" + js + "[s]" : std::string("c")) << ";\n";
-    if (a.acc == ACC_SUM_X)  // the LDS window as a global partial (status 0: rare rows went global)
+    if (a.acc == ACC_SUM_X && fx_limbs())  // the limb window as a global partial
+      o << "      qu64 i0, i1, i2, i3;\n      {\n        qu64 v[4];\n        fxl_partial((qu64)acc, s_idx" << js
+        << "[s], s_idx" << js << "[SS + s], s_idx" << js << "[2 * SS + s], s_idx" << js << "[3 * SS + s], s_idx" << js
+        << "[4 * SS + s], v, &i3);\n        acc = (qi64)v[0]; i0 = v[1]; i1 = v[2]; i2 = v[3];\n      }\n";
+    else if (a.acc == ACC_SUM_X)  // the LDS window as a global partial (status 0: rare rows went global)
       o << "      qu64 i0, i1, i2;\n      const qu64 i3 = 0;\n      {\n        qu64 v[4];\n        fxw_words((qu64)acc, s_idx" << js
         << "[s], s_idx" << js << "[SS + s], v);\n        acc = (qi64)v[0]; i0 = v[1]; i1 = v[2]; i2 = v[3];\n      }\n";
     else if (acc_has_idx(a.acc))

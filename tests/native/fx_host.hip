@@ -75,5 +75,37 @@ extern "C" double qe_fx_host_window_sum(const double* xs, long n, int nslots, in
   return v;
 }
 
+// The same split with the limb window (fxl_add / fxl_partial, the kernels' default).
+extern "C" double qe_fx_host_limb_sum(const double* xs, long n, int nslots, int* err, long* rare,
+                                      unsigned long long* words) {
+  qu64 win[64][FXL_WORDS] = {};
+  Slot tot;
+  *rare = 0;
+  if (nslots < 1 || nslots > 64) return 0.0;
+  for (long i = 0; i < n; ++i) {
+    const qi64 b = f64_bits(xs[i]);
+    if (fx_rare(b)) {
+      qu64 w[5];
+      fx_row_words(b, w);
+      fx_add_words<false>([&](int k) { return tot.word(k); }, w[0], w[1], w[2], w[3], w[4], &tot.st);
+      ++*rare;
+    } else {
+      qu64* u = win[i % nslots];
+      fxl_add<false>([&](int k) { return &u[k]; }, b);
+    }
+  }
+  for (int k = 0; k < nslots; ++k) {
+    qu64 v[4], st;
+    fxl_partial(win[k][0], win[k][1], win[k][2], win[k][3], win[k][4], win[k][5], v, &st);
+    fx_add_words<false>([&](int w) { return tot.word(w); }, v[0], v[1], v[2], v[3], st, &tot.st);
+  }
+  for (int i = 0; i < 4; ++i) words[i] = tot.w[i];
+  words[4] = tot.st;
+  bool e = false;
+  const double v = fx_result(tot.w[0], tot.w[1], tot.w[2], tot.w[3], tot.st, (qu64)n, &e);
+  *err = e;
+  return v;
+}
+
 // The RowVal image of one input (fx_row_words): words[5].
 extern "C" void qe_fx_host_row_words(double x, unsigned long long* words) { fx_row_words(f64_bits(x), (qu64*)words); }

@@ -30,10 +30,10 @@ def fx():
                                    ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_int),
                                    ctypes.POINTER(ctypes.c_ulonglong)]
     lib.qe_fx_host_row_words.argtypes = [ctypes.c_double, ctypes.POINTER(ctypes.c_ulonglong)]
-    lib.qe_fx_host_window_sum.restype = ctypes.c_double
-    lib.qe_fx_host_window_sum.argtypes = [ctypes.POINTER(ctypes.c_double), ctypes.c_long, ctypes.c_int,
-                                          ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_long),
-                                          ctypes.POINTER(ctypes.c_ulonglong)]
+    for f in (lib.qe_fx_host_window_sum, lib.qe_fx_host_limb_sum):
+        f.restype = ctypes.c_double
+        f.argtypes = [ctypes.POINTER(ctypes.c_double), ctypes.c_long, ctypes.c_int, ctypes.POINTER(ctypes.c_int),
+                      ctypes.POINTER(ctypes.c_long), ctypes.POINTER(ctypes.c_ulonglong)]
 
     def run(xs, nslots=1, order=None):
         xs = np.ascontiguousarray(xs, dtype=np.float64)
@@ -166,19 +166,22 @@ def test_row_words_merge_like_rows(fx):
     assert tuple(w) == (0, 0, 2 ** 64 - 1, 2 ** 64 - 1, 0)  # -1.0 = -(2^128) units: sign extended
 
 
-def window(fx, xs, nslots):
+def window(fx, xs, nslots, limbs=False):
     xs = np.ascontiguousarray(xs, dtype=np.float64)
     err, rare = ctypes.c_int(), ctypes.c_long()
     words = (ctypes.c_ulonglong * 5)()
-    v = fx.lib.qe_fx_host_window_sum(xs.ctypes.data_as(ctypes.POINTER(ctypes.c_double)), len(xs), nslots,
-                                     ctypes.byref(err), ctypes.byref(rare), words)
+    f = fx.lib.qe_fx_host_limb_sum if limbs else fx.lib.qe_fx_host_window_sum
+    v = f(xs.ctypes.data_as(ctypes.POINTER(ctypes.c_double)), len(xs), nslots, ctypes.byref(err), ctypes.byref(rare),
+          words)
     return v, bool(err.value), rare.value, tuple(words)
 
 
-def test_lds_window_split(fx):
-    """The specialised kernels keep a 192-bit window per LDS slot (units 2^-96) and send rows
-    outside [2^-44, 2^62) to the global accumulator: the merged words equal those of adding every
-    row to one full accumulator, whatever the split."""
+@pytest.mark.parametrize("limbs", [True, False], ids=["limb_window", "carry_window"])
+def test_lds_window_split(fx, limbs):
+    """The specialised kernels keep a window per LDS slot — six signed limb words (default) or a
+    192-bit carry window (units 2^-96) — and send rows outside [2^-44, 2^62) to the global
+    accumulator: the merged words equal those of adding every row to one full accumulator,
+    whatever the split."""
     rng = np.random.default_rng(7)
     for trial in range(20):
         n = int(rng.integers(1, 4000))
@@ -187,7 +190,7 @@ def test_lds_window_split(fx):
         xs[rng.random(n) < 0.02] = -0.0
         xs[rng.random(n) < 0.01] = 5e-324
         full = fx(xs)
-        v, err, rare, w = window(fx, xs, int(rng.integers(1, 65)))
+        v, err, rare, w = window(fx, xs, int(rng.integers(1, 65)), limbs)
         assert w == full[2] and same(v, full[0]) and err == full[1], trial
         assert rare == int(np.sum((np.abs(xs) < 2.0 ** -44) & (xs != 0) | (np.abs(xs) >= 2.0 ** 62)))
     # window edges: the smallest and largest fast-path magnitudes, both signs, carries into u2
@@ -195,5 +198,20 @@ def test_lds_window_split(fx):
             np.nextafter(2.0 ** -44, 0), 1.0, -1.0, 2.0 ** 20 + 2.0 ** -30]
     xs = np.array(edge * 50)
     for ns in (1, 3):
-        v, err, rare, w = window(fx, rng.permutation(xs), ns)
+        v, err, rare, w = window(fx, rng.permutation(xs), ns, limbs)
         assert not err and same(v, exact(xs)) and rare == 100
+
+
+def test_limb_window_many_rows_and_signs(fx):
+    """Limb words are signed sums without carries: long runs of one sign (every limb of every
+    word positive, or negative) and alternating magnitudes across the whole window fold exactly."""
+    rng = np.random.default_rng(8)
+    for trial in range(6):
+        n = 20_000
+        mag = np.exp2(rng.integers(-44, 62, n).astype(np.float64)) * (1 + rng.random(n))
+        mag = np.minimum(mag, np.nextafter(2.0 ** 62, 0))
+        sign = np.ones(n) if trial % 3 == 0 else (-np.ones(n) if trial % 3 == 1 else rng.choice([-1.0, 1.0], n))
+        xs = mag * sign
+        v, err, rare, w = window(fx, xs, 3, True)
+        assert rare == 0 and not err and same(v, exact(xs)), trial
+        assert w == fx(xs)[2]
