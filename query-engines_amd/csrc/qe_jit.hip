@@ -358,12 +358,12 @@ std::vector<int> fx_queue_aggs(const Plan& P) {
   return q;
 }
 
-bool fx_queue_enabled() {  // (the limb window needs no queue: its adds have no carries)
+bool fx_queue_enabled() {
   static const bool v = [] {
     const char* e = getenv("QE_FX_QUEUE");
     return !(e && e[0] == '0');
   }();
-  return v && !fx_limbs();
+  return v;
 }
 
 size_t fx_queue_bytes(const Plan& P, int block) {
@@ -392,6 +392,10 @@ void emit_fx_queue_run(const Plan& P, std::ostringstream& o, const std::string& 
   for (int k = 0; k < nq; ++k)
     o << "        qx[" << k << "] = ((qe >> " << 24 + k << ") & 1u) ? q_x" << k << "[qp] : 0ll;\n"
       << "        if (fx_rare(qx[" << k << "])) { rare |= 1u << " << k << "; qx[" << k << "] = 0; }\n";
+  if (fx_limbs()) {  // limb window: three adds per input, no carries
+    for (int k = 0; k < nq; ++k)
+      o << "        if (qx[" << k << "]) lds_fxl_add(s_acc" << q[k] << ", s_idx" << q[k] << ", SS, s, qx[" << k << "]);\n";
+  } else {
   o << "        qu64* wp0[" << nq << "];\n        qu64* wp1[" << nq << "];\n        qu64 lo[" << nq << "], hi[" << nq
     << "];\n        bool ng[" << nq << "], k0[" << nq << "];\n";
   for (int k = 0; k < nq; ++k) {
@@ -416,6 +420,7 @@ void emit_fx_queue_run(const Plan& P, std::ostringstream& o, const std::string& 
     o << "        if (k0[" << ks << "]) {\n          const qi64 d = (qi64)((t[" << ks << "] < hi[" << ks << "] ? 1 : 0) + (o1[" << ks
       << "] + t[" << ks << "] < o1[" << ks << "] ? 1 : 0)) - (ng[" << ks << "] ? 1 : 0);\n"
       << "          if (d) atomicAdd(&s_idx" << j << "[SS + s], (qu64)d);\n        }\n";
+  }
   }
   o << "        if (rare) {\n          const bool knl = s == S;\n"
     << "          const qi64 key = knl ? 0 : (s == S + 1 ? EMPTY_KEY : s_keys[s]);\n";
@@ -504,9 +509,9 @@ void emit_agg_rows(const Plan& P, std::ostringstream& o, const std::vector<std::
       case ACC_SUM_I: o << "        atomicAdd((qu64*)&s_acc" << js << "[s], (qu64)x);\n"; break;
       case ACC_SUM_F: o << "        atomicAdd((double*)&s_acc" << js << "[s], bits_f64(x));\n"; break;
       case ACC_SUM_X:
-        if (fx_limbs()) o << "        lds_fxl_add(s_acc" << js << ", s_idx" << js << ", SS, s, x);\n";
-        else if (!fx_queue) o << "        lds_fxw_add(s_acc" << js << ", s_idx" << js << ", SS, s, x);\n";
-        else o << "        (void)x; (void)s;\n";
+        if (fx_queue) o << "        (void)x; (void)s;\n";
+        else if (fx_limbs()) o << "        lds_fxl_add(s_acc" << js << ", s_idx" << js << ", SS, s, x);\n";
+        else o << "        lds_fxw_add(s_acc" << js << ", s_idx" << js << ", SS, s, x);\n";
         break;
       case ACC_MIN_I: o << "        atomicMin(&s_acc" << js << "[s], x);\n"; break;
       case ACC_MAX_I: o << "        atomicMax(&s_acc" << js << "[s], x);\n"; break;
