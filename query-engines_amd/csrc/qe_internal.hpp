@@ -80,8 +80,8 @@ int parallel_h2d_copy(qe_ctx* ctx, void* dst, const void* src, size_t n);
 int parallel_h2d_file(qe_ctx* ctx, void* dst, int fd, int64_t off, size_t n);
 // Per-plan kernel specialisation (qe_jit.hip).
 bool gen_fused_source(const qe::Plan& P, int log2, std::string* src, size_t* lds_bytes, bool spill = false);
-// Exact fp64 SUM in the specialised kernels' LDS tables: the six-word limb window (default) or the
-// 192-bit carry window with its per-wave queue (QE_FX_LIMBS=0). LDS words per slot beyond acc.
+// Exact fp64 SUM in the specialised kernels' LDS tables: the 192-bit carry window (default) or the
+// six-word limb window (QE_FX_LIMBS=1), both through the per-wave queue. LDS words per slot beyond acc.
 bool fx_limbs();
 inline int fx_window_idx_words() { return fx_limbs() ? qe::FXL_WORDS - 1 : 2; }
 // compact fused LDS table (Plan.lds_compact): plan shapes it supports, bytes per slot, 32-bit MIN/MAX
