@@ -127,3 +127,32 @@ def test_fp64_sum_finalize_errors_do_not_stick(gpu_ctx):
     got = dict(zip(keys[0].to_pylist(), vals[0].to_pylist()))
     for g in range(7):
         assert got[g] == math.fsum([0.1] * int(np.sum(k == g)))
+
+
+_LIMBS_CHILD = r'''
+import pathlib, sys
+root = pathlib.Path(sys.argv[1])
+sys.path[:0] = [str(root), str(root / "query-engines_amd"), str(root / "tests")]
+from kquery.columnar import Context
+import test_fp64_sum_gpu as T
+ctx = Context.get(0)
+for groups, expected, path in [(1024, 1024, "lds"), (4500, 4500, "two-bucket"), (6, 16, "fused")]:
+    for det in (False, True):
+        T.test_fp64_sum_adversarial(ctx, groups, expected, path, det)
+print("ok")
+'''
+
+
+def test_fp64_sum_limb_window():
+    """The opt-in limb window (QE_FX_LIMBS=1, read once per process: a child process) on the
+    adversarial groups of the LDS, two-bucket and fused paths."""
+    import os
+    import pathlib
+    import subprocess
+    import sys
+
+    root = pathlib.Path(__file__).resolve().parents[1]
+    env = dict(os.environ, QE_FX_LIMBS="1")
+    r = subprocess.run([sys.executable, "-c", _LIMBS_CHILD, str(root)], cwd=str(root), env=env, capture_output=True,
+                       text=True, timeout=280)
+    assert r.returncode == 0 and "ok" in r.stdout, r.stdout[-2000:] + r.stderr[-3000:]
