@@ -18,6 +18,7 @@
 #   prof_fp64          tools/prof_fp64_sum.sh (C5 trace + SQ / LDS counters per mode)
 #   fxq                tools/exp_fxq.sh (exact-sum kernel code-shape A/B on C5)
 #   csvpmc             tools/prof_csv_pmc.sh (SQ / LDS counters of the tripdata kernels, 4M rows)
+#   triptraffic        tools/prof_trip_traffic.sh (FETCH_SIZE / WRITE_SIZE of the tripdata kernels)
 #   env:NAME=VALUE     set an environment variable for the following steps (env:TAG=x suffixes the
 #                      output files of tripdata / configs / fp64 with _x)
 set -o pipefail
@@ -47,6 +48,7 @@ for s in "$@"; do
     tripdata) step tripdata 300 bash -c "python3 tools/bench_tripdata.py > '$OUT/tripdata${TAG:+_$TAG}.json' 2> '$OUT/tripdata${TAG:+_$TAG}.err'" ;;
     fp64) step fp64 300 bash -c "python3 tools/exp_fp64_sum.py C5 C4 --rounds 3 > '$OUT/fp64${TAG:+_$TAG}.jsonl' 2>&1" ;;
     csvpmc) step csvpmc 700 env ROWS=4000000 bash tools/prof_csv_pmc.sh ;;
+    triptraffic) step triptraffic 700 env ROWS=4000000 bash tools/prof_trip_traffic.sh ;;
     profile) step profile 600 bash profiles/run_profile.sh ;;
     prof_trip) step prof_trip 500 env ROWS=4000000 bash tools/prof_tripdata.sh ;;
     prof_fp64) step prof_fp64 600 bash tools/prof_fp64_sum.sh ;;
