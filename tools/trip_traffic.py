@@ -21,6 +21,7 @@ def per_kernel(path, counter):
 
 def short(name):
     n = name.replace("qe::(anonymous namespace)::", "").replace("qe::", "")
+    n = n[5:] if n.startswith("void ") else n
     return n.split("(")[0]
 
 
@@ -37,7 +38,6 @@ def main():
         "k_csv_terms<true>": csv_bytes and csv_bytes + 8 * rows,
         "k_dict_encode<true>": 4 * rows + 1 * rows + 8 * rows,  # offsets, 1-byte keys, int64 codes
         "qe_fused": 16 * rows,  # int64 code + fp64 fare
-        "k_cast_utf8_f64": None,
     }
     print("| kernel | calls | avg us | FETCH x2 (MB) | WRITE (MB) | moved (GB/s) | algorithmic (MB) |")
     print("|---|---|---|---|---|---|---|")
@@ -51,10 +51,9 @@ def main():
         wb = 1024 * w if w is not None else 0.0
         rate = (fb + wb) / (us * 1e3) if us else 0.0
         sn = short(name)
-        a = next((v for k, v in alg.items() if sn.startswith(k.split("<")[0]) and (("<" not in k) or k in name.replace("(anonymous namespace)::", "") or True)), None)
-        a = alg.get(sn, a)
-        print(f"| {sn} | {r['Calls']} | {us:.1f} | {fb / 1e6:.1f} | {wb / 1e6:.1f} | {rate:.0f} | "
-              f"{a / 1e6:.1f} |" if a else f"| {sn} | {r['Calls']} | {us:.1f} | {fb / 1e6:.1f} | {wb / 1e6:.1f} | {rate:.0f} | |")
+        a = alg.get(sn)
+        at = f"{a / 1e6:.1f}" if a else ""
+        print(f"| {sn} | {r['Calls']} | {us:.1f} | {fb / 1e6:.1f} | {wb / 1e6:.1f} | {rate:.0f} | {at} |")
 
 
 if __name__ == "__main__":
