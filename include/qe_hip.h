@@ -517,6 +517,10 @@ int qe_strdict_decode_bytes(qe_strdict* dict, const qe_column* codes, int64_t* o
 /* out (UTF8): offsets for codes->length+1 entries, values >= decode_bytes bytes, validity
  * iff codes has one. QE_ERR_INVALID_ARG if a code was not issued by this dictionary. */
 int qe_strdict_decode(qe_strdict* dict, const qe_column* codes, qe_column* out);
+/* The same for codes this dictionary produced (no range check is promised): wide INT64 codes of a
+ * dictionary that holds no long key are all packed, and decode then needs no host round trip —
+ * `out->values` must hold 7 bytes per row. Otherwise as qe_strdict_decode. */
+int qe_strdict_decode_trusted(qe_strdict* dict, const qe_column* codes, qe_column* out);
 /* Composite group keys (K:621-626 `List` of key values) whose packing exceeds 63 bits: each row's
  * tuple of up to QE_MAX_KEYS fixed-width / BOOL key columns (nulls and fp64 NaNs as
  * List/Double.equals see them) gets a dense int32 code; codes->validity (optional) is set all-valid.

@@ -1224,14 +1224,29 @@ int qe_strdict_decode_bytes(qe_strdict* d, const qe_column* codes, int64_t* out_
   return QE_OK;
 }
 
-int qe_strdict_decode(qe_strdict* d, const qe_column* codes, qe_column* out) {
+static int strdict_decode(qe_strdict* d, const qe_column* codes, qe_column* out, bool trusted) {
   QE_CHECK(d && codes && out, QE_ERR_INVALID_ARG, "null argument");
   qe_ctx* ctx = d->ctx;
+  QE_TRY(ctx_enter(ctx));
   QE_CHECK(out->type == QE_TYPE_UTF8 && out->offsets, QE_ERR_INVALID_ARG, "output must be UTF8 with offsets");
   const int64_t n = codes->length;
   QE_CHECK(!codes->validity || out->validity, QE_ERR_INVALID_ARG, "output validity buffer required");
   int64_t total = 0;
-  if (d->dec_codes == codes->values && d->dec_valid == codes->validity && d->dec_n == n && n > 0 &&
+  if (trusted && codes->type == QE_TYPE_INT64 && d->ncodes == 0 && n > 0 && n < (1ll << 28)) {
+    // every code is packed (no long key was ever inserted): lengths and starts on the device, no
+    // host round trip; the caller's values buffer holds WIDE_MAX bytes per row
+    void* sp;
+    QE_TRY(ctx_scratch(ctx, (size_t)(2 * n + 2) * 8, &sp));
+    int64_t* lens = (int64_t*)sp;
+    int64_t* starts = lens + n;
+    unsigned int* bad = (unsigned int*)(starts + n + 1);
+    const int g = (int)std::min<int64_t>((int64_t)div_up((uint64_t)n, 256), (int64_t)ctx->num_cus * 8);
+    hipLaunchKernelGGL(k_dict_decode_len<true>, dim3(g), dim3(256), 0, ctx->stream, codes->values, codes->validity, n,
+                       d->code_len, d->ncodes, lens, bad);
+    QE_TRY(launch_check("k_dict_decode_len"));
+    QE_TRY(exclusive_scan_i64(ctx, lens, starts, n));
+    total = 0;
+  } else if (d->dec_codes == codes->values && d->dec_valid == codes->validity && d->dec_n == n && n > 0 &&
       d->dec_epoch == ctx->scratch_epoch) {
     total = d->dec_total;  // qe_strdict_decode_bytes of these codes just ran: its starts are in scratch
   } else {
@@ -1244,7 +1259,7 @@ int qe_strdict_decode(qe_strdict* d, const qe_column* codes, qe_column* out) {
     QE_HIP(hipMemsetAsync(out->offsets, 0, 4, ctx->stream));
     return QE_OK;
   }
-  QE_CHECK(out->values || total == 0, QE_ERR_CAPACITY, "output values buffer required");
+  QE_CHECK(out->values || (total == 0 && !trusted), QE_ERR_CAPACITY, "output values buffer required");
   const int64_t* starts = (const int64_t*)ctx->scratch + n;
   const int grid = (int)std::min<int64_t>((int64_t)div_up((uint64_t)n + 1, 256), (int64_t)ctx->num_cus * 8);
   if (codes->type == QE_TYPE_INT64)
@@ -1259,6 +1274,14 @@ int qe_strdict_decode(qe_strdict* d, const qe_column* codes, qe_column* out) {
     QE_HIP(hipMemcpyAsync(out->validity, codes->validity, (size_t)div_up((uint64_t)n, 8),
                           hipMemcpyDeviceToDevice, ctx->stream));
   return QE_OK;
+}
+
+int qe_strdict_decode(qe_strdict* d, const qe_column* codes, qe_column* out) {
+  return strdict_decode(d, codes, out, false);
+}
+
+int qe_strdict_decode_trusted(qe_strdict* d, const qe_column* codes, qe_column* out) {
+  return strdict_decode(d, codes, out, true);
 }
 
 }  // extern "C"

@@ -293,7 +293,7 @@ class HashAggregateState:
         keys, aggs = cols[:nk], cols[nk:]
         if self.tuple_dict is not None:
             keys = self.tuple_dict.decode_tuple(keys[0], self.member_types)
-        keys = [self.dicts[i].decode(k) if i in self.dicts else k for i, k in enumerate(keys)]
+        keys = [self.dicts[i].decode(k, trusted=True) if i in self.dicts else k for i, k in enumerate(keys)]
         return keys, aggs
 
     # ---- partial records (exchange) -----------------------------------------------------------------

@@ -253,6 +253,7 @@ SIGNATURES = [
     ("qe_strdict_encode", C.c_int, [_P, _COLP, _COLP]),
     ("qe_strdict_decode_bytes", C.c_int, [_P, _COLP, _I64P]),
     ("qe_strdict_decode", C.c_int, [_P, _COLP, _COLP]),
+    ("qe_strdict_decode_trusted", C.c_int, [_P, _COLP, _COLP]),
     ("qe_strdict_encode_tuple", C.c_int, [_P, _COLP, C.c_int32, _COLP]),
     ("qe_strdict_decode_tuple", C.c_int, [_P, _COLP, C.c_int32, _COLP]),
     ("qe_hash_partition", C.c_int, [_P, _COLP, C.c_int32, C.c_int32, _P]),

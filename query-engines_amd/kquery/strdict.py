@@ -46,11 +46,21 @@ class StringDictionary:
         N.check(N.lib().qe_strdict_encode(self.handle, N.C.byref(ic), N.C.byref(oc)))
         return out
 
-    def decode(self, codes: DeviceColumn) -> DeviceColumn:
-        """INT32 / wide INT64 codes -> UTF8 column."""
+    def decode(self, codes: DeviceColumn, trusted: bool = False) -> DeviceColumn:
+        """INT32 / wide INT64 codes -> UTF8 column. ``trusted``: codes this dictionary produced; wide
+        codes are then decoded without a host round trip while every key is packed."""
         import torch
 
         cc = codes.as_c()
+        if trusted and self.wide and self.size() == 0 and codes.length < (1 << 28):
+            dev = self.ctx.torch_device
+            n = codes.length
+            out = DeviceColumn(N.TYPE_UTF8, n, torch.empty(max(1, 7 * n), dtype=torch.uint8, device=dev),
+                               codes.validity.clone() if codes.validity is not None else None,
+                               torch.empty(n + 1, dtype=torch.int32, device=dev), self.ctx)
+            oc = out.as_c()
+            N.check(N.lib().qe_strdict_decode_trusted(self.handle, N.C.byref(cc), N.C.byref(oc)))
+            return out
         nbytes = N.C.c_int64()
         N.check(N.lib().qe_strdict_decode_bytes(self.handle, N.C.byref(cc), N.C.byref(nbytes)))
         dev = self.ctx.torch_device
