@@ -115,9 +115,12 @@ __device__ __forceinline__ uint32_t terms16(const Lane16& v, uint32_t next, int6
                                             uint32_t inq, uint32_t* inq_out) {
   if (!has_byte(v, '"') || eq16(v, '"') == 0) {  // no quote: the state is constant (common case)
     *inq_out = inq;
-    if (inq || (!has_byte(v, '\n') && !has_byte(v, '\r'))) return 0;
+    if (inq) return 0;
+    // VALU-bound kernels (every wave instruction is 4 cycles on a SIMD): the '\n' mask directly, a
+    // '\r' mask only where the cheap test sees one (a wave step nearly always holds a '\n' somewhere,
+    // so testing for it first only added work)
     const uint32_t valid = pos + 16 <= nbytes ? 0xFFFFu : ((1u << (nbytes - pos)) - 1u);
-    const uint32_t nl = eq16(v, '\n') & valid, cr = eq16(v, '\r') & valid;
+    const uint32_t nl = eq16(v, '\n') & valid, cr = has_byte(v, '\r') ? (eq16(v, '\r') & valid) : 0u;
     const uint32_t next_nl = (nl >> 1) | ((pos + 16 < nbytes && next == '\n') ? 0x8000u : 0u);
     return nl | (cr & ~next_nl);
   }
@@ -472,7 +475,7 @@ __device__ void walk_record(const D& data, int64_t s, int64_t e, const FieldArgs
     const uint32_t lo = (uint32_t)(s > a ? s - a : 0);
     const uint32_t hi = (uint32_t)(e - a < 16 ? e - a : 16);
     const uint32_t in = (hi >= 32 ? 0xFFFFu : ((1u << hi) - 1u)) & ~((1u << lo) - 1u);
-    uint32_t q = eq16(v, '"') & in, d = eq16(v, (uint32_t)A.delim) & in;
+    uint32_t q = (has_byte(v, '"') ? eq16(v, '"') : 0u) & in, d = eq16(v, (uint32_t)A.delim) & in;
     if (q == 0 && inq) continue;
     while (d && f <= A.max_field) {
       const int k = __builtin_ctz(d);
