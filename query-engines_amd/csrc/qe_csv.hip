@@ -111,9 +111,10 @@ __device__ __forceinline__ uint32_t eq16(const Lane16& v, uint32_t b) {
 }
 
 // `next` = the byte after these 16 (the next lane's first byte, passed by shuffle; 0 past the end).
+// `maybe_q` false: the caller knows the 16 bytes hold no '"'.
 __device__ __forceinline__ uint32_t terms16(const Lane16& v, uint32_t next, int64_t nbytes, int64_t pos,
-                                            uint32_t inq, uint32_t* inq_out) {
-  if (!has_byte(v, '"') || eq16(v, '"') == 0) {  // no quote: the state is constant (common case)
+                                            uint32_t inq, uint32_t* inq_out, bool maybe_q = true) {
+  if (!maybe_q || !has_byte(v, '"') || eq16(v, '"') == 0) {  // no quote: the state is constant (common case)
     *inq_out = inq;
     if (inq) return 0;
     // VALU-bound kernels (every wave instruction is 4 cycles on a SIMD): the '\n' mask directly, a
@@ -177,7 +178,8 @@ __global__ void __launch_bounds__(256) k_csv_terms(const uint8_t* __restrict__ d
       case 2: v = vq[2]; break;
       default: v = vq[3]; break;
     }
-    const uint32_t qodd = has_byte(v, '"') ? (uint32_t)(quotes16(v) & 1) : 0u;
+    const bool mq = has_byte(v, '"');
+    const uint32_t qodd = mq ? (uint32_t)(quotes16(v) & 1) : 0u;
     const uint64_t par = __ballot(qodd);
     const uint32_t inq0 = carry ^ ((uint32_t)__popcll(par & below) & 1u);
     uint32_t inq1;
@@ -186,7 +188,7 @@ __global__ void __launch_bounds__(256) k_csv_terms(const uint8_t* __restrict__ d
     // lane 63: only a trailing '\r' needs the next byte (a load here on every step would put a
     // full memory round trip on every step's critical path)
     if (lane == 63) next = (v.byte(15) == '\r' && pos + 16 < nbytes) ? data[pos + 16] : 0u;
-    const uint32_t m = terms16(v, next, nbytes, pos, inq0, &inq1);
+    const uint32_t m = terms16(v, next, nbytes, pos, inq0, &inq1, mq);
     carry ^= (uint32_t)__popcll(par) & 1u;
     const int c = __popc(m);  // 0..16
     // wave exclusive prefix and total of c from its 5 bit-planes (ballot + popcount, no LDS)
@@ -256,7 +258,7 @@ __global__ void __launch_bounds__(256) k_csv_count2(const uint8_t* __restrict__ 
     if (lane == 63) next = (v.byte(15) == '\r' && pos + 16 < nbytes) ? data[pos + 16] : 0u;
     uint32_t dummy;
     if (nq == 0) {
-      const uint32_t mm = terms16(v, next, nbytes, pos, 0u, &dummy);
+      const uint32_t mm = terms16(v, next, nbytes, pos, 0u, &dummy, false);
       if (mm) {
         const int64_t last = pos + 31 - __builtin_clz(mm);
         if (x) {
