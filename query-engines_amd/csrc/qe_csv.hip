@@ -344,6 +344,8 @@ struct FieldArgs {
   int32_t max_field;                  // largest projected field index
   int32_t delim;
   uint64_t low_mask;                  // bit f: field f < 64 is projected (skips the table lookup)
+  int16_t pf[CSV_MAX_FIELDS];         // the projected field indices, ascending
+  int32_t npf;
 };
 
 // Bytes of the file by global position: straight from HBM, or from a wave's LDS copy of a block.
@@ -497,6 +499,54 @@ __device__ void walk_record(const D& data, int64_t s, int64_t e, const FieldArgs
   if (f <= A.max_field) record_field(data, A, f, fs, e, r);
 }
 
+// Position of the k-th (0-based) set bit of a 16-bit mask that has more than k set bits.
+__device__ __forceinline__ int nth_bit16(uint32_t d, int k) {
+  int pos = 0, c = __popc(d & 0xFFu);
+  if (k >= c) { k -= c; d >>= 8; pos += 8; }
+  c = __popc(d & 0xFu);
+  if (k >= c) { k -= c; d >>= 4; pos += 4; }
+  c = __popc(d & 0x3u);
+  if (k >= c) { k -= c; d >>= 2; pos += 2; }
+  return pos + (k >= (int)(d & 1u) ? 1 : 0);
+}
+
+// walk_record for a line without a '"' byte (false: the line has one; nothing was written, the
+// caller walks it with walk_record). No per-delimiter loop: a 16-byte chunk holding n delimiters
+// ends fields f .. f + n - 1 at once, and only the projected fields among them (A.pf, ascending)
+// locate their bounds by bit selection — the walk's work follows the projected fields, not the
+// line's field count (the line pass is VALU-bound).
+template <typename D>
+__device__ bool walk_record_unquoted(const D& data, int64_t s, int64_t e, const FieldArgs& A, int32_t nproj, int64_t r) {
+  for (int c = 0; c < nproj; ++c) {  // fields the line does not reach read as "" (K:263)
+    A.start[c][r] = s;
+    A.len[c][r] = 0;
+    A.quoted[c][r] = 0;
+  }
+  int f = 0, t = 0;
+  int64_t fs = s;
+  for (int64_t a = s & ~(int64_t)15; a < e && t < A.npf; a += 16) {
+    const Lane16 v = data.load16(a);
+    const uint32_t lo = (uint32_t)(s > a ? s - a : 0);
+    const uint32_t hi = (uint32_t)(e - a < 16 ? e - a : 16);
+    const uint32_t in = (hi >= 32 ? 0xFFFFu : ((1u << hi) - 1u)) & ~((1u << lo) - 1u);
+    if (has_byte(v, '"') && (eq16(v, '"') & in)) return false;
+    const uint32_t d = eq16(v, (uint32_t)A.delim) & in;
+    const int n = __popc(d);
+    while (t < A.npf && A.pf[t] < f + n) {  // projected field A.pf[t] ends in this chunk
+      const int ft = A.pf[t], k = ft - f;
+      const int64_t st = k == 0 ? fs : a + nth_bit16(d, k - 1) + 1;
+      record_field(data, A, ft, st, a + nth_bit16(d, k), r);
+      ++t;
+    }
+    if (n) {
+      fs = a + (31 - __builtin_clz(d)) + 1;
+      f += n;
+    }
+  }
+  if (t < A.npf && A.pf[t] == f) record_field(data, A, f, fs, e, r);  // the line's last field
+  return true;
+}
+
 // The field table in LDS: indexing kernel arguments by a per-lane field number would turn every
 // field into a memory round trip.
 __device__ __forceinline__ void stage_args(FieldArgs& S, const FieldArgs& A) {
@@ -508,10 +558,12 @@ __device__ __forceinline__ void stage_args(FieldArgs& S, const FieldArgs& A) {
     S.quoted[threadIdx.x] = A.quoted[threadIdx.x];
     S.stage[threadIdx.x] = A.stage[threadIdx.x];
   }
+  if (threadIdx.x < CSV_MAX_FIELDS) S.pf[threadIdx.x] = A.pf[threadIdx.x];
   if (threadIdx.x == 0) {
     S.max_field = A.max_field;
     S.delim = A.delim;
     S.low_mask = A.low_mask;
+    S.npf = A.npf;
   }
   __syncthreads();
 }
@@ -574,12 +626,14 @@ __global__ void __launch_bounds__(256) k_csv_lines(const uint8_t* __restrict__ d
         const LBytes d{L, base};
         if (s < e && d[s] != '#')
           for (int64_t p = s; p < e && !keep; ++p) keep = d[p] > 0x20;
-        if (keep && li >= first) walk_record(d, s, e, A, nproj, li - first);
+        if (keep && li >= first && !walk_record_unquoted(d, s, e, A, nproj, li - first))
+          walk_record(d, s, e, A, nproj, li - first);
       } else {
         const GBytes d{data, nbytes};
         if (s < e && d[s] != '#')
           for (int64_t p = s; p < e && !keep; ++p) keep = d[p] > 0x20;
-        if (keep && li >= first) walk_record(d, s, e, A, nproj, li - first);
+        if (keep && li >= first && !walk_record_unquoted(d, s, e, A, nproj, li - first))
+          walk_record(d, s, e, A, nproj, li - first);
       }
       if (!keep) atomicAdd(nskip, 1ull);
     }
@@ -843,6 +897,9 @@ int csv_parse(qe_ctx* ctx, const uint8_t* data, int64_t nbytes, const qe_csv_opt
     A.max_field = std::max(A.max_field, f);
     if (f < 64) A.low_mask |= 1ull << f;
   }
+  A.npf = 0;  // the projected field indices, ascending (walk_record_unquoted)
+  for (int f = 0; f <= A.max_field; ++f)
+    if (A.slot[f] >= 0) A.pf[A.npf++] = (int16_t)f;
   // ---- record terminators
   const int64_t nseg = (int64_t)div_up((uint64_t)(nbytes > 0 ? nbytes : 1), SEG);
   void* p;
