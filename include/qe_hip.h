@@ -521,6 +521,16 @@ int qe_strdict_decode(qe_strdict* dict, const qe_column* codes, qe_column* out);
  * dictionary that holds no long key are all packed, and decode then needs no host round trip —
  * `out->values` must hold 7 bytes per row. Otherwise as qe_strdict_decode. */
 int qe_strdict_decode_trusted(qe_strdict* dict, const qe_column* codes, qe_column* out);
+/* Wide codes without a dictionary, for a UTF8 column whose every value is known to be at most 7
+ * bytes (a CSV column with qe_csv_column_max_len <= 7): the packed code qe_strdict_encode gives
+ * each value (validity copied), in one streaming kernel with no host round trip, so the
+ * aggregation that consumes the codes queues right behind it. The bound is the caller's promise
+ * (not checked: a longer value gets a code of its first 7 bytes). */
+int qe_strdict_encode_packed(qe_ctx* ctx, const qe_column* in, qe_column* codes);
+/* Packed wide codes (encode_packed's, or a trusted dictionary's while it holds no long key) ->
+ * UTF8: offsets for codes->length+1 entries, `out->values` 7 bytes per row, validity iff codes has
+ * one; stream-ordered, no synchronisation (one kernel up to 65536 rows). */
+int qe_strdict_decode_packed(qe_ctx* ctx, const qe_column* codes, qe_column* out);
 /* Composite group keys (K:621-626 `List` of key values) whose packing exceeds 63 bits: each row's
  * tuple of up to QE_MAX_KEYS fixed-width / BOOL key columns (nulls and fp64 NaNs as
  * List/Double.equals see them) gets a dense int32 code; codes->validity (optional) is set all-valid.
@@ -636,6 +646,9 @@ int qe_csv_column(const qe_csv_table* table, int32_t i, qe_column* out);
  * rows+1 entries, values >= qe_csv_column_bytes; stream-ordered, no synchronisation). */
 int qe_csv_column_bytes(const qe_csv_table* table, int32_t i, int64_t* nbytes);
 int qe_csv_column_copy(const qe_csv_table* table, int32_t i, qe_column* dst);
+/* Length in bytes of projected column i's longest value (known at parse time, no device work):
+ * lets a caller take qe_strdict_encode_packed for short keys. */
+int qe_csv_column_max_len(const qe_csv_table* table, int32_t i, int64_t* nbytes);
 int qe_csv_destroy(qe_csv_table* table);
 /* Streaming a file larger than one device batch (ReaderIterator's batches, K:239-252): host bytes
  * data[0, nbytes) that start at a record boundary are cut after their last complete record.

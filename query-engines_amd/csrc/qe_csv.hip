@@ -13,13 +13,15 @@
 //   * a field value is its bytes with chars <= 0x20 trimmed from both ends; if that starts and ends
 //     with '"' (length >= 2) the quotes are removed, "" becomes ", and the result is trimmed again
 //     (K:263 calls String.trim() on every value); a missing trailing field reads as "" (K:263).
-// Pipeline (all HBM-streaming, one wave per 64 KiB segment for the byte passes):
+// Pipeline (all HBM-streaming, one wave per 16 KiB segment for the byte passes):
 //   k_csv_count2   per segment: quotes, and terminators under both starting quote states
-//                  -> scan of quotes (state at segment start) -> pick -> scan -> k_csv_terms<true>:
-//                  terminator positions
-//   k_csv_keep     per line: kept?                   -> scan -> kept-line list
-//   k_csv_fields   per kept row: projected field ranges, unescaped lengths
-//   k_csv_copy_wave per projected column: offsets (scan of lengths) + bytes
+//   k_csv_seg_reduce / _apply: quote state at each segment start, terminator prefixes, line count
+//   k_csv_terms<true> terminator positions (the line-end list)
+//   k_csv_lines    per line (64 per wave, staged in LDS): projected field lengths, short values
+//                  into a 16-byte stage (kept-line path k_csv_keep / k_csv_fields when a line is
+//                  blank or a comment)
+//   k_csv_len_*    reduce / scan / apply: every column's value byte starts and size in 3 launches
+//   k_csv_copy_wave per projected column: Utf8 offsets + bytes
 #include <vector>
 
 #include "qe_internal.hpp"
@@ -31,15 +33,18 @@ struct qe_csv_table {
   int64_t consumed = 0;           // bytes up to and including the last record (all of them unless QE_CSV_PARTIAL_TAIL)
   int64_t stride = 0;             // entries per array of the block (>= rows + 1)
   int32_t nproj = 0;
-  void* block = nullptr;          // per projected column: start i64, len i64, byte start i64 [stride], quoted u8
+  void* block = nullptr;          // per projected column: start i64, meta u32, byte start u32 [stride]
   uint8_t* stage_block = nullptr; // per projected column: 16 bytes per row (short unquoted values)
   std::vector<int64_t> total;     // per projected column: bytes
+  std::vector<int64_t> maxlen;    // per projected column: longest value, bytes
   std::vector<qe_column> cols;    // materialised views (qe_csv_column), built on first request
   std::vector<void*> owned;
+  // start: file position of the value, written only where the column build reads it (quoted, or
+  // longer than its 16-byte stage); meta: output length | quoted << 31; bstart: the value's byte
+  // start in the column (the Utf8 offsets, < 2^31), entry rows = the column's size
   int64_t* start(int c) { return (int64_t*)block + (size_t)c * stride; }
-  int64_t* len(int c) { return (int64_t*)block + (size_t)(nproj + c) * stride; }
-  int64_t* bstart(int c) { return (int64_t*)block + (size_t)(2 * nproj + c) * stride; }
-  uint8_t* quoted(int c) { return (uint8_t*)((int64_t*)block + (size_t)3 * nproj * stride) + (size_t)c * stride; }
+  uint32_t* meta(int c) { return (uint32_t*)((int64_t*)block + (size_t)nproj * stride) + (size_t)c * stride; }
+  uint32_t* bstart(int c) { return meta(0) + (size_t)(nproj + c) * stride; }
   uint8_t* stage(int c) { return stage_block + (size_t)c * stride * 16; }
 };
 
@@ -108,6 +113,16 @@ __device__ __forceinline__ uint32_t eq16(const Lane16& v, uint32_t b) {
     m |= (((hb >> 7) & 1u) | ((hb >> 14) & 2u) | ((hb >> 21) & 4u) | ((hb >> 28) & 8u)) << (4 * i);
   }
   return m;
+}
+
+// The '\n' bytes of 16 as bit 7 of each matching byte, per 32-bit word (no packing to a 16-bit mask:
+// counts and positions come straight from these words, and the byte passes are VALU-bound).
+__device__ __forceinline__ void nl_words(const Lane16& v, uint32_t (&h)[4]) {
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const uint32_t x = v.w[i] ^ 0x0A0A0A0Au;
+    h[i] = ~(((x & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | x | 0x7F7F7F7Fu);
+  }
 }
 
 // `next` = the byte after these 16 (the next lane's first byte, passed by shuffle; 0 past the end).
@@ -182,15 +197,23 @@ __global__ void __launch_bounds__(256) k_csv_terms(const uint8_t* __restrict__ d
     const uint32_t qodd = mq ? (uint32_t)(quotes16(v) & 1) : 0u;
     const uint64_t par = __ballot(qodd);
     const uint32_t inq0 = carry ^ ((uint32_t)__popcll(par & below) & 1u);
-    uint32_t inq1;
+    uint32_t inq1;  // (the carry advances from the ballot; the state after the 16 bytes is unused here)
     // byte after this lane's 16: the next lane's first byte; lane 63 reads it (rare)
     uint32_t next = (uint32_t)__shfl_down((int)(v.w[0] & 0xFFu), 1);
     // lane 63: only a trailing '\r' needs the next byte (a load here on every step would put a
     // full memory round trip on every step's critical path)
     if (lane == 63) next = (v.byte(15) == '\r' && pos + 16 < nbytes) ? data[pos + 16] : 0u;
-    const uint32_t m = terms16(v, next, nbytes, pos, inq0, &inq1, mq);
+    // no quote, no '\r', a full chunk: the '\n' words directly (outside quotes) or nothing
+    const bool plain = !mq && pos + 16 <= nbytes && !has_byte(v, '\r');
+    uint32_t h[4] = {0, 0, 0, 0};
+    uint32_t m = 0;
+    if (plain) {
+      if (!inq0) nl_words(v, h);
+    } else {
+      m = terms16(v, next, nbytes, pos, inq0, &inq1, mq);
+    }
     carry ^= (uint32_t)__popcll(par) & 1u;
-    const int c = __popc(m);  // 0..16
+    const int c = plain ? __popc(h[0]) + __popc(h[1]) + __popc(h[2]) + __popc(h[3]) : __popc(m);  // 0..16
     // wave exclusive prefix and total of c from its 5 bit-planes (ballot + popcount, no LDS)
     int excl = 0, total = 0;
 #pragma unroll
@@ -201,11 +224,22 @@ __global__ void __launch_bounds__(256) k_csv_terms(const uint8_t* __restrict__ d
     }
     if (EMIT) {
       int64_t o = out + excl;
-      uint32_t mm = m;
-      while (mm) {
-        const int k = __builtin_ctz(mm);
-        mm &= mm - 1;
-        ends[o++] = pos + k;
+      if (plain) {
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {  // two 64-bit halves: fewer divergent loops than four words
+          uint64_t hh = h[2 * i] | ((uint64_t)h[2 * i + 1] << 32);
+          while (hh) {
+            ends[o++] = pos + 8 * i + (__builtin_ctzll(hh) >> 3);
+            hh &= hh - 1;
+          }
+        }
+      } else {
+        uint32_t mm = m;
+        while (mm) {
+          const int k = __builtin_ctz(mm);
+          mm &= mm - 1;
+          ends[o++] = pos + k;
+        }
       }
       out += total;
     }
@@ -257,7 +291,22 @@ __global__ void __launch_bounds__(256) k_csv_count2(const uint8_t* __restrict__ 
     uint32_t next = (uint32_t)__shfl_down((int)(v.w[0] & 0xFFu), 1);
     if (lane == 63) next = (v.byte(15) == '\r' && pos + 16 < nbytes) ? data[pos + 16] : 0u;
     uint32_t dummy;
-    if (nq == 0) {
+    if (nq == 0 && pos + 16 <= nbytes && !has_byte(v, '\r')) {  // '\n' terminators only: straight from the words
+      uint32_t h[4];
+      nl_words(v, h);
+      const int c = __popc(h[0]) + __popc(h[1]) + __popc(h[2]) + __popc(h[3]);
+      if (c) {
+        const int i = h[3] ? 3 : h[2] ? 2 : h[1] ? 1 : 0;
+        const int64_t last = pos + 4 * i + ((31 - __builtin_clz(h[i])) >> 3);
+        if (x) {
+          c1 += c;
+          l1 = last;
+        } else {
+          c0 += c;
+          l0 = last;
+        }
+      }
+    } else if (nq == 0) {
       const uint32_t mm = terms16(v, next, nbytes, pos, 0u, &dummy, false);
       if (mm) {
         const int64_t last = pos + 31 - __builtin_clz(mm);
@@ -295,16 +344,127 @@ __global__ void __launch_bounds__(256) k_csv_count2(const uint8_t* __restrict__ 
   }
 }
 
-// Terminator count of each segment under its actual starting quote state, and the file's last
-// terminator position (atomic max into *last, which starts at -1).
-__global__ void k_csv_pick(const int64_t* __restrict__ seg_qs, const int64_t* __restrict__ t0,
-                           const int64_t* __restrict__ t1, int64_t nseg, int64_t* __restrict__ seg_t,
-                           long long* __restrict__ last) {
-  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < nseg; i += (int64_t)gridDim.x * blockDim.x) {
-    const bool odd = seg_qs[i] & 1;
-    seg_t[i] = odd ? t1[i] : t0[i];
-    const int64_t l = odd ? t1[2 * nseg + i] : t0[2 * nseg + i];
-    if (l >= 0) atomicMax(last, (long long)l);
+// The segment plan: the quote state at each segment's start (parity of all earlier quotes), the
+// terminator count under that state, its prefixes, and the last terminator's position — in two
+// launches over blocks of 2048 segments. k_csv_seg_reduce: per block, its quote count and its
+// terminator total and last terminator under both possible states at the block's start.
+// k_csv_seg_apply: each block resolves its start state and prefixes from the blocks before it (a
+// short serial pass over their totals), then writes its segments' quote and terminator prefixes;
+// the last block also leaves the terminator count and the last terminator's position in host[0..1]
+// (fine-grained pinned memory) for the one read-back that sizes the line list. (One 1024-thread
+// block doing it all took 52 us on tripdata's 27K segments: a single CU's memory round trips.)
+constexpr int SP_THREADS = 256, SP_TILE = SP_THREADS * 8;
+struct SegAgg {
+  int64_t q, t[2], last[2];  // [P]: the block starts inside quotes (P = 1) or not
+};
+
+__device__ __forceinline__ void seg_load(const int64_t* __restrict__ seg_q, const int64_t* __restrict__ t0,
+                                         const int64_t* __restrict__ t1, int64_t nseg, int64_t g0, int64_t (&q)[8],
+                                         int64_t (&a)[8], int64_t (&b)[8], int64_t (&la)[8], int64_t (&lb)[8]) {
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    const int64_t e = tile_elem(g0, k);
+    const bool in = e < nseg;
+    q[k] = in ? seg_q[e] : 0;
+    a[k] = in ? t0[e] : 0;
+    b[k] = in ? t1[e] : 0;
+    la[k] = in ? t0[2 * nseg + e] : -1;  // seg_l0 / seg_l1 follow the two count arrays
+    lb[k] = in ? t1[2 * nseg + e] : -1;
+  }
+}
+
+__global__ void __launch_bounds__(SP_THREADS) k_csv_seg_reduce(const int64_t* __restrict__ seg_q,
+                                                               const int64_t* __restrict__ t0,
+                                                               const int64_t* __restrict__ t1, int64_t nseg,
+                                                               SegAgg* __restrict__ agg) {
+  __shared__ int64_t ws[SP_THREADS / 64];
+  __shared__ int64_t red[SP_THREADS / 64][5];
+  int64_t q[8], a[8], b[8], la[8], lb[8], ex[8];
+  seg_load(seg_q, t0, t1, nseg, (int64_t)blockIdx.x * SP_TILE, q, a, b, la, lb);
+  const int64_t qt = tile_excl<int64_t, SP_THREADS / 64>(q, ex, ws);
+  int64_t s0 = 0, s1 = 0, m0 = -1, m1 = -1;
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    const bool odd = ex[k] & 1;  // quotes before this segment within the block
+    s0 += odd ? b[k] : a[k];
+    s1 += odd ? a[k] : b[k];
+    m0 = max(m0, odd ? lb[k] : la[k]);
+    m1 = max(m1, odd ? la[k] : lb[k]);
+  }
+  for (int d = 32; d >= 1; d >>= 1) {
+    s0 += __shfl_xor(s0, d);
+    s1 += __shfl_xor(s1, d);
+    m0 = max(m0, (int64_t)__shfl_xor(m0, d));
+    m1 = max(m1, (int64_t)__shfl_xor(m1, d));
+  }
+  const int wid = threadIdx.x >> 6;
+  if ((threadIdx.x & 63) == 0) {
+    red[wid][0] = s0;
+    red[wid][1] = s1;
+    red[wid][2] = m0;
+    red[wid][3] = m1;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    SegAgg g{qt, {0, 0}, {-1, -1}};
+    for (int w = 0; w < SP_THREADS / 64; ++w) {
+      g.t[0] += red[w][0];
+      g.t[1] += red[w][1];
+      g.last[0] = max(g.last[0], red[w][2]);
+      g.last[1] = max(g.last[1], red[w][3]);
+    }
+    agg[blockIdx.x] = g;
+  }
+}
+
+__global__ void __launch_bounds__(SP_THREADS) k_csv_seg_apply(const int64_t* __restrict__ seg_q,
+                                                              const int64_t* __restrict__ t0,
+                                                              const int64_t* __restrict__ t1, int64_t nseg,
+                                                              const SegAgg* __restrict__ agg, int64_t nb,
+                                                              int64_t* __restrict__ seg_qs, int64_t* __restrict__ seg_ts,
+                                                              int64_t* host) {
+  __shared__ int64_t ws[SP_THREADS / 64];
+  __shared__ int64_t base[2];
+  const int64_t blk = blockIdx.x;
+  if (threadIdx.x == 0) {  // this block's start state and prefixes from the blocks before it
+    int64_t qp = 0, tp = 0, last = -1;
+    for (int64_t j = 0; j < blk; ++j) {
+      const SegAgg g = agg[j];
+      const int P = (int)(qp & 1);
+      tp += g.t[P];
+      last = max(last, g.last[P]);
+      qp += g.q;
+    }
+    base[0] = qp;
+    base[1] = tp;
+    if (blk == nb - 1) {  // the file's totals
+      const SegAgg g = agg[blk];
+      const int P = (int)(qp & 1);
+      const int64_t tall = tp + g.t[P];
+      seg_qs[nseg] = qp + g.q;
+      seg_ts[nseg] = tall;
+      __hip_atomic_store(&host[0], tall, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      __hip_atomic_store(&host[1], max(last, g.last[P]), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+  }
+  __syncthreads();
+  const int64_t qp = base[0], tp = base[1];
+  const int64_t g0 = blk * SP_TILE;
+  int64_t q[8], a[8], b[8], la[8], lb[8], ex[8];
+  seg_load(seg_q, t0, t1, nseg, g0, q, a, b, la, lb);
+  (void)tile_excl<int64_t, SP_THREADS / 64>(q, ex, ws);
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    const int64_t qs = qp + ex[k];
+    const int64_t e = tile_elem(g0, k);
+    if (e < nseg) seg_qs[e] = qs;
+    q[k] = (qs & 1) ? b[k] : a[k];  // the terminator count under the segment's actual start state
+  }
+  (void)tile_excl<int64_t, SP_THREADS / 64>(q, ex, ws);
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    const int64_t e = tile_elem(g0, k);
+    if (e < nseg) seg_ts[e] = tp + ex[k];
   }
 }
 
@@ -338,8 +498,7 @@ __global__ void k_csv_compact_lines(const int64_t* __restrict__ keep, const int6
 struct FieldArgs {
   int16_t slot[CSV_MAX_FIELD_INDEX];  // field index -> projected column slot, -1 = not projected
   int64_t* start[CSV_MAX_FIELDS];     // per column: byte position of the (trimmed, unquoted) value
-  int64_t* len[CSV_MAX_FIELDS];       // per column: output length (after unescaping)
-  uint8_t* quoted[CSV_MAX_FIELDS];    // per column: 1 if "" sequences must be unescaped
+  uint32_t* meta[CSV_MAX_FIELDS];     // per column: output length (after unescaping) | quoted << 31
   uint8_t* stage[CSV_MAX_FIELDS];     // per column: 16 bytes per row, the value when unquoted and <= 16 bytes
   int32_t max_field;                  // largest projected field index
   int32_t delim;
@@ -454,22 +613,18 @@ __device__ void record_field(const D& d, const FieldArgs& A, int f, int64_t s, i
     len = n;
     q = 1;
   }
-  A.start[sl][row] = s;
-  A.len[sl][row] = len;
-  A.quoted[sl][row] = q;
-  // Short unquoted values are also staged densely, 16 bytes per row, while the line sits in LDS;
-  // the column build then reads them there instead of gathering from every line of the file.
+  A.meta[sl][row] = (uint32_t)len | ((uint32_t)q << 31);
+  // Short unquoted values are staged densely, 16 bytes per row, while the line sits in LDS; the
+  // column build reads them there instead of gathering from every line of the file (and needs no
+  // file position for them).
   if (!q && len <= 16) *(uint4*)(A.stage[sl] + row * 16) = d.bytes16(s, len);
+  else A.start[sl][row] = s;
 }
 
 // One record [s, e): the projected fields' ranges into row `r` (missing fields read as "").
 template <typename D>
 __device__ void walk_record(const D& data, int64_t s, int64_t e, const FieldArgs& A, int32_t nproj, int64_t r) {
-  for (int c = 0; c < nproj; ++c) {
-    A.start[c][r] = s;
-    A.len[c][r] = 0;
-    A.quoted[c][r] = 0;
-  }
+  for (int c = 0; c < nproj; ++c) A.meta[c][r] = 0;
   int f = 0;
   int64_t fs = s;
   uint32_t inq = 0;
@@ -517,11 +672,7 @@ __device__ __forceinline__ int nth_bit16(uint32_t d, int k) {
 // line's field count (the line pass is VALU-bound).
 template <typename D>
 __device__ bool walk_record_unquoted(const D& data, int64_t s, int64_t e, const FieldArgs& A, int32_t nproj, int64_t r) {
-  for (int c = 0; c < nproj; ++c) {  // fields the line does not reach read as "" (K:263)
-    A.start[c][r] = s;
-    A.len[c][r] = 0;
-    A.quoted[c][r] = 0;
-  }
+  for (int c = 0; c < nproj; ++c) A.meta[c][r] = 0;  // fields the line does not reach read as "" (K:263)
   int f = 0, t = 0;
   int64_t fs = s;
   for (int64_t a = s & ~(int64_t)15; a < e && t < A.npf; a += 16) {
@@ -554,8 +705,7 @@ __device__ __forceinline__ void stage_args(FieldArgs& S, const FieldArgs& A) {
   for (int i = threadIdx.x; i <= A.max_field; i += blockDim.x) S.slot[i] = src[i];
   if (threadIdx.x < CSV_MAX_FIELDS) {
     S.start[threadIdx.x] = A.start[threadIdx.x];
-    S.len[threadIdx.x] = A.len[threadIdx.x];
-    S.quoted[threadIdx.x] = A.quoted[threadIdx.x];
+    S.meta[threadIdx.x] = A.meta[threadIdx.x];
     S.stage[threadIdx.x] = A.stage[threadIdx.x];
   }
   if (threadIdx.x < CSV_MAX_FIELDS) S.pf[threadIdx.x] = A.pf[threadIdx.x];
@@ -789,37 +939,151 @@ __global__ void __launch_bounds__(256) k_csv_seg_fields(const uint8_t* __restric
   if (lane == 0 && sus) atomicAdd(suspect, sus);
 }
 
-__global__ void k_csv_offsets(const int64_t* __restrict__ starts64, int64_t n, int32_t* __restrict__ offs) {
-  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i <= n; i += (int64_t)gridDim.x * blockDim.x)
-    offs[i] = (int32_t)starts64[i];
+// Byte starts of the projected columns' values (the Utf8 offsets): a scan of the lengths in meta,
+// every column per launch (blockIdx.y = column). Per 8192-row tile its sum (int64), the tiles'
+// prefixes, then each tile's rows in 32-bit arithmetic — exact whenever the column's size is below
+// 2^31, which the host checks on the int64 total (round 5: int64 lengths, the generic int64 scan
+// per column, then a kernel narrowing the starts to int32 offsets).
+// (The longest value of each tile goes to maxs, same layout as sums.)
+__global__ void __launch_bounds__(1024) k_csv_len_reduce(const uint32_t* __restrict__ meta0, int64_t stride, int64_t n,
+                                                         int64_t nb, int64_t* __restrict__ sums,
+                                                         int64_t* __restrict__ maxs) {
+  __shared__ int64_t ws[16], wm[16];
+  const uint32_t* __restrict__ m = meta0 + (size_t)blockIdx.y * stride;
+  uint32_t v[8];
+  tile_load_u32(m, (int64_t)blockIdx.x * 8192, n, v);
+  int64_t t = 0, mx = 0;
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    const int64_t l = v[k] & 0x7FFFFFFFu;
+    t += l;
+    mx = max(mx, l);
+  }
+  for (int d = 32; d >= 1; d >>= 1) {
+    t += __shfl_xor(t, d);
+    mx = max(mx, (int64_t)__shfl_xor(mx, d));
+  }
+  if ((threadIdx.x & 63) == 0) {
+    ws[threadIdx.x >> 6] = t;
+    wm[threadIdx.x >> 6] = mx;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    int64_t all = 0;
+    for (int w = 0; w < 16; ++w) {
+      all += ws[w];
+      mx = max(mx, wm[w]);
+    }
+    sums[(size_t)blockIdx.y * (nb + 1) + blockIdx.x] = all;
+    maxs[(size_t)blockIdx.y * (nb + 1) + blockIdx.x] = mx;
+  }
 }
 
-// Field bytes of one projected column into its Utf8 values buffer. A wave takes 64 rows, puts their output offsets and source
-// starts in LDS, and its lanes then walk the wave's contiguous output range 4 bytes per lane —
-// byte j's row found by binary search over the 64 offsets. Stores land contiguous across lanes,
-// and the source loads are independent (not one dependent loop per row). A wave holding a quoted
-// field (escape-aware copy: `""` -> `"`) copies row by row. (One thread per row, byte by byte,
-// took 132 / 95 us for tripdata's fare_amount / VendorID columns.)
+// One block per column: the tile sums' exclusive prefixes in place, the column's size at entry n of
+// its starts and in host[1 + c], its longest value in host[1 + nproj + c]; host[0] = *nskip
+// (lines that are not records), so one sync returns everything the host needs.
+__global__ void __launch_bounds__(1024) k_csv_len_scan(int64_t* __restrict__ sums, const int64_t* __restrict__ maxs,
+                                                       int64_t nb, uint32_t* __restrict__ bstart0,
+                                                       int64_t stride, int64_t n,
+                                                       const unsigned long long* __restrict__ nskip, int64_t* host) {
+  __shared__ int64_t ws[16];
+  int64_t* __restrict__ sm = sums + (size_t)blockIdx.x * (nb + 1);
+  const int64_t* __restrict__ mm = maxs + (size_t)blockIdx.x * (nb + 1);
+  int64_t carry = 0, mx = 0;
+  for (int64_t g0 = 0; g0 < nb; g0 += 8192) {
+    int64_t v[8], ex[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const int64_t e = tile_elem(g0, k);
+      v[k] = e < nb ? sm[e] : 0;
+      if (e < nb) mx = max(mx, mm[e]);
+    }
+    const int64_t t = tile_excl(v, ex, ws);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const int64_t e = tile_elem(g0, k);
+      if (e < nb) sm[e] = carry + ex[k];
+    }
+    carry += t;
+  }
+  for (int d = 32; d >= 1; d >>= 1) mx = max(mx, (int64_t)__shfl_xor(mx, d));
+  if ((threadIdx.x & 63) == 0) ws[threadIdx.x >> 6] = mx;  // (tile_excl's last barrier freed ws)
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    for (int w = 0; w < 16; ++w) mx = max(mx, ws[w]);
+    __hip_atomic_store(&host[1 + gridDim.x + blockIdx.x], mx, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    sm[nb] = carry;
+    bstart0[(size_t)blockIdx.x * stride + n] = (uint32_t)carry;
+    __hip_atomic_store(&host[1 + blockIdx.x], carry, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    if (blockIdx.x == 0)
+      __hip_atomic_store(&host[0], nskip ? (int64_t)*nskip : (int64_t)0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
+}
+
+__global__ void __launch_bounds__(1024) k_csv_len_apply(const uint32_t* __restrict__ meta0, int64_t stride, int64_t n,
+                                                        int64_t nb, const int64_t* __restrict__ sums,
+                                                        uint32_t* __restrict__ bstart0) {
+  __shared__ uint32_t ws[16];
+  const uint32_t* __restrict__ m = meta0 + (size_t)blockIdx.y * stride;
+  uint32_t* __restrict__ b = bstart0 + (size_t)blockIdx.y * stride;
+  const int64_t g0 = (int64_t)blockIdx.x * 8192;
+  uint32_t v[8], ex[8];
+  tile_load_u32(m, g0, n, v);
+#pragma unroll
+  for (int k = 0; k < 8; ++k) v[k] &= 0x7FFFFFFFu;
+  (void)tile_excl(v, ex, ws);
+  const uint32_t base = (uint32_t)sums[(size_t)blockIdx.y * (nb + 1) + blockIdx.x];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) ex[k] += base;
+  const int64_t e0 = tile_elem(g0, 0);
+  if (e0 + 8 <= n) {
+    *(uint4*)(b + e0) = make_uint4(ex[0], ex[1], ex[2], ex[3]);
+    *(uint4*)(b + e0 + 4) = make_uint4(ex[4], ex[5], ex[6], ex[7]);
+  } else {
+#pragma unroll
+    for (int k = 0; k < 8; ++k)
+      if (e0 + k < n) b[e0 + k] = ex[k];
+  }
+}
+
+// Offsets and bytes of one projected column into its Utf8 buffers. A wave takes 64 rows, puts their
+// output offsets and byte sources in LDS, and its lanes then walk the wave's contiguous output range
+// 4 bytes per lane — byte j's row found by binary search over the 64 offsets. Stores land
+// contiguous across lanes, and the source loads are independent (not one dependent loop per row).
+// A short unquoted value comes from its 16-byte stage, any other from the file. A wave holding a
+// quoted field (escape-aware copy: `""` -> `"`) copies row by row. (One thread per row, byte by
+// byte, took 132 / 95 us for tripdata's fare_amount / VendorID columns.)
 __global__ void __launch_bounds__(256) k_csv_copy_wave(const uint8_t* __restrict__ data, const int64_t* __restrict__ start,
-                                                       const int64_t* __restrict__ len, const uint8_t* __restrict__ quoted,
-                                                       const uint8_t* __restrict__ stage, const int32_t* __restrict__ offs,
-                                                       int64_t n, uint8_t* __restrict__ out) {
+                                                       const uint32_t* __restrict__ meta, const uint8_t* __restrict__ stage,
+                                                       const uint32_t* __restrict__ bstart, int64_t n,
+                                                       int32_t* __restrict__ offs, uint8_t* __restrict__ out,
+                                                       int lds_path) {
   __shared__ int32_t s_o[4][65];
   __shared__ int64_t s_s[4][64];  // source of the row's first byte: file position, or -1 - row (staged)
+  __shared__ __attribute__((aligned(16))) uint8_t s_b[4][1056];  // a staged wave's output bytes
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int64_t nw = ((int64_t)gridDim.x * blockDim.x) >> 6;
+  const bool out16 = lds_path && ((uintptr_t)out & 15) == 0;
   for (int64_t r0 = (((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6) * 64; r0 < n; r0 += nw * 64) {
     const int64_t r = r0 + lane;
     const bool in = r < n;
-    const int64_t s = in ? start[r] : 0;
-    if (__ballot(in && quoted[r])) {
+    const uint32_t mt = in ? meta[r] : 0u;
+    const int64_t l = mt & 0x7FFFFFFFu;
+    const bool q = mt >> 31;
+    const bool staged = !q && l <= 16;
+    const int32_t o = in ? (int32_t)bstart[r] : 0x7FFFFFFF;
+    if (in) offs[r] = o;
+    if (r == n - 1) offs[n] = (int32_t)bstart[n];
+    if (__ballot(q)) {
       if (in) {
-        const int64_t l = len[r];
-        uint8_t* dst = out + offs[r];
-        if (!quoted[r]) {  // an unquoted field keeps any `""` verbatim
+        uint8_t* dst = out + o;
+        if (staged) {
+          for (int64_t k = 0; k < l; ++k) dst[k] = stage[r * 16 + k];
+        } else if (!q) {  // an unquoted field keeps any `""` verbatim
+          const int64_t s = start[r];
           for (int64_t k = 0; k < l; ++k) dst[k] = data[s + k];
         } else {
-          int64_t p = s;
+          int64_t p = start[r];
           for (int64_t k = 0; k < l; ++k) {
             const uint8_t c = data[p];
             dst[k] = c;
@@ -830,9 +1094,41 @@ __global__ void __launch_bounds__(256) k_csv_copy_wave(const uint8_t* __restrict
       continue;
     }
     const int64_t rend = r0 + 64 < n ? r0 + 64 : n;
-    s_o[w][lane] = in ? offs[r] : 0x7FFFFFFF;
-    s_s[w][lane] = (in && len[r] <= 16) ? -1 - r : s;  // unquoted here: short values are staged
-    if (lane == 0) s_o[w][64] = offs[rend];
+    if (out16 && !__ballot(in && !staged)) {
+      // every value of the wave sits in its 16-byte stage (<= 1 KiB in all): one 16-byte load per
+      // row, the bytes assembled in LDS at their output positions, then 16-byte stores of the
+      // wave's output range (byte stores only at its two ends)
+      const int32_t obeg = __shfl(o, 0), oend = (int32_t)bstart[rend];
+      const int32_t a0 = obeg & ~15;
+      uint8_t* B = s_b[w];
+      if (in && l) {
+        const uint4 st = *(const uint4*)(stage + r * 16);
+        const uint64_t lo = ((uint64_t)st.y << 32) | st.x, hi = ((uint64_t)st.w << 32) | st.z;
+        uint8_t* d = B + (o - a0);
+        // 16 predicated byte stores with constant shifts (a loop over l was vectorised by the compiler
+        // into dword / 16-byte LDS stores at unaligned addresses, and corrupted bytes)
+#pragma unroll
+        for (int k = 0; k < 16; ++k)
+          if (k < (int)l) d[k] = (uint8_t)(k < 8 ? lo >> (8 * k) : hi >> (8 * (k - 8)));
+      }
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      for (int32_t c = a0 + lane * 16; c < oend; c += 1024) {
+        if (c >= obeg && c + 16 <= oend) {
+          *(uint4*)(out + c) = *(const uint4*)(B + (c - a0));
+        } else {
+          for (int k = 0; k < 16; ++k)
+            if (c + k >= obeg && c + k < oend) out[c + k] = B[c + k - a0];
+        }
+      }
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");  // s_b is rewritten next
+      __builtin_amdgcn_wave_barrier();
+      continue;
+    }
+    s_o[w][lane] = o;
+    s_s[w][lane] = staged ? -1 - r : (in ? start[r] : 0);
+    if (lane == 0) s_o[w][64] = (int32_t)bstart[rend];
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
@@ -877,6 +1173,44 @@ int read_i64(qe_ctx* ctx, const int64_t* p, int64_t* out) {
   return QE_OK;
 }
 
+// The value byte starts of every projected column for `rows` rows (their lengths in meta), the
+// columns' sizes into t->total, and host[0] = *nskip (0 without one): one sync. Sets t->rows.
+int column_sizes(qe_csv_table* t, int64_t rows, const unsigned long long* nskip, volatile int64_t* host) {
+  qe_ctx* ctx = t->ctx;
+  const int32_t nproj = t->nproj;
+  t->rows = rows;
+  t->total.assign((size_t)nproj, 0);
+  t->maxlen.assign((size_t)nproj, 0);
+  host[0] = 0;
+  const int64_t nb = (int64_t)div_up((uint64_t)(rows > 0 ? rows : 1), 8192);
+  void* p;
+  QE_TRY(ctx_workspace(ctx, 3, (size_t)nproj * (size_t)(nb + 1) * 16, &p));
+  int64_t* sums = (int64_t*)p;
+  int64_t* maxs = sums + (size_t)nproj * (size_t)(nb + 1);
+  if (rows > 0) {
+    hipLaunchKernelGGL(k_csv_len_reduce, dim3((unsigned)nb, (unsigned)nproj), dim3(1024), 0, ctx->stream, t->meta(0),
+                       t->stride, rows, nb, sums, maxs);
+    QE_TRY(launch_check("k_csv_len_reduce"));
+  } else {
+    QE_HIP(hipMemsetAsync(sums, 0, (size_t)nproj * (size_t)(nb + 1) * 16, ctx->stream));
+  }
+  hipLaunchKernelGGL(k_csv_len_scan, dim3((unsigned)nproj), dim3(1024), 0, ctx->stream, sums, maxs, nb, t->bstart(0),
+                     t->stride, rows, nskip, (int64_t*)host);
+  QE_TRY(launch_check("k_csv_len_scan"));
+  if (rows > 0) {
+    hipLaunchKernelGGL(k_csv_len_apply, dim3((unsigned)nb, (unsigned)nproj), dim3(1024), 0, ctx->stream, t->meta(0),
+                       t->stride, rows, nb, sums, t->bstart(0));
+    QE_TRY(launch_check("k_csv_len_apply"));
+  }
+  QE_TRY(ctx_sync(ctx));
+  for (int c = 0; c < nproj; ++c) {
+    t->total[(size_t)c] = host[1 + c];
+    t->maxlen[(size_t)c] = host[1 + nproj + c];
+    QE_CHECK(t->total[(size_t)c] < (1ll << 31), QE_ERR_CAPACITY, "CSV column %d holds more than 2^31 bytes", c);
+  }
+  return QE_OK;
+}
+
 int csv_parse(qe_ctx* ctx, const uint8_t* data, int64_t nbytes, const qe_csv_options* opt, qe_csv_table* t) {
   const int32_t nproj = opt->nfields;
   QE_CHECK(nproj >= 1 && nproj <= CSV_MAX_FIELDS, QE_ERR_UNSUPPORTED, "CSV scan projects 1..%d fields (got %d)",
@@ -903,14 +1237,12 @@ int csv_parse(qe_ctx* ctx, const uint8_t* data, int64_t nbytes, const qe_csv_opt
   // ---- record terminators
   const int64_t nseg = (int64_t)div_up((uint64_t)(nbytes > 0 ? nbytes : 1), SEG);
   void* p;
-  QE_TRY(ctx_workspace(ctx, 0, (size_t)(8 * nseg + 6) * 8, &p));
+  QE_TRY(ctx_workspace(ctx, 0, (size_t)(8 * nseg + 6) * 8 + (size_t)div_up((uint64_t)nseg, SP_TILE) * sizeof(SegAgg), &p));
   int64_t* seg_q = (int64_t*)p;
   int64_t* seg_qs = seg_q + nseg;
-  int64_t* seg_t = seg_qs + nseg + 1;
-  int64_t* seg_ts = seg_t + nseg;
+  int64_t* seg_ts = seg_qs + nseg + 1;
   int64_t* seg_t0 = seg_ts + nseg + 1;  // then seg_t1 [nseg], seg_l0 [nseg], seg_l1 [nseg]
   int64_t* seg_t1 = seg_t0 + nseg;
-  long long* last_term = (long long*)(seg_t0 + 4 * nseg);
   const int wgrid = (int)div_up((uint64_t)nseg, 4);  // 4 waves per 256-thread block
   if (nbytes > 0) {
     hipLaunchKernelGGL(k_csv_count2, dim3(wgrid), dim3(256), 0, ctx->stream, data, nbytes, nseg, seg_q, seg_t0, seg_t1);
@@ -920,23 +1252,21 @@ int csv_parse(qe_ctx* ctx, const uint8_t* data, int64_t nbytes, const qe_csv_opt
     QE_HIP(hipMemsetAsync(seg_t0, 0, 16, ctx->stream));
     QE_HIP(hipMemsetAsync(seg_t0 + 2, 0xFF, 16, ctx->stream));  // no terminator (nseg == 1)
   }
-  QE_HIP(hipMemsetAsync(last_term, 0xFF, 8, ctx->stream));
-  QE_TRY(exclusive_scan_i64(ctx, seg_q, seg_qs, nseg));
-  hipLaunchKernelGGL(k_csv_pick, dim3(grid_for(ctx, nseg)), dim3(256), 0, ctx->stream, seg_qs, seg_t0, seg_t1, nseg, seg_t,
-                     last_term);
-  QE_TRY(launch_check("k_csv_pick"));
-  QE_TRY(exclusive_scan_i64(ctx, seg_t, seg_ts, nseg));
-  // one read-back for the terminator count and the last terminator's position
-  int64_t nterm = 0, last_end = -1;
-  {
-    void* pin2;
-    QE_TRY(ctx_pinned(ctx, 16, &pin2));
-    QE_HIP(hipMemcpyAsync(pin2, seg_ts + nseg, 8, hipMemcpyDeviceToHost, ctx->stream));
-    QE_HIP(hipMemcpyAsync((int64_t*)pin2 + 1, last_term, 8, hipMemcpyDeviceToHost, ctx->stream));
-    QE_TRY(ctx_sync(ctx));
-    nterm = ((int64_t*)pin2)[0];
-    last_end = ((int64_t*)pin2)[1];
-  }
+  // the kernels below leave their few host-bound words in fine-grained pinned memory: one sync, no
+  // read-back copies
+  void* hp;
+  QE_TRY(ctx_pinned_coherent(ctx, (size_t)(2 * nproj + 2) * 8, &hp));
+  volatile int64_t* host = (volatile int64_t*)hp;
+  const int64_t spb = (int64_t)div_up((uint64_t)nseg, SP_TILE);
+  SegAgg* agg = (SegAgg*)(seg_t1 + 3 * nseg);  // after seg_t1 / seg_l0 / seg_l1
+  hipLaunchKernelGGL(k_csv_seg_reduce, dim3((unsigned)spb), dim3(SP_THREADS), 0, ctx->stream, seg_q, seg_t0, seg_t1, nseg,
+                     agg);
+  QE_TRY(launch_check("k_csv_seg_reduce"));
+  hipLaunchKernelGGL(k_csv_seg_apply, dim3((unsigned)spb), dim3(SP_THREADS), 0, ctx->stream, seg_q, seg_t0, seg_t1, nseg,
+                     agg, spb, seg_qs, seg_ts, (int64_t*)hp);
+  QE_TRY(launch_check("k_csv_seg_apply"));
+  QE_TRY(ctx_sync(ctx));
+  const int64_t nterm = host[0], last_end = host[1];
   QE_TRY(ctx_workspace(ctx, 1, (size_t)(3 * nterm + 7) * 8, &p));
   int64_t* ends = (int64_t*)p;
   int64_t* keep = ends + nterm + 2;
@@ -949,15 +1279,14 @@ int csv_parse(qe_ctx* ctx, const uint8_t* data, int64_t nbytes, const qe_csv_opt
   const int64_t first = opt->has_header ? 1 : 0;
   t->nproj = nproj;
   t->data = data;
-  t->stride = nlines + 1;
-  QE_TRY(dmalloc(t, (size_t)nproj * (size_t)t->stride * 25 + 64, &p));
+  t->stride = (nlines + 1 + 63) & ~(int64_t)63;  // every per-column array 256-byte aligned
+  QE_TRY(dmalloc(t, (size_t)nproj * (size_t)t->stride * 16 + 64, &p));
   t->block = p;
   QE_TRY(dmalloc(t, (size_t)nproj * (size_t)t->stride * 16, &p));
   t->stage_block = (uint8_t*)p;
   for (int c = 0; c < nproj; ++c) {
     A.start[c] = t->start(c);
-    A.len[c] = t->len(c);
-    A.quoted[c] = t->quoted(c);
+    A.meta[c] = t->meta(c);
     A.stage[c] = t->stage(c);
   }
   int64_t rows = 0;
@@ -974,29 +1303,14 @@ int csv_parse(qe_ctx* ctx, const uint8_t* data, int64_t nbytes, const qe_csv_opt
   const int64_t rows_all = std::max<int64_t>(0, nlines - first);
   if (seg_env && nlines > 0 && A.delim > 0x20) {
     // fields a record does not have read as "" (K:263): lengths and quote flags start at zero
-    QE_HIP(hipMemsetAsync(t->len(0), 0, (size_t)nproj * (size_t)t->stride * 8, ctx->stream));
-    QE_HIP(hipMemsetAsync(t->quoted(0), 0, (size_t)nproj * (size_t)t->stride, ctx->stream));
+    QE_HIP(hipMemsetAsync(t->meta(0), 0, (size_t)nproj * (size_t)t->stride * 4, ctx->stream));
     unsigned long long* suspect = (unsigned long long*)keep;
     QE_HIP(hipMemsetAsync(suspect, 0, 8, ctx->stream));
     hipLaunchKernelGGL(k_csv_seg_fields, dim3(wgrid), dim3(256), 0, ctx->stream, data, nbytes, nseg, seg_qs, seg_ts,
                        nlines, first, A, suspect);
     QE_TRY(launch_check("k_csv_seg_fields"));
-    for (int c = 0; c < nproj && rows_all > 0; ++c) QE_TRY(exclusive_scan_i64(ctx, A.len[c], t->bstart(c), rows_all));
-    void* pin;
-    QE_TRY(ctx_pinned(ctx, (size_t)(nproj + 1) * 8, &pin));
-    QE_HIP(hipMemcpyAsync(pin, suspect, 8, hipMemcpyDeviceToHost, ctx->stream));
-    for (int c = 0; c < nproj && rows_all > 0; ++c)
-      QE_HIP(hipMemcpyAsync((int64_t*)pin + 1 + c, t->bstart(c) + rows_all, 8, hipMemcpyDeviceToHost, ctx->stream));
-    QE_TRY(ctx_sync(ctx));
-    if (((int64_t*)pin)[0] == 0) {
-      t->rows = rows_all;
-      t->total.assign((size_t)nproj, 0);
-      for (int c = 0; c < nproj && rows_all > 0; ++c) {
-        t->total[(size_t)c] = ((int64_t*)pin)[1 + c];
-        QE_CHECK(t->total[(size_t)c] < (1ll << 31), QE_ERR_CAPACITY, "CSV column %d holds more than 2^31 bytes", c);
-      }
-      return QE_OK;
-    }
+    QE_TRY(column_sizes(t, rows_all, suspect, host));
+    if (host[0] == 0) return QE_OK;
     // a line that may not be a record: the line-end list and the kept-line path below decide
   }
   if (nterm > 0) {
@@ -1018,23 +1332,11 @@ int csv_parse(qe_ctx* ctx, const uint8_t* data, int64_t nbytes, const qe_csv_opt
                        A, nproj, nskip);
     QE_TRY(launch_check("k_csv_lines"));
     // Speculatively every line a record (the common case): the columns' length scans run now, and
-    // the skipped-line count and the column sizes come back in one read.
-    for (int c = 0; c < nproj && rows_all > 0; ++c) QE_TRY(exclusive_scan_i64(ctx, A.len[c], t->bstart(c), rows_all));
-    void* pin;
-    QE_TRY(ctx_pinned(ctx, (size_t)(nproj + 1) * 8, &pin));
-    QE_HIP(hipMemcpyAsync(pin, nskip, 8, hipMemcpyDeviceToHost, ctx->stream));
-    for (int c = 0; c < nproj && rows_all > 0; ++c)
-      QE_HIP(hipMemcpyAsync((int64_t*)pin + 1 + c, t->bstart(c) + rows_all, 8, hipMemcpyDeviceToHost, ctx->stream));
-    QE_TRY(ctx_sync(ctx));
-    const int64_t skipped = ((int64_t*)pin)[0];
-    if (skipped == 0) {
+    // the skipped-line count and the column sizes come back with one sync.
+    QE_TRY(column_sizes(t, rows_all, nskip, host));
+    if (host[0] == 0) {
       rows = rows_all;
       scanned = true;
-      t->total.assign((size_t)nproj, 0);
-      for (int c = 0; c < nproj && rows > 0; ++c) {
-        t->total[(size_t)c] = ((int64_t*)pin)[1 + c];
-        QE_CHECK(t->total[(size_t)c] < (1ll << 31), QE_ERR_CAPACITY, "CSV column %d holds more than 2^31 bytes", c);
-      }
     } else {  // blank or comment lines: kept-line list, then the fields of the kept rows
       hipLaunchKernelGGL(k_csv_keep, dim3(grid_for(ctx, nlines)), dim3(256), 0, ctx->stream, data, ends, nlines, keep);
       QE_TRY(launch_check("k_csv_keep"));
@@ -1056,23 +1358,17 @@ int csv_parse(qe_ctx* ctx, const uint8_t* data, int64_t nbytes, const qe_csv_opt
       }
     }
   }
-  t->rows = rows;
   if (scanned) return QE_OK;
   // ---- per column: byte positions of the values (scan of lengths) and the column's size
-  t->total.assign((size_t)nproj, 0);
-  for (int c = 0; c < nproj && rows > 0; ++c) QE_TRY(exclusive_scan_i64(ctx, A.len[c], t->bstart(c), rows));
-  if (rows > 0) {
-    void* pin;
-    QE_TRY(ctx_pinned(ctx, (size_t)nproj * 8, &pin));
-    for (int c = 0; c < nproj; ++c)
-      QE_HIP(hipMemcpyAsync((int64_t*)pin + c, t->bstart(c) + rows, 8, hipMemcpyDeviceToHost, ctx->stream));
-    QE_TRY(ctx_sync(ctx));
-    for (int c = 0; c < nproj; ++c) {
-      t->total[(size_t)c] = ((int64_t*)pin)[c];
-      QE_CHECK(t->total[(size_t)c] < (1ll << 31), QE_ERR_CAPACITY, "CSV column %d holds more than 2^31 bytes", c);
-    }
-  }
-  return QE_OK;
+  return column_sizes(t, rows, nullptr, host);
+}
+
+bool copy_lds() {
+  static const bool on = [] {
+    const char* e = getenv("QE_CSV_COPY_LDS");
+    return !(e && e[0] == '0');
+  }();
+  return on;
 }
 
 // Offsets + bytes of projected column c into dst (offsets for rows+1 entries, values >= total).
@@ -1083,15 +1379,9 @@ int build_column(qe_csv_table* t, int c, int32_t* offsets, uint8_t* values) {
     QE_HIP(hipMemsetAsync(offsets, 0, 4, ctx->stream));
     return QE_OK;
   }
-  hipLaunchKernelGGL(k_csv_offsets, dim3(grid_for(ctx, rows + 1)), dim3(256), 0, ctx->stream, t->bstart(c), rows,
-                     offsets);
-  QE_TRY(launch_check("k_csv_offsets"));
-  if (t->total[(size_t)c] > 0) {
-    hipLaunchKernelGGL(k_csv_copy_wave, dim3(grid_for(ctx, rows)), dim3(256), 0, ctx->stream, t->data, t->start(c),
-                       t->len(c), t->quoted(c), t->stage(c), offsets, rows, values);
-    QE_TRY(launch_check("k_csv_copy_wave"));
-  }
-  return QE_OK;
+  hipLaunchKernelGGL(k_csv_copy_wave, dim3(grid_for(ctx, rows)), dim3(256), 0, ctx->stream, t->data, t->start(c),
+                     t->meta(c), t->stage(c), t->bstart(c), rows, offsets, values, copy_lds() ? 1 : 0);
+  return launch_check("k_csv_copy_wave");
 }
 
 }  // namespace
@@ -1155,6 +1445,13 @@ int qe_csv_column_bytes(const qe_csv_table* t, int32_t i, int64_t* nbytes) {
   QE_CHECK(t && nbytes, QE_ERR_INVALID_ARG, "null argument");
   QE_CHECK(i >= 0 && i < t->nproj, QE_ERR_INVALID_ARG, "CSV column %d out of range", i);
   *nbytes = t->total[(size_t)i];
+  return QE_OK;
+}
+
+int qe_csv_column_max_len(const qe_csv_table* t, int32_t i, int64_t* nbytes) {
+  QE_CHECK(t && nbytes, QE_ERR_INVALID_ARG, "null argument");
+  QE_CHECK(i >= 0 && i < t->nproj, QE_ERR_INVALID_ARG, "CSV column %d out of range", i);
+  *nbytes = t->maxlen.empty() ? 0 : t->maxlen[(size_t)i];
   return QE_OK;
 }
 

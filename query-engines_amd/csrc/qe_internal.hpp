@@ -202,4 +202,56 @@ __host__ __device__ __forceinline__ uint64_t gen_u64(uint64_t seed, uint64_t col
   return splitmix64(seed ^ (col * PHI64) ^ row);
 }
 
+// Exclusive prefixes of a block's tile of 8 values per thread, 8 consecutive ones per thread
+// (thread t holds elements 8t .. 8t + 7): a serial scan in registers, one wave scan of the thread
+// totals, one across the block's NW waves. Returns the tile's total. `ws`: NW words of LDS. (A
+// layout with a wave scan per row of 64 needed 8 of them and spilled its int64 form.)
+template <typename T, int NW = 16>
+__device__ __forceinline__ T tile_excl(const T (&v)[8], T (&ex)[8], T* ws) {
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  T s = 0;
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    ex[k] = s;
+    s += v[k];
+  }
+  T x = s;
+#pragma unroll
+  for (int off = 1; off < 64; off <<= 1) {
+    const T y = __shfl_up(x, off);
+    if (lane >= off) x += y;
+  }
+  if (lane == 63) ws[wid] = x;
+  __syncthreads();
+  T wp = 0, all = 0;
+#pragma unroll
+  for (int w = 0; w < NW; ++w) {
+    if (w < wid) wp += ws[w];
+    all += ws[w];
+  }
+  __syncthreads();  // ws is rewritten by the next tile
+  const T base = wp + x - s;
+#pragma unroll
+  for (int k = 0; k < 8; ++k) ex[k] += base;
+  return all;
+}
+
+// Element k of this thread in the tile starting at g0.
+__device__ __forceinline__ int64_t tile_elem(int64_t g0, int k) { return g0 + (int64_t)threadIdx.x * 8 + k; }
+
+// This thread's 8 uint32 of a tile: two 16-byte loads when the tile is full (p 32-byte aligned),
+// else element by element with `fill` past n.
+__device__ __forceinline__ void tile_load_u32(const uint32_t* __restrict__ p, int64_t g0, int64_t n, uint32_t (&v)[8],
+                                              uint32_t fill = 0) {
+  const int64_t e0 = g0 + (int64_t)threadIdx.x * 8;
+  if (e0 + 8 <= n) {
+    const uint4 a = *(const uint4*)(p + e0), b = *(const uint4*)(p + e0 + 4);
+    v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w;
+    v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
+  } else {
+#pragma unroll
+    for (int k = 0; k < 8; ++k) v[k] = e0 + k < n ? p[e0 + k] : fill;
+  }
+}
+
 }  // namespace qe

@@ -798,6 +798,56 @@ __global__ void k_dict_decode_copy(const void* __restrict__ codes, const uint8_t
   }
 }
 
+// Wide codes of UTF8 values all known to be at most WIDE_MAX bytes (qe_strdict_encode_packed): the
+// code is the value itself, no dictionary — a streaming pass (offsets, up to 8 key bytes, one code
+// per row), and no control-block read-back: the caller's next kernel can follow on the stream.
+__global__ void __launch_bounds__(256) k_pack_codes(const int32_t* __restrict__ offs, const uint8_t* __restrict__ bytes,
+                                                    const uint8_t* __restrict__ valid, int64_t n,
+                                                    int64_t* __restrict__ codes64) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    const bool live = !valid || ((valid[i >> 3] >> (i & 7)) & 1);
+    int64_t c = 0;
+    if (live) {
+      const int32_t s0 = offs[i];
+      const int len = min(offs[i + 1] - s0, WIDE_MAX);
+      c = wide_pack(load_u64_unaligned(bytes + s0, len), len);
+    }
+    codes64[i] = c;
+  }
+}
+
+// Decode of packed wide codes in one 1024-thread block (small results: a finalize's groups): the
+// lengths, their prefixes (tile by tile) and the bytes, where the general decode runs a length
+// pass, a device scan and a copy pass.
+__global__ void __launch_bounds__(1024) k_unpack_codes_small(const int64_t* __restrict__ codes,
+                                                             const uint8_t* __restrict__ valid, int64_t n,
+                                                             int32_t* __restrict__ out_offs, uint8_t* __restrict__ out) {
+  __shared__ int32_t ws[16];
+  int32_t carry = 0;
+  for (int64_t g0 = 0; g0 < n; g0 += 8192) {
+    int32_t v[8], ex[8];
+    uint64_t x[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const int64_t e = tile_elem(g0, k);
+      const bool live = e < n && (!valid || ((valid[e >> 3] >> (e & 7)) & 1));
+      x[k] = live ? (uint64_t)codes[e] : 0ull;
+      v[k] = (int32_t)((x[k] >> 56) & 7);
+    }
+    const int32_t t = tile_excl(v, ex, ws);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const int64_t e = tile_elem(g0, k);
+      if (e >= n) continue;
+      const int32_t o = carry + ex[k];
+      out_offs[e] = o;
+      for (int b = 0; b < v[k]; ++b) out[o + b] = (uint8_t)(x[k] >> (8 * b));
+    }
+    carry += t;
+  }
+  if (threadIdx.x == 0) out_offs[n] = carry;
+}
+
 }  // namespace
 
 }  // namespace qe
@@ -1282,6 +1332,64 @@ int qe_strdict_decode(qe_strdict* d, const qe_column* codes, qe_column* out) {
 
 int qe_strdict_decode_trusted(qe_strdict* d, const qe_column* codes, qe_column* out) {
   return strdict_decode(d, codes, out, true);
+}
+
+int qe_strdict_encode_packed(qe_ctx* ctx, const qe_column* in, qe_column* codes) {
+  QE_CHECK(ctx && in && codes, QE_ERR_INVALID_ARG, "null argument");
+  QE_TRY(ctx_enter(ctx));
+  QE_CHECK(in->type == QE_TYPE_UTF8 && in->offsets, QE_ERR_UNSUPPORTED, "packed codes take a UTF8 column");
+  QE_CHECK(codes->type == QE_TYPE_INT64, QE_ERR_INVALID_ARG, "packed codes are INT64 (wide codes)");
+  const int64_t n = in->length;
+  QE_CHECK(codes->length >= n && (codes->values || n == 0), QE_ERR_CAPACITY, "codes column too small");
+  QE_CHECK(!in->validity || codes->validity, QE_ERR_INVALID_ARG, "codes validity buffer required");
+  codes->length = n;
+  if (n == 0) return QE_OK;
+  if (in->validity)
+    QE_HIP(hipMemcpyAsync(codes->validity, in->validity, (size_t)div_up((uint64_t)n, 8), hipMemcpyDeviceToDevice,
+                          ctx->stream));
+  const int grid = (int)std::min<int64_t>((int64_t)div_up((uint64_t)n, 256), (int64_t)ctx->num_cus * 8);
+  hipLaunchKernelGGL(k_pack_codes, dim3(grid), dim3(256), 0, ctx->stream, in->offsets, (const uint8_t*)in->values,
+                     in->validity, n, (int64_t*)codes->values);
+  return launch_check("k_pack_codes");
+}
+
+int qe_strdict_decode_packed(qe_ctx* ctx, const qe_column* codes, qe_column* out) {
+  QE_CHECK(ctx && codes && out, QE_ERR_INVALID_ARG, "null argument");
+  QE_TRY(ctx_enter(ctx));
+  QE_CHECK(codes->type == QE_TYPE_INT64, QE_ERR_INVALID_ARG, "packed codes are INT64 (wide codes)");
+  QE_CHECK(out->type == QE_TYPE_UTF8 && out->offsets, QE_ERR_INVALID_ARG, "output must be UTF8 with offsets");
+  const int64_t n = codes->length;
+  QE_CHECK(n < (1ll << 28), QE_ERR_CAPACITY, "packed decode takes fewer than 2^28 rows");
+  QE_CHECK(!codes->validity || out->validity, QE_ERR_INVALID_ARG, "output validity buffer required");
+  QE_CHECK(out->values || n == 0, QE_ERR_CAPACITY, "output values buffer required (7 bytes per row)");
+  out->length = n;
+  if (n == 0) {
+    QE_HIP(hipMemsetAsync(out->offsets, 0, 4, ctx->stream));
+    return QE_OK;
+  }
+  if (n <= 65536) {
+    hipLaunchKernelGGL(k_unpack_codes_small, dim3(1), dim3(1024), 0, ctx->stream, (const int64_t*)codes->values,
+                       codes->validity, n, out->offsets, (uint8_t*)out->values);
+    QE_TRY(launch_check("k_unpack_codes_small"));
+  } else {
+    void* sp;
+    QE_TRY(ctx_scratch(ctx, (size_t)(2 * n + 2) * 8, &sp));
+    int64_t* lens = (int64_t*)sp;
+    int64_t* starts = lens + n;
+    unsigned int* bad = (unsigned int*)(starts + n + 1);
+    const int g = (int)std::min<int64_t>((int64_t)div_up((uint64_t)n + 1, 256), (int64_t)ctx->num_cus * 8);
+    hipLaunchKernelGGL(k_dict_decode_len<true>, dim3(g), dim3(256), 0, ctx->stream, codes->values, codes->validity, n,
+                       nullptr, (int64_t)0, lens, bad);
+    QE_TRY(launch_check("k_dict_decode_len"));
+    QE_TRY(exclusive_scan_i64(ctx, lens, starts, n));
+    hipLaunchKernelGGL(k_dict_decode_copy<true>, dim3(g), dim3(256), 0, ctx->stream, codes->values, codes->validity, n,
+                       nullptr, nullptr, (int64_t)0, nullptr, starts, out->offsets, (uint8_t*)out->values);
+    QE_TRY(launch_check("k_dict_decode_copy"));
+  }
+  if (codes->validity)
+    QE_HIP(hipMemcpyAsync(out->validity, codes->validity, (size_t)div_up((uint64_t)n, 8), hipMemcpyDeviceToDevice,
+                          ctx->stream));
+  return QE_OK;
 }
 
 }  // extern "C"

@@ -185,6 +185,7 @@ class DeviceColumn(ColumnVector):
         self.offsets = offsets
         self.ctx = ctx or Context.get(values.device.index if values is not None else 0)
         self._c = None
+        self.max_len = None  # UTF8: a host-known bound on the values' byte lengths (None: unknown)
 
     # ---- allocation ------------------------------------------------------------------------
     @classmethod

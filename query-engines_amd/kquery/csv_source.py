@@ -88,6 +88,13 @@ def _chunk_bytes() -> int:
     return (int(v) if v else 0) << 20
 
 
+def _view(c: DeviceColumn, s: int, m: int, ctx: Context) -> DeviceColumn:
+    """Rows [s, s + m) of a UTF8 column (its offsets sliced, the values shared)."""
+    v = DeviceColumn(N.TYPE_UTF8, m, c.values, None, c.offsets[s:s + m + 1], ctx)
+    v.max_len = c.max_len  # a bound for every row is one for these rows
+    return v
+
+
 class CsvDataSource(DataSource):
     def __init__(self, filename: str, hasHeaders: bool = True, batchSize: int = 0,  # noqa: N803
                  schema: Optional[Schema] = None, ctx: Optional[Context] = None):
@@ -146,8 +153,7 @@ class CsvDataSource(DataSource):
         step = self.batchSize if self.batchSize and self.batchSize > 0 else max(n, 1)
         for s in range(0, n, step):
             m = min(step, n - s)
-            yield RecordBatch(read_schema, [DeviceColumn(N.TYPE_UTF8, m, c.values, None, c.offsets[s:s + m + 1], ctx)
-                                            for c in cols])
+            yield RecordBatch(read_schema, [_view(c, s, m, ctx) for c in cols])
 
     def _scan_chunked(self, ctx: Context, read_schema: Schema, idx: List[int], size: int,
                       chunk: int) -> Iterator[RecordBatch]:
@@ -235,8 +241,12 @@ class CsvDataSource(DataSource):
                                        torch.empty(rows.value + 1, dtype=torch.int32, device=ctx.torch_device), ctx)
                     cc = col.as_c()
                     N.check(N.lib().qe_csv_column_copy(h, c, N.C.byref(cc)))
+                    ml = N.C.c_int64()
+                    N.check(N.lib().qe_csv_column_max_len(h, c, N.C.byref(ml)))
+                    col.max_len = ml.value  # (short keys then take packed dictionary codes)
                     out.append(col)
-                ctx.synchronize()
+                # no sync: the column builds and the table's release are ordered on the ctx stream,
+                # which is torch's current stream (the tensors' allocator stream)
             finally:
                 N.lib().qe_csv_destroy(h)
         return out, consumed

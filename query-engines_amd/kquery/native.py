@@ -254,6 +254,8 @@ SIGNATURES = [
     ("qe_strdict_decode_bytes", C.c_int, [_P, _COLP, _I64P]),
     ("qe_strdict_decode", C.c_int, [_P, _COLP, _COLP]),
     ("qe_strdict_decode_trusted", C.c_int, [_P, _COLP, _COLP]),
+    ("qe_strdict_encode_packed", C.c_int, [_P, _COLP, _COLP]),
+    ("qe_strdict_decode_packed", C.c_int, [_P, _COLP, _COLP]),
     ("qe_strdict_encode_tuple", C.c_int, [_P, _COLP, C.c_int32, _COLP]),
     ("qe_strdict_decode_tuple", C.c_int, [_P, _COLP, C.c_int32, _COLP]),
     ("qe_hash_partition", C.c_int, [_P, _COLP, C.c_int32, C.c_int32, _P]),
@@ -265,6 +267,7 @@ SIGNATURES = [
     ("qe_csv_consumed", C.c_int, [_P, _I64P]),
     ("qe_csv_column", C.c_int, [_P, C.c_int32, _COLP]),
     ("qe_csv_column_bytes", C.c_int, [_P, C.c_int32, _I64P]),
+    ("qe_csv_column_max_len", C.c_int, [_P, C.c_int32, _I64P]),
     ("qe_csv_column_copy", C.c_int, [_P, C.c_int32, _COLP]),
     ("qe_csv_destroy", C.c_int, [_P]),
     ("qe_csv_record_end", C.c_int, [_P, C.c_int64, C.c_int32, _I64P]),

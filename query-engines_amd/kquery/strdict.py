@@ -17,14 +17,27 @@ class StringDictionary:
         self.ctx = ctx
         self.wide = bool(wide)
         self.code_type = N.TYPE_INT64 if self.wide else N.TYPE_INT32
+        self.expected_distinct = int(expected_distinct)
+        self._handle = None
+        if not self.wide:
+            self._create()
+
+    def _create(self):
         h = N.C.c_void_p()
-        N.check(N.lib().qe_strdict_create(ctx.handle, int(expected_distinct), N.C.byref(h)))
-        self.handle = h
+        N.check(N.lib().qe_strdict_create(self.ctx.handle, self.expected_distinct, N.C.byref(h)))
+        self._handle = h
+        return h
+
+    @property
+    def handle(self):
+        """The device dictionary; a wide one is created on its first long key (short keys are their
+        own codes and never need it)."""
+        return self._handle if self._handle is not None else self._create()
 
     def close(self) -> None:
-        if getattr(self, "handle", None) is not None:
-            N.lib().qe_strdict_destroy(self.handle)
-            self.handle = None
+        if getattr(self, "_handle", None) is not None:
+            N.lib().qe_strdict_destroy(self._handle)
+            self._handle = None
 
     def __del__(self):
         try:
@@ -33,6 +46,8 @@ class StringDictionary:
             pass
 
     def size(self) -> int:
+        if self._handle is None:
+            return 0
         n = N.C.c_int64()
         N.check(N.lib().qe_strdict_size(self.handle, N.C.byref(n)))
         return n.value
@@ -43,7 +58,11 @@ class StringDictionary:
             raise N.IllegalStateException(N.QE_ERR_UNSUPPORTED, f"string dictionary input type {col.type}")
         out = DeviceColumn.empty(self.code_type, col.length, col.nullable, ctx=self.ctx)
         ic, oc = col.as_c(), out.as_c()
-        N.check(N.lib().qe_strdict_encode(self.handle, N.C.byref(ic), N.C.byref(oc)))
+        if self.wide and col.max_len is not None and col.max_len <= 7:
+            # every value is its own code: one stream-ordered kernel, no dictionary, no host round trip
+            N.check(N.lib().qe_strdict_encode_packed(self.ctx.handle, N.C.byref(ic), N.C.byref(oc)))
+        else:
+            N.check(N.lib().qe_strdict_encode(self.handle, N.C.byref(ic), N.C.byref(oc)))
         return out
 
     def decode(self, codes: DeviceColumn, trusted: bool = False) -> DeviceColumn:
@@ -59,7 +78,7 @@ class StringDictionary:
                                codes.validity.clone() if codes.validity is not None else None,
                                torch.empty(n + 1, dtype=torch.int32, device=dev), self.ctx)
             oc = out.as_c()
-            N.check(N.lib().qe_strdict_decode_trusted(self.handle, N.C.byref(cc), N.C.byref(oc)))
+            N.check(N.lib().qe_strdict_decode_packed(self.ctx.handle, N.C.byref(cc), N.C.byref(oc)))
             return out
         nbytes = N.C.c_int64()
         N.check(N.lib().qe_strdict_decode_bytes(self.handle, N.C.byref(cc), N.C.byref(nbytes)))

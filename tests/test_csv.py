@@ -103,7 +103,15 @@ def _gpu_scan(ctx, tmp_path, data, projection=None, has_header=True, batch=0):
     cols = [[] for _ in proj]
     for b in batches:
         for i in range(len(proj)):
-            cols[i] += b.field(i).to_pylist()
+            vals = b.field(i).to_pylist()
+            cols[i] += vals
+            # the scan's longest-value bound (qe_csv_column_max_len): exact for a whole parse, an
+            # upper bound for a batch cut from one
+            longest = max((len(v.encode()) for v in vals), default=0)
+            ml = b.field(i).max_len
+            assert ml is not None and ml >= longest
+            if len(batches) == 1 and not batch:
+                assert ml == longest
     return names, proj, cols, batches
 
 

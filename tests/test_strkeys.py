@@ -112,6 +112,36 @@ def test_strdict_wide_codes_roundtrip(gpu_ctx, n, distinct):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("n", [1, 777, 70_000, 300_001])
+def test_strdict_packed_codes_match_dictionary(gpu_ctx, n):
+    """qe_strdict_encode_packed (a column known to hold values of at most 7 bytes, e.g. from the
+    CSV scan's max length) gives exactly qe_strdict_encode's wide codes, without a dictionary;
+    qe_strdict_decode_packed (one-block path up to 65536 rows, the general one above) restores
+    the strings, nulls included."""
+    from kquery.columnar import DeviceColumn
+    from kquery.strdict import StringDictionary
+
+    rng = random.Random(n)
+    alphabet = "abcxyz0129åé,\"\0 "
+    strings = ["", "a", "\0", "abcdefg", "åäö", "1234567"][: n] + [
+        None if rng.random() < 0.05 else "".join(rng.choice(alphabet) for _ in range(rng.randint(0, 3)))
+        for _ in range(max(0, n - 6))]
+    strings = [s if s is None or len(s.encode()) <= 7 else s[:2] for s in strings]
+    col = DeviceColumn.from_strings(strings, ctx=gpu_ctx)
+    ref = StringDictionary(gpu_ctx, 16, wide=True)
+    want = ref.encode(col)  # max_len unknown: the dictionary kernel
+    col.max_len = 7
+    d = StringDictionary(gpu_ctx, 16, wide=True)
+    got = d.encode(col)
+    assert d._handle is None  # no device dictionary was needed
+    gv, wv = got.valid_mask(), want.valid_mask()
+    assert gv.tolist() == wv.tolist() == [s is not None for s in strings]
+    assert (got.to_numpy()[gv] == want.to_numpy()[wv]).all()
+    assert d.decode(got, trusted=True).to_pylist() == strings
+    assert ref.decode(want).to_pylist() == strings
+
+
+@pytest.mark.gpu
 def test_group_by_lone_utf8_key_wide_codes(gpu_ctx):
     """A lone UTF-8 group key takes wide codes: short and long keys, nulls and empty strings
     group by content against the oracle's HashAggregateExec loop."""
