@@ -161,19 +161,21 @@ __device__ __forceinline__ uint32_t terms16(const Lane16& v, uint32_t next, int6
   return m;
 }
 
-// EMIT = false: count terminators per segment; true: write their positions.
-template <bool EMIT>
+// Terminator positions of every segment (the line-end list), given the quote state at each
+// segment's start and its first line's index. HASQ / HASCR: the file holds a '"' / a '\r' at all
+// (k_csv_count2 reports both); without them a step is only the '\n' compare (the byte passes are
+// VALU-bound: tripdata, no quotes and no '\r', 160 -> ~110 VALU instructions per wave step).
+template <bool HASQ, bool HASCR>
 __global__ void __launch_bounds__(256) k_csv_terms(const uint8_t* __restrict__ data, int64_t nbytes, int64_t nseg,
-                                                   const int64_t* __restrict__ seg_qstart, int64_t* __restrict__ seg_t,
+                                                   const int64_t* __restrict__ seg_qstart,
                                                    const int64_t* __restrict__ seg_tstart, int64_t* __restrict__ ends) {
   const int lane = threadIdx.x & 63;
   const int64_t seg = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
   if (seg >= nseg) return;
   const int64_t base = seg * SEG;
   const uint64_t below = (1ull << lane) - 1;
-  uint32_t carry = (uint32_t)(seg_qstart[seg] & 1);
-  int64_t out = EMIT ? seg_tstart[seg] : 0;
-  int64_t count = 0;
+  uint32_t carry = HASQ ? (uint32_t)(seg_qstart[seg] & 1) : 0u;
+  int64_t out = seg_tstart[seg];
   Lane16 vq[4];
   for (int step = 0; step < SEG / 1024; ++step) {
     const int64_t row0 = base + step * 1024;
@@ -193,26 +195,33 @@ __global__ void __launch_bounds__(256) k_csv_terms(const uint8_t* __restrict__ d
       case 2: v = vq[2]; break;
       default: v = vq[3]; break;
     }
-    const bool mq = has_byte(v, '"');
-    const uint32_t qodd = mq ? (uint32_t)(quotes16(v) & 1) : 0u;
-    const uint64_t par = __ballot(qodd);
-    const uint32_t inq0 = carry ^ ((uint32_t)__popcll(par & below) & 1u);
-    uint32_t inq1;  // (the carry advances from the ballot; the state after the 16 bytes is unused here)
-    // byte after this lane's 16: the next lane's first byte; lane 63 reads it (rare)
-    uint32_t next = (uint32_t)__shfl_down((int)(v.w[0] & 0xFFu), 1);
-    // lane 63: only a trailing '\r' needs the next byte (a load here on every step would put a
-    // full memory round trip on every step's critical path)
-    if (lane == 63) next = (v.byte(15) == '\r' && pos + 16 < nbytes) ? data[pos + 16] : 0u;
+    bool mq = false;
+    uint32_t inq0 = 0;
+    uint64_t par = 0;
+    if (HASQ) {
+      mq = has_byte(v, '"');
+      const uint32_t qodd = mq ? (uint32_t)(quotes16(v) & 1) : 0u;
+      par = __ballot(qodd);
+      inq0 = carry ^ ((uint32_t)__popcll(par & below) & 1u);
+    }
+    // byte after this lane's 16, for a '\r' there: the next lane's first byte (the shuffle runs on
+    // the whole wave, before any lane branches off); lane 63 reads it (rare)
+    uint32_t next = 0;
+    if (HASCR) {
+      next = (uint32_t)__shfl_down((int)(v.w[0] & 0xFFu), 1);
+      if (lane == 63) next = (v.byte(15) == '\r' && pos + 16 < nbytes) ? data[pos + 16] : 0u;
+    }
     // no quote, no '\r', a full chunk: the '\n' words directly (outside quotes) or nothing
-    const bool plain = !mq && pos + 16 <= nbytes && !has_byte(v, '\r');
+    const bool plain = !mq && pos + 16 <= nbytes && (!HASCR || !has_byte(v, '\r'));
     uint32_t h[4] = {0, 0, 0, 0};
     uint32_t m = 0;
     if (plain) {
       if (!inq0) nl_words(v, h);
     } else {
+      uint32_t inq1;  // (the state after the 16 bytes is unused here: the carry follows the ballot)
       m = terms16(v, next, nbytes, pos, inq0, &inq1, mq);
     }
-    carry ^= (uint32_t)__popcll(par) & 1u;
+    if (HASQ) carry ^= (uint32_t)__popcll(par) & 1u;
     const int c = plain ? __popc(h[0]) + __popc(h[1]) + __popc(h[2]) + __popc(h[3]) : __popc(m);  // 0..16
     // wave exclusive prefix and total of c from its 5 bit-planes (ballot + popcount, no LDS)
     int excl = 0, total = 0;
@@ -222,30 +231,26 @@ __global__ void __launch_bounds__(256) k_csv_terms(const uint8_t* __restrict__ d
       excl += __popcll(plane & below) << b;
       total += __popcll(plane) << b;
     }
-    if (EMIT) {
-      int64_t o = out + excl;
-      if (plain) {
+    int64_t o = out + excl;
+    if (plain) {
 #pragma unroll
-        for (int i = 0; i < 2; ++i) {  // two 64-bit halves: fewer divergent loops than four words
-          uint64_t hh = h[2 * i] | ((uint64_t)h[2 * i + 1] << 32);
-          while (hh) {
-            ends[o++] = pos + 8 * i + (__builtin_ctzll(hh) >> 3);
-            hh &= hh - 1;
-          }
-        }
-      } else {
-        uint32_t mm = m;
-        while (mm) {
-          const int k = __builtin_ctz(mm);
-          mm &= mm - 1;
-          ends[o++] = pos + k;
+      for (int i = 0; i < 2; ++i) {  // two 64-bit halves: fewer divergent loops than four words
+        uint64_t hh = h[2 * i] | ((uint64_t)h[2 * i + 1] << 32);
+        while (hh) {
+          ends[o++] = pos + 8 * i + (__builtin_ctzll(hh) >> 3);
+          hh &= hh - 1;
         }
       }
-      out += total;
+    } else {
+      uint32_t mm = m;
+      while (mm) {
+        const int k = __builtin_ctz(mm);
+        mm &= mm - 1;
+        ends[o++] = pos + k;
+      }
     }
-    count += total;
+    out += total;
   }
-  if (!EMIT && lane == 0) seg_t[seg] = count;
 }
 
 // One read of the file for the counting pass: per segment its quote count and its terminator
@@ -255,7 +260,7 @@ __global__ void __launch_bounds__(256) k_csv_terms(const uint8_t* __restrict__ d
 // terminator pass that needed the scanned quote counts (two reads of the file).
 __global__ void __launch_bounds__(256) k_csv_count2(const uint8_t* __restrict__ data, int64_t nbytes, int64_t nseg,
                                                     int64_t* __restrict__ seg_q, int64_t* __restrict__ seg_t0,
-                                                    int64_t* __restrict__ seg_t1) {
+                                                    int64_t* __restrict__ seg_t1, uint8_t* __restrict__ seg_cr) {
   const int lane = threadIdx.x & 63;
   const int64_t seg = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
   if (seg >= nseg) return;
@@ -263,6 +268,7 @@ __global__ void __launch_bounds__(256) k_csv_count2(const uint8_t* __restrict__ 
   const uint64_t below = (1ull << lane) - 1;
   uint32_t rel = 0;  // parity of this segment's quotes before the current step
   int q = 0, c0 = 0, c1 = 0;
+  bool anycr = false;  // a '\r' in the segment (the position pass then needs its '\r' handling)
   int64_t l0 = -1, l1 = -1;  // last terminator position under each hypothesis
   Lane16 vq[4];
   for (int step = 0; step < SEG / 1024; ++step) {
@@ -283,15 +289,27 @@ __global__ void __launch_bounds__(256) k_csv_count2(const uint8_t* __restrict__ 
       case 2: v = vq[2]; break;
       default: v = vq[3]; break;
     }
+    // (wave-uniform tests first: a step without any '"' or '\r' skips the parity ballot and the
+    // next-byte shuffle — the pass is VALU-bound)
     const bool hasq = has_byte(v, '"');
-    const int nq = hasq ? quotes16(v) : 0;
-    q += nq;
-    const uint64_t par = __ballot(nq & 1);
-    const uint32_t x = rel ^ ((uint32_t)__popcll(par & below) & 1u);  // state at this lane's first byte if the segment starts outside quotes
-    uint32_t next = (uint32_t)__shfl_down((int)(v.w[0] & 0xFFu), 1);
-    if (lane == 63) next = (v.byte(15) == '\r' && pos + 16 < nbytes) ? data[pos + 16] : 0u;
+    int nq = 0;
+    uint32_t x = rel;  // state at this lane's first byte if the segment starts outside quotes
+    uint64_t par = 0;
+    if (__ballot(hasq)) {
+      nq = hasq ? quotes16(v) : 0;
+      q += nq;
+      par = __ballot(nq & 1);
+      x = rel ^ ((uint32_t)__popcll(par & below) & 1u);
+    }
+    const bool cr = has_byte(v, '\r');
+    anycr |= cr;
+    uint32_t next = 0;
+    if (__ballot(cr)) {
+      next = (uint32_t)__shfl_down((int)(v.w[0] & 0xFFu), 1);
+      if (lane == 63) next = (v.byte(15) == '\r' && pos + 16 < nbytes) ? data[pos + 16] : 0u;
+    }
     uint32_t dummy;
-    if (nq == 0 && pos + 16 <= nbytes && !has_byte(v, '\r')) {  // '\n' terminators only: straight from the words
+    if (nq == 0 && pos + 16 <= nbytes && !cr) {  // '\n' terminators only: straight from the words
       uint32_t h[4];
       nl_words(v, h);
       const int c = __popc(h[0]) + __popc(h[1]) + __popc(h[2]) + __popc(h[3]);
@@ -335,7 +353,9 @@ __global__ void __launch_bounds__(256) k_csv_count2(const uint8_t* __restrict__ 
     l0 = max(l0, (int64_t)__shfl_xor(l0, d));
     l1 = max(l1, (int64_t)__shfl_xor(l1, d));
   }
+  const bool segcr = __ballot(anycr) != 0;
   if (lane == 0) {
+    seg_cr[seg] = segcr ? 1 : 0;
     seg_q[seg] = q;
     seg_t0[seg] = c0;
     seg_t1[seg] = c1;
@@ -356,6 +376,7 @@ __global__ void __launch_bounds__(256) k_csv_count2(const uint8_t* __restrict__ 
 constexpr int SP_THREADS = 256, SP_TILE = SP_THREADS * 8;
 struct SegAgg {
   int64_t q, t[2], last[2];  // [P]: the block starts inside quotes (P = 1) or not
+  int64_t flags;             // bit 0: a '"' in the block; bit 1: a '\r'
 };
 
 __device__ __forceinline__ void seg_load(const int64_t* __restrict__ seg_q, const int64_t* __restrict__ t0,
@@ -376,11 +397,20 @@ __device__ __forceinline__ void seg_load(const int64_t* __restrict__ seg_q, cons
 __global__ void __launch_bounds__(SP_THREADS) k_csv_seg_reduce(const int64_t* __restrict__ seg_q,
                                                                const int64_t* __restrict__ t0,
                                                                const int64_t* __restrict__ t1, int64_t nseg,
+                                                               const uint8_t* __restrict__ seg_cr,
                                                                SegAgg* __restrict__ agg) {
   __shared__ int64_t ws[SP_THREADS / 64];
   __shared__ int64_t red[SP_THREADS / 64][5];
   int64_t q[8], a[8], b[8], la[8], lb[8], ex[8];
-  seg_load(seg_q, t0, t1, nseg, (int64_t)blockIdx.x * SP_TILE, q, a, b, la, lb);
+  const int64_t g0 = (int64_t)blockIdx.x * SP_TILE;
+  seg_load(seg_q, t0, t1, nseg, g0, q, a, b, la, lb);
+  int cr = 0;
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    const int64_t e = tile_elem(g0, k);
+    if (e < nseg) cr |= seg_cr[e];
+  }
+  const bool anycr = __syncthreads_or(cr) != 0;
   const int64_t qt = tile_excl<int64_t, SP_THREADS / 64>(q, ex, ws);
   int64_t s0 = 0, s1 = 0, m0 = -1, m1 = -1;
 #pragma unroll
@@ -406,7 +436,7 @@ __global__ void __launch_bounds__(SP_THREADS) k_csv_seg_reduce(const int64_t* __
   }
   __syncthreads();
   if (threadIdx.x == 0) {
-    SegAgg g{qt, {0, 0}, {-1, -1}};
+    SegAgg g{qt, {0, 0}, {-1, -1}, (qt > 0 ? 1 : 0) | (anycr ? 2 : 0)};
     for (int w = 0; w < SP_THREADS / 64; ++w) {
       g.t[0] += red[w][0];
       g.t[1] += red[w][1];
@@ -427,13 +457,14 @@ __global__ void __launch_bounds__(SP_THREADS) k_csv_seg_apply(const int64_t* __r
   __shared__ int64_t base[2];
   const int64_t blk = blockIdx.x;
   if (threadIdx.x == 0) {  // this block's start state and prefixes from the blocks before it
-    int64_t qp = 0, tp = 0, last = -1;
+    int64_t qp = 0, tp = 0, last = -1, fl = 0;
     for (int64_t j = 0; j < blk; ++j) {
       const SegAgg g = agg[j];
       const int P = (int)(qp & 1);
       tp += g.t[P];
       last = max(last, g.last[P]);
       qp += g.q;
+      fl |= g.flags;
     }
     base[0] = qp;
     base[1] = tp;
@@ -445,6 +476,7 @@ __global__ void __launch_bounds__(SP_THREADS) k_csv_seg_apply(const int64_t* __r
       seg_ts[nseg] = tall;
       __hip_atomic_store(&host[0], tall, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
       __hip_atomic_store(&host[1], max(last, g.last[P]), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      __hip_atomic_store(&host[2], fl | g.flags, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     }
   }
   __syncthreads();
@@ -505,6 +537,7 @@ struct FieldArgs {
   uint64_t low_mask;                  // bit f: field f < 64 is projected (skips the table lookup)
   int16_t pf[CSV_MAX_FIELDS];         // the projected field indices, ascending
   int32_t npf;
+  int32_t noq;                        // 1: the bytes hold no '"' at all (the line walk skips its quote test)
 };
 
 // Bytes of the file by global position: straight from HBM, or from a wave's LDS copy of a block.
@@ -680,7 +713,7 @@ __device__ bool walk_record_unquoted(const D& data, int64_t s, int64_t e, const 
     const uint32_t lo = (uint32_t)(s > a ? s - a : 0);
     const uint32_t hi = (uint32_t)(e - a < 16 ? e - a : 16);
     const uint32_t in = (hi >= 32 ? 0xFFFFu : ((1u << hi) - 1u)) & ~((1u << lo) - 1u);
-    if (has_byte(v, '"') && (eq16(v, '"') & in)) return false;
+    if (!A.noq && has_byte(v, '"') && (eq16(v, '"') & in)) return false;
     const uint32_t d = eq16(v, (uint32_t)A.delim) & in;
     const int n = __popc(d);
     while (t < A.npf && A.pf[t] < f + n) {  // projected field A.pf[t] ends in this chunk
@@ -714,6 +747,7 @@ __device__ __forceinline__ void stage_args(FieldArgs& S, const FieldArgs& A) {
     S.delim = A.delim;
     S.low_mask = A.low_mask;
     S.npf = A.npf;
+    S.noq = A.noq;
   }
   __syncthreads();
 }
@@ -1236,37 +1270,43 @@ int csv_parse(qe_ctx* ctx, const uint8_t* data, int64_t nbytes, const qe_csv_opt
     if (A.slot[f] >= 0) A.pf[A.npf++] = (int16_t)f;
   // ---- record terminators
   const int64_t nseg = (int64_t)div_up((uint64_t)(nbytes > 0 ? nbytes : 1), SEG);
+  const int64_t spb = (int64_t)div_up((uint64_t)nseg, SP_TILE);
   void* p;
-  QE_TRY(ctx_workspace(ctx, 0, (size_t)(8 * nseg + 6) * 8 + (size_t)div_up((uint64_t)nseg, SP_TILE) * sizeof(SegAgg), &p));
+  QE_TRY(ctx_workspace(ctx, 0, (size_t)(8 * nseg + 6) * 8 + (size_t)div_up((uint64_t)nseg, SP_TILE) * sizeof(SegAgg) + (size_t)nseg,
+                       &p));
   int64_t* seg_q = (int64_t*)p;
   int64_t* seg_qs = seg_q + nseg;
   int64_t* seg_ts = seg_qs + nseg + 1;
   int64_t* seg_t0 = seg_ts + nseg + 1;  // then seg_t1 [nseg], seg_l0 [nseg], seg_l1 [nseg]
   int64_t* seg_t1 = seg_t0 + nseg;
   const int wgrid = (int)div_up((uint64_t)nseg, 4);  // 4 waves per 256-thread block
+  SegAgg* agg = (SegAgg*)(seg_t1 + 3 * nseg);  // after seg_t1 / seg_l0 / seg_l1
+  uint8_t* seg_cr = (uint8_t*)(agg + spb);
   if (nbytes > 0) {
-    hipLaunchKernelGGL(k_csv_count2, dim3(wgrid), dim3(256), 0, ctx->stream, data, nbytes, nseg, seg_q, seg_t0, seg_t1);
+    hipLaunchKernelGGL(k_csv_count2, dim3(wgrid), dim3(256), 0, ctx->stream, data, nbytes, nseg, seg_q, seg_t0, seg_t1,
+                       seg_cr);
     QE_TRY(launch_check("k_csv_count2"));
   } else {
     QE_HIP(hipMemsetAsync(seg_q, 0, 8, ctx->stream));
     QE_HIP(hipMemsetAsync(seg_t0, 0, 16, ctx->stream));
     QE_HIP(hipMemsetAsync(seg_t0 + 2, 0xFF, 16, ctx->stream));  // no terminator (nseg == 1)
+    QE_HIP(hipMemsetAsync(seg_cr, 0, 1, ctx->stream));
   }
   // the kernels below leave their few host-bound words in fine-grained pinned memory: one sync, no
   // read-back copies
   void* hp;
-  QE_TRY(ctx_pinned_coherent(ctx, (size_t)(2 * nproj + 2) * 8, &hp));
+  QE_TRY(ctx_pinned_coherent(ctx, (size_t)(2 * nproj + 3) * 8, &hp));
   volatile int64_t* host = (volatile int64_t*)hp;
-  const int64_t spb = (int64_t)div_up((uint64_t)nseg, SP_TILE);
-  SegAgg* agg = (SegAgg*)(seg_t1 + 3 * nseg);  // after seg_t1 / seg_l0 / seg_l1
   hipLaunchKernelGGL(k_csv_seg_reduce, dim3((unsigned)spb), dim3(SP_THREADS), 0, ctx->stream, seg_q, seg_t0, seg_t1, nseg,
-                     agg);
+                     seg_cr, agg);
   QE_TRY(launch_check("k_csv_seg_reduce"));
   hipLaunchKernelGGL(k_csv_seg_apply, dim3((unsigned)spb), dim3(SP_THREADS), 0, ctx->stream, seg_q, seg_t0, seg_t1, nseg,
                      agg, spb, seg_qs, seg_ts, (int64_t*)hp);
   QE_TRY(launch_check("k_csv_seg_apply"));
   QE_TRY(ctx_sync(ctx));
   const int64_t nterm = host[0], last_end = host[1];
+  const bool file_q = (host[2] & 1) != 0, file_cr = (host[2] & 2) != 0;  // any '"' / '\r' in the bytes
+  A.noq = file_q ? 0 : 1;
   QE_TRY(ctx_workspace(ctx, 1, (size_t)(3 * nterm + 7) * 8, &p));
   int64_t* ends = (int64_t*)p;
   int64_t* keep = ends + nterm + 2;
@@ -1314,8 +1354,9 @@ int csv_parse(qe_ctx* ctx, const uint8_t* data, int64_t nbytes, const qe_csv_opt
     // a line that may not be a record: the line-end list and the kept-line path below decide
   }
   if (nterm > 0) {
-    hipLaunchKernelGGL(k_csv_terms<true>, dim3(wgrid), dim3(256), 0, ctx->stream, data, nbytes, nseg, seg_qs, nullptr,
-                       seg_ts, ends);
+    auto kt = file_q ? (file_cr ? k_csv_terms<true, true> : k_csv_terms<true, false>)
+                     : (file_cr ? k_csv_terms<false, true> : k_csv_terms<false, false>);
+    hipLaunchKernelGGL(kt, dim3(wgrid), dim3(256), 0, ctx->stream, data, nbytes, nseg, seg_qs, seg_ts, ends);
     QE_TRY(launch_check("k_csv_terms<emit>"));
   }
   if (nlines > nterm) {
