@@ -629,7 +629,7 @@ __device__ void record_field(const D& d, const FieldArgs& A, int f, int64_t s, i
   trim(d, s, e);
   uint8_t q = 0;
   int64_t len = e - s;
-  if (len >= 2 && d[s] == '"' && d[e - 1] == '"') {
+  if (!A.noq && len >= 2 && d[s] == '"' && d[e - 1] == '"') {
     ++s;
     --e;
     // unescaped length: every "" pair counts once; then trim again (String.trim on the value)
@@ -705,7 +705,6 @@ __device__ __forceinline__ int nth_bit16(uint32_t d, int k) {
 // line's field count (the line pass is VALU-bound).
 template <typename D>
 __device__ bool walk_record_unquoted(const D& data, int64_t s, int64_t e, const FieldArgs& A, int32_t nproj, int64_t r) {
-  for (int c = 0; c < nproj; ++c) A.meta[c][r] = 0;  // fields the line does not reach read as "" (K:263)
   int f = 0, t = 0;
   int64_t fs = s;
   for (int64_t a = s & ~(int64_t)15; a < e && t < A.npf; a += 16) {
@@ -727,7 +726,11 @@ __device__ bool walk_record_unquoted(const D& data, int64_t s, int64_t e, const 
       f += n;
     }
   }
-  if (t < A.npf && A.pf[t] == f) record_field(data, A, f, fs, e, r);  // the line's last field
+  if (t < A.npf && A.pf[t] == f) {  // the line's last field
+    record_field(data, A, f, fs, e, r);
+    ++t;
+  }
+  for (; t < A.npf; ++t) A.meta[A.slot[A.pf[t]]][r] = 0;  // fields the line does not reach read as "" (K:263)
   return true;
 }
 
