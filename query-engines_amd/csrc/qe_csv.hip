@@ -1240,6 +1240,9 @@ int column_sizes(qe_csv_table* t, int64_t rows, const unsigned long long* nskip,
     QE_TRY(launch_check("k_csv_len_apply"));
   }
   QE_TRY(ctx_sync(ctx));
+  // Lines that were not records left their rows' lengths unwritten: the sizes are meaningless and
+  // the caller reruns the kept-line path (which rewrites every row) before it asks again.
+  if (nskip && host[0] != 0) return QE_OK;
   for (int c = 0; c < nproj; ++c) {
     t->total[(size_t)c] = host[1 + c];
     t->maxlen[(size_t)c] = host[1 + nproj + c];
