@@ -90,14 +90,27 @@ __device__ __forceinline__ void gpart_wave_reduce(GPart& p) {
     o.first_nan = (uint64_t)shfl_x((int64_t)p.first_nan, m);
     o.first_negz = (uint64_t)shfl_x((int64_t)p.first_negz, m);
     o.first_posz = (uint64_t)shfl_x((int64_t)p.first_posz, m);
-    // fixed pairing order: lower lane is the left operand
-    if (threadIdx.x & m) {
-      GPart t = o;
-      gpart_merge(t, p);
-      p = t;
-    } else {
-      gpart_merge(p, o);
-    }
+    // fixed pairing order: the lower lane's partial is the left operand (operands selected, one
+    // merge: a branch on the lane bit ran both merges in every wave)
+    const bool hi = (threadIdx.x & m) != 0;
+    GPart l, r;
+    l.rows = hi ? o.rows : p.rows;           r.rows = hi ? p.rows : o.rows;
+    l.count = hi ? o.count : p.count;        r.count = hi ? p.count : o.count;
+    l.isum = hi ? o.isum : p.isum;           r.isum = hi ? p.isum : o.isum;
+    l.imin = hi ? o.imin : p.imin;           r.imin = hi ? p.imin : o.imin;
+    l.imax = hi ? o.imax : p.imax;           r.imax = hi ? p.imax : o.imax;
+    l.s = hi ? o.s : p.s;                    r.s = hi ? p.s : o.s;
+    l.c = hi ? o.c : p.c;                    r.c = hi ? p.c : o.c;
+    l.a = hi ? o.a : p.a;                    r.a = hi ? p.a : o.a;
+    l.ninf = hi ? o.ninf : p.ninf;           r.ninf = hi ? p.ninf : o.ninf;
+    l.kmin = hi ? o.kmin : p.kmin;           r.kmin = hi ? p.kmin : o.kmin;
+    l.kmax = hi ? o.kmax : p.kmax;           r.kmax = hi ? p.kmax : o.kmax;
+    l.first_nn = hi ? o.first_nn : p.first_nn;       r.first_nn = hi ? p.first_nn : o.first_nn;
+    l.first_nan = hi ? o.first_nan : p.first_nan;    r.first_nan = hi ? p.first_nan : o.first_nan;
+    l.first_negz = hi ? o.first_negz : p.first_negz; r.first_negz = hi ? p.first_negz : o.first_negz;
+    l.first_posz = hi ? o.first_posz : p.first_posz; r.first_posz = hi ? p.first_posz : o.first_posz;
+    gpart_merge(l, r);
+    p = l;
   }
 }
 
@@ -180,58 +193,12 @@ __global__ void __launch_bounds__(256) k_agg_global(const int64_t* __restrict__ 
   }
 }
 
-// Publishes a workgroup's partial (partials[blockIdx.x]); the last workgroup of the launch to
-// finish (the one whose ticket on the monotonic counter `done` is ticket0 + gridDim.x - 1) folds
-// all partials in index order into partials[gridDim.x], and into host_out / host_flag like
-// k_agg_global_final. The fold order depends only on the indices: bit-reproducible whichever
-// workgroup ends last. Saves the second launch and its serial fold (7.9 us at 2048 partials).
-template <int NW>
-__device__ __forceinline__ void publish_and_fold(GPart p, GPart* __restrict__ partials, unsigned long long* done,
-                                                 unsigned long long ticket0, GPart* __restrict__ host_out,
-                                                 unsigned long long* __restrict__ host_flag) {
-  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-  gpart_wave_reduce(p);
-  __shared__ GPart wp[NW];
-  __shared__ int last;
-  if (lane == 0) wp[wid] = p;
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    GPart b = wp[0];
-    for (int w = 1; w < NW; ++w) gpart_merge(b, wp[w]);
-    partials[blockIdx.x] = b;
-    __threadfence();  // release the partial before the ticket
-    last = atomicAdd(done, 1ull) == ticket0 + gridDim.x - 1;
-  }
-  __syncthreads();
-  if (!last) return;
-  __threadfence();  // acquire: every other workgroup's partial is visible
-  GPart q;
-  gpart_init(q);
-  if (wid < 4) {
-    for (unsigned i = threadIdx.x; i < gridDim.x; i += 256) gpart_merge(q, partials[i]);
-    gpart_wave_reduce(q);
-    if (lane == 0) wp[wid] = q;
-  }
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    GPart b = wp[0];
-    for (int w = 1; w < 4; ++w) gpart_merge(b, wp[w]);
-    partials[gridDim.x] = b;
-    if (host_out) *host_out = b;
-    if (host_flag) __hip_atomic_store(host_flag, 1ull, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
-  }
-}
-
 // Dense fp64 column (no validity, no mask): the C3 shape. Eight independent compensated sums per
 // thread (one per row slot) break the fp64 add dependency chain that otherwise bounds the
 // kernel; min/max run on the doubles with fmin/fmax (which ignore NaN: NaN rows are recorded in a
 // rare branch), first-row indices are set on first sight (each thread visits rows in order).
-// One 1024-thread workgroup per CU (16 waves, each step a wave reads 4 KiB: the best stream-read
-// shape of one column), the partials folded by the last workgroup (publish_and_fold).
-__global__ void __launch_bounds__(1024) k_agg_global_f64_dense(const int64_t* __restrict__ vals, int64_t n,
-                                                               GPart* __restrict__ partials, unsigned long long* done,
-                                                               unsigned long long ticket0, GPart* __restrict__ host_out,
-                                                               unsigned long long* __restrict__ host_flag) {
+__global__ void __launch_bounds__(256) k_agg_global_f64_dense(const int64_t* __restrict__ vals, int64_t n,
+                                                              GPart* __restrict__ partials) {
   const int lane = threadIdx.x & 63;
   const int64_t wave = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 6;
   const int64_t nwaves = ((int64_t)gridDim.x * blockDim.x) >> 6;
@@ -311,7 +278,15 @@ __global__ void __launch_bounds__(1024) k_agg_global_f64_dense(const int64_t* __
     p.kmin = INT64_MAX;  // only NaNs seen by this thread
     p.kmax = INT64_MIN;
   }
-  publish_and_fold<16>(p, partials, done, ticket0, host_out, host_flag);
+  gpart_wave_reduce(p);
+  __shared__ GPart wp[4];
+  if (lane == 0) wp[threadIdx.x >> 6] = p;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    GPart b = wp[0];
+    for (int w = 1; w < 4; ++w) gpart_merge(b, wp[w]);
+    partials[blockIdx.x] = b;
+  }
 }
 
 static_assert(sizeof(GPart) <= QE_GLOBAL_PARTIAL_BYTES, "partial record size");
@@ -372,10 +347,18 @@ __global__ void __launch_bounds__(256) k_agg_global_fx(const int64_t* __restrict
 __global__ void __launch_bounds__(256) k_agg_global_final(GPart* __restrict__ partials, int nparts,
                                                           GPart* __restrict__ host_out,
                                                           unsigned long long* __restrict__ host_flag) {
-  // Fixed-order reduction: thread t folds partials t, t+256, ...; then a fixed wave/block tree.
+  // Fixed-order reduction: thread t folds partials t, t+256, ... (two loads in flight per round);
+  // then a fixed wave / block tree. (1024 threads took 15 us: sixteen waves' shuffle trees on one CU.)
   GPart p;
   gpart_init(p);
-  for (int i = threadIdx.x; i < nparts; i += 256) gpart_merge(p, partials[i]);
+  for (int i = threadIdx.x; i < nparts; i += 512) {
+    const GPart a = partials[i];
+    GPart b;
+    const bool two = i + 256 < nparts;
+    if (two) b = partials[i + 256];
+    gpart_merge(p, a);
+    if (two) gpart_merge(p, b);
+  }
   gpart_wave_reduce(p);
   __shared__ GPart wp[4];
   if ((threadIdx.x & 63) == 0) wp[threadIdx.x >> 6] = p;
@@ -432,7 +415,16 @@ static int agg_global_partial(qe_ctx* ctx, const qe_column* col, const qe_column
   const bool f64 = col->type == QE_TYPE_FLOAT64;
   const int64_t waves_needed = (int64_t)div_up((uint64_t)(n > 0 ? n : 1), 512);
   int64_t blocks = (int64_t)div_up((uint64_t)waves_needed, 4);
-  const int64_t cap = (int64_t)ctx->num_cus * 8;
+  // dense fp64 (C3): QE_AG_PER_CU workgroups per CU (100M rows, one box: 8 -> 0.1427 ms per call,
+  // 4 -> 0.1443, 5 -> 0.1642; a one-launch form whose last workgroup folded the partials behind a
+  // device-scope fence took 0.153-0.229 ms)
+  static const int ag_per_cu = [] {
+    const char* e = getenv("QE_AG_PER_CU");
+    const int v = e && *e ? atoi(e) : 8;
+    return v >= 1 && v <= 16 ? v : 8;
+  }();
+  const bool dense = col->type == QE_TYPE_FLOAT64 && !col->validity && !mask;
+  const int64_t cap = (int64_t)ctx->num_cus * (dense ? ag_per_cu : 8);
   if (blocks > cap) blocks = cap;
   if (blocks < 1) blocks = 1;
   void* s;
@@ -440,24 +432,10 @@ static int agg_global_partial(qe_ctx* ctx, const qe_column* col, const qe_column
   GPart* parts = (GPart*)s;
   const uint8_t* mv = mask ? (const uint8_t*)mask->values : nullptr;
   const uint8_t* ml = mask ? mask->validity : nullptr;
-  if (f64 && !col->validity && !mv) {
-    // one launch: 1024-thread workgroups, at most one per CU, the last one folds the partials
-    const int64_t wg = std::max<int64_t>(1, std::min<int64_t>((int64_t)div_up((uint64_t)waves_needed, 16),
-                                                              (int64_t)ctx->num_cus));
-    if (!ctx->ag_done) {
-      QE_HIP(hipMalloc((void**)&ctx->ag_done, 64));
-      QE_HIP(hipMemsetAsync(ctx->ag_done, 0, 64, ctx->stream));
-      ctx->ag_ticket = 0;
-    }
-    hipLaunchKernelGGL(k_agg_global_f64_dense, dim3((unsigned)wg), dim3(1024), 0, ctx->stream,
-                       (const int64_t*)col->values, n, parts, ctx->ag_done, (unsigned long long)ctx->ag_ticket,
-                       host_out, host_flag);
-    QE_TRY(launch_check("k_agg_global_f64_dense"));
-    ctx->ag_ticket += (uint64_t)wg;
-    *result = parts + wg;
-    return QE_OK;
-  }
-  if (f64)
+  if (f64 && !col->validity && !mv)
+    hipLaunchKernelGGL(k_agg_global_f64_dense, dim3((unsigned)blocks), dim3(256), 0, ctx->stream,
+                       (const int64_t*)col->values, n, parts);
+  else if (f64)
     hipLaunchKernelGGL(k_agg_global<true>, dim3((unsigned)blocks), dim3(256), 0, ctx->stream,
                        (const int64_t*)col->values, col->validity, mv, ml, n, parts);
   else

@@ -2214,6 +2214,11 @@ static int launch_pass(qe_hashagg* h, Plan& P, size_t& lds, hipFunction_t pfn, i
                                          : std::max<int64_t>(ctx->num_cus, h->grid * 512 / fused_block(P.lds_log2));
         jgrid = (int)std::min<int64_t>(std::min<int64_t>((int64_t)ctx->num_cus * bpc, per_state),
                                        (int64_t)div_up((uint64_t)waves, fused_block(P.lds_log2) / 64));
+        static const int64_t max_wg = [] {  // (experiments: cap the fused grid)
+          const char* e = getenv("QE_FUSED_MAX_WG");
+          return e && *e ? (int64_t)atoll(e) : (int64_t)0;
+        }();
+        if (max_wg > 0 && jgrid > max_wg) jgrid = (int)max_wg;
         if (jgrid < 1) jgrid = 1;
         h->jit_note.clear();
         if (P.lds_compact) h->jit_note = "compact LDS table: " + std::to_string(P.lds_compact) + " slots";
@@ -2555,7 +2560,17 @@ static int run_update(qe_hashagg* h, Plan& P) {
       const size_t pbudget = pagg_block() == 1024 ? (size_t)152 * 1024 : HA_LDS_BUDGET;
       while (tl >= 8 && lds_layout_at(h, &Q, tl) > pbudget) --tl;
     }
-    if (cs_env && nsl >= 512 && tl >= 8 && h->expected_groups <= nsl * 3 / 4 + ((int64_t)1 << tl) / 2) {
+    // QE_SPILL_MAXPCT: the spilled groups (expected groups beyond the kept share, 7/8 of the
+    // compact slots) may fill this percentage of the aggregation table (unset: the kept share
+    // counted at 3/4 and half the table)
+    static const int sp_pct = [] {
+      const char* e = getenv("QE_SPILL_MAXPCT");
+      const int v = e && *e ? atoi(e) : 0;
+      return v >= 10 && v <= 90 ? v : 0;
+    }();
+    const int64_t spill_max = sp_pct ? nsl * 7 / 8 + ((int64_t)1 << tl) * sp_pct / 100
+                                     : nsl * 3 / 4 + ((int64_t)1 << tl) / 2;
+    if (cs_env && nsl >= 512 && tl >= 8 && h->expected_groups <= spill_max) {
       T.lds_compact = (qi32)nsl;
       T.mp_n = 2;
       T.mp_pass = 0;

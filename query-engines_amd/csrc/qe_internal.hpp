@@ -32,8 +32,6 @@ struct qe_ctx {
   void* sp_status = nullptr;     // per-tile counts of the register-resident select-project
   size_t sp_status_bytes = 0;
   uint32_t sp_epoch = 0;         // (epoch-tagged, so no memset per call; qe_selproj.hip)
-  unsigned long long* ag_done = nullptr;  // global aggregate: monotonic count of finished workgroups
-  uint64_t ag_ticket = 0;                 // (its value before the next launch; qe_agg_global.hip)
 };
 
 namespace qe {

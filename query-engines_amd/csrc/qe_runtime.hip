@@ -534,7 +534,6 @@ int qe_ctx_destroy(qe_ctx* ctx) {
   if (ctx->scratch) (void)hipFree(ctx->scratch);
   if (ctx->scan_tmp) (void)hipFree(ctx->scan_tmp);
   if (ctx->sp_status) (void)hipFree(ctx->sp_status);
-  if (ctx->ag_done) (void)hipFree(ctx->ag_done);
   for (void* w : ctx->ws)
     if (w) (void)hipFree(w);
   if (ctx->pinned) (void)hipHostFree(ctx->pinned);
