@@ -364,6 +364,131 @@ __global__ void __launch_bounds__(256) k_csv_count2(const uint8_t* __restrict__ 
   }
 }
 
+// One pass for the line-end list of a file without '"' or '\r' (speculative: the host does not
+// know that yet). Replaces k_csv_count2 -> k_csv_seg_reduce / _apply -> k_csv_terms, whose two byte
+// passes each spent their VALU on the same '\n' compare. A wave takes the next segment by ticket,
+// computes the '\n' words of its 16 KiB once (kept in registers, 64 VGPRs), publishes its count and
+// last '\n' (decoupled look-back over the segments before it, which hold lower tickets and so are
+// running or done: no wave waits for one that may not start), then writes the positions from the
+// same words. Any '"' or '\r' in the file (host[2] bit 0), a list longer than `cap` (bit 1) or a
+// look-back that does not finish (bit 2) makes the host rerun the general passes. nbytes < 2^31:
+// a status word packs flag (2 bits) | count (31) | last '\n' + 1 (31).
+constexpr uint64_t LB_AGG = 1ull << 62, LB_INC = 2ull << 62, LB_M31 = (1ull << 31) - 1;
+
+// Any '"' or '\r' among the 16 bytes (has-zero-byte tests; bytes past the end read as 0).
+__device__ __forceinline__ bool quote_or_cr(const Lane16& v) {
+  uint32_t any = 0;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const uint32_t x = v.w[i] ^ 0x22222222u, y = v.w[i] ^ 0x0D0D0D0Du;
+    any |= ((x - 0x01010101u) & ~x) | ((y - 0x01010101u) & ~y);
+  }
+  return (any & 0x80808080u) != 0;
+}
+
+__global__ void __launch_bounds__(256) k_csv_ends1(const uint8_t* __restrict__ data, int64_t nbytes, int64_t nseg,
+                                                   unsigned int* __restrict__ ticket, uint64_t* __restrict__ status,
+                                                   int64_t* __restrict__ ends, int64_t cap, int64_t* host) {
+  const int lane = threadIdx.x & 63;
+  int64_t seg = 0;
+  if (lane == 0) seg = (int64_t)atomicAdd(ticket, 1u);
+  seg = __shfl(seg, 0);
+  if (seg >= nseg) return;
+  const int64_t base = seg * SEG;
+  const uint64_t below = (1ull << lane) - 1;
+  uint32_t h[SEG / 1024][4];
+  int cnt = 0;
+  int64_t last = -1;
+  bool bad = false;
+#pragma unroll
+  for (int g = 0; g < SEG / 4096; ++g) {  // four loads in flight per lane
+    Lane16 v[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int64_t pu = base + (4 * g + u) * 1024 + lane * 16;
+      v[u] = pu < nbytes ? load16(data, nbytes, pu) : Lane16{{0, 0, 0, 0}};
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int st = 4 * g + u;
+      bad |= quote_or_cr(v[u]);
+      nl_words(v[u], h[st]);
+      const int c = __popc(h[st][0]) + __popc(h[st][1]) + __popc(h[st][2]) + __popc(h[st][3]);
+      if (c) {
+        const int i = h[st][3] ? 3 : h[st][2] ? 2 : h[st][1] ? 1 : 0;
+        last = base + st * 1024 + lane * 16 + 4 * i + ((31 - __builtin_clz(h[st][i])) >> 3);
+      }
+      cnt += c;
+    }
+  }
+  int tot = cnt;
+  for (int d = 32; d >= 1; d >>= 1) {
+    tot += __shfl_xor(tot, d);
+    last = max(last, (int64_t)__shfl_xor(last, d));
+  }
+  const bool anybad = __ballot(bad) != 0;
+  int64_t excl = 0;
+  if (lane == 0) {
+    if (anybad) __hip_atomic_fetch_or((unsigned long long*)&host[2], 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    const uint64_t mine = ((uint64_t)tot << 31) | (uint64_t)(last + 1);
+    uint64_t el = 0;
+    if (seg > 0) {
+      __hip_atomic_store(&status[seg], LB_AGG | mine, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      int64_t j = seg - 1;
+      uint32_t spins = 0;
+      for (;;) {
+        const uint64_t w = __hip_atomic_load(&status[j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if ((w >> 62) == 0) {
+          if (++spins > (1u << 24)) {  // never expected: give up, the host reruns the general passes
+            __hip_atomic_fetch_or((unsigned long long*)&host[2], 4ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            break;
+          }
+          __builtin_amdgcn_s_sleep(1);
+          continue;
+        }
+        excl += (int64_t)((w >> 31) & LB_M31);
+        if (el == 0) el = w & LB_M31;
+        if ((w >> 62) == 2) break;
+        --j;
+      }
+    }
+    const uint64_t lp1 = last >= 0 ? (uint64_t)(last + 1) : el;  // last '\n' so far, + 1 (0: none)
+    __hip_atomic_store(&status[seg], LB_INC | ((uint64_t)(excl + tot) << 31) | lp1, __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_AGENT);
+    if (excl + tot > cap)
+      __hip_atomic_fetch_or((unsigned long long*)&host[2], 2ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    if (seg == nseg - 1) {  // the file's totals (the host reads them after the stream sync)
+      __hip_atomic_store(&host[0], excl + tot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      __hip_atomic_store(&host[1], (int64_t)lp1 - 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+  }
+  excl = __shfl(excl, 0);
+  if (anybad || excl + tot > cap) return;  // the result is discarded
+  int64_t out = excl;
+#pragma unroll
+  for (int st = 0; st < SEG / 1024; ++st) {
+    const int c = __popc(h[st][0]) + __popc(h[st][1]) + __popc(h[st][2]) + __popc(h[st][3]);
+    int ex = 0, total = 0;
+#pragma unroll
+    for (int b = 0; b < 5; ++b) {
+      const uint64_t plane = __ballot((c >> b) & 1);
+      ex += __popcll(plane & below) << b;
+      total += __popcll(plane) << b;
+    }
+    int64_t o = out + ex;
+    const int64_t pos = base + st * 1024 + lane * 16;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      uint64_t hh = h[st][2 * i] | ((uint64_t)h[st][2 * i + 1] << 32);
+      while (hh) {
+        ends[o++] = pos + 8 * i + (__builtin_ctzll(hh) >> 3);
+        hh &= hh - 1;
+      }
+    }
+    out += total;
+  }
+}
+
 // The segment plan: the quote state at each segment's start (parity of all earlier quotes), the
 // terminator count under that state, its prefixes, and the last terminator's position — in two
 // launches over blocks of 2048 segments. k_csv_seg_reduce: per block, its quote count and its
@@ -1277,45 +1402,85 @@ int csv_parse(qe_ctx* ctx, const uint8_t* data, int64_t nbytes, const qe_csv_opt
   // ---- record terminators
   const int64_t nseg = (int64_t)div_up((uint64_t)(nbytes > 0 ? nbytes : 1), SEG);
   const int64_t spb = (int64_t)div_up((uint64_t)nseg, SP_TILE);
-  void* p;
-  QE_TRY(ctx_workspace(ctx, 0, (size_t)(8 * nseg + 6) * 8 + (size_t)div_up((uint64_t)nseg, SP_TILE) * sizeof(SegAgg) + (size_t)nseg,
-                       &p));
-  int64_t* seg_q = (int64_t*)p;
-  int64_t* seg_qs = seg_q + nseg;
-  int64_t* seg_ts = seg_qs + nseg + 1;
-  int64_t* seg_t0 = seg_ts + nseg + 1;  // then seg_t1 [nseg], seg_l0 [nseg], seg_l1 [nseg]
-  int64_t* seg_t1 = seg_t0 + nseg;
   const int wgrid = (int)div_up((uint64_t)nseg, 4);  // 4 waves per 256-thread block
-  SegAgg* agg = (SegAgg*)(seg_t1 + 3 * nseg);  // after seg_t1 / seg_l0 / seg_l1
-  uint8_t* seg_cr = (uint8_t*)(agg + spb);
-  if (nbytes > 0) {
-    hipLaunchKernelGGL(k_csv_count2, dim3(wgrid), dim3(256), 0, ctx->stream, data, nbytes, nseg, seg_q, seg_t0, seg_t1,
-                       seg_cr);
-    QE_TRY(launch_check("k_csv_count2"));
-  } else {
-    QE_HIP(hipMemsetAsync(seg_q, 0, 8, ctx->stream));
-    QE_HIP(hipMemsetAsync(seg_t0, 0, 16, ctx->stream));
-    QE_HIP(hipMemsetAsync(seg_t0 + 2, 0xFF, 16, ctx->stream));  // no terminator (nseg == 1)
-    QE_HIP(hipMemsetAsync(seg_cr, 0, 1, ctx->stream));
-  }
   // the kernels below leave their few host-bound words in fine-grained pinned memory: one sync, no
   // read-back copies
   void* hp;
   QE_TRY(ctx_pinned_coherent(ctx, (size_t)(2 * nproj + 3) * 8, &hp));
   volatile int64_t* host = (volatile int64_t*)hp;
-  hipLaunchKernelGGL(k_csv_seg_reduce, dim3((unsigned)spb), dim3(SP_THREADS), 0, ctx->stream, seg_q, seg_t0, seg_t1, nseg,
-                     seg_cr, agg);
-  QE_TRY(launch_check("k_csv_seg_reduce"));
-  hipLaunchKernelGGL(k_csv_seg_apply, dim3((unsigned)spb), dim3(SP_THREADS), 0, ctx->stream, seg_q, seg_t0, seg_t1, nseg,
-                     agg, spb, seg_qs, seg_ts, (int64_t*)hp);
-  QE_TRY(launch_check("k_csv_seg_apply"));
-  QE_TRY(ctx_sync(ctx));
-  const int64_t nterm = host[0], last_end = host[1];
-  const bool file_q = (host[2] & 1) != 0, file_cr = (host[2] & 2) != 0;  // any '"' / '\r' in the bytes
+  static const bool seg_env = [] {  // (the segment field pass, below)
+    const char* e = getenv("QE_CSV_SEGFIELDS");
+    return e && e[0] == '1';
+  }();
+  // One pass for files without '"' or '\r' (k_csv_ends1; QE_CSV_ONEPASS=0: off), else — or when it
+  // finds one — the general passes: k_csv_count2 -> segment plan -> k_csv_terms.
+  static const bool onepass_env = [] {
+    const char* e = getenv("QE_CSV_ONEPASS");
+    return !(e && e[0] == '0');
+  }();
+  void* p;
+  int64_t* ends = nullptr;
+  int64_t nterm = 0, last_end = -1;
+  bool file_q = false, file_cr = false, have_ends = false;
+  int64_t* seg_qs = nullptr;
+  int64_t* seg_ts = nullptr;
+  if (onepass_env && !seg_env && nbytes > 0 && nbytes < (1ll << 31)) {
+    const int64_t cap = nbytes / 16 + 1024;  // line ends the list can take (else: the general passes)
+    QE_TRY(ctx_workspace(ctx, 0, (size_t)(nseg + 1) * 8, &p));
+    uint64_t* status = (uint64_t*)p;
+    QE_TRY(ctx_workspace(ctx, 1, (size_t)(cap + 2) * 8, &p));
+    ends = (int64_t*)p;
+    QE_HIP(hipMemsetAsync(status, 0, (size_t)(nseg + 1) * 8, ctx->stream));
+    host[0] = 0;
+    host[1] = -1;
+    host[2] = 0;
+    hipLaunchKernelGGL(k_csv_ends1, dim3(wgrid), dim3(256), 0, ctx->stream, data, nbytes, nseg,
+                       (unsigned int*)(status + nseg), status, ends, cap, (int64_t*)hp);
+    QE_TRY(launch_check("k_csv_ends1"));
+    QE_TRY(ctx_sync(ctx));
+    if (host[2] == 0) {
+      nterm = host[0];
+      last_end = host[1];
+      have_ends = true;
+    }
+  }
+  if (!have_ends) {
+    QE_TRY(ctx_workspace(ctx, 0, (size_t)(8 * nseg + 6) * 8 + (size_t)div_up((uint64_t)nseg, SP_TILE) * sizeof(SegAgg) + (size_t)nseg,
+                         &p));
+    int64_t* seg_q = (int64_t*)p;
+    seg_qs = seg_q + nseg;
+    seg_ts = seg_qs + nseg + 1;
+    int64_t* seg_t0 = seg_ts + nseg + 1;  // then seg_t1 [nseg], seg_l0 [nseg], seg_l1 [nseg]
+    int64_t* seg_t1 = seg_t0 + nseg;
+    SegAgg* agg = (SegAgg*)(seg_t1 + 3 * nseg);  // after seg_t1 / seg_l0 / seg_l1
+    uint8_t* seg_cr = (uint8_t*)(agg + spb);
+    if (nbytes > 0) {
+      hipLaunchKernelGGL(k_csv_count2, dim3(wgrid), dim3(256), 0, ctx->stream, data, nbytes, nseg, seg_q, seg_t0, seg_t1,
+                         seg_cr);
+      QE_TRY(launch_check("k_csv_count2"));
+    } else {
+      QE_HIP(hipMemsetAsync(seg_q, 0, 8, ctx->stream));
+      QE_HIP(hipMemsetAsync(seg_t0, 0, 16, ctx->stream));
+      QE_HIP(hipMemsetAsync(seg_t0 + 2, 0xFF, 16, ctx->stream));  // no terminator (nseg == 1)
+      QE_HIP(hipMemsetAsync(seg_cr, 0, 1, ctx->stream));
+    }
+    hipLaunchKernelGGL(k_csv_seg_reduce, dim3((unsigned)spb), dim3(SP_THREADS), 0, ctx->stream, seg_q, seg_t0, seg_t1, nseg,
+                       seg_cr, agg);
+    QE_TRY(launch_check("k_csv_seg_reduce"));
+    hipLaunchKernelGGL(k_csv_seg_apply, dim3((unsigned)spb), dim3(SP_THREADS), 0, ctx->stream, seg_q, seg_t0, seg_t1, nseg,
+                       agg, spb, seg_qs, seg_ts, (int64_t*)hp);
+    QE_TRY(launch_check("k_csv_seg_apply"));
+    QE_TRY(ctx_sync(ctx));
+    nterm = host[0];
+    last_end = host[1];
+    file_q = (host[2] & 1) != 0;  // any '"' / '\r' in the bytes
+    file_cr = (host[2] & 2) != 0;
+    QE_TRY(ctx_workspace(ctx, 1, (size_t)(nterm + 2) * 8, &p));
+    ends = (int64_t*)p;
+  }
   A.noq = file_q ? 0 : 1;
-  QE_TRY(ctx_workspace(ctx, 1, (size_t)(3 * nterm + 7) * 8, &p));
-  int64_t* ends = (int64_t*)p;
-  int64_t* keep = ends + nterm + 2;
+  QE_TRY(ctx_workspace(ctx, 4, (size_t)(2 * nterm + 5) * 8, &p));
+  int64_t* keep = (int64_t*)p;
   int64_t* kstart = keep + nterm + 2;
   // bytes after the last terminator form a final record (also an unterminated quote at EOF), unless
   // the caller says more of the file follows (QE_CSV_PARTIAL_TAIL: they start its next chunk)
@@ -1342,10 +1507,6 @@ int csv_parse(qe_ctx* ctx, const uint8_t* data, int64_t nbytes, const qe_csv_opt
   // for the line-end list + per-line walk below (k_csv_seg_fields 635 us vs k_csv_terms<emit> 160 +
   // k_csv_lines 283 us): a wave walks its 16 KiB segment step by step, each lane's boundaries in a
   // serial loop, where the line pass runs 64 independent lines per wave.
-  static const bool seg_env = [] {
-    const char* e = getenv("QE_CSV_SEGFIELDS");
-    return e && e[0] == '1';
-  }();
   const int64_t rows_all = std::max<int64_t>(0, nlines - first);
   if (seg_env && nlines > 0 && A.delim > 0x20) {
     // fields a record does not have read as "" (K:263): lengths and quote flags start at zero
@@ -1359,7 +1520,7 @@ int csv_parse(qe_ctx* ctx, const uint8_t* data, int64_t nbytes, const qe_csv_opt
     if (host[0] == 0) return QE_OK;
     // a line that may not be a record: the line-end list and the kept-line path below decide
   }
-  if (nterm > 0) {
+  if (nterm > 0 && !have_ends) {
     auto kt = file_q ? (file_cr ? k_csv_terms<true, true> : k_csv_terms<true, false>)
                      : (file_cr ? k_csv_terms<false, true> : k_csv_terms<false, false>);
     hipLaunchKernelGGL(kt, dim3(wgrid), dim3(256), 0, ctx->stream, data, nbytes, nseg, seg_qs, seg_ts, ends);

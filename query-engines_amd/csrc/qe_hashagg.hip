@@ -2560,12 +2560,15 @@ static int run_update(qe_hashagg* h, Plan& P) {
       const size_t pbudget = pagg_block() == 1024 ? (size_t)152 * 1024 : HA_LDS_BUDGET;
       while (tl >= 8 && lds_layout_at(h, &Q, tl) > pbudget) --tl;
     }
-    // QE_SPILL_MAXPCT: the spilled groups (expected groups beyond the kept share, 7/8 of the
-    // compact slots) may fill this percentage of the aggregation table (unset: the kept share
-    // counted at 3/4 and half the table)
+    // QE_SPILL_MAXPCT (default 60): the spilled groups (expected groups beyond the kept share, 7/8
+    // of the compact slots) may fill this percentage of the aggregation table; 0 = round 4's rule
+    // (kept share counted at 3/4, half the table: to ~6.7K groups for C4). 1B rows, one box, C4
+    // shape (profiles/r05_spill_reach.jsonl), 7,000 groups: 7.04 ms spilled (60 %) against 7.64 ms
+    // partitioned; 8,192 groups spilled (70 %) 8.71 against 7.62 ms partitioned, so 60 % stops at
+    // ~7.9K groups
     static const int sp_pct = [] {
       const char* e = getenv("QE_SPILL_MAXPCT");
-      const int v = e && *e ? atoi(e) : 0;
+      const int v = e && *e ? atoi(e) : 60;
       return v >= 10 && v <= 90 ? v : 0;
     }();
     const int64_t spill_max = sp_pct ? nsl * 7 / 8 + ((int64_t)1 << tl) * sp_pct / 100
