@@ -365,14 +365,15 @@ __global__ void __launch_bounds__(256) k_csv_count2(const uint8_t* __restrict__ 
 }
 
 // One pass for the line-end list of a file without '"' or '\r' (speculative: the host does not
-// know that yet). Replaces k_csv_count2 -> k_csv_seg_reduce / _apply -> k_csv_terms, whose two byte
-// passes each spent their VALU on the same '\n' compare. A wave takes the next segment by ticket,
-// computes the '\n' words of its 16 KiB once (kept in registers, 64 VGPRs), publishes its count and
-// last '\n' (decoupled look-back over the segments before it, which hold lower tickets and so are
-// running or done: no wave waits for one that may not start), then writes the positions from the
-// same words. Any '"' or '\r' in the file (host[2] bit 0), a list longer than `cap` (bit 1) or a
-// look-back that does not finish (bit 2) makes the host rerun the general passes. nbytes < 2^31:
-// a status word packs flag (2 bits) | count (31) | last '\n' + 1 (31).
+// know that yet). Replaces k_csv_count2 -> k_csv_seg_reduce / _apply -> k_csv_terms. A wave counts
+// the '\n' bytes of its 16 KiB segment, publishes its count and last '\n' (decoupled look-back, 64
+// predecessors per round), then reads the segment again to write the positions (holding its '\n'
+// words in registers spilled them). Segments follow the wave index: workgroups are dispatched in
+// order, so every segment a wave waits for is resident or done (a ticket counter instead — one
+// device atomic per wave on one word — took 400 us for tripdata's 23.5K segments); a look-back that
+// still does not finish gives up. Any '"' or '\r' in the file (host[2] bit 0), a list longer than
+// `cap` (bit 1) or a look-back that gave up (bit 2) makes the host rerun the general passes.
+// nbytes < 2^31: a status word packs flag (2 bits) | count (31) | last '\n' + 1 (31).
 constexpr uint64_t LB_AGG = 1ull << 62, LB_INC = 2ull << 62, LB_M31 = (1ull << 31) - 1;
 
 // Any '"' or '\r' among the 16 bytes (has-zero-byte tests; bytes past the end read as 0).
@@ -387,20 +388,16 @@ __device__ __forceinline__ bool quote_or_cr(const Lane16& v) {
 }
 
 __global__ void __launch_bounds__(256) k_csv_ends1(const uint8_t* __restrict__ data, int64_t nbytes, int64_t nseg,
-                                                   unsigned int* __restrict__ ticket, uint64_t* __restrict__ status,
+                                                   uint64_t* __restrict__ status,
                                                    int64_t* __restrict__ ends, int64_t cap, int64_t* host) {
   const int lane = threadIdx.x & 63;
-  int64_t seg = 0;
-  if (lane == 0) seg = (int64_t)atomicAdd(ticket, 1u);
-  seg = __shfl(seg, 0);
+  const int64_t seg = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
   if (seg >= nseg) return;
   const int64_t base = seg * SEG;
   const uint64_t below = (1ull << lane) - 1;
-  uint32_t h[SEG / 1024][4];
   int cnt = 0;
   int64_t last = -1;
   bool bad = false;
-#pragma unroll
   for (int g = 0; g < SEG / 4096; ++g) {  // four loads in flight per lane
     Lane16 v[4];
 #pragma unroll
@@ -411,12 +408,13 @@ __global__ void __launch_bounds__(256) k_csv_ends1(const uint8_t* __restrict__ d
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
       const int st = 4 * g + u;
+      uint32_t h[4];
       bad |= quote_or_cr(v[u]);
-      nl_words(v[u], h[st]);
-      const int c = __popc(h[st][0]) + __popc(h[st][1]) + __popc(h[st][2]) + __popc(h[st][3]);
+      nl_words(v[u], h);
+      const int c = __popc(h[0]) + __popc(h[1]) + __popc(h[2]) + __popc(h[3]);
       if (c) {
-        const int i = h[st][3] ? 3 : h[st][2] ? 2 : h[st][1] ? 1 : 0;
-        last = base + st * 1024 + lane * 16 + 4 * i + ((31 - __builtin_clz(h[st][i])) >> 3);
+        const int i = h[3] ? 3 : h[2] ? 2 : h[1] ? 1 : 0;
+        last = base + st * 1024 + lane * 16 + 4 * i + ((31 - __builtin_clz(h[i])) >> 3);
       }
       cnt += c;
     }
@@ -427,31 +425,46 @@ __global__ void __launch_bounds__(256) k_csv_ends1(const uint8_t* __restrict__ d
     last = max(last, (int64_t)__shfl_xor(last, d));
   }
   const bool anybad = __ballot(bad) != 0;
+  if (anybad && lane == 0)
+    __hip_atomic_fetch_or((unsigned long long*)&host[2], 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  const uint64_t mine = ((uint64_t)tot << 31) | (uint64_t)(last + 1);
+  if (seg > 0 && lane == 0) __hip_atomic_store(&status[seg], LB_AGG | mine, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  // look-back, 64 predecessors per round (lane i reads segment j - i): sum the counts up to the
+  // nearest inclusive prefix; the nearest segment with a '\n' gives the last one so far
   int64_t excl = 0;
-  if (lane == 0) {
-    if (anybad) __hip_atomic_fetch_or((unsigned long long*)&host[2], 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-    const uint64_t mine = ((uint64_t)tot << 31) | (uint64_t)(last + 1);
-    uint64_t el = 0;
-    if (seg > 0) {
-      __hip_atomic_store(&status[seg], LB_AGG | mine, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      int64_t j = seg - 1;
-      uint32_t spins = 0;
-      for (;;) {
-        const uint64_t w = __hip_atomic_load(&status[j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if ((w >> 62) == 0) {
-          if (++spins > (1u << 24)) {  // never expected: give up, the host reruns the general passes
+  uint64_t el = 0;
+  if (seg > 0) {
+    int64_t j = seg - 1;
+    uint32_t spins = 0;
+    for (;;) {
+      const int64_t idx = j - lane;
+      const uint64_t w = idx >= 0 ? __hip_atomic_load(&status[idx], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                                  : LB_INC;  // before segment 0: an inclusive prefix of nothing
+      const uint64_t incm = __ballot((w >> 62) == 2);
+      const int lim = incm ? __builtin_ctzll(incm) : 63;  // lanes 0..lim take part
+      const uint64_t part = lim == 63 ? ~0ull : ((2ull << lim) - 1ull);
+      if (__ballot((w >> 62) == 0) & part) {  // a predecessor has not published yet
+        if (++spins > (1u << 20)) {  // never expected: give up, the host reruns the general passes
+          if (lane == 0)
             __hip_atomic_fetch_or((unsigned long long*)&host[2], 4ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-            break;
-          }
-          __builtin_amdgcn_s_sleep(1);
-          continue;
+          break;
         }
-        excl += (int64_t)((w >> 31) & LB_M31);
-        if (el == 0) el = w & LB_M31;
-        if ((w >> 62) == 2) break;
-        --j;
+        __builtin_amdgcn_s_sleep(2);
+        continue;
       }
+      const bool in = (part >> lane) & 1;
+      int64_t c = in ? (int64_t)((w >> 31) & LB_M31) : 0;
+      for (int d = 32; d >= 1; d >>= 1) c += __shfl_xor(c, d);
+      excl += c;
+      if (el == 0) {
+        const uint64_t hasl = __ballot(in && (w & LB_M31) != 0) ;
+        if (hasl) el = (uint64_t)__shfl((int64_t)(w & LB_M31), __builtin_ctzll(hasl));
+      }
+      if (incm) break;
+      j -= 64;
     }
+  }
+  if (lane == 0) {
     const uint64_t lp1 = last >= 0 ? (uint64_t)(last + 1) : el;  // last '\n' so far, + 1 (0: none)
     __hip_atomic_store(&status[seg], LB_INC | ((uint64_t)(excl + tot) << 31) | lp1, __ATOMIC_RELAXED,
                        __HIP_MEMORY_SCOPE_AGENT);
@@ -465,9 +478,26 @@ __global__ void __launch_bounds__(256) k_csv_ends1(const uint8_t* __restrict__ d
   excl = __shfl(excl, 0);
   if (anybad || excl + tot > cap) return;  // the result is discarded
   int64_t out = excl;
+  Lane16 vq[4];
+  for (int st = 0; st < SEG / 1024; ++st) {  // the segment again (mostly from the caches): positions
+    const int64_t pos = base + st * 1024 + lane * 16;
+    if ((st & 3) == 0) {
 #pragma unroll
-  for (int st = 0; st < SEG / 1024; ++st) {
-    const int c = __popc(h[st][0]) + __popc(h[st][1]) + __popc(h[st][2]) + __popc(h[st][3]);
+      for (int u = 0; u < 4; ++u) {
+        const int64_t pu = pos + u * 1024;
+        vq[u] = pu < nbytes ? load16(data, nbytes, pu) : Lane16{{0, 0, 0, 0}};
+      }
+    }
+    Lane16 v;
+    switch (st & 3) {  // constant indices keep vq in registers
+      case 0: v = vq[0]; break;
+      case 1: v = vq[1]; break;
+      case 2: v = vq[2]; break;
+      default: v = vq[3]; break;
+    }
+    uint32_t h[4];
+    nl_words(v, h);
+    const int c = __popc(h[0]) + __popc(h[1]) + __popc(h[2]) + __popc(h[3]);
     int ex = 0, total = 0;
 #pragma unroll
     for (int b = 0; b < 5; ++b) {
@@ -476,10 +506,9 @@ __global__ void __launch_bounds__(256) k_csv_ends1(const uint8_t* __restrict__ d
       total += __popcll(plane) << b;
     }
     int64_t o = out + ex;
-    const int64_t pos = base + st * 1024 + lane * 16;
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
-      uint64_t hh = h[st][2 * i] | ((uint64_t)h[st][2 * i + 1] << 32);
+      uint64_t hh = h[2 * i] | ((uint64_t)h[2 * i + 1] << 32);
       while (hh) {
         ends[o++] = pos + 8 * i + (__builtin_ctzll(hh) >> 3);
         hh &= hh - 1;
@@ -812,15 +841,35 @@ __device__ void walk_record(const D& data, int64_t s, int64_t e, const FieldArgs
   if (f <= A.max_field) record_field(data, A, f, fs, e, r);
 }
 
-// Position of the k-th (0-based) set bit of a 16-bit mask that has more than k set bits.
-__device__ __forceinline__ int nth_bit16(uint32_t d, int k) {
-  int pos = 0, c = __popc(d & 0xFFu);
-  if (k >= c) { k -= c; d >>= 8; pos += 8; }
-  c = __popc(d & 0xFu);
-  if (k >= c) { k -= c; d >>= 4; pos += 4; }
-  c = __popc(d & 0x3u);
-  if (k >= c) { k -= c; d >>= 2; pos += 2; }
-  return pos + (k >= (int)(d & 1u) ? 1 : 0);
+// The delimiter bytes among a lane's 16 as bit 7 of each matching byte, in two 64-bit words (bytes
+// 0-7 and 8-15), restricted to bytes [lo, hi): counts and positions come straight from these words
+// (packing them to a 16-bit mask cost the line walk ~40 VALU instructions per 16 bytes).
+__device__ __forceinline__ uint64_t byte_lowmask(int n) {  // bytes [0, n) of a 64-bit word, n in 0..8
+  return n >= 8 ? ~0ull : ((1ull << (8 * n)) - 1ull);
+}
+__device__ __forceinline__ void delim_words(const Lane16& v, uint32_t delim, int lo, int hi, uint64_t& d0,
+                                            uint64_t& d1) {
+  const uint32_t rep = delim * 0x01010101u;
+  uint32_t hb[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const uint32_t x = v.w[i] ^ rep;
+    hb[i] = ~(((x & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | x | 0x7F7F7F7Fu);
+  }
+  d0 = hb[0] | ((uint64_t)hb[1] << 32);
+  d1 = hb[2] | ((uint64_t)hb[3] << 32);
+  if (lo != 0 || hi != 16) {  // the line's first or last chunk
+    d0 &= byte_lowmask(min(hi, 8)) & ~byte_lowmask(min(lo, 8));
+    d1 &= byte_lowmask(max(hi - 8, 0)) & ~byte_lowmask(max(lo - 8, 0));
+  }
+}
+// Byte index (0..15) of the k-th (0-based) delimiter of (d0, d1), which hold more than k.
+__device__ __forceinline__ int nth_delim(uint64_t d0, uint64_t d1, int k) {
+  const int c0 = __popcll(d0);
+  uint64_t w = k < c0 ? d0 : d1;
+  const int b = k < c0 ? 0 : 8;
+  for (k = k < c0 ? k : k - c0; k > 0; --k) w &= w - 1;
+  return b + (__builtin_ctzll(w) >> 3);
 }
 
 // walk_record for a line without a '"' byte (false: the line has one; nothing was written, the
@@ -834,20 +883,22 @@ __device__ bool walk_record_unquoted(const D& data, int64_t s, int64_t e, const 
   int64_t fs = s;
   for (int64_t a = s & ~(int64_t)15; a < e && t < A.npf; a += 16) {
     const Lane16 v = data.load16(a);
-    const uint32_t lo = (uint32_t)(s > a ? s - a : 0);
-    const uint32_t hi = (uint32_t)(e - a < 16 ? e - a : 16);
-    const uint32_t in = (hi >= 32 ? 0xFFFFu : ((1u << hi) - 1u)) & ~((1u << lo) - 1u);
-    if (!A.noq && has_byte(v, '"') && (eq16(v, '"') & in)) return false;
-    const uint32_t d = eq16(v, (uint32_t)A.delim) & in;
-    const int n = __popc(d);
+    const int lo = s > a ? (int)(s - a) : 0;
+    const int hi = e - a < 16 ? (int)(e - a) : 16;
+    if (!A.noq && has_byte(v, '"') &&
+        (eq16(v, '"') & ((hi >= 16 ? 0xFFFFu : ((1u << hi) - 1u)) & ~((1u << lo) - 1u))))
+      return false;
+    uint64_t d0, d1;
+    delim_words(v, (uint32_t)A.delim, lo, hi, d0, d1);
+    const int n = __popcll(d0) + __popcll(d1);
     while (t < A.npf && A.pf[t] < f + n) {  // projected field A.pf[t] ends in this chunk
       const int ft = A.pf[t], k = ft - f;
-      const int64_t st = k == 0 ? fs : a + nth_bit16(d, k - 1) + 1;
-      record_field(data, A, ft, st, a + nth_bit16(d, k), r);
+      const int64_t st = k == 0 ? fs : a + nth_delim(d0, d1, k - 1) + 1;
+      record_field(data, A, ft, st, a + nth_delim(d0, d1, k), r);
       ++t;
     }
     if (n) {
-      fs = a + (31 - __builtin_clz(d)) + 1;
+      fs = a + (d1 ? 8 + ((63 - __builtin_clzll(d1)) >> 3) : ((63 - __builtin_clzll(d0)) >> 3)) + 1;
       f += n;
     }
   }
@@ -1412,11 +1463,13 @@ int csv_parse(qe_ctx* ctx, const uint8_t* data, int64_t nbytes, const qe_csv_opt
     const char* e = getenv("QE_CSV_SEGFIELDS");
     return e && e[0] == '1';
   }();
-  // One pass for files without '"' or '\r' (k_csv_ends1; QE_CSV_ONEPASS=0: off), else — or when it
-  // finds one — the general passes: k_csv_count2 -> segment plan -> k_csv_terms.
+  // The general passes (k_csv_count2 -> segment plan -> k_csv_terms), or with QE_CSV_ONEPASS=1 one
+  // look-back pass for files without '"' or '\r' (k_csv_ends1, falling back to the general passes
+  // when it finds one). Opt-in: tripdata (4M rows, one box) 213 us against 96 + 16 + 92 us for the
+  // general passes — its VALU per byte is lower, but waves wait on their predecessors' counts.
   static const bool onepass_env = [] {
     const char* e = getenv("QE_CSV_ONEPASS");
-    return !(e && e[0] == '0');
+    return e && e[0] == '1';
   }();
   void* p;
   int64_t* ends = nullptr;
@@ -1426,16 +1479,16 @@ int csv_parse(qe_ctx* ctx, const uint8_t* data, int64_t nbytes, const qe_csv_opt
   int64_t* seg_ts = nullptr;
   if (onepass_env && !seg_env && nbytes > 0 && nbytes < (1ll << 31)) {
     const int64_t cap = nbytes / 16 + 1024;  // line ends the list can take (else: the general passes)
-    QE_TRY(ctx_workspace(ctx, 0, (size_t)(nseg + 1) * 8, &p));
+    QE_TRY(ctx_workspace(ctx, 0, (size_t)nseg * 8, &p));
     uint64_t* status = (uint64_t*)p;
     QE_TRY(ctx_workspace(ctx, 1, (size_t)(cap + 2) * 8, &p));
     ends = (int64_t*)p;
-    QE_HIP(hipMemsetAsync(status, 0, (size_t)(nseg + 1) * 8, ctx->stream));
+    QE_HIP(hipMemsetAsync(status, 0, (size_t)nseg * 8, ctx->stream));
     host[0] = 0;
     host[1] = -1;
     host[2] = 0;
-    hipLaunchKernelGGL(k_csv_ends1, dim3(wgrid), dim3(256), 0, ctx->stream, data, nbytes, nseg,
-                       (unsigned int*)(status + nseg), status, ends, cap, (int64_t*)hp);
+    hipLaunchKernelGGL(k_csv_ends1, dim3(wgrid), dim3(256), 0, ctx->stream, data, nbytes, nseg, status, ends, cap,
+                       (int64_t*)hp);
     QE_TRY(launch_check("k_csv_ends1"));
     QE_TRY(ctx_sync(ctx));
     if (host[2] == 0) {

@@ -274,3 +274,50 @@ def test_gpu_csv_chunked_overlapped_scan(gpu_ctx, tmp_path, monkeypatch, newline
     assert names == onames
     assert len(batches) > 1
     assert cols == R.project(rows, range(3))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("shape", ["plain", "short_lines", "no_trailing_newline", "one_quote_at_end", "cr_at_end"])
+def test_gpu_csv_onepass_vs_general(gpu_ctx, tmp_path, monkeypatch, shape):
+    """With QE_CSV_ONEPASS=1, files without '"' or '\\r' take the one-pass line-end list
+    (k_csv_ends1, segments chained by look-back); a '"' or '\\r' anywhere (here only in the last
+    line), or more line ends than its list holds (lines shorter than 16 bytes), sends the parse back
+    to the general passes. The default (general) passes equal the oracle on every shape, and the
+    one-pass scan (a fresh process: the switch is read once) gives the same columns."""
+    import subprocess
+    import sys
+
+    rng = random.Random(len(shape))
+    if shape == "short_lines":
+        body = [f"{i % 7},{i % 3}" for i in range(300_000)]  # 4-byte lines: over the list's capacity
+    else:
+        body = [f"{i % 13},{rng.random():.6f},{'x' * (i % 40)},{i}" for i in range(120_000)]
+    text = "k,v,s,i\n" + "\n".join(body)
+    if shape == "one_quote_at_end":
+        text += '\n1,"2",3,4'
+    elif shape == "cr_at_end":
+        text += "\r\n1,2,3,4"
+    if shape != "no_trailing_newline":
+        text += "\n"
+    data = text.encode()
+    assert len(data) > 1 << 20  # many 16 KiB segments
+    names, proj, cols, _ = _gpu_scan(gpu_ctx, tmp_path, data)
+    onames, _, rows = R.parse(data)
+    assert names == onames
+    assert cols == R.project(rows, range(len(names)))
+    # the one-pass scan in a process of their own (the switch is read once per process)
+    code = ("import sys, json; sys.path[:0] = [{root!r}, {root!r} + '/query-engines_amd']\n"
+            "from kquery.columnar import Context\nfrom kquery.csv_source import CsvDataSource\n"
+            "ds = CsvDataSource({path!r}, True, 0, ctx=Context.get(0))\n"
+            "cols = [[] for _ in range(4)]\n"
+            "for b in ds.scan(['k', 'v', 's', 'i'][:{n}]):\n"
+            "    for i in range({n}): cols[i] += b.field(i).to_pylist()\n"
+            "print(json.dumps(cols))\n")
+    import pathlib
+
+    root = str(pathlib.Path(__file__).resolve().parents[1])
+    p = tmp_path / "t.csv"
+    env = dict(__import__("os").environ, QE_CSV_ONEPASS="1")
+    out = subprocess.run([sys.executable, "-c", code.format(root=root, path=str(p), n=len(names))], env=env,
+                         capture_output=True, text=True, timeout=240, check=True).stdout
+    assert __import__("json").loads(out.strip().splitlines()[-1]) == cols
