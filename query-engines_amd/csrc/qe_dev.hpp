@@ -1014,17 +1014,30 @@ __device__ inline void lds_fx_add(qi64* acc, qu64* idx, int SS, int s, qi64 x) {
   fx_add_row<true>([&](int w) { return w == 0 ? (qu64*)&acc[s] : &idx[(w - 1) * SS + s]; }, r, &idx[3 * SS + s]);
 }
 
+// LDS MIN / MAX that read first: the atomic only when the value would change the slot. Slots only
+// move one way, so a value no better than what the read returns cannot change it; with few groups
+// most rows skip their same-address atomics (64 lanes on one slot serialise), and a same-address
+// read is a broadcast.
+template <typename T>
+__device__ __forceinline__ void lds_min_rf(T* p, T x) {
+  if (x < __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) atomicMin(p, x);
+}
+template <typename T>
+__device__ __forceinline__ void lds_max_rf(T* p, T x) {
+  if (x > __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) atomicMax(p, x);
+}
+
 // fp64 MIN/MAX row into LDS accumulators (MaxAccumulator order semantics, Main.kt:538-561).
 template <bool IS_MAX>
 __device__ inline void lds_f64mm(qi64* acc, qu64* idx, int SS, int s, qi64 x, qu64 row) {
   const double d = bits_f64(x);
-  atomicMin(&idx[s], row);
+  lds_min_rf(&idx[s], row);
   if (d != d) {
-    atomicMin(&idx[SS + s], row);
+    lds_min_rf(&idx[SS + s], row);
   } else {
-    if (IS_MAX) atomicMax(&acc[s], f64_okey(d));
-    else atomicMin(&acc[s], f64_okey(d));
-    if (d == 0.0) atomicMin(&idx[(x < 0 ? 2 : 3) * SS + s], row);
+    if (IS_MAX) lds_max_rf(&acc[s], f64_okey(d));
+    else lds_min_rf(&acc[s], f64_okey(d));
+    if (d == 0.0) lds_min_rf(&idx[(x < 0 ? 2 : 3) * SS + s], row);
   }
 }
 

@@ -515,8 +515,8 @@ void emit_agg_rows(const Plan& P, std::ostringstream& o, const std::vector<std::
         else if (fx_limbs()) o << "        lds_fxl_add(s_acc" << js << ", s_idx" << js << ", SS, s, x);\n";
         else o << "        lds_fxw_add(s_acc" << js << ", s_idx" << js << ", SS, s, x);\n";
         break;
-      case ACC_MIN_I: o << "        atomicMin(&s_acc" << js << "[s], x);\n"; break;
-      case ACC_MAX_I: o << "        atomicMax(&s_acc" << js << "[s], x);\n"; break;
+      case ACC_MIN_I: o << "        lds_min_rf(&s_acc" << js << "[s], x);\n"; break;
+      case ACC_MAX_I: o << "        lds_max_rf(&s_acc" << js << "[s], x);\n"; break;
       case ACC_MIN_F:
       case ACC_MAX_F:
         o << "        lds_f64mm<" << (a.acc == ACC_MAX_F ? "true" : "false") << ">(s_acc" << js << ", s_idx" << js
@@ -681,8 +681,8 @@ void emit_agg_rows_c(const Plan& P, std::ostringstream& o, const std::vector<std
     if (a.track_nn) o << "      atomicAdd(&s_nn" << js << "[s], 1u);\n";
     switch (a.acc) {
       case ACC_SUM_I: o << "      atomicAdd((qu64*)&s_acc" << js << "[s], (qu64)x);\n"; break;
-      case ACC_MIN_I: o << "      atomicMin(&s_acc" << js << "[s], " << (a32 ? "(qi32)x" : "x") << ");\n"; break;
-      case ACC_MAX_I: o << "      atomicMax(&s_acc" << js << "[s], " << (a32 ? "(qi32)x" : "x") << ");\n"; break;
+      case ACC_MIN_I: o << "      lds_min_rf(&s_acc" << js << "[s], " << (a32 ? "(qi32)x" : "x") << ");\n"; break;
+      case ACC_MAX_I: o << "      lds_max_rf(&s_acc" << js << "[s], " << (a32 ? "(qi32)x" : "x") << ");\n"; break;
       default: break;
     }
     o << "    }\n";
