@@ -305,8 +305,26 @@ def main():
         if world > 1:
             dist.barrier()
 
+    # the same read ceiling before any warm-up (the device straight from idle), for the record
+    cc0 = (N.QeColumn * 3)(*[c.as_c() for c in cols])
+    ms0 = C.c_double()
+    shape0 = C.create_string_buffer(128)
+    N.check(N.lib().qe_stream_read_best(ctx.handle, cc0, 3, 1, C.byref(ms0), shape0, 128))
+    cold_gbs = rows * BYTES_PER_ROW / (ms0.value * 1e-3) / 1e9
+    t_w = time.perf_counter()
     for _ in range(args.warmup):
         step()
+    # Clock warm-up (untimed, like the W warm-up steps): on a box fresh from idle the first
+    # process's kernels and stream reads ran ~7 % slower (2.65e11 vs 2.85e11 rows/s, ceiling 6.70 vs
+    # 7.02 TB/s, same box, back-to-back processes); keep stepping until the device has been busy
+    # for QE_BENCH_PREWARM_S seconds (default 2) before the timed region. One rank only: ranks
+    # must run the same number of steps (each holds collectives), so N > 1 runs none.
+    prewarm_s = float(os.environ.get("QE_BENCH_PREWARM_S", "2")) if world == 1 else 0.0
+    prewarm_steps = 0
+    while time.perf_counter() - t_w < prewarm_s:
+        step()
+        torch.cuda.synchronize()
+        prewarm_steps += 1
     kinds.append(partial.last_kernel_kind())
     kernel_ms.clear()
     barrier()
@@ -425,6 +443,8 @@ def main():
             "avg_kernel_ms": avg_kernel_ms,
             "bytes_per_launch": rows * BYTES_PER_ROW,
             "stream_read_ceiling_gbs": stream_gbs,
+            "stream_read_cold_gbs": cold_gbs,
+            "prewarm_steps": prewarm_steps,
             "stream_read_ceiling_shape": shape.value.decode(),
         },
         "check": check,
