@@ -93,7 +93,7 @@ __global__ void __launch_bounds__(CAST_THREADS) k_cast_utf8_f64(const int32_t* _
         DecScan ds;
         const int r = parse_fast(bytes + s0, s1 - s0, &v, &ds);
         if (r == P_ERR) {
-          atomicMin(err_row, (unsigned long long)i);
+          atomicMax(err_row, ~(unsigned long long)i);  // (the first failing row: the largest complement)
           v = 0.0;
         } else {
           ok = true;
@@ -154,20 +154,21 @@ extern "C" int qe_cast_utf8_to_f64(qe_ctx* ctx, const qe_column* in, qe_column* 
   const int64_t groups = (n + 7) / 8;
   void* s;
   QE_TRY(ctx_scratch(ctx, 16 + (size_t)groups, &s));
-  unsigned long long* err = (unsigned long long*)s;
+  unsigned long long* err = (unsigned long long*)s;  // ~(first failing row), 0: none
   unsigned int* nslow = (unsigned int*)((char*)s + 8);
   uint8_t* slow = (uint8_t*)s + 16;
-  QE_HIP(hipMemsetAsync(s, 0xFF, 8, ctx->stream));
-  QE_HIP(hipMemsetAsync((char*)s + 8, 0, 8, ctx->stream));
+  QE_HIP(hipMemsetAsync(s, 0, 16, ctx->stream));
   const int grid = (int)std::min<int64_t>((int64_t)div_up((uint64_t)n, CAST_THREADS), (int64_t)ctx->num_cus * 16);
   hipLaunchKernelGGL(k_cast_utf8_f64, dim3(grid), dim3(CAST_THREADS), 0, ctx->stream, in->offsets,
                      (const uint8_t*)in->values, in->validity, n, (double*)out->values, out->validity, slow, err, nslow);
   QE_TRY(launch_check("k_cast_utf8_f64"));
-  uint64_t hdr[2] = {~0ull, 0};
-  QE_HIP(hipMemcpyAsync(hdr, s, 16, hipMemcpyDeviceToHost, ctx->stream));
+  void* hp;  // pinned: the read-back is one DMA, not a staged pageable copy
+  QE_TRY(ctx_pinned(ctx, 16, &hp));
+  QE_HIP(hipMemcpyAsync(hp, s, 16, hipMemcpyDeviceToHost, ctx->stream));
   QE_TRY(ctx_sync(ctx));
-  if (hdr[0] != ~0ull) {
-    const uint64_t row = hdr[0];
+  const uint64_t hdr[2] = {((const uint64_t*)hp)[0], ((const uint64_t*)hp)[1]};
+  if (hdr[0] != 0) {
+    const uint64_t row = ~hdr[0];
     if (error_row) *error_row = (int64_t)row;
     int32_t o[2] = {0, 0};
     char buf[96] = {0};
