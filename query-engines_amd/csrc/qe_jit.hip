@@ -474,7 +474,7 @@ void emit_fx_queue_append(const Plan& P, std::ostringstream& o, const std::vecto
 // for row r; `row`: the row's global index (fp64 MIN/MAX order); all are C expressions of r.
 void emit_agg_rows(const Plan& P, std::ostringstream& o, const std::vector<std::string>& val,
                    const std::vector<std::string>& ok, const std::string& row, const std::string& didx,
-                   bool fx_queue = false) {
+                   bool fx_queue = false, bool few_groups = false) {
   o << "    int slot[4];\n    qu32 h[4];\n    qi64 k0[4];\n"
     << "#pragma unroll\n    for (int r = 0; r < 4; ++r) { h[r] = lds_hash((qu64)key[r]) >> (32 - LOG2); k0[r] = ((act >> r) & 1) ? s_keys[h[r]] : 0; }\n"
     << "#pragma unroll\n    for (int r = 0; r < 4; ++r) slot[r] = ((knull >> r) & 1) ? S : (key[r] == EMPTY_KEY ? S + 1 : (k0[r] == key[r] ? (int)h[r] : -1));\n"
@@ -495,8 +495,19 @@ void emit_agg_rows(const Plan& P, std::ostringstream& o, const std::vector<std::
         o << "      rare = rare || ((" << ok[j] << ") && fx_rare(" << val[j] << "));\n";
     o << "      glob |= (qu32)rare << r;\n    }\n";
   }
-  o << "    glob &= act;\n    const qu32 loc = act & ~glob;\n"
-    << "#pragma unroll\n    for (int r = 0; r < 4; ++r) if ((loc >> r) & 1) atomicAdd(&s_cst[slot[r]], 1u);\n";
+  o << "    glob &= act;\n    const qu32 loc = act & ~glob;\n";
+  if (few_groups && !any_x)
+    // A table of a few groups (the smallest, 256 slots): most lanes of a row position hit the same
+    // few slots, and 64 lanes' atomics on one LDS word serialise. The lanes on the first active
+    // lane's slot add their COUNT(*) as one atomic (tripdata, 3 groups; MIN / MAX read first).
+    o << "#pragma unroll\n    for (int r = 0; r < 4; ++r) {\n      const bool lr = (loc >> r) & 1;\n"
+      << "      const qu64 am = __ballot(lr);\n      if (am) {\n"
+      << "        const int s0 = __builtin_amdgcn_readlane(slot[r], (int)__builtin_ctzll(am));\n"
+      << "        const bool mine = lr && slot[r] == s0;\n        const qu64 m = __ballot(mine);\n"
+      << "        if (mine) { if (lane == (int)__builtin_ctzll(m)) atomicAdd(&s_cst[s0], (qu32)__popcll(m)); }\n"
+      << "        else if (lr) atomicAdd(&s_cst[slot[r]], 1u);\n      }\n    }\n";
+  else
+    o << "#pragma unroll\n    for (int r = 0; r < 4; ++r) if ((loc >> r) & 1) atomicAdd(&s_cst[slot[r]], 1u);\n";
   for (int j = 0; j < P.naggs; ++j) {
     const DAgg& a = P.aggs[j];
     if (a.pkind == 0 || a.share) continue;  // (a shared accumulator takes the row once)
@@ -900,7 +911,8 @@ bool gen_fused_source(const Plan& P, int log2, std::string* src, size_t* lds_byt
   if (compact)
     emit_agg_rows_c(P, o, val, ok, "P.row_base + r0 + 128 * (r >> 1) + (r & 1)", "r0 + 128 * (r >> 1) + (r & 1)");
   else
-    emit_agg_rows(P, o, val, ok, "P.row_base + r0 + 128 * (r >> 1) + (r & 1)", "r0 + 128 * (r >> 1) + (r & 1)", fxq);
+    emit_agg_rows(P, o, val, ok, "P.row_base + r0 + 128 * (r >> 1) + (r & 1)", "r0 + 128 * (r >> 1) + (r & 1)", fxq,
+                  log2 <= 8);
   o << (pf ? "    } while (0);\n  }\n  }\n" : "  }\n");
   if (fxq) {  // the rest of the wave's queue
     o << "  if (q_n) {\n";
