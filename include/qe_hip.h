@@ -80,10 +80,15 @@ extern "C" {
 #define QE_TYPE_UINT8 6
 #define QE_TYPE_DATE32 7 /* int32 days since epoch */
 
-/* One Arrow array (offset 0). Used for inputs and outputs. */
+/* One Arrow array (offset 0). Used for inputs and outputs.
+ * max_len: UTF8 inputs only — when > 0, the producer's bound on every value's byte length
+ * (qe_csv_column fills it from the parse); 0 = unknown. A hash aggregate keyed by a lone UTF8
+ * column uses a bound <= 7 to encode the keys with no dictionary and no host round trip; the bound
+ * is checked on the device, and a longer value fails the aggregate's next read-back (finalize,
+ * num_groups) instead of grouping wrongly. Ignored for other types and for outputs. */
 typedef struct qe_column {
   int32_t type;
-  int32_t reserved;
+  int32_t max_len;
   int64_t length;
   uint8_t* validity; /* device; NULL = all valid (inputs) / do not write (outputs) */
   void* values;      /* device; fixed-width values, bit-packed bools, or UTF-8 bytes */
@@ -262,10 +267,23 @@ int qe_agg_global_partial(qe_ctx* ctx, const qe_column* col, const qe_column* ma
 int qe_agg_global_merge(qe_ctx* ctx, int32_t type, const void* partials, int32_t n, qe_global_agg* out);
 
 /* ---- HashAggregateExec (K4b) ------------------------------------------------------------ */
-/* Group keys: 0..4 columns. One key of any fixed-width type, or several narrow keys
- * (uint8/int32/date32/bool) whose widths + one null bit each fit in 63 bits. A null key
- * is a group of its own (List.equals semantics, K:621-627). Group order is unspecified
- * (HashMap iteration, K:639). */
+/* Group keys: 0..4 columns of any type — INT64, FLOAT64 (Double.equals: one NaN group, +0.0 and
+ * -0.0 apart), INT32, DATE32, UINT8, BOOL, UTF8 (byte equality of String(bytes), K:620-627). A null
+ * key is a group of its own (List.equals semantics, K:621-627). Group order is unspecified
+ * (HashMap iteration, K:639).
+ * The table groups by one 64-bit word per row. One INT64/FLOAT64 key is that word; narrow keys
+ * (INT32/DATE32/UINT8) whose widths + one null bit each fit in 63 bits are packed into it. Every
+ * other key list is DICTIONARY-KEYED, and the state owns its dictionaries:
+ *   - a lone UTF8 key gets wide INT64 codes (a value of at most 7 bytes is its own code, longer ones
+ *     go through a string dictionary: qe_strdict_encode);
+ *   - a UTF8 key in a list gets INT32 dictionary codes, packed with the narrow keys;
+ *   - a list that still does not pack (INT64 + UTF8, BOOL, three INT32 ...) groups by one INT32
+ *     code per distinct key tuple (qe_strdict_encode_tuple).
+ * Updates and fused updates take the ORIGINAL key columns (UTF8 included) and encode them; finalize
+ * writes the original key types back (qe_hashagg_finalize_sizes sizes UTF8 outputs). The codes are
+ * local to the state, so its partials move between states only by key content:
+ * qe_hashagg_merge / qe_hashagg_export_keyed / qe_hashagg_import_keyed / qe_hashagg_exchange. The
+ * raw record calls (export*, import*) refuse a dictionary-keyed state with QE_ERR_UNSUPPORTED. */
 #define QE_MAX_KEYS 4
 #define QE_MAX_AGGS 8
 #define QE_MAX_COLS 8
@@ -280,6 +298,7 @@ typedef struct qe_agg_desc {
 } qe_agg_desc;
 
 typedef struct qe_hashagg qe_hashagg;
+typedef struct qe_strdict qe_strdict; /* string / key-tuple dictionary (UTF-8 group keys, below) */
 
 int qe_hashagg_create(qe_ctx* ctx, int32_t nkeys, const int32_t* key_types, int32_t naggs,
                       const qe_agg_desc* aggs, int64_t expected_groups, qe_hashagg** out);
@@ -401,13 +420,22 @@ int qe_hashagg_num_groups(qe_hashagg* agg, int64_t* out);
  * *out_groups is exact on return; the column contents are stream-ordered: they are written by
  * work queued on the ctx stream (read them on that stream, or after qe_ctx_synchronize).
  * Output types: keys as declared; SUM/MIN/MAX as input type; COUNT/COUNT_STAR int64;
- * AVG fp64. */
+ * AVG fp64. A UTF8 key output needs offsets for groups+1 entries, a validity buffer, and a values
+ * buffer of at least the bytes qe_hashagg_finalize_sizes reports for it. */
 int qe_hashagg_finalize(qe_hashagg* agg, qe_column* out_keys, qe_column* out_aggs,
                         int64_t* out_groups);
+/* Output sizes of the next finalize (synchronises): *groups, and key_bytes[k] (one entry per
+ * declared key, may be NULL) = a bound on the value bytes finalize writes for UTF8 key k (0 for
+ * other keys). Exact when the key has dictionary codes; 7 bytes per group while a lone UTF8 key's
+ * values have all been at most 7 bytes (no device work then). */
+int qe_hashagg_finalize_sizes(qe_hashagg* agg, int64_t* groups, int64_t* key_bytes);
 
 /* Two-phase / multi-GPU aggregate (K:1309-1325 pattern):
  * export the partial groups bucketed by destination partition = hash(key) mod nparts
- * as fixed-size records, then import records (from any rank) into another state. */
+ * as fixed-size records, then import records (from any rank) into another state.
+ * Records carry the table's key word as is, so these calls (and the slot calls below) refuse a
+ * dictionary-keyed state (QE_ERR_UNSUPPORTED): its partials move by content (qe_hashagg_merge,
+ * qe_hashagg_export_keyed / qe_hashagg_import_keyed). */
 int qe_hashagg_record_bytes(qe_hashagg* agg, int64_t* out);
 /* counts[p] = records for partition p (host array of nparts, synchronises). */
 int qe_hashagg_export_counts(qe_hashagg* agg, int32_t nparts, int64_t* counts);
@@ -417,6 +445,38 @@ int qe_hashagg_export_counts(qe_hashagg* agg, int32_t nparts, int64_t* counts);
 int qe_hashagg_export(qe_hashagg* agg, int32_t nparts, void* dst);
 /* Merge `nrecords` records (device) into this state (combine semantics per aggregate). */
 int qe_hashagg_import(qe_hashagg* agg, const void* records, int64_t nrecords);
+
+/* Partials by key CONTENT (K:1309-1325 with the reference's String(bytes) keys, K:620-627): the
+ * form every state supports, and the only one for dictionary-keyed states, whose codes mean nothing
+ * to another state. A block is self-describing: a 128-byte header (magic, records, key types, UTF8
+ * byte counts), the records with their key words cleared, then per key its validity (one byte per
+ * record) and its values (8 bytes per record, or UTF8 lengths + bytes). Records are routed by a
+ * content hash of the keys (qe_hash_partition), so equal keys reach the same partition on every
+ * rank whatever each rank's dictionaries hold; the importer re-encodes the keys into its own
+ * dictionaries, so equal strings merge and different strings never share a group.
+ * export_keyed_sizes (synchronises) computes block_bytes[p] for each of `nparts` partitions and
+ * keeps the state's groups ready for export_keyed, which writes the blocks partition-major into
+ * `dst` (device, sum(block_bytes); stream-ordered). Any update, import or reset in between
+ * invalidates it (QE_ERR_INVALID_ARG). import_keyed merges `nblocks` received blocks, packed
+ * back to back in `blocks` (device) with sizes block_bytes[b] (0 = no block); the blocks' layout
+ * must be this state's (same key types, aggregates and options, else QE_ERR_INVALID_ARG). */
+#define QE_KEYED_HEADER 128
+int qe_hashagg_export_keyed_sizes(qe_hashagg* agg, int32_t nparts, int64_t* block_bytes);
+int qe_hashagg_export_keyed(qe_hashagg* agg, int32_t nparts, void* dst);
+int qe_hashagg_import_keyed(qe_hashagg* agg, const void* blocks, int32_t nblocks, const int64_t* block_bytes);
+/* main()'s partial -> final merge inside one process (K:1314-1325): every group of `src` is merged
+ * into `dst` (same ctx, same key types and aggregates). By key content when either state is
+ * dictionary-keyed, else by raw records. `src` is unchanged. */
+int qe_hashagg_merge(qe_hashagg* dst, qe_hashagg* src);
+/* A state created with INT32 (or, for a lone key, wide INT64) key `key` whose codes the CALLER
+ * takes from `dict` (qe_strdict_encode): binding the dictionary makes the state dictionary-keyed —
+ * finalize, merge and the keyed exchange decode and re-encode through `dict`, and the raw record
+ * calls refuse it. Updates then take either the codes or the UTF8 column itself. `dict` must
+ * outlive the state. Bind before the first update. */
+int qe_hashagg_bind_key_dict(qe_hashagg* agg, int32_t key, qe_strdict* dict);
+/* How the state groups: *dictionary_keyed (0: raw key words; 1: string codes; 2: key-tuple codes),
+ * and the types of the columns the table groups by (device_types: QE_MAX_KEYS entries). */
+int qe_hashagg_key_layout(qe_hashagg* agg, int32_t* dictionary_keyed, int32_t* device_nkeys, int32_t* device_types);
 
 /* Fixed-capacity exchange: ONE equal-split all-to-all and no host synchronisation before it.
  * export_slots writes `nparts` slots of QE_SLOT_HEADER + slot_records * record_bytes bytes into
@@ -473,7 +533,11 @@ int qe_comm_create_loopback(qe_ctx* ctx, int32_t world, int32_t rank, void* hub,
  * ranks with headroom), one grouped send/recv on the ctx stream, one read-back; if a partition
  * overflowed its slot on any rank, every rank falls back to counts + records. A stream-ordered
  * (qe_hashagg_set_async) partial is exported without a host wait. *nrecords (optional) = records
- * this rank merged. partial, owner and comm must share the ctx. */
+ * this rank merged. partial, owner and comm must share the ctx.
+ * Dictionary-keyed states (UTF8 / key-tuple codes) exchange by key content instead: block sizes in
+ * one all-to-all, then the blocks (qe_hashagg_export_keyed / qe_hashagg_import_keyed), routed by a
+ * content hash and re-encoded on the owner — the reference's VendorID-keyed merge (K:1336) across
+ * GPUs. */
 int qe_hashagg_exchange(qe_comm* comm, qe_hashagg* partial, qe_hashagg* owner, int64_t slot_records,
                         int64_t* nrecords);
 
@@ -497,8 +561,9 @@ int qe_hashagg_last_kernel_kind(qe_hashagg* agg, int32_t* specialized, char* not
  * A device string dictionary maps each distinct byte string to a dense int32 code, stable for
  * the dictionary's lifetime (codes are assigned in first-insertion order within a call, which
  * is unordered across rows). A hash aggregate groups by the codes (key type INT32); finalize
- * decodes them back to strings. Equality is byte equality of the whole string. */
-typedef struct qe_strdict qe_strdict;
+ * decodes them back to strings. Equality is byte equality of the whole string. (A hash aggregate
+ * with UTF8 keys owns such dictionaries itself; these calls are for callers that encode keys on
+ * their own, qe_hashagg_bind_key_dict.) */
 int qe_strdict_create(qe_ctx* ctx, int64_t expected_distinct, qe_strdict** out);
 int qe_strdict_destroy(qe_strdict* dict);
 /* Number of distinct strings inserted so far. */

@@ -95,6 +95,7 @@ struct qe_loop_hub {
   uint64_t generation = 0;
   std::vector<const uint8_t*> send;
   std::vector<const size_t*> soff, sbytes;
+  std::vector<int> failed;
   void barrier() {
     std::unique_lock<std::mutex> g(mu);
     const uint64_t gen = generation;
@@ -136,12 +137,16 @@ int exchange_bytes(qe_comm* c, const uint8_t* send, const size_t* soff, const si
                    const size_t* roff, const size_t* rbytes) {
   if (c->hub) {  // in-process ranks: publish, wait, copy what the peers address to this rank, wait
     qe_loop_hub* h = c->hub;
-    QE_TRY(ctx_sync(c->ctx));  // the send buffers are complete
+    // a rank that fails still passes both barriers (its peers would wait forever otherwise) and
+    // publishes the failure, so that every rank skips the copies and reports it
+    int st = ctx_sync(c->ctx);  // the send buffers are complete
     h->send[c->rank] = send;
     h->soff[c->rank] = soff;
     h->sbytes[c->rank] = sbytes;
+    h->failed[c->rank] = st != QE_OK;
     h->barrier();
-    int st = QE_OK;
+    for (int p = 0; p < c->world && st == QE_OK; ++p)
+      if (h->failed[p]) st = fail(QE_ERR_COMM, "loopback exchange: rank %d failed before the exchange", p);
     for (int p = 0; p < c->world && st == QE_OK; ++p) {
       if (h->sbytes[p][c->rank] != rbytes[p])
         st = fail(QE_ERR_COMM, "loopback exchange: rank %d sends %zu bytes to rank %d, which expects %zu", p,
@@ -164,6 +169,48 @@ int exchange_bytes(qe_comm* c, const uint8_t* send, const size_t* soff, const si
   const ncclResult_t e = R.group_end();  // the group is closed whatever failed inside it
   QE_NCCL(r);
   QE_NCCL(e);
+  return QE_OK;
+}
+
+// Dictionary-keyed partials (K:1336's VendorID): blocks by key content. One all-to-all of the block
+// sizes, then the blocks; the owner re-encodes the keys into its own dictionaries.
+int exchange_keyed(qe_comm* c, qe_hashagg* partial, qe_hashagg* owner, int64_t* nrecords) {
+  const int world = c->world;
+  std::vector<int64_t> sb(world), rb(world);
+  QE_TRY(qe_hashagg_export_keyed_sizes(partial, world, sb.data()));
+  QE_TRY(comm_buffer(c, (size_t)2 * world * 8));
+  int64_t* dsz = (int64_t*)c->buf;
+  QE_HIP(hipMemcpyAsync(dsz, sb.data(), (size_t)world * 8, hipMemcpyHostToDevice, c->ctx->stream));
+  std::vector<size_t> o8(world), l8(world, 8);
+  for (int p = 0; p < world; ++p) o8[p] = (size_t)p * 8;
+  QE_TRY(exchange_bytes(c, (const uint8_t*)dsz, o8.data(), l8.data(), (uint8_t*)(dsz + world), o8.data(), l8.data()));
+  QE_HIP(hipMemcpyAsync(rb.data(), dsz + world, (size_t)world * 8, hipMemcpyDeviceToHost, c->ctx->stream));
+  QE_TRY(ctx_sync(c->ctx));
+  std::vector<size_t> so(world), sl(world), ro(world), rl(world);
+  size_t a = 0, b = 0;
+  for (int p = 0; p < world; ++p) {
+    so[p] = a;
+    sl[p] = (size_t)sb[p];
+    a += sl[p];
+    ro[p] = b;
+    rl[p] = (size_t)rb[p];
+    b += rl[p];
+  }
+  QE_TRY(comm_buffer(c, std::max<size_t>(a + b, 8)));
+  uint8_t* send = c->buf;
+  uint8_t* recv = c->buf + a;
+  QE_TRY(qe_hashagg_export_keyed(partial, world, send));
+  QE_TRY(exchange_bytes(c, send, so.data(), sl.data(), recv, ro.data(), rl.data()));
+  QE_TRY(qe_hashagg_import_keyed(owner, recv, world, rb.data()));
+  if (nrecords) {  // records this rank merged: the received blocks' counts (header word 1)
+    std::vector<int64_t> nrec(world, 0);
+    for (int p = 0; p < world; ++p)
+      if (rb[p]) QE_HIP(hipMemcpyAsync(&nrec[p], recv + ro[p] + 8, 8, hipMemcpyDeviceToHost, c->ctx->stream));
+    QE_TRY(ctx_sync(c->ctx));
+    int64_t n = 0;
+    for (int64_t x : nrec) n += x;
+    *nrecords = n;
+  }
   return QE_OK;
 }
 
@@ -217,6 +264,7 @@ int qe_comm_loopback_hub_create(int32_t world, void** hub) {
   h->send.assign(world, nullptr);
   h->soff.assign(world, nullptr);
   h->sbytes.assign(world, nullptr);
+  h->failed.assign(world, 0);
   *hub = h;
   return QE_OK;
 }
@@ -260,6 +308,8 @@ int qe_hashagg_exchange(qe_comm* c, qe_hashagg* partial, qe_hashagg* owner, int6
   QE_TRY(qe_hashagg_record_bytes(partial, &rb));
   QE_CHECK(hashagg_ctx(partial) == c->ctx && hashagg_ctx(owner) == c->ctx, QE_ERR_INVALID_ARG,
            "partial, owner and communicator must share one qe_ctx (one stream)");
+  if (keyed_dict(hashagg_info(partial).keyed) || keyed_dict(hashagg_info(owner).keyed))
+    return exchange_keyed(c, partial, owner, nrecords);
   int64_t cap = slot_records;
   if (cap <= 0) QE_TRY(qe_hashagg_slot_capacity(partial, world, &cap));
   const size_t slot_bytes = (size_t)QE_SLOT_HEADER + (size_t)cap * (size_t)rb;

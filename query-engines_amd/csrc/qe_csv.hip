@@ -1697,6 +1697,9 @@ int qe_csv_column(const qe_csv_table* tc, int32_t i, qe_column* out) {
     c.length = t->rows;
     c.offsets = (int32_t*)o;
     c.values = v;
+    // the parse's bound on the values' lengths travels with the column (a lone UTF8 GROUP BY key of
+    // short values then needs no dictionary, qe_column.max_len)
+    if (!t->maxlen.empty()) c.max_len = (int32_t)std::min<int64_t>(t->maxlen[(size_t)i], INT32_MAX);
   }
   *out = c;
   return QE_OK;
@@ -1726,6 +1729,7 @@ int qe_csv_column_copy(const qe_csv_table* tc, int32_t i, qe_column* dst) {
   QE_TRY(ctx_enter(t->ctx));
   QE_TRY(build_column(t, i, dst->offsets, (uint8_t*)dst->values));
   dst->length = t->rows;
+  if (!t->maxlen.empty()) dst->max_len = (int32_t)std::min<int64_t>(t->maxlen[(size_t)i], INT32_MAX);
   return QE_OK;
 }
 

@@ -1211,12 +1211,6 @@ struct OutCols {
   qe_column aggs[QE_MAX_AGGS];
 };
 
-struct KeyMeta {
-  qi32 mode, nkeys;
-  qi32 type[QE_MAX_KEYS], shift[QE_MAX_KEYS], nullbit[QE_MAX_KEYS];
-  qi64 fmask[QE_MAX_KEYS];
-};
-
 __device__ __forceinline__ void set_bit(qu8* bm, qi64 i, bool v) {
   // bytes are written by whole 32-bit atomics: the host zeroes validity buffers first
   if (v) atomicOr((qu32*)bm + (i >> 5), 1u << (i & 31));
@@ -1277,6 +1271,7 @@ __device__ __forceinline__ void finalize_slot(const DTable& t, const AggMeta& m,
   const qu64 cst = t.cstar[s];
 #pragma unroll 1
   for (int j = 0; j < m.naggs; ++j) {
+    if (!out.aggs[j].values) continue;  // keys only (qe_hashagg_finalize_sizes of a keyed state)
     const qu64 nn = slot_nn(t, m, j, s);
     const qi64 acc = t.acc[j][s];
     qi64 val = 0;
@@ -1470,6 +1465,11 @@ struct qe_hashagg {
   // that reads the state fails with this status until qe_hashagg_reset
   int poisoned = 0;
   std::string poison_msg;
+  // the declared (original) key columns and their dictionaries (qe_keyed.hip); the fields above
+  // describe the DEVICE key columns the table groups by
+  qe::Keyed* keyed = nullptr;
+  int32_t flags = 0;      // qe_hashagg_create_ex flags
+  uint64_t version = 0;   // bumped by every change of the groups
 };
 
 namespace qe {
@@ -1483,6 +1483,20 @@ int hashagg_expected_groups(const qe_hashagg* h, int64_t* out) {
 }
 
 qe_ctx* hashagg_ctx(const qe_hashagg* h) { return h ? h->ctx : nullptr; }
+
+HashaggInfo hashagg_info(const qe_hashagg* h) {
+  HashaggInfo I{};
+  I.ctx = h->ctx;
+  I.km = h->km;
+  I.rec_bytes = h->rec_bytes;
+  I.naggs = h->naggs;
+  I.flags = h->flags;
+  for (int j = 0; j < h->naggs; ++j) I.aggs[j] = h->aggs[j];
+  I.version = h->version;
+  I.ctl = (uint64_t*)h->ctl;
+  I.keyed = h->keyed;
+  return I;
+}
 
 static AggMeta agg_meta(const qe_hashagg* h) {
   AggMeta m{};
@@ -1568,6 +1582,8 @@ static int read_ctl(qe_hashagg* h, uint64_t out[8]) {
   QE_HIP(hipMemcpyAsync(p, h->ctl, 64, hipMemcpyDeviceToHost, h->ctx->stream));
   QE_TRY(ctx_sync(h->ctx));
   memcpy(out, p, 64);
+  QE_CHECK((out[3] & CTL_KEY_TOO_LONG) == 0, QE_ERR_INVALID_ARG,
+           "a UTF8 group key is longer than its column's max_len promised (qe_column.max_len)");
   QE_CHECK(out[3] == 0, QE_ERR_CAPACITY, "hash aggregate lost %llu groups (probe limit or overflow area)",
            (unsigned long long)out[3]);
   return QE_OK;
@@ -2285,6 +2301,8 @@ static int settle_pass(qe_hashagg* h, const Plan& P, int* out_i, const uint32_t*
   uint64_t c[8];
   QE_HIP(hipEventSynchronize(h->ev_ctl));
   memcpy(c, h->ctl_pin, 64);
+  QE_CHECK((c[3] & CTL_KEY_TOO_LONG) == 0, QE_ERR_INVALID_ARG,
+           "a UTF8 group key is longer than its column's max_len promised (qe_column.max_len)");
   QE_CHECK(c[3] == 0, QE_ERR_CAPACITY, "hash aggregate lost %llu groups (probe limit or overflow area)",
            (unsigned long long)c[3]);
   {
@@ -2778,15 +2796,28 @@ int qe_hashagg_create_ex(qe_ctx* ctx, int32_t nkeys, const int32_t* key_types, i
   QE_CHECK(naggs == 0 || aggs, QE_ERR_INVALID_ARG, "null aggs");
   qe_hashagg* h = new qe_hashagg();
   h->ctx = ctx;
-  h->nkeys = nkeys;
   h->naggs = naggs;
+  h->flags = flags;
   auto bail = [&](int code) {
     for (hipEvent_t e : {h->ev[0], h->ev[1], h->ev_ctl})
       if (e) (void)hipEventDestroy(e);
     if (h->ctl_pin) pinned_slot_free(h->ctl_pin, h->ctx->stream);
+    if (h->keyed) keyed_destroy(ctx, h->keyed);
     delete h;
     return code;
   };
+  // the declared keys -> the device key columns the table groups by (UTF8 keys and key lists that
+  // do not pack into one 64-bit word become dictionary codes, qe_keyed.hip)
+  int32_t dev_types[QE_MAX_KEYS] = {};
+  {
+    int32_t dn = 0;
+    const int st = keyed_create(ctx, nkeys, key_types, expected_groups > 0 ? expected_groups : 1024, &h->keyed, &dn,
+                                dev_types);
+    if (st != QE_OK) return bail(st);
+    nkeys = dn;
+    key_types = dev_types;
+  }
+  h->nkeys = nkeys;
   // key packing
   if (nkeys == 0) {
     h->km.mode = 0;
@@ -2890,6 +2921,7 @@ int qe_hashagg_destroy(qe_hashagg* h) {
   qe_ctx* ctx = h->ctx;  // blocks go back to the caching allocator behind this stream's work
   void* bufs[] = {h->table_mem, h->ctl, h->ovf, h->part_cnt, h->part_rec, h->part_slc, h->defer[0], h->defer[1]};
   for (void* b : bufs) dev_free(ctx, b);
+  if (h->keyed) keyed_destroy(ctx, h->keyed);
   for (int i = 0; i < 2; ++i) {
     if (h->ev[i]) (void)hipEventDestroy(h->ev[i]);
   }
@@ -2948,6 +2980,7 @@ int qe_hashagg_reset(qe_hashagg* h) {
   h->ctl_rows_clean = true;
   h->row_base = 0;
   h->known_groups = 0;
+  ++h->version;
   return QE_OK;
 }
 
@@ -2962,15 +2995,30 @@ static_assert(sizeof(Plan) <= 4096, "kernel argument must stay under 4 KiB");
 int qe_hashagg_update_fused(qe_hashagg* h, const qe_column* cols, int32_t ncols, const qe_fused_spec* spec) {
   QE_CHECK(h && cols && spec, QE_ERR_INVALID_ARG, "null argument");
   QE_TRY(ctx_enter(h->ctx));
-  Plan P;
-  QE_TRY(compile_plan(h, cols, ncols, spec, &P));
-  return run_update(h, P);
+  if (keyed_dict(h->keyed)) return keyed_update_fused(h, cols, ncols, spec);
+  return hashagg_update_fused_raw(h, cols, ncols, spec);
 }
 
 int qe_hashagg_update(qe_hashagg* h, const qe_column* keys, const qe_column* agg_inputs, const qe_column* mask) {
   QE_CHECK(h, QE_ERR_INVALID_ARG, "null state");
   QE_TRY(ctx_enter(h->ctx));
   QE_CHECK(h->nkeys == 0 || keys, QE_ERR_INVALID_ARG, "null keys");
+  if (keyed_dict(h->keyed)) return keyed_update(h, keys, agg_inputs, mask);
+  return hashagg_update_raw(h, keys, agg_inputs, mask);
+}
+
+}  // extern "C"
+
+namespace qe {
+
+int hashagg_update_fused_raw(qe_hashagg* h, const qe_column* cols, int32_t ncols, const qe_fused_spec* spec) {
+  Plan P;
+  QE_TRY(compile_plan(h, cols, ncols, spec, &P));
+  ++h->version;
+  return run_update(h, P);
+}
+
+int hashagg_update_raw(qe_hashagg* h, const qe_column* keys, const qe_column* agg_inputs, const qe_column* mask) {
   QE_CHECK(h->naggs == 0 || agg_inputs, QE_ERR_INVALID_ARG, "null agg_inputs");
   // Column slots: distinct buffers only (shared columns are read once).
   qe_column cols[QE_MAX_COLS];
@@ -3023,8 +3071,13 @@ int qe_hashagg_update(qe_hashagg* h, const qe_column* keys, const qe_column* agg
   }
   Plan P;
   QE_TRY(compile_plan(h, cols, ncols, &spec, &P));
+  ++h->version;
   return run_update(h, P);
 }
+
+}  // namespace qe
+
+extern "C" {
 
 int qe_hashagg_num_groups(qe_hashagg* h, int64_t* out) {
   QE_CHECK(h && out, QE_ERR_INVALID_ARG, "null argument");
@@ -3057,6 +3110,14 @@ static int check_fx_final(qe_hashagg* h) {
 int qe_hashagg_finalize(qe_hashagg* h, qe_column* out_keys, qe_column* out_aggs, int64_t* out_groups) {
   QE_CHECK(h, QE_ERR_INVALID_ARG, "null state");
   QE_TRY(ctx_enter(h->ctx));
+  if (keyed_dict(h->keyed)) return keyed_finalize(h, out_keys, out_aggs, out_groups);
+  return hashagg_finalize_raw(h, out_keys, out_aggs, out_groups, false);
+}
+
+}  // extern "C"
+
+int qe::hashagg_finalize_raw(qe_hashagg* h, qe_column* out_keys, qe_column* out_aggs, int64_t* out_groups,
+                             bool keys_only) {
   qe_ctx* ctx = h->ctx;
   int64_t groups;
   QE_TRY(qe_hashagg_num_groups(h, &groups));
@@ -3075,7 +3136,7 @@ int qe_hashagg_finalize(qe_hashagg* h, qe_column* out_keys, qe_column* out_aggs,
     oc.keys[k] = c;
     if (c.validity && !small) QE_HIP(hipMemsetAsync(c.validity, 0, div_up((uint64_t)groups, 32) * 4, ctx->stream));
   }
-  for (int j = 0; j < h->naggs; ++j) {
+  for (int j = 0; j < h->naggs && !keys_only; ++j) {
     QE_CHECK(out_aggs, QE_ERR_INVALID_ARG, "null out_aggs");
     const qe_column& c = out_aggs[j];
     const int fn = h->aggs[j].fn;
@@ -3090,10 +3151,10 @@ int qe_hashagg_finalize(qe_hashagg* h, qe_column* out_keys, qe_column* out_aggs,
     if (c.validity && !small) QE_HIP(hipMemsetAsync(c.validity, 0, div_up((uint64_t)groups, 32) * 4, ctx->stream));
   }
   for (int k = 0; k < h->nkeys; ++k) out_keys[k].length = groups;
-  for (int j = 0; j < h->naggs; ++j) out_aggs[j].length = groups;
+  for (int j = 0; j < h->naggs && !keys_only; ++j) out_aggs[j].length = groups;
   if (groups == 0) return QE_OK;
   bool det = false;
-  for (int j = 0; j < h->naggs; ++j) det = det || h->acc[j] == ACC_SUM_X;
+  for (int j = 0; j < h->naggs && !keys_only; ++j) det = det || h->acc[j] == ACC_SUM_X;
   if (det) QE_HIP(hipMemsetAsync(h->ctl + 6, 0, 8, ctx->stream));
   if (small) {
     hipLaunchKernelGGL(k_finalize_small, dim3(1), dim3(FS_THREADS), 0, ctx->stream, h->t, agg_meta(h), h->km, oc,
@@ -3119,6 +3180,19 @@ int qe_hashagg_finalize(qe_hashagg* h, qe_column* out_keys, qe_column* out_aggs,
   return det ? check_fx_final(h) : QE_OK;
 }
 
+namespace {
+// The raw record calls carry the table's key word: meaningless to another state when it is a
+// dictionary code (K:620-627 keys compare by content), so they refuse such states.
+int refuse_dict_records(const qe_hashagg* h) {
+  QE_CHECK(!keyed_dict(h->keyed), QE_ERR_UNSUPPORTED,
+           "dictionary-keyed state (UTF8 / key-tuple codes are local to it): merge by key content with "
+           "qe_hashagg_merge or qe_hashagg_export_keyed / qe_hashagg_import_keyed");
+  return QE_OK;
+}
+}  // namespace
+
+extern "C" {
+
 int qe_hashagg_record_bytes(qe_hashagg* h, int64_t* out) {
   QE_CHECK(h && out, QE_ERR_INVALID_ARG, "null argument");
   *out = h->rec_bytes;
@@ -3127,6 +3201,7 @@ int qe_hashagg_record_bytes(qe_hashagg* h, int64_t* out) {
 
 int qe_hashagg_export_counts(qe_hashagg* h, int32_t nparts, int64_t* counts) {
   QE_CHECK(h && counts && nparts >= 1, QE_ERR_INVALID_ARG, "bad arguments");
+  QE_TRY(refuse_dict_records(h));
   QE_TRY(ctx_enter(h->ctx));
   QE_TRY(settle_pending(h));
   qe_ctx* ctx = h->ctx;
@@ -3143,7 +3218,14 @@ int qe_hashagg_export_counts(qe_hashagg* h, int32_t nparts, int64_t* counts) {
 
 int qe_hashagg_export(qe_hashagg* h, int32_t nparts, void* dst) {
   QE_CHECK(h && nparts >= 1, QE_ERR_INVALID_ARG, "bad arguments");
+  QE_TRY(refuse_dict_records(h));
   QE_TRY(ctx_enter(h->ctx));
+  return hashagg_export_raw(h, nparts, dst);
+}
+
+}  // extern "C"
+
+int qe::hashagg_export_raw(qe_hashagg* h, int32_t nparts, void* dst) {
   qe_ctx* ctx = h->ctx;
   int64_t groups;
   QE_TRY(qe_hashagg_num_groups(h, &groups));
@@ -3164,8 +3246,11 @@ int qe_hashagg_export(qe_hashagg* h, int32_t nparts, void* dst) {
   return QE_OK;
 }
 
+extern "C" {
+
 int qe_hashagg_export_slots(qe_hashagg* h, int32_t nparts, int64_t slot_records, void* dst) {
   QE_CHECK(h && nparts >= 1 && slot_records >= 1 && dst, QE_ERR_INVALID_ARG, "bad arguments");
+  QE_TRY(refuse_dict_records(h));
   QE_TRY(ctx_enter(h->ctx));
   // a pending update is NOT settled here: the exchange queues behind it with no host round trip,
   // and the slot headers force the variable-size exchange if it left the table incomplete
@@ -3188,8 +3273,10 @@ int qe_hashagg_export_slots(qe_hashagg* h, int32_t nparts, int64_t slot_records,
 int qe_hashagg_import_slots(qe_hashagg* h, const void* slots, int32_t nslots, int64_t slot_records,
                             int64_t* max_count, int64_t* nrecords) {
   QE_CHECK(h && slots && nslots >= 1 && slot_records >= 1 && max_count, QE_ERR_INVALID_ARG, "bad arguments");
+  QE_TRY(refuse_dict_records(h));
   QE_TRY(ctx_enter(h->ctx));
   QE_TRY(settle_pending(h));
+  ++h->version;
   QE_TRY(nn_materialize(h, h->nn_implicit));  // records carry real non-null counts
   qe_ctx* ctx = h->ctx;
   // room for every record the slots can hold (duplicates counted: an upper bound) before the
@@ -3220,9 +3307,26 @@ int qe_hashagg_import_slots(qe_hashagg* h, const void* slots, int32_t nslots, in
 
 int qe_hashagg_import(qe_hashagg* h, const void* records, int64_t nrecords) {
   QE_CHECK(h && nrecords >= 0 && (records || nrecords == 0), QE_ERR_INVALID_ARG, "bad arguments");
+  QE_TRY(refuse_dict_records(h));
   QE_TRY(ctx_enter(h->ctx));
+  return hashagg_import_raw(h, records, nrecords);
+}
+
+int qe_hashagg_key_layout(qe_hashagg* h, int32_t* dictionary_keyed, int32_t* device_nkeys, int32_t* device_types) {
+  QE_CHECK(h, QE_ERR_INVALID_ARG, "null state");
+  if (dictionary_keyed) *dictionary_keyed = !keyed_dict(h->keyed) ? 0 : keyed_tuple(h->keyed) ? 2 : 1;
+  if (device_nkeys) *device_nkeys = h->nkeys;
+  if (device_types)
+    for (int k = 0; k < QE_MAX_KEYS; ++k) device_types[k] = k < h->nkeys ? h->key_types[k] : 0;
+  return QE_OK;
+}
+
+}  // extern "C"
+
+int qe::hashagg_import_raw(qe_hashagg* h, const void* records, int64_t nrecords) {
   QE_TRY(settle_pending(h));
   if (nrecords == 0) return QE_OK;
+  ++h->version;
   QE_TRY(nn_materialize(h, h->nn_implicit));  // records carry real non-null counts
   h->known_groups = -1;
   uint64_t c[8];
@@ -3230,5 +3334,3 @@ int qe_hashagg_import(qe_hashagg* h, const void* records, int64_t nrecords) {
   if (2 * (c[0] + (uint64_t)nrecords) > h->t.cap) QE_TRY(table_grow(h, 2 * (c[0] + (uint64_t)nrecords)));
   return import_records(h, records, nrecords);
 }
-
-}  // extern "C"

@@ -117,9 +117,48 @@ int pscatter_block_for(int log2p);
 int pagg_block();
 bool fused_prefetch();
 int fused_block(int lds_log2);
-// hash-aggregate state accessors for other translation units (qe_comm.hip)
+// hash-aggregate state accessors for other translation units (qe_comm.hip, qe_keyed.hip)
 int hashagg_expected_groups(const qe_hashagg* h, int64_t* out);
 qe_ctx* hashagg_ctx(const qe_hashagg* h);
+// How the table packs its device key columns into the 64-bit group word: mode 0 no keys, 1 one
+// INT64/FLOAT64 key (record word 1 = null flag), 2 narrow keys at shift with a null bit each.
+struct KeyMeta {
+  int32_t mode, nkeys;
+  int32_t type[QE_MAX_KEYS], shift[QE_MAX_KEYS], nullbit[QE_MAX_KEYS];
+  int64_t fmask[QE_MAX_KEYS];
+};
+struct Keyed;  // original key columns <-> device key columns (qe_keyed.hip)
+struct HashaggInfo {
+  qe_ctx* ctx;
+  KeyMeta km;
+  int32_t rec_bytes, naggs, flags;
+  qe_agg_desc aggs[QE_MAX_AGGS];
+  uint64_t version;  // bumped by every change of the groups (update, import, reset)
+  uint64_t* ctl;     // device control words (ctl[3]: sticky error word)
+  Keyed* keyed;
+};
+HashaggInfo hashagg_info(const qe_hashagg* h);
+// The raw record / update / finalize paths (no dictionary handling), for qe_keyed.hip.
+int hashagg_export_raw(qe_hashagg* h, int32_t nparts, void* dst);
+int hashagg_import_raw(qe_hashagg* h, const void* recs, int64_t nrec);
+int hashagg_update_raw(qe_hashagg* h, const qe_column* dev_keys, const qe_column* agg_inputs, const qe_column* mask);
+int hashagg_update_fused_raw(qe_hashagg* h, const qe_column* cols, int32_t ncols, const qe_fused_spec* spec);
+// keys_only: write the device key columns and skip the aggregates (out_aggs may be NULL)
+int hashagg_finalize_raw(qe_hashagg* h, qe_column* dev_keys, qe_column* out_aggs, int64_t* out_groups, bool keys_only);
+// qe_keyed.hip: create from the declared key types (device key list out), destroy, and the
+// dictionary-keyed forms of update / fused update / finalize.
+int keyed_create(qe_ctx* ctx, int32_t nkeys, const int32_t* types, int64_t expected, Keyed** out, int32_t* dev_nkeys,
+                 int32_t* dev_types);
+void keyed_destroy(qe_ctx* ctx, Keyed* K);
+bool keyed_dict(const Keyed* K);
+bool keyed_tuple(const Keyed* K);
+int keyed_update(qe_hashagg* h, const qe_column* keys, const qe_column* agg_inputs, const qe_column* mask);
+int keyed_update_fused(qe_hashagg* h, const qe_column* cols, int32_t ncols, const qe_fused_spec* spec);
+int keyed_finalize(qe_hashagg* h, qe_column* out_keys, qe_column* out_aggs, int64_t* out_groups);
+// Wide codes of UTF8 values promised to be at most 7 bytes (qe_strdict.hip): a longer value sets
+// bit 62 of *err (the hash aggregate's sticky ctl[3]), so the state fails its next read-back.
+int strdict_encode_packed_checked(qe_ctx* ctx, const qe_column* in, qe_column* codes, unsigned long long* err);
+constexpr uint64_t CTL_KEY_TOO_LONG = 1ull << 62;
 bool gen_pscatter_staged_source(const qe::Plan& P, int log2p, std::string* src, bool chunked = false, bool soa = false);
 bool part_static();  // chunked staged scatter: per-workgroup chunk id ranges (QE_PART_STATIC)
 bool part_soa();  // chunked partition records stored chunk-columnar (QE_PART_SOA)

@@ -803,17 +803,24 @@ __global__ void k_dict_decode_copy(const void* __restrict__ codes, const uint8_t
 // per row), and no control-block read-back: the caller's next kernel can follow on the stream.
 __global__ void __launch_bounds__(256) k_pack_codes(const int32_t* __restrict__ offs, const uint8_t* __restrict__ bytes,
                                                     const uint8_t* __restrict__ valid, int64_t n,
-                                                    int64_t* __restrict__ codes64) {
+                                                    int64_t* __restrict__ codes64,
+                                                    unsigned long long* __restrict__ err) {
+  bool too_long = false;
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
     const bool live = !valid || ((valid[i >> 3] >> (i & 7)) & 1);
     int64_t c = 0;
     if (live) {
       const int32_t s0 = offs[i];
-      const int len = min(offs[i + 1] - s0, WIDE_MAX);
+      const int32_t full = offs[i + 1] - s0;
+      const int len = min(full, WIDE_MAX);
+      too_long |= full > WIDE_MAX;
       c = wide_pack(load_u64_unaligned(bytes + s0, len), len);
     }
     codes64[i] = c;
   }
+  // the caller's length bound was wrong: flag it (one atomic per wave that saw such a value)
+  const unsigned long long b = __ballot(too_long);
+  if (err && b && (int)(threadIdx.x & 63) == __ffsll((long long)b) - 1) atomicOr(err, (unsigned long long)CTL_KEY_TOO_LONG);
 }
 
 // Decode of packed wide codes in one 1024-thread block (small results: a finalize's groups): the
@@ -1349,7 +1356,7 @@ int qe_strdict_encode_packed(qe_ctx* ctx, const qe_column* in, qe_column* codes)
                           ctx->stream));
   const int grid = (int)std::min<int64_t>((int64_t)div_up((uint64_t)n, 256), (int64_t)ctx->num_cus * 8);
   hipLaunchKernelGGL(k_pack_codes, dim3(grid), dim3(256), 0, ctx->stream, in->offsets, (const uint8_t*)in->values,
-                     in->validity, n, (int64_t*)codes->values);
+                     in->validity, n, (int64_t*)codes->values, (unsigned long long*)nullptr);
   return launch_check("k_pack_codes");
 }
 
@@ -1393,3 +1400,16 @@ int qe_strdict_decode_packed(qe_ctx* ctx, const qe_column* codes, qe_column* out
 }
 
 }  // extern "C"
+
+int qe::strdict_encode_packed_checked(qe_ctx* ctx, const qe_column* in, qe_column* codes, unsigned long long* err) {
+  const int64_t n = in->length;
+  codes->length = n;
+  if (n == 0) return QE_OK;
+  if (in->validity)
+    QE_HIP(hipMemcpyAsync(codes->validity, in->validity, (size_t)div_up((uint64_t)n, 8), hipMemcpyDeviceToDevice,
+                          ctx->stream));
+  const int grid = (int)std::min<int64_t>((int64_t)div_up((uint64_t)n, 256), (int64_t)ctx->num_cus * 8);
+  hipLaunchKernelGGL(k_pack_codes, dim3(grid), dim3(256), 0, ctx->stream, in->offsets, (const uint8_t*)in->values,
+                     in->validity, n, (int64_t*)codes->values, err);
+  return launch_check("k_pack_codes");
+}

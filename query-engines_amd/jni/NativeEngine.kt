@@ -89,7 +89,9 @@ object NativeEngine {
                                        tokArg: IntArray, tokLitType: IntArray, tokLitBits: LongArray): Long
     @JvmStatic external fun specFree(spec: Long)
 
-    // HashAggregateExec (K:605-660)
+    // HashAggregateExec (K:605-660). keyTypes may hold UTF8: the state keeps the dictionaries, updates
+    // take the Utf8 key columns, aggFinalize returns Utf8 key columns, aggMergeInto / aggExchange
+    // merge by key content.
     @JvmStatic external fun aggCreate(ctx: Long, keyTypes: IntArray, fns: IntArray, inputTypes: IntArray,
                                       expectedGroups: Long, flags: Int): Long
     @JvmStatic external fun aggDestroy(agg: Long)
@@ -108,7 +110,7 @@ object NativeEngine {
     @JvmStatic external fun selectProjectAsync(ctx: Long, cols: LongArray, spec: Long, outs: LongArray): Long
     @JvmStatic external fun selectProjectWait(pending: Long, outs: LongArray): Long
 
-    // Utf8 group keys (K:620-627)
+    // Utf8 codes for callers that encode keys themselves (K:620-627); aggregates need none of these
     @JvmStatic external fun dictCreate(ctx: Long, expected: Long): Long
     @JvmStatic external fun dictDestroy(dict: Long)
     @JvmStatic external fun dictEncode(ctx: Long, dict: Long, input: Long): Long

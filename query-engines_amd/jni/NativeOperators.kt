@@ -144,13 +144,15 @@ private class NativeBinaryExpression(
     }
 }
 
-// HashAggregateExec (K:605-660) on the device: every input batch is one aggregate update (Utf8
-// keys through a string dictionary), then ONE output batch (K:649-650). MAX follows
-// MaxAccumulator (K:538-561). A MAX over a Utf8 column is the reference's own operator: its
-// accumulator keeps the first String of a group with no type check and throws
-// UnsupportedOperationException at the second (K:541-550), row-order behaviour the device has no
-// use for; that row loop reads these batches through NativeColumnVector.getValue. (Called
-// directly, aggCreate throws the same UnsupportedOperationException for a Utf8 MAX input.)
+// HashAggregateExec (K:605-660) on the device: every input batch is one aggregate update, then ONE
+// output batch (K:649-650). Utf8 keys go in as they are: the native state keeps their dictionaries
+// (a lone Utf8 key like K:1336's VendorID gets wide codes — values of up to 7 bytes are their own
+// code, and a CSV column's length bound lets them skip the dictionary entirely) and finalize hands
+// the strings back. MAX follows MaxAccumulator (K:538-561). A MAX over a Utf8 column is the
+// reference's own operator: its accumulator keeps the first String of a group with no type check
+// and throws UnsupportedOperationException at the second (K:541-550), row-order behaviour the
+// device has no use for; that row loop reads these batches through NativeColumnVector.getValue.
+// (Called directly, aggCreate throws the same UnsupportedOperationException for a Utf8 MAX input.)
 private class NativeHashAggregateExec(
     private val input: PhysicalPlan,
     private val groupExpr: List<Expression>,
@@ -172,39 +174,22 @@ private class NativeHashAggregateExec(
                 else -> throw IllegalStateException("Unsupported aggregate function: ${aggregateExpr[i]}") // K:696
             }
         }
-        val dicts = LongArray(groupExpr.size) // Utf8 key k: its dictionary, else 0
         var agg = 0L
         try {
             input.execute().forEach { batch ->
                 val keys = groupExpr.map { toDevice(it.evaluate(batch)) }
                 val inputs = aggregateExpr.map { toDevice(it.inputExpression().evaluate(batch)) }
-                val codes = keys.mapIndexed { k, c ->
-                    if (c.type != NativeEngine.UTF8) c
-                    else {
-                        if (dicts[k] == 0L) dicts[k] = NativeEngine.dictCreate(ctx, 0)
-                        NativeColumnVector(NativeEngine.dictEncode(ctx, dicts[k], c.handle))
-                    }
-                }
                 if (agg == 0L) {
-                    agg = NativeEngine.aggCreate(ctx, IntArray(codes.size) { codes[it].type }, fns,
+                    agg = NativeEngine.aggCreate(ctx, IntArray(keys.size) { keys[it].type }, fns,
                                                  IntArray(inputs.size) { inputs[it].type }, 0, 0)
                 }
-                NativeEngine.aggUpdate(agg, LongArray(codes.size) { codes[it].handle },
+                NativeEngine.aggUpdate(agg, LongArray(keys.size) { keys[it].handle },
                                        LongArray(inputs.size) { inputs[it].handle }, 0)
             }
             if (agg == 0L) return sequenceOf(RecordBatch(schema, schema.fields.map { emptyColumn(ctx, it.dataType) }))
-            val outs = NativeEngine.aggFinalize(agg)
-            val cols = outs.mapIndexed { j, h ->
-                if (j < groupExpr.size && dicts[j] != 0L) {
-                    val decoded = NativeEngine.dictDecode(ctx, dicts[j], h)
-                    NativeEngine.columnFree(h)
-                    NativeColumnVector(decoded)
-                } else NativeColumnVector(h)
-            }
-            return sequenceOf(RecordBatch(schema, cols))
+            return sequenceOf(RecordBatch(schema, NativeEngine.aggFinalize(agg).map { NativeColumnVector(it) }))
         } finally {
             if (agg != 0L) NativeEngine.aggDestroy(agg)
-            dicts.forEach { if (it != 0L) NativeEngine.dictDestroy(it) }
         }
     }
 

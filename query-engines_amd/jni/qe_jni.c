@@ -37,6 +37,7 @@ typedef struct qj_col {
   qe_ctx* ctx;   /* owner of the blocks below; NULL for a view */
   void* blk[3];  /* values, validity, offsets */
   int64_t capacity;
+  qe_strdict* dict; /* dictEncode output: the dictionary its codes belong to */
 } qj_col;
 
 /* HashAggregateExec state: the native aggregate and what finalize needs to shape its output. */
@@ -46,6 +47,8 @@ typedef struct qj_agg {
   int32_t nkeys, naggs;
   int32_t key_types[QE_MAX_KEYS];
   qe_agg_desc aggs[QE_MAX_AGGS];
+  qe_strdict* bound[QE_MAX_KEYS]; /* dictionaries of keys fed dictEncode codes (bound at the first update) */
+  int64_t updates;
 } qj_agg;
 
 /* CSV table: the parsed table and the device copy of the file it indexes. */
@@ -994,8 +997,10 @@ static qj_agg* agg_of(JNIEnv* env, jlong h) {
   return (qj_agg*)(intptr_t)h;
 }
 
-/* fns[j] / inputTypes[j]: aggregate j (QE_AGG_*, input type; ignored for COUNT_STAR).
- * expectedGroups 0 = 1024 (the reference has no hint). flags: QE_HASHAGG_DETERMINISTIC. */
+/* keyTypes: the group keys' column types, UTF8 included (the state owns the dictionaries: aggUpdate
+ * takes the Utf8 key columns, aggFinalize returns Utf8 key columns). fns[j] / inputTypes[j]:
+ * aggregate j (QE_AGG_*, input type; ignored for COUNT_STAR). expectedGroups 0 = 1024 (the reference
+ * has no hint). flags: QE_HASHAGG_DETERMINISTIC / QE_HASHAGG_FAST_FP64. */
 JNIEXPORT jlong JNICALL Java_NativeEngine_aggCreate(JNIEnv* env, jclass k, jlong ctx, jintArray keyTypes,
                                                     jintArray fns, jintArray inputTypes, jlong expectedGroups,
                                                     jint flags) {
@@ -1077,6 +1082,21 @@ JNIEXPORT void JNICALL Java_NativeEngine_aggUpdate(JNIEnv* env, jclass k, jlong 
   const int ni = get_cols(env, inputCols, in, QE_MAX_AGGS, 1, "aggregate inputs");
   if (ni < 0) return;
   QJ_NEED(env, nk == a->nkeys && ni == a->naggs, "one column per key and per aggregate", );
+  /* keys that are dictEncode codes: the state learns their dictionary at the first update (so
+   * finalize stays codes but merges and exchanges go by string content), and a later batch may not
+   * bring codes of another dictionary */
+  int64_t kh[QE_MAX_KEYS];
+  (void)get_longs(env, keyCols, kh, QE_MAX_KEYS, "key columns");
+  for (int i = 0; i < nk; ++i) {
+    qe_strdict* d = ((qj_col*)(intptr_t)kh[i])->dict;
+    if (a->updates == 0 && d) {
+      QJ_TRY(env, qe_hashagg_bind_key_dict(a->h, i, d), );
+      a->bound[i] = d;
+      a->key_types[i] = QE_TYPE_UTF8; /* finalize decodes through the dictionary */
+    }
+    QJ_NEED(env, d == a->bound[i], "group key codes from another dictionary than the state's first batch", );
+  }
+  ++a->updates;
   if (a->nkeys == 0) /* COUNT(*) of a key-less state counts the batch's rows */
     for (int j = 0; j < ni; ++j)
       if (!in[j].values && a->aggs[j].fn == QE_AGG_COUNT_STAR)
@@ -1100,6 +1120,7 @@ JNIEXPORT void JNICALL Java_NativeEngine_aggUpdateFused(JNIEnv* env, jclass k, j
   if (n < 0) return;
   QJ_NEED(env, n >= s->ncols_min, "the plan reads a column slot beyond the batch's columns", );
   QJ_TRY(env, qe_hashagg_update_fused(a->h, c, n, &s->u.fused), );
+  ++a->updates;
 }
 
 JNIEXPORT jlong JNICALL Java_NativeEngine_aggNumGroups(JNIEnv* env, jclass k, jlong agg) {
@@ -1121,8 +1142,9 @@ JNIEXPORT jlongArray JNICALL Java_NativeEngine_aggFinalize(JNIEnv* env, jclass k
   (void)k;
   qj_agg* a = agg_of(env, agg);
   if (!a) return NULL;
-  int64_t groups = 0;
-  QJ_TRY(env, qe_hashagg_num_groups(a->h, &groups), NULL);
+  int64_t groups = 0, key_bytes[QE_MAX_KEYS] = {0, 0, 0, 0};
+  /* the groups, and the bytes of each Utf8 key's strings (the state decodes its own dictionaries) */
+  QJ_TRY(env, qe_hashagg_finalize_sizes(a->h, &groups, key_bytes), NULL);
   const int n = a->nkeys + a->naggs;
   qj_col* oc[QE_MAX_KEYS + QE_MAX_AGGS] = {0};
   qe_column keys[QE_MAX_KEYS], out[QE_MAX_AGGS];
@@ -1131,7 +1153,8 @@ JNIEXPORT jlongArray JNICALL Java_NativeEngine_aggFinalize(JNIEnv* env, jclass k
     const int is_key = i < a->nkeys;
     const int32_t t = is_key ? a->key_types[i] : agg_out_type(&a->aggs[i - a->nkeys]);
     const int fn = is_key ? 0 : a->aggs[i - a->nkeys].fn;
-    oc[i] = col_new(env, a->ctx, t, groups, 0, is_key || (fn != QE_AGG_COUNT && fn != QE_AGG_COUNT_STAR));
+    oc[i] = col_new(env, a->ctx, t, groups, is_key ? key_bytes[i] : 0,
+                    is_key || (fn != QE_AGG_COUNT && fn != QE_AGG_COUNT_STAR));
     if (!oc[i]) st = QE_ERR_OOM;
     else if (is_key) keys[i] = oc[i]->c;
     else out[i - a->nkeys] = oc[i]->c;
@@ -1155,23 +1178,16 @@ JNIEXPORT jlongArray JNICALL Java_NativeEngine_aggFinalize(JNIEnv* env, jclass k
 }
 
 /* main()'s partial -> final merge inside one process (K:1314-1325): every group of `partial`
- * is merged into `owner` (combine semantics per aggregate). */
+ * is merged into `owner` (combine semantics per aggregate). Utf8 / key-tuple keyed states merge by
+ * key CONTENT (qe_hashagg_merge re-encodes the partial's keys into the owner's dictionaries), so two
+ * partitions whose dictionaries number the same string differently still meet in one group. */
 JNIEXPORT void JNICALL Java_NativeEngine_aggMergeInto(JNIEnv* env, jclass k, jlong owner, jlong partial) {
   (void)k;
   qj_agg* o = agg_of(env, owner);
   qj_agg* p = o ? agg_of(env, partial) : NULL;
   if (!p) return;
   QJ_NEED(env, o->ctx == p->ctx, "owner and partial must share a ctx", );
-  int64_t cnt = 0, rb = 0;
-  QJ_TRY(env, qe_hashagg_export_counts(p->h, 1, &cnt), );
-  if (!cnt) return;
-  QJ_TRY(env, qe_hashagg_record_bytes(p->h, &rb), );
-  void* buf = NULL;
-  QJ_TRY(env, qe_device_alloc(p->ctx, (size_t)(cnt * rb), &buf), );
-  int st = qe_hashagg_export(p->h, 1, buf);
-  if (st == QE_OK) st = qe_hashagg_import(o->h, buf, cnt);
-  qe_device_free(p->ctx, buf); /* stream-ordered: the import is queued before the block's reuse */
-  if (st != QE_OK) throw_status(env, st);
+  QJ_TRY(env, qe_hashagg_merge(o->h, p->h), );
 }
 
 /* Device time (ms) of the last update's aggregation kernels. */
@@ -1284,6 +1300,7 @@ JNIEXPORT jlong JNICALL Java_NativeEngine_dictEncode(JNIEnv* env, jclass k, jlon
     throw_status(env, st);
     return 0;
   }
+  out->dict = (qe_strdict*)(intptr_t)dict;
   return (jlong)(intptr_t)out;
 }
 

@@ -20,23 +20,6 @@ def output_type(fn: int, input_type: int) -> int:
 _KEY_BITS = {N.TYPE_INT32: 32, N.TYPE_DATE32: 32, N.TYPE_UINT8: 8}
 
 
-def _device_column(ctx, type_id: int, vals, valid) -> DeviceColumn:
-    """DeviceColumn from int64 device values (narrowed to `type_id`) and a bool validity tensor."""
-    import torch
-
-    from .columnar import bitmap_bytes
-
-    n = vals.numel()
-    dt = {N.TYPE_INT32: torch.int32, N.TYPE_DATE32: torch.int32, N.TYPE_UINT8: torch.uint8,
-          N.TYPE_INT64: torch.int64}[type_id]
-    v = vals.to(dt).contiguous() if n else torch.zeros(1, dtype=dt, device=vals.device)
-    bits = torch.zeros(max(bitmap_bytes(n), 4) * 8, dtype=torch.uint8, device=vals.device)
-    bits[:n] = valid.to(torch.uint8)
-    w = torch.tensor([1, 2, 4, 8, 16, 32, 64, 128], dtype=torch.uint8, device=vals.device)
-    vb = (bits.view(-1, 8) * w).sum(dim=1).to(torch.uint8)
-    return DeviceColumn(type_id, n, v, vb, None, ctx)
-
-
 def packable(key_types) -> bool:
     """Whether qe_hashagg packs these keys itself (one int64/fp64 key, or narrow keys whose values
     plus null bits fit 63 bits — qe_hashagg_create's rule)."""
@@ -76,9 +59,12 @@ def _trim(c: DeviceColumn, n: int) -> DeviceColumn:
     """The first n rows of a carved output column (views of its buffers)."""
     from .columnar import bitmap_bytes
 
-    v = c.values[: max(n, 1)]
     vb = c.validity[: max(bitmap_bytes(n), 4)] if c.validity is not None else None
-    return DeviceColumn(c.type, n, v, vb, None, c.ctx)
+    if c.type == N.TYPE_UTF8:
+        return DeviceColumn(c.type, n, c.values, vb, c.offsets[: n + 1], c.ctx)
+    if c.type == N.TYPE_BOOL:
+        return DeviceColumn(c.type, n, c.values[: max(bitmap_bytes(n), 4)], vb, None, c.ctx)
+    return DeviceColumn(c.type, n, c.values[: max(n, 1)], vb, None, c.ctx)
 
 
 def _order_for_reader(ctx: Context) -> None:
@@ -93,17 +79,20 @@ def _order_for_reader(ctx: Context) -> None:
 
 
 def dictionary_keys(key_types) -> Optional[int]:
-    """None when qe_hashagg groups by these keys directly; otherwise the number of device key
-    columns the dictionaries turn them into (UTF-8 keys -> one int32 code each; a key set that
-    does not pack -> one tuple code)."""
+    """None when qe_hashagg groups by these keys directly; otherwise the column slots a fused update
+    adds for them: the key columns themselves (their codes take the UTF-8 slots in place), plus one
+    for key-tuple codes when the coded keys still do not pack into 63 bits."""
     member = [N.TYPE_INT32 if t == N.TYPE_UTF8 else t for t in key_types]
+    if len(key_types) == 1 and key_types[0] == N.TYPE_UTF8:
+        member = [N.TYPE_INT64]  # a lone UTF-8 key: wide codes
     if not packable(member):
-        return 1
-    return len(member) if N.TYPE_UTF8 in key_types else None
+        return len(key_types) + 1
+    return len(key_types) if N.TYPE_UTF8 in key_types else None
 
 
 class HashAggregateState:
-    """Owns one qe_hashagg. Keys: ``key_types``; aggregates: (fn, input_type) pairs."""
+    """Owns one qe_hashagg. Keys: ``key_types`` (UTF-8 and key lists that do not pack included: the
+    C state keeps their dictionaries); aggregates: (fn, input_type) pairs."""
 
     def __init__(self, ctx: Context, key_types: Sequence[int], aggs: Sequence[Tuple[int, int]],
                  expected_groups: int = 1024, async_update: bool = False, deterministic: bool = False,
@@ -116,36 +105,25 @@ class HashAggregateState:
         run, like the reference's ordered row loop with exact arithmetic); ``deterministic`` names
         that default (QE_HASHAGG_DETERMINISTIC). ``fast_fp64``: plain fp64 atomics instead
         (QE_HASHAGG_FAST_FP64), without the 1e-9 guarantee for cancelling groups."""
-        from .strdict import StringDictionary
-
         self.ctx = ctx
         self.expected_groups = int(expected_groups)
         self.key_types = list(key_types)
         self.aggs = [(int(f), int(t)) for f, t in aggs]
-        # UTF-8 keys: grouped by their dictionary code, decoded in finalize. A lone UTF-8 key takes
-        # wide INT64 codes (keys of up to 7 bytes packed in place, no dictionary traffic); in a
-        # key set, INT32 codes keep the set packable into 63 bits
-        wide = len(self.key_types) == 1
-        self.dicts = {i: StringDictionary(ctx, expected_groups, wide=wide) for i, t in enumerate(self.key_types)
-                      if t == N.TYPE_UTF8}
-        self.member_types = [self.dicts[i].code_type if t == N.TYPE_UTF8 else t for i, t in enumerate(self.key_types)]
-        # key sets that do not pack into 63 bits group by one code per distinct key tuple
-        self.tuple_dict = None
-        if not packable(self.member_types):
-            if len(self.member_types) > N.MAX_KEYS:
-                raise N.IllegalStateException(N.QE_ERR_UNSUPPORTED, f"at most {N.MAX_KEYS} group keys")
-            self.tuple_dict = StringDictionary(ctx, expected_groups)
-        self.device_key_types = [N.TYPE_INT32] if self.tuple_dict is not None else list(self.member_types)
-        kt = (N.C.c_int32 * max(1, len(self.device_key_types)))(*self.device_key_types)
+        kt = (N.C.c_int32 * max(1, len(self.key_types)))(*self.key_types)
         ad = (N.QeAggDesc * max(1, len(self.aggs)))(*[N.QeAggDesc(f, t) for f, t in self.aggs])
         h = N.C.c_void_p()
-        N.check(N.lib().qe_hashagg_create_ex(ctx.handle, len(self.device_key_types), kt, len(self.aggs), ad,
+        N.check(N.lib().qe_hashagg_create_ex(ctx.handle, len(self.key_types), kt, len(self.aggs), ad,
                                              int(expected_groups),
                                              (N.HASHAGG_DETERMINISTIC if deterministic else 0) |
                                              (N.HASHAGG_FAST_FP64 if fast_fp64 else 0),
                                              N.C.byref(h)))
         self.deterministic = not fast_fp64
         self.handle = h
+        kind, nd = N.C.c_int32(), N.C.c_int32()
+        dt = (N.C.c_int32 * N.MAX_KEYS)()
+        N.check(N.lib().qe_hashagg_key_layout(h, N.C.byref(kind), N.C.byref(nd), dt))
+        self.key_layout = kind.value  # 0: raw key words, 1: string codes, 2: key-tuple codes
+        self.device_key_types = list(dt)[: nd.value]
         self._out_rows = max(1, 2 * self.expected_groups)  # finalize's first output sizing guess
         self.async_update = bool(async_update)
         self._held = None  # async: the last update's columns, alive until the state settles it
@@ -153,10 +131,6 @@ class HashAggregateState:
             N.check(N.lib().qe_hashagg_set_async(h, 1))
 
     def close(self) -> None:
-        for d in getattr(self, "dicts", {}).values():
-            d.close()
-        if getattr(self, "tuple_dict", None) is not None:
-            self.tuple_dict.close()
         if getattr(self, "handle", None) is not None:
             N.lib().qe_hashagg_destroy(self.handle)
             self.handle = None
@@ -167,19 +141,25 @@ class HashAggregateState:
         except Exception:
             pass
 
-    # ---- updates --------------------------------------------------------------------------------
-    def device_keys(self, keys: Sequence[DeviceColumn]) -> List[DeviceColumn]:
-        """The key columns qe_hashagg groups by: dictionary codes for UTF-8 keys / key tuples."""
-        keys = [self.dicts[i].encode(k) if i in self.dicts else k for i, k in enumerate(keys)]
-        if self.tuple_dict is not None:
-            keys = [self.tuple_dict.encode_tuple(keys)]
-        return keys
+    def bind_key_dict(self, key: int, dictionary) -> None:
+        """Key `key` (INT32, or a lone INT64 key of wide codes) takes codes the caller encodes with
+        `dictionary` (kquery.strdict.StringDictionary): the state decodes through it at finalize
+        (the key comes out as UTF-8) and merges / exchanges by content (qe_hashagg_bind_key_dict)."""
+        N.check(N.lib().qe_hashagg_bind_key_dict(self.handle, int(key), dictionary.handle))
+        self.key_types[key] = N.TYPE_UTF8
+        self._bound = getattr(self, "_bound", []) + [dictionary]  # it must outlive the state
+        self.key_layout = 1
 
+    @property
+    def keyed_by_dictionary(self) -> bool:
+        """The table groups by dictionary codes local to this state: partials move by key content."""
+        return self.key_layout != 0
+
+    # ---- updates --------------------------------------------------------------------------------
     def update(self, keys: Sequence[DeviceColumn], inputs: Sequence[Optional[DeviceColumn]],
                mask: Optional[DeviceColumn] = None) -> None:
-        """A COUNT(*) input may be any column of the batch: with no keys and no other inputs its
-        length is the row count (qe_hashagg_update)."""
-        keys = self.device_keys(keys)
+        """Keys as declared (UTF-8 columns included). A COUNT(*) input may be any column of the batch:
+        with no keys and no other inputs its length is the row count (qe_hashagg_update)."""
         kc = (N.QeColumn * max(1, len(keys)))(*[k.as_c() for k in keys])
         ic = (N.QeColumn * max(1, len(self.aggs)))(
             *[(x.as_c() if x is not None else N.QeColumn()) for x in inputs])
@@ -190,21 +170,20 @@ class HashAggregateState:
 
     def update_fused(self, cols: Sequence[DeviceColumn], spec: N.QeFusedSpec,
                      key_cols: Optional[Sequence[DeviceColumn]] = None) -> None:
-        """Dictionary-keyed states take the original key columns in `key_cols`: they are encoded
-        (over every row; codes of rows the predicate drops never form a group) and their codes
-        join the fused launch as extra column slots after `cols`."""
+        """Dictionary-keyed states take the declared key columns in `key_cols`: they join the launch
+        as extra column slots after `cols` (the C state encodes them; codes of rows the predicate
+        drops never form a group)."""
         cols = list(cols)
         if self.keyed_by_dictionary:
             if key_cols is None:
                 raise N.IllegalStateException(N.QE_ERR_UNSUPPORTED,
                                               "fused update with dictionary-encoded keys needs the key columns")
-            codes = self.device_keys(key_cols)
-            if len(cols) + len(codes) > N.MAX_COLS:
+            if len(cols) + dictionary_keys(self.key_types) > N.MAX_COLS:
                 raise N.IllegalStateException(N.QE_ERR_UNSUPPORTED, f"fused plan takes at most {N.MAX_COLS} columns")
             spec = N.QeFusedSpec.from_buffer_copy(spec)
-            for k in range(len(codes)):
+            for k in range(len(key_cols)):
                 spec.key_cols[k] = len(cols) + k
-            cols += codes
+            cols += list(key_cols)
         cc = (N.QeColumn * len(cols))(*[c.as_c() for c in cols])
         N.check(N.lib().qe_hashagg_update_fused(self.handle, cc, len(cols), N.C.byref(spec)))
         if self.async_update:  # a pending update may re-read its columns when it is settled
@@ -254,28 +233,51 @@ class HashAggregateState:
         """Carve the next finalize's output columns now (at the last result's size), so that the
         host work is done before a call that waits for the device (kquery.exchange calls it
         before the import's read-back)."""
-        if getattr(self, "_stash", None) is None:
+        if getattr(self, "_stash", None) is None and N.TYPE_UTF8 not in self.key_types:
             self._stash = self._carve_c(self._out_rows)
 
-    def _carve_c(self, rows: int):
-        specs = ([(t, True) for t in self.device_key_types] +
+    def _carve_c(self, rows: int, key_bytes=None):
+        import torch
+
+        from .columnar import bitmap_bytes
+
+        specs = ([(t, True) for t in self.key_types if t not in (N.TYPE_UTF8, N.TYPE_BOOL)] +
                  [(output_type(f, t), f not in (N.AGG_COUNT, N.AGG_COUNT_STAR)) for f, t in self.aggs])
-        nk = len(self.device_key_types)
-        cols = _carve(self.ctx, rows, specs)
+        fixed = _carve(self.ctx, rows, specs) if specs else []
+        dev = self.ctx.torch_device
+        keys, it = [], iter(fixed)
+        for k, t in enumerate(self.key_types):
+            if t == N.TYPE_UTF8:  # offsets, values of the size finalize_sizes reported, validity
+                nb = int(key_bytes[k]) if key_bytes is not None else 7 * rows
+                keys.append(DeviceColumn(N.TYPE_UTF8, rows, torch.empty(max(1, nb), dtype=torch.uint8, device=dev),
+                                         torch.empty(max(bitmap_bytes(rows), 4), dtype=torch.uint8, device=dev),
+                                         torch.empty(rows + 1, dtype=torch.int32, device=dev), self.ctx))
+            elif t == N.TYPE_BOOL:
+                keys.append(DeviceColumn.empty(N.TYPE_BOOL, rows, True, ctx=self.ctx))
+            else:
+                keys.append(next(it))
+        cols = keys + list(it)
+        nk = len(self.key_types)
         kc = (N.QeColumn * max(1, nk))(*[k.as_c() for k in cols[:nk]])
         ac = (N.QeColumn * max(1, len(cols) - nk))(*[a.as_c() for a in cols[nk:]])
         return rows, cols, kc, ac
 
     def finalize(self) -> Tuple[List[DeviceColumn], List[DeviceColumn]]:
-        """One output batch (Main.kt:635-650): key columns, aggregate columns.
+        """One output batch (Main.kt:635-650): key columns (as declared, UTF-8 included), aggregate
+        columns.
 
         The outputs are carved before the call (or earlier, prepare_output), at the size of the
         last result (or 2x the expected groups), so that the host work is done before
         qe_hashagg_finalize waits for the aggregation; a larger result (QE_ERR_CAPACITY, with the
-        exact count) carves again."""
-        nk = len(self.device_key_types)
+        exact count) carves again. UTF-8 keys are sized first (qe_hashagg_finalize_sizes)."""
+        nk = len(self.key_types)
         out = N.C.c_int64(-1)
         stash, self._stash = getattr(self, "_stash", None), None
+        if N.TYPE_UTF8 in self.key_types:
+            g = N.C.c_int64()
+            kb = (N.C.c_int64 * max(1, nk))()
+            N.check(N.lib().qe_hashagg_finalize_sizes(self.handle, N.C.byref(g), kb))
+            stash = self._carve_c(max(1, g.value), list(kb))
         while True:
             rows, cols, kc, ac = stash if stash is not None else self._carve_c(self._out_rows)
             stash = None
@@ -290,11 +292,7 @@ class HashAggregateState:
         _order_for_reader(self.ctx)
         if g != rows:
             cols = [_trim(c, g) for c in cols]
-        keys, aggs = cols[:nk], cols[nk:]
-        if self.tuple_dict is not None:
-            keys = self.tuple_dict.decode_tuple(keys[0], self.member_types)
-        keys = [self.dicts[i].decode(k, trusted=True) if i in self.dicts else k for i, k in enumerate(keys)]
-        return keys, aggs
+        return cols[:nk], cols[nk:]
 
     # ---- partial records (exchange) -----------------------------------------------------------------
     def record_bytes(self) -> int:
@@ -302,120 +300,14 @@ class HashAggregateState:
         N.check(N.lib().qe_hashagg_record_bytes(self.handle, N.C.byref(n)))
         return n.value
 
-    def _check_exportable(self) -> None:
-        if self.dicts or self.tuple_dict is not None:  # codes are local to this state's dictionary
-            raise N.IllegalStateException(N.QE_ERR_UNSUPPORTED,
-                                          "dictionary-keyed partials move by key content: use "
-                                          "kquery.exchange.exchange_partials (export_all / import_keyed)")
-
-    # ---- dictionary-keyed states: keys travel as their content (kquery/exchange.py) -----------------
-    @property
-    def keyed_by_dictionary(self) -> bool:
-        return bool(self.dicts) or self.tuple_dict is not None
-
-    def _wide_key(self) -> bool:
-        """One INT64 device key (a lone UTF-8 key's wide codes): records carry it whole, with the
-        null group flagged in the record's second word, instead of packed narrow keys."""
-        return self.device_key_types == [N.TYPE_INT64]
-
-    def _packing(self):
-        """(shift, nullbit, width) per device key, as qe_hashagg_create packs narrow keys."""
-        if self._wide_key():
-            return []
-        out, bit = [], 0
-        for t in self.device_key_types:
-            w = _KEY_BITS[t]
-            out.append((bit, bit + w, w))
-            bit += w + 1
-        return out
-
-    def record_key_columns(self, records, n: int) -> List[DeviceColumn]:
-        """The original key columns (UTF8 included) of `n` exported records of this state."""
-        import torch
-
-        if n == 0:
-            return self._empty_keys()
-        rec = records[: n * self.record_bytes()].view(torch.int64).view(n, -1)
-        packed = rec[:, 0]
-        members = []
-        if self._wide_key():  # one INT64 key (wide string codes): the key word and the null flag
-            members.append(_device_column(self.ctx, N.TYPE_INT64, packed, rec[:, 1] == 0))
-        for (shift, nullbit, w), t in zip(self._packing(), self.device_key_types):
-            vals = (packed >> shift) & ((1 << w) - 1)
-            valid = ((packed >> nullbit) & 1) == 0
-            members.append(_device_column(self.ctx, t, vals, valid))
-        if self.tuple_dict is not None:
-            members = self.tuple_dict.decode_tuple(members[0], self.member_types)
-        return [self.dicts[i].decode(k) if i in self.dicts else k for i, k in enumerate(members)]
-
-    def _empty_keys(self) -> List[DeviceColumn]:
-        import torch
-
-        out = []
-        for t in self.key_types:
-            if t == N.TYPE_UTF8:
-                out.append(DeviceColumn(N.TYPE_UTF8, 0, torch.zeros(1, dtype=torch.uint8, device=self.ctx.torch_device),
-                                        None, torch.zeros(1, dtype=torch.int32, device=self.ctx.torch_device), self.ctx))
-            else:
-                out.append(DeviceColumn.empty(t, 0, True, ctx=self.ctx))
-        return out
-
-    def packed_keys(self, key_cols: Sequence[DeviceColumn]):
-        """(int64 device key words, null-group flags) of rows given as original key columns
-        (encodes new strings / tuples into this state's dictionaries)."""
-        import torch
-
-        members = [self.dicts[i].encode(k) if i in self.dicts else k for i, k in enumerate(key_cols)]
-        if self.tuple_dict is not None:
-            members = [self.tuple_dict.encode_tuple(members)]
-        n = members[0].length
-        packed = torch.zeros(n, dtype=torch.int64, device=self.ctx.torch_device)
-        knull = torch.zeros(n, dtype=torch.int64, device=self.ctx.torch_device)
-        if self._wide_key():
-            m = members[0]
-            valid = torch.from_numpy(m.valid_mask()).to(self.ctx.torch_device)
-            packed = torch.where(valid, m.values[:n].to(torch.int64), packed)
-            knull = (~valid).to(torch.int64)
-        for (shift, nullbit, w), m in zip(self._packing(), members):
-            vals = m.values[:n].to(torch.int64) & ((1 << w) - 1)
-            valid = torch.from_numpy(m.valid_mask()).to(self.ctx.torch_device)
-            packed |= torch.where(valid, vals << shift, torch.zeros_like(vals)) | ((~valid).to(torch.int64) << nullbit)
-        return packed, knull
-
-    def import_keyed(self, records, n: int, key_cols: Sequence[DeviceColumn]) -> None:
-        """Import records whose keys come from another state: rewrite their key field from the
-        key columns' content, then merge (qe_hashagg_import)."""
-        import torch
-
-        if n == 0:
-            return
-        rec = records[: n * self.record_bytes()].view(torch.int64).view(n, -1)
-        rec[:, 0], rec[:, 1] = self.packed_keys(key_cols)  # (narrow packed keys: null flag 0)
-        N.check(N.lib().qe_hashagg_import(self.handle, N.C.c_void_p(records.data_ptr()), int(n)))
-
-    def export_all(self):
-        """All partial records, unbucketed: (uint8 device tensor, count)."""
-        import torch
-
-        counts = self._export_counts_raw(1)
-        rb = self.record_bytes()
-        buf = torch.empty(max(1, counts[0] * rb), dtype=torch.uint8, device=self.ctx.torch_device)
-        N.check(N.lib().qe_hashagg_export(self.handle, 1, N.C.c_void_p(buf.data_ptr())))
-        return buf, counts[0]
-
-    def _export_counts_raw(self, nparts: int) -> List[int]:
-        arr = (N.C.c_int64 * nparts)()
-        N.check(N.lib().qe_hashagg_export_counts(self.handle, nparts, arr))
-        return list(arr)
-
     def export_counts(self, nparts: int) -> List[int]:
-        self._check_exportable()
         arr = (N.C.c_int64 * nparts)()
         N.check(N.lib().qe_hashagg_export_counts(self.handle, nparts, arr))
         return list(arr)
 
     def export(self, nparts: int):
-        """-> (uint8 device tensor of records, per-partition counts)."""
+        """-> (uint8 device tensor of records, per-partition counts). Raw key words: refused for a
+        dictionary-keyed state (export_keyed)."""
         import torch
 
         counts = self.export_counts(nparts)
@@ -432,7 +324,6 @@ class HashAggregateState:
         no host synchronisation, so the all-to-all can follow the aggregation kernel directly."""
         import torch
 
-        self._check_exportable()
         buf = torch.empty(nparts * self.slot_bytes(slot_records), dtype=torch.uint8, device=self.ctx.torch_device)
         N.check(N.lib().qe_hashagg_export_slots(self.handle, int(nparts), int(slot_records),
                                                 N.C.c_void_p(buf.data_ptr())))
@@ -441,14 +332,45 @@ class HashAggregateState:
     def import_slots(self, slots, nslots: int, slot_records: int) -> Optional[int]:
         """Merges received slots; returns the records merged, or None when some sender's
         partition exceeded the slot capacity (nothing merged; the same on every rank)."""
-        self._check_exportable()
         mx, n = N.C.c_int64(), N.C.c_int64()
         N.check(N.lib().qe_hashagg_import_slots(self.handle, N.C.c_void_p(slots.data_ptr()), int(nslots),
                                                 int(slot_records), N.C.byref(mx), N.C.byref(n)))
         return None if mx.value > slot_records else n.value
 
     def import_records(self, records, nrecords: int) -> None:
-        self._check_exportable()
         if nrecords == 0:
             return
         N.check(N.lib().qe_hashagg_import(self.handle, N.C.c_void_p(records.data_ptr()), int(nrecords)))
+
+    # ---- partials by key content (every state; the only form for dictionary-keyed ones) -------------
+    def export_keyed(self, nparts: int):
+        """-> (uint8 device tensor of `nparts` keyed blocks back to back, their sizes)
+        (qe_hashagg_export_keyed_sizes + qe_hashagg_export_keyed)."""
+        import torch
+
+        sizes = (N.C.c_int64 * nparts)()
+        N.check(N.lib().qe_hashagg_export_keyed_sizes(self.handle, int(nparts), sizes))
+        sizes = list(sizes)
+        buf = torch.empty(max(1, sum(sizes)), dtype=torch.uint8, device=self.ctx.torch_device)
+        N.check(N.lib().qe_hashagg_export_keyed(self.handle, int(nparts), N.C.c_void_p(buf.data_ptr())))
+        return buf, sizes
+
+    def import_keyed(self, blocks, sizes: Sequence[int]) -> int:
+        """Merges keyed blocks (packed back to back, `sizes` bytes each) re-encoding their keys into
+        this state's dictionaries; returns the records merged."""
+        import numpy as np
+
+        n = len(sizes)
+        arr = (N.C.c_int64 * max(1, n))(*[int(x) for x in sizes])
+        N.check(N.lib().qe_hashagg_import_keyed(self.handle, N.C.c_void_p(blocks.data_ptr()), n, arr))
+        recs, off = 0, 0
+        for sz in sizes:  # each block's header word 1 is its record count
+            if sz:
+                recs += int(np.frombuffer(blocks[off + 8: off + 16].cpu().numpy().tobytes(), dtype=np.int64)[0])
+            off += int(sz)
+        return recs
+
+    def merge(self, other: "HashAggregateState") -> None:
+        """Every group of `other` merged into this state (qe_hashagg_merge: by key content when
+        either is dictionary-keyed) — main()'s partial -> final merge (Main.kt:1314-1325)."""
+        N.check(N.lib().qe_hashagg_merge(self.handle, other.handle))

@@ -251,9 +251,10 @@ class DeviceColumn(ColumnVector):
 
     # ---- C ABI view ------------------------------------------------------------------------
     def as_c(self) -> N.QeColumn:
+        ml = self.max_len if self.type == N.TYPE_UTF8 and self.max_len is not None else 0
         return N.QeColumn(
             self.type,
-            0,
+            int(min(ml, (1 << 31) - 1)),
             self.length,
             self.validity.data_ptr() if self.validity is not None else None,
             self.values.data_ptr() if self.values is not None else None,

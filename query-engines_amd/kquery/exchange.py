@@ -56,98 +56,20 @@ def _a2a_bytes(chunks: List[torch.Tensor], group=None) -> Tuple[torch.Tensor, Li
     return (out.to(dev) if stage else out), rs
 
 
-def _split_rows(col, part: torch.Tensor, world: int):
-    """Per destination rank: (valid u8 per row, value bytes, UTF-8 lengths i32 or None) of `col`."""
-    import numpy as np
-
-    from . import native as N
-    from .columnar import DeviceColumn
-
-    n = col.length
-    valid = torch.from_numpy(col.valid_mask().astype(np.uint8)).to(part.device)
-    out = []
-    for p in range(world):
-        idx = torch.nonzero(part[:n] == p).flatten()
-        if col.type == N.TYPE_UTF8:
-            offs = col.offsets[: n + 1].to(torch.int64)
-            lens = (offs[1:] - offs[:-1])[idx]
-            starts = offs[:-1][idx]
-            # gather the bytes of the selected rows (row order kept)
-            if idx.numel():
-                rep = torch.repeat_interleave(starts - torch.cumsum(lens, 0) + lens, lens)
-                pos = rep + torch.arange(int(lens.sum()), device=part.device)
-                data = col.values[pos] if pos.numel() else torch.empty(0, dtype=torch.uint8, device=part.device)
-            else:
-                data = torch.empty(0, dtype=torch.uint8, device=part.device)
-            out.append((valid[idx], data, lens.to(torch.int32)))
-        elif col.type == N.TYPE_BOOL:  # one byte per row on the wire
-            bits = (col.values[(idx >> 3)] >> (idx & 7).to(torch.uint8)) & 1
-            out.append((valid[idx], bits.to(torch.uint8), None))
-        else:
-            vals = col.values[:n][idx]
-            out.append((valid[idx], vals.contiguous().view(torch.uint8), None))
-    return out
-
-
-def _join_rows(ctx, type_id: int, valid: torch.Tensor, data: torch.Tensor, lens: Optional[torch.Tensor]):
-    """Received per-row arrays -> DeviceColumn (validity bitmap, UTF-8 offsets rebuilt)."""
-    from . import native as N
-    from .columnar import DeviceColumn, _torch_dtype, bitmap_bytes
-
-    n = valid.numel()
-    bits = torch.zeros(max(bitmap_bytes(n), 4) * 8, dtype=torch.uint8, device=valid.device)
-    bits[:n] = valid
-    w = torch.tensor([1, 2, 4, 8, 16, 32, 64, 128], dtype=torch.uint8, device=valid.device)
-    vb = (bits.view(-1, 8) * w).sum(dim=1).to(torch.uint8)
-    if type_id == N.TYPE_UTF8:
-        offs = torch.zeros(n + 1, dtype=torch.int32, device=valid.device)
-        if n:
-            offs[1:] = torch.cumsum(lens.to(torch.int64), 0).to(torch.int32)
-        vals = data if data.numel() else torch.zeros(1, dtype=torch.uint8, device=valid.device)
-        return DeviceColumn(N.TYPE_UTF8, n, vals, vb, offs, ctx)
-    if type_id == N.TYPE_BOOL:
-        b = torch.zeros(max(bitmap_bytes(n), 4) * 8, dtype=torch.uint8, device=valid.device)
-        b[:n] = data
-        return DeviceColumn(N.TYPE_BOOL, n, (b.view(-1, 8) * w).sum(dim=1).to(torch.uint8), vb, None, ctx)
-    vals = data.view(_torch_dtype(type_id)) if n else torch.zeros(1, dtype=_torch_dtype(type_id), device=valid.device)
-    return DeviceColumn(type_id, n, vals, vb, None, ctx)
-
-
 def exchange_keyed_partials(partial, owner, group: Optional[dist.ProcessGroup] = None) -> int:
-    """Dictionary-keyed partials (UTF-8 or composite keys): codes are local to a state, so rows
-    travel with their key CONTENT. Each record's owner is qe_hash_partition of the decoded key
-    columns; records and per-row key data move in all-to-alls; the owner re-encodes the keys
-    into its own dictionaries and imports (HashAggregateState.import_keyed)."""
-    from . import native as N
-
+    """Dictionary-keyed partials (UTF-8 or composite keys): codes are local to a state, so groups
+    travel with their key CONTENT, through the same C entry points a JNI host uses:
+    qe_hashagg_export_keyed (records + key values, routed by a content hash of the keys), one
+    all-to-all of the blocks, qe_hashagg_import_keyed (the owner re-encodes the keys into its own
+    dictionaries). Returns the records this rank merged."""
     world = dist.get_world_size(group)
-    ctx = partial.ctx
-    recs, n = partial.export_all()
-    rb = partial.record_bytes()
-    keys = partial.record_key_columns(recs, n)
-    part = torch.zeros(max(1, n), dtype=torch.int32, device=ctx.torch_device)
-    if n:
-        kc = (N.QeColumn * len(keys))(*[k.as_c() for k in keys])
-        N.check(N.lib().qe_hash_partition(ctx.handle, kc, len(keys), world, N.C.c_void_p(part.data_ptr())))
-    rows = recs[: n * rb].view(n, rb)
-    rec_chunks = []
-    for p in range(world):
-        idx = torch.nonzero(part[:n] == p).flatten()
-        rec_chunks.append(rows[idx].reshape(-1))
-    rrecs, rsz = _a2a_bytes(rec_chunks, group)
-    nrecv = sum(rsz) // rb
-    cols = []
-    for k, t in zip(keys, partial.key_types):
-        per_dest = _split_rows(k, part, world)
-        rvalid, _ = _a2a_bytes([v for v, _, _ in per_dest], group)
-        rdata, _ = _a2a_bytes([d for _, d, _ in per_dest], group)
-        rlens = None
-        if t == N.TYPE_UTF8:
-            rl, _ = _a2a_bytes([ln.contiguous().view(torch.uint8) for _, _, ln in per_dest], group)
-            rlens = rl.view(torch.int32)
-        cols.append(_join_rows(ctx, t, rvalid, rdata, rlens))
-    owner.import_keyed(rrecs, nrecv, cols)
-    return nrecv
+    blocks, sizes = partial.export_keyed(world)
+    chunks, off = [], 0
+    for sz in sizes:
+        chunks.append(blocks[off: off + sz])
+        off += sz
+    rblocks, rsz = _a2a_bytes(chunks, group)
+    return owner.import_keyed(rblocks, rsz)
 
 
 def all_to_all_slots(send: torch.Tensor, group: Optional[dist.ProcessGroup] = None) -> torch.Tensor:
@@ -173,7 +95,7 @@ def exchange_partials(partial, owner, group: Optional[dist.ProcessGroup] = None,
     before it. If any rank had more groups for one owner than a slot holds, every rank sees it in
     the slot headers and all of them fall back to the variable-size exchange (counts all-to-all,
     then records)."""
-    if getattr(partial, "keyed_by_dictionary", False):
+    if getattr(partial, "keyed_by_dictionary", False) or getattr(owner, "keyed_by_dictionary", False):
         return exchange_keyed_partials(partial, owner, group)
     world = dist.get_world_size(group)
     cap = int(slot_records or partial.slot_capacity(world))
@@ -229,7 +151,6 @@ def exchange_partials_native(partial, owner, comm: NativeComm, slot_records: int
     this rank merged."""
     from . import native as N
 
-    partial._check_exportable()
     owner.prepare_output()  # host work of the owner's finalize, before the import's read-back
     n = N.C.c_int64()
     N.check(N.lib().qe_hashagg_exchange(comm.handle, partial.handle, owner.handle, int(slot_records), N.C.byref(n)))

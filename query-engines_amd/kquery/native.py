@@ -97,7 +97,7 @@ _ERR_CLASS = {
 class QeColumn(C.Structure):
     _fields_ = [
         ("type", C.c_int32),
-        ("reserved", C.c_int32),
+        ("max_len", C.c_int32),  # UTF8: the producer's bound on value lengths (0: unknown)
         ("length", C.c_int64),
         ("validity", C.c_void_p),
         ("values", C.c_void_p),
@@ -189,6 +189,7 @@ _I64P = C.POINTER(C.c_int64)
 _COLP = C.POINTER(QeColumn)
 _OPP = C.POINTER(QeOperand)
 SLOT_HEADER = 64  # QE_SLOT_HEADER: bytes before a slot's records
+KEYED_HEADER = 128  # QE_KEYED_HEADER: bytes before a keyed block's sections
 GLOBAL_PARTIAL_BYTES = 128  # QE_GLOBAL_PARTIAL_BYTES
 
 SIGNATURES = [
@@ -235,6 +236,13 @@ SIGNATURES = [
     ("qe_hashagg_export_slots", C.c_int, [_P, C.c_int32, C.c_int64, _P]),
     ("qe_hashagg_import_slots", C.c_int, [_P, _P, C.c_int32, C.c_int64, _I64P, _I64P]),
     ("qe_hashagg_slot_capacity", C.c_int, [_P, C.c_int32, _I64P]),
+    ("qe_hashagg_finalize_sizes", C.c_int, [_P, _I64P, _I64P]),
+    ("qe_hashagg_export_keyed_sizes", C.c_int, [_P, C.c_int32, _I64P]),
+    ("qe_hashagg_export_keyed", C.c_int, [_P, C.c_int32, _P]),
+    ("qe_hashagg_import_keyed", C.c_int, [_P, _P, C.c_int32, _I64P]),
+    ("qe_hashagg_merge", C.c_int, [_P, _P]),
+    ("qe_hashagg_bind_key_dict", C.c_int, [_P, C.c_int32, _P]),
+    ("qe_hashagg_key_layout", C.c_int, [_P, C.POINTER(C.c_int32), C.POINTER(C.c_int32), C.POINTER(C.c_int32)]),
     ("qe_comm_unique_id", C.c_int, [_P]),
     ("qe_comm_create", C.c_int, [_P, C.c_int32, C.c_int32, _P, C.POINTER(C.c_void_p)]),
     ("qe_comm_destroy", C.c_int, [_P]),

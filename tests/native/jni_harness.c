@@ -793,21 +793,22 @@ static void gpu_cases(void) {
   }
   end(f0);
 
-  /* GROUP BY a Utf8 key (K:620-627): string dictionary codes, decoded at finalize */
+  /* GROUP BY a Utf8 key (K:620-627): the state keeps the dictionary, finalize returns strings; the
+   * same through codes the caller encoded itself (dictEncode: the state binds that dictionary) */
   begin("utf8_group_keys");
   f0 = g_fail;
-  {
+  for (int external = 0; external < 2; ++external) {
     const char* s[] = {"CA", "NY", "CA", "TX", "NY", "CA", NULL};
     const jlong c = utf8_col(ctx, s, 7);
-    const jlong d = OK(Java_NativeEngine_dictCreate(E, K, ctx, 0));
-    const jlong codes = OK(Java_NativeEngine_dictEncode(E, K, ctx, d, c));
-    const jlong agg = OK(Java_NativeEngine_aggCreate(E, K, ctx, INTS(QE_TYPE_INT32), INTS(QE_AGG_COUNT_STAR), INTS(0), 0, 0));
-    OKV(Java_NativeEngine_aggUpdate(E, K, agg, LONGS(codes), LONGS(0), 0));
+    const jlong d = external ? OK(Java_NativeEngine_dictCreate(E, K, ctx, 0)) : 0;
+    const jlong keyc = external ? OK(Java_NativeEngine_dictEncode(E, K, ctx, d, c)) : c;
+    const jlong agg = OK(Java_NativeEngine_aggCreate(E, K, ctx, INTS(external ? QE_TYPE_INT32 : QE_TYPE_UTF8),
+                                                     INTS(QE_AGG_COUNT_STAR), INTS(0), 0, 0));
+    OKV(Java_NativeEngine_aggUpdate(E, K, agg, LONGS(keyc), LONGS(0), 0));
     jlongArray outs = OK(Java_NativeEngine_aggFinalize(E, K, agg));
     if (outs) {
-      const jlong keys = OK(Java_NativeEngine_dictDecode(E, K, ctx, d, LV(outs)[0]));
       jlong n = 0;
-      char** ks = fetch_strings(ctx, keys, &n);
+      char** ks = fetch_strings(ctx, LV(outs)[0], &n);
       uint8_t* v;
       int64_t* cnt = fetch_longs(ctx, LV(outs)[1], &v);
       int seen = 0;
@@ -817,14 +818,87 @@ static void gpu_cases(void) {
         ++seen;
       }
       CHECK(seen == 4, "%d groups (CA, NY, TX, null)", seen);
-      OKV(Java_NativeEngine_columnFree(E, K, keys));
       OKV(Java_NativeEngine_columnFree(E, K, LV(outs)[0]));
       OKV(Java_NativeEngine_columnFree(E, K, LV(outs)[1]));
     }
     OKV(Java_NativeEngine_aggDestroy(E, K, agg));
-    OKV(Java_NativeEngine_columnFree(E, K, codes));
-    OKV(Java_NativeEngine_dictDestroy(E, K, d));
+    if (external) {
+      OKV(Java_NativeEngine_columnFree(E, K, keyc));
+      OKV(Java_NativeEngine_dictDestroy(E, K, d));
+    }
     OKV(Java_NativeEngine_columnFree(E, K, c));
+  }
+  end(f0);
+
+  /* main()'s partial -> final merge with Utf8 keys (K:1309-1325 over K:1336's string key): two
+   * partitions whose dictionaries number the same strings differently (keys longer than 7 bytes,
+   * inserted in different orders), merged by content (aggMergeInto); also for partials keyed by
+   * codes their callers encoded with two different dictionaries */
+  begin("utf8_merge_by_content");
+  f0 = g_fail;
+  for (int external = 0; external < 2; ++external) {
+    const char* s0[] = {"long-key-alpha-1", "beta-long-key-2", "CA", "gamma-key-3", "long-key-alpha-1", NULL};
+    const double x0[] = {1.0, 2.0, 3.0, 4.0, 5.0, 6.0};
+    const char* s1[] = {"gamma-key-3", "delta-key-4", "long-key-alpha-1", "NY", NULL, "CA"};
+    const double x1[] = {10.0, 20.0, 30.0, 40.0, 50.0, 60.0};
+    const char** ss[2] = {s0, s1};
+    const double* xs[2] = {x0, x1};
+    jlong parts[2], cols[2][2], dicts[2] = {0, 0}, codes[2] = {0, 0};
+    for (int q = 0; q < 2; ++q) {
+      cols[q][0] = utf8_col(ctx, ss[q], 6);
+      cols[q][1] = OK(Java_NativeEngine_columnFromDoubles(E, K, ctx, JD(xs[q], 6), NULL));
+      jlong kc = cols[q][0];
+      if (external) {
+        dicts[q] = OK(Java_NativeEngine_dictCreate(E, K, ctx, 0));
+        codes[q] = OK(Java_NativeEngine_dictEncode(E, K, ctx, dicts[q], kc));
+        kc = codes[q];
+      }
+      parts[q] = OK(Java_NativeEngine_aggCreate(E, K, ctx, INTS(external ? QE_TYPE_INT32 : QE_TYPE_UTF8),
+                                                INTS(QE_AGG_SUM, QE_AGG_COUNT_STAR), INTS(QE_TYPE_FLOAT64, 0), 0, 0));
+      OKV(Java_NativeEngine_aggUpdate(E, K, parts[q], LONGS(kc), LONGS(cols[q][1], 0), 0));
+    }
+    const jlong owner = OK(Java_NativeEngine_aggCreate(E, K, ctx, INTS(QE_TYPE_UTF8), INTS(QE_AGG_SUM, QE_AGG_COUNT_STAR),
+                                                       INTS(QE_TYPE_FLOAT64, 0), 0, 0));
+    OKV(Java_NativeEngine_aggMergeInto(E, K, owner, parts[1]));
+    OKV(Java_NativeEngine_aggMergeInto(E, K, owner, parts[0]));
+    /* external: also partition 0's codes (dictionary A) into partition 1's state (dictionary B) */
+    if (external) OKV(Java_NativeEngine_aggMergeInto(E, K, parts[1], parts[0]));
+    const jlong targets[2] = {owner, external ? parts[1] : 0};
+    for (int t = 0; t < 2 && targets[t]; ++t) {
+      jlongArray outs = OK(Java_NativeEngine_aggFinalize(E, K, targets[t]));
+      if (!outs) continue;
+      jlong n = 0;
+      char** ks = fetch_strings(ctx, LV(outs)[0], &n);
+      uint8_t *v1, *v2;
+      double* sum = fetch_doubles(ctx, LV(outs)[1], &v1);
+      int64_t* cnt = fetch_longs(ctx, LV(outs)[2], &v2);
+      const char* names[] = {"long-key-alpha-1", "beta-long-key-2", "CA", "gamma-key-3", "delta-key-4", "NY", NULL};
+      const double wsum[] = {36.0, 2.0, 63.0, 14.0, 20.0, 40.0, 56.0};
+      const int64_t wcnt[] = {3, 1, 2, 2, 1, 1, 2};
+      int seen = 0;
+      for (jlong r = 0; r < n; ++r) {
+        int w = -1;
+        for (int i = 0; i < 7; ++i)
+          if ((!ks[r] && !names[i]) || (ks[r] && names[i] && !strcmp(ks[r], names[i]))) w = i;
+        CHECK(w >= 0, "unexpected group [%s]", ks[r] ? ks[r] : "null");
+        if (w < 0) continue;
+        ++seen;
+        CHECK(sum[r] == wsum[w] && cnt[r] == wcnt[w], "group %s: sum %g count %lld (want %g, %lld)",
+              ks[r] ? ks[r] : "null", sum[r], (long long)cnt[r], wsum[w], (long long)wcnt[w]);
+      }
+      CHECK(seen == 7 && n == 7, "%lld groups, %d expected ones", (long long)n, seen);
+      for (int j = 0; j < 3; ++j) OKV(Java_NativeEngine_columnFree(E, K, LV(outs)[j]));
+    }
+    OKV(Java_NativeEngine_aggDestroy(E, K, owner));
+    for (int q = 0; q < 2; ++q) {
+      OKV(Java_NativeEngine_aggDestroy(E, K, parts[q]));
+      OKV(Java_NativeEngine_columnFree(E, K, cols[q][0]));
+      OKV(Java_NativeEngine_columnFree(E, K, cols[q][1]));
+      if (external) {
+        OKV(Java_NativeEngine_columnFree(E, K, codes[q]));
+        OKV(Java_NativeEngine_dictDestroy(E, K, dicts[q]));
+      }
+    }
   }
   end(f0);
 
@@ -910,13 +984,12 @@ static void gpu_cases(void) {
       const jlong state = OK(Java_NativeEngine_csvColumn(E, K, t, 1));
       const jlong salary = OK(Java_NativeEngine_csvColumn(E, K, t, 2));
       const jlong sal = OK(Java_NativeEngine_castToDouble(E, K, ctx, salary));
-      const jlong d = OK(Java_NativeEngine_dictCreate(E, K, ctx, 0));
-      const jlong codes = OK(Java_NativeEngine_dictEncode(E, K, ctx, d, state));
-      const jlong agg = OK(Java_NativeEngine_aggCreate(E, K, ctx, INTS(QE_TYPE_INT32), INTS(QE_AGG_MAX), INTS(QE_TYPE_FLOAT64), 0, 0));
-      OKV(Java_NativeEngine_aggUpdate(E, K, agg, LONGS(codes), LONGS(sal), 0));
+      /* NativeHashAggregateExec: the Utf8 key column itself (the state keeps the dictionary) */
+      const jlong agg = OK(Java_NativeEngine_aggCreate(E, K, ctx, INTS(QE_TYPE_UTF8), INTS(QE_AGG_MAX), INTS(QE_TYPE_FLOAT64), 0, 0));
+      OKV(Java_NativeEngine_aggUpdate(E, K, agg, LONGS(state), LONGS(sal), 0));
       jlongArray outs = OK(Java_NativeEngine_aggFinalize(E, K, agg));
       if (outs) {
-        const jlong keys = OK(Java_NativeEngine_dictDecode(E, K, ctx, d, LV(outs)[0]));
+        const jlong keys = LV(outs)[0];
         jlong n = 0;
         char** ks = fetch_strings(ctx, keys, &n);
         uint8_t* v;
@@ -934,7 +1007,6 @@ static void gpu_cases(void) {
           }
         }
         CHECK(seen == 2 && n == 2, "groups %lld", (long long)n);
-        OKV(Java_NativeEngine_columnFree(E, K, keys));
         OKV(Java_NativeEngine_columnFree(E, K, LV(outs)[0]));
         OKV(Java_NativeEngine_columnFree(E, K, LV(outs)[1]));
       }
@@ -952,10 +1024,9 @@ static void gpu_cases(void) {
         CHECK(n == 2 && ids[0] && ids[1] && !strcmp(ids[0], "1") && !strcmp(ids[1], "2"), "Uppsala ids");
         OKV(Java_NativeEngine_columnFree(E, K, LV(sel)[0]));
       }
-      const jlong tmp[] = {mca, mup, lca, lup, id, state, salary, sal, codes};
-      for (int i = 0; i < 9; ++i) OKV(Java_NativeEngine_columnFree(E, K, tmp[i]));
+      const jlong tmp[] = {mca, mup, lca, lup, id, state, salary, sal};
+      for (int i = 0; i < 8; ++i) OKV(Java_NativeEngine_columnFree(E, K, tmp[i]));
       OKV(Java_NativeEngine_aggDestroy(E, K, agg));
-      OKV(Java_NativeEngine_dictDestroy(E, K, d));
       OKV(Java_NativeEngine_csvDestroy(E, K, t));
     }
     end(f0);

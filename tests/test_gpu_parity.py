@@ -396,7 +396,7 @@ def test_hashagg_multi_key_too_wide(gpu_ctx):
     st = N.lib().qe_hashagg_create(gpu_ctx.handle, 2, kt, 1, ad, 16, N.C.byref(h))
     assert st == N.QE_ERR_UNSUPPORTED and "66 bits" in N.lib().qe_last_error().decode()
     state = HashAggregateState(gpu_ctx, [N.TYPE_INT32, N.TYPE_DATE32], [(N.AGG_COUNT_STAR, N.TYPE_INT64)], 16)
-    assert state.tuple_dict is not None and state.device_key_types == [N.TYPE_INT32]
+    assert state.key_layout == 2 and state.device_key_types == [N.TYPE_INT32]
 
 
 @pytest.mark.parametrize("types", [(N.TYPE_UINT8, N.TYPE_UINT8), (N.TYPE_INT32, N.TYPE_UINT8),

@@ -78,7 +78,7 @@ def test_tuple_group_by(gpu_ctx, kinds, distinct, n):
     types = [TYPES[t] for t in kinds]
     aggs = [(N.AGG_SUM, N.TYPE_INT64), (N.AGG_COUNT_STAR, N.TYPE_INT64), (N.AGG_MAX, N.TYPE_INT64)]
     st = HashAggregateState(gpu_ctx, types, aggs, 64)
-    assert st.tuple_dict is not None
+    assert st.key_layout == 2  # key-tuple codes
     # two batches: the dictionary keeps codes across update calls
     h = n // 2
     for a, b in ((0, h), (h, n)):

@@ -120,11 +120,9 @@ def main():
     for _ in range(3):
         t_create, st = wall(lambda: HashAggregateState(ctx, [N.TYPE_UTF8], [(N.AGG_MAX, N.TYPE_FLOAT64)], 16,
                                                        async_update=True))
-        t_enc, codes = wall(lambda: st.dicts[0].encode(vendor))
-        t_upd, _ = wall(lambda: N.check(N.lib().qe_hashagg_update(
-            st.handle, (N.QeColumn * 1)(codes.as_c()), (N.QeColumn * 1)(fare.as_c()), None)))
+        t_upd, _ = wall(lambda: st.update([vendor], [fare]))  # the key encode happens inside (C state)
         t_fin, _ = wall(st.finalize)
-        parts = {"create": t_create, "encode": t_enc, "update": t_upd, "finalize_decode": t_fin}
+        parts = {"create": t_create, "encode_update": t_upd, "finalize_decode": t_fin}
         st.close()
     n = vendor.length
     check = None
