@@ -364,124 +364,43 @@ __global__ void __launch_bounds__(256) k_csv_count2(const uint8_t* __restrict__ 
   }
 }
 
-// One pass for the line-end list of a file without '"' or '\r' (speculative: the host does not
-// know that yet). Replaces k_csv_count2 -> k_csv_seg_reduce / _apply -> k_csv_terms. A wave counts
-// the '\n' bytes of its 16 KiB segment, publishes its count and last '\n' (decoupled look-back, 64
-// predecessors per round), then reads the segment again to write the positions (holding its '\n'
-// words in registers spilled them). Segments follow the wave index: workgroups are dispatched in
-// order, so every segment a wave waits for is resident or done (a ticket counter instead — one
-// device atomic per wave on one word — took 400 us for tripdata's 23.5K segments); a look-back that
-// still does not finish gives up. Any '"' or '\r' in the file (host[2] bit 0), a list longer than
-// `cap` (bit 1) or a look-back that gave up (bit 2) makes the host rerun the general passes.
-// nbytes < 2^31: a status word packs flag (2 bits) | count (31) | last '\n' + 1 (31).
-constexpr uint64_t LB_AGG = 1ull << 62, LB_INC = 2ull << 62, LB_M31 = (1ull << 31) - 1;
-
-// Any '"' or '\r' among the 16 bytes (has-zero-byte tests; bytes past the end read as 0).
-__device__ __forceinline__ bool quote_or_cr(const Lane16& v) {
-  uint32_t any = 0;
+// One read of the file that classifies its bytes four at a time (SWAR on 32-bit words) for the fast
+// path of a file without '"' or '\r' (tripdata, K:1335): two bitmaps of one bit per byte, in byte
+// order — '\n' and the delimiter — and per 16 KiB segment what k_csv_count2 reports for such a file
+// (its '\n' count and last '\n'; no quote, so no quote state) plus one flag: the segment holds a '"'
+// or a '\r'. The host then takes the general passes (k_csv_count2 ...) instead.
+//   test of a word x against byte c < 0x80: s = ((x & 0x7F7F7F7F) ^ c) + 0x7F7F7F7F leaves bit 7 of
+//   a byte clear iff its low seven bits equal c — for an ASCII byte, iff the byte is c (a byte
+//   >= 0x80 is marked "no match" on a branch of its own);
+//   16-bit mask in byte order: the bytes of (s & 0x80808080) dotted with weights 1, 2, 4, 8
+//   (v_dot4_u32_u8) give 128 x the inverted nibble of each word.
+// Requires delim < 0x80 (the host checks).
+__device__ __forceinline__ uint32_t nib_mask16(const uint32_t (&s)[4]) {  // bit k: byte k matched
+  uint32_t m = 0;
 #pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const uint32_t x = v.w[i] ^ 0x22222222u, y = v.w[i] ^ 0x0D0D0D0Du;
-    any |= ((x - 0x01010101u) & ~x) | ((y - 0x01010101u) & ~y);
-  }
-  return (any & 0x80808080u) != 0;
+  for (int i = 0; i < 4; ++i) m += __builtin_amdgcn_udot4(s[i] & 0x80808080u, 0x08040201u, 0u, false) << (4 * i);
+  return ~(m >> 7) & 0xFFFFu;
 }
 
-__global__ void __launch_bounds__(256) k_csv_ends1(const uint8_t* __restrict__ data, int64_t nbytes, int64_t nseg,
-                                                   uint64_t* __restrict__ status,
-                                                   int64_t* __restrict__ ends, int64_t cap, int64_t* host) {
+__global__ void __launch_bounds__(256) k_csv_classify(const uint8_t* __restrict__ data, int64_t nbytes, int64_t nseg,
+                                                      uint32_t delim, uint16_t* __restrict__ nlbm,
+                                                      uint16_t* __restrict__ dbm, int64_t* __restrict__ seg_q,
+                                                      int64_t* __restrict__ seg_t0, int64_t* __restrict__ seg_t1,
+                                                      uint8_t* __restrict__ seg_cr) {
   const int lane = threadIdx.x & 63;
   const int64_t seg = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
   if (seg >= nseg) return;
   const int64_t base = seg * SEG;
-  const uint64_t below = (1ull << lane) - 1;
+  const uint32_t K7 = 0x7F7F7F7Fu, CN = 0x0A0A0A0Au, CQ = 0x22222222u, CR = 0x0D0D0D0Du, CD = delim * 0x01010101u;
+  uint32_t qr = 0xFFFFFFFFu;  // AND of the '"' / '\r' tests: a clear bit 7 = one was seen
   int cnt = 0;
   int64_t last = -1;
-  bool bad = false;
-  for (int g = 0; g < SEG / 4096; ++g) {  // four loads in flight per lane
-    Lane16 v[4];
-#pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      const int64_t pu = base + (4 * g + u) * 1024 + lane * 16;
-      v[u] = pu < nbytes ? load16(data, nbytes, pu) : Lane16{{0, 0, 0, 0}};
-    }
-#pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      const int st = 4 * g + u;
-      uint32_t h[4];
-      bad |= quote_or_cr(v[u]);
-      nl_words(v[u], h);
-      const int c = __popc(h[0]) + __popc(h[1]) + __popc(h[2]) + __popc(h[3]);
-      if (c) {
-        const int i = h[3] ? 3 : h[2] ? 2 : h[1] ? 1 : 0;
-        last = base + st * 1024 + lane * 16 + 4 * i + ((31 - __builtin_clz(h[i])) >> 3);
-      }
-      cnt += c;
-    }
-  }
-  int tot = cnt;
-  for (int d = 32; d >= 1; d >>= 1) {
-    tot += __shfl_xor(tot, d);
-    last = max(last, (int64_t)__shfl_xor(last, d));
-  }
-  const bool anybad = __ballot(bad) != 0;
-  if (anybad && lane == 0)
-    __hip_atomic_fetch_or((unsigned long long*)&host[2], 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-  const uint64_t mine = ((uint64_t)tot << 31) | (uint64_t)(last + 1);
-  if (seg > 0 && lane == 0) __hip_atomic_store(&status[seg], LB_AGG | mine, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  // look-back, 64 predecessors per round (lane i reads segment j - i): sum the counts up to the
-  // nearest inclusive prefix; the nearest segment with a '\n' gives the last one so far
-  int64_t excl = 0;
-  uint64_t el = 0;
-  if (seg > 0) {
-    int64_t j = seg - 1;
-    uint32_t spins = 0;
-    for (;;) {
-      const int64_t idx = j - lane;
-      const uint64_t w = idx >= 0 ? __hip_atomic_load(&status[idx], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
-                                  : LB_INC;  // before segment 0: an inclusive prefix of nothing
-      const uint64_t incm = __ballot((w >> 62) == 2);
-      const int lim = incm ? __builtin_ctzll(incm) : 63;  // lanes 0..lim take part
-      const uint64_t part = lim == 63 ? ~0ull : ((2ull << lim) - 1ull);
-      if (__ballot((w >> 62) == 0) & part) {  // a predecessor has not published yet
-        if (++spins > (1u << 20)) {  // never expected: give up, the host reruns the general passes
-          if (lane == 0)
-            __hip_atomic_fetch_or((unsigned long long*)&host[2], 4ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-          break;
-        }
-        __builtin_amdgcn_s_sleep(2);
-        continue;
-      }
-      const bool in = (part >> lane) & 1;
-      int64_t c = in ? (int64_t)((w >> 31) & LB_M31) : 0;
-      for (int d = 32; d >= 1; d >>= 1) c += __shfl_xor(c, d);
-      excl += c;
-      if (el == 0) {
-        const uint64_t hasl = __ballot(in && (w & LB_M31) != 0) ;
-        if (hasl) el = (uint64_t)__shfl((int64_t)(w & LB_M31), __builtin_ctzll(hasl));
-      }
-      if (incm) break;
-      j -= 64;
-    }
-  }
-  if (lane == 0) {
-    const uint64_t lp1 = last >= 0 ? (uint64_t)(last + 1) : el;  // last '\n' so far, + 1 (0: none)
-    __hip_atomic_store(&status[seg], LB_INC | ((uint64_t)(excl + tot) << 31) | lp1, __ATOMIC_RELAXED,
-                       __HIP_MEMORY_SCOPE_AGENT);
-    if (excl + tot > cap)
-      __hip_atomic_fetch_or((unsigned long long*)&host[2], 2ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-    if (seg == nseg - 1) {  // the file's totals (the host reads them after the stream sync)
-      __hip_atomic_store(&host[0], excl + tot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-      __hip_atomic_store(&host[1], (int64_t)lp1 - 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-    }
-  }
-  excl = __shfl(excl, 0);
-  if (anybad || excl + tot > cap) return;  // the result is discarded
-  int64_t out = excl;
   Lane16 vq[4];
-  for (int st = 0; st < SEG / 1024; ++st) {  // the segment again (mostly from the caches): positions
-    const int64_t pos = base + st * 1024 + lane * 16;
-    if ((st & 3) == 0) {
+  for (int step = 0; step < SEG / 1024; ++step) {
+    const int64_t row0 = base + step * 1024;
+    if (row0 >= nbytes) break;
+    const int64_t pos = row0 + lane * 16;
+    if ((step & 3) == 0) {  // 4 loads in flight per lane: this step and the next three
 #pragma unroll
       for (int u = 0; u < 4; ++u) {
         const int64_t pu = pos + u * 1024;
@@ -489,32 +408,91 @@ __global__ void __launch_bounds__(256) k_csv_ends1(const uint8_t* __restrict__ d
       }
     }
     Lane16 v;
-    switch (st & 3) {  // constant indices keep vq in registers
+    switch (step & 3) {  // constant indices keep vq in registers
       case 0: v = vq[0]; break;
       case 1: v = vq[1]; break;
       case 2: v = vq[2]; break;
       default: v = vq[3]; break;
     }
-    uint32_t h[4];
-    nl_words(v, h);
-    const int c = __popc(h[0]) + __popc(h[1]) + __popc(h[2]) + __popc(h[3]);
-    int ex = 0, total = 0;
+    uint32_t sn[4], sd[4], t[4], hi = 0;
 #pragma unroll
-    for (int b = 0; b < 5; ++b) {
-      const uint64_t plane = __ballot((c >> b) & 1);
-      ex += __popcll(plane & below) << b;
-      total += __popcll(plane) << b;
+    for (int i = 0; i < 4; ++i) {
+      const uint32_t a = v.w[i] & K7;
+      sn[i] = (a ^ CN) + K7;
+      sd[i] = (a ^ CD) + K7;
+      t[i] = ((a ^ CQ) + K7) & ((a ^ CR) + K7);
+      hi |= v.w[i];
     }
-    int64_t o = out + ex;
+    if (hi & 0x80808080u) {  // bytes >= 0x80 (UTF-8) match no class
 #pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      uint64_t hh = h[2 * i] | ((uint64_t)h[2 * i + 1] << 32);
-      while (hh) {
-        ends[o++] = pos + 8 * i + (__builtin_ctzll(hh) >> 3);
-        hh &= hh - 1;
+      for (int i = 0; i < 4; ++i) {
+        const uint32_t h = v.w[i] & 0x80808080u;
+        sn[i] |= h;
+        sd[i] |= h;
+        t[i] |= h;
       }
     }
-    out += total;
+    qr &= t[0] & t[1] & t[2] & t[3];
+    const uint32_t nl = nib_mask16(sn), dl = nib_mask16(sd);
+    cnt += __popc(nl);
+    if (nl) last = pos + 31 - __builtin_clz(nl);
+    if (pos < nbytes) {
+      nlbm[pos >> 4] = (uint16_t)nl;
+      dbm[pos >> 4] = (uint16_t)dl;
+    }
+  }
+  for (int d = 32; d >= 1; d >>= 1) {
+    cnt += __shfl_xor(cnt, d);
+    last = max(last, (int64_t)__shfl_xor(last, d));
+  }
+  const bool special = __ballot((qr & 0x80808080u) != 0x80808080u) != 0;
+  if (lane == 0) {
+    seg_cr[seg] = special ? 1 : 0;
+    seg_q[seg] = special ? 1 : 0;
+    seg_t0[seg] = cnt;
+    seg_t1[seg] = 0;
+    seg_t0[2 * nseg + seg] = last;  // seg_l0 / seg_l1 follow the two count arrays
+    seg_t1[2 * nseg + seg] = -1;
+  }
+}
+
+// The line-end list from the '\n' bitmap (fast path): one wave per 16 KiB segment, 256 bitmap bytes
+// per lane read with two 16-byte loads, the wave prefix of the lanes' counts, then each lane's
+// positions by count-trailing-zeros.
+__global__ void __launch_bounds__(256) k_csv_ends_bm(const uint64_t* __restrict__ nlbm, int64_t nbytes, int64_t nseg,
+                                                     const int64_t* __restrict__ seg_ts, int64_t* __restrict__ ends) {
+  const int lane = threadIdx.x & 63;
+  const int64_t seg = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  if (seg >= nseg) return;
+  const uint64_t below = (1ull << lane) - 1;
+  const int64_t b0 = seg * SEG + (int64_t)lane * 256;  // this lane's first byte
+  uint64_t w[4] = {0, 0, 0, 0};
+  if (b0 < nbytes) {
+    const uint4* p = (const uint4*)(nlbm + (b0 >> 6));
+    const uint4 x = p[0], y = p[1];
+    w[0] = x.x | ((uint64_t)x.y << 32);
+    w[1] = x.z | ((uint64_t)x.w << 32);
+    w[2] = y.x | ((uint64_t)y.y << 32);
+    w[3] = y.z | ((uint64_t)y.w << 32);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {  // bits past the file's end (pieces the classify pass never wrote)
+      const int64_t lo = b0 + 64 * k;
+      if (lo >= nbytes) w[k] = 0;
+      else if (nbytes - lo < 64) w[k] &= (1ull << (nbytes - lo)) - 1;
+    }
+  }
+  const int c = __popcll(w[0]) + __popcll(w[1]) + __popcll(w[2]) + __popcll(w[3]);  // 0..256
+  int excl = 0;
+#pragma unroll
+  for (int b = 0; b < 9; ++b) excl += __popcll(__ballot((c >> b) & 1) & below) << b;
+  int64_t o = seg_ts[seg] + excl;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    uint64_t x = w[k];
+    while (x) {
+      ends[o++] = b0 + 64 * k + __builtin_ctzll(x);
+      x &= x - 1;
+    }
   }
 }
 
@@ -700,6 +678,22 @@ struct GBytes {
   int64_t nbytes;
   __device__ __forceinline__ uint32_t operator[](int64_t i) const { return d[i]; }
   __device__ __forceinline__ uint4 bytes16(int64_t s, int64_t n) const {  // bytes [s, s + n), n <= 16
+    const int64_t a = s & ~(int64_t)15;
+    if (a + 32 <= nbytes) {  // two aligned 16-byte loads and a funnel shift
+      const int sh = (int)(s - a);
+      const uint4 x = *(const uint4*)(d + a);
+      unsigned __int128 v = ((unsigned __int128)(((uint64_t)x.w << 32) | x.z) << 64) | (((uint64_t)x.y << 32) | x.x);
+      if (sh) {
+        v >>= 8 * sh;
+        if (sh + n > 16) {
+          const uint4 y = *(const uint4*)(d + a + 16);
+          const unsigned __int128 w = ((unsigned __int128)(((uint64_t)y.w << 32) | y.z) << 64) | (((uint64_t)y.y << 32) | y.x);
+          v |= w << (128 - 8 * sh);
+        }
+      }
+      if (n < 16) v &= (((unsigned __int128)1) << (8 * n)) - 1;
+      return make_uint4((uint32_t)v, (uint32_t)(v >> 32), (uint32_t)(v >> 64), (uint32_t)(v >> 96));
+    }
     uint64_t lo = 0, hi = 0;
     for (int64_t k = 0; k < n; ++k) {
       const uint64_t b = d[s + k];
@@ -739,32 +733,6 @@ struct LBytes {
     v.w[2] = t.z;
     v.w[3] = t.w;
     return v;
-  }
-};
-
-// Bytes by global position from a wave's 2 KiB LDS ring holding the last two 1 KiB steps of its
-// segment walk (positions [lo, hi)); anything outside comes from HBM (fields longer than a step).
-struct RBytes {
-  const uint8_t* R;  // ring: position i at R[i & 2047]
-  int64_t lo, hi;
-  const uint8_t* d;
-  __device__ __forceinline__ uint32_t operator[](int64_t i) const { return (i >= lo && i < hi) ? R[i & 2047] : d[i]; }
-  __device__ __forceinline__ uint4 bytes16(int64_t s, int64_t n) const {  // bytes [s, s + n), n <= 16
-    if (s < lo || s + n > hi) return GBytes{d, hi}.bytes16(s, n);
-    const int64_t a = s & ~(int64_t)15;
-    const int sh = (int)(s & 15);
-    const uint4 x = *(const uint4*)(R + (a & 2047));
-    unsigned __int128 v = ((unsigned __int128)(((uint64_t)x.w << 32) | x.z) << 64) | (((uint64_t)x.y << 32) | x.x);
-    if (sh) {
-      v >>= 8 * sh;
-      if (sh + n > 16) {
-        const uint4 y = *(const uint4*)(R + ((a + 16) & 2047));
-        const unsigned __int128 w = ((unsigned __int128)(((uint64_t)y.w << 32) | y.z) << 64) | (((uint64_t)y.y << 32) | y.x);
-        v |= w << (128 - 8 * sh);
-      }
-    }
-    if (n < 16) v &= (((unsigned __int128)1) << (8 * n)) - 1;
-    return make_uint4((uint32_t)v, (uint32_t)(v >> 32), (uint32_t)(v >> 64), (uint32_t)(v >> 96));
   }
 };
 
@@ -1005,151 +973,83 @@ __global__ void __launch_bounds__(256) k_csv_lines(const uint8_t* __restrict__ d
   }
 }
 
-// Terminator and delimiter masks of a lane's 16 bytes whose first byte has quote state `inq` (the
-// per-byte walk of a lane holding a quote; lanes without one use SWAR compares).
-__device__ __forceinline__ void bounds16_quoted(const Lane16& v, uint32_t next, int64_t nbytes, int64_t pos, uint32_t inq,
-                                                uint32_t delim, uint32_t* tm, uint32_t* dm) {
-  uint32_t t = 0, d = 0;
-#pragma unroll
-  for (int k = 0; k < 16; ++k) {
-    const uint32_t c = v.byte(k);
-    if (pos + k >= nbytes) break;
-    if (c == '"') {
-      inq ^= 1u;
-    } else if (!inq) {
-      if (c == '\n') {
-        t |= 1u << k;
-      } else if (c == '\r') {
-        const uint32_t nx = k < 15 ? v.byte(k + 1) : (pos + 16 < nbytes ? next : 0u);
-        if (pos + k + 1 >= nbytes || nx != '\n') t |= 1u << k;
-      } else if (c == delim) {
-        d |= 1u << k;
-      }
-    }
+// Bit index of the k-th (0-based) set bit of w, which has more than k.
+__device__ __forceinline__ int select64(uint64_t w, int k) {
+  int pos = 0;
+  const int c = __popcll(w & 0xFFFFFFFFull);
+  if (k >= c) {
+    k -= c;
+    w >>= 32;
+    pos = 32;
   }
-  *tm = t;
-  *dm = d;
+  uint32_t x = (uint32_t)w;
+  int h = __popc(x & 0xFFFFu);
+  if (k >= h) {
+    k -= h;
+    x >>= 16;
+    pos += 16;
+  }
+  h = __popc(x & 0xFFu);
+  if (k >= h) {
+    k -= h;
+    x >>= 8;
+    pos += 8;
+  }
+  for (; k > 0; --k) x &= x - 1;
+  return pos + __ffs(x) - 1;
 }
 
-// The projected fields of every record, one wave per 16 KiB segment, straight from the file bytes and
-// the count pass's per-segment quote / terminator prefixes — no line-end list and no per-line walk
-// (round 4's k_csv_terms<true> + k_csv_lines, 160 + 283 us on tripdata). A wave owns the lines that
-// START in its segment (after each of its terminators; line 0 in segment 0) and runs past the
-// segment's end until the last of them ends. Per 1 KiB step, each lane has terminator and delimiter
-// masks of its 16 bytes (outside quotes); a wave prefix of (terminators, delimiters) per lane gives
-// the line and field ordinal at the lane's first byte (the field ordinal restarts at the last lane
-// holding a terminator), and each lane walks its boundaries in order, recording the projected
-// fields of its lines. Lines that may not be records — no delimiter at all (blank, or one field) or
-// '#' first — are counted in *suspect: the host then takes the kept-line path, which decides
-// exactly. Requires a delimiter above 0x20 (a blank line then has no delimiter).
-__global__ void __launch_bounds__(256) k_csv_seg_fields(const uint8_t* __restrict__ data, int64_t nbytes, int64_t nseg,
-                                                        const int64_t* __restrict__ seg_qs,
-                                                        const int64_t* __restrict__ seg_ts, int64_t nlines,
-                                                        int64_t first, FieldArgs Ag,
-                                                        unsigned long long* __restrict__ suspect) {
+// The fast path's line walk (a file without '"' or '\r'): a lane per line reads the delimiter bitmap
+// words that cover it (one bit per byte, k_csv_classify) instead of its bytes — a 64-byte stretch of
+// the line is one load, a popcount and, for the projected fields ending there, a bit select — and
+// touches the file's bytes only for the blank-line test and the projected values (trim, 16-byte
+// stage). Row r = line r + first; `nskip` counts the lines that are not records (blank, '#').
+__global__ void __launch_bounds__(256) k_csv_lines_bm(const uint8_t* __restrict__ data, int64_t nbytes,
+                                                      const uint64_t* __restrict__ dbm, const int64_t* __restrict__ ends,
+                                                      int64_t nlines, int64_t first, FieldArgs Ag, int32_t nproj,
+                                                      unsigned long long* __restrict__ nskip) {
   __shared__ FieldArgs A;
-  __shared__ __attribute__((aligned(16))) uint8_t ring[4][2048];
   stage_args(A, Ag);
-  const int lane = threadIdx.x & 63;
-  uint8_t* const R = ring[threadIdx.x >> 6];
-  const int64_t seg = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
-  if (seg >= nseg) return;
-  const uint64_t below = (1ull << lane) - 1;
-  const int64_t first_own = seg == 0 ? 0 : seg_ts[seg] + 1;
-  const int64_t last_own = min(seg_ts[seg + 1], nlines - 1);
-  if (first_own > last_own) return;
-  const GBytes G{data, nbytes};
-  const uint32_t delim = (uint32_t)A.delim;
-  uint32_t qcarry = (uint32_t)(seg_qs[seg] & 1);
-  int64_t row_c = seg == 0 ? 0 : seg_ts[seg];  // line holding the segment's first byte
-  int32_t f_c = 0;
-  int64_t fs_c = seg * SEG;
-  unsigned long long sus = 0;
-  if (seg == 0 && lane == 0 && nbytes > 0 && data[0] == '#') sus = 1;
-  for (int64_t p0 = seg * SEG; p0 < nbytes; p0 += 1024) {
-    const int64_t pos = p0 + lane * 16;
-    const Lane16 v = pos < nbytes ? load16(data, nbytes, pos) : Lane16{{0, 0, 0, 0}};
-    // the step's bytes into the ring (the step before stays there): field bytes are read from LDS
-    *(uint4*)(R + (pos & 2047)) = make_uint4(v.w[0], v.w[1], v.w[2], v.w[3]);
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    const RBytes Rb{R, p0 == seg * SEG ? p0 : p0 - 1024, min(p0 + 1024, nbytes), data};
-    const bool hasq = has_byte(v, '"') && eq16(v, '"') != 0;
-    const uint32_t qodd = hasq ? (uint32_t)(quotes16(v) & 1) : 0u;
-    const uint64_t par = __ballot(qodd);
-    const uint32_t inq0 = qcarry ^ ((uint32_t)__popcll(par & below) & 1u);
-    qcarry ^= (uint32_t)__popcll(par) & 1u;
-    uint32_t next = (uint32_t)__shfl_down((int)(v.w[0] & 0xFFu), 1);
-    if (lane == 63) next = (v.byte(15) == '\r' && pos + 16 < nbytes) ? data[pos + 16] : 0u;
-    uint32_t T = 0, D = 0;
-    if (pos < nbytes) {
-      if (hasq) {
-        bounds16_quoted(v, next, nbytes, pos, inq0, delim, &T, &D);
-      } else if (!inq0) {
-        uint32_t dummy;
-        T = terms16(v, next, nbytes, pos, 0u, &dummy);
-        const uint32_t valid = pos + 16 <= nbytes ? 0xFFFFu : ((1u << (nbytes - pos)) - 1u);
-        D = has_byte(v, delim) ? (eq16(v, delim) & valid) : 0u;
+  const GBytes d{data, nbytes};
+  for (int64_t li = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; li < nlines; li += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t s = line_start(ends, li), e = ends[li];
+    bool keep = false;
+    if (s < e) {
+      const uint32_t c0 = d[s];
+      keep = c0 > 0x20 && c0 != '#';
+      if (!keep && c0 != '#')
+        for (int64_t p = s + 1; p < e && !keep; ++p) keep = d[p] > 0x20;
+    }
+    if (!keep) {
+      atomicAdd(nskip, 1ull);
+      continue;
+    }
+    if (li < first) continue;
+    const int64_t r = li - first;
+    int f = 0, t = 0;
+    int64_t fs = s;
+    for (int64_t wb = s & ~(int64_t)63; wb < e && t < A.npf; wb += 64) {
+      uint64_t w = dbm[wb >> 6];
+      if (wb < s) w &= ~0ull << (s - wb);
+      if (e - wb < 64) w &= (1ull << (e - wb)) - 1;
+      const int n = __popcll(w);
+      while (t < A.npf && A.pf[t] < f + n) {  // projected field A.pf[t] ends in this stretch
+        const int ft = A.pf[t], k = ft - f;
+        const int64_t st = k == 0 ? fs : wb + select64(w, k - 1) + 1;
+        record_field(d, A, ft, st, wb + select64(w, k), r);
+        ++t;
+      }
+      if (n) {
+        fs = wb + (63 - __builtin_clzll(w)) + 1;
+        f += n;
       }
     }
-    // line and field ordinal at this lane's first byte
-    const uint32_t tc = (uint32_t)__popc(T), dc = (uint32_t)__popc(D);
-    const uint32_t cnt = (tc << 16) | dc;
-    uint32_t incl = cnt;
-#pragma unroll
-    for (int off = 1; off < 64; off <<= 1) {
-      const uint32_t y = (uint32_t)__shfl_up((int)incl, off);
-      if (lane >= off) incl += y;
+    if (t < A.npf && A.pf[t] == f) {  // the line's last field
+      record_field(d, A, f, fs, e, r);
+      ++t;
     }
-    const uint32_t excl = incl - cnt;
-    const uint64_t hasT = __ballot(T != 0), hasB = __ballot((T | D) != 0);
-    const int lastT = T ? 31 - __builtin_clz(T) : -1;
-    const int dtail = T ? __popc(D >> lastT) : 0;  // delimiters after the lane's last terminator
-    const int lastB = (T | D) ? 31 - __builtin_clz(T | D) : -1;
-    const uint64_t mt = hasT & below, mb = hasB & below;
-    const int pt = mt ? 63 - __builtin_clzll(mt) : 0;
-    const int pb = mb ? 63 - __builtin_clzll(mb) : 0;
-    const int dtail_p = __shfl(dtail, pt);
-    const uint32_t dincl_p = (uint32_t)__shfl((int)(incl & 0xFFFFu), pt);
-    const int lastB_p = __shfl(lastB, pb);
-    int64_t row = row_c + (int64_t)(excl >> 16);
-    int32_t f = mt ? dtail_p + (int32_t)((excl & 0xFFFFu) - dincl_p) : f_c + (int32_t)(excl & 0xFFFFu);
-    int64_t fs = mb ? (p0 + pb * 16 + lastB_p + 1) : fs_c;
-    // this lane's boundaries, in order
-    uint32_t bm = T | D;
-    while (bm) {
-      const int k = __builtin_ctz(bm);
-      bm &= bm - 1;
-      const int64_t pb_ = pos + k;
-      const bool is_t = (T >> k) & 1;
-      const bool own = row >= first_own && row <= last_own;
-      if (own && row >= first) record_field(Rb, A, f, fs, pb_, row - first);
-      if (is_t) {
-        if (own && f == 0) sus += 1;  // no delimiter: blank, comment or a one-field line?
-        ++row;
-        f = 0;
-        fs = pb_ + 1;
-        if (row >= first_own && row <= last_own && fs < nbytes && Rb[fs] == '#') sus += 1;
-      } else {
-        ++f;
-        fs = pb_ + 1;
-      }
-    }
-    row_c = __shfl(row, 63);
-    f_c = __shfl(f, 63);
-    fs_c = __shfl(fs, 63);
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");  // the ring's older half is rewritten next step
-    __builtin_amdgcn_wave_barrier();
-    if (row_c > last_own) break;  // the last line that started in this segment has ended
+    for (; t < A.npf; ++t) A.meta[A.slot[A.pf[t]]][r] = 0;  // fields the line does not reach read as "" (K:263)
   }
-  // a final line without a terminator ends at the end of the file
-  if (lane == 0 && row_c == nlines - 1 && row_c >= first_own && row_c <= last_own && fs_c <= nbytes) {
-    if (row_c >= first) record_field(G, A, f_c, fs_c, nbytes, row_c - first);
-    if (f_c == 0) sus += 1;
-  }
-  for (int d = 32; d >= 1; d >>= 1) sus += __shfl_xor(sus, d);
-  if (lane == 0 && sus) atomicAdd(suspect, sus);
 }
 
 // Byte starts of the projected columns' values (the Utf8 offsets): a scan of the lengths in meta,
@@ -1459,55 +1359,34 @@ int csv_parse(qe_ctx* ctx, const uint8_t* data, int64_t nbytes, const qe_csv_opt
   void* hp;
   QE_TRY(ctx_pinned_coherent(ctx, (size_t)(2 * nproj + 3) * 8, &hp));
   volatile int64_t* host = (volatile int64_t*)hp;
-  static const bool seg_env = [] {  // (the segment field pass, below)
-    const char* e = getenv("QE_CSV_SEGFIELDS");
-    return e && e[0] == '1';
-  }();
-  // The general passes (k_csv_count2 -> segment plan -> k_csv_terms), or with QE_CSV_ONEPASS=1 one
-  // look-back pass for files without '"' or '\r' (k_csv_ends1, falling back to the general passes
-  // when it finds one). Opt-in: tripdata (4M rows, one box) 213 us against 96 + 16 + 92 us for the
-  // general passes — its VALU per byte is lower, but waves wait on their predecessors' counts.
-  static const bool onepass_env = [] {
-    const char* e = getenv("QE_CSV_ONEPASS");
-    return e && e[0] == '1';
-  }();
   void* p;
   int64_t* ends = nullptr;
   int64_t nterm = 0, last_end = -1;
-  bool file_q = false, file_cr = false, have_ends = false;
+  bool file_q = false, file_cr = false;
   int64_t* seg_qs = nullptr;
   int64_t* seg_ts = nullptr;
-  if (onepass_env && !seg_env && nbytes > 0 && nbytes < (1ll << 31)) {
-    const int64_t cap = nbytes / 16 + 1024;  // line ends the list can take (else: the general passes)
-    QE_TRY(ctx_workspace(ctx, 0, (size_t)nseg * 8, &p));
-    uint64_t* status = (uint64_t*)p;
-    QE_TRY(ctx_workspace(ctx, 1, (size_t)(cap + 2) * 8, &p));
-    ends = (int64_t*)p;
-    QE_HIP(hipMemsetAsync(status, 0, (size_t)nseg * 8, ctx->stream));
-    host[0] = 0;
-    host[1] = -1;
-    host[2] = 0;
-    hipLaunchKernelGGL(k_csv_ends1, dim3(wgrid), dim3(256), 0, ctx->stream, data, nbytes, nseg, status, ends, cap,
-                       (int64_t*)hp);
-    QE_TRY(launch_check("k_csv_ends1"));
-    QE_TRY(ctx_sync(ctx));
-    if (host[2] == 0) {
-      nterm = host[0];
-      last_end = host[1];
-      have_ends = true;
-    }
-  }
-  if (!have_ends) {
-    QE_TRY(ctx_workspace(ctx, 0, (size_t)(8 * nseg + 6) * 8 + (size_t)div_up((uint64_t)nseg, SP_TILE) * sizeof(SegAgg) + (size_t)nseg,
-                         &p));
-    int64_t* seg_q = (int64_t*)p;
-    seg_qs = seg_q + nseg;
-    seg_ts = seg_qs + nseg + 1;
-    int64_t* seg_t0 = seg_ts + nseg + 1;  // then seg_t1 [nseg], seg_l0 [nseg], seg_l1 [nseg]
-    int64_t* seg_t1 = seg_t0 + nseg;
-    SegAgg* agg = (SegAgg*)(seg_t1 + 3 * nseg);  // after seg_t1 / seg_l0 / seg_l1
-    uint8_t* seg_cr = (uint8_t*)(agg + spb);
-    if (nbytes > 0) {
+  QE_TRY(ctx_workspace(ctx, 0, (size_t)(8 * nseg + 6) * 8 + (size_t)div_up((uint64_t)nseg, SP_TILE) * sizeof(SegAgg) + (size_t)nseg,
+                       &p));
+  int64_t* seg_q = (int64_t*)p;
+  seg_qs = seg_q + nseg;
+  seg_ts = seg_qs + nseg + 1;
+  int64_t* seg_t0 = seg_ts + nseg + 1;  // then seg_t1 [nseg], seg_l0 [nseg], seg_l1 [nseg]
+  int64_t* seg_t1 = seg_t0 + nseg;
+  SegAgg* agg = (SegAgg*)(seg_t1 + 3 * nseg);  // after seg_t1 / seg_l0 / seg_l1
+  uint8_t* seg_cr = (uint8_t*)(agg + spb);
+  // Fast path (a file without '"' or '\r', which only its bytes can tell): one classification pass
+  // writes the '\n' and delimiter bitmaps and the segment counts; the line-end list and the line walk
+  // then read bitmaps. A file with either byte reruns the general passes (k_csv_count2 ...).
+  bool fast = nbytes > 0 && A.delim < 0x80;
+  const size_t bmw = (size_t)div_up((uint64_t)(nbytes > 0 ? nbytes : 1), 64) + 4;  // 64-bit words per bitmap
+  uint64_t* nlbm = nullptr;
+  uint64_t* dbm = nullptr;
+  auto plan = [&](bool classify) -> int {
+    if (classify) {
+      hipLaunchKernelGGL(k_csv_classify, dim3(wgrid), dim3(256), 0, ctx->stream, data, nbytes, nseg, (uint32_t)A.delim,
+                         (uint16_t*)nlbm, (uint16_t*)dbm, seg_q, seg_t0, seg_t1, seg_cr);
+      QE_TRY(launch_check("k_csv_classify"));
+    } else if (nbytes > 0) {
       hipLaunchKernelGGL(k_csv_count2, dim3(wgrid), dim3(256), 0, ctx->stream, data, nbytes, nseg, seg_q, seg_t0, seg_t1,
                          seg_cr);
       QE_TRY(launch_check("k_csv_count2"));
@@ -1523,14 +1402,22 @@ int csv_parse(qe_ctx* ctx, const uint8_t* data, int64_t nbytes, const qe_csv_opt
     hipLaunchKernelGGL(k_csv_seg_apply, dim3((unsigned)spb), dim3(SP_THREADS), 0, ctx->stream, seg_q, seg_t0, seg_t1, nseg,
                        agg, spb, seg_qs, seg_ts, (int64_t*)hp);
     QE_TRY(launch_check("k_csv_seg_apply"));
-    QE_TRY(ctx_sync(ctx));
-    nterm = host[0];
-    last_end = host[1];
-    file_q = (host[2] & 1) != 0;  // any '"' / '\r' in the bytes
-    file_cr = (host[2] & 2) != 0;
-    QE_TRY(ctx_workspace(ctx, 1, (size_t)(nterm + 2) * 8, &p));
-    ends = (int64_t*)p;
+    return ctx_sync(ctx);
+  };
+  if (fast) {
+    QE_TRY(ctx_workspace(ctx, 5, bmw * 16, &p));
+    nlbm = (uint64_t*)p;
+    dbm = nlbm + bmw;
+    QE_TRY(plan(true));
+    if (host[2] & 3) fast = false;  // a '"' or '\r': the general passes decide the records
   }
+  if (!fast) QE_TRY(plan(false));
+  nterm = host[0];
+  last_end = host[1];
+  file_q = (host[2] & 1) != 0;  // any '"' / '\r' in the bytes
+  file_cr = (host[2] & 2) != 0;
+  QE_TRY(ctx_workspace(ctx, 1, (size_t)(nterm + 2) * 8, &p));
+  ends = (int64_t*)p;
   A.noq = file_q ? 0 : 1;
   QE_TRY(ctx_workspace(ctx, 4, (size_t)(2 * nterm + 5) * 8, &p));
   int64_t* keep = (int64_t*)p;
@@ -1555,25 +1442,12 @@ int csv_parse(qe_ctx* ctx, const uint8_t* data, int64_t nbytes, const qe_csv_opt
   }
   int64_t rows = 0;
   bool scanned = false;  // column sizes already known (the all-records fast path)
-  // ---- the segment-parallel field pass (k_csv_seg_fields, QE_CSV_SEGFIELDS=1): every line a record,
-  // no line-end list. Opt-in: tripdata (4M rows, one box) scanned in 1.15 ms with it against 0.90 ms
-  // for the line-end list + per-line walk below (k_csv_seg_fields 635 us vs k_csv_terms<emit> 160 +
-  // k_csv_lines 283 us): a wave walks its 16 KiB segment step by step, each lane's boundaries in a
-  // serial loop, where the line pass runs 64 independent lines per wave.
   const int64_t rows_all = std::max<int64_t>(0, nlines - first);
-  if (seg_env && nlines > 0 && A.delim > 0x20) {
-    // fields a record does not have read as "" (K:263): lengths and quote flags start at zero
-    QE_HIP(hipMemsetAsync(t->meta(0), 0, (size_t)nproj * (size_t)t->stride * 4, ctx->stream));
-    unsigned long long* suspect = (unsigned long long*)keep;
-    QE_HIP(hipMemsetAsync(suspect, 0, 8, ctx->stream));
-    hipLaunchKernelGGL(k_csv_seg_fields, dim3(wgrid), dim3(256), 0, ctx->stream, data, nbytes, nseg, seg_qs, seg_ts,
-                       nlines, first, A, suspect);
-    QE_TRY(launch_check("k_csv_seg_fields"));
-    QE_TRY(column_sizes(t, rows_all, suspect, host));
-    if (host[0] == 0) return QE_OK;
-    // a line that may not be a record: the line-end list and the kept-line path below decide
-  }
-  if (nterm > 0 && !have_ends) {
+  if (nterm > 0 && fast) {
+    hipLaunchKernelGGL(k_csv_ends_bm, dim3(wgrid), dim3(256), 0, ctx->stream, (const uint64_t*)nlbm, nbytes, nseg, seg_ts,
+                       ends);
+    QE_TRY(launch_check("k_csv_ends_bm"));
+  } else if (nterm > 0) {
     auto kt = file_q ? (file_cr ? k_csv_terms<true, true> : k_csv_terms<true, false>)
                      : (file_cr ? k_csv_terms<false, true> : k_csv_terms<false, false>);
     hipLaunchKernelGGL(kt, dim3(wgrid), dim3(256), 0, ctx->stream, data, nbytes, nseg, seg_qs, seg_ts, ends);
@@ -1589,9 +1463,15 @@ int csv_parse(qe_ctx* ctx, const uint8_t* data, int64_t nbytes, const qe_csv_opt
     unsigned long long* nskip = (unsigned long long*)keep;
     QE_HIP(hipMemsetAsync(nskip, 0, 8, ctx->stream));
     const int64_t blocks = std::min<int64_t>((int64_t)div_up(div_up((uint64_t)nlines, 64), 4), (int64_t)ctx->num_cus * 8);
-    hipLaunchKernelGGL(k_csv_lines, dim3((unsigned)blocks), dim3(256), 0, ctx->stream, data, nbytes, ends, nlines, first,
-                       A, nproj, nskip);
-    QE_TRY(launch_check("k_csv_lines"));
+    if (fast) {
+      hipLaunchKernelGGL(k_csv_lines_bm, dim3((unsigned)blocks), dim3(256), 0, ctx->stream, data, nbytes,
+                         (const uint64_t*)dbm, ends, nlines, first, A, nproj, nskip);
+      QE_TRY(launch_check("k_csv_lines_bm"));
+    } else {
+      hipLaunchKernelGGL(k_csv_lines, dim3((unsigned)blocks), dim3(256), 0, ctx->stream, data, nbytes, ends, nlines, first,
+                         A, nproj, nskip);
+      QE_TRY(launch_check("k_csv_lines"));
+    }
     // Speculatively every line a record (the common case): the columns' length scans run now, and
     // the skipped-line count and the column sizes come back with one sync.
     QE_TRY(column_sizes(t, rows_all, nskip, host));

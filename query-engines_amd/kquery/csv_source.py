@@ -79,15 +79,6 @@ def _upload_ctx(device: int) -> Context:
     return _UPLOAD_CTX[device][1]
 
 
-def _chunk_bytes() -> int:
-    """Chunk size of the overlapped scan of large files (QE_CSV_CHUNK_MB; unset / 0: off). Off by
-    default: tripdata (386 MB, one box) took 10.4 ms file -> columns in 128 MB chunks against 8.9 ms
-    for one staged upload + one parse — every chunk's upload call drains and refills the staging
-    pipeline, and the per-chunk parses' host round trips land on the critical path."""
-    v = os.environ.get("QE_CSV_CHUNK_MB")
-    return (int(v) if v else 0) << 20
-
-
 def _view(c: DeviceColumn, s: int, m: int, ctx: Context) -> DeviceColumn:
     """Rows [s, s + m) of a UTF8 column (its offsets sliced, the values shared)."""
     v = DeviceColumn(N.TYPE_UTF8, m, c.values, None, c.offsets[s:s + m + 1], ctx)
@@ -97,7 +88,12 @@ def _view(c: DeviceColumn, s: int, m: int, ctx: Context) -> DeviceColumn:
 
 class CsvDataSource(DataSource):
     def __init__(self, filename: str, hasHeaders: bool = True, batchSize: int = 0,  # noqa: N803
-                 schema: Optional[Schema] = None, ctx: Optional[Context] = None):
+                 schema: Optional[Schema] = None, ctx: Optional[Context] = None, chunk_bytes: int = 0):
+        """``chunk_bytes`` > 0: scan a file of at least two such chunks chunk by chunk, uploading the
+        next while this one parses (one batch per chunk, like the JNI scan). Off by default: tripdata
+        (386 MB, one box) took 10.4 ms file -> columns in 128 MB chunks against 8.9 ms for one staged
+        upload + one parse (docs/csv_ab.md)."""
+        self.chunk_bytes = int(chunk_bytes)
         self.filename = filename
         self.hasHeaders = hasHeaders
         self.batchSize = batchSize
@@ -140,7 +136,7 @@ class CsvDataSource(DataSource):
         idx = [names.index(f.name) for f in read_schema.fields]
         ctx = self.ctx or Context.get(0)
         size = os.path.getsize(self.filename)
-        chunk = _chunk_bytes()
+        chunk = self.chunk_bytes
         if (not self.batchSize or self.batchSize <= 0) and chunk > 0 and size >= 2 * chunk:
             yield from self._scan_chunked(ctx, read_schema, idx, size, chunk)
             return

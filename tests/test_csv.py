@@ -91,12 +91,12 @@ def test_host_header_helpers_match_oracle():
 
 
 # ---- GPU -----------------------------------------------------------------------------------------
-def _gpu_scan(ctx, tmp_path, data, projection=None, has_header=True, batch=0):
+def _gpu_scan(ctx, tmp_path, data, projection=None, has_header=True, batch=0, chunk_bytes=0):
     from kquery.csv_source import CsvDataSource
 
     p = tmp_path / "t.csv"
     p.write_bytes(data)
-    ds = CsvDataSource(str(p), has_header, batch, ctx=ctx)
+    ds = CsvDataSource(str(p), has_header, batch, ctx=ctx, chunk_bytes=chunk_bytes)
     names = [f.name for f in ds.schema().fields]
     proj = projection if projection is not None else names
     batches = list(ds.scan(proj))
@@ -206,56 +206,13 @@ def test_gpu_csv_long_lines_and_blank_lines(gpu_ctx, tmp_path):
         assert cols == R.project(rows, range(len(onames)))
 
 
-_SEG_CHILD = r'''
-import pathlib, random, sys, tempfile
-root = pathlib.Path(sys.argv[1])
-sys.path[:0] = [str(root), str(root / "query-engines_amd"), str(root / "tests")]
-from kquery.columnar import Context
-from oracle import csv_ref as R
-import test_csv as T
-ctx = Context.get(0)
-tmp = pathlib.Path(tempfile.mkdtemp())
-for seed in range(8):
-    rng = random.Random(100 + seed)
-    delim = rng.choice([",", ";", "|"])
-    data = T.random_csv(rng, rng.choice([1, 300, 5000]), rng.randint(1, 7), delim, rng.choice(["\n", "\r\n", "mixed"]))
-    names, proj, cols, _ = T._gpu_scan(ctx, tmp, data)
-    onames, _, rows = R.parse(data)
-    assert names == onames and cols == R.project(rows, range(len(onames))), seed
-body = [f"{i % 97},{i},\"q,{i}\",{i * 0.5}" for i in range(200_000)]
-data = ("k,v,q,f\n" + "\n".join(body) + "\n").encode()
-names, proj, cols, _ = T._gpu_scan(ctx, tmp, data)
-onames, _, rows = R.parse(data)
-assert cols == R.project(rows, range(4))
-print("ok")
-'''
-
-
-@pytest.mark.gpu
-def test_gpu_csv_segment_field_pass(tmp_path):
-    """The opt-in segment field pass (QE_CSV_SEGFIELDS=1, read once per process: a child process)
-    against the oracle: random files (blank / comment lines take the kept-line path), and a large
-    all-records file with quoted fields, which it handles itself."""
-    import os
-    import pathlib
-    import subprocess
-    import sys
-
-    root = pathlib.Path(__file__).resolve().parents[1]
-    env = dict(os.environ, QE_CSV_SEGFIELDS="1")
-    r = subprocess.run([sys.executable, "-c", _SEG_CHILD, str(root)], cwd=str(root), env=env, capture_output=True,
-                       text=True, timeout=240)
-    assert r.returncode == 0 and "ok" in r.stdout, r.stdout[-2000:] + r.stderr[-3000:]
-
-
 @pytest.mark.gpu
 @pytest.mark.parametrize("newline", ["\n", "\r\n"])
-def test_gpu_csv_chunked_overlapped_scan(gpu_ctx, tmp_path, monkeypatch, newline):
-    """A large file scans in chunks (QE_CSV_CHUNK_MB; 1 MiB here), the next chunk uploading while
+def test_gpu_csv_chunked_overlapped_scan(gpu_ctx, tmp_path, newline):
+    """A large file scans in chunks (chunk_bytes; 1 MiB here), the next chunk uploading while
     this one parses: chunk boundaries land inside quoted fields with embedded newlines and
     delimiters, between '\\r' and '\\n', and in blank / comment lines; the concatenated batches equal
     one parse of the file (oracle), and there is more than one batch."""
-    monkeypatch.setenv("QE_CSV_CHUNK_MB", "1")
     rng = random.Random(11 + len(newline))
     body = []
     for i in range(200_000):
@@ -269,7 +226,7 @@ def test_gpu_csv_chunked_overlapped_scan(gpu_ctx, tmp_path, monkeypatch, newline
             body.append(f"{i % 13},{q},{rng.random():.5f}")
     data = ("k,v,f" + newline + newline.join(body) + newline).encode()
     assert len(data) > 3 << 20  # three 1 MiB chunks at least
-    names, proj, cols, batches = _gpu_scan(gpu_ctx, tmp_path, data)
+    names, proj, cols, batches = _gpu_scan(gpu_ctx, tmp_path, data, chunk_bytes=1 << 20)
     onames, _, rows = R.parse(data)
     assert names == onames
     assert len(batches) > 1
@@ -277,22 +234,31 @@ def test_gpu_csv_chunked_overlapped_scan(gpu_ctx, tmp_path, monkeypatch, newline
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("shape", ["plain", "short_lines", "no_trailing_newline", "one_quote_at_end", "cr_at_end"])
-def test_gpu_csv_onepass_vs_general(gpu_ctx, tmp_path, monkeypatch, shape):
-    """With QE_CSV_ONEPASS=1, files without '"' or '\\r' take the one-pass line-end list
-    (k_csv_ends1, segments chained by look-back); a '"' or '\\r' anywhere (here only in the last
-    line), or more line ends than its list holds (lines shorter than 16 bytes), sends the parse back
-    to the general passes. The default (general) passes equal the oracle on every shape, and the
-    one-pass scan (a fresh process: the switch is read once) gives the same columns."""
-    import subprocess
-    import sys
-
+@pytest.mark.parametrize("shape", ["plain", "short_lines", "no_trailing_newline", "one_quote_at_end", "cr_at_end",
+                                   "utf8", "tabs", "blank_and_comment_lines", "long_lines"])
+def test_gpu_csv_fast_path_vs_oracle(gpu_ctx, tmp_path, shape):
+    """A file without '"' or '\r' takes the classification pass (k_csv_classify: '\n' and delimiter
+    bitmaps) with the bitmap line-end list and line walk; a '"' or '\r' anywhere (here only in the
+    last line) sends it back to the general passes. Every shape equals the oracle: UTF-8 bytes whose
+    low seven bits alias '\n' / ',' / '"' / '\r' (0x8A, 0xAC, 0xA2, 0x8D), tab delimiters, blank and
+    comment lines (the kept-line path), lines longer than a 64-byte bitmap word, many 16 KiB
+    segments."""
     rng = random.Random(len(shape))
+    d = "\t" if shape == "tabs" else ","
     if shape == "short_lines":
-        body = [f"{i % 7},{i % 3}" for i in range(300_000)]  # 4-byte lines: over the list's capacity
+        body = [f"{i % 7}{d}{i % 3}" for i in range(300_000)]
+    elif shape == "utf8":
+        words = ["Ê", "¬", "¢", "ō", "Pärsson", "x"]
+        body = [f"{i % 13}{d}{rng.choice(words)}{d}{''.join(rng.choice(words) for _ in range(i % 9))}{d}{i}"
+                for i in range(120_000)]
+    elif shape == "long_lines":
+        body = [f"{i % 13}{d}{'y' * rng.choice([1, 60, 200, 3000])}{d}{'z' * (i % 70)}{d}{i}" for i in range(20_000)]
     else:
-        body = [f"{i % 13},{rng.random():.6f},{'x' * (i % 40)},{i}" for i in range(120_000)]
-    text = "k,v,s,i\n" + "\n".join(body)
+        body = [f"{i % 13}{d}{rng.random():.6f}{d}{'x' * (i % 40)}{d}{i}" for i in range(120_000)]
+    if shape == "blank_and_comment_lines":
+        for at in (7, 50_000, 119_990):
+            body.insert(at, rng.choice(["", "   ", "#comment,x", "\t"]))
+    text = f"k{d}v{d}s{d}i\n" + "\n".join(body)
     if shape == "one_quote_at_end":
         text += '\n1,"2",3,4'
     elif shape == "cr_at_end":
@@ -305,19 +271,7 @@ def test_gpu_csv_onepass_vs_general(gpu_ctx, tmp_path, monkeypatch, shape):
     onames, _, rows = R.parse(data)
     assert names == onames
     assert cols == R.project(rows, range(len(names)))
-    # the one-pass scan in a process of their own (the switch is read once per process)
-    code = ("import sys, json; sys.path[:0] = [{root!r}, {root!r} + '/query-engines_amd']\n"
-            "from kquery.columnar import Context\nfrom kquery.csv_source import CsvDataSource\n"
-            "ds = CsvDataSource({path!r}, True, 0, ctx=Context.get(0))\n"
-            "cols = [[] for _ in range(4)]\n"
-            "for b in ds.scan(['k', 'v', 's', 'i'][:{n}]):\n"
-            "    for i in range({n}): cols[i] += b.field(i).to_pylist()\n"
-            "print(json.dumps(cols))\n")
-    import pathlib
-
-    root = str(pathlib.Path(__file__).resolve().parents[1])
-    p = tmp_path / "t.csv"
-    env = dict(__import__("os").environ, QE_CSV_ONEPASS="1")
-    out = subprocess.run([sys.executable, "-c", code.format(root=root, path=str(p), n=len(names))], env=env,
-                         capture_output=True, text=True, timeout=240, check=True).stdout
-    assert __import__("json").loads(out.strip().splitlines()[-1]) == cols
+    # projections of single fields (the line walk's bit selection skips the others)
+    for f in (names[-1], names[1]):
+        _, _, c1, _ = _gpu_scan(gpu_ctx, tmp_path, data, [f])
+        assert c1[0] == R.project(rows, [names.index(f)])[0]
