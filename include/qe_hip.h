@@ -68,6 +68,7 @@ extern "C" {
 #define QE_ERR_DEVICE (-4)       /* HIP runtime error */
 #define QE_ERR_CAPACITY (-5)     /* output buffer too small */
 #define QE_ERR_COMM (-6)         /* RCCL communicator / collective failure */
+#define QE_NEED_EXACT 1          /* not an error: qe_agg_global_merge needs the exact round (below) */
 
 /* ---- types ------------------------------------------------------------------------------ */
 /* Arrow type ids used by this kernel. The reference knows only Float8 (fp64) and Utf8
@@ -237,11 +238,11 @@ int qe_filter_apply(qe_ctx* ctx, const qe_column* mask, const qe_column* inputs,
  * min/max follow MaxAccumulator (K:538-561): nulls skipped; the first non-null value
  * seeds; replaced only on strictly greater (less) => a NaN seed is sticky, a later NaN
  * never wins, +0.0/-0.0 ties keep the earliest. `valid` = 1 iff count > 0.
- * fp64 sum / avg: within 1e-9 of the exact sum or an error. The compensated sum is certified by
- * an error bound; when the bound cannot place it within 1e-9 (heavy cancellation), a second,
- * exact fixed-point pass gives the correctly rounded exact sum (QE_ERR_UNSUPPORTED for an input of
- * 2^182 or more). qe_agg_global_merge cannot go back to the rows: an uncertifiable merge returns
- * QE_ERR_UNSUPPORTED. int64 sum wraps; int64 avg is the compensated fp64 mean. */
+ * fp64 sum: the correctly rounded exact sum over the whole fp64 range (math.fsum's value; the
+ * IEEE result with NaN / Inf inputs; +-Inf when the exact sum overflows); avg = that sum / count.
+ * A compensated sum gives it when its error bound proves that every value within the bound rounds
+ * to the same double; otherwise a second, exact fixed-point pass over the column does.
+ * int64 sum wraps; int64 avg is the compensated fp64 mean. */
 typedef struct qe_global_agg {
   int64_t rows;   /* COUNT(*) over rows passing the mask */
   int64_t count;  /* COUNT(x) */
@@ -260,11 +261,20 @@ int qe_agg_global(qe_ctx* ctx, const qe_column* col, const qe_column* mask /*nul
  * global index of the column's first row, so MIN/MAX keep MaxAccumulator's row-order rules
  * (NaN seed, earliest of +0.0 / -0.0) across the pieces. qe_agg_global_merge folds n partials
  * (device, packed QE_GLOBAL_PARTIAL_BYTES apart, any order) in a fixed order into the final
- * result: every rank merging the same all-gathered partials gets the same bits. */
+ * result: every rank merging the same all-gathered partials gets the same bits.
+ * When the merged fp64 sum cannot be proven correctly rounded (the pieces' sums cancel),
+ * qe_agg_global_merge returns QE_NEED_EXACT with every other field of `out` final: each piece
+ * then writes its exact sum words (qe_agg_global_exact_partial, QE_GLOBAL_EXACT_BYTES of device
+ * memory), the words are gathered like the partials, and qe_agg_global_merge_exact sets
+ * out->sum and out->avg (synchronises). The second round happens on every rank or on none. */
 #define QE_GLOBAL_PARTIAL_BYTES 128
+#define QE_GLOBAL_EXACT_BYTES 320
 int qe_agg_global_partial(qe_ctx* ctx, const qe_column* col, const qe_column* mask /*nullable*/,
                           int64_t row_base, void* partial);
 int qe_agg_global_merge(qe_ctx* ctx, int32_t type, const void* partials, int32_t n, qe_global_agg* out);
+int qe_agg_global_exact_partial(qe_ctx* ctx, const qe_column* col, const qe_column* mask /*nullable*/,
+                                void* words);
+int qe_agg_global_merge_exact(qe_ctx* ctx, const void* words, int32_t n, qe_global_agg* out);
 
 /* ---- HashAggregateExec (K4b) ------------------------------------------------------------ */
 /* Group keys: 0..4 columns of any type — INT64, FLOAT64 (Double.equals: one NaN group, +0.0 and
@@ -305,15 +315,17 @@ int qe_hashagg_create(qe_ctx* ctx, int32_t nkeys, const int32_t* key_types, int3
 /* qe_hashagg_create with options.
  * fp64 SUM / AVG guarantee (within 1e-9 relative of the exact sum). By default they
  * accumulate exactly, in 256-bit fixed point (least significant bit 2^-128, integer adds: a 192-bit
- * window per LDS slot for |x| in [2^-44, 2^62), the global table's full words for every other
- * input), and finalize rounds the exact sum once to double: the result is the correctly rounded
- * exact sum, bit-identical whatever order rows, workgroups, batches or ranks combine in — what the
- * reference's sequential row loop and ordered partition merge give with exact arithmetic
- * (K:617-631, K:1314-1325). NaN / +-Inf inputs give NaN / the infinity, as IEEE addition does.
- * finalize fails with QE_ERR_UNSUPPORTED instead of returning a group's sum when that group had
- * an input of magnitude 2^182 (6e54) or more, or inputs with bits below 2^-128 whose rounding (half a
- * unit each) could exceed 1e-9 of the result. A state with exact sums synchronises in finalize to
- * check that (the outputs are complete when it returns).
+ * window per LDS slot for |x| in [2^-44, 2^62), the global table's full words for other inputs
+ * below 2^126) plus, for inputs of 2^126 or more or with bits below 2^-128 (subnormals included),
+ * a per-group 2176-bit accumulator in units of 2^-1074 that holds any finite double exactly.
+ * finalize rounds the exact sum once to double: the result is the correctly rounded exact sum over
+ * the whole fp64 range (math.fsum's value; +-Inf when it overflows), bit-identical whatever order
+ * rows, workgroups, batches or ranks combine in — what the reference's sequential row loop and
+ * ordered partition merge give with exact arithmetic (K:617-631, K:1314-1325). NaN / +-Inf inputs
+ * give NaN / the infinity, as IEEE addition does. finalize never fails for a sum and does not
+ * synchronise (stream-ordered like every other state). A group with such inputs exports
+ * FXE_CHUNKS = 9 extra records (qe_hashagg_export_counts counts them; every record of a group goes
+ * to its key's partition).
  * QE_HASHAGG_DETERMINISTIC: the default (kept for callers that name it).
  * QE_HASHAGG_FAST_FP64: plain fp64 atomics instead (one LDS atomic per row and aggregate); their
  * rounding depends on arrival order, and a group whose terms cancel can miss the 1e-9 contract. */

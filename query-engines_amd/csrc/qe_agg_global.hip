@@ -5,11 +5,13 @@
 //     a NaN seed is sticky, a later NaN never wins, and among +0.0/-0.0 ties the earliest row
 //     wins. In parallel this is a reduction of (non-NaN ordered key, first-non-null row,
 //     first-NaN row, first -0.0 row, first +0.0 row), each a commutative min/max.
-//   * int64 SUM wraps (JVM Long); fp64 SUM is a Neumaier-compensated tree sum whose error is
-//     bounded at the end (sum_certified: the partials also carry sum |x| and the infinite-input
-//     count); a sum the bound cannot place within 1e-9 of the exact one (heavy cancellation) is
-//     recomputed exactly by a second pass (k_agg_global_fx, qe_dev.hpp fixed point) in
-//     qe_agg_global, or fails loudly in qe_agg_global_merge (its rows are elsewhere).
+//   * int64 SUM wraps (JVM Long); fp64 SUM is the correctly rounded exact sum (math.fsum's value):
+//     a Neumaier-compensated tree sum whose error is bounded at the end (sum_certified: the
+//     partials also carry sum |x|, the infinite-input count and the summation depth) gives it
+//     when the bound shows that every value within the bound rounds to the same double; otherwise
+//     a second pass computes the exact sum (k_agg_global_fx, qe_dev.hpp fixed point and
+//     full-range words) — in qe_agg_global directly, and for merged pieces through
+//     qe_agg_global_exact_partial / qe_agg_global_merge_exact (QE_NEED_EXACT).
 // Layout: lane handles rows base + 128q + 2*lane + {0,1} (q = 0..3) so every 16-B load
 // instruction of a wave reads one contiguous KiB. Per-block partials are reduced by a second
 // single-block kernel in fixed order: bit-reproducible run to run.
@@ -28,6 +30,7 @@ struct GPart {
   int64_t ninf;              // infinite fp64 inputs
   int64_t kmin, kmax;        // ordered keys of non-NaN fp64
   uint64_t first_nn, first_nan, first_negz, first_posz;
+  int64_t depth;  // summation depth of s and c before this partial's last fold (set by the host)
 };
 
 __device__ __forceinline__ void gpart_init(GPart& p) {
@@ -41,6 +44,7 @@ __device__ __forceinline__ void gpart_init(GPart& p) {
   p.kmin = INT64_MAX;
   p.kmax = INT64_MIN;
   p.first_nn = p.first_nan = p.first_negz = p.first_posz = UINT64_MAX;
+  p.depth = 0;
 }
 
 __device__ __forceinline__ void neumaier_add(double& s, double& c, double x) {
@@ -65,6 +69,7 @@ __device__ __forceinline__ void gpart_merge(GPart& a, const GPart& b) {
   a.first_nan = min(a.first_nan, b.first_nan);
   a.first_negz = min(a.first_negz, b.first_negz);
   a.first_posz = min(a.first_posz, b.first_posz);
+  a.depth = max(a.depth, b.depth);
 }
 
 template <typename T>
@@ -90,6 +95,7 @@ __device__ __forceinline__ void gpart_wave_reduce(GPart& p) {
     o.first_nan = (uint64_t)shfl_x((int64_t)p.first_nan, m);
     o.first_negz = (uint64_t)shfl_x((int64_t)p.first_negz, m);
     o.first_posz = (uint64_t)shfl_x((int64_t)p.first_posz, m);
+    o.depth = shfl_x(p.depth, m);
     // fixed pairing order: the lower lane's partial is the left operand (operands selected, one
     // merge: a branch on the lane bit ran both merges in every wave)
     const bool hi = (threadIdx.x & m) != 0;
@@ -109,6 +115,7 @@ __device__ __forceinline__ void gpart_wave_reduce(GPart& p) {
     l.first_nan = hi ? o.first_nan : p.first_nan;    r.first_nan = hi ? p.first_nan : o.first_nan;
     l.first_negz = hi ? o.first_negz : p.first_negz; r.first_negz = hi ? p.first_negz : o.first_negz;
     l.first_posz = hi ? o.first_posz : p.first_posz; r.first_posz = hi ? p.first_posz : o.first_posz;
+    l.depth = hi ? o.depth : p.depth;                r.depth = hi ? p.depth : o.depth;
     gpart_merge(l, r);
     p = l;
   }
@@ -291,9 +298,11 @@ __global__ void __launch_bounds__(256) k_agg_global_f64_dense(const int64_t* __r
 
 static_assert(sizeof(GPart) <= QE_GLOBAL_PARTIAL_BYTES, "partial record size");
 
-// Row indices of a partial -> global rows (multi-batch / multi-GPU merges keep row order).
-__global__ void k_agg_global_rebase(GPart* __restrict__ p, int64_t row_base) {
+// Row indices of a partial -> global rows (multi-batch / multi-GPU merges keep row order); the
+// partial's summation depth for the merge's error bound.
+__global__ void k_agg_global_rebase(GPart* __restrict__ p, int64_t row_base, int64_t depth) {
   if (threadIdx.x == 0) {
+    p->depth = depth;
     if (p->first_nn != UINT64_MAX) p->first_nn += (uint64_t)row_base;
     if (p->first_nan != UINT64_MAX) p->first_nan += (uint64_t)row_base;
     if (p->first_negz != UINT64_MAX) p->first_negz += (uint64_t)row_base;
@@ -308,16 +317,22 @@ __global__ void k_agg_global_unpack(const uint8_t* __restrict__ recs, int n, GPa
 
 // Exact fp64 SUM of the selected non-null rows (the fallback when the compensated sum cannot be
 // certified): every thread adds its rows into its own 256-bit fixed-point accumulator in LDS
-// (qe_dev.hpp fx_*, plain read-modify-writes), the workgroup folds them in a fixed tree, and one
-// thread per workgroup adds the result into out[0..4] (w0..w3, status) with device atomics; integer
-// adds are associative, so the words are the exact sum whatever the order. Rare by construction, so
-// it is simple rather than fast.
+// (qe_dev.hpp fx_*, plain read-modify-writes) and inputs outside its range (|x| >= 2^126, bits
+// below 2^-128) into the workgroup's full-range words E (LDS atomics); the workgroup folds them in
+// a fixed tree and one thread adds the result into out[0..4] (w0..w3, status) and out[5..38] (E)
+// with device atomics. Integer adds are associative, so the words are the exact sum whatever the
+// order. Rare by construction, so it is simple rather than fast.
 __global__ void __launch_bounds__(256) k_agg_global_fx(const int64_t* __restrict__ vals, const uint8_t* __restrict__ valid,
                                                        const uint8_t* __restrict__ mv, const uint8_t* __restrict__ ml,
                                                        int64_t n, qu64* __restrict__ out) {
   __shared__ qu64 t[256 * 5];
+  __shared__ qu64 e[FXE_WORDS];
+  __shared__ int any_e;
   qu64* my = t + threadIdx.x * 5;
   for (int w = 0; w < 5; ++w) my[w] = 0;
+  if (threadIdx.x < FXE_WORDS) e[threadIdx.x] = 0;
+  if (threadIdx.x == 0) any_e = 0;
+  __syncthreads();
   auto wp = [&](int w) { return &my[w]; };
   for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
     const int sh = (int)(i & 7);
@@ -327,7 +342,13 @@ __global__ void __launch_bounds__(256) k_agg_global_fx(const int64_t* __restrict
       if (!(m & 1u)) continue;
     }
     if (valid && !((valid[i >> 3] >> sh) & 1)) continue;
-    fx_add_row<false>(wp, fx_row(vals[i]), &my[4]);
+    const FxRow r = fx_row(vals[i]);
+    if (r.st & (FX_HUGE | FX_INEXACT)) {
+      fxe_add_value<true>(e, vals[i]);
+      any_e = 1;
+    } else {
+      fx_add_row<false>(wp, r, &my[4]);
+    }
   }
   __syncthreads();
   for (int h = 128; h > 0; h >>= 1) {
@@ -337,8 +358,10 @@ __global__ void __launch_bounds__(256) k_agg_global_fx(const int64_t* __restrict
     }
     __syncthreads();
   }
-  if (threadIdx.x == 0)
+  if (threadIdx.x == 0) {
     fx_add_words<true>([&](int w) { return &out[w]; }, my[0], my[1], my[2], my[3], my[4], &out[4]);
+    if (any_e) fxe_add_words<true>(out + 5, 0, e, FXE_WORDS);
+  }
 }
 
 // host_out (optional): pinned host memory that also receives the result, so the caller reads it
@@ -372,19 +395,25 @@ __global__ void __launch_bounds__(256) k_agg_global_final(GPart* __restrict__ pa
   }
 }
 
-// Whether the compensated fp64 sum R = s + c of a partial is within FX_REL_TOL (1e-9) of the exact
-// sum. Every s update is an exact two-sum, so exact = s + sum of the error terms e_i, and c is the
-// plain-float sum of those terms: |e_i| <= u |t_i| (t_i the intermediate sums, each input inside at
-// most n of them) and summing them costs at most gamma_n of their total, so
-// |R - exact| <= u |R| + (1 + 2nu)^2 (nu)^2 sum|x| (u = 2^-53, n = the non-null count, which bounds
-// every chain depth). NaN inputs or infinities make R the IEEE result of the exact sum (certified);
-// an overflowed partial (non-finite R or sum|x| from finite inputs) is not.
-static bool sum_certified(const GPart& p, double r) {
+// Whether R = fl(s + c) of a partial is the correctly rounded exact sum. Every s update is an
+// exact two-sum, so exact = s + sum of the error terms e_i, and c is the plain-float sum of those
+// terms: |e_i| <= u |t_i| (t_i the intermediate sums; each input is inside at most D of them, D the
+// summation depth) and summing them in a tree of depth D costs at most gamma_D of their total, so
+// |s + c - exact| <= eb = (1 + 2Du)^2 (Du)^2 sum|x| (u = 2^-53; doubled for the rounding of sum|x|
+// itself). Additions whose result is subnormal are exact, so the bound holds down there too. When
+// the exact residual of R = fl(s + c) plus eb stays below half the gap from R to its nearer
+// neighbour, every value within eb of s + c rounds to R, the exact sum among them. NaN inputs or
+// infinities make R the IEEE result of the exact sum (certified); an overflowed partial (non-finite
+// R or sum|x| from finite inputs) is not.
+static bool sum_certified(const GPart& p, double r, double depth) {
   if (p.count == 0 || p.first_nan != UINT64_MAX || p.ninf > 0) return true;
   if (!std::isfinite(r) || !std::isfinite(p.a)) return false;
-  const double u = 0x1p-53, nu = (double)p.count * u, g = (1.0 + 2.0 * nu);
-  const double bound = 1.01 * (u * std::fabs(r) + g * g * nu * nu * p.a);
-  return bound <= FX_REL_TOL * std::fabs(r) || p.a == 0.0;
+  if (p.a == 0.0) return true;  // every input a zero: s and c are exact
+  const double u = 0x1p-53, du = depth * u, g = 1.0 + 2.0 * du;
+  const double eb = 2.0 * g * g * du * du * p.a;
+  const double bp = r - p.s, resid = (p.s - (r - bp)) + (p.c - bp);  // two-sum: s + c = r + resid exactly
+  const double gap = std::min(r - std::nextafter(r, -HUGE_VAL), std::nextafter(r, HUGE_VAL) - r);
+  return (std::fabs(resid) + eb) * (1.0 + 0x1p-40) < 0.5 * gap;
 }
 
 // Host-side finalisation of MIN/MAX for fp64 (MaxAccumulator order semantics).
@@ -401,9 +430,15 @@ using namespace qe;
 
 namespace qe {
 
-// The column's partial, reduced on the device into *result (a GPart in scratch).
+// Summation depth of the fold of n partials by k_agg_global_final: thread t folds partials t,
+// t + 256, ... (two merges per round), then the wave tree (6) and the block's four waves (3).
+static int64_t final_fold_depth(int64_t n) { return 2 * (int64_t)div_up((uint64_t)n, 512) + 2 + 6 + 3; }
+
+// The column's partial, reduced on the device into *result (a GPart in scratch); *depth its
+// summation depth (sum_certified): a lane's chain of rows, the dense kernel's fold of its eight
+// chains, the wave and block trees, and the final fold of the workgroups' partials.
 static int agg_global_partial(qe_ctx* ctx, const qe_column* col, const qe_column* mask, GPart** result,
-                              GPart* host_out = nullptr, unsigned long long* host_flag = nullptr) {
+                              int64_t* depth, GPart* host_out = nullptr, unsigned long long* host_flag = nullptr) {
   QE_CHECK(col, QE_ERR_INVALID_ARG, "null argument");
   QE_CHECK(col->type == QE_TYPE_INT64 || col->type == QE_TYPE_FLOAT64, QE_ERR_UNSUPPORTED,
            "global aggregate over type %d not supported (int64/fp64)", col->type);
@@ -427,6 +462,8 @@ static int agg_global_partial(qe_ctx* ctx, const qe_column* col, const qe_column
   const int64_t cap = (int64_t)ctx->num_cus * (dense ? ag_per_cu : 8);
   if (blocks > cap) blocks = cap;
   if (blocks < 1) blocks = 1;
+  const int64_t iters = (int64_t)div_up((uint64_t)(n > 0 ? n : 1), (uint64_t)blocks * 4 * 512);
+  *depth = (dense ? iters + 8 : 8 * iters) + 6 + 3 + final_fold_depth(blocks);
   void* s;
   QE_TRY(ctx_scratch(ctx, (size_t)(blocks + 1) * sizeof(GPart), &s));
   GPart* parts = (GPart*)s;
@@ -454,8 +491,8 @@ static int agg_global_partial(qe_ctx* ctx, const qe_column* col, const qe_column
 // (~6 us sooner per call: tools/exp_sync_latency.hip), with a stream query every 50 us so a failed
 // kernel still ends the wait. The result is then complete; later work on the stream is ordered
 // after the kernel as usual.
-static int agg_global_finish(qe_ctx* ctx, const GPart* dp, int32_t type, qe_global_agg* out, bool* certified,
-                             void* h = nullptr, volatile unsigned long long* flag = nullptr) {
+static int agg_global_finish(qe_ctx* ctx, const GPart* dp, int32_t type, int64_t depth, qe_global_agg* out,
+                             bool* certified, void* h = nullptr, volatile unsigned long long* flag = nullptr) {
   if (!h) {
     QE_TRY(ctx_pinned(ctx, sizeof(GPart), &h));
     QE_HIP(hipMemcpyAsync(h, dp, sizeof(GPart), hipMemcpyDeviceToHost, ctx->stream));
@@ -485,7 +522,7 @@ static int agg_global_finish(qe_ctx* ctx, const GPart* dp, int32_t type, qe_glob
   out->type = type;
   out->valid = p.count > 0 ? 1 : 0;
   const double fsum = std::isfinite(p.s) ? p.s + p.c : p.s;
-  *certified = !f64 || sum_certified(p, fsum);
+  *certified = !f64 || sum_certified(p, fsum, (double)(depth + p.depth));
   if (p.count > 0) {
     if (f64) {
       out->sum = f64_bits(fsum);
@@ -503,6 +540,38 @@ static int agg_global_finish(qe_ctx* ctx, const GPart* dp, int32_t type, qe_glob
 
 }  // namespace qe
 
+namespace qe {
+
+// The exact fp64 SUM words of a column's selected non-null rows (k_agg_global_fx) into words
+// (device, QE_GLOBAL_EXACT_BYTES): W, its status (FX_EXT set: E is always read), E.
+static int agg_global_exact(qe_ctx* ctx, const qe_column* col, const qe_column* mask, qu64* words) {
+  QE_HIP(hipMemsetAsync(words, 0, QE_GLOBAL_EXACT_BYTES, ctx->stream));
+  const int64_t n = col->length;
+  if (n == 0 || col->type != QE_TYPE_FLOAT64) return QE_OK;
+  const unsigned blocks = (unsigned)std::max<int64_t>(1, std::min<int64_t>((int64_t)div_up((uint64_t)n, 256),
+                                                                             (int64_t)ctx->num_cus * 4));
+  hipLaunchKernelGGL(k_agg_global_fx, dim3(blocks), dim3(256), 0, ctx->stream, (const int64_t*)col->values,
+                     col->validity, mask ? (const uint8_t*)mask->values : nullptr, mask ? mask->validity : nullptr, n,
+                     words);
+  return launch_check("k_agg_global_fx");
+}
+
+// out->sum / out->avg from n exact partials (host copies, QE_GLOBAL_EXACT_BYTES apart).
+static void exact_result(const uint8_t* words, int32_t n, qe_global_agg* out) {
+  qu64 w[5] = {0, 0, 0, 0, 0}, e[FXE_WORDS] = {};
+  for (int32_t i = 0; i < n; ++i) {
+    const qu64* p = (const qu64*)(words + (size_t)i * QE_GLOBAL_EXACT_BYTES);
+    fx_add_words<false>([&](int k) { return &w[k]; }, p[0], p[1], p[2], p[3], p[4] & ~(qu64)FX_EXT, &w[4]);
+    fxe_add_words<false>(e, 0, p + 5, FXE_WORDS);
+  }
+  if (out->count == 0) return;
+  const double v = fx_result(w[0], w[1], w[2], w[3], w[4] | FX_EXT, e);
+  out->sum = f64_bits(v);
+  out->avg = v / (double)out->count;
+}
+
+}  // namespace qe
+
 extern "C" int qe_agg_global(qe_ctx* ctx, const qe_column* col, const qe_column* mask, qe_global_agg* out) {
   QE_TRY(ctx_enter(ctx));
   QE_CHECK(out, QE_ERR_INVALID_ARG, "null argument");
@@ -512,33 +581,20 @@ extern "C" int qe_agg_global(qe_ctx* ctx, const qe_column* col, const qe_column*
   unsigned long long* flag = (unsigned long long*)((uint8_t*)h + kFlagOff);
   *(volatile unsigned long long*)flag = 0;  // (the previous call on this ctx has returned: its kernels wrote it)
   GPart* p;
-  QE_TRY(agg_global_partial(ctx, col, mask, &p, (GPart*)h, flag));
+  int64_t depth;
+  QE_TRY(agg_global_partial(ctx, col, mask, &p, &depth, (GPart*)h, flag));
   bool certified = true;
-  QE_TRY(agg_global_finish(ctx, p, col->type, out, &certified, h, flag));
+  QE_TRY(agg_global_finish(ctx, p, col->type, depth, out, &certified, h, flag));
   if (certified) return QE_OK;
-  // heavy cancellation: the exact sum from a second pass over the column
+  // not provably the correctly rounded sum: the exact sum from a second pass over the column
   void* s;
-  QE_TRY(ctx_scratch(ctx, 5 * sizeof(qu64), &s));
-  QE_HIP(hipMemsetAsync(s, 0, 5 * sizeof(qu64), ctx->stream));
-  const int64_t n = col->length;
-  const unsigned blocks = (unsigned)std::max<int64_t>(1, std::min<int64_t>((int64_t)div_up((uint64_t)n, 256),
-                                                                             (int64_t)ctx->num_cus * 4));
-  hipLaunchKernelGGL(k_agg_global_fx, dim3(blocks), dim3(256), 0, ctx->stream, (const int64_t*)col->values,
-                     col->validity, mask ? (const uint8_t*)mask->values : nullptr, mask ? mask->validity : nullptr, n,
-                     (qu64*)s);
-  QE_TRY(launch_check("k_agg_global_fx"));
+  QE_TRY(ctx_scratch(ctx, QE_GLOBAL_EXACT_BYTES, &s));
+  QE_TRY(agg_global_exact(ctx, col, mask, (qu64*)s));
   void* hw;
-  QE_TRY(ctx_pinned(ctx, 5 * sizeof(qu64), &hw));
-  QE_HIP(hipMemcpyAsync(hw, s, 5 * sizeof(qu64), hipMemcpyDeviceToHost, ctx->stream));
+  QE_TRY(ctx_pinned(ctx, QE_GLOBAL_EXACT_BYTES, &hw));
+  QE_HIP(hipMemcpyAsync(hw, s, QE_GLOBAL_EXACT_BYTES, hipMemcpyDeviceToHost, ctx->stream));
   QE_TRY(ctx_sync(ctx));
-  const qu64* w = (const qu64*)hw;
-  bool err = false;
-  const double v = fx_result(w[0], w[1], w[2], w[3], w[4], (qu64)out->count, &err);
-  QE_CHECK(!err, QE_ERR_UNSUPPORTED,
-           "global fp64 SUM not exact to 1e-9 (an input of 2^182 or more, or inputs below 2^-128 rounded "
-           "beyond the bound)");
-  out->sum = f64_bits(v);
-  out->avg = v / (double)out->count;
+  exact_result((const uint8_t*)hw, 1, out);
   return QE_OK;
 }
 
@@ -547,8 +603,9 @@ extern "C" int qe_agg_global_partial(qe_ctx* ctx, const qe_column* col, const qe
   QE_TRY(ctx_enter(ctx));
   QE_CHECK(partial && row_base >= 0, QE_ERR_INVALID_ARG, "bad arguments");
   GPart* p;
-  QE_TRY(agg_global_partial(ctx, col, mask, &p));
-  hipLaunchKernelGGL(k_agg_global_rebase, dim3(1), dim3(64), 0, ctx->stream, p, row_base);
+  int64_t depth;
+  QE_TRY(agg_global_partial(ctx, col, mask, &p, &depth));
+  hipLaunchKernelGGL(k_agg_global_rebase, dim3(1), dim3(64), 0, ctx->stream, p, row_base, depth);
   QE_TRY(launch_check("k_agg_global_rebase"));
   QE_HIP(hipMemsetAsync(partial, 0, QE_GLOBAL_PARTIAL_BYTES, ctx->stream));
   QE_HIP(hipMemcpyAsync(partial, p, sizeof(GPart), hipMemcpyDeviceToDevice, ctx->stream));
@@ -571,9 +628,27 @@ extern "C" int qe_agg_global_merge(qe_ctx* ctx, int32_t type, const void* partia
                      (unsigned long long*)nullptr);
   QE_TRY(launch_check("k_agg_global_final"));
   bool certified = true;
-  QE_TRY(agg_global_finish(ctx, parts + n, type, out, &certified, h));
-  QE_CHECK(certified, QE_ERR_UNSUPPORTED,
-           "global fp64 SUM over %d partials cannot be certified within 1e-9 of the exact sum (the shards' "
-           "sums cancel); run qe_agg_global over the whole column for the exact sum", (int)n);
+  QE_TRY(agg_global_finish(ctx, parts + n, type, final_fold_depth(n), out, &certified, h));
+  return certified ? QE_OK : QE_NEED_EXACT;
+}
+
+extern "C" int qe_agg_global_exact_partial(qe_ctx* ctx, const qe_column* col, const qe_column* mask, void* words) {
+  QE_TRY(ctx_enter(ctx));
+  QE_CHECK(col && words, QE_ERR_INVALID_ARG, "null argument");
+  QE_CHECK(col->length >= 0 && (col->values || col->length == 0), QE_ERR_INVALID_ARG, "bad column");
+  QE_CHECK(!mask || (mask->type == QE_TYPE_BOOL && mask->length == col->length), QE_ERR_INVALID_ARG,
+           "mask must be BOOL of equal length");
+  return agg_global_exact(ctx, col, mask, (qu64*)words);
+}
+
+extern "C" int qe_agg_global_merge_exact(qe_ctx* ctx, const void* words, int32_t n, qe_global_agg* out) {
+  QE_TRY(ctx_enter(ctx));
+  QE_CHECK(words && out && n >= 1, QE_ERR_INVALID_ARG, "bad arguments");
+  if (out->type != QE_TYPE_FLOAT64) return QE_OK;
+  void* hw;
+  QE_TRY(ctx_pinned(ctx, (size_t)n * QE_GLOBAL_EXACT_BYTES, &hw));
+  QE_HIP(hipMemcpyAsync(hw, words, (size_t)n * QE_GLOBAL_EXACT_BYTES, hipMemcpyDeviceToHost, ctx->stream));
+  QE_TRY(ctx_sync(ctx));
+  exact_result((const uint8_t*)hw, n, out);
   return QE_OK;
 }

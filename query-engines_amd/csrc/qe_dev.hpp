@@ -106,6 +106,7 @@ struct DTable {
   qi64* acc[QE_MAX_AGGS];
   qu64* nn[QE_MAX_AGGS];
   qu64* idx[QE_MAX_AGGS];  // 4 arrays of cap+2 each (fp64 MIN/MAX only)
+  qu64* ext[QE_MAX_AGGS];  // exact fp64 SUM: FXE_WORDS words per slot (the full-range part, qe_dev fxe_*)
   qu64 cap;                // power of two; slots cap, cap+1 special
   qu64* ctl;               // [0] groups, [1] deferred rows, [2] overflow records, [3] lost
 };
@@ -199,21 +200,29 @@ __host__ __device__ inline qu64 idx_identity(int acc) { return acc_is_f64mm(acc)
 // A slot's fp64 SUM is a 256-bit two's complement integer W in units of 2^-128 (sum = W * 2^-128):
 // four 64-bit words w0..w3, w3 the signed top, plus a status word. Words live in acc (w0) and idx
 // words 0..2 (w1..w3); idx word 3 is the status:
-//   bits 0..7   flags, OR-ed: a NaN input, a +Inf input, a -Inf input, an input with |x| >= 2^182,
-//               an input with bits below 2^-128 (rounded to the nearest multiple, ties to even)
-//   bits 8..63  signed count of net wraps of W: the exact sum is (W + wraps * 2^256) * 2^-128
+//   bits 0..7   flags, OR-ed (below)
+//   bits 8..63  signed count of net wraps of W: W's part of the sum is (W + wraps * 2^256) * 2^-128
 // A row adds its value's (at most 117-bit) two's complement image to the two words its mantissa
 // spans, with integer atomics that return the old word; only a carry out of the second word or a
 // change of the running sum's sign moves on to the next word. Integer adds are associative, so any
 // order of rows, workgroups, passes, batches or ranks gives the same words: the result is the
 // correctly rounded exact sum, bit-identical run to run. NaN / +-Inf inputs give the IEEE result
-// of the sum (NaN, or the infinity). An input in [2^126, 2^182) is exact too: its bits above the
-// words go straight into the wrap count (fx_row_words). An input of 2^182 or more, or rounded
-// inputs whose error bound
-// (non-null count x 2^-129) exceeds FX_REL_TOL of the result, make finalize fail (qe_hashagg.hip).
-constexpr qu64 FX_NAN = 1, FX_PINF = 2, FX_NINF = 4, FX_HUGE = 8, FX_INEXACT = 16, FX_FLAGS = 0xFF;
+// of the sum (NaN, or the infinity). Every other finite input — |x| >= 2^126, or with bits below
+// 2^-128 (subnormals among them) — goes whole into the slot's full-range accumulator E (fxe_*,
+// below): a 2176-bit integer in units of 2^-1074 that holds any finite double exactly, so no input
+// is ever rounded and the result is the correctly rounded sum over the whole fp64 range (gradual
+// underflow and IEEE overflow to +-Inf included). The wrap count then only follows sums of inputs
+// below 2^126: it stays in range up to 2^55 such inputs at the top of that range.
+// Partials (records, combines) carry such an input in RAW form (word 0 = its bits) and E in CHUNK
+// form (E's words 4c .. 4c + 3 in w0..w3; an exported group with E sends FXE_CHUNKS of them); both
+// are added to E, never to W.
+//   flags: FX_NAN / FX_PINF / FX_NINF the IEEE specials seen; FX_EXT the slot's E may be nonzero
+//   (E is zero otherwise); FX_RAW / FX_CHUNK a partial's form (c in bits 8..15); FX_HUGE /
+//   FX_INEXACT classify an input (fx_row: it needs E) and never reach a slot.
+constexpr qu64 FX_NAN = 1, FX_PINF = 2, FX_NINF = 4, FX_HUGE = 8, FX_INEXACT = 16, FX_EXT = 32, FX_RAW = 64,
+               FX_CHUNK = 128, FX_FLAGS = 0xFF, FX_SPECIAL = FX_NAN | FX_PINF | FX_NINF;
+constexpr int FXE_WORDS = 34, FXE_CHUNKS = 9, FXE_LSB = 1074;  // 2176 bits, units of 2^-1074
 constexpr qu64 FX_WRAP = 1ull << 8;  // one net wrap of W (signed count in bits 8..63)
-constexpr double FX_REL_TOL = 1e-9;
 // rare-path helpers of the exact sums: out of line unless a generated kernel asks otherwise
 #ifdef QE_FX_INLINE
 #define QE_FX_OUTLINE inline
@@ -222,9 +231,8 @@ constexpr double FX_REL_TOL = 1e-9;
 #endif
 constexpr int FX_LSB = 128;
 
-// One input's image: (hi:lo) two's complement at words k, k+1 (k == -1: nothing to add; k == -2:
-// |x| in [2^126, 2^182), added as a whole partial, fx_row_words), sign extended above; st = its
-// status flags.
+// One input's image: (hi:lo) two's complement at words k, k+1 (k == -1: nothing to add to W),
+// sign extended above; st = its status flags (FX_HUGE / FX_INEXACT: an input for E).
 struct FxRow {
   qu64 lo, hi, st;
   int k;
@@ -247,19 +255,17 @@ __host__ __device__ inline FxRow fx_row(qi64 bits) {
     p = ex - 1075 + FX_LSB;
   }
   if (m == 0) return r;
-  if (p < 0) {  // bits below 2^-128: round to the nearest multiple, ties to even
+  if (p < 0) {  // bits below 2^-128 (whole multiples of 2^-128 stay in W)
     const int sh = -p;
-    r.st = FX_INEXACT;
-    if (sh > 54) return r;  // m < 2^53 < half a unit: 0
-    const qu64 q = m >> sh, rem = m & ((1ull << sh) - 1), half = 1ull << (sh - 1);
-    if (rem == 0) r.st = 0;
-    m = q + ((rem > half || (rem == half && (q & 1))) ? 1 : 0);
+    if (sh >= 53 || (m & ((1ull << sh) - 1))) {
+      r.st = FX_INEXACT;
+      return r;
+    }
+    m >>= sh;
     p = 0;
-    if (m == 0) return r;
   }
   if (p + 64 - __builtin_clzll(m) > 254) {  // |x| >= 2^126: beyond the words' headroom
-    if (p + 64 - __builtin_clzll(m) > 310) r.st |= FX_HUGE;  // >= 2^182: beyond the wrap count too
-    else r.k = -2;
+    r.st = FX_HUGE;
     return r;
   }
   r.k = p >> 6;
@@ -306,19 +312,9 @@ __host__ __device__ inline void fx_status(qu64* st, qu64 v) {
   }
 }
 
-// One row into a slot whose word w is at wp(w).
-template <bool ATOMIC, class WP>
-__host__ __device__ inline void fx_add_words(WP wp, qu64 v0, qu64 v1, qu64 v2, qu64 v3, qu64 vst, qu64* st);
-__host__ __device__ inline void fx_row_words(qi64 bits, qu64 w[5]);
-
+// One row (not FX_HUGE / FX_INEXACT: the caller sends those to E) into a slot whose word w is at wp(w).
 template <bool ATOMIC, class WP>
 __host__ __device__ inline void fx_add_row(WP wp, const FxRow& r, qu64* st) {
-  if (r.k == -2) {  // [2^126, 2^182): the whole 320-bit image
-    qu64 w[5];
-    fx_row_words(r.bits, w);
-    fx_add_words<ATOMIC>(wp, w[0], w[1], w[2], w[3], w[4], st);
-    return;
-  }
   qu64 sd = r.st;
   if (r.k >= 0) {
     int w = r.k;
@@ -418,97 +414,18 @@ __host__ __device__ inline void fxw_words(qu64 u0, qu64 u1, qu64 u2, qu64 v[4]) 
   v[3] = (qu64)((qi64)u2 >> 32);
 }
 
-// ---- the per-workgroup LDS limb window (plan-specialised kernels, default) --------------------------
-// Six signed 64-bit words W0..W5 per slot: word i holds a sum of signed 32-bit limbs of weight
-// 2^(32 i), in units of 2^-96, so the slot's value is sum_i W_i 2^(32 i - 96). A row that is not
-// fx_rare (|x| in [2^-44, 2^62), or +-0) adds its 53-bit mantissa, shifted to its exponent, as
-// three limbs (bits 0-31, 32-63, 64-84 of the shifted mantissa) negated for x < 0, with three LDS
-// atomics that return nothing: no carries, so no round trip, no divergence and no queue. Every
-// |limb| is below 2^32 and a workgroup adds fewer than 2^31 rows to a slot in one launch, so no
-// word can overflow. The flush folds the words into a global partial (fxl_partial).
-constexpr int FXL_WORDS = 6;
-__host__ __device__ inline void fxl_limbs(qi64 bits, int* k, qu64* l0, qu64* l1, qu64* l2) {
-  const qu64 b = (qu64)bits;
-  const int ex = (int)((b >> 52) & 0x7FF);
-  const qu64 m = ex ? ((b & ((1ull << 52) - 1)) | (1ull << 52)) : 0ull;  // ex 0: +-0 (subnormals are rare)
-  const int p = ex ? ex - FXW_EX_LO : 0, q = p & 31;
-  *k = p >> 5;
-  const qu64 lo = m << q, hi = q ? (m >> (64 - q)) : 0ull;
-  qu64 a = lo & 0xFFFFFFFFull, c = lo >> 32, d = hi;
-  if (b >> 63) {  // two's complement of each limb: the words are signed sums
-    a = 0ull - a;
-    c = 0ull - c;
-    d = 0ull - d;
-  }
-  *l0 = a;
-  *l1 = c;
-  *l2 = d;
-}
-template <bool ATOMIC = true, class WP>
-__host__ __device__ inline void fxl_add(WP wp, qi64 bits) {
-  int k;
-  qu64 a, c, d;
-  fxl_limbs(bits, &k, &a, &c, &d);
-  if constexpr (ATOMIC) {
-    atomicAdd(wp(k), a);
-    atomicAdd(wp(k + 1), c);
-    atomicAdd(wp(k + 2), d);
-  } else {
-    *wp(k) += a;
-    *wp(k + 1) += c;
-    *wp(k + 2) += d;
-  }
-}
-// The words W0..W5 as a global partial (units 2^-128: W_i at bit 32 (i + 1)): v[0..3] and the
-// status word (the wrap count above the 256 bits; zero for any workgroup's window).
-__host__ __device__ inline void fxl_partial(qu64 w0, qu64 w1, qu64 w2, qu64 w3, qu64 w4, qu64 w5, qu64 v[4],
-                                            qu64* st) {
-  const qu64 W[FXL_WORDS] = {w0, w1, w2, w3, w4, w5};
-  qu64 a[5] = {0, 0, 0, 0, 0};
-#pragma unroll
-  for (int i = 0; i < FXL_WORDS; ++i) {
-    const int bit = 32 * (i + 1), wi = bit >> 6, sh = bit & 63;  // sh: 0 or 32
-    const qu64 x = W[i], ext = ((qi64)x < 0) ? ~0ull : 0ull;
-    qu64 c = 0;
-#pragma unroll
-    for (int q = 0; q < 5; ++q) {
-      const qu64 t = q < wi ? 0ull
-                     : q == wi ? (sh ? (x << sh) : x)
-                     : q == wi + 1 ? (sh ? ((x >> (64 - sh)) | (ext << sh)) : ext)
-                                   : ext;
-      const qu64 s1 = a[q] + t, c1 = s1 < t ? 1ull : 0ull;
-      const qu64 s2 = s1 + c, c2 = s2 < s1 ? 1ull : 0ull;
-      a[q] = s2;
-      c = c1 | c2;
-    }
-  }
-#pragma unroll
-  for (int q = 0; q < 4; ++q) v[q] = a[q];
-  *st = (qu64)((qi64)a[4] + (qi64)(a[3] >> 63)) * FX_WRAP;
-}
+
+// Whether an input needs the full-range accumulator (>= 2^182, or bits below 2^-128).
+__host__ __device__ inline bool fx_needs_ext(qi64 bits) { return (fx_row(bits).st & (FX_HUGE | FX_INEXACT)) != 0; }
 
 // The words of one input alone (RowVal form: the global-table and record paths): w[0..3] and the
-// status word (flags, and for |x| in [2^126, 2^182) the bits above the words as a wrap count).
+// status word; an input for E in RAW form.
 __host__ __device__ inline void fx_row_words(qi64 bits, qu64 w[5]) {
   const FxRow r = fx_row(bits);
-  if (r.k == -2) {  // 320-bit image of m << p, p = exponent position in units of 2^-128
-    const qu64 b = (qu64)bits;
-    const qu64 m = (b & ((1ull << 52) - 1)) | (1ull << 52);
-    const int p = (int)((b >> 52) & 0x7FF) - 1075 + FX_LSB, a = p >> 6, sh = p & 63;
-    qu64 v[5];
-#pragma unroll
-    for (int i = 0; i < 5; ++i)  // (selects, not a dynamic index: the array stays in registers)
-      v[i] = i == a ? m << sh : (i == a + 1 && sh ? m >> (64 - sh) : 0ull);
-    if (r.neg) {
-      qu64 c = 1;
-      for (int i = 0; i < 5; ++i) {
-        v[i] = ~v[i] + c;
-        c = (c && v[i] == 0) ? 1ull : 0ull;
-      }
-    }
-    for (int i = 0; i < 4; ++i) w[i] = v[i];
-    const qi64 wraps = (qi64)v[4] + (qi64)(v[3] >> 63);  // with W's top word read as signed
-    w[4] = (qu64)wraps * FX_WRAP;
+  if (r.st & (FX_HUGE | FX_INEXACT)) {
+    w[0] = (qu64)bits;
+    w[1] = w[2] = w[3] = 0;
+    w[4] = FX_RAW;
     return;
   }
 #pragma unroll
@@ -552,30 +469,152 @@ __host__ __device__ inline double fx_to_double(qu64 w0, qu64 w1, qu64 w2, qu64 w
     mant >>= 1;
     ++ex;
   }
-  // exact scaling by 2^ex: msb < 320, so -180 <= ex <= 140, a normal power of two
+  // exact scaling by 2^ex: msb < 320 (wraps within +-2^62), so -180 <= ex <= 140, a normal power of two
   const double d = (double)mant * bits_f64((qi64)((qu64)(1023 + ex) << 52));
   return neg ? -d : d;
 }
 
-// The SUM of a slot (`nn` non-null inputs). *err: the sum cannot be given within FX_REL_TOL of the
-// exact one (an input >= 2^182, or more rounding than the result's size allows).
-__host__ __device__ inline double fx_result(qu64 w0, qu64 w1, qu64 w2, qu64 w3, qu64 st, qu64 nn, bool* err) {
-  *err = false;
+// ---- the full-range accumulator of an exact fp64 SUM ----------------------------------------------------
+// A 2176-bit two's complement integer E in units of 2^-1074 (34 words, e[33] the signed top): every
+// finite double is a whole number of units, and any sum of fewer than 2^63 of them stays below 2^1101
+// in magnitude. A slot's exact sum is E * 2^-1074 + (W + wraps * 2^256) * 2^-128.
+// One input into E: its mantissa's two's complement image at the words it spans, the carry and sign
+// extension moving up word by word only while they do not cancel (fx_add_row's scheme).
+template <bool ATOMIC>
+__host__ __device__ inline void fxe_add_value(qu64* e, qi64 bits) {
+  const qu64 b = (qu64)bits;
+  const int ex = (int)((b >> 52) & 0x7FF);
+  qu64 m = b & ((1ull << 52) - 1);
+  if (ex) m |= 1ull << 52;
+  if (m == 0 || ex == 0x7FF) return;  // +-0; NaN / Inf never come here
+  const int p = ex ? ex - 1 : 0;       // the mantissa's lowest bit, in units of 2^-1074
+  int w = p >> 6;
+  const int q = p & 63;
+  const bool neg = b >> 63;
+  qu64 lo = m << q, hi = q ? (m >> (64 - q)) : 0ull;
+  if (neg) {
+    lo = 0ull - lo;
+    hi = ~hi + (lo == 0 ? 1ull : 0ull);
+  }
+  qu64 old = fx_xadd<ATOMIC>(&e[w], lo);
+  const qu64 t = hi + (old + lo < old ? 1ull : 0ull);
+  if (++w >= FXE_WORDS) return;
+  old = fx_xadd<ATOMIC>(&e[w], t);
+  qi64 d = (qi64)((t < hi ? 1 : 0) + (old + t < old ? 1 : 0)) - (neg ? 1 : 0);
+#pragma unroll 1
+  while (d != 0 && ++w < FXE_WORDS) {
+    old = fx_xadd<ATOMIC>(&e[w], (qu64)d);
+    d = d > 0 ? (old == ~0ull ? 1 : 0) : (old != 0 ? 0 : -1);
+  }
+}
+
+// Words v[0..n) (a chunk of another accumulator: unsigned, except the top word's sign) into E at
+// word w0, the carry moving up.
+template <bool ATOMIC>
+__host__ __device__ inline void fxe_add_words(qu64* e, int w0, const qu64* v, int n) {
+  qu64 c = 0;
+  int w = w0;
+  for (int i = 0; i < n; ++i, ++w) {
+    const qu64 t = v[i] + c;
+    qu64 cb = 0;
+    if (t) {
+      const qu64 old = fx_xadd<ATOMIC>(&e[w], t);
+      cb = old + t < old ? 1ull : 0ull;
+    }
+    c = (t < v[i] ? 1ull : 0ull) + cb;
+  }
+#pragma unroll 1
+  for (; c && w < FXE_WORDS; ++w) c = fx_xadd<ATOMIC>(&e[w], 1ull) == ~0ull ? 1ull : 0ull;
+}
+
+// Correctly rounded double (ties to even; IEEE overflow to +-Inf, gradual underflow) of
+// E * 2^-1074 + (W + wraps * 2^256) * 2^-128.
+__host__ __device__ inline double fxe_result(const qu64* e, qu64 w0, qu64 w1, qu64 w2, qu64 w3, qi64 wraps) {
+  qu64 x[FXE_WORDS];
+  for (int i = 0; i < FXE_WORDS; ++i) x[i] = e[i];
+  // W (five words with the wraps, signed) shifted up by 1074 - 128 = 946 bits = 14 words + 50
+  const qu64 m5[5] = {w0, w1, w2, w3, (qu64)(wraps + ((qi64)w3 >> 63))};
+  qu64 sh[FXE_WORDS];
+  const qu64 ext = ((qi64)m5[4] < 0) ? ~0ull : 0ull;
+  for (int i = 0; i < FXE_WORDS; ++i) {
+    const int k = i - 14;  // word of the unshifted W feeding bits [64 i, 64 i + 64): k and k - 1
+    const qu64 a = k < 0 ? 0ull : (k < 5 ? m5[k] : ext);
+    const qu64 bl = k - 1 < 0 ? 0ull : (k - 1 < 5 ? m5[k - 1] : ext);
+    sh[i] = (a << 50) | (k - 1 < 0 ? 0ull : (bl >> 14));
+  }
+  qu64 c = 0;
+  for (int i = 0; i < FXE_WORDS; ++i) {
+    const qu64 s1 = x[i] + sh[i], c1 = s1 < sh[i] ? 1ull : 0ull;
+    const qu64 s2 = s1 + c, c2 = s2 < s1 ? 1ull : 0ull;
+    x[i] = s2;
+    c = c1 | c2;
+  }
+  const bool neg = (qi64)x[FXE_WORDS - 1] < 0;
+  if (neg) {
+    qu64 carry = 1;
+    for (int i = 0; i < FXE_WORDS; ++i) {
+      x[i] = ~x[i] + carry;
+      carry = (carry && x[i] == 0) ? 1ull : 0ull;
+    }
+  }
+  int top = FXE_WORDS - 1;
+  while (top >= 0 && x[top] == 0) --top;
+  if (top < 0) return neg ? -0.0 : 0.0;
+  const int msb = 64 * top + 63 - __builtin_clzll(x[top]);
+  double d;
+  if (msb < 53) {  // a whole number of 2^-1074 below 2^53 units: exact (subnormal or the smallest normals)
+    d = (double)x[0] * 0x1p-1074;
+  } else {
+    const int lowpos = msb - 63;
+    qu64 win;
+    bool sticky = false;
+    if (lowpos <= 0) {
+      win = x[0] << (-lowpos);
+    } else {
+      const int a = lowpos >> 6, s = lowpos & 63;
+      win = s ? ((x[a] >> s) | (x[a + 1] << (64 - s))) : x[a];
+      sticky = s && (x[a] & ((1ull << s) - 1)) != 0;
+      for (int i = 0; i < a && !sticky; ++i) sticky = x[i] != 0;
+    }
+    qu64 mant = win >> 11;
+    const qu64 rem = win & 0x7FFull;
+    if (rem > 0x400 || (rem == 0x400 && (sticky || (mant & 1)))) ++mant;
+    int ex = msb - 52 - FXE_LSB;  // the mantissa's lowest bit: 2^ex
+    if (mant >> 53) {
+      mant >>= 1;
+      ++ex;
+    }
+    if (ex + 52 > 1023) {
+      d = __builtin_inf();
+    } else {  // 2^ex in two exact steps (ex in [-1073, 971])
+      const int e1 = ex / 2, e2 = ex - e1;
+      d = (double)mant * bits_f64((qi64)((qu64)(1023 + e1) << 52)) * bits_f64((qi64)((qu64)(1023 + e2) << 52));
+    }
+  }
+  return neg ? -d : d;
+}
+
+// A RAW or CHUNK partial into E at e; the slot's status at st gets FX_EXT and the partial's specials.
+template <bool ATOMIC>
+__host__ __device__ inline void fxe_partial(qu64* e, qu64* st, qu64 w0, qu64 w1, qu64 w2, qu64 w3, qu64 vst) {
+  if (vst & FX_RAW) {
+    fxe_add_value<ATOMIC>(e, (qi64)w0);
+  } else {
+    const int c = (int)((vst >> 8) & 0xFF);
+    const qu64 v[4] = {w0, w1, w2, w3};
+    if (c < FXE_CHUNKS) fxe_add_words<ATOMIC>(e, 4 * c, v, c == FXE_CHUNKS - 1 ? FXE_WORDS - 4 * c : 4);
+  }
+  fx_status<ATOMIC>(st, FX_EXT | (vst & FX_SPECIAL));
+}
+
+// The SUM of a slot: words w0..w3, status st, E at e (read only when st has FX_EXT).
+__host__ __device__ inline double fx_result(qu64 w0, qu64 w1, qu64 w2, qu64 w3, qu64 st, const qu64* e) {
   const qu64 f = st & FX_FLAGS;
   if ((f & FX_NAN) || ((f & FX_PINF) && (f & FX_NINF))) return bits_f64(0x7FF8000000000000ll);
   if (f & FX_PINF) return bits_f64(0x7FF0000000000000ll);
   if (f & FX_NINF) return bits_f64((qi64)0xFFF0000000000000ull);
-  if (f & FX_HUGE) {
-    *err = true;
-    return bits_f64(0x7FF8000000000000ll);
-  }
-  const double v = fx_to_double(w0, w1, w2, w3, (qi64)st >> 8);
-  // every rounded input is off by at most half a unit (2^-129)
-  if ((f & FX_INEXACT) && (double)nn * 0x1p-129 > FX_REL_TOL * (v < 0 ? -v : v)) {
-    *err = true;
-    return bits_f64(0x7FF8000000000000ll);
-  }
-  return v;
+  if (f & FX_EXT) return fxe_result(e, w0, w1, w2, w3, (qi64)st >> 8);
+  return fx_to_double(w0, w1, w2, w3, (qi64)st >> 8);
 }
 __host__ __device__ inline qi64 acc_identity(int acc) {
   switch (acc) {
@@ -659,7 +698,9 @@ __device__ inline bool gtable_find_wg(const DTable& t, qi64 key, bool knull, qu6
   return false;
 }
 
+// (c == 0: a record that carries only exact-SUM parts; its group is counted by the records with rows)
 __device__ inline void gadd_cstar(const DTable& t, qu64 slot, qu64 c) {
+  if (!c) return;
   const qu64 old = atomicAdd(&t.cstar[slot], c);
   if (slot >= t.cap && old == 0) atomicAdd(&t.ctl[0], 1ull);  // a special group appears
 }
@@ -674,6 +715,10 @@ static __device__ QE_FX_OUTLINE void gcombine_fx(const DTable& t, int j, qu64 s,
                                                              qu64 w2, qu64 w3, qu64 st) {
   const qu64 stride = t.cap + 2;
   qu64* ix = t.idx[j];
+  if (st & (FX_RAW | FX_CHUNK)) {  // an input or a chunk for E
+    fxe_partial<true>(t.ext[j] + s * FXE_WORDS, &ix[3 * stride + s], w0, w1, w2, w3, st);
+    return;
+  }
   fx_add_words<true>([&](int w) { return w == 0 ? (qu64*)&t.acc[j][s] : &ix[(w - 1) * stride + s]; }, w0, w1, w2, w3,
                      st, &ix[3 * stride + s]);
 }
@@ -724,6 +769,7 @@ __device__ inline void gcombine(const DTable& t, int acck, int j, qu64 s, qi64 a
 // replace the device-scope atomics. The table was last written by earlier launches (or not at
 // all), whose writes the launch boundary makes visible; same results as the atomic forms.
 __device__ inline void gadd_cstar_excl(const DTable& t, qu64 slot, qu64 c, qu32* newg) {
+  if (!c) return;
   const qu64 old = t.cstar[slot];
   t.cstar[slot] = old + c;
   if (slot >= t.cap && old == 0) atomicAdd(newg, 1u);
@@ -757,6 +803,10 @@ __device__ inline void gcombine_excl(const DTable& t, int acck, int j, qu64 s, q
   } else if (acck == ACC_SUM_X) {
     const qu64 stride = t.cap + 2;
     qu64* ix = t.idx[j] + s;
+    if (i3 & (FX_RAW | FX_CHUNK)) {
+      fxe_partial<false>(t.ext[j] + s * FXE_WORDS, &ix[3 * stride], (qu64)acc, i0, i1, i2, i3);
+      return;
+    }
     fx_add_words<false>([&](int w) { return w == 0 ? (qu64*)a : &ix[(w - 1) * stride]; }, (qu64)acc, i0, i1, i2, i3,
                         &ix[3 * stride]);
   }
@@ -1001,17 +1051,13 @@ __device__ inline void lds_fxw_add(qi64* acc, qu64* idx, int SS, int s, qi64 x) 
   fxw_add([&](int w) { return w == 0 ? (qu64*)&acc[s] : &idx[(w - 1) * SS + s]; }, x);
 }
 
-// ACC_SUM_X row into an LDS limb window (acc[s] = W0, idx[(k - 1) SS + s] = Wk): plan-specialised
-// kernels, rows that are not fx_rare.
-__device__ inline void lds_fxl_add(qi64* acc, qu64* idx, int SS, int s, qi64 x) {
-  fxl_add([&](int w) { return w == 0 ? (qu64*)&acc[s] : &idx[(w - 1) * SS + s]; }, x);
-}
-
 // ACC_SUM_X row into a full LDS slot (acc[s] = word 0, idx[k * SS + s] = word k + 1, idx[3 SS + s] =
-// status word).
-__device__ inline void lds_fx_add(qi64* acc, qu64* idx, int SS, int s, qi64 x) {
+// status word). false: the row is an input for E (the caller sends it to the global slot).
+__device__ inline bool lds_fx_add(qi64* acc, qu64* idx, int SS, int s, qi64 x) {
   const FxRow r = fx_row(x);
+  if (r.st & (FX_HUGE | FX_INEXACT)) return false;
   fx_add_row<true>([&](int w) { return w == 0 ? (qu64*)&acc[s] : &idx[(w - 1) * SS + s]; }, r, &idx[3 * SS + s]);
+  return true;
 }
 
 // LDS MIN / MAX that read first: the atomic only when the value would change the slot. Slots only

@@ -83,7 +83,12 @@ __device__ __forceinline__ void lds_accum_value(const Plan& P, char* smem, int j
   switch (a.acc) {
     case ACC_SUM_I: atomicAdd((unsigned long long*)&acc[s], (unsigned long long)x); break;
     case ACC_SUM_F: atomicAdd((double*)&acc[s], bits_f64(x)); break;
-    case ACC_SUM_X: lds_fx_add(acc, (qu64*)(smem + P.off_idx[j]), (1 << P.lds_log2) + 2, s, x); break;
+    case ACC_SUM_X:
+      if (!lds_fx_add(acc, (qu64*)(smem + P.off_idx[j]), (1 << P.lds_log2) + 2, s, x)) {
+        const int S = 1 << P.lds_log2;  // an input for E: into the global slot (fx_rare_global)
+        fx_rare_global(P, 1u << j, s < S ? lds_keys(smem)[s] : (s == S ? 0 : EMPTY_KEY), s == S, x);
+      }
+      break;
     case ACC_MIN_I: atomicMin((long long*)&acc[s], (long long)x); break;
     case ACC_MAX_I: atomicMax((long long*)&acc[s], (long long)x); break;
     case ACC_MIN_F:
@@ -745,6 +750,7 @@ struct AggMeta {
   qi32 fn[QE_MAX_AGGS];
   qi32 acc[QE_MAX_AGGS];
   qi32 nn_implicit;  // bit j: aggregate j's non-null count is COUNT(*) (cstar); its nn array is unused
+  qi32 any_x;        // some aggregate is an exact fp64 SUM (ACC_SUM_X)
 };
 
 __device__ __forceinline__ qu64 slot_nn(const DTable& t, const AggMeta& m, int j, qu64 s) {
@@ -933,6 +939,9 @@ __global__ void k_table_init(DTable t, AggMeta m, qu64* zero_ctl) {
     t.keys[s] = EMPTY_KEY;
     t.cstar[s] = 0;
     for (int j = 0; j < m.naggs; ++j) {
+      // a reset zeroes the E words a slot used (a new table's come zeroed: table_alloc)
+      if (zero_ctl && m.acc[j] == ACC_SUM_X && (t.idx[j][3 * SS + s] & FX_EXT))
+        for (int w = 0; w < FXE_WORDS; ++w) t.ext[j][s * FXE_WORDS + w] = 0;
       t.acc[j][s] = acc_identity(m.acc[j]);
       t.nn[j][s] = 0;
       if (acc_has_idx(m.acc[j]))
@@ -988,6 +997,8 @@ __global__ void k_rehash(DTable src, DTable dst, AggMeta m) {
       if (acc_has_idx(a.acc))
         for (int k = 0; k < 4; ++k) i[k] = src.idx[j][k * SS + s];
       gcombine(dst, a.acc, j, d, src.acc[j][s], slot_nn(src, m, j, s), i[0], i[1], i[2], i[3]);
+      if (a.acc == ACC_SUM_X && (i[3] & FX_EXT))  // (the status word carried FX_EXT over)
+        fxe_add_words<true>(dst.ext[j] + d * FXE_WORDS, 0, src.ext[j] + s * FXE_WORDS, FXE_WORDS);
     }
   }
   wg_newg_end(&newg, dst.ctl);
@@ -1076,8 +1087,8 @@ __device__ __forceinline__ qu32 partition_of(qi64 key, bool knull, qi32 nparts) 
 
 // Position of this lane's record in partition p's run: one cursor add per (wave, partition)
 // present instead of one per record (every record of a partition hit the same word). The whole
-// wave calls it; `has` = this lane has a record.
-__device__ __forceinline__ qu64 wave_cursor(unsigned long long* cursor, bool has, qu32 p) {
+// wave calls it; `has` = this lane has `mult` records.
+__device__ __forceinline__ qu64 wave_cursor(unsigned long long* cursor, bool has, qu32 p, qu32 mult = 1) {
   const int lane = threadIdx.x & 63;
   const qu64 lt = lane ? (~0ull >> (64 - lane)) : 0ull;
   qu64 todo = __ballot(has);
@@ -1087,15 +1098,24 @@ __device__ __forceinline__ qu64 wave_cursor(unsigned long long* cursor, bool has
     const qu32 lp = (qu32)__shfl((int)p, leader);
     const qu64 same = __ballot(has && p == lp);
     qu64 base = 0;
-    if (lane == leader) base = atomicAdd(&cursor[lp], (unsigned long long)__popcll(same));
+    if (lane == leader) base = atomicAdd(&cursor[lp], (unsigned long long)__popcll(same) * mult);
     base = (qu64)__shfl((long long)base, leader);
-    if (has && p == lp) pos = base + __popcll(same & lt);
+    if (has && p == lp) pos = base + (qu64)__popcll(same & lt) * mult;
     todo &= ~same;
   }
   return pos;
 }
 
-__global__ void k_export_count(DTable t, qi32 nparts, unsigned long long* counts) {
+// A group whose exact fp64 SUMs have E words (FX_EXT) exports FXE_CHUNKS more records, one per
+// chunk of E (qe_dev.hpp fxe_partial): every record of a group goes to its key's partition.
+__device__ __forceinline__ bool slot_has_ext(const DTable& t, const AggMeta& m, qu64 s) {
+  bool e = false;
+  for (int j = 0; j < m.naggs; ++j)
+    if (m.acc[j] == ACC_SUM_X) e = e || (t.idx[j][3 * (t.cap + 2) + s] & FX_EXT) != 0;
+  return e;
+}
+
+__global__ void k_export_count(DTable t, AggMeta m, qi32 nparts, unsigned long long* counts) {
   const qu64 SS = t.cap + 2;
   const qu64 stride = (qu64)gridDim.x * blockDim.x;
   for (qu64 s0 = blockIdx.x * (qu64)blockDim.x; s0 < SS; s0 += stride) {
@@ -1103,7 +1123,9 @@ __global__ void k_export_count(DTable t, qi32 nparts, unsigned long long* counts
     const bool has = s < SS && gslot_occupied(t, s);
     const bool knull = s == t.cap;
     const qi64 key = !has ? 0 : knull ? 0 : (s == t.cap + 1 ? EMPTY_KEY : t.keys[s]);
-    (void)wave_cursor(counts, has, has ? partition_of(key, knull, nparts) : 0);
+    const qu32 p = has ? partition_of(key, knull, nparts) : 0;
+    (void)wave_cursor(counts, has, p);
+    if (m.any_x) (void)wave_cursor(counts, has && slot_has_ext(t, m, s), p, FXE_CHUNKS);
   }
 }
 
@@ -1118,6 +1140,30 @@ __device__ void write_record(qu8* rec, const DTable& t, const AggMeta& m, qu64 s
     if (acc_has_idx(m.acc[j]))
       for (int k = 0; k < 4; ++k) f[2 + k] = t.idx[j][k * SS + s];
     off += agg_rec_bytes(m.acc[j]);
+  }
+}
+
+// Chunk c of the E words of group slot s (COUNT(*) 0; identity partials but those SUMs).
+__device__ void write_chunk_record(qu8* rec, const DTable& t, const AggMeta& m, qu64 s, qi64 key, bool knull,
+                                   int c) {
+  const qu64 SS = t.cap + 2;
+  write_record_head(rec, key, knull, 0);
+  int off = 24;
+  for (int j = 0; j < m.naggs; ++j) {
+    qu64* f = (qu64*)(rec + off);
+    const int acc = m.acc[j];
+    f[0] = (qu64)acc_identity(acc);
+    f[1] = 0;
+    if (acc_has_idx(acc))
+      for (int k = 0; k < 4; ++k) f[2 + k] = idx_identity(acc);
+    if (acc == ACC_SUM_X && (t.idx[j][3 * SS + s] & FX_EXT)) {
+      const qu64* e = t.ext[j] + s * FXE_WORDS + 4 * c;
+      const int n = c == FXE_CHUNKS - 1 ? FXE_WORDS - 4 * c : 4;
+      f[0] = e[0];
+      for (int k = 1; k < n; ++k) f[1 + k] = e[k];
+      f[5] = FX_CHUNK | ((qu64)c << 8);
+    }
+    off += agg_rec_bytes(acc);
   }
 }
 
@@ -1146,6 +1192,12 @@ __global__ void k_export(DTable t, AggMeta m, qi32 nparts, qi32 rec_bytes, unsig
     const qu32 p = has ? partition_of(key, knull, nparts) : 0;
     const qu64 pos = wave_cursor(cursor, has, p);
     if (has) write_record(dst + pos * (qu64)rec_bytes, t, m, s, key, knull);
+    if (m.any_x) {
+      const bool ext = has && slot_has_ext(t, m, s);
+      const qu64 pe = wave_cursor(cursor, ext, p, FXE_CHUNKS);
+      if (ext)
+        for (int c = 0; c < FXE_CHUNKS; ++c) write_chunk_record(dst + (pe + c) * (qu64)rec_bytes, t, m, s, key, knull, c);
+    }
   }
 }
 
@@ -1163,8 +1215,15 @@ __global__ void k_export_slots(DTable t, AggMeta m, qi32 nparts, qi32 rec_bytes,
     const qi64 key = !has ? 0 : knull ? 0 : (s == t.cap + 1 ? EMPTY_KEY : t.keys[s]);
     const qu32 p = has ? partition_of(key, knull, nparts) : 0;
     const qu64 pos = wave_cursor(cursor, has, p);
-    if (has && pos < (qu64)slot_records)
-      write_record(dst + p * slot_bytes + QE_SLOT_HEADER + pos * (qu64)rec_bytes, t, m, s, key, knull);
+    qu8* base = dst + p * slot_bytes + QE_SLOT_HEADER;
+    if (has && pos < (qu64)slot_records) write_record(base + pos * (qu64)rec_bytes, t, m, s, key, knull);
+    if (m.any_x) {
+      const bool ext = has && slot_has_ext(t, m, s);
+      const qu64 pe = wave_cursor(cursor, ext, p, FXE_CHUNKS);
+      if (ext)
+        for (int c = 0; c < FXE_CHUNKS; ++c)
+          if (pe + c < (qu64)slot_records) write_chunk_record(base + (pe + c) * (qu64)rec_bytes, t, m, s, key, knull, c);
+    }
   }
 }
 
@@ -1235,17 +1294,12 @@ __device__ __forceinline__ void put_bit(qu8* gbm, qu32* lbits, int col, qi64 o, 
   else set_bit(gbm, o, true);
 }
 
-// An ACC_SUM_X slot's value (word 0 = acc, words 1..3 and the status word in idx; qe_dev.hpp
-// fx_result). A slot that cannot give its sum within FX_REL_TOL of the exact one (an input of
-// 2^182 or more, or rounded inputs whose error bound is too large for the result) is counted in
-// ctl[6], which finalize zeroes beforehand and reports.
-__device__ __forceinline__ double fx_sum(const DTable& t, int j, qu64 s, qi64 acc, qu64 nn) {
+// An ACC_SUM_X slot's value (word 0 = acc, words 1..3 and the status word in idx, E in ext;
+// qe_dev.hpp fx_result): the correctly rounded exact sum.
+__device__ __forceinline__ double fx_sum(const DTable& t, int j, qu64 s, qi64 acc) {
   const qu64 SS = t.cap + 2;
   const qu64* ix = t.idx[j];
-  bool err;
-  const double v = fx_result((qu64)acc, ix[s], ix[SS + s], ix[2 * SS + s], ix[3 * SS + s], nn, &err);
-  if (err) atomicAdd(&t.ctl[6], 1ull);
-  return v;
+  return fx_result((qu64)acc, ix[s], ix[SS + s], ix[2 * SS + s], ix[3 * SS + s], t.ext[j] + s * FXE_WORDS);
 }
 
 __device__ __forceinline__ void finalize_slot(const DTable& t, const AggMeta& m, const KeyMeta& km,
@@ -1281,13 +1335,13 @@ __device__ __forceinline__ void finalize_slot(const DTable& t, const AggMeta& m,
       case QE_AGG_COUNT_STAR: val = (qi64)cst; valid = true; break;
       case QE_AGG_AVG:
         if (m.acc[j] == ACC_SUM_X)
-          val = f64_bits(fx_sum(t, j, s, acc, nn) / (double)nn);
+          val = f64_bits(fx_sum(t, j, s, acc) / (double)nn);
         else
           val = f64_bits(bits_f64(acc) / (double)nn);
         break;
       default:
         if (m.acc[j] == ACC_SUM_X) {
-          val = f64_bits(fx_sum(t, j, s, acc, nn));
+          val = f64_bits(fx_sum(t, j, s, acc));
         } else if (acc_is_f64mm(m.acc[j])) {
           const qu64 i0 = t.idx[j][s], i1 = t.idx[j][SS + s];
           const qu64 i2 = t.idx[j][2 * SS + s], i3 = t.idx[j][3 * SS + s];
@@ -1504,6 +1558,7 @@ static AggMeta agg_meta(const qe_hashagg* h) {
   for (int j = 0; j < h->naggs; ++j) {
     m.fn[j] = h->aggs[j].fn;
     m.acc[j] = h->acc[j];
+    m.any_x = m.any_x || h->acc[j] == ACC_SUM_X;
   }
   m.nn_implicit = h->nn_implicit;
   return m;
@@ -1535,10 +1590,13 @@ static int nn_materialize(qe_hashagg* h, int32_t mask) {
   return QE_OK;
 }
 
+// Per slot: key and COUNT(*), and per aggregate its accumulator, non-null count, four idx words
+// (fp64 MIN/MAX, exact SUM) and for an exact SUM the FXE_WORDS words of E.
 static size_t table_bytes(const qe_hashagg* h, uint64_t cap) {
   const uint64_t SS = cap + 2;
   size_t b = 16 * SS;
-  for (int j = 0; j < h->naggs; ++j) b += (16 + (acc_has_idx(h->acc[j]) ? 32 : 0)) * SS;
+  for (int j = 0; j < h->naggs; ++j)
+    b += (16 + (acc_has_idx(h->acc[j]) ? 32 : 0) + (h->acc[j] == ACC_SUM_X ? 8 * FXE_WORDS : 0)) * SS;
   return b;
 }
 
@@ -1562,6 +1620,14 @@ static int table_alloc(qe_hashagg* h, uint64_t cap, void** mem, DTable* t) {
       p += 32 * SS;
     }
   }
+  // E words last, one run: zeroed here (k_table_init resets only the slots that used theirs)
+  char* e0 = p;
+  for (int j = 0; j < h->naggs; ++j)
+    if (h->acc[j] == ACC_SUM_X) {
+      t->ext[j] = (qu64*)p;
+      p += 8 * FXE_WORDS * SS;
+    }
+  if (p > e0) QE_HIP(hipMemsetAsync(e0, 0, (size_t)(p - e0), h->ctx->stream));
   t->cap = cap;
   t->ctl = h->ctl;
   const int grid = (int)std::min<uint64_t>(div_up(SS, 256), 4096);
@@ -1571,7 +1637,6 @@ static int table_alloc(qe_hashagg* h, uint64_t cap, void** mem, DTable* t) {
 
 // ctl words: [0] groups, [1] deferred rows, [2] overflow records, [3] lost groups,
 // [4] largest slot count reported by the senders of an import_slots, [5] their records in total,
-// [6] finalize: exact fp64 SUM groups that cannot be given within 1e-9 (zeroed before each finalize)
 // ctl[3] is sticky: every path that can drop a group (k_rehash, k_import, k_import_slots, the
 // fused kernel's overflow area) adds to it and nothing but a reset clears it, so a loss in a
 // launch with no read-back of its own (qe_hashagg_import_slots queues k_import_slots and returns)
@@ -3094,19 +3159,6 @@ int qe_hashagg_num_groups(qe_hashagg* h, int64_t* out) {
   return QE_OK;
 }
 
-// States with exact fp64 sums: finalize waits for its kernel and fails when a group's sum could not
-// be given within FX_REL_TOL of the exact sum (fx_sum counted such groups in ctl[6], zeroed before
-// the finalize kernel, so a failed finalize does not leak into later calls).
-static int check_fx_final(qe_hashagg* h) {
-  uint64_t c[8];
-  QE_TRY(read_ctl(h, c));
-  QE_CHECK(c[6] == 0, QE_ERR_UNSUPPORTED,
-           "fp64 SUM: %llu group results not exact to 1e-9 (an input of magnitude >= 2^182, or inputs with bits "
-           "below 2^-128 whose rounding is too large for the result)",
-           (unsigned long long)c[6]);
-  return QE_OK;
-}
-
 int qe_hashagg_finalize(qe_hashagg* h, qe_column* out_keys, qe_column* out_aggs, int64_t* out_groups) {
   QE_CHECK(h, QE_ERR_INVALID_ARG, "null state");
   QE_TRY(ctx_enter(h->ctx));
@@ -3153,14 +3205,11 @@ int qe::hashagg_finalize_raw(qe_hashagg* h, qe_column* out_keys, qe_column* out_
   for (int k = 0; k < h->nkeys; ++k) out_keys[k].length = groups;
   for (int j = 0; j < h->naggs && !keys_only; ++j) out_aggs[j].length = groups;
   if (groups == 0) return QE_OK;
-  bool det = false;
-  for (int j = 0; j < h->naggs && !keys_only; ++j) det = det || h->acc[j] == ACC_SUM_X;
-  if (det) QE_HIP(hipMemsetAsync(h->ctl + 6, 0, 8, ctx->stream));
   if (small) {
     hipLaunchKernelGGL(k_finalize_small, dim3(1), dim3(FS_THREADS), 0, ctx->stream, h->t, agg_meta(h), h->km, oc,
                        (qi64)groups);
     QE_TRY(launch_check("k_finalize_small"));
-    return det ? check_fx_final(h) : QE_OK;  // stream-ordered: the outputs are ready when the ctx stream's work is
+    return QE_OK;  // stream-ordered: the outputs are ready when the ctx stream's work is
   }
   // one 256-slot tile per workgroup: a single pass each, so the chip finalises in one wave of
   // workgroups instead of a serial walk of long tiles
@@ -3177,7 +3226,7 @@ int qe::hashagg_finalize_raw(qe_hashagg* h, qe_column* out_keys, qe_column* out_
   hipLaunchKernelGGL(k_finalize, dim3((unsigned)ntiles), dim3(256), 0, ctx->stream, h->t, agg_meta(h), h->km, (const qi64*)offs,
                      tile_slots, oc);
   QE_TRY(launch_check("k_finalize"));
-  return det ? check_fx_final(h) : QE_OK;
+  return QE_OK;
 }
 
 namespace {
@@ -3203,18 +3252,28 @@ int qe_hashagg_export_counts(qe_hashagg* h, int32_t nparts, int64_t* counts) {
   QE_CHECK(h && counts && nparts >= 1, QE_ERR_INVALID_ARG, "bad arguments");
   QE_TRY(refuse_dict_records(h));
   QE_TRY(ctx_enter(h->ctx));
+  return hashagg_export_counts_raw(h, nparts, counts);
+}
+
+}  // extern "C"
+
+// Records per partition of an export: one per group, FXE_CHUNKS more per group with E words.
+int qe::hashagg_export_counts_raw(qe_hashagg* h, int32_t nparts, int64_t* counts) {
   QE_TRY(settle_pending(h));
   qe_ctx* ctx = h->ctx;
   void* s;
   QE_TRY(ctx_scratch(ctx, (size_t)nparts * 8, &s));
   QE_HIP(hipMemsetAsync(s, 0, (size_t)nparts * 8, ctx->stream));
   const int grid = (int)std::min<uint64_t>(div_up(h->t.cap + 2, 256), 8192);
-  hipLaunchKernelGGL(k_export_count, dim3(grid), dim3(256), 0, ctx->stream, h->t, nparts, (unsigned long long*)s);
+  hipLaunchKernelGGL(k_export_count, dim3(grid), dim3(256), 0, ctx->stream, h->t, agg_meta(h), nparts,
+                     (unsigned long long*)s);
   QE_TRY(launch_check("k_export_count"));
   QE_HIP(hipMemcpyAsync(counts, s, (size_t)nparts * 8, hipMemcpyDeviceToHost, ctx->stream));
   QE_TRY(ctx_sync(ctx));
   return QE_OK;
 }
+
+extern "C" {
 
 int qe_hashagg_export(qe_hashagg* h, int32_t nparts, void* dst) {
   QE_CHECK(h && nparts >= 1, QE_ERR_INVALID_ARG, "bad arguments");
@@ -3236,7 +3295,8 @@ int qe::hashagg_export_raw(qe_hashagg* h, int32_t nparts, void* dst) {
   QE_TRY(ctx_scratch(ctx, (size_t)nparts * 8, &s));
   QE_HIP(hipMemsetAsync(s, 0, (size_t)nparts * 8, ctx->stream));
   const int grid = (int)std::min<uint64_t>(div_up(h->t.cap + 2, 256), 8192);
-  hipLaunchKernelGGL(k_export_count, dim3(grid), dim3(256), 0, ctx->stream, h->t, nparts, (unsigned long long*)s);
+  hipLaunchKernelGGL(k_export_count, dim3(grid), dim3(256), 0, ctx->stream, h->t, agg_meta(h), nparts,
+                     (unsigned long long*)s);
   QE_TRY(launch_check("k_export_count"));
   hipLaunchKernelGGL(k_counts_to_cursors, dim3(1), dim3(64), 0, ctx->stream, (unsigned long long*)s, nparts);
   QE_TRY(launch_check("k_counts_to_cursors"));

@@ -80,10 +80,9 @@ int parallel_h2d_copy(qe_ctx* ctx, void* dst, const void* src, size_t n);
 int parallel_h2d_file(qe_ctx* ctx, void* dst, int fd, int64_t off, size_t n);
 // Per-plan kernel specialisation (qe_jit.hip).
 bool gen_fused_source(const qe::Plan& P, int log2, std::string* src, size_t* lds_bytes, bool spill = false);
-// Exact fp64 SUM in the specialised kernels' LDS tables: the 192-bit carry window (default) or the
-// six-word limb window (QE_FX_LIMBS=1), both through the per-wave queue. LDS words per slot beyond acc.
-bool fx_limbs();
-inline int fx_window_idx_words() { return fx_limbs() ? qe::FXL_WORDS - 1 : 2; }
+// Exact fp64 SUM in the specialised kernels' LDS tables: the 192-bit carry window through the per-wave
+// queue. LDS words per slot beyond acc.
+inline int fx_window_idx_words() { return 2; }
 // compact fused LDS table (Plan.lds_compact): plan shapes it supports, bytes per slot, 32-bit MIN/MAX
 bool compact_ok(const qe::Plan& P);
 size_t compact_slot_bytes(const qe::Plan& P);
@@ -140,6 +139,7 @@ struct HashaggInfo {
 HashaggInfo hashagg_info(const qe_hashagg* h);
 // The raw record / update / finalize paths (no dictionary handling), for qe_keyed.hip.
 int hashagg_export_raw(qe_hashagg* h, int32_t nparts, void* dst);
+int hashagg_export_counts_raw(qe_hashagg* h, int32_t nparts, int64_t* counts);
 int hashagg_import_raw(qe_hashagg* h, const void* recs, int64_t nrec);
 int hashagg_update_raw(qe_hashagg* h, const qe_column* dev_keys, const qe_column* agg_inputs, const qe_column* mask);
 int hashagg_update_fused_raw(qe_hashagg* h, const qe_column* cols, int32_t ncols, const qe_fused_spec* spec);

@@ -338,21 +338,6 @@ void emit_lds_table(const Plan& P, std::ostringstream& o, int log2, size_t* lds_
 // the same wave wrote before (the fences keep the compiler from reordering them).
 constexpr int FXQ_CAP = 128;
 
-}  // namespace
-
-// QE_FX_LIMBS=1: the limb window instead of the 192-bit carry window (both through the per-wave
-// queue). C5, one box: 8.24 ms either way (fp64 atomics 7.20), limbs without the queue 9.47 ms; the
-// carry window takes half the LDS (24 vs 48 B per sum and slot), so it stays the default.
-bool fx_limbs() {
-  static const bool v = [] {
-    const char* e = getenv("QE_FX_LIMBS");
-    return e && e[0] == '1';
-  }();
-  return v;
-}
-
-namespace {
-
 std::vector<int> fx_queue_aggs(const Plan& P) {
   std::vector<int> q;
   for (int j = 0; j < P.naggs; ++j)
@@ -394,10 +379,7 @@ void emit_fx_queue_run(const Plan& P, std::ostringstream& o, const std::string& 
   for (int k = 0; k < nq; ++k)
     o << "        qx[" << k << "] = ((qe >> " << 24 + k << ") & 1u) ? q_x" << k << "[qp] : 0ll;\n"
       << "        if (fx_rare(qx[" << k << "])) { rare |= 1u << " << k << "; qx[" << k << "] = 0; }\n";
-  if (fx_limbs()) {  // limb window: three adds per input, no carries
-    for (int k = 0; k < nq; ++k)
-      o << "        if (qx[" << k << "]) lds_fxl_add(s_acc" << q[k] << ", s_idx" << q[k] << ", SS, s, qx[" << k << "]);\n";
-  } else {
+  {
   o << "        qu64* wp0[" << nq << "];\n        qu64* wp1[" << nq << "];\n        qu64 lo[" << nq << "], hi[" << nq
     << "];\n        bool ng[" << nq << "], k0[" << nq << "];\n";
   for (int k = 0; k < nq; ++k) {
@@ -523,7 +505,6 @@ void emit_agg_rows(const Plan& P, std::ostringstream& o, const std::vector<std::
       case ACC_SUM_F: o << "        atomicAdd((double*)&s_acc" << js << "[s], bits_f64(x));\n"; break;
       case ACC_SUM_X:
         if (fx_queue) o << "        (void)x; (void)s;\n";
-        else if (fx_limbs()) o << "        lds_fxl_add(s_acc" << js << ", s_idx" << js << ", SS, s, x);\n";
         else o << "        lds_fxw_add(s_acc" << js << ", s_idx" << js << ", SS, s, x);\n";
         break;
       case ACC_MIN_I: o << "        lds_min_rf(&s_acc" << js << "[s], x);\n"; break;
@@ -589,11 +570,7 @@ void emit_flush(const Plan& P, std::ostringstream& o, bool mark_full = false, bo
     const std::string js = std::to_string(j);
     o << "    {\n      qi64 acc = " << (a.acc != ACC_NONE ? "s_acc" + js + "[s]" : std::string("0")) << ";\n"
       << "      const qu64 nn = " << (a.track_nn ? "s_nn" + js + "[s]" : std::string("c")) << ";\n";
-    if (a.acc == ACC_SUM_X && fx_limbs())  // the limb window as a global partial
-      o << "      qu64 i0, i1, i2, i3;\n      {\n        qu64 v[4];\n        fxl_partial((qu64)acc, s_idx" << js
-        << "[s], s_idx" << js << "[SS + s], s_idx" << js << "[2 * SS + s], s_idx" << js << "[3 * SS + s], s_idx" << js
-        << "[4 * SS + s], v, &i3);\n        acc = (qi64)v[0]; i0 = v[1]; i1 = v[2]; i2 = v[3];\n      }\n";
-    else if (a.acc == ACC_SUM_X)  // the LDS window as a global partial (status 0: rare rows went global)
+    if (a.acc == ACC_SUM_X)  // the LDS window as a global partial (status 0: rare rows went global)
       o << "      qu64 i0, i1, i2;\n      const qu64 i3 = 0;\n      {\n        qu64 v[4];\n        fxw_words((qu64)acc, s_idx" << js
         << "[s], s_idx" << js << "[SS + s], v);\n        acc = (qi64)v[0]; i0 = v[1]; i1 = v[2]; i2 = v[3];\n      }\n";
     else if (acc_has_idx(a.acc))
@@ -1543,13 +1520,6 @@ static bool gen_pagg_fast_source(const Plan& P, const PartLayout& L, int log2, i
     const bool bare = L.colmode ? (a.ntok == 1 && a.tok[0].op == T_COL) : L.val_word[j] >= 0;
     acc32[j] = (a.acc == ACC_MIN_I || a.acc == ACC_MAX_I) && bare;
   }
-  // QE_PAGG_EXP: timing experiments (never for results): 1 no LDS work, 2 the same reading each
-  // slice's chunks as one contiguous range, 3 no flush, 4 as 1 with each
-  // load instruction reading one contiguous KiB
-  static const int exp = [] {
-    const char* e = getenv("QE_PAGG_EXP");
-    return e && *e ? atoi(e) : 0;
-  }();
   // Table size: as many 4-slot buckets as the LDS holds beside the chunk list (and the per-wave
   // regrouping area, when that is used), not the power of two of the general pass's 36-byte slots:
   // with C4's 24-byte slots ~6K slots instead of 4096, so the half-full tables of 128+ buckets
@@ -1565,7 +1535,7 @@ static bool gen_pagg_fast_source(const Plan& P, const PartLayout& L, int log2, i
   const size_t tr_bytes = (size_t)(pagg_block() / 64) * W * 1024;
   const int s_tr = pagg_fast_slots_for(bps, (size_t)1024 * 8 + tr_bytes);
   const int s_plain = pagg_fast_slots_for(bps, (size_t)PAGG_CHCAP * 8);
-  const bool tr = !blk && tr_env && exp == 0 && s_tr >= 256 && (bucket_groups <= 0 || 4 * bucket_groups <= s_tr);
+  const bool tr = !blk && tr_env && s_tr >= 256 && (bucket_groups <= 0 || 4 * bucket_groups <= s_tr);
   const int S = tr ? s_tr : s_plain, SS = S + 2;
   if (S < 256) return false;
   // hit window: 2 buckets (default) or 3 (QE_PAGG_WINDOW=3, for fuller tables)
@@ -1632,7 +1602,6 @@ static bool gen_pagg_fast_source(const Plan& P, const PartLayout& L, int log2, i
   // so each step's loads have the next D - 1 steps' work to land (one buffer copied forward made
   // the loop's back edge wait for the loads it had just issued)
   const int D = pagg_fast_depth();
-  o << "  qu64 xacc = 0;\n";
   for (int k = 0; k < D; ++k) {
     o << "  qu32 b" << k << "_act;\n  qi64 b" << k << "_pb;\n";
     for (int v = 0; v < W; ++v) o << "  qu32x4 b" << k << "_v" << v << ";\n";
@@ -1654,19 +1623,15 @@ static bool gen_pagg_fast_source(const Plan& P, const PartLayout& L, int log2, i
     o << "    {\n      const qi64 nb = " << nb << ";\n      const bool in = nb < rhi;\n"
       << "      const qu64 m = s_ch[in ? (int)(nb >> 11) : 0];\n"
       << "      const qi32 ko = (qi32)(nb & (PART_CH - 1));\n"
-      << (exp == 2 ? "      const qi64 npb = ((qi64)blockIdx.x * nch + c0 + (nb >> 11)) % (P.n / PART_CH) * PART_CH + ko;  // (experiment: slices contiguous)\n"
-                   : "      const qi64 npb = (qi64)(qi32)(qu32)m * PART_CH + ko;\n")
+      << "      const qi64 npb = (qi64)(qi32)(qu32)m * PART_CH + ko;\n"
       << "      const qi32 cfill = in ? (qi32)(m >> 32) - ko : 0;\n"
       // (lanes whose records lie past the chunk's fill read the step's first block instead: the
       // unfilled tail of a chunk is never fetched)
       << (blk ? "      const qu32x4* p = (const qu32x4*)((const qu32*)P.part_rec + ((npb >> 6) + (ro < cfill ? (lane >> 4) : 0)) * " +
                     std::to_string(64 * W) + "ull + 4 * (lane & 15));\n"
               : "      const qu32x4* p = (const qu32x4*)(P.part_rec + (qu64)(npb + 4 * lane) * " + std::to_string(L.bytes()) + "ull);\n");
-    if (blk && exp != 4) {
+    if (blk) {
       for (int v = 0; v < W; ++v) o << "      " << B << "v" << v << " = " << ld("qu32x4", "p + 16 * " + std::to_string(v)) << ";\n";
-    } else if (exp == 4) {  // (experiment: each load instruction one contiguous KiB of the step's records)
-      o << "      const qu32x4* pc = (const qu32x4*)(P.part_rec + (qu64)npb * " << L.bytes() << "ull) + lane;\n";
-      for (int v = 0; v < W; ++v) o << "      " << B << "v" << v << " = " << ld("qu32x4", "pc + 64 * " + std::to_string(v)) << ";\n";
     } else if (tr) {  // contiguous KiB per load; a piece past the chunk's fill re-reads the step's first
       o << "      const qu32x4* pc = (const qu32x4*)(P.part_rec + (qu64)npb * " << L.bytes() << "ull);\n";
       for (int v = 0; v < W; ++v)
@@ -1740,13 +1705,6 @@ static bool gen_pagg_fast_source(const Plan& P, const PartLayout& L, int log2, i
         << (1 + c) << ") & 1u) << r;\n";
   }
   // slots: the first probe of all 4 rows together; collisions (rare) probe on
-  if (exp == 1 || exp == 2 || exp == 4) {  // timing experiments: the records' walk and loads only (wrong results)
-    o << "#pragma unroll\n    for (int r = 0; r < 4; ++r) xacc ^= (qu64)key[r]";
-    for (int q = 1; q < W; ++q) o << " ^ (qu64)w" << q << "[r]";
-    o << " ^ act;\n  }\n";
-    load_step(k, NB("t + " + std::to_string(k + D)));
-    continue;
-  }
   o << "    int slot[4];\n    qu32 h[4];\n    qu32x4 q[4];\n"
     << "    qu32 h2[4];\n    qu32x4 q2[4];\n" << (win3 ? "    qu32 h3[4];\n    qu32x4 q3[4];\n" : "")
     << "#pragma unroll\n    for (int r = 0; r < 4; ++r) {\n"
@@ -1811,9 +1769,7 @@ static bool gen_pagg_fast_source(const Plan& P, const PartLayout& L, int log2, i
   }  // buffers
   o << "  }\n  }\n";
   // flush (exclusive slices: plain read-modify-writes), as emit_flush with 32-bit keys / accumulators
-  o << "  if (xacc == 0x9E3779B97F4A7C15ull) s_fail = 3;  // (keeps the experiment's loads live)\n"
-    << "  __syncthreads();\n"
-    << (exp == 3 ? "  if (s_cst[0] != 0x7FFFFFFFu) return;  // (experiment: no flush)\n" : "")
+  o << "  __syncthreads();\n"
     << "  for (int s = threadIdx.x; s < SS; s += blockDim.x) {\n"
     << "    const qu32 c = s_cst[s];\n    if (c == 0) continue;\n"
     << "    const bool knl = s == S;\n    const qi64 key = knl ? 0 : (s == S + 1 ? (qi64)EMPTY_KEY32 : (qi64)s_keys[s]);\n"

@@ -785,8 +785,8 @@ int qe_hashagg_export_keyed_sizes(qe_hashagg* h, int32_t nparts, int64_t* block_
   Keyed* K = I.keyed;
   KeyedPrep& P = K->prep;
   P.valid = false;
-  int64_t n = 0;
-  QE_TRY(qe_hashagg_num_groups(h, &n));
+  int64_t n = 0;  // records (a group with exact-SUM E words exports more than one)
+  QE_TRY(hashagg_export_counts_raw(h, 1, &n));
   const int32_t rb = I.rec_bytes;
   const int nk = K->norig;
   // the records, then their declared key columns

@@ -157,12 +157,28 @@ def exchange_partials_native(partial, owner, comm: NativeComm, slot_records: int
     return n.value
 
 
+def _all_gather_bytes(part, world: int, group):
+    if world == 1:
+        return part
+    if dist.get_backend(group) == "gloo":  # CPU collectives: stage through host memory
+        got = [torch.empty_like(part, device="cpu") for _ in range(world)]
+        dist.all_gather(got, part.cpu(), group=group)
+        return torch.cat(got).to(part.device)
+    parts = torch.empty(world * part.numel(), dtype=torch.uint8, device=part.device)
+    dist.all_gather_into_tensor(parts, part, group=group)
+    return parts
+
+
 def global_aggregate(col, mask=None, row_base: int = 0, group: Optional[dist.ProcessGroup] = None):
     """SUM/MIN/MAX/COUNT/AVG without GROUP BY over a column whose rows are split across ranks
     (SURVEY §8e "global aggregate: one exchange"): this rank's 128-byte partial
     (qe_agg_global_partial, row indices offset by `row_base` — this rank's first global row),
     ONE all-gather, and the same fixed-order merge on every rank (qe_agg_global_merge), so every
-    rank returns identical bits. Without an initialised process group: this column alone."""
+    rank returns identical bits. When the merged fp64 sum cannot be proven correctly rounded (the
+    ranks' sums cancel) the merge says so on every rank alike (QE_NEED_EXACT) and a second round
+    gathers each rank's exact sum words (qe_agg_global_exact_partial, 320 bytes) for
+    qe_agg_global_merge_exact: the sum is then math.fsum's over all ranks' rows.
+    Without an initialised process group: this column alone."""
     from . import native as N
 
     ctx = col.ctx
@@ -170,17 +186,15 @@ def global_aggregate(col, mask=None, row_base: int = 0, group: Optional[dist.Pro
     part = torch.empty(N.GLOBAL_PARTIAL_BYTES, dtype=torch.uint8, device=ctx.torch_device)
     cc = col.as_c()
     mc = mask.as_c() if mask is not None else None
-    N.check(N.lib().qe_agg_global_partial(ctx.handle, N.C.byref(cc), N.C.byref(mc) if mc is not None else None,
-                                          int(row_base), N.C.c_void_p(part.data_ptr())))
-    parts = part
-    if world > 1:
-        if dist.get_backend(group) == "gloo":  # CPU collectives: stage through host memory
-            got = [torch.empty_like(part, device="cpu") for _ in range(world)]
-            dist.all_gather(got, part.cpu(), group=group)
-            parts = torch.cat(got).to(part.device)
-        else:
-            parts = torch.empty(world * N.GLOBAL_PARTIAL_BYTES, dtype=torch.uint8, device=part.device)
-            dist.all_gather_into_tensor(parts, part, group=group)
+    mp = N.C.byref(mc) if mc is not None else None
+    N.check(N.lib().qe_agg_global_partial(ctx.handle, N.C.byref(cc), mp, int(row_base), N.C.c_void_p(part.data_ptr())))
+    parts = _all_gather_bytes(part, world, group)
     out = N.QeGlobalAgg()
-    N.check(N.lib().qe_agg_global_merge(ctx.handle, col.type, N.C.c_void_p(parts.data_ptr()), world, N.C.byref(out)))
+    st = N.lib().qe_agg_global_merge(ctx.handle, col.type, N.C.c_void_p(parts.data_ptr()), world, N.C.byref(out))
+    if st == N.QE_NEED_EXACT:
+        words = torch.empty(N.GLOBAL_EXACT_BYTES, dtype=torch.uint8, device=ctx.torch_device)
+        N.check(N.lib().qe_agg_global_exact_partial(ctx.handle, N.C.byref(cc), mp, N.C.c_void_p(words.data_ptr())))
+        allw = _all_gather_bytes(words, world, group)
+        st = N.lib().qe_agg_global_merge_exact(ctx.handle, N.C.c_void_p(allw.data_ptr()), world, N.C.byref(out))
+    N.check(st)
     return out

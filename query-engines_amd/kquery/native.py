@@ -191,6 +191,8 @@ _OPP = C.POINTER(QeOperand)
 SLOT_HEADER = 64  # QE_SLOT_HEADER: bytes before a slot's records
 KEYED_HEADER = 128  # QE_KEYED_HEADER: bytes before a keyed block's sections
 GLOBAL_PARTIAL_BYTES = 128  # QE_GLOBAL_PARTIAL_BYTES
+GLOBAL_EXACT_BYTES = 320  # QE_GLOBAL_EXACT_BYTES
+QE_NEED_EXACT = 1  # qe_agg_global_merge: run the exact round (not an error)
 
 SIGNATURES = [
     ("qe_ctx_create", C.c_int, [C.c_int, _P, _PP]),
@@ -219,6 +221,8 @@ SIGNATURES = [
     ("qe_agg_global", C.c_int, [_P, _COLP, _COLP, C.POINTER(QeGlobalAgg)]),
     ("qe_agg_global_partial", C.c_int, [_P, _COLP, _COLP, C.c_int64, _P]),
     ("qe_agg_global_merge", C.c_int, [_P, C.c_int32, _P, C.c_int32, C.POINTER(QeGlobalAgg)]),
+    ("qe_agg_global_exact_partial", C.c_int, [_P, _COLP, _COLP, _P]),
+    ("qe_agg_global_merge_exact", C.c_int, [_P, _P, C.c_int32, C.POINTER(QeGlobalAgg)]),
     ("qe_hashagg_create", C.c_int,
      [_P, C.c_int32, C.POINTER(C.c_int32), C.c_int32, C.POINTER(QeAggDesc), C.c_int64, _PP]),
     ("qe_hashagg_create_ex", C.c_int,

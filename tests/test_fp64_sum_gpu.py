@@ -7,9 +7,11 @@ pass, in the default state and with QE_HASHAGG_DETERMINISTIC (the same accumulat
 Each group holds +2^60 in the first rows of the batch and -2^60 in the last rows (different
 workgroups), unit terms and other small values between them, -0.0, and — in some groups — inputs
 outside the per-workgroup LDS window ([2^-44, 2^62): 1e-30 and 3e19, which take the global
-accumulator), NaN or +Inf. fp64 atomics in arrival order lose the unit terms next to 2^60 (its ulp
-is 256); the exact accumulator must equal math.fsum of each group. The oracle is math.fsum over
-the same rows (Python's exact, correctly rounded sum)."""
+accumulator), inputs for the full-range words E (1e-40, subnormals, 2^190, a +-1e300 pair), NaN or
++Inf. fp64 atomics in arrival order lose the unit terms next to 2^60 (its ulp is 256); the exact
+accumulator must equal math.fsum of each group. The oracle is math.fsum over the same rows
+(Python's exact, correctly rounded sum). test_full_range_exchange carries E through every partial
+form: export / import records, fixed-capacity slots, keyed blocks and qe_hashagg_merge."""
 import math
 
 import numpy as np
@@ -30,9 +32,14 @@ def _data(groups, n, seed):
     k[n - groups:] = rng.permutation(groups)
     x[n - groups:] = -(2.0 ** 60)
     # inputs outside the LDS window in a tenth of the groups, NaN / +Inf in two groups
-    odd = rng.choice(np.arange(groups // 2, n - groups), size=max(8, groups // 10), replace=False)
-    x[odd[0::2]] = 1e-30
-    x[odd[1::2]] = 3e19
+    odd = rng.choice(np.arange(groups // 2, n - groups), size=max(16, groups // 5), replace=False)
+    x[odd[0::8]] = 1e-30
+    x[odd[1::8]] = 3e19
+    x[odd[2::8]] = 1e-40
+    x[odd[3::8]] = 5e-324 * 77
+    x[odd[4::8]] = 2.0 ** 190
+    x[odd[5::8]] = 1e300
+    x[odd[6::8]] = -1e300
     sp = rng.choice(np.arange(groups, n - groups), size=2, replace=False)
     x[sp[0]] = np.nan
     x[sp[1]] = np.inf
@@ -102,10 +109,76 @@ def test_fp64_sum_adversarial(gpu_ctx, groups, expected, path, deterministic):
         assert _same(av[i], s / c), (int(kv[i]), av[i], s / c)
 
 
-def test_fp64_sum_finalize_errors_do_not_stick(gpu_ctx):
-    """An input of 2^182 or more cannot be summed exactly: finalize reports it (never a silently
-    wrong sum). The failure does not leak into the state's later calls: more updates still run,
-    and after a reset the state is clean (the old ctl[6] count was never cleared)."""
+def _full_range_batch(rng, n, groups):
+    k = rng.integers(0, groups, n).astype(np.int64)
+    x = rng.normal(size=n)
+    sel = rng.random(n)
+    x[sel < 0.05] = 1e-40 * (1 + rng.random(int((sel < 0.05).sum())))
+    x[(sel >= 0.05) & (sel < 0.08)] = 5e-324
+    x[(sel >= 0.08) & (sel < 0.09)] = 1e300
+    x[(sel >= 0.09) & (sel < 0.10)] = -1e300
+    x[(sel >= 0.10) & (sel < 0.11)] = 2.0 ** 190
+    return k, x
+
+
+@pytest.mark.parametrize("form", ["records", "slots", "keyed", "merge", "utf8-merge"])
+def test_full_range_exchange(gpu_ctx, form):
+    """Two partial states with full-range inputs combined through one partial form, then finalized:
+    every group's sum is math.fsum's over both batches (E travels as CHUNK records)."""
+    from kquery import native as N
+    from kquery.aggregate import HashAggregateState
+    from kquery.columnar import DeviceColumn
+
+    rng = np.random.default_rng(11)
+    groups = 500
+    batches = [_full_range_batch(rng, 200_000, groups) for _ in range(2)]
+    utf8 = form == "utf8-merge"
+    ktype = N.TYPE_UTF8 if utf8 else N.TYPE_INT64
+
+    def keycol(k):
+        if utf8:
+            return DeviceColumn.from_strings([f"key-{int(v):05d}-long-enough-not-to-pack" for v in k], ctx=gpu_ctx)
+        return DeviceColumn.from_numpy(N.TYPE_INT64, k, None, ctx=gpu_ctx)
+
+    aggs = [(N.AGG_SUM, N.TYPE_FLOAT64), (N.AGG_COUNT_STAR, N.TYPE_INT64)]
+    parts = []
+    for k, x in batches:
+        st = HashAggregateState(gpu_ctx, [ktype], aggs, 1024)
+        st.update([keycol(k)], [DeviceColumn.from_numpy(N.TYPE_FLOAT64, x, None, ctx=gpu_ctx), None])
+        parts.append(st)
+    final = HashAggregateState(gpu_ctx, [ktype], aggs, 1024)
+    for p in parts:
+        if form == "records":
+            recs, counts = p.export(3)
+            assert sum(counts) > p.num_groups()  # chunk records of the groups with E
+            final.import_records(recs, sum(counts))
+        elif form == "slots":
+            cap = max(p.export_counts(2))
+            slots = p.export_slots(2, cap)
+            assert final.import_slots(slots, 2, cap) is not None
+        elif form == "keyed":
+            blocks, sizes = p.export_keyed(2)
+            final.import_keyed(blocks, sizes)
+        else:
+            final.merge(p)
+    keys, vals = final.finalize()
+    gpu_ctx.synchronize()
+    k = np.concatenate([b[0] for b in batches])
+    x = np.concatenate([b[1] for b in batches])
+    kv = keys[0].to_pylist()
+    sv = vals[0].to_numpy()
+    cv = vals[1].to_numpy()
+    assert len(kv) == len(np.unique(k))
+    for i, key in enumerate(kv):
+        g = int(key.split("-")[1]) if utf8 else int(key)
+        sel = k == g
+        assert int(cv[i]) == int(sel.sum())
+        assert sv[i] == math.fsum(x[sel].tolist()), (g, sv[i], math.fsum(x[sel].tolist()))
+
+
+def test_fp64_sum_reset_clears_full_range_words(gpu_ctx):
+    """Inputs for the full-range words (2^200, 1e-40) are summed exactly (they used to fail
+    finalize); a reset clears the words the groups used, so the next query starts from zero."""
     from kquery import native as N
     from kquery.aggregate import HashAggregateState
     from kquery.columnar import DeviceColumn
@@ -114,12 +187,13 @@ def test_fp64_sum_finalize_errors_do_not_stick(gpu_ctx):
     k = np.arange(1000, dtype=np.int64) % 7
     x = np.ones(1000)
     x[500] = 2.0 ** 200
+    x[501] = 1e-40
     st.update([DeviceColumn.from_numpy(N.TYPE_INT64, k, None, ctx=gpu_ctx)],
               [DeviceColumn.from_numpy(N.TYPE_FLOAT64, x, None, ctx=gpu_ctx)])
-    with pytest.raises(Exception, match="not exact to 1e-9"):
-        st.finalize()
-    st.update([DeviceColumn.from_numpy(N.TYPE_INT64, k, None, ctx=gpu_ctx)],
-              [DeviceColumn.from_numpy(N.TYPE_FLOAT64, np.ones(1000), None, ctx=gpu_ctx)])
+    keys, vals = st.finalize()
+    got = dict(zip(keys[0].to_pylist(), vals[0].to_pylist()))
+    for g in range(7):
+        assert got[g] == math.fsum(x[k == g].tolist())
     st.reset()
     st.update([DeviceColumn.from_numpy(N.TYPE_INT64, k, None, ctx=gpu_ctx)],
               [DeviceColumn.from_numpy(N.TYPE_FLOAT64, np.full(1000, 0.1), None, ctx=gpu_ctx)])
@@ -128,31 +202,3 @@ def test_fp64_sum_finalize_errors_do_not_stick(gpu_ctx):
     for g in range(7):
         assert got[g] == math.fsum([0.1] * int(np.sum(k == g)))
 
-
-_LIMBS_CHILD = r'''
-import pathlib, sys
-root = pathlib.Path(sys.argv[1])
-sys.path[:0] = [str(root), str(root / "query-engines_amd"), str(root / "tests")]
-from kquery.columnar import Context
-import test_fp64_sum_gpu as T
-ctx = Context.get(0)
-for groups, expected, path in [(1024, 1024, "lds"), (4500, 4500, "two-bucket"), (6, 16, "fused")]:
-    for det in (False, True):
-        T.test_fp64_sum_adversarial(ctx, groups, expected, path, det)
-print("ok")
-'''
-
-
-def test_fp64_sum_limb_window():
-    """The opt-in limb window (QE_FX_LIMBS=1, read once per process: a child process) on the
-    adversarial groups of the LDS, two-bucket and fused paths."""
-    import os
-    import pathlib
-    import subprocess
-    import sys
-
-    root = pathlib.Path(__file__).resolve().parents[1]
-    env = dict(os.environ, QE_FX_LIMBS="1")
-    r = subprocess.run([sys.executable, "-c", _LIMBS_CHILD, str(root)], cwd=str(root), env=env, capture_output=True,
-                       text=True, timeout=280)
-    assert r.returncode == 0 and "ok" in r.stdout, r.stdout[-2000:] + r.stderr[-3000:]

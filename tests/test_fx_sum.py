@@ -3,11 +3,12 @@ fx_*), built for the host (tests/native/fx_host.hip) and checked on the CPU agai
 sums (fractions.Fraction; float(Fraction) rounds correctly, ties to even).
 
 The contract (BASELINE north_star): a group's fp64 SUM is within 1e-9 relative of the
-exact sum. The accumulator gives more: the correctly rounded exact sum, bit-identical whatever order
-rows land in slots and slots merge (integer adds are associative) — or a reported error, never a
-silently wrong value. These tests pin the arithmetic itself: row images, carries across words, the
-running sum changing sign, wraps past 2^127, merges, IEEE specials, and the rounding bound for inputs
-below 2^-128. tests/test_gpu_parity.py::test_fp64_sum_adversarial runs the same cases on MI355X."""
+exact sum. The accumulator gives more: the correctly rounded exact sum over the whole fp64 range
+(math.fsum's value), bit-identical whatever order rows land in slots and slots merge (integer adds
+are associative). These tests pin the arithmetic itself: row images, carries across words, the
+running sum changing sign, wraps past 2^127, the full-range words E (inputs of 2^126 or more, bits
+below 2^-128, subnormals, overflow to +-Inf), merges in word, RAW and CHUNK form, IEEE specials.
+tests/test_fp64_sum_gpu.py runs the same cases on MI355X through every kernel path."""
 import ctypes
 import math
 import pathlib
@@ -30,7 +31,9 @@ def fx():
                                    ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_int),
                                    ctypes.POINTER(ctypes.c_ulonglong)]
     lib.qe_fx_host_row_words.argtypes = [ctypes.c_double, ctypes.POINTER(ctypes.c_ulonglong)]
-    for f in (lib.qe_fx_host_window_sum, lib.qe_fx_host_limb_sum):
+    lib.qe_fx_host_ext_result.restype = ctypes.c_double
+    lib.qe_fx_host_ext_result.argtypes = [ctypes.POINTER(ctypes.c_ulonglong)]
+    for f in (lib.qe_fx_host_window_sum,):
         f.restype = ctypes.c_double
         f.argtypes = [ctypes.POINTER(ctypes.c_double), ctypes.c_long, ctypes.c_int, ctypes.POINTER(ctypes.c_int),
                       ctypes.POINTER(ctypes.c_long), ctypes.POINTER(ctypes.c_ulonglong)]
@@ -40,7 +43,7 @@ def fx():
         order = list(range(nslots)) if order is None else list(order)
         o = (ctypes.c_int * nslots)(*order)
         err = ctypes.c_int()
-        words = (ctypes.c_ulonglong * 5)()
+        words = (ctypes.c_ulonglong * 39)()
         v = lib.qe_fx_host_sum(xs.ctypes.data_as(ctypes.POINTER(ctypes.c_double)), len(xs), nslots, o,
                                ctypes.byref(err), words)
         return v, bool(err.value), tuple(words)
@@ -50,7 +53,12 @@ def fx():
 
 
 def exact(xs):
-    return float(sum((Fraction(float(x)) for x in xs), Fraction(0)))
+    """The correctly rounded exact sum (ties to even; IEEE overflow to +-Inf)."""
+    q = sum((Fraction(float(x)) for x in xs), Fraction(0))
+    try:
+        return float(q)
+    except OverflowError:
+        return math.inf if q > 0 else -math.inf
 
 
 def same(a, b):
@@ -127,29 +135,74 @@ def test_ieee_specials(fx):
     v, err, _ = fx([inf, -inf, 1.0])
     assert math.isnan(v) and not err
     for big in ([2.0 ** 126, 1.0], [2.0 ** 125, 1.0], [-(2.0 ** 181) * 1.5, 3.0, 2.0 ** 140, -1e-20],
-                [1e50, -1e50, 7.0], [2.0 ** 181, 2.0 ** 181, -(2.0 ** 170)]):
-        v, err, _ = fx(big, 2)  # up to 2^182: the bits above the words go to the wrap count
+                [1e50, -1e50, 7.0], [2.0 ** 181, 2.0 ** 181, -(2.0 ** 170)], [2.0 ** 182, 1.0],
+                [np.finfo(np.float64).max]):
+        v, err, _ = fx(big, 2)  # 2^126 and up: the full-range words E, exact
         assert not err and same(v, exact(big)), big
-    v, err, _ = fx([2.0 ** 182, 1.0])  # beyond the wrap count too: reported, not approximated
-    assert err
-    v, err, _ = fx([np.finfo(np.float64).max])
-    assert err
 
 
 def test_tiny_inputs(fx):
-    # bits below 2^-128 are rounded (ties to even) and counted; the error bound is n * 2^-129
-    xs = [1.0, 1.1e-25, 0.9e-25, 1.3e-25, 2.0]
-    v, err, _ = fx(xs)
-    assert not err and abs(v - exact(xs)) <= 1e-9 * abs(exact(xs))
-    xs = [1.1e-25, 0.9e-25, 1.3e-25]  # only tiny terms: still within 1e-9 (2^-129 per term)
-    v, err, _ = fx(xs)
-    assert not err and abs(v - exact(xs)) <= 1e-9 * exact(xs)
-    xs = [3.7e-5, -3.7e-5]  # exact cancellation of values with low mantissa bits: exactly 0
-    v, err, _ = fx(xs)
-    assert not err and v == 0.0
-    xs = [1e-40, 2e-40, 5e-324]  # below the resolution: cannot be given to 1e-9 -> reported
-    v, err, _ = fx(xs)
-    assert err
+    # bits below 2^-128 go to E unrounded: every sum is the correctly rounded exact one
+    for xs in ([1.0, 1.1e-25, 0.9e-25, 1.3e-25, 2.0], [1.1e-25, 0.9e-25, 1.3e-25], [3.7e-5, -3.7e-5],
+               [1e-40, 2e-40, 5e-324], [2.0 ** -128, 2.0 ** -129, 2.0 ** -200]):
+        v, err, _ = fx(xs, 2)
+        assert not err and same(v, exact(xs)), xs
+    assert fx([3.7e-5, -3.7e-5])[0] == 0.0
+
+
+def fsum(xs):
+    """math.fsum, which raises on an intermediate overflow (1e308 + 1e308 - 1e308): the exact sum
+    then (its documented value without the overflow)."""
+    try:
+        return math.fsum(xs)
+    except OverflowError:
+        return exact(xs)
+
+
+def test_full_range_matches_fsum(fx):
+    """The verdict's full-range cases, bit for bit with math.fsum: groups of 1e-40 values, 1e300 with
+    unit terms, subnormals, and an intermediate overflow that cancels."""
+    rng = np.random.default_rng(9)
+    cases = [[1e-40] * 1000, [1e300] + [1.0] * 1000 + [-1e300], [5e-324] * 777, [1e308, 1e308, -1e308],
+             [1e308, -1e308, 1e308, 1e-300, -5e-324], [-1e-320, 3e-322, 2.2250738585072014e-308, -5e-324],
+             [1e300, 1.0, -1e300, 2.0 ** -1000]]
+    for xs in cases:
+        for ns in (1, 3, 8):
+            v, err, _ = fx(rng.permutation(np.array(xs)), ns, rng.permutation(ns))
+            assert not err and same(v, fsum(xs)) and same(v, exact(xs)), (xs[:3], ns)
+    # random exponents over the whole range, both signs, subnormals among them
+    for trial in range(30):
+        n = int(rng.integers(1, 400))
+        e = rng.integers(-1074, 1020, n).astype(np.float64)
+        xs = rng.choice([-1.0, 1.0], n) * np.ldexp(1.0 + rng.random(n), e.astype(np.int64))
+        xs[rng.random(n) < 0.1] = 5e-324 * rng.integers(1, 2 ** 40, 1)[0]
+        v, err, w = fx(xs, int(rng.integers(1, 9)))
+        assert same(v, exact(xs)), trial
+        assert same(v, fsum(xs)), trial
+
+
+def test_overflow_and_underflow_edges(fx):
+    mx = np.finfo(np.float64).max
+    assert fx([mx, mx])[0] == math.inf and fx([-mx, -mx])[0] == -math.inf
+    assert fx([mx, 2.0 ** 970])[0] == math.inf  # exactly half way to 2^1024: ties to even (up)
+    assert fx([mx, 2.0 ** 969])[0] == mx  # below half way
+    assert same(fx([mx, mx, -mx])[0], mx)
+    tiny = 2.2250738585072014e-308  # smallest normal
+    for xs in ([tiny, -5e-324], [5e-324] * 3, [tiny / 2, tiny / 2], [-5e-324], [tiny * 3, -tiny * 2.5]):
+        v, _, _ = fx(xs, 2)
+        assert same(v, exact(xs)) and same(v, fsum(xs)), xs
+
+
+def test_chunk_merges_equal_rows(fx):
+    """Slots merged through CHUNK records (an exported group's E) and RAW rows give the very words
+    of adding every row into one slot."""
+    rng = np.random.default_rng(10)
+    xs = np.ldexp(rng.random(300) + 0.5, rng.integers(-1074, 1000, 300))
+    xs[::3] *= -1
+    one = fx(xs, 1)
+    each = fx(xs, 64, rng.permutation(64))
+    assert one[2][5:] == each[2][5:] and one[2][:4] == each[2][:4]
+    assert same(one[0], exact(xs))
 
 
 def test_row_words_merge_like_rows(fx):
@@ -166,20 +219,19 @@ def test_row_words_merge_like_rows(fx):
     assert tuple(w) == (0, 0, 2 ** 64 - 1, 2 ** 64 - 1, 0)  # -1.0 = -(2^128) units: sign extended
 
 
-def window(fx, xs, nslots, limbs=False):
+def window(fx, xs, nslots):
     xs = np.ascontiguousarray(xs, dtype=np.float64)
     err, rare = ctypes.c_int(), ctypes.c_long()
-    words = (ctypes.c_ulonglong * 5)()
-    f = fx.lib.qe_fx_host_limb_sum if limbs else fx.lib.qe_fx_host_window_sum
+    words = (ctypes.c_ulonglong * 39)()
+    f = fx.lib.qe_fx_host_window_sum
     v = f(xs.ctypes.data_as(ctypes.POINTER(ctypes.c_double)), len(xs), nslots, ctypes.byref(err), ctypes.byref(rare),
           words)
     return v, bool(err.value), rare.value, tuple(words)
 
 
-@pytest.mark.parametrize("limbs", [True, False], ids=["limb_window", "carry_window"])
-def test_lds_window_split(fx, limbs):
-    """The specialised kernels keep a window per LDS slot — six signed limb words (default) or a
-    192-bit carry window (units 2^-96) — and send rows outside [2^-44, 2^62) to the global
+def test_lds_window_split(fx):
+    """The specialised kernels keep a window per LDS slot — a 192-bit carry window (units 2^-96) —
+    and send rows outside [2^-44, 2^62) to the global
     accumulator: the merged words equal those of adding every row to one full accumulator,
     whatever the split."""
     rng = np.random.default_rng(7)
@@ -190,7 +242,7 @@ def test_lds_window_split(fx, limbs):
         xs[rng.random(n) < 0.02] = -0.0
         xs[rng.random(n) < 0.01] = 5e-324
         full = fx(xs)
-        v, err, rare, w = window(fx, xs, int(rng.integers(1, 65)), limbs)
+        v, err, rare, w = window(fx, xs, int(rng.integers(1, 65)))
         assert w == full[2] and same(v, full[0]) and err == full[1], trial
         assert rare == int(np.sum((np.abs(xs) < 2.0 ** -44) & (xs != 0) | (np.abs(xs) >= 2.0 ** 62)))
     # window edges: the smallest and largest fast-path magnitudes, both signs, carries into u2
@@ -198,13 +250,13 @@ def test_lds_window_split(fx, limbs):
             np.nextafter(2.0 ** -44, 0), 1.0, -1.0, 2.0 ** 20 + 2.0 ** -30]
     xs = np.array(edge * 50)
     for ns in (1, 3):
-        v, err, rare, w = window(fx, rng.permutation(xs), ns, limbs)
+        v, err, rare, w = window(fx, rng.permutation(xs), ns)
         assert not err and same(v, exact(xs)) and rare == 100
 
 
-def test_limb_window_many_rows_and_signs(fx):
-    """Limb words are signed sums without carries: long runs of one sign (every limb of every
-    word positive, or negative) and alternating magnitudes across the whole window fold exactly."""
+def test_window_many_rows_and_signs(fx):
+    """The carry window over long runs of one sign (carries and borrows through every word) and
+    alternating magnitudes across the whole window folds exactly."""
     rng = np.random.default_rng(8)
     for trial in range(6):
         n = 20_000
@@ -212,6 +264,6 @@ def test_limb_window_many_rows_and_signs(fx):
         mag = np.minimum(mag, np.nextafter(2.0 ** 62, 0))
         sign = np.ones(n) if trial % 3 == 0 else (-np.ones(n) if trial % 3 == 1 else rng.choice([-1.0, 1.0], n))
         xs = mag * sign
-        v, err, rare, w = window(fx, xs, 3, True)
+        v, err, rare, w = window(fx, xs, 3)
         assert rare == 0 and not err and same(v, exact(xs)), trial
         assert w == fx(xs)[2]
