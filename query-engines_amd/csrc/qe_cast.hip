@@ -46,9 +46,8 @@ __device__ __forceinline__ void load16_words(const uint8_t* p, int n, uint64_t* 
 // column's bytes): the byte-by-byte form spent ~5 VALU instructions and a memory instruction per
 // byte on address arithmetic and assembly.
 __device__ __forceinline__ void load16_words_wide(const uint8_t* p, int n, uint64_t* w0, uint64_t* w1) {
-  typedef uint4 uint4_u __attribute__((aligned(1)));  // declared unaligned: no aligned-pointer UB
-  const uint4 t = *(const uint4_u*)p;
-  uint64_t a = ((uint64_t)t.y << 32) | t.x, b = ((uint64_t)t.w << 32) | t.z;
+  typedef uint64_t u64_unaligned __attribute__((aligned(1)));  // declared unaligned: no aligned-pointer UB
+  uint64_t a = ((const u64_unaligned*)p)[0], b = ((const u64_unaligned*)p)[1];
   if (n < 8) {
     a &= (1ull << (8 * n)) - 1ull;
     b = 0;

@@ -640,14 +640,27 @@ static void gpu_cases(void) {
       OKV(Java_NativeEngine_aggDestroy(E, K, agg));
     }
     CHECK(!memcmp(got[0], got[1], sizeof got[0]), "sums differ between batch splits");
-    /* an input the exact sum cannot hold (|x| >= 2^182) fails finalize loudly (1e30 and 1e40 sum
-     * exactly since round 5; 1e60 does not) */
+    /* the whole finite range sums exactly (round 6: 1e60, 1e300 and subnormals used to fail
+     * finalize): key 1 = 1e300 + 1 - 1e300 = 1, key 2 = 1e60 + 1e60, key 3 = 3 x 5e-324 */
     const jlong agg = OK(Java_NativeEngine_aggCreate(E, K, ctx, INTS(QE_TYPE_INT64), INTS(QE_AGG_SUM), INTS(QE_TYPE_FLOAT64), 0,
                                                      QE_HASHAGG_DETERMINISTIC));
-    const jlong kc = OK(Java_NativeEngine_columnFromLongs(E, K, ctx, QE_TYPE_INT64, LONGS(1, 2), NULL));
-    const jlong vc = OK(Java_NativeEngine_columnFromDoubles(E, K, ctx, JD((const double[]){1.0, 1e60}, 2), NULL));
+    const jlong kc = OK(Java_NativeEngine_columnFromLongs(E, K, ctx, QE_TYPE_INT64, LONGS(1, 2, 1, 3, 2, 3, 1, 3), NULL));
+    const jlong vc = OK(Java_NativeEngine_columnFromDoubles(
+        E, K, ctx, JD(((const double[]){1e300, 1e60, 1.0, 5e-324, 1e60, 5e-324, -1e300, 5e-324}), 8), NULL));
     OKV(Java_NativeEngine_aggUpdate(E, K, agg, LONGS(kc), LONGS(vc), 0));
-    THROWS("java/lang/IllegalStateException", { Java_NativeEngine_aggFinalize(E, K, agg); });
+    jlongArray outs = OK(Java_NativeEngine_aggFinalize(E, K, agg));
+    if (outs) {
+      uint8_t *vk, *vs;
+      int64_t* keys = fetch_longs(ctx, LV(outs)[0], &vk);
+      double* sums = fetch_doubles(ctx, LV(outs)[1], &vs);
+      const jlong g = OK(Java_NativeEngine_columnLength(E, K, LV(outs)[0]));
+      CHECK(g == 3, "groups %lld", (long long)g);
+      for (jlong r = 0; r < g; ++r) {
+        const double want = keys[r] == 1 ? 1.0 : keys[r] == 2 ? 2e60 : 3 * 5e-324;
+        CHECK(sums[r] == want, "full-range key %lld sum %.17g, want %.17g", (long long)keys[r], sums[r], want);
+      }
+      for (int j = 0; j < 2; ++j) OKV(Java_NativeEngine_columnFree(E, K, LV(outs)[j]));
+    }
     OKV(Java_NativeEngine_aggDestroy(E, K, agg));
     OKV(Java_NativeEngine_columnFree(E, K, kc));
     OKV(Java_NativeEngine_columnFree(E, K, vc));

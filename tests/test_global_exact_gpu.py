@@ -22,9 +22,12 @@ def _global(ctx, x, valid=None, mask=None):
     from kquery.columnar import DeviceColumn
 
     r = N.QeGlobalAgg()
-    c = DeviceColumn.from_numpy(N.TYPE_FLOAT64, x, valid, ctx=ctx).as_c()
-    m = DeviceColumn.from_numpy(N.TYPE_BOOL, mask, None, ctx=ctx).as_c() if mask is not None else None
+    col = DeviceColumn.from_numpy(N.TYPE_FLOAT64, x, valid, ctx=ctx)  # (held: the C views borrow its memory)
+    mcol = DeviceColumn.from_numpy(N.TYPE_BOOL, mask, None, ctx=ctx) if mask is not None else None
+    c = col.as_c()
+    m = mcol.as_c() if mcol is not None else None
     N.check(N.lib().qe_agg_global(ctx.handle, N.C.byref(c), N.C.byref(m) if m is not None else None, N.C.byref(r)))
+    ctx.synchronize()
     return r
 
 

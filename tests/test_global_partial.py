@@ -15,14 +15,16 @@ REL = 1e-9
 def _partials(ctx, N, DeviceColumn, pieces, t):
     import torch
 
-    parts = []
+    parts, cols = [], []
     base = 0
     for x, xv in pieces:
         p = torch.empty(N.GLOBAL_PARTIAL_BYTES, dtype=torch.uint8, device=ctx.torch_device)
-        c = DeviceColumn.from_numpy(t, x, xv, ctx=ctx).as_c()
+        cols.append(DeviceColumn.from_numpy(t, x, xv, ctx=ctx))  # held until the kernels are done
+        c = cols[-1].as_c()
         N.check(N.lib().qe_agg_global_partial(ctx.handle, N.C.byref(c), None, base, N.C.c_void_p(p.data_ptr())))
         parts.append(p)
         base += len(x)
+    ctx.synchronize()
     return parts
 
 

@@ -388,13 +388,19 @@ def test_hashagg_f64_key_and_multibatch_order(agg_ctx):
 
 
 def test_hashagg_multi_key_too_wide(gpu_ctx):
-    """Two 32-bit keys + null bits exceed the packed 63-bit key: the C ABI rejects the packing
-    loudly; HashAggregateState then groups by key-tuple codes (tests/test_tuplekeys.py)."""
+    """Two 32-bit keys + null bits exceed the packed 63-bit key: the C ABI groups by key-tuple
+    codes instead (one INT32 device key; qe_hashagg_key_layout says so), as HashAggregateState
+    does (tests/test_tuplekeys.py)."""
     kt = (N.C.c_int32 * 2)(N.TYPE_INT32, N.TYPE_DATE32)
     ad = (N.QeAggDesc * 1)(N.QeAggDesc(N.AGG_COUNT_STAR, N.TYPE_INT64))
     h = N.C.c_void_p()
-    st = N.lib().qe_hashagg_create(gpu_ctx.handle, 2, kt, 1, ad, 16, N.C.byref(h))
-    assert st == N.QE_ERR_UNSUPPORTED and "66 bits" in N.lib().qe_last_error().decode()
+    N.check(N.lib().qe_hashagg_create(gpu_ctx.handle, 2, kt, 1, ad, 16, N.C.byref(h)))
+    try:
+        dk, nk, types = N.C.c_int32(), N.C.c_int32(), (N.C.c_int32 * 4)()
+        N.check(N.lib().qe_hashagg_key_layout(h, N.C.byref(dk), N.C.byref(nk), types))
+        assert dk.value == 1 and nk.value == 1 and types[0] == N.TYPE_INT32
+    finally:
+        N.check(N.lib().qe_hashagg_destroy(h))
     state = HashAggregateState(gpu_ctx, [N.TYPE_INT32, N.TYPE_DATE32], [(N.AGG_COUNT_STAR, N.TYPE_INT64)], 16)
     assert state.key_layout == 2 and state.device_key_types == [N.TYPE_INT32]
 

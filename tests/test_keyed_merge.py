@@ -171,8 +171,8 @@ def test_max_len_bound_is_checked(gpu_ctx):
     c = DeviceColumn.from_strings(["short", "much-longer-than-seven"], ctx=gpu_ctx)
     c.max_len = 5
     v = DeviceColumn.from_numpy(N.TYPE_INT64, np.array([1, 2], dtype=np.int64), ctx=gpu_ctx)
-    st.update([c], [v, None, v])
-    with pytest.raises(N.IllegalArgumentException):
+    with pytest.raises(N.IllegalArgumentException, match="max_len"):  # at the update's read-back or at finalize
+        st.update([c], [v, None, v])
         st.finalize()
 
 
