@@ -450,16 +450,11 @@ static int agg_global_partial(qe_ctx* ctx, const qe_column* col, const qe_column
   const bool f64 = col->type == QE_TYPE_FLOAT64;
   const int64_t waves_needed = (int64_t)div_up((uint64_t)(n > 0 ? n : 1), 512);
   int64_t blocks = (int64_t)div_up((uint64_t)waves_needed, 4);
-  // dense fp64 (C3): QE_AG_PER_CU workgroups per CU (100M rows, one box: 8 -> 0.1427 ms per call,
-  // 4 -> 0.1443, 5 -> 0.1642; a one-launch form whose last workgroup folded the partials behind a
-  // device-scope fence took 0.153-0.229 ms)
-  static const int ag_per_cu = [] {
-    const char* e = getenv("QE_AG_PER_CU");
-    const int v = e && *e ? atoi(e) : 8;
-    return v >= 1 && v <= 16 ? v : 8;
-  }();
+  // eight workgroups per CU (dense fp64, C3 at 100M rows: 8 -> 0.1427 ms per call, 4 -> 0.1443,
+  // 5 -> 0.1642; a one-launch form whose last workgroup folded the partials behind a device-scope
+  // fence took 0.153-0.229 ms: docs/experiments.md)
+  const int64_t cap = (int64_t)ctx->num_cus * 8;
   const bool dense = col->type == QE_TYPE_FLOAT64 && !col->validity && !mask;
-  const int64_t cap = (int64_t)ctx->num_cus * (dense ? ag_per_cu : 8);
   if (blocks > cap) blocks = cap;
   if (blocks < 1) blocks = 1;
   const int64_t iters = (int64_t)div_up((uint64_t)(n > 0 ? n : 1), (uint64_t)blocks * 4 * 512);

@@ -2295,11 +2295,6 @@ static int launch_pass(qe_hashagg* h, Plan& P, size_t& lds, hipFunction_t pfn, i
                                          : std::max<int64_t>(ctx->num_cus, h->grid * 512 / fused_block(P.lds_log2));
         jgrid = (int)std::min<int64_t>(std::min<int64_t>((int64_t)ctx->num_cus * bpc, per_state),
                                        (int64_t)div_up((uint64_t)waves, fused_block(P.lds_log2) / 64));
-        static const int64_t max_wg = [] {  // (experiments: cap the fused grid)
-          const char* e = getenv("QE_FUSED_MAX_WG");
-          return e && *e ? (int64_t)atoll(e) : (int64_t)0;
-        }();
-        if (max_wg > 0 && jgrid > max_wg) jgrid = (int)max_wg;
         if (jgrid < 1) jgrid = 1;
         h->jit_note.clear();
         if (P.lds_compact) h->jit_note = "compact LDS table: " + std::to_string(P.lds_compact) + " slots";

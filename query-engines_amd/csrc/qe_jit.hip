@@ -1485,7 +1485,7 @@ static bool pagg_fast_ok(const Plan& P, const PartLayout& L) {
 // p's word q at dword (p / 64) * 64W + 64q + p % 64), written by the fast staged scatter and read
 // by the fast aggregation pass: a load instruction there takes 4 x 256 contiguous bytes (16 lanes
 // x 4 records of one word per block) instead of 16 bytes every 48 (record-major). Measured on the
-// records' walk alone (QE_PAGG_EXP 1 vs 4, 1B rows, 64K groups): 1.70 vs 1.26 ms.
+// records' walk alone (a round-5 timing probe, since removed: docs/experiments.md; 1B rows, 64K groups): 1.70 vs 1.26 ms.
 // (QE_PART_BLK64=1; off: the scatter's write-out then stores each record's words 256 B apart and
 // took 8.5 instead of 6.5 ms at 64K groups, more than the reads gain)
 bool part_blk64(const Plan& P, const PartLayout& L) {
@@ -1572,7 +1572,7 @@ static bool gen_pagg_fast_source(const Plan& P, const PartLayout& L, int log2, i
   }
   // record-major records loaded as contiguous KiB per load instruction and regrouped per lane
   // through a per-wave LDS staging area (W KiB per wave; `tr` above): each lane then holds 4
-  // consecutive records as before. Measured on the walk alone (QE_PAGG_EXP 1 vs 4, 1B rows, 64K
+  // consecutive records as before. Measured on the walk alone (a round-5 timing probe, since removed: docs/experiments.md; 1B rows, 64K
   // groups): 1.70 vs 1.26 ms. (QE_PAGG_TRANSPOSE=0: direct 48-byte lane loads)
   const int chcap = 1024;
   if (tr) lds += tr_bytes;

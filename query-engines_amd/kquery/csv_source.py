@@ -92,7 +92,7 @@ class CsvDataSource(DataSource):
         """``chunk_bytes`` > 0: scan a file of at least two such chunks chunk by chunk, uploading the
         next while this one parses (one batch per chunk, like the JNI scan). Off by default: tripdata
         (386 MB, one box) took 10.4 ms file -> columns in 128 MB chunks against 8.9 ms for one staged
-        upload + one parse (docs/csv_ab.md)."""
+        upload + one parse (docs/experiments.md)."""
         self.chunk_bytes = int(chunk_bytes)
         self.filename = filename
         self.hasHeaders = hasHeaders

@@ -17,8 +17,6 @@
 #   prof_trip          tools/prof_tripdata.sh (tripdata kernel trace)
 #   prof_fp64          tools/prof_fp64_sum.sh (C5 trace + SQ / LDS counters per mode)
 #   fxq                tools/exp_fxq.sh (exact-sum kernel code-shape A/B on C5)
-#   c3                 tools/exp_c3.sh (C3 global aggregate launch shapes + kernel trace)
-#   tripagg            tools/exp_tripagg.sh (tripdata aggregate kernel vs fused grid cap)
 #   spill              tools/exp_spill.sh (spilling pass reach past the compact table, QE_SPILL_MAXPCT)
 #   csvpmc             tools/prof_csv_pmc.sh (SQ / LDS counters of the tripdata kernels, 4M rows)
 #   triptraffic        tools/prof_trip_traffic.sh (FETCH_SIZE / WRITE_SIZE of the tripdata kernels)
@@ -56,8 +54,6 @@ for s in "$@"; do
     prof_trip) step prof_trip 500 env ROWS=4000000 bash tools/prof_tripdata.sh ;;
     prof_fp64) step prof_fp64 600 bash tools/prof_fp64_sum.sh ;;
     fxq) step fxq 900 bash tools/exp_fxq.sh ;;
-    c3) step c3 700 bash tools/exp_c3.sh ;;
-    tripagg) step tripagg 800 bash tools/exp_tripagg.sh ;;
     spill) step spill 1100 bash tools/exp_spill.sh ;;
     *) echo "unknown step $s" >> "$OUT/steps.log"; exit 2 ;;
   esac
