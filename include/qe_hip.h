@@ -225,6 +225,16 @@ int qe_filter_count(qe_ctx* ctx, const qe_column* mask, int64_t* out_count);
  * *out_count receives the number of rows written (also set as outs[i].length). */
 int qe_filter_apply(qe_ctx* ctx, const qe_column* mask, const qe_column* inputs,
                     int32_t ncols, qe_column* outs, int64_t* out_count);
+/* The same without a host round trip (the per-family chain cmp -> filter -> arith stream-ordered,
+ * SelectionExec -> ProjectionExec): fixed-width columns only, every output holds the mask's
+ * length rows (an upper bound), and the number of rows written goes to the device word *d_count
+ * (queued on the ctx stream like the gather). outs[i].length is set to the mask's length; rows at
+ * and beyond *d_count are unspecified. qe_eval_arith_dlen computes only the rows below such a
+ * device count; the caller reads the count back once, at the end of the chain. */
+int qe_filter_apply_async(qe_ctx* ctx, const qe_column* mask, const qe_column* inputs,
+                          int32_t ncols, qe_column* outs, int64_t* d_count);
+int qe_eval_arith_dlen(qe_ctx* ctx, int32_t op, const qe_operand* lhs, const qe_operand* rhs,
+                       qe_column* out, const int64_t* d_len);
 
 /* ---- aggregates ------------------------------------------------------------------------- */
 #define QE_AGG_SUM 1

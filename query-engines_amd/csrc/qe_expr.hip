@@ -95,8 +95,12 @@ __device__ __forceinline__ void store8(int64_t* out, int64_t i0, int nrows, cons
   }
 }
 
+// dn: a device-side row count (a stream-ordered selection's, qe_filter_apply_async): only rows
+// below min(n, *dn) are computed.
 __global__ void __launch_bounds__(256) k_arith(Src a, Src b, int32_t op, int32_t ct, int64_t* __restrict__ out,
-                                               uint8_t* __restrict__ out_valid, int64_t n) {
+                                               uint8_t* __restrict__ out_valid, int64_t n,
+                                               const int64_t* __restrict__ dn) {
+  if (dn) n = min(n, *dn);
   const int64_t ngroups = (n + 7) >> 3;
   for (int64_t g = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; g < ngroups;
        g += (int64_t)gridDim.x * blockDim.x) {
@@ -295,7 +299,8 @@ using namespace qe;
 
 extern "C" {
 
-int qe_eval_arith(qe_ctx* ctx, int32_t op, const qe_operand* lhs, const qe_operand* rhs, qe_column* out) {
+static int eval_arith(qe_ctx* ctx, int32_t op, const qe_operand* lhs, const qe_operand* rhs, qe_column* out,
+                      const int64_t* dn) {
   QE_TRY(ctx_enter(ctx));
   QE_CHECK(op >= QE_OP_ADD && op <= QE_OP_DIV, QE_ERR_INVALID_ARG, "not an arithmetic op: %d", op);
   int64_t n;
@@ -315,8 +320,18 @@ int qe_eval_arith(qe_ctx* ctx, int32_t op, const qe_operand* lhs, const qe_opera
   out->length = n;
   if (n == 0) return QE_OK;
   hipLaunchKernelGGL(k_arith, dim3(grid_for(ctx, (n + 7) / 8)), dim3(256), 0, ctx->stream, a, b, op, ct,
-                     (int64_t*)out->values, out->validity, n);
+                     (int64_t*)out->values, out->validity, n, dn);
   return launch_check("k_arith");
+}
+
+int qe_eval_arith(qe_ctx* ctx, int32_t op, const qe_operand* lhs, const qe_operand* rhs, qe_column* out) {
+  return eval_arith(ctx, op, lhs, rhs, out, nullptr);
+}
+
+int qe_eval_arith_dlen(qe_ctx* ctx, int32_t op, const qe_operand* lhs, const qe_operand* rhs, qe_column* out,
+                       const int64_t* d_len) {
+  QE_CHECK(d_len, QE_ERR_INVALID_ARG, "null device row count");
+  return eval_arith(ctx, op, lhs, rhs, out, d_len);
 }
 
 int qe_eval_cmp(qe_ctx* ctx, int32_t op, const qe_operand* lhs, const qe_operand* rhs, qe_column* out) {

@@ -500,3 +500,52 @@ int qe_filter_apply(qe_ctx* ctx, const qe_column* mask, const qe_column* inputs,
 }
 
 }  // extern "C"
+
+namespace qe {
+__global__ void k_copy_count(const int64_t* __restrict__ src, int64_t* __restrict__ dst) { *dst = *src; }
+}  // namespace qe
+
+extern "C" int qe_filter_apply_async(qe_ctx* ctx, const qe_column* mask, const qe_column* inputs, int32_t ncols,
+                                     qe_column* outs, int64_t* d_count) {
+  QE_TRY(ctx_enter(ctx));
+  QE_CHECK(ncols >= 0 && ncols <= FT_MAX_COLS, QE_ERR_UNSUPPORTED, "at most %d columns per call", FT_MAX_COLS);
+  QE_CHECK(ncols == 0 || (inputs && outs), QE_ERR_INVALID_ARG, "null column arrays");
+  QE_CHECK(mask != nullptr && d_count != nullptr, QE_ERR_INVALID_ARG, "null mask or count");
+  const int64_t n = mask->length;
+  GatherArgs args{};
+  args.ncols = ncols;
+  for (int i = 0; i < ncols; ++i) {
+    const qe_column& in = inputs[i];
+    const qe_column& out = outs[i];
+    QE_CHECK(in.length == n, QE_ERR_INVALID_ARG, "column %d has %lld rows, mask %lld", i, (long long)in.length,
+             (long long)n);
+    QE_CHECK(is_fixed(in.type), QE_ERR_UNSUPPORTED,
+             "stream-ordered filter: column %d type %d is not fixed-width (qe_filter_apply sizes UTF8 outputs)", i,
+             in.type);
+    QE_CHECK(out.type == in.type && (out.values || n == 0), QE_ERR_INVALID_ARG, "output %d must have the input's type", i);
+    QE_CHECK(out.length >= n, QE_ERR_CAPACITY, "output %d holds %lld rows, need the mask's %lld (an upper bound)", i,
+             (long long)out.length, (long long)n);
+    QE_CHECK(!in.validity || (out.validity && ((uintptr_t)out.validity & 3) == 0), QE_ERR_INVALID_ARG,
+             "output %d needs a 4-byte aligned validity buffer", i);
+    args.cols[i] = GatherCol{in.values, in.validity, out.values, in.validity ? (uint32_t*)out.validity : nullptr,
+                             type_width(in.type), 0, nullptr};
+  }
+  FilterPlan fp;
+  QE_TRY(filter_prepare(ctx, mask, &fp));
+  for (int i = 0; i < ncols; ++i)
+    if (args.cols[i].out_valid && n > 0)
+      QE_HIP(hipMemsetAsync(outs[i].validity, 0, (size_t)div_up((uint64_t)n, 32) * 4, ctx->stream));
+  if (n > 0 && ncols > 0) {
+    hipLaunchKernelGGL(k_compact, dim3((unsigned)fp.ntiles), dim3(FT_THREADS), 0, ctx->stream,
+                       (const uint8_t*)mask->values, mask->validity, n, fp.offsets, args);
+    QE_TRY(launch_check("k_compact"));
+  }
+  if (n > 0) {
+    hipLaunchKernelGGL(k_copy_count, dim3(1), dim3(1), 0, ctx->stream, fp.offsets + fp.ntiles, d_count);
+    QE_TRY(launch_check("k_copy_count"));
+  } else {
+    QE_HIP(hipMemsetAsync(d_count, 0, 8, ctx->stream));
+  }
+  for (int i = 0; i < ncols; ++i) outs[i].length = n;
+  return QE_OK;
+}

@@ -174,18 +174,57 @@ def bitmap_bytes(n: int) -> int:
     return ((n + 31) // 32) * 4
 
 
+class DeviceCount:
+    """A row count that lives in HBM (the selected rows of a stream-ordered selection,
+    qe_filter_apply_async): read back once, on first use, after the ctx stream's work."""
+
+    def __init__(self, tensor, ctx: "Context"):
+        self.tensor = tensor  # int64 [1] on the device
+        self.ctx = ctx
+        self._v: Optional[int] = None
+
+    def ptr(self):
+        return N.C.c_void_p(self.tensor.data_ptr())
+
+    def get(self) -> int:
+        if self._v is None:
+            self.ctx.synchronize()
+            self._v = int(self.tensor.cpu().item())
+        return self._v
+
+
 class DeviceColumn(ColumnVector):
-    """An Arrow array in HBM (offset 0). Replaces ArrowFieldVector (Main.kt:176-202)."""
+    """An Arrow array in HBM (offset 0). Replaces ArrowFieldVector (Main.kt:176-202).
+    `length` may be pending: a column produced by a stream-ordered selection holds `capacity`
+    rows of which the first DeviceCount rows are real; reading `length` resolves it (one sync)."""
 
     def __init__(self, type_id: int, length: int, values, validity=None, offsets=None, ctx: Optional[Context] = None):
         self.type = type_id
-        self.length = int(length)
+        self._length = int(length)
+        self.pending: Optional[DeviceCount] = None
         self.values = values
         self.validity = validity
         self.offsets = offsets
         self.ctx = ctx or Context.get(values.device.index if values is not None else 0)
         self._c = None
         self.max_len = None  # UTF8: a host-known bound on the values' byte lengths (None: unknown)
+
+    @property
+    def length(self) -> int:
+        if self.pending is not None:
+            self._length = self.pending.get()
+            self.pending = None
+        return self._length
+
+    @length.setter
+    def length(self, n: int) -> None:
+        self._length = int(n)
+        self.pending = None
+
+    @property
+    def capacity(self) -> int:
+        """Rows held: the length, or the upper bound of a pending one (no sync)."""
+        return self._length
 
     # ---- allocation ------------------------------------------------------------------------
     @classmethod
@@ -250,12 +289,14 @@ class DeviceColumn(ColumnVector):
                    torch.from_numpy(offs).to(ctx.torch_device), ctx)
 
     # ---- C ABI view ------------------------------------------------------------------------
-    def as_c(self) -> N.QeColumn:
+    def as_c(self, pending_ok: bool = False) -> N.QeColumn:
+        """The C view. pending_ok: a pending length stays unresolved and the view holds `capacity`
+        rows (for the device-count calls, qe_eval_arith_dlen)."""
         ml = self.max_len if self.type == N.TYPE_UTF8 and self.max_len is not None else 0
         return N.QeColumn(
             self.type,
             int(min(ml, (1 << 31) - 1)),
-            self.length,
+            self._length if pending_ok else self.length,
             self.validity.data_ptr() if self.validity is not None else None,
             self.values.data_ptr() if self.values is not None else None,
             self.offsets.data_ptr() if self.offsets is not None else None,

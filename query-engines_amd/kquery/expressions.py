@@ -98,11 +98,11 @@ def _ctx_of(batch: RecordBatch):
     return Context.get(0)
 
 
-def _operand(cv: ColumnVector, keep: list) -> N.QeOperand:
+def _operand(cv: ColumnVector, keep: list, pending_ok: bool = False) -> N.QeOperand:
     if isinstance(cv, ScalarColumn):
         return N.QeOperand(None, cv.as_scalar())
     if isinstance(cv, DeviceColumn):
-        c = cv.as_c()
+        c = cv.as_c(pending_ok)
         keep.append(c)
         return N.QeOperand(N.C.pointer(c), N.QeScalar())
     raise N.IllegalStateException(N.QE_ERR_UNSUPPORTED, f"operand {type(cv).__name__} is not device-resident")
@@ -116,6 +116,18 @@ def _nullable(cv: ColumnVector) -> bool:
     if isinstance(cv, ScalarColumn):
         return cv.value is None
     return cv.validity is not None
+
+
+def _pending(*cvs):
+    """The one DeviceCount the device columns among cvs share, or None (then every length is
+    resolved first: columns of different selections never mix unresolved)."""
+    cols = [cv for cv in cvs if isinstance(cv, DeviceColumn)]
+    ps = {id(c.pending): c.pending for c in cols}
+    if len(ps) == 1 and None not in ps.values():
+        return next(iter(ps.values()))
+    for c in cols:
+        _ = c.length
+    return None
 
 
 def _ref_column(*cvs) -> DeviceColumn:
@@ -145,8 +157,17 @@ class ArithmeticExpression(BinaryExpression):
         ref = _ref_column(lv, rv)
         out_t = N.TYPE_FLOAT64 if (_is_f64(lv) or _is_f64(rv)) else N.TYPE_INT64
         nullable = _nullable(lv) or _nullable(rv) or (out_t == N.TYPE_INT64 and self.op == N.OP_DIV)
-        out = DeviceColumn.empty(out_t, ref.length, nullable, ctx=ref.ctx)
+        pend = _pending(lv, rv)
         keep: list = []
+        if pend is not None:  # rows of a stream-ordered selection: compute below its device count
+            out = DeviceColumn.empty(out_t, ref.capacity, nullable, ctx=ref.ctx)
+            a, b = _operand(lv, keep, True), _operand(rv, keep, True)
+            oc = out.as_c()
+            N.check(N.lib().qe_eval_arith_dlen(ref.ctx.handle, self.op, N.C.byref(a), N.C.byref(b), N.C.byref(oc),
+                                               pend.ptr()))
+            out.pending = pend
+            return out
+        out = DeviceColumn.empty(out_t, ref.length, nullable, ctx=ref.ctx)
         a, b = _operand(lv, keep), _operand(rv, keep)
         oc = out.as_c()
         N.check(N.lib().qe_eval_arith(ref.ctx.handle, self.op, N.C.byref(a), N.C.byref(b), N.C.byref(oc)))

@@ -218,6 +218,8 @@ SIGNATURES = [
     ("qe_cast_utf8_to_f64", C.c_int, [_P, _COLP, _COLP, _I64P]),
     ("qe_filter_count", C.c_int, [_P, _COLP, _I64P]),
     ("qe_filter_apply", C.c_int, [_P, _COLP, _COLP, C.c_int32, _COLP, _I64P]),
+    ("qe_filter_apply_async", C.c_int, [_P, _COLP, _COLP, C.c_int32, _COLP, _P]),
+    ("qe_eval_arith_dlen", C.c_int, [_P, C.c_int32, _OPP, _OPP, _COLP, _P]),
     ("qe_agg_global", C.c_int, [_P, _COLP, _COLP, C.POINTER(QeGlobalAgg)]),
     ("qe_agg_global_partial", C.c_int, [_P, _COLP, _COLP, C.c_int64, _P]),
     ("qe_agg_global_merge", C.c_int, [_P, C.c_int32, _P, C.c_int32, C.POINTER(QeGlobalAgg)]),

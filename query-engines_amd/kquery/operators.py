@@ -12,7 +12,7 @@ from typing import Iterator, List, Optional, Sequence
 
 from . import native as N
 from .aggregate import HashAggregateState, dictionary_keys, output_type
-from .columnar import DeviceColumn, Field, RecordBatch, Schema
+from .columnar import DeviceColumn, DeviceCount, Field, RecordBatch, Schema
 from .expressions import (
     AggregateExpression,
     AndExpression,
@@ -119,7 +119,25 @@ def _alloc_like(c: DeviceColumn, n: int, ctx) -> DeviceColumn:
 
 
 def filter_batch(batch: RecordBatch, mask: DeviceColumn) -> RecordBatch:
+    """SelectionExec's compaction. Fixed-width columns (at most 8) take the stream-ordered form
+    (qe_filter_apply_async): outputs sized by the mask, the selected-row count left in HBM and read
+    back only when a consumer needs a length (DeviceColumn.length), so cmp -> filter -> arith runs
+    without a host round trip. UTF8 columns take qe_filter_apply (their byte sizes need the count)."""
     ctx = mask.ctx
+    cols = batch.fields
+    if (0 < len(cols) <= N.MAX_COLS and all(isinstance(c, DeviceColumn) and c.type in N.FIXED_WIDTH for c in cols)):
+        import torch
+
+        n = mask.length
+        outs = [DeviceColumn.empty(c.type, n, c.nullable, ctx=ctx) for c in cols]
+        cnt = DeviceCount(torch.empty(1, dtype=torch.int64, device=ctx.torch_device), ctx)
+        mc = mask.as_c()
+        ins = (N.QeColumn * len(cols))(*[c.as_c() for c in cols])
+        os_ = (N.QeColumn * len(cols))(*[o.as_c() for o in outs])
+        N.check(N.lib().qe_filter_apply_async(ctx.handle, N.C.byref(mc), ins, len(cols), os_, cnt.ptr()))
+        for o in outs:
+            o.pending = cnt
+        return RecordBatch(batch.schema, outs)
     cnt = N.C.c_int64()
     mc = mask.as_c()
     N.check(N.lib().qe_filter_count(ctx.handle, N.C.byref(mc), N.C.byref(cnt)))

@@ -68,11 +68,12 @@ def main():
                               [AddExpression(ColumnExpression(0), ColumnExpression(1))])
         out = {}
 
-        def run():
+        def run():  # the selected-row count comes back once, at the end of the chain
             out["b"] = next(proj.execute())
+            out["n"] = out["b"].rowCount()
 
         ms = timed(run)
-        sel_rows = out["b"].rowCount()
+        sel_rows = out["n"]
         # algorithmic: read a, b (16 B) + write a+b for the selected rows
         report("C2 filter(a>2^19)+project(a+b), 10M int64 (160 MB: fits the 256 MB MALL)", n,
                16 + 8 * sel_rows / n, ms, selected=sel_rows, path="per-family operators (cmp, count, compact, arith)")
