@@ -398,7 +398,7 @@ def test_hashagg_multi_key_too_wide(gpu_ctx):
     try:
         dk, nk, types = N.C.c_int32(), N.C.c_int32(), (N.C.c_int32 * 4)()
         N.check(N.lib().qe_hashagg_key_layout(h, N.C.byref(dk), N.C.byref(nk), types))
-        assert dk.value == 1 and nk.value == 1 and types[0] == N.TYPE_INT32
+        assert dk.value == 2 and nk.value == 1 and types[0] == N.TYPE_INT32  # key-tuple codes
     finally:
         N.check(N.lib().qe_hashagg_destroy(h))
     state = HashAggregateState(gpu_ctx, [N.TYPE_INT32, N.TYPE_DATE32], [(N.AGG_COUNT_STAR, N.TYPE_INT64)], 16)
