@@ -595,8 +595,11 @@ __host__ __device__ inline double fxe_result(const qu64* e, qu64 w0, qu64 w1, qu
 }
 
 // A RAW or CHUNK partial into E at e; the slot's status at st gets FX_EXT and the partial's specials.
+// Always out of line (also where QE_FX_INLINE inlines the other rare paths): the generated kernels
+// reach it only through gcombine_fx / gcombine_excl, and an inlined copy grew the C5 kernel by ~800
+// instructions and 9 VGPRs.
 template <bool ATOMIC>
-__host__ __device__ inline void fxe_partial(qu64* e, qu64* st, qu64 w0, qu64 w1, qu64 w2, qu64 w3, qu64 vst) {
+__host__ __device__ __attribute__((noinline)) void fxe_partial(qu64* e, qu64* st, qu64 w0, qu64 w1, qu64 w2, qu64 w3, qu64 vst) {
   if (vst & FX_RAW) {
     fxe_add_value<ATOMIC>(e, (qi64)w0);
   } else {

@@ -14,6 +14,8 @@
 #   tripdata           tools/bench_tripdata.py (the reference's own query, K:1336)
 #   fp64               tools/exp_fp64_sum.py C5 C4 (exact vs opt-in fast fp64 sums)
 #   profile            profiles/run_profile.sh (bench kernel trace + PMC traffic)
+#   c3pmc              tools/prof_c3_pmc.sh (C3 kernel trace, FETCH/WRITE, SQ and TA counters)
+#   c2prof             tools/prof_c2.sh with CFG=C2 (C2 kernel trace + counters)
 #   prof_trip          tools/prof_tripdata.sh (tripdata kernel trace)
 #   prof_fp64          tools/prof_fp64_sum.sh (C5 trace + SQ / LDS counters per mode)
 #   fxq                tools/exp_fxq.sh (exact-sum kernel code-shape A/B on C5)
@@ -54,6 +56,8 @@ for s in "$@"; do
     prof_trip) step prof_trip 500 env ROWS=4000000 bash tools/prof_tripdata.sh ;;
     prof_fp64) step prof_fp64 600 bash tools/prof_fp64_sum.sh ;;
     fxq) step fxq 900 bash tools/exp_fxq.sh ;;
+    c3pmc) step c3pmc 900 bash tools/prof_c3_pmc.sh ;;
+    c2prof) step c2prof 600 env CFG=C2 bash tools/prof_c2.sh ;;
     spill) step spill 1100 bash tools/exp_spill.sh ;;
     *) echo "unknown step $s" >> "$OUT/steps.log"; exit 2 ;;
   esac
