@@ -595,11 +595,8 @@ __host__ __device__ inline double fxe_result(const qu64* e, qu64 w0, qu64 w1, qu
 }
 
 // A RAW or CHUNK partial into E at e; the slot's status at st gets FX_EXT and the partial's specials.
-// Always out of line (also where QE_FX_INLINE inlines the other rare paths): the generated kernels
-// reach it only through gcombine_fx / gcombine_excl, and an inlined copy grew the C5 kernel by ~800
-// instructions and 9 VGPRs.
 template <bool ATOMIC>
-__host__ __device__ __attribute__((noinline)) void fxe_partial(qu64* e, qu64* st, qu64 w0, qu64 w1, qu64 w2, qu64 w3, qu64 vst) {
+__host__ __device__ inline void fxe_partial(qu64* e, qu64* st, qu64 w0, qu64 w1, qu64 w2, qu64 w3, qu64 vst) {
   if (vst & FX_RAW) {
     fxe_add_value<ATOMIC>(e, (qi64)w0);
   } else {
@@ -608,6 +605,19 @@ __host__ __device__ __attribute__((noinline)) void fxe_partial(qu64* e, qu64* st
     if (c < FXE_CHUNKS) fxe_add_words<ATOMIC>(e, 4 * c, v, c == FXE_CHUNKS - 1 ? FXE_WORDS - 4 * c : 4);
   }
   fx_status<ATOMIC>(st, FX_EXT | (vst & FX_SPECIAL));
+}
+
+// The table paths reach fxe_partial through these, always out of line (also where QE_FX_INLINE
+// inlines the other rare paths): inlined at every combine site it grew the C5 kernel by ~800
+// instructions and 9 VGPRs. (Static: a non-static out-of-line template made hipRTC's code object
+// fail to load, HSA_STATUS_ERROR_INVALID_ISA.)
+static __device__ __attribute__((noinline)) void fxe_partial_atomic(qu64* e, qu64* st, qu64 w0, qu64 w1, qu64 w2,
+                                                                     qu64 w3, qu64 vst) {
+  fxe_partial<true>(e, st, w0, w1, w2, w3, vst);
+}
+static __device__ __attribute__((noinline)) void fxe_partial_plain(qu64* e, qu64* st, qu64 w0, qu64 w1, qu64 w2,
+                                                                    qu64 w3, qu64 vst) {
+  fxe_partial<false>(e, st, w0, w1, w2, w3, vst);
 }
 
 // The SUM of a slot: words w0..w3, status st, E at e (read only when st has FX_EXT).
@@ -719,7 +729,7 @@ static __device__ QE_FX_OUTLINE void gcombine_fx(const DTable& t, int j, qu64 s,
   const qu64 stride = t.cap + 2;
   qu64* ix = t.idx[j];
   if (st & (FX_RAW | FX_CHUNK)) {  // an input or a chunk for E
-    fxe_partial<true>(t.ext[j] + s * FXE_WORDS, &ix[3 * stride + s], w0, w1, w2, w3, st);
+    fxe_partial_atomic(t.ext[j] + s * FXE_WORDS, &ix[3 * stride + s], w0, w1, w2, w3, st);
     return;
   }
   fx_add_words<true>([&](int w) { return w == 0 ? (qu64*)&t.acc[j][s] : &ix[(w - 1) * stride + s]; }, w0, w1, w2, w3,
@@ -807,7 +817,7 @@ __device__ inline void gcombine_excl(const DTable& t, int acck, int j, qu64 s, q
     const qu64 stride = t.cap + 2;
     qu64* ix = t.idx[j] + s;
     if (i3 & (FX_RAW | FX_CHUNK)) {
-      fxe_partial<false>(t.ext[j] + s * FXE_WORDS, &ix[3 * stride], (qu64)acc, i0, i1, i2, i3);
+      fxe_partial_plain(t.ext[j] + s * FXE_WORDS, &ix[3 * stride], (qu64)acc, i0, i1, i2, i3);
       return;
     }
     fx_add_words<false>([&](int w) { return w == 0 ? (qu64*)a : &ix[(w - 1) * stride]; }, (qu64)acc, i0, i1, i2, i3,
