@@ -607,19 +607,6 @@ __host__ __device__ inline void fxe_partial(qu64* e, qu64* st, qu64 w0, qu64 w1,
   fx_status<ATOMIC>(st, FX_EXT | (vst & FX_SPECIAL));
 }
 
-// The table paths reach fxe_partial through these, always out of line (also where QE_FX_INLINE
-// inlines the other rare paths): inlined at every combine site it grew the C5 kernel by ~800
-// instructions and 9 VGPRs. (Static: a non-static out-of-line template made hipRTC's code object
-// fail to load, HSA_STATUS_ERROR_INVALID_ISA.)
-static __device__ __attribute__((noinline)) void fxe_partial_atomic(qu64* e, qu64* st, qu64 w0, qu64 w1, qu64 w2,
-                                                                     qu64 w3, qu64 vst) {
-  fxe_partial<true>(e, st, w0, w1, w2, w3, vst);
-}
-static __device__ __attribute__((noinline)) void fxe_partial_plain(qu64* e, qu64* st, qu64 w0, qu64 w1, qu64 w2,
-                                                                    qu64 w3, qu64 vst) {
-  fxe_partial<false>(e, st, w0, w1, w2, w3, vst);
-}
-
 // The SUM of a slot: words w0..w3, status st, E at e (read only when st has FX_EXT).
 __host__ __device__ inline double fx_result(qu64 w0, qu64 w1, qu64 w2, qu64 w3, qu64 st, const qu64* e) {
   const qu64 f = st & FX_FLAGS;
@@ -724,12 +711,15 @@ __device__ inline void gadd_cstar(const DTable& t, qu64 slot, qu64 c) {
 // An exact fp64 SUM partial into global slot s (device-scope atomics). Out of line: the kernels call
 // it from their flush and from rare rows, and inlined copies of its carry chain at every such site
 // made the C5 fused kernel 8x larger than the instruction cache.
+// WORDS: the partial is known to be words (an LDS window or slot at a flush): no RAW / CHUNK test,
+// so the generated kernels carry E's code only on the rare-row paths.
+template <bool WORDS = false>
 static __device__ QE_FX_OUTLINE void gcombine_fx(const DTable& t, int j, qu64 s, qu64 w0, qu64 w1,
                                                              qu64 w2, qu64 w3, qu64 st) {
   const qu64 stride = t.cap + 2;
   qu64* ix = t.idx[j];
-  if (st & (FX_RAW | FX_CHUNK)) {  // an input or a chunk for E
-    fxe_partial_atomic(t.ext[j] + s * FXE_WORDS, &ix[3 * stride + s], w0, w1, w2, w3, st);
+  if (!WORDS && (st & (FX_RAW | FX_CHUNK))) {  // an input or a chunk for E
+    fxe_partial<true>(t.ext[j] + s * FXE_WORDS, &ix[3 * stride + s], w0, w1, w2, w3, st);
     return;
   }
   fx_add_words<true>([&](int w) { return w == 0 ? (qu64*)&t.acc[j][s] : &ix[(w - 1) * stride + s]; }, w0, w1, w2, w3,
@@ -745,7 +735,8 @@ static __device__ QE_FX_OUTLINE void gcombine_fx_row(const DTable& t, int j, qu6
 }
 
 // An exact fp64 SUM partial may carry words with nn == 0: a rare input whose row was counted in an
-// LDS slot (fx_rare_global).
+// LDS slot (fx_rare_global). WORDS: as gcombine_fx's (a flush).
+template <bool WORDS = false>
 __device__ inline void gcombine(const DTable& t, int acck, int j, qu64 s, qi64 acc, qu64 nn, qu64 i0, qu64 i1,
                                 qu64 i2, qu64 i3, bool add_nn = true) {
   if (nn == 0 && acck != ACC_SUM_X) return;
@@ -773,7 +764,7 @@ __device__ inline void gcombine(const DTable& t, int acck, int j, qu64 s, qi64 a
     if (i2 != ~0ull) atomicMin(&ix[2 * stride + s], i2);
     if (i3 != ~0ull) atomicMin(&ix[3 * stride + s], i3);
   } else if (acck == ACC_SUM_X) {  // 256-bit add with carries (words: acc, idx 0..2; status idx 3)
-    gcombine_fx(t, j, s, (qu64)acc, i0, i1, i2, i3);
+    gcombine_fx<WORDS>(t, j, s, (qu64)acc, i0, i1, i2, i3);
   }
 }
 
@@ -788,6 +779,7 @@ __device__ inline void gadd_cstar_excl(const DTable& t, qu64 slot, qu64 c, qu32*
   if (slot >= t.cap && old == 0) atomicAdd(newg, 1u);
 }
 
+template <bool WORDS = false>
 __device__ inline void gcombine_excl(const DTable& t, int acck, int j, qu64 s, qi64 acc, qu64 nn, qu64 i0,
                                      qu64 i1, qu64 i2, qu64 i3) {
   if (nn == 0 && acck != ACC_SUM_X) return;
@@ -816,8 +808,8 @@ __device__ inline void gcombine_excl(const DTable& t, int acck, int j, qu64 s, q
   } else if (acck == ACC_SUM_X) {
     const qu64 stride = t.cap + 2;
     qu64* ix = t.idx[j] + s;
-    if (i3 & (FX_RAW | FX_CHUNK)) {
-      fxe_partial_plain(t.ext[j] + s * FXE_WORDS, &ix[3 * stride], (qu64)acc, i0, i1, i2, i3);
+    if (!WORDS && (i3 & (FX_RAW | FX_CHUNK))) {
+      fxe_partial<false>(t.ext[j] + s * FXE_WORDS, &ix[3 * stride], (qu64)acc, i0, i1, i2, i3);
       return;
     }
     fx_add_words<false>([&](int w) { return w == 0 ? (qu64*)a : &ix[(w - 1) * stride]; }, (qu64)acc, i0, i1, i2, i3,
@@ -886,6 +878,7 @@ static __device__ QE_FX_OUTLINE void fx_rare_global(const Plan& P, qu32 jmask, q
   fx_row_words(x, w);
   qu64 gs;
   if (gtable_find(P.t, key, knull, gs)) {
+#pragma unroll 1  // (one copy of the combine: unrolled over QE_MAX_AGGS it was 8 per call site)
     for (int j = 0; j < P.naggs; ++j)
       if ((jmask >> j) & 1) gcombine(P.t, ACC_SUM_X, j, gs, (qi64)w[0], 0, w[1], w[2], w[3], w[4], false);
     return;
@@ -898,6 +891,7 @@ static __device__ QE_FX_OUTLINE void fx_rare_global(const Plan& P, qu32 jmask, q
   qu8* rec = P.ovf + ri * (qu64)P.rec_bytes;
   write_record_head(rec, key, knull, 0);
   int off = 24;
+#pragma unroll 1
   for (int a = 0; a < P.naggs; ++a) {
     qu64* f = (qu64*)(rec + off);
     const int acc = P.aggs[a].acc;

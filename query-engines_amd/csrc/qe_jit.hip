@@ -580,11 +580,12 @@ void emit_flush(const Plan& P, std::ostringstream& o, bool mark_full = false, bo
       o << "      const qu64 i0 = ~0ull, i1 = ~0ull, i2 = ~0ull, i3 = ~0ull;\n";
     const bool skip_nn = (P.nn_skip >> j) & 1;
     const char* add_nn = skip_nn ? "false" : "true";
+    const char* words = a.acc == ACC_SUM_X ? "<true>" : "";  // (an exact SUM's window: words, never E)
     if (a.fn != QE_AGG_COUNT_STAR && part)
-      o << "      if (ok) { if (excl) gcombine_excl(P.t, " << a.acc << ", " << j << ", gs, acc, nn, i0, i1, i2, i3);"
-        << " else gcombine(P.t, " << a.acc << ", " << j << ", gs, acc, nn, i0, i1, i2, i3, " << add_nn << "); }\n";
+      o << "      if (ok) { if (excl) gcombine_excl" << words << "(P.t, " << a.acc << ", " << j << ", gs, acc, nn, i0, i1, i2, i3);"
+        << " else gcombine" << words << "(P.t, " << a.acc << ", " << j << ", gs, acc, nn, i0, i1, i2, i3, " << add_nn << "); }\n";
     else if (a.fn != QE_AGG_COUNT_STAR && !(a.acc == ACC_NONE && skip_nn))  // implicit COUNT(x): nothing to add
-      o << "      if (ok) gcombine(P.t, " << a.acc << ", " << j << ", gs, acc, nn, i0, i1, i2, i3, " << add_nn << ");\n";
+      o << "      if (ok) gcombine" << words << "(P.t, " << a.acc << ", " << j << ", gs, acc, nn, i0, i1, i2, i3, " << add_nn << ");\n";
     o << "      if (!ok) { qu64* f = (qu64*)(rec + " << off << "); f[0] = (qu64)acc; f[1] = nn;";
     if (acc_has_idx(a.acc)) o << " f[2] = i0; f[3] = i1; f[4] = i2; f[5] = i3;";
     o << " }\n    }\n";
