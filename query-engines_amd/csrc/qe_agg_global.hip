@@ -53,6 +53,13 @@ __device__ __forceinline__ void neumaier_add(double& s, double& c, double x) {
   s = t;
 }
 
+// Knuth's two-sum (s + x = t + err exactly, no compare or select): the dense kernel's row step.
+__device__ __forceinline__ void two_sum_add(double& s, double& c, double x) {
+  const double t = s + x, bp = t - s;
+  c += (s - (t - bp)) + (x - bp);
+  s = t;
+}
+
 __device__ __forceinline__ void gpart_merge(GPart& a, const GPart& b) {
   a.rows += b.rows;
   a.count += b.count;
@@ -238,18 +245,21 @@ __global__ void __launch_bounds__(256) k_agg_global_f64_dense(const int64_t* __r
 #pragma unroll
       for (int k = 0; k < 8; ++k) count += (base + 128 * (k >> 1) + 2 * lane + (k & 1) < n) ? 1 : 0;
     }
-    bool special = false;
+    // NaN, +-Inf, zeros (and subnormals) have an exponent field of all ones or zero: (hi + 2^20) &
+    // 0x7FE00000 is 0 for exactly those (integer ops on the high word, not fp64 compares)
+    uint32_t ex_min = 0xFFFFFFFFu;
 #pragma unroll
     for (int k = 0; k < 8; ++k) {
-      neumaier_add(s[k], c[k], d[k]);  // out-of-range rows read as 0.0: no effect on the sum
+      two_sum_add(s[k], c[k], d[k]);  // out-of-range rows read as 0.0: no effect on the sum
       const bool in = full || base + 128 * (k >> 1) + 2 * lane + (k & 1) < n;
       const double dm = in ? d[k] : __builtin_nan("");  // fmin/fmax ignore NaN
       mn = fmin(mn, dm);
       mx = fmax(mx, dm);
       a += fabs(d[k]);
-      special |= ((d[k] - d[k]) != 0.0) | (d[k] == 0.0);  // NaN, +-Inf or a zero
+      const uint32_t hi = (uint32_t)((uint64_t)f64_bits(d[k]) >> 32);
+      ex_min = min(ex_min, (hi + 0x00100000u) & 0x7FE00000u);
     }
-    if (special) {  // NaN, an infinity or a zero among these 8 rows (rare): exact first-occurrence bookkeeping
+    if (ex_min == 0) {  // NaN, an infinity or a zero among these 8 rows (rare): exact first-occurrence bookkeeping
 #pragma unroll
       for (int k = 0; k < 8; ++k) {
         const int64_t row = base + 128 * (k >> 1) + 2 * lane + (k & 1);
@@ -372,11 +382,25 @@ __global__ void __launch_bounds__(256) k_agg_global_fx(const int64_t* __restrict
 // instead of four), then a tree in LDS (1024 partials x 128 B) with block barriers down to one
 // wave and wave barriers below. (Round 5: 256 threads in four dependent rounds and a shuffle tree
 // per wave took 7.9 us.)
-constexpr int FOLD_THREADS = 1024;
+// The LDS copies are padded to 33 dwords: at the struct's 32-dword stride every lane of a wave hit
+// the same two banks (the unpadded tree took 19 us).
+constexpr int FOLD_THREADS = 1024, GP_WORDS = sizeof(GPart) / 4, GP_STRIDE = GP_WORDS + 1;
+__device__ __forceinline__ void gp_store(uint32_t* L, int i, const GPart& p) {
+  const uint32_t* w = (const uint32_t*)&p;
+#pragma unroll
+  for (int k = 0; k < GP_WORDS; ++k) L[i * GP_STRIDE + k] = w[k];
+}
+__device__ __forceinline__ GPart gp_load(const uint32_t* L, int i) {
+  GPart p;
+  uint32_t* w = (uint32_t*)&p;
+#pragma unroll
+  for (int k = 0; k < GP_WORDS; ++k) w[k] = L[i * GP_STRIDE + k];
+  return p;
+}
 __global__ void __launch_bounds__(FOLD_THREADS) k_agg_global_final(GPart* __restrict__ partials, int nparts,
                                                                    GPart* __restrict__ host_out,
                                                                    unsigned long long* __restrict__ host_flag) {
-  __shared__ GPart L[FOLD_THREADS];
+  __shared__ uint32_t L[FOLD_THREADS * GP_STRIDE];
   const int t = threadIdx.x;
   GPart p;
   gpart_init(p);
@@ -388,29 +412,29 @@ __global__ void __launch_bounds__(FOLD_THREADS) k_agg_global_final(GPart* __rest
     gpart_merge(p, a);
     if (two) gpart_merge(p, b);
   }
-  L[t] = p;
+  gp_store(L, t, p);
   __syncthreads();
   for (int h = FOLD_THREADS / 2; h >= 64; h >>= 1) {
     if (t < h) {
-      GPart a = L[t];
-      gpart_merge(a, L[t + h]);
-      L[t] = a;
+      GPart a = gp_load(L, t);
+      gpart_merge(a, gp_load(L, t + h));
+      gp_store(L, t, a);
     }
     __syncthreads();
   }
   if (t < 64) {
     for (int h = 32; h >= 1; h >>= 1) {
       if (t < h) {
-        GPart a = L[t];
-        gpart_merge(a, L[t + h]);
-        L[t] = a;
+        GPart a = gp_load(L, t);
+        gpart_merge(a, gp_load(L, t + h));
+        gp_store(L, t, a);
       }
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
       __builtin_amdgcn_wave_barrier();
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     }
     if (t == 0) {
-      const GPart b = L[0];
+      const GPart b = gp_load(L, 0);
       partials[nparts] = b;
       if (host_out) *host_out = b;
       if (host_flag) __hip_atomic_store(host_flag, 1ull, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
