@@ -1031,23 +1031,30 @@ __device__ __forceinline__ void walk_record_bm(const D& d, const BM& bm, int64_t
   for (; t < A.npf; ++t) A.meta[A.slot[A.pf[t]]][r] = 0;  // fields the line does not reach read as "" (K:263)
 }
 
-// One wave's block of 64 consecutive lines: each lane's line, the block's byte span (16-byte aligned
-// base) and whether it fits the LDS stage.
+// One wave's block of 64 consecutive lines: each lane's line (line_ends: the loads only), then the
+// block's byte span (16-byte aligned base) and whether it fits the LDS stage (line_block: the
+// shuffles, which wait for those loads — and, memory operations completing in order, for every
+// load issued before them).
 struct LineBlock {
   int64_t s, e, base, span;
   bool live, staged;
 };
-__device__ __forceinline__ LineBlock line_block(const int64_t* __restrict__ ends, int64_t nlines, int64_t l0, int lane) {
+__device__ __forceinline__ LineBlock line_ends(const int64_t* __restrict__ ends, int64_t nlines, int64_t l0, int lane) {
   LineBlock b;
   const int64_t li = l0 + lane;
   b.live = li < nlines;
   b.s = b.live ? line_start(ends, li) : 0;
   b.e = b.live ? ends[li] : 0;
+  b.base = 0;
+  b.span = 0;
+  b.staged = false;
+  return b;
+}
+__device__ __forceinline__ void line_block(LineBlock& b, int64_t nlines, int64_t l0) {
   const int last = (int)(min(l0 + 63, nlines - 1) - l0);
   b.base = __shfl(b.s, 0) & ~(int64_t)15;
   b.span = __shfl(b.e, last) - b.base;
   b.staged = b.span <= LB_BYTES;
-  return b;
 }
 
 constexpr int LB_WORDS = LB_BYTES / 64 + 2;  // bitmap words covering a staged block
@@ -1063,10 +1070,10 @@ struct GBits {
 
 // The fast path's line walk (a file without '"' or '\r'): one wave per 64 consecutive lines, their
 // bytes and delimiter-bitmap words staged in LDS, the fields located on the bitmap (walk_record_bm)
-// instead of classifying the bytes again. Software-pipelined: while a block is walked out of LDS,
-// the next block's bytes and bitmap words are in flight into registers, and the line ends of the
-// block after it are read. (A lane per line reading HBM directly took 243 us on tripdata; staged
-// without the pipeline 147 us.)
+// instead of classifying the bytes again. Software-pipelined: while a block is walked out of LDS
+// (no global loads in the walk), the next block's bytes and bitmap words are in flight into
+// registers, and the line ends of the block after it are read. (A lane per line reading HBM
+// directly took 243 us on tripdata; staged without the pipeline 147 us.)
 __global__ void __launch_bounds__(256) k_csv_lines_bm(const uint8_t* __restrict__ data, int64_t nbytes,
                                                       const uint64_t* __restrict__ dbm, const int64_t* __restrict__ ends,
                                                       int64_t nlines, int64_t first, FieldArgs Ag, int32_t nproj,
@@ -1098,11 +1105,12 @@ __global__ void __launch_bounds__(256) k_csv_lines_bm(const uint8_t* __restrict_
       bw[k] = (lane + 64 * k < LB_WORDS && wi < nwords) ? dbm[wi] : 0ull;
     }
   };
-  LineBlock cur = line_block(ends, nlines, l0, lane);
+  LineBlock cur = line_ends(ends, nlines, l0, lane);
+  line_block(cur, nlines, l0);
   fetch(cur);
-  LineBlock nxt = cur;
+  LineBlock nxt = cur;  // only its line ends are loaded here (line_block: next iteration)
   nxt.live = false;
-  if (l0 + wstride < nlines) nxt = line_block(ends, nlines, l0 + wstride, lane);
+  if (l0 + wstride < nlines) nxt = line_ends(ends, nlines, l0 + wstride, lane);
   for (; l0 < nlines; l0 += wstride) {
     if (cur.staged) {
 #pragma unroll
@@ -1119,10 +1127,13 @@ __global__ void __launch_bounds__(256) k_csv_lines_bm(const uint8_t* __restrict_
     }
     // the next block's bytes in flight, and the line ends of the one after it
     const bool more = l0 + wstride < nlines;
-    if (more) fetch(nxt);
+    if (more) {
+      line_block(nxt, nlines, l0 + wstride);  // (its line ends came with the previous block's bytes)
+      fetch(nxt);
+    }
     LineBlock nn = nxt;
     nn.live = false;
-    if (l0 + 2 * wstride < nlines) nn = line_block(ends, nlines, l0 + 2 * wstride, lane);
+    if (l0 + 2 * wstride < nlines) nn = line_ends(ends, nlines, l0 + 2 * wstride, lane);
     const int64_t li = l0 + lane, s = cur.s, e = cur.e;
     if (cur.live) {
       bool keep = false;
