@@ -377,68 +377,33 @@ __global__ void __launch_bounds__(256) k_agg_global_fx(const int64_t* __restrict
 // host_out (optional): pinned host memory that also receives the result, so the caller reads it
 // after a stream sync with no device-to-host copy launch.
 // host_flag (optional): set once host_out is written, for a host polling it (release, system scope).
-// Fixed-order fold of the workgroups' partials: 1024 threads, thread t folds partials t, t + 1024,
-// ... (C3's 2048 partials: two loads in flight per thread, one round trip to the other XCDs' L2s
-// instead of four), then a tree in LDS (1024 partials x 128 B) with block barriers down to one
-// wave and wave barriers below. (Round 5: 256 threads in four dependent rounds and a shuffle tree
-// per wave took 7.9 us.)
-// The LDS copies are padded to 33 dwords: at the struct's 32-dword stride every lane of a wave hit
-// the same two banks (the unpadded tree took 19 us).
-constexpr int FOLD_THREADS = 1024, GP_WORDS = sizeof(GPart) / 4, GP_STRIDE = GP_WORDS + 1;
-__device__ __forceinline__ void gp_store(uint32_t* L, int i, const GPart& p) {
-  const uint32_t* w = (const uint32_t*)&p;
-#pragma unroll
-  for (int k = 0; k < GP_WORDS; ++k) L[i * GP_STRIDE + k] = w[k];
-}
-__device__ __forceinline__ GPart gp_load(const uint32_t* L, int i) {
-  GPart p;
-  uint32_t* w = (uint32_t*)&p;
-#pragma unroll
-  for (int k = 0; k < GP_WORDS; ++k) w[k] = L[i * GP_STRIDE + k];
-  return p;
-}
-__global__ void __launch_bounds__(FOLD_THREADS) k_agg_global_final(GPart* __restrict__ partials, int nparts,
-                                                                   GPart* __restrict__ host_out,
-                                                                   unsigned long long* __restrict__ host_flag) {
-  __shared__ uint32_t L[FOLD_THREADS * GP_STRIDE];
-  const int t = threadIdx.x;
+// (Round 6 A/B: 1024 threads with one load round and an LDS tree took 16.5-19 us, padded or not;
+// docs/experiments.md.)
+__global__ void __launch_bounds__(256) k_agg_global_final(GPart* __restrict__ partials, int nparts,
+                                                          GPart* __restrict__ host_out,
+                                                          unsigned long long* __restrict__ host_flag) {
+  // Fixed-order reduction: thread t folds partials t, t+256, ... (two loads in flight per round);
+  // then a fixed wave / block tree. (1024 threads took 15 us: sixteen waves' shuffle trees on one CU.)
   GPart p;
   gpart_init(p);
-  for (int i = t; i < nparts; i += 2 * FOLD_THREADS) {
+  for (int i = threadIdx.x; i < nparts; i += 512) {
     const GPart a = partials[i];
     GPart b;
-    const bool two = i + FOLD_THREADS < nparts;
-    if (two) b = partials[i + FOLD_THREADS];
+    const bool two = i + 256 < nparts;
+    if (two) b = partials[i + 256];
     gpart_merge(p, a);
     if (two) gpart_merge(p, b);
   }
-  gp_store(L, t, p);
+  gpart_wave_reduce(p);
+  __shared__ GPart wp[4];
+  if ((threadIdx.x & 63) == 0) wp[threadIdx.x >> 6] = p;
   __syncthreads();
-  for (int h = FOLD_THREADS / 2; h >= 64; h >>= 1) {
-    if (t < h) {
-      GPart a = gp_load(L, t);
-      gpart_merge(a, gp_load(L, t + h));
-      gp_store(L, t, a);
-    }
-    __syncthreads();
-  }
-  if (t < 64) {
-    for (int h = 32; h >= 1; h >>= 1) {
-      if (t < h) {
-        GPart a = gp_load(L, t);
-        gpart_merge(a, gp_load(L, t + h));
-        gp_store(L, t, a);
-      }
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-      __builtin_amdgcn_wave_barrier();
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    }
-    if (t == 0) {
-      const GPart b = gp_load(L, 0);
-      partials[nparts] = b;
-      if (host_out) *host_out = b;
-      if (host_flag) __hip_atomic_store(host_flag, 1ull, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
-    }
+  if (threadIdx.x == 0) {
+    GPart b = wp[0];
+    for (int w = 1; w < 4; ++w) gpart_merge(b, wp[w]);
+    partials[nparts] = b;
+    if (host_out) *host_out = b;
+    if (host_flag) __hip_atomic_store(host_flag, 1ull, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
   }
 }
 
@@ -478,8 +443,8 @@ using namespace qe;
 namespace qe {
 
 // Summation depth of the fold of n partials by k_agg_global_final: thread t folds partials t,
-// t + 1024, ..., then the ten levels of the LDS tree (and a margin).
-static int64_t final_fold_depth(int64_t n) { return (int64_t)div_up((uint64_t)n, FOLD_THREADS) + 10 + 2; }
+// t + 256, ... (two merges per round), then the wave tree (6) and the block's four waves (3).
+static int64_t final_fold_depth(int64_t n) { return 2 * (int64_t)div_up((uint64_t)n, 512) + 2 + 6 + 3; }
 
 // The column's partial, reduced on the device into *result (a GPart in scratch); *depth its
 // summation depth (sum_certified): a lane's chain of rows, the dense kernel's fold of its eight
@@ -521,7 +486,7 @@ static int agg_global_partial(qe_ctx* ctx, const qe_column* col, const qe_column
     hipLaunchKernelGGL(k_agg_global<false>, dim3((unsigned)blocks), dim3(256), 0, ctx->stream,
                        (const int64_t*)col->values, col->validity, mv, ml, n, parts);
   QE_TRY(launch_check("k_agg_global"));
-  hipLaunchKernelGGL(k_agg_global_final, dim3(1), dim3(FOLD_THREADS), 0, ctx->stream, parts, (int)blocks, host_out, host_flag);
+  hipLaunchKernelGGL(k_agg_global_final, dim3(1), dim3(256), 0, ctx->stream, parts, (int)blocks, host_out, host_flag);
   QE_TRY(launch_check("k_agg_global_final"));
   *result = parts + blocks;
   return QE_OK;
@@ -666,7 +631,7 @@ extern "C" int qe_agg_global_merge(qe_ctx* ctx, int32_t type, const void* partia
   // fixed-order fold: the same partials give the same bits on every rank
   void* h;
   QE_TRY(ctx_pinned(ctx, sizeof(GPart), &h));
-  hipLaunchKernelGGL(k_agg_global_final, dim3(1), dim3(FOLD_THREADS), 0, ctx->stream, parts, (int)n, (GPart*)h,
+  hipLaunchKernelGGL(k_agg_global_final, dim3(1), dim3(256), 0, ctx->stream, parts, (int)n, (GPart*)h,
                      (unsigned long long*)nullptr);
   QE_TRY(launch_check("k_agg_global_final"));
   bool certified = true;

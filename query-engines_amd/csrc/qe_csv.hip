@@ -1000,16 +1000,16 @@ __device__ __forceinline__ int select64(uint64_t w, int k) {
 }
 
 // walk_record_unquoted on the delimiter bitmap (one bit per byte, k_csv_classify) instead of the
-// line's bytes: a 64-byte stretch of the line is one 8-byte word (bm(i): bitmap word i, bytes
-// [64 i, 64 i + 64)), a popcount and, for the projected fields ending there, a bit select. Bytes are
-// touched only for the projected values (trim, 16-byte stage).
-template <typename D, typename BM>
-__device__ __forceinline__ void walk_record_bm(const D& d, const BM& bm, int64_t s, int64_t e, const FieldArgs& A,
-                                               int64_t r) {
+// line's bytes: a 64-byte stretch of the line is one 8-byte load (the wave's lines are consecutive,
+// so its lanes share a few cached bitmap lines), a popcount and, for the projected fields ending
+// there, a bit select. Bytes are touched only for the projected values (trim, 16-byte stage).
+template <typename D>
+__device__ __forceinline__ void walk_record_bm(const D& d, const uint64_t* __restrict__ dbm, int64_t s, int64_t e,
+                                               const FieldArgs& A, int64_t r) {
   int f = 0, t = 0;
   int64_t fs = s;
   for (int64_t wb = s & ~(int64_t)63; wb < e && t < A.npf; wb += 64) {
-    uint64_t w = bm(wb >> 6);
+    uint64_t w = dbm[wb >> 6];
     if (wb < s) w &= ~0ull << (s - wb);
     if (e - wb < 64) w &= (1ull << (e - wb)) - 1;
     const int n = __popcll(w);
@@ -1031,129 +1031,61 @@ __device__ __forceinline__ void walk_record_bm(const D& d, const BM& bm, int64_t
   for (; t < A.npf; ++t) A.meta[A.slot[A.pf[t]]][r] = 0;  // fields the line does not reach read as "" (K:263)
 }
 
-// One wave's block of 64 consecutive lines: each lane's line (line_ends: the loads only), then the
-// block's byte span (16-byte aligned base) and whether it fits the LDS stage (line_block: the
-// shuffles, which wait for those loads — and, memory operations completing in order, for every
-// load issued before them).
-struct LineBlock {
-  int64_t s, e, base, span;
-  bool live, staged;
-};
-__device__ __forceinline__ LineBlock line_ends(const int64_t* __restrict__ ends, int64_t nlines, int64_t l0, int lane) {
-  LineBlock b;
-  const int64_t li = l0 + lane;
-  b.live = li < nlines;
-  b.s = b.live ? line_start(ends, li) : 0;
-  b.e = b.live ? ends[li] : 0;
-  b.base = 0;
-  b.span = 0;
-  b.staged = false;
-  return b;
-}
-__device__ __forceinline__ void line_block(LineBlock& b, int64_t nlines, int64_t l0) {
-  const int last = (int)(min(l0 + 63, nlines - 1) - l0);
-  b.base = __shfl(b.s, 0) & ~(int64_t)15;
-  b.span = __shfl(b.e, last) - b.base;
-  b.staged = b.span <= LB_BYTES;
-}
-
-constexpr int LB_WORDS = LB_BYTES / 64 + 2;  // bitmap words covering a staged block
-struct LBits {
-  const uint64_t* W;  // LDS copy of bitmap words [w0, w0 + LB_WORDS)
-  int64_t w0;
-  __device__ __forceinline__ uint64_t operator()(int64_t i) const { return W[i - w0]; }
-};
-struct GBits {
-  const uint64_t* W;
-  __device__ __forceinline__ uint64_t operator()(int64_t i) const { return W[i]; }
-};
-
-// The fast path's line walk (a file without '"' or '\r'): one wave per 64 consecutive lines, their
-// bytes and delimiter-bitmap words staged in LDS, the fields located on the bitmap (walk_record_bm)
-// instead of classifying the bytes again. Software-pipelined: while a block is walked out of LDS
-// (no global loads in the walk), the next block's bytes and bitmap words are in flight into
-// registers, and the line ends of the block after it are read. (A lane per line reading HBM
-// directly took 243 us on tripdata; staged without the pipeline 147 us.)
+// The fast path's line walk (a file without '"' or '\r'): k_csv_lines' shape — one wave per 64
+// consecutive lines, their bytes staged in LDS with coalesced 16-byte loads — with the fields
+// located on the delimiter bitmap (walk_record_bm) instead of classifying the bytes again. (A lane
+// per line reading the bytes from HBM directly took 243 us on tripdata against 169 us staged.)
 __global__ void __launch_bounds__(256) k_csv_lines_bm(const uint8_t* __restrict__ data, int64_t nbytes,
                                                       const uint64_t* __restrict__ dbm, const int64_t* __restrict__ ends,
                                                       int64_t nlines, int64_t first, FieldArgs Ag, int32_t nproj,
                                                       unsigned long long* __restrict__ nskip) {
   __shared__ __attribute__((aligned(16))) uint8_t lds[4][LB_BYTES];
-  __shared__ uint64_t ldw[4][LB_WORDS];
   __shared__ FieldArgs A;
   stage_args(A, Ag);
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   uint8_t* L = lds[wid];
-  uint64_t* LW = ldw[wid];
-  const int64_t nwords = (nbytes + 63) >> 6;
   const int64_t wstride = (int64_t)gridDim.x * 4 * 64;
-  int64_t l0 = ((int64_t)blockIdx.x * 4 + wid) * 64;
-  if (l0 >= nlines) return;
-  Lane16 v[LB_BYTES / 1024];
-  uint64_t bw[3];
-  auto fetch = [&](const LineBlock& b) {  // the block's bytes and bitmap words into registers
-    if (!b.staged) return;
-#pragma unroll
-    for (int k = 0; k < LB_BYTES / 1024; ++k) {
-      const int64_t off = (int64_t)k * 1024 + lane * 16;
-      if (off < b.span) v[k] = load16(data, nbytes, b.base + off);
-    }
-    const int64_t w0 = b.base >> 6;
-#pragma unroll
-    for (int k = 0; k < 3; ++k) {
-      const int64_t wi = w0 + lane + 64 * k;
-      bw[k] = (lane + 64 * k < LB_WORDS && wi < nwords) ? dbm[wi] : 0ull;
-    }
-  };
-  LineBlock cur = line_ends(ends, nlines, l0, lane);
-  line_block(cur, nlines, l0);
-  fetch(cur);
-  LineBlock nxt = cur;  // only its line ends are loaded here (line_block: next iteration)
-  nxt.live = false;
-  if (l0 + wstride < nlines) nxt = line_ends(ends, nlines, l0 + wstride, lane);
-  for (; l0 < nlines; l0 += wstride) {
-    if (cur.staged) {
+  for (int64_t l0 = ((int64_t)blockIdx.x * 4 + wid) * 64; l0 < nlines; l0 += wstride) {
+    const int64_t li = l0 + lane;
+    const bool live = li < nlines;
+    const int64_t s = live ? line_start(ends, li) : 0, e = live ? ends[li] : 0;
+    const int last = (int)(min(l0 + 63, nlines - 1) - l0);
+    const int64_t base = __shfl(s, 0) & ~(int64_t)15;
+    const int64_t span = __shfl(e, last) - base;
+    const bool staged = span <= LB_BYTES;
+    if (staged) {  // all of the block's loads in flight at once, then into LDS
+      Lane16 v[LB_BYTES / 1024];
 #pragma unroll
       for (int k = 0; k < LB_BYTES / 1024; ++k) {
         const int64_t off = (int64_t)k * 1024 + lane * 16;
-        if (off < cur.span) *(uint4*)(L + off) = make_uint4(v[k].w[0], v[k].w[1], v[k].w[2], v[k].w[3]);
+        if (off < span) v[k] = load16(data, nbytes, base + off);
       }
 #pragma unroll
-      for (int k = 0; k < 3; ++k)
-        if (lane + 64 * k < LB_WORDS) LW[lane + 64 * k] = bw[k];
+      for (int k = 0; k < LB_BYTES / 1024; ++k) {
+        const int64_t off = (int64_t)k * 1024 + lane * 16;
+        if (off < span) *(uint4*)(L + off) = make_uint4(v[k].w[0], v[k].w[1], v[k].w[2], v[k].w[3]);
+      }
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
       __builtin_amdgcn_wave_barrier();
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     }
-    // the next block's bytes in flight, and the line ends of the one after it
-    const bool more = l0 + wstride < nlines;
-    if (more) {
-      line_block(nxt, nlines, l0 + wstride);  // (its line ends came with the previous block's bytes)
-      fetch(nxt);
-    }
-    LineBlock nn = nxt;
-    nn.live = false;
-    if (l0 + 2 * wstride < nlines) nn = line_ends(ends, nlines, l0 + 2 * wstride, lane);
-    const int64_t li = l0 + lane, s = cur.s, e = cur.e;
-    if (cur.live) {
+    if (live) {
       bool keep = false;
-      if (cur.staged) {
-        const LBytes d{L, cur.base};
+      if (staged) {
+        const LBytes d{L, base};
         if (s < e && d[s] != '#')
           for (int64_t p = s; p < e && !keep; ++p) keep = d[p] > 0x20;
-        if (keep && li >= first) walk_record_bm(d, LBits{LW, cur.base >> 6}, s, e, A, li - first);
+        if (keep && li >= first) walk_record_bm(d, dbm, s, e, A, li - first);
       } else {
         const GBytes d{data, nbytes};
         if (s < e && d[s] != '#')
           for (int64_t p = s; p < e && !keep; ++p) keep = d[p] > 0x20;
-        if (keep && li >= first) walk_record_bm(d, GBits{dbm}, s, e, A, li - first);
+        if (keep && li >= first) walk_record_bm(d, dbm, s, e, A, li - first);
       }
       if (!keep) atomicAdd(nskip, 1ull);
     }
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");  // the block's LDS is rewritten next
     __builtin_amdgcn_wave_barrier();
-    cur = nxt;
-    nxt = nn;
   }
 }
 
