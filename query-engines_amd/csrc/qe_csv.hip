@@ -395,25 +395,7 @@ __global__ void __launch_bounds__(256) k_csv_classify(const uint8_t* __restrict_
   uint32_t qr = 0xFFFFFFFFu;  // AND of the '"' / '\r' tests: a clear bit 7 = one was seen
   int cnt = 0;
   int64_t last = -1;
-  Lane16 vq[4];
-  for (int step = 0; step < SEG / 1024; ++step) {
-    const int64_t row0 = base + step * 1024;
-    if (row0 >= nbytes) break;
-    const int64_t pos = row0 + lane * 16;
-    if ((step & 3) == 0) {  // 4 loads in flight per lane: this step and the next three
-#pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        const int64_t pu = pos + u * 1024;
-        vq[u] = pu < nbytes ? load16(data, nbytes, pu) : Lane16{{0, 0, 0, 0}};
-      }
-    }
-    Lane16 v;
-    switch (step & 3) {  // constant indices keep vq in registers
-      case 0: v = vq[0]; break;
-      case 1: v = vq[1]; break;
-      case 2: v = vq[2]; break;
-      default: v = vq[3]; break;
-    }
+  auto step_bytes = [&](const Lane16& v, int64_t pos) {
     uint32_t sn[4], sd[4], t[4], hi = 0;
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
@@ -439,6 +421,47 @@ __global__ void __launch_bounds__(256) k_csv_classify(const uint8_t* __restrict_
     if (pos < nbytes) {
       nlbm[pos >> 4] = (uint16_t)nl;
       dbm[pos >> 4] = (uint16_t)dl;
+    }
+  };
+  if (base + SEG <= nbytes) {
+    // a whole segment inside the file: no bounds checks, eight 16-byte loads in flight per lane
+    // (the checked form below issued four, each under a branch)
+#pragma unroll
+    for (int g = 0; g < SEG / 1024 / 8; ++g) {
+      Lane16 v8[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+        const u32x4 x = __builtin_nontemporal_load((const u32x4*)(data + base + (g * 8 + u) * 1024 + lane * 16));
+        v8[u].w[0] = x.x;
+        v8[u].w[1] = x.y;
+        v8[u].w[2] = x.z;
+        v8[u].w[3] = x.w;
+      }
+#pragma unroll
+      for (int u = 0; u < 8; ++u) step_bytes(v8[u], base + (g * 8 + u) * 1024 + lane * 16);
+    }
+  } else {
+    Lane16 vq[4];
+    for (int step = 0; step < SEG / 1024; ++step) {
+      const int64_t row0 = base + step * 1024;
+      if (row0 >= nbytes) break;
+      const int64_t pos = row0 + lane * 16;
+      if ((step & 3) == 0) {  // 4 loads in flight per lane: this step and the next three
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          const int64_t pu = pos + u * 1024;
+          vq[u] = pu < nbytes ? load16(data, nbytes, pu) : Lane16{{0, 0, 0, 0}};
+        }
+      }
+      Lane16 v;
+      switch (step & 3) {  // constant indices keep vq in registers
+        case 0: v = vq[0]; break;
+        case 1: v = vq[1]; break;
+        case 2: v = vq[2]; break;
+        default: v = vq[3]; break;
+      }
+      step_bytes(v, pos);
     }
   }
   for (int d = 32; d >= 1; d >>= 1) {

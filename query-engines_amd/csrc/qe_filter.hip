@@ -96,11 +96,12 @@ __device__ __forceinline__ int64_t tile_scan_store(const int64_t (&v)[GS_PER], i
   return all;
 }
 
-// One block, any n (writes the total to out[n]): KS_TILES tiles' loads are issued before the first
-// of them is scanned, so up to KS_TILES tiles the block waits for memory once.
+// One block, any n (writes the total to out[n], and to *total2 when given): KS_TILES tiles' loads
+// are issued before the first of them is scanned, so up to KS_TILES tiles the block waits for
+// memory once.
 constexpr int KS_TILES = 1;
 __global__ void __launch_bounds__(1024) k_scan(const int64_t* __restrict__ in, int64_t* __restrict__ out,
-                                               int64_t n) {
+                                               int64_t n, int64_t* __restrict__ total2 = nullptr) {
   __shared__ int64_t wsum[16];
   int64_t carry = 0;
   for (int64_t g0 = 0; g0 < n; g0 += KS_TILES * GS_TILE) {
@@ -111,7 +112,10 @@ __global__ void __launch_bounds__(1024) k_scan(const int64_t* __restrict__ in, i
     for (int t = 0; t < KS_TILES; ++t)
       if (g0 + t * GS_TILE < n) carry += tile_scan_store(v[t], out, n, g0 + t * GS_TILE, carry, wsum);
   }
-  if (threadIdx.x == 0) out[n] = carry;
+  if (threadIdx.x == 0) {
+    out[n] = carry;
+    if (total2) *total2 = carry;
+  }
 }
 
 __global__ void __launch_bounds__(GS_THREADS) k_scan_reduce(const int64_t* __restrict__ in, int64_t n,
@@ -143,7 +147,7 @@ __global__ void __launch_bounds__(GS_THREADS) k_scan_apply(const int64_t* __rest
 
 int exclusive_scan_i64(qe_ctx* ctx, const int64_t* in, int64_t* out, int64_t n) {
   if (n <= KS_TILES * GS_TILE) {
-    hipLaunchKernelGGL(k_scan, dim3(1), dim3(1024), 0, ctx->stream, in, out, n);
+    hipLaunchKernelGGL(k_scan, dim3(1), dim3(1024), 0, ctx->stream, in, out, n, (int64_t*)nullptr);
     return launch_check("k_scan");
   }
   const int64_t nb = (n + GS_TILE - 1) / GS_TILE;
@@ -162,7 +166,7 @@ int exclusive_scan_i64(qe_ctx* ctx, const int64_t* in, int64_t* out, int64_t n) 
   int64_t* offs = sums + nb + 1;
   hipLaunchKernelGGL(k_scan_reduce, dim3((unsigned)nb), dim3(GS_THREADS), 0, ctx->stream, in, n, sums);
   QE_TRY(launch_check("k_scan_reduce"));
-  hipLaunchKernelGGL(k_scan, dim3(1), dim3(1024), 0, ctx->stream, sums, offs, nb);
+  hipLaunchKernelGGL(k_scan, dim3(1), dim3(1024), 0, ctx->stream, sums, offs, nb, (int64_t*)nullptr);
   QE_TRY(launch_check("k_scan"));
   hipLaunchKernelGGL(k_scan_apply, dim3((unsigned)nb), dim3(GS_THREADS), 0, ctx->stream, in, out, n, offs, nb);
   return launch_check("k_scan_apply");
@@ -368,7 +372,7 @@ struct FilterPlan {
   int64_t* offsets;  // ntiles + 1
 };
 
-static int filter_prepare(qe_ctx* ctx, const qe_column* mask, FilterPlan* fp) {
+static int filter_prepare(qe_ctx* ctx, const qe_column* mask, FilterPlan* fp, int64_t* d_total = nullptr) {
   QE_CHECK(mask && mask->type == QE_TYPE_BOOL, QE_ERR_INVALID_ARG, "mask must be a BOOL column");
   QE_CHECK(mask->values || mask->length == 0, QE_ERR_INVALID_ARG, "null mask values");
   const int64_t n = mask->length;
@@ -379,12 +383,13 @@ static int filter_prepare(qe_ctx* ctx, const qe_column* mask, FilterPlan* fp) {
   fp->offsets = fp->counts + fp->ntiles;
   if (n == 0) {
     QE_HIP(hipMemsetAsync(fp->offsets, 0, 8, ctx->stream));
+    if (d_total) QE_HIP(hipMemsetAsync(d_total, 0, 8, ctx->stream));
     return QE_OK;
   }
   hipLaunchKernelGGL(k_tile_count, dim3((unsigned)fp->ntiles), dim3(FT_THREADS), 0, ctx->stream,
                      (const uint8_t*)mask->values, mask->validity, n, fp->counts);
   QE_TRY(launch_check("k_tile_count"));
-  hipLaunchKernelGGL(k_scan, dim3(1), dim3(1024), 0, ctx->stream, fp->counts, fp->offsets, fp->ntiles);
+  hipLaunchKernelGGL(k_scan, dim3(1), dim3(1024), 0, ctx->stream, fp->counts, fp->offsets, fp->ntiles, d_total);
   return launch_check("k_scan");
 }
 
@@ -501,10 +506,6 @@ int qe_filter_apply(qe_ctx* ctx, const qe_column* mask, const qe_column* inputs,
 
 }  // extern "C"
 
-namespace qe {
-__global__ void k_copy_count(const int64_t* __restrict__ src, int64_t* __restrict__ dst) { *dst = *src; }
-}  // namespace qe
-
 extern "C" int qe_filter_apply_async(qe_ctx* ctx, const qe_column* mask, const qe_column* inputs, int32_t ncols,
                                      qe_column* outs, int64_t* d_count) {
   QE_TRY(ctx_enter(ctx));
@@ -531,7 +532,7 @@ extern "C" int qe_filter_apply_async(qe_ctx* ctx, const qe_column* mask, const q
                              type_width(in.type), 0, nullptr};
   }
   FilterPlan fp;
-  QE_TRY(filter_prepare(ctx, mask, &fp));
+  QE_TRY(filter_prepare(ctx, mask, &fp, d_count));  // (the scan also leaves the count in *d_count)
   for (int i = 0; i < ncols; ++i)
     if (args.cols[i].out_valid && n > 0)
       QE_HIP(hipMemsetAsync(outs[i].validity, 0, (size_t)div_up((uint64_t)n, 32) * 4, ctx->stream));
@@ -539,12 +540,6 @@ extern "C" int qe_filter_apply_async(qe_ctx* ctx, const qe_column* mask, const q
     hipLaunchKernelGGL(k_compact, dim3((unsigned)fp.ntiles), dim3(FT_THREADS), 0, ctx->stream,
                        (const uint8_t*)mask->values, mask->validity, n, fp.offsets, args);
     QE_TRY(launch_check("k_compact"));
-  }
-  if (n > 0) {
-    hipLaunchKernelGGL(k_copy_count, dim3(1), dim3(1), 0, ctx->stream, fp.offsets + fp.ntiles, d_count);
-    QE_TRY(launch_check("k_copy_count"));
-  } else {
-    QE_HIP(hipMemsetAsync(d_count, 0, 8, ctx->stream));
   }
   for (int i = 0; i < ncols; ++i) outs[i].length = n;
   return QE_OK;
