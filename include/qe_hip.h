@@ -451,6 +451,12 @@ int qe_hashagg_finalize(qe_hashagg* agg, qe_column* out_keys, qe_column* out_agg
  * other keys). Exact when the key has dictionary codes; 7 bytes per group while a lone UTF8 key's
  * values have all been at most 7 bytes (no device work then). */
 int qe_hashagg_finalize_sizes(qe_hashagg* agg, int64_t* groups, int64_t* key_bytes);
+/* Without synchronising: *per_group = a bound on the value bytes per group that finalize writes for
+ * UTF8 key `key` (7 while every value of a lone UTF8 key has been at most 7 bytes and is its own
+ * code), or 0 when only qe_hashagg_finalize_sizes can tell. A caller with a bound sizes the key's
+ * output at per_group x its row capacity and calls qe_hashagg_finalize directly (QE_ERR_CAPACITY,
+ * with the group count, if the rows do not suffice). */
+int qe_hashagg_key_bytes_bound(qe_hashagg* agg, int32_t key, int64_t* per_group);
 
 /* Two-phase / multi-GPU aggregate (K:1309-1325 pattern):
  * export the partial groups bucketed by destination partition = hash(key) mod nparts

@@ -777,6 +777,15 @@ int qe_hashagg_finalize_sizes(qe_hashagg* h, int64_t* groups, int64_t* key_bytes
   return QE_OK;
 }
 
+int qe_hashagg_key_bytes_bound(qe_hashagg* h, int32_t key, int64_t* per_group) {
+  QE_CHECK(h && per_group, QE_ERR_INVALID_ARG, "null argument");
+  const HashaggInfo I = hashagg_info(h);
+  Keyed* K = I.keyed;
+  QE_CHECK(K && key >= 0 && key < K->norig, QE_ERR_INVALID_ARG, "no key %d", key);
+  *per_group = K->orig[key] == QE_TYPE_UTF8 && !K->tdict && all_packed(K, key) ? 7 : 0;
+  return QE_OK;
+}
+
 int qe_hashagg_export_keyed_sizes(qe_hashagg* h, int32_t nparts, int64_t* block_bytes) {
   QE_CHECK(h && block_bytes && nparts >= 1, QE_ERR_INVALID_ARG, "bad arguments");
   const HashaggInfo I = hashagg_info(h);

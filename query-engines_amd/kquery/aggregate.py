@@ -274,10 +274,22 @@ class HashAggregateState:
         out = N.C.c_int64(-1)
         stash, self._stash = getattr(self, "_stash", None), None
         if N.TYPE_UTF8 in self.key_types:
-            g = N.C.c_int64()
-            kb = (N.C.c_int64 * max(1, nk))()
-            N.check(N.lib().qe_hashagg_finalize_sizes(self.handle, N.C.byref(g), kb))
-            stash = self._carve_c(max(1, g.value), list(kb))
+            # keys that are their own codes have a per-group byte bound: carve at the last result's
+            # size while the update still runs, and let finalize report a larger count; otherwise
+            # size them first (qe_hashagg_finalize_sizes, which waits for the update)
+            bound = N.C.c_int64()
+            packed = True
+            for k, t in enumerate(self.key_types):
+                if t == N.TYPE_UTF8:
+                    N.check(N.lib().qe_hashagg_key_bytes_bound(self.handle, k, N.C.byref(bound)))
+                    packed = packed and bound.value == 7
+            if packed:
+                stash = self._carve_c(self._out_rows)
+            else:
+                g = N.C.c_int64()
+                kb = (N.C.c_int64 * max(1, nk))()
+                N.check(N.lib().qe_hashagg_finalize_sizes(self.handle, N.C.byref(g), kb))
+                stash = self._carve_c(max(1, g.value), list(kb))
         while True:
             rows, cols, kc, ac = stash if stash is not None else self._carve_c(self._out_rows)
             stash = None

@@ -248,6 +248,7 @@ SIGNATURES = [
     ("qe_hashagg_import_keyed", C.c_int, [_P, _P, C.c_int32, _I64P]),
     ("qe_hashagg_merge", C.c_int, [_P, _P]),
     ("qe_hashagg_bind_key_dict", C.c_int, [_P, C.c_int32, _P]),
+    ("qe_hashagg_key_bytes_bound", C.c_int, [_P, C.c_int32, _I64P]),
     ("qe_hashagg_key_layout", C.c_int, [_P, C.POINTER(C.c_int32), C.POINTER(C.c_int32), C.POINTER(C.c_int32)]),
     ("qe_comm_unique_id", C.c_int, [_P]),
     ("qe_comm_create", C.c_int, [_P, C.c_int32, C.c_int32, _P, C.POINTER(C.c_void_p)]),
