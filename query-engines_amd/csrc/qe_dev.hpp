@@ -422,16 +422,13 @@ __host__ __device__ inline bool fx_needs_ext(qi64 bits) { return (fx_row(bits).s
 // status word; an input for E in RAW form.
 __host__ __device__ inline void fx_row_words(qi64 bits, qu64 w[5]) {
   const FxRow r = fx_row(bits);
-  if (r.st & (FX_HUGE | FX_INEXACT)) {
-    w[0] = (qu64)bits;
-    w[1] = w[2] = w[3] = 0;
-    w[4] = FX_RAW;
-    return;
-  }
+  const bool raw = (r.st & (FX_HUGE | FX_INEXACT)) != 0;  // (selects, not an early return: the
+                                                          // words stay in registers)
 #pragma unroll
   for (int i = 0; i < 4; ++i)
-    w[i] = r.k < 0 ? 0ull : i == r.k ? r.lo : i == r.k + 1 ? r.hi : (i > r.k + 1 && r.neg) ? ~0ull : 0ull;
-  w[4] = r.st;
+    w[i] = raw ? (i == 0 ? (qu64)bits : 0ull)
+               : (r.k < 0 ? 0ull : i == r.k ? r.lo : i == r.k + 1 ? r.hi : (i > r.k + 1 && r.neg) ? ~0ull : 0ull);
+  w[4] = raw ? FX_RAW : r.st;
 }
 
 // Correctly rounded double of (w0..w3 + wraps * 2^256) * 2^-128 (ties to even).
@@ -527,6 +524,29 @@ __host__ __device__ inline void fxe_add_words(qu64* e, int w0, const qu64* v, in
   for (; c && w < FXE_WORDS; ++w) c = fx_xadd<ATOMIC>(&e[w], 1ull) == ~0ull ? 1ull : 0ull;
 }
 
+// Four words in registers (n of them used: 2 or 4) into E at word w0: fxe_add_words with constant
+// indices, so a CHUNK partial's words stay in registers (an array indexed by the loop counter went to
+// scratch memory in every generated kernel).
+template <bool ATOMIC>
+__host__ __device__ inline void fxe_add_words4(qu64* e, int w0, qu64 v0, qu64 v1, qu64 v2, qu64 v3, int n) {
+  qu64 c = 0;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const qu64 vi = i == 0 ? v0 : i == 1 ? v1 : i == 2 ? v2 : v3;
+    if (i < n) {
+      const qu64 t = vi + c;
+      qu64 cb = 0;
+      if (t) {
+        const qu64 old = fx_xadd<ATOMIC>(&e[w0 + i], t);
+        cb = old + t < old ? 1ull : 0ull;
+      }
+      c = (t < vi ? 1ull : 0ull) + cb;
+    }
+  }
+#pragma unroll 1
+  for (int w = w0 + n; c && w < FXE_WORDS; ++w) c = fx_xadd<ATOMIC>(&e[w], 1ull) == ~0ull ? 1ull : 0ull;
+}
+
 // Correctly rounded double (ties to even; IEEE overflow to +-Inf, gradual underflow) of
 // E * 2^-1074 + (W + wraps * 2^256) * 2^-128.
 __host__ __device__ inline double fxe_result(const qu64* e, qu64 w0, qu64 w1, qu64 w2, qu64 w3, qi64 wraps) {
@@ -601,8 +621,7 @@ __host__ __device__ inline void fxe_partial(qu64* e, qu64* st, qu64 w0, qu64 w1,
     fxe_add_value<ATOMIC>(e, (qi64)w0);
   } else {
     const int c = (int)((vst >> 8) & 0xFF);
-    const qu64 v[4] = {w0, w1, w2, w3};
-    if (c < FXE_CHUNKS) fxe_add_words<ATOMIC>(e, 4 * c, v, c == FXE_CHUNKS - 1 ? FXE_WORDS - 4 * c : 4);
+    if (c < FXE_CHUNKS) fxe_add_words4<ATOMIC>(e, 4 * c, w0, w1, w2, w3, c == FXE_CHUNKS - 1 ? FXE_WORDS - 4 * c : 4);
   }
   fx_status<ATOMIC>(st, FX_EXT | (vst & FX_SPECIAL));
 }
@@ -898,8 +917,10 @@ static __device__ QE_FX_OUTLINE void fx_rare_global(const Plan& P, qu32 jmask, q
     const bool mine = (jmask >> a) & 1;
     f[0] = mine ? w[0] : (qu64)acc_identity(acc);
     f[1] = 0;
-    if (acc_has_idx(acc))
+    if (acc_has_idx(acc)) {
+#pragma unroll
       for (int i = 0; i < 4; ++i) f[2 + i] = mine ? w[1 + i] : idx_identity(acc);
+    }
     off += agg_rec_bytes(acc);
   }
 }
