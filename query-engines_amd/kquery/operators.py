@@ -118,6 +118,43 @@ def _alloc_like(c: DeviceColumn, n: int, ctx) -> DeviceColumn:
                         torch.empty(n + 1, dtype=torch.int32, device=dev), ctx)
 
 
+# How SelectionExec compacts non-nullable int64 / fp64 columns: "select_project" (one pass of the
+# select-project kernel with the mask as the selection, then a wait for its row count: C2 10M rows
+# 0.130-0.133 ms per cmp -> compact -> arith chain) or "gather" (count, scan and gather with the
+# count left in HBM and read back at the end, qe_filter_apply_async: 0.148 ms; the form every other
+# fixed-width batch takes).
+SELECTION_COMPACTION = "select_project"
+
+
+def _compact_selproj(batch: RecordBatch, cols, mask: DeviceColumn) -> Optional[RecordBatch]:
+    """The compaction through the select-project kernel (qe_select_project_async with the mask
+    column as the selection and the columns themselves as the outputs: one pass with a decoupled
+    look-back instead of count, scan and gather), then its row count. None: the kernel cannot take
+    the plan."""
+    ctx = mask.ctx
+    n = mask.length
+    spec = N.QeSelectSpec()
+    spec.mask_col = len(cols)
+    spec.nterms = 0
+    spec.nout = len(cols)
+    for i in range(len(cols)):
+        spec.outputs[i].ntokens = 1
+        spec.outputs[i].tokens[0] = N.QeToken(N.TOK_COL, i, N.QeScalar())
+    outs = [DeviceColumn.empty(c.type, n, False, ctx=ctx) for c in cols]
+    cc = (N.QeColumn * (len(cols) + 1))(*([c.as_c() for c in cols] + [mask.as_c()]))
+    oc = (N.QeColumn * len(outs))(*[o.as_c() for o in outs])
+    pending = N.C.c_void_p()
+    st = N.lib().qe_select_project_async(ctx.handle, cc, len(cols) + 1, N.C.byref(spec), oc, N.C.byref(pending))
+    if st == N.QE_ERR_UNSUPPORTED:
+        return None
+    N.check(st)
+    cnt = N.C.c_int64()
+    N.check(N.lib().qe_select_pending_wait(pending, N.C.byref(cnt)))
+    for o in outs:
+        o.length = cnt.value
+    return RecordBatch(batch.schema, outs)
+
+
 def filter_batch(batch: RecordBatch, mask: DeviceColumn) -> RecordBatch:
     """SelectionExec's compaction. Fixed-width columns (at most 8) take the stream-ordered form
     (qe_filter_apply_async): outputs sized by the mask, the selected-row count left in HBM and read
@@ -125,6 +162,12 @@ def filter_batch(batch: RecordBatch, mask: DeviceColumn) -> RecordBatch:
     without a host round trip. UTF8 columns take qe_filter_apply (their byte sizes need the count)."""
     ctx = mask.ctx
     cols = batch.fields
+    if (SELECTION_COMPACTION == "select_project" and 0 < len(cols) < N.MAX_COLS and len(cols) <= N.MAX_AGGS
+            and all(isinstance(c, DeviceColumn) and c.type in (N.TYPE_INT64, N.TYPE_FLOAT64) and not c.nullable
+                    for c in cols)):
+        done = _compact_selproj(batch, cols, mask)
+        if done is not None:
+            return done
     if (0 < len(cols) <= N.MAX_COLS and all(isinstance(c, DeviceColumn) and c.type in N.FIXED_WIDTH for c in cols)):
         import torch
 

@@ -76,7 +76,13 @@ def main():
         sel_rows = out["n"]
         # algorithmic: read a, b (16 B) + write a+b for the selected rows
         report("C2 filter(a>2^19)+project(a+b), 10M int64 (160 MB: fits the 256 MB MALL)", n,
-               16 + 8 * sel_rows / n, ms, selected=sel_rows, path="per-family operators (cmp, count, compact, arith)")
+               16 + 8 * sel_rows / n, ms, selected=sel_rows, path="per-family operators (cmp, compact, arith)")
+        from kquery import operators as ops  # the same chain with the count / scan / gather compaction
+        ops.SELECTION_COMPACTION = "gather"
+        ms_b = timed(run)
+        ops.SELECTION_COMPACTION = "select_project"
+        report("C2 per-family, compaction by count + scan + gather (qe_filter_apply_async)", n,
+               16 + 8 * sel_rows / n, ms_b, selected=out["n"], path="per-family operators (cmp, count, gather, arith)")
         fused = fuse(proj)
         assert type(fused).__name__ == "FusedSelectProjectExec"
 
