@@ -1,8 +1,10 @@
-"""SelectionExec -> ProjectionExec stream-ordered: qe_filter_apply_async leaves
-the selected-row count in HBM, qe_eval_arith_dlen computes only the rows below it, and the count
-comes back once, when a consumer reads a length. Checked per row against numpy on the same seeded
-inputs (bit-exact: int64 wraps, fp64 IEEE, nulls propagate), for empty, full and partial
-selections, nullable inputs, and against qe_filter_apply's synchronous result."""
+"""SelectionExec -> ProjectionExec on device. SelectionExec compacts
+non-nullable int64 / fp64 columns with one select-project pass (the mask column as the selection),
+and every other fixed-width batch stream-ordered: qe_filter_apply_async leaves the selected-row
+count in HBM, qe_eval_arith_dlen computes only the rows below it, and the count comes back once, when
+a consumer reads a length. Both forms are checked per row against numpy on the same seeded inputs
+(bit-exact: int64 wraps, fp64 IEEE, nulls propagate), for empty, full and partial selections,
+nullable inputs, and against qe_filter_apply's synchronous result."""
 import numpy as np
 import pytest
 
