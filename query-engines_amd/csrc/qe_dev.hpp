@@ -41,6 +41,8 @@ typedef unsigned char qu8;
 typedef long long qi64x2 __attribute__((ext_vector_type(2)));
 typedef int qi32x2 __attribute__((ext_vector_type(2)));
 typedef unsigned int qu32x4 __attribute__((ext_vector_type(4)));
+typedef unsigned int qu32x2 __attribute__((ext_vector_type(2)));
+typedef unsigned int qu32x3 __attribute__((ext_vector_type(3)));
 
 constexpr qi64 EMPTY_KEY = (qi64)0x8000000000000000ull;  // LDS/global slot sentinel (INT64_MIN)
 constexpr qi64 PART_EXCL = 1ll << 62;  // partition-aggregate slice flag: the slice holds its whole bucket
@@ -148,7 +150,7 @@ struct Plan {
   // fused aggregate with a compact LDS table (qe_jit.hip compact_*): this many slots of 32-bit keys
   // (and 32-bit MIN / MAX where the input is a bare column), 0 = the regular 2^lds_log2 table
   qi32 lds_compact;
-  // spilling first pass (spill_update): rows with fmix64(key) >> 32 >= mp_keep are spilled as records
+  // spilling first pass (spill_update): rows with spill_hash(key) >= mp_keep are spilled as records
   qu64 mp_keep;
   // select-project: pinned host words the kernel writes its results to ([0] rows written, [1] the
   // persistent look-back's stall flag), so no copy command follows the kernel (null: device only)
@@ -175,6 +177,18 @@ __host__ __device__ inline qu64 fmix64(qu64 k) {
   k *= 0xC4CEB9FE1A85EC53ull;
   k ^= k >> 33;
   return k;
+}
+
+// Kept / spilled split of the spilling pass (Plan.mp_keep): the murmur3 32-bit finaliser over the
+// folded key. Half the multiplies of fmix64's 64-bit ones (this runs for every row of the pass), and
+// independent of lds_hash's buckets, so the kept share spreads over the whole LDS table.
+__device__ inline qu32 spill_hash(qu64 key) {
+  qu32 x = (qu32)key ^ (qu32)(key >> 32) * 0x27D4EB2Fu;
+  x ^= x >> 16;
+  x *= 0x85EBCA6Bu;
+  x ^= x >> 13;
+  x *= 0xC2B2AE35u;
+  return x ^ (x >> 16);
 }
 
 // Cheap slot hash for the per-workgroup LDS table: one 32-bit multiply (Fibonacci hashing).

@@ -2433,6 +2433,13 @@ static int settle_pending(qe_hashagg* h) {
   return st;
 }
 
+// Kept share of the spilling pass in eighths of the kept table's slots (QE_SPILL_LOAD, 4..7, read
+// per call; default 6).
+static int spill_load8() {
+  const char* le = getenv("QE_SPILL_LOAD");
+  return le && *le ? std::max(4, std::min(7, atoi(le))) : 6;
+}
+
 // Two key-hash buckets (groups just beyond one LDS table; QE_MP_SPILL, read per call, 0 = two
 // fused passes): pass 0 of the fused kernel keeps bucket 0 in its LDS tables and appends the other
 // bucket's selected rows as partition records (part_layout, chunk-columnar) in per-wave chunks;
@@ -2459,7 +2466,8 @@ static int spill_update(qe_hashagg* h, Plan& P, size_t lds, int64_t rows, bool* 
   if (tlog2 < 8) return QE_OK;
   std::string ss, sa;
   size_t jl = 0;
-  if (!gen_fused_source(P, P.lds_log2, &ss, &jl, true) || !gen_pagg_source(Q, tlog2, &sa, &jl, true, true)) return QE_OK;
+  // (the spilling pass writes whole records: the aggregation pass reads them record-major)
+  if (!gen_fused_source(P, P.lds_log2, &ss, &jl, true) || !gen_pagg_source(Q, tlog2, &sa, &jl, true, false)) return QE_OK;
   hipFunction_t fs = nullptr, fa = nullptr;
   int bpc = 0, bpc_a = 0;
   const int sblock = fused_block(P.lds_log2);
@@ -2481,13 +2489,11 @@ static int spill_update(qe_hashagg* h, Plan& P, size_t lds, int64_t rows, bool* 
   QE_HIP(hipMemsetAsync(meta, 0, 8, ctx->stream));
   if (L.narrow) QE_HIP(hipMemsetAsync(h->ctl + 7, 0, 8, ctx->stream));
   // kept share: as many groups as one LDS table holds at a 6/8 load, the rest spilled (4096
-  // expected groups of the C4 shape: 75 % kept, half the records of an even split). QE_SPILL_LOAD
-  // (eighths, 4..7, read per call); 1B rows, 4096 / 5000 groups: 5/8 7.27 / 8.12 ms, 6/8 6.56 /
-  // 7.85, 7/8 6.62 / 10.79
-  // (compact kept table: 7/8 by default — it holds ~80 % load and more without the serial probe
-  // loop; 1B rows, 5,500 / 6,500 groups: 5/8 6.29 / 7.12 ms, 6/8 5.75 / 6.48, 7/8 4.16 / 6.41)
-  const char* le = getenv("QE_SPILL_LOAD");
-  const int load8 = le && *le ? std::max(4, std::min(7, atoi(le))) : (P.lds_compact ? 7 : 6);
+  // expected groups of the C4 shape: 75 % kept, half the records of an even split; 1B rows, 4096 /
+  // 5000 groups: 5/8 7.27 / 8.12 ms, 6/8 6.56 / 7.85, 7/8 6.62 / 10.79). The compact kept table
+  // too since round 6's record-major spill (7,000 groups, 1B rows, spilling pass + aggregation
+  // pass: 4/8 5.30 + 3.08 ms, 5/8 5.09 + 1.05, 6/8 4.94 + 0.61, 7/8 5.95 + 0.40)
+  const int load8 = spill_load8();
   const int64_t kept_cap = P.lds_compact ? (int64_t)P.lds_compact : ((int64_t)1 << P.lds_log2);  // kept table's slots
   const double keep = std::min(1.0, (double)(kept_cap * load8 / 8) / (double)std::max<int64_t>(1, h->expected_groups));
   P.mp_keep = (qu64)(keep * 4294967296.0);
@@ -2638,18 +2644,18 @@ static int run_update(qe_hashagg* h, Plan& P) {
       const size_t pbudget = pagg_block() == 1024 ? (size_t)152 * 1024 : HA_LDS_BUDGET;
       while (tl >= 8 && lds_layout_at(h, &Q, tl) > pbudget) --tl;
     }
-    // QE_SPILL_MAXPCT (default 60): the spilled groups (expected groups beyond the kept share, 7/8
-    // of the compact slots) may fill this percentage of the aggregation table; 0 = round 4's rule
-    // (kept share counted at 3/4, half the table: to ~6.7K groups for C4). 1B rows, one box, C4
-    // shape (profiles/r05_spill_reach.jsonl), 7,000 groups: 7.04 ms spilled (60 %) against 7.64 ms
-    // partitioned; 8,192 groups spilled (70 %) 8.71 against 7.62 ms partitioned, so 60 % stops at
-    // ~7.9K groups
+    // QE_SPILL_MAXPCT (default 85): the spilled groups (expected groups beyond the kept share)
+    // may fill this percentage of the aggregation table; 0 = round 4's rule (kept share counted at
+    // 3/4, half the table). 1B rows, one box, C4 shape, record-major spill at a 6/8 kept share:
+    // 7,500 groups 5.97 ms, 8,192 groups (84 % of the aggregation table) 6.82 ms, against 7.63 ms
+    // partitioned at 8,192 (round 5, chunk-columnar spill at 7/8: 7.04 ms at 7,000 groups, 8.71 at
+    // 8,192, so 60 % stopped at ~7.9K groups)
     static const int sp_pct = [] {
       const char* e = getenv("QE_SPILL_MAXPCT");
-      const int v = e && *e ? atoi(e) : 60;
+      const int v = e && *e ? atoi(e) : 85;
       return v >= 10 && v <= 90 ? v : 0;
     }();
-    const int64_t spill_max = sp_pct ? nsl * 7 / 8 + ((int64_t)1 << tl) * sp_pct / 100
+    const int64_t spill_max = sp_pct ? nsl * spill_load8() / 8 + ((int64_t)1 << tl) * sp_pct / 100
                                      : nsl * 3 / 4 + ((int64_t)1 << tl) / 2;
     if (cs_env && nsl >= 512 && tl >= 8 && h->expected_groups <= spill_max) {
       T.lds_compact = (qi32)nsl;

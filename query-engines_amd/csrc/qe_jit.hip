@@ -740,16 +740,16 @@ static void emit_fit_check(const PartLayout& L, const std::string& w, std::ostri
 // Returns false when the plan shape is outside what the generator emits (caller uses the
 // generic kernel). `log2` is the LDS table size chosen for this launch.
 //
-// `spill` (with P.mp_n > 1): rows whose key hash is at or above P.mp_keep (the kept share sized
-// to fill the LDS table) are not dropped but appended as
+// `spill` (with P.mp_n > 1): rows whose spill_hash(key) is at or above P.mp_keep (the kept share
+// sized to fill the LDS table) are not dropped but appended as
 // partition records (part_layout) for one chunked qe_pagg pass afterwards: the columns are read
 // once, and only the spilled rows' records are written and re-read. Each wave fills its own
 // PART_CH-record chunks, claimed from P.part_chunk[0] (one device atomic per 2048 records; one per
 // wave step on a single cursor serialised the kernel: 49 ms at 1B rows); in a step the spilling
-// lanes take consecutive slots (ballot + popcount among the lanes still in the step). Chunk c's
-// fill goes to P.part_chunk[1 + c] (bucket 0), as the chunked scatter leaves it. Records are stored
-// chunk-columnar (word q of a chunk's records together; gen_pagg_source `soa`): a step's spilling
-// lanes then write whole 512-byte runs per word instead of 8 bytes every 24.
+// lanes take consecutive slots (ballot + mbcnt). Chunk c's fill goes to P.part_chunk[1 + c]
+// (bucket 0), as the chunked scatter leaves it. Records are stored whole (record-major, read by
+// gen_pagg_source with `soa` off): one or two vector stores per record instead of one store
+// instruction per word.
 bool compact_acc32(const Plan& P, int j) {
   const DAgg& a = P.aggs[j];
   if (a.acc != ACC_MIN_I && a.acc != ACC_MAX_I) return false;
@@ -793,9 +793,8 @@ bool gen_fused_source(const Plan& P, int log2, std::string* src, size_t* lds_byt
   o << "\nusing namespace qe;\n"
     << "extern \"C\" __global__ void __launch_bounds__(" << fused_block(log2) << ") qe_fused(const Plan P) {\n"
     << "  __shared__ qu32 s_newg;\n  if (threadIdx.x == 0) s_newg = 0;\n";
-  if (spill)
-    o << "  __shared__ qi64 s_spc[16];\n  __shared__ qu32 s_spf[16];\n  qu32 nfit = 0;\n"
-      << "  if (threadIdx.x < 16) { s_spc[threadIdx.x] = -1; s_spf[threadIdx.x] = 0; }\n";
+  if (spill)  // the wave's open record chunk (-1: none) and its fill: wave-uniform registers
+    o << "  qi64 sp_cid = -1;\n  qu32 sp_fill = 0;\n  qu32 nfit = 0;\n";
   if (compact) emit_lds_table_c(P, o, lds_bytes);
   else emit_lds_table(P, o, log2, lds_bytes);
   // exact fp64 SUMs through the per-wave queue when the plan's step loop allows it and it fits
@@ -832,57 +831,96 @@ bool gen_fused_source(const Plan& P, int log2, std::string* src, size_t* lds_byt
       << "    const qi64 r0 = base + 2 * lane;\n";
     emit_col_loads(P, o, ~0u);
   }
-  emit_active_rows(P, o, true, !fxq);
+  // (the spilling pass keeps every lane in the step until its wave-uniform chunk state is updated)
+  emit_active_rows(P, o, true, !fxq && !spill);
   emit_keys(P, o);
   if (spill) {
     const PartLayout L = part_layout(P);
     // per wave: the open record chunk (PART_CH slots claimed from the chunk counter P.part_chunk[0])
-    // and its fill, in LDS so that every lane still in the step sees the current values (the same
-    // state in registers, with every lane running the block, measured 6.40 against 6.19 ms)
+    // and its fill, wave-uniform (scalar registers: a step's spill count is a ballot popcount).
+    // Records are whole (record-major): a step whose records fit the open chunk stores each with
+    // one or two vector stores off the chunk's buffer descriptor (base in scalar registers, a
+    // 32-bit lane offset); a step that opens the next chunk (one in ~PART_CH / spilled-per-step)
+    // takes the general form. Round 5 kept the state in LDS, did 64-bit slot arithmetic per row
+    // and stored records chunk-columnar (one store instruction per record word): 7,000 groups,
+    // 1B rows, 7.37 ms against 6.1 ms now (docs/experiments.md).
+    const int RB = L.bytes();
+    const int wb = L.narrow ? 4 : 8;
+    // the record's words as 16 / 12 / 8 / 4-byte stores: (first word, words) pieces
+    std::vector<std::pair<int, int>> pieces;
+    for (int q = 0; q < L.words;) {
+      const int left = (L.words - q) * wb;
+      const int n = (left >= 16 ? 16 : left >= 12 && L.narrow ? 12 : left >= 8 ? 8 : 4) / wb;
+      pieces.push_back({q, n});
+      q += n;
+    }
+    auto piece_store = [&](int q, int n) {
+      const int bytes = n * wb;
+      o << "            {\n";
+      if (bytes == 4) {
+        o << "              __builtin_amdgcn_raw_buffer_store_b32((qu32)w[" << q << "], cb, off, " << q * wb << ", 0);\n";
+      } else {
+        const int d = bytes / 4;
+        o << "              qu32x" << d << " v;\n";
+        for (int i = 0; i < n; ++i)
+          if (L.narrow)
+            o << "              v[" << i << "] = (qu32)w[" << q + i << "];\n";
+          else
+            o << "              v[" << 2 * i << "] = (qu32)w[" << q + i << "]; v[" << 2 * i + 1 << "] = (qu32)((qu64)w[" << q + i
+              << "] >> 32);\n";
+        o << "              __builtin_amdgcn_raw_buffer_store_b" << bytes * 8 << "(v, cb, off, " << q * wb << ", 0);\n";
+      }
+      o << "            }\n";
+    };
     o << "    qu32 sp = 0;\n"
       << "#pragma unroll\n    for (int r = 0; r < 4; ++r)\n"
-      << "      if (((act >> r) & 1) && (fmix64((qu64)key[r]) >> 32) >= P.mp_keep) sp |= 1u << r;\n"
+      << "      if (((act >> r) & 1) && spill_hash((qu64)key[r]) >= P.mp_keep) sp |= 1u << r;\n"
       << "    act &= ~sp;\n"
       << "    {\n      qu64 bal[4];\n      qu32 tot = 0;\n"
       << "#pragma unroll\n      for (int r = 0; r < 4; ++r) { bal[r] = __ballot((sp >> r) & 1u); tot += (qu32)__popcll(bal[r]); }\n"
-      << "      if (tot) {\n"
-      << "        const int leader = __ffsll((long long)__ballot(1)) - 1;\n"
-      << "        const int wv = threadIdx.x >> 6;\n"
-      << "        const qi64 cid = s_spc[wv];\n"
-      << "        const qu32 fill = s_spf[wv];\n"
-      << "        const qu32 room = cid >= 0 ? (qu32)PART_CH - fill : 0u;\n"
-      << "        qi64 nid = cid;\n"
-      << "        if (tot > room) {\n"
-      << "          qi64 id = 0;\n"
-      << "          if (lane == leader) {\n"
-      << "            if (cid >= 0) P.part_chunk[1 + cid] = PART_CH;\n"
-      << "            id = (qi64)atomicAdd((qu64*)P.part_chunk, 1ull);\n"
-      << "          }\n"
-      << "          nid = __shfl(id, leader);\n"
-      << "        }\n"
-      << "        if (lane == leader) {\n"
-      << "          if (tot > room) { s_spc[wv] = nid; s_spf[wv] = tot - room; } else s_spf[wv] = fill + tot;\n"
-      << "        }\n"
-      << "        const qu64 below = (1ull << lane) - 1;\n"
+      << "      const qu32 room = sp_cid >= 0 ? (qu32)PART_CH - sp_fill : 0u;\n"
+      << "      if (tot && tot <= room) {\n"
+      << "        const __amdgpu_buffer_rsrc_t cb = __builtin_amdgcn_make_buffer_rsrc((void*)(P.part_rec + sp_cid * (PART_CH * "
+      << RB << "ll)), (short)0, (int)(PART_CH * " << RB << "), 0x00020000);\n"
       << "        qu32 kb = 0;\n"
       << "#pragma unroll\n        for (int r = 0; r < 4; ++r) {\n"
       << "          if ((sp >> r) & 1) {\n"
-      << "            const qu32 k = kb + (qu32)__popcll(bal[r] & below);\n"
-      << "            const qu64 pos = k < room ? (qu64)cid * PART_CH + fill + k : (qu64)nid * PART_CH + (k - room);\n"
+      << "            const qu32 k = __builtin_amdgcn_mbcnt_hi((qu32)(bal[r] >> 32), __builtin_amdgcn_mbcnt_lo((qu32)bal[r], kb));\n"
+      << "            const int off = (int)((sp_fill + k) * " << RB << "u);\n"
       << "            qi64 w[" << L.words << "];\n";
     emit_record_words(P, L, ex, "w", o);
     emit_fit_check(L, "w", o);
-    // chunk-columnar: word q of slot `pos` at ((chunk * W + q) * PART_CH + pos % PART_CH) * 8 (4 for
-    // 32-bit words), so the lanes of one row position store consecutive words
+    for (const auto& pc : pieces) piece_store(pc.first, pc.second);
+    o << "          }\n          kb += (qu32)__popcll(bal[r]);\n        }\n"
+      << "        sp_fill += tot;\n"
+      << "      } else if (tot) {\n"
+      << "        const int leader = __ffsll((long long)__ballot(1)) - 1;\n"
+      << "        qi64 id = 0;\n"
+      << "        if (lane == leader) {\n"
+      << "          if (sp_cid >= 0) P.part_chunk[1 + sp_cid] = PART_CH;\n"
+      << "          id = (qi64)atomicAdd((qu64*)P.part_chunk, 1ull);\n"
+      << "        }\n"
+      << "        id = __shfl(id, leader);\n"
+      << "        const qi64 nid = (qi64)(((qu64)__builtin_amdgcn_readfirstlane((qu32)((qu64)id >> 32)) << 32) |\n"
+      << "                                (qu64)__builtin_amdgcn_readfirstlane((qu32)id));\n"
+      << "        qu32 kb = 0;\n"
+      << "#pragma unroll\n        for (int r = 0; r < 4; ++r) {\n"
+      << "          if ((sp >> r) & 1) {\n"
+      << "            const qu32 k = kb + (qu32)__popcll(bal[r] & ((1ull << lane) - 1));\n"
+      << "            const qu64 pos = k < room ? (qu64)sp_cid * PART_CH + sp_fill + k : (qu64)nid * PART_CH + (k - room);\n"
+      << "            qi64 w[" << L.words << "];\n";
+    emit_record_words(P, L, ex, "w", o);
+    emit_fit_check(L, "w", o);
     const char* wt = L.narrow ? "qi32" : "qi64";
-    o << "            " << wt << "* dst = (" << wt << "*)P.part_rec + (pos / PART_CH) * (" << L.words << " * PART_CH) + pos % PART_CH;\n";
-    for (int q = 0; q < L.words; ++q)
-      o << "            dst[" << q << " * PART_CH] = " << (L.narrow ? "(qi32)" : "") << "w[" << q << "];\n";
-    o << "          }\n          kb += (qu32)__popcll(bal[r]);\n        }\n      }\n    }\n"
+    o << "            " << wt << "* const dst = (" << wt << "*)(P.part_rec + pos * " << RB << "ull);\n";
+    for (int q = 0; q < L.words; ++q) o << "            dst[" << q << "] = (" << wt << ")w[" << q << "];\n";
+    o << "          }\n          kb += (qu32)__popcll(bal[r]);\n        }\n"
+      << "        sp_cid = nid;\n        sp_fill = tot - room;\n"
+      << "      }\n    }\n"
       << "    if (act == 0) continue;\n";
   } else if (P.mp_n > 1)
     o << "#pragma unroll\n    for (int r = 0; r < 4; ++r)\n"
-      << "      if (((act >> r) & 1) && (P.mp_pass < 0 ? (fmix64((qu64)key[r]) >> 32) < P.mp_keep\n"
+      << "      if (((act >> r) & 1) && (P.mp_pass < 0 ? spill_hash((qu64)key[r]) < P.mp_keep\n"
       << "                                              : (qu32)__umul64hi(fmix64((qu64)key[r]), (qu64)P.mp_n) != (qu32)P.mp_pass))\n"
       << "        act &= ~(1u << r);\n"
       << "    if (act == 0) continue;\n";
@@ -897,9 +935,8 @@ bool gen_fused_source(const Plan& P, int log2, std::string* src, size_t* lds_byt
     emit_fx_queue_run(P, o, "q_n");
     o << "  }\n";
   }
-  if (spill)  // each wave's open chunk: its fill (a wave's LDS writes are seen by its own later reads)
-    o << "  if ((threadIdx.x & 63) == 0 && s_spc[threadIdx.x >> 6] >= 0)\n"
-      << "    P.part_chunk[1 + s_spc[threadIdx.x >> 6]] = (qi64)s_spf[threadIdx.x >> 6];\n"
+  if (spill)  // each wave's open chunk: its fill
+    o << "  if ((threadIdx.x & 63) == 0 && sp_cid >= 0) P.part_chunk[1 + sp_cid] = (qi64)sp_fill;\n"
       << "  if (nfit) atomicOr(&P.t.ctl[7], 1ull);\n";
   if (compact) emit_flush_c(P, o);
   else emit_flush(P, o);
@@ -977,7 +1014,9 @@ PartLayout part_layout(const Plan& P) {
 static void emit_fit_check(const PartLayout& L, const std::string& w, std::ostringstream& o) {
   if (!L.narrow) return;
   for (int q = 0; q < L.words; ++q)
-    o << "      nfit |= (qu32)(" << w << "[" << q << "] != (qi64)(qi32)" << w << "[" << q << "]);\n";
+    // (nonzero when the high word is not the low word's sign: two ops per word instead of a 64-bit
+    // compare and select)
+    o << "      nfit |= (qu32)((qu64)" << w << "[" << q << "] >> 32) ^ (qu32)((qi32)" << w << "[" << q << "] >> 31);\n";
 }
 
 // Narrow records: chunk value q of a record whose words are `w` (G = 1: one word, G = 2: a pair).

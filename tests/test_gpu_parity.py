@@ -743,8 +743,8 @@ def test_fused_c4_one_pass_large_table(agg_ctx):
 def test_fused_c4_compact_vs_oracle(agg_ctx, groups):
     """Groups just past the regular LDS table: ONE fused pass over a compact table (32-bit keys,
     32-bit MIN / MAX of bare columns, ~6.4K slots in 152 KiB) instead of key-hash passes; past
-    that table (to ~7.9K groups: QE_SPILL_MAXPCT 60), one spilling pass whose kept share stays in
-    the compact table; beyond, the partitioned update."""
+    that table (to ~8.2K groups: a 6/8 kept share plus QE_SPILL_MAXPCT 85 of the aggregation table),
+    one spilling pass whose kept share stays in the compact table; beyond, the partitioned update."""
     from kquery.datasource import C4_COLUMNS, ColumnSpec, generate_column
 
     n, row0 = 2_000_003, 5
@@ -756,7 +756,7 @@ def test_fused_c4_compact_vs_oracle(agg_ctx, groups):
     if agg_ctx.kernel_mode == "jit":
         spec, note = st.last_kernel_kind()
         want = ("compact LDS table" if groups <= 5500 else "multi-pass: 2 buckets (compact kept table)"
-                if groups <= 7500 else "radix-partitioned")
+                if groups <= 8192 else "radix-partitioned")
         assert spec and note.startswith(want), note
     kk, aa = st.finalize()
     k, _ = gen.generate(gen.GEN_MOD, groups, 42, 0, row0, n)
