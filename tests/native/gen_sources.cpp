@@ -148,10 +148,10 @@ static int emit_agg(const char* dir, const char* name, const qe_column* cols, in
     fprintf(stderr, "%s: narrow partition sources not generated\n", name);
     return 1;
   }
-  // 32-bit chunk-columnar records of the spilling pass and their aggregation pass
+  // 32-bit records of the spilling pass and their (record-major) aggregation pass
   std::string k, l;
   P.mp_n = 2;
-  if (!gen_fused_source(P, log2, &k, &lds, true) || !gen_pagg_source(P, log2, &l, &lds, true, true)) {
+  if (!gen_fused_source(P, log2, &k, &lds, true) || !gen_pagg_source(P, log2, &l, &lds, true, false)) {
     fprintf(stderr, "%s: narrow spill sources not generated\n", name);
     return 1;
   }
