@@ -609,8 +609,8 @@ __device__ __forceinline__ void process_step(const Plan& P, char* smem, const Co
   if (P.mp_n > 1) {
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
-      const qu64 hk = fmix64((qu64)key[r]);
-      const bool other = P.mp_pass < 0 ? (hk >> 32) < P.mp_keep : (qu32)__umul64hi(hk, (qu64)P.mp_n) != (qu32)P.mp_pass;
+      const bool other = P.mp_pass < 0 ? spill_hash((qu64)key[r]) < P.mp_keep
+                                        : (qu32)__umul64hi(fmix64((qu64)key[r]), (qu64)P.mp_n) != (qu32)P.mp_pass;
       if (other) act &= ~(1u << r);
     }
     if (act == 0) return;
@@ -2450,7 +2450,9 @@ static int spill_update(qe_hashagg* h, Plan& P, size_t lds, int64_t rows, bool* 
   qe_ctx* ctx = h->ctx;
   *used = false;
   const char* e = getenv("QE_MP_SPILL");
-  if ((e && e[0] == '0') || P.mp_n != 2) return QE_OK;
+  if ((e && e[0] == '0') || P.mp_n < 2) return QE_OK;
+  const int SB = P.mp_n - 1;  // sub-buckets of the spilled share (a power of two, <= 8)
+  if (SB > 8 || (SB & (SB - 1))) return QE_OK;
   P.part_narrow = (!h->part_wide && part_narrow_env()) ? 1 : 0;  // 32-bit record words while values fit
   P.t = h->t;
   const PartLayout L = part_layout(P);
@@ -2476,14 +2478,21 @@ static int spill_update(qe_hashagg* h, Plan& P, size_t lds, int64_t rows, bool* 
   const int64_t waves = (int64_t)div_up((uint64_t)rows, 256);
   const int sgrid = (int)std::max<int64_t>(
       1, std::min<int64_t>((int64_t)ctx->num_cus * std::max(1, bpc), (int64_t)div_up((uint64_t)waves, sblock / 64)));
-  // chunks: the full ones plus one open chunk per wave of the grid
-  const int64_t cmax = (int64_t)div_up((uint64_t)rows, (uint64_t)PART_CH) + (int64_t)sgrid * (sblock / 64) + 1;
+  // chunks: the full ones plus one open chunk per wave of the grid and sub-bucket
+  const int64_t cmax = (int64_t)div_up((uint64_t)rows, (uint64_t)PART_CH) + (int64_t)sgrid * (sblock / 64) * SB + 1;
   QE_TRY(grow_buffer(&h->part_rec, &h->part_rec_bytes, (size_t)cmax * PART_CH * rb, ctx, "spill records"));
-  QE_TRY(grow_buffer(&h->part_cnt, &h->part_cnt_bytes, (size_t)(1 + cmax) * 8 + (size_t)cmax * 4, ctx, "chunk table"));
+  // chunk table: meta (count, then bucket << 32 | fill per chunk), the chunk ids grouped by
+  // sub-bucket, and (SB > 1) the planning counters: records (8 B), chunks, cursor, base per sub-bucket
+  const size_t tbl = ((size_t)(1 + cmax) * 8 + (size_t)cmax * 4 + 7) & ~(size_t)7;
+  QE_TRY(grow_buffer(&h->part_cnt, &h->part_cnt_bytes, tbl + (size_t)SB * 20, ctx, "chunk table"));
   qi64* meta = (qi64*)h->part_cnt;
   qi32* sorted = (qi32*)(meta + 1 + cmax);
-  const int64_t tmax = ctx->num_cus;  // aggregation slices of the spilled bucket
-  QE_TRY(grow_buffer(&h->part_slc, &h->part_slc_bytes, (size_t)(2 + 2 * (tmax + 1)) * 8, ctx, "spill slices"));
+  unsigned long long* prec = (unsigned long long*)((uint8_t*)h->part_cnt + tbl);
+  qu32* pcnt = (qu32*)(prec + SB);
+  qu32* pcur = pcnt + SB;
+  qu32* pbase = pcur + SB;
+  const int64_t tmax = ctx->num_cus;  // aggregation slices of the spilled share (+ one per sub-bucket)
+  QE_TRY(grow_buffer(&h->part_slc, &h->part_slc_bytes, (size_t)(2 + 2 * (tmax + SB)) * 8, ctx, "spill slices"));
   QE_TRY(ensure_defer(h, cmax * PART_CH));  // the aggregation pass's retry bitmaps index record slots
   *used = true;
   QE_HIP(hipMemsetAsync(meta, 0, 8, ctx->stream));
@@ -2532,9 +2541,22 @@ static int spill_update(qe_hashagg* h, Plan& P, size_t lds, int64_t rows, bool* 
     h->jit_note = "multi-pass: 2 buckets, bucket 1 spilled, then re-read (a value outside the 32-bit records)";
     return QE_OK;
   }
-  hipLaunchKernelGGL(k_spill_plan, dim3((unsigned)div_up((uint64_t)cmax, 256)), dim3(256), 0, ctx->stream,
-                     (const qi64*)meta, (qi64)tmax, (qi64*)h->part_slc, sorted);
-  QE_TRY(launch_check("k_spill_plan"));
+  if (SB == 1) {
+    hipLaunchKernelGGL(k_spill_plan, dim3((unsigned)div_up((uint64_t)cmax, 256)), dim3(256), 0, ctx->stream,
+                       (const qi64*)meta, (qi64)tmax, (qi64*)h->part_slc, sorted);
+    QE_TRY(launch_check("k_spill_plan"));
+  } else {  // chunks grouped by sub-bucket and sliced, as after the radix scatter
+    QE_HIP(hipMemsetAsync(prec, 0, (size_t)SB * 20, ctx->stream));
+    const unsigned pg = (unsigned)div_up((uint64_t)cmax, CHUNK_PER_WG);
+    hipLaunchKernelGGL(k_chunk_hist, dim3(pg), dim3(256), 0, ctx->stream, (const qi64*)meta, (qi32)SB, pcnt, prec);
+    QE_TRY(launch_check("k_chunk_hist"));
+    hipLaunchKernelGGL(k_chunk_slices, dim3(1), dim3(1024), 0, ctx->stream, (const qi64*)meta, (qi32)SB, (qi64)tmax,
+                       (const qu32*)pcnt, (const unsigned long long*)prec, (qi64*)h->part_slc, pbase);
+    QE_TRY(launch_check("k_chunk_slices"));
+    hipLaunchKernelGGL(k_chunk_place, dim3(pg), dim3(256), 0, ctx->stream, (const qi64*)meta, (qi32)SB,
+                       (const qu32*)pbase, pcur, sorted);
+    QE_TRY(launch_check("k_chunk_place"));
+  }
   Q.n = cmax * PART_CH;  // record slots (the retry bitmaps index them)
   Q.part_rec = h->part_rec;
   Q.part_chunk = meta;
@@ -2544,14 +2566,14 @@ static int spill_update(qe_hashagg* h, Plan& P, size_t lds, int64_t rows, bool* 
   Q.ovf_cap = h->ovf_cap;
   defer_in = nullptr;
   for (int pass = 0;; ++pass) {
-    QE_TRY(launch_pass(h, Q, lds, fa, (int)(tmax + 1), pass, 1, out_i, defer_in));
+    QE_TRY(launch_pass(h, Q, lds, fa, (int)(tmax + SB), pass, 1, out_i, defer_in));
     bool done = false;
     QE_TRY(settle_pass(h, Q, &out_i, &defer_in, &done));
     if (done) break;
   }
   h->jit_note = std::string("multi-pass: 2 buckets") + (P.lds_compact ? " (compact kept table)" : "") +
-                ", bucket 1 spilled as " + std::to_string(rb) + " B records (" + (L.colmode ? "column" : "value") +
-                (L.narrow ? " words, 32-bit)" : " words)");
+                ", bucket 1 spilled" + (SB > 1 ? " in " + std::to_string(SB) + " sub-buckets" : std::string()) + " as " +
+                std::to_string(rb) + " B records (" + (L.colmode ? "column" : "value") + (L.narrow ? " words, 32-bit)" : " words)");
   return QE_OK;
 }
 
@@ -2644,22 +2666,36 @@ static int run_update(qe_hashagg* h, Plan& P) {
       const size_t pbudget = pagg_block() == 1024 ? (size_t)152 * 1024 : HA_LDS_BUDGET;
       while (tl >= 8 && lds_layout_at(h, &Q, tl) > pbudget) --tl;
     }
-    // QE_SPILL_MAXPCT (default 85): the spilled groups (expected groups beyond the kept share)
-    // may fill this percentage of the aggregation table; 0 = round 4's rule (kept share counted at
-    // 3/4, half the table). 1B rows, one box, C4 shape, record-major spill at a 6/8 kept share:
-    // 7,500 groups 5.97 ms, 8,192 groups (84 % of the aggregation table) 6.82 ms, against 7.63 ms
-    // partitioned at 8,192 (round 5, chunk-columnar spill at 7/8: 7.04 ms at 7,000 groups, 8.71 at
-    // 8,192, so 60 % stopped at ~7.9K groups)
+    // QE_SPILL_MAXPCT (default 70): the spilled groups (expected groups beyond the kept share)
+    // may fill this percentage of each sub-bucket's aggregation table; 0 = round 4's rule (kept
+    // share counted at 3/4, half the table). 1B rows, one box, C4 shape, record-major spill at a
+    // 6/8 kept share: 7,500 groups 5.97 ms, 8,192 groups in one spilled bucket (84 % of its table)
+    // 6.82 ms, against 7.63 ms partitioned at 8,192; two sub-buckets reach ~10.5K groups (11,500
+    // groups at 85 %: 8.63 ms, past the partitioned update's ~8.0). Round 5 (chunk-columnar spill
+    // at 7/8): 7.04 ms at 7,000 groups, 8.71 at 8,192, so 60 % stopped at ~7.9K groups
     static const int sp_pct = [] {
       const char* e = getenv("QE_SPILL_MAXPCT");
-      const int v = e && *e ? atoi(e) : 85;
+      const int v = e && *e ? atoi(e) : 70;
       return v >= 10 && v <= 90 ? v : 0;
     }();
-    const int64_t spill_max = sp_pct ? nsl * spill_load8() / 8 + ((int64_t)1 << tl) * sp_pct / 100
-                                     : nsl * 3 / 4 + ((int64_t)1 << tl) / 2;
+    // the spilled share in SB sub-buckets (spill_hash's low bits), each aggregated by its own
+    // slices: the fewest (1 or 2) whose aggregation tables stay within that percentage
+    // (QE_SPILL_SUBBUCKETS: the most, 1, 2 or 4). 1B rows, one box: 8,192 groups 7.19 ms with
+    // one spilled bucket, 7.07 with two (at 7,000 groups one: 6.24 against 6.55); 9,000 / 10,000
+    // groups in two 7.28 / 7.66 ms, 12,000 / 16,000 in four 8.57 / 9.53, against 8.0–8.2 ms
+    // partitioned on that box
+    static const int sb_max = [] {
+      const char* e = getenv("QE_SPILL_SUBBUCKETS");
+      const int v = e && *e ? atoi(e) : 2;
+      return v == 1 || v == 2 || v == 4 ? v : 2;
+    }();
+    const int64_t kept_share = nsl * spill_load8() / 8, per_sb = ((int64_t)1 << tl) * sp_pct / 100;
+    int sb = 1;
+    while (sp_pct && sb < sb_max && h->expected_groups - kept_share > sb * per_sb) sb *= 2;
+    const int64_t spill_max = sp_pct ? kept_share + sb * per_sb : nsl * 3 / 4 + ((int64_t)1 << tl) / 2;
     if (cs_env && nsl >= 512 && tl >= 8 && h->expected_groups <= spill_max) {
       T.lds_compact = (qi32)nsl;
-      T.mp_n = 2;
+      T.mp_n = 1 + sb;
       T.mp_pass = 0;
       std::string src;
       size_t jl = 0;

@@ -793,8 +793,14 @@ bool gen_fused_source(const Plan& P, int log2, std::string* src, size_t* lds_byt
   o << "\nusing namespace qe;\n"
     << "extern \"C\" __global__ void __launch_bounds__(" << fused_block(log2) << ") qe_fused(const Plan P) {\n"
     << "  __shared__ qu32 s_newg;\n  if (threadIdx.x == 0) s_newg = 0;\n";
-  if (spill)  // the wave's open record chunk (-1: none) and its fill: wave-uniform registers
-    o << "  qi64 sp_cid = -1;\n  qu32 sp_fill = 0;\n  qu32 nfit = 0;\n";
+  // spilled rows go to SB = mp_n - 1 sub-buckets (spill_hash's low bits), each aggregated by its own
+  // slices afterwards; per sub-bucket the wave's open record chunk (-1: none) and its fill, in
+  // wave-uniform registers
+  const int SB = spill ? P.mp_n - 1 : 0;
+  if (spill && (SB & (SB - 1))) return false;  // (a power of two)
+  if (spill)
+    o << "  constexpr int SB = " << SB << ";\n  qi64 sp_cid[SB];\n  qu32 sp_fill[SB];\n"
+      << "#pragma unroll\n  for (int b = 0; b < SB; ++b) { sp_cid[b] = -1; sp_fill[b] = 0; }\n  qu32 nfit = 0;\n";
   if (compact) emit_lds_table_c(P, o, lds_bytes);
   else emit_lds_table(P, o, log2, lds_bytes);
   // exact fp64 SUMs through the per-wave queue when the plan's step loop allows it and it fits
@@ -872,32 +878,34 @@ bool gen_fused_source(const Plan& P, int log2, std::string* src, size_t* lds_byt
       }
       o << "            }\n";
     };
-    o << "    qu32 sp = 0;\n"
-      << "#pragma unroll\n    for (int r = 0; r < 4; ++r)\n"
-      << "      if (((act >> r) & 1) && spill_hash((qu64)key[r]) >= P.mp_keep) sp |= 1u << r;\n"
+    o << "    qu32 sp = 0, sbk[4] = {0, 0, 0, 0};\n"
+      << "#pragma unroll\n    for (int r = 0; r < 4; ++r) {\n"
+      << "      const qu32 hs = spill_hash((qu64)key[r]);\n"
+      << "      if (((act >> r) & 1) && hs >= P.mp_keep) sp |= 1u << r;\n"
+      << "      sbk[r] = hs & (qu32)(SB - 1);\n    }\n"
       << "    act &= ~sp;\n"
-      << "    {\n      qu64 bal[4];\n      qu32 tot = 0;\n"
-      << "#pragma unroll\n      for (int r = 0; r < 4; ++r) { bal[r] = __ballot((sp >> r) & 1u); tot += (qu32)__popcll(bal[r]); }\n"
-      << "      const qu32 room = sp_cid >= 0 ? (qu32)PART_CH - sp_fill : 0u;\n"
+      << "#pragma unroll\n    for (int b = 0; b < SB; ++b) {\n      qu64 bal[4];\n      qu32 tot = 0;\n"
+      << "#pragma unroll\n      for (int r = 0; r < 4; ++r) { bal[r] = __ballot(((sp >> r) & 1u) && sbk[r] == (qu32)b); tot += (qu32)__popcll(bal[r]); }\n"
+      << "      const qu32 room = sp_cid[b] >= 0 ? (qu32)PART_CH - sp_fill[b] : 0u;\n"
       << "      if (tot && tot <= room) {\n"
-      << "        const __amdgpu_buffer_rsrc_t cb = __builtin_amdgcn_make_buffer_rsrc((void*)(P.part_rec + sp_cid * (PART_CH * "
+      << "        const __amdgpu_buffer_rsrc_t cb = __builtin_amdgcn_make_buffer_rsrc((void*)(P.part_rec + sp_cid[b] * (PART_CH * "
       << RB << "ll)), (short)0, (int)(PART_CH * " << RB << "), 0x00020000);\n"
       << "        qu32 kb = 0;\n"
       << "#pragma unroll\n        for (int r = 0; r < 4; ++r) {\n"
-      << "          if ((sp >> r) & 1) {\n"
+      << "          if ((bal[r] >> lane) & 1) {\n"
       << "            const qu32 k = __builtin_amdgcn_mbcnt_hi((qu32)(bal[r] >> 32), __builtin_amdgcn_mbcnt_lo((qu32)bal[r], kb));\n"
-      << "            const int off = (int)((sp_fill + k) * " << RB << "u);\n"
+      << "            const int off = (int)((sp_fill[b] + k) * " << RB << "u);\n"
       << "            qi64 w[" << L.words << "];\n";
     emit_record_words(P, L, ex, "w", o);
     emit_fit_check(L, "w", o);
     for (const auto& pc : pieces) piece_store(pc.first, pc.second);
     o << "          }\n          kb += (qu32)__popcll(bal[r]);\n        }\n"
-      << "        sp_fill += tot;\n"
+      << "        sp_fill[b] += tot;\n"
       << "      } else if (tot) {\n"
       << "        const int leader = __ffsll((long long)__ballot(1)) - 1;\n"
       << "        qi64 id = 0;\n"
       << "        if (lane == leader) {\n"
-      << "          if (sp_cid >= 0) P.part_chunk[1 + sp_cid] = PART_CH;\n"
+      << "          if (sp_cid[b] >= 0) P.part_chunk[1 + sp_cid[b]] = ((qi64)b << 32) | PART_CH;\n"
       << "          id = (qi64)atomicAdd((qu64*)P.part_chunk, 1ull);\n"
       << "        }\n"
       << "        id = __shfl(id, leader);\n"
@@ -905,9 +913,9 @@ bool gen_fused_source(const Plan& P, int log2, std::string* src, size_t* lds_byt
       << "                                (qu64)__builtin_amdgcn_readfirstlane((qu32)id));\n"
       << "        qu32 kb = 0;\n"
       << "#pragma unroll\n        for (int r = 0; r < 4; ++r) {\n"
-      << "          if ((sp >> r) & 1) {\n"
+      << "          if ((bal[r] >> lane) & 1) {\n"
       << "            const qu32 k = kb + (qu32)__popcll(bal[r] & ((1ull << lane) - 1));\n"
-      << "            const qu64 pos = k < room ? (qu64)sp_cid * PART_CH + sp_fill + k : (qu64)nid * PART_CH + (k - room);\n"
+      << "            const qu64 pos = k < room ? (qu64)sp_cid[b] * PART_CH + sp_fill[b] + k : (qu64)nid * PART_CH + (k - room);\n"
       << "            qi64 w[" << L.words << "];\n";
     emit_record_words(P, L, ex, "w", o);
     emit_fit_check(L, "w", o);
@@ -915,7 +923,7 @@ bool gen_fused_source(const Plan& P, int log2, std::string* src, size_t* lds_byt
     o << "            " << wt << "* const dst = (" << wt << "*)(P.part_rec + pos * " << RB << "ull);\n";
     for (int q = 0; q < L.words; ++q) o << "            dst[" << q << "] = (" << wt << ")w[" << q << "];\n";
     o << "          }\n          kb += (qu32)__popcll(bal[r]);\n        }\n"
-      << "        sp_cid = nid;\n        sp_fill = tot - room;\n"
+      << "        sp_cid[b] = nid;\n        sp_fill[b] = tot - room;\n"
       << "      }\n    }\n"
       << "    if (act == 0) continue;\n";
   } else if (P.mp_n > 1)
@@ -935,8 +943,9 @@ bool gen_fused_source(const Plan& P, int log2, std::string* src, size_t* lds_byt
     emit_fx_queue_run(P, o, "q_n");
     o << "  }\n";
   }
-  if (spill)  // each wave's open chunk: its fill
-    o << "  if ((threadIdx.x & 63) == 0 && sp_cid >= 0) P.part_chunk[1 + sp_cid] = (qi64)sp_fill;\n"
+  if (spill)  // each wave's open chunks: sub-bucket and fill
+    o << "#pragma unroll\n  for (int b = 0; b < SB; ++b)\n"
+      << "    if ((threadIdx.x & 63) == 0 && sp_cid[b] >= 0) P.part_chunk[1 + sp_cid[b]] = ((qi64)b << 32) | (qi64)sp_fill[b];\n"
       << "  if (nfit) atomicOr(&P.t.ctl[7], 1ull);\n";
   if (compact) emit_flush_c(P, o);
   else emit_flush(P, o);

@@ -172,6 +172,13 @@ static int emit_agg(const char* dir, const char* name, const qe_column* cols, in
       fprintf(stderr, "%s: compact spill source not generated\n", name);
       return 1;
     }
+    // ... with the spilled share in 4 sub-buckets
+    std::string m4;
+    P.mp_n = 5;
+    if (!gen_fused_source(P, log2, &m4, &lds, true) || write_src(dir, std::string(name) + "_spill_compact_sb4", m4)) {
+      fprintf(stderr, "%s: compact spill source (4 sub-buckets) not generated\n", name);
+      return 1;
+    }
     P.mp_n = 0;
   }
   P.lds_compact = 0;

@@ -739,12 +739,13 @@ def test_fused_c4_one_pass_large_table(agg_ctx):
     assert_groups_equal(result_dict(kk, aa), ref, C4_FNS)
 
 
-@pytest.mark.parametrize("groups", [3500, 4096, 5000, 5500, 6500, 7500, 8192, 9500])
+@pytest.mark.parametrize("groups", [3500, 4096, 5000, 5500, 6500, 7500, 8192, 9500, 12000])
 def test_fused_c4_compact_vs_oracle(agg_ctx, groups):
     """Groups just past the regular LDS table: ONE fused pass over a compact table (32-bit keys,
     32-bit MIN / MAX of bare columns, ~6.4K slots in 152 KiB) instead of key-hash passes; past
-    that table (to ~8.2K groups: a 6/8 kept share plus QE_SPILL_MAXPCT 85 of the aggregation table),
-    one spilling pass whose kept share stays in the compact table; beyond, the partitioned update."""
+    that table (to ~10.5K groups: a 6/8 kept share plus up to two spilled sub-buckets, each filling
+    at most QE_SPILL_MAXPCT 70 of its aggregation table), one spilling pass whose kept share stays
+    in the compact table; beyond, the partitioned update."""
     from kquery.datasource import C4_COLUMNS, ColumnSpec, generate_column
 
     n, row0 = 2_000_003, 5
@@ -756,8 +757,9 @@ def test_fused_c4_compact_vs_oracle(agg_ctx, groups):
     if agg_ctx.kernel_mode == "jit":
         spec, note = st.last_kernel_kind()
         want = ("compact LDS table" if groups <= 5500 else "multi-pass: 2 buckets (compact kept table)"
-                if groups <= 8192 else "radix-partitioned")
+                if groups <= 9500 else "radix-partitioned")
         assert spec and note.startswith(want), note
+        assert ("2 sub-buckets" in note) == (groups in (8192, 9500)), note
     kk, aa = st.finalize()
     k, _ = gen.generate(gen.GEN_MOD, groups, 42, 0, row0, n)
     a, _ = gen.generate(gen.GEN_MOD, 1 << 20, 42, 1, row0, n)
@@ -767,17 +769,18 @@ def test_fused_c4_compact_vs_oracle(agg_ctx, groups):
     assert_groups_equal(result_dict(kk, aa), ref, C4_FNS)
 
 
-@pytest.mark.parametrize("case,spill", [("fits", False), ("key_wide", False), ("value_wide", False), ("nullable", False),
-                                        ("fits", True), ("key_wide", True), ("value_wide", True)])
+@pytest.mark.parametrize("case,spill", [("fits", 0), ("key_wide", 0), ("value_wide", 0), ("nullable", 0),
+                                        ("fits", 1), ("key_wide", 1), ("value_wide", 1), ("fits", 2), ("value_wide", 2)])
 def test_compact_table_speculation(agg_ctx, case, spill):
     """The compact table speculates that keys and MIN / MAX inputs fit 32 bits. A batch where one
     does not is still exact (those rows go to the global table) and the state's later batches take
     the bucket passes instead; null keys, INT32_MIN keys and nullable inputs keep their semantics.
-    `spill`: 6,300 groups, past the one-pass table: the spilling pass over the compact kept table,
-    where a wide key or value in the spilled share also makes its 32-bit records misfit."""
+    `spill` 1: 6,300 groups, past the one-pass table: the spilling pass over the compact kept table,
+    where a wide key or value in the spilled share also makes its 32-bit records misfit; 2: 9,500
+    groups, the spilled share in two sub-buckets."""
     rng = np.random.default_rng(len(case) * 7 + spill)
     # (nullable inputs add a non-null count per aggregate to the slot: fewer slots, fewer groups)
-    n, groups = 400_000, 2600 if case == "nullable" else (6300 if spill else 4200)
+    n, groups = 400_000, 2600 if case == "nullable" else (9500 if spill == 2 else 6300 if spill else 4200)
     k = (rng.integers(0, groups, n).astype(np.int64) - groups // 2) * 1021
     k[::997] = -2**31  # the 32-bit table's empty marker is a real key here
     x = rng.integers(-2**31, 2**31, n).astype(np.int64)
@@ -801,6 +804,8 @@ def test_compact_table_speculation(agg_ctx, case, spill):
         want = "multi-pass: 2 buckets (compact kept table)" if spill else "compact LDS table"
         # (a misfit in the spilled share reruns that share and names it: "multi-pass: 2 buckets, ...")
         assert notes[0].startswith("multi-pass: 2 buckets" if spill and case != "fits" else want), notes
+        if spill and case == "fits":
+            assert ("in 2 sub-buckets" in notes[0]) == (spill == 2), notes
         if case in ("key_wide", "value_wide"):
             assert not notes[1].startswith(want), notes
         else:

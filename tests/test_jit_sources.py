@@ -34,7 +34,7 @@ def test_all_modes_emitted(sources):
                            [f"{s}_{k}.hip" for s in ("c4", "f64max", "det")
                             for k in ("fused", "spill", "pagg", "pscatter", "pscatter_soa", "pagg_rows",
                                       "pscatter_n32", "pdirect_n32", "pagg_n32", "pagg_unchunked_n32", "spill_n32",
-                                      "pagg_soa_n32", "pagg_big_n32", "fused1")] + ["c4_fused_compact.hip", "c4_spill_compact.hip",
+                                      "pagg_soa_n32", "pagg_big_n32", "fused1")] + ["c4_fused_compact.hip", "c4_spill_compact.hip", "c4_spill_compact_sb4.hip",
                                                                              "c5_fused1.hip"])
 
 
@@ -44,7 +44,7 @@ def test_all_modes_emitted(sources):
                                   "c4_pscatter_soa", "c4_pagg_rows", "det_pscatter_soa", "f64max_pscatter_soa",
                                   "c4_pscatter_n32", "c4_pdirect_n32", "c4_pagg_n32", "c4_pagg_unchunked_n32",
                                   "f64max_pagg_n32", "c4_spill_n32", "c4_pagg_soa_n32", "c4_fused_compact",
-                                  "c4_pagg_big_n32", "c4_spill_compact", "c4_fused1", "det_fused1", "c5_fused1"])
+                                  "c4_pagg_big_n32", "c4_spill_compact", "c4_spill_compact_sb4", "c4_fused1", "det_fused1", "c5_fused1"])
 def test_compiles_for_gfx950(sources, name, tmp_path):
     if name in ("det_fused1", "c5_fused1"):  # exact fp64 SUMs of a single-pass plan go through the per-wave queue
         assert "q_slot" in next(p for p in sources if p.stem == name).read_text()
