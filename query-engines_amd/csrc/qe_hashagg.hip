@@ -932,15 +932,16 @@ __global__ void k_spill_plan(const qi64* __restrict__ meta, qi64 tmax, qi64* __r
   if (threadIdx.x == 0) out[0] = ns;
 }
 
-__global__ void k_table_init(DTable t, AggMeta m, qu64* zero_ctl) {
+// zero_ctl: the control words too (a reset, or a new state); reset: the slots' E words were in use
+__global__ void k_table_init(DTable t, AggMeta m, qu64* zero_ctl, int reset) {
   const qu64 SS = t.cap + 2;
-  if (zero_ctl && blockIdx.x == 0 && threadIdx.x < 8) zero_ctl[threadIdx.x] = 0;  // reset: the control words too
+  if (zero_ctl && blockIdx.x == 0 && threadIdx.x < 8) zero_ctl[threadIdx.x] = 0;
   for (qu64 s = blockIdx.x * (qu64)blockDim.x + threadIdx.x; s < SS; s += (qu64)gridDim.x * blockDim.x) {
     t.keys[s] = EMPTY_KEY;
     t.cstar[s] = 0;
     for (int j = 0; j < m.naggs; ++j) {
       // a reset zeroes the E words a slot used (a new table's come zeroed: table_alloc)
-      if (zero_ctl && m.acc[j] == ACC_SUM_X && (t.idx[j][3 * SS + s] & FX_EXT))
+      if (reset && m.acc[j] == ACC_SUM_X && (t.idx[j][3 * SS + s] & FX_EXT))
         for (int w = 0; w < FXE_WORDS; ++w) t.ext[j][s * FXE_WORDS + w] = 0;
       t.acc[j][s] = acc_identity(m.acc[j]);
       t.nn[j][s] = 0;
@@ -1600,7 +1601,8 @@ static size_t table_bytes(const qe_hashagg* h, uint64_t cap) {
   return b;
 }
 
-static int table_alloc(qe_hashagg* h, uint64_t cap, void** mem, DTable* t) {
+// zero_ctl: a new state's control words, zeroed by the same init launch (no separate memset)
+static int table_alloc(qe_hashagg* h, uint64_t cap, void** mem, DTable* t, qu64* zero_ctl = nullptr) {
   const size_t bytes = table_bytes(h, cap);
   QE_TRY(dev_alloc(h->ctx, bytes, mem));
   const uint64_t SS = cap + 2;
@@ -1631,7 +1633,7 @@ static int table_alloc(qe_hashagg* h, uint64_t cap, void** mem, DTable* t) {
   t->cap = cap;
   t->ctl = h->ctl;
   const int grid = (int)std::min<uint64_t>(div_up(SS, 256), 4096);
-  hipLaunchKernelGGL(k_table_init, dim3(grid), dim3(256), 0, h->ctx->stream, *t, agg_meta(h), (qu64*)nullptr);
+  hipLaunchKernelGGL(k_table_init, dim3(grid), dim3(256), 0, h->ctx->stream, *t, agg_meta(h), zero_ctl, 0);
   return launch_check("k_table_init");
 }
 
@@ -1700,10 +1702,9 @@ static int ensure_defer(qe_hashagg* h, int64_t n) {
     dev_free(h->ctx, h->defer[i]);
     h->defer[i] = nullptr;
   }
-  for (int i = 0; i < 2; ++i) {
+  for (int i = 0; i < 2; ++i) {  // (zeroed by launch_pass before a launch first writes one)
     QE_TRY(dev_alloc(h->ctx, words * 4, (void**)&h->defer[i]));
-    QE_HIP(hipMemsetAsync(h->defer[i], 0, words * 4, h->ctx->stream));
-    h->defer_dirty[i] = false;
+    h->defer_dirty[i] = true;
   }
   h->defer_words = words;
   return QE_OK;
@@ -2981,7 +2982,7 @@ int qe_hashagg_create_ex(qe_ctx* ctx, int32_t nkeys, const int32_t* key_types, i
     return bail(fail(QE_ERR_DEVICE, "hipEventCreate failed"));
   if (pinned_slot_alloc(&h->ctl_pin) != QE_OK) return bail(QE_ERR_OOM);
   if (dev_alloc(ctx, 64, (void**)&h->ctl) != QE_OK) return bail(fail(QE_ERR_OOM, "control allocation failed"));
-  if (hipMemsetAsync(h->ctl, 0, 64, ctx->stream) != hipSuccess) return bail(fail(QE_ERR_DEVICE, "memset failed"));
+  // (the control words are zeroed by the table's init launch below)
   // LDS table: 2x the expected groups (load factor <= 0.5); a launch may shrink it down to
   // 1.25x (lds_log2_min) to fit the per-workgroup budget, else the launch is global-only.
   const int64_t eg = expected_groups > 0 ? expected_groups : 1024;
@@ -3006,13 +3007,14 @@ int qe_hashagg_create_ex(qe_ctx* ctx, int32_t nkeys, const int32_t* key_types, i
     }
   }
   // global table: 2x expected groups
-  const int st = table_alloc(h, std::max<uint64_t>(1024, next_pow2((uint64_t)(2 * eg))), &h->table_mem, &h->t);
+  const int st = table_alloc(h, std::max<uint64_t>(1024, next_pow2((uint64_t)(2 * eg))), &h->table_mem, &h->t, h->ctl);
   h->nn_implicit = all_nn_bits(h);
   if (st != QE_OK) {
     dev_free(ctx, h->ovf);
     dev_free(ctx, h->ctl);
     return bail(st);
   }
+  h->ctl_rows_clean = true;  // (zeroed by the init launch)
   *out = h;
   return QE_OK;
 }
@@ -3076,7 +3078,7 @@ int qe_hashagg_reset(qe_hashagg* h) {
   h->poisoned = 0;
   h->poison_msg.clear();
   const int grid = (int)std::min<uint64_t>(div_up(h->t.cap + 2, 256), 4096);
-  hipLaunchKernelGGL(k_table_init, dim3(grid), dim3(256), 0, h->ctx->stream, h->t, agg_meta(h), (qu64*)h->ctl);
+  hipLaunchKernelGGL(k_table_init, dim3(grid), dim3(256), 0, h->ctx->stream, h->t, agg_meta(h), (qu64*)h->ctl, 1);
   QE_TRY(launch_check("k_table_init"));
   h->nn_implicit = all_nn_bits(h);
   h->ctl_rows_clean = true;
