@@ -126,6 +126,9 @@ def _alloc_like(c: DeviceColumn, n: int, ctx) -> DeviceColumn:
 SELECTION_COMPACTION = "select_project"
 
 
+_SELPROJ_SPECS = {}  # column count -> the compaction's select-project spec (read-only once built)
+
+
 def _compact_selproj(batch: RecordBatch, cols, mask: DeviceColumn) -> Optional[RecordBatch]:
     """The compaction through the select-project kernel (qe_select_project_async with the mask
     column as the selection and the columns themselves as the outputs: one pass with a decoupled
@@ -133,13 +136,16 @@ def _compact_selproj(batch: RecordBatch, cols, mask: DeviceColumn) -> Optional[R
     the plan."""
     ctx = mask.ctx
     n = mask.length
-    spec = N.QeSelectSpec()
-    spec.mask_col = len(cols)
-    spec.nterms = 0
-    spec.nout = len(cols)
-    for i in range(len(cols)):
-        spec.outputs[i].ntokens = 1
-        spec.outputs[i].tokens[0] = N.QeToken(N.TOK_COL, i, N.QeScalar())
+    spec = _SELPROJ_SPECS.get(len(cols))
+    if spec is None:  # (the spec depends only on the column count: built once)
+        spec = N.QeSelectSpec()
+        spec.mask_col = len(cols)
+        spec.nterms = 0
+        spec.nout = len(cols)
+        for i in range(len(cols)):
+            spec.outputs[i].ntokens = 1
+            spec.outputs[i].tokens[0] = N.QeToken(N.TOK_COL, i, N.QeScalar())
+        _SELPROJ_SPECS[len(cols)] = spec
     outs = [DeviceColumn.empty(c.type, n, False, ctx=ctx) for c in cols]
     cc = (N.QeColumn * (len(cols) + 1))(*([c.as_c() for c in cols] + [mask.as_c()]))
     oc = (N.QeColumn * len(outs))(*[o.as_c() for o in outs])
