@@ -2612,13 +2612,14 @@ static int run_update(qe_hashagg* h, Plan& P) {
     T.lds_log2 = 16;  // (unused by the compact kernel; keeps adapt_after_update from resizing)
     const size_t bps = compact_slot_bytes(T);
     const int64_t nsl = ((int64_t)((lds_budget(ctx) - 512) / bps) - 66) & ~(int64_t)63;  // (+2 special, 64 sinks)
-    // expected groups at most QE_COMPACT_LOAD percent of the slots (default 92: 1B rows, one box,
-    // 5,400 / 5,700 groups 3.76 / 3.87 ms in one pass at 88-92 %, against 4.08 / 4.76 ms for the
-    // spilling pass the 80 % limit sent them to)
+    // expected groups at most QE_COMPACT_LOAD percent of the slots (default 98; 1B rows, one box,
+    // 6336 slots: 5,900 / 6,000 / 6,150 / 6,250 groups 4.04 / 4.02–4.15 / 4.24 / 4.97 ms in one pass
+    // at 93–99 %, against 5.45–5.71 ms for the spilling pass; round 5: 5,400 / 5,700 groups 3.76 /
+    // 3.87 ms at 88–92 %)
     static const int cload = [] {
       const char* e = getenv("QE_COMPACT_LOAD");
-      const int v = e && *e ? atoi(e) : 92;
-      return v >= 50 && v <= 95 ? v : 92;
+      const int v = e && *e ? atoi(e) : 98;
+      return v >= 50 && v <= 99 ? v : 98;
     }();
     if (nsl >= 512 && nsl * cload >= h->expected_groups * 100) {
       T.lds_compact = (qi32)nsl;
